@@ -1,0 +1,135 @@
+#!/usr/bin/env python
+"""Headline benchmark: Trainer examples/sec (whole node), Chicago-Taxi Wide&Deep, 1/2/4/8 MI355X.
+
+Model: the reference W&D (`airflow-dags/taxi_utils.py:148-191,300-345`): DNN [100,70,48,34] on
+3 dense floats + linear part over 9 categorical identity columns (2127 buckets), sigmoid CE,
+Adagrad(DNN) + FTRL(linear) — full training step (fwd + bwd + all-reduce + optimizer) in the
+timed region. Data: synthetic transformed-taxi records resident in HBM (no network for the
+real CSV); random-init weights. Weak scaling: fixed batch per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-gpu B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from mifx.data.synthetic import synthetic_records  # noqa: E402
+from mifx.models.wide_deep import WideDeepModel  # noqa: E402
+from mifx.parallel import dist as mdist  # noqa: E402
+
+METRIC = "Trainer examples/sec (whole node), Chicago-Taxi Wide&Deep at 1/2/4/8 MI355X"
+MODEL = "chicago-taxi-wide-deep (DNNLinearCombinedClassifier: dnn [100,70,48,34] on 3 dense, linear on 9 cat cols)"
+
+
+def run(trainer, steps: int, warmup: int, device) -> float:
+    for _ in range(warmup):
+        trainer.step()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    mdist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    mdist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    return time.perf_counter() - t0
+
+
+def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool):
+    model = WideDeepModel(seed=0)
+    if device.type == "cuda":
+        from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+        tr = FusedWideDeepTrainer(model, batch=batch, device=device, process_group=pg)
+    else:
+        from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
+
+        tr = TorchWideDeepTrainer(model, batch=batch, device=device)
+    tr.set_data(synthetic_records(n_data, device=device, seed=seed))
+    if graph and device.type == "cuda":
+        tr.capture()
+    return tr
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch-per-gpu", type=int, default=65536,
+                    help="throughput batch per replica (BASELINE.md protocol: 8K-64K); 40 = reference batch")
+    ap.add_argument("--ref-batch", type=int, default=40, help="also time the reference batch (0 = skip)")
+    ap.add_argument("--ref-steps", type=int, default=2000)
+    ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args(argv)
+
+    env = mdist.init()
+    use_cuda = torch.cuda.is_available()
+    device = torch.device("cuda", env.local_rank) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(device)
+    else:  # CPU dev fallback: keep it quick
+        a.batch_per_gpu = min(a.batch_per_gpu, 4096)
+        a.data_per_gpu = min(a.data_per_gpu, 1 << 16)
+        a.steps, a.warmup, a.ref_steps = min(a.steps, 20), min(a.warmup, 2), min(a.ref_steps, 50)
+    pg = torch.distributed.group.WORLD if env.world_size > 1 else None
+    n = env.world_size
+
+    tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph)
+    dt = mdist.max_over_ranks(run(tr, a.steps, a.warmup, device), device if use_cuda else None)
+    loss = tr.last_loss() / a.batch_per_gpu
+    value = a.batch_per_gpu * n * a.steps / dt
+
+    ref = None
+    if a.ref_batch:
+        del tr
+        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph)
+        dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
+        ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
+               "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps}
+
+    if env.is_main:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "examples/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * dt / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (transformed Chicago-Taxi-shaped records, HBM-resident); random-init weights",
+            "config": {"model": MODEL, "global_batch": a.batch_per_gpu * n, "seq_len": None,
+                       "parallelism": f"dp{n}", "batch_per_gpu": a.batch_per_gpu,
+                       "optimizer": "adagrad(dnn,lr=0.05)+ftrl(linear,lr=0.2)",
+                       "precision": "bf16 MFMA compute, fp32 master weights/optimizer state",
+                       "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
+                       "hipgraph": bool(use_cuda and not a.no_graph)},
+            "final_mean_loss": loss,
+            "reference_batch": ref,
+        }
+        print(json.dumps(out))
+    mdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,254 @@
+"""Chicago-Taxi Wide&Deep model (DNNLinearCombinedClassifier equivalent).
+
+Reference parity: ``airflow-dags/taxi_utils.py:148-191`` (`_build_estimator`) and
+``trainer_fn`` (`taxi_utils.py:285-356`): DNN over the 3 z-scored dense floats with hidden units
+``[max(2, int(100 * 0.7**i)) for i in range(4)] == [100, 70, 48, 34]``; linear part over
+categorical identity columns (``default_value=0`` clamps out-of-range ids to bucket 0) — the
+vocab features (1000 + 10 OOV buckets), the 4 bucketized lat/lon features (10 buckets) and the
+``zip``-truncated categorical keys ``trip_start_hour/day/month`` with 24/31/12 buckets
+(`taxi_utils.py:178-185`). Head: binary logistic (sigmoid cross-entropy).
+
+Two implementations share one parameterisation:
+  * :class:`WideDeepModel` — plain PyTorch (fp32), runs anywhere; the numerics reference.
+  * the fused HIP step in :mod:`mifx.trainer.fused_wide_deep` (gfx950), which uses the padded
+    "canonical" layout produced by :func:`pack_canonical` (biases folded into a constant-1 input
+    column of every layer).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+from torch import nn
+
+# ---- taxi feature contract (taxi_utils.py:32-67) ------------------------------------------
+DENSE_FLOAT_FEATURE_KEYS = ["trip_miles", "fare", "trip_seconds"]
+VOCAB_FEATURE_KEYS = ["payment_type", "company"]
+BUCKET_FEATURE_KEYS = ["pickup_latitude", "pickup_longitude", "dropoff_latitude", "dropoff_longitude"]
+CATEGORICAL_FEATURE_KEYS = [
+    "trip_start_hour", "trip_start_day", "trip_start_month", "pickup_census_tract",
+    "dropoff_census_tract", "pickup_community_area", "dropoff_community_area",
+]
+MAX_CATEGORICAL_FEATURE_VALUES = [24, 31, 12]
+VOCAB_SIZE = 1000
+OOV_SIZE = 10
+FEATURE_BUCKET_COUNT = 10
+LABEL_KEY = "tips"
+FARE_KEY = "fare"
+
+
+def transformed_name(key: str) -> str:
+    return key + "_xf"
+
+
+def wide_columns() -> list[tuple[str, int]]:
+    """(transformed feature name, num_buckets) of the linear part, in kernel order."""
+    cols = [(transformed_name(k), VOCAB_SIZE + OOV_SIZE) for k in VOCAB_FEATURE_KEYS]
+    cols += [(transformed_name(k), FEATURE_BUCKET_COUNT) for k in BUCKET_FEATURE_KEYS]
+    # zip() truncation of the 7 categorical keys to the 3 max values (taxi_utils.py:178-185)
+    cols += [(transformed_name(k), nb) for k, nb in zip(CATEGORICAL_FEATURE_KEYS, MAX_CATEGORICAL_FEATURE_VALUES)]
+    return cols
+
+
+def dnn_hidden_units(first: int = 100, num_layers: int = 4, decay: float = 0.7) -> list[int]:
+    return [max(2, int(first * decay ** i)) for i in range(num_layers)]
+
+
+@dataclass
+class WideDeepConfig:
+    dense_features: list[str] = field(default_factory=lambda: [transformed_name(k) for k in DENSE_FLOAT_FEATURE_KEYS])
+    wide: list[tuple[str, int]] = field(default_factory=wide_columns)
+    hidden_units: list[int] = field(default_factory=dnn_hidden_units)
+    label: str = transformed_name(LABEL_KEY)
+
+    @property
+    def wide_offsets(self) -> list[int]:
+        out, o = [], 0
+        for _, nb in self.wide:
+            out.append(o)
+            o += nb
+        return out
+
+    @property
+    def wide_rows(self) -> int:
+        return sum(nb for _, nb in self.wide)
+
+
+# ---- record layout shared with csrc/wide_deep.hip --------------------------------------------
+RECORD_DTYPE = np.dtype([("d", "<f4", (3,)), ("id", "<u2", (9,)), ("label", "<u2")])
+assert RECORD_DTYPE.itemsize == 32
+
+
+class WideDeepModel(nn.Module):
+    """fp32 PyTorch Wide&Deep; TF initialisers (glorot-uniform kernels, zero biases/linear)."""
+
+    def __init__(self, cfg: WideDeepConfig | None = None, seed: int | None = 0):
+        super().__init__()
+        self.cfg = cfg or WideDeepConfig()
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        dims = [len(self.cfg.dense_features)] + list(self.cfg.hidden_units)
+        self.dnn = nn.ModuleList(nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1))
+        self.head = nn.Linear(dims[-1], 1)
+        for lin in list(self.dnn) + [self.head]:
+            bound = math.sqrt(6.0 / (lin.in_features + lin.out_features))
+            with torch.no_grad():
+                lin.weight.copy_(torch.rand(lin.weight.shape, generator=g) * 2 * bound - bound)
+                lin.bias.zero_()
+        self.wide = nn.Parameter(torch.zeros(self.cfg.wide_rows))
+        self.wide_bias = nn.Parameter(torch.zeros(1))
+        self.register_buffer("wide_off", torch.tensor(self.cfg.wide_offsets, dtype=torch.long), persistent=False)
+        self.register_buffer("wide_nb", torch.tensor([nb for _, nb in self.cfg.wide], dtype=torch.long),
+                             persistent=False)
+
+    def wide_index(self, ids: torch.Tensor) -> torch.Tensor:
+        ids = ids.long()
+        ids = torch.where((ids >= 0) & (ids < self.wide_nb), ids, torch.zeros_like(ids))
+        return ids + self.wide_off
+
+    def forward(self, dense: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+        h = dense.float()
+        for lin in self.dnn:
+            h = torch.relu(lin(h))
+        deep = self.head(h).squeeze(-1)
+        wide = self.wide[self.wide_index(ids)].sum(-1) + self.wide_bias
+        return deep + wide
+
+    def loss(self, dense, ids, labels, reduction: str = "sum") -> torch.Tensor:
+        return nn.functional.binary_cross_entropy_with_logits(self(dense, ids), labels.float(), reduction=reduction)
+
+
+# ---- canonical padded layout (must match csrc/wide_deep.hip) --------------------------------
+LAYER_KN = [(32, 128), (128, 96), (96, 64), (64, 64), (64, 16)]
+WTOT = sum(k * n for k, n in LAYER_KN)  # 27648
+NWIDE = 2128
+NTILE = 108
+STRIDE = NTILE * 256 + 2176
+
+
+def _offsets():
+    off, tb, o, t = [], [], 0, 0
+    for k, n in LAYER_KN:
+        off.append(o)
+        tb.append(t)
+        o += k * n
+        t += (n // 16) * (k // 16)
+    return off, tb
+
+
+LAYER_OFF, TILE_BASE = _offsets()
+
+
+def _real_dims(cfg: WideDeepConfig) -> list[tuple[int, int]]:
+    dims = [len(cfg.dense_features)] + list(cfg.hidden_units) + [1]
+    return [(dims[i], dims[i + 1]) for i in range(len(dims) - 1)]
+
+
+def check_fused_compatible(cfg: WideDeepConfig) -> None:
+    real = _real_dims(cfg)
+    if len(real) != len(LAYER_KN):
+        raise ValueError("fused kernel is specialised for 4 hidden layers")
+    for li, ((kr, nr), (k, n)) in enumerate(zip(real, LAYER_KN)):
+        last = li == len(LAYER_KN) - 1
+        if kr + 1 > k or (nr if last else nr + 1) > n:
+            raise ValueError(f"layer {kr}->{nr} does not fit padded {k}x{n}")
+    if [nb for _, nb in cfg.wide] != [1010, 1010, 10, 10, 10, 10, 24, 31, 12]:
+        raise ValueError("fused kernel is specialised for the taxi wide columns")
+
+
+def canonical_index_maps(cfg: WideDeepConfig | None = None):
+    """Return (gidx int32 [WTOT+NWIDE], mask uint8 [WTOT+NWIDE]).
+
+    gidx maps each canonical parameter to its position in the kernel's tile-native gradient
+    slab; mask marks trainable entries (real weights + folded biases)."""
+    cfg = cfg or WideDeepConfig()
+    check_fused_compatible(cfg)
+    gidx = np.zeros(WTOT + NWIDE, np.int32)
+    mask = np.zeros(WTOT + NWIDE, np.uint8)
+    for li, ((K, N), (kr, nr)) in enumerate(zip(LAYER_KN, _real_dims(cfg))):
+        n = np.arange(N)[:, None]
+        k = np.arange(K)[None, :]
+        tile = TILE_BASE[li] + (n // 16) * (K // 16) + (k // 16)
+        lane = 16 * ((n % 16) // 4) + (k % 16)
+        idx = tile * 256 + (n % 4) * 64 + lane
+        gidx[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = idx.reshape(-1)
+        m = (n < nr) & (k <= kr)
+        mask[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = m.reshape(-1)
+    gidx[WTOT:] = NTILE * 256 + np.arange(NWIDE)
+    mask[WTOT:] = 1
+    return gidx, mask
+
+
+def pack_canonical(model: WideDeepModel) -> np.ndarray:
+    """torch model -> fp32 canonical parameter vector [WTOT + NWIDE]."""
+    check_fused_compatible(model.cfg)
+    out = np.zeros(WTOT + NWIDE, np.float32)
+    lins = list(model.dnn) + [model.head]
+    for li, ((K, N), lin) in enumerate(zip(LAYER_KN, lins)):
+        wt = np.zeros((N, K), np.float32)
+        nr, kr = lin.weight.shape
+        wt[:nr, :kr] = lin.weight.detach().cpu().numpy()
+        wt[:nr, kr] = lin.bias.detach().cpu().numpy()
+        if li < len(LAYER_KN) - 1:
+            wt[nr, kr] = 1.0  # produces the constant-1 column of the next layer's input
+        out[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = wt.reshape(-1)
+    nw = model.wide.numel()
+    out[WTOT:WTOT + nw] = model.wide.detach().cpu().numpy()
+    out[WTOT + nw] = float(model.wide_bias.detach().cpu().item())
+    return out
+
+
+def unpack_canonical(vec, model: WideDeepModel) -> WideDeepModel:
+    """fp32 canonical vector -> torch model parameters (in place)."""
+    vec = np.asarray(vec.detach().cpu() if torch.is_tensor(vec) else vec, dtype=np.float32)
+    lins = list(model.dnn) + [model.head]
+    with torch.no_grad():
+        for li, ((K, N), lin) in enumerate(zip(LAYER_KN, lins)):
+            wt = vec[LAYER_OFF[li]:LAYER_OFF[li] + K * N].reshape(N, K)
+            nr, kr = lin.weight.shape
+            lin.weight.copy_(torch.from_numpy(wt[:nr, :kr].copy()))
+            lin.bias.copy_(torch.from_numpy(wt[:nr, kr].copy()))
+        nw = model.wide.numel()
+        model.wide.copy_(torch.from_numpy(vec[WTOT:WTOT + nw].copy()))
+        model.wide_bias.fill_(float(vec[WTOT + nw]))
+    return model
+
+
+def canonical_grad_to_torch(grad_tile_native: np.ndarray, model: WideDeepModel) -> dict[str, np.ndarray]:
+    """Map a tile-native gradient slab back to named torch-shaped gradients (for tests)."""
+    gidx, _ = canonical_index_maps(model.cfg)
+    canon = np.asarray(grad_tile_native)[gidx]
+    out = {}
+    lins = list(model.dnn) + [model.head]
+    names = [f"dnn.{i}" for i in range(len(model.dnn))] + ["head"]
+    for li, ((K, N), lin, nm) in enumerate(zip(LAYER_KN, lins, names)):
+        wt = canon[LAYER_OFF[li]:LAYER_OFF[li] + K * N].reshape(N, K)
+        nr, kr = lin.weight.shape
+        out[nm + ".weight"] = wt[:nr, :kr]
+        out[nm + ".bias"] = wt[:nr, kr]
+    nw = model.wide.numel()
+    out["wide"] = canon[WTOT:WTOT + nw]
+    out["wide_bias"] = canon[WTOT + nw:WTOT + nw + 1]
+    return out
+
+
+def records_to_tensors(rec: np.ndarray | torch.Tensor):
+    """Decode packed 32-B records into (dense f32 [N,3], ids int64 [N,9], label f32 [N])."""
+    if torch.is_tensor(rec):
+        raw = rec.view(torch.uint8).reshape(-1, 32)
+        dense = raw[:, :12].contiguous().view(torch.float32).reshape(-1, 3)
+        u16 = raw[:, 12:32].contiguous().view(torch.int16).reshape(-1, 10).to(torch.int32) & 0xFFFF
+        return dense, u16[:, :9].long(), u16[:, 9].float()
+    rec = np.asarray(rec).view(RECORD_DTYPE)
+    return (torch.from_numpy(rec["d"].copy()), torch.from_numpy(rec["id"].astype(np.int64)),
+            torch.from_numpy(rec["label"].astype(np.float32)))
+
+
+def tensors_to_records(dense, ids, label) -> np.ndarray:
+    n = len(label)
+    rec = np.zeros(n, RECORD_DTYPE)
+    rec["d"] = np.asarray(dense, np.float32).reshape(n, 3)
+    rec["id"] = np.clip(np.asarray(ids), 0, 65535).astype(np.uint16)
+    rec["label"] = np.asarray(label).astype(np.uint16)
+    return rec

@@ -1,0 +1,88 @@
+"""In-tree native build for mifx (gfx950 HIP kernels + host C++ runtime pieces).
+
+Every ``csrc/*.hip`` file becomes ``mifx/ops/lib/libmifx_<stem>.so`` (hipcc, gfx950 only) and
+every ``csrc/*.cpp`` file becomes a host-only ``libmifx_<stem>.so`` (g++). The libraries expose
+plain C ABIs that :mod:`mifx.ops._lib` binds with ctypes, so building needs no torch headers
+and the ``.so`` files travel with the repository snapshot to the GPU box.
+
+Usage: ``python -m mifx.ops.build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+CSRC = ROOT / "csrc"
+LIBDIR = Path(__file__).resolve().parent / "lib"
+ARCH = "gfx950"
+
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-shared",
+    "-fPIC",
+    "-std=c++17",
+    "-Wno-unused-result",
+    "-Wno-unused-value",
+]
+CXX_FLAGS = ["-O3", "-shared", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (expected /opt/rocm/bin/hipcc)")
+
+
+def _needs_build(src: Path, out: Path) -> bool:
+    if not out.exists():
+        return True
+    deps = [src] + sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("include/*.h"))
+    return any(d.stat().st_mtime > out.stat().st_mtime for d in deps if d.exists())
+
+
+def _build_one(src: Path, force: bool) -> tuple[str, str]:
+    out = LIBDIR / f"libmifx_{src.stem}.so"
+    if not force and not _needs_build(src, out):
+        return src.name, "up-to-date"
+    tmp = out.with_suffix(".so.tmp")
+    if src.suffix == ".hip":
+        cmd = [hipcc()] + HIP_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp)]
+    else:
+        cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp), "-lz"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"build of {src.name} failed:\n{' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    tmp.replace(out)
+    return src.name, "built"
+
+
+def build_all(force: bool = False, jobs: int | None = None, verbose: bool = True) -> list[Path]:
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
+    jobs = jobs or min(8, max(1, len(srcs)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        for name, status in ex.map(lambda s: _build_one(s, force), srcs):
+            if verbose:
+                print(f"[mifx.build] {name}: {status}", file=sys.stderr)
+    return [LIBDIR / f"libmifx_{s.stem}.so" for s in srcs]
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    build_all(force=a.force, jobs=a.jobs)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,52 @@
+"""ctypes bindings for csrc/wide_deep.hip (fused Wide&Deep train/eval step on gfx950)."""
+from __future__ import annotations
+
+import ctypes
+import functools
+
+import torch
+
+from . import _lib
+from ._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
+
+
+@functools.lru_cache(maxsize=None)
+def _fns():
+    lib = _lib.load("wide_deep")
+    return {
+        "constants": sig(lib, "mifx_wd_constants", [VP, I32]),
+        "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP]),
+        "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, VP]),
+        "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+    }
+
+
+@functools.lru_cache(maxsize=None)
+def constants() -> dict[str, int]:
+    buf = (ctypes.c_int * 32)()
+    n = _fns()["constants"](buf, 32)
+    names = ["T", "WTOT", "NWIDE", "STRIDE", "NTILE", "LDS_BYTES", "OFF1", "OFF2", "OFF3", "OFF4", "OFF5",
+             "TB1", "TB2", "TB3", "TB4", "TB5"]
+    return {k: buf[i] for i, k in enumerate(names[:n])}
+
+
+def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
+          wt_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
+          logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool) -> None:
+    rc = _fns()["fused"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wt_bf16), ptr(wide), ptr(slab),
+                         ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
+                         stream_handle(records.device))
+    check(rc, "mifx_wd_fused")
+
+
+def reduce(slab: torch.Tensor, groups: int, nsplit: int, partial: torch.Tensor) -> None:
+    check(_fns()["reduce"](ptr(slab), groups, nsplit, ptr(partial), stream_handle(slab.device)), "mifx_wd_reduce")
+
+
+def optimizer(partial: torch.Tensor, nparts: int, gidx: torch.Tensor, mask: torch.Tensor, param: torch.Tensor,
+              s0: torch.Tensor, s1: torch.Tensor, wt_out: torch.Tensor, step_ctr: torch.Tensor,
+              hyper_dnn: torch.Tensor, hyper_wide: torch.Tensor) -> None:
+    # hyper tensors live on the host (read by the launcher, passed by value)
+    rc = _fns()["optimizer"](ptr(partial), nparts, ptr(gidx), ptr(mask), ptr(param), ptr(s0), ptr(s1), ptr(wt_out),
+                             ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide), stream_handle(param.device))
+    check(rc, "mifx_wd_optimizer")

@@ -1,0 +1,188 @@
+"""Device-resident, hipGraph-captured Wide&Deep trainer on the fused gfx950 kernels.
+
+One training step = ``wd_fused`` (forward + loss + backward, per-workgroup gradient slabs)
+-> ``wd_reduce`` (slab sum) -> [RCCL all-reduce of ONE flat 119 KB gradient bucket over xGMI
+when data-parallel] -> ``wd_optimizer`` (Adagrad/FTRL/Adam/SGD + bf16 weight image). The input
+shard lives in HBM; the data offset advances through a device-side step counter, so the whole
+step (collective included) can be captured once and replayed as a hipGraph.
+
+Reference behaviour: Estimator train loop of `taxi_utils.py:285-356` (read_batch_features ->
+DNNLinearCombinedClassifier step with FTRL + Adagrad).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..models import wide_deep as wdm
+from ..ops import wide_deep as wdk
+
+OPT_KIND = {"sgd": 0, "adagrad": 1, "ftrl": 2, "adam": 3}
+
+
+@dataclass
+class OptSpec:
+    kind: str = "adagrad"
+    lr: float = 0.05
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-8
+    l1: float = 0.0
+    l2: float = 0.0
+    lr_power: float = -0.5
+    initial_accumulator_value: float = 0.1
+
+    def encode(self) -> torch.Tensor:
+        return torch.tensor([OPT_KIND[self.kind], self.lr, self.beta1, self.beta2, self.eps, self.l1, self.l2,
+                             self.lr_power], dtype=torch.float32)
+
+
+def default_dnn_opt() -> OptSpec:
+    return OptSpec("adagrad", lr=0.05)
+
+
+def default_wide_opt(num_linear_columns: int = 9) -> OptSpec:
+    return OptSpec("ftrl", lr=min(0.2, 1.0 / math.sqrt(num_linear_columns)))
+
+
+class FusedWideDeepTrainer:
+    def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
+                 dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
+                 grid: int | None = None, process_group=None, max_grid: int = 256):
+        self.device = torch.device(device)
+        self.model = model or wdm.WideDeepModel()
+        wdm.check_fused_compatible(self.model.cfg)
+        c = wdk.constants()
+        assert c["WTOT"] == wdm.WTOT and c["STRIDE"] == wdm.STRIDE and c["NWIDE"] == wdm.NWIDE
+        self.T = c["T"]
+        self.batch = int(batch)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        ntiles = (self.batch + self.T - 1) // self.T
+        self.grid = int(grid or min(ntiles, max_grid))
+        self.dnn_opt = dnn_opt or default_dnn_opt()
+        self.wide_opt = wide_opt or default_wide_opt(len(self.model.cfg.wide))
+        self.loss_reduction = loss_reduction
+        dev = self.device
+        gidx, mask = wdm.canonical_index_maps(self.model.cfg)
+        self.gidx = torch.from_numpy(gidx).to(dev)
+        self.mask = torch.from_numpy(mask).to(dev)
+        self.param = torch.from_numpy(wdm.pack_canonical(self.model)).to(dev)
+        n = wdm.WTOT + wdm.NWIDE
+        self.s0 = torch.zeros(n, device=dev)
+        self.s1 = torch.zeros(n, device=dev)
+        for sl, spec in ((slice(0, wdm.WTOT), self.dnn_opt), (slice(wdm.WTOT, n), self.wide_opt)):
+            if spec.kind in ("adagrad", "ftrl"):
+                self.s0[sl] = spec.initial_accumulator_value
+        self.wt = self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16).contiguous()
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.slab = torch.empty(self.grid, wdm.STRIDE, device=dev)
+        self.slab_loss = torch.zeros(self.grid, device=dev)
+        self.nsplit = max(1, min(16, self.grid // 8))
+        self.partial = torch.empty(self.nsplit, wdm.STRIDE, device=dev)
+        self.grad = torch.empty(1, wdm.STRIDE, device=dev)
+        self.h_dnn = self.dnn_opt.encode()
+        self.h_wide = self.wide_opt.encode()
+        self.records = None
+        self.n_data = 0
+        self.graph = None
+
+    # ---------------------------------------------------------------- data
+    def set_data(self, records: torch.Tensor) -> None:
+        """records: uint8 [N, 32] packed taxi records (see models.wide_deep.RECORD_DTYPE)."""
+        if records.dim() != 2 or records.shape[1] != 32 or records.dtype != torch.uint8:
+            raise ValueError("records must be uint8 [N, 32]")
+        self.records = records.to(self.device).contiguous()
+        self.n_data = self.records.shape[0]
+        self.graph = None
+
+    @property
+    def grad_scale(self) -> float:
+        if self.loss_reduction == "sum":
+            return 1.0
+        return 1.0 / (self.batch * self.world)
+
+    # ---------------------------------------------------------------- step
+    def _step_impl(self) -> None:
+        wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
+                  self.slab_loss, None, self.grad_scale, self.grid, True)
+        if self.world == 1:
+            if self.grid == 1:
+                src, nparts = self.slab, 1
+            else:
+                wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
+                src, nparts = self.partial, self.nsplit
+        else:
+            if self.grid == 1:
+                self.grad.copy_(self.slab)
+            else:
+                wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
+                wdk.reduce(self.partial, self.nsplit, 1, self.grad)
+            torch.distributed.all_reduce(self.grad, group=self.pg)
+            src, nparts = self.grad, 1
+        wdk.optimizer(src, nparts, self.gidx, self.mask, self.param, self.s0, self.s1, self.wt, self.step_ctr,
+                      self.h_dnn, self.h_wide)
+
+    def step(self) -> None:
+        if self.records is None:
+            raise RuntimeError("call set_data() first")
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step_impl()
+
+    def capture(self, warmup: int = 2) -> None:
+        """Capture one full step into a hipGraph (after `warmup` eager steps on a side stream)."""
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_impl()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_impl()
+        self.graph = g
+
+    # ---------------------------------------------------------------- introspection
+    def last_loss(self) -> float:
+        """Sum of per-example losses of the most recent step on this rank."""
+        return float(self.slab_loss.sum().item())
+
+    @property
+    def steps_done(self) -> int:
+        return int(self.step_ctr.item())
+
+    def gradients_once(self) -> np.ndarray:
+        """Run fwd/bwd on the current batch WITHOUT updating; return the tile-native gradient."""
+        wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
+                  self.slab_loss, None, self.grad_scale, self.grid, True)
+        if self.grid > 1:
+            wdk.reduce(self.slab, self.grid, 1, self.grad)
+            return self.grad[0].cpu().numpy()
+        return self.slab[0].cpu().numpy()
+
+    @torch.no_grad()
+    def predict_logits(self, records: torch.Tensor) -> torch.Tensor:
+        records = records.to(self.device).contiguous()
+        n = records.shape[0]
+        out = torch.empty(n, device=self.device)
+        grid = min((n + self.T - 1) // self.T, 1024)
+        wdk.fused(records, n, n, 0, None, self.wt, self.param[wdm.WTOT:], None, None, out, 1.0, grid, False)
+        return out
+
+    def sync_to_model(self) -> wdm.WideDeepModel:
+        return wdm.unpack_canonical(self.param.cpu(), self.model)
+
+    def state_dict(self) -> dict:
+        return {"param": self.param.cpu(), "s0": self.s0.cpu(), "s1": self.s1.cpu(), "step": self.step_ctr.cpu()}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.param.copy_(sd["param"])
+        self.s0.copy_(sd["s0"])
+        self.s1.copy_(sd["s1"])
+        self.step_ctr.copy_(sd["step"])
+        self.wt.copy_(self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16))

@@ -1,0 +1,176 @@
+"""Wide&Deep: canonical-layout packing (CPU) and fused gfx950 kernel vs fp32 PyTorch (GPU)."""
+import numpy as np
+import pytest
+import torch
+
+from mifx.data.synthetic import synthetic_records
+from mifx.models import wide_deep as wdm
+from mifx.trainer.fused_wide_deep import OptSpec
+from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
+
+
+def _canonical_forward(vec, dense, ids):
+    """numpy emulation of the kernel's padded forward (fp32), biases via constant-1 column."""
+    a = np.zeros((len(dense), wdm.LAYER_KN[0][0]), np.float32)
+    a[:, :3] = dense
+    a[:, 3] = 1.0
+    for li, (K, N) in enumerate(wdm.LAYER_KN):
+        wt = vec[wdm.LAYER_OFF[li]:wdm.LAYER_OFF[li] + K * N].reshape(N, K)
+        z = a[:, :K] @ wt.T
+        if li < len(wdm.LAYER_KN) - 1:
+            a = np.maximum(z, 0)
+        else:
+            deep = z[:, 0]
+    cfg = wdm.WideDeepConfig()
+    nb = np.array([n for _, n in cfg.wide])
+    off = np.array(cfg.wide_offsets)
+    idc = np.where(ids < nb, ids, 0) + off
+    wide = vec[wdm.WTOT:][idc].sum(1) + vec[wdm.WTOT + cfg.wide_rows]
+    return deep + wide
+
+
+def test_hidden_units_match_reference():
+    assert wdm.dnn_hidden_units() == [100, 70, 48, 34]
+    assert wdm.WideDeepConfig().wide_rows == 2127
+
+
+def test_pack_roundtrip_and_forward():
+    m = wdm.WideDeepModel(seed=3)
+    with torch.no_grad():
+        m.wide.normal_()
+        m.wide_bias.fill_(0.3)
+        for lin in m.dnn:
+            lin.bias.normal_()
+    vec = wdm.pack_canonical(m)
+    rec = synthetic_records(300, seed=5)
+    dense, ids, _ = wdm.records_to_tensors(rec)
+    ref = m(dense, ids).detach().numpy()
+    got = _canonical_forward(vec, dense.numpy(), ids.numpy())
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
+    m2 = wdm.unpack_canonical(vec, wdm.WideDeepModel(seed=9))
+    np.testing.assert_allclose(m2(dense, ids).detach().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_index_maps_are_bijective_on_slab():
+    gidx, mask = wdm.canonical_index_maps()
+    assert len(np.unique(gidx)) == len(gidx)
+    assert gidx.max() < wdm.STRIDE
+    # trainable = real weights + biases: 3*100+100 + 100*70+70 + 70*48+48 + 48*34+34 + 34+1 + 2128
+    assert mask.sum() == 400 + 7070 + 3408 + 1666 + 35 + 2128
+
+
+def test_records_roundtrip():
+    rec = synthetic_records(100, seed=1)
+    d, i, l = wdm.records_to_tensors(rec)
+    back = wdm.tensors_to_records(d.numpy(), i.numpy(), l.numpy())
+    assert back.tobytes() == rec.numpy().tobytes()
+    assert set(np.unique(l.numpy())) <= {0.0, 1.0}
+
+
+def test_torch_trainer_learns():
+    torch.manual_seed(0)
+    tr = TorchWideDeepTrainer(wdm.WideDeepModel(seed=0), batch=256)
+    tr.set_data(synthetic_records(8192, seed=2))
+    losses = []
+    for _ in range(60):
+        tr.step()
+        losses.append(tr.last_loss() / 256)
+    assert np.mean(losses[-10:]) < np.mean(losses[:10]) - 0.02
+
+
+# ------------------------------------------------------------------------------------ GPU
+def _torch_grads(model, rec, reduction="sum"):
+    dense, ids, label = wdm.records_to_tensors(rec.cpu())
+    model.zero_grad()
+    loss = model.loss(dense, ids, label, reduction=reduction)
+    loss.backward()
+    g = {n: p.grad.detach().numpy().copy() for n, p in model.named_parameters()}
+    return float(loss), g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [40, 64, 1000, 8192])
+def test_fused_gradients_match_torch(batch):
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    m = wdm.WideDeepModel(seed=1)
+    with torch.no_grad():
+        m.wide.normal_(0, 0.3)
+        m.wide_bias.fill_(-0.2)
+        for lin in m.dnn:
+            lin.bias.normal_(0, 0.1)
+    rec = synthetic_records(batch, seed=7)
+    tr = FusedWideDeepTrainer(m, batch=batch, device=dev)
+    tr.set_data(rec.to(dev))
+    g_tn = tr.gradients_once()
+    torch.cuda.synchronize()
+    got = wdm.canonical_grad_to_torch(g_tn, m)
+    # reference uses the bf16-rounded weights the kernel computes with
+    mref = wdm.unpack_canonical(tr.param.cpu(), wdm.WideDeepModel(seed=1))
+    loss_ref, ref = _torch_grads(mref, rec)
+    assert abs(tr.slab_loss.sum().item() - loss_ref) <= 0.02 * abs(loss_ref) + 1e-3
+    for name, r in ref.items():
+        gk = got[name].reshape(r.shape)
+        scale = np.abs(r).max() + 1e-6
+        err = np.abs(gk - r).max() / scale
+        assert err < 0.05, f"{name}: rel max err {err:.4f} (scale {scale:.3g})"
+
+
+@pytest.mark.gpu
+def test_fused_step_matches_torch_trainer():
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(4096, seed=11)
+    ft = FusedWideDeepTrainer(wdm.WideDeepModel(seed=4), batch=512, device=dev)
+    ft.set_data(rec.to(dev))
+    tt = TorchWideDeepTrainer(wdm.WideDeepModel(seed=4), batch=512)
+    tt.set_data(rec)
+    for _ in range(5):
+        ft.step()
+        tt.step()
+    torch.cuda.synchronize()
+    assert ft.steps_done == 5
+    fm = ft.sync_to_model()
+    dense, ids, label = wdm.records_to_tensors(rec[:2048])
+    a = fm(dense, ids).detach()
+    b = tt.model(dense, ids).detach()
+    assert torch.corrcoef(torch.stack([a, b]))[0, 1] > 0.99
+    assert (a - b).abs().mean() < 0.05
+
+
+@pytest.mark.gpu
+def test_fused_training_converges_and_graph_replay():
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=0), batch=4096, device=dev, loss_reduction="mean",
+                              dnn_opt=OptSpec("adam", lr=3e-3), wide_opt=OptSpec("adam", lr=3e-2))
+    tr.set_data(synthetic_records(1 << 18, device=dev, seed=3))
+    tr.step()
+    first = tr.last_loss() / 4096
+    tr.capture()
+    for _ in range(200):
+        tr.step()
+    torch.cuda.synchronize()
+    last = tr.last_loss() / 4096
+    assert tr.steps_done >= 200
+    assert last < first - 0.03, (first, last)
+
+
+@pytest.mark.gpu
+def test_fused_predict_matches_torch():
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    m = wdm.WideDeepModel(seed=2)
+    with torch.no_grad():
+        m.wide.normal_(0, 0.5)
+    tr = FusedWideDeepTrainer(m, batch=64, device=dev)
+    rec = synthetic_records(5000, seed=8)
+    got = tr.predict_logits(rec.to(dev)).cpu()
+    mref = wdm.unpack_canonical(tr.param.cpu(), wdm.WideDeepModel(seed=2))
+    dense, ids, _ = wdm.records_to_tensors(rec)
+    ref = mref(dense, ids).detach()
+    assert (got - ref).abs().max() < 0.05 * (ref.abs().max() + 1)
