@@ -85,12 +85,59 @@ def _torch_grads(model, rec, reduction="sum"):
     loss = model.loss(dense, ids, label, reduction=reduction)
     loss.backward()
     g = {n: p.grad.detach().numpy().copy() for n, p in model.named_parameters()}
-    return float(loss), g
+    return float(loss.detach()), g
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _emulated_grads(vec, rec):
+    """fp32 emulation of the kernel's bf16 data path on the canonical padded layout
+    (bf16 weights/activations/activation-grads, fp32 accumulation)."""
+    vec = torch.as_tensor(vec, dtype=torch.float32)
+    dense, ids, label = wdm.records_to_tensors(rec.cpu())
+    B = len(label)
+    a = torch.zeros(B, wdm.LAYER_KN[0][0])
+    a[:, :3] = dense
+    a[:, 3] = 1.0
+    acts = [_bf(a)]
+    wts = []
+    for li, (K, N) in enumerate(wdm.LAYER_KN):
+        wt = _bf(vec[wdm.LAYER_OFF[li]:wdm.LAYER_OFF[li] + K * N].reshape(N, K))
+        wts.append(wt)
+        z = acts[-1][:, :K] @ wt.T
+        if li < 4:
+            acts.append(_bf(torch.relu(z)))
+        else:
+            deep = z[:, 0]
+    cfg = wdm.WideDeepConfig()
+    nb = torch.tensor([n for _, n in cfg.wide])
+    idc = torch.where(ids < nb, ids, torch.zeros_like(ids)) + torch.tensor(cfg.wide_offsets)
+    wvec = vec[wdm.WTOT:]
+    x = deep + wvec[idc].sum(1) + wvec[cfg.wide_rows]
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(x, label, reduction="sum")
+    dl = torch.sigmoid(x) - label
+    dz = torch.zeros(B, 16)
+    dz[:, 0] = dl
+    dz = _bf(dz)
+    grads = {}
+    for li in range(4, -1, -1):
+        grads[li] = dz.T @ acts[li]          # dWt [N][K]
+        if li > 0:
+            da = dz @ wts[li]                # [B][K]
+            dz = _bf(da * (acts[li] > 0).float())
+    gw = torch.zeros(wdm.NWIDE)
+    gw.index_add_(0, idc.reshape(-1), dl[:, None].expand(-1, 9).reshape(-1))
+    gw[cfg.wide_rows] = dl.sum()
+    canon = torch.cat([grads[li].reshape(-1) for li in range(5)] + [gw])
+    return float(loss), canon.numpy()
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", [40, 64, 1000, 8192])
 def test_fused_gradients_match_torch(batch):
+    torch.manual_seed(batch)
     from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
 
     dev = torch.device("cuda")
@@ -105,16 +152,27 @@ def test_fused_gradients_match_torch(batch):
     tr.set_data(rec.to(dev))
     g_tn = tr.gradients_once()
     torch.cuda.synchronize()
-    got = wdm.canonical_grad_to_torch(g_tn, m)
-    # reference uses the bf16-rounded weights the kernel computes with
+    gidx, mask = wdm.canonical_index_maps()
+    got = g_tn[gidx]
+    loss_em, em = _emulated_grads(tr.param.cpu(), rec)
+    # 1) exact data-path check against the bf16 emulation (only accumulation order differs)
+    msk = mask.astype(bool)
+    err = np.abs(got - em)[msk]
+    tol = 2e-3 * np.abs(em[msk]).max() + 1e-5
+    bad = np.argsort(-err)[:5]
+    assert err.max() <= tol, f"max err {err.max():.3g} > {tol:.3g}; worst canon idx {np.flatnonzero(msk)[bad]}"
+    assert abs(tr.slab_loss.sum().item() - loss_em) <= 1e-3 * abs(loss_em) + 1e-3
+    # 2) against the fp32 PyTorch model: relative Frobenius error per tensor. The bf16 data path
+    #    (inputs, activations, activation-grads rounded to 8 mantissa bits) costs a few % on the
+    #    first layer at tiny batches (cancellation over 40 examples), <3 % at >= 1000.
+    named = wdm.canonical_grad_to_torch(g_tn, m)
     mref = wdm.unpack_canonical(tr.param.cpu(), wdm.WideDeepModel(seed=1))
-    loss_ref, ref = _torch_grads(mref, rec)
-    assert abs(tr.slab_loss.sum().item() - loss_ref) <= 0.02 * abs(loss_ref) + 1e-3
+    _, ref = _torch_grads(mref, rec)
+    lim = 0.15 if batch < 1000 else 0.06
     for name, r in ref.items():
-        gk = got[name].reshape(r.shape)
-        scale = np.abs(r).max() + 1e-6
-        err = np.abs(gk - r).max() / scale
-        assert err < 0.05, f"{name}: rel max err {err:.4f} (scale {scale:.3g})"
+        gk = named[name].reshape(r.shape)
+        rel = np.linalg.norm(gk - r) / (np.linalg.norm(r) + 1e-8)
+        assert rel < lim, f"{name}: relative Frobenius err {rel:.4f}"
 
 
 @pytest.mark.gpu
