@@ -16,14 +16,25 @@
 //    in accumulator registers across ALL tiles the workgroup processes (MFMA K-accumulation
 //    == batch reduction). Operands with examples along K come from the row-major images
 //    through ds_read_b64_tr_b16 (hardware transpose), so no second image is written.
+//    Tile ownership is chosen per layer so each wave re-uses its dZ / activation fragments
+//    across the tiles it owns (104 transposed reads per wave per tile instead of 216).
+//  * Every phase issues all LDS operand reads of a batch before its MFMAs (and prefetches
+//    the next batch), so MFMAs do not each wait out a full LDS round trip.
 //  * Biases live in the weight matrices: each layer input carries a constant-1 column,
 //    so bias-add, bias-grad and the dense GEMM are one MFMA chain.
 //  * The wide (linear) part is an embedding-bag gather of 9 fp32 weights per example from
-//    the L2-resident table; its gradient is a ds_add_f32 histogram in LDS.
+//    the L2-resident table (issued before the forward so its latency hides under MFMAs);
+//    its gradient is a ds_add_f32 histogram in LDS.
+//  * Block barriers wait only on LDS (lgkmcnt) so the next tile's record prefetch stays in
+//    flight across them.
 //  * Each workgroup writes one fp32 gradient slab (tile-native order, fully coalesced);
 //    wd_reduce sums slabs, wd_optimizer applies Adagrad (DNN) / FTRL (wide) / Adam / SGD and
 //    re-emits the bf16 weight image. A device-side step counter drives the data offset so
 //    the whole step is hipGraph-capturable.
+//
+// MIFX_HIPCC_FLAGS: -fno-honor-nans -fno-honor-infinities -mllvm -amdgpu-mfma-vgpr-form
+// (no NaN canonicalisation v_max before every ReLU; MFMA results in VGPRs instead of
+//  AGPR->VGPR copies feeding the epilogues)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -82,7 +93,7 @@ constexpr int STRIDE = NTILE * 256 + WIDE_PAD;   // 29824 floats per slab
 constexpr int LDS_BYTES = LEND * 2 + WIDE_PAD * 4 + 64 * 4;
 static_assert(LDS_BYTES <= 163840, "LDS budget");
 
-// tile bases in tile-native order
+// tile bases in tile-native order (tile id = TB + nt * (K/16) + kt)
 constexpr int TB1 = 0, TB2 = TB1 + (N1 / 16) * (K1 / 16), TB3 = TB2 + (N2 / 16) * (K2 / 16),
               TB4 = TB3 + (N3 / 16) * (K3 / 16), TB5 = TB4 + (N4 / 16) * (K4 / 16);
 static_assert(TB5 + (N5 / 16) * (K5 / 16) == NTILE, "tile count");
@@ -91,13 +102,6 @@ static_assert(TB5 + (N5 / 16) * (K5 / 16) == NTILE, "tile count");
 // trip_start_hour (24), trip_start_day (31), trip_start_month (12)
 __constant__ int kWideOff[9] = {0, 1010, 2020, 2030, 2040, 2050, 2060, 2084, 2115};
 __constant__ int kWideNb[9] = {1010, 1010, 10, 10, 10, 10, 24, 31, 12};
-
-struct __attribute__((packed, aligned(16))) Rec {
-  float d[3];
-  uint16_t id[9];
-  uint16_t label;
-};
-static_assert(sizeof(Rec) == 32, "record is 32 B");
 
 __device__ __forceinline__ v4s tr_read(const uint16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
@@ -110,133 +114,218 @@ __device__ __forceinline__ v8bf ld8(const uint16_t* p) { return *(const v8bf*)p;
 __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+#ifdef WD_STAMPS  // diagnostic build only: per-wave s_memtime at phase boundaries of block 0
+__device__ unsigned long long g_stamps[4][32];
+#define STAMP(i)                                                                       \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    if (blockIdx.x == 0 && lane == 0 && stamp_on) g_stamps[w][i] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
+// Same-wave LDS write->read ordering: DS ops of one wave execute in order, so only the
+// compiler must be kept from reordering (no s_waitcnt, outstanding global loads survive).
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("" ::: "memory");
+}
+// Block barrier that waits for LDS traffic only (global prefetches stay in flight).
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // ---------------------------------------------------------------- forward layer (wave-local)
 // Z^T[n][t] = sum_k Wt[n][k] * A[t][k]; A rows t in [16w, 16w+16). RELU -> bf16 -> Aout.
-template <int K, int N, bool RELU_STORE>
-__device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, uint16_t* Aout,
-                                          int w, int r, int h, v4f* zlast) {
-  constexpr int KS = K / 32;
+// Weight fragments are read in batches of NB n-tiles, the next batch prefetched.
+template <int K, int N, bool LAST>
+__device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, uint16_t* Aout, int w, int r,
+                                          int h, v4f* zlast) {
+  constexpr int KS = K / 32, NT = N / 16;
+  constexpr int NB = KS >= 3 ? 2 : (KS == 2 ? 4 : 8);
+  constexpr int NBATCH = (NT + NB - 1) / NB;
   v8bf b[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) b[s] = ld8(A + (16 * w + r) * (K + PAD) + 32 * s + 8 * h);
+  v8bf wa[2][NB][KS];
 #pragma unroll
-  for (int nt = 0; nt < N / 16; ++nt) {
-    v4f acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NB; ++j)
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = mfma(ld8(W + (16 * nt + r) * (K + PAD) + 32 * s + 8 * h), b[s], acc);
-    if constexpr (RELU_STORE) {
-      v4bf o;
+    for (int s = 0; s < KS; ++s)
+      if (j < NT) wa[0][j][s] = ld8(W + (16 * j + r) * (K + PAD) + 32 * s + 8 * h);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = (bf16)fmaxf(acc[i], 0.f);
-      *(v4bf*)(Aout + (16 * w + r) * (N + PAD) + 16 * nt + 4 * h) = o;
-    } else {
-      *zlast = acc;
+  for (int bi = 0; bi < NBATCH; ++bi) {
+    if (bi + 1 < NBATCH) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int nt = (bi + 1) * NB + j;
+          if (nt < NT) wa[(bi + 1) & 1][j][s] = ld8(W + (16 * nt + r) * (K + PAD) + 32 * s + 8 * h);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int nt = bi * NB + j;
+      if (nt >= NT) continue;
+      v4f acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = mfma(wa[bi & 1][j][s], b[s], acc);
+      if constexpr (!LAST) {
+        v4bf o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)fmaxf(acc[i], 0.f);
+        *(v4bf*)(Aout + (16 * w + r) * (N + PAD) + 16 * nt + 4 * h) = o;
+      } else {
+        *zlast = acc;
+      }
     }
   }
 }
 
 // ------------------------------------------------------- activation gradient (wave-local)
 // dA^T[k][t] = sum_n W[k][n] dZ^T[n][t]   (W = layer with dims K x N, stored as Wt[N][K])
-// dZout[t][k] = dA[t][k] * (Aact[t][k] > 0)
+// dZout[t][k] = dA[t][k] * (Aact[t][k] > 0). Weight fragments via transposed reads, batched.
 template <int K, int N>
-__device__ __forceinline__ void bwd_dA(const uint16_t* W, const uint16_t* dZ, const uint16_t* Aact,
-                                       uint16_t* dZout, int w, int r, int h) {
-  constexpr int NS = (N + 31) / 32;
+__device__ __forceinline__ void bwd_dA(const uint16_t* W, const uint16_t* dZ, const uint16_t* Aact, uint16_t* dZout,
+                                       int w, int r, int h) {
+  constexpr int NS = (N + 31) / 32, KT = K / 16;
+  constexpr int KB = NS >= 3 ? 2 : 4;
+  constexpr int NBATCH = (KT + KB - 1) / KB;
   const int q = r >> 2, p = r & 3;
+  const bool live = (N % 32 == 0) || (8 * h < N % 32);  // only the last k-step can be partial
   v8bf b[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     v8bf v = ld8(dZ + (16 * w + r) * (N + PAD) + 32 * s + 8 * h);
-    if (N % 32 != 0 && 32 * s + 8 * h >= N) v = (v8bf){};
+    if (s == NS - 1 && !live) v = (v8bf){};
     b[s] = v;
   }
+  v8bf wa[2][KB][NS];
+  auto load = [&](int buf, int bi) {
 #pragma unroll
-  for (int kt = 0; kt < K / 16; ++kt) {
-    v4f acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < KB; ++j)
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint16_t* pa = W + (32 * s + 8 * h + q) * (K + PAD) + 16 * kt + 4 * p;
-      v8bf a = cat8(tr_read(pa), tr_read(pa + 4 * (K + PAD)));
-      if (N % 32 != 0 && 32 * s + 8 * h >= N) a = (v8bf){};
-      acc = mfma(a, b[s], acc);
+      for (int s = 0; s < NS; ++s) {
+        const int kt = bi * KB + j;
+        if (kt < KT) {
+          const uint16_t* pa = W + (32 * s + 8 * h + q) * (K + PAD) + 16 * kt + 4 * p;
+          v8bf a = cat8(tr_read(pa), tr_read(pa + 4 * (K + PAD)));
+          if (s == NS - 1 && !live) a = (v8bf){};
+          wa[buf][j][s] = a;
+        }
+      }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int bi = 0; bi < NBATCH; ++bi) {
+    if (bi + 1 < NBATCH) load((bi + 1) & 1, bi + 1);
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      const int kt = bi * KB + j;
+      if (kt >= KT) continue;
+      v4f acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc = mfma(wa[bi & 1][j][s], b[s], acc);
+      const int off = (16 * w + r) * (K + PAD) + 16 * kt + 4 * h;
+      const uint2 m = *(const uint2*)(Aact + off);
+      v4bf o;
+      o[0] = (bf16)((m.x & 0xffffu) ? acc[0] : 0.f);
+      o[1] = (bf16)((m.x >> 16) ? acc[1] : 0.f);
+      o[2] = (bf16)((m.y & 0xffffu) ? acc[2] : 0.f);
+      o[3] = (bf16)((m.y >> 16) ? acc[3] : 0.f);
+      *(v4bf*)(dZout + off) = o;
     }
-    const int off = (16 * w + r) * (K + PAD) + 16 * kt + 4 * h;
-    const uint2 m = *(const uint2*)(Aact + off);
-    const uint16_t mk[4] = {(uint16_t)(m.x & 0xffff), (uint16_t)(m.x >> 16), (uint16_t)(m.y & 0xffff),
-                            (uint16_t)(m.y >> 16)};
-    v4bf o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (bf16)(mk[i] ? acc[i] : 0.f);
-    *(v4bf*)(dZout + off) = o;
   }
 }
 
 // ------------------------------------------------------------- weight gradient (cooperative)
-// dWt[n][k] += sum_t dZ[t][n] * A[t][k] over the 64 tile rows; wave w owns tiles
-// [w*CNT, (w+1)*CNT) of this layer (row-major over (nt, kt)).
-template <int K, int N, int CNT>
-__device__ __forceinline__ void dw_phase(v4f (&acc)[CNT], const uint16_t* dZ, const uint16_t* A,
-                                         int w, int r, int h) {
-  constexpr int KT = K / 16;
+// dWt[n][k] += sum_t dZ[t][n] * A[t][k] over the 64 tile rows. The wave owns the NTW x KTW
+// tiles nt = nt0 + i*ntS, kt = kt0 + j*ktS; all operand fragments are loaded first (each
+// dZ n-block once, each activation k-block once), then 2*NTW*KTW MFMAs.
+template <int K, int N, int NTW, int KTW>
+__device__ __forceinline__ void dw_phase(v4f (&acc)[NTW * KTW], const uint16_t* dZ, const uint16_t* A, int nt0,
+                                         int ntS, int kt0, int ktS, int r, int h) {
   const int q = r >> 2, p = r & 3;
+  v8bf fa[NTW][2], fb[KTW][2];
 #pragma unroll
-  for (int j = 0; j < CNT; ++j) {
-    const int idx = w * CNT + j;
-    const int nt = idx / KT, kt = idx % KT;
+  for (int i = 0; i < NTW; ++i)
 #pragma unroll
-    for (int s = 0; s < T / 32; ++s) {
-      const uint16_t* pa = dZ + (32 * s + 8 * h + q) * (N + PAD) + 16 * nt + 4 * p;
-      const uint16_t* pb = A + (32 * s + 8 * h + q) * (K + PAD) + 16 * kt + 4 * p;
-      v8bf a = cat8(tr_read(pa), tr_read(pa + 4 * (N + PAD)));
-      v8bf b = cat8(tr_read(pb), tr_read(pb + 4 * (K + PAD)));
-      acc[j] = mfma(a, b, acc[j]);
+    for (int s = 0; s < 2; ++s) {
+      const uint16_t* pa = dZ + (32 * s + 8 * h + q) * (N + PAD) + 16 * (nt0 + i * ntS) + 4 * p;
+      fa[i][s] = cat8(tr_read(pa), tr_read(pa + 4 * (N + PAD)));
     }
-  }
+#pragma unroll
+  for (int j = 0; j < KTW; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint16_t* pb = A + (32 * s + 8 * h + q) * (K + PAD) + 16 * (kt0 + j * ktS) + 4 * p;
+      fb[j][s] = cat8(tr_read(pb), tr_read(pb + 4 * (K + PAD)));
+    }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int j = 0; j < KTW; ++j) acc[i * KTW + j] = mfma(fa[i][s], fb[j][s], acc[i * KTW + j]);
 }
 
-template <int CNT>
-__device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[CNT], int tbase, int w, int lane) {
+template <int K, int NTW, int KTW>
+__device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NTW * KTW], int tbase, int nt0, int ntS,
+                                            int kt0, int ktS, int lane) {
 #pragma unroll
-  for (int j = 0; j < CNT; ++j) {
-    float* dst = slab + (size_t)(tbase + w * CNT + j) * 256 + lane;
+  for (int i = 0; i < NTW; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dst[i * 64] = acc[j][i];
-  }
+    for (int j = 0; j < KTW; ++j) {
+      const int tile = tbase + (nt0 + i * ntS) * (K / 16) + kt0 + j * ktS;
+      float* dst = slab + (size_t)tile * 256 + lane;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[e * 64] = acc[i * KTW + j][e];
+    }
 }
 
-__device__ __forceinline__ void wt_locate(int e, int& lofs, int& k, int& n, int& K) {
-  int base;
-  if (e < OFF2) { base = OFF1; K = K1; lofs = LW1; }
-  else if (e < OFF3) { base = OFF2; K = K2; lofs = LW2; }
-  else if (e < OFF4) { base = OFF3; K = K3; lofs = LW3; }
-  else if (e < OFF5) { base = OFF4; K = K4; lofs = LW4; }
-  else { base = OFF5; K = K5; lofs = LW5; }
-  n = (e - base) / K;
-  k = (e - base) % K;
+template <int BASE, int K, int LOFS>
+__device__ __forceinline__ int wt_off(int e) {  // constant divisor per layer
+  return LOFS + ((e - BASE) / K) * (K + PAD) + (e - BASE) % K;
+}
+__device__ __forceinline__ int wt_lds_offset(int e) {
+  if (e < OFF2) return wt_off<OFF1, K1, LW1>(e);
+  if (e < OFF3) return wt_off<OFF2, K2, LW2>(e);
+  if (e < OFF4) return wt_off<OFF3, K3, LW3>(e);
+  if (e < OFF5) return wt_off<OFF4, K4, LW4>(e);
+  return wt_off<OFF5, K5, LW5>(e);
 }
 
 template <bool TRAIN>
 __global__ __launch_bounds__(NTHR, 1) void wd_fused(
-    const Rec* __restrict__ data, long long n_data, long long batch, long long start_fixed,
+    const uint4* __restrict__ data, long long n_data, long long batch, long long start_fixed,
     const long long* __restrict__ step_ctr, const uint16_t* __restrict__ wt, const float* __restrict__ wide,
-    float* __restrict__ slab, float* __restrict__ slab_loss, float* __restrict__ logits_out,
-    float grad_scale) {
+    float* __restrict__ slab, float* __restrict__ slab_loss, float* __restrict__ logits_out, float grad_scale) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LEND);
   float* red = wgrad + WIDE_PAD;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
+#ifdef WD_STAMPS
+  if (blockIdx.x == 0 && lane == 0) g_stamps[w][0] = __builtin_amdgcn_s_memtime();
+#endif
 
-  // stage the bf16 weight image (canonical [N][K] per layer) into padded LDS rows
-  for (int c = tid; c < WTOT / 8; c += NTHR) {
-    int lofs, k, n, K;
-    wt_locate(c * 8, lofs, k, n, K);
-    *(uint4*)(lds + lofs + n * (K + PAD) + k) = *(const uint4*)(wt + c * 8);
+  // stage the bf16 weight image: issue all global loads, then all LDS stores
+  {
+    constexpr int NCH = WTOT / 8, PER = (NCH + NTHR - 1) / NTHR;
+    uint4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = *(const uint4*)(wt + min(tid + i * NTHR, NCH - 1) * 8);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NTHR;
+      if (c < NCH) *(uint4*)(lds + wt_lds_offset(c * 8)) = v[i];
+    }
   }
   for (int c = tid; c < T * (K1 + PAD) / 8; c += NTHR) *(uint4*)(lds + LA0 + c * 8) = make_uint4(0, 0, 0, 0);
   if (TRAIN) {
@@ -244,10 +333,15 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     for (int c = tid; c < T * (N5 + PAD) / 8; c += NTHR) *(uint4*)(lds + LD5 + c * 8) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
+  bool stamp_on = true;
+  (void)stamp_on;
+  STAMP(1);
 
   const long long start = step_ctr ? (step_ctr[0] * batch) % n_data : start_fixed;
-  const long long ntiles = (batch + T - 1) / T;
+  const int ntiles = (int)((batch + T - 1) / T);
 
+  // dW tile ownership (see dw_phase): L1 nt{w,w+4} x kt{0,1}; L2 nt{0..5} x kt{2w,2w+1};
+  // L3 nt{w} x kt{0..5}; L4 nt{w} x kt{0..3}; L5 nt{0} x kt{w}
   v4f acc1[4], acc2[12], acc3[6], acc4[4], acc5[1];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc1[j] = acc4[j] = (v4f){0.f, 0.f, 0.f, 0.f};
@@ -267,59 +361,71 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   uint16_t* P = lds + LP;
   uint16_t* Q = lds + LQ;
 
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const long long row = tile * T + 16 * w + r;
-    const bool valid = row < batch;
+  // Branch-free record fetch (a conditional load makes hipcc drain vmcnt at the join, which
+  // would serialise the prefetch). Rows past the batch read a valid record; they carry
+  // dl = 0 and are excluded from loss and wide-gradient, so they contribute nothing.
+  auto fetch = [&](int tile, uint4& a, uint4& b) {
+    const long long row = min((long long)tile * T + 16 * w + r, batch - 1);
     long long di = start + row;
-    di = di % n_data;
-    uint4 u0 = make_uint4(0, 0, 0, 0), u1 = make_uint4(0, 0, 0, 0);
-    if (valid) {
-      const uint4* src = (const uint4*)(data + di);
-      u0 = src[0];
-      u1 = src[1];
-    }
-    const float d0 = __uint_as_float(u0.x), d1 = __uint_as_float(u0.y), d2 = __uint_as_float(u0.z);
-    const uint32_t idw[5] = {u0.w, u1.x, u1.y, u1.z, u1.w};
-    if (h == 0) {
-      v8bf x = {(bf16)d0, (bf16)d1, (bf16)d2, (bf16)1.0f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-      *(v8bf*)(A0 + (16 * w + r) * (K1 + PAD)) = x;
-    }
-    wave_sync();
-    v4f z5;
-    fwd_layer<K1, N1, true>(lds + LW1, A0, A1, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K2, N2, true>(lds + LW2, A1, A2, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K3, N3, true>(lds + LW3, A2, A3, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K4, N4, true>(lds + LW4, A3, A4, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K5, N5, false>(lds + LW5, A4, nullptr, w, r, h, &z5);
+    if (di >= n_data) di -= n_data;  // host guarantees batch <= n_data
+    a = data[2 * di];
+    b = data[2 * di + 1];
+  };
+  uint4 nu0, nu1;
+  fetch(blockIdx.x, nu0, nu1);
 
-    // ---- wide part + loss (every lane recomputes for example r; lane h==0 owns it)
-    const float zd = __shfl(z5[0], r);
-    float wl = wide[WIDE_BIAS];
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long row = (long long)tile * T + 16 * w + r;
+    const bool valid = row < batch;
+    const uint4 u0 = nu0, u1 = nu1;
+    fetch(tile + gridDim.x, nu0, nu1);  // prefetch the next tile's records
+
+    const uint32_t idw[5] = {u0.w, u1.x, u1.y, u1.z, u1.w};
     int ids[9];
+    float wv[9];
 #pragma unroll
     for (int f = 0; f < 9; ++f) {
       int id = (f & 1) ? (idw[f >> 1] >> 16) : (idw[f >> 1] & 0xffff);
       id = id < kWideNb[f] ? id : 0;
       ids[f] = kWideOff[f] + id;
-      wl += wide[ids[f]];
+      wv[f] = wide[ids[f]];  // issued now, consumed after the forward
     }
-    const float x = zd + wl;
+    const float wbias = wide[WIDE_BIAS];
+    if (h == 0) {
+      v8bf x = {(bf16)__uint_as_float(u0.x), (bf16)__uint_as_float(u0.y), (bf16)__uint_as_float(u0.z),
+                (bf16)1.0f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      *(v8bf*)(A0 + (16 * w + r) * (K1 + PAD)) = x;
+    }
+    wave_sync();
+    v4f z5;
+    fwd_layer<K1, N1, false>(lds + LW1, A0, A1, w, r, h, nullptr);
+    wave_sync();
+    fwd_layer<K2, N2, false>(lds + LW2, A1, A2, w, r, h, nullptr);
+    wave_sync();
+    fwd_layer<K3, N3, false>(lds + LW3, A2, A3, w, r, h, nullptr);
+    wave_sync();
+    fwd_layer<K4, N4, false>(lds + LW4, A3, A4, w, r, h, nullptr);
+    wave_sync();
+    fwd_layer<K5, N5, true>(lds + LW5, A4, nullptr, w, r, h, &z5);
+    STAMP(2);
+
+    // ---- wide part + loss (every lane recomputes for example r; lane h==0 owns it)
+    float wl = wbias;
+#pragma unroll
+    for (int f = 0; f < 9; ++f) wl += wv[f];
+    const float x = __shfl(z5[0], r) + wl;
     const float y = (float)(idw[4] >> 16);
+    const float lossv = fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
     if (!TRAIN) {
-      if (h == 0 && valid) logits_out[row] = x;
-      if (h == 0 && valid) loss_sum += fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
+      if (h == 0 && valid) {
+        logits_out[row] = x;
+        loss_sum += lossv;
+      }
       continue;
     }
-    float dl = 0.f;
-    if (valid) {
-      if (h == 0) loss_sum += fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
-      dl = (1.f / (1.f + __expf(-x)) - y) * grad_scale;
-    }
+    const float dl = valid ? (1.f / (1.f + __expf(-x)) - y) * grad_scale : 0.f;
     if (h == 0 && valid) {
+      loss_sum += lossv;
 #pragma unroll
       for (int f = 0; f < 9; ++f) atomicAdd(&wgrad[ids[f]], dl);
       dl_sum += dl;
@@ -329,20 +435,35 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
       *(v4bf*)(D5 + (16 * w + r) * (N5 + PAD) + 4 * h) = o;
     }
     wave_sync();
+    STAMP(3);
     bwd_dA<K5, N5>(lds + LW5, D5, A4, P, w, r, h);   // dz4 -> P
-    __syncthreads();                                  // B1
-    dw_phase<K5, N5, 1>(acc5, D5, A4, w, r, h);
-    dw_phase<K4, N4, 4>(acc4, P, A3, w, r, h);
+    STAMP(4);
+    block_sync_lds();                                 // B1
+    STAMP(5);
+    dw_phase<K5, N5, 1, 1>(acc5, D5, A4, 0, 0, w, 0, r, h);
+    dw_phase<K4, N4, 1, 4>(acc4, P, A3, w, 0, 0, 1, r, h);
+    STAMP(6);
     bwd_dA<K4, N4>(lds + LW4, P, A3, Q, w, r, h);    // dz3 -> Q
-    __syncthreads();                                  // B2
-    dw_phase<K3, N3, 6>(acc3, Q, A2, w, r, h);
+    STAMP(7);
+    block_sync_lds();                                 // B2
+    STAMP(8);
+    dw_phase<K3, N3, 1, 6>(acc3, Q, A2, w, 0, 0, 1, r, h);
+    STAMP(9);
     bwd_dA<K3, N3>(lds + LW3, Q, A2, P, w, r, h);    // dz2 -> P
-    __syncthreads();                                  // B3
-    dw_phase<K2, N2, 12>(acc2, P, A1, w, r, h);
+    STAMP(10);
+    block_sync_lds();                                 // B3
+    STAMP(11);
+    dw_phase<K2, N2, 6, 2>(acc2, P, A1, 0, 1, 2 * w, 1, r, h);
+    STAMP(12);
     bwd_dA<K2, N2>(lds + LW2, P, A1, Q, w, r, h);    // dz1 -> Q
-    __syncthreads();                                  // B4
-    dw_phase<K1, N1, 4>(acc1, Q, A0, w, r, h);
-    __syncthreads();                                  // B5
+    STAMP(13);
+    block_sync_lds();                                 // B4
+    STAMP(14);
+    dw_phase<K1, N1, 2, 2>(acc1, Q, A0, w, 4, 0, 1, r, h);
+    STAMP(15);
+    block_sync_lds();                                 // B5
+    STAMP(16);
+    stamp_on = false;
   }
 
   // ---- epilogue: per-workgroup slab
@@ -350,14 +471,17 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     loss_sum += __shfl_xor(loss_sum, o);
     dl_sum += __shfl_xor(dl_sum, o);
   }
-  if (lane == 0) { red[w] = loss_sum; red[4 + w] = dl_sum; }
+  if (lane == 0) {
+    red[w] = loss_sum;
+    red[4 + w] = dl_sum;
+  }
   if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * STRIDE;
-    store_tiles<4>(my, acc1, TB1, w, lane);
-    store_tiles<12>(my, acc2, TB2, w, lane);
-    store_tiles<6>(my, acc3, TB3, w, lane);
-    store_tiles<4>(my, acc4, TB4, w, lane);
-    store_tiles<1>(my, acc5, TB5, w, lane);
+    store_tiles<K1, 2, 2>(my, acc1, TB1, w, 4, 0, 1, lane);
+    store_tiles<K2, 6, 2>(my, acc2, TB2, 0, 1, 2 * w, 1, lane);
+    store_tiles<K3, 1, 6>(my, acc3, TB3, w, 0, 0, 1, lane);
+    store_tiles<K4, 1, 4>(my, acc4, TB4, w, 0, 0, 1, lane);
+    store_tiles<K5, 1, 1>(my, acc5, TB5, 0, 0, w, 0, lane);
   }
   __syncthreads();
   if (TRAIN) {
@@ -369,9 +493,11 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     }
   }
   if (tid == 0 && slab_loss) slab_loss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  stamp_on = true;
+  STAMP(17);
 }
 
-// partial[sp][e] = sum_{g in split sp} slab[g][e]   (float4 granules)
+// partial[sp][e] = sum_{g in split sp} slab[g][e]   (float4 granules, 4 loads in flight)
 __global__ __launch_bounds__(256) void wd_reduce(const float4* __restrict__ slab, int G, int gchunk,
                                                  float4* __restrict__ partial) {
   constexpr int S4 = STRIDE / 4;
@@ -379,24 +505,61 @@ __global__ __launch_bounds__(256) void wd_reduce(const float4* __restrict__ slab
   if (e >= S4) return;
   const int g0 = blockIdx.y * gchunk;
   const int g1 = min(G, g0 + gchunk);
-  float4 a = make_float4(0, 0, 0, 0), b = a;
+  float4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = make_float4(0, 0, 0, 0);
   int g = g0;
-  for (; g + 1 < g1; g += 2) {
-    float4 u = slab[(size_t)g * S4 + e], v = slab[(size_t)(g + 1) * S4 + e];
-    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  for (; g + 3 < g1; g += 4) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = slab[(size_t)(g + u) * S4 + e];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+    }
   }
-  if (g < g1) {
-    float4 u = slab[(size_t)g * S4 + e];
-    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+  for (; g < g1; ++g) {
+    const float4 v = slab[(size_t)g * S4 + e];
+    acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
   }
-  partial[(size_t)blockIdx.y * S4 + e] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  partial[(size_t)blockIdx.y * S4 + e] =
+      make_float4(acc[0].x + acc[1].x + acc[2].x + acc[3].x, acc[0].y + acc[1].y + acc[2].y + acc[3].y,
+                  acc[0].z + acc[1].z + acc[2].z + acc[3].z, acc[0].w + acc[1].w + acc[2].w + acc[3].w);
 }
 
 struct OptHyper {
   int kind;        // 0 sgd, 1 adagrad, 2 ftrl, 3 adam
   float lr, beta1, beta2, eps, l1, l2, lr_power;
 };
+
+__device__ __forceinline__ float opt_update(const OptHyper& hp, float w, float g, float& a0, float& a1,
+                                            long long step) {
+  if (hp.kind == 0) return w - hp.lr * g;
+  if (hp.kind == 1) {
+    a0 += g * g;
+    return w - hp.lr * g * rsqrtf(a0);
+  }
+  if (hp.kind == 2) {  // TF ApplyFtrl
+    const float a = a0, an = a + g * g;
+    float sq_new, sq_old;
+    if (hp.lr_power == -0.5f) {
+      sq_new = sqrtf(an);
+      sq_old = sqrtf(a);
+    } else {
+      sq_new = powf(an, -hp.lr_power);
+      sq_old = powf(a, -hp.lr_power);
+    }
+    a1 += g - (sq_new - sq_old) / hp.lr * w;
+    const float quad = sq_new / hp.lr + 2.f * hp.l2;
+    a0 = an;
+    return fabsf(a1) > hp.l1 ? (copysignf(hp.l1, a1) - a1) / quad : 0.f;
+  }
+  a0 = hp.beta1 * a0 + (1.f - hp.beta1) * g;
+  a1 = hp.beta2 * a1 + (1.f - hp.beta2) * g * g;
+  const float bc1 = 1.f - powf(hp.beta1, (float)step);
+  const float bc2 = 1.f - powf(hp.beta2, (float)step);
+  return w - hp.lr * (a0 / bc1) / (sqrtf(a1 / bc2) + hp.eps);
+}
 
 // One thread per canonical parameter. DNN segment [0, WTOT) then wide segment [WTOT, WTOT+NWIDE).
 __global__ __launch_bounds__(256) void wd_optimizer(
@@ -407,39 +570,21 @@ __global__ __launch_bounds__(256) void wd_optimizer(
   const long long step = step_ctr[0] + 1;
   if (c < WTOT + NWIDE) {
     const bool dnn = c < WTOT;
-    const OptHyper& hp = dnn ? hd : hw;
     float w = param[c];
     if (mask[c]) {
       const int gi = gidx[c];
-      float g = 0.f;
-      for (int pidx = 0; pidx < nparts; ++pidx) g += partial[(size_t)pidx * STRIDE + gi];
-      if (hp.kind == 0) {
-        w -= hp.lr * g;
-      } else if (hp.kind == 1) {
-        float a = s0[c] + g * g;
-        s0[c] = a;
-        w -= hp.lr * g * rsqrtf(a);
-      } else if (hp.kind == 2) {
-        const float a = s0[c];
-        const float an = a + g * g;
-        float lin = s1[c];
-        float sq_new, sq_old;
-        if (hp.lr_power == -0.5f) { sq_new = sqrtf(an); sq_old = sqrtf(a); }
-        else { sq_new = powf(an, -hp.lr_power); sq_old = powf(a, -hp.lr_power); }
-        lin += g - (sq_new - sq_old) / hp.lr * w;
-        const float quad = sq_new / hp.lr + 2.f * hp.l2;
-        w = fabsf(lin) > hp.l1 ? (copysignf(hp.l1, lin) - lin) / quad : 0.f;
-        s0[c] = an;
-        s1[c] = lin;
-      } else {
-        float m = hp.beta1 * s0[c] + (1.f - hp.beta1) * g;
-        float v = hp.beta2 * s1[c] + (1.f - hp.beta2) * g * g;
-        s0[c] = m;
-        s1[c] = v;
-        const float bc1 = 1.f - powf(hp.beta1, (float)step);
-        const float bc2 = 1.f - powf(hp.beta2, (float)step);
-        w -= hp.lr * (m / bc1) / (sqrtf(v / bc2) + hp.eps);
+      float gs[4] = {0.f, 0.f, 0.f, 0.f};
+      int pidx = 0;
+      for (; pidx + 3 < nparts; pidx += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gs[u] += partial[(size_t)(pidx + u) * STRIDE + gi];
       }
+      for (; pidx < nparts; ++pidx) gs[0] += partial[(size_t)pidx * STRIDE + gi];
+      const float g = (gs[0] + gs[1]) + (gs[2] + gs[3]);
+      float a0 = s0[c], a1 = s1[c];
+      w = opt_update(dnn ? hd : hw, w, g, a0, a1, step);
+      s0[c] = a0;
+      s1[c] = a1;
       param[c] = w;
     }
     if (dnn) wt_out[c] = __builtin_bit_cast(uint16_t, (bf16)w);
@@ -464,16 +609,16 @@ int mifx_wd_fused(const void* data, long long n_data, long long batch, long long
                   float* logits_out, float grad_scale, int grid, int train, hipStream_t stream) {
   static bool attr_done = false;
   if (!attr_done) {
-    hipFuncSetAttribute((const void*)wd_fused<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    hipFuncSetAttribute((const void*)wd_fused<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)wd_fused<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)wd_fused<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_done = true;
   }
-  if (grid <= 0 || n_data <= 0 || batch <= 0) return -1;
+  if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data) return -1;
   if (train)
-    hipLaunchKernelGGL(wd_fused<true>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const Rec*)data, n_data, batch,
+    hipLaunchKernelGGL(wd_fused<true>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
                        start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale);
   else
-    hipLaunchKernelGGL(wd_fused<false>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const Rec*)data, n_data, batch,
+    hipLaunchKernelGGL(wd_fused<false>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
                        start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale);
   return (int)hipGetLastError();
 }
@@ -498,5 +643,11 @@ int mifx_wd_optimizer(const float* partial, int nparts, const int* gidx, const u
                      s1, (uint16_t*)wt_out, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
+
+#ifdef WD_STAMPS
+int mifx_wd_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // extern "C"

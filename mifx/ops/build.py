@@ -41,6 +41,14 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (expected /opt/rocm/bin/hipcc)")
 
 
+def _file_flags(src: Path) -> list[str]:
+    """Per-file extra flags from a `// MIFX_HIPCC_FLAGS: ...` line in the source."""
+    for line in src.read_text().splitlines()[:80]:
+        if line.startswith("// MIFX_HIPCC_FLAGS:"):
+            return line.split(":", 1)[1].split()
+    return []
+
+
 def _needs_build(src: Path, out: Path) -> bool:
     if not out.exists():
         return True
@@ -54,7 +62,7 @@ def _build_one(src: Path, force: bool) -> tuple[str, str]:
         return src.name, "up-to-date"
     tmp = out.with_suffix(".so.tmp")
     if src.suffix == ".hip":
-        cmd = [hipcc()] + HIP_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp)]
+        cmd = [hipcc()] + HIP_FLAGS + _file_flags(src) + ["-I", str(CSRC), str(src), "-o", str(tmp)]
     else:
         cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp), "-lz"]
     res = subprocess.run(cmd, capture_output=True, text=True)
