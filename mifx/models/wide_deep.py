@@ -245,6 +245,16 @@ def records_to_tensors(rec: np.ndarray | torch.Tensor):
             torch.from_numpy(rec["label"].astype(np.float32)))
 
 
+def pack_transformed_columns(cols: dict, cfg: WideDeepConfig | None = None, with_label: bool = True) -> np.ndarray:
+    """Transform outputs (dict of columns, `taxi_utils.py:106-145` names) -> packed 32-B records."""
+    cfg = cfg or WideDeepConfig()
+    n = len(next(iter(cols.values())))
+    dense = np.stack([np.asarray(cols[k], np.float32) for k in cfg.dense_features], 1) if n else np.zeros((0, 3))
+    ids = np.stack([np.asarray(cols[k], np.int64) for k, _ in cfg.wide], 1) if n else np.zeros((0, 9))
+    label = np.asarray(cols[cfg.label], np.int64) if with_label and cfg.label in cols else np.zeros(n, np.int64)
+    return tensors_to_records(dense, ids, label)
+
+
 def tensors_to_records(dense, ids, label) -> np.ndarray:
     n = len(label)
     rec = np.zeros(n, RECORD_DTYPE)

@@ -64,7 +64,7 @@ def _build_one(src: Path, force: bool) -> tuple[str, str]:
     if src.suffix == ".hip":
         cmd = [hipcc()] + HIP_FLAGS + _file_flags(src) + ["-I", str(CSRC), str(src), "-o", str(tmp)]
     else:
-        cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp), "-lz"]
+        cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"build of {src.name} failed:\n{' '.join(cmd)}\n{res.stdout}\n{res.stderr}")

@@ -1,0 +1,251 @@
+"""Estimator-style training API used by Trainer user modules (`trainer_fn(hparams, schema)`).
+
+Reference: `airflow-dags/taxi_utils.py:285-356` — `RunConfig(save_checkpoints_steps=999,
+keep_checkpoint_max=1).replace(model_dir=serving_model_dir)`, `TrainSpec(input_fn, max_steps)`,
+`EvalSpec(input_fn, steps, exporters=[FinalExporter('chicago-taxi', serving_receiver_fn)])`,
+`DNNLinearCombinedClassifier(... warm_start_from=...)` and `train_and_evaluate`. Our estimator
+trains on the fused gfx950 step when a GPU is visible (PyTorch reference path otherwise),
+checkpoints to `model_dir` (safetensors, keep_checkpoint_max), and exports the
+SavedModel-equivalent directories consumed by Evaluator / Pusher / serving.
+"""
+from __future__ import annotations
+
+import dataclasses
+import glob
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable
+
+import numpy as np
+import torch
+from safetensors.torch import load_file, save_file
+
+from ..models import wide_deep as wdm
+
+
+@dataclass
+class RunConfig:
+    model_dir: str | None = None
+    save_checkpoints_steps: int | None = 999
+    keep_checkpoint_max: int = 1
+    tf_random_seed: int = 0
+    device: str | None = None
+
+    def replace(self, **kw) -> "RunConfig":
+        return dataclasses.replace(self, **kw)
+
+
+@dataclass
+class TrainSpec:
+    input_fn: Callable
+    max_steps: int
+
+
+@dataclass
+class EvalSpec:
+    input_fn: Callable
+    steps: int | None = None
+    exporters: list = field(default_factory=list)
+    name: str | None = None
+
+
+@dataclass
+class FinalExporter:
+    name: str
+    serving_input_receiver_fn: Callable
+
+    def export(self, estimator, export_path: str) -> str:
+        return estimator.export_saved_model(export_path, self.serving_input_receiver_fn)
+
+
+class HParams:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def values(self) -> dict:
+        return dict(self.__dict__)
+
+
+def _default_device(cfg: RunConfig) -> torch.device:
+    if cfg.device:
+        return torch.device(cfg.device)
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+def _auc(labels: np.ndarray, scores: np.ndarray) -> float:
+    pos = labels > 0.5
+    npos, nneg = int(pos.sum()), int((~pos).sum())
+    if npos == 0 or nneg == 0:
+        return float("nan")
+    order = np.argsort(scores, kind="mergesort")
+    ranks = np.empty(len(scores))
+    ranks[order] = np.arange(1, len(scores) + 1)
+    # average ranks for ties
+    s = scores[order]
+    i = 0
+    while i < len(s):
+        j = i
+        while j + 1 < len(s) and s[j + 1] == s[i]:
+            j += 1
+        if j > i:
+            ranks[order[i:j + 1]] = (i + j + 2) / 2.0
+        i = j + 1
+    return float((ranks[pos].sum() - npos * (npos + 1) / 2) / (npos * nneg))
+
+
+class WideDeepEstimator:
+    """DNNLinearCombinedClassifier equivalent for the taxi feature set."""
+
+    def __init__(self, config: RunConfig, hidden_units: list[int] | None = None, warm_start_from: str | None = None,
+                 batch_size: int = 40, loss_reduction: str = "sum", dnn_optimizer=None, linear_optimizer=None):
+        self.config = config
+        self.cfg = wdm.WideDeepConfig(hidden_units=list(hidden_units or wdm.dnn_hidden_units()))
+        self.device = _default_device(config)
+        self.batch_size = batch_size
+        self.loss_reduction = loss_reduction
+        self.dnn_optimizer, self.linear_optimizer = dnn_optimizer, linear_optimizer
+        self.model = wdm.WideDeepModel(self.cfg, seed=config.tf_random_seed)
+        self.global_step = 0
+        if warm_start_from:
+            self._load_weights(warm_start_from)
+        elif config.model_dir and self.latest_checkpoint():
+            self._restore(self.latest_checkpoint())
+        self._trainer = None
+
+    # ------------------------------------------------------------------ checkpoints
+    def latest_checkpoint(self) -> str | None:
+        if not self.config.model_dir:
+            return None
+        c = sorted(glob.glob(os.path.join(self.config.model_dir, "ckpt-*.safetensors")),
+                   key=lambda p: int(p.rsplit("-", 1)[1].split(".")[0]))
+        return c[-1] if c else None
+
+    def _restore(self, path: str) -> None:
+        sd = load_file(path)
+        self.global_step = int(sd.pop("global_step").item()) if "global_step" in sd else 0
+        self.model.load_state_dict({k: v for k, v in sd.items() if not k.startswith("opt.")}, strict=False)
+        self._opt_state = {k[4:]: v for k, v in sd.items() if k.startswith("opt.")}
+
+    def _load_weights(self, path: str) -> None:
+        if os.path.isdir(path):
+            cand = glob.glob(os.path.join(path, "**", "variables.safetensors"), recursive=True) or \
+                glob.glob(os.path.join(path, "ckpt-*.safetensors"))
+            path = sorted(cand)[-1]
+        sd = load_file(path)
+        self.model.load_state_dict({k: v for k, v in sd.items() if k in self.model.state_dict()}, strict=False)
+
+    def _save_checkpoint(self) -> None:
+        d = self.config.model_dir
+        if not d:
+            return
+        os.makedirs(d, exist_ok=True)
+        sd = {k: v.detach().cpu().contiguous() for k, v in self.model.state_dict().items()}
+        sd["global_step"] = torch.tensor([self.global_step], dtype=torch.int64)
+        tr = self._trainer
+        if tr is not None and hasattr(tr, "s0"):
+            sd["opt.s0"], sd["opt.s1"] = tr.s0.cpu(), tr.s1.cpu()
+        save_file(sd, os.path.join(d, f"ckpt-{self.global_step}.safetensors"))
+        ck = sorted(glob.glob(os.path.join(d, "ckpt-*.safetensors")),
+                    key=lambda p: int(p.rsplit("-", 1)[1].split(".")[0]))
+        for old in ck[:-max(1, self.config.keep_checkpoint_max)]:
+            os.remove(old)
+
+    # ------------------------------------------------------------------ train / eval
+    def _make_trainer(self, records: torch.Tensor):
+        from .fused_wide_deep import FusedWideDeepTrainer, default_dnn_opt, default_wide_opt
+        from .torch_wide_deep import TorchWideDeepTrainer
+
+        dopt = self.dnn_optimizer or default_dnn_opt()
+        wopt = self.linear_optimizer or default_wide_opt(len(self.cfg.wide))
+        bs = min(self.batch_size, records.shape[0])
+        if self.device.type == "cuda":
+            tr = FusedWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
+                                      loss_reduction=self.loss_reduction)
+            if getattr(self, "_opt_state", None):
+                tr.s0.copy_(self._opt_state["s0"])
+                tr.s1.copy_(self._opt_state["s1"])
+            tr.step_ctr.fill_(self.global_step)
+        else:
+            tr = TorchWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
+                                      loss_reduction=self.loss_reduction)
+            tr.step_idx = self.global_step
+        tr.set_data(records)
+        return tr
+
+    def train(self, input_fn: Callable, max_steps: int, hooks: list | None = None) -> "WideDeepEstimator":
+        records = input_fn()
+        self._trainer = tr = self._make_trainer(records)
+        every = self.config.save_checkpoints_steps or 0
+        t0, n0 = time.time(), self.global_step
+        while self.global_step < max_steps:
+            tr.step()
+            self.global_step += 1
+            if every and self.global_step % every == 0:
+                tr.sync_to_model()
+                self._save_checkpoint()
+            for h in hooks or []:
+                h(self.global_step, tr)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.train_seconds = time.time() - t0
+        self.examples_per_sec = (self.global_step - n0) * tr.batch / max(self.train_seconds, 1e-9)
+        tr.sync_to_model()
+        self._save_checkpoint()
+        return self
+
+    def predict_logits(self, records: torch.Tensor) -> np.ndarray:
+        if self.device.type == "cuda":
+            if self._trainer is None:
+                self._trainer = self._make_trainer(records)
+            return self._trainer.predict_logits(records).cpu().numpy()
+        dense, ids, _ = wdm.records_to_tensors(records)
+        with torch.no_grad():
+            return self.model(dense, ids).numpy()
+
+    def evaluate(self, input_fn: Callable, steps: int | None = None, name: str | None = None) -> dict:
+        records = input_fn()
+        n = records.shape[0] if not steps else min(records.shape[0], steps * self.batch_size)
+        records = records[:n]
+        logits = self.predict_logits(records)
+        _, _, label = wdm.records_to_tensors(records.cpu())
+        y = label.numpy()
+        p = 1.0 / (1.0 + np.exp(-logits))
+        loss = np.maximum(logits, 0) - logits * y + np.log1p(np.exp(-np.abs(logits)))
+        m = {"loss": float(loss.mean() * self.batch_size), "average_loss": float(loss.mean()),
+             "accuracy": float(((p > 0.5) == (y > 0.5)).mean()), "auc": _auc(y, p),
+             "prediction/mean": float(p.mean()), "label/mean": float(y.mean()), "global_step": self.global_step}
+        self.last_eval = m
+        if self.config.model_dir:
+            import json
+
+            d = os.path.join(self.config.model_dir, f"eval_{name or 'default'}")
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, "metrics.json"), "w") as f:
+                json.dump(m, f)
+        return m
+
+    # ------------------------------------------------------------------ export
+    def export_saved_model(self, export_dir_base: str, serving_input_receiver_fn: Callable | None = None) -> str:
+        from ..serving import saved_model
+
+        receiver = serving_input_receiver_fn() if serving_input_receiver_fn else {}
+        path = os.path.join(export_dir_base, str(int(time.time() * 1000)))
+        saved_model.save_wide_deep(path, self.model, receiver, global_step=self.global_step)
+        return path
+
+    export_savedmodel = export_saved_model
+
+
+def train_and_evaluate(estimator, train_spec: TrainSpec, eval_spec: EvalSpec) -> tuple[dict, list[str]]:
+    estimator.train(train_spec.input_fn, max_steps=train_spec.max_steps)
+    metrics = estimator.evaluate(eval_spec.input_fn, steps=eval_spec.steps, name=eval_spec.name)
+    exports = []
+    for ex in eval_spec.exporters:
+        base = os.path.join(estimator.config.model_dir or ".", "export", ex.name)
+        exports.append(ex.export(estimator, base))
+    return metrics, exports
+
+
+__all__ = ["RunConfig", "TrainSpec", "EvalSpec", "FinalExporter", "HParams", "WideDeepEstimator",
+           "train_and_evaluate", "Any"]

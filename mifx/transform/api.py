@@ -1,0 +1,288 @@
+"""Full-pass analyzers + per-row mappers (tf.Transform-equivalent) with analyze/apply phases.
+
+Reference semantics (`airflow-dags/taxi_utils.py:86-145`, `kubeflow-pipelines/taxi/preprocessing.py:65-101`,
+`03_TensorFlow_Transform.ipynb`): `scale_to_z_score`, `compute_and_apply_vocabulary(top_k,
+num_oov_buckets)`, `bucketize(x, num_buckets)` (quantile boundaries), `scale_to_0_1`, `mean`,
+`string_to_int`, `_fill_in_missing`. A user `preprocessing_fn(inputs) -> outputs` runs twice:
+
+* ANALYZE (Transform component, full dataset): each analyzer computes its statistics over the whole
+  column and records them, in call order, into a :class:`TransformState`;
+* APPLY (transformed examples, eval and serving): the same function replays with the recorded
+  constants — identical math on any batch, so train/serve skew cannot creep in.
+
+Numeric analyzers reduce on the GPU (mifx.ops.analyzers HIP kernels) when a device is set.
+
+Parity notes: vocabulary order is frequency-descending with ties broken by value descending
+(tft's ordering); OOV buckets use a stable 64-bit FNV-1a hash instead of TF's FarmHash (bucket
+ids of OOV strings are therefore not byte-identical to TF — parity unpinned, no TF available).
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import threading
+from dataclasses import dataclass, field
+from typing import Any
+
+import numpy as np
+
+_LOCAL = threading.local()
+
+
+@dataclass
+class TransformState:
+    entries: list = field(default_factory=list)  # [{"kind":..., "params":..., "values":...}]
+
+    def to_json(self) -> str:
+        return json.dumps({"entries": self.entries})
+
+    @staticmethod
+    def from_json(s: str) -> "TransformState":
+        return TransformState(json.loads(s)["entries"])
+
+
+class _Ctx:
+    def __init__(self, mode: str, state: TransformState, device=None):
+        self.mode = mode
+        self.state = state
+        self.cursor = 0
+        self.device = device
+
+
+def _ctx() -> _Ctx:
+    c = getattr(_LOCAL, "ctx", None)
+    if c is None:
+        raise RuntimeError("mifx.transform analyzers must run inside analyze()/apply()")
+    return c
+
+
+@contextlib.contextmanager
+def _phase(mode: str, state: TransformState, device=None):
+    prev = getattr(_LOCAL, "ctx", None)
+    _LOCAL.ctx = _Ctx(mode, state, device)
+    try:
+        yield _LOCAL.ctx
+    finally:
+        _LOCAL.ctx = prev
+
+
+def _analyzer(kind: str, params: dict, compute):
+    c = _ctx()
+    if c.mode == "analyze":
+        values = compute()
+        c.state.entries.append({"kind": kind, "params": params, "values": values})
+        return values
+    if c.cursor >= len(c.state.entries):
+        raise RuntimeError("preprocessing_fn called more analyzers than were recorded")
+    e = c.state.entries[c.cursor]
+    c.cursor += 1
+    if e["kind"] != kind:
+        raise RuntimeError(f"analyzer order changed: recorded {e['kind']}, now {kind}")
+    return e["values"]
+
+
+def analyze(preprocessing_fn, inputs: dict, device=None) -> tuple[dict, TransformState]:
+    """Run the ANALYZE phase over the full dataset; returns (transformed columns, state)."""
+    st = TransformState()
+    with _phase("analyze", st, device):
+        out = preprocessing_fn(dict(inputs))
+    return _materialize(out), st
+
+
+def apply(preprocessing_fn, inputs: dict, state: TransformState) -> dict:
+    """APPLY phase: replay with recorded analyzer constants."""
+    with _phase("apply", state):
+        out = preprocessing_fn(dict(inputs))
+    return _materialize(out)
+
+
+def _materialize(out: dict) -> dict:
+    return {k: np.asarray(v) for k, v in out.items()}
+
+
+# ------------------------------------------------------------------------------- helpers
+def _num(x) -> np.ndarray:
+    a = np.asarray(x)
+    if a.dtype == object:
+        a = np.array([np.nan if v is None else v for v in a], dtype=np.float64)
+    return a.astype(np.float64)
+
+
+def _str(x) -> np.ndarray:
+    a = np.asarray(x, dtype=object)
+    return np.array(["" if v is None else (v.decode() if isinstance(v, bytes) else str(v)) for v in a], dtype=object)
+
+
+def fill_in_missing(x, default=None) -> np.ndarray:
+    """Densify an optional column (`taxi_utils.py:86-103`): None/NaN -> '' or 0."""
+    a = np.asarray(x, dtype=object) if not isinstance(x, np.ndarray) else x
+    if a.dtype == object:
+        is_str = any(isinstance(v, (str, bytes)) for v in a if v is not None)
+        d = ("" if is_str else 0) if default is None else default
+        out = np.array([d if v is None or (isinstance(v, float) and np.isnan(v)) else v for v in a], dtype=object)
+        if not is_str:
+            out = out.astype(np.float64)
+            if all(float(v).is_integer() for v in out):
+                out = out.astype(np.int64)
+        return out
+    if np.issubdtype(a.dtype, np.floating):
+        return np.where(np.isnan(a), 0.0 if default is None else default, a)
+    return a
+
+
+def _moments(a: np.ndarray) -> dict:
+    c = _ctx()
+    if c.device is not None and a.size >= 1 << 16:
+        from ..ops import analyzers
+
+        m = analyzers.column_moments(a, device=c.device)
+        return {"mean": m["mean"], "var": m["std"] ** 2, "min": m["min"], "max": m["max"], "count": int(a.size)}
+    return {"mean": float(a.mean()) if a.size else 0.0, "var": float(a.var()) if a.size else 0.0,
+            "min": float(a.min()) if a.size else 0.0, "max": float(a.max()) if a.size else 0.0,
+            "count": int(a.size)}
+
+
+# ------------------------------------------------------------------------------ analyzers
+def mean(x) -> float:
+    a = _num(x)
+    return _analyzer("moments", {}, lambda: _moments(a))["mean"]
+
+
+def var(x) -> float:
+    a = _num(x)
+    return _analyzer("moments", {}, lambda: _moments(a))["var"]
+
+
+def min(x) -> float:  # noqa: A001
+    a = _num(x)
+    return _analyzer("moments", {}, lambda: _moments(a))["min"]
+
+
+def max(x) -> float:  # noqa: A001
+    a = _num(x)
+    return _analyzer("moments", {}, lambda: _moments(a))["max"]
+
+
+def size(x) -> int:
+    a = np.asarray(x)
+    return _analyzer("size", {}, lambda: int(a.size))
+
+
+def sum(x) -> float:  # noqa: A001
+    a = _num(x)
+    return _analyzer("sum", {}, lambda: float(a.sum()))
+
+
+def quantiles(x, num_buckets: int) -> list[float]:
+    a = _num(x)
+
+    def compute():
+        if a.size == 0:
+            return []
+        qs = np.quantile(a, np.arange(1, num_buckets) / num_buckets, method="higher")
+        return sorted(set(float(q) for q in qs))
+
+    return _analyzer("quantiles", {"num_buckets": num_buckets}, compute)
+
+
+def vocabulary(x, top_k: int | None = None, frequency_threshold: int | None = None,
+               vocab_filename: str | None = None) -> list[str]:
+    s = _str(x)
+
+    def compute():
+        vals, counts = np.unique(s, return_counts=True)
+        order = sorted(zip(counts.tolist(), vals.tolist()), reverse=True)
+        if frequency_threshold is not None:
+            order = [(c, v) for c, v in order if c >= frequency_threshold]
+        if top_k is not None:
+            order = order[:top_k]
+        return [v for _, v in order]
+
+    return _analyzer("vocabulary", {"top_k": top_k, "vocab_filename": vocab_filename}, compute)
+
+
+# -------------------------------------------------------------------------------- mappers
+def scale_to_z_score(x) -> np.ndarray:
+    a = _num(x)
+    m = _analyzer("moments", {}, lambda: _moments(a))
+    sd = np.sqrt(m["var"])
+    return (a - m["mean"]) / sd if sd > 0 else a - m["mean"]
+
+
+def scale_to_0_1(x) -> np.ndarray:
+    a = _num(x)
+    m = _analyzer("moments", {}, lambda: _moments(a))
+    rng = m["max"] - m["min"]
+    return (a - m["min"]) / rng if rng > 0 else np.full_like(a, 0.5)
+
+
+def scale_by_min_max(x, output_min: float = 0.0, output_max: float = 1.0) -> np.ndarray:
+    return scale_to_0_1(x) * (output_max - output_min) + output_min
+
+
+_FNV_OFF, _FNV_PRIME = 0xCBF29CE484222325, 0x100000001B3
+
+
+def fingerprint64(s: str) -> int:
+    h = _FNV_OFF
+    for b in s.encode():
+        h = ((h ^ b) * _FNV_PRIME) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def hash_strings(x, hash_buckets: int) -> np.ndarray:
+    return np.array([fingerprint64(v) % hash_buckets for v in _str(x)], dtype=np.int64)
+
+
+def apply_vocabulary(x, vocab: list[str], default_value: int = -1, num_oov_buckets: int = 0) -> np.ndarray:
+    s = _str(x)
+    index = {v: i for i, v in enumerate(vocab)}
+    n = len(vocab)
+    out = np.empty(len(s), dtype=np.int64)
+    for i, v in enumerate(s):
+        j = index.get(v)
+        if j is not None:
+            out[i] = j
+        elif num_oov_buckets > 0:
+            out[i] = n + fingerprint64(v) % num_oov_buckets
+        else:
+            out[i] = default_value
+    return out
+
+
+def compute_and_apply_vocabulary(x, default_value: int = -1, top_k: int | None = None,
+                                 frequency_threshold: int | None = None, num_oov_buckets: int = 0,
+                                 vocab_filename: str | None = None) -> np.ndarray:
+    vocab = vocabulary(x, top_k=top_k, frequency_threshold=frequency_threshold, vocab_filename=vocab_filename)
+    return apply_vocabulary(x, vocab, default_value=default_value, num_oov_buckets=num_oov_buckets)
+
+
+def string_to_int(x, default_value: int = -1, top_k: int | None = None, frequency_threshold: int | None = None,
+                  num_oov_buckets: int = 0, vocab_filename: str | None = None) -> np.ndarray:
+    """Older tft name used by the KFP taxi module (`kubeflow-pipelines/taxi/preprocessing.py:77-85`)."""
+    return compute_and_apply_vocabulary(x, default_value, top_k, frequency_threshold, num_oov_buckets,
+                                        vocab_filename)
+
+
+def apply_buckets(x, boundaries) -> np.ndarray:
+    a = _num(x)
+    b = np.asarray(boundaries, dtype=np.float64)
+    c = _ctx()
+    if c.device is not None and a.size >= 1 << 16:
+        from ..ops import analyzers
+
+        return analyzers.bucketize(a, b, device=c.device)
+    return np.searchsorted(b, a, side="right").astype(np.int64)
+
+
+def bucketize(x, num_buckets: int, epsilon: float | None = None) -> np.ndarray:
+    return apply_buckets(x, quantiles(x, num_buckets))
+
+
+def as_string(x) -> np.ndarray:
+    a = np.asarray(x)
+    return np.array([str(v) for v in a.tolist()], dtype=object)
+
+
+def state_summary(state: TransformState) -> list[dict[str, Any]]:
+    return [{"kind": e["kind"], **e["params"]} for e in state.entries]
