@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void segment_hist_k(const int* __restrict__ se
     const float y = label[i];
     const float p = fminf(fmaxf(prob[i], 1e-7f), 1.f - 1e-7f);
     const int yb = y > 0.5f ? 1 : 0;
-    int b = (int)(p * nb);
+    int b = (int)((double)p * nb);  // fp64 product: bucket edges must match the host definition
     b = b >= nb ? nb - 1 : b;
     const int bin = (s * nb + b) * 2 + yb;
     if (use_lds) atomicAdd(&lhist[bin], 1u);
