@@ -1,0 +1,169 @@
+"""Bucketed data-parallel gradient synchronisation (one process per GPU, RCCL over xGMI).
+
+Replaces the reference's delegated DP mechanisms — TFJob parameter servers, MPIJob/Horovod ring
+all-reduce, PyTorchJob DDP (`tf-job-simple-v1beta2.jsonnet:22-74`,
+`mpi-job.libsonnet:22-85`, `pytorch-job.jsonnet:63-81`) — with an in-process engine:
+
+* gradients are packed into flat buckets in reverse registration order (≈ backward order), so the
+  first bucket is complete while backward is still producing the rest;
+* each bucket's all-reduce is launched the moment its last gradient is accumulated (post-accumulate
+  hook) on a dedicated communication stream, overlapping RCCL with the remaining backward kernels;
+* bucket size defaults to 32 MiB: on MI355X a ring all-reduce over point-to-point xGMI is per-link
+  bandwidth bound (≈150 GB/s/link), so a bucket has to be several MB before the ring's
+  2(N-1)/N·S/BW term dominates its ≈10-20 µs latency term, and few buckets keep the launch count low
+  (the 288 GB HBM per GPU makes the flat buffers free);
+* optional bf16 wire format halves xGMI bytes for bandwidth-bound models (fp32 accumulate on the
+  receiving side is RCCL's; the master gradient stays fp32).
+
+`DataParallel.finish()` (or `step_ready()`) waits for outstanding work and writes averaged gradients
+back into `param.grad`. Works unchanged on gloo/CPU, which is how the tests exercise it."""
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class _Bucket:
+    params: list
+    numel: int
+    buf: torch.Tensor
+    offsets: list = field(default_factory=list)
+    pending: int = 0
+    work: object = None
+    ready: set = field(default_factory=set)
+
+
+class DataParallel:
+    """Wraps a module; call `finish()` after `loss.backward()` and before `optimizer.step()`."""
+
+    def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
+                 wire_dtype: torch.dtype | None = None, broadcast_init: bool = True, average: bool = True):
+        self.module = module
+        self.pg = process_group if process_group is not None else (dist.group.WORLD if dist.is_initialized()
+                                                                    else None)
+        self.world = dist.get_world_size(self.pg) if self.pg is not None else 1
+        self.average = average
+        self.wire_dtype = wire_dtype
+        self._sync = True
+        params = [p for p in module.parameters() if p.requires_grad]
+        if broadcast_init and self.world > 1:
+            with torch.no_grad():
+                for p in list(module.parameters()) + list(module.buffers()):
+                    dist.broadcast(p.data, src=dist.get_global_rank(self.pg, 0) if self.pg is not dist.group.WORLD
+                                   else 0, group=self.pg)
+        cap = int(bucket_cap_mb * 1024 * 1024)
+        self.buckets: list[_Bucket] = []
+        cur, cur_bytes = [], 0
+        for p in reversed(params):
+            nbytes = p.numel() * p.element_size()
+            if cur and cur_bytes + nbytes > cap:
+                self._add_bucket(cur)
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += nbytes
+        if cur:
+            self._add_bucket(cur)
+        self._where = {}
+        for bi, b in enumerate(self.buckets):
+            for pi, p in enumerate(b.params):
+                self._where[p] = (bi, pi)
+        dev = params[0].device if params else torch.device("cpu")
+        self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if self.world > 1 else []
+
+    def _add_bucket(self, params: list) -> None:
+        n = sum(p.numel() for p in params)
+        dt = self.wire_dtype or params[0].dtype
+        b = _Bucket(params=list(params), numel=n, buf=torch.empty(n, dtype=dt, device=params[0].device))
+        off = 0
+        for p in params:
+            b.offsets.append(off)
+            off += p.numel()
+        b.pending = len(params)
+        self.buckets.append(b)
+
+    # ---- hooks ------------------------------------------------------------------------------
+    def _on_grad(self, p: torch.Tensor) -> None:
+        if not self._sync or p.grad is None:
+            return
+        bi, pi = self._where[p]
+        b = self.buckets[bi]
+        if pi in b.ready:
+            return
+        b.ready.add(pi)
+        off = b.offsets[pi]
+        b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        if len(b.ready) == len(b.params):
+            self._launch(b)
+
+    def _launch(self, b: _Bucket) -> None:
+        if self._comm_stream is not None:
+            self._comm_stream.wait_stream(torch.cuda.current_stream(b.buf.device))
+            with torch.cuda.stream(self._comm_stream):
+                b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
+        else:
+            b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
+
+    # ---- public API ---------------------------------------------------------------------------
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (e.g. micro-batches) without communicating."""
+        old, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = old
+
+    def __call__(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+    def finish(self) -> None:
+        """Complete all bucket all-reduces (launching buckets whose params got no gradient) and write
+        the averaged gradients back into `param.grad`."""
+        if self.world == 1 or not self._sync:
+            return
+        for b in self.buckets:
+            if b.work is None:  # unused params this step: contribute zeros for them
+                for pi, p in enumerate(b.params):
+                    if pi not in b.ready:
+                        off = b.offsets[pi]
+                        if p.grad is None:
+                            b.buf[off:off + p.numel()].zero_()
+                        else:
+                            b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
+                self._launch(b)
+        cur = torch.cuda.current_stream(self.buckets[0].buf.device) if self._comm_stream is not None else None
+        scale = 1.0 / self.world if self.average else 1.0
+        for b in self.buckets:
+            b.work.wait()
+            if cur is not None:
+                cur.wait_stream(self._comm_stream)
+            for pi, p in enumerate(b.params):
+                off = b.offsets[pi]
+                g = b.buf[off:off + p.numel()].view_as(p).to(p.dtype)
+                if p.grad is None:
+                    p.grad = g.mul(scale)
+                else:
+                    p.grad.copy_(g).mul_(scale)
+            b.work, b.ready = None, set()
+
+    step_ready = finish
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def allreduce_flat_(t: torch.Tensor, group=None, average: bool = True) -> torch.Tensor:
+    """In-place all-reduce of one flat tensor (the latency-bound small-gradient path, e.g. W&D's
+    ≈120 KB gradient: one collective per step is the minimum)."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, group=group)
+        if average:
+            t.div_(dist.get_world_size(group))
+    return t

@@ -89,6 +89,7 @@ class FusedWideDeepTrainer:
         self.records = None
         self.n_data = 0
         self.graph = None
+        self._graphs = None
 
     # ---------------------------------------------------------------- data
     def set_data(self, records: torch.Tensor) -> None:
@@ -97,7 +98,7 @@ class FusedWideDeepTrainer:
             raise ValueError("records must be uint8 [N, 32]")
         self.records = records.to(self.device).contiguous()
         self.n_data = self.records.shape[0]
-        self.graph = None
+        self.graph, self._graphs = None, None
 
     @property
     def grad_scale(self) -> float:
@@ -106,46 +107,73 @@ class FusedWideDeepTrainer:
         return 1.0 / (self.batch * self.world)
 
     # ---------------------------------------------------------------- step
-    def _step_impl(self) -> None:
+    def _local_grad(self) -> None:
+        """fused fwd/bwd + slab reduction; for world>1 the result lands in `self.grad` (one row)."""
         wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
                   self.slab_loss, None, self.grad_scale, self.grid, True)
         if self.world == 1:
-            if self.grid == 1:
-                src, nparts = self.slab, 1
-            else:
+            if self.grid > 1:
                 wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
-                src, nparts = self.partial, self.nsplit
+        elif self.grid == 1:
+            self.grad.copy_(self.slab)
         else:
-            if self.grid == 1:
-                self.grad.copy_(self.slab)
-            else:
-                wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
-                wdk.reduce(self.partial, self.nsplit, 1, self.grad)
-            torch.distributed.all_reduce(self.grad, group=self.pg)
+            wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
+            wdk.reduce(self.partial, self.nsplit, 1, self.grad)
+
+    def _apply(self) -> None:
+        if self.world == 1:
+            src, nparts = (self.slab, 1) if self.grid == 1 else (self.partial, self.nsplit)
+        else:
             src, nparts = self.grad, 1
         wdk.optimizer(src, nparts, self.gidx, self.mask, self.param, self.s0, self.s1, self.wt, self.step_ctr,
                       self.h_dnn, self.h_wide)
+
+    def _allreduce(self) -> None:
+        if self.world > 1:
+            torch.distributed.all_reduce(self.grad, group=self.pg)
+
+    def _step_impl(self) -> None:
+        self._local_grad()
+        self._allreduce()
+        self._apply()
 
     def step(self) -> None:
         if self.records is None:
             raise RuntimeError("call set_data() first")
         if self.graph is not None:
             self.graph.replay()
+        elif self._graphs is not None:  # split capture: eager collective between two graphs
+            self._graphs[0].replay()
+            self._allreduce()
+            self._graphs[1].replay()
         else:
             self._step_impl()
 
-    def capture(self, warmup: int = 2) -> None:
-        """Capture one full step into a hipGraph (after `warmup` eager steps on a side stream)."""
+    def capture(self, warmup: int = 2, include_collective: bool = False) -> None:
+        """Capture the step as hipGraph(s) after `warmup` eager steps on a side stream.
+
+        Single rank: one graph. Multi-rank: by default two graphs (local grad, optimizer) with the RCCL
+        all-reduce issued eagerly between them; `include_collective=True` captures the all-reduce too
+        (one graph launch per step, requires a graph-capturable RCCL)."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._step_impl()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._step_impl()
-        self.graph = g
+        self.graph, self._graphs = None, None
+        if self.world == 1 or include_collective:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_impl()
+            self.graph = g
+            return
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            self._local_grad()
+        with torch.cuda.graph(g2):
+            self._apply()
+        self._graphs = (g1, g2)
 
     # ---------------------------------------------------------------- introspection
     def last_loss(self) -> float:

@@ -6,6 +6,7 @@ from __future__ import annotations
 import torch
 
 from ..models import wide_deep as wdm
+from ..parallel.ddp import DataParallel
 from .fused_wide_deep import OptSpec, default_dnn_opt, default_wide_opt
 from .optim import make_optimizer
 
@@ -23,9 +24,14 @@ def _mk(spec: OptSpec, params):
 
 class TorchWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cpu",
-                 dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum"):
+                 dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
+                 process_group=None):
         self.device = torch.device(device)
         self.model = (model or wdm.WideDeepModel()).to(self.device)
+        # DP: "sum" losses are summed across ranks (global-batch sum, like the fused trainer); "mean"
+        # losses are averaged, i.e. the mean over the global batch
+        self.dp = DataParallel(self.model, process_group, average=(loss_reduction == "mean")) \
+            if process_group is not None else None
         self.batch = batch
         self.loss_reduction = loss_reduction
         dnn_params = [p for n, p in self.model.named_parameters() if not n.startswith("wide")]
@@ -52,6 +58,8 @@ class TorchWideDeepTrainer:
         self.opt_dnn.zero_grad(set_to_none=True)
         self.opt_wide.zero_grad(set_to_none=True)
         loss.backward()
+        if self.dp is not None:
+            self.dp.finish()
         self.opt_dnn.step()
         self.opt_wide.step()
         self.step_idx += 1

@@ -1,0 +1,112 @@
+"""Data-parallel engine on gloo, world_size 2 (CPU): bucketed/overlapped all-reduce must give the
+same parameters as one process stepping on the concatenated global batch."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mifx.data.synthetic import synthetic_records
+from mifx.models import wide_deep as wdm
+from mifx.parallel.ddp import DataParallel
+from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _wd_worker(rank, world, port, out_dir, steps, batch):
+    torch.manual_seed(0)
+    _init(rank, world, port)
+    recs = synthetic_records(batch * world * steps, device="cpu", seed=7)
+    shard = recs.view(steps, world, batch, 32)[:, rank].reshape(-1, 32).contiguous()
+    tr = TorchWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=batch, process_group=dist.group.WORLD)
+    tr.set_data(shard)
+    for _ in range(steps):
+        tr.step()
+    if rank == 0:
+        torch.save({k: v.detach().clone() for k, v in tr.model.state_dict().items()},
+                   os.path.join(out_dir, "dp.pt"))
+    dist.destroy_process_group()
+
+
+def test_wide_deep_dp_matches_single_process():
+    steps, batch, world = 3, 16, 2
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_wd_worker, args=(world, port, d, steps, batch), nprocs=world, start_method="spawn")
+        got = torch.load(os.path.join(d, "dp.pt"), weights_only=True)
+    torch.manual_seed(0)
+    ref = TorchWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=batch * world)
+    recs = synthetic_records(batch * world * steps, device="cpu", seed=7)
+    ref.set_data(recs)  # step i uses rows [i*2b, (i+1)*2b) == both ranks' shards of step i
+    for _ in range(steps):
+        ref.step()
+    for k, v in ref.model.state_dict().items():
+        np.testing.assert_allclose(got[k].numpy(), v.detach().numpy(), rtol=2e-5, atol=2e-6, err_msg=k)
+
+
+class _Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 64)
+        self.b = torch.nn.Linear(64, 64)
+        self.unused = torch.nn.Linear(4, 4)
+        self.c = torch.nn.Linear(64, 3)
+
+    def forward(self, x):
+        return self.c(torch.relu(self.b(torch.relu(self.a(x)))))
+
+
+def _ddp_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    torch.manual_seed(100 + rank)  # different init per rank: DataParallel must broadcast rank 0's
+    net = _Net()
+    dp = DataParallel(net, bucket_cap_mb=0.01)  # tiny buckets -> several overlapped all-reduces
+    assert len(dp.buckets) > 2
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(world * 8, 16, generator=g)
+    y = torch.randint(0, 3, (world * 8,), generator=g)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    for _ in range(2):
+        opt.zero_grad()
+        with dp.no_sync():  # two micro-batches accumulated locally
+            torch.nn.functional.cross_entropy(net(x[rank * 8:rank * 8 + 4]), y[rank * 8:rank * 8 + 4],
+                                              reduction="sum").backward()
+        torch.nn.functional.cross_entropy(net(x[rank * 8 + 4:rank * 8 + 8]), y[rank * 8 + 4:rank * 8 + 8],
+                                          reduction="sum").backward()
+        dp.finish()
+        opt.step()
+    if rank == 0:
+        torch.save(net.state_dict(), os.path.join(out_dir, "ddp.pt"))
+    dist.destroy_process_group()
+
+
+def test_bucketed_ddp_matches_single_process():
+    world, port = 2, _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ddp_worker, args=(world, port, d), nprocs=world, start_method="spawn")
+        got = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
+    torch.manual_seed(100)
+    net = _Net()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(world * 8, 16, generator=g)
+    y = torch.randint(0, 3, (world * 8,), generator=g)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    for _ in range(2):
+        opt.zero_grad()
+        (torch.nn.functional.cross_entropy(net(x), y, reduction="sum") / world).backward()
+        opt.step()
+    for k, v in net.state_dict().items():
+        np.testing.assert_allclose(got[k].numpy(), v.numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
