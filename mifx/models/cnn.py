@@ -1,0 +1,174 @@
+"""Image CNN families from the reference notebooks / research code (PyTorch, channels-last NHWC
+so MIOpen picks its NHWC implicit-GEMM (MFMA) convolution kernels on gfx950).
+
+* `MnistDPCNN` — DP-SGD tutorial CNN (`privacy/tutorials/mnist_dpsgd_tutorial.py:42-58`):
+  Conv16 8x8 s2 SAME -> MaxPool2 s1 -> Conv32 4x4 s2 VALID -> MaxPool2 s1 -> Dense32 -> Dense10.
+* `PateCNN` — PATE-2017 `deep_cnn.inference` (`research/pate_2017/deep_cnn.py:84-191`):
+  conv5x5->64, maxpool3 s2, LRN(4, 1, 0.001/9, 0.75), conv5x5->128, LRN, maxpool3 s2, fc384, fc192, fc C;
+  `deeper=True` gives `inference_deeper` (3x3 convs 96/96/96s2/192/192/192s2/192, fc192, fc C).
+* `FashionCNN` — serving notebook model (`serving/Predict_Fashion_MNIST.ipynb`): Conv8 3x3 s2 + Dense10.
+* `TpuMnistCNN` — TPU notebook model (`tpu/Keras_MNIST_TPU.ipynb`): Conv32-Pool-Conv64-Pool-Conv64-
+  Dense64-Dropout-Dense10.
+TF "SAME" padding is reproduced exactly (asymmetric when needed) so shapes match the reference."""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _same_pad(x: torch.Tensor, k: int, s: int, value: float = 0.0) -> torch.Tensor:
+    """TF SAME padding for NCHW tensors (pads more on the bottom/right when odd)."""
+    h, w = x.shape[-2:]
+    ph = max((math.ceil(h / s) - 1) * s + k - h, 0)
+    pw = max((math.ceil(w / s) - 1) * s + k - w, 0)
+    if ph == 0 and pw == 0:
+        return x
+    return F.pad(x, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2), value=value)
+
+
+class SameConv2d(nn.Conv2d):
+    def __init__(self, cin, cout, k, stride=1):
+        super().__init__(cin, cout, k, stride=stride, padding=0)
+
+    def forward(self, x):
+        return super().forward(_same_pad(x, self.kernel_size[0], self.stride[0]))
+
+
+def same_maxpool(x, k, s):
+    return F.max_pool2d(_same_pad(x, k, s, value=-math.inf), k, s)
+
+
+def _he_normal_(m: nn.Module) -> None:
+    for mod in m.modules():
+        if isinstance(mod, (nn.Conv2d, nn.Linear)):
+            nn.init.kaiming_normal_(mod.weight, nonlinearity="relu")
+            nn.init.zeros_(mod.bias)
+
+
+class MnistDPCNN(nn.Module):
+    def __init__(self, num_classes: int = 10):
+        super().__init__()
+        self.conv1 = SameConv2d(1, 16, 8, stride=2)
+        self.conv2 = nn.Conv2d(16, 32, 4, stride=2)
+        self.fc1 = nn.Linear(32 * 4 * 4, 32)
+        self.fc2 = nn.Linear(32, num_classes)
+        _he_normal_(self)
+
+    def forward(self, x):  # x: [B, 28, 28] or [B, 1, 28, 28]
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        y = F.max_pool2d(self.conv1(x), 2, 1)   # 14x14 -> 13x13
+        y = F.max_pool2d(self.conv2(y), 2, 1)   # 5x5 -> 4x4
+        y = self.fc1(y.flatten(1))               # tutorial uses linear Dense(32)
+        return self.fc2(y)
+
+
+class PateCNN(nn.Module):
+    def __init__(self, in_ch: int = 1, num_classes: int = 10, image: int = 28, deeper: bool = False,
+                 dropout: bool = False):
+        super().__init__()
+        self.deeper, self.dropout = deeper, dropout
+        if not deeper:
+            self.c1 = SameConv2d(in_ch, 64, 5)
+            self.c2 = SameConv2d(64, 128, 5)
+            s = math.ceil(math.ceil(image / 2) / 2)
+            self.f3 = nn.Linear(128 * s * s, 384)
+            self.f4 = nn.Linear(384, 192)
+            self.out = nn.Linear(192, num_classes)
+        else:
+            chans = [(in_ch, 96, 1), (96, 96, 1), (96, 96, 2), (96, 192, 1), (192, 192, 1), (192, 192, 2),
+                     (192, 192, 1)]
+            self.convs = nn.ModuleList([SameConv2d(a, b, 3, st) for a, b, st in chans])
+            s = math.ceil(math.ceil(image / 2) / 2)
+            self.f1 = nn.Linear(192 * s * s, 192)
+            self.out = nn.Linear(192, num_classes)
+        for mod in self.modules():
+            if isinstance(mod, (nn.Conv2d, nn.Linear)):
+                nn.init.trunc_normal_(mod.weight, std=0.05 if isinstance(mod, nn.Conv2d) else 0.04)
+                nn.init.constant_(mod.bias, 0.1 if isinstance(mod, nn.Linear) else 0.0)
+
+    @staticmethod
+    def _lrn(x):  # tf.nn.lrn(depth_radius=4, bias=1.0, alpha=0.001/9, beta=0.75)
+        # torch's alpha is divided by size: alpha_t = alpha_tf * (2r+1)
+        return F.local_response_norm(x, size=9, alpha=0.001 / 9.0 * 9, beta=0.75, k=1.0)
+
+    def forward(self, x):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        drop = self.dropout and self.training
+        if not self.deeper:
+            y = F.relu(self.c1(x))
+            y = F.dropout(y, 0.7, drop)  # tf keep_prob 0.3
+            y = self._lrn(same_maxpool(y, 3, 2))
+            y = F.relu(self.c2(y))
+            y = F.dropout(y, 0.7, drop)
+            y = same_maxpool(self._lrn(y), 3, 2)
+            y = F.dropout(F.relu(self.f3(y.flatten(1))), 0.5, drop)
+            y = F.dropout(F.relu(self.f4(y)), 0.5, drop)
+            return self.out(y)
+        y = x
+        for i, c in enumerate(self.convs):
+            y = F.relu(c(y))
+            if i in (2, 5):
+                y = F.dropout(y, 0.5, drop)
+        y = F.dropout(F.relu(self.f1(y.flatten(1))), 0.5, drop)
+        return self.out(y)
+
+
+class FashionCNN(nn.Module):
+    def __init__(self, num_classes: int = 10):
+        super().__init__()
+        self.conv = nn.Conv2d(1, 8, 3, stride=2)
+        self.fc = nn.Linear(8 * 13 * 13, num_classes)
+
+    def forward(self, x):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        return self.fc(F.relu(self.conv(x)).flatten(1))
+
+
+class TpuMnistCNN(nn.Module):
+    def __init__(self, num_classes: int = 10, dropout: float = 0.5):
+        super().__init__()
+        self.c1 = nn.Conv2d(1, 32, 3)
+        self.c2 = nn.Conv2d(32, 64, 3)
+        self.c3 = nn.Conv2d(64, 64, 3)
+        self.fc = nn.Linear(64 * 3 * 3, 64)
+        self.out = nn.Linear(64, num_classes)
+        self.p = dropout
+
+    def forward(self, x):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        y = F.max_pool2d(F.relu(self.c1(x)), 2)
+        y = F.max_pool2d(F.relu(self.c2(y)), 2)
+        y = F.relu(self.c3(y))
+        y = F.dropout(F.relu(self.fc(y.flatten(1))), self.p, self.training)
+        return self.out(y)
+
+
+def to_channels_last(model: nn.Module) -> nn.Module:
+    """NHWC weights/activations: MIOpen's MFMA implicit-GEMM path on gfx950."""
+    return model.to(memory_format=torch.channels_last)
+
+
+class EMA:
+    """Exponential moving average of weights (`deep_cnn.py:419-422`, decay 0.9999), applied in-place
+    with fused multi-tensor ops after each optimizer step."""
+
+    def __init__(self, model: nn.Module, decay: float = 0.9999):
+        self.decay = decay
+        self.shadow = [p.detach().clone() for p in model.parameters()]
+        self.params = list(model.parameters())
+
+    @torch.no_grad()
+    def update(self) -> None:
+        torch._foreach_lerp_(self.shadow, [p.detach() for p in self.params], 1.0 - self.decay)
+
+    @torch.no_grad()
+    def copy_to(self, model: nn.Module) -> None:
+        for s, p in zip(self.shadow, model.parameters()):
+            p.copy_(s)
