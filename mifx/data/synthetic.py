@@ -101,3 +101,18 @@ def synthetic_taxi_csv_rows(n: int, seed: int = 0, missing_rate: float = 0.02) -
                 r[k] = None
         rows.append(r)
     return rows
+
+
+def synthetic_images(n: int, shape=(28, 28), num_classes: int = 10, seed: int = 0, channels: int = 1,
+                     noise: float = 0.35):
+    """MNIST/SVHN/CIFAR-shaped images with a learnable class signal (no dataset downloads offline):
+    each class owns a fixed random smooth template; samples are template + noise, clipped to [0, 1].
+    Returns (float32 [n, C, H, W] or [n, H, W] when channels == 1, int64 labels [n])."""
+    g = torch.Generator().manual_seed(seed)
+    h, w = shape
+    base = torch.rand(num_classes, channels, h // 4 + 1, w // 4 + 1, generator=g)
+    templates = torch.nn.functional.interpolate(base, size=(h, w), mode="bilinear", align_corners=False)
+    labels = torch.randint(0, num_classes, (n,), generator=g)
+    x = templates[labels] + noise * torch.randn(n, channels, h, w, generator=g)
+    x = x.clamp_(0.0, 1.0)
+    return (x[:, 0] if channels == 1 else x), labels
