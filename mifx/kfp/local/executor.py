@@ -95,8 +95,9 @@ class LocalWorkflowExecutor:
         self.run_dir = os.path.abspath(run_dir)
         os.makedirs(self.run_dir, exist_ok=True)
         self.params = {p["name"]: p.get("value") for p in self.spec.get("arguments", {}).get("parameters", [])}
-        for k, v in (arguments or {}).items():
-            self.params[k] = str(v)
+        for k, v in (arguments or {}).items():  # names as in the compiled spec (k8s-sanitised)
+            key = k if k in self.params else re.sub("-+", "-", re.sub("[^-0-9a-z]+", "-", k.lower())).strip("-")
+            self.params[key] = str(v)
         missing = [k for k, v in self.params.items() if v is None]
         if missing:
             raise WorkflowError(f"missing values for workflow parameters: {missing}")
@@ -274,9 +275,10 @@ class LocalWorkflowExecutor:
         return {p: os.path.join(sandbox, p.lstrip("/")) for p in sorted(set(paths), key=len, reverse=True)}
 
     def _exec_container(self, tmpl: dict, scope: dict, display: str, node: NodeStatus) -> dict:
+        pod = re.sub(r"[^A-Za-z0-9_.-]+", "_", display) + f"-{node.attempts}"
+        scope = dict(scope, **{"pod.name": pod})
         c = _substitute(tmpl["container"], scope)
-        sandbox = os.path.join(self.run_dir, "steps", re.sub(r"[^A-Za-z0-9_.-]+", "_", display) +
-                               f"-{node.attempts}")
+        sandbox = os.path.join(self.run_dir, "steps", pod)
         os.makedirs(sandbox, exist_ok=True)
         remap = self._sandbox_paths(tmpl, sandbox)
 

@@ -9,7 +9,8 @@ def mount_pvc(pvc_name: str = "pipeline-claim", volume_name: str = "pipeline", v
 
     def _mount_pvc(task):
         pvc = V1PersistentVolumeClaimVolumeSource(claim_name=pvc_name)
-        return (task.add_volume(V1Volume(name=volume_name, persistent_volume_claim=pvc))
-                .add_volume_mount(V1VolumeMount(mount_path=volume_mount_path, name=volume_name)))
+        task.add_volume(V1Volume(name=volume_name, persistent_volume_claim=pvc))
+        task.container.add_volume_mount(V1VolumeMount(mount_path=volume_mount_path, name=volume_name))
+        return task
 
     return _mount_pvc

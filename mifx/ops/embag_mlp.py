@@ -1,0 +1,56 @@
+"""ctypes bindings for csrc/embag_mlp.hip (KFP taxi DNN gather fwd/bwd + sparse Adagrad)."""
+from __future__ import annotations
+
+import ctypes
+import functools
+
+import torch
+
+from . import _lib
+from ._lib import F32, I32, VP, check, ptr, sig, stream_handle
+
+
+@functools.lru_cache(maxsize=None)
+def _fns():
+    lib = _lib.load("embag_mlp")
+    return {
+        "limits": sig(lib, "mifx_tdnn_limits", [VP]),
+        "fwd_bwd": sig(lib, "mifx_tdnn_fwd_bwd", [VP, VP, VP, VP, VP, I32, VP, I32, I32, VP, I32, I32, F32, I32,
+                                                  VP, VP, VP, VP, VP, VP]),
+        "adagrad": sig(lib, "mifx_tdnn_adagrad", [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, I32, VP, I32, I32,
+                                                  VP, VP, VP, I32, I32, F32, VP]),
+    }
+
+
+def limits() -> dict:
+    out = (ctypes.c_int * 3)()
+    _fns()["limits"](out)
+    return {"max_hidden": out[0], "max_fields": out[1], "max_dense": out[2]}
+
+
+def fwd_bwd(W1, b1, w2, b2, rows, xd, y, dense_row0: int, grad_scale: float, train: bool, bufs: dict):
+    """rows int32 [B, F] (global W1 rows), xd float [B, D], y float [B] -> fills bufs (a, dz, logit, dlogit, loss)."""
+    B, F = rows.shape
+    D = xd.shape[1]
+    H = W1.shape[1]
+    check(_fns()["fwd_bwd"](ptr(W1), ptr(b1), ptr(w2), ptr(b2), ptr(rows), F, ptr(xd), D, dense_row0,
+                            ptr(y), B, H, float(grad_scale), int(train), ptr(bufs.get("a")), ptr(bufs.get("dz")),
+                            ptr(bufs["logit"]), ptr(bufs.get("dlogit")), ptr(bufs.get("loss")),
+                            stream_handle(W1.device)), "mifx_tdnn_fwd_bwd")
+
+
+def adagrad(params: dict, accs: dict, rows: torch.Tensor, xd, dense_row0: int, bufs: dict, lr: float) -> None:
+    """Sparse-row + dense Adagrad (TF semantics) from the buffers of `fwd_bwd`."""
+    B, F = rows.shape
+    flat = rows.reshape(-1)
+    srt, order = torch.sort(flat, stable=True)
+    urows, counts = torch.unique_consecutive(srt, return_counts=True)
+    seg = torch.zeros(urows.numel() + 1, dtype=torch.int32, device=rows.device)
+    seg[1:] = torch.cumsum(counts, 0)
+    H = params["W1"].shape[1]
+    urows32, order32 = urows.to(torch.int32), order.to(torch.int32)  # keep alive across the launch
+    check(_fns()["adagrad"](ptr(params["W1"]), ptr(accs["W1"]), ptr(params["b1"]), ptr(accs["b1"]),
+                            ptr(params["w2"]), ptr(accs["w2"]), ptr(params["b2"]), ptr(accs["b2"]),
+                            ptr(urows32), ptr(seg), ptr(order32), urows.numel(), F,
+                            ptr(xd), xd.shape[1], dense_row0, ptr(bufs["a"]), ptr(bufs["dz"]), ptr(bufs["dlogit"]),
+                            B, H, float(lr), stream_handle(rows.device)), "mifx_tdnn_adagrad")
