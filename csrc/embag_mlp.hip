@@ -11,14 +11,13 @@
 // only needs to visit the <= B*13 distinct gathered rows plus the dense parameters — exactly the
 // TF result at a fraction of the 9.26M-parameter dense update.
 //
-//  * tdnn_fwd_bwd: one 256-thread workgroup per example; each thread owns H/256 hidden units,
-//    gathers its slice of the 16 rows (coalesced 128-B segments per wave), block-reduces the
-//    logit with wave64 shuffles + LDS, writes a_b, dz_b, logit_b, loss_b.
+//  * tdnn_fwd + tdnn_head_bwd: grid (B, H/256) — each thread gathers its hidden unit from the 16
+//    rows (coalesced across the wave), partial logits per block, then logit/BCE/dz per example.
 //  * tdnn_sparse_adagrad: one workgroup per DISTINCT sparse row (rows pre-sorted on device);
 //    sums dz over the examples that touched the row in a fixed order (deterministic, no atomics),
 //    then acc += g^2; w -= lr * g * rsqrt(acc).
-//  * tdnn_dense_adagrad: per hidden unit, reduces over the batch for the dense W1 rows, b1, w2 and
-//    applies the same update; block 0 also updates b2.
+//  * tdnn_dense_partial + tdnn_dense_apply: batch-chunked reductions for the dense W1 rows, b1, w2
+//    (grid H/256 x chunks), then a fixed-order combine and the same update; block 0 updates b2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,59 +41,56 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-__global__ __launch_bounds__(kThreads) void tdnn_fwd_bwd(const float* __restrict__ W1, const float* __restrict__ b1,
-                                                        const float* __restrict__ w2, const float* __restrict__ b2,
-                                                        const int* __restrict__ rows, int F,
-                                                        const float* __restrict__ xd, int D, int dense_row0,
-                                                        const float* __restrict__ y, int H, float grad_scale,
-                                                        int train, float* __restrict__ a_out,
-                                                        float* __restrict__ dz_out, float* __restrict__ logit_out,
-                                                        float* __restrict__ dlogit_out, float* __restrict__ loss_out) {
+// grid (B, nh): block (b, c) owns hidden units [256c, 256c + 256) of example b — B x ceil(H/256)
+// workgroups so even the B=32 reference batch puts ~200 WGs in flight; each thread issues its
+// 16 independent row loads back to back. Writes a = relu(z) and this block's partial logit.
+__global__ __launch_bounds__(kThreads) void tdnn_fwd(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                    const float* __restrict__ w2, const int* __restrict__ rows, int F,
+                                                    const float* __restrict__ xd, int D, int dense_row0, int H,
+                                                    float* __restrict__ a_out, float* __restrict__ part_out) {
   __shared__ int srow[kMaxFields];
   __shared__ float sx[kMaxDense];
   __shared__ float red[kThreads / 64];
-  __shared__ float s_dlogit;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, nh = gridDim.y;
   if (threadIdx.x < F) srow[threadIdx.x] = rows[(size_t)b * F + threadIdx.x];
   if (threadIdx.x < D) sx[threadIdx.x] = xd[(size_t)b * D + threadIdx.x];
   __syncthreads();
-  constexpr int kPer = kMaxH / kThreads;
-  float z[kPer];
-  float part = 0.f;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int h = threadIdx.x + k * kThreads;
-    float acc = 0.f;
-    if (h < H) {
-      acc = b1[h];
-      for (int f = 0; f < F; ++f) acc += W1[(size_t)srow[f] * H + h];
-      for (int d = 0; d < D; ++d) acc += sx[d] * W1[(size_t)(dense_row0 + d) * H + h];
-      const float a = fmaxf(acc, 0.f);
-      part += a * w2[h];
-      if (train) a_out[(size_t)b * H + h] = a;
-    }
-    z[k] = acc;
+  const int h = blockIdx.y * kThreads + threadIdx.x;
+  float p = 0.f;
+  if (h < H) {
+    float acc = b1[h];
+#pragma unroll 4
+    for (int f = 0; f < F; ++f) acc += W1[(size_t)srow[f] * H + h];
+    for (int d = 0; d < D; ++d) acc += sx[d] * W1[(size_t)(dense_row0 + d) * H + h];
+    const float a = fmaxf(acc, 0.f);
+    a_out[(size_t)b * H + h] = a;
+    p = a * w2[h];
   }
-  const float logit = block_sum(part, red) + b2[0];
-  if (threadIdx.x == 0) {
-    logit_out[b] = logit;
-    if (train) {
-      const float yy = y[b];
-      // stable BCE with logits: max(l,0) - l*y + log1p(exp(-|l|))
-      loss_out[b] = fmaxf(logit, 0.f) - logit * yy + log1pf(expf(-fabsf(logit)));
-      const float d = (1.f / (1.f + expf(-logit)) - yy) * grad_scale;
-      dlogit_out[b] = d;
-      s_dlogit = d;
-    }
-  }
+  const float t = block_sum(p, red);
+  if (threadIdx.x == 0) part_out[(size_t)b * nh + blockIdx.y] = t;
+}
+
+// grid (B, nh): logit from the partials (fixed order), BCE loss, dlogit, dz = dlogit * w2 * [a > 0]
+__global__ __launch_bounds__(kThreads) void tdnn_head_bwd(const float* __restrict__ w2, const float* __restrict__ b2,
+                                                         const float* __restrict__ y, const float* __restrict__ part,
+                                                         const float* __restrict__ a, int H, float grad_scale,
+                                                         int train, float* __restrict__ dz_out,
+                                                         float* __restrict__ logit_out, float* __restrict__ dlogit_out,
+                                                         float* __restrict__ loss_out) {
+  const int b = blockIdx.x, nh = gridDim.y;
+  float logit = b2[0];
+  for (int c = 0; c < nh; ++c) logit += part[(size_t)b * nh + c];
+  if (blockIdx.y == 0 && threadIdx.x == 0) logit_out[b] = logit;
   if (!train) return;
-  __syncthreads();
-  const float dl = s_dlogit;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int h = threadIdx.x + k * kThreads;
-    if (h < H) dz_out[(size_t)b * H + h] = z[k] > 0.f ? dl * w2[h] : 0.f;
+  const float yy = y[b];
+  const float dl = (1.f / (1.f + expf(-logit)) - yy) * grad_scale;
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    // stable BCE with logits: max(l,0) - l*y + log1p(exp(-|l|))
+    loss_out[b] = fmaxf(logit, 0.f) - logit * yy + log1pf(expf(-fabsf(logit)));
+    dlogit_out[b] = dl;
   }
+  const int h = blockIdx.y * kThreads + threadIdx.x;
+  if (h < H) dz_out[(size_t)b * H + h] = a[(size_t)b * H + h] > 0.f ? dl * w2[h] : 0.f;
 }
 
 // urows[U]: distinct sparse rows (ascending); seg[U+1]: offsets into order[]; order[P]: pair ids
@@ -116,51 +112,69 @@ __global__ __launch_bounds__(kThreads) void tdnn_sparse_adagrad(float* __restric
   }
 }
 
-__global__ __launch_bounds__(kThreads) void tdnn_dense_adagrad(float* __restrict__ W1, float* __restrict__ acc1,
-                                                              float* __restrict__ b1, float* __restrict__ accb1,
-                                                              float* __restrict__ w2, float* __restrict__ accw2,
-                                                              float* __restrict__ b2, float* __restrict__ accb2,
-                                                              const float* __restrict__ xd, int D, int dense_row0,
-                                                              const float* __restrict__ a, const float* __restrict__ dz,
+// grid (ceil(H/256), nchunk): per-chunk batch reductions for the dense params, into
+// part[chunk][k][h] with k = 0..D-1 dense W1 rows, D = b1, D+1 = w2
+__global__ __launch_bounds__(kThreads) void tdnn_dense_partial(const float* __restrict__ xd, int D,
+                                                              const float* __restrict__ a,
+                                                              const float* __restrict__ dz,
                                                               const float* __restrict__ dlogit, int B, int H,
-                                                              float lr) {
+                                                              float* __restrict__ part) {
+  const int h = blockIdx.x * kThreads + threadIdx.x;
+  if (h >= H) return;
+  const int nchunk = gridDim.y, c = blockIdx.y;
+  const int b0 = (int)((long long)B * c / nchunk), b1e = (int)((long long)B * (c + 1) / nchunk);
+  float gd[kMaxDense];
+#pragma unroll
+  for (int d = 0; d < kMaxDense; ++d) gd[d] = 0.f;
+  float gb1 = 0.f, gw2 = 0.f;
+  for (int b = b0; b < b1e; ++b) {
+    const float g = dz[(size_t)b * H + h];
+    gb1 += g;
+    gw2 += dlogit[b] * a[(size_t)b * H + h];
+#pragma unroll
+    for (int d = 0; d < kMaxDense; ++d)
+      if (d < D) gd[d] += xd[(size_t)b * D + d] * g;
+  }
+  float* out = part + (size_t)c * (D + 2) * H;
+  for (int d = 0; d < D; ++d) out[(size_t)d * H + h] = gd[d];
+  out[(size_t)D * H + h] = gb1;
+  out[(size_t)(D + 1) * H + h] = gw2;
+}
+
+__device__ __forceinline__ void adagrad_one(float* w, float* acc, float g, float lr) {
+  const float s = *acc + g * g;
+  *acc = s;
+  *w -= lr * g * rsqrtf(s);
+}
+
+__global__ __launch_bounds__(kThreads) void tdnn_dense_apply(float* __restrict__ W1, float* __restrict__ acc1,
+                                                            float* __restrict__ b1, float* __restrict__ accb1,
+                                                            float* __restrict__ w2, float* __restrict__ accw2,
+                                                            float* __restrict__ b2, float* __restrict__ accb2,
+                                                            int D, int dense_row0, const float* __restrict__ part,
+                                                            int nchunk, const float* __restrict__ dlogit, int B,
+                                                            int H, float lr) {
   const int h = blockIdx.x * kThreads + threadIdx.x;
   if (h < H) {
-    float gd[kMaxDense];
-#pragma unroll
-    for (int d = 0; d < kMaxDense; ++d) gd[d] = 0.f;
-    float gb1 = 0.f, gw2 = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const float g = dz[(size_t)b * H + h];
-      gb1 += g;
-      gw2 += dlogit[b] * a[(size_t)b * H + h];
-#pragma unroll
-      for (int d = 0; d < kMaxDense; ++d)
-        if (d < D) gd[d] += xd[(size_t)b * D + d] * g;
+    for (int k = 0; k < D + 2; ++k) {
+      float g = 0.f;
+      for (int c = 0; c < nchunk; ++c) g += part[((size_t)c * (D + 2) + k) * H + h];  // fixed order
+      if (k < D) {
+        const size_t i = (size_t)(dense_row0 + k) * H + h;
+        adagrad_one(W1 + i, acc1 + i, g, lr);
+      } else if (k == D) {
+        adagrad_one(b1 + h, accb1 + h, g, lr);
+      } else {
+        adagrad_one(w2 + h, accw2 + h, g, lr);
+      }
     }
-    for (int d = 0; d < D; ++d) {
-      const size_t i = (size_t)(dense_row0 + d) * H + h;
-      const float s = acc1[i] + gd[d] * gd[d];
-      acc1[i] = s;
-      W1[i] -= lr * gd[d] * rsqrtf(s);
-    }
-    float s = accb1[h] + gb1 * gb1;
-    accb1[h] = s;
-    b1[h] -= lr * gb1 * rsqrtf(s);
-    s = accw2[h] + gw2 * gw2;
-    accw2[h] = s;
-    w2[h] -= lr * gw2 * rsqrtf(s);
   }
   if (blockIdx.x == 0) {
     __shared__ float red[kThreads / 64];
     float p = 0.f;
     for (int b = threadIdx.x; b < B; b += kThreads) p += dlogit[b];
     const float g = block_sum(p, red);
-    if (threadIdx.x == 0) {
-      const float s = accb2[0] + g * g;
-      accb2[0] = s;
-      b2[0] -= lr * g * rsqrtf(s);
-    }
+    if (threadIdx.x == 0) adagrad_one(b2, accb2, g, lr);
   }
 }
 
@@ -175,26 +189,37 @@ int mifx_tdnn_limits(int* out) {
   return 0;
 }
 
+int mifx_tdnn_chunks(int B) { return B < 64 ? 1 : (B / 32 < 64 ? B / 32 : 64); }
+
+// scratch: part_logit [B * ceil(H/256)]
 int mifx_tdnn_fwd_bwd(const float* W1, const float* b1, const float* w2, const float* b2, const int* rows, int F,
                       const float* xd, int D, int dense_row0, const float* y, int B, int H, float grad_scale,
-                      int train, float* a_out, float* dz_out, float* logit_out, float* dlogit_out, float* loss_out,
-                      hipStream_t st) {
+                      int train, float* a_out, float* part_logit, float* dz_out, float* logit_out, float* dlogit_out,
+                      float* loss_out, hipStream_t st) {
   if (H <= 0 || H > kMaxH || F > kMaxFields || D > kMaxDense || B <= 0) return -1;
-  hipLaunchKernelGGL(tdnn_fwd_bwd, dim3(B), dim3(kThreads), 0, st, W1, b1, w2, b2, rows, F, xd, D, dense_row0, y, H,
-                     grad_scale, train, a_out, dz_out, logit_out, dlogit_out, loss_out);
+  const dim3 grid(B, (H + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(tdnn_fwd, grid, dim3(kThreads), 0, st, W1, b1, w2, rows, F, xd, D, dense_row0, H, a_out,
+                     part_logit);
+  hipLaunchKernelGGL(tdnn_head_bwd, grid, dim3(kThreads), 0, st, w2, b2, y, part_logit, a_out, H, grad_scale, train,
+                     dz_out, logit_out, dlogit_out, loss_out);
   return (int)hipGetLastError();
 }
 
+// scratch: dense_part [mifx_tdnn_chunks(B) * (D + 2) * H]
 int mifx_tdnn_adagrad(float* W1, float* acc1, float* b1, float* accb1, float* w2, float* accw2, float* b2,
                       float* accb2, const int* urows, const int* seg, const int* order, int U, int F,
                       const float* xd, int D, int dense_row0, const float* a, const float* dz, const float* dlogit,
-                      int B, int H, float lr, hipStream_t st) {
+                      int B, int H, float lr, float* dense_part, hipStream_t st) {
   if (H <= 0 || H > kMaxH || D > kMaxDense || B <= 0) return -1;
   if (U > 0)
     hipLaunchKernelGGL(tdnn_sparse_adagrad, dim3(U), dim3(kThreads), 0, st, W1, acc1, urows, seg, order, F, dz, H,
                        lr);
-  hipLaunchKernelGGL(tdnn_dense_adagrad, dim3((H + kThreads - 1) / kThreads), dim3(kThreads), 0, st, W1, acc1, b1,
-                     accb1, w2, accw2, b2, accb2, xd, D, dense_row0, a, dz, dlogit, B, H, lr);
+  const int nchunk = mifx_tdnn_chunks(B);
+  const int hb = (H + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(tdnn_dense_partial, dim3(hb, nchunk), dim3(kThreads), 0, st, xd, D, a, dz, dlogit, B, H,
+                     dense_part);
+  hipLaunchKernelGGL(tdnn_dense_apply, dim3(hb), dim3(kThreads), 0, st, W1, acc1, b1, accb1, w2, accw2, b2, accb2, D,
+                     dense_row0, dense_part, nchunk, dlogit, B, H, lr);
   return (int)hipGetLastError();
 }
 

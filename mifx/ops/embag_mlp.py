@@ -16,9 +16,10 @@ def _fns():
     return {
         "limits": sig(lib, "mifx_tdnn_limits", [VP]),
         "fwd_bwd": sig(lib, "mifx_tdnn_fwd_bwd", [VP, VP, VP, VP, VP, I32, VP, I32, I32, VP, I32, I32, F32, I32,
-                                                  VP, VP, VP, VP, VP, VP]),
+                                                  VP, VP, VP, VP, VP, VP, VP]),
         "adagrad": sig(lib, "mifx_tdnn_adagrad", [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, I32, VP, I32, I32,
-                                                  VP, VP, VP, I32, I32, F32, VP]),
+                                                  VP, VP, VP, I32, I32, F32, VP, VP]),
+        "chunks": sig(lib, "mifx_tdnn_chunks", [I32]),
     }
 
 
@@ -28,13 +29,23 @@ def limits() -> dict:
     return {"max_hidden": out[0], "max_fields": out[1], "max_dense": out[2]}
 
 
+def make_buffers(B: int, H: int, D: int, device) -> dict:
+    """Activation / gradient / scratch buffers for batch B (reused every step)."""
+    nh = (H + 255) // 256
+    return {"a": torch.empty(B, H, device=device), "dz": torch.empty(B, H, device=device),
+            "part": torch.empty(B * nh, device=device), "logit": torch.empty(B, device=device),
+            "dlogit": torch.empty(B, device=device), "loss": torch.empty(B, device=device),
+            "dpart": torch.empty(_fns()["chunks"](B) * (D + 2) * H, device=device)}
+
+
 def fwd_bwd(W1, b1, w2, b2, rows, xd, y, dense_row0: int, grad_scale: float, train: bool, bufs: dict):
     """rows int32 [B, F] (global W1 rows), xd float [B, D], y float [B] -> fills bufs (a, dz, logit, dlogit, loss)."""
     B, F = rows.shape
     D = xd.shape[1]
     H = W1.shape[1]
     check(_fns()["fwd_bwd"](ptr(W1), ptr(b1), ptr(w2), ptr(b2), ptr(rows), F, ptr(xd), D, dense_row0,
-                            ptr(y), B, H, float(grad_scale), int(train), ptr(bufs.get("a")), ptr(bufs.get("dz")),
+                            ptr(y), B, H, float(grad_scale), int(train), ptr(bufs["a"]), ptr(bufs["part"]),
+                            ptr(bufs.get("dz")),
                             ptr(bufs["logit"]), ptr(bufs.get("dlogit")), ptr(bufs.get("loss")),
                             stream_handle(W1.device)), "mifx_tdnn_fwd_bwd")
 
@@ -53,4 +64,4 @@ def adagrad(params: dict, accs: dict, rows: torch.Tensor, xd, dense_row0: int, b
                             ptr(params["w2"]), ptr(accs["w2"]), ptr(params["b2"]), ptr(accs["b2"]),
                             ptr(urows32), ptr(seg), ptr(order32), urows.numel(), F,
                             ptr(xd), xd.shape[1], dense_row0, ptr(bufs["a"]), ptr(bufs["dz"]), ptr(bufs["dlogit"]),
-                            B, H, float(lr), stream_handle(rows.device)), "mifx_tdnn_adagrad")
+                            B, H, float(lr), ptr(bufs["dpart"]), stream_handle(rows.device)), "mifx_tdnn_adagrad")

@@ -27,12 +27,7 @@ class TaxiDNNTrainer:
             p = {n: getattr(self.model, n) for n in ("W1", "b1", "w2", "b2")}
             self.params = {n: t.data for n, t in p.items()}
             self.accs = {n: torch.full_like(t, initial_accumulator_value) for n, t in self.params.items()}
-            H = self.model.cfg.hidden
-            B = batch
-            dev = self.device
-            self.bufs = {"a": torch.empty(B, H, device=dev), "dz": torch.empty(B, H, device=dev),
-                         "logit": torch.empty(B, device=dev), "dlogit": torch.empty(B, device=dev),
-                         "loss": torch.empty(B, device=dev)}
+            self.bufs = embag_mlp.make_buffers(batch, self.model.cfg.hidden, len(self.model.cfg.dense), self.device)
         else:
             self.opt = TFAdagrad(self.model.parameters(), lr=lr, initial_accumulator_value=initial_accumulator_value)
         self.step_idx = 0
@@ -78,10 +73,10 @@ class TaxiDNNTrainer:
             r = self.model.rows(ids[s:s + batch].to(self.device)).to(torch.int32).contiguous()
             xd = dense[s:s + batch].to(self.device).float().contiguous()
             if self.native:
-                lg = torch.empty(len(r), device=self.device)
+                bufs = self._k.make_buffers(len(r), self.model.cfg.hidden, xd.shape[1], self.device)
                 self._k.fwd_bwd(self.params["W1"], self.params["b1"], self.params["w2"], self.params["b2"], r, xd,
-                                lg, self.dense_row0, 1.0, False, {"logit": lg})
-                out.append(lg.cpu())
+                                bufs["logit"], self.dense_row0, 1.0, False, bufs)
+                out.append(bufs["logit"].cpu())
             else:
                 out.append(self._forward_rows(r, xd).cpu())
         return torch.cat(out).numpy()
