@@ -1,0 +1,206 @@
+"""BERT (base by default) encoder + sequence-classification head, tensor-parallel over RCCL.
+
+BASELINE config 4 ("BERT-base fine-tune Trainer component, TP=8"); there is no BERT in the
+reference, so this follows the public BERT-base architecture: 12 layers, hidden 768, 12 heads,
+FFN 3072, vocab 30522, 512 positions, 2 token types, post-LN, GELU(erf).
+
+Per layer on each TP rank: one fused QKV column-parallel GEMM for the rank's heads (uneven head
+split when heads % tp != 0), SDPA on the local heads, row-parallel output projection (+1
+all-reduce), fused residual-add + LayerNorm (HIP), column-parallel FFN-in with fused bias+GELU
+(HIP), row-parallel FFN-out (+1 all-reduce), fused residual-add + LayerNorm."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import fused_bert as fb
+from ..parallel.tensor_parallel import (ColumnParallelLinear, RowParallelLinear, TPGroup, VocabParallelEmbedding,
+                                        copy_to_tp, head_partition, split_sizes)
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    dropout: float = 0.1
+    num_labels: int = 2
+    ln_eps: float = 1e-12
+    init_std: float = 0.02
+
+    @staticmethod
+    def tiny(**kw) -> "BertConfig":
+        d = dict(vocab_size=1000, hidden=64, layers=2, heads=4, intermediate=128, max_position=64)
+        d.update(kw)
+        return BertConfig(**d)
+
+
+class BertLayer(nn.Module):
+    def __init__(self, cfg: BertConfig, tp: TPGroup):
+        super().__init__()
+        self.cfg, self.tp = cfg, tp
+        self.head_dim = cfg.hidden // cfg.heads
+        self.heads_per_rank = head_partition(cfg.heads, tp.size)
+        self.local_heads = self.heads_per_rank[tp.rank]
+        hs = [h * self.head_dim for h in self.heads_per_rank]
+        self.qkv = ColumnParallelLinear(cfg.hidden, 3 * cfg.hidden, tp, sizes=[3 * s for s in hs])
+        self.attn_out = RowParallelLinear(cfg.hidden, cfg.hidden, tp, sizes=hs)
+        self.ln1 = nn.LayerNorm(cfg.hidden, eps=cfg.ln_eps)
+        self.ffn_in = ColumnParallelLinear(cfg.hidden, cfg.intermediate, tp,
+                                           sizes=split_sizes(cfg.intermediate, tp.size))
+        self.ffn_out = RowParallelLinear(cfg.intermediate, cfg.hidden, tp, sizes=self.ffn_in.sizes)
+        self.ln2 = nn.LayerNorm(cfg.hidden, eps=cfg.ln_eps)
+
+    def load_full(self, sd: dict, prefix: str) -> None:
+        """Shard a full (TP=1) layer state dict into this rank's pieces."""
+        H, d = self.cfg.hidden, self.head_dim
+        w, b = sd[prefix + "qkv.weight"], sd[prefix + "qkv.bias"]
+        h0 = sum(self.heads_per_rank[:self.tp.rank])
+        rows = torch.cat([torch.arange(k * H + h0 * d, k * H + (h0 + self.local_heads) * d) for k in range(3)])
+        with torch.no_grad():
+            self.qkv.weight.copy_(w[rows])
+            self.qkv.bias.copy_(b[rows])
+        self.attn_out.load_full(sd[prefix + "attn_out.weight"], sd[prefix + "attn_out.bias"])
+        self.ffn_in.load_full(sd[prefix + "ffn_in.weight"], sd[prefix + "ffn_in.bias"])
+        self.ffn_out.load_full(sd[prefix + "ffn_out.weight"], sd[prefix + "ffn_out.bias"])
+        for n in ("ln1", "ln2"):
+            getattr(self, n).load_state_dict({"weight": sd[f"{prefix}{n}.weight"], "bias": sd[f"{prefix}{n}.bias"]})
+
+    def forward(self, x, mask):
+        B, S, _ = x.shape
+        h, d = self.local_heads, self.head_dim
+        qkv = self.qkv(x).view(B, S, 3, h, d).permute(2, 0, 3, 1, 4)  # [3, B, h, S, d]
+        drop = self.cfg.dropout if self.training else 0.0
+        ctx = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=mask, dropout_p=drop)
+        ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
+        a = F.dropout(self.attn_out(ctx), drop, self.training)
+        x = fb.add_layernorm(a, x, self.ln1.weight, self.ln1.bias, self.cfg.ln_eps)
+        f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
+        f = F.dropout(self.ffn_out(f), drop, self.training)
+        return fb.add_layernorm(f, x, self.ln2.weight, self.ln2.bias, self.cfg.ln_eps)
+
+
+class BertForSequenceClassification(nn.Module):
+    def __init__(self, cfg: BertConfig | None = None, tp: TPGroup | None = None, seed: int | None = 0):
+        super().__init__()
+        self.cfg = cfg or BertConfig()
+        self.tp = tp or TPGroup(None)
+        c = self.cfg
+        self.word = VocabParallelEmbedding(c.vocab_size, c.hidden, self.tp)
+        self.pos = nn.Embedding(c.max_position, c.hidden)
+        self.tok_type = nn.Embedding(c.type_vocab, c.hidden)
+        self.ln_emb = nn.LayerNorm(c.hidden, eps=c.ln_eps)
+        self.layers = nn.ModuleList([BertLayer(c, self.tp) for _ in range(c.layers)])
+        self.pooler = nn.Linear(c.hidden, c.hidden)
+        self.classifier = nn.Linear(c.hidden, c.num_labels)
+        if seed is not None:
+            self.init_weights(seed)
+
+    def init_weights(self, seed: int) -> None:
+        """Initialise as the full model would, then take this rank's shard (so any TP degree matches TP=1)."""
+        full = full_init_state(self.cfg, seed)
+        self.load_full(full)
+
+    def load_full(self, sd: dict) -> None:
+        self.word.load_full(sd["word.weight"])
+        for n in ("pos", "tok_type", "ln_emb", "pooler", "classifier"):
+            getattr(self, n).load_state_dict({k.split(".", 1)[1]: v for k, v in sd.items() if k.startswith(n + ".")})
+        for i, layer in enumerate(self.layers):
+            layer.load_full(sd, f"layers.{i}.")
+
+    def forward(self, input_ids, token_type_ids=None, attention_mask=None):
+        B, S = input_ids.shape
+        pos = torch.arange(S, device=input_ids.device)
+        tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
+        x = self.word(input_ids) + self.pos(pos)[None] + self.tok_type(tt)
+        x = F.dropout(self.ln_emb(x), self.cfg.dropout, self.training)
+        mask = None
+        if attention_mask is not None:  # additive mask [B, 1, 1, S]
+            mask = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * torch.finfo(x.dtype).min
+        for layer in self.layers:
+            x = layer(x, mask)
+        pooled = torch.tanh(self.pooler(x[:, 0]))
+        return self.classifier(F.dropout(pooled, self.cfg.dropout, self.training))
+
+
+def full_init_state(cfg: BertConfig, seed: int) -> dict:
+    """TP=1 parameter dict (BERT init: N(0, 0.02) weights, zero biases, unit LayerNorm)."""
+    g = torch.Generator().manual_seed(seed)
+
+    def n(*shape):
+        return torch.randn(*shape, generator=g) * cfg.init_std
+
+    H, I = cfg.hidden, cfg.intermediate
+    sd = {"word.weight": n(cfg.vocab_size, H), "pos.weight": n(cfg.max_position, H), "tok_type.weight": n(cfg.type_vocab, H),
+          "ln_emb.weight": torch.ones(H), "ln_emb.bias": torch.zeros(H), "pooler.weight": n(H, H),
+          "pooler.bias": torch.zeros(H), "classifier.weight": n(cfg.num_labels, H),
+          "classifier.bias": torch.zeros(cfg.num_labels)}
+    for i in range(cfg.layers):
+        p = f"layers.{i}."
+        sd.update({p + "qkv.weight": n(3 * H, H), p + "qkv.bias": torch.zeros(3 * H),
+                   p + "attn_out.weight": n(H, H), p + "attn_out.bias": torch.zeros(H),
+                   p + "ln1.weight": torch.ones(H), p + "ln1.bias": torch.zeros(H),
+                   p + "ffn_in.weight": n(I, H), p + "ffn_in.bias": torch.zeros(I),
+                   p + "ffn_out.weight": n(H, I), p + "ffn_out.bias": torch.zeros(H),
+                   p + "ln2.weight": torch.ones(H), p + "ln2.bias": torch.zeros(H)})
+    return sd
+
+
+def gather_full_state(model: BertForSequenceClassification) -> dict:
+    """Reassemble the TP=1 state dict from all ranks (for checkpoints / equivalence tests)."""
+    import torch.distributed as dist
+
+    tp = model.tp
+
+    def gather(t: torch.Tensor, dim: int, sizes) -> torch.Tensor:
+        if tp.size == 1:
+            return t.detach().clone()
+        mx = max(sizes)
+        pad = [0, 0] * (t.dim() - 1 - dim) + [0, mx - t.shape[dim]]
+        tt = F.pad(t.detach(), pad).contiguous()
+        outs = [torch.empty_like(tt) for _ in range(tp.size)]
+        dist.all_gather(outs, tt, group=tp.group)
+        return torch.cat([o.narrow(dim, 0, s) for o, s in zip(outs, sizes)], dim)
+
+    sd = {"word.weight": gather(model.word.weight, 0, model.word.sizes)}
+    for n in ("pos", "tok_type", "ln_emb", "pooler", "classifier"):
+        for k, v in getattr(model, n).state_dict().items():
+            sd[f"{n}.{k}"] = v.detach().clone()
+    for i, L in enumerate(model.layers):
+        p = f"layers.{i}."
+        d = L.head_dim
+        w = gather(L.qkv.weight, 0, L.qkv.sizes)
+        b = gather(L.qkv.bias, 0, L.qkv.sizes)
+        # re-interleave per-rank [q_r; k_r; v_r] blocks into [Q; K; V]
+        chunks_w, chunks_b, off = [[], [], []], [[], [], []], 0
+        for h in L.heads_per_rank:
+            for k in range(3):
+                chunks_w[k].append(w[off + k * h * d: off + (k + 1) * h * d])
+                chunks_b[k].append(b[off + k * h * d: off + (k + 1) * h * d])
+            off += 3 * h * d
+        sd[p + "qkv.weight"] = torch.cat([torch.cat(c) for c in chunks_w])
+        sd[p + "qkv.bias"] = torch.cat([torch.cat(c) for c in chunks_b])
+        sd[p + "attn_out.weight"] = gather(L.attn_out.weight, 1, L.attn_out.sizes)
+        sd[p + "attn_out.bias"] = L.attn_out.bias.detach().clone()
+        sd[p + "ffn_in.weight"] = gather(L.ffn_in.weight, 0, L.ffn_in.sizes)
+        sd[p + "ffn_in.bias"] = gather(L.ffn_in.bias, 0, L.ffn_in.sizes)
+        sd[p + "ffn_out.weight"] = gather(L.ffn_out.weight, 1, L.ffn_out.sizes)
+        sd[p + "ffn_out.bias"] = L.ffn_out.bias.detach().clone()
+        for n in ("ln1", "ln2"):
+            sd[f"{p}{n}.weight"] = getattr(L, n).weight.detach().clone()
+            sd[f"{p}{n}.bias"] = getattr(L, n).bias.detach().clone()
+    return sd
+
+
+def num_params(cfg: BertConfig) -> int:
+    H, I, L = cfg.hidden, cfg.intermediate, cfg.layers
+    per_layer = 3 * H * H + 3 * H + H * H + H + 2 * H + I * H + I + H * I + H + 2 * H
+    return (cfg.vocab_size + cfg.max_position + cfg.type_vocab) * H + 2 * H + L * per_layer + H * H + H \
+        + cfg.num_labels * (H + 1)

@@ -1,0 +1,123 @@
+"""BERT + Megatron-style tensor parallelism: TP=2/3 (gloo, CPU) must equal the TP=1 model exactly
+(uneven head split at TP=3), for the forward logits and for parameters after an optimizer step."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mifx.models.bert import BertConfig, BertForSequenceClassification, full_init_state, gather_full_state, num_params
+from mifx.parallel.tensor_parallel import TPGroup, head_partition, split_sizes
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batch(cfg, B=3, S=16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), generator=g)
+    tt = torch.randint(0, 2, (B, S), generator=g)
+    am = torch.ones(B, S)
+    am[0, 12:] = 0
+    y = torch.randint(0, cfg.num_labels, (B,), generator=g)
+    return ids, tt, am, y
+
+
+def _step(model, cfg, lr=0.1):
+    ids, tt, am, y = _batch(cfg)
+    logits = model(ids, tt, am)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    with torch.no_grad():
+        for p in model.parameters():
+            p -= lr * p.grad
+    return logits.detach()
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = BertConfig.tiny(dropout=0.0)
+    m = BertForSequenceClassification(cfg, TPGroup(), seed=1)
+    logits = _step(m, cfg)
+    full = gather_full_state(m)
+    if rank == 0:
+        torch.save({"logits": logits, "state": full}, out)
+    dist.destroy_process_group()
+
+
+def test_partitions():
+    assert head_partition(12, 8) == [2, 2, 2, 2, 1, 1, 1, 1]
+    assert split_sizes(3072, 8) == [384] * 8 and sum(split_sizes(30522, 8)) == 30522
+    assert num_params(BertConfig()) == sum(v.numel() for v in full_init_state(BertConfig(layers=1), 0).values()) \
+        + 11 * (sum(v.numel() for k, v in full_init_state(BertConfig(layers=1), 0).items() if k.startswith("layers.")))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tp_matches_single_process(world):
+    cfg = BertConfig.tiny(dropout=0.0)
+    ref = BertForSequenceClassification(cfg, None, seed=1)
+    ref_logits = _step(ref, cfg)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        got = torch.load(out, weights_only=True)
+    torch.testing.assert_close(got["logits"], ref_logits, rtol=1e-5, atol=1e-5)
+    ref_sd = gather_full_state(ref)
+    for k, v in ref_sd.items():
+        np.testing.assert_allclose(got["state"][k].numpy(), v.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_fused_add_layernorm_and_bias_gelu_gpu():
+    from mifx.ops import fused_bert as fb
+
+    torch.manual_seed(0)
+    for dtype, tol in ((torch.float32, 1e-5), (torch.bfloat16, 2e-2)):
+        for H in (64, 768, 1000):
+            a = torch.randn(37, 5, H, device="cuda", dtype=dtype, requires_grad=True)
+            r = torch.randn(37, 5, H, device="cuda", dtype=dtype, requires_grad=True)
+            w = torch.randn(H, device="cuda", requires_grad=True)
+            b = torch.randn(H, device="cuda", requires_grad=True)
+            y = fb.add_layernorm(a, r, w, b, 1e-12)
+            a32, r32 = a.detach().float().requires_grad_(), r.detach().float().requires_grad_()
+            w2, b2 = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+            ref = torch.nn.functional.layer_norm(a32 + r32, (H,), w2, b2, 1e-12)
+            torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+            g = torch.randn_like(ref)
+            y.backward(g.to(dtype))
+            ref.backward(g)
+            torch.testing.assert_close(a.grad.float(), a32.grad, rtol=tol * 4, atol=tol * 4)
+            torch.testing.assert_close(w.grad, w2.grad, rtol=tol * 4, atol=tol * 40)
+            torch.testing.assert_close(b.grad, b2.grad, rtol=tol * 4, atol=tol * 40)
+        x = torch.randn(64, 3072, device="cuda", dtype=dtype, requires_grad=True)
+        bias = torch.randn(3072, device="cuda", requires_grad=True)
+        y = fb.bias_gelu(x, bias)
+        x2, b2 = x.detach().float().requires_grad_(), bias.detach().clone().requires_grad_()
+        ref = torch.nn.functional.gelu(x2 + b2)
+        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+        g = torch.randn_like(ref)
+        y.backward(g.to(dtype))
+        ref.backward(g)
+        torch.testing.assert_close(x.grad.float(), x2.grad, rtol=tol * 4, atol=tol * 4)
+        torch.testing.assert_close(bias.grad, b2.grad, rtol=tol * 4, atol=tol * 60)
+
+
+@pytest.mark.gpu
+def test_bert_base_gpu_train_step_bf16():
+    cfg = BertConfig(dropout=0.0)
+    m = BertForSequenceClassification(cfg, None, seed=0).cuda()
+    ids, tt, am, y = (t.cuda() for t in _batch(cfg, B=8, S=128))
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-5, fused=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = torch.nn.functional.cross_entropy(m(ids, tt, am).float(), y)
+    loss.backward()
+    opt.step()
+    assert torch.isfinite(loss)
