@@ -10,7 +10,8 @@
 //  * add_ln_bwd: recomputes x_hat from (a + r); dx = rstd (g - mean(g) - x_hat mean(g x_hat)), g = dy w;
 //    dw / db accumulated per lane across the workgroup's rows, written as per-block partials
 //    [nblocks, H] (deterministic; summed by the caller).
-//  * bias_gelu_fwd / bwd: 8 elements per thread with 16-byte vector loads for bf16.
+//  * bias_gelu_fwd / bwd: column-per-thread over row chunks (no per-element index math); the
+//    backward also produces the bias-gradient column partials, reduced by col_reduce2.
 // Activations are bf16 or fp32 (template), LayerNorm params and statistics fp32.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
@@ -36,6 +37,15 @@ __device__ __forceinline__ void st(T* p, float v) {
 template <>
 __device__ __forceinline__ void st<__hip_bfloat16>(__hip_bfloat16* p, float v) {
   *p = __float2bfloat16(v);
+}
+
+template <typename T>
+__device__ __forceinline__ float cvt_round(float v) {
+  return (float)(T)v;
+}
+template <>
+__device__ __forceinline__ float cvt_round<__hip_bfloat16>(float v) {
+  return __bfloat162float(__float2bfloat16(v));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -150,19 +160,53 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * expf(-0.5f * x * x);
 }
 
+// grid (ceil(N / kThreads), row chunks): thread owns one column, walks its chunk of rows —
+// no per-element 64-bit div/mod, coalesced across the wave, and the bias-gradient column
+// partial falls out of the same loop (written to db_part[chunk][col]).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bias_gelu_fwd(const T* __restrict__ x, const float* __restrict__ bias,
-                                                         long long n, int N, T* __restrict__ y) {
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads)
-    st(y + i, gelu_f(ld(x + i) + bias[i % N]));
+                                                         int M, int N, T* __restrict__ y) {
+  const int col = blockIdx.x * kThreads + threadIdx.x;
+  if (col >= N) return;
+  const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
+  const float bb = bias[col];
+  for (int r = r0; r < r1; ++r) {
+    const size_t i = (size_t)r * N + col;
+    st(y + i, gelu_f(ld(x + i) + bb));
+  }
 }
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bias_gelu_bwd(const T* __restrict__ dy, const T* __restrict__ x,
-                                                         const float* __restrict__ bias, long long n, int N,
-                                                         T* __restrict__ dx) {
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads)
-    st(dx + i, ld(dy + i) * gelu_grad(ld(x + i) + bias[i % N]));
+                                                         const float* __restrict__ bias, int M, int N,
+                                                         T* __restrict__ dx, float* __restrict__ db_part) {
+  const int col = blockIdx.x * kThreads + threadIdx.x;
+  if (col >= N) return;
+  const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
+  const float bb = bias[col];
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const size_t i = (size_t)r * N + col;
+    const float g = ld(dy + i) * gelu_grad(ld(x + i) + bb);
+    st(dx + i, g);
+    acc += (float)cvt_round<T>(g);  // bias grad of the value actually stored
+  }
+  db_part[(size_t)blockIdx.y * N + col] = acc;
+}
+
+// sum `rows` partial rows of width N (fixed order) for up to two buffers in one launch
+__global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                       int rows, int N, float* __restrict__ o0,
+                                                       float* __restrict__ o1) {
+  const int col = blockIdx.x * kThreads + threadIdx.x;
+  if (col >= N) return;
+  float a = 0.f, b = 0.f;
+  for (int r = 0; r < rows; ++r) {
+    a += p0[(size_t)r * N + col];
+    if (p1 != nullptr) b += p1[(size_t)r * N + col];
+  }
+  o0[col] = a;
+  if (o1 != nullptr) o1[col] = b;
 }
 
 template <typename T, int PER>
@@ -193,52 +237,65 @@ int dispatch_add_ln(int fwd, const void* dy, const void* a, const void* r, const
 
 extern "C" {
 
+// partial-row count used by add_ln_bwd (fewer, fatter blocks: each wave walks many rows)
 int mifx_bert_ln_blocks(int R) {
   const int need = (R + 3) / 4;
-  return need < 2048 ? (need > 0 ? need : 1) : 2048;
+  return need < 256 ? (need > 0 ? need : 1) : 256;
 }
+
+// rows of partials for bias_gelu_bwd
+int mifx_bert_gelu_chunks(int M) { return M < 64 ? 1 : (M / 64 < 128 ? M / 64 : 128); }
 
 // dtype: 0 fp32, 1 bf16
 int mifx_bert_add_ln_fwd(int dtype, const void* a, const void* r, const float* w, const float* b, int R, int H,
                          float eps, void* y, float* mean, float* rstd, hipStream_t st) {
   if (H <= 0 || H > 64 * kMaxPer || R <= 0) return -1;
-  const int blocks = mifx_bert_ln_blocks(R);
+  const int need = (R + 3) / 4;
+  const int blocks = need < 4096 ? need : 4096;
   return dtype ? dispatch_add_ln<__hip_bfloat16>(1, nullptr, a, r, w, b, R, H, eps, y, mean, rstd, nullptr, nullptr,
                                                  blocks, st)
                : dispatch_add_ln<float>(1, nullptr, a, r, w, b, R, H, eps, y, mean, rstd, nullptr, nullptr, blocks, st);
 }
 
-// dw_part / db_part: [mifx_bert_ln_blocks(R), H]
+// scratch: dw_part / db_part [mifx_bert_ln_blocks(R), H]; outputs dw, db [H] (fp32)
 int mifx_bert_add_ln_bwd(int dtype, const void* dy, const void* a, const void* r, const float* w, const float* mean,
-                         const float* rstd, int R, int H, void* dx, float* dw_part, float* db_part, hipStream_t st) {
+                         const float* rstd, int R, int H, void* dx, float* dw_part, float* db_part, float* dw,
+                         float* db, hipStream_t st) {
   if (H <= 0 || H > 64 * kMaxPer || R <= 0) return -1;
   const int blocks = mifx_bert_ln_blocks(R);
-  return dtype ? dispatch_add_ln<__hip_bfloat16>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd,
-                                                 dw_part, db_part, blocks, st)
-               : dispatch_add_ln<float>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd, dw_part,
-                                        db_part, blocks, st);
+  const int rc = dtype ? dispatch_add_ln<__hip_bfloat16>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean,
+                                                         (float*)rstd, dw_part, db_part, blocks, st)
+                       : dispatch_add_ln<float>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd,
+                                                dw_part, db_part, blocks, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(col_reduce2, dim3((H + kThreads - 1) / kThreads), dim3(kThreads), 0, st, dw_part, db_part, blocks,
+                     H, dw, db);
+  return (int)hipGetLastError();
 }
 
-int mifx_bert_bias_gelu(int dtype, int fwd, const void* dy, const void* x, const float* bias, long long n, int N,
-                        void* out, hipStream_t st) {
-  if (n <= 0 || N <= 0) return -1;
-  const long long need = (n + kThreads - 1) / kThreads;
-  const int blocks = (int)(need < 8192 ? need : 8192);
+// x: [M, N]; fwd -> out = gelu(x + bias); bwd -> out = dx, db [N] (scratch db_part [gelu_chunks(M), N])
+int mifx_bert_bias_gelu(int dtype, int fwd, const void* dy, const void* x, const float* bias, int M, int N, void* out,
+                        float* db_part, float* db, hipStream_t st) {
+  if (M <= 0 || N <= 0) return -1;
+  const int chunks = fwd ? (M < 1024 ? M : 1024) : mifx_bert_gelu_chunks(M);
+  const dim3 grid((N + kThreads - 1) / kThreads, chunks);
   if (dtype) {
     if (fwd)
-      hipLaunchKernelGGL(bias_gelu_fwd<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st,
-                         (const __hip_bfloat16*)x, bias, n, N, (__hip_bfloat16*)out);
+      hipLaunchKernelGGL(bias_gelu_fwd<__hip_bfloat16>, grid, dim3(kThreads), 0, st, (const __hip_bfloat16*)x, bias, M,
+                         N, (__hip_bfloat16*)out);
     else
-      hipLaunchKernelGGL(bias_gelu_bwd<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st,
-                         (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, bias, n, N, (__hip_bfloat16*)out);
+      hipLaunchKernelGGL(bias_gelu_bwd<__hip_bfloat16>, grid, dim3(kThreads), 0, st, (const __hip_bfloat16*)dy,
+                         (const __hip_bfloat16*)x, bias, M, N, (__hip_bfloat16*)out, db_part);
   } else {
     if (fwd)
-      hipLaunchKernelGGL(bias_gelu_fwd<float>, dim3(blocks), dim3(kThreads), 0, st, (const float*)x, bias, n, N,
-                         (float*)out);
+      hipLaunchKernelGGL(bias_gelu_fwd<float>, grid, dim3(kThreads), 0, st, (const float*)x, bias, M, N, (float*)out);
     else
-      hipLaunchKernelGGL(bias_gelu_bwd<float>, dim3(blocks), dim3(kThreads), 0, st, (const float*)dy, (const float*)x,
-                         bias, n, N, (float*)out);
+      hipLaunchKernelGGL(bias_gelu_bwd<float>, grid, dim3(kThreads), 0, st, (const float*)dy, (const float*)x, bias, M,
+                         N, (float*)out, db_part);
   }
+  if (!fwd)
+    hipLaunchKernelGGL(col_reduce2, dim3((N + kThreads - 1) / kThreads), dim3(kThreads), 0, st, db_part, nullptr,
+                       chunks, N, db, nullptr);
   return (int)hipGetLastError();
 }
 

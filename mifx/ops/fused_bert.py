@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from ._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
+from ._lib import F32, I32, VP, check, ptr, sig, stream_handle
 
 
 @functools.lru_cache(maxsize=None)
@@ -18,9 +18,10 @@ def _fns():
     lib = _lib.load("fused_bert")
     return {
         "blocks": sig(lib, "mifx_bert_ln_blocks", [I32]),
+        "gchunks": sig(lib, "mifx_bert_gelu_chunks", [I32]),
         "ln_fwd": sig(lib, "mifx_bert_add_ln_fwd", [I32, VP, VP, VP, VP, I32, I32, F32, VP, VP, VP, VP]),
-        "ln_bwd": sig(lib, "mifx_bert_add_ln_bwd", [I32, VP, VP, VP, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
-        "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, VP, VP, VP, I64, I32, VP, VP]),
+        "ln_bwd": sig(lib, "mifx_bert_add_ln_bwd", [I32, VP, VP, VP, VP, VP, VP, I32, I32, VP, VP, VP, VP, VP, VP]),
+        "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
     }
 
 
@@ -56,12 +57,12 @@ class _AddLayerNorm(torch.autograd.Function):
         R = a.numel() // H
         nb = _fns()["blocks"](R)
         dx = torch.empty_like(a)
-        dwp = torch.empty(nb, H, device=a.device, dtype=torch.float32)
-        dbp = torch.empty_like(dwp)
+        part = torch.empty(2, nb, H, device=a.device, dtype=torch.float32)
+        dwdb = torch.empty(2, H, device=a.device, dtype=torch.float32)
         check(_fns()["ln_bwd"](_dt(a), ptr(dy), ptr(a), ptr(r), ptr(w32), ptr(mean), ptr(rstd), R, H, ptr(dx),
-                               ptr(dwp), ptr(dbp), stream_handle(a.device)), "mifx_bert_add_ln_bwd")
-        dw, db = dwp.sum(0).to(ctx.wdtype), dbp.sum(0).to(ctx.wdtype)
-        return dx, dx, dw, db, None
+                               ptr(part[0]), ptr(part[1]), ptr(dwdb[0]), ptr(dwdb[1]), stream_handle(a.device)),
+              "mifx_bert_add_ln_bwd")
+        return dx, dx, dwdb[0].to(ctx.wdtype), dwdb[1].to(ctx.wdtype), None
 
 
 class _BiasGelu(torch.autograd.Function):
@@ -70,7 +71,8 @@ class _BiasGelu(torch.autograd.Function):
         x = x.contiguous()
         b32 = bias.float().contiguous()
         y = torch.empty_like(x)
-        check(_fns()["gelu"](_dt(x), 1, None, ptr(x), ptr(b32), x.numel(), x.shape[-1], ptr(y),
+        N = x.shape[-1]
+        check(_fns()["gelu"](_dt(x), 1, None, ptr(x), ptr(b32), x.numel() // N, N, ptr(y), None, None,
                              stream_handle(x.device)), "mifx_bert_bias_gelu")
         ctx.save_for_backward(x, b32)
         ctx.bdtype = bias.dtype
@@ -81,9 +83,13 @@ class _BiasGelu(torch.autograd.Function):
         x, b32 = ctx.saved_tensors
         dy = dy.contiguous().to(x.dtype)
         dx = torch.empty_like(x)
-        check(_fns()["gelu"](_dt(x), 0, ptr(dy), ptr(x), ptr(b32), x.numel(), x.shape[-1], ptr(dx),
+        N = x.shape[-1]
+        M = x.numel() // N
+        part = torch.empty(_fns()["gchunks"](M), N, device=x.device, dtype=torch.float32)
+        db = torch.empty(N, device=x.device, dtype=torch.float32)
+        check(_fns()["gelu"](_dt(x), 0, ptr(dy), ptr(x), ptr(b32), M, N, ptr(dx), ptr(part), ptr(db),
                              stream_handle(x.device)), "mifx_bert_bias_gelu")
-        return dx, dx.reshape(-1, x.shape[-1]).float().sum(0).to(ctx.bdtype)
+        return dx, db.to(ctx.bdtype)
 
 
 def add_layernorm(a: torch.Tensor, r: torch.Tensor, weight, bias, eps: float = 1e-12) -> torch.Tensor:

@@ -153,7 +153,8 @@ class RowParallelLinear(nn.Module):
 
     def forward(self, x_shard):
         y = reduce_from_tp(F.linear(x_shard, self.weight), self.tp)
-        return y + self.bias if self.bias is not None else y
+        # add the bias in the activation dtype (keeps a bf16 residual stream under autocast)
+        return y + self.bias.to(y.dtype) if self.bias is not None else y
 
 
 class VocabParallelEmbedding(nn.Module):
