@@ -231,8 +231,9 @@ class Client:
     KUBE_PROXY_PATH = "api/v1/namespaces/{}/services/ml-pipeline:http/proxy/"
 
     def __init__(self, host: str | None = None, client_id: str | None = None, namespace: str = "kubeflow",
-                 max_parallel: int = 4):
+                 max_parallel: int = 4, poll_interval: float = 5.0):
         self._host = host
+        self.poll_interval = poll_interval
         if host is not None and (host == "local" or host.startswith("local://")):
             root = host[len("local://"):] if host.startswith("local://") else \
                 os.path.join(os.path.expanduser("~"), ".mifx", "pipelines")
@@ -394,7 +395,7 @@ class Client:
                 raise TimeoutError("Run timeout")
             logging.info("Waiting for the job to complete...")
             if not self.is_local:
-                time.sleep(5)
+                time.sleep(self.poll_interval)
 
     def _get_workflow_json(self, run_id: str) -> dict:
         return json.loads(self.get_run(run_id).pipeline_runtime.workflow_manifest)

@@ -320,3 +320,39 @@ def test_workflow_status_written(tmp_path):
     st = _run_local(PIPELINES["retry"], tmp_path)
     with open(tmp_path / "run" / "status.json") as f:
         assert json.load(f)["phase"] == st["phase"]
+
+
+def test_pipelines_api_server_with_rest_client(tmp_path):
+    import threading
+
+    import uvicorn
+
+    from mifx.kfp.server import create_app
+    from tests.test_parallel_cpu import _free_port
+
+    port = _free_port()
+    server = uvicorn.Server(uvicorn.Config(create_app(str(tmp_path / "api")), host="127.0.0.1", port=port,
+                                           log_level="error"))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    try:
+        import time as _t
+
+        for _ in range(100):
+            if server.started:
+                break
+            _t.sleep(0.05)
+        pkg = str(tmp_path / "p.tar.gz")
+        compiler.Compiler().compile(PIPELINES["retry"], pkg)
+        client = Client(host=f"http://127.0.0.1:{port}", poll_interval=0.2)
+        exp = client.create_experiment("rest-exp")
+        assert client.get_experiment(experiment_name="rest-exp").id == exp.id
+        run = client.run_pipeline(exp.id, "rest-run", pkg, {})
+        detail = client.wait_for_run_completion(run.id, timeout=120)
+        assert detail.run.status in ("Succeeded", "Failed")  # random failures are the sample's point
+        assert client.list_runs(experiment_id=exp.id).runs[0].id == run.id
+        pl = client.upload_pipeline(pkg, "retry")
+        assert any(p.id == pl.id for p in client.list_pipelines().pipelines)
+    finally:
+        server.should_exit = True
+        th.join(timeout=10)

@@ -1,0 +1,58 @@
+"""Training-job specs (TFJob / PyTorchJob / MIFXJob) and the local multi-process launcher."""
+import json
+import sys
+
+import pytest
+import yaml
+
+from mifx.launch import JobSpec, launch_local, to_indexed_job, validate
+
+_WORKER = """
+import json, os, sys
+import torch.distributed as dist
+dist.init_process_group("gloo")
+t = __import__("torch").tensor([float(dist.get_rank() + 1)])
+dist.all_reduce(t)
+out = {"rank": dist.get_rank(), "world": dist.get_world_size(), "sum": float(t), "tf": os.environ.get("TF_CONFIG")}
+open(os.path.join(sys.argv[1], f"r{dist.get_rank()}.json"), "w").write(json.dumps(out))
+dist.destroy_process_group()
+"""
+
+
+def _job(kind, key, roles, worker, out):
+    return {"apiVersion": "kubeflow.org/v1", "kind": kind, "metadata": {"name": "t"},
+            "spec": {key: {role: {"replicas": n, "template": {"spec": {"containers": [
+                {"name": "c", "image": "img", "command": ["python", str(worker), str(out)]}]}}} for role, n in roles}}}
+
+
+def test_validation_rules():
+    with pytest.raises(ValueError):
+        JobSpec.from_dict({"kind": "TFJob", "spec": {"tfReplicaSpecs": {"Chief": {"replicas": 2, "template": {
+            "spec": {"containers": [{"command": ["x"]}]}}}}}})
+    with pytest.raises(ValueError):
+        JobSpec.from_dict({"kind": "PyTorchJob", "spec": {"pytorchReplicaSpecs": {"Worker": {"replicas": 0}}}})
+
+
+@pytest.mark.parametrize("kind,key,roles", [("PyTorchJob", "pytorchReplicaSpecs", [("Master", 1), ("Worker", 2)]),
+                                             ("TFJob", "tfReplicaSpecs", [("Worker", 3)])])
+def test_launch_local_ranks(tmp_path, kind, key, roles):
+    worker = tmp_path / "w.py"
+    worker.write_text(_WORKER)
+    spec = JobSpec.from_dict(_job(kind, key, roles, worker, tmp_path))
+    validate(spec)
+    codes = launch_local(spec, num_gpus=0, timeout=120, log_dir=str(tmp_path / "logs"))
+    assert all(c == 0 for c in codes.values()), codes
+    outs = [json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(3)]
+    assert {o["rank"] for o in outs} == {0, 1, 2} and all(o["sum"] == 6.0 for o in outs)
+    if kind == "TFJob":
+        tf = json.loads(outs[0]["tf"])
+        assert len(tf["cluster"]["worker"]) == 3 and tf["task"]["type"] == "worker"
+
+
+def test_render_indexed_job(tmp_path):
+    spec = JobSpec.from_yaml("deploy/k8s/wide-deep-dp8-job.yaml")
+    job = to_indexed_job(spec)
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert "--nproc-per-node=8" in c["command"] and c["resources"]["limits"]["amd.com/gpu"] == "8"
+    assert yaml.safe_load(yaml.safe_dump(job)) == job
+    _ = sys
