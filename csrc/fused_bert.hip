@@ -185,25 +185,70 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_bwd(const T* __restrict__ 
   const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
   const float bb = bias[col];
   float acc = 0.f;
-  for (int r = r0; r < r1; ++r) {
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {  // 8 independent loads in flight per thread
+    float d[4], v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t i = (size_t)(r + u) * N + col;
+      d[u] = ld(dy + i);
+      v[u] = ld(x + i);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float g = d[u] * gelu_grad(v[u] + bb);
+      st(dx + (size_t)(r + u) * N + col, g);
+      acc += cvt_round<T>(g);  // bias grad of the value actually stored
+    }
+  }
+  for (; r < r1; ++r) {
     const size_t i = (size_t)r * N + col;
     const float g = ld(dy + i) * gelu_grad(ld(x + i) + bb);
     st(dx + i, g);
-    acc += (float)cvt_round<T>(g);  // bias grad of the value actually stored
+    acc += cvt_round<T>(g);
   }
   db_part[(size_t)blockIdx.y * N + col] = acc;
 }
 
 // sum `rows` partial rows of width N (fixed order) for up to two buffers in one launch
+// block = kRedCols columns x kRedSlices row slices (each slice strides the rows, 4 loads in
+// flight), slices combined in LDS in a fixed order -> deterministic, ~N/32 workgroups
+constexpr int kRedCols = 32, kRedSlices = kThreads / kRedCols;
+
 __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict__ p0, const float* __restrict__ p1,
                                                        int rows, int N, float* __restrict__ o0,
                                                        float* __restrict__ o1) {
-  const int col = blockIdx.x * kThreads + threadIdx.x;
-  if (col >= N) return;
+  __shared__ float sa[kRedSlices][kRedCols];
+  __shared__ float sb[kRedSlices][kRedCols];
+  const int cx = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int col = blockIdx.x * kRedCols + cx;
   float a = 0.f, b = 0.f;
-  for (int r = 0; r < rows; ++r) {
-    a += p0[(size_t)r * N + col];
-    if (p1 != nullptr) b += p1[(size_t)r * N + col];
+  if (col < N) {
+    int r = sl;
+    for (; r + 3 * kRedSlices < rows; r += 4 * kRedSlices) {
+      const float a0 = p0[(size_t)r * N + col], a1 = p0[(size_t)(r + kRedSlices) * N + col];
+      const float a2 = p0[(size_t)(r + 2 * kRedSlices) * N + col], a3 = p0[(size_t)(r + 3 * kRedSlices) * N + col];
+      a += (a0 + a1) + (a2 + a3);
+      if (p1 != nullptr) {
+        const float b0 = p1[(size_t)r * N + col], b1 = p1[(size_t)(r + kRedSlices) * N + col];
+        const float b2 = p1[(size_t)(r + 2 * kRedSlices) * N + col], b3 = p1[(size_t)(r + 3 * kRedSlices) * N + col];
+        b += (b0 + b1) + (b2 + b3);
+      }
+    }
+    for (; r < rows; r += kRedSlices) {
+      a += p0[(size_t)r * N + col];
+      if (p1 != nullptr) b += p1[(size_t)r * N + col];
+    }
+  }
+  sa[sl][cx] = a;
+  sb[sl][cx] = b;
+  __syncthreads();
+  if (sl != 0 || col >= N) return;
+  a = 0.f;
+  b = 0.f;
+  for (int i = 0; i < kRedSlices; ++i) {
+    a += sa[i][cx];
+    b += sb[i][cx];
   }
   o0[col] = a;
   if (o1 != nullptr) o1[col] = b;
@@ -268,7 +313,7 @@ int mifx_bert_add_ln_bwd(int dtype, const void* dy, const void* a, const void* r
                        : dispatch_add_ln<float>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd,
                                                 dw_part, db_part, blocks, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(col_reduce2, dim3((H + kThreads - 1) / kThreads), dim3(kThreads), 0, st, dw_part, db_part, blocks,
+  hipLaunchKernelGGL(col_reduce2, dim3((H + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, dw_part, db_part, blocks,
                      H, dw, db);
   return (int)hipGetLastError();
 }
@@ -294,7 +339,7 @@ int mifx_bert_bias_gelu(int dtype, int fwd, const void* dy, const void* x, const
                          N, (float*)out, db_part);
   }
   if (!fwd)
-    hipLaunchKernelGGL(col_reduce2, dim3((N + kThreads - 1) / kThreads), dim3(kThreads), 0, st, db_part, nullptr,
+    hipLaunchKernelGGL(col_reduce2, dim3((N + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, db_part, nullptr,
                        chunks, N, db, nullptr);
   return (int)hipGetLastError();
 }
