@@ -103,11 +103,15 @@ def generate_statistics_from_table(table: pa.Table, name: str = "", device=None)
     return {"datasets": [{"name": name, "num_examples": int(n), "features": feats}]}
 
 
+_CSV_CONVERT = pacsv.ConvertOptions(strings_can_be_null=True)  # empty CSV field == missing (TFDV semantics)
+
+
 def read_csv_table(path: str) -> pa.Table:
     if os.path.isdir(path):
         files = sorted(os.path.join(path, f) for f in os.listdir(path) if f.endswith(".csv"))
-        return pa.concat_tables([pacsv.read_csv(f) for f in files], promote_options="default")
-    return pacsv.read_csv(path)
+        return pa.concat_tables([pacsv.read_csv(f, convert_options=_CSV_CONVERT) for f in files],
+                                promote_options="default")
+    return pacsv.read_csv(path, convert_options=_CSV_CONVERT)
 
 
 def generate_statistics_from_csv(path: str, name: str = "", device=None) -> dict:

@@ -1,0 +1,53 @@
+"""The notebook-equivalent examples (examples/notebooks/nXX_*.py) run end to end at small sizes."""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+NB = os.path.join(os.path.dirname(__file__), "..", "examples", "notebooks")
+
+
+def _load(name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(NB, name + ".py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_n02_data_validation(tmp_path):
+    r = _load("n02_data_validation").main(["--workdir", str(tmp_path), "--rows", "1500"])
+    assert bool(r["anomalies"])          # unseen company / payment type in eval
+    assert not bool(r["relaxed"])        # min_domain_mass 0.9 + added domain value
+    assert not bool(r["serving"])        # tips not expected in SERVING
+    assert bool(r["skew_drift"])         # L-inf thresholds 0.01 / 0.001 trip
+    assert os.path.exists(r["schema_path"])
+
+
+def test_n03_transform_matches_tft_doc_output():
+    out = _load("n03_transform").main()
+    assert [o["x_centered"] for o in out] == [-1.0, 0.0, 1.0]
+    assert [o["y_normalized"] for o in out] == [0.0, 0.5, 1.0]
+    assert [o["s_integerized"] for o in out] == [0, 1, 0]
+    assert [o["x_centered_times_y_normalized"] for o in out] == [-0.0, 0.0, 1.0]
+
+
+def test_n03a_census(tmp_path):
+    r = _load("n03a_transform_census").main(["--workdir", str(tmp_path), "--train_rows", "2000", "--test_rows",
+                                             "600", "--epochs", "3", "--device", "cpu"])
+    assert r["bad_elements"] == 6 and r["train"] == 2000 and r["test"] == 600
+    assert r["accuracy"] > 0.7
+
+
+@pytest.mark.timeout(1200)
+def test_n04_n06_n07_pipeline_analysis(tmp_path):
+    r4 = _load("n04_model_analysis").main(["--root", str(tmp_path / "n04"), "--rows", "1200", "--steps", "30", "60"])
+    assert len(r4["series"]) == 2 and (r4["series"]["example_count"] > 0).all()
+    r6 = _load("n06_airflow_feature_analysis").main(["--root", str(tmp_path / "n06"), "--rows", "1200",
+                                                     "--steps", "30"])
+    assert float(r6["pipeline_transform"]["trip_start_hour_xf"].iloc[0]) == 12
+    assert int(r6["pipeline_transform"]["tips_xf"].iloc[0]) == 0  # 10 <= 0.2 * 100
+    r7 = _load("n07_airflow_model_analysis").main(["--root", str(tmp_path / "n07"), "--rows", "1200",
+                                                   "--steps", "30", "60"])
+    assert len(r7["models"]) == 2 and len(r7["by_hour"]) > 0 and os.path.exists(r7["png"])
+    assert np.isfinite(r7["comparison"].to_numpy(dtype=float, na_value=0)).all()
