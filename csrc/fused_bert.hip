@@ -54,6 +54,148 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// one global access of N contiguous elements (8 or 16 bytes) converted to / from fp32
+template <typename T, int N>
+struct alignas(sizeof(T) * N) Pack {
+  T v[N];
+};
+template <typename T, int N>
+__device__ __forceinline__ void ldv(const T* p, float* o) {
+  const Pack<T, N> pk = *(const Pack<T, N>*)p;
+#pragma unroll
+  for (int i = 0; i < N; ++i) o[i] = ld(&pk.v[i]);
+}
+template <typename T, int N>
+__device__ __forceinline__ void stv(T* p, const float* v) {
+  Pack<T, N> pk;
+#pragma unroll
+  for (int i = 0; i < N; ++i) st(&pk.v[i], v[i]);
+  *(Pack<T, N>*)p = pk;
+}
+
+// ---- vectorised LayerNorm (H % 256 == 0): lane owns NC chunks of 4 contiguous columns,
+// chunk j of lane l = columns [4 (64 j + l), +4) -> every access is one 8/16-byte load per lane
+template <typename T, int NC>
+__global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a, const T* __restrict__ r,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        int R, float eps, T* __restrict__ y,
+                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int H = NC * 256;
+  const int lane = threadIdx.x & 63;
+  const int wpb = kThreads / 64;
+  for (int row = blockIdx.x * wpb + (threadIdx.x >> 6); row < R; row += gridDim.x * wpb) {
+    const size_t base = (size_t)row * H;
+    float v[NC][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = 4 * (64 * j + lane);
+      float t[4];
+      ldv<T, 4>(a + base + c, v[j]);
+      ldv<T, 4>(r + base + c, t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[j][e] += t[e];
+        s += v[j][e];
+      }
+    }
+    const float mean = wave_sum(s) * (1.f / H);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[j][e] - mean;
+        q += d * d;
+      }
+    const float rstd = rsqrtf(wave_sum(q) * (1.f / H) + eps);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = 4 * (64 * j + lane);
+      const float4 wv = *(const float4*)(w + c), bv = *(const float4*)(b + c);
+      float o[4] = {(v[j][0] - mean) * rstd * wv.x + bv.x, (v[j][1] - mean) * rstd * wv.y + bv.y,
+                    (v[j][2] - mean) * rstd * wv.z + bv.z, (v[j][3] - mean) * rstd * wv.w + bv.w};
+      stv<T, 4>(y + base + c, o);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <typename T, int NC>
+__global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ dy, const T* __restrict__ a,
+                                                        const T* __restrict__ r, const float* __restrict__ w,
+                                                        const float* __restrict__ mean_in,
+                                                        const float* __restrict__ rstd_in, int R,
+                                                        T* __restrict__ dx, float* __restrict__ dw_part,
+                                                        float* __restrict__ db_part) {
+  constexpr int H = NC * 256;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wpb = kThreads / 64;
+  float dw[NC][4], db[NC][4], wreg[NC][4];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const float4 t = *(const float4*)(w + 4 * (64 * j + lane));
+    wreg[j][0] = t.x, wreg[j][1] = t.y, wreg[j][2] = t.z, wreg[j][3] = t.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dw[j][e] = db[j][e] = 0.f;
+  }
+  for (int row = blockIdx.x * wpb + wv; row < R; row += gridDim.x * wpb) {
+    const size_t base = (size_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NC][4], g[NC][4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = 4 * (64 * j + lane);
+      float d[4], av[4], rv[4];
+      ldv<T, 4>(dy + base + c, d);
+      ldv<T, 4>(a + base + c, av);
+      ldv<T, 4>(r + base + c, rv);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[j][e] = (av[e] + rv[e] - mean) * rstd;
+        g[j][e] = d[e] * wreg[j][e];
+        dw[j][e] += d[e] * xh[j][e];
+        db[j][e] += d[e];
+        sg += g[j][e];
+        sgx += g[j][e] * xh[j][e];
+      }
+    }
+    const float mg = wave_sum(sg) * (1.f / H), mgx = wave_sum(sgx) * (1.f / H);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - mg - xh[j][e] * mgx);
+      stv<T, 4>(dx + base + 4 * (64 * j + lane), o);
+    }
+  }
+  // combine the 4 waves' column partials: LDS image [wave][H] x2, then each thread sums its
+  // H/256 columns over the waves in a fixed order -> one partial row per block
+  __shared__ float sdw[kThreads / 64][H];
+  __shared__ float sdb[kThreads / 64][H];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = 4 * (64 * j + lane);
+    *(float4*)&sdw[wv][c] = make_float4(dw[j][0], dw[j][1], dw[j][2], dw[j][3]);
+    *(float4*)&sdb[wv][c] = make_float4(db[j][0], db[j][1], db[j][2], db[j][3]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += kThreads) {
+    float tw = 0.f, tb = 0.f;
+#pragma unroll
+    for (int i = 0; i < wpb; ++i) {
+      tw += sdw[i][c];
+      tb += sdb[i][c];
+    }
+    dw_part[(size_t)blockIdx.x * H + c] = tw;
+    db_part[(size_t)blockIdx.x * H + c] = tb;
+  }
+}
+
 template <typename T, int PER>
 __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, const T* __restrict__ r,
                                                       const float* __restrict__ w, const float* __restrict__ b, int R,
@@ -210,6 +352,73 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_bwd(const T* __restrict__ 
   db_part[(size_t)blockIdx.y * N + col] = acc;
 }
 
+// ---- vectorised bias+GELU (N % VW == 0, VW = 16 B / sizeof(T)): block = 64 column groups of VW
+// contiguous columns x 4 row slices; grid (ceil(N / (64 VW)), row chunks). 16-byte accesses per
+// lane; the backward combines its 4 slices' bias-grad partials in LDS (fixed order) and writes one
+// partial row per chunk.
+constexpr int kGCols = 64, kGSlices = kThreads / kGCols;
+
+template <typename T, int VW>
+__global__ __launch_bounds__(kThreads) void bias_gelu_fwd_v(const T* __restrict__ x, const float* __restrict__ bias,
+                                                           int M, int N, T* __restrict__ y) {
+  const int cg = threadIdx.x % kGCols, sl = threadIdx.x / kGCols;
+  const int col = (blockIdx.x * kGCols + cg) * VW;
+  if (col >= N) return;
+  const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
+  float bb[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) bb[e] = bias[col + e];
+  for (int r = r0 + sl; r < r1; r += kGSlices) {
+    const size_t i = (size_t)r * N + col;
+    float v[VW];
+    ldv<T, VW>(x + i, v);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) v[e] = gelu_f(v[e] + bb[e]);
+    stv<T, VW>(y + i, v);
+  }
+}
+
+template <typename T, int VW>
+__global__ __launch_bounds__(kThreads) void bias_gelu_bwd_v(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const float* __restrict__ bias, int M, int N,
+                                                           T* __restrict__ dx, float* __restrict__ db_part) {
+  __shared__ float sdb[kGSlices][kGCols * VW];
+  const int cg = threadIdx.x % kGCols, sl = threadIdx.x / kGCols;
+  const int col = (blockIdx.x * kGCols + cg) * VW;
+  const bool ok = col < N;
+  const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
+  float bb[VW], acc[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) {
+    bb[e] = ok ? bias[col + e] : 0.f;
+    acc[e] = 0.f;
+  }
+  if (ok) {
+    for (int r = r0 + sl; r < r1; r += kGSlices) {
+      const size_t i = (size_t)r * N + col;
+      float d[VW], v[VW];
+      ldv<T, VW>(dy + i, d);
+      ldv<T, VW>(x + i, v);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) d[e] *= gelu_grad(v[e] + bb[e]);
+      stv<T, VW>(dx + i, d);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) acc[e] += cvt_round<T>(d[e]);  // bias grad of the value actually stored
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VW; ++e) sdb[sl][cg * VW + e] = acc[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < kGCols * VW; c += kThreads) {
+    const int gc = blockIdx.x * kGCols * VW + c;
+    if (gc >= N) continue;
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kGSlices; ++i) t += sdb[i][c];
+    db_part[(size_t)blockIdx.y * N + gc] = t;
+  }
+}
+
 // sum `rows` partial rows of width N (fixed order) for up to two buffers in one launch
 // block = kRedCols columns x kRedSlices row slices (each slice strides the rows, 4 loads in
 // flight), slices combined in LDS in a fixed order -> deterministic, ~N/32 workgroups
@@ -267,10 +476,31 @@ int launch_add_ln(int fwd, const void* dy, const void* a, const void* r, const f
   return (int)hipGetLastError();
 }
 
+template <typename T, int NC>
+int launch_add_ln_v(int fwd, const void* dy, const void* a, const void* r, const float* w, const float* b, int R,
+                    float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
+                    hipStream_t st) {
+  if (fwd)
+    hipLaunchKernelGGL((add_ln_fwd_v<T, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r, w, b, R,
+                       eps, (T*)out, mean, rstd);
+  else
+    hipLaunchKernelGGL((add_ln_bwd_v<T, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
+                       (const T*)r, w, mean, rstd, R, (T*)out, dw_part, db_part);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int dispatch_add_ln(int fwd, const void* dy, const void* a, const void* r, const float* w, const float* b, int R,
                     int H, float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
                     hipStream_t st) {
+  const uintptr_t al = (uintptr_t)dy | (uintptr_t)a | (uintptr_t)r | (uintptr_t)w | (uintptr_t)b | (uintptr_t)out;
+  switch (H % 256 == 0 && al % 16 == 0 ? H / 256 : 0) {  // vectorised paths (BERT-base 768 -> NC 3, large 1024 -> 4)
+    case 1: return launch_add_ln_v<T, 1>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 2: return launch_add_ln_v<T, 2>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 3: return launch_add_ln_v<T, 3>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 4: return launch_add_ln_v<T, 4>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    default: break;
+  }
   const int per = (H + 63) / 64;
   if (per <= 4) return launch_add_ln<T, 4>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
   if (per <= 12) return launch_add_ln<T, 12>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
@@ -284,12 +514,12 @@ extern "C" {
 
 // partial-row count used by add_ln_bwd (fewer, fatter blocks: each wave walks many rows)
 int mifx_bert_ln_blocks(int R) {
-  const int need = (R + 3) / 4;
-  return need < 256 ? (need > 0 ? need : 1) : 256;
+  const int need = (R + 7) / 8;  // 2 rows per wave
+  return need < 1024 ? (need > 0 ? need : 1) : 1024;
 }
 
 // rows of partials for bias_gelu_bwd
-int mifx_bert_gelu_chunks(int M) { return M < 64 ? 1 : (M / 64 < 128 ? M / 64 : 128); }
+int mifx_bert_gelu_chunks(int M) { return M < 16 ? 1 : (M / 16 < 512 ? M / 16 : 512); }
 
 // dtype: 0 fp32, 1 bf16
 int mifx_bert_add_ln_fwd(int dtype, const void* a, const void* r, const float* w, const float* b, int R, int H,
@@ -323,6 +553,30 @@ int mifx_bert_bias_gelu(int dtype, int fwd, const void* dy, const void* x, const
                         float* db_part, float* db, hipStream_t st) {
   if (M <= 0 || N <= 0) return -1;
   const int chunks = fwd ? (M < 1024 ? M : 1024) : mifx_bert_gelu_chunks(M);
+  const int vw = dtype ? 8 : 4;
+  if (N % vw == 0 && ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)out) % 16 == 0) {
+    const dim3 vgrid((N / vw + kGCols - 1) / kGCols, chunks);
+    if (dtype) {
+      if (fwd)
+        hipLaunchKernelGGL((bias_gelu_fwd_v<__hip_bfloat16, 8>), vgrid, dim3(kThreads), 0, st,
+                           (const __hip_bfloat16*)x, bias, M, N, (__hip_bfloat16*)out);
+      else
+        hipLaunchKernelGGL((bias_gelu_bwd_v<__hip_bfloat16, 8>), vgrid, dim3(kThreads), 0, st,
+                           (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, bias, M, N, (__hip_bfloat16*)out,
+                           db_part);
+    } else {
+      if (fwd)
+        hipLaunchKernelGGL((bias_gelu_fwd_v<float, 4>), vgrid, dim3(kThreads), 0, st, (const float*)x, bias, M, N,
+                           (float*)out);
+      else
+        hipLaunchKernelGGL((bias_gelu_bwd_v<float, 4>), vgrid, dim3(kThreads), 0, st, (const float*)dy,
+                           (const float*)x, bias, M, N, (float*)out, db_part);
+    }
+    if (!fwd)
+      hipLaunchKernelGGL(col_reduce2, dim3((N + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, db_part, nullptr,
+                         chunks, N, db, nullptr);
+    return (int)hipGetLastError();
+  }
   const dim3 grid((N + kThreads - 1) / kThreads, chunks);
   if (dtype) {
     if (fwd)

@@ -70,7 +70,10 @@ def _func_to_component_spec(func, extra_code: str = "", base_image: str = _defau
         base_image = deco_image
     elif base_image is None:
         raise ValueError("base_image cannot be None")
-    sig = inspect.signature(func)
+    try:  # resolve string annotations (modules using `from __future__ import annotations`)
+        sig = inspect.signature(func, eval_str=True)
+    except Exception:  # noqa: BLE001 - unresolvable names keep their string form
+        sig = inspect.signature(func)
     types = OrderedDict()
     inputs, outputs, out_names, arguments = [], [], [], []
     for p in sig.parameters.values():

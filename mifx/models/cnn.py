@@ -119,15 +119,21 @@ class PateCNN(nn.Module):
 
 
 class FashionCNN(nn.Module):
+    """`Predict_Fashion_MNIST.ipynb` cell 8: Conv2D(8, 3x3, stride 2, relu) -> Dense(10, softmax).
+    `forward` returns class probabilities (what the served model answers); train on `logits`."""
+
     def __init__(self, num_classes: int = 10):
         super().__init__()
         self.conv = nn.Conv2d(1, 8, 3, stride=2)
         self.fc = nn.Linear(8 * 13 * 13, num_classes)
 
-    def forward(self, x):
+    def logits(self, x):
         if x.dim() == 3:
             x = x.unsqueeze(1)
         return self.fc(F.relu(self.conv(x)).flatten(1))
+
+    def forward(self, x):
+        return F.softmax(self.logits(x), dim=-1)
 
 
 class TpuMnistCNN(nn.Module):

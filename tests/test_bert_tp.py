@@ -81,7 +81,7 @@ def test_fused_add_layernorm_and_bias_gelu_gpu():
 
     torch.manual_seed(0)
     for dtype, tol in ((torch.float32, 1e-5), (torch.bfloat16, 2e-2)):
-        for H in (64, 768, 1000):
+        for H in (64, 256, 768, 1000, 1024):  # 256/768/1024: vectorised paths; 64/1000: scalar
             a = torch.randn(37, 5, H, device="cuda", dtype=dtype, requires_grad=True)
             r = torch.randn(37, 5, H, device="cuda", dtype=dtype, requires_grad=True)
             w = torch.randn(H, device="cuda", requires_grad=True)
@@ -97,17 +97,18 @@ def test_fused_add_layernorm_and_bias_gelu_gpu():
             torch.testing.assert_close(a.grad.float(), a32.grad, rtol=tol * 4, atol=tol * 4)
             torch.testing.assert_close(w.grad, w2.grad, rtol=tol * 4, atol=tol * 40)
             torch.testing.assert_close(b.grad, b2.grad, rtol=tol * 4, atol=tol * 40)
-        x = torch.randn(64, 3072, device="cuda", dtype=dtype, requires_grad=True)
-        bias = torch.randn(3072, device="cuda", requires_grad=True)
-        y = fb.bias_gelu(x, bias)
-        x2, b2 = x.detach().float().requires_grad_(), bias.detach().clone().requires_grad_()
-        ref = torch.nn.functional.gelu(x2 + b2)
-        torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
-        g = torch.randn_like(ref)
-        y.backward(g.to(dtype))
-        ref.backward(g)
-        torch.testing.assert_close(x.grad.float(), x2.grad, rtol=tol * 4, atol=tol * 4)
-        torch.testing.assert_close(bias.grad, b2.grad, rtol=tol * 4, atol=tol * 60)
+        for M, N in ((64, 3072), (1000, 3072), (70, 3070)):  # last: scalar fallback (N % 8 != 0)
+            x = torch.randn(M, N, device="cuda", dtype=dtype, requires_grad=True)
+            bias = torch.randn(N, device="cuda", requires_grad=True)
+            y = fb.bias_gelu(x, bias)
+            x2, b2 = x.detach().float().requires_grad_(), bias.detach().clone().requires_grad_()
+            ref = torch.nn.functional.gelu(x2 + b2)
+            torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+            g = torch.randn_like(ref)
+            y.backward(g.to(dtype))
+            ref.backward(g)
+            torch.testing.assert_close(x.grad.float(), x2.grad, rtol=tol * 4, atol=tol * 4)
+            torch.testing.assert_close(bias.grad, b2.grad, rtol=tol * 4, atol=tol * 60)
 
 
 @pytest.mark.gpu

@@ -51,3 +51,38 @@ def test_n04_n06_n07_pipeline_analysis(tmp_path):
                                                    "--steps", "30", "60"])
     assert len(r7["models"]) == 2 and len(r7["by_hour"]) > 0 and os.path.exists(r7["png"])
     assert np.isfinite(r7["comparison"].to_numpy(dtype=float, na_value=0)).all()
+
+
+def test_n08_simple_kfp_pipeline_local_run(tmp_path):
+    r = _load("n08_simple_kfp_pipeline").main(["--workdir", str(tmp_path)])
+    status = r["run"].run.status if hasattr(r["run"], "run") else r["run"]
+    assert status == "Succeeded"
+
+
+def test_n15_fashion_mnist_rest_serving(tmp_path):
+    r = _load("n15_fashion_mnist_serving").main(["--model_dir", str(tmp_path / "fm"), "--train_size", "2000",
+                                                 "--epochs", "2"])
+    assert np.allclose(np.sum(r["latest"], 1), 1.0, atol=1e-5)  # softmax head
+    assert np.allclose(r["latest"], r["pinned"])
+    assert r["accuracy"] > 0.8
+
+
+def test_n16_eager_matmul():
+    r = _load("n16_eager_execution").main(iters=5)
+    assert r["cpu_fp32_ms"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_n17_data_parallel_two_ranks_gloo(tmp_path):
+    import subprocess
+    import sys
+
+    w = tmp_path / "w.safetensors"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29581", os.path.join(NB, "n17_mnist_cnn_data_parallel.py"),
+           "--epochs", "1", "--steps_per_epoch", "3", "--train_size", "4096", "--batch_size", "256",
+           "--weights", str(w)]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=500, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "on 2 rank(s)" in p.stdout and w.exists()
