@@ -128,3 +128,43 @@ class TensorStore:
             op, *args = c
             getattr(self, op.lower())(*args)
         return "OK"
+
+    # ---- command interface (`rai.execute_command('AI.TENSORSET', ...)` in the notebook) ----------
+    def execute_command(self, cmd: str, *args):
+        """RedisAI command syntax: AI.TENSORSET key TYPE d1..dn [BLOB b | VALUES v..]; AI.TENSORGET key
+        [VALUES|BLOB|META]; AI.MODELSET key BACKEND DEVICE [INPUTS ..] [OUTPUTS ..] <model>;
+        AI.SCRIPTSET key DEVICE <source>; AI.SCRIPTRUN key fn INPUTS .. OUTPUTS ..;
+        AI.MODELRUN key INPUTS .. OUTPUTS ..; AI.TENSORDEL / AI.DAGRUN-free subset."""
+        c = cmd.upper()
+        a = [x.decode() if isinstance(x, bytes) and i < 1 else x for i, x in enumerate(args)]
+        if c == "AI.TENSORSET":
+            key, dtype, rest = a[0], str(a[1]), list(a[2:])
+            shape = []
+            while rest and not (isinstance(rest[0], str) and rest[0].upper() in ("BLOB", "VALUES")):
+                shape.append(int(rest.pop(0)))
+            if rest and rest[0].upper() == "BLOB":
+                return self.tensorset(key, dtype, shape, blob=rest[1])
+            if rest and rest[0].upper() == "VALUES":
+                return self.tensorset(key, dtype, shape, values=[float(v) for v in rest[1:]])
+            return self.tensorset(key, dtype, shape)
+        if c == "AI.TENSORGET":
+            return self.tensorget(a[0], str(a[1]) if len(a) > 1 else "VALUES")
+        if c == "AI.TENSORDEL":
+            return self.delete(a[0])
+        if c == "AI.MODELSET":
+            key, backend, device = a[0], str(a[1]), str(a[2])
+            model = a[-1]
+            if isinstance(model, str):
+                return self.modelset(key, backend, device, path=model)
+            return self.modelset(key, "TORCH", device, model=model)
+        if c == "AI.SCRIPTSET":
+            src = a[2].decode() if isinstance(a[2], bytes) else a[2]
+            return self.scriptset(a[0], str(a[1]), src)
+        if c in ("AI.SCRIPTRUN", "AI.MODELRUN"):
+            key = a[0]
+            rest = list(a[1:])
+            fn = rest.pop(0) if c == "AI.SCRIPTRUN" else None
+            i_in, i_out = rest.index("INPUTS"), rest.index("OUTPUTS")
+            ins, outs = rest[i_in + 1:i_out], rest[i_out + 1:]
+            return self.scriptrun(key, fn, ins, outs) if fn else self.modelrun(key, ins, outs)
+        raise ValueError(f"unsupported command {cmd}")

@@ -56,3 +56,22 @@ def test_render_indexed_job(tmp_path):
     assert "--nproc-per-node=8" in c["command"] and c["resources"]["limits"]["amd.com/gpu"] == "8"
     assert yaml.safe_load(yaml.safe_dump(job)) == job
     _ = sys
+
+
+@pytest.mark.timeout(600)
+def test_notebook10_distributed_training_job_runs_three_workers(tmp_path):
+    import os
+
+    from mifx.launch.job import JobSpec, launch_local
+
+    root = os.path.join(os.path.dirname(__file__), "..")
+    spec = JobSpec.from_yaml(os.path.join(root, "examples", "training-jobs", "distributed-training-job.yaml"))
+    assert spec.world_size == 3
+    spec.replicas[0].command = spec.replicas[0].command[:2] + ["--epochs", "1", "--steps_per_epoch", "2",
+                                                               "--train_size", "3060", "--batch_size", "306",
+                                                               "--weights", str(tmp_path / "w.safetensors")]
+    spec.replicas[0].env["CUDA_VISIBLE_DEVICES"] = ""
+    spec.replicas[0].env["OMP_NUM_THREADS"] = "2"
+    codes = launch_local(spec, num_gpus=0, timeout=500, cwd=root, log_dir=str(tmp_path))
+    assert set(codes.values()) == {0}, codes
+    assert (tmp_path / "w.safetensors").exists()

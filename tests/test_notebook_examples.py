@@ -86,3 +86,16 @@ def test_n17_data_parallel_two_ranks_gloo(tmp_path):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=500, env=env)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "on 2 rank(s)" in p.stdout and w.exists()
+
+
+def test_n18_tensorstore_command_chain():
+    lat = _load("n18_tensorstore_resnet").main(repeats=2)
+    assert set(lat) == {"cat", "dog", "guitar", "salvatore"}
+    assert all(0 <= v["index"] < 1000 for v in lat.values())
+
+
+def test_env_report():
+    from mifx.utils.env import report
+
+    r = report()
+    assert r["torch"] and any(f.startswith("libmifx_") for f in r["native_libs"])
