@@ -1,0 +1,367 @@
+// Fused BatchNorm(train) + ReLU for NHWC activations on gfx950 (ResNet-50 v2, BASELINE config 5).
+//
+// Profile that motivated it (profiles/resnet50_steady_kernels_r1.md, B=256 bf16 channels_last):
+// MIOpen BatchNorm fwd/bwd kernels + the separate ReLU clamp / threshold-backward kernels were
+// ~16.5 ms of the 37.4 ms step — more than all convolutions. Pre-activation ResNet applies ReLU
+// right after every BatchNorm, so both directions fuse:
+//
+//   forward : stats pass (per-channel sum / sum of squares)  -> finalize (mean, rstd, running
+//             stats, scale = w*rstd, shift = b - mean*scale)  -> apply y = relu(x*scale + shift)
+//   backward: reduce pass (g = dy * [x*scale + shift > 0];  sum g, sum g*xhat) -> finalize
+//             (dgamma, dbeta, per-channel coefficients) -> apply dx = k1 (g - k2 - xhat k3)
+//
+// 3 + 5 activation passes instead of MIOpen's 5 + 8 with the unfused ReLU. The activation is
+// viewed as [M = N*H*W, C] (channels_last memory): a thread owns 8 consecutive channels (one
+// 16-byte bf16 load), C/8 threads cover a row, 256/(C/8) rows are in flight per block. Partial
+// sums are per block (fp32, fixed order) and combined in fp64 in a fixed order by the finalize
+// kernels -> bitwise deterministic, no atomics. The ReLU mask is recomputed in backward with the
+// same fused multiply-add as forward, so it matches the forward output exactly.
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kVec = 8;  // channels per thread
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p) {
+  return (float)*p;
+}
+template <>
+__device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p) {
+  return __bfloat162float(*p);
+}
+template <typename T>
+__device__ __forceinline__ T cvt(float v) {
+  return (T)v;
+}
+template <>
+__device__ __forceinline__ __hip_bfloat16 cvt<__hip_bfloat16>(float v) {
+  return __float2bfloat16(v);
+}
+
+template <typename T>
+struct alignas(sizeof(T) * kVec) Pack {
+  T v[kVec];
+};
+template <typename T>
+__device__ __forceinline__ void ldv(const T* p, float* o) {
+  const Pack<T> pk = *(const Pack<T>*)p;
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) o[i] = ld(&pk.v[i]);
+}
+template <typename T>
+__device__ __forceinline__ void stv(T* p, const float* v) {
+  Pack<T> pk;
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) pk.v[i] = cvt<T>(v[i]);
+  *(Pack<T>*)p = pk;
+}
+__device__ __forceinline__ void ld8f(const float* p, float* o) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = b.x, o[5] = b.y, o[6] = b.z, o[7] = b.w;
+}
+
+// rows [r0, r1) of block b
+__device__ __forceinline__ void block_rows(long long M, int& r0, int& r1) {
+  r0 = (int)(M * blockIdx.x / gridDim.x);
+  r1 = (int)(M * (blockIdx.x + 1) / gridDim.x);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, long long M, int C,
+                                                    float* __restrict__ psum, float* __restrict__ psq) {
+  __shared__ float s1[kThreads * kVec];
+  __shared__ float s2[kThreads * kVec];
+  const int tpr = C / kVec, rpb = kThreads / tpr;
+  const int slice = threadIdx.x / tpr, cg = threadIdx.x % tpr;
+  int r0, r1;
+  block_rows(M, r0, r1);
+  float a[kVec] = {}, q[kVec] = {};
+  if (slice < rpb) {
+    const T* p = x + (size_t)cg * kVec;
+    int r = r0 + slice;
+    for (; r + rpb < r1; r += 2 * rpb) {  // two rows in flight per thread
+      float u[kVec], w[kVec];
+      ldv(p + (size_t)r * C, u);
+      ldv(p + (size_t)(r + rpb) * C, w);
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        a[e] += u[e] + w[e];
+        q[e] += u[e] * u[e] + w[e] * w[e];
+      }
+    }
+    for (; r < r1; r += rpb) {
+      float u[kVec];
+      ldv(p + (size_t)r * C, u);
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        a[e] += u[e];
+        q[e] += u[e] * u[e];
+      }
+    }
+  }
+  // LDS image [slice][C] (slice < rpb); every thread of the block owns kVec entries
+#pragma unroll
+  for (int e = 0; e < kVec; ++e) {
+    s1[threadIdx.x * kVec + e] = a[e];
+    s2[threadIdx.x * kVec + e] = q[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float t1 = 0.f, t2 = 0.f;
+    const int g = c / kVec, e = c % kVec;
+    for (int s = 0; s < rpb; ++s) {
+      t1 += s1[(s * tpr + g) * kVec + e];
+      t2 += s2[(s * tpr + g) * kVec + e];
+    }
+    psum[(size_t)blockIdx.x * C + c] = t1;
+    psq[(size_t)blockIdx.x * C + c] = t2;
+  }
+}
+
+// one thread per channel: fp64 combine of the partials in block order
+__global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restrict__ psum,
+                                                           const float* __restrict__ psq, int nb, long long M, int C,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           float eps, float momentum, float* __restrict__ run_mean,
+                                                           float* __restrict__ run_var, float* __restrict__ mean_out,
+                                                           float* __restrict__ rstd_out, float* __restrict__ scale,
+                                                           float* __restrict__ shift) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < nb; ++i) {
+    s += psum[(size_t)i * C + c];
+    q += psq[(size_t)i * C + c];
+  }
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rstd;
+  const float sc = w[c] * rstd;
+  scale[c] = sc;
+  shift[c] = b[c] - (float)mean * sc;
+  if (run_mean != nullptr) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+  }
+}
+
+// y = relu(x * scale + shift) (relu optional), vectors of 8 channels, grid-stride
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, long long nvec, int C,
+                                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                                    int relu, T* __restrict__ y) {
+  const int tpr = C / kVec;
+  for (long long v = (long long)blockIdx.x * kThreads + threadIdx.x; v < nvec; v += (long long)gridDim.x * kThreads) {
+    const int c0 = (int)(v % tpr) * kVec;
+    float u[kVec], sc[kVec], sh[kVec];
+    ldv(x + v * kVec, u);
+    ld8f(scale + c0, sc);
+    ld8f(shift + c0, sh);
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) {
+      const float t = fmaf(u[e], sc[e], sh[e]);
+      u[e] = relu ? fmaxf(t, 0.f) : t;
+    }
+    stv(y + v * kVec, u);
+  }
+}
+
+// backward reduction: g = dy * mask; sums of g and g * xhat per channel
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce(const T* __restrict__ dy, const T* __restrict__ x, long long M,
+                                                         int C, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, int relu,
+                                                         float* __restrict__ pg, float* __restrict__ pgx) {
+  __shared__ float s1[kThreads * kVec];
+  __shared__ float s2[kThreads * kVec];
+  const int tpr = C / kVec, rpb = kThreads / tpr;
+  const int slice = threadIdx.x / tpr, cg = threadIdx.x % tpr;
+  int r0, r1;
+  block_rows(M, r0, r1);
+  float a[kVec] = {}, q[kVec] = {};
+  if (slice < rpb) {
+    const int c0 = cg * kVec;
+    float sc[kVec], sh[kVec], mu[kVec], rs[kVec];
+    ld8f(scale + c0, sc);
+    ld8f(shift + c0, sh);
+    ld8f(mean + c0, mu);
+    ld8f(rstd + c0, rs);
+    for (int r = r0 + slice; r < r1; r += rpb) {
+      float d[kVec], u[kVec];
+      ldv(dy + (size_t)r * C + c0, d);
+      ldv(x + (size_t)r * C + c0, u);
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        const float g = (relu && fmaf(u[e], sc[e], sh[e]) <= 0.f) ? 0.f : d[e];
+        a[e] += g;
+        q[e] += g * ((u[e] - mu[e]) * rs[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < kVec; ++e) {
+    s1[threadIdx.x * kVec + e] = a[e];
+    s2[threadIdx.x * kVec + e] = q[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float t1 = 0.f, t2 = 0.f;
+    const int g = c / kVec, e = c % kVec;
+    for (int s = 0; s < rpb; ++s) {
+      t1 += s1[(s * tpr + g) * kVec + e];
+      t2 += s2[(s * tpr + g) * kVec + e];
+    }
+    pg[(size_t)blockIdx.x * C + c] = t1;
+    pgx[(size_t)blockIdx.x * C + c] = t2;
+  }
+}
+
+// dbeta = sum g, dgamma = sum g xhat; dx coefficients k1 = w rstd, k2 = dbeta / M, k3 = dgamma / M
+__global__ __launch_bounds__(kThreads) void bn_finalize_bwd(const float* __restrict__ pg, const float* __restrict__ pgx,
+                                                           int nb, long long M, int C, const float* __restrict__ w,
+                                                           const float* __restrict__ rstd,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float* __restrict__ k) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < nb; ++i) {
+    s += pg[(size_t)i * C + c];
+    q += pgx[(size_t)i * C + c];
+  }
+  dbeta[c] = (float)s;
+  dgamma[c] = (float)q;
+  k[c] = w[c] * rstd[c];
+  k[C + c] = (float)(s / (double)M);
+  k[2 * C + c] = (float)(q / (double)M);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
+                                                        long long nvec, int C, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, const float* __restrict__ k,
+                                                        int relu, T* __restrict__ dx) {
+  const int tpr = C / kVec;
+  for (long long v = (long long)blockIdx.x * kThreads + threadIdx.x; v < nvec; v += (long long)gridDim.x * kThreads) {
+    const int c0 = (int)(v % tpr) * kVec;
+    float d[kVec], u[kVec], sc[kVec], sh[kVec], mu[kVec], rs[kVec], k1[kVec], k2[kVec], k3[kVec];
+    ldv(dy + v * kVec, d);
+    ldv(x + v * kVec, u);
+    ld8f(scale + c0, sc);
+    ld8f(shift + c0, sh);
+    ld8f(mean + c0, mu);
+    ld8f(rstd + c0, rs);
+    ld8f(k + c0, k1);
+    ld8f(k + C + c0, k2);
+    ld8f(k + 2 * C + c0, k3);
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) {
+      const float g = (relu && fmaf(u[e], sc[e], sh[e]) <= 0.f) ? 0.f : d[e];
+      d[e] = k1[e] * (g - k2[e] - (u[e] - mu[e]) * rs[e] * k3[e]);
+    }
+    stv(dx + v * kVec, d);
+  }
+}
+
+int blocks_for(long long M, int C) {
+  const int rpb = kThreads / (C / kVec);
+  long long nb = (M + (long long)rpb * 16 - 1) / ((long long)rpb * 16);  // >= 16 rows per thread
+  if (nb > 1024) nb = 1024;
+  return nb < 1 ? 1 : (int)nb;
+}
+
+int apply_grid(long long nvec) {
+  long long g = (nvec + kThreads - 1) / kThreads;
+  if (g > 8192) g = 8192;
+  return g < 1 ? 1 : (int)g;
+}
+
+bool shape_ok(long long M, int C) { return M > 0 && C >= kVec && C % kVec == 0 && C / kVec <= kThreads; }
+
+}  // namespace
+
+extern "C" {
+
+// scratch rows (blocks) used by the reductions for [M, C]
+int mifx_bn_blocks(long long M, int C) { return shape_ok(M, C) ? blocks_for(M, C) : -1; }
+
+// dtype 1 = bf16, 0 = fp32. stats6 = [mean, rstd, scale, shift] (4*C floats) out;
+// part = scratch [2, blocks, C]; run_mean / run_var may be null (no running-stat update).
+int mifx_bn_relu_fwd(int dtype, const void* x, long long M, int C, const float* w, const float* b, float eps,
+                     float momentum, float* run_mean, float* run_var, int relu, float* part, float* stats, void* y,
+                     hipStream_t st) {
+  if (!shape_ok(M, C)) return -1;
+  const int nb = blocks_for(M, C);
+  if (dtype)
+    hipLaunchKernelGGL(bn_stats<__hip_bfloat16>, dim3(nb), dim3(kThreads), 0, st, (const __hip_bfloat16*)x, M, C, part,
+                       part + (size_t)nb * C);
+  else
+    hipLaunchKernelGGL(bn_stats<float>, dim3(nb), dim3(kThreads), 0, st, (const float*)x, M, C, part,
+                       part + (size_t)nb * C);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, st, part,
+                     part + (size_t)nb * C, nb, M, C, w, b, eps, momentum, run_mean, run_var, stats, stats + C,
+                     stats + 2 * C, stats + 3 * C);
+  const long long nvec = M * C / kVec;
+  if (dtype)
+    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)x, nvec, C, stats + 2 * C, stats + 3 * C, relu, (__hip_bfloat16*)y);
+  else
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st, (const float*)x, nvec, C,
+                       stats + 2 * C, stats + 3 * C, relu, (float*)y);
+  return (int)hipGetLastError();
+}
+
+// eval / inference: y = relu(x * scale + shift) with precomputed per-channel scale / shift
+int mifx_bn_relu_apply(int dtype, const void* x, long long M, int C, const float* scale, const float* shift, int relu,
+                       void* y, hipStream_t st) {
+  if (!shape_ok(M, C)) return -1;
+  const long long nvec = M * C / kVec;
+  if (dtype)
+    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)x, nvec, C, scale, shift, relu, (__hip_bfloat16*)y);
+  else
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st, (const float*)x, nvec, C, scale,
+                       shift, relu, (float*)y);
+  return (int)hipGetLastError();
+}
+
+// backward: stats = forward's [mean, rstd, scale, shift]; part = scratch [2, blocks, C];
+// kbuf = scratch [3, C]; outputs dx, dgamma, dbeta
+int mifx_bn_relu_bwd(int dtype, const void* dy, const void* x, long long M, int C, const float* w,
+                     const float* stats, int relu, float* part, float* kbuf, void* dx, float* dgamma, float* dbeta,
+                     hipStream_t st) {
+  if (!shape_ok(M, C)) return -1;
+  const int nb = blocks_for(M, C);
+  const float *mean = stats, *rstd = stats + C, *scale = stats + 2 * C, *shift = stats + 3 * C;
+  if (dtype)
+    hipLaunchKernelGGL(bn_bwd_reduce<__hip_bfloat16>, dim3(nb), dim3(kThreads), 0, st, (const __hip_bfloat16*)dy,
+                       (const __hip_bfloat16*)x, M, C, scale, shift, mean, rstd, relu, part, part + (size_t)nb * C);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce<float>, dim3(nb), dim3(kThreads), 0, st, (const float*)dy, (const float*)x, M, C,
+                       scale, shift, mean, rstd, relu, part, part + (size_t)nb * C);
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, st, part,
+                     part + (size_t)nb * C, nb, M, C, w, rstd, dgamma, dbeta, kbuf);
+  const long long nvec = M * C / kVec;
+  if (dtype)
+    hipLaunchKernelGGL(bn_bwd_apply<__hip_bfloat16>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, nvec, C, scale, shift, mean, rstd, kbuf,
+                       relu, (__hip_bfloat16*)dx);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st, (const float*)dy,
+                       (const float*)x, nvec, C, scale, shift, mean, rstd, kbuf, relu, (float*)dx);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -7,6 +7,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.bn_relu import BatchNormReLU2d
+
 
 class PreActBottleneck(nn.Module):
     expansion = 4
@@ -14,20 +16,20 @@ class PreActBottleneck(nn.Module):
     def __init__(self, cin: int, width: int, stride: int):
         super().__init__()
         cout = width * self.expansion
-        self.bn0 = nn.BatchNorm2d(cin)
+        self.bn0 = BatchNormReLU2d(cin)  # every BN of the pre-activation net feeds a ReLU: fused
         self.shortcut = nn.Conv2d(cin, cout, 1, stride=stride, bias=False) if (stride != 1 or cin != cout) else None
         self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNormReLU2d(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BatchNormReLU2d(width)
         self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
 
     def forward(self, x):
-        pre = F.relu(self.bn0(x))
+        pre = self.bn0(x)
         sc = self.shortcut(pre) if self.shortcut is not None else x
         y = self.conv1(pre)
-        y = self.conv2(F.relu(self.bn1(y)))
-        y = self.conv3(F.relu(self.bn2(y)))
+        y = self.conv2(self.bn1(y))
+        y = self.conv3(self.bn2(y))
         return y + sc
 
 
@@ -42,13 +44,13 @@ class ResNetV2(nn.Module):
                 blocks.append(PreActBottleneck(cin, w, stride))
                 cin = w * 4
         self.blocks = nn.Sequential(*blocks)
-        self.post_bn = nn.BatchNorm2d(cin)
+        self.post_bn = BatchNormReLU2d(cin)
         self.fc = nn.Linear(cin, num_classes)
 
     def forward(self, x):  # x: [B, 3, H, W] in [0, 1] (NHWC memory format preferred)
         y = F.max_pool2d(self.stem(x), 3, 2, 1)
         y = self.blocks(y)
-        y = F.relu(self.post_bn(y))
+        y = self.post_bn(y)
         return self.fc(y.mean((2, 3)))
 
 

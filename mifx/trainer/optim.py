@@ -66,3 +66,45 @@ def make_optimizer(kind: str, params, lr: float, **kw) -> torch.optim.Optimizer:
     if kind == "sgd":
         return torch.optim.SGD(params, lr=lr, **kw)
     raise ValueError(f"unknown optimizer {kind}")
+
+
+class FlatAdamW:
+    """AdamW over a model whose parameters are re-homed as bf16 views of ONE flat buffer, with their
+    gradients as views of one flat bf16 gradient buffer (autograd accumulates in place), and fp32
+    master weights / moments kept here. `step()` is a single fused HIP launch (mifx.ops.adamw);
+    `zero_grad()` is one memset. Both are hipGraph-capturable (device-side step counter)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 dtype: torch.dtype = torch.bfloat16):
+        self.params = [p for p in params if p.requires_grad]
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.n = n
+        self.flat = torch.empty(n, device=dev, dtype=dtype)
+        self.flat_grad = torch.zeros(n, device=dev, dtype=dtype)
+        self.master = torch.empty(n, device=dev, dtype=torch.float32)
+        self.m = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.v = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.step_count = torch.zeros((), device=dev, dtype=torch.int32)
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.master[off:off + k].copy_(p.detach().reshape(-1).float())
+                self.flat[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + k].view(p.shape)
+                p.grad = self.flat_grad[off:off + k].view(p.shape)
+                off += k
+
+    def zero_grad(self, set_to_none: bool = False) -> None:  # grads stay views of the flat buffer
+        self.flat_grad.zero_()
+
+    def step(self) -> None:
+        from ..ops.adamw import adamw_flat_
+
+        adamw_flat_(self.flat, self.flat_grad, self.master, self.m, self.v, self.step_count, self.lr,
+                    self.betas[0], self.betas[1], self.eps, self.wd)
+
+    def state_dict(self) -> dict:
+        return {"master": self.master, "m": self.m, "v": self.v, "step": self.step_count}

@@ -1,0 +1,69 @@
+"""Fused BatchNorm+ReLU (csrc/bn_relu.hip) vs the PyTorch fp32 reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mifx.ops.bn_relu import BatchNormReLU2d, bn_relu
+
+
+def test_cpu_reference_path_matches_batchnorm_relu():
+    torch.manual_seed(0)
+    m = BatchNormReLU2d(16)
+    ref = torch.nn.BatchNorm2d(16)
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(4, 16, 5, 5)
+    torch.testing.assert_close(m(x), F.relu(ref(x)))
+    torch.testing.assert_close(m.running_var, ref.running_var)
+    m.eval(), ref.eval()
+    torch.testing.assert_close(m(x), F.relu(ref(x)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 14), (8, 256, 7, 7), (2, 2048, 3, 3), (3, 24, 5, 7)])
+def test_fused_bn_relu_matches_fp32_reference(dtype, tol, shape):
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    x = (torch.randn(shape, device="cuda") * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.rand(C, device="cuda") + 0.5).requires_grad_()
+    b = (torch.randn(C, device="cuda") * 0.2).requires_grad_()
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    xg = x.detach().requires_grad_()
+    y = bn_relu(xg, w, b, rm, rv, True, 0.1, 1e-5)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.dtype == dtype
+    x32 = x.detach().float().requires_grad_()
+    w2, b2 = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    rm2, rv2 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    ref = F.relu(F.batch_norm(x32, rm2, rv2, w2, b2, True, 0.1, 1e-5))
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(rm, rm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv, rv2, rtol=1e-4, atol=1e-5)
+    g = torch.randn_like(ref)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    ref.backward(g)
+    torch.testing.assert_close(xg.grad.float(), x32.grad, rtol=tol * 3, atol=tol * 3)
+    m = N * H * W
+    torch.testing.assert_close(w.grad, w2.grad, rtol=tol * 3, atol=tol * 3 * m ** 0.5)
+    torch.testing.assert_close(b.grad, b2.grad, rtol=tol * 3, atol=tol * 3 * m ** 0.5)
+    # eval path (running statistics)
+    ye = bn_relu(x, w.detach(), b.detach(), rm, rv, False, 0.1, 1e-5)
+    re = F.relu(F.batch_norm(x.float(), rm, rv, w.detach(), b.detach(), False, 0.1, 1e-5))
+    torch.testing.assert_close(ye.float(), re, rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+def test_fused_bn_relu_is_deterministic():
+    torch.manual_seed(1)
+    x = torch.randn(16, 128, 28, 28, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.ones(128, device="cuda", requires_grad=True)
+    b = torch.zeros(128, device="cuda", requires_grad=True)
+    outs = []
+    for _ in range(2):
+        xg = x.detach().requires_grad_()
+        y = bn_relu(xg, w, b, None, None, True)
+        y.sum().backward()
+        outs.append((y.detach().clone(), xg.grad.clone(), w.grad.clone()))
+        w.grad = None
+        b.grad = None
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
