@@ -70,8 +70,27 @@ __device__ __forceinline__ void block_rows(long long M, int& r0, int& r1) {
   r1 = (int)(M * (blockIdx.x + 1) / gridDim.x);
 }
 
+// x2 != null: the activation is the residual sum s = x + x2, rounded to T, written to s_out and
+// reduced as stored (so the apply pass, which reads s_out, normalises exactly what was measured)
 template <typename T>
-__global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, long long M, int C,
+__device__ __forceinline__ void load_sum(const T* x, const T* x2, T* s_out, size_t off, float* u) {
+  ldv(x + off, u);
+  if (x2 != nullptr) {
+    float v[kVec];
+    ldv(x2 + off, v);
+    Pack<T> pk;
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) {
+      pk.v[e] = cvt<T>(u[e] + v[e]);
+      u[e] = ld(&pk.v[e]);
+    }
+    *(Pack<T>*)(s_out + off) = pk;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, const T* __restrict__ x2,
+                                                    T* __restrict__ s_out, long long M, int C,
                                                     float* __restrict__ psum, float* __restrict__ psq) {
   __shared__ float s1[kThreads * kVec];
   __shared__ float s2[kThreads * kVec];
@@ -81,12 +100,12 @@ __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, lo
   block_rows(M, r0, r1);
   float a[kVec] = {}, q[kVec] = {};
   if (slice < rpb) {
-    const T* p = x + (size_t)cg * kVec;
+    const size_t c0 = (size_t)cg * kVec;
     int r = r0 + slice;
     for (; r + rpb < r1; r += 2 * rpb) {  // two rows in flight per thread
       float u[kVec], w[kVec];
-      ldv(p + (size_t)r * C, u);
-      ldv(p + (size_t)(r + rpb) * C, w);
+      load_sum(x, x2, s_out, (size_t)r * C + c0, u);
+      load_sum(x, x2, s_out, (size_t)(r + rpb) * C + c0, w);
 #pragma unroll
       for (int e = 0; e < kVec; ++e) {
         a[e] += u[e] + w[e];
@@ -95,7 +114,7 @@ __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, lo
     }
     for (; r < r1; r += rpb) {
       float u[kVec];
-      ldv(p + (size_t)r * C, u);
+      load_sum(x, x2, s_out, (size_t)r * C + c0, u);
 #pragma unroll
       for (int e = 0; e < kVec; ++e) {
         a[e] += u[e];
@@ -122,7 +141,36 @@ __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, lo
   }
 }
 
-// one thread per channel: fp64 combine of the partials in block order
+// Partial-sum combine: block = 32 channels x 8 slices; slice s sums partial rows s, s+8, ... in
+// fp64, then the 8 slices are added in slice order (fixed order -> deterministic). grid = C / 32.
+constexpr int kFinCols = 32, kFinSlices = kThreads / kFinCols;
+
+__device__ __forceinline__ void combine2(const float* __restrict__ p0, const float* __restrict__ p1, int nb, int C,
+                                         int c, int sl, double& s0, double& s1) {
+  __shared__ double l0[kFinSlices][kFinCols];
+  __shared__ double l1[kFinSlices][kFinCols];
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    int i = sl;
+    for (; i + kFinSlices < nb; i += 2 * kFinSlices) {
+      a += (double)p0[(size_t)i * C + c] + (double)p0[(size_t)(i + kFinSlices) * C + c];
+      b += (double)p1[(size_t)i * C + c] + (double)p1[(size_t)(i + kFinSlices) * C + c];
+    }
+    for (; i < nb; i += kFinSlices) {
+      a += p0[(size_t)i * C + c];
+      b += p1[(size_t)i * C + c];
+    }
+  }
+  l0[sl][threadIdx.x % kFinCols] = a;
+  l1[sl][threadIdx.x % kFinCols] = b;
+  __syncthreads();
+  s0 = s1 = 0.0;
+  for (int k = 0; k < kFinSlices; ++k) {
+    s0 += l0[k][threadIdx.x % kFinCols];
+    s1 += l1[k][threadIdx.x % kFinCols];
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restrict__ psum,
                                                            const float* __restrict__ psq, int nb, long long M, int C,
                                                            const float* __restrict__ w, const float* __restrict__ b,
@@ -130,13 +178,10 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restr
                                                            float* __restrict__ run_var, float* __restrict__ mean_out,
                                                            float* __restrict__ rstd_out, float* __restrict__ scale,
                                                            float* __restrict__ shift) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int i = 0; i < nb; ++i) {
-    s += psum[(size_t)i * C + c];
-    q += psq[(size_t)i * C + c];
-  }
+  const int sl = threadIdx.x / kFinCols, c = blockIdx.x * kFinCols + threadIdx.x % kFinCols;
+  double s, q;
+  combine2(psum, psq, nb, C, c, sl, s, q);
+  if (sl != 0 || c >= C) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   var = var > 0.0 ? var : 0.0;
@@ -153,24 +198,30 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restr
   }
 }
 
-// y = relu(x * scale + shift) (relu optional), vectors of 8 channels, grid-stride
+// y = relu(x * scale + shift) (relu optional). Same [row slice x channel group] layout as the
+// reductions: a thread keeps its 8 channels' scale/shift in registers across all its rows.
 template <typename T>
-__global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, long long nvec, int C,
+__global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, long long M, int C,
                                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                                     int relu, T* __restrict__ y) {
-  const int tpr = C / kVec;
-  for (long long v = (long long)blockIdx.x * kThreads + threadIdx.x; v < nvec; v += (long long)gridDim.x * kThreads) {
-    const int c0 = (int)(v % tpr) * kVec;
-    float u[kVec], sc[kVec], sh[kVec];
-    ldv(x + v * kVec, u);
-    ld8f(scale + c0, sc);
-    ld8f(shift + c0, sh);
+  const int tpr = C / kVec, rpb = kThreads / tpr;
+  const int slice = threadIdx.x / tpr, cg = threadIdx.x % tpr;
+  if (slice >= rpb) return;
+  int r0, r1;
+  block_rows(M, r0, r1);
+  const int c0 = cg * kVec;
+  float sc[kVec], sh[kVec];
+  ld8f(scale + c0, sc);
+  ld8f(shift + c0, sh);
+  for (int r = r0 + slice; r < r1; r += rpb) {
+    float u[kVec];
+    ldv(x + (size_t)r * C + c0, u);
 #pragma unroll
     for (int e = 0; e < kVec; ++e) {
       const float t = fmaf(u[e], sc[e], sh[e]);
       u[e] = relu ? fmaxf(t, 0.f) : t;
     }
-    stv(y + v * kVec, u);
+    stv(y + (size_t)r * C + c0, u);
   }
 }
 
@@ -226,65 +277,74 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce(const T* __restrict__ 
   }
 }
 
-// dbeta = sum g, dgamma = sum g xhat; dx coefficients k1 = w rstd, k2 = dbeta / M, k3 = dgamma / M
+// dbeta = sum g, dgamma = sum g xhat. dx = w rstd (g - dbeta/M - xhat dgamma/M) is folded into
+// dx = A g + B x + Cc per channel (A = w rstd, B = -A rstd dgamma/M, Cc = -A dbeta/M - B mean).
 __global__ __launch_bounds__(kThreads) void bn_finalize_bwd(const float* __restrict__ pg, const float* __restrict__ pgx,
                                                            int nb, long long M, int C, const float* __restrict__ w,
+                                                           const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                            float* __restrict__ k) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int i = 0; i < nb; ++i) {
-    s += pg[(size_t)i * C + c];
-    q += pgx[(size_t)i * C + c];
-  }
+  const int sl = threadIdx.x / kFinCols, c = blockIdx.x * kFinCols + threadIdx.x % kFinCols;
+  double s, q;
+  combine2(pg, pgx, nb, C, c, sl, s, q);
+  if (sl != 0 || c >= C) return;
   dbeta[c] = (float)s;
   dgamma[c] = (float)q;
-  k[c] = w[c] * rstd[c];
-  k[C + c] = (float)(s / (double)M);
-  k[2 * C + c] = (float)(q / (double)M);
+  const double A = (double)w[c] * rstd[c];
+  const double B = -A * rstd[c] * (q / (double)M);
+  k[c] = (float)A;
+  k[C + c] = (float)B;
+  k[2 * C + c] = (float)(-A * (s / (double)M) - B * mean[c]);
 }
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
-                                                        long long nvec, int C, const float* __restrict__ scale,
-                                                        const float* __restrict__ shift,
-                                                        const float* __restrict__ mean,
-                                                        const float* __restrict__ rstd, const float* __restrict__ k,
-                                                        int relu, T* __restrict__ dx) {
-  const int tpr = C / kVec;
-  for (long long v = (long long)blockIdx.x * kThreads + threadIdx.x; v < nvec; v += (long long)gridDim.x * kThreads) {
-    const int c0 = (int)(v % tpr) * kVec;
-    float d[kVec], u[kVec], sc[kVec], sh[kVec], mu[kVec], rs[kVec], k1[kVec], k2[kVec], k3[kVec];
-    ldv(dy + v * kVec, d);
-    ldv(x + v * kVec, u);
-    ld8f(scale + c0, sc);
-    ld8f(shift + c0, sh);
-    ld8f(mean + c0, mu);
-    ld8f(rstd + c0, rs);
-    ld8f(k + c0, k1);
-    ld8f(k + C + c0, k2);
-    ld8f(k + 2 * C + c0, k3);
+                                                        long long M, int C, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, const float* __restrict__ k,
+                                                        int relu, const T* __restrict__ dres, T* __restrict__ dx) {
+  const int tpr = C / kVec, rpb = kThreads / tpr;
+  const int slice = threadIdx.x / tpr, cg = threadIdx.x % tpr;
+  if (slice >= rpb) return;
+  int r0, r1;
+  block_rows(M, r0, r1);
+  const int c0 = cg * kVec;
+  float sc[kVec], sh[kVec], A[kVec], B[kVec], Cc[kVec];
+  ld8f(scale + c0, sc);
+  ld8f(shift + c0, sh);
+  ld8f(k + c0, A);
+  ld8f(k + C + c0, B);
+  ld8f(k + 2 * C + c0, Cc);
+  for (int r = r0 + slice; r < r1; r += rpb) {
+    float d[kVec], u[kVec];
+    ldv(dy + (size_t)r * C + c0, d);
+    ldv(x + (size_t)r * C + c0, u);
 #pragma unroll
     for (int e = 0; e < kVec; ++e) {
       const float g = (relu && fmaf(u[e], sc[e], sh[e]) <= 0.f) ? 0.f : d[e];
-      d[e] = k1[e] * (g - k2[e] - (u[e] - mu[e]) * rs[e] * k3[e]);
+      d[e] = fmaf(A[e], g, fmaf(B[e], u[e], Cc[e]));
     }
-    stv(dx + v * kVec, d);
+    if (dres != nullptr) {  // gradient arriving through the identity shortcut, accumulated here
+      float rr[kVec];
+      ldv(dres + (size_t)r * C + c0, rr);
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) d[e] += rr[e];
+    }
+    stv(dx + (size_t)r * C + c0, d);
   }
 }
 
 int blocks_for(long long M, int C) {
   const int rpb = kThreads / (C / kVec);
   long long nb = (M + (long long)rpb * 16 - 1) / ((long long)rpb * 16);  // >= 16 rows per thread
-  if (nb > 1024) nb = 1024;
+  if (nb > 512) nb = 512;
   return nb < 1 ? 1 : (int)nb;
 }
 
-int apply_grid(long long nvec) {
-  long long g = (nvec + kThreads - 1) / kThreads;
-  if (g > 8192) g = 8192;
+int apply_blocks(long long M, int C) {  // ~8 rows per thread, params loaded once per thread
+  const int rpb = kThreads / (C / kVec);
+  long long g = (M + (long long)rpb * 8 - 1) / ((long long)rpb * 8);
+  if (g > 16384) g = 16384;
   return g < 1 ? 1 : (int)g;
 }
 
@@ -299,26 +359,27 @@ int mifx_bn_blocks(long long M, int C) { return shape_ok(M, C) ? blocks_for(M, C
 
 // dtype 1 = bf16, 0 = fp32. stats6 = [mean, rstd, scale, shift] (4*C floats) out;
 // part = scratch [2, blocks, C]; run_mean / run_var may be null (no running-stat update).
-int mifx_bn_relu_fwd(int dtype, const void* x, long long M, int C, const float* w, const float* b, float eps,
-                     float momentum, float* run_mean, float* run_var, int relu, float* part, float* stats, void* y,
-                     hipStream_t st) {
+// x2 / sum_out non-null: normalise s = x + x2 (written to sum_out) -- residual add fused in
+int mifx_bn_relu_fwd(int dtype, const void* x, const void* x2, void* sum_out, long long M, int C, const float* w,
+                     const float* b, float eps, float momentum, float* run_mean, float* run_var, int relu, float* part,
+                     float* stats, void* y, hipStream_t st) {
   if (!shape_ok(M, C)) return -1;
   const int nb = blocks_for(M, C);
   if (dtype)
-    hipLaunchKernelGGL(bn_stats<__hip_bfloat16>, dim3(nb), dim3(kThreads), 0, st, (const __hip_bfloat16*)x, M, C, part,
-                       part + (size_t)nb * C);
+    hipLaunchKernelGGL(bn_stats<__hip_bfloat16>, dim3(nb), dim3(kThreads), 0, st, (const __hip_bfloat16*)x,
+                       (const __hip_bfloat16*)x2, (__hip_bfloat16*)sum_out, M, C, part, part + (size_t)nb * C);
   else
-    hipLaunchKernelGGL(bn_stats<float>, dim3(nb), dim3(kThreads), 0, st, (const float*)x, M, C, part,
-                       part + (size_t)nb * C);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, st, part,
+    hipLaunchKernelGGL(bn_stats<float>, dim3(nb), dim3(kThreads), 0, st, (const float*)x, (const float*)x2,
+                       (float*)sum_out, M, C, part, part + (size_t)nb * C);
+  const void* xa = x2 != nullptr ? (const void*)sum_out : x;  // apply normalises the stored sum
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kFinCols - 1) / kFinCols), dim3(kThreads), 0, st, part,
                      part + (size_t)nb * C, nb, M, C, w, b, eps, momentum, run_mean, run_var, stats, stats + C,
                      stats + 2 * C, stats + 3 * C);
-  const long long nvec = M * C / kVec;
   if (dtype)
-    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
-                       (const __hip_bfloat16*)x, nvec, C, stats + 2 * C, stats + 3 * C, relu, (__hip_bfloat16*)y);
+    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)xa, M, C, stats + 2 * C, stats + 3 * C, relu, (__hip_bfloat16*)y);
   else
-    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st, (const float*)x, nvec, C,
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)xa, M, C,
                        stats + 2 * C, stats + 3 * C, relu, (float*)y);
   return (int)hipGetLastError();
 }
@@ -327,19 +388,19 @@ int mifx_bn_relu_fwd(int dtype, const void* x, long long M, int C, const float* 
 int mifx_bn_relu_apply(int dtype, const void* x, long long M, int C, const float* scale, const float* shift, int relu,
                        void* y, hipStream_t st) {
   if (!shape_ok(M, C)) return -1;
-  const long long nvec = M * C / kVec;
   if (dtype)
-    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
-                       (const __hip_bfloat16*)x, nvec, C, scale, shift, relu, (__hip_bfloat16*)y);
+    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)x, M, C, scale, shift, relu, (__hip_bfloat16*)y);
   else
-    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st, (const float*)x, nvec, C, scale,
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)x, M, C, scale,
                        shift, relu, (float*)y);
   return (int)hipGetLastError();
 }
 
 // backward: stats = forward's [mean, rstd, scale, shift]; part = scratch [2, blocks, C];
 // kbuf = scratch [3, C]; outputs dx, dgamma, dbeta
-int mifx_bn_relu_bwd(int dtype, const void* dy, const void* x, long long M, int C, const float* w,
+// dres non-null: dx += dres (gradient of the residual sum through its identity-shortcut use)
+int mifx_bn_relu_bwd(int dtype, const void* dy, const void* x, const void* dres, long long M, int C, const float* w,
                      const float* stats, int relu, float* part, float* kbuf, void* dx, float* dgamma, float* dbeta,
                      hipStream_t st) {
   if (!shape_ok(M, C)) return -1;
@@ -351,16 +412,15 @@ int mifx_bn_relu_bwd(int dtype, const void* dy, const void* x, long long M, int 
   else
     hipLaunchKernelGGL(bn_bwd_reduce<float>, dim3(nb), dim3(kThreads), 0, st, (const float*)dy, (const float*)x, M, C,
                        scale, shift, mean, rstd, relu, part, part + (size_t)nb * C);
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, st, part,
-                     part + (size_t)nb * C, nb, M, C, w, rstd, dgamma, dbeta, kbuf);
-  const long long nvec = M * C / kVec;
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kFinCols - 1) / kFinCols), dim3(kThreads), 0, st, part,
+                     part + (size_t)nb * C, nb, M, C, w, mean, rstd, dgamma, dbeta, kbuf);
   if (dtype)
-    hipLaunchKernelGGL(bn_bwd_apply<__hip_bfloat16>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
-                       (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, nvec, C, scale, shift, mean, rstd, kbuf,
-                       relu, (__hip_bfloat16*)dx);
+    hipLaunchKernelGGL(bn_bwd_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, M, C, scale, shift, kbuf, relu,
+                       (const __hip_bfloat16*)dres, (__hip_bfloat16*)dx);
   else
-    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(apply_grid(nvec)), dim3(kThreads), 0, st, (const float*)dy,
-                       (const float*)x, nvec, C, scale, shift, mean, rstd, kbuf, relu, (float*)dx);
+    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)dy,
+                       (const float*)x, M, C, scale, shift, kbuf, relu, (const float*)dres, (float*)dx);
   return (int)hipGetLastError();
 }
 

@@ -25,12 +25,18 @@ class PreActBottleneck(nn.Module):
         self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
 
     def forward(self, x):
-        pre = self.bn0(x)
-        sc = self.shortcut(pre) if self.shortcut is not None else x
+        """x: a tensor, or the (branch, shortcut) pair of the previous block whose sum is this block's
+        input -- the residual add then happens inside bn0's fused kernels (fwd and bwd). Returns the
+        un-added (branch, shortcut) pair for the next block / the final BN."""
+        if isinstance(x, tuple):
+            pre, s = self.bn0.forward_add(*x)
+        else:
+            pre, s = self.bn0(x), x
+        sc = self.shortcut(pre) if self.shortcut is not None else s
         y = self.conv1(pre)
         y = self.conv2(self.bn1(y))
         y = self.conv3(self.bn2(y))
-        return y + sc
+        return y, sc
 
 
 class ResNetV2(nn.Module):
@@ -49,8 +55,7 @@ class ResNetV2(nn.Module):
 
     def forward(self, x):  # x: [B, 3, H, W] in [0, 1] (NHWC memory format preferred)
         y = F.max_pool2d(self.stem(x), 3, 2, 1)
-        y = self.blocks(y)
-        y = self.post_bn(y)
+        y, _ = self.post_bn.forward_add(*self.blocks(y))
         return self.fc(y.mean((2, 3)))
 
 

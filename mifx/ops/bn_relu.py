@@ -22,9 +22,10 @@ def _fns():
     lib = _lib.load("bn_relu")
     return {
         "blocks": sig(lib, "mifx_bn_blocks", [I64, I32]),
-        "fwd": sig(lib, "mifx_bn_relu_fwd", [I32, VP, I64, I32, VP, VP, F32, F32, VP, VP, I32, VP, VP, VP, VP]),
+        "fwd": sig(lib, "mifx_bn_relu_fwd",
+                   [I32, VP, VP, VP, I64, I32, VP, VP, F32, F32, VP, VP, I32, VP, VP, VP, VP]),
         "apply": sig(lib, "mifx_bn_relu_apply", [I32, VP, I64, I32, VP, VP, I32, VP, VP]),
-        "bwd": sig(lib, "mifx_bn_relu_bwd", [I32, VP, VP, I64, I32, VP, VP, I32, VP, VP, VP, VP, VP, VP]),
+        "bwd": sig(lib, "mifx_bn_relu_bwd", [I32, VP, VP, VP, I64, I32, VP, VP, I32, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -50,20 +51,49 @@ def _dt(t: torch.Tensor) -> int:
     return 1 if t.dtype == torch.bfloat16 else 0
 
 
+def _fwd(x, x2, weight, bias, run_mean, run_var, momentum, eps, relu):
+    """Launch the fused forward; returns (y, s, w32, stats) where s = x + x2 (or x when x2 is None)."""
+    v = _nhwc_view(x)
+    M, C = v.shape
+    w32, b32 = weight.float().contiguous(), bias.float().contiguous()
+    nb = _fns()["blocks"](M, C)
+    part = torch.empty(2, nb, C, device=x.device, dtype=torch.float32)
+    stats = torch.empty(4, C, device=x.device, dtype=torch.float32)
+    y = torch.empty_like(x)  # same (channels_last) layout
+    s = torch.empty_like(x) if x2 is not None else x
+    v2 = _nhwc_view(x2) if x2 is not None else None
+    sv = _nhwc_view(s) if x2 is not None else None
+    check(_fns()["fwd"](_dt(x), ptr(v), ptr(v2), ptr(sv), M, C, ptr(w32), ptr(b32), float(eps), float(momentum),
+                        ptr(run_mean), ptr(run_var if run_mean is not None else None), int(relu), ptr(part),
+                        ptr(stats), ptr(y), stream_handle(x.device)), "mifx_bn_relu_fwd")
+    return y, s, w32, stats
+
+
+def _bwd(dy, x, w32, stats, relu, dres):
+    if dy.dim() == 4 and not dy.is_contiguous(memory_format=torch.channels_last):
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    dy = dy.to(x.dtype)
+    if dres is not None:
+        if dres.dim() == 4 and not dres.is_contiguous(memory_format=torch.channels_last):
+            dres = dres.contiguous(memory_format=torch.channels_last)
+        dres = dres.to(x.dtype)
+    v, dv = _nhwc_view(x), _nhwc_view(dy)
+    M, C = v.shape
+    nb = _fns()["blocks"](M, C)
+    part = torch.empty(2, nb, C, device=x.device, dtype=torch.float32)
+    kbuf = torch.empty(3, C, device=x.device, dtype=torch.float32)
+    dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    dx = torch.empty_like(x)
+    check(_fns()["bwd"](_dt(x), ptr(dv), ptr(v), ptr(_nhwc_view(dres) if dres is not None else None), M, C, ptr(w32),
+                        ptr(stats), int(relu), ptr(part), ptr(kbuf), ptr(dx), ptr(dgb[0]), ptr(dgb[1]),
+                        stream_handle(x.device)), "mifx_bn_relu_bwd")
+    return dx, dgb
+
+
 class _BNReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, run_mean, run_var, momentum, eps, relu):
-        v = _nhwc_view(x)
-        M, C = v.shape
-        w32, b32 = weight.float().contiguous(), bias.float().contiguous()
-        nb = _fns()["blocks"](M, C)
-        part = torch.empty(2, nb, C, device=x.device, dtype=torch.float32)
-        stats = torch.empty(4, C, device=x.device, dtype=torch.float32)
-        y = torch.empty_like(x)  # same (channels_last) layout
-        rm = run_mean if run_mean is not None else None
-        check(_fns()["fwd"](_dt(x), ptr(v), M, C, ptr(w32), ptr(b32), float(eps), float(momentum), ptr(rm),
-                            ptr(run_var if rm is not None else None), int(relu), ptr(part), ptr(stats), ptr(y),
-                            stream_handle(x.device)), "mifx_bn_relu_fwd")
+        y, _, w32, stats = _fwd(x, None, weight, bias, run_mean, run_var, momentum, eps, relu)
         ctx.save_for_backward(x, w32, stats)
         ctx.relu, ctx.wdtype = relu, weight.dtype
         return y
@@ -71,19 +101,30 @@ class _BNReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w32, stats = ctx.saved_tensors
-        if not dy.is_contiguous(memory_format=torch.channels_last) and dy.dim() == 4:
-            dy = dy.contiguous(memory_format=torch.channels_last)
-        dy = dy.to(x.dtype)
-        v, dv = _nhwc_view(x), _nhwc_view(dy)
-        M, C = v.shape
-        nb = _fns()["blocks"](M, C)
-        part = torch.empty(2, nb, C, device=x.device, dtype=torch.float32)
-        kbuf = torch.empty(3, C, device=x.device, dtype=torch.float32)
-        dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
-        dx = torch.empty_like(x)
-        check(_fns()["bwd"](_dt(x), ptr(dv), ptr(v), M, C, ptr(w32), ptr(stats), int(ctx.relu), ptr(part), ptr(kbuf),
-                            ptr(dx), ptr(dgb[0]), ptr(dgb[1]), stream_handle(x.device)), "mifx_bn_relu_bwd")
+        dx, dgb = _bwd(dy, x, w32, stats, ctx.relu, None)
         return dx, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None, None
+
+
+class _AddBNReLU(torch.autograd.Function):
+    """(y, s) = (relu(bn(a + b)), a + b): the residual sum of a pre-activation block feeds both the next
+    BN+ReLU and (often) the next identity shortcut. Forward: the add is done inside the statistics
+    pass; backward: the shortcut's gradient ds is accumulated by the dx kernel, so neither direction
+    launches a separate add kernel."""
+
+    @staticmethod
+    def forward(ctx, a, b, weight, bias, run_mean, run_var, momentum, eps):
+        y, s, w32, stats = _fwd(a, b.to(a.dtype), weight, bias, run_mean, run_var, momentum, eps, True)
+        ctx.save_for_backward(s, w32, stats)
+        ctx.wdtype = weight.dtype
+        return y, s
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, w32, stats = ctx.saved_tensors
+        if dy is None:
+            return ds, ds, None, None, None, None, None, None
+        dx, dgb = _bwd(dy, s, w32, stats, True, ds)
+        return dx, dx, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None
 
 
 def bn_relu(x, weight, bias, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5,
@@ -106,13 +147,30 @@ def bn_relu(x, weight, bias, running_mean=None, running_var=None, training=True,
     return F.relu(y) if relu else y
 
 
-class BatchNormReLU2d(nn.BatchNorm2d):
-    """nn.BatchNorm2d followed by ReLU, fused on the GPU. Parameters/buffers/state_dict == BatchNorm2d."""
+def add_bn_relu(a, b, weight, bias, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5):
+    """(relu(batch_norm(a + b)), a + b) with the add fused into the BN kernels on the GPU."""
+    if training and native_ok(a) and b.shape == a.shape and native_ok(b.to(a.dtype)):
+        return _AddBNReLU.apply(a, b, weight, bias, running_mean, running_var, momentum, eps)
+    s = a + b
+    return bn_relu(s, weight, bias, running_mean, running_var, training, momentum, eps, True), s
 
-    def forward(self, x):
+
+class BatchNormReLU2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d followed by ReLU, fused on the GPU. Parameters/buffers/state_dict == BatchNorm2d.
+    `forward_add(a, b)` normalises the residual sum a + b and also returns it."""
+
+    def _args(self):
         if self.training and self.track_running_stats:
             self.num_batches_tracked.add_(1)
         use_batch_stats = self.training or not self.track_running_stats
-        return bn_relu(x, self.weight, self.bias, self.running_mean if self.track_running_stats else None,
-                       self.running_var if self.track_running_stats else None, use_batch_stats, self.momentum,
-                       self.eps, True)
+        rm = self.running_mean if self.track_running_stats else None
+        rv = self.running_var if self.track_running_stats else None
+        return rm, rv, use_batch_stats
+
+    def forward(self, x):
+        rm, rv, train = self._args()
+        return bn_relu(x, self.weight, self.bias, rm, rv, train, self.momentum, self.eps, True)
+
+    def forward_add(self, a, b):
+        rm, rv, train = self._args()
+        return add_bn_relu(a, b, self.weight, self.bias, rm, rv, train, self.momentum, self.eps)

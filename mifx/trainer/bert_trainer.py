@@ -99,7 +99,15 @@ def main(argv=None):
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one captured hipGraph")
     ap.add_argument("--no-flat-adamw", action="store_true", help="fp32 params + torch fused AdamW")
+    ap.add_argument("--tunable", default=None, metavar="CSV",
+                    help="enable PyTorch TunableOp: benchmark hipBLASLt/rocBLAS solutions per GEMM shape during "
+                         "warmup and keep the best (results cached in CSV)")
     a = ap.parse_args(argv)
+    if a.tunable and torch.cuda.is_available():
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_filename(a.tunable)
+        torch.cuda.tunable.set_max_tuning_iterations(30)
     env = mdist.init()
     dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":

@@ -67,3 +67,64 @@ def test_fused_bn_relu_is_deterministic():
         b.grad = None
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
+
+
+def test_cpu_add_bn_relu_reference():
+    from mifx.ops.bn_relu import add_bn_relu
+
+    a, b = torch.randn(2, 8, 3, 3), torch.randn(2, 8, 3, 3)
+    w, bias = torch.ones(8), torch.zeros(8)
+    y, s = add_bn_relu(a, b, w, bias, None, None, True)
+    torch.testing.assert_close(s, a + b)
+    torch.testing.assert_close(y, F.relu(F.batch_norm(a + b, None, None, w, bias, True)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+def test_fused_add_bn_relu_matches_reference(dtype, tol):
+    from mifx.ops.bn_relu import add_bn_relu
+
+    torch.manual_seed(0)
+    shape = (4, 256, 14, 14)
+    C = shape[1]
+    mk = lambda: torch.randn(shape, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)  # noqa
+    a, b = mk().requires_grad_(), mk().requires_grad_()
+    w = (torch.rand(C, device="cuda") + 0.5).requires_grad_()
+    bias = (torch.randn(C, device="cuda") * 0.2).requires_grad_()
+    y, s = add_bn_relu(a, b, w, bias, None, None, True)
+    a32, b32 = a.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    w2, bias2 = w.detach().clone().requires_grad_(), bias.detach().clone().requires_grad_()
+    s_ref = (a32 + b32).to(dtype).float()  # the fused kernel normalises the stored (rounded) sum
+    s_ref = a32 + b32 + (s_ref - (a32 + b32)).detach()
+    y_ref = F.relu(F.batch_norm(s_ref, None, None, w2, bias2, True, 0.1, 1e-5))
+    torch.testing.assert_close(s.float(), s_ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(y.float(), y_ref, rtol=tol, atol=tol)
+    gy, gs = torch.randn_like(y_ref), torch.randn_like(y_ref)
+    torch.autograd.backward([y, s], [gy.to(dtype).contiguous(memory_format=torch.channels_last),
+                                     gs.to(dtype).contiguous(memory_format=torch.channels_last)])
+    torch.autograd.backward([y_ref, s_ref], [gy, gs])
+    torch.testing.assert_close(a.grad.float(), a32.grad, rtol=tol * 3, atol=tol * 3)
+    torch.testing.assert_close(b.grad.float(), b32.grad, rtol=tol * 3, atol=tol * 3)
+    m = shape[0] * shape[2] * shape[3]
+    torch.testing.assert_close(w.grad, w2.grad, rtol=tol * 3, atol=tol * 3 * m ** 0.5)
+
+
+@pytest.mark.gpu
+def test_resnet_fused_blocks_match_unfused_reference():
+    """Whole ResNet-50 v2 forward/backward with the fused kernels vs the same weights on the PyTorch
+    reference path (fp32 input, NCHW -> every BN runs F.batch_norm + ReLU)."""
+    from mifx.models.resnet import resnet50_v2
+
+    torch.manual_seed(0)
+    m = resnet50_v2(10).cuda()
+    x = torch.rand(4, 3, 64, 64, device="cuda")
+    ref_out = m(x)  # NCHW fp32: reference path
+    ref_out.sum().backward()
+    gref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    m2 = m.to(memory_format=torch.channels_last)
+    out = m2(x.contiguous(memory_format=torch.channels_last))  # fused native path (fp32)
+    out.sum().backward()
+    torch.testing.assert_close(out, ref_out, rtol=2e-3, atol=2e-3)
+    for n, p in m2.named_parameters():
+        torch.testing.assert_close(p.grad, gref[n], rtol=5e-2, atol=5e-3 * (1 + gref[n].abs().max().item()))
