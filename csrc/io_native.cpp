@@ -83,7 +83,7 @@ long long mifx_tfrecord_scan(const char* buf, size_t len, long long* offsets, lo
     uint32_t hc;
     std::memcpy(&hc, buf + pos + 8, 4);
     if (verify && mask(mifx_crc32c(buf + pos, 8, 0)) != hc) return -(1 + n);
-    if (pos + 12 + sz + 4 > len) return -(1 + n);
+    if (len - pos < 16 || sz > len - pos - 16) return -(1 + n);  // overflow-safe bound (corrupt length)
     if (verify) {
       uint32_t dc;
       std::memcpy(&dc, buf + pos + 12 + sz, 4);

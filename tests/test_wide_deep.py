@@ -232,3 +232,23 @@ def test_fused_predict_matches_torch():
     dense, ids, _ = wdm.records_to_tensors(rec)
     ref = mref(dense, ids).detach()
     assert (got - ref).abs().max() < 0.05 * (ref.abs().max() + 1)
+
+
+@pytest.mark.gpu
+def test_fused_training_is_run_to_run_deterministic():
+    """Two trainers from the same init on the same data must produce bit-identical parameters:
+    slab reduction is fixed-order; checks that the in-LDS wide-gradient accumulation is too."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(1 << 16, device=dev, seed=5)
+    params = []
+    for _ in range(2):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=1), batch=8192, device=dev)
+        tr.set_data(rec)
+        for _ in range(10):
+            tr.step()
+        torch.cuda.synchronize()
+        params.append(tr.param.clone())
+    diff = (params[0] - params[1]).abs().max().item()
+    assert torch.equal(params[0], params[1]), f"max |diff| {diff}"
