@@ -339,6 +339,16 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
 
   const long long start = step_ctr ? (step_ctr[0] * batch) % n_data : start_fixed;
   const int ntiles = (int)((batch + T - 1) / T);
+  // Wide-part gradient: LDS histogram in 32-bit fixed point, so the result does not depend on the
+  // order in which lanes/waves hit a bucket (integer adds commute; fp32 ds_add_f32 would not).
+  // |dl| <= |grad_scale| for labels in {0, 1}; the scale is the largest power of two that keeps
+  // this workgroup's whole-bucket sum below 2^30, i.e. ~2^-30 of the bucket bound per unit.
+  const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const float qbound = fmaxf(fabsf(grad_scale) * (float)(max(my_tiles, 1) * T), 1e-30f);
+  const float qscale = exp2f(fminf(floorf(log2f(1073741824.f / qbound)), 100.f));
+  const float qinv = 1.f / qscale;  // exact: power of two
+  const float qmax = 1073741824.f / (float)(max(my_tiles, 1) * T);
+  int* wgi = (int*)wgrad;
 
   // dW tile ownership (see dw_phase): L1 nt{w,w+4} x kt{0,1}; L2 nt{0..5} x kt{2w,2w+1};
   // L3 nt{w} x kt{0..5}; L4 nt{w} x kt{0..3}; L5 nt{0} x kt{w}
@@ -426,8 +436,9 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     const float dl = valid ? (1.f / (1.f + __expf(-x)) - y) * grad_scale : 0.f;
     if (h == 0 && valid) {
       loss_sum += lossv;
+      const int q = __float2int_rn(fminf(fmaxf(dl * qscale, -qmax), qmax));
 #pragma unroll
-      for (int f = 0; f < 9; ++f) atomicAdd(&wgrad[ids[f]], dl);
+      for (int f = 0; f < 9; ++f) atomicAdd(&wgi[ids[f]], q);
       dl_sum += dl;
     }
     {
@@ -487,7 +498,7 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * STRIDE + NTILE * 256;
     for (int c = tid; c < WIDE_PAD; c += NTHR) {
-      float v = wgrad[c];
+      float v = (float)wgi[c] * qinv;
       if (c == WIDE_BIAS) v += red[4] + red[5] + red[6] + red[7];
       my[c] = v;
     }

@@ -18,6 +18,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import cnn_ops
+
 
 def _same_pad(x: torch.Tensor, k: int, s: int, value: float = 0.0) -> torch.Tensor:
     """TF SAME padding for NCHW tensors (pads more on the bottom/right when odd)."""
@@ -92,8 +94,8 @@ class PateCNN(nn.Module):
 
     @staticmethod
     def _lrn(x):  # tf.nn.lrn(depth_radius=4, bias=1.0, alpha=0.001/9, beta=0.75)
-        # torch's alpha is divided by size: alpha_t = alpha_tf * (2r+1)
-        return F.local_response_norm(x, size=9, alpha=0.001 / 9.0 * 9, beta=0.75, k=1.0)
+        # NHWC GPU activations: HIP LRN fwd/bwd kernels (csrc/cnn_ops.hip); else torch's LRN
+        return cnn_ops.lrn(x, depth_radius=4, bias=1.0, alpha=0.001 / 9.0, beta=0.75)
 
     def forward(self, x):
         if x.dim() == 3:

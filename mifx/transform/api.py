@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import contextlib
 import json
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import Any
@@ -89,9 +90,9 @@ def analyze(preprocessing_fn, inputs: dict, device=None) -> tuple[dict, Transfor
     return _materialize(out), st
 
 
-def apply(preprocessing_fn, inputs: dict, state: TransformState) -> dict:
-    """APPLY phase: replay with recorded analyzer constants."""
-    with _phase("apply", state):
+def apply(preprocessing_fn, inputs: dict, state: TransformState, device=None) -> dict:
+    """APPLY phase: replay with recorded analyzer constants (mappers run on `device` when set)."""
+    with _phase("apply", state, device):
         out = preprocessing_fn(dict(inputs))
     return _materialize(out)
 
@@ -130,9 +131,22 @@ def fill_in_missing(x, default=None) -> np.ndarray:
     return a
 
 
+GPU_MIN_ROWS = int(os.environ.get("MIFX_GPU_ANALYZER_MIN_ROWS", "8192"))
+
+
+def _gpu_ctx(n: int):
+    """The active phase's device when it is a GPU and the column is big enough to be worth a launch."""
+    c = getattr(_LOCAL, "ctx", None)
+    if c is None or c.device is None or n < GPU_MIN_ROWS:
+        return None
+    import torch
+
+    return c.device if torch.device(c.device).type == "cuda" else None
+
+
 def _moments(a: np.ndarray) -> dict:
     c = _ctx()
-    if c.device is not None and a.size >= 1 << 16:
+    if _gpu_ctx(a.size) is not None:
         from ..ops import analyzers
 
         m = analyzers.column_moments(a, device=c.device)
@@ -190,6 +204,11 @@ def vocabulary(x, top_k: int | None = None, frequency_threshold: int | None = No
     s = _str(x)
 
     def compute():
+        dev = _gpu_ctx(len(s))
+        if dev is not None:  # HIP hash-table count (csrc/vocab.hip); identical ordering and cut
+            from ..ops import vocab as V
+
+            return V.vocabulary(s, top_k=top_k, frequency_threshold=frequency_threshold, device=dev)
         vals, counts = np.unique(s, return_counts=True)
         order = sorted(zip(counts.tolist(), vals.tolist()), reverse=True)
         if frequency_threshold is not None:
@@ -236,6 +255,11 @@ def hash_strings(x, hash_buckets: int) -> np.ndarray:
 
 def apply_vocabulary(x, vocab: list[str], default_value: int = -1, num_oov_buckets: int = 0) -> np.ndarray:
     s = _str(x)
+    dev = _gpu_ctx(len(s))
+    if dev is not None:  # device hash-table lookup + FNV OOV buckets (csrc/vocab.hip)
+        from ..ops import vocab as V
+
+        return V.apply_vocabulary(s, vocab, default_value=default_value, num_oov_buckets=num_oov_buckets, device=dev)
     index = {v: i for i, v in enumerate(vocab)}
     n = len(vocab)
     out = np.empty(len(s), dtype=np.int64)
@@ -267,11 +291,11 @@ def string_to_int(x, default_value: int = -1, top_k: int | None = None, frequenc
 def apply_buckets(x, boundaries) -> np.ndarray:
     a = _num(x)
     b = np.asarray(boundaries, dtype=np.float64)
-    c = _ctx()
-    if c.device is not None and a.size >= 1 << 16:
+    dev = _gpu_ctx(a.size)
+    if dev is not None:
         from ..ops import analyzers
 
-        return analyzers.bucketize(a, b, device=c.device)
+        return analyzers.bucketize(a, b, device=dev)
     return np.searchsorted(b, a, side="right").astype(np.int64)
 
 
