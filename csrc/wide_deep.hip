@@ -276,15 +276,27 @@ __device__ __forceinline__ void dw_phase(v4f (&acc)[NTW * KTW], const uint16_t* 
       for (int j = 0; j < KTW; ++j) acc[i * KTW + j] = mfma(fa[i][s], fb[j][s], acc[i * KTW + j]);
 }
 
+// tmap: tile -> position in the compact slab (-1: tile holds only padding, never stored/reduced).
+// The wave's entries are fetched once at kernel start (load_ct) so the epilogue stores do not wait
+// on dependent scalar loads.
 template <int K, int NTW, int KTW>
-__device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NTW * KTW], int tbase, int nt0, int ntS,
-                                            int kt0, int ktS, int lane) {
+__device__ __forceinline__ void load_ct(int (&ct)[NTW * KTW], int tbase, int nt0, int ntS, int kt0, int ktS,
+                                        const int* __restrict__ tmap) {
+#pragma unroll
+  for (int i = 0; i < NTW; ++i)
+#pragma unroll
+    for (int j = 0; j < KTW; ++j) ct[i * KTW + j] = tmap[tbase + (nt0 + i * ntS) * (K / 16) + kt0 + j * ktS];
+}
+
+template <int NTW, int KTW>
+__device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NTW * KTW], const int (&ct)[NTW * KTW],
+                                            int lane) {
 #pragma unroll
   for (int i = 0; i < NTW; ++i)
 #pragma unroll
     for (int j = 0; j < KTW; ++j) {
-      const int tile = tbase + (nt0 + i * ntS) * (K / 16) + kt0 + j * ktS;
-      float* dst = slab + (size_t)tile * 256 + lane;
+      if (ct[i * KTW + j] < 0) continue;
+      float* dst = slab + (size_t)ct[i * KTW + j] * 256 + lane;
 #pragma unroll
       for (int e = 0; e < 4; ++e) dst[e * 64] = acc[i * KTW + j][e];
     }
@@ -302,11 +314,19 @@ __device__ __forceinline__ int wt_lds_offset(int e) {
   return wt_off<OFF5, K5, LW5>(e);
 }
 
+// live rows / 16-byte granules per row of each layer's weight image (host: models.wide_deep.stage_dims)
+struct StageDims {
+  int rows[5];
+  int gpr[5];
+  int total;
+};
+
 template <bool TRAIN>
 __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     const uint4* __restrict__ data, long long n_data, long long batch, long long start_fixed,
     const long long* __restrict__ step_ctr, const uint16_t* __restrict__ wt, const float* __restrict__ wide,
-    float* __restrict__ slab, float* __restrict__ slab_loss, float* __restrict__ logits_out, float grad_scale) {
+    float* __restrict__ slab, float* __restrict__ slab_loss, float* __restrict__ logits_out, float grad_scale,
+    const int* __restrict__ tmap, int stride, StageDims sd) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LEND);
   float* red = wgrad + WIDE_PAD;
@@ -315,16 +335,38 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   if (blockIdx.x == 0 && lane == 0) g_stamps[w][0] = __builtin_amdgcn_s_memtime();
 #endif
 
-  // stage the bf16 weight image: issue all global loads, then all LDS stores
+  // Stage the LIVE part of the bf16 weight image: per layer the rows that hold real weights (plus the
+  // constant-1 producer row) and the 16-byte granules up to the last real column -- 1715 of the 3456
+  // granules for the taxi tower, so the every-CU-at-once prologue burst moves half the bytes. The rest
+  // of the weight region is zero-filled in LDS while the global loads are in flight.
   {
-    constexpr int NCH = WTOT / 8, PER = (NCH + NTHR - 1) / NTHR;
+    constexpr int PER = (WTOT / 8 + NTHR - 1) / NTHR;  // bound: every granule live
     uint4 v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = *(const uint4*)(wt + min(tid + i * NTHR, NCH - 1) * 8);
+    int dst[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = tid + i * NTHR;
-      if (c < NCH) *(uint4*)(lds + wt_lds_offset(c * 8)) = v[i];
+      if (i * NTHR >= sd.total) break;  // uniform
+      const int c = min(tid + i * NTHR, sd.total - 1);
+      int l = 0, cc = c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (l == q && cc >= sd.rows[q] * sd.gpr[q]) {
+          cc -= sd.rows[q] * sd.gpr[q];
+          l = q + 1;
+        }
+      const int gpr = sd.gpr[l], row = cc / gpr, g = cc - row * gpr;
+      const int K = l == 0 ? K1 : l == 1 ? K2 : l == 2 ? K3 : l == 3 ? K4 : K5;
+      const int off = l == 0 ? OFF1 : l == 1 ? OFF2 : l == 2 ? OFF3 : l == 3 ? OFF4 : OFF5;
+      const int lw = l == 0 ? LW1 : l == 1 ? LW2 : l == 2 ? LW3 : l == 3 ? LW4 : LW5;
+      v[i] = *(const uint4*)(wt + off + row * K + g * 8);
+      dst[i] = tid + i * NTHR < sd.total ? lw + row * (K + PAD) + g * 8 : -1;
+    }
+    for (int c = tid; c < LWEND / 8; c += NTHR) *(uint4*)(lds + c * 8) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (i * NTHR >= sd.total) break;
+      if (dst[i] >= 0) *(uint4*)(lds + dst[i]) = v[i];
     }
   }
   for (int c = tid; c < T * (K1 + PAD) / 8; c += NTHR) *(uint4*)(lds + LA0 + c * 8) = make_uint4(0, 0, 0, 0);
@@ -361,6 +403,14 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   for (int j = 0; j < 6; ++j) acc3[j] = (v4f){0.f, 0.f, 0.f, 0.f};
   acc5[0] = (v4f){0.f, 0.f, 0.f, 0.f};
   float loss_sum = 0.f, dl_sum = 0.f;
+  int ct1[4], ct2[12], ct3[6], ct4[4], ct5[1];  // compact slab positions of this wave's dW tiles
+  if (TRAIN) {
+    load_ct<K1, 2, 2>(ct1, TB1, w, 4, 0, 1, tmap);
+    load_ct<K2, 6, 2>(ct2, TB2, 0, 1, 2 * w, 1, tmap);
+    load_ct<K3, 1, 6>(ct3, TB3, w, 0, 0, 1, tmap);
+    load_ct<K4, 1, 4>(ct4, TB4, w, 0, 0, 1, tmap);
+    load_ct<K5, 1, 1>(ct5, TB5, 0, 0, w, 0, tmap);
+  }
 
   uint16_t* A0 = lds + LA0;
   uint16_t* A1 = lds + LA1;
@@ -487,16 +537,16 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     red[4 + w] = dl_sum;
   }
   if (TRAIN) {
-    float* my = slab + (size_t)blockIdx.x * STRIDE;
-    store_tiles<K1, 2, 2>(my, acc1, TB1, w, 4, 0, 1, lane);
-    store_tiles<K2, 6, 2>(my, acc2, TB2, 0, 1, 2 * w, 1, lane);
-    store_tiles<K3, 1, 6>(my, acc3, TB3, w, 0, 0, 1, lane);
-    store_tiles<K4, 1, 4>(my, acc4, TB4, w, 0, 0, 1, lane);
-    store_tiles<K5, 1, 1>(my, acc5, TB5, 0, 0, w, 0, lane);
+    float* my = slab + (size_t)blockIdx.x * stride;
+    store_tiles<2, 2>(my, acc1, ct1, lane);
+    store_tiles<6, 2>(my, acc2, ct2, lane);
+    store_tiles<1, 6>(my, acc3, ct3, lane);
+    store_tiles<1, 4>(my, acc4, ct4, lane);
+    store_tiles<1, 1>(my, acc5, ct5, lane);
   }
   __syncthreads();
   if (TRAIN) {
-    float* my = slab + (size_t)blockIdx.x * STRIDE + NTILE * 256;
+    float* my = slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD);
     for (int c = tid; c < WIDE_PAD; c += NTHR) {
       float v = (float)wgi[c] * qinv;
       if (c == WIDE_BIAS) v += red[4] + red[5] + red[6] + red[7];
@@ -510,8 +560,8 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
 
 // partial[sp][e] = sum_{g in split sp} slab[g][e]   (float4 granules, 4 loads in flight)
 __global__ __launch_bounds__(256) void wd_reduce(const float4* __restrict__ slab, int G, int gchunk,
-                                                 float4* __restrict__ partial) {
-  constexpr int S4 = STRIDE / 4;
+                                                 float4* __restrict__ partial, int stride) {
+  const int S4 = stride / 4;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= S4) return;
   const int g0 = blockIdx.y * gchunk;
@@ -576,7 +626,7 @@ __device__ __forceinline__ float opt_update(const OptHyper& hp, float w, float g
 __global__ __launch_bounds__(256) void wd_optimizer(
     const float* __restrict__ partial, int nparts, const int* __restrict__ gidx, const uint8_t* __restrict__ mask,
     float* __restrict__ param, float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
-    long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+    long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw, int stride) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const long long step = step_ctr[0] + 1;
   if (c < WTOT + NWIDE) {
@@ -588,9 +638,9 @@ __global__ __launch_bounds__(256) void wd_optimizer(
       int pidx = 0;
       for (; pidx + 3 < nparts; pidx += 4) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) gs[u] += partial[(size_t)(pidx + u) * STRIDE + gi];
+        for (int u = 0; u < 4; ++u) gs[u] += partial[(size_t)(pidx + u) * stride + gi];
       }
-      for (; pidx < nparts; ++pidx) gs[0] += partial[(size_t)pidx * STRIDE + gi];
+      for (; pidx < nparts; ++pidx) gs[0] += partial[(size_t)pidx * stride + gi];
       const float g = (gs[0] + gs[1]) + (gs[2] + gs[3]);
       float a0 = s0[c], a1 = s1[c];
       w = opt_update(dnn ? hd : hw, w, g, a0, a1, step);
@@ -617,7 +667,8 @@ int mifx_wd_constants(int* out, int n) {
 
 int mifx_wd_fused(const void* data, long long n_data, long long batch, long long start_fixed,
                   const long long* step_ctr, const void* wt, const float* wide, float* slab, float* slab_loss,
-                  float* logits_out, float grad_scale, int grid, int train, hipStream_t stream) {
+                  float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
+                  const int* stage_dims, hipStream_t stream) {
   static bool attr_done = false;
   if (!attr_done) {
     (void)hipFuncSetAttribute((const void*)wd_fused<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -625,33 +676,46 @@ int mifx_wd_fused(const void* data, long long n_data, long long batch, long long
     attr_done = true;
   }
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data) return -1;
+  if (train && (tmap == nullptr || stride < WIDE_PAD || stride > STRIDE || stride % 4 != 0)) return -1;
+  // stage_dims (host array of 10 ints: rows[5], granules-per-row[5]); null = the whole padded image
+  StageDims sd;
+  const int KL[5] = {K1, K2, K3, K4, K5}, NL[5] = {N1, N2, N3, N4, N5};
+  sd.total = 0;
+  for (int l = 0; l < 5; ++l) {
+    sd.rows[l] = stage_dims ? stage_dims[l] : NL[l];
+    sd.gpr[l] = stage_dims ? stage_dims[5 + l] : KL[l] / 8;
+    if (sd.rows[l] < 1 || sd.rows[l] > NL[l] || sd.gpr[l] < 1 || sd.gpr[l] > KL[l] / 8) return -1;
+    sd.total += sd.rows[l] * sd.gpr[l];
+  }
   if (train)
     hipLaunchKernelGGL(wd_fused<true>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
-                       start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale);
+                       start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale,
+                       tmap, stride, sd);
   else
     hipLaunchKernelGGL(wd_fused<false>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
-                       start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale);
+                       start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale,
+                       tmap, stride, sd);
   return (int)hipGetLastError();
 }
 
-int mifx_wd_reduce(const float* slab, int G, int nsplit, float* partial, hipStream_t stream) {
-  if (G <= 0 || nsplit <= 0) return -1;
+int mifx_wd_reduce(const float* slab, int G, int nsplit, float* partial, int stride, hipStream_t stream) {
+  if (G <= 0 || nsplit <= 0 || stride <= 0 || stride > STRIDE || stride % 4 != 0) return -1;
   const int gchunk = (G + nsplit - 1) / nsplit;
-  dim3 grid((STRIDE / 4 + 255) / 256, nsplit);
-  hipLaunchKernelGGL(wd_reduce, grid, dim3(256), 0, stream, (const float4*)slab, G, gchunk, (float4*)partial);
+  dim3 grid((stride / 4 + 255) / 256, nsplit);
+  hipLaunchKernelGGL(wd_reduce, grid, dim3(256), 0, stream, (const float4*)slab, G, gchunk, (float4*)partial, stride);
   return (int)hipGetLastError();
 }
 
 int mifx_wd_optimizer(const float* partial, int nparts, const int* gidx, const uint8_t* mask, float* param,
                       float* s0, float* s1, void* wt_out, long long* step_ctr, const float* hyper_dnn,
-                      const float* hyper_wide, hipStream_t stream) {
+                      const float* hyper_wide, int stride, hipStream_t stream) {
   OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5], hyper_dnn[6],
               hyper_dnn[7]};
   OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
               hyper_wide[6], hyper_wide[7]};
   const int n = WTOT + NWIDE;
   hipLaunchKernelGGL(wd_optimizer, dim3((n + 255) / 256), dim3(256), 0, stream, partial, nparts, gidx, mask, param, s0,
-                     s1, (uint16_t*)wt_out, step_ctr, hd, hw);
+                     s1, (uint16_t*)wt_out, step_ctr, hd, hw, stride);
   return (int)hipGetLastError();
 }
 

@@ -19,12 +19,16 @@ from ..orchestration.component import BaseComponent, BaseExecutor, ChannelParame
 from .statistics import load_schema_from_artifact
 
 
-def table_to_inputs(table: pa.Table) -> dict:
-    """Arrow columns -> numpy (object arrays with None for missing strings/ints, NaN floats)."""
+def table_to_inputs(table: pa.Table, arrow_strings: bool = False) -> dict:
+    """Arrow columns -> numpy (object arrays with None for missing strings/ints, NaN floats).
+    `arrow_strings`: string columns stay Arrow arrays (offsets + bytes buffers) so the GPU vocabulary
+    kernels consume them without a per-row Python pass (mifx.transform.api accepts both forms)."""
     out = {}
     for name in table.column_names:
         col = table.column(name)
-        if pa.types.is_floating(col.type):
+        if arrow_strings and (pa.types.is_string(col.type) or pa.types.is_large_string(col.type)):
+            out[name] = col
+        elif pa.types.is_floating(col.type):
             out[name] = col.to_numpy(zero_copy_only=False).astype(np.float64)
         elif col.null_count or pa.types.is_string(col.type) or pa.types.is_large_string(col.type):
             out[name] = np.array(col.to_pylist(), dtype=object)
@@ -62,7 +66,16 @@ class TransformExecutor(BaseExecutor):
         splits = {a.split: a for a in input_dict["input_data"]}
         train = splits.get("train") or next(iter(splits.values()))
         raw_schema = load_schema_from_artifact(input_dict["schema"][0].uri)
-        cols, state = mt.analyze(fn, table_to_inputs(dataset.read_split(train.uri)), device=self.context.device)
+        dev = self.context.device
+        gpu = dev is not None and str(dev).startswith("cuda")
+        table = dataset.read_split(train.uri)
+        try:
+            cols, state = mt.analyze(fn, table_to_inputs(table, arrow_strings=gpu), device=dev)
+        except (TypeError, AttributeError, ValueError):
+            if not gpu:
+                raise
+            # user code that needs numpy string columns: same analysis on the numpy form
+            cols, state = mt.analyze(fn, table_to_inputs(table), device=dev)
         t_stats = dv.generate_statistics_from_table(outputs_to_table(cols), name="train")
         t_schema = dv.infer_schema(t_stats)
         out = output_dict["transform_output"][0]
@@ -71,7 +84,7 @@ class TransformExecutor(BaseExecutor):
             if art.split == train.split:
                 res = cols
             else:
-                res = mt.apply(fn, table_to_inputs(dataset.read_split(splits[art.split].uri)), state)
+                res = mt.apply(fn, table_to_inputs(dataset.read_split(splits[art.split].uri)), state, device=dev)
             dataset.write_split(art.uri, outputs_to_table(res))
             art.custom_properties["num_examples"] = int(len(next(iter(res.values()))))
 

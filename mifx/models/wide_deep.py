@@ -157,25 +157,67 @@ def check_fused_compatible(cfg: WideDeepConfig) -> None:
         raise ValueError("fused kernel is specialised for the taxi wide columns")
 
 
+WIDE_PAD = 2176
+
+
+def _trainable_masks(cfg: WideDeepConfig) -> list[np.ndarray]:
+    """Per layer [N, K] bool: real weights + folded biases (the trainable entries)."""
+    out = []
+    for (K, N), (kr, nr) in zip(LAYER_KN, _real_dims(cfg)):
+        out.append((np.arange(N)[:, None] < nr) & (np.arange(K)[None, :] <= kr))
+    return out
+
+
+def compact_tile_map(cfg: WideDeepConfig | None = None) -> tuple[np.ndarray, int]:
+    """(tmap int32 [NTILE], stride): tile -> position in the compact gradient slab, -1 for 16x16 dW tiles
+    that hold only padding. The kernel skips those tiles when it writes its slab, so the slab write,
+    the slab reduction and the DP all-reduce move ~1/3 fewer bytes (72 of 108 tiles are live for the
+    taxi [100, 70, 48, 34] tower)."""
+    cfg = cfg or WideDeepConfig()
+    check_fused_compatible(cfg)
+    tmap = np.full(NTILE, -1, np.int32)
+    c = 0
+    for li, ((K, N), m) in enumerate(zip(LAYER_KN, _trainable_masks(cfg))):
+        for nt in range(N // 16):
+            for kt in range(K // 16):
+                if m[16 * nt:16 * nt + 16, 16 * kt:16 * kt + 16].any():
+                    tmap[TILE_BASE[li] + nt * (K // 16) + kt] = c
+                    c += 1
+    return tmap, c * 256 + WIDE_PAD
+
+
+def stage_dims(cfg: WideDeepConfig | None = None) -> list[int]:
+    """Live part of the padded bf16 weight image the fused kernel stages into LDS: per layer the rows
+    that carry real weights or the constant-1 producer (n <= n_real; the head has no producer row) and
+    the 16-byte granules up to the bias column k_real. -> rows[5] + granules_per_row[5]."""
+    cfg = cfg or WideDeepConfig()
+    check_fused_compatible(cfg)
+    real = _real_dims(cfg)
+    rows = [nr + (1 if li < len(real) - 1 else 0) for li, (_, nr) in enumerate(real)]
+    gpr = [kr // 8 + 1 for kr, _ in real]
+    return rows + gpr
+
+
 def canonical_index_maps(cfg: WideDeepConfig | None = None):
     """Return (gidx int32 [WTOT+NWIDE], mask uint8 [WTOT+NWIDE]).
 
-    gidx maps each canonical parameter to its position in the kernel's tile-native gradient
-    slab; mask marks trainable entries (real weights + folded biases)."""
+    gidx maps each canonical parameter to its position in the kernel's compact tile-native gradient
+    slab (see compact_tile_map); mask marks trainable entries (real weights + folded biases). Entries
+    of dead tiles are never trainable (gidx 0, mask 0)."""
     cfg = cfg or WideDeepConfig()
-    check_fused_compatible(cfg)
+    tmap, stride = compact_tile_map(cfg)
     gidx = np.zeros(WTOT + NWIDE, np.int32)
     mask = np.zeros(WTOT + NWIDE, np.uint8)
-    for li, ((K, N), (kr, nr)) in enumerate(zip(LAYER_KN, _real_dims(cfg))):
+    for li, ((K, N), m) in enumerate(zip(LAYER_KN, _trainable_masks(cfg))):
         n = np.arange(N)[:, None]
         k = np.arange(K)[None, :]
-        tile = TILE_BASE[li] + (n // 16) * (K // 16) + (k // 16)
+        ct = tmap[TILE_BASE[li] + (n // 16) * (K // 16) + (k // 16)]
         lane = 16 * ((n % 16) // 4) + (k % 16)
-        idx = tile * 256 + (n % 4) * 64 + lane
+        idx = np.where(ct >= 0, ct * 256 + (n % 4) * 64 + lane, 0)
+        assert (ct[m] >= 0).all()
         gidx[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = idx.reshape(-1)
-        m = (n < nr) & (k <= kr)
         mask[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = m.reshape(-1)
-    gidx[WTOT:] = NTILE * 256 + np.arange(NWIDE)
+    gidx[WTOT:] = stride - WIDE_PAD + np.arange(NWIDE)
     mask[WTOT:] = 1
     return gidx, mask
 

@@ -42,19 +42,49 @@ def _as_str(v) -> str:
     return v.decode() if isinstance(v, bytes) else str(v)
 
 
-def pack_strings(values) -> tuple[np.ndarray, np.ndarray, list[bytes]]:
-    """-> (uint8 byte buffer, int64 offsets [n+1], encoded list) for a column of str/bytes/None."""
+def _is_arrow(values) -> bool:
+    return type(values).__module__.startswith("pyarrow")
+
+
+def _pack_arrow(values):
+    """Arrow string/binary column -> its own (data, int64 offsets) buffers: no per-row Python work
+    (nulls read as "")."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    a = values.combine_chunks() if isinstance(values, pa.ChunkedArray) else values
+    if a.null_count:
+        a = pc.fill_null(a, "")
+    a = a.cast(pa.large_binary())  # int64 offsets
+    _, ob, db = a.buffers()
+    offs = np.frombuffer(ob, dtype=np.int64)[a.offset:a.offset + len(a) + 1]
+    buf = np.frombuffer(db, dtype=np.uint8) if db is not None and db.size else np.zeros(1, dtype=np.uint8)
+    return buf, offs, lambda i: a[i].as_py().decode()
+
+
+def pack_strings(values) -> tuple[np.ndarray, np.ndarray, "callable"]:
+    """-> (uint8 byte buffer, int64 offsets [n+1], row -> str) for a column of str/bytes/None, or an
+    Arrow string/binary column (zero-copy)."""
+    if _is_arrow(values):
+        return _pack_arrow(values)
     enc = [v if isinstance(v, bytes) else _as_str(v).encode() for v in values]
     lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=len(enc))
     offs = np.zeros(len(enc) + 1, dtype=np.int64)
     np.cumsum(lens, out=offs[1:])
     buf = np.frombuffer(b"".join(enc), dtype=np.uint8) if offs[-1] else np.zeros(1, dtype=np.uint8)
-    return buf, offs, enc
+    return buf, offs, lambda i: enc[i].decode()
 
 
 def _to_dev(buf: np.ndarray, offs: np.ndarray, dev):
-    return (torch.from_numpy(np.ascontiguousarray(buf)).to(dev),
-            torch.from_numpy(np.ascontiguousarray(offs)).to(dev))
+    # host buffers may be read-only views (bytes / Arrow): torch copies them to the device anyway
+    return (torch.from_numpy(np.require(buf, requirements=["C", "W"])).to(dev),
+            torch.from_numpy(np.require(offs, requirements=["C", "W"])).to(dev))
+
+
+def _host_strs(values) -> list[str]:
+    if _is_arrow(values):
+        return ["" if v is None else (v.decode() if isinstance(v, bytes) else v) for v in values.to_pylist()]
+    return [_as_str(v) for v in values]
 
 
 def _capacity(n: int) -> int:
@@ -75,7 +105,7 @@ def fnv1a64(b: bytes) -> int:
 def hash_strings(values, device=None) -> np.ndarray:
     """uint64 FNV-1a fingerprints of a string column (== mifx.transform.api.fingerprint64)."""
     if not _is_gpu(device):
-        return np.array([fnv1a64(_as_str(v).encode()) for v in values], dtype=np.uint64)
+        return np.array([fnv1a64(v.encode()) for v in _host_strs(values)], dtype=np.uint64)
     dev = torch.device(device)
     buf, offs, _ = pack_strings(values)
     n = len(offs) - 1
@@ -89,11 +119,11 @@ def count_unique(values, device=None) -> tuple[list[str], list[int]] | None:
     """Unique tokens and their counts. GPU: hash-table count; returns None on a detected hash
     collision / table overflow (the caller then uses the exact CPU path)."""
     if not _is_gpu(device):
-        vals, counts = np.unique(np.array([_as_str(v) for v in values], dtype=object), return_counts=True)
+        vals, counts = np.unique(np.array(_host_strs(values), dtype=object), return_counts=True)
         return [str(v) for v in vals.tolist()], [int(c) for c in counts.tolist()]
     dev = torch.device(device)
-    buf, offs, enc = pack_strings(values)
-    n = len(enc)
+    buf, offs, get = pack_strings(values)
+    n = len(offs) - 1
     if n == 0:
         return [], []
     cap = _capacity(n)
@@ -110,7 +140,7 @@ def count_unique(values, device=None) -> tuple[list[str], list[int]] | None:
     used = counts > 0
     c = counts[used].cpu().tolist()
     r = rep[used].cpu().tolist()
-    return [enc[i].decode() for i in r], c
+    return [get(i) for i in r], c
 
 
 def order_vocabulary(tokens: list[str], counts: list[int], top_k: int | None = None,
@@ -135,8 +165,7 @@ def _lookup_host(values, vocab: list[str], default_value: int, num_oov_buckets: 
     index = {v: i for i, v in enumerate(vocab)}
     n = len(vocab)
     out = np.empty(len(values), dtype=np.int64)
-    for i, v in enumerate(values):
-        s = _as_str(v)
+    for i, s in enumerate(_host_strs(values)):
         j = index.get(s)
         if j is not None:
             out[i] = j

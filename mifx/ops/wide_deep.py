@@ -15,9 +15,9 @@ def _fns():
     lib = _lib.load("wide_deep")
     return {
         "constants": sig(lib, "mifx_wd_constants", [VP, I32]),
-        "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP]),
-        "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, VP]),
-        "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP, VP]),
+        "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, I32, VP]),
+        "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
     }
 
 
@@ -32,15 +32,31 @@ def constants() -> dict[str, int]:
 
 def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
           wt_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
-          logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool) -> None:
+          logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
+          tmap: torch.Tensor | None = None, stage_dims=None) -> None:
+    """slab: [grid, stride] with stride = slab.shape[1] (compact layout of `tmap`, see
+    models.wide_deep.compact_tile_map). stage_dims: 10 ints (live rows[5], 16-B granules per row[5]) of
+    the weight image to stage (models.wide_deep.stage_dims); None stages the whole padded image."""
+    sd = None
+    if stage_dims is not None:
+        sd = (ctypes.c_int * 10)(*[int(v) for v in stage_dims])
+    stride = int(slab.shape[-1]) if slab is not None else 0
+    if train:
+        if tmap is None or tmap.dtype != torch.int32 or tmap.numel() != constants()["NTILE"]:
+            raise ValueError("training launch needs the int32 tile map of the compact slab layout")
+        if slab.shape[0] < grid or not slab.is_contiguous():
+            raise ValueError("slab must be a contiguous [>= grid, stride] tensor")
     rc = _fns()["fused"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wt_bf16), ptr(wide), ptr(slab),
-                         ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
-                         stream_handle(records.device))
+                         ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train), ptr(tmap), stride,
+                         sd, stream_handle(records.device))
     check(rc, "mifx_wd_fused")
 
 
 def reduce(slab: torch.Tensor, groups: int, nsplit: int, partial: torch.Tensor) -> None:
-    check(_fns()["reduce"](ptr(slab), groups, nsplit, ptr(partial), stream_handle(slab.device)), "mifx_wd_reduce")
+    if partial.shape[-1] != slab.shape[-1] or partial.numel() < nsplit * slab.shape[-1]:
+        raise ValueError("partial must be [>= nsplit, stride] with the slab's stride")
+    check(_fns()["reduce"](ptr(slab), groups, nsplit, ptr(partial), int(slab.shape[-1]), stream_handle(slab.device)),
+          "mifx_wd_reduce")
 
 
 def optimizer(partial: torch.Tensor, nparts: int, gidx: torch.Tensor, mask: torch.Tensor, param: torch.Tensor,
@@ -48,5 +64,6 @@ def optimizer(partial: torch.Tensor, nparts: int, gidx: torch.Tensor, mask: torc
               hyper_dnn: torch.Tensor, hyper_wide: torch.Tensor) -> None:
     # hyper tensors live on the host (read by the launcher, passed by value)
     rc = _fns()["optimizer"](ptr(partial), nparts, ptr(gidx), ptr(mask), ptr(param), ptr(s0), ptr(s1), ptr(wt_out),
-                             ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide), stream_handle(param.device))
+                             ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide), int(partial.shape[-1]),
+                             stream_handle(param.device))
     check(rc, "mifx_wd_optimizer")

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from ..models.bert import BertConfig, BertForSequenceClassification
 from ..parallel import dist as mdist
 from ..parallel.tensor_parallel import TPGroup
+from ..utils.meter import heartbeat
 from .optim import FlatAdamW
 
 
@@ -115,8 +116,11 @@ def main(argv=None):
     tp = TPGroup(torch.distributed.group.WORLD if env.world_size > 1 else None)
     tr = BertTrainer(BertConfig(layers=a.layers), a.batch, a.seq, dev, tp, graph=not a.no_graph,
                      flat_adamw=not a.no_flat_adamw)
-    for _ in range(a.warmup):
-        tr.step()
+    with heartbeat("bert warmup"):
+        for _ in range(a.warmup):
+            tr.step()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     mdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()

@@ -68,6 +68,9 @@ class FusedWideDeepTrainer:
         self.loss_reduction = loss_reduction
         dev = self.device
         gidx, mask = wdm.canonical_index_maps(self.model.cfg)
+        tmap, self.stride = wdm.compact_tile_map(self.model.cfg)
+        self.stage_dims = wdm.stage_dims(self.model.cfg)
+        self.tmap = torch.from_numpy(tmap).to(dev)
         self.gidx = torch.from_numpy(gidx).to(dev)
         self.mask = torch.from_numpy(mask).to(dev)
         self.param = torch.from_numpy(wdm.pack_canonical(self.model)).to(dev)
@@ -79,11 +82,11 @@ class FusedWideDeepTrainer:
                 self.s0[sl] = spec.initial_accumulator_value
         self.wt = self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16).contiguous()
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.slab = torch.empty(self.grid, wdm.STRIDE, device=dev)
+        self.slab = torch.empty(self.grid, self.stride, device=dev)
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
-        self.partial = torch.empty(self.nsplit, wdm.STRIDE, device=dev)
-        self.grad = torch.empty(1, wdm.STRIDE, device=dev)
+        self.partial = torch.empty(self.nsplit, self.stride, device=dev)
+        self.grad = torch.empty(1, self.stride, device=dev)  # the DP all-reduce payload (compact)
         self.h_dnn = self.dnn_opt.encode()
         self.h_wide = self.wide_opt.encode()
         self.records = None
@@ -110,7 +113,8 @@ class FusedWideDeepTrainer:
     def _local_grad(self) -> None:
         """fused fwd/bwd + slab reduction; for world>1 the result lands in `self.grad` (one row)."""
         wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
-                  self.slab_loss, None, self.grad_scale, self.grid, True)
+                  self.slab_loss, None, self.grad_scale, self.grid, True, self.tmap,
+                  self.stage_dims)
         if self.world == 1:
             if self.grid > 1:
                 wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
@@ -187,7 +191,8 @@ class FusedWideDeepTrainer:
     def gradients_once(self) -> np.ndarray:
         """Run fwd/bwd on the current batch WITHOUT updating; return the tile-native gradient."""
         wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
-                  self.slab_loss, None, self.grad_scale, self.grid, True)
+                  self.slab_loss, None, self.grad_scale, self.grid, True, self.tmap,
+                  self.stage_dims)
         if self.grid > 1:
             wdk.reduce(self.slab, self.grid, 1, self.grad)
             return self.grad[0].cpu().numpy()
@@ -199,7 +204,8 @@ class FusedWideDeepTrainer:
         n = records.shape[0]
         out = torch.empty(n, device=self.device)
         grid = min((n + self.T - 1) // self.T, 1024)
-        wdk.fused(records, n, n, 0, None, self.wt, self.param[wdm.WTOT:], None, None, out, 1.0, grid, False)
+        wdk.fused(records, n, n, 0, None, self.wt, self.param[wdm.WTOT:], None, None, out, 1.0, grid, False,
+                  stage_dims=self.stage_dims)
         return out
 
     def sync_to_model(self) -> wdm.WideDeepModel:

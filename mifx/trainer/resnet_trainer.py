@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
 import time
 
 import torch
@@ -17,6 +18,7 @@ from ..models.resnet import resnet50_v2
 from ..ops.image_ops import IMAGENET_MEAN, IMAGENET_STD, crop_flip_normalize
 from ..parallel import dist as mdist
 from ..parallel.ddp import DataParallel
+from ..utils.meter import heartbeat
 
 
 def synthetic_imagenet(n: int, size: int = 256, classes: int = 1000, seed: int = 0, device="cpu"):
@@ -98,8 +100,15 @@ def main(argv=None):
     imgs, labels = synthetic_imagenet(a.images, seed=env.rank, device=dev)
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=pg, warmup_steps=10)
-    for _ in range(a.warmup):
-        tr.step()
+    for i in range(a.warmup):  # first steps include MIOpen solver search/compile: report progress
+        t1 = time.perf_counter()
+        with heartbeat("resnet warmup"):
+            tr.step()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+        if env.rank == 0:
+            print(f"[resnet] warmup step {i + 1}/{a.warmup}: {time.perf_counter() - t1:.2f}s", file=sys.stderr,
+                  flush=True)
     mdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()

@@ -98,24 +98,53 @@ def apply(preprocessing_fn, inputs: dict, state: TransformState, device=None) ->
 
 
 def _materialize(out: dict) -> dict:
-    return {k: np.asarray(v) for k, v in out.items()}
+    return {k: np.asarray(_np(v)) for k, v in out.items()}
 
 
 # ------------------------------------------------------------------------------- helpers
+def _is_arrow(x) -> bool:
+    """A pyarrow (Chunked)Array: string columns may stay in Arrow form (offsets + bytes buffers) so the
+    GPU vocabulary kernels read them without a per-row Python pass."""
+    mod = type(x).__module__
+    return mod.startswith("pyarrow")
+
+
+def _arrow_is_str(x) -> bool:
+    import pyarrow as pa
+
+    return pa.types.is_string(x.type) or pa.types.is_large_string(x.type) or pa.types.is_binary(x.type) \
+        or pa.types.is_large_binary(x.type)
+
+
+def _np(x):
+    return np.array(x.to_pylist(), dtype=object) if _is_arrow(x) else x
+
+
 def _num(x) -> np.ndarray:
-    a = np.asarray(x)
+    a = np.asarray(_np(x))
     if a.dtype == object:
         a = np.array([np.nan if v is None else v for v in a], dtype=np.float64)
     return a.astype(np.float64)
 
 
 def _str(x) -> np.ndarray:
-    a = np.asarray(x, dtype=object)
+    a = np.asarray(_np(x), dtype=object)
     return np.array(["" if v is None else (v.decode() if isinstance(v, bytes) else str(v)) for v in a], dtype=object)
+
+
+def _str_or_arrow(x):
+    """Arrow string columns pass through untouched (GPU paths consume their buffers); else _str."""
+    return x if _is_arrow(x) and _arrow_is_str(x) else _str(x)
 
 
 def fill_in_missing(x, default=None) -> np.ndarray:
     """Densify an optional column (`taxi_utils.py:86-103`): None/NaN -> '' or 0."""
+    if _is_arrow(x):
+        if _arrow_is_str(x):
+            import pyarrow.compute as pc
+
+            return pc.fill_null(x, "" if default is None else default) if x.null_count else x
+        x = _np(x)
     a = np.asarray(x, dtype=object) if not isinstance(x, np.ndarray) else x
     if a.dtype == object:
         is_str = any(isinstance(v, (str, bytes)) for v in a if v is not None)
@@ -178,8 +207,8 @@ def max(x) -> float:  # noqa: A001
 
 
 def size(x) -> int:
-    a = np.asarray(x)
-    return _analyzer("size", {}, lambda: int(a.size))
+    n = len(x) if _is_arrow(x) else int(np.asarray(x).size)
+    return _analyzer("size", {}, lambda: n)
 
 
 def sum(x) -> float:  # noqa: A001
@@ -201,14 +230,16 @@ def quantiles(x, num_buckets: int) -> list[float]:
 
 def vocabulary(x, top_k: int | None = None, frequency_threshold: int | None = None,
                vocab_filename: str | None = None) -> list[str]:
-    s = _str(x)
+    s = _str_or_arrow(x)
 
     def compute():
+        nonlocal s
         dev = _gpu_ctx(len(s))
         if dev is not None:  # HIP hash-table count (csrc/vocab.hip); identical ordering and cut
             from ..ops import vocab as V
 
             return V.vocabulary(s, top_k=top_k, frequency_threshold=frequency_threshold, device=dev)
+        s = _str(s)
         vals, counts = np.unique(s, return_counts=True)
         order = sorted(zip(counts.tolist(), vals.tolist()), reverse=True)
         if frequency_threshold is not None:
@@ -254,13 +285,14 @@ def hash_strings(x, hash_buckets: int) -> np.ndarray:
 
 
 def apply_vocabulary(x, vocab: list[str], default_value: int = -1, num_oov_buckets: int = 0) -> np.ndarray:
-    s = _str(x)
+    s = _str_or_arrow(x)
     dev = _gpu_ctx(len(s))
     if dev is not None:  # device hash-table lookup + FNV OOV buckets (csrc/vocab.hip)
         from ..ops import vocab as V
 
         return V.apply_vocabulary(s, vocab, default_value=default_value, num_oov_buckets=num_oov_buckets, device=dev)
-    index = {v: i for i, v in enumerate(vocab)}
+    s = _str(s)
+    index ={v: i for i, v in enumerate(vocab)}
     n = len(vocab)
     out = np.empty(len(s), dtype=np.int64)
     for i, v in enumerate(s):
@@ -304,7 +336,9 @@ def bucketize(x, num_buckets: int, epsilon: float | None = None) -> np.ndarray:
 
 
 def as_string(x) -> np.ndarray:
-    a = np.asarray(x)
+    if _is_arrow(x) and _arrow_is_str(x):
+        return x
+    a = np.asarray(_np(x))
     return np.array([str(v) for v in a.tolist()], dtype=object)
 
 

@@ -69,3 +69,28 @@ def trace_range(name: str):
             torch.cuda.nvtx.range_pop()
     else:
         yield
+
+
+@contextlib.contextmanager
+def heartbeat(label: str, every_s: float = 30.0, stream=None):
+    """Print `[label] still running (N s)` every `every_s` seconds while the block runs. First
+    training steps can spend minutes inside one call (MIOpen solver search, hipBLASLt tuning, kernel
+    JIT); the heartbeat makes such phases visible to whoever watches the log."""
+    import sys
+    import threading
+
+    out = stream or sys.stderr
+    done = threading.Event()
+    t0 = time.perf_counter()
+
+    def beat():
+        while not done.wait(every_s):
+            print(f"[{label}] still running ({time.perf_counter() - t0:.0f} s)", file=out, flush=True)
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        done.set()
+        th.join(timeout=1.0)

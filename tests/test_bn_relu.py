@@ -110,21 +110,39 @@ def test_fused_add_bn_relu_matches_reference(dtype, tol):
 
 
 @pytest.mark.gpu
-def test_resnet_fused_blocks_match_unfused_reference():
-    """Whole ResNet-50 v2 forward/backward with the fused kernels vs the same weights on the PyTorch
-    reference path (fp32 input, NCHW -> every BN runs F.batch_norm + ReLU)."""
-    from mifx.models.resnet import resnet50_v2
+def test_resnet_fused_blocks_match_fp64_reference():
+    """Pre-activation ResNet (every bottleneck kind: conv shortcut, stride 2, fused residual add) with
+    the fused BN kernels in fp32 vs the same weights in fp64 on the PyTorch path, per-parameter relative
+    Frobenius error of every gradient.
 
-    torch.manual_seed(0)
-    m = resnet50_v2(10).cuda()
-    x = torch.rand(4, 3, 64, 64, device="cuda")
-    ref_out = m(x)  # NCHW fp32: reference path
-    ref_out.sum().backward()
-    gref = {n: p.grad.clone() for n, p in m.named_parameters()}
-    m.zero_grad()
-    m2 = m.to(memory_format=torch.channels_last)
-    out = m2(x.contiguous(memory_format=torch.channels_last))  # fused native path (fp32)
-    out.sum().backward()
-    torch.testing.assert_close(out, ref_out, rtol=2e-3, atol=2e-3)
-    for n, p in m2.named_parameters():
-        torch.testing.assert_close(p.grad, gref[n], rtol=5e-2, atol=5e-3 * (1 + gref[n].abs().max().item()))
+    Conditioning notes (tools/diag/resnet_grad_fp64.py, tools/diag/bn_model_divergence.py on MI355X):
+    (1) the full 16-block net at 64x64 / batch 4 has train-mode BN over as few as 16 samples per
+    channel and its gradients are noise-dominated even for the fp32 PyTorch path (1-3 % vs fp64), so a
+    one-block-per-stage net is used; (2) MIOpen's reduced-precision (xf32) convolution solvers are
+    selected while `allow_tf32` is on (~3e-3 gradient error on both the PyTorch and the fused path), so
+    the check runs with it off. Measured: fused 3.6e-6 vs PyTorch fp32 3.3e-6 global rel. error."""
+    import copy
+
+    from mifx.models.resnet import ResNetV2
+
+    saved = torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        torch.manual_seed(0)
+        m = ResNetV2((1, 1, 1, 1), 10).cuda()
+        x = torch.rand(8, 3, 64, 64, device="cuda")
+        gout = torch.randn(8, 10, device="cuda")
+        m64 = copy.deepcopy(m).double()
+        out64 = m64(x.double())
+        out64.backward(gout.double())
+        mf = copy.deepcopy(m).to(memory_format=torch.channels_last)
+        out = mf(x.contiguous(memory_format=torch.channels_last))  # fused native path (fp32)
+        out.backward(gout)
+    finally:
+        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = saved
+    torch.testing.assert_close(out.double(), out64, rtol=1e-4, atol=1e-4)
+    g64 = dict(m64.named_parameters())
+    for n, p in mf.named_parameters():
+        ref = g64[n].grad
+        rel = ((p.grad.double() - ref).norm() / (ref.norm() + 1e-30)).item()
+        assert rel < 1e-4, f"{n}: relative gradient error {rel:.2e}"

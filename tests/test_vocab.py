@@ -21,10 +21,24 @@ def _column(n=50000, seed=0):
 
 def test_pack_strings_roundtrip():
     col = ["a", "", None, b"xyz", "Ünï"]
-    buf, offs, enc = V.pack_strings(col)
-    assert offs.tolist()[0] == 0 and offs[-1] == sum(len(e) for e in enc)
+    buf, offs, get = V.pack_strings(col)
+    assert offs.tolist()[0] == 0 and offs[-1] == len("axyzÜnï".encode())
     got = [bytes(buf[offs[i]:offs[i + 1]]).decode() for i in range(len(col))]
-    assert got == ["a", "", "", "xyz", "Ünï"]
+    assert got == ["a", "", "", "xyz", "Ünï"] == [get(i) for i in range(len(col))]
+
+
+def test_pack_strings_arrow_zero_copy_matches_list():
+    import pyarrow as pa
+
+    col = ["a", None, "", "xyz", "Ünï"] * 3
+    arr = pa.chunked_array([pa.array(col[:7]), pa.array(col[7:])])
+    buf, offs, get = V.pack_strings(arr)
+    got = [bytes(buf[offs[i]:offs[i + 1]]).decode() for i in range(len(col))]
+    assert got == [c or "" for c in col] == [get(i) for i in range(len(col))]
+    sl = pa.array(col).slice(3, 5)  # non-zero Arrow offset
+    buf, offs, get = V.pack_strings(sl)
+    assert [bytes(buf[offs[i]:offs[i + 1]]).decode() for i in range(5)] == [c or "" for c in col[3:8]]
+    assert V.vocabulary(arr, device=None) == V.vocabulary(col, device=None)
 
 
 def test_fnv_matches_transform_fingerprint():
@@ -92,3 +106,15 @@ def test_transform_api_uses_gpu_vocab_path(monkeypatch):
     assert any(d is not None for d in calls)
     assert st_gpu.entries == st_cpu.entries
     assert np.array_equal(out_gpu["c"], out_cpu["c"])
+
+
+@pytest.mark.gpu
+def test_gpu_arrow_column_matches_host():
+    import pyarrow as pa
+
+    col = [v.decode() if isinstance(v, bytes) else v for v in _column(100000, seed=5)]
+    arr = pa.chunked_array([pa.array(col[:40000]), pa.array(col[40000:])])
+    vocab = V.vocabulary(arr, top_k=1000, device="cuda")
+    assert vocab == V.vocabulary(col, top_k=1000, device=None)
+    got = V.apply_vocabulary(arr, vocab, default_value=-1, num_oov_buckets=10, device="cuda")
+    assert np.array_equal(got, tft.apply_vocabulary(col, vocab, default_value=-1, num_oov_buckets=10))

@@ -53,8 +53,17 @@ def test_pack_roundtrip_and_forward():
 
 def test_index_maps_are_bijective_on_slab():
     gidx, mask = wdm.canonical_index_maps()
-    assert len(np.unique(gidx)) == len(gidx)
-    assert gidx.max() < wdm.STRIDE
+    tmap, stride = wdm.compact_tile_map()
+    live = gidx[mask.astype(bool)]
+    assert len(np.unique(live)) == len(live)  # every trainable entry has its own compact slot
+    assert live.max() < stride <= wdm.STRIDE and stride % 4 == 0
+    assert (tmap >= 0).sum() == 72 and sorted(tmap[tmap >= 0]) == list(range(72))
+    # every trainable entry's tile is live; dead tiles hold padding only
+    for li, ((K, N), m) in enumerate(zip(wdm.LAYER_KN, wdm._trainable_masks(wdm.WideDeepConfig()))):
+        for nt in range(N // 16):
+            for kt in range(K // 16):
+                t = wdm.TILE_BASE[li] + nt * (K // 16) + kt
+                assert (tmap[t] >= 0) == bool(m[16 * nt:16 * nt + 16, 16 * kt:16 * kt + 16].any())
     # trainable = real weights + biases: 3*100+100 + 100*70+70 + 70*48+48 + 48*34+34 + 34+1 + 2128
     assert mask.sum() == 400 + 7070 + 3408 + 1666 + 35 + 2128
 
@@ -252,3 +261,22 @@ def test_fused_training_is_run_to_run_deterministic():
         params.append(tr.param.clone())
     diff = (params[0] - params[1]).abs().max().item()
     assert torch.equal(params[0], params[1]), f"max |diff| {diff}"
+
+
+def test_stage_dims_cover_every_nonzero_weight():
+    """The fused kernel stages only the live rows/granules of the bf16 weight image into LDS and
+    zero-fills the rest: every non-zero entry of the packed image must lie inside the staged part."""
+    m = wdm.WideDeepModel(seed=3)
+    with torch.no_grad():
+        for lin in list(m.dnn) + [m.head]:
+            lin.bias.normal_()
+    vec = wdm.pack_canonical(m)
+    sd = wdm.stage_dims(m.cfg)
+    rows, gpr = sd[:5], sd[5:]
+    for li, (K, N) in enumerate(wdm.LAYER_KN):
+        img = vec[wdm.LAYER_OFF[li]:wdm.LAYER_OFF[li] + K * N].reshape(N, K)
+        n, k = np.nonzero(img)
+        assert n.max() < rows[li] and k.max() < 8 * gpr[li], li
+        staged = np.zeros_like(img)
+        staged[:rows[li], :8 * gpr[li]] = img[:rows[li], :8 * gpr[li]]
+        assert np.array_equal(staged, img)

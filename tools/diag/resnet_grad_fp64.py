@@ -24,7 +24,10 @@ def rel_fro(a, b):
 
 def main():
     native_ok = bnr.native_ok
-    for layers, hw, bs in (((3, 4, 6, 3), 64, 4), ((1, 1, 1, 1), 64, 8), ((3, 4, 6, 3), 128, 8)):
+    cases = [((1, 1, 1, 1), 64, 8, True), ((1, 1, 1, 1), 64, 8, False), ((3, 4, 6, 3), 64, 4, False)]
+    for layers, hw, bs, tf32 in cases:
+        torch.backends.cudnn.allow_tf32 = tf32
+        torch.backends.cuda.matmul.allow_tf32 = tf32
         torch.manual_seed(0)
         m = ResNetV2(layers, 10).cuda()
         x = torch.rand(bs, 3, hw, hw, device="cuda")
@@ -41,7 +44,7 @@ def main():
         rows = [(rel_fro(gf[n], g64[n]), rel_fro(gl[n], g64[n]), rel_fro(g32[n], g64[n]), n) for n in g64]
         rows.sort(reverse=True)
         cat = lambda g: torch.cat([v.flatten() for v in g.values()])  # noqa: E731
-        print(f"layers={layers} hw={hw} bs={bs}: out err nchw32={(o32 - o64).abs().max().item():.2e} "
+        print(f"layers={layers} hw={hw} bs={bs} allow_tf32={tf32}: out err nchw32={(o32 - o64).abs().max().item():.2e} "
               f"nhwc32={(ol - o64).abs().max().item():.2e} fused={(of - o64).abs().max().item():.2e}")
         print(f"   global rel-fro: fused {rel_fro(cat(gf), cat(g64)):.2e}  nhwc32 {rel_fro(cat(gl), cat(g64)):.2e}  "
               f"nchw32 {rel_fro(cat(g32), cat(g64)):.2e}")
