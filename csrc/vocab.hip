@@ -8,10 +8,10 @@
 // Strings arrive as one packed byte buffer + int64 offsets (n+1). Design:
 //  * str_hash: one lane per string, 64-bit FNV-1a over its bytes (identical to the host
 //    `mifx.transform.api.fingerprint64`, so OOV buckets agree with the CPU path bit-for-bit).
-//  * vocab_count: open-addressing hash table in global memory (power-of-two capacity, linear
-//    probing). Keys are inserted with a 64-bit atomicCAS; occurrences counted with atomicAdd;
-//    each slot keeps the smallest row index that produced it (atomicMin) as its representative,
-//    so the result is independent of scheduling.
+//  * vocab_count_lds: open-addressing hash table in global memory (power-of-two capacity, linear
+//    probing), fed by per-block LDS pre-aggregation. Keys are inserted with a 64-bit atomicCAS;
+//    occurrences counted with atomicAdd; each slot keeps the smallest row index that produced it
+//    (atomicMin) as its representative, so the result is independent of scheduling.
 //  * vocab_verify: every row compares its bytes with its slot's representative; a genuine 64-bit
 //    hash collision between distinct strings raises a flag and the host redoes the column on the
 //    exact CPU path. (The host sorts the few unique (count, token) pairs: frequency desc, token desc.)
@@ -58,26 +58,62 @@ __global__ __launch_bounds__(256) void str_hash(const uint8_t* __restrict__ buf,
   }
 }
 
-__global__ __launch_bounds__(256) void vocab_count(const unsigned long long* __restrict__ hash, long long n,
-                                                   unsigned long long* __restrict__ keys,
-                                                   unsigned int* __restrict__ counts, int* __restrict__ rep,
-                                                   unsigned int mask, int* __restrict__ overflow) {
+// Zipf-distributed columns (a few tokens carry most rows) make one global counter per hot token a
+// serialisation point: 1M rows spent 3 ms in vocab_count (profiles/analyzers_kernels_s2.md). Each
+// block therefore pre-aggregates its rows in an LDS hash table (count + smallest row per key, LDS
+// atomics) and flushes one global insert per distinct key it saw; rows whose key finds no LDS slot
+// within kLdsProbe probes go straight to the global table.
+constexpr int kLdsSlots = 2048;
+constexpr int kLdsProbe = 32;
+
+__device__ __forceinline__ void global_insert(unsigned long long k, unsigned int cnt, int row,
+                                              unsigned long long* keys, unsigned int* counts, int* rep,
+                                              unsigned int mask, int* overflow) {
+  unsigned int s = slot0(k, mask);
+  for (unsigned int probe = 0; probe <= mask; ++probe) {
+    const unsigned long long prev = atomicCAS(&keys[s], kEmpty, k);
+    if (prev == kEmpty || prev == k) {
+      atomicAdd(&counts[s], cnt);
+      atomicMin(&rep[s], row);
+      return;
+    }
+    s = (s + 1) & mask;
+  }
+  atomicOr(overflow, 1);
+}
+
+__global__ __launch_bounds__(256) void vocab_count_lds(const unsigned long long* __restrict__ hash, long long n,
+                                                       unsigned long long* __restrict__ keys,
+                                                       unsigned int* __restrict__ counts, int* __restrict__ rep,
+                                                       unsigned int mask, int* __restrict__ overflow) {
+  __shared__ unsigned long long lk[kLdsSlots];
+  __shared__ unsigned int lc[kLdsSlots];
+  __shared__ int lr[kLdsSlots];
+  for (int s = threadIdx.x; s < kLdsSlots; s += 256) {
+    lk[s] = kEmpty;
+    lc[s] = 0u;
+    lr[s] = 0x7fffffff;
+  }
+  __syncthreads();
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const unsigned long long k = as_key(hash[i]);
-    unsigned int s = slot0(k, mask);
+    unsigned int s = slot0(k, kLdsSlots - 1);
     bool done = false;
-    for (unsigned int probe = 0; probe <= mask; ++probe) {
-      const unsigned long long prev = atomicCAS(&keys[s], kEmpty, k);
+    for (int probe = 0; probe < kLdsProbe; ++probe) {
+      const unsigned long long prev = atomicCAS(&lk[s], kEmpty, k);
       if (prev == kEmpty || prev == k) {
-        atomicAdd(&counts[s], 1u);
-        atomicMin(&rep[s], (int)i);
+        atomicAdd(&lc[s], 1u);
+        if (lr[s] > (int)i) atomicMin(&lr[s], (int)i);  // racy pre-check only skips useless atomics
         done = true;
         break;
       }
-      s = (s + 1) & mask;
+      s = (s + 1) & (kLdsSlots - 1);
     }
-    if (!done) atomicOr(overflow, 1);
+    if (!done) global_insert(k, 1u, (int)i, keys, counts, rep, mask, overflow);
   }
+  __syncthreads();
+  for (int s = threadIdx.x; s < kLdsSlots; s += 256)
+    if (lc[s] != 0u) global_insert(lk[s], lc[s], lr[s], keys, counts, rep, mask, overflow);
 }
 
 __device__ __forceinline__ int find_slot(const unsigned long long* keys, unsigned long long k, unsigned int mask) {
@@ -182,7 +218,10 @@ int mifx_vocab_count(const uint8_t* buf, const long long* offs, long long n, uns
   if (n == 0) return 0;
   const int g = grid_for(n);
   hipLaunchKernelGGL(str_hash, dim3(g), dim3(256), 0, st, buf, offs, n, hash);
-  hipLaunchKernelGGL(vocab_count, dim3(g), dim3(256), 0, st, hash, n, keys, counts, rep, mask, flags);
+  // ~2K rows per block for the LDS pre-aggregation (flush cost is per block), at least one block per CU
+  const long long cb = (n + 2047) / 2048;
+  const int gc = (int)(cb < 256 ? 256 : (cb > 4096 ? 4096 : cb));
+  hipLaunchKernelGGL(vocab_count_lds, dim3(gc), dim3(256), 0, st, hash, n, keys, counts, rep, mask, flags);
   hipLaunchKernelGGL(vocab_verify, dim3(g), dim3(256), 0, st, buf, offs, hash, n, keys, rep, mask, flags + 1);
   return (int)hipGetLastError();
 }

@@ -168,13 +168,15 @@ def _trainable_masks(cfg: WideDeepConfig) -> list[np.ndarray]:
     return out
 
 
-def compact_tile_map(cfg: WideDeepConfig | None = None) -> tuple[np.ndarray, int]:
+def compact_tile_map(cfg: WideDeepConfig | None = None, compact: bool = True) -> tuple[np.ndarray, int]:
     """(tmap int32 [NTILE], stride): tile -> position in the compact gradient slab, -1 for 16x16 dW tiles
     that hold only padding. The kernel skips those tiles when it writes its slab, so the slab write,
     the slab reduction and the DP all-reduce move ~1/3 fewer bytes (72 of 108 tiles are live for the
     taxi [100, 70, 48, 34] tower)."""
     cfg = cfg or WideDeepConfig()
     check_fused_compatible(cfg)
+    if not compact:  # every tile stored (the full padded slab)
+        return np.arange(NTILE, dtype=np.int32), STRIDE
     tmap = np.full(NTILE, -1, np.int32)
     c = 0
     for li, ((K, N), m) in enumerate(zip(LAYER_KN, _trainable_masks(cfg))):
@@ -198,14 +200,14 @@ def stage_dims(cfg: WideDeepConfig | None = None) -> list[int]:
     return rows + gpr
 
 
-def canonical_index_maps(cfg: WideDeepConfig | None = None):
+def canonical_index_maps(cfg: WideDeepConfig | None = None, compact: bool = True):
     """Return (gidx int32 [WTOT+NWIDE], mask uint8 [WTOT+NWIDE]).
 
     gidx maps each canonical parameter to its position in the kernel's compact tile-native gradient
     slab (see compact_tile_map); mask marks trainable entries (real weights + folded biases). Entries
     of dead tiles are never trainable (gidx 0, mask 0)."""
     cfg = cfg or WideDeepConfig()
-    tmap, stride = compact_tile_map(cfg)
+    tmap, stride = compact_tile_map(cfg, compact)
     gidx = np.zeros(WTOT + NWIDE, np.int32)
     mask = np.zeros(WTOT + NWIDE, np.uint8)
     for li, ((K, N), m) in enumerate(zip(LAYER_KN, _trainable_masks(cfg))):

@@ -7,6 +7,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 
 import torch
@@ -103,7 +104,10 @@ def main(argv=None):
     ap.add_argument("--tunable", default=None, metavar="CSV",
                     help="enable PyTorch TunableOp: benchmark hipBLASLt/rocBLAS solutions per GEMM shape during "
                          "warmup and keep the best (results cached in CSV)")
+    ap.add_argument("--seed", type=int, default=None, help="torch.manual_seed before building the trainer")
     a = ap.parse_args(argv)
+    if a.seed is not None:
+        torch.manual_seed(a.seed)
     if a.tunable and torch.cuda.is_available():
         torch.cuda.tunable.enable(True)
         torch.cuda.tunable.tuning_enable(True)
@@ -124,9 +128,12 @@ def main(argv=None):
     mdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    trace = os.environ.get("MIFX_BERT_TRACE") == "1"  # diagnostic: per-step loss (adds a sync per step)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         loss = tr.step()
+        if trace and env.rank == 0:
+            print(f"[bert] step {i} loss {float(loss):.5f}", file=sys.stderr, flush=True)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     mdist.barrier()

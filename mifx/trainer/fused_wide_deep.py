@@ -51,7 +51,8 @@ def default_wide_opt(num_linear_columns: int = 9) -> OptSpec:
 class FusedWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
-                 grid: int | None = None, process_group=None, max_grid: int = 256):
+                 grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
+                 live_staging: bool = True):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
@@ -67,9 +68,11 @@ class FusedWideDeepTrainer:
         self.wide_opt = wide_opt or default_wide_opt(len(self.model.cfg.wide))
         self.loss_reduction = loss_reduction
         dev = self.device
-        gidx, mask = wdm.canonical_index_maps(self.model.cfg)
-        tmap, self.stride = wdm.compact_tile_map(self.model.cfg)
-        self.stage_dims = wdm.stage_dims(self.model.cfg)
+        # compact_slab: store/reduce/all-reduce only the dW tiles that hold trainable entries;
+        # live_staging: stage only the live rows/granules of the weight image into LDS
+        gidx, mask = wdm.canonical_index_maps(self.model.cfg, compact_slab)
+        tmap, self.stride = wdm.compact_tile_map(self.model.cfg, compact_slab)
+        self.stage_dims = wdm.stage_dims(self.model.cfg) if live_staging else None
         self.tmap = torch.from_numpy(tmap).to(dev)
         self.gidx = torch.from_numpy(gidx).to(dev)
         self.mask = torch.from_numpy(mask).to(dev)

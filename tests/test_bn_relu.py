@@ -3,6 +3,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+import mifx.ops.bn_relu as bnr
 from mifx.ops.bn_relu import BatchNormReLU2d, bn_relu
 
 
@@ -115,6 +116,10 @@ def test_resnet_fused_blocks_match_fp64_reference():
     the fused BN kernels in fp32 vs the same weights in fp64 on the PyTorch path, per-parameter relative
     Frobenius error of every gradient.
 
+    The tight check is against the same network with PyTorch BN + ReLU on the same NHWC convolutions
+    (run first, so both use the same MIOpen solvers); fp64 is a loose sanity bound, because MIOpen's
+    solver choice for a first-seen fp32 NHWC problem can be a reduced-precision one (measured 3e-3 on
+    the stem's weight gradient when the fused model ran first).
     Conditioning notes (tools/diag/resnet_grad_fp64.py, tools/diag/bn_model_divergence.py on MI355X):
     (1) the full 16-block net at 64x64 / batch 4 has train-mode BN over as few as 16 samples per
     channel and its gradients are noise-dominated even for the fp32 PyTorch path (1-3 % vs fp64), so a
@@ -131,18 +136,30 @@ def test_resnet_fused_blocks_match_fp64_reference():
         torch.manual_seed(0)
         m = ResNetV2((1, 1, 1, 1), 10).cuda()
         x = torch.rand(8, 3, 64, 64, device="cuda")
+        xl = x.contiguous(memory_format=torch.channels_last)
         gout = torch.randn(8, 10, device="cuda")
         m64 = copy.deepcopy(m).double()
         out64 = m64(x.double())
         out64.backward(gout.double())
+        # same NHWC convolutions (same MIOpen solvers, chosen on this first run), PyTorch BN + ReLU
+        mr = copy.deepcopy(m).to(memory_format=torch.channels_last)
+        real_ok = bnr.native_ok
+        bnr.native_ok = lambda t: False
+        try:
+            out_r = mr(xl)
+            out_r.backward(gout)
+        finally:
+            bnr.native_ok = real_ok
         mf = copy.deepcopy(m).to(memory_format=torch.channels_last)
-        out = mf(x.contiguous(memory_format=torch.channels_last))  # fused native path (fp32)
+        out = mf(xl)  # fused native path (fp32)
         out.backward(gout)
     finally:
         torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = saved
     torch.testing.assert_close(out.double(), out64, rtol=1e-4, atol=1e-4)
-    g64 = dict(m64.named_parameters())
+    g64, gr = dict(m64.named_parameters()), dict(mr.named_parameters())
     for n, p in mf.named_parameters():
-        ref = g64[n].grad
+        ref = gr[n].grad.double()
         rel = ((p.grad.double() - ref).norm() / (ref.norm() + 1e-30)).item()
-        assert rel < 1e-4, f"{n}: relative gradient error {rel:.2e}"
+        assert rel < 1e-4, f"{n}: fused vs PyTorch-BN relative gradient error {rel:.2e}"
+        rel64 = ((p.grad.double() - g64[n].grad).norm() / (g64[n].grad.norm() + 1e-30)).item()
+        assert rel64 < 1e-2, f"{n}: fused vs fp64 relative gradient error {rel64:.2e}"
