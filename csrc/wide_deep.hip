@@ -335,11 +335,24 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   if (blockIdx.x == 0 && lane == 0) g_stamps[w][0] = __builtin_amdgcn_s_memtime();
 #endif
 
-  // Stage the LIVE part of the bf16 weight image: per layer the rows that hold real weights (plus the
-  // constant-1 producer row) and the 16-byte granules up to the last real column -- 1715 of the 3456
-  // granules for the taxi tower, so the every-CU-at-once prologue burst moves half the bytes. The rest
-  // of the weight region is zero-filled in LDS while the global loads are in flight.
-  {
+  if (sd.total == WTOT / 8) {
+    // stage the whole padded bf16 weight image: issue all global loads, then all LDS stores
+    constexpr int NCH = WTOT / 8, PER = (NCH + NTHR - 1) / NTHR;
+    uint4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = *(const uint4*)(wt + min(tid + i * NTHR, NCH - 1) * 8);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NTHR;
+      if (c < NCH) *(uint4*)(lds + wt_lds_offset(c * 8)) = v[i];
+    }
+  } else {
+    // Stage only the LIVE part of the image: per layer the rows that hold real weights (plus the
+    // constant-1 producer row) and the 16-byte granules up to the last real column (1715 of the 3456
+    // granules for the taxi tower); the rest of the weight region is zero-filled in LDS while the
+    // global loads are in flight. (rocprof: same kernel time as the full image at B=65536 and 2.8 us
+    // slower for the single-workgroup B=40 step -- the prologue is latency-, not byte-bound -- so the
+    // trainer stages the full image by default.)
     constexpr int PER = (WTOT / 8 + NTHR - 1) / NTHR;  // bound: every granule live
     uint4 v[PER];
     int dst[PER];

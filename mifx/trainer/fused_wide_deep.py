@@ -52,7 +52,7 @@ class FusedWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
-                 live_staging: bool = True):
+                 live_staging: bool = False):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)

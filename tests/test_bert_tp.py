@@ -129,9 +129,24 @@ def test_bert_hipgraph_step_matches_eager():
     from mifx.trainer.bert_trainer import BertTrainer
 
     cfg = BertConfig(layers=2, dropout=0.0)
-    eager = BertTrainer(cfg, 8, 64, "cuda", graph=False)
+    eager = BertTrainer(cfg, 8, 64, "cuda", graph=False, flat_adamw=False)  # same optimizer as graph mode
     graphed = BertTrainer(cfg, 8, 64, "cuda", graph=True)
     le = [float(eager.step()) for _ in range(6)]
     lg = [float(graphed.step()) for _ in range(3)]  # capture runs 3 eager warmup steps first
     assert graphed.graph is not None
     np.testing.assert_allclose(lg, le[3:], rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_bert_trainer_main_default_config_stays_finite(capsys):
+    """Regression: the default 12-layer B=32 S=128 configuration of bert_trainer.main must keep a finite
+    loss over its timed steps (the hipGraph-replayed step went NaN after ~10 updates; eager is default)."""
+    import json
+
+    from mifx.trainer.bert_trainer import main
+
+    main(["--steps", "15", "--warmup", "5"])
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["hipgraph"] is False
+    assert np.isfinite(out["loss"]), out
+    assert out["value"] > 0
