@@ -635,13 +635,23 @@ __device__ __forceinline__ float opt_update(const OptHyper& hp, float w, float g
   return w - hp.lr * (a0 / bc1) / (sqrtf(a1 / bc2) + hp.eps);
 }
 
+// Step counters: the optimizer step is needed by every workgroup (Adam bias correction) and the next fused
+// launch derives its data offset from it. A single counter bumped by one workgroup races with the others'
+// reads, and a last-workgroup-done atomic costs an agent-scope fence (L2 writeback) per workgroup, so each
+// workgroup owns a slot: step_ctr[blockIdx.x] is read and bumped by that workgroup only; slot 0 is the
+// canonical step the fused kernel reads. All STEP_SLOTS slots start equal (host set_step).
+constexpr int STEP_SLOTS = 512;
+
 // One thread per canonical parameter. DNN segment [0, WTOT) then wide segment [WTOT, WTOT+NWIDE).
 __global__ __launch_bounds__(256) void wd_optimizer(
     const float* __restrict__ partial, int nparts, const int* __restrict__ gidx, const uint8_t* __restrict__ mask,
     float* __restrict__ param, float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
     long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw, int stride) {
   const int c = blockIdx.x * 256 + threadIdx.x;
-  const long long step = step_ctr[0] + 1;
+  __shared__ long long s_step;
+  if (threadIdx.x == 0) s_step = step_ctr[blockIdx.x] + 1;  // the slot's only reader and writer: thread 0
+  __syncthreads();
+  const long long step = s_step;
   if (c < WTOT + NWIDE) {
     const bool dnn = c < WTOT;
     float w = param[c];
@@ -663,7 +673,88 @@ __global__ __launch_bounds__(256) void wd_optimizer(
     }
     if (dnn) wt_out[c] = __builtin_bit_cast(uint16_t, (bf16)w);
   }
-  if (c == 0) step_ctr[0] = step;
+  if (threadIdx.x == 0) step_ctr[blockIdx.x] = step;
+}
+
+// Fused slab reduction + optimizer: one workgroup owns RQ float4 columns (4*RQ gradient entries) of the
+// compact slab and sums ALL G rows of them (row groups of 256/RQ threads, fixed order -> deterministic), so
+// the full per-column gradient is available in one workgroup and the optimizer runs right there through
+// the inverse map inv[slab column] -> canonical parameter (-1 = padding). Replaces wd_reduce + wd_optimizer
+// (two launches, a [nsplit, stride] round trip) on the single-rank step; with OPT=false it is the local
+// full reduction feeding the DP all-reduce.
+constexpr int RQ = 16;               // float4 columns per workgroup
+constexpr int RG = 256 / RQ;         // row groups
+constexpr int RU = 8;                // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
+                                     // 8 x 16 B = the whole 21 MB slab requested in two rounds)
+template <bool OPT>
+__global__ __launch_bounds__(256) void wd_reduce_opt(
+    const float4* __restrict__ slab, int G, int stride, float4* __restrict__ out, const int* __restrict__ inv,
+    float* __restrict__ param, float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
+    long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+  __shared__ float4 part[RG][RQ];
+  __shared__ float gsum[4 * RQ];
+  __shared__ long long s_step;
+  if (OPT && threadIdx.x == 0) s_step = step_ctr[blockIdx.x] + 1;  // slot read and written by thread 0 only
+  const int S4 = stride / 4;
+  const int lq = threadIdx.x % RQ, r = threadIdx.x / RQ;
+  const int q = blockIdx.x * RQ + lq;
+  float4 acc[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) acc[u] = make_float4(0, 0, 0, 0);
+  if (q < S4) {
+    int g = r;
+    for (; g + (RU - 1) * RG < G; g += RU * RG) {
+      float4 v[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) v[u] = slab[(size_t)(g + u * RG) * S4 + q];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
+    }
+    for (; g < G; g += RG) {
+      const float4 v = slab[(size_t)g * S4 + q];
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+  }
+#pragma unroll
+  for (int h = RU / 2; h >= 1; h /= 2)
+#pragma unroll
+    for (int u = 0; u < h; ++u) {
+      acc[u].x += acc[u + h].x; acc[u].y += acc[u + h].y; acc[u].z += acc[u + h].z; acc[u].w += acc[u + h].w;
+    }
+  part[r][lq] = acc[0];
+  __syncthreads();
+  if (threadIdx.x < RQ) {
+    float4 s = part[0][lq];
+#pragma unroll
+    for (int k = 1; k < RG; ++k) {
+      const float4 v = part[k][lq];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (!OPT) {
+      if (q < S4) out[q] = s;
+    } else {
+      gsum[4 * lq + 0] = s.x; gsum[4 * lq + 1] = s.y; gsum[4 * lq + 2] = s.z; gsum[4 * lq + 3] = s.w;
+    }
+  }
+  if (!OPT) return;
+  __syncthreads();
+  const long long step = s_step;
+  if (threadIdx.x < 4 * RQ) {
+    const int gi = blockIdx.x * 4 * RQ + threadIdx.x;
+    const int c = gi < stride ? inv[gi] : -1;
+    if (c >= 0) {
+      const bool dnn = c < WTOT;
+      float a0 = s0[c], a1 = s1[c];
+      const float w = opt_update(dnn ? hd : hw, param[c], gsum[threadIdx.x], a0, a1, step);
+      s0[c] = a0;
+      s1[c] = a1;
+      param[c] = w;
+      if (dnn) wt_out[c] = __builtin_bit_cast(uint16_t, (bf16)w);
+    }
+  }
+  if (threadIdx.x == 0) step_ctr[blockIdx.x] = step;
 }
 
 }  // namespace
@@ -727,8 +818,33 @@ int mifx_wd_optimizer(const float* partial, int nparts, const int* gidx, const u
   OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
               hyper_wide[6], hyper_wide[7]};
   const int n = WTOT + NWIDE;
+  static_assert((WTOT + NWIDE + 255) / 256 <= STEP_SLOTS, "optimizer grid exceeds the step slots");
   hipLaunchKernelGGL(wd_optimizer, dim3((n + 255) / 256), dim3(256), 0, stream, partial, nparts, gidx, mask, param, s0,
                      s1, (uint16_t*)wt_out, step_ctr, hd, hw, stride);
+  return (int)hipGetLastError();
+}
+
+// slab [G, stride] -> full sum; with inv != null the optimizer is applied in the same launch (out unused),
+// otherwise the sum is written to out [stride]. step_ctr must hold STEP_SLOTS int64 (per-workgroup step slots).
+int mifx_wd_reduce_opt(const float* slab, int G, int stride, float* out, const int* inv, float* param, float* s0,
+                       float* s1, void* wt_out, long long* step_ctr, const float* hyper_dnn,
+                       const float* hyper_wide, hipStream_t stream) {
+  if (G <= 0 || stride <= 0 || stride > STRIDE || stride % 4 != 0) return -1;
+  const dim3 grid((stride / 4 + RQ - 1) / RQ);
+  if (grid.x > STEP_SLOTS) return -1;
+  if (inv == nullptr) {
+    if (out == nullptr) return -1;
+    hipLaunchKernelGGL(wd_reduce_opt<false>, grid, dim3(256), 0, stream, (const float4*)slab, G, stride,
+                       (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{}, OptHyper{});
+    return (int)hipGetLastError();
+  }
+  if (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr || step_ctr == nullptr) return -1;
+  OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5], hyper_dnn[6],
+              hyper_dnn[7]};
+  OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+              hyper_wide[6], hyper_wide[7]};
+  hipLaunchKernelGGL(wd_reduce_opt<true>, grid, dim3(256), 0, stream, (const float4*)slab, G, stride, nullptr, inv,
+                     param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ def _fns():
         "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP, VP]),
         "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, I32, VP]),
         "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
+        "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -59,10 +60,46 @@ def reduce(slab: torch.Tensor, groups: int, nsplit: int, partial: torch.Tensor) 
           "mifx_wd_reduce")
 
 
+STEP_SLOTS = 512  # csrc/wide_deep.hip: one step slot per optimizer workgroup, slot 0 = canonical step
+
+
+def _check_step_ctr(step_ctr: torch.Tensor) -> None:
+    if step_ctr.dtype != torch.int64 or step_ctr.numel() < STEP_SLOTS or not step_ctr.is_contiguous():
+        raise ValueError(f"step_ctr must be a contiguous int64 tensor of {STEP_SLOTS} per-workgroup step slots")
+
+
+def reduce_full(slab: torch.Tensor, groups: int, out: torch.Tensor) -> None:
+    """out[stride] = sum of the first `groups` slab rows (one launch, fixed summation order)."""
+    stride = int(slab.shape[-1])
+    if out.numel() < stride or slab.numel() < groups * stride or not slab.is_contiguous():
+        raise ValueError("slab must be contiguous [>= groups, stride] and out hold >= stride floats")
+    rc = _fns()["reduce_opt"](ptr(slab), int(groups), stride, ptr(out), None, None, None, None, None, None, None,
+                              None, stream_handle(slab.device))
+    check(rc, "mifx_wd_reduce_opt")
+
+
+def reduce_apply(slab: torch.Tensor, groups: int, inv: torch.Tensor, param: torch.Tensor, s0: torch.Tensor,
+                 s1: torch.Tensor, wt_out: torch.Tensor, step_ctr: torch.Tensor, hyper_dnn: torch.Tensor,
+                 hyper_wide: torch.Tensor) -> None:
+    """Sum the first `groups` slab rows and apply the optimizer in the same launch. inv: int32 [stride]
+    slab column -> canonical parameter index (-1 for padding), see FusedWideDeepTrainer."""
+    stride = int(slab.shape[-1])
+    if inv.dtype != torch.int32 or inv.numel() != stride:
+        raise ValueError("inv must be int32 [stride]")
+    if slab.numel() < groups * stride or not slab.is_contiguous():
+        raise ValueError("slab must be contiguous [>= groups, stride]")
+    _check_step_ctr(step_ctr)
+    rc = _fns()["reduce_opt"](ptr(slab), int(groups), stride, None, ptr(inv), ptr(param), ptr(s0), ptr(s1),
+                              ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
+                              stream_handle(param.device))
+    check(rc, "mifx_wd_reduce_opt")
+
+
 def optimizer(partial: torch.Tensor, nparts: int, gidx: torch.Tensor, mask: torch.Tensor, param: torch.Tensor,
               s0: torch.Tensor, s1: torch.Tensor, wt_out: torch.Tensor, step_ctr: torch.Tensor,
               hyper_dnn: torch.Tensor, hyper_wide: torch.Tensor) -> None:
     # hyper tensors live on the host (read by the launcher, passed by value)
+    _check_step_ctr(step_ctr)
     rc = _fns()["optimizer"](ptr(partial), nparts, ptr(gidx), ptr(mask), ptr(param), ptr(s0), ptr(s1), ptr(wt_out),
                              ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide), int(partial.shape[-1]),
                              stream_handle(param.device))

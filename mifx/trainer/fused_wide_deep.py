@@ -1,8 +1,10 @@
 """Device-resident, hipGraph-captured Wide&Deep trainer on the fused gfx950 kernels.
 
 One training step = ``wd_fused`` (forward + loss + backward, per-workgroup gradient slabs)
--> ``wd_reduce`` (slab sum) -> [RCCL all-reduce of ONE flat 119 KB gradient bucket over xGMI
-when data-parallel] -> ``wd_optimizer`` (Adagrad/FTRL/Adam/SGD + bf16 weight image). The input
+-> ``wd_reduce_opt`` (full slab sum + Adagrad/FTRL/Adam/SGD + bf16 weight image in ONE launch). When
+data-parallel the local sum is written to ONE flat 82 KB gradient bucket, RCCL all-reduced over xGMI,
+and the optimizer launch reads that bucket. (The older two-launch ``wd_reduce`` -> ``wd_optimizer``
+path stays selectable with ``fused_update=False`` for A/B.) The input
 shard lives in HBM; the data offset advances through a device-side step counter, so the whole
 step (collective included) can be captured once and replayed as a hipGraph.
 
@@ -52,7 +54,7 @@ class FusedWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
-                 live_staging: bool = False):
+                 live_staging: bool = False, fused_update: bool = True):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
@@ -84,7 +86,14 @@ class FusedWideDeepTrainer:
             if spec.kind in ("adagrad", "ftrl"):
                 self.s0[sl] = spec.initial_accumulator_value
         self.wt = self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16).contiguous()
-        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        # inverse of the (bijective on live entries) canonical -> slab-column map, -1 on padding columns
+        inv = np.full(self.stride, -1, dtype=np.int32)
+        live = np.nonzero(mask)[0]
+        inv[gidx[live]] = live.astype(np.int32)
+        self.inv = torch.from_numpy(inv).to(dev)
+        self.fused_update = bool(fused_update)
+        # per-optimizer-workgroup step slots (slot 0 = the step; see csrc/wide_deep.hip STEP_SLOTS)
+        self.step_ctr = torch.zeros(wdk.STEP_SLOTS, dtype=torch.int64, device=dev)
         self.slab = torch.empty(self.grid, self.stride, device=dev)
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
@@ -118,7 +127,10 @@ class FusedWideDeepTrainer:
         wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
                   self.slab_loss, None, self.grad_scale, self.grid, True, self.tmap,
                   self.stage_dims)
-        if self.world == 1:
+        if self.fused_update:
+            if self.world > 1:
+                wdk.reduce_full(self.slab, self.grid, self.grad)
+        elif self.world == 1:
             if self.grid > 1:
                 wdk.reduce(self.slab, self.grid, self.nsplit, self.partial)
         elif self.grid == 1:
@@ -128,6 +140,11 @@ class FusedWideDeepTrainer:
             wdk.reduce(self.partial, self.nsplit, 1, self.grad)
 
     def _apply(self) -> None:
+        if self.fused_update:
+            src, groups = (self.slab, self.grid) if self.world == 1 else (self.grad, 1)
+            wdk.reduce_apply(src, groups, self.inv, self.param, self.s0, self.s1, self.wt, self.step_ctr,
+                             self.h_dnn, self.h_wide)
+            return
         if self.world == 1:
             src, nparts = (self.slab, 1) if self.grid == 1 else (self.partial, self.nsplit)
         else:
@@ -189,7 +206,10 @@ class FusedWideDeepTrainer:
 
     @property
     def steps_done(self) -> int:
-        return int(self.step_ctr.item())
+        return int(self.step_ctr[0].item())
+
+    def set_step(self, step: int) -> None:
+        self.step_ctr.fill_(int(step))
 
     def gradients_once(self) -> np.ndarray:
         """Run fwd/bwd on the current batch WITHOUT updating; return the tile-native gradient."""
@@ -215,11 +235,11 @@ class FusedWideDeepTrainer:
         return wdm.unpack_canonical(self.param.cpu(), self.model)
 
     def state_dict(self) -> dict:
-        return {"param": self.param.cpu(), "s0": self.s0.cpu(), "s1": self.s1.cpu(), "step": self.step_ctr.cpu()}
+        return {"param": self.param.cpu(), "s0": self.s0.cpu(), "s1": self.s1.cpu(), "step": self.step_ctr[:1].cpu()}
 
     def load_state_dict(self, sd: dict) -> None:
         self.param.copy_(sd["param"])
         self.s0.copy_(sd["s0"])
         self.s1.copy_(sd["s1"])
-        self.step_ctr.copy_(sd["step"])
+        self.set_step(int(sd["step"].reshape(-1)[0]))
         self.wt.copy_(self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16))

@@ -280,3 +280,54 @@ def test_stage_dims_cover_every_nonzero_weight():
         staged = np.zeros_like(img)
         staged[:rows[li], :8 * gpr[li]] = img[:rows[li], :8 * gpr[li]]
         assert np.array_equal(staged, img)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["adagrad_ftrl", "adam", "sgd"])
+@pytest.mark.parametrize("batch", [40, 16384])
+def test_fused_reduce_opt_matches_two_launch_path(kind, batch):
+    """wd_reduce_opt (full slab sum + optimizer in one launch) against wd_reduce -> wd_optimizer: the same
+    update up to summation order. Compared after ONE step (over several steps the trajectories drift
+    apart legitimately: a last-bit change of an fp32 master weight can flip its bf16 image). Adam checks
+    the step counter: every optimizer workgroup keeps its own step slot; all must agree."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    opts = {"adagrad_ftrl": (None, None), "adam": (OptSpec("adam", lr=3e-3), OptSpec("adam", lr=1e-2)),
+            "sgd": (OptSpec("sgd", lr=1e-4), OptSpec("sgd", lr=1e-4))}[kind]
+    rec = synthetic_records(batch * 8, device=dev, seed=21)
+    out, losses = [], []
+    for fused_update in (False, True):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=6), batch=batch, device=dev, dnn_opt=opts[0],
+                                  wide_opt=opts[1], fused_update=fused_update)
+        tr.set_data(rec)
+        tr.step()
+        torch.cuda.synchronize()
+        out.append((tr.param.clone(), tr.s0.clone(), tr.s1.clone(), tr.wt.clone()))
+        tr.capture(warmup=1)
+        for _ in range(6):
+            tr.step()
+        torch.cuda.synchronize()
+        assert tr.steps_done == 8 and bool((tr.step_ctr[:117] == 8).all())  # slots of the launched workgroups
+        losses.append(tr.last_loss())
+    for a, b, name in zip(out[0], out[1], ("param", "s0", "s1")):
+        scale = a.abs().max().item() + 1e-6
+        tol = (1e-3 if kind == "adam" else 2e-5) * scale  # Adam: m/sqrt(v) of a near-zero g is order noise
+        assert (a - b).abs().max().item() <= tol, name
+    # the bf16 weight image must be the rounding of the fp32 master
+    assert torch.equal(out[1][0][: wdm.WTOT].to(torch.bfloat16).view(torch.int16), out[1][3])
+    assert abs(losses[0] - losses[1]) <= 2e-2 * abs(losses[0]), losses
+
+
+@pytest.mark.gpu
+def test_reduce_full_matches_fp64_sum():
+    from mifx.ops import wide_deep as wdk
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for groups, stride in ((1, 20608), (7, 20608), (256, 20608), (300, 4096)):
+        slab = torch.randn(groups, stride, generator=g).mul_(100).cuda()
+        out = torch.empty(stride, device="cuda")
+        wdk.reduce_full(slab, groups, out)
+        ref = slab.double().sum(0)
+        err = (out.double() - ref).abs().max().item()
+        assert err <= 1e-6 * slab.abs().sum(0).max().item(), (groups, stride, err)
