@@ -99,3 +99,16 @@ def test_env_report():
 
     r = report()
     assert r["torch"] and any(f.startswith("libmifx_") for f in r["native_libs"])
+
+
+def test_n00_environment_report():
+    r = _load("n00_explore_environment").main()
+    assert r["python"] and r["torch"] and isinstance(r["gpus"], list)
+
+
+def test_n19_privacy_analysis_and_dpsgd(capsys):
+    r = _load("n19_tensorflow_privacy").main(["--train", "1"])
+    out = capsys.readouterr().out
+    assert "satisfies differential privacy with eps = 2.49 and delta = 1e-05." in out
+    assert r["opt_order"] == 7.0
+    assert r["train"] is not None

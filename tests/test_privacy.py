@@ -71,6 +71,32 @@ def test_composition_golden():
     assert acc.epsilon(1e-5) == pytest.approx(8.509656, abs=5e-6)
 
 
+NOTEBOOK_ORDERS = [1.25, 1.5, 1.75, 2., 2.25, 2.5, 3., 3.5, 4., 4.5] + list(range(5, 64)) + [128, 256, 512]
+
+
+def _notebook_analysis(n, batch, sigma, epochs, delta=1e-5):
+    """apply_dp_sgd_analysis of notebooks/privacy/TensorFlow_Privacy.ipynb (cell 3), same order list."""
+    import math
+
+    q = batch / n
+    steps = int(math.ceil(epochs * n / batch))
+    eps, _, order = rdp.get_privacy_spent(NOTEBOOK_ORDERS, rdp.compute_rdp(q, sigma, steps, NOTEBOOK_ORDERS),
+                                          target_delta=delta)
+    return eps, order
+
+
+def test_notebook_privacy_statement_2_92():
+    """The notebook's markdown (TensorFlow_Privacy.ipynb cell 2) states "(2.92, 1e-5)-DP". That figure is the
+    TF-Privacy MNIST tutorial configuration (N=60000, B=256, sigma=1.12, 60 epochs) run through the notebook's
+    own analysis cell; we reproduce it to 3 digits. The cell's printed output for its local variables
+    (N=600, B=32, sigma=1.12, 1 epoch) is not recorded in the reference: ours is eps=2.487 at order 7
+    (parity unpinned, pinned here as a regression value)."""
+    eps, _ = _notebook_analysis(60000, 256, 1.12, 60)
+    assert round(eps, 2) == 2.92
+    eps_nb, order_nb = _notebook_analysis(600, 32, 1.12, 1)
+    assert eps_nb == pytest.approx(2.48666, abs=1e-4) and order_nb == 7
+
+
 def test_dp_sgd_tutorial_epsilon_is_sane():
     eps, _ = rdp.compute_dp_sgd_privacy(60000, 256, 1.1, 60, 1e-5)
     assert 2.0 < eps < 4.0  # the tutorial reports eps ~= 3 for these settings
