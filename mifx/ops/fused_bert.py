@@ -5,6 +5,7 @@ reference implementation of the same math runs."""
 from __future__ import annotations
 
 import functools
+import os
 
 import torch
 import torch.nn.functional as F
@@ -92,15 +93,19 @@ class _BiasGelu(torch.autograd.Function):
         return dx, db.to(ctx.bdtype)
 
 
+# diagnostic switch: MIFX_BERT_TORCH_OPS=1 runs the PyTorch reference ops on the GPU too (bisection only)
+_TORCH_OPS = os.environ.get("MIFX_BERT_TORCH_OPS") == "1"
+
+
 def add_layernorm(a: torch.Tensor, r: torch.Tensor, weight, bias, eps: float = 1e-12) -> torch.Tensor:
     """LayerNorm(a + r) * weight + bias."""
-    if a.is_cuda:
+    if a.is_cuda and not _TORCH_OPS:
         return _AddLayerNorm.apply(a, r, weight, bias, eps)
     return F.layer_norm(a + r, (a.shape[-1],), weight, bias, eps)
 
 
 def bias_gelu(x: torch.Tensor, bias) -> torch.Tensor:
     """GELU(erf)(x + bias)."""
-    if x.is_cuda:
+    if x.is_cuda and not _TORCH_OPS:
         return _BiasGelu.apply(x, bias)
     return F.gelu(x + bias)

@@ -5,6 +5,7 @@ with fp32 master weights, fused AdamW, synthetic GLUE-shaped batches (no dataset
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -42,15 +43,19 @@ class BertTrainer:
     weights (mifx.trainer.optim.FlatAdamW), removing the per-step weight/grad cast kernels."""
 
     def __init__(self, cfg: BertConfig, batch: int, seq: int, device, tp: TPGroup | None = None, lr: float = 2e-5,
-                 graph: bool | None = None, flat_adamw: bool | None = None):
+                 graph: bool | None = None, flat_adamw: bool | None = None, sdpa: str | None = None):
         self.cfg, self.batch, self.seq, self.device = cfg, batch, seq, torch.device(device)
         self.tp = tp or TPGroup(None)
         self.model = BertForSequenceClassification(cfg, self.tp, seed=0).to(self.device)
         cuda = self.device.type == "cuda"
-        # hipGraph replay of the whole step is OPT-IN: on MI355X the captured 12-layer B=32 step went
-        # non-finite after ~10 replays with either optimizer and once raised an illegal memory access
-        # (tools/gpu_s2j.sh, tools/gpu_s2l.sh; eager steps stay finite), so until that is understood the
-        # default is the eager step (measured 10.1 ms/step graph vs ~12 ms eager).
+        # hipGraph replay of the whole step is OPT-IN: on MI355X the captured B=32 S=128 step (2 or 12
+        # layers) goes non-finite at the ~10th replay and can then raise an illegal memory access, while
+        # the same step run eagerly stays finite (45+ steps). Bisection (tools/gpu_s3c..e.sh): it is NOT
+        # the optimizer (fused / foreach AdamW and plain SGD all fail at the same replay), NOT the HIP
+        # LN/GELU kernels (MIFX_BERT_TORCH_OPS=1 fails too), NOT dropout or the SDPA backend (dropout 0,
+        # math and efficient attention fail), NOT the BLAS library (hipBLASLt and rocBLAS) and NOT the
+        # capture stream. Until the cause is found the default is the eager step (10.0 ms/step graph vs
+        # ~12-13 ms eager).
         self.use_graph = False if graph is None else (graph and cuda)
         default_flat = cuda and not self.use_graph
         self.flat = default_flat if flat_adamw is None else (flat_adamw and cuda)
@@ -63,6 +68,7 @@ class BertTrainer:
                                          capturable=self.use_graph)
         self.data = synthetic_batch(cfg, batch, seq, self.device)
         self.amp = cuda
+        self.sdpa = sdpa  # None = PyTorch's choice; "math" / "efficient" / "flash" pins the SDPA backend
         self.graph = None
         self.static_loss = None
 
@@ -73,12 +79,20 @@ class BertTrainer:
         # the autocast weight-cast cache must be off for a step that is captured into a graph (PyTorch's
         # CUDA-graph rules: cached casts created outside the capture must not be referenced by it)
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp,
-                            cache_enabled=not self.use_graph):
+                            cache_enabled=not self.use_graph), self._sdpa_ctx():
             logits = self.model(ids, tt, am)
         loss = F.cross_entropy(logits.float(), y)
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+    def _sdpa_ctx(self):
+        if self.sdpa is None:
+            return contextlib.nullcontext()
+        from torch.nn.attention import SDPBackend, sdpa_kernel
+
+        return sdpa_kernel({"math": SDPBackend.MATH, "efficient": SDPBackend.EFFICIENT_ATTENTION,
+                            "flash": SDPBackend.FLASH_ATTENTION}[self.sdpa])
 
     def _capture(self, warmup: int = 3) -> None:
         side = torch.cuda.Stream(self.device)
@@ -120,6 +134,8 @@ def main(argv=None):
                          "warmup and keep the best (results cached in CSV)")
     ap.add_argument("--seed", type=int, default=None, help="torch.manual_seed before building the trainer")
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--sdpa", choices=["math", "efficient", "flash"], default=None,
+                    help="pin the scaled-dot-product-attention backend (default: PyTorch's choice)")
     a = ap.parse_args(argv)
     if a.seed is not None:
         torch.manual_seed(a.seed)
@@ -135,7 +151,7 @@ def main(argv=None):
     tp = TPGroup(torch.distributed.group.WORLD if env.world_size > 1 else None)
     tr = BertTrainer(BertConfig(layers=a.layers, dropout=a.dropout), a.batch, a.seq, dev, tp,
                      graph=a.graph and not a.no_graph,
-                     flat_adamw=False if a.no_flat_adamw else None)
+                     flat_adamw=False if a.no_flat_adamw else None, sdpa=a.sdpa)
     with heartbeat("bert warmup"):
         for _ in range(a.warmup):
             tr.step()
