@@ -12,7 +12,9 @@
 //    [nblocks, H] (deterministic; summed by the caller).
 //  * bias_gelu_fwd / bwd: column-per-thread over row chunks (no per-element index math); the
 //    backward also produces the bias-gradient column partials, reduced by col_reduce2.
-// Activations are bf16 or fp32 (template), LayerNorm params and statistics fp32.
+// Activations are bf16 or fp32 (template T); LayerNorm gamma/beta, the GELU bias and the parameter
+// gradients dw/db are bf16 or fp32 (template P: a bf16 model's parameters are read and their gradients
+// written in bf16 directly, no cast kernels around each call); statistics and reductions are fp32.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -75,9 +77,9 @@ __device__ __forceinline__ void stv(T* p, const float* v) {
 
 // ---- vectorised LayerNorm (H % 256 == 0): lane owns NC chunks of 4 contiguous columns,
 // chunk j of lane l = columns [4 (64 j + l), +4) -> every access is one 8/16-byte load per lane
-template <typename T, int NC>
+template <typename T, typename P, int NC>
 __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a, const T* __restrict__ r,
-                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        const P* __restrict__ w, const P* __restrict__ b,
                                                         int R, float eps, T* __restrict__ y,
                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out) {
   constexpr int H = NC * 256;
@@ -112,9 +114,11 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       const int c = 4 * (64 * j + lane);
-      const float4 wv = *(const float4*)(w + c), bv = *(const float4*)(b + c);
-      float o[4] = {(v[j][0] - mean) * rstd * wv.x + bv.x, (v[j][1] - mean) * rstd * wv.y + bv.y,
-                    (v[j][2] - mean) * rstd * wv.z + bv.z, (v[j][3] - mean) * rstd * wv.w + bv.w};
+      float wv[4], bv[4];
+      ldv<P, 4>(w + c, wv);
+      ldv<P, 4>(b + c, bv);
+      float o[4] = {(v[j][0] - mean) * rstd * wv[0] + bv[0], (v[j][1] - mean) * rstd * wv[1] + bv[1],
+                    (v[j][2] - mean) * rstd * wv[2] + bv[2], (v[j][3] - mean) * rstd * wv[3] + bv[3]};
       stv<T, 4>(y + base + c, o);
     }
     if (lane == 0) {
@@ -124,9 +128,9 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
   }
 }
 
-template <typename T, int NC>
+template <typename T, typename P, int NC>
 __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ dy, const T* __restrict__ a,
-                                                        const T* __restrict__ r, const float* __restrict__ w,
+                                                        const T* __restrict__ r, const P* __restrict__ w,
                                                         const float* __restrict__ mean_in,
                                                         const float* __restrict__ rstd_in, int R,
                                                         T* __restrict__ dx, float* __restrict__ dw_part,
@@ -137,8 +141,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ d
   float dw[NC][4], db[NC][4], wreg[NC][4];
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
-    const float4 t = *(const float4*)(w + 4 * (64 * j + lane));
-    wreg[j][0] = t.x, wreg[j][1] = t.y, wreg[j][2] = t.z, wreg[j][3] = t.w;
+    ldv<P, 4>(w + 4 * (64 * j + lane), wreg[j]);
 #pragma unroll
     for (int e = 0; e < 4; ++e) dw[j][e] = db[j][e] = 0.f;
   }
@@ -196,9 +199,9 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ d
   }
 }
 
-template <typename T, int PER>
+template <typename T, typename P, int PER>
 __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, const T* __restrict__ r,
-                                                      const float* __restrict__ w, const float* __restrict__ b, int R,
+                                                      const P* __restrict__ w, const P* __restrict__ b, int R,
                                                       int H, float eps, T* __restrict__ y, float* __restrict__ mean_out,
                                                       float* __restrict__ rstd_out) {
   const int lane = threadIdx.x & 63;
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, 
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int c = lane + k * 64;
-      if (c < H) st(y + base + c, (v[k] - mean) * rstd * w[c] + b[c]);
+      if (c < H) st(y + base + c, (v[k] - mean) * rstd * ld(w + c) + ld(b + c));
     }
     if (lane == 0) {
       mean_out[row] = mean;
@@ -234,9 +237,9 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, 
   }
 }
 
-template <typename T, int PER>
+template <typename T, typename P, int PER>
 __global__ __launch_bounds__(kThreads) void add_ln_bwd(const T* __restrict__ dy, const T* __restrict__ a,
-                                                      const T* __restrict__ r, const float* __restrict__ w,
+                                                      const T* __restrict__ r, const P* __restrict__ w,
                                                       const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, int R, int H,
                                                       T* __restrict__ dx, float* __restrict__ dw_part,
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd(const T* __restrict__ dy,
       if (c < H) {
         const float d = ld(dy + base + c);
         xh[k] = (ld(a + base + c) + ld(r + base + c) - mean) * rstd;
-        g[k] = d * w[c];
+        g[k] = d * ld(w + c);
         dw[k] += d * xh[k];
         db[k] += d;
       } else {
@@ -305,27 +308,27 @@ __device__ __forceinline__ float gelu_grad(float x) {
 // grid (ceil(N / kThreads), row chunks): thread owns one column, walks its chunk of rows —
 // no per-element 64-bit div/mod, coalesced across the wave, and the bias-gradient column
 // partial falls out of the same loop (written to db_part[chunk][col]).
-template <typename T>
-__global__ __launch_bounds__(kThreads) void bias_gelu_fwd(const T* __restrict__ x, const float* __restrict__ bias,
+template <typename T, typename P>
+__global__ __launch_bounds__(kThreads) void bias_gelu_fwd(const T* __restrict__ x, const P* __restrict__ bias,
                                                          int M, int N, T* __restrict__ y) {
   const int col = blockIdx.x * kThreads + threadIdx.x;
   if (col >= N) return;
   const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
-  const float bb = bias[col];
+  const float bb = ld(bias + col);
   for (int r = r0; r < r1; ++r) {
     const size_t i = (size_t)r * N + col;
     st(y + i, gelu_f(ld(x + i) + bb));
   }
 }
 
-template <typename T>
+template <typename T, typename P>
 __global__ __launch_bounds__(kThreads) void bias_gelu_bwd(const T* __restrict__ dy, const T* __restrict__ x,
-                                                         const float* __restrict__ bias, int M, int N,
+                                                         const P* __restrict__ bias, int M, int N,
                                                          T* __restrict__ dx, float* __restrict__ db_part) {
   const int col = blockIdx.x * kThreads + threadIdx.x;
   if (col >= N) return;
   const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
-  const float bb = bias[col];
+  const float bb = ld(bias + col);
   float acc = 0.f;
   int r = r0;
   for (; r + 4 <= r1; r += 4) {  // 8 independent loads in flight per thread
@@ -358,8 +361,8 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_bwd(const T* __restrict__ 
 // partial row per chunk.
 constexpr int kGCols = 64, kGSlices = kThreads / kGCols;
 
-template <typename T, int VW>
-__global__ __launch_bounds__(kThreads) void bias_gelu_fwd_v(const T* __restrict__ x, const float* __restrict__ bias,
+template <typename T, typename P, int VW>
+__global__ __launch_bounds__(kThreads) void bias_gelu_fwd_v(const T* __restrict__ x, const P* __restrict__ bias,
                                                            int M, int N, T* __restrict__ y) {
   const int cg = threadIdx.x % kGCols, sl = threadIdx.x / kGCols;
   const int col = (blockIdx.x * kGCols + cg) * VW;
@@ -367,7 +370,7 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_fwd_v(const T* __restrict_
   const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
   float bb[VW];
 #pragma unroll
-  for (int e = 0; e < VW; ++e) bb[e] = bias[col + e];
+  for (int e = 0; e < VW; ++e) bb[e] = ld(bias + col + e);
   for (int r = r0 + sl; r < r1; r += kGSlices) {
     const size_t i = (size_t)r * N + col;
     float v[VW];
@@ -378,9 +381,9 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_fwd_v(const T* __restrict_
   }
 }
 
-template <typename T, int VW>
+template <typename T, typename P, int VW>
 __global__ __launch_bounds__(kThreads) void bias_gelu_bwd_v(const T* __restrict__ dy, const T* __restrict__ x,
-                                                           const float* __restrict__ bias, int M, int N,
+                                                           const P* __restrict__ bias, int M, int N,
                                                            T* __restrict__ dx, float* __restrict__ db_part) {
   __shared__ float sdb[kGSlices][kGCols * VW];
   const int cg = threadIdx.x % kGCols, sl = threadIdx.x / kGCols;
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_bwd_v(const T* __restrict_
   float bb[VW], acc[VW];
 #pragma unroll
   for (int e = 0; e < VW; ++e) {
-    bb[e] = ok ? bias[col + e] : 0.f;
+    bb[e] = ok ? ld(bias + col + e) : 0.f;
     acc[e] = 0.f;
   }
   if (ok) {
@@ -419,14 +422,66 @@ __global__ __launch_bounds__(kThreads) void bias_gelu_bwd_v(const T* __restrict_
   }
 }
 
+// Column sums of an activation gradient [M, N] (the bias gradient of a Linear / bias-add): same block
+// shape as bias_gelu_bwd_v (64 column groups of VW contiguous columns x 4 row slices, 16-B loads), one
+// partial row per row chunk, reduced by col_reduce2 -> deterministic, replaces a generic reduce kernel.
+template <typename T, int VW>
+__global__ __launch_bounds__(kThreads) void col_sum_v(const T* __restrict__ x, int M, int N, float* __restrict__ part) {
+  __shared__ float sp[kGSlices][kGCols * VW];
+  const int cg = threadIdx.x % kGCols, sl = threadIdx.x / kGCols;
+  const int col = (blockIdx.x * kGCols + cg) * VW;
+  const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
+  float acc[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) acc[e] = 0.f;
+  if (col < N) {
+    int r = r0 + sl;
+    for (; r + kGSlices < r1; r += 2 * kGSlices) {  // 2 rows in flight per thread
+      float v0[VW], v1[VW];
+      ldv<T, VW>(x + (size_t)r * N + col, v0);
+      ldv<T, VW>(x + (size_t)(r + kGSlices) * N + col, v1);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) acc[e] += v0[e] + v1[e];
+    }
+    for (; r < r1; r += kGSlices) {
+      float v0[VW];
+      ldv<T, VW>(x + (size_t)r * N + col, v0);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) acc[e] += v0[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VW; ++e) sp[sl][cg * VW + e] = acc[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < kGCols * VW; c += kThreads) {
+    const int gc = blockIdx.x * kGCols * VW + c;
+    if (gc >= N) continue;
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kGSlices; ++i) t += sp[i][c];
+    part[(size_t)blockIdx.y * N + gc] = t;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void col_sum(const T* __restrict__ x, int M, int N, float* __restrict__ part) {
+  const int col = blockIdx.x * kThreads + threadIdx.x;
+  if (col >= N) return;
+  const int r0 = (int)((long long)M * blockIdx.y / gridDim.y), r1 = (int)((long long)M * (blockIdx.y + 1) / gridDim.y);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) acc += ld(x + (size_t)r * N + col);
+  part[(size_t)blockIdx.y * N + col] = acc;
+}
+
 // sum `rows` partial rows of width N (fixed order) for up to two buffers in one launch
 // block = kRedCols columns x kRedSlices row slices (each slice strides the rows, 4 loads in
 // flight), slices combined in LDS in a fixed order -> deterministic, ~N/32 workgroups
 constexpr int kRedCols = 32, kRedSlices = kThreads / kRedCols;
 
+template <typename PO>
 __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict__ p0, const float* __restrict__ p1,
-                                                       int rows, int N, float* __restrict__ o0,
-                                                       float* __restrict__ o1) {
+                                                       int rows, int N, PO* __restrict__ o0,
+                                                       PO* __restrict__ o1) {
   __shared__ float sa[kRedSlices][kRedCols];
   __shared__ float sb[kRedSlices][kRedCols];
   const int cx = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
@@ -459,53 +514,111 @@ __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict_
     a += sa[i][cx];
     b += sb[i][cx];
   }
-  o0[col] = a;
-  if (o1 != nullptr) o1[col] = b;
+  st(o0 + col, a);
+  if (o1 != nullptr) st(o1 + col, b);
 }
 
-template <typename T, int PER>
-int launch_add_ln(int fwd, const void* dy, const void* a, const void* r, const float* w, const float* b, int R, int H,
+template <typename T, typename P, int PER>
+int launch_add_ln(int fwd, const void* dy, const void* a, const void* r, const void* w, const void* b, int R, int H,
                   float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
                   hipStream_t st) {
   if (fwd)
-    hipLaunchKernelGGL((add_ln_fwd<T, PER>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r, w, b, R,
-                       H, eps, (T*)out, mean, rstd);
+    hipLaunchKernelGGL((add_ln_fwd<T, P, PER>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r,
+                       (const P*)w, (const P*)b, R, H, eps, (T*)out, mean, rstd);
   else
-    hipLaunchKernelGGL((add_ln_bwd<T, PER>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
-                       (const T*)r, w, mean, rstd, R, H, (T*)out, dw_part, db_part);
+    hipLaunchKernelGGL((add_ln_bwd<T, P, PER>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
+                       (const T*)r, (const P*)w, mean, rstd, R, H, (T*)out, dw_part, db_part);
   return (int)hipGetLastError();
 }
 
-template <typename T, int NC>
-int launch_add_ln_v(int fwd, const void* dy, const void* a, const void* r, const float* w, const float* b, int R,
+template <typename T, typename P, int NC>
+int launch_add_ln_v(int fwd, const void* dy, const void* a, const void* r, const void* w, const void* b, int R,
                     float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
                     hipStream_t st) {
   if (fwd)
-    hipLaunchKernelGGL((add_ln_fwd_v<T, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r, w, b, R,
-                       eps, (T*)out, mean, rstd);
+    hipLaunchKernelGGL((add_ln_fwd_v<T, P, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r,
+                       (const P*)w, (const P*)b, R, eps, (T*)out, mean, rstd);
   else
-    hipLaunchKernelGGL((add_ln_bwd_v<T, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
-                       (const T*)r, w, mean, rstd, R, (T*)out, dw_part, db_part);
+    hipLaunchKernelGGL((add_ln_bwd_v<T, P, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
+                       (const T*)r, (const P*)w, mean, rstd, R, (T*)out, dw_part, db_part);
   return (int)hipGetLastError();
 }
 
-template <typename T>
-int dispatch_add_ln(int fwd, const void* dy, const void* a, const void* r, const float* w, const float* b, int R,
+template <typename T, typename P>
+int dispatch_add_ln(int fwd, const void* dy, const void* a, const void* r, const void* w, const void* b, int R,
                     int H, float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
                     hipStream_t st) {
   const uintptr_t al = (uintptr_t)dy | (uintptr_t)a | (uintptr_t)r | (uintptr_t)w | (uintptr_t)b | (uintptr_t)out;
   switch (H % 256 == 0 && al % 16 == 0 ? H / 256 : 0) {  // vectorised paths (BERT-base 768 -> NC 3, large 1024 -> 4)
-    case 1: return launch_add_ln_v<T, 1>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-    case 2: return launch_add_ln_v<T, 2>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-    case 3: return launch_add_ln_v<T, 3>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-    case 4: return launch_add_ln_v<T, 4>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 1: return launch_add_ln_v<T, P, 1>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 2: return launch_add_ln_v<T, P, 2>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 3: return launch_add_ln_v<T, P, 3>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+    case 4: return launch_add_ln_v<T, P, 4>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
     default: break;
   }
   const int per = (H + 63) / 64;
-  if (per <= 4) return launch_add_ln<T, 4>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  if (per <= 12) return launch_add_ln<T, 12>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  if (per <= 16) return launch_add_ln<T, 16>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  return launch_add_ln<T, kMaxPer>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  if (per <= 4)
+    return launch_add_ln<T, P, 4>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  if (per <= 12)
+    return launch_add_ln<T, P, 12>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  if (per <= 16)
+    return launch_add_ln<T, P, 16>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  return launch_add_ln<T, P, kMaxPer>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+}
+
+// (activation dtype, parameter dtype) -> dispatch_add_ln<T, P>; dtype / pdt: 0 fp32, 1 bf16
+int dispatch_add_ln_any(int dtype, int pdt, int fwd, const void* dy, const void* a, const void* r, const void* w,
+                        const void* b, int R, int H, float eps, void* out, float* mean, float* rstd, float* dw_part,
+                        float* db_part, int blocks, hipStream_t st) {
+  typedef __hip_bfloat16 bf;
+  if (dtype && pdt)
+    return dispatch_add_ln<bf, bf>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  if (dtype)
+    return dispatch_add_ln<bf, float>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  if (pdt)
+    return dispatch_add_ln<float, bf>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  return dispatch_add_ln<float, float>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+}
+
+template <typename T, typename P>
+int launch_gelu(int fwd, const void* dy, const void* x, const void* bias, int M, int N, void* out, float* db_part,
+                void* db, int chunks, hipStream_t st) {
+  constexpr int VW = 16 / sizeof(T);
+  if (N % VW == 0 && ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)out) % 16 == 0) {
+    const dim3 vgrid((N / VW + kGCols - 1) / kGCols, chunks);
+    if (fwd)
+      hipLaunchKernelGGL((bias_gelu_fwd_v<T, P, VW>), vgrid, dim3(kThreads), 0, st, (const T*)x, (const P*)bias, M, N,
+                         (T*)out);
+    else
+      hipLaunchKernelGGL((bias_gelu_bwd_v<T, P, VW>), vgrid, dim3(kThreads), 0, st, (const T*)dy, (const T*)x,
+                         (const P*)bias, M, N, (T*)out, db_part);
+  } else {
+    const dim3 grid((N + kThreads - 1) / kThreads, chunks);
+    if (fwd)
+      hipLaunchKernelGGL((bias_gelu_fwd<T, P>), grid, dim3(kThreads), 0, st, (const T*)x, (const P*)bias, M, N,
+                         (T*)out);
+    else
+      hipLaunchKernelGGL((bias_gelu_bwd<T, P>), grid, dim3(kThreads), 0, st, (const T*)dy, (const T*)x,
+                         (const P*)bias, M, N, (T*)out, db_part);
+  }
+  if (!fwd)
+    hipLaunchKernelGGL(col_reduce2<P>, dim3((N + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, db_part, nullptr,
+                       chunks, N, (P*)db, (P*)nullptr);
+  return (int)hipGetLastError();
+}
+
+template <typename T, typename P>
+int launch_col_sum(const void* x, int M, int N, float* part, void* out, int chunks, hipStream_t st) {
+  constexpr int VW = 16 / sizeof(T);
+  if (N % VW == 0 && (uintptr_t)x % 16 == 0)
+    hipLaunchKernelGGL((col_sum_v<T, VW>), dim3((N / VW + kGCols - 1) / kGCols, chunks), dim3(kThreads), 0, st,
+                       (const T*)x, M, N, part);
+  else
+    hipLaunchKernelGGL(col_sum<T>, dim3((N + kThreads - 1) / kThreads, chunks), dim3(kThreads), 0, st, (const T*)x, M,
+                       N, part);
+  hipLaunchKernelGGL(col_reduce2<P>, dim3((N + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, part, nullptr, chunks,
+                     N, (P*)out, (P*)nullptr);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -521,81 +634,57 @@ int mifx_bert_ln_blocks(int R) {
 // rows of partials for bias_gelu_bwd
 int mifx_bert_gelu_chunks(int M) { return M < 16 ? 1 : (M / 16 < 512 ? M / 16 : 512); }
 
-// dtype: 0 fp32, 1 bf16
-int mifx_bert_add_ln_fwd(int dtype, const void* a, const void* r, const float* w, const float* b, int R, int H,
+// dtype: activations, pdt: gamma/beta (and dw/db): 0 fp32, 1 bf16
+int mifx_bert_add_ln_fwd(int dtype, int pdt, const void* a, const void* r, const void* w, const void* b, int R, int H,
                          float eps, void* y, float* mean, float* rstd, hipStream_t st) {
   if (H <= 0 || H > 64 * kMaxPer || R <= 0) return -1;
   const int need = (R + 3) / 4;
   const int blocks = need < 4096 ? need : 4096;
-  return dtype ? dispatch_add_ln<__hip_bfloat16>(1, nullptr, a, r, w, b, R, H, eps, y, mean, rstd, nullptr, nullptr,
-                                                 blocks, st)
-               : dispatch_add_ln<float>(1, nullptr, a, r, w, b, R, H, eps, y, mean, rstd, nullptr, nullptr, blocks, st);
+  return dispatch_add_ln_any(dtype, pdt, 1, nullptr, a, r, w, b, R, H, eps, y, mean, rstd, nullptr, nullptr, blocks,
+                             st);
 }
 
-// scratch: dw_part / db_part [mifx_bert_ln_blocks(R), H]; outputs dw, db [H] (fp32)
-int mifx_bert_add_ln_bwd(int dtype, const void* dy, const void* a, const void* r, const float* w, const float* mean,
-                         const float* rstd, int R, int H, void* dx, float* dw_part, float* db_part, float* dw,
-                         float* db, hipStream_t st) {
+// scratch: dw_part / db_part [mifx_bert_ln_blocks(R), H]; outputs dw, db [H] in the parameter dtype
+int mifx_bert_add_ln_bwd(int dtype, int pdt, const void* dy, const void* a, const void* r, const void* w,
+                         const float* mean, const float* rstd, int R, int H, void* dx, float* dw_part, float* db_part,
+                         void* dw, void* db, hipStream_t st) {
   if (H <= 0 || H > 64 * kMaxPer || R <= 0) return -1;
   const int blocks = mifx_bert_ln_blocks(R);
-  const int rc = dtype ? dispatch_add_ln<__hip_bfloat16>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean,
-                                                         (float*)rstd, dw_part, db_part, blocks, st)
-                       : dispatch_add_ln<float>(0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd,
-                                                dw_part, db_part, blocks, st);
+  const int rc = dispatch_add_ln_any(dtype, pdt, 0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd,
+                                     dw_part, db_part, blocks, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(col_reduce2, dim3((H + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, dw_part, db_part, blocks,
-                     H, dw, db);
+  const dim3 g((H + kRedCols - 1) / kRedCols);
+  if (pdt)
+    hipLaunchKernelGGL(col_reduce2<__hip_bfloat16>, g, dim3(kThreads), 0, st, dw_part, db_part, blocks, H,
+                       (__hip_bfloat16*)dw, (__hip_bfloat16*)db);
+  else
+    hipLaunchKernelGGL(col_reduce2<float>, g, dim3(kThreads), 0, st, dw_part, db_part, blocks, H, (float*)dw,
+                       (float*)db);
   return (int)hipGetLastError();
 }
 
-// x: [M, N]; fwd -> out = gelu(x + bias); bwd -> out = dx, db [N] (scratch db_part [gelu_chunks(M), N])
-int mifx_bert_bias_gelu(int dtype, int fwd, const void* dy, const void* x, const float* bias, int M, int N, void* out,
-                        float* db_part, float* db, hipStream_t st) {
+// x: [M, N]; fwd -> out = gelu(x + bias); bwd -> out = dx, db [N] in the bias dtype
+// (scratch db_part [gelu_chunks(M), N])
+int mifx_bert_bias_gelu(int dtype, int pdt, int fwd, const void* dy, const void* x, const void* bias, int M, int N,
+                        void* out, float* db_part, void* db, hipStream_t st) {
   if (M <= 0 || N <= 0) return -1;
   const int chunks = fwd ? (M < 1024 ? M : 1024) : mifx_bert_gelu_chunks(M);
-  const int vw = dtype ? 8 : 4;
-  if (N % vw == 0 && ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)out) % 16 == 0) {
-    const dim3 vgrid((N / vw + kGCols - 1) / kGCols, chunks);
-    if (dtype) {
-      if (fwd)
-        hipLaunchKernelGGL((bias_gelu_fwd_v<__hip_bfloat16, 8>), vgrid, dim3(kThreads), 0, st,
-                           (const __hip_bfloat16*)x, bias, M, N, (__hip_bfloat16*)out);
-      else
-        hipLaunchKernelGGL((bias_gelu_bwd_v<__hip_bfloat16, 8>), vgrid, dim3(kThreads), 0, st,
-                           (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, bias, M, N, (__hip_bfloat16*)out,
-                           db_part);
-    } else {
-      if (fwd)
-        hipLaunchKernelGGL((bias_gelu_fwd_v<float, 4>), vgrid, dim3(kThreads), 0, st, (const float*)x, bias, M, N,
-                           (float*)out);
-      else
-        hipLaunchKernelGGL((bias_gelu_bwd_v<float, 4>), vgrid, dim3(kThreads), 0, st, (const float*)dy,
-                           (const float*)x, bias, M, N, (float*)out, db_part);
-    }
-    if (!fwd)
-      hipLaunchKernelGGL(col_reduce2, dim3((N + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, db_part, nullptr,
-                         chunks, N, db, nullptr);
-    return (int)hipGetLastError();
-  }
-  const dim3 grid((N + kThreads - 1) / kThreads, chunks);
-  if (dtype) {
-    if (fwd)
-      hipLaunchKernelGGL(bias_gelu_fwd<__hip_bfloat16>, grid, dim3(kThreads), 0, st, (const __hip_bfloat16*)x, bias, M,
-                         N, (__hip_bfloat16*)out);
-    else
-      hipLaunchKernelGGL(bias_gelu_bwd<__hip_bfloat16>, grid, dim3(kThreads), 0, st, (const __hip_bfloat16*)dy,
-                         (const __hip_bfloat16*)x, bias, M, N, (__hip_bfloat16*)out, db_part);
-  } else {
-    if (fwd)
-      hipLaunchKernelGGL(bias_gelu_fwd<float>, grid, dim3(kThreads), 0, st, (const float*)x, bias, M, N, (float*)out);
-    else
-      hipLaunchKernelGGL(bias_gelu_bwd<float>, grid, dim3(kThreads), 0, st, (const float*)dy, (const float*)x, bias, M,
-                         N, (float*)out, db_part);
-  }
-  if (!fwd)
-    hipLaunchKernelGGL(col_reduce2, dim3((N + kRedCols - 1) / kRedCols), dim3(kThreads), 0, st, db_part, nullptr,
-                       chunks, N, db, nullptr);
-  return (int)hipGetLastError();
+  typedef __hip_bfloat16 bf;
+  if (dtype && pdt) return launch_gelu<bf, bf>(fwd, dy, x, bias, M, N, out, db_part, db, chunks, st);
+  if (dtype) return launch_gelu<bf, float>(fwd, dy, x, bias, M, N, out, db_part, db, chunks, st);
+  if (pdt) return launch_gelu<float, bf>(fwd, dy, x, bias, M, N, out, db_part, db, chunks, st);
+  return launch_gelu<float, float>(fwd, dy, x, bias, M, N, out, db_part, db, chunks, st);
+}
+
+// out[N] (dtype pdt) = column sums of x [M, N] (dtype); scratch part [gelu_chunks(M), N] fp32
+int mifx_bert_col_sum(int dtype, int pdt, const void* x, int M, int N, float* part, void* out, hipStream_t st) {
+  if (M <= 0 || N <= 0) return -1;
+  const int chunks = mifx_bert_gelu_chunks(M);
+  typedef __hip_bfloat16 bf;
+  if (dtype && pdt) return launch_col_sum<bf, bf>(x, M, N, part, out, chunks, st);
+  if (dtype) return launch_col_sum<bf, float>(x, M, N, part, out, chunks, st);
+  if (pdt) return launch_col_sum<float, bf>(x, M, N, part, out, chunks, st);
+  return launch_col_sum<float, float>(x, M, N, part, out, chunks, st);
 }
 
 }  // extern "C"

@@ -119,7 +119,7 @@ class BertForSequenceClassification(nn.Module):
         B, S = input_ids.shape
         pos = torch.arange(S, device=input_ids.device)
         tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
-        x = self.word(input_ids) + self.pos(pos)[None] + self.tok_type(tt)
+        x = self.word(input_ids) + fb.embedding(pos, self.pos.weight)[None] + fb.embedding(tt, self.tok_type.weight)
         x = F.dropout(self.ln_emb(x), self.cfg.dropout, self.training)
         mask = None
         if attention_mask is not None:  # additive mask [B, 1, 1, S]

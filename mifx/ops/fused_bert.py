@@ -20,9 +20,11 @@ def _fns():
     return {
         "blocks": sig(lib, "mifx_bert_ln_blocks", [I32]),
         "gchunks": sig(lib, "mifx_bert_gelu_chunks", [I32]),
-        "ln_fwd": sig(lib, "mifx_bert_add_ln_fwd", [I32, VP, VP, VP, VP, I32, I32, F32, VP, VP, VP, VP]),
-        "ln_bwd": sig(lib, "mifx_bert_add_ln_bwd", [I32, VP, VP, VP, VP, VP, VP, I32, I32, VP, VP, VP, VP, VP, VP]),
-        "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
+        "ln_fwd": sig(lib, "mifx_bert_add_ln_fwd", [I32, I32, VP, VP, VP, VP, I32, I32, F32, VP, VP, VP, VP]),
+        "ln_bwd": sig(lib, "mifx_bert_add_ln_bwd", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, VP, VP, VP, VP, VP,
+                                                    VP]),
+        "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
+        "colsum": sig(lib, "mifx_bert_col_sum", [I32, I32, VP, I32, I32, VP, VP, VP]),
     }
 
 
@@ -34,63 +36,179 @@ def _dt(t: torch.Tensor) -> int:
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 
+def _param(p: torch.Tensor) -> torch.Tensor:
+    """LayerNorm / bias parameters are read in their own dtype (fp32 or bf16) by the kernels."""
+    p = p if p.dtype in (torch.float32, torch.bfloat16) else p.float()
+    return p.contiguous()
+
+
 class _AddLayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, r, w, b, eps):
         a, r = a.contiguous(), r.contiguous().to(a.dtype)
         H = a.shape[-1]
         R = a.numel() // H
-        w32, b32 = w.float().contiguous(), b.float().contiguous()
+        wp, bp = _param(w), _param(b.to(_param(w).dtype))
         y = torch.empty_like(a)
         mean = torch.empty(R, device=a.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
-        check(_fns()["ln_fwd"](_dt(a), ptr(a), ptr(r), ptr(w32), ptr(b32), R, H, float(eps), ptr(y), ptr(mean),
+        check(_fns()["ln_fwd"](_dt(a), _dt(wp), ptr(a), ptr(r), ptr(wp), ptr(bp), R, H, float(eps), ptr(y), ptr(mean),
                                ptr(rstd), stream_handle(a.device)), "mifx_bert_add_ln_fwd")
-        ctx.save_for_backward(a, r, w32, mean, rstd)
+        ctx.save_for_backward(a, r, wp, mean, rstd)
         ctx.wdtype = w.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        a, r, w32, mean, rstd = ctx.saved_tensors
+        a, r, wp, mean, rstd = ctx.saved_tensors
         dy = dy.contiguous().to(a.dtype)
         H = a.shape[-1]
         R = a.numel() // H
         nb = _fns()["blocks"](R)
         dx = torch.empty_like(a)
         part = torch.empty(2, nb, H, device=a.device, dtype=torch.float32)
-        dwdb = torch.empty(2, H, device=a.device, dtype=torch.float32)
-        check(_fns()["ln_bwd"](_dt(a), ptr(dy), ptr(a), ptr(r), ptr(w32), ptr(mean), ptr(rstd), R, H, ptr(dx),
-                               ptr(part[0]), ptr(part[1]), ptr(dwdb[0]), ptr(dwdb[1]), stream_handle(a.device)),
+        dw = torch.empty(H, device=a.device, dtype=wp.dtype)  # written in the parameter dtype by the kernel
+        db = torch.empty(H, device=a.device, dtype=wp.dtype)
+        check(_fns()["ln_bwd"](_dt(a), _dt(wp), ptr(dy), ptr(a), ptr(r), ptr(wp), ptr(mean), ptr(rstd), R, H,
+                               ptr(dx), ptr(part[0]), ptr(part[1]), ptr(dw), ptr(db), stream_handle(a.device)),
               "mifx_bert_add_ln_bwd")
-        return dx, dx, dwdb[0].to(ctx.wdtype), dwdb[1].to(ctx.wdtype), None
+        if wp.dtype != ctx.wdtype:
+            dw, db = dw.to(ctx.wdtype), db.to(ctx.wdtype)
+        return dx, dx, dw, db, None
 
 
 class _BiasGelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias):
         x = x.contiguous()
-        b32 = bias.float().contiguous()
+        bp = _param(bias)
         y = torch.empty_like(x)
         N = x.shape[-1]
-        check(_fns()["gelu"](_dt(x), 1, None, ptr(x), ptr(b32), x.numel() // N, N, ptr(y), None, None,
+        check(_fns()["gelu"](_dt(x), _dt(bp), 1, None, ptr(x), ptr(bp), x.numel() // N, N, ptr(y), None, None,
                              stream_handle(x.device)), "mifx_bert_bias_gelu")
-        ctx.save_for_backward(x, b32)
+        ctx.save_for_backward(x, bp)
         ctx.bdtype = bias.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, b32 = ctx.saved_tensors
+        x, bp = ctx.saved_tensors
         dy = dy.contiguous().to(x.dtype)
         dx = torch.empty_like(x)
         N = x.shape[-1]
         M = x.numel() // N
         part = torch.empty(_fns()["gchunks"](M), N, device=x.device, dtype=torch.float32)
-        db = torch.empty(N, device=x.device, dtype=torch.float32)
-        check(_fns()["gelu"](_dt(x), 0, ptr(dy), ptr(x), ptr(b32), M, N, ptr(dx), ptr(part), ptr(db),
+        db = torch.empty(N, device=x.device, dtype=bp.dtype)  # written in the bias dtype by the kernel
+        check(_fns()["gelu"](_dt(x), _dt(bp), 0, ptr(dy), ptr(x), ptr(bp), M, N, ptr(dx), ptr(part), ptr(db),
                              stream_handle(x.device)), "mifx_bert_bias_gelu")
-        return dx, db.to(ctx.bdtype)
+        return dx, db if bp.dtype == ctx.bdtype else db.to(ctx.bdtype)
+
+
+def col_sum(x: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """Column sums of a 2-D [M, N] fp32/bf16 tensor -> [N] in out_dtype (fp32 or bf16): the bias gradient,
+    deterministic (fixed-order partials + col_reduce2) instead of a generic reduction kernel."""
+    x = x.contiguous()
+    M, N = x.shape
+    if not x.is_cuda or _TORCH_OPS:
+        return x.float().sum(0).to(out_dtype)
+    pdt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
+    part = torch.empty(_fns()["gchunks"](M), N, device=x.device, dtype=torch.float32)
+    out = torch.empty(N, device=x.device, dtype=pdt)
+    check(_fns()["colsum"](_dt(x), int(pdt == torch.bfloat16), ptr(x), M, N, ptr(part), ptr(out),
+                           stream_handle(x.device)), "mifx_bert_col_sum")
+    return out if pdt == out_dtype else out.to(out_dtype)
+
+
+def _compute_dtype(x: torch.Tensor) -> torch.dtype:
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
+class _BiasAdd(torch.autograd.Function):
+    """y + bias (broadcast over leading dims); backward: bias grad by col_sum."""
+
+    @staticmethod
+    def forward(ctx, y, bias):
+        ctx.bdtype = bias.dtype
+        return y + bias.to(y.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, col_sum(dy.reshape(-1, dy.shape[-1]), ctx.bdtype)
+
+
+class _Linear(torch.autograd.Function):
+    """F.linear(x, w, b) (bias in the GEMM epilogue) with the backward's bias gradient by col_sum; casts
+    to the autocast dtype itself (like F.linear under autocast) and returns gradients in the inputs' dtypes."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        cdt = _compute_dtype(x)
+        with torch.autocast("cuda", enabled=False):
+            xc, wc = x.to(cdt), w.to(cdt)
+            y = F.linear(xc, wc, None if b is None else b.to(cdt))
+        ctx.save_for_backward(xc, wc)
+        ctx.dtypes = (x.dtype, w.dtype, None if b is None else b.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        xdt, wdt, bdt = ctx.dtypes
+        with torch.autocast("cuda", enabled=False):
+            dy = dy.to(wc.dtype)
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            dx = dw = db = None
+            if ctx.needs_input_grad[0]:
+                dx = dy.matmul(wc).to(xdt)
+            if ctx.needs_input_grad[1]:
+                dw = dy2.t().mm(xc.reshape(-1, xc.shape[-1])).to(wdt)
+            if bdt is not None and ctx.needs_input_grad[2]:
+                db = col_sum(dy2, bdt)
+        return dx, dw, db
+
+
+class _Embedding(torch.autograd.Function):
+    """F.embedding whose backward is a scatter-add into an fp32 [V, H] gradient (index_add_), not the sort +
+    unique-by-key (rocPRIM partition with decoupled look-back) of PyTorch's embedding backward: that kernel
+    faults under hipGraph replay on ROCm (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION in
+    rocprim::partition_kernel on the first replay of a captured BERT fwd+bwd, tools/diag_bert_graph.py), and
+    corrupted the captured training step (non-finite loss after ~10 replays)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight):
+        ctx.save_for_backward(ids)
+        ctx.wshape, ctx.wdtype = weight.shape, weight.dtype
+        return F.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        V, H = ctx.wshape
+        g = torch.zeros(V, H, device=dy.device, dtype=torch.float32)
+        g.index_add_(0, ids.reshape(-1), dy.reshape(-1, H).float())
+        return None, g.to(ctx.wdtype)
+
+
+def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Embedding lookup with a hipGraph-safe dense backward on the GPU."""
+    if ids.is_cuda and not _TORCH_OPS:
+        return _Embedding.apply(ids, weight)
+    return F.embedding(ids, weight)
+
+
+def bias_add(y: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    if y.is_cuda and not _TORCH_OPS:
+        return _BiasAdd.apply(y, bias)
+    return y + bias.to(y.dtype)
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """F.linear with a deterministic HIP bias-gradient reduction on the GPU."""
+    if x.is_cuda and bias is not None and not _TORCH_OPS:
+        return _Linear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
 
 
 # diagnostic switch: MIFX_BERT_TORCH_OPS=1 runs the PyTorch reference ops on the GPU too (bisection only)

@@ -22,6 +22,8 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import fused_bert as fb
+
 
 class TPGroup:
     """The tensor-parallel process group (default: WORLD, or a single-rank no-op group)."""
@@ -129,7 +131,7 @@ class ColumnParallelLinear(nn.Module):
                 self.bias.copy_(bias[self.offset:self.offset + self.local])
 
     def forward(self, x):
-        y = F.linear(copy_to_tp(x, self.tp), self.weight, self.bias)
+        y = fb.linear(copy_to_tp(x, self.tp), self.weight, self.bias)
         return gather_from_tp(y, self.tp, self.sizes) if self.gather_output else y
 
 
@@ -153,8 +155,9 @@ class RowParallelLinear(nn.Module):
 
     def forward(self, x_shard):
         y = reduce_from_tp(F.linear(x_shard, self.weight), self.tp)
-        # add the bias in the activation dtype (keeps a bf16 residual stream under autocast)
-        return y + self.bias.to(y.dtype) if self.bias is not None else y
+        # add the bias in the activation dtype (keeps a bf16 residual stream under autocast); its gradient
+        # is a deterministic HIP column reduction on the GPU
+        return fb.bias_add(y, self.bias) if self.bias is not None else y
 
 
 class VocabParallelEmbedding(nn.Module):
@@ -172,9 +175,9 @@ class VocabParallelEmbedding(nn.Module):
 
     def forward(self, ids):
         if self.tp.size == 1:
-            return F.embedding(ids, self.weight)
+            return fb.embedding(ids, self.weight)
         local = ids - self.offset
         mask = (local < 0) | (local >= self.local)
-        out = F.embedding(local.clamp(0, self.local - 1), self.weight)
+        out = fb.embedding(local.clamp(0, self.local - 1), self.weight)
         out = out.masked_fill(mask.unsqueeze(-1), 0.0)
         return reduce_from_tp(out, self.tp)

@@ -34,13 +34,13 @@ def synthetic_batch(cfg: BertConfig, batch: int, seq: int, device, seed: int = 0
 
 
 class BertTrainer:
-    """One fine-tuning step = forward + backward + fused AdamW. On the GPU the whole step (HIP LN/GELU
-    kernels, hipBLASLt GEMMs, attention, dropout RNG, optimizer, and the TP all-reduces) is captured
-    can be captured once into a hipGraph and replayed (opt-in, `graph=True`), removing the ~1.5 ms/step
-    of host launch gaps measured on the eager step (profiles/bert_base_steady_kernels_r1.md: 10.9 ms GPU
-    time vs 12.4 ms wall), with torch's capturable fused AdamW. The default eager step keeps the model
-    weights as bf16 views of one flat buffer updated by a single fused HIP AdamW launch with fp32 master
-    weights (mifx.trainer.optim.FlatAdamW), removing the per-step weight/grad cast kernels."""
+    """One fine-tuning step = forward + backward + fused AdamW. On the GPU the whole step (HIP LN/GELU /
+    bias-grad kernels, hipBLASLt GEMMs, attention, dropout RNG, optimizer, and the TP all-reduces) is
+    captured once into a hipGraph and replayed: the eager step is host-bound (12.8 ms wall for 10.0 ms of
+    GPU work). The model weights are bf16 views of one flat buffer updated by a single fused HIP AdamW
+    launch with fp32 master weights that reads autograd's own gradient tensors in place
+    (mifx.trainer.optim.FlatAdamW): no per-step weight/grad cast kernels, no gradient zero-fill, no
+    per-parameter accumulate kernels."""
 
     def __init__(self, cfg: BertConfig, batch: int, seq: int, device, tp: TPGroup | None = None, lr: float = 2e-5,
                  graph: bool | None = None, flat_adamw: bool | None = None, sdpa: str | None = None):
@@ -48,19 +48,13 @@ class BertTrainer:
         self.tp = tp or TPGroup(None)
         self.model = BertForSequenceClassification(cfg, self.tp, seed=0).to(self.device)
         cuda = self.device.type == "cuda"
-        # hipGraph replay of the whole step is OPT-IN: on MI355X the captured B=32 S=128 step (2 or 12
-        # layers) goes non-finite at the ~10th replay and can then raise an illegal memory access, while
-        # the same step run eagerly stays finite (45+ steps). Bisection (tools/gpu_s3c..e.sh): it is NOT
-        # the optimizer (fused / foreach AdamW and plain SGD all fail at the same replay), NOT the HIP
-        # LN/GELU kernels (MIFX_BERT_TORCH_OPS=1 fails too), NOT dropout or the SDPA backend (dropout 0,
-        # math and efficient attention fail), NOT the BLAS library (hipBLASLt and rocBLAS) and NOT the
-        # capture stream. Until the cause is found the default is the eager step (10.0 ms/step graph vs
-        # ~12-13 ms eager).
-        self.use_graph = False if graph is None else (graph and cuda)
-        default_flat = cuda and not self.use_graph
-        self.flat = default_flat if flat_adamw is None else (flat_adamw and cuda)
-        if self.flat and self.use_graph:
-            raise ValueError("flat AdamW is not supported together with hipGraph capture")
+        # The whole step is captured once as a hipGraph and replayed by default on the GPU (9.2 ms/step vs
+        # 12.8 ms eager: the eager step is host-bound). The embeddings use a scatter-add backward
+        # (mifx.ops.fused_bert.embedding): PyTorch's sort/unique embedding backward faults under hipGraph
+        # replay on ROCm (rocPRIM partition kernel, tools/diag_bert_graph.py) and made the captured step go
+        # non-finite after ~10 replays.
+        self.use_graph = cuda if graph is None else (graph and cuda)
+        self.flat = cuda if flat_adamw is None else (flat_adamw and cuda)
         if self.flat:  # bf16 weights/grads as flat-buffer views + fp32 master, one fused HIP update
             self.opt = FlatAdamW(self.model.parameters(), lr=lr, weight_decay=0.01)
         else:
@@ -124,9 +118,8 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=12)
-    ap.add_argument("--graph", action="store_true",
-                    help="capture the step as one hipGraph (experimental: see BertTrainer.__init__)")
-    ap.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)  # eager is the default
+    ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)  # the default on the GPU
+    ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one captured hipGraph")
     ap.add_argument("--no-flat-adamw", action="store_true",
                     help="eager mode: fp32 params + torch fused AdamW instead of the flat HIP AdamW")
     ap.add_argument("--tunable", default=None, metavar="CSV",
@@ -150,7 +143,7 @@ def main(argv=None):
         torch.cuda.set_device(dev)
     tp = TPGroup(torch.distributed.group.WORLD if env.world_size > 1 else None)
     tr = BertTrainer(BertConfig(layers=a.layers, dropout=a.dropout), a.batch, a.seq, dev, tp,
-                     graph=a.graph and not a.no_graph,
+                     graph=not a.no_graph,
                      flat_adamw=False if a.no_flat_adamw else None, sdpa=a.sdpa)
     with heartbeat("bert warmup"):
         for _ in range(a.warmup):

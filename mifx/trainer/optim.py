@@ -69,42 +69,99 @@ def make_optimizer(kind: str, params, lr: float, **kw) -> torch.optim.Optimizer:
 
 
 class FlatAdamW:
-    """AdamW over a model whose parameters are re-homed as bf16 views of ONE flat buffer, with their
-    gradients as views of one flat bf16 gradient buffer (autograd accumulates in place), and fp32
-    master weights / moments kept here. `step()` is a single fused HIP launch (mifx.ops.adamw);
-    `zero_grad()` is one memset. Both are hipGraph-capturable (device-side step counter)."""
+    """AdamW over a model whose parameters are re-homed as bf16 views of ONE flat buffer, with fp32 master
+    weights / moments kept here. `step()` is a single fused HIP launch (mifx.ops.adamw).
+
+    Gradients (`grads=`):
+      * "own" (default on the GPU): autograd's own per-parameter gradient tensors are read in place by the
+        chunked kernel (a per-step table of their addresses), `zero_grad()` sets them to None -- no zero-fill
+        and no `grad += new` accumulate kernel per parameter per step;
+      * "views": gradients are views of one flat gradient buffer that autograd accumulates into (one memset
+        per `zero_grad()`); the flat kernel is then hipGraph-capturable (device-side step counter)."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 dtype: torch.dtype = torch.bfloat16):
+                 dtype: torch.dtype = torch.bfloat16, grads: str | None = None):
         self.params = [p for p in params if p.requires_grad]
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
+        if grads is None:
+            grads = "own" if dev.type == "cuda" and dtype == torch.bfloat16 else "views"
+        if grads not in ("own", "views"):
+            raise ValueError("grads must be 'own' or 'views'")
+        if grads == "own" and (dev.type != "cuda" or dtype != torch.bfloat16):
+            raise ValueError("grads='own' needs bf16 parameters on the GPU")
+        self.mode = grads
+        align = 8 if grads == "own" else 1  # 16-byte aligned bf16 / 32-byte fp32 vectors per parameter
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += (p.numel() + align - 1) // align * align
+        n = off
         self.n = n
-        self.flat = torch.empty(n, device=dev, dtype=dtype)
-        self.flat_grad = torch.zeros(n, device=dev, dtype=dtype)
-        self.master = torch.empty(n, device=dev, dtype=torch.float32)
+        self.flat = torch.zeros(n, device=dev, dtype=dtype)
+        self.flat_grad = torch.zeros(n, device=dev, dtype=dtype) if grads == "views" else None
+        self.master = torch.zeros(n, device=dev, dtype=torch.float32)
         self.m = torch.zeros(n, device=dev, dtype=torch.float32)
         self.v = torch.zeros(n, device=dev, dtype=torch.float32)
         self.step_count = torch.zeros((), device=dev, dtype=torch.int32)
-        off = 0
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, offs):
                 k = p.numel()
                 self.master[off:off + k].copy_(p.detach().reshape(-1).float())
                 self.flat[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = self.flat[off:off + k].view(p.shape)
-                p.grad = self.flat_grad[off:off + k].view(p.shape)
-                off += k
+                p.grad = self.flat_grad[off:off + k].view(p.shape) if grads == "views" else None
+        if grads == "own":
+            from ..ops.adamw import chunk_size
 
-    def zero_grad(self, set_to_none: bool = False) -> None:  # grads stay views of the flat buffer
-        self.flat_grad.zero_()
+            ch = chunk_size()
+            bp, bo, bn = [], [], []
+            for i, p in enumerate(self.params):
+                for o in range(0, p.numel(), ch):
+                    bp.append(i)
+                    bo.append(o)
+                    bn.append(min(ch, p.numel() - o))
+            self.poff = torch.tensor(offs, dtype=torch.int64, device=dev)
+            self._gptr = torch.zeros(len(self.params), dtype=torch.int64, device=dev)  # grad addresses
+            self._capture_host = torch.zeros(len(self.params), dtype=torch.int64).pin_memory()
+            self._addr = None
+            self.bp, self.bo, self.bn = (torch.tensor(x, dtype=torch.int32, device=dev) for x in (bp, bo, bn))
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        if self.mode == "own":
+            for p in self.params:
+                p.grad = None
+        else:  # grads stay views of the flat buffer
+            self.flat_grad.zero_()
 
     def step(self) -> None:
-        from ..ops.adamw import adamw_flat_
+        from ..ops.adamw import adamw_chunks_, adamw_flat_
 
-        adamw_flat_(self.flat, self.flat_grad, self.master, self.m, self.v, self.step_count, self.lr,
-                    self.betas[0], self.betas[1], self.eps, self.wd)
+        if self.mode == "views":
+            adamw_flat_(self.flat, self.flat_grad, self.master, self.m, self.v, self.step_count, self.lr,
+                        self.betas[0], self.betas[1], self.eps, self.wd)
+            return
+        addr = []
+        for p in self.params:
+            g = p.grad
+            if g is not None and (g.dtype != torch.bfloat16 or not g.is_contiguous() or g.device != p.device):
+                raise RuntimeError("FlatAdamW(grads='own') needs contiguous bf16 gradients on the parameter's device")
+            addr.append(0 if g is None else g.data_ptr())
+        addr = tuple(addr)
+        if torch.cuda.is_current_stream_capturing():
+            # hipGraph capture: no pinned allocation is allowed here, so the table goes through the pinned
+            # buffer reserved at construction; the captured copy reads it on every replay, so it is never
+            # written again (the captured gradients keep their addresses on every replay)
+            if self._capture_host is None:
+                raise RuntimeError("FlatAdamW(grads='own') supports one captured step per optimizer")
+            self._capture_host.numpy()[:] = addr
+            self._gptr.copy_(self._capture_host, non_blocking=True)
+            self._capture_host, self._addr = None, addr
+        elif addr != self._addr:  # eager: upload only when autograd handed out new gradient addresses
+            self._gptr.copy_(torch.tensor(addr, dtype=torch.int64).pin_memory(), non_blocking=True)
+            self._addr = addr
+        adamw_chunks_(self.flat, self._gptr, self.poff, self.bp, self.bo, self.bn, self.master, self.m, self.v,
+                      self.step_count, self.lr, self.betas[0], self.betas[1], self.eps, self.wd)
 
     def state_dict(self) -> dict:
         return {"master": self.master, "m": self.m, "v": self.v, "step": self.step_count}

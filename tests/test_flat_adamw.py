@@ -41,3 +41,36 @@ def test_flat_adamw_kernel_matches_reference():
         torch.testing.assert_close(b.cpu(), a, rtol=1e-5, atol=1e-6)
     assert torch.equal(bufs_gpu[0].cpu(), bufs_gpu[2].cpu().bfloat16())
     assert int(bufs_gpu[5]) == 3
+
+
+@pytest.mark.gpu
+def test_flat_adamw_own_grads_matches_views_mode():
+    """grads='own' (chunked kernel reading autograd's per-parameter gradients in place, no zero-fill / no
+    accumulate kernels) must give the same update as grads='views' (flat gradient buffer); a parameter
+    without a gradient is left untouched (torch AdamW semantics). Odd sizes exercise the 8-aligned
+    flat offsets and the scalar tails; a 20000-wide layer spans several 8192-element chunks."""
+    torch.manual_seed(0)
+
+    def make():
+        torch.manual_seed(1)
+        return torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.GELU(), torch.nn.Linear(7, 20000),
+                                   torch.nn.Linear(20000, 3)).cuda().bfloat16()
+
+    ma, mb = make(), make()
+    unused = torch.nn.Parameter(torch.randn(13, device="cuda", dtype=torch.bfloat16))
+    before = unused.detach().clone()
+    oa = FlatAdamW(list(ma.parameters()), lr=1e-3, weight_decay=0.01, grads="views")
+    ob = FlatAdamW(list(mb.parameters()) + [unused], lr=1e-3, weight_decay=0.01, grads="own")
+    x = torch.randn(64, 5, device="cuda", dtype=torch.bfloat16)
+    for _ in range(4):
+        for m, o in ((ma, oa), (mb, ob)):
+            o.zero_grad()
+            m(x).float().pow(2).mean().backward()
+            o.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ma.parameters(), mb.parameters()):
+        torch.testing.assert_close(b.float(), a.float(), rtol=0, atol=0)
+    assert torch.equal(unused.detach(), before)
+    assert int(ob.step_count) == 4 and all(p.grad is not None for p in mb.parameters())
+    ob.zero_grad()
+    assert all(p.grad is None for p in mb.parameters())
