@@ -50,7 +50,8 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 constexpr int T = 64;       // examples per tile
 constexpr int PAD = 8;      // bf16 elements of row padding (2-way max bank conflicts)
-constexpr int NTHR = 256;
+constexpr int NTHR = 512;   // 8 waves: 4 row groups x 2 halves of every layer's output tiles
+constexpr int NWAVE = NTHR / 64;
 
 // padded layer dims: layer l maps K_l -> N_l ; real: 3->100->70->48->34->1
 constexpr int K1 = 32, N1 = 128;
@@ -115,7 +116,7 @@ __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 #ifdef WD_STAMPS  // diagnostic build only: per-wave s_memtime at phase boundaries of block 0
-__device__ unsigned long long g_stamps[4][32];
+__device__ unsigned long long g_stamps[NWAVE][32];
 #define STAMP(i)                                                                       \
   do {                                                                                 \
     __builtin_amdgcn_sched_barrier(0);                                                 \
@@ -141,24 +142,27 @@ __device__ __forceinline__ void block_sync_lds() {
   asm volatile("" ::: "memory");
 }
 
-// ---------------------------------------------------------------- forward layer (wave-local)
-// Z^T[n][t] = sum_k Wt[n][k] * A[t][k]; A rows t in [16w, 16w+16). RELU -> bf16 -> Aout.
-// Weight fragments are read in batches of NB n-tiles, the next batch prefetched.
+// ---------------------------------------------------------------- forward layer (wave pair)
+// Z^T[n][t] = sum_k Wt[n][k] * A[t][k]; A rows t in [16 wr, 16 wr + 16). The two waves of row group wr
+// split the layer's n-tiles (half 0: the first ceil(NT/2), half 1: the rest), so the caller must barrier
+// before the next layer reads Aout. RELU -> bf16 -> Aout. Weight fragments are read in batches of NB
+// n-tiles, the next batch prefetched.
 template <int K, int N, bool LAST>
-__device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, uint16_t* Aout, int w, int r,
-                                          int h, v4f* zlast) {
-  constexpr int KS = K / 32, NT = N / 16;
+__device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, uint16_t* Aout, int wr, int half,
+                                          int r, int h, v4f* zlast) {
+  constexpr int KS = K / 32, NT = N / 16, NTH = (NT + 1) / 2;
   constexpr int NB = KS >= 3 ? 2 : (KS == 2 ? 4 : 8);
-  constexpr int NBATCH = (NT + NB - 1) / NB;
+  constexpr int NBATCH = (NTH + NB - 1) / NB;
+  const int nt0 = half * NTH;
   v8bf b[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) b[s] = ld8(A + (16 * w + r) * (K + PAD) + 32 * s + 8 * h);
+  for (int s = 0; s < KS; ++s) b[s] = ld8(A + (16 * wr + r) * (K + PAD) + 32 * s + 8 * h);
   v8bf wa[2][NB][KS];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      if (j < NT) wa[0][j][s] = ld8(W + (16 * j + r) * (K + PAD) + 32 * s + 8 * h);
+      if (j < NTH && nt0 + j < NT) wa[0][j][s] = ld8(W + (16 * (nt0 + j) + r) * (K + PAD) + 32 * s + 8 * h);
 #pragma unroll
   for (int bi = 0; bi < NBATCH; ++bi) {
     if (bi + 1 < NBATCH) {
@@ -166,14 +170,15 @@ __device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, 
       for (int j = 0; j < NB; ++j)
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          const int nt = (bi + 1) * NB + j;
-          if (nt < NT) wa[(bi + 1) & 1][j][s] = ld8(W + (16 * nt + r) * (K + PAD) + 32 * s + 8 * h);
+          const int jl = (bi + 1) * NB + j;
+          if (jl < NTH && nt0 + jl < NT)
+            wa[(bi + 1) & 1][j][s] = ld8(W + (16 * (nt0 + jl) + r) * (K + PAD) + 32 * s + 8 * h);
         }
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int nt = bi * NB + j;
-      if (nt >= NT) continue;
+      const int jl = bi * NB + j, nt = nt0 + jl;
+      if (jl >= NTH || nt >= NT) continue;
       v4f acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) acc = mfma(wa[bi & 1][j][s], b[s], acc);
@@ -181,7 +186,7 @@ __device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, 
         v4bf o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (bf16)fmaxf(acc[i], 0.f);
-        *(v4bf*)(Aout + (16 * w + r) * (N + PAD) + 16 * nt + 4 * h) = o;
+        *(v4bf*)(Aout + (16 * wr + r) * (N + PAD) + 16 * nt + 4 * h) = o;
       } else {
         *zlast = acc;
       }
@@ -189,21 +194,24 @@ __device__ __forceinline__ void fwd_layer(const uint16_t* W, const uint16_t* A, 
   }
 }
 
-// ------------------------------------------------------- activation gradient (wave-local)
+// ------------------------------------------------------- activation gradient (wave pair)
 // dA^T[k][t] = sum_n W[k][n] dZ^T[n][t]   (W = layer with dims K x N, stored as Wt[N][K])
-// dZout[t][k] = dA[t][k] * (Aact[t][k] > 0). Weight fragments via transposed reads, batched.
+// dZout[t][k] = dA[t][k] * (Aact[t][k] > 0) for the rows of row group wr; the two halves split the
+// k-tiles. Weight fragments via transposed reads, batched.
 template <int K, int N>
 __device__ __forceinline__ void bwd_dA(const uint16_t* W, const uint16_t* dZ, const uint16_t* Aact, uint16_t* dZout,
-                                       int w, int r, int h) {
-  constexpr int NS = (N + 31) / 32, KT = K / 16;
+                                       int wr, int half, int r, int h) {
+  constexpr int NS = (N + 31) / 32, KT = K / 16, KTH = KT / 2;
+  static_assert(KT % 2 == 0, "k-tiles split evenly between the two halves");
   constexpr int KB = NS >= 3 ? 2 : 4;
-  constexpr int NBATCH = (KT + KB - 1) / KB;
+  constexpr int NBATCH = (KTH + KB - 1) / KB;
+  const int kt0 = half * KTH;
   const int q = r >> 2, p = r & 3;
   const bool live = (N % 32 == 0) || (8 * h < N % 32);  // only the last k-step can be partial
   v8bf b[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    v8bf v = ld8(dZ + (16 * w + r) * (N + PAD) + 32 * s + 8 * h);
+    v8bf v = ld8(dZ + (16 * wr + r) * (N + PAD) + 32 * s + 8 * h);
     if (s == NS - 1 && !live) v = (v8bf){};
     b[s] = v;
   }
@@ -213,8 +221,8 @@ __device__ __forceinline__ void bwd_dA(const uint16_t* W, const uint16_t* dZ, co
     for (int j = 0; j < KB; ++j)
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const int kt = bi * KB + j;
-        if (kt < KT) {
+        const int jl = bi * KB + j, kt = kt0 + jl;
+        if (jl < KTH) {
           const uint16_t* pa = W + (32 * s + 8 * h + q) * (K + PAD) + 16 * kt + 4 * p;
           v8bf a = cat8(tr_read(pa), tr_read(pa + 4 * (K + PAD)));
           if (s == NS - 1 && !live) a = (v8bf){};
@@ -228,12 +236,12 @@ __device__ __forceinline__ void bwd_dA(const uint16_t* W, const uint16_t* dZ, co
     if (bi + 1 < NBATCH) load((bi + 1) & 1, bi + 1);
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
-      const int kt = bi * KB + j;
-      if (kt >= KT) continue;
+      const int jl = bi * KB + j, kt = kt0 + jl;
+      if (jl >= KTH) continue;
       v4f acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NS; ++s) acc = mfma(wa[bi & 1][j][s], b[s], acc);
-      const int off = (16 * w + r) * (K + PAD) + 16 * kt + 4 * h;
+      const int off = (16 * wr + r) * (K + PAD) + 16 * kt + 4 * h;
       const uint2 m = *(const uint2*)(Aact + off);
       v4bf o;
       o[0] = (bf16)((m.x & 0xffffu) ? acc[0] : 0.f);
@@ -331,6 +339,7 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   float* wgrad = (float*)(lds + LEND);
   float* red = wgrad + WIDE_PAD;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
+  const int wr = w & 3, half = w >> 2;  // row group (16 examples of the tile) and half of the layer's tiles
 #ifdef WD_STAMPS
   if (blockIdx.x == 0 && lane == 0) g_stamps[w][0] = __builtin_amdgcn_s_memtime();
 #endif
@@ -349,17 +358,14 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   } else {
     // Stage only the LIVE part of the image: per layer the rows that hold real weights (plus the
     // constant-1 producer row) and the 16-byte granules up to the last real column (1715 of the 3456
-    // granules for the taxi tower); the rest of the weight region is zero-filled in LDS while the
-    // global loads are in flight. (rocprof: same kernel time as the full image at B=65536 and 2.8 us
-    // slower for the single-workgroup B=40 step -- the prologue is latency-, not byte-bound -- so the
-    // trainer stages the full image by default.)
-    constexpr int PER = (WTOT / 8 + NTHR - 1) / NTHR;  // bound: every granule live
-    uint4 v[PER];
-    int dst[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      if (i * NTHR >= sd.total) break;  // uniform
-      const int c = min(tid + i * NTHR, sd.total - 1);
+    // granules for the taxi tower) after zero-filling the weight region. (rocprof: same kernel time as
+    // the full image at B=65536 and slower for the single-workgroup B=40 step -- the prologue is
+    // latency-, not byte-bound -- so the trainer stages the full image by default.) A plain strided
+    // loop: register arrays of the granules were demoted to scratch by the compiler, which made every
+    // launch of the kernel (either path) reserve scratch.
+    for (int c = tid; c < LWEND / 8; c += NTHR) *(uint4*)(lds + c * 8) = make_uint4(0, 0, 0, 0);
+    block_sync_lds();
+    for (int c = tid; c < sd.total; c += NTHR) {
       int l = 0, cc = c;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -367,19 +373,13 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
           cc -= sd.rows[q] * sd.gpr[q];
           l = q + 1;
         }
-      const int gpr = sd.gpr[l], row = cc / gpr, g = cc - row * gpr;
+      // select chain, not sd.gpr[l]: a runtime index into the by-value struct would put it in scratch
+      const int gpr = l == 0 ? sd.gpr[0] : l == 1 ? sd.gpr[1] : l == 2 ? sd.gpr[2] : l == 3 ? sd.gpr[3] : sd.gpr[4];
+      const int row = cc / gpr, g = cc - row * gpr;
       const int K = l == 0 ? K1 : l == 1 ? K2 : l == 2 ? K3 : l == 3 ? K4 : K5;
       const int off = l == 0 ? OFF1 : l == 1 ? OFF2 : l == 2 ? OFF3 : l == 3 ? OFF4 : OFF5;
       const int lw = l == 0 ? LW1 : l == 1 ? LW2 : l == 2 ? LW3 : l == 3 ? LW4 : LW5;
-      v[i] = *(const uint4*)(wt + off + row * K + g * 8);
-      dst[i] = tid + i * NTHR < sd.total ? lw + row * (K + PAD) + g * 8 : -1;
-    }
-    for (int c = tid; c < LWEND / 8; c += NTHR) *(uint4*)(lds + c * 8) = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      if (i * NTHR >= sd.total) break;
-      if (dst[i] >= 0) *(uint4*)(lds + dst[i]) = v[i];
+      *(uint4*)(lds + lw + row * (K + PAD) + g * 8) = *(const uint4*)(wt + off + row * K + g * 8);
     }
   }
   for (int c = tid; c < T * (K1 + PAD) / 8; c += NTHR) *(uint4*)(lds + LA0 + c * 8) = make_uint4(0, 0, 0, 0);
@@ -405,24 +405,25 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   const float qmax = 1073741824.f / (float)(max(my_tiles, 1) * T);
   int* wgi = (int*)wgrad;
 
-  // dW tile ownership (see dw_phase): L1 nt{w,w+4} x kt{0,1}; L2 nt{0..5} x kt{2w,2w+1};
-  // L3 nt{w} x kt{0..5}; L4 nt{w} x kt{0..3}; L5 nt{0} x kt{w}
-  v4f acc1[4], acc2[12], acc3[6], acc4[4], acc5[1];
+  // dW tile ownership (see dw_phase), wave w = 4 half + wr: L1 nt{w} x kt{0,1}; L2 nt{0..5} x kt{w};
+  // L3 nt{wr} x kt{3 half..+2}; L4 nt{wr} x kt{2 half, +1}; L5 nt{0} x kt{wr} (half 0 only)
+  v4f acc1[2], acc2[6], acc3[3], acc4[2], acc5[1];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc1[j] = acc4[j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 2; ++j) acc1[j] = acc4[j] = (v4f){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 12; ++j) acc2[j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 6; ++j) acc2[j] = (v4f){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 6; ++j) acc3[j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 3; ++j) acc3[j] = (v4f){0.f, 0.f, 0.f, 0.f};
   acc5[0] = (v4f){0.f, 0.f, 0.f, 0.f};
   float loss_sum = 0.f, dl_sum = 0.f;
-  int ct1[4], ct2[12], ct3[6], ct4[4], ct5[1];  // compact slab positions of this wave's dW tiles
+  int ct1[2], ct2[6], ct3[3], ct4[2], ct5[1];  // compact slab positions of this wave's dW tiles
   if (TRAIN) {
-    load_ct<K1, 2, 2>(ct1, TB1, w, 4, 0, 1, tmap);
-    load_ct<K2, 6, 2>(ct2, TB2, 0, 1, 2 * w, 1, tmap);
-    load_ct<K3, 1, 6>(ct3, TB3, w, 0, 0, 1, tmap);
-    load_ct<K4, 1, 4>(ct4, TB4, w, 0, 0, 1, tmap);
-    load_ct<K5, 1, 1>(ct5, TB5, 0, 0, w, 0, tmap);
+    load_ct<K1, 1, 2>(ct1, TB1, w, 0, 0, 1, tmap);
+    load_ct<K2, 6, 1>(ct2, TB2, 0, 1, w, 0, tmap);
+    load_ct<K3, 1, 3>(ct3, TB3, wr, 0, 3 * half, 1, tmap);
+    load_ct<K4, 1, 2>(ct4, TB4, wr, 0, 2 * half, 1, tmap);
+    load_ct<K5, 1, 1>(ct5, TB5, 0, 0, wr, 0, tmap);
+    if (half) ct5[0] = -1;  // L5 has 4 dW tiles: owned by half 0
   }
 
   uint16_t* A0 = lds + LA0;
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   // would serialise the prefetch). Rows past the batch read a valid record; they carry
   // dl = 0 and are excluded from loss and wide-gradient, so they contribute nothing.
   auto fetch = [&](int tile, uint4& a, uint4& b) {
-    const long long row = min((long long)tile * T + 16 * w + r, batch - 1);
+    const long long row = min((long long)tile * T + 16 * wr + r, batch - 1);
     long long di = start + row;
     if (di >= n_data) di -= n_data;  // host guarantees batch <= n_data
     a = data[2 * di];
@@ -448,7 +449,12 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   fetch(blockIdx.x, nu0, nu1);
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const long long row = (long long)tile * T + 16 * w + r;
+#ifdef WD_STAMPS
+    // stamp the second tile of the workgroup when there is one (steady state: records prefetched)
+    stamp_on = ntiles > (int)gridDim.x ? tile == (int)(blockIdx.x + gridDim.x) : tile == (int)blockIdx.x;
+    STAMP(1);
+#endif
+    const long long row = (long long)tile * T + 16 * wr + r;
     const bool valid = row < batch;
     const uint4 u0 = nu0, u1 = nu1;
     fetch(tile + gridDim.x, nu0, nu1);  // prefetch the next tile's records
@@ -464,22 +470,23 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
       wv[f] = wide[ids[f]];  // issued now, consumed after the forward
     }
     const float wbias = wide[WIDE_BIAS];
-    if (h == 0) {
+    if (h == 0 && half == 0) {
       v8bf x = {(bf16)__uint_as_float(u0.x), (bf16)__uint_as_float(u0.y), (bf16)__uint_as_float(u0.z),
                 (bf16)1.0f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-      *(v8bf*)(A0 + (16 * w + r) * (K1 + PAD)) = x;
+      *(v8bf*)(A0 + (16 * wr + r) * (K1 + PAD)) = x;
     }
-    wave_sync();
-    v4f z5;
-    fwd_layer<K1, N1, false>(lds + LW1, A0, A1, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K2, N2, false>(lds + LW2, A1, A2, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K3, N3, false>(lds + LW3, A2, A3, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K4, N4, false>(lds + LW4, A3, A4, w, r, h, nullptr);
-    wave_sync();
-    fwd_layer<K5, N5, true>(lds + LW5, A4, nullptr, w, r, h, &z5);
+    // each layer's output is written by both waves of a row group: barrier before the next layer reads it
+    block_sync_lds();
+    v4f z5 = {0.f, 0.f, 0.f, 0.f};
+    fwd_layer<K1, N1, false>(lds + LW1, A0, A1, wr, half, r, h, nullptr);
+    block_sync_lds();
+    fwd_layer<K2, N2, false>(lds + LW2, A1, A2, wr, half, r, h, nullptr);
+    block_sync_lds();
+    fwd_layer<K3, N3, false>(lds + LW3, A2, A3, wr, half, r, h, nullptr);
+    block_sync_lds();
+    fwd_layer<K4, N4, false>(lds + LW4, A3, A4, wr, half, r, h, nullptr);
+    block_sync_lds();
+    fwd_layer<K5, N5, true>(lds + LW5, A4, nullptr, wr, half, r, h, &z5);  // 1 n-tile: half 0
     STAMP(2);
 
     // ---- wide part + loss (every lane recomputes for example r; lane h==0 owns it)
@@ -490,50 +497,50 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     const float y = (float)(idw[4] >> 16);
     const float lossv = fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
     if (!TRAIN) {
-      if (h == 0 && valid) {
+      if (h == 0 && half == 0 && valid) {
         logits_out[row] = x;
         loss_sum += lossv;
       }
       continue;
     }
     const float dl = valid ? (1.f / (1.f + __expf(-x)) - y) * grad_scale : 0.f;
-    if (h == 0 && valid) {
+    if (h == 0 && half == 0 && valid) {
       loss_sum += lossv;
       const int q = __float2int_rn(fminf(fmaxf(dl * qscale, -qmax), qmax));
 #pragma unroll
       for (int f = 0; f < 9; ++f) atomicAdd(&wgi[ids[f]], q);
       dl_sum += dl;
     }
-    {
+    if (half == 0) {
       v4bf o = {(bf16)(h == 0 ? dl : 0.f), (bf16)0.f, (bf16)0.f, (bf16)0.f};
-      *(v4bf*)(D5 + (16 * w + r) * (N5 + PAD) + 4 * h) = o;
+      *(v4bf*)(D5 + (16 * wr + r) * (N5 + PAD) + 4 * h) = o;
     }
-    wave_sync();
+    block_sync_lds();  // D5 rows come from half 0, read by both halves
     STAMP(3);
-    bwd_dA<K5, N5>(lds + LW5, D5, A4, P, w, r, h);   // dz4 -> P
+    bwd_dA<K5, N5>(lds + LW5, D5, A4, P, wr, half, r, h);   // dz4 -> P
     STAMP(4);
     block_sync_lds();                                 // B1
     STAMP(5);
-    dw_phase<K5, N5, 1, 1>(acc5, D5, A4, 0, 0, w, 0, r, h);
-    dw_phase<K4, N4, 1, 4>(acc4, P, A3, w, 0, 0, 1, r, h);
+    if (half == 0) dw_phase<K5, N5, 1, 1>(acc5, D5, A4, 0, 0, wr, 0, r, h);
+    dw_phase<K4, N4, 1, 2>(acc4, P, A3, wr, 0, 2 * half, 1, r, h);
     STAMP(6);
-    bwd_dA<K4, N4>(lds + LW4, P, A3, Q, w, r, h);    // dz3 -> Q
+    bwd_dA<K4, N4>(lds + LW4, P, A3, Q, wr, half, r, h);    // dz3 -> Q
     STAMP(7);
     block_sync_lds();                                 // B2
     STAMP(8);
-    dw_phase<K3, N3, 1, 6>(acc3, Q, A2, w, 0, 0, 1, r, h);
+    dw_phase<K3, N3, 1, 3>(acc3, Q, A2, wr, 0, 3 * half, 1, r, h);
     STAMP(9);
-    bwd_dA<K3, N3>(lds + LW3, Q, A2, P, w, r, h);    // dz2 -> P
+    bwd_dA<K3, N3>(lds + LW3, Q, A2, P, wr, half, r, h);    // dz2 -> P
     STAMP(10);
     block_sync_lds();                                 // B3
     STAMP(11);
-    dw_phase<K2, N2, 6, 2>(acc2, P, A1, 0, 1, 2 * w, 1, r, h);
+    dw_phase<K2, N2, 6, 1>(acc2, P, A1, 0, 1, w, 0, r, h);
     STAMP(12);
-    bwd_dA<K2, N2>(lds + LW2, P, A1, Q, w, r, h);    // dz1 -> Q
+    bwd_dA<K2, N2>(lds + LW2, P, A1, Q, wr, half, r, h);    // dz1 -> Q
     STAMP(13);
     block_sync_lds();                                 // B4
     STAMP(14);
-    dw_phase<K1, N1, 2, 2>(acc1, Q, A0, w, 4, 0, 1, r, h);
+    dw_phase<K1, N1, 1, 2>(acc1, Q, A0, w, 0, 0, 1, r, h);
     STAMP(15);
     block_sync_lds();                                 // B5
     STAMP(16);
@@ -547,14 +554,14 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   }
   if (lane == 0) {
     red[w] = loss_sum;
-    red[4 + w] = dl_sum;
+    red[NWAVE + w] = dl_sum;
   }
   if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * stride;
-    store_tiles<2, 2>(my, acc1, ct1, lane);
-    store_tiles<6, 2>(my, acc2, ct2, lane);
-    store_tiles<1, 6>(my, acc3, ct3, lane);
-    store_tiles<1, 4>(my, acc4, ct4, lane);
+    store_tiles<1, 2>(my, acc1, ct1, lane);
+    store_tiles<6, 1>(my, acc2, ct2, lane);
+    store_tiles<1, 3>(my, acc3, ct3, lane);
+    store_tiles<1, 2>(my, acc4, ct4, lane);
     store_tiles<1, 1>(my, acc5, ct5, lane);
   }
   __syncthreads();
@@ -562,11 +569,19 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     float* my = slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD);
     for (int c = tid; c < WIDE_PAD; c += NTHR) {
       float v = (float)wgi[c] * qinv;
-      if (c == WIDE_BIAS) v += red[4] + red[5] + red[6] + red[7];
+      if (c == WIDE_BIAS) {
+#pragma unroll
+        for (int i = 0; i < NWAVE; ++i) v += red[NWAVE + i];
+      }
       my[c] = v;
     }
   }
-  if (tid == 0 && slab_loss) slab_loss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0 && slab_loss) {
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < NWAVE; ++i) l += red[i];
+    slab_loss[blockIdx.x] = l;
+  }
   stamp_on = true;
   STAMP(17);
 }

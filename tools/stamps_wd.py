@@ -33,13 +33,14 @@ for batch in (64, 65536):
     for _ in range(3):
         tr.step()
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 128)()
+    NW = 8  # waves per workgroup (csrc/wide_deep.hip NWAVE)
+    buf = (ctypes.c_ulonglong * (32 * NW))()
     assert diag.mifx_wd_stamps(buf) == 0
-    st = [[buf[w * 32 + i] for i in range(32)] for w in range(4)]
-    print(f"== batch {batch} grid {tr.grid}: cycles per phase (block 0, first tile), per wave")
+    st = [[buf[w * 32 + i] for i in range(32)] for w in range(NW)]
+    print(f"== batch {batch} grid {tr.grid}: cycles per phase (block 0, 2nd tile if any; stage = kernel start -> that tile), per wave")
     for i in range(1, 18):
-        d = [st[w][i] - st[w][i - 1] for w in range(4)]
+        d = [st[w][i] - st[w][i - 1] for w in range(NW)]
         if i == 17:
-            d = [st[w][17] - st[w][16] for w in range(4)]
+            d = [st[w][17] - st[w][16] for w in range(NW)]
         print(f"  {NAMES[i]:>9}: " + " ".join(f"{x:8d}" for x in d))
     print(f"  total kernel (wave0 start->end): {st[0][17] - st[0][0]}")
