@@ -117,6 +117,7 @@ __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
 }
 #ifdef WD_STAMPS  // diagnostic build only: per-wave s_memtime at phase boundaries of block 0
 __device__ unsigned long long g_stamps[NWAVE][32];
+__device__ unsigned long long g_blk[1024][2];  // per-workgroup (start, end) s_memrealtime (100 MHz)
 #define STAMP(i)                                                                       \
   do {                                                                                 \
     __builtin_amdgcn_sched_barrier(0);                                                 \
@@ -342,6 +343,7 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   const int wr = w & 3, half = w >> 2;  // row group (16 examples of the tile) and half of the layer's tiles
 #ifdef WD_STAMPS
   if (blockIdx.x == 0 && lane == 0) g_stamps[w][0] = __builtin_amdgcn_s_memtime();
+  if (tid == 0 && blockIdx.x < 1024) g_blk[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
 #endif
 
   if (sd.total == WTOT / 8) {
@@ -584,6 +586,10 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   }
   stamp_on = true;
   STAMP(17);
+#ifdef WD_STAMPS
+  __syncthreads();
+  if (tid == 0 && blockIdx.x < 1024) g_blk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // partial[sp][e] = sum_{g in split sp} slab[g][e]   (float4 granules, 4 loads in flight)
@@ -866,6 +872,9 @@ int mifx_wd_reduce_opt(const float* slab, int G, int stride, float* out, const i
 #ifdef WD_STAMPS
 int mifx_wd_stamps(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps), 0, hipMemcpyDeviceToHost);
+}
+int mifx_wd_blk_times(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk), sizeof(g_blk), 0, hipMemcpyDeviceToHost);
 }
 #endif
 

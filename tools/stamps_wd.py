@@ -44,3 +44,15 @@ for batch in (64, 65536):
             d = [st[w][17] - st[w][16] for w in range(NW)]
         print(f"  {NAMES[i]:>9}: " + " ".join(f"{x:8d}" for x in d))
     print(f"  total kernel (wave0 start->end): {st[0][17] - st[0][0]}")
+    blk = (ctypes.c_ulonglong * 2048)()
+    assert diag.mifx_wd_blk_times(blk) == 0
+    nb = tr.grid
+    st0 = [blk[2 * b] for b in range(nb)]
+    en0 = [blk[2 * b + 1] for b in range(nb)]
+    t0 = min(st0)
+    starts = sorted((x - t0) / 100.0 for x in st0)  # us (100 MHz)
+    ends = sorted((x - t0) / 100.0 for x in en0)
+    q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))]  # noqa: E731
+    print(f"  workgroup start us: min {starts[0]:.2f} p50 {q(starts, .5):.2f} p90 {q(starts, .9):.2f} max {starts[-1]:.2f}")
+    print(f"  workgroup end   us: min {ends[0]:.2f} p50 {q(ends, .5):.2f} p90 {q(ends, .9):.2f} max {ends[-1]:.2f}")
+
