@@ -474,9 +474,10 @@ __global__ __launch_bounds__(kThreads) void col_sum(const T* __restrict__ x, int
 }
 
 // sum `rows` partial rows of width N (fixed order) for up to two buffers in one launch
-// block = kRedCols columns x kRedSlices row slices (each slice strides the rows, 4 loads in
-// flight), slices combined in LDS in a fixed order -> deterministic, ~N/32 workgroups
-constexpr int kRedCols = 32, kRedSlices = kThreads / kRedCols;
+// block = kRedCols columns x kRedSlices row slices; each slice strides the rows with 8 loads per buffer in
+// flight (the partials are L2-resident: the kernel is latency-, not bandwidth-bound), slices combined in
+// LDS in a fixed order -> deterministic, N/16 workgroups
+constexpr int kRedCols = 16, kRedSlices = kThreads / kRedCols, kRedU = 8;
 
 template <typename PO>
 __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict__ p0, const float* __restrict__ p1,
@@ -489,14 +490,18 @@ __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict_
   float a = 0.f, b = 0.f;
   if (col < N) {
     int r = sl;
-    for (; r + 3 * kRedSlices < rows; r += 4 * kRedSlices) {
-      const float a0 = p0[(size_t)r * N + col], a1 = p0[(size_t)(r + kRedSlices) * N + col];
-      const float a2 = p0[(size_t)(r + 2 * kRedSlices) * N + col], a3 = p0[(size_t)(r + 3 * kRedSlices) * N + col];
-      a += (a0 + a1) + (a2 + a3);
+    for (; r + (kRedU - 1) * kRedSlices < rows; r += kRedU * kRedSlices) {
+      float va[kRedU], vb[kRedU];
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) va[u] = p0[(size_t)(r + u * kRedSlices) * N + col];
       if (p1 != nullptr) {
-        const float b0 = p1[(size_t)r * N + col], b1 = p1[(size_t)(r + kRedSlices) * N + col];
-        const float b2 = p1[(size_t)(r + 2 * kRedSlices) * N + col], b3 = p1[(size_t)(r + 3 * kRedSlices) * N + col];
-        b += (b0 + b1) + (b2 + b3);
+#pragma unroll
+        for (int u = 0; u < kRedU; ++u) vb[u] = p1[(size_t)(r + u * kRedSlices) * N + col];
+      }
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) {
+        a += va[u];
+        if (p1 != nullptr) b += vb[u];
       }
     }
     for (; r < rows; r += kRedSlices) {

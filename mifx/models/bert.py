@@ -76,9 +76,11 @@ class BertLayer(nn.Module):
     def forward(self, x, mask):
         B, S, _ = x.shape
         h, d = self.local_heads, self.head_dim
-        qkv = self.qkv(x).view(B, S, 3, h, d).permute(2, 0, 3, 1, 4)  # [3, B, h, S, d]
+        # q/k/v as [B, h, S, d] views of the fused QKV output; unbind (not indexing a permuted view) so the
+        # backward assembles dq/dk/dv with ONE stack copy instead of a zero-fill plus three slice copies
+        q, k, v = (t.transpose(1, 2) for t in self.qkv(x).view(B, S, 3, h, d).unbind(2))
         drop = self.cfg.dropout if self.training else 0.0
-        ctx = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=mask, dropout_p=drop)
+        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=drop)
         ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
         a = F.dropout(self.attn_out(ctx), drop, self.training)
         x = fb.add_layernorm(a, x, self.ln1.weight, self.ln1.bias, self.cfg.ln_eps)
