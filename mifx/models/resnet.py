@@ -56,7 +56,9 @@ class ResNetV2(nn.Module):
     def forward(self, x):  # x: [B, 3, H, W] in [0, 1] (NHWC memory format preferred)
         y = F.max_pool2d(self.stem(x), 3, 2, 1)
         y, _ = self.post_bn.forward_add(*self.blocks(y))
-        return self.fc(y.mean((2, 3)))
+        # global average pool whose backward keeps the channels_last layout (a plain mean's backward
+        # materialises an NCHW gradient, copied back to NHWC by the final BN backward)
+        return self.fc(F.adaptive_avg_pool2d(y, 1).flatten(1))
 
 
 def resnet50_v2(num_classes: int = 1001) -> ResNetV2:

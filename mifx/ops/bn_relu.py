@@ -69,7 +69,14 @@ def _fwd(x, x2, weight, bias, run_mean, run_var, momentum, eps, relu):
     return y, s, w32, stats
 
 
+_LAYOUT_DIAG = __import__("os").environ.get("MIFX_BN_LAYOUT_DIAG") == "1"
+
+
 def _bwd(dy, x, w32, stats, relu, dres):
+    if _LAYOUT_DIAG:
+        for nm, t in (("dy", dy), ("dres", dres)):
+            if t is not None and t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
+                print(f"[bn-layout] {nm} {tuple(t.shape)} strides {t.stride()} dtype {t.dtype}", flush=True)
     if dy.dim() == 4 and not dy.is_contiguous(memory_format=torch.channels_last):
         dy = dy.contiguous(memory_format=torch.channels_last)
     dy = dy.to(x.dtype)
@@ -116,12 +123,18 @@ class _AddBNReLU(torch.autograd.Function):
         y, s, w32, stats = _fwd(a, b.to(a.dtype), weight, bias, run_mean, run_var, momentum, eps, True)
         ctx.save_for_backward(s, w32, stats)
         ctx.wdtype = weight.dtype
+        # an unused output (s, when the next block has a projection shortcut) arrives as None instead of
+        # a materialised zero tensor: autograd created those in NCHW, forcing a full channels_last copy
+        # (plus a read of zeros) in the backward of the first block of every stage
+        ctx.set_materialize_grads(False)
         return y, s
 
     @staticmethod
     def backward(ctx, dy, ds):
         s, w32, stats = ctx.saved_tensors
         if dy is None:
+            if ds is None:
+                return None, None, None, None, None, None, None, None
             return ds, ds, None, None, None, None, None, None
         dx, dgb = _bwd(dy, s, w32, stats, True, ds)
         return dx, dx, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None
