@@ -53,7 +53,9 @@ class BertTrainer:
         # (mifx.ops.fused_bert.embedding): PyTorch's sort/unique embedding backward faults under hipGraph
         # replay on ROCm (rocPRIM partition kernel, tools/diag_bert_graph.py) and made the captured step go
         # non-finite after ~10 replays.
-        self.use_graph = cuda if graph is None else (graph and cuda)
+        # (default only at TP=1: capturing the TP all-reduces into the graph is not yet validated on a
+        # multi-GPU node, so TP>1 steps eagerly unless graph=True is passed)
+        self.use_graph = (cuda and self.tp.size == 1) if graph is None else (graph and cuda)
         self.flat = cuda if flat_adamw is None else (flat_adamw and cuda)
         if self.flat:  # bf16 weights/grads as flat-buffer views + fp32 master, one fused HIP update
             self.opt = FlatAdamW(self.model.parameters(), lr=lr, weight_decay=0.01)
@@ -118,7 +120,7 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=12)
-    ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)  # the default on the GPU
+    ap.add_argument("--graph", action="store_true", help="capture the step as one hipGraph also at TP>1")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one captured hipGraph")
     ap.add_argument("--no-flat-adamw", action="store_true",
                     help="eager mode: fp32 params + torch fused AdamW instead of the flat HIP AdamW")
@@ -143,7 +145,7 @@ def main(argv=None):
         torch.cuda.set_device(dev)
     tp = TPGroup(torch.distributed.group.WORLD if env.world_size > 1 else None)
     tr = BertTrainer(BertConfig(layers=a.layers, dropout=a.dropout), a.batch, a.seq, dev, tp,
-                     graph=not a.no_graph,
+                     graph=False if a.no_graph else (True if a.graph else None),
                      flat_adamw=False if a.no_flat_adamw else None, sdpa=a.sdpa)
     with heartbeat("bert warmup"):
         for _ in range(a.warmup):
