@@ -102,14 +102,16 @@ __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, co
   if (slice < rpb) {
     const size_t c0 = (size_t)cg * kVec;
     int r = r0 + slice;
-    for (; r + rpb < r1; r += 2 * rpb) {  // two rows in flight per thread
-      float u[kVec], w[kVec];
-      load_sum(x, x2, s_out, (size_t)r * C + c0, u);
-      load_sum(x, x2, s_out, (size_t)(r + rpb) * C + c0, w);
+    // four rows in flight per thread: at 512 workgroups x 256 threads that is ~8 MB of loads in flight,
+    // enough to cover HBM latency (two rows ran at ~half the bandwidth of the apply pass)
+    for (; r + 3 * rpb < r1; r += 4 * rpb) {
+      float u[4][kVec];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) load_sum(x, x2, s_out, (size_t)(r + k * rpb) * C + c0, u[k]);
 #pragma unroll
       for (int e = 0; e < kVec; ++e) {
-        a[e] += u[e] + w[e];
-        q[e] += u[e] * u[e] + w[e] * w[e];
+        a[e] += (u[0][e] + u[1][e]) + (u[2][e] + u[3][e]);
+        q[e] += (u[0][e] * u[0][e] + u[1][e] * u[1][e]) + (u[2][e] * u[2][e] + u[3][e] * u[3][e]);
       }
     }
     for (; r < r1; r += rpb) {
@@ -247,7 +249,24 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce(const T* __restrict__ 
     ld8f(shift + c0, sh);
     ld8f(mean + c0, mu);
     ld8f(rstd + c0, rs);
-    for (int r = r0 + slice; r < r1; r += rpb) {
+    int r = r0 + slice;
+    for (; r + 3 * rpb < r1; r += 4 * rpb) {  // four rows (eight 16-B loads) in flight per thread
+      float d[4][kVec], u[4][kVec];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ldv(dy + (size_t)(r + k * rpb) * C + c0, d[k]);
+        ldv(x + (size_t)(r + k * rpb) * C + c0, u[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          const float g = (relu && fmaf(u[k][e], sc[e], sh[e]) <= 0.f) ? 0.f : d[k][e];
+          a[e] += g;
+          q[e] += g * ((u[k][e] - mu[e]) * rs[e]);
+        }
+    }
+    for (; r < r1; r += rpb) {
       float d[kVec], u[kVec];
       ldv(dy + (size_t)r * C + c0, d);
       ldv(x + (size_t)r * C + c0, u);
