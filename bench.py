@@ -49,19 +49,50 @@ def run(trainer, steps: int, warmup: int, device) -> float:
     return time.perf_counter() - t0
 
 
-def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool):
-    model = WideDeepModel(seed=0)
-    if device.type == "cuda":
-        from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+def _ranks_agree(tr) -> bool:
+    """All ranks apply the same all-reduced gradient to the same initial weights: their parameters must be
+    bit-identical. Eager MAX/MIN all-reduce of a checksum, outside any graph."""
+    chk = torch.stack([tr.param.double().sum(), tr.param.double().abs().sum()])
+    hi, lo = chk.clone(), chk.clone()
+    torch.distributed.all_reduce(hi, op=torch.distributed.ReduceOp.MAX)
+    torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo)) and bool(torch.isfinite(chk).all())
 
-        tr = FusedWideDeepTrainer(model, batch=batch, device=device, process_group=pg)
-    else:
-        from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
 
-        tr = TorchWideDeepTrainer(model, batch=batch, device=device)
-    tr.set_data(synthetic_records(n_data, device=device, seed=seed))
-    if graph and device.type == "cuda":
-        tr.capture()
+def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, split_collective: bool = False):
+    def build():
+        model = WideDeepModel(seed=0)
+        if device.type == "cuda":
+            from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+            t = FusedWideDeepTrainer(model, batch=batch, device=device, process_group=pg)
+        else:
+            from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
+
+            t = TorchWideDeepTrainer(model, batch=batch, device=device)
+        t.set_data(synthetic_records(n_data, device=device, seed=seed))
+        return t
+
+    tr = build()
+    if not (graph and device.type == "cuda"):
+        return tr
+    # Multi-rank over RCCL: the all-reduce is captured INTO the step's hipGraph (one replay per step).
+    # Measured on one MI355X with the DP code path forced (tools/dp_step_overhead.py): split-phase step
+    # (graph, eager all-reduce, graph) 67.4 us at B=65536 (host 41.6 us) vs 51.2 us captured; B=40: 37.7 vs
+    # 22.5 us. Guard: after two replays every rank must hold bit-identical weights, else fall back.
+    captured = pg is not None and not split_collective and torch.distributed.get_backend(pg) == "nccl"
+    tr.capture(include_collective=captured)
+    tr.collective_in_graph = captured
+    if captured:
+        for _ in range(2):
+            tr.step()
+        torch.cuda.synchronize(device)
+        if not _ranks_agree(tr):
+            print("[bench] captured all-reduce: ranks disagree, falling back to split-phase graphs",
+                  file=sys.stderr, flush=True)
+            tr = build()
+            tr.capture(include_collective=False)
+            tr.collective_in_graph = False
     return tr
 
 
@@ -76,6 +107,8 @@ def main(argv=None) -> int:
     ap.add_argument("--ref-steps", type=int, default=2000)
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--split-collective", action="store_true",
+                    help="multi-rank: eager all-reduce between two graphs instead of capturing it")
     a = ap.parse_args(argv)
 
     env = mdist.init()
@@ -90,7 +123,9 @@ def main(argv=None) -> int:
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     n = env.world_size
 
-    tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph)
+    tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph,
+                      a.split_collective)
+    collective_in_graph = bool(getattr(tr, "collective_in_graph", False))
     dt = mdist.max_over_ranks(run(tr, a.steps, a.warmup, device), device if use_cuda else None)
     loss = tr.last_loss() / a.batch_per_gpu
     value = a.batch_per_gpu * n * a.steps / dt
@@ -98,7 +133,7 @@ def main(argv=None) -> int:
     ref = None
     if a.ref_batch:
         del tr
-        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph)
+        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.split_collective)
         dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
                "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps}
@@ -122,7 +157,8 @@ def main(argv=None) -> int:
                        "optimizer": "adagrad(dnn,lr=0.05)+ftrl(linear,lr=0.2)",
                        "precision": "bf16 MFMA compute, fp32 master weights/optimizer state",
                        "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
-                       "hipgraph": bool(use_cuda and not a.no_graph)},
+                       "hipgraph": bool(use_cuda and not a.no_graph),
+                       "collective_in_graph": collective_in_graph},
             "final_mean_loss": loss,
             "reference_batch": ref,
         }

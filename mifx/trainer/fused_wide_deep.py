@@ -176,9 +176,11 @@ class FusedWideDeepTrainer:
     def capture(self, warmup: int = 2, include_collective: bool = False) -> None:
         """Capture the step as hipGraph(s) after `warmup` eager steps on a side stream.
 
-        Single rank: one graph. Multi-rank: by default two graphs (local grad, optimizer) with the RCCL
-        all-reduce issued eagerly between them; `include_collective=True` captures the all-reduce too
-        (one graph launch per step, requires a graph-capturable RCCL)."""
+        Single rank: one graph. Multi-rank: by default two graphs (local grad, optimizer) with the
+        all-reduce issued eagerly between them (works with any backend, e.g. gloo); `include_collective=True`
+        captures the RCCL all-reduce too -- one graph launch per step. bench.py uses the latter over RCCL:
+        on one MI355X with the DP path forced (tools/dp_step_overhead.py) the split-phase step costs
+        67.4 us vs 51.2 us captured at B=65536 (host 41.6 vs 11.4 us per step)."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

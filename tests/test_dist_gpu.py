@@ -59,3 +59,33 @@ def test_fused_dp_two_ranks_matches_single():
     ref = tr.sync_to_model().state_dict()
     for k, v in ref.items():
         np.testing.assert_allclose(got[k].numpy(), v.detach().cpu().numpy(), rtol=2e-3, atol=2e-5, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_captured_rccl_allreduce_step_matches_split_phase():
+    """bench.py captures the RCCL all-reduce inside the step's hipGraph at N>1. On one GPU (1-rank RCCL
+    group, trainer forced onto its data-parallel path) the captured step must produce exactly the weights
+    of the split-phase step (graph, eager all-reduce, graph)."""
+    from mifx.data.synthetic import synthetic_records
+    from mifx.models import wide_deep as wdm
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        recs = synthetic_records(1 << 16, device="cuda", seed=4)
+        out = []
+        for captured in (False, True):
+            tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=2), batch=4096, device="cuda",
+                                      process_group=dist.group.WORLD)
+            tr.world = 2  # take the DP code path (reduce_full -> all-reduce -> optimizer) on one rank
+            tr.set_data(recs)
+            tr.capture(include_collective=captured)
+            assert (tr.graph is not None) == captured and (tr._graphs is not None) != captured
+            for _ in range(6):
+                tr.step()
+            torch.cuda.synchronize()
+            out.append(tr.param.clone())
+        assert torch.equal(out[0], out[1])
+    finally:
+        dist.destroy_process_group()
