@@ -1,0 +1,145 @@
+// 3x3 / stride 2 / pad 1 max pooling for NHWC bf16 activations (ResNet-50 stem, BASELINE config 5).
+//
+// PyTorch's NHWC max-pool saves an int64 argmax per OUTPUT element and scatters the backward through it
+// (profiles/resnet50_steady_kernels_s3.md: 252 us fwd + 620 us bwd per step at B=256, 112x112x64). Here:
+//  * forward: one thread per (n, oh, ow, 8 channels): nine 16-byte window loads, per-channel max, and a
+//    1-byte window position (0..8) per channel -> the index traffic is 1/8 of int64 indices;
+//  * backward in gather form: one thread per (n, ih, iw, 8 channels) visits the (at most 2x2) output
+//    windows that contain its input position and adds dout where the stored position points at it.
+//    Every input gradient is written exactly once (no zero-fill, no atomics: deterministic).
+// Semantics follow PyTorch: padding never wins, ties keep the first position in window order, NaN wins.
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kVec = 8;  // channels per thread (16 bytes of bf16)
+
+struct alignas(16) Bf8 {
+  __hip_bfloat16 v[kVec];
+};
+struct alignas(8) U8x8 {
+  uint8_t v[kVec];
+};
+
+__global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __restrict__ x, int N, int H, int W, int C,
+                                                       int OH, int OW, __hip_bfloat16* __restrict__ y,
+                                                       uint8_t* __restrict__ idx) {
+  const int cg = C / kVec;
+  const long long total = (long long)N * OH * OW * cg;
+  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+    const int g = (int)(t % cg);
+    long long p = t / cg;
+    const int ow = (int)(p % OW);
+    p /= OW;
+    const int oh = (int)(p % OH);
+    const int n = (int)(p / OH);
+    float m[kVec];
+    U8x8 k8;
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) {
+      m[e] = -INFINITY;
+      k8.v[e] = 0;
+    }
+    bool first = true;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        const Bf8 v8 = *(const Bf8*)(x + (((size_t)n * H + ih) * W + iw) * C + g * kVec);
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          const float v = __bfloat162float(v8.v[e]);
+          if (first || v > m[e] || (v != v && m[e] == m[e])) {  // first valid tap, strictly greater, or NaN
+            m[e] = v;
+            k8.v[e] = (uint8_t)(kh * 3 + kw);
+          }
+        }
+        first = false;
+      }
+    }
+    Bf8 o;
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) o.v[e] = __float2bfloat16(m[e]);
+    const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + g * kVec;
+    *(Bf8*)(y + off) = o;
+    *(U8x8*)(idx + off) = k8;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __restrict__ dy,
+                                                       const uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                       int OH, int OW, __hip_bfloat16* __restrict__ dx) {
+  const int cg = C / kVec;
+  const long long total = (long long)N * H * W * cg;
+  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+    const int g = (int)(t % cg);
+    long long p = t / cg;
+    const int iw = (int)(p % W);
+    p /= W;
+    const int ih = (int)(p % H);
+    const int n = (int)(p / H);
+    // output windows containing ih: 2 oh - 1 <= ih <= 2 oh + 1
+    const int oh0 = ih >> 1, oh1 = (ih & 1) ? oh0 + 1 : oh0;
+    const int ow0 = iw >> 1, ow1 = (iw & 1) ? ow0 + 1 : ow0;
+    float acc[kVec];
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int oh = a ? oh1 : oh0;
+      if ((a && oh1 == oh0) || oh >= OH) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ow = b ? ow1 : ow0;
+        if ((b && ow1 == ow0) || ow >= OW) continue;
+        const uint8_t k = (uint8_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+        const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + g * kVec;
+        const U8x8 k8 = *(const U8x8*)(idx + off);
+        const Bf8 d8 = *(const Bf8*)(dy + off);
+#pragma unroll
+        for (int e = 0; e < kVec; ++e)
+          if (k8.v[e] == k) acc[e] += __bfloat162float(d8.v[e]);
+      }
+    }
+    Bf8 o;
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) o.v[e] = __float2bfloat16(acc[e]);
+    *(Bf8*)(dx + (((size_t)n * H + ih) * W + iw) * C + g * kVec) = o;
+  }
+}
+
+int grid_for(long long total) {
+  long long g = (total + kThreads - 1) / kThreads;
+  if (g > 65536) g = 65536;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+// x, y, dx: NHWC bf16 (channels_last), C % 8 == 0, 16-byte aligned; idx: [N, OH, OW, C] uint8
+int mifx_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* y, void* idx, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec) return -1;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_fwd, dim3(grid_for((long long)N * OH * OW * (C / kVec))), dim3(kThreads), 0, st,
+                     (const __hip_bfloat16*)x, N, H, W, C, OH, OW, (__hip_bfloat16*)y, (uint8_t*)idx);
+  return (int)hipGetLastError();
+}
+
+int mifx_maxpool3s2_bwd(const void* dy, const void* idx, int N, int H, int W, int C, void* dx, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec) return -1;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_bwd, dim3(grid_for((long long)N * H * W * (C / kVec))), dim3(kThreads), 0, st,
+                     (const __hip_bfloat16*)dy, (const uint8_t*)idx, N, H, W, C, OH, OW, (__hip_bfloat16*)dx);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -8,6 +8,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn_relu import BatchNormReLU2d
+from ..ops.pool import max_pool3s2
 
 
 class PreActBottleneck(nn.Module):
@@ -54,7 +55,7 @@ class ResNetV2(nn.Module):
         self.fc = nn.Linear(cin, num_classes)
 
     def forward(self, x):  # x: [B, 3, H, W] in [0, 1] (NHWC memory format preferred)
-        y = F.max_pool2d(self.stem(x), 3, 2, 1)
+        y = max_pool3s2(self.stem(x))  # HIP NHWC kernels (1-byte argmax) on the GPU, F.max_pool2d elsewhere
         y, _ = self.post_bn.forward_add(*self.blocks(y))
         # global average pool whose backward keeps the channels_last layout (a plain mean's backward
         # materialises an NCHW gradient, copied back to NHWC by the final BN backward)

@@ -176,3 +176,33 @@ def test_resnet_fused_blocks_match_fp64_reference():
         if n.startswith(tight):
             assert a < 1e-4, f"{n}: fused vs PyTorch-BN relative gradient error {a:.2e}\n{table}"
         assert b < 1e-2, f"{n}: fused vs fp64 relative gradient error {b:.2e}\n{table}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 9, 7), (2, 8, 1, 1)])
+def test_maxpool3s2_matches_pytorch(shape):
+    """HIP 3x3/s2/p1 NHWC max-pool (1-byte argmax, gather backward) vs F.max_pool2d: identical forward, and
+    the backward equal to PyTorch's (ties are avoided by distinct values so both pick the same position)."""
+    from mifx.ops.pool import _MaxPool3s2, native_ok
+
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    vals = torch.randperm(N * C * H * W, device="cuda").float() / (N * C * H * W)  # distinct, bf16-exact steps
+    x = (vals.view(N, C, H, W) * 256).round().bfloat16().contiguous(memory_format=torch.channels_last)
+    x = x + torch.randn_like(x.float()).mul(1e-3).bfloat16()  # break most bf16 ties
+    assert native_ok(x)
+    xa = x.detach().requires_grad_()
+    xb = x.detach().float().requires_grad_()
+    ya = _MaxPool3s2.apply(xa)
+    yb = torch.nn.functional.max_pool2d(xb, 3, 2, 1)
+    assert ya.shape == yb.shape and ya.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(ya.float(), yb, rtol=0, atol=0)
+    g = torch.randn_like(yb).bfloat16().float()
+    ya.backward(g.bfloat16().contiguous(memory_format=torch.channels_last))
+    yb.backward(g)
+    # the kernel rounds each input gradient (a sum of <= 4 window gradients) to bf16 once: compare against the
+    # fp32 reference rounded the same way. Positions that are an exact bf16 tie may route to a different tap
+    # than PyTorch's, so require exact equality almost everywhere rather than everywhere.
+    ref = xb.grad.bfloat16().float()
+    same = xa.grad.float() == ref
+    assert same.float().mean() > 0.999, f"{(~same).sum().item()} of {same.numel()} input gradients differ"
