@@ -112,3 +112,27 @@ def test_n19_privacy_analysis_and_dpsgd(capsys):
     assert "satisfies differential privacy with eps = 2.49 and delta = 1e-05." in out
     assert r["opt_order"] == 7.0
     assert r["train"] is not None
+
+
+def test_n01_explore_cluster_after_a_run(tmp_path):
+    _load("n08_simple_kfp_pipeline").main(["--workdir", str(tmp_path)])
+    r = _load("n01_explore_cluster").main(["--host", f"local://{tmp_path / 'kfp'}"])
+    assert len(r["runs"]) == 1 and r["runs"][0]["status"] == "Succeeded"
+    assert r["steps"] and all(p == "Succeeded" for p in r["steps"].values() if p)
+    assert r["logs"], "per-step logs of the local backend were not found"
+
+
+def test_n05_airflow_dag_written_and_triggered(tmp_path):
+    r = _load("n05_airflow_pipeline").main(["--workdir", str(tmp_path), "--rows", "600", "--train-steps", "20"])
+    src = open(r["dag_file"]).read()
+    compile(src, r["dag_file"], "exec")  # the generated Airflow DAG is valid Python
+    assert "schedule_interval=None" in src and "datetime.datetime(2019, 1, 1)" in src
+    assert src.count("BashOperator(") == 9  # the reference's 9-component taxi DAG
+    assert r["result"].succeeded
+
+
+def test_n09_upload_compiled_taxi_pipeline(tmp_path):
+    r = _load("n09_advanced_kfp_pipeline").main(["--workdir", str(tmp_path)])
+    assert [p["name"] for p in r["listed"]] == ["taxi-cab-classification-pipeline"]
+    names = {p["name"] for p in r["pipeline"].parameters}
+    assert {"output", "project", "column-names", "train", "evaluation"} <= names
