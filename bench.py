@@ -59,7 +59,7 @@ def _ranks_agree(tr) -> bool:
     return bool(torch.equal(hi, lo)) and bool(torch.isfinite(chk).all())
 
 
-def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, split_collective: bool = False):
+def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, capture_collective: bool = False):
     def build():
         model = WideDeepModel(seed=0)
         if device.type == "cuda":
@@ -76,11 +76,14 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, sp
     tr = build()
     if not (graph and device.type == "cuda"):
         return tr
-    # Multi-rank over RCCL: the all-reduce is captured INTO the step's hipGraph (one replay per step).
-    # Measured on one MI355X with the DP code path forced (tools/dp_step_overhead.py): split-phase step
-    # (graph, eager all-reduce, graph) 67.4 us at B=65536 (host 41.6 us) vs 51.2 us captured; B=40: 37.7 vs
-    # 22.5 us. Guard: after two replays every rank must hold bit-identical weights, else fall back.
-    captured = pg is not None and not split_collective and torch.distributed.get_backend(pg) == "nccl"
+    # Multi-rank over RCCL, default: split-phase step (graph: fused fwd/bwd + slab reduce; eager RCCL all-reduce
+    # of the flat gradient; graph: optimizer). --capture-collective captures the all-reduce INTO the step's
+    # hipGraph (one replay per step). Measured on one MI355X with the DP code path forced
+    # (tools/dp_step_overhead.py): split-phase 67.4 us at B=65536 vs 51.2 us captured; B=40: 37.7 vs 22.5 us.
+    # The captured variant stays opt-in until it has run on a multi-GPU node (only 1-GPU boxes were available
+    # to validate it); its guard: after two replays every rank must hold bit-identical weights, else the
+    # trainer (and its HBM-resident data) is released and a split-phase one is built instead.
+    captured = pg is not None and capture_collective and torch.distributed.get_backend(pg) == "nccl"
     tr.capture(include_collective=captured)
     tr.collective_in_graph = captured
     if captured:
@@ -90,6 +93,9 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, sp
         if not _ranks_agree(tr):
             print("[bench] captured all-reduce: ranks disagree, falling back to split-phase graphs",
                   file=sys.stderr, flush=True)
+            del tr
+            torch.cuda.synchronize(device)
+            torch.cuda.empty_cache()
             tr = build()
             tr.capture(include_collective=False)
             tr.collective_in_graph = False
@@ -107,8 +113,9 @@ def main(argv=None) -> int:
     ap.add_argument("--ref-steps", type=int, default=2000)
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--split-collective", action="store_true",
-                    help="multi-rank: eager all-reduce between two graphs instead of capturing it")
+    ap.add_argument("--capture-collective", action="store_true",
+                    help="multi-rank: capture the RCCL all-reduce inside the step's hipGraph (default: split-phase, "
+                         "eager all-reduce between two graphs)")
     a = ap.parse_args(argv)
 
     env = mdist.init()
@@ -124,7 +131,7 @@ def main(argv=None) -> int:
     n = env.world_size
 
     tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph,
-                      a.split_collective)
+                      a.capture_collective)
     collective_in_graph = bool(getattr(tr, "collective_in_graph", False))
     dt = mdist.max_over_ranks(run(tr, a.steps, a.warmup, device), device if use_cuda else None)
     loss = tr.last_loss() / a.batch_per_gpu
@@ -133,7 +140,10 @@ def main(argv=None) -> int:
     ref = None
     if a.ref_batch:
         del tr
-        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.split_collective)
+        if use_cuda:
+            torch.cuda.synchronize(device)
+            torch.cuda.empty_cache()
+        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.capture_collective)
         dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
                "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps}

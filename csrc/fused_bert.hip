@@ -75,16 +75,63 @@ __device__ __forceinline__ void stv(T* p, const float* v) {
   *(Pack<T, N>*)p = pk;
 }
 
-// ---- vectorised LayerNorm (H % 256 == 0): lane owns NC chunks of 4 contiguous columns,
-// chunk j of lane l = columns [4 (64 j + l), +4) -> every access is one 8/16-byte load per lane
+// ---- dropout mask: counter-based, recomputed in the backward (nothing stored) and hipGraph-replay safe.
+// rng points at device int64 [seed, step counter]; the counter is advanced by an in-graph op once per step,
+// so replays draw fresh masks without any host-side state. A 64-bit finaliser (murmur3 fmix64) of
+// (seed, counter, site) gives the per-call key; each group of 4 consecutive elements (flat index 4g..4g+3)
+// takes the four 16-bit lanes of mix64(key + g * golden) and keeps element e iff lane_e >= thr
+// (thr = round(p * 65536)). The same bits are produced by mifx.ops.fused_bert._keep_mask_cpu, so CPU and GPU
+// runs of a model draw identical masks, and every tensor-parallel rank (same seed) draws the same mask for a
+// replicated activation.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z ^= z >> 33;
+  z *= 0xff51afd7ed558ccdULL;
+  z ^= z >> 33;
+  z *= 0xc4ceb9fe1a85ec53ULL;
+  z ^= z >> 33;
+  return z;
+}
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
+
+__device__ __forceinline__ uint64_t drop_key(const int64_t* rng, int site) {
+  return mix64((uint64_t)rng[0] ^ mix64((uint64_t)rng[1] * kGolden + (uint64_t)site));
+}
+__device__ __forceinline__ uint32_t keep4(uint64_t key, uint64_t g, uint32_t thr) {
+  const uint64_t h = mix64(key + g * kGolden);
+  return (uint32_t)((h & 0xffff) >= thr) | ((uint32_t)(((h >> 16) & 0xffff) >= thr) << 1) |
+         ((uint32_t)(((h >> 32) & 0xffff) >= thr) << 2) | ((uint32_t)((h >> 48) >= thr) << 3);
+}
+
+// Drop: the optional (bias, dropout) prologue of the fused LayerNorm: s = keep ? (a + bias) * scale : 0, + r.
+// thr == 0 disables dropout (no hashing); bias == nullptr disables the bias.
+template <typename P>
+struct Drop {
+  const P* bias;
+  const int64_t* rng;
+  int site;
+  uint32_t thr;
+  float scale;
+};
+
+// ---- vectorised fused [bias +] [dropout +] residual-add + LayerNorm (H % 256 == 0): lane owns NC chunks of
+// 4 contiguous columns, chunk j of lane l = columns [4 (64 j + l), +4) -> every access is one 8/16-byte load
 template <typename T, typename P, int NC>
 __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a, const T* __restrict__ r,
                                                         const P* __restrict__ w, const P* __restrict__ b,
-                                                        int R, float eps, T* __restrict__ y,
+                                                        Drop<P> dp, int R, float eps, T* __restrict__ y,
                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out) {
   constexpr int H = NC * 256;
   const int lane = threadIdx.x & 63;
   const int wpb = kThreads / 64;
+  float bias[NC][4];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    if (dp.bias != nullptr)
+      ldv<P, 4>(dp.bias + 4 * (64 * j + lane), bias[j]);
+    else
+      bias[j][0] = bias[j][1] = bias[j][2] = bias[j][3] = 0.f;
+  }
+  const uint64_t key = dp.thr ? drop_key(dp.rng, dp.site) : 0;
   for (int row = blockIdx.x * wpb + (threadIdx.x >> 6); row < R; row += gridDim.x * wpb) {
     const size_t base = (size_t)row * H;
     float v[NC][4];
@@ -95,9 +142,11 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
       float t[4];
       ldv<T, 4>(a + base + c, v[j]);
       ldv<T, 4>(r + base + c, t);
+      const uint32_t k = dp.thr ? keep4(key, (base + c) >> 2, dp.thr) : 0xf;
+      const float sc = dp.thr ? dp.scale : 1.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[j][e] += t[e];
+        v[j][e] = ((k >> e) & 1 ? (v[j][e] + bias[j][e]) * sc : 0.f) + t[e];
         s += v[j][e];
       }
     }
@@ -128,27 +177,39 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
   }
 }
 
+// backward: recomputes s (bias, mask, residual) and x_hat; ds = rstd (g - mean(g) - x_hat mean(g x_hat)),
+// g = dy w. dr = ds; da = keep ? ds * scale : 0 (only written when da != dr, i.e. bias or dropout present).
+// Column partials (LayerNorm dw, db and the bias gradient = column sums of da) per block, fixed order.
 template <typename T, typename P, int NC>
 __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ dy, const T* __restrict__ a,
                                                         const T* __restrict__ r, const P* __restrict__ w,
-                                                        const float* __restrict__ mean_in,
+                                                        Drop<P> dp, const float* __restrict__ mean_in,
                                                         const float* __restrict__ rstd_in, int R,
-                                                        T* __restrict__ dx, float* __restrict__ dw_part,
-                                                        float* __restrict__ db_part) {
+                                                        T* __restrict__ dr, T* __restrict__ da,
+                                                        float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                        float* __restrict__ dbias_part) {
   constexpr int H = NC * 256;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wpb = kThreads / 64;
-  float dw[NC][4], db[NC][4], wreg[NC][4];
+  float dw[NC][4], db[NC][4], dbi[NC][4], wreg[NC][4], bias[NC][4];
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
     ldv<P, 4>(w + 4 * (64 * j + lane), wreg[j]);
+    if (dp.bias != nullptr)
+      ldv<P, 4>(dp.bias + 4 * (64 * j + lane), bias[j]);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dw[j][e] = db[j][e] = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      dw[j][e] = db[j][e] = dbi[j][e] = 0.f;
+      if (dp.bias == nullptr) bias[j][e] = 0.f;
+    }
   }
+  const uint64_t key = dp.thr ? drop_key(dp.rng, dp.site) : 0;
+  const float sc = dp.thr ? dp.scale : 1.f;
   for (int row = blockIdx.x * wpb + wv; row < R; row += gridDim.x * wpb) {
     const size_t base = (size_t)row * H;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float xh[NC][4], g[NC][4];
+    uint32_t kp[NC];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
@@ -157,9 +218,11 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ d
       ldv<T, 4>(dy + base + c, d);
       ldv<T, 4>(a + base + c, av);
       ldv<T, 4>(r + base + c, rv);
+      kp[j] = dp.thr ? keep4(key, (base + c) >> 2, dp.thr) : 0xf;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        xh[j][e] = (av[e] + rv[e] - mean) * rstd;
+        const float sv = ((kp[j] >> e) & 1 ? (av[e] + bias[j][e]) * sc : 0.f) + rv[e];
+        xh[j][e] = (sv - mean) * rstd;
         g[j][e] = d[e] * wreg[j][e];
         dw[j][e] += d[e] * xh[j][e];
         db[j][e] += d[e];
@@ -170,42 +233,58 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ d
     const float mg = wave_sum(sg) * (1.f / H), mgx = wave_sum(sgx) * (1.f / H);
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      float o[4];
+      const int c = 4 * (64 * j + lane);
+      float o[4], oa[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - mg - xh[j][e] * mgx);
-      stv<T, 4>(dx + base + 4 * (64 * j + lane), o);
+      for (int e = 0; e < 4; ++e) {
+        o[e] = rstd * (g[j][e] - mg - xh[j][e] * mgx);
+        oa[e] = (kp[j] >> e) & 1 ? o[e] * sc : 0.f;
+        dbi[j][e] += cvt_round<T>(oa[e]);  // bias grad of the value actually stored
+      }
+      stv<T, 4>(dr + base + c, o);
+      if (da != dr) stv<T, 4>(da + base + c, oa);
     }
   }
-  // combine the 4 waves' column partials: LDS image [wave][H] x2, then each thread sums its
+  // combine the 4 waves' column partials: LDS image [wave][H] x3, then each thread sums its
   // H/256 columns over the waves in a fixed order -> one partial row per block
   __shared__ float sdw[kThreads / 64][H];
   __shared__ float sdb[kThreads / 64][H];
+  __shared__ float sdi[kThreads / 64][H];
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
     const int c = 4 * (64 * j + lane);
     *(float4*)&sdw[wv][c] = make_float4(dw[j][0], dw[j][1], dw[j][2], dw[j][3]);
     *(float4*)&sdb[wv][c] = make_float4(db[j][0], db[j][1], db[j][2], db[j][3]);
+    *(float4*)&sdi[wv][c] = make_float4(dbi[j][0], dbi[j][1], dbi[j][2], dbi[j][3]);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < H; c += kThreads) {
-    float tw = 0.f, tb = 0.f;
+    float tw = 0.f, tb = 0.f, ti = 0.f;
 #pragma unroll
     for (int i = 0; i < wpb; ++i) {
       tw += sdw[i][c];
       tb += sdb[i][c];
+      ti += sdi[i][c];
     }
     dw_part[(size_t)blockIdx.x * H + c] = tw;
     db_part[(size_t)blockIdx.x * H + c] = tb;
+    if (dbias_part != nullptr) dbias_part[(size_t)blockIdx.x * H + c] = ti;
   }
+}
+
+// scalar-path mask bit of flat element idx
+__device__ __forceinline__ bool keep1(uint64_t key, uint64_t idx, uint32_t thr) {
+  return (keep4(key, idx >> 2, thr) >> (idx & 3)) & 1;
 }
 
 template <typename T, typename P, int PER>
 __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, const T* __restrict__ r,
-                                                      const P* __restrict__ w, const P* __restrict__ b, int R,
-                                                      int H, float eps, T* __restrict__ y, float* __restrict__ mean_out,
-                                                      float* __restrict__ rstd_out) {
+                                                      const P* __restrict__ w, const P* __restrict__ b, Drop<P> dp,
+                                                      int R, int H, float eps, T* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out) {
   const int lane = threadIdx.x & 63;
   const int wpb = kThreads / 64;
+  const uint64_t key = dp.thr ? drop_key(dp.rng, dp.site) : 0;
   for (int row = blockIdx.x * wpb + (threadIdx.x >> 6); row < R; row += gridDim.x * wpb) {
     const size_t base = (size_t)row * H;
     float v[PER];
@@ -213,7 +292,13 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, 
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int c = lane + k * 64;
-      v[k] = c < H ? ld(a + base + c) + ld(r + base + c) : 0.f;
+      if (c < H) {
+        float x = ld(a + base + c) + (dp.bias != nullptr ? ld(dp.bias + c) : 0.f);
+        if (dp.thr) x = keep1(key, base + c, dp.thr) ? x * dp.scale : 0.f;
+        v[k] = x + ld(r + base + c);
+      } else {
+        v[k] = 0.f;
+      }
       s += v[k];
     }
     const float mean = wave_sum(s) / H;
@@ -239,27 +324,37 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, 
 
 template <typename T, typename P, int PER>
 __global__ __launch_bounds__(kThreads) void add_ln_bwd(const T* __restrict__ dy, const T* __restrict__ a,
-                                                      const T* __restrict__ r, const P* __restrict__ w,
+                                                      const T* __restrict__ r, const P* __restrict__ w, Drop<P> dp,
                                                       const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, int R, int H,
-                                                      T* __restrict__ dx, float* __restrict__ dw_part,
-                                                      float* __restrict__ db_part) {
+                                                      T* __restrict__ dr, T* __restrict__ da,
+                                                      float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                      float* __restrict__ dbias_part) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wpb = kThreads / 64;
-  float dw[PER], db[PER];
+  const uint64_t key = dp.thr ? drop_key(dp.rng, dp.site) : 0;
+  const float sc = dp.thr ? dp.scale : 1.f;
+  float dw[PER], db[PER], dbi[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) dw[k] = db[k] = 0.f;
+  for (int k = 0; k < PER; ++k) dw[k] = db[k] = dbi[k] = 0.f;
   for (int row = blockIdx.x * wpb + wv; row < R; row += gridDim.x * wpb) {
     const size_t base = (size_t)row * H;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float xh[PER], g[PER];
+    bool kp[PER];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int c = lane + k * 64;
+      kp[k] = true;
       if (c < H) {
         const float d = ld(dy + base + c);
-        xh[k] = (ld(a + base + c) + ld(r + base + c) - mean) * rstd;
+        float x = ld(a + base + c) + (dp.bias != nullptr ? ld(dp.bias + c) : 0.f);
+        if (dp.thr) {
+          kp[k] = keep1(key, base + c, dp.thr);
+          x = kp[k] ? x * sc : 0.f;
+        }
+        xh[k] = (x + ld(r + base + c) - mean) * rstd;
         g[k] = d * ld(w + c);
         dw[k] += d * xh[k];
         db[k] += d;
@@ -273,30 +368,57 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd(const T* __restrict__ dy,
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int c = lane + k * 64;
-      if (c < H) st(dx + base + c, rstd * (g[k] - mg - xh[k] * mgx));
+      if (c < H) {
+        const float o = rstd * (g[k] - mg - xh[k] * mgx);
+        const float oa = kp[k] ? o * sc : 0.f;
+        dbi[k] += cvt_round<T>(oa);
+        st(dr + base + c, o);
+        if (da != dr) st(da + base + c, oa);
+      }
     }
   }
   // combine the 4 waves' column partials in LDS, one row of partials per block
   __shared__ float sdw[kThreads / 64][64];
   __shared__ float sdb[kThreads / 64][64];
+  __shared__ float sdi[kThreads / 64][64];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     sdw[wv][lane] = dw[k];
     sdb[wv][lane] = db[k];
+    sdi[wv][lane] = dbi[k];
     __syncthreads();
     if (wv == 0) {
       const int c = lane + k * 64;
-      float tw = 0.f, tb = 0.f;
+      float tw = 0.f, tb = 0.f, ti = 0.f;
       for (int i = 0; i < wpb; ++i) {
         tw += sdw[i][lane];
         tb += sdb[i][lane];
+        ti += sdi[i][lane];
       }
       if (c < H) {
         dw_part[(size_t)blockIdx.x * H + c] = tw;
         db_part[(size_t)blockIdx.x * H + c] = tb;
+        if (dbias_part != nullptr) dbias_part[(size_t)blockIdx.x * H + c] = ti;
       }
     }
     __syncthreads();
+  }
+}
+
+// standalone dropout (the embedding-LayerNorm output and the pooled output): y = keep ? x * scale : 0 with the
+// same mask function; the backward is the same kernel applied to dy. One group of 4 elements per thread.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void dropout_k(const T* __restrict__ x, long long n, const int64_t* rng,
+                                                     int site, uint32_t thr, float scale, T* __restrict__ y) {
+  const uint64_t key = drop_key(rng, site);
+  const long long groups = (n + 3) >> 2;
+  for (long long g = (long long)blockIdx.x * kThreads + threadIdx.x; g < groups; g += (long long)gridDim.x * kThreads) {
+    const uint32_t k = keep4(key, (uint64_t)g, thr);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * g + e;
+      if (i < n) st(y + i, (k >> e) & 1 ? ld(x + i) * scale : 0.f);
+    }
   }
 }
 
@@ -523,66 +645,79 @@ __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict_
   if (o1 != nullptr) st(o1 + col, b);
 }
 
+// one launch description for the fused [bias +] [dropout +] residual-add + LayerNorm, forward or backward
+struct LnArgs {
+  int fwd;
+  const void *dy, *a, *r, *w, *b, *bias;
+  const int64_t* rng;
+  int site;
+  uint32_t thr;
+  float scale;
+  int R, H;
+  float eps;
+  void *out, *da;  // fwd: y; bwd: dr (out) and da
+  float *mean, *rstd, *dw_part, *db_part, *dbias_part;
+  int blocks;
+  hipStream_t st;
+};
+
 template <typename T, typename P, int PER>
-int launch_add_ln(int fwd, const void* dy, const void* a, const void* r, const void* w, const void* b, int R, int H,
-                  float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
-                  hipStream_t st) {
-  if (fwd)
-    hipLaunchKernelGGL((add_ln_fwd<T, P, PER>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r,
-                       (const P*)w, (const P*)b, R, H, eps, (T*)out, mean, rstd);
+int launch_add_ln(const LnArgs& x) {
+  const Drop<P> dp{(const P*)x.bias, x.rng, x.site, x.thr, x.scale};
+  if (x.fwd)
+    hipLaunchKernelGGL((add_ln_fwd<T, P, PER>), dim3(x.blocks), dim3(kThreads), 0, x.st, (const T*)x.a, (const T*)x.r,
+                       (const P*)x.w, (const P*)x.b, dp, x.R, x.H, x.eps, (T*)x.out, x.mean, x.rstd);
   else
-    hipLaunchKernelGGL((add_ln_bwd<T, P, PER>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
-                       (const T*)r, (const P*)w, mean, rstd, R, H, (T*)out, dw_part, db_part);
+    hipLaunchKernelGGL((add_ln_bwd<T, P, PER>), dim3(x.blocks), dim3(kThreads), 0, x.st, (const T*)x.dy, (const T*)x.a,
+                       (const T*)x.r, (const P*)x.w, dp, x.mean, x.rstd, x.R, x.H, (T*)x.out, (T*)x.da, x.dw_part,
+                       x.db_part, x.dbias_part);
   return (int)hipGetLastError();
 }
 
 template <typename T, typename P, int NC>
-int launch_add_ln_v(int fwd, const void* dy, const void* a, const void* r, const void* w, const void* b, int R,
-                    float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
-                    hipStream_t st) {
-  if (fwd)
-    hipLaunchKernelGGL((add_ln_fwd_v<T, P, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)a, (const T*)r,
-                       (const P*)w, (const P*)b, R, eps, (T*)out, mean, rstd);
+int launch_add_ln_v(const LnArgs& x) {
+  const Drop<P> dp{(const P*)x.bias, x.rng, x.site, x.thr, x.scale};
+  if (x.fwd)
+    hipLaunchKernelGGL((add_ln_fwd_v<T, P, NC>), dim3(x.blocks), dim3(kThreads), 0, x.st, (const T*)x.a,
+                       (const T*)x.r, (const P*)x.w, (const P*)x.b, dp, x.R, x.eps, (T*)x.out, x.mean, x.rstd);
   else
-    hipLaunchKernelGGL((add_ln_bwd_v<T, P, NC>), dim3(blocks), dim3(kThreads), 0, st, (const T*)dy, (const T*)a,
-                       (const T*)r, (const P*)w, mean, rstd, R, (T*)out, dw_part, db_part);
+    hipLaunchKernelGGL((add_ln_bwd_v<T, P, NC>), dim3(x.blocks), dim3(kThreads), 0, x.st, (const T*)x.dy,
+                       (const T*)x.a, (const T*)x.r, (const P*)x.w, dp, x.mean, x.rstd, x.R, (T*)x.out, (T*)x.da,
+                       x.dw_part, x.db_part, x.dbias_part);
   return (int)hipGetLastError();
 }
 
 template <typename T, typename P>
-int dispatch_add_ln(int fwd, const void* dy, const void* a, const void* r, const void* w, const void* b, int R,
-                    int H, float eps, void* out, float* mean, float* rstd, float* dw_part, float* db_part, int blocks,
-                    hipStream_t st) {
-  const uintptr_t al = (uintptr_t)dy | (uintptr_t)a | (uintptr_t)r | (uintptr_t)w | (uintptr_t)b | (uintptr_t)out;
-  switch (H % 256 == 0 && al % 16 == 0 ? H / 256 : 0) {  // vectorised paths (BERT-base 768 -> NC 3, large 1024 -> 4)
-    case 1: return launch_add_ln_v<T, P, 1>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-    case 2: return launch_add_ln_v<T, P, 2>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-    case 3: return launch_add_ln_v<T, P, 3>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-    case 4: return launch_add_ln_v<T, P, 4>(fwd, dy, a, r, w, b, R, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+int dispatch_add_ln(const LnArgs& x) {
+  const uintptr_t al = (uintptr_t)x.dy | (uintptr_t)x.a | (uintptr_t)x.r | (uintptr_t)x.w | (uintptr_t)x.b |
+                       (uintptr_t)x.bias | (uintptr_t)x.out | (uintptr_t)x.da;
+  switch (x.H % 256 == 0 && al % 16 == 0 ? x.H / 256 : 0) {  // vectorised paths (BERT-base 768 -> NC 3, large 1024 -> 4)
+    case 1: return launch_add_ln_v<T, P, 1>(x);
+    case 2: return launch_add_ln_v<T, P, 2>(x);
+    case 3: return launch_add_ln_v<T, P, 3>(x);
+    case 4: return launch_add_ln_v<T, P, 4>(x);
     default: break;
   }
-  const int per = (H + 63) / 64;
-  if (per <= 4)
-    return launch_add_ln<T, P, 4>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  if (per <= 12)
-    return launch_add_ln<T, P, 12>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  if (per <= 16)
-    return launch_add_ln<T, P, 16>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  return launch_add_ln<T, P, kMaxPer>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  const int per = (x.H + 63) / 64;
+  if (per <= 4) return launch_add_ln<T, P, 4>(x);
+  if (per <= 12) return launch_add_ln<T, P, 12>(x);
+  if (per <= 16) return launch_add_ln<T, P, 16>(x);
+  return launch_add_ln<T, P, kMaxPer>(x);
 }
 
 // (activation dtype, parameter dtype) -> dispatch_add_ln<T, P>; dtype / pdt: 0 fp32, 1 bf16
-int dispatch_add_ln_any(int dtype, int pdt, int fwd, const void* dy, const void* a, const void* r, const void* w,
-                        const void* b, int R, int H, float eps, void* out, float* mean, float* rstd, float* dw_part,
-                        float* db_part, int blocks, hipStream_t st) {
+int dispatch_add_ln_any(int dtype, int pdt, const LnArgs& x) {
   typedef __hip_bfloat16 bf;
-  if (dtype && pdt)
-    return dispatch_add_ln<bf, bf>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  if (dtype)
-    return dispatch_add_ln<bf, float>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  if (pdt)
-    return dispatch_add_ln<float, bf>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
-  return dispatch_add_ln<float, float>(fwd, dy, a, r, w, b, R, H, eps, out, mean, rstd, dw_part, db_part, blocks, st);
+  if (dtype && pdt) return dispatch_add_ln<bf, bf>(x);
+  if (dtype) return dispatch_add_ln<bf, float>(x);
+  if (pdt) return dispatch_add_ln<float, bf>(x);
+  return dispatch_add_ln<float, float>(x);
+}
+
+uint32_t drop_threshold(float p) {
+  if (!(p > 0.f)) return 0;
+  const float t = p * 65536.f + 0.5f;
+  return t >= 65536.f ? 65536u : (uint32_t)t;
 }
 
 template <typename T, typename P>
@@ -639,32 +774,102 @@ int mifx_bert_ln_blocks(int R) {
 // rows of partials for bias_gelu_bwd
 int mifx_bert_gelu_chunks(int M) { return M < 16 ? 1 : (M / 16 < 512 ? M / 16 : 512); }
 
-// dtype: activations, pdt: gamma/beta (and dw/db): 0 fp32, 1 bf16
-int mifx_bert_add_ln_fwd(int dtype, int pdt, const void* a, const void* r, const void* w, const void* b, int R, int H,
-                         float eps, void* y, float* mean, float* rstd, hipStream_t st) {
-  if (H <= 0 || H > 64 * kMaxPer || R <= 0) return -1;
+// Fused y = LayerNorm(dropout_p(a [+ bias]) + r) * w + b, and its backward.
+// dtype: activations, pdt: gamma/beta/bias (and their gradients): 0 fp32, 1 bf16. bias may be null; p == 0
+// disables dropout (rng unused). rng: device int64 [seed, counter]; site distinguishes the call sites of a step.
+int mifx_bert_bdaln_fwd(int dtype, int pdt, const void* a, const void* bias, const void* r, const void* w,
+                        const void* b, int R, int H, float eps, float p, const int64_t* rng, int site, void* y,
+                        float* mean, float* rstd, hipStream_t st) {
+  if (H <= 0 || H > 64 * kMaxPer || R <= 0 || p < 0.f || p >= 1.f) return -1;
+  if (p > 0.f && rng == nullptr) return -1;
   const int need = (R + 3) / 4;
-  const int blocks = need < 4096 ? need : 4096;
-  return dispatch_add_ln_any(dtype, pdt, 1, nullptr, a, r, w, b, R, H, eps, y, mean, rstd, nullptr, nullptr, blocks,
-                             st);
+  LnArgs x{};
+  x.fwd = 1;
+  x.a = a;
+  x.r = r;
+  x.w = w;
+  x.b = b;
+  x.bias = bias;
+  x.rng = rng;
+  x.site = site;
+  x.thr = drop_threshold(p);
+  x.scale = 1.f / (1.f - p);
+  x.R = R;
+  x.H = H;
+  x.eps = eps;
+  x.out = y;
+  x.mean = mean;
+  x.rstd = rstd;
+  x.blocks = need < 4096 ? need : 4096;
+  x.st = st;
+  return dispatch_add_ln_any(dtype, pdt, x);
 }
 
-// scratch: dw_part / db_part [mifx_bert_ln_blocks(R), H]; outputs dw, db [H] in the parameter dtype
-int mifx_bert_add_ln_bwd(int dtype, int pdt, const void* dy, const void* a, const void* r, const void* w,
-                         const float* mean, const float* rstd, int R, int H, void* dx, float* dw_part, float* db_part,
-                         void* dw, void* db, hipStream_t st) {
-  if (H <= 0 || H > 64 * kMaxPer || R <= 0) return -1;
+// backward: dr = dL/dr, da = dL/da (da may alias dr when there is neither bias nor dropout), dw, db and dbias
+// ([H], parameter dtype; dbias only with a bias). scratch: part [3, mifx_bert_ln_blocks(R), H] fp32.
+int mifx_bert_bdaln_bwd(int dtype, int pdt, const void* dy, const void* a, const void* bias, const void* r,
+                        const void* w, const float* mean, const float* rstd, int R, int H, float p, const int64_t* rng,
+                        int site, void* dr, void* da, float* part, void* dw, void* db, void* dbias, hipStream_t st) {
+  if (H <= 0 || H > 64 * kMaxPer || R <= 0 || p < 0.f || p >= 1.f) return -1;
+  if (p > 0.f && rng == nullptr) return -1;
+  if ((p > 0.f || bias != nullptr) && da == dr) return -1;
   const int blocks = mifx_bert_ln_blocks(R);
-  const int rc = dispatch_add_ln_any(dtype, pdt, 0, dy, a, r, w, nullptr, R, H, 0.f, dx, (float*)mean, (float*)rstd,
-                                     dw_part, db_part, blocks, st);
+  LnArgs x{};
+  x.fwd = 0;
+  x.dy = dy;
+  x.a = a;
+  x.r = r;
+  x.w = w;
+  x.bias = bias;
+  x.rng = rng;
+  x.site = site;
+  x.thr = drop_threshold(p);
+  x.scale = 1.f / (1.f - p);
+  x.R = R;
+  x.H = H;
+  x.out = dr;
+  x.da = da;
+  x.mean = (float*)mean;
+  x.rstd = (float*)rstd;
+  x.dw_part = part;
+  x.db_part = part + (size_t)blocks * H;
+  x.dbias_part = bias != nullptr ? part + 2 * (size_t)blocks * H : nullptr;
+  x.blocks = blocks;
+  x.st = st;
+  const int rc = dispatch_add_ln_any(dtype, pdt, x);
   if (rc) return rc;
   const dim3 g((H + kRedCols - 1) / kRedCols);
-  if (pdt)
-    hipLaunchKernelGGL(col_reduce2<__hip_bfloat16>, g, dim3(kThreads), 0, st, dw_part, db_part, blocks, H,
-                       (__hip_bfloat16*)dw, (__hip_bfloat16*)db);
-  else
-    hipLaunchKernelGGL(col_reduce2<float>, g, dim3(kThreads), 0, st, dw_part, db_part, blocks, H, (float*)dw,
+  typedef __hip_bfloat16 bf;
+  if (pdt) {
+    hipLaunchKernelGGL(col_reduce2<bf>, g, dim3(kThreads), 0, st, x.dw_part, x.db_part, blocks, H, (bf*)dw, (bf*)db);
+    if (bias != nullptr)
+      hipLaunchKernelGGL(col_reduce2<bf>, g, dim3(kThreads), 0, st, x.dbias_part, nullptr, blocks, H, (bf*)dbias,
+                         (bf*)nullptr);
+  } else {
+    hipLaunchKernelGGL(col_reduce2<float>, g, dim3(kThreads), 0, st, x.dw_part, x.db_part, blocks, H, (float*)dw,
                        (float*)db);
+    if (bias != nullptr)
+      hipLaunchKernelGGL(col_reduce2<float>, g, dim3(kThreads), 0, st, x.dbias_part, nullptr, blocks, H,
+                         (float*)dbias, (float*)nullptr);
+  }
+  return (int)hipGetLastError();
+}
+
+// y = keep ? x * 1/(1-p) : 0 over n elements (dtype 0 fp32, 1 bf16); the backward is the same call on dy
+int mifx_bert_dropout(int dtype, const void* x, long long n, float p, const int64_t* rng, int site, void* y,
+                      hipStream_t st) {
+  if (n <= 0 || p <= 0.f || p >= 1.f || rng == nullptr) return -1;
+  const long long groups = (n + 3) / 4;
+  const long long need = (groups + kThreads - 1) / kThreads;
+  const int blocks = (int)(need < 2048 ? need : 2048);
+  const uint32_t thr = drop_threshold(p);
+  const float scale = 1.f / (1.f - p);
+  if (dtype)
+    hipLaunchKernelGGL(dropout_k<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st, (const __hip_bfloat16*)x, n,
+                       rng, site, thr, scale, (__hip_bfloat16*)y);
+  else
+    hipLaunchKernelGGL(dropout_k<float>, dim3(blocks), dim3(kThreads), 0, st, (const float*)x, n, rng, site, thr, scale,
+                       (float*)y);
   return (int)hipGetLastError();
 }
 

@@ -31,6 +31,8 @@ class BertConfig:
     max_position: int = 512
     type_vocab: int = 2
     dropout: float = 0.1
+    attn_dropout: float | None = None  # attention-probability dropout (None: same as dropout)
+    dropout_seed: int = 1234  # hidden-dropout mask seed (identical on every TP rank)
     num_labels: int = 2
     ln_eps: float = 1e-12
     init_std: float = 0.02
@@ -73,20 +75,28 @@ class BertLayer(nn.Module):
         for n in ("ln1", "ln2"):
             getattr(self, n).load_state_dict({"weight": sd[f"{prefix}{n}.weight"], "bias": sd[f"{prefix}{n}.bias"]})
 
-    def forward(self, x, mask):
+    def forward(self, x, mask, rng=None, site=0):
+        """Dropout RNG: attention-probability dropout runs inside SDPA on this rank's own heads with the torch
+        generator (per-rank stream: its offset use differs with the uneven head split and never reaches the
+        replicated activations); the hidden dropouts act on REPLICATED activations (every TP rank holds the
+        same [B, S, H] tensor) and use the counter-based mask of fb.bias_dropout_add_layernorm keyed by
+        (model seed, step counter, site) — identical on all TP ranks by construction, fused with the row-parallel
+        bias, the residual add and the LayerNorm. Sites `site` and `site + 1`."""
         B, S, _ = x.shape
         h, d = self.local_heads, self.head_dim
         # q/k/v as [B, h, S, d] views of the fused QKV output; unbind (not indexing a permuted view) so the
         # backward assembles dq/dk/dv with ONE stack copy instead of a zero-fill plus three slice copies
         q, k, v = (t.transpose(1, 2) for t in self.qkv(x).view(B, S, 3, h, d).unbind(2))
-        drop = self.cfg.dropout if self.training else 0.0
-        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=drop)
+        c = self.cfg
+        drop = c.dropout if self.training else 0.0
+        adrop = (c.dropout if c.attn_dropout is None else c.attn_dropout) if self.training else 0.0
+        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=adrop)
         ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
-        a = F.dropout(self.attn_out(ctx), drop, self.training)
-        x = fb.add_layernorm(a, x, self.ln1.weight, self.ln1.bias, self.cfg.ln_eps)
+        x = fb.bias_dropout_add_layernorm(self.attn_out(ctx, add_bias=False), self.attn_out.bias, x, self.ln1.weight,
+                                          self.ln1.bias, c.ln_eps, drop, rng, site)
         f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
-        f = F.dropout(self.ffn_out(f), drop, self.training)
-        return fb.add_layernorm(f, x, self.ln2.weight, self.ln2.bias, self.cfg.ln_eps)
+        return fb.bias_dropout_add_layernorm(self.ffn_out(f, add_bias=False), self.ffn_out.bias, x, self.ln2.weight,
+                                             self.ln2.bias, c.ln_eps, drop, rng, site + 1)
 
 
 class BertForSequenceClassification(nn.Module):
@@ -102,6 +112,8 @@ class BertForSequenceClassification(nn.Module):
         self.layers = nn.ModuleList([BertLayer(c, self.tp) for _ in range(c.layers)])
         self.pooler = nn.Linear(c.hidden, c.hidden)
         self.classifier = nn.Linear(c.hidden, c.num_labels)
+        # hidden-dropout RNG state [seed, step counter] (device int64; advanced in-graph once per training forward)
+        self.register_buffer("drop_rng", torch.tensor([c.dropout_seed, 0], dtype=torch.int64), persistent=False)
         if seed is not None:
             self.init_weights(seed)
 
@@ -122,14 +134,17 @@ class BertForSequenceClassification(nn.Module):
         pos = torch.arange(S, device=input_ids.device)
         tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
         x = self.word(input_ids) + fb.embedding(pos, self.pos.weight)[None] + fb.embedding(tt, self.tok_type.weight)
-        x = F.dropout(self.ln_emb(x), self.cfg.dropout, self.training)
+        drop = self.cfg.dropout if self.training else 0.0
+        if drop > 0:
+            self.drop_rng[1:].add_(1)  # new masks every step (captured into the step's hipGraph)
+        x = fb.dropout(self.ln_emb(x), drop, self.drop_rng, 0)
         mask = None
         if attention_mask is not None:  # additive mask [B, 1, 1, S]
             mask = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * torch.finfo(x.dtype).min
-        for layer in self.layers:
-            x = layer(x, mask)
+        for i, layer in enumerate(self.layers):
+            x = layer(x, mask, self.drop_rng, 1 + 2 * i)
         pooled = torch.tanh(self.pooler(x[:, 0]))
-        return self.classifier(F.dropout(pooled, self.cfg.dropout, self.training))
+        return self.classifier(fb.dropout(pooled, drop, self.drop_rng, 1 + 2 * len(self.layers)))
 
 
 def full_init_state(cfg: BertConfig, seed: int) -> dict:

@@ -1,4 +1,5 @@
-"""Fused residual-add + LayerNorm and bias + GELU (csrc/fused_bert.hip) as autograd functions.
+"""Fused [bias +] [dropout +] residual-add + LayerNorm, standalone dropout and bias + GELU
+(csrc/fused_bert.hip) as autograd functions.
 
 On CUDA/HIP tensors the native kernels run (required — no silent fallback); on CPU the PyTorch
 reference implementation of the same math runs."""
@@ -7,11 +8,12 @@ from __future__ import annotations
 import functools
 import os
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 from . import _lib
-from ._lib import F32, I32, VP, check, ptr, sig, stream_handle
+from ._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
 
 
 @functools.lru_cache(maxsize=None)
@@ -20,9 +22,11 @@ def _fns():
     return {
         "blocks": sig(lib, "mifx_bert_ln_blocks", [I32]),
         "gchunks": sig(lib, "mifx_bert_gelu_chunks", [I32]),
-        "ln_fwd": sig(lib, "mifx_bert_add_ln_fwd", [I32, I32, VP, VP, VP, VP, I32, I32, F32, VP, VP, VP, VP]),
-        "ln_bwd": sig(lib, "mifx_bert_add_ln_bwd", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, VP, VP, VP, VP, VP,
-                                                    VP]),
+        "ln_fwd": sig(lib, "mifx_bert_bdaln_fwd", [I32, I32, VP, VP, VP, VP, VP, I32, I32, F32, F32, VP, I32, VP, VP,
+                                                   VP, VP]),
+        "ln_bwd": sig(lib, "mifx_bert_bdaln_bwd", [I32, I32, VP, VP, VP, VP, VP, VP, VP, I32, I32, F32, VP, I32, VP,
+                                                   VP, VP, VP, VP, VP, VP]),
+        "dropout": sig(lib, "mifx_bert_dropout", [I32, VP, I64, F32, VP, I32, VP, VP]),
         "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
         "colsum": sig(lib, "mifx_bert_col_sum", [I32, I32, VP, I32, I32, VP, VP, VP]),
     }
@@ -42,39 +46,111 @@ def _param(p: torch.Tensor) -> torch.Tensor:
     return p.contiguous()
 
 
-class _AddLayerNorm(torch.autograd.Function):
+# ---- counter-based dropout masks (same bits as the HIP kernels in csrc/fused_bert.hip)
+_M64 = (1 << 64) - 1
+_GOLDEN = 0x9E3779B97F4A7C15
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    """murmur3 fmix64 on a uint64 array (wrapping arithmetic)."""
+    z = z ^ (z >> np.uint64(33))
+    z = z * np.uint64(0xFF51AFD7ED558CCD)
+    z = z ^ (z >> np.uint64(33))
+    z = z * np.uint64(0xC4CEB9FE1A85EC53)
+    return z ^ (z >> np.uint64(33))
+
+
+def drop_threshold(p: float) -> int:
+    """keep element iff its 16-bit hash lane >= threshold (float32 math, as the kernel computes it)."""
+    if not p > 0:
+        return 0
+    t = np.float32(p) * np.float32(65536.0) + np.float32(0.5)
+    return 65536 if t >= 65536 else int(t)
+
+
+def keep_mask(n: int, rng: torch.Tensor, site: int, p: float) -> torch.Tensor:
+    """Bool keep-mask of n flat elements for (rng = [seed, counter], site): the host twin of the kernels'
+    keep4(drop_key(rng, site), g, thr) — group g of 4 consecutive elements takes the four 16-bit lanes of
+    mix64(key + g * golden)."""
+    seed, ctr = (int(v) for v in rng.detach().cpu().tolist()[:2])
+    with np.errstate(over="ignore"):
+        inner = _mix64(np.array([(ctr * _GOLDEN + site) & _M64], dtype=np.uint64))
+        key = _mix64(np.array([seed & _M64], dtype=np.uint64) ^ inner)
+        g = np.arange((n + 3) // 4, dtype=np.uint64)
+        h = _mix64(key + g * np.uint64(_GOLDEN))
+    lanes = (h[:, None] >> np.array([0, 16, 32, 48], dtype=np.uint64)) & np.uint64(0xFFFF)
+    keep = (lanes >= np.uint64(drop_threshold(p))).reshape(-1)[:n]
+    return torch.from_numpy(keep)
+
+
+def _drop_scale(p: float) -> float:
+    return float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+
+
+class _BiasDropAddLN(torch.autograd.Function):
+    """y = LayerNorm(dropout_p(a [+ bias]) + r) * w + b in one HIP kernel (and one backward kernel producing
+    dr, da and the gamma / beta / bias gradients); the dropout mask is recomputed in the backward."""
+
     @staticmethod
-    def forward(ctx, a, r, w, b, eps):
+    def forward(ctx, a, bias, r, w, b, eps, p, rng, site):
         a, r = a.contiguous(), r.contiguous().to(a.dtype)
         H = a.shape[-1]
         R = a.numel() // H
-        wp, bp = _param(w), _param(b.to(_param(w).dtype))
+        wp = _param(w)
+        bp = _param(b.to(wp.dtype))
+        biasp = None if bias is None else _param(bias.to(wp.dtype))
         y = torch.empty_like(a)
         mean = torch.empty(R, device=a.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
-        check(_fns()["ln_fwd"](_dt(a), _dt(wp), ptr(a), ptr(r), ptr(wp), ptr(bp), R, H, float(eps), ptr(y), ptr(mean),
-                               ptr(rstd), stream_handle(a.device)), "mifx_bert_add_ln_fwd")
-        ctx.save_for_backward(a, r, wp, mean, rstd)
+        check(_fns()["ln_fwd"](_dt(a), _dt(wp), ptr(a), ptr(biasp), ptr(r), ptr(wp), ptr(bp), R, H, float(eps),
+                               float(p), ptr(rng if p > 0 else None), int(site), ptr(y), ptr(mean), ptr(rstd),
+                               stream_handle(a.device)), "mifx_bert_bdaln_fwd")
+        ctx.save_for_backward(a, r, wp, biasp, mean, rstd)
+        ctx.rng, ctx.p, ctx.site = rng, float(p), int(site)  # rng is advanced only between steps
         ctx.wdtype = w.dtype
+        ctx.bdtype = None if bias is None else bias.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        a, r, wp, mean, rstd = ctx.saved_tensors
+        a, r, wp, biasp, mean, rstd = ctx.saved_tensors
         dy = dy.contiguous().to(a.dtype)
         H = a.shape[-1]
         R = a.numel() // H
         nb = _fns()["blocks"](R)
-        dx = torch.empty_like(a)
-        part = torch.empty(2, nb, H, device=a.device, dtype=torch.float32)
+        dr = torch.empty_like(a)
+        da = torch.empty_like(a) if (ctx.p > 0 or biasp is not None) else dr
+        part = torch.empty(3, nb, H, device=a.device, dtype=torch.float32)
         dw = torch.empty(H, device=a.device, dtype=wp.dtype)  # written in the parameter dtype by the kernel
         db = torch.empty(H, device=a.device, dtype=wp.dtype)
-        check(_fns()["ln_bwd"](_dt(a), _dt(wp), ptr(dy), ptr(a), ptr(r), ptr(wp), ptr(mean), ptr(rstd), R, H,
-                               ptr(dx), ptr(part[0]), ptr(part[1]), ptr(dw), ptr(db), stream_handle(a.device)),
-              "mifx_bert_add_ln_bwd")
+        dbias = None if biasp is None else torch.empty(H, device=a.device, dtype=wp.dtype)
+        check(_fns()["ln_bwd"](_dt(a), _dt(wp), ptr(dy), ptr(a), ptr(biasp), ptr(r), ptr(wp), ptr(mean), ptr(rstd), R,
+                               H, ctx.p, ptr(ctx.rng if ctx.p > 0 else None), ctx.site, ptr(dr), ptr(da), ptr(part),
+                               ptr(dw), ptr(db), ptr(dbias), stream_handle(a.device)), "mifx_bert_bdaln_bwd")
         if wp.dtype != ctx.wdtype:
             dw, db = dw.to(ctx.wdtype), db.to(ctx.wdtype)
-        return dx, dx, dw, db, None
+        if dbias is not None and dbias.dtype != ctx.bdtype:
+            dbias = dbias.to(ctx.bdtype)
+        return da, dbias, dr, dw, db, None, None, None, None
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, rng, site):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        check(_fns()["dropout"](_dt(x), ptr(x), x.numel(), float(p), ptr(rng), int(site), ptr(y),
+                                stream_handle(x.device)), "mifx_bert_dropout")
+        ctx.rng, ctx.p, ctx.site = rng, float(p), int(site)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        check(_fns()["dropout"](_dt(dy), ptr(dy), dy.numel(), ctx.p, ptr(ctx.rng), ctx.site, ptr(dx),
+                                stream_handle(dy.device)), "mifx_bert_dropout")
+        return dx, None, None, None
 
 
 class _BiasGelu(torch.autograd.Function):
@@ -215,11 +291,36 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
 _TORCH_OPS = os.environ.get("MIFX_BERT_TORCH_OPS") == "1"
 
 
+def bias_dropout_add_layernorm(a: torch.Tensor, bias, r: torch.Tensor, weight, ln_bias, eps: float = 1e-12,
+                               p: float = 0.0, rng: torch.Tensor | None = None, site: int = 0) -> torch.Tensor:
+    """LayerNorm(dropout_p(a + bias) + r) * weight + ln_bias (bias optional; p > 0 needs rng = device int64
+    [seed, counter]). The mask depends only on (seed, counter, site, element index): every tensor-parallel rank
+    with the same seed drops the same elements of a replicated activation, and a captured hipGraph draws a new
+    mask per replay once the counter is advanced in-graph."""
+    if p > 0 and rng is None:
+        raise ValueError("dropout p > 0 needs an rng state tensor [seed, counter]")
+    if a.is_cuda and not _TORCH_OPS:
+        return _BiasDropAddLN.apply(a, bias, r, weight, ln_bias, eps, p, rng, site)
+    x = a if bias is None else a + bias.to(a.dtype)
+    if p > 0:
+        keep = keep_mask(x.numel(), rng, site, p).to(x.device).view(x.shape)
+        x = torch.where(keep, x * _drop_scale(p), torch.zeros((), dtype=x.dtype, device=x.device))
+    return F.layer_norm(x + r, (a.shape[-1],), weight, ln_bias, eps)
+
+
 def add_layernorm(a: torch.Tensor, r: torch.Tensor, weight, bias, eps: float = 1e-12) -> torch.Tensor:
     """LayerNorm(a + r) * weight + bias."""
-    if a.is_cuda and not _TORCH_OPS:
-        return _AddLayerNorm.apply(a, r, weight, bias, eps)
-    return F.layer_norm(a + r, (a.shape[-1],), weight, bias, eps)
+    return bias_dropout_add_layernorm(a, None, r, weight, bias, eps)
+
+
+def dropout(x: torch.Tensor, p: float, rng: torch.Tensor, site: int) -> torch.Tensor:
+    """Counter-based dropout with the same mask function as bias_dropout_add_layernorm."""
+    if not p > 0:
+        return x
+    if x.is_cuda and not _TORCH_OPS:
+        return _Dropout.apply(x, p, rng, site)
+    keep = keep_mask(x.numel(), rng, site, p).to(x.device).view(x.shape)
+    return torch.where(keep, x * _drop_scale(p), torch.zeros((), dtype=x.dtype, device=x.device))
 
 
 def bias_gelu(x: torch.Tensor, bias) -> torch.Tensor:

@@ -153,11 +153,13 @@ class RowParallelLinear(nn.Module):
             if self.bias is not None and bias is not None:
                 self.bias.copy_(bias)
 
-    def forward(self, x_shard):
+    def forward(self, x_shard, add_bias: bool = True):
+        """add_bias=False returns the reduced partial products only (the caller fuses the bias, e.g. into
+        fb.bias_dropout_add_layernorm)."""
         y = reduce_from_tp(F.linear(x_shard, self.weight), self.tp)
         # add the bias in the activation dtype (keeps a bf16 residual stream under autocast); its gradient
         # is a deterministic HIP column reduction on the GPU
-        return fb.bias_add(y, self.bias) if self.bias is not None else y
+        return fb.bias_add(y, self.bias) if (self.bias is not None and add_bias) else y
 
 
 class VocabParallelEmbedding(nn.Module):

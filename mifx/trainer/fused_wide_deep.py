@@ -178,9 +178,9 @@ class FusedWideDeepTrainer:
 
         Single rank: one graph. Multi-rank: by default two graphs (local grad, optimizer) with the
         all-reduce issued eagerly between them (works with any backend, e.g. gloo); `include_collective=True`
-        captures the RCCL all-reduce too -- one graph launch per step. bench.py uses the latter over RCCL:
-        on one MI355X with the DP path forced (tools/dp_step_overhead.py) the split-phase step costs
-        67.4 us vs 51.2 us captured at B=65536 (host 41.6 vs 11.4 us per step)."""
+        captures the RCCL all-reduce too -- one graph launch per step (bench.py --capture-collective; opt-in
+        until validated on a multi-GPU node). On one MI355X with the DP path forced (tools/dp_step_overhead.py)
+        the split-phase step costs 67.4 us vs 51.2 us captured at B=65536 (host 41.6 vs 11.4 us per step)."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

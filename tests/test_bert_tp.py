@@ -41,13 +41,21 @@ def _step(model, cfg, lr=0.1):
     return logits.detach()
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, cfg_kw=None, steps=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = BertConfig.tiny(dropout=0.0)
+    cfg = BertConfig.tiny(**(cfg_kw or {"dropout": 0.0}))
+    torch.manual_seed(100 + rank)  # per-rank torch generator streams: replicated dropout must not depend on them
     m = BertForSequenceClassification(cfg, TPGroup(), seed=1)
-    logits = _step(m, cfg)
+    for _ in range(steps):
+        logits = _step(m, cfg)
     full = gather_full_state(m)
+    # replicated parameters (LayerNorms, row-parallel biases, pos / token-type embeddings, pooler, classifier)
+    # as this rank holds them, to check they stayed bit-identical across the TP ranks
+    repl = {n: p.detach().clone() for n, p in m.named_parameters()
+            if not any(s in n for s in ("qkv.", "ffn_in.", "word.")) and not n.endswith(("attn_out.weight",
+                                                                                            "ffn_out.weight"))}
+    torch.save(repl, f"{out}.repl{rank}")
     if rank == 0:
         torch.save({"logits": logits, "state": full}, out)
     dist.destroy_process_group()
@@ -73,6 +81,96 @@ def test_tp_matches_single_process(world):
     ref_sd = gather_full_state(ref)
     for k, v in ref_sd.items():
         np.testing.assert_allclose(got["state"][k].numpy(), v.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+def test_tp_dropout_replicated_params_identical_and_match_tp1():
+    """Hidden dropout > 0 at TP=2 (gloo): the replicated activations' masks are keyed by (seed, step, site), not by
+    each rank's torch generator, so (a) replicated parameters stay bit-identical across ranks over several steps
+    and (b) with attention-probability dropout off the TP=2 trajectory equals TP=1 (same masks)."""
+    kw = {"dropout": 0.1, "attn_dropout": 0.0}
+    cfg = BertConfig.tiny(**kw)
+    ref = BertForSequenceClassification(cfg, None, seed=1)
+    for _ in range(3):
+        ref_logits = _step(ref, cfg)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_worker, args=(2, _port(), out, kw, 3), nprocs=2, start_method="spawn")
+        got = torch.load(out, weights_only=True)
+        r0 = torch.load(f"{out}.repl0", weights_only=True)
+        r1 = torch.load(f"{out}.repl1", weights_only=True)
+    assert len(r0) > 10 and r0.keys() == r1.keys()
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), f"replicated parameter {k} diverged across TP ranks"
+    torch.testing.assert_close(got["logits"], ref_logits, rtol=1e-4, atol=1e-5)
+    for k, v in gather_full_state(ref).items():
+        np.testing.assert_allclose(got["state"][k].numpy(), v.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
+
+
+def test_tp_attention_dropout_keeps_replicated_params_identical():
+    """With attention-probability dropout on too (per-rank torch generator on the local heads, uneven split at
+    TP=3), the replicated parameters still stay bit-identical across ranks."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_worker, args=(3, _port(), out, {"dropout": 0.1}, 2), nprocs=3, start_method="spawn")
+        reps = [torch.load(f"{out}.repl{r}", weights_only=True) for r in range(3)]
+    for k in reps[0]:
+        assert torch.equal(reps[0][k], reps[1][k]) and torch.equal(reps[0][k], reps[2][k]), k
+
+
+def test_counter_dropout_mask_cpu():
+    from mifx.ops import fused_bert as fb
+
+    rng = torch.tensor([7, 3], dtype=torch.int64)
+    m = fb.keep_mask(100_003, rng, 5, 0.1)
+    assert abs(1 - m.float().mean().item() - 0.1) < 0.005
+    assert torch.equal(m, fb.keep_mask(100_003, rng, 5, 0.1))  # deterministic
+    assert not torch.equal(m, fb.keep_mask(100_003, rng, 6, 0.1))  # per site
+    assert not torch.equal(m, fb.keep_mask(100_003, torch.tensor([7, 4]), 5, 0.1))  # per step
+    a, r = torch.randn(6, 32), torch.randn(6, 32)
+    bias, w, b = torch.randn(32), torch.randn(32), torch.randn(32)
+    y = fb.bias_dropout_add_layernorm(a, bias, r, w, b, 1e-5, 0.25, rng, 2)
+    keep = fb.keep_mask(a.numel(), rng, 2, 0.25).view(6, 32)
+    ref = torch.nn.functional.layer_norm(torch.where(keep, (a + bias) / 0.75, 0.0) + r, (32,), w, b, 1e-5)
+    torch.testing.assert_close(y, ref)
+    x = torch.randn(5, 9)
+    torch.testing.assert_close(fb.dropout(x, 0.5, rng, 1), torch.where(fb.keep_mask(45, rng, 1, 0.5).view(5, 9),
+                                                                      x * 2, 0.0))
+
+
+@pytest.mark.gpu
+def test_fused_bias_dropout_add_layernorm_gpu():
+    """HIP fused bias + dropout + residual + LayerNorm (fwd/bwd) and standalone dropout against the CPU
+    composition with the same counter-based mask (bit-identical keep pattern), fp32 / bf16, vectorised and
+    scalar H."""
+    from mifx.ops import fused_bert as fb
+
+    torch.manual_seed(3)
+    rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
+    for dtype, tol in ((torch.float32, 1e-5), (torch.bfloat16, 2e-2)):
+        for H in (64, 768, 1000):
+            a = torch.randn(29, 3, H, device="cuda", dtype=dtype, requires_grad=True)
+            r = torch.randn(29, 3, H, device="cuda", dtype=dtype, requires_grad=True)
+            bias, w, b = (torch.randn(H, device="cuda", requires_grad=True) for _ in range(3))
+            y = fb.bias_dropout_add_layernorm(a, bias, r, w, b, 1e-12, 0.1, rng, 4)
+            keep = fb.keep_mask(a.numel(), rng, 4, 0.1).cuda().view(a.shape)
+            a2, r2 = a.detach().float().requires_grad_(), r.detach().float().requires_grad_()
+            bias2, w2, b2 = (t.detach().clone().requires_grad_() for t in (bias, w, b))
+            ref = torch.nn.functional.layer_norm(torch.where(keep, (a2 + bias2) * fb._drop_scale(0.1), 0.0) + r2,
+                                                 (H,), w2, b2, 1e-12)
+            torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+            g = torch.randn_like(ref)
+            y.backward(g.to(dtype))
+            ref.backward(g)
+            assert torch.equal(a.grad == 0, ~keep) or dtype == torch.bfloat16  # dropped elements get no gradient
+            for got, want, sc in ((a.grad, a2.grad, 4), (r.grad, r2.grad, 4), (w.grad, w2.grad, 40),
+                                  (b.grad, b2.grad, 40), (bias.grad, bias2.grad, 40)):
+                torch.testing.assert_close(got.float(), want, rtol=tol * 4, atol=tol * sc)
+        x = torch.randn(1001, 7, device="cuda", dtype=dtype, requires_grad=True)
+        y = fb.dropout(x, 0.3, rng, 9)
+        keep = fb.keep_mask(x.numel(), rng, 9, 0.3).cuda().view(x.shape)
+        torch.testing.assert_close(y, torch.where(keep, x * fb._drop_scale(0.3), 0.0).to(dtype))
+        y.backward(torch.ones_like(y))
+        torch.testing.assert_close(x.grad, torch.where(keep, fb._drop_scale(0.3), 0.0).to(dtype))
 
 
 @pytest.mark.gpu

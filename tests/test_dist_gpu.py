@@ -63,7 +63,7 @@ def test_fused_dp_two_ranks_matches_single():
 
 @pytest.mark.gpu
 def test_captured_rccl_allreduce_step_matches_split_phase():
-    """bench.py captures the RCCL all-reduce inside the step's hipGraph at N>1. On one GPU (1-rank RCCL
+    """bench.py --capture-collective captures the RCCL all-reduce inside the step's hipGraph at N>1. On one GPU (1-rank RCCL
     group, trainer forced onto its data-parallel path) the captured step must produce exactly the weights
     of the split-phase step (graph, eager all-reduce, graph)."""
     from mifx.data.synthetic import synthetic_records
