@@ -13,7 +13,8 @@
 // 3 + 5 activation passes instead of MIOpen's 5 + 8 with the unfused ReLU. The activation is
 // viewed as [M = N*H*W, C] (channels_last memory): a thread owns 8 consecutive channels (one
 // 16-byte bf16 load), C/8 threads cover a row, 256/(C/8) rows are in flight per block. Partial
-// sums are per block (fp32, fixed order) and combined in fp64 in a fixed order by the finalize
+// sums of the shifted values x - K_c (K_c = the channel's row-0 value, so large means do not cancel)
+// are per block (fp32, fixed order) and combined in fp64 in a fixed order by the finalize
 // kernels -> bitwise deterministic, no atomics. The ReLU mask is recomputed in backward with the
 // same fused multiply-add as forward, so it matches the forward output exactly.
 #include <hip/hip_bf16.h>
@@ -91,7 +92,8 @@ __device__ __forceinline__ void load_sum(const T* x, const T* x2, T* s_out, size
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, const T* __restrict__ x2,
                                                     T* __restrict__ s_out, long long M, int C,
-                                                    float* __restrict__ psum, float* __restrict__ psq) {
+                                                    float* __restrict__ psum, float* __restrict__ psq,
+                                                    float* __restrict__ kout) {
   __shared__ float s1[kThreads * kVec];
   __shared__ float s2[kThreads * kVec];
   const int tpr = C / kVec, rpb = kThreads / tpr;
@@ -101,13 +103,38 @@ __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, co
   float a[kVec] = {}, q[kVec] = {};
   if (slice < rpb) {
     const size_t c0 = (size_t)cg * kVec;
+    // Shifted sums: accumulate d = x - K_c with K_c = row 0's (stored) value of the channel, the same for every
+    // block. |mean - K| is of the order of the channel's std, so sum d^2 stays well conditioned in fp32 even
+    // when the mean dwarfs the std (e.g. residual sums); finalize recovers mean = K + S/M, var = Q/M - (S/M)^2
+    // in fp64. Block 0 hands K to finalize through the mean slot of the stats output.
+    float ks[kVec];
+    {
+      ldv(x + c0, ks);
+      if (x2 != nullptr) {
+        float v[kVec];
+        ldv(x2 + c0, v);
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          const T t = cvt<T>(ks[e] + v[e]);
+          ks[e] = ld(&t);
+        }
+      }
+    }
+    if (blockIdx.x == 0 && slice == 0) {
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) kout[c0 + e] = ks[e];
+    }
     int r = r0 + slice;
     // four rows in flight per thread: at 512 workgroups x 256 threads that is ~8 MB of loads in flight,
     // enough to cover HBM latency (two rows ran at ~half the bandwidth of the apply pass)
     for (; r + 3 * rpb < r1; r += 4 * rpb) {
       float u[4][kVec];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) load_sum(x, x2, s_out, (size_t)(r + k * rpb) * C + c0, u[k]);
+      for (int k = 0; k < 4; ++k) {
+        load_sum(x, x2, s_out, (size_t)(r + k * rpb) * C + c0, u[k]);
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) u[k][e] -= ks[e];
+      }
 #pragma unroll
       for (int e = 0; e < kVec; ++e) {
         a[e] += (u[0][e] + u[1][e]) + (u[2][e] + u[3][e]);
@@ -119,6 +146,7 @@ __global__ __launch_bounds__(kThreads) void bn_stats(const T* __restrict__ x, co
       load_sum(x, x2, s_out, (size_t)r * C + c0, u);
 #pragma unroll
       for (int e = 0; e < kVec; ++e) {
+        u[e] -= ks[e];
         a[e] += u[e];
         q[e] += u[e] * u[e];
       }
@@ -189,8 +217,9 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restr
   double s, q;
   combine2(psum, psq, nb, C, c, sl, s, q);
   if (sl != 0 || c >= C) return;
-  const double mean = s / (double)M;
-  double var = q / (double)M - mean * mean;
+  const double dm = s / (double)M;  // mean of the shifted values x - K
+  const double mean = (double)mean_out[c] + dm;  // bn_stats left K in mean_out
+  double var = q / (double)M - dm * dm;
   var = var > 0.0 ? var : 0.0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   mean_out[c] = (float)mean;
@@ -391,10 +420,10 @@ int mifx_bn_relu_fwd(int dtype, const void* x, const void* x2, void* sum_out, lo
   const int nb = blocks_for(M, C);
   if (dtype)
     hipLaunchKernelGGL(bn_stats<__hip_bfloat16>, dim3(nb), dim3(kThreads), 0, st, (const __hip_bfloat16*)x,
-                       (const __hip_bfloat16*)x2, (__hip_bfloat16*)sum_out, M, C, part, part + (size_t)nb * C);
+                       (const __hip_bfloat16*)x2, (__hip_bfloat16*)sum_out, M, C, part, part + (size_t)nb * C, stats);
   else
     hipLaunchKernelGGL(bn_stats<float>, dim3(nb), dim3(kThreads), 0, st, (const float*)x, (const float*)x2,
-                       (float*)sum_out, M, C, part, part + (size_t)nb * C);
+                       (float*)sum_out, M, C, part, part + (size_t)nb * C, stats);
   const void* xa = x2 != nullptr ? (const void*)sum_out : x;  // apply normalises the stored sum
   hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kFinCols - 1) / kFinCols), dim3(kThreads), 0, st, part,
                      part + (size_t)nb * C, nb, M, C, w, b, eps, momentum, run_mean, run_var, stats, stats + C,

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __
 #pragma unroll
         for (int e = 0; e < kVec; ++e) {
           const float v = __bfloat162float(v8.v[e]);
-          if (first || v > m[e] || (v != v && m[e] == m[e])) {  // first valid tap, strictly greater, or NaN
+          if (first || v > m[e] || v != v) {  // first valid tap, strictly greater, or NaN (PyTorch: last NaN wins)
             m[e] = v;
             k8.v[e] = (uint8_t)(kh * 3 + kw);
           }

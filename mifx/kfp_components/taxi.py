@@ -12,6 +12,7 @@ Schema format is the reference's column schema JSON: [{"name": ..., "type": CATE
 from __future__ import annotations
 
 import argparse
+import ast
 import csv
 import json
 import math
@@ -64,12 +65,36 @@ def _load_columns(path: str, column_names_file: str | None):
     return _read_csv(path, names)
 
 
-def _safe_lambda(src: str):
-    """Evaluate a `lambda x: ...` target expression with no builtins (pipeline-author supplied)."""
-    src = src.strip()
-    if not src.startswith("lambda"):
+_LAMBDA_NAMES = {"float": float, "int": int, "abs": abs, "min": min, "max": max, "round": round, "math": math}
+_LAMBDA_NODES = (ast.Expression, ast.Lambda, ast.arguments, ast.arg, ast.Name, ast.Load, ast.Constant, ast.BinOp,
+                 ast.UnaryOp, ast.BoolOp, ast.Compare, ast.IfExp, ast.Call, ast.Attribute, ast.Subscript, ast.operator,
+                 ast.unaryop, ast.boolop, ast.cmpop, ast.Tuple)
+
+
+def _compile_target_lambda(src: str):
+    """Compile the pipeline's `target_lambda` (e.g. "lambda x: (x['target'] > x['fare'] * 0.2)", the reference's
+    taxi-cab-classification-pipeline.py:60 argument) into a function.
+
+    The expression is pipeline-author code, as in the reference (which runs it unchecked). It is parsed with
+    `ast` and only a whitelist of expression nodes is accepted: one lambda; names limited to its parameters and
+    float / int / abs / min / max / round / math; attributes only on `math` and never dunder; subscripts,
+    arithmetic, comparisons, boolean ops and conditional expressions. Anything else (attribute walks such as
+    ().__class__, comprehensions, other names) is rejected before evaluation."""
+    tree = ast.parse(src.strip(), mode="eval")
+    if not isinstance(tree.body, ast.Lambda):
         raise ValueError("target_lambda must be a lambda expression")
-    return eval(src, {"__builtins__": {}}, {"float": float, "int": int, "abs": abs, "math": math})  # noqa: S307
+    params = {a.arg for a in tree.body.args.args}
+    if sum(isinstance(n, ast.Lambda) for n in ast.walk(tree)) != 1:
+        raise ValueError("target_lambda: nested lambdas are not allowed")
+    for node in ast.walk(tree):
+        if not isinstance(node, _LAMBDA_NODES):
+            raise ValueError(f"target_lambda: {type(node).__name__} is not allowed")
+        if isinstance(node, ast.Name) and node.id not in params and node.id not in _LAMBDA_NAMES:
+            raise ValueError(f"target_lambda: name {node.id!r} is not allowed")
+        if isinstance(node, ast.Attribute) and (node.attr.startswith("_") or not (
+                isinstance(node.value, ast.Name) and node.value.id == "math")):
+            raise ValueError(f"target_lambda: attribute {node.attr!r} is not allowed")
+    return eval(compile(tree, "<target_lambda>", "eval"), {"__builtins__": {}, **_LAMBDA_NAMES})  # noqa: S307
 
 
 # ---------------------------------------------------------------------------------------------
@@ -289,7 +314,7 @@ def _num(v):
 
 def confusion_matrix(a) -> None:
     rows = _prediction_rows(a.predictions, a.target_column)
-    fn = _safe_lambda(a.target_lambda) if a.target_lambda else None
+    fn = _compile_target_lambda(a.target_lambda) if a.target_lambda else None
     tgt = [int(bool(fn(r))) if fn else int(r["target"]) for r in rows]
     pred = [int(r["predicted"]) for r in rows]
     labels = [0, 1]
@@ -313,7 +338,7 @@ def confusion_matrix(a) -> None:
 
 def roc(a) -> None:
     rows = _prediction_rows(a.predictions_dir, a.target_column)
-    fn = _safe_lambda(a.target_lambda) if a.target_lambda else None
+    fn = _compile_target_lambda(a.target_lambda) if a.target_lambda else None
     y = np.array([int(fn(r)) if fn else int(r["target"]) for r in rows], np.int64)
     p = np.array([r["prob_1"] for r in rows], np.float64)
     order = np.argsort(-p, kind="stable")

@@ -206,3 +206,42 @@ def test_maxpool3s2_matches_pytorch(shape):
     ref = xb.grad.bfloat16().float()
     same = xa.grad.float() == ref
     assert same.float().mean() > 0.999, f"{(~same).sum().item()} of {same.numel()} input gradients differ"
+
+
+@pytest.mark.gpu
+def test_fused_bn_large_mean_variance_vs_fp64():
+    """Channels whose mean dwarfs their std (mean 100, std 1, e.g. residual sums): the shifted-sum statistics
+    must match an fp64 reference (E[x^2]-E[x]^2 from fp32 partials loses ~all digits of the variance here)."""
+    torch.manual_seed(5)
+    C = 64
+    x = (torch.randn(8, C, 16, 16, device="cuda") + 100.0 + torch.arange(C, device="cuda").view(1, C, 1, 1))
+    x = x.contiguous(memory_format=torch.channels_last)
+    w, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    y = bn_relu(x, w, b, rm, rv, True, 1.0, 1e-5, relu=False)  # momentum 1: running stats = batch stats
+    x64 = x.double()
+    var64 = x64.var(dim=(0, 2, 3), unbiased=False)
+    ref = (x64 - x64.mean(dim=(0, 2, 3), keepdim=True)) / (var64.view(1, C, 1, 1) + 1e-5).sqrt()
+    torch.testing.assert_close(y.double(), ref, rtol=0, atol=2e-3)
+    torch.testing.assert_close(rv.double(), x64.var(dim=(0, 2, 3), unbiased=True), rtol=2e-3, atol=0)
+    torch.testing.assert_close(rm.double(), x64.mean(dim=(0, 2, 3)), rtol=1e-6, atol=0)
+
+
+@pytest.mark.gpu
+def test_maxpool3s2_nan_routing_matches_pytorch():
+    """Several NaNs in one window: forward NaN and the gradient routed to the LAST NaN (PyTorch's rule)."""
+    from mifx.ops.pool import _MaxPool3s2
+
+    x = torch.randn(1, 8, 6, 6, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x[0, :, 1, 1] = float("nan")
+    x[0, :, 1, 2] = float("nan")
+    x[0, :, 4, 3] = float("nan")
+    xa = x.detach().requires_grad_()
+    xb = x.detach().float().requires_grad_()
+    ya = _MaxPool3s2.apply(xa)
+    yb = torch.nn.functional.max_pool2d(xb, 3, 2, 1)
+    assert torch.equal(torch.isnan(ya.float()), torch.isnan(yb))
+    g = torch.ones_like(yb)
+    ya.backward(g.bfloat16().contiguous(memory_format=torch.channels_last))
+    yb.backward(g)
+    torch.testing.assert_close(xa.grad.float(), xb.grad, rtol=0, atol=0)

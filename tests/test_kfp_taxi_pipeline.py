@@ -81,3 +81,15 @@ def test_taxi_pipeline_on_reference_csv(tmp_path):
     st = _run(tmp_path, REF_TAXI, 300, "128")
     assert st["phase"] == "Succeeded", st["message"]
     assert float(_outputs(st, "roc")[0]["value"]) > 0.8
+
+
+def test_target_lambda_whitelist():
+    from mifx.kfp_components.taxi import _compile_target_lambda
+
+    f = _compile_target_lambda("lambda x: (x['target'] > x['fare'] * 0.2)")
+    assert f({"target": 3.0, "fare": 10.0}) is True
+    assert _compile_target_lambda("lambda x: math.sqrt(abs(x)) if x else 0.0")(-4) == 2.0
+    for bad in ("lambda x: ().__class__.__base__.__subclasses__()", "lambda x: open(x)", "__import__('os')",
+                "lambda x: [y for y in x]", "lambda x: math.__dict__", "lambda x: (lambda: 1)()"):
+        with pytest.raises((ValueError, SyntaxError)):
+            _compile_target_lambda(bad)
