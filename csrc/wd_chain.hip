@@ -1,0 +1,589 @@
+// Register-chained fused Wide&Deep training step for gfx950 (second-generation kernel).
+//
+// Parity target: reference `airflow-dags/taxi_utils.py:148-191` (_build_estimator: DNNLinearCombinedClassifier,
+// DNN [100, 70, 48, 34] on 3 dense floats, linear part over 9 categorical identity columns, sigmoid CE) with
+// the hidden sizes of `trainer_fn` (`taxi_utils.py:300-345`). Same math and gradient-slab contract as
+// csrc/wide_deep.hip (wd_fused); the data flow inside a workgroup is different:
+//
+//  * 4 waves x 32 examples = 128 examples per iteration. A wave carries ITS 32 examples (two 16-column
+//    blocks) through the whole forward in registers: layer l's 16x16 MFMA output tiles (lane = example,
+//    4 consecutive output features per lane) are ReLU'd, packed to bf16 and used directly as the B operand of
+//    layer l+1 (tiles 2s and 2s+1 form k-step s). This makes layer l+1's k order a fixed permutation of the
+//    natural feature order inside every 32-block (position 8H + E <-> feature 16(E/4) + 4H + E%4), so each
+//    layer's weight image is stored with its COLUMNS in that "C order" (host: models.wide_deep.chain_perm).
+//    No LDS activation traffic and no block barrier in the forward; each weight fragment read from LDS
+//    feeds two MFMAs (both column blocks).
+//  * The activation-gradient chain dA_{l-1} = W_l^T dZ_l stays in registers the same way (output tiles of
+//    one layer are the B operand of the next); its A operand is read from the same weight image with
+//    ds_read_b64_tr_b16 at the permuted rows that match (rows 32s + 16(h%2) + 4(h/2) + {0..3, 8..11}).
+//    Layer 5 (one logit row) is a rank-1 product done on the VALU.
+//  * Weight gradients dW_l^T = dZ_l^T A_{l-1} reduce over examples, so they need the transpose: per layer the
+//    128 x N_l gradient (natural order) and the 128 x K_l activation (C order) are staged in LDS once and read
+//    back with ds_read_b64_tr_b16; every wave owns a fixed set of 16x16 dW tiles and keeps their fp32
+//    accumulators in registers across ALL iterations (MFMA K-accumulation == batch reduction), so the
+//    workgroup writes one gradient slab at the end, in the same tile-native layout as wd_fused.
+//    The ReLU masks of the backward come from the staged activations (C order, 8-byte reads).
+//  * Wide part: embedding-bag gather of 9 fp32 weights per example (issued before the forward), fixed-point
+//    LDS histogram for its gradient (order-independent -> deterministic), as in wd_fused.
+//
+// MIFX_HIPCC_FLAGS: -fno-honor-nans -fno-honor-infinities
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int T = 128;     // examples per workgroup iteration
+constexpr int NTHR = 256;  // 4 waves x 32 examples
+constexpr int NWAVE = NTHR / 64;
+constexpr int PAD = 8;
+
+constexpr int K1 = 32, N1 = 128;
+constexpr int K2 = 128, N2 = 96;
+constexpr int K3 = 96, N3 = 64;
+constexpr int K4 = 64, N4 = 64;
+constexpr int K5 = 64, N5 = 16;
+
+// weight image (bf16, LDS layout == global image layout): W_l^T [N_l][K_l + PAD], columns in C order
+constexpr int LW1 = 0;
+constexpr int LW2 = LW1 + N1 * (K1 + PAD);
+constexpr int LW3 = LW2 + N2 * (K2 + PAD);
+constexpr int LW4 = LW3 + N3 * (K3 + PAD);
+constexpr int LW5 = LW4 + N4 * (K4 + PAD);
+constexpr int LWEND = LW5 + N5 * (K5 + PAD);  // 30592
+// dW staging: dZ_l [T][N_l + PAD] (natural order) followed by A_{l-1} [T][K_l + PAD] (C order)
+constexpr int stage_len(int K, int N) { return T * (N + PAD) + T * (K + PAD); }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int LSLEN = cmax(cmax(cmax(stage_len(K1, N1), stage_len(K2, N2)), cmax(stage_len(K3, N3), stage_len(K4, N4))),
+                           stage_len(K5, N5));
+constexpr int LS = LWEND;
+constexpr int LSEND = LS + LSLEN;
+constexpr int NWIDE = 2128;
+constexpr int WIDE_BIAS = 2127;
+constexpr int WIDE_PAD = 2176;
+constexpr int NTILE = 108;
+constexpr int LDS_BYTES = LSEND * 2 + WIDE_PAD * 4 + 64 * 4;
+static_assert(LDS_BYTES <= 163840, "LDS budget");
+static_assert((LSEND * 2) % 16 == 0 && (LS * 2) % 16 == 0, "16-B aligned regions");
+
+constexpr int TB1 = 0, TB2 = TB1 + (N1 / 16) * (K1 / 16), TB3 = TB2 + (N2 / 16) * (K2 / 16),
+              TB4 = TB3 + (N3 / 16) * (K3 / 16), TB5 = TB4 + (N4 / 16) * (K4 / 16);
+static_assert(TB5 + (N5 / 16) * (K5 / 16) == NTILE, "tile count");
+
+__constant__ int kWideOff[9] = {0, 1010, 2020, 2030, 2040, 2050, 2060, 2084, 2115};
+__constant__ int kWideNb[9] = {1010, 1010, 10, 10, 10, 10, 24, 31, 12};
+
+__device__ __forceinline__ v4s tr_read(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+}
+__device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
+  v8s r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
+__device__ __forceinline__ v8bf ld8(const uint16_t* p) { return *(const v8bf*)p; }
+__device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ v8bf pack_relu(v4f a, v4f b) {
+  v8bf o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[i] = (bf16)fmaxf(a[i], 0.f);
+    o[4 + i] = (bf16)fmaxf(b[i], 0.f);
+  }
+  return o;
+}
+__device__ __forceinline__ v4bf to_bf4(v4f a) {
+  v4bf o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = (bf16)a[i];
+  return o;
+}
+__device__ __forceinline__ v8bf cat_bf(v4bf a, v4bf b) {
+  v8bf o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[i] = a[i];
+    o[4 + i] = b[i];
+  }
+  return o;
+}
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+constexpr v4f kZero4 = {0.f, 0.f, 0.f, 0.f};
+
+// ---- forward layer for the wave's two column blocks: acc[tb][nt] = W^T[16 nt ..][.] . B[tb][.]
+// W image rows natural, columns C order; B[tb][s] is the k-step-s fragment (C order) of the layer input.
+template <int K, int N>
+__device__ __forceinline__ void fwd(const uint16_t* W, const v8bf (&B)[2][K / 32], v4f (&acc)[2][N / 16], int r, int h) {
+  constexpr int KS = K / 32, NT = N / 16;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[0][nt] = acc[1][nt] = kZero4;
+  v8bf wa[2][NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) wa[0][nt] = ld8(W + (16 * nt + r) * (K + PAD) + 8 * h);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) wa[(s + 1) & 1][nt] = ld8(W + (16 * nt + r) * (K + PAD) + 32 * (s + 1) + 8 * h);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      acc[0][nt] = mfma(wa[s & 1][nt], B[0][s], acc[0][nt]);
+      acc[1][nt] = mfma(wa[s & 1][nt], B[1][s], acc[1][nt]);
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void relu_pack(const v4f (&acc)[2][N / 16], v8bf (&out)[2][N / 32]) {
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int s = 0; s < N / 32; ++s) out[tb][s] = pack_relu(acc[tb][2 * s], acc[tb][2 * s + 1]);
+}
+
+// ---- activation gradient: dA^T[k][t] = sum_n W[n][k] dZ[n][t] for the W image of a layer (K x N), its
+// rows (n, natural) read transposed at the rows that match the chained dZ fragments (C order of the layer
+// above). dz[tb][kt'] are the previous gradient tiles (N/16 of them); out[tb][kt] the K/16 output tiles.
+template <int K, int N>
+__device__ __forceinline__ void bwd_dA(const uint16_t* W, const v4bf (&dz)[2][N / 16], v4f (&out)[2][K / 16], int r,
+                                       int h) {
+  constexpr int NS = N / 32, KT = K / 16;
+  const int q = r >> 2, p = r & 3;
+  const int rb = 16 * (h & 1) + 4 * (h >> 1) + q;
+  v8bf b[2][NS];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) b[tb][s] = cat_bf(dz[tb][2 * s], dz[tb][2 * s + 1]);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) out[0][kt] = out[1][kt] = kZero4;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    v8bf a[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint16_t* pa = W + (32 * s + rb) * (K + PAD) + 16 * kt + 4 * p;
+      a[s] = cat8(tr_read(pa), tr_read(pa + 8 * (K + PAD)));
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      out[0][kt] = mfma(a[s], b[0][s], out[0][kt]);
+      out[1][kt] = mfma(a[s], b[1][s], out[1][kt]);
+    }
+  }
+}
+
+// ReLU mask of the layer input from the staged activation (C order) and bf16 pack of the gradient
+template <int K>
+__device__ __forceinline__ void mask_grad(const v4f (&g)[2][K / 16], const uint16_t* SA, int w, int r, int h,
+                                          v4bf (&dz)[2][K / 16]) {
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int kt = 0; kt < K / 16; ++kt) {
+      const uint2 m = *(const uint2*)(SA + (32 * w + 16 * tb + r) * (K + PAD) + 16 * kt + 4 * h);
+      v4bf o;
+      o[0] = (bf16)((m.x & 0xffffu) ? g[tb][kt][0] : 0.f);
+      o[1] = (bf16)((m.x >> 16) ? g[tb][kt][1] : 0.f);
+      o[2] = (bf16)((m.y & 0xffffu) ? g[tb][kt][2] : 0.f);
+      o[3] = (bf16)((m.y >> 16) ? g[tb][kt][3] : 0.f);
+      dz[tb][kt] = o;
+    }
+}
+
+// stage dZ (gradient tiles in C order of the layer above -> natural order columns) and the layer's input
+// activation fragments (C order) for the dW product of a layer with dims K x N
+template <int K, int N>
+__device__ __forceinline__ void stage(uint16_t* S, const v4bf (&dz)[2][N / 16], const v8bf (&a)[2][K / 32], int w, int r,
+                                      int h) {
+  uint16_t* SZ = S;
+  uint16_t* SA = S + T * (N + PAD);
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb) {
+    const int row = 32 * w + 16 * tb + r;
+#pragma unroll
+    for (int kt = 0; kt < N / 16; ++kt) {
+      const int f0 = 32 * (kt >> 1) + 16 * (h & 1) + 8 * (kt & 1) + 4 * (h >> 1);
+      *(v4bf*)(SZ + row * (N + PAD) + f0) = dz[tb][kt];
+    }
+#pragma unroll
+    for (int s = 0; s < K / 32; ++s) *(v8bf*)(SA + row * (K + PAD) + 32 * s + 8 * h) = a[tb][s];
+  }
+}
+
+// ---- weight gradient: the wave's NTW x KTW tiles (nt = nt0 + i ntS, kt = kt0 + j ktS) accumulate
+// dW^T[n][k] += sum_t dZ[t][n] A[t][k] over the T staged rows (4 k-steps of 32 examples)
+template <int K, int N, int NTW, int KTW>
+__device__ __forceinline__ void dw_phase(v4f (&acc)[NTW * KTW], const uint16_t* S, int nt0, int ntS, int kt0, int ktS,
+                                         int r, int h) {
+  const uint16_t* SZ = S;
+  const uint16_t* SA = S + T * (N + PAD);
+  const int q = r >> 2, p = r & 3;
+#pragma unroll
+  for (int ts = 0; ts < T / 32; ++ts) {
+    v8bf fa[NTW], fb[KTW];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const uint16_t* pa = SZ + (32 * ts + 8 * h + q) * (N + PAD) + 16 * (nt0 + i * ntS) + 4 * p;
+      fa[i] = cat8(tr_read(pa), tr_read(pa + 4 * (N + PAD)));
+    }
+#pragma unroll
+    for (int j = 0; j < KTW; ++j) {
+      const uint16_t* pb = SA + (32 * ts + 8 * h + q) * (K + PAD) + 16 * (kt0 + j * ktS) + 4 * p;
+      fb[j] = cat8(tr_read(pb), tr_read(pb + 4 * (K + PAD)));
+    }
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int j = 0; j < KTW; ++j) acc[i * KTW + j] = mfma(fa[i], fb[j], acc[i * KTW + j]);
+  }
+}
+
+template <int K, int NTW, int KTW>
+__device__ __forceinline__ void load_ct(int (&ct)[NTW * KTW], int tbase, int nt0, int ntS, int kt0, int ktS,
+                                        const int* __restrict__ tmap) {
+#pragma unroll
+  for (int i = 0; i < NTW; ++i)
+#pragma unroll
+    for (int j = 0; j < KTW; ++j) ct[i * KTW + j] = tmap[tbase + (nt0 + i * ntS) * (K / 16) + kt0 + j * ktS];
+}
+
+template <int NT>
+__device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], const int (&ct)[NT], int lane) {
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (ct[i] < 0) continue;
+    float* dst = slab + (size_t)ct[i] * 256 + lane;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[e * 64] = acc[i][e];
+  }
+}
+
+template <bool TRAIN>
+__global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ data, long long n_data, long long batch,
+                                                     long long start_fixed, const long long* __restrict__ step_ctr,
+                                                     const uint4* __restrict__ wimg, const float* __restrict__ wide,
+                                                     float* __restrict__ slab, float* __restrict__ slab_loss,
+                                                     float* __restrict__ logits_out, float grad_scale,
+                                                     const int* __restrict__ tmap, int stride) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  float* wgrad = (float*)(lds + LSEND);
+  float* red = wgrad + WIDE_PAD;
+  int* wgi = (int*)wgrad;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
+
+  {  // stage the bf16 weight image (already in LDS layout): all global loads, then all LDS stores
+    constexpr int NCH = LWEND / 8, PER = (NCH + NTHR - 1) / NTHR;
+    uint4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = wimg[min(tid + i * NTHR, NCH - 1)];
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (tid + i * NTHR < NCH) *(uint4*)(lds + (tid + i * NTHR) * 8) = v[i];
+  }
+  if (TRAIN)
+    for (int c = tid; c < WIDE_PAD; c += NTHR) wgrad[c] = 0.f;
+  __syncthreads();
+
+  const long long start = step_ctr ? (step_ctr[0] * batch) % n_data : start_fixed;
+  const int niters = (int)((batch + T - 1) / T);
+  const int my_iters = (niters - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const float qbound = fmaxf(fabsf(grad_scale) * (float)(max(my_iters, 1) * T), 1e-30f);
+  const float qscale = exp2f(fminf(floorf(log2f(1073741824.f / qbound)), 100.f));
+  const float qinv = 1.f / qscale;
+  const float qmax = 1073741824.f / (float)(max(my_iters, 1) * T);
+
+  // dW tile ownership (wave w): L1 nt {2w, 2w+1} x kt 0 (kt 1 holds only padding columns);
+  // L2 nt 0..5 x kt {2w, 2w+1}; L3 nt w x kt 0..5; L4 nt w x kt 0..3; L5 nt 0 x kt w
+  v4f acc1[2], acc2[12], acc3[6], acc4[4], acc5[1];
+  int ct1[2], ct2[12], ct3[6], ct4[4], ct5[1];
+  if (TRAIN) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc1[i] = kZero4;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) acc2[i] = kZero4;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc3[i] = kZero4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc4[i] = kZero4;
+    acc5[0] = kZero4;
+    load_ct<K1, 2, 1>(ct1, TB1, 2 * w, 1, 0, 0, tmap);
+    load_ct<K2, 6, 2>(ct2, TB2, 0, 1, 2 * w, 1, tmap);
+    load_ct<K3, 1, 6>(ct3, TB3, w, 0, 0, 1, tmap);
+    load_ct<K4, 1, 4>(ct4, TB4, w, 0, 0, 1, tmap);
+    load_ct<K5, 1, 1>(ct5, TB5, 0, 0, w, 0, tmap);
+  }
+  float loss_sum = 0.f, dl_sum = 0.f;
+  const int mtb = h & 1;  // the column block whose wide part / loss this lane computes (lanes h < 2 own it)
+
+  auto fetch = [&](int it, uint4 (&u)[2][2]) {
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      const long long row = min((long long)it * T + 32 * w + 16 * tb + r, batch - 1);
+      long long di = start + row;
+      if (di >= n_data) di -= n_data;  // host guarantees batch <= n_data
+      u[tb][0] = data[2 * di];
+      u[tb][1] = data[2 * di + 1];
+    }
+  };
+  uint4 nu[2][2];
+  fetch(blockIdx.x, nu);
+
+  for (int it = blockIdx.x; it < niters; it += gridDim.x) {
+    uint4 u[2][2];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      u[tb][0] = nu[tb][0];
+      u[tb][1] = nu[tb][1];
+    }
+    fetch(it + gridDim.x, nu);  // next iteration's records
+
+    // wide gather for the lane's column block (issued before the forward: its latency hides under MFMAs)
+    const uint4 m0 = mtb ? u[1][0] : u[0][0], m1 = mtb ? u[1][1] : u[0][1];
+    const uint32_t idw[5] = {m0.w, m1.x, m1.y, m1.z, m1.w};
+    int ids[9];
+    float wv[9];
+#pragma unroll
+    for (int f = 0; f < 9; ++f) {
+      int id = (f & 1) ? (idw[f >> 1] >> 16) : (idw[f >> 1] & 0xffff);
+      id = id < kWideNb[f] ? id : 0;
+      ids[f] = kWideOff[f] + id;
+      wv[f] = wide[ids[f]];
+    }
+    const float wbias = wide[WIDE_BIAS];
+
+    // ---- forward, in registers
+    v8bf a0[2][1];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      const v8bf x = {(bf16)__uint_as_float(u[tb][0].x), (bf16)__uint_as_float(u[tb][0].y),
+                      (bf16)__uint_as_float(u[tb][0].z), (bf16)1.0f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      a0[tb][0] = h == 0 ? x : (v8bf){};
+    }
+    v8bf a1[2][N1 / 32], a2[2][N2 / 32], a3[2][N3 / 32], a4[2][N4 / 32];
+    v4f z5[2][1];
+    {
+      v4f acc[2][N1 / 16];
+      fwd<K1, N1>(lds + LW1, a0, acc, r, h);
+      relu_pack<N1>(acc, a1);
+    }
+    {
+      v4f acc[2][N2 / 16];
+      fwd<K2, N2>(lds + LW2, a1, acc, r, h);
+      relu_pack<N2>(acc, a2);
+    }
+    {
+      v4f acc[2][N3 / 16];
+      fwd<K3, N3>(lds + LW3, a2, acc, r, h);
+      relu_pack<N3>(acc, a3);
+    }
+    {
+      v4f acc[2][N4 / 16];
+      fwd<K4, N4>(lds + LW4, a3, acc, r, h);
+      relu_pack<N4>(acc, a4);
+    }
+    fwd<K5, N5>(lds + LW5, a4, z5, r, h);
+
+    // ---- logit = deep (row 0 of the layer-5 tile: lane (r, h = 0)) + wide; loss and dlogit
+    const float zd0 = __shfl(z5[0][0][0], r), zd1 = __shfl(z5[1][0][0], r);
+    float wl = wbias;
+#pragma unroll
+    for (int f = 0; f < 9; ++f) wl += wv[f];
+    const float x = (mtb ? zd1 : zd0) + wl;
+    const long long grow = (long long)it * T + 32 * w + 16 * mtb + r;
+    const bool own = h < 2 && grow < batch;
+    const float y = (float)(idw[4] >> 16);
+    const float lossv = fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
+    if (!TRAIN) {
+      if (own) {
+        logits_out[grow] = x;
+        loss_sum += lossv;
+      }
+      continue;
+    }
+    const float dl = own ? (1.f / (1.f + __expf(-x)) - y) * grad_scale : 0.f;
+    if (own) {
+      loss_sum += lossv;
+      dl_sum += dl;
+    }
+    // dlogit of the lane's example in both column blocks, rounded to bf16 like the staged dZ5 the dW5 MFMA reads
+    const float dlb[2] = {(float)(bf16)__shfl(dl, r), (float)(bf16)__shfl(dl, 16 + r)};
+
+    // ---- layer 5: stage (dZ5, A4); dW5; dA4 = w5 (x) dl on the VALU, masked
+    uint16_t* S = lds + LS;
+    block_sync_lds();  // previous iteration's dW1 reads of the staging area are done
+    if (own) {
+      const int q = __float2int_rn(fminf(fmaxf(dl * qscale, -qmax), qmax));
+#pragma unroll
+      for (int f = 0; f < 9; ++f) atomicAdd(&wgi[ids[f]], q);
+    }
+    {
+      v4bf d5[2][1];
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb) {
+        v4bf o = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+        if (h == 0) o[0] = (bf16)dlb[tb];
+        d5[tb][0] = o;
+      }
+      // dZ5 has one natural-order tile (N5 = 16): stage it directly (row t: [dl, 0 ... 0])
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb) {
+        const int row = 32 * w + 16 * tb + r;
+        *(v4bf*)(S + row * (N5 + PAD) + 4 * h) = d5[tb][0];
+#pragma unroll
+        for (int s = 0; s < K5 / 32; ++s) *(v8bf*)(S + T * (N5 + PAD) + row * (K5 + PAD) + 32 * s + 8 * h) = a4[tb][s];
+      }
+    }
+    block_sync_lds();
+    dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w, 0, r, h);
+    v4bf dz4[2][K5 / 16];
+    {
+      v4f g[2][K5 / 16];
+#pragma unroll
+      for (int kt = 0; kt < K5 / 16; ++kt) {
+        const uint2 wv2 = *(const uint2*)(lds + LW5 + 16 * kt + 4 * h);  // W5 row 0 (the logit row), C order
+        const float w5[4] = {__uint_as_float(wv2.x << 16), __uint_as_float(wv2.x & 0xffff0000u),
+                             __uint_as_float(wv2.y << 16), __uint_as_float(wv2.y & 0xffff0000u)};
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) g[tb][kt][e] = w5[e] * dlb[tb];
+      }
+      mask_grad<K5>(g, S + T * (N5 + PAD), w, r, h, dz4);
+    }
+    block_sync_lds();
+
+    // ---- layer 4
+    stage<K4, N4>(S, dz4, a3, w, r, h);
+    block_sync_lds();
+    dw_phase<K4, N4, 1, 4>(acc4, S, w, 0, 0, 1, r, h);
+    v4bf dz3[2][K4 / 16];
+    {
+      v4f g[2][K4 / 16];
+      bwd_dA<K4, N4>(lds + LW4, dz4, g, r, h);
+      mask_grad<K4>(g, S + T * (N4 + PAD), w, r, h, dz3);
+    }
+    block_sync_lds();
+
+    // ---- layer 3
+    stage<K3, N3>(S, dz3, a2, w, r, h);
+    block_sync_lds();
+    dw_phase<K3, N3, 1, 6>(acc3, S, w, 0, 0, 1, r, h);
+    v4bf dz2[2][K3 / 16];
+    {
+      v4f g[2][K3 / 16];
+      bwd_dA<K3, N3>(lds + LW3, dz3, g, r, h);
+      mask_grad<K3>(g, S + T * (N3 + PAD), w, r, h, dz2);
+    }
+    block_sync_lds();
+
+    // ---- layer 2
+    stage<K2, N2>(S, dz2, a1, w, r, h);
+    block_sync_lds();
+    dw_phase<K2, N2, 6, 2>(acc2, S, 0, 1, 2 * w, 1, r, h);
+    v4bf dz1[2][K2 / 16];
+    {
+      v4f g[2][K2 / 16];
+      bwd_dA<K2, N2>(lds + LW2, dz2, g, r, h);
+      mask_grad<K2>(g, S + T * (N2 + PAD), w, r, h, dz1);
+    }
+    block_sync_lds();
+
+    // ---- layer 1
+    stage<K1, N1>(S, dz1, a0, w, r, h);
+    block_sync_lds();
+    dw_phase<K1, N1, 2, 1>(acc1, S, 2 * w, 1, 0, 0, r, h);
+  }
+
+  // ---- epilogue: per-workgroup slab (same layout as wd_fused)
+  for (int o = 32; o > 0; o >>= 1) {
+    loss_sum += __shfl_xor(loss_sum, o);
+    dl_sum += __shfl_xor(dl_sum, o);
+  }
+  __syncthreads();  // last dW reads done; red/wgrad final
+  if (lane == 0) {
+    red[w] = loss_sum;
+    red[NWAVE + w] = dl_sum;
+  }
+  if (TRAIN) {
+    float* my = slab + (size_t)blockIdx.x * stride;
+    store_tiles<2>(my, acc1, ct1, lane);
+    store_tiles<12>(my, acc2, ct2, lane);
+    store_tiles<6>(my, acc3, ct3, lane);
+    store_tiles<4>(my, acc4, ct4, lane);
+    store_tiles<1>(my, acc5, ct5, lane);
+  }
+  __syncthreads();
+  if (TRAIN) {
+    float* my = slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD);
+    for (int c = tid; c < WIDE_PAD; c += NTHR) {
+      float v = (float)wgi[c] * qinv;
+      if (c == WIDE_BIAS) {
+#pragma unroll
+        for (int i = 0; i < NWAVE; ++i) v += red[NWAVE + i];
+      }
+      my[c] = v;
+    }
+  }
+  if (tid == 0 && slab_loss) {
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < NWAVE; ++i) l += red[i];
+    slab_loss[blockIdx.x] = l;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// T, LWEND (weight image elements), LDS_BYTES, PAD, NTILE, WIDE_PAD
+int mifx_wdc_constants(int* out, int n) {
+  const int v[] = {T, LWEND, LDS_BYTES, PAD, NTILE, WIDE_PAD, LW1, LW2, LW3, LW4, LW5};
+  const int m = (int)(sizeof(v) / sizeof(int));
+  for (int i = 0; i < n && i < m; ++i) out[i] = v[i];
+  return m;
+}
+
+// One launch = forward (+ loss) [+ backward into the per-workgroup slab] over `batch` records starting at
+// (step_ctr[0] * batch) % n_data (or start_fixed when step_ctr is null). wimg: the bf16 weight image in LDS
+// layout (LWEND elements, C-ordered columns, see models.wide_deep.chain_image).
+int mifx_wdc_fused(const void* data, long long n_data, long long batch, long long start_fixed,
+                   const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
+                   float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
+                   hipStream_t stream) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)wdc_fused<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)wdc_fused<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr_done = true;
+  }
+  if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
+  if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
+  if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;
+  if (!train && logits_out == nullptr) return -1;
+  if (train)
+    hipLaunchKernelGGL(wdc_fused<true>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
+                       start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out, grad_scale, tmap,
+                       stride);
+  else
+    hipLaunchKernelGGL(wdc_fused<false>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
+                       start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out, grad_scale, tmap,
+                       stride);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

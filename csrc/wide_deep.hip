@@ -711,7 +711,7 @@ template <bool OPT>
 __global__ __launch_bounds__(256) void wd_reduce_opt(
     const float4* __restrict__ slab, int G, int stride, float4* __restrict__ out, const int* __restrict__ inv,
     float* __restrict__ param, float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
-    long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+    const int* __restrict__ wmap, long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
   __shared__ float4 part[RG][RQ];
   __shared__ float gsum[4 * RQ];
   __shared__ long long s_step;
@@ -772,7 +772,9 @@ __global__ __launch_bounds__(256) void wd_reduce_opt(
       s0[c] = a0;
       s1[c] = a1;
       param[c] = w;
-      if (dnn) wt_out[c] = __builtin_bit_cast(uint16_t, (bf16)w);
+      // bf16 weight image: canonical order, or through wmap (canonical -> image offset) for the
+      // register-chained kernel's C-ordered LDS image (csrc/wd_chain.hip)
+      if (dnn) wt_out[wmap != nullptr ? wmap[c] : c] = __builtin_bit_cast(uint16_t, (bf16)w);
     }
   }
   if (threadIdx.x == 0) step_ctr[blockIdx.x] = step;
@@ -846,9 +848,9 @@ int mifx_wd_optimizer(const float* partial, int nparts, const int* gidx, const u
 }
 
 // slab [G, stride] -> full sum; with inv != null the optimizer is applied in the same launch (out unused),
-// otherwise the sum is written to out [stride]. step_ctr must hold STEP_SLOTS int64 (per-workgroup step slots).
+// otherwise the sum is written to out [stride]. wmap (nullable): canonical DNN index -> bf16 image offset. step_ctr must hold STEP_SLOTS int64 (per-workgroup step slots).
 int mifx_wd_reduce_opt(const float* slab, int G, int stride, float* out, const int* inv, float* param, float* s0,
-                       float* s1, void* wt_out, long long* step_ctr, const float* hyper_dnn,
+                       float* s1, void* wt_out, const int* wmap, long long* step_ctr, const float* hyper_dnn,
                        const float* hyper_wide, hipStream_t stream) {
   if (G <= 0 || stride <= 0 || stride > STRIDE || stride % 4 != 0) return -1;
   const dim3 grid((stride / 4 + RQ - 1) / RQ);
@@ -856,7 +858,8 @@ int mifx_wd_reduce_opt(const float* slab, int G, int stride, float* out, const i
   if (inv == nullptr) {
     if (out == nullptr) return -1;
     hipLaunchKernelGGL(wd_reduce_opt<false>, grid, dim3(256), 0, stream, (const float4*)slab, G, stride,
-                       (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{}, OptHyper{});
+                       (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{},
+                       OptHyper{});
     return (int)hipGetLastError();
   }
   if (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr || step_ctr == nullptr) return -1;
@@ -865,7 +868,7 @@ int mifx_wd_reduce_opt(const float* slab, int G, int stride, float* out, const i
   OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
               hyper_wide[6], hyper_wide[7]};
   hipLaunchKernelGGL(wd_reduce_opt<true>, grid, dim3(256), 0, stream, (const float4*)slab, G, stride, nullptr, inv,
-                     param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
+                     param, s0, s1, (uint16_t*)wt_out, wmap, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
 

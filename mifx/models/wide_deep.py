@@ -259,9 +259,12 @@ def unpack_canonical(vec, model: WideDeepModel) -> WideDeepModel:
     return model
 
 
-def canonical_grad_to_torch(grad_tile_native: np.ndarray, model: WideDeepModel) -> dict[str, np.ndarray]:
-    """Map a tile-native gradient slab back to named torch-shaped gradients (for tests)."""
-    gidx, _ = canonical_index_maps(model.cfg)
+def canonical_grad_to_torch(grad_tile_native: np.ndarray, model: WideDeepModel,
+                            gidx: np.ndarray | None = None) -> dict[str, np.ndarray]:
+    """Map a tile-native gradient slab back to named torch-shaped gradients (for tests). gidx: the kernel's
+    canonical -> slab map (default: the tile kernel's compact layout)."""
+    if gidx is None:
+        gidx, _ = canonical_index_maps(model.cfg)
     canon = np.asarray(grad_tile_native)[gidx]
     out = {}
     lins = list(model.dnn) + [model.head]
@@ -306,3 +309,71 @@ def tensors_to_records(dense, ids, label) -> np.ndarray:
     rec["id"] = np.clip(np.asarray(ids), 0, 65535).astype(np.uint16)
     rec["label"] = np.asarray(label).astype(np.uint16)
     return rec
+
+
+# ---- register-chained kernel layout (csrc/wd_chain.hip) ---------------------------------------
+# The chained kernel feeds layer l's MFMA output tiles straight into layer l+1 as its B operand, so layer
+# l+1's k axis is consumed in "C order": inside every 32-block, position 8H + E holds feature
+# 16 (E // 4) + 4 H + E % 4. Its LDS weight image W_l^T [N][K + PAD] therefore has natural rows and
+# C-ordered columns; dW tiles come out in the same image coordinates.
+CHAIN_PAD = 8
+CHAIN_LW = [int(v) for v in np.cumsum([0] + [n * (k + CHAIN_PAD) for k, n in LAYER_KN])[:-1]]
+CHAIN_LWEND = sum(n * (k + CHAIN_PAD) for k, n in LAYER_KN)  # 30592
+
+
+def chain_perm(K: int) -> np.ndarray:
+    """f[c] = natural feature held at C-order position c of a K-wide (K % 32 == 0) chained input axis."""
+    c = np.arange(K)
+    return 32 * (c // 32) + 16 * ((c % 8) // 4) + 4 * ((c % 32) // 8) + c % 4
+
+
+def chain_image(param) -> np.ndarray:
+    """fp32 canonical vector -> fp32 weight image in the chained kernel's LDS layout [CHAIN_LWEND]
+    (cast to bf16 on the device)."""
+    p = np.asarray(param.detach().cpu() if torch.is_tensor(param) else param, dtype=np.float32)
+    img = np.zeros(CHAIN_LWEND, np.float32)
+    for li, (K, N) in enumerate(LAYER_KN):
+        w = p[LAYER_OFF[li]:LAYER_OFF[li] + K * N].reshape(N, K)
+        blk = np.zeros((N, K + CHAIN_PAD), np.float32)
+        blk[:, :K] = w[:, chain_perm(K)]
+        img[CHAIN_LW[li]:CHAIN_LW[li] + N * (K + CHAIN_PAD)] = blk.reshape(-1)
+    return img
+
+
+def chain_maps(cfg: WideDeepConfig | None = None):
+    """Index maps of the chained kernel: (tmap int32 [NTILE], stride, gidx int32 [WTOT+NWIDE],
+    mask uint8 [WTOT+NWIDE], wmap int32 [WTOT]).
+
+    tmap: dW tile (image coordinates, id TILE_BASE + nt * K/16 + kt) -> compact slab position (-1: only
+    padding); gidx: canonical parameter -> slab position (tile-native order inside a tile, as wd_fused);
+    wmap: canonical DNN parameter -> offset in the bf16 image the optimizer re-emits."""
+    cfg = cfg or WideDeepConfig()
+    check_fused_compatible(cfg)
+    masks = _trainable_masks(cfg)
+    tmap = np.full(NTILE, -1, np.int32)
+    c = 0
+    for li, ((K, N), m) in enumerate(zip(LAYER_KN, masks)):
+        mi = m[:, chain_perm(K)]  # image coordinates
+        for nt in range(N // 16):
+            for kt in range(K // 16):
+                if mi[16 * nt:16 * nt + 16, 16 * kt:16 * kt + 16].any():
+                    tmap[TILE_BASE[li] + nt * (K // 16) + kt] = c
+                    c += 1
+    stride = c * 256 + WIDE_PAD
+    gidx = np.zeros(WTOT + NWIDE, np.int32)
+    mask = np.zeros(WTOT + NWIDE, np.uint8)
+    wmap = np.zeros(WTOT, np.int32)
+    for li, ((K, N), m) in enumerate(zip(LAYER_KN, masks)):
+        cinv = np.argsort(chain_perm(K))  # natural k -> image column
+        n = np.arange(N)[:, None]
+        col = cinv[None, :].repeat(N, 0)
+        ct = tmap[TILE_BASE[li] + (n // 16) * (K // 16) + col // 16]
+        lane = 16 * ((n % 16) // 4) + col % 16
+        idx = np.where(ct >= 0, ct * 256 + (n % 4) * 64 + lane, 0)
+        assert (ct[m] >= 0).all()
+        gidx[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = idx.reshape(-1)
+        mask[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = m.reshape(-1)
+        wmap[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = (CHAIN_LW[li] + n * (K + CHAIN_PAD) + col).reshape(-1)
+    gidx[WTOT:] = stride - WIDE_PAD + np.arange(NWIDE)
+    mask[WTOT:] = 1
+    return tmap, stride, gidx, mask, wmap

@@ -1,0 +1,54 @@
+"""ctypes bindings for csrc/wd_chain.hip (register-chained fused Wide&Deep step on gfx950)."""
+from __future__ import annotations
+
+import ctypes
+import functools
+
+import torch
+
+from . import _lib
+from ._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
+
+
+@functools.lru_cache(maxsize=None)
+def _fns():
+    lib = _lib.load("wd_chain")
+    return {
+        "constants": sig(lib, "mifx_wdc_constants", [VP, I32]),
+        "fused": sig(lib, "mifx_wdc_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP]),
+    }
+
+
+@functools.lru_cache(maxsize=None)
+def constants() -> dict[str, int]:
+    buf = (ctypes.c_int * 16)()
+    n = _fns()["constants"](buf, 16)
+    names = ["T", "LWEND", "LDS_BYTES", "PAD", "NTILE", "WIDE_PAD", "LW1", "LW2", "LW3", "LW4", "LW5"]
+    return {k: buf[i] for i, k in enumerate(names[:n])}
+
+
+def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
+          wimg_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
+          logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
+          tmap: torch.Tensor | None = None) -> None:
+    """One chained-kernel launch. wimg_bf16: [LWEND] bf16 (or int16) weight image in the kernel's LDS layout
+    (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout."""
+    c = constants()
+    if wimg_bf16.numel() != c["LWEND"] or wimg_bf16.element_size() != 2 or not wimg_bf16.is_contiguous():
+        raise ValueError("weight image must be a contiguous 16-bit [LWEND] tensor")
+    if records.dim() != 2 or records.shape[1] != 32 or not records.is_contiguous():
+        raise ValueError("records must be contiguous uint8 [N, 32]")
+    stride = int(slab.shape[-1]) if slab is not None else 0
+    if train:
+        if tmap is None or tmap.dtype != torch.int32 or tmap.numel() != c["NTILE"]:
+            raise ValueError("training launch needs the int32 tile map of the chained slab layout")
+        if slab.shape[0] < grid or not slab.is_contiguous():
+            raise ValueError("slab must be a contiguous [>= grid, stride] tensor")
+        if slab_loss is not None and slab_loss.numel() < grid:
+            raise ValueError("slab_loss must hold >= grid floats")
+    elif logits_out is None or logits_out.numel() < batch:
+        raise ValueError("eval launch needs logits_out with >= batch floats")
+    rc = _fns()["fused"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide), ptr(slab),
+                         ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train), ptr(tmap), stride,
+                         stream_handle(records.device))
+    check(rc, "mifx_wdc_fused")

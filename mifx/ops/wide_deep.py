@@ -18,7 +18,7 @@ def _fns():
         "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP, VP]),
         "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, I32, VP]),
         "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
-        "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -74,15 +74,19 @@ def reduce_full(slab: torch.Tensor, groups: int, out: torch.Tensor) -> None:
     if out.numel() < stride or slab.numel() < groups * stride or not slab.is_contiguous():
         raise ValueError("slab must be contiguous [>= groups, stride] and out hold >= stride floats")
     rc = _fns()["reduce_opt"](ptr(slab), int(groups), stride, ptr(out), None, None, None, None, None, None, None,
-                              None, stream_handle(slab.device))
+                              None, None, stream_handle(slab.device))
     check(rc, "mifx_wd_reduce_opt")
 
 
 def reduce_apply(slab: torch.Tensor, groups: int, inv: torch.Tensor, param: torch.Tensor, s0: torch.Tensor,
                  s1: torch.Tensor, wt_out: torch.Tensor, step_ctr: torch.Tensor, hyper_dnn: torch.Tensor,
-                 hyper_wide: torch.Tensor) -> None:
+                 hyper_wide: torch.Tensor, wmap: torch.Tensor | None = None) -> None:
     """Sum the first `groups` slab rows and apply the optimizer in the same launch. inv: int32 [stride]
-    slab column -> canonical parameter index (-1 for padding), see FusedWideDeepTrainer."""
+    slab column -> canonical parameter index (-1 for padding), see FusedWideDeepTrainer. wmap: int32 [WTOT]
+    canonical DNN index -> offset in wt_out (the register-chained kernel's C-ordered image); None writes
+    wt_out in canonical order."""
+    if wmap is not None and (wmap.dtype != torch.int32 or wmap.numel() < param.numel() - 2128):
+        raise ValueError("wmap must be int32 [WTOT]")
     stride = int(slab.shape[-1])
     if inv.dtype != torch.int32 or inv.numel() != stride:
         raise ValueError("inv must be int32 [stride]")
@@ -90,7 +94,7 @@ def reduce_apply(slab: torch.Tensor, groups: int, inv: torch.Tensor, param: torc
         raise ValueError("slab must be contiguous [>= groups, stride]")
     _check_step_ctr(step_ctr)
     rc = _fns()["reduce_opt"](ptr(slab), int(groups), stride, None, ptr(inv), ptr(param), ptr(s0), ptr(s1),
-                              ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
+                              ptr(wt_out), ptr(wmap), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
                               stream_handle(param.device))
     check(rc, "mifx_wd_reduce_opt")
 

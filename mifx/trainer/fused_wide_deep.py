@@ -1,7 +1,7 @@
 """Device-resident, hipGraph-captured Wide&Deep trainer on the fused gfx950 kernels.
 
-One training step = ``wd_fused`` (forward + loss + backward, per-workgroup gradient slabs)
--> ``wd_reduce_opt`` (full slab sum + Adagrad/FTRL/Adam/SGD + bf16 weight image in ONE launch). When
+One training step = ``wdc_fused`` (csrc/wd_chain.hip; or ``wd_fused`` with kernel="tile") (forward + loss +
+backward, per-workgroup gradient slabs) -> ``wd_reduce_opt`` (full slab sum + Adagrad/FTRL/Adam/SGD + bf16 weight image in ONE launch). When
 data-parallel the local sum is written to ONE flat 82 KB gradient bucket, RCCL all-reduced over xGMI,
 and the optimizer launch reads that bucket. (The older two-launch ``wd_reduce`` -> ``wd_optimizer``
 path stays selectable with ``fused_update=False`` for A/B.) The input
@@ -51,16 +51,32 @@ def default_wide_opt(num_linear_columns: int = 9) -> OptSpec:
 
 
 class FusedWideDeepTrainer:
+    """kernel="chain" (default): csrc/wd_chain.hip, register-chained MFMA forward/backward, 128 examples per
+    workgroup iteration; kernel="tile": csrc/wide_deep.hip (wd_fused), LDS-staged activations, 64 per tile.
+    Both write the same kind of per-workgroup gradient slab, reduced + applied by wd_reduce_opt."""
+
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
-                 live_staging: bool = False, fused_update: bool = True):
+                 live_staging: bool = False, fused_update: bool = True, kernel: str = "chain"):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
+        if kernel not in ("chain", "tile"):
+            raise ValueError("kernel must be 'chain' or 'tile'")
+        self.kernel = kernel
         c = wdk.constants()
         assert c["WTOT"] == wdm.WTOT and c["STRIDE"] == wdm.STRIDE and c["NWIDE"] == wdm.NWIDE
-        self.T = c["T"]
+        if kernel == "chain":
+            from ..ops import wd_chain as wdc
+
+            cc = wdc.constants()
+            assert cc["LWEND"] == wdm.CHAIN_LWEND and cc["PAD"] == wdm.CHAIN_PAD
+            if not fused_update or not compact_slab or live_staging:
+                raise ValueError("the chained kernel uses the compact slab, full staging and the fused update")
+            self.T = cc["T"]
+        else:
+            self.T = c["T"]
         self.batch = int(batch)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
@@ -72,8 +88,14 @@ class FusedWideDeepTrainer:
         dev = self.device
         # compact_slab: store/reduce/all-reduce only the dW tiles that hold trainable entries;
         # live_staging: stage only the live rows/granules of the weight image into LDS
-        gidx, mask = wdm.canonical_index_maps(self.model.cfg, compact_slab)
-        tmap, self.stride = wdm.compact_tile_map(self.model.cfg, compact_slab)
+        if kernel == "chain":
+            tmap, self.stride, gidx, mask, wmap = wdm.chain_maps(self.model.cfg)
+            self.wmap = torch.from_numpy(wmap).to(dev)
+        else:
+            gidx, mask = wdm.canonical_index_maps(self.model.cfg, compact_slab)
+            tmap, self.stride = wdm.compact_tile_map(self.model.cfg, compact_slab)
+            self.wmap = None
+        self.gidx_np = gidx
         self.stage_dims = wdm.stage_dims(self.model.cfg) if live_staging else None
         self.tmap = torch.from_numpy(tmap).to(dev)
         self.gidx = torch.from_numpy(gidx).to(dev)
@@ -85,7 +107,7 @@ class FusedWideDeepTrainer:
         for sl, spec in ((slice(0, wdm.WTOT), self.dnn_opt), (slice(wdm.WTOT, n), self.wide_opt)):
             if spec.kind in ("adagrad", "ftrl"):
                 self.s0[sl] = spec.initial_accumulator_value
-        self.wt = self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16).contiguous()
+        self.wt = self._weight_image()
         # inverse of the (bijective on live entries) canonical -> slab-column map, -1 on padding columns
         inv = np.full(self.stride, -1, dtype=np.int32)
         live = np.nonzero(mask)[0]
@@ -106,6 +128,25 @@ class FusedWideDeepTrainer:
         self.graph = None
         self._graphs = None
 
+    def _weight_image(self) -> torch.Tensor:
+        """bf16 (as int16) weight image the fused kernel stages: canonical order (tile kernel) or the chained
+        kernel's C-ordered LDS layout."""
+        if self.kernel == "chain":
+            img = torch.from_numpy(wdm.chain_image(self.param.cpu()))
+            return img.to(self.device).to(torch.bfloat16).view(torch.int16).contiguous()
+        return self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16).contiguous()
+
+    def _launch(self, records, n, batch, start_fixed, step_ctr, slab, slab_loss, logits, grid, train) -> None:
+        if self.kernel == "chain":
+            from ..ops import wd_chain as wdc
+
+            wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.param[wdm.WTOT:], slab, slab_loss,
+                      logits, self.grad_scale, grid, train, self.tmap if train else None)
+        else:
+            wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.param[wdm.WTOT:], slab, slab_loss,
+                      logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
+                      self.stage_dims)
+
     # ---------------------------------------------------------------- data
     def set_data(self, records: torch.Tensor) -> None:
         """records: uint8 [N, 32] packed taxi records (see models.wide_deep.RECORD_DTYPE)."""
@@ -124,9 +165,8 @@ class FusedWideDeepTrainer:
     # ---------------------------------------------------------------- step
     def _local_grad(self) -> None:
         """fused fwd/bwd + slab reduction; for world>1 the result lands in `self.grad` (one row)."""
-        wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
-                  self.slab_loss, None, self.grad_scale, self.grid, True, self.tmap,
-                  self.stage_dims)
+        self._launch(self.records, self.n_data, self.batch, 0, self.step_ctr, self.slab, self.slab_loss, None,
+                     self.grid, True)
         if self.fused_update:
             if self.world > 1:
                 wdk.reduce_full(self.slab, self.grid, self.grad)
@@ -143,7 +183,7 @@ class FusedWideDeepTrainer:
         if self.fused_update:
             src, groups = (self.slab, self.grid) if self.world == 1 else (self.grad, 1)
             wdk.reduce_apply(src, groups, self.inv, self.param, self.s0, self.s1, self.wt, self.step_ctr,
-                             self.h_dnn, self.h_wide)
+                             self.h_dnn, self.h_wide, self.wmap)
             return
         if self.world == 1:
             src, nparts = (self.slab, 1) if self.grid == 1 else (self.partial, self.nsplit)
@@ -214,10 +254,10 @@ class FusedWideDeepTrainer:
         self.step_ctr.fill_(int(step))
 
     def gradients_once(self) -> np.ndarray:
-        """Run fwd/bwd on the current batch WITHOUT updating; return the tile-native gradient."""
-        wdk.fused(self.records, self.n_data, self.batch, 0, self.step_ctr, self.wt, self.param[wdm.WTOT:], self.slab,
-                  self.slab_loss, None, self.grad_scale, self.grid, True, self.tmap,
-                  self.stage_dims)
+        """Run fwd/bwd on the current batch WITHOUT updating; return the tile-native gradient (index it with
+        `self.gidx_np` for canonical order)."""
+        self._launch(self.records, self.n_data, self.batch, 0, self.step_ctr, self.slab, self.slab_loss, None,
+                     self.grid, True)
         if self.grid > 1:
             wdk.reduce(self.slab, self.grid, 1, self.grad)
             return self.grad[0].cpu().numpy()
@@ -229,8 +269,7 @@ class FusedWideDeepTrainer:
         n = records.shape[0]
         out = torch.empty(n, device=self.device)
         grid = min((n + self.T - 1) // self.T, 1024)
-        wdk.fused(records, n, n, 0, None, self.wt, self.param[wdm.WTOT:], None, None, out, 1.0, grid, False,
-                  stage_dims=self.stage_dims)
+        self._launch(records, n, n, 0, None, None, None, out, grid, False)
         return out
 
     def sync_to_model(self) -> wdm.WideDeepModel:
@@ -244,4 +283,4 @@ class FusedWideDeepTrainer:
         self.s0.copy_(sd["s0"])
         self.s1.copy_(sd["s1"])
         self.set_step(int(sd["step"].reshape(-1)[0]))
-        self.wt.copy_(self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16))
+        self.wt.copy_(self._weight_image())

@@ -144,8 +144,9 @@ def _emulated_grads(vec, rec):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["chain", "tile"])
 @pytest.mark.parametrize("batch", [40, 64, 1000, 8192])
-def test_fused_gradients_match_torch(batch):
+def test_fused_gradients_match_torch(batch, kernel):
     torch.manual_seed(batch)
     from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
 
@@ -157,11 +158,12 @@ def test_fused_gradients_match_torch(batch):
         for lin in m.dnn:
             lin.bias.normal_(0, 0.1)
     rec = synthetic_records(batch, seed=7)
-    tr = FusedWideDeepTrainer(m, batch=batch, device=dev)
+    tr = FusedWideDeepTrainer(m, batch=batch, device=dev, kernel=kernel)
     tr.set_data(rec.to(dev))
     g_tn = tr.gradients_once()
     torch.cuda.synchronize()
-    gidx, mask = wdm.canonical_index_maps()
+    _, mask = wdm.canonical_index_maps()
+    gidx = tr.gidx_np
     got = g_tn[gidx]
     loss_em, em = _emulated_grads(tr.param.cpu(), rec)
     # 1) exact data-path check against the bf16 emulation (only accumulation order differs)
@@ -174,7 +176,7 @@ def test_fused_gradients_match_torch(batch):
     # 2) against the fp32 PyTorch model: relative Frobenius error per tensor. The bf16 data path
     #    (inputs, activations, activation-grads rounded to 8 mantissa bits) costs a few % on the
     #    first layer at tiny batches (cancellation over 40 examples), <3 % at >= 1000.
-    named = wdm.canonical_grad_to_torch(g_tn, m)
+    named = wdm.canonical_grad_to_torch(g_tn, m, gidx)
     mref = wdm.unpack_canonical(tr.param.cpu(), wdm.WideDeepModel(seed=1))
     _, ref = _torch_grads(mref, rec)
     lim = 0.15 if batch < 1000 else 0.06
@@ -227,14 +229,15 @@ def test_fused_training_converges_and_graph_replay():
 
 
 @pytest.mark.gpu
-def test_fused_predict_matches_torch():
+@pytest.mark.parametrize("kernel", ["chain", "tile"])
+def test_fused_predict_matches_torch(kernel):
     from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
 
     dev = torch.device("cuda")
     m = wdm.WideDeepModel(seed=2)
     with torch.no_grad():
         m.wide.normal_(0, 0.5)
-    tr = FusedWideDeepTrainer(m, batch=64, device=dev)
+    tr = FusedWideDeepTrainer(m, batch=64, device=dev, kernel=kernel)
     rec = synthetic_records(5000, seed=8)
     got = tr.predict_logits(rec.to(dev)).cpu()
     mref = wdm.unpack_canonical(tr.param.cpu(), wdm.WideDeepModel(seed=2))
@@ -244,7 +247,8 @@ def test_fused_predict_matches_torch():
 
 
 @pytest.mark.gpu
-def test_fused_training_is_run_to_run_deterministic():
+@pytest.mark.parametrize("kernel", ["chain", "tile"])
+def test_fused_training_is_run_to_run_deterministic(kernel):
     """Two trainers from the same init on the same data must produce bit-identical parameters:
     slab reduction is fixed-order; checks that the in-LDS wide-gradient accumulation is too."""
     from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
@@ -253,7 +257,7 @@ def test_fused_training_is_run_to_run_deterministic():
     rec = synthetic_records(1 << 16, device=dev, seed=5)
     params = []
     for _ in range(2):
-        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=1), batch=8192, device=dev)
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=1), batch=8192, device=dev, kernel=kernel)
         tr.set_data(rec)
         for _ in range(10):
             tr.step()
@@ -299,7 +303,7 @@ def test_fused_reduce_opt_matches_two_launch_path(kind, batch):
     out, losses = [], []
     for fused_update in (False, True):
         tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=6), batch=batch, device=dev, dnn_opt=opts[0],
-                                  wide_opt=opts[1], fused_update=fused_update)
+                                  wide_opt=opts[1], fused_update=fused_update, kernel="tile")
         tr.set_data(rec)
         tr.step()
         torch.cuda.synchronize()
@@ -331,3 +335,45 @@ def test_reduce_full_matches_fp64_sum():
         ref = slab.double().sum(0)
         err = (out.double() - ref).abs().max().item()
         assert err <= 1e-6 * slab.abs().sum(0).max().item(), (groups, stride, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [40, 16384])
+def test_chain_kernel_step_matches_tile_kernel(batch):
+    """The register-chained kernel against the LDS-tile kernel: same data, same init, one fused step each
+    (gradient-slab sum + Adagrad/FTRL). Both are bf16 data paths with different accumulation orders, so the
+    updates agree to a tolerance; the chained kernel's re-emitted C-ordered bf16 image must equal the image
+    built from its own fp32 master weights."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(batch * 4, device=dev, seed=31)
+    out = []
+    for kernel in ("tile", "chain"):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=9), batch=batch, device=dev, kernel=kernel)
+        tr.set_data(rec)
+        tr.step()
+        torch.cuda.synchronize()
+        out.append((tr.param.clone(), tr.last_loss()))
+        if kernel == "chain":
+            img = torch.from_numpy(wdm.chain_image(tr.param.cpu())).to(dev).to(torch.bfloat16).view(torch.int16)
+            assert torch.equal(img, tr.wt)
+    (pa, la), (pb, lb) = out
+    assert abs(la - lb) <= 1e-2 * abs(la) + 1e-3, (la, lb)
+    d = (pa - pb).abs()
+    assert d.max().item() <= 5e-3 * (pa.abs().max().item() + 1e-3), d.max().item()
+
+
+def test_chain_maps_cover_trainable_parameters():
+    """chain_maps: every trainable canonical parameter has its own slab slot inside a live tile, and the
+    image map is a bijection onto the weight image's non-pad positions."""
+    tmap, stride, gidx, mask, wmap = wdm.chain_maps()
+    live = mask.astype(bool)
+    assert len(np.unique(gidx[live])) == live.sum()
+    assert (gidx[live] < stride).all()
+    assert len(np.unique(wmap)) == wdm.WTOT and wmap.max() < wdm.CHAIN_LWEND
+    m = wdm.WideDeepModel(seed=3)
+    vec = wdm.pack_canonical(m)
+    img = wdm.chain_image(vec)
+    np.testing.assert_array_equal(img[wmap], vec[:wdm.WTOT])
+    assert np.count_nonzero(img) == np.count_nonzero(vec[:wdm.WTOT])

@@ -1,6 +1,7 @@
 """Interleaved A/B timing of fused W&D trainer variants in one process (removes box-to-box variance):
-compact slab on/off x live weight staging on/off, at the throughput batch and the reference batch."""
-import itertools
+the register-chained kernel (csrc/wd_chain.hip) vs the LDS-tile kernel (csrc/wide_deep.hip), at several
+throughput batches and the reference batch. `--kernels chain,tile --batches 65536,40`."""
+import argparse
 import json
 import os
 import sys
@@ -15,18 +16,23 @@ from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernels", default="chain,tile")
+    ap.add_argument("--batches", default="65536,131072,40")
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
     dev = torch.device("cuda")
     data = synthetic_records(1 << 22, device=dev, seed=1)
     res = {}
-    for batch, steps in ((65536, 300), (40, 3000)):
+    for batch in (int(b) for b in a.batches.split(",")):
+        steps = 3000 if batch <= 1024 else 300
         trs = {}
-        for compact, live in itertools.product((False, True), (False, True)):
-            tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=dev, compact_slab=compact,
-                                      live_staging=live)
+        for k in a.kernels.split(","):
+            tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=dev, kernel=k)
             tr.set_data(data)
             tr.capture()
-            trs[(compact, live)] = tr
-        for _ in range(3):
+            trs[k] = tr
+        for _ in range(a.rounds):
             for key, tr in trs.items():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -34,9 +40,12 @@ def main():
                     tr.step()
                 torch.cuda.synchronize()
                 us = 1e6 * (time.perf_counter() - t0) / steps
-                res.setdefault(f"B={batch} compact={key[0]} live={key[1]}", []).append(round(us, 2))
+                res.setdefault(f"B={batch} kernel={key}", []).append(round(us, 2))
+        for key, tr in trs.items():
+            res.setdefault(f"B={batch} kernel={key} loss", []).append(round(tr.last_loss() / batch, 5))
+        del trs
     for k, v in res.items():
-        print(json.dumps({"config": k, "us_per_step": v, "best": min(v)}), flush=True)
+        print(json.dumps({"config": k, "values": v, "best": min(v)}), flush=True)
 
 
 if __name__ == "__main__":
