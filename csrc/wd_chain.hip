@@ -40,9 +40,15 @@ typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-constexpr int T = 128;     // examples per workgroup iteration
-constexpr int NTHR = 256;  // 4 waves x 32 examples
-constexpr int NWAVE = NTHR / 64;
+constexpr int T = 128;  // examples per workgroup iteration
+constexpr int MAXW = 8;  // waves per workgroup: T / (16 TBN), TBN = 16-example column blocks per wave (1 or 2)
+// Row padding (elements): WPAD for the weight images, PAD for the staging images. With the per-row XOR swizzles
+// below set to zero these are the bank-conflict controls: tools/lds_banks.py models every access site; WPAD 16
+// makes the forward row reads conflict-free and halves the transposed-read conflicts of the activation-gradient
+// product (3.1x -> 2x of the ideal LDS cycles); PAD 8 is the best plain pad for the staging images. (Non-zero
+// swizzle masks remove the remaining conflicts in the model, but their per-lane XORs defeat the compiler's
+// immediate-offset addressing and the 4- and 8-wave kernels then spill: measured, not adopted.)
+constexpr int WPAD = 16;
 constexpr int PAD = 8;
 
 constexpr int K1 = 32, N1 = 128;
@@ -51,13 +57,13 @@ constexpr int K3 = 96, N3 = 64;
 constexpr int K4 = 64, N4 = 64;
 constexpr int K5 = 64, N5 = 16;
 
-// weight image (bf16, LDS layout == global image layout): W_l^T [N_l][K_l + PAD], columns in C order
+// weight image (bf16, LDS layout == global image layout): W_l^T [N_l][K_l + WPAD], columns in C order
 constexpr int LW1 = 0;
-constexpr int LW2 = LW1 + N1 * (K1 + PAD);
-constexpr int LW3 = LW2 + N2 * (K2 + PAD);
-constexpr int LW4 = LW3 + N3 * (K3 + PAD);
-constexpr int LW5 = LW4 + N4 * (K4 + PAD);
-constexpr int LWEND = LW5 + N5 * (K5 + PAD);  // 30592
+constexpr int LW2 = LW1 + N1 * (K1 + WPAD);
+constexpr int LW3 = LW2 + N2 * (K2 + WPAD);
+constexpr int LW4 = LW3 + N3 * (K3 + WPAD);
+constexpr int LW5 = LW4 + N4 * (K4 + WPAD);
+constexpr int LWEND = LW5 + N5 * (K5 + WPAD);  // 33536
 // dW staging: dZ_l [T][N_l + PAD] (natural order) followed by A_{l-1} [T][K_l + PAD] (C order)
 constexpr int stage_len(int K, int N) { return T * (N + PAD) + T * (K + PAD); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -122,34 +128,85 @@ __device__ __forceinline__ void block_sync_lds() {
 }
 constexpr v4f kZero4 = {0.f, 0.f, 0.f, 0.f};
 
+// ---- LDS image swizzles: element (row, col) of a [rows][C] bf16 image lives at row * C + 4 * (col / 4 ^ X(row)) +
+// col % 4, X(row) = XOR of m[b] over the set bits b of row (8-byte granules; masks even, so the 16-byte pairs
+// that ds_read_b128 / ds_write_b128 move stay contiguous). Masks chosen by tools/lds_banks.py (bank model of
+// every access site in this kernel): weight images -> conflict-free forward row reads and activation-gradient
+// transposed reads; staging images -> near conflict-free dW transposed reads, stores and mask reads.
+// models.wide_deep.CHAIN_WSWZ mirrors WSwz for the host-built image.
+struct Swz {
+  int m[7];
+};
+// conflict-free in the bank model but not adopted (register cost, see WPAD): weight K=128 {4, 8, 16, 0, 16, 0, 0},
+// K=64 {0, 4, 8, 0, 8, 0, 0}, K=32/96 {0, 0, 4, 0, 4, 0, 0}; staging C=128 {4, 8, 2, 16}, C=64 {2, 4, 8, 10},
+// C=32/96 {0, 2, 4, 6}
+template <int K>
+__host__ __device__ constexpr Swz wswz() {
+  return Swz{{0, 0, 0, 0, 0, 0, 0}};
+}
+template <int C>
+__host__ __device__ constexpr Swz sswz() {
+  return Swz{{0, 0, 0, 0, 0, 0, 0}};
+}
+__host__ __device__ constexpr int xmask(const Swz& s, int row) {
+  int x = 0;
+  for (int b = 0; b < 7; ++b)
+    if ((row >> b) & 1) x ^= s.m[b];
+  return x;
+}
+// element offset of (row_lane + row_c, col) in an image with rows of RL elements, where row_lane and row_c have
+// disjoint bits (so the row mask is xmask(row_lane) ^ xmask(row_c): the constant part folds at compile time)
+template <int RL>
+__device__ __forceinline__ int soff(const Swz& s, int xl, int row_lane, int row_c, int col) {
+  return (row_lane + row_c) * RL + 4 * ((col >> 2) ^ xl ^ xmask(s, row_c)) + (col & 3);
+}
+
+#ifdef WDC_STAMPS  // diagnostic build only (tools/build_stamps.sh): per-wave shader-clock stamps of block 0
+__device__ unsigned long long g_wdc_stamps[MAXW][32];
+#define STAMP(i)                                                                                  \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (blockIdx.x == 0 && lane == 0 && stamp_on) g_wdc_stamps[w][i] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 // ---- forward layer for the wave's two column blocks: acc[tb][nt] = W^T[16 nt ..][.] . B[tb][.]
 // W image rows natural, columns C order; B[tb][s] is the k-step-s fragment (C order) of the layer input.
-template <int K, int N>
-__device__ __forceinline__ void fwd(const uint16_t* W, const v8bf (&B)[2][K / 32], v4f (&acc)[2][N / 16], int r, int h) {
+template <int K, int N, int TBN>
+__device__ __forceinline__ void fwd(const uint16_t* W, const v8bf (&B)[TBN][K / 32], v4f (&acc)[TBN][N / 16], int r,
+                                    int h) {
   constexpr int KS = K / 32, NT = N / 16;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[0][nt] = acc[1][nt] = kZero4;
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int tb = 0; tb < TBN; ++tb) acc[tb][nt] = kZero4;
+  constexpr Swz sw = wswz<K>();
+  const int xl = xmask(sw, r);
   v8bf wa[2][NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) wa[0][nt] = ld8(W + (16 * nt + r) * (K + PAD) + 8 * h);
+  for (int nt = 0; nt < NT; ++nt) wa[0][nt] = ld8(W + soff<K + WPAD>(sw, xl, r, 16 * nt, 8 * h));
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (s + 1 < KS) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) wa[(s + 1) & 1][nt] = ld8(W + (16 * nt + r) * (K + PAD) + 32 * (s + 1) + 8 * h);
+      for (int nt = 0; nt < NT; ++nt) wa[(s + 1) & 1][nt] = ld8(W + soff<K + WPAD>(sw, xl, r, 16 * nt, 32 * (s + 1) + 8 * h));
     }
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      acc[0][nt] = mfma(wa[s & 1][nt], B[0][s], acc[0][nt]);
-      acc[1][nt] = mfma(wa[s & 1][nt], B[1][s], acc[1][nt]);
-    }
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int tb = 0; tb < TBN; ++tb) acc[tb][nt] = mfma(wa[s & 1][nt], B[tb][s], acc[tb][nt]);
   }
 }
 
-template <int N>
-__device__ __forceinline__ void relu_pack(const v4f (&acc)[2][N / 16], v8bf (&out)[2][N / 32]) {
+template <int N, int TBN>
+__device__ __forceinline__ void relu_pack(const v4f (&acc)[TBN][N / 16], v8bf (&out)[TBN][N / 32]) {
 #pragma unroll
-  for (int tb = 0; tb < 2; ++tb)
+  for (int tb = 0; tb < TBN; ++tb)
 #pragma unroll
     for (int s = 0; s < N / 32; ++s) out[tb][s] = pack_relu(acc[tb][2 * s], acc[tb][2 * s + 1]);
 }
@@ -157,44 +214,51 @@ __device__ __forceinline__ void relu_pack(const v4f (&acc)[2][N / 16], v8bf (&ou
 // ---- activation gradient: dA^T[k][t] = sum_n W[n][k] dZ[n][t] for the W image of a layer (K x N), its
 // rows (n, natural) read transposed at the rows that match the chained dZ fragments (C order of the layer
 // above). dz[tb][kt'] are the previous gradient tiles (N/16 of them); out[tb][kt] the K/16 output tiles.
-template <int K, int N>
-__device__ __forceinline__ void bwd_dA(const uint16_t* W, const v4bf (&dz)[2][N / 16], v4f (&out)[2][K / 16], int r,
+template <int K, int N, int TBN>
+__device__ __forceinline__ void bwd_dA(const uint16_t* W, const v4bf (&dz)[TBN][N / 16], v4f (&out)[TBN][K / 16], int r,
                                        int h) {
   constexpr int NS = N / 32, KT = K / 16;
   const int q = r >> 2, p = r & 3;
   const int rb = 16 * (h & 1) + 4 * (h >> 1) + q;
-  v8bf b[2][NS];
+  constexpr Swz sw = wswz<K>();
+  const int xl = xmask(sw, rb);
+  v8bf b[TBN][NS];
 #pragma unroll
-  for (int tb = 0; tb < 2; ++tb)
+  for (int tb = 0; tb < TBN; ++tb)
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[tb][s] = cat_bf(dz[tb][2 * s], dz[tb][2 * s + 1]);
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt) out[0][kt] = out[1][kt] = kZero4;
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int tb = 0; tb < TBN; ++tb) out[tb][kt] = kZero4;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     v8bf a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const uint16_t* pa = W + (32 * s + rb) * (K + PAD) + 16 * kt + 4 * p;
-      a[s] = cat8(tr_read(pa), tr_read(pa + 8 * (K + PAD)));
+      a[s] = cat8(tr_read(W + soff<K + WPAD>(sw, xl, rb, 32 * s, 16 * kt + 4 * p)),
+                  tr_read(W + soff<K + WPAD>(sw, xl, rb, 32 * s + 8, 16 * kt + 4 * p)));
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      out[0][kt] = mfma(a[s], b[0][s], out[0][kt]);
-      out[1][kt] = mfma(a[s], b[1][s], out[1][kt]);
-    }
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int tb = 0; tb < TBN; ++tb) out[tb][kt] = mfma(a[s], b[tb][s], out[tb][kt]);
   }
 }
 
 // ReLU mask of the layer input from the staged activation (C order) and bf16 pack of the gradient
-template <int K>
-__device__ __forceinline__ void mask_grad(const v4f (&g)[2][K / 16], const uint16_t* SA, int w, int r, int h,
-                                          v4bf (&dz)[2][K / 16]) {
+template <int K, int TBN>
+__device__ __forceinline__ void mask_grad(const v4f (&g)[TBN][K / 16], const uint16_t* SA, int w, int r, int h,
+                                          v4bf (&dz)[TBN][K / 16]) {
+  constexpr Swz sw = sswz<K>();
+  const int xl = xmask(sw, r);
 #pragma unroll
-  for (int tb = 0; tb < 2; ++tb)
+  for (int tb = 0; tb < TBN; ++tb)
 #pragma unroll
     for (int kt = 0; kt < K / 16; ++kt) {
-      const uint2 m = *(const uint2*)(SA + (32 * w + 16 * tb + r) * (K + PAD) + 16 * kt + 4 * h);
+      // row 16 TBN w + 16 tb + r: the wave part is not a compile-time constant, fold it at run time
+      const int rc = 16 * TBN * w + 16 * tb;
+      const uint2 m = *(const uint2*)(SA + (rc + r) * (K + PAD) + 4 * ((4 * kt + h) ^ xl ^ xmask(sw, rc)));
       v4bf o;
       o[0] = (bf16)((m.x & 0xffffu) ? g[tb][kt][0] : 0.f);
       o[1] = (bf16)((m.x >> 16) ? g[tb][kt][1] : 0.f);
@@ -206,21 +270,24 @@ __device__ __forceinline__ void mask_grad(const v4f (&g)[2][K / 16], const uint1
 
 // stage dZ (gradient tiles in C order of the layer above -> natural order columns) and the layer's input
 // activation fragments (C order) for the dW product of a layer with dims K x N
-template <int K, int N>
-__device__ __forceinline__ void stage(uint16_t* S, const v4bf (&dz)[2][N / 16], const v8bf (&a)[2][K / 32], int w, int r,
-                                      int h) {
+template <int K, int N, int TBN>
+__device__ __forceinline__ void stage(uint16_t* S, const v4bf (&dz)[TBN][N / 16], const v8bf (&a)[TBN][K / 32], int w,
+                                      int r, int h) {
   uint16_t* SZ = S;
   uint16_t* SA = S + T * (N + PAD);
+  constexpr Swz szw = sswz<N>(), saw = sswz<K>();
+  const int xz = xmask(szw, r), xa = xmask(saw, r);
 #pragma unroll
-  for (int tb = 0; tb < 2; ++tb) {
-    const int row = 32 * w + 16 * tb + r;
+  for (int tb = 0; tb < TBN; ++tb) {
+    const int rc = 16 * TBN * w + 16 * tb, row = rc + r;
+    const int xzr = xz ^ xmask(szw, rc), xar = xa ^ xmask(saw, rc);
 #pragma unroll
     for (int kt = 0; kt < N / 16; ++kt) {
       const int f0 = 32 * (kt >> 1) + 16 * (h & 1) + 8 * (kt & 1) + 4 * (h >> 1);
-      *(v4bf*)(SZ + row * (N + PAD) + f0) = dz[tb][kt];
+      *(v4bf*)(SZ + row * (N + PAD) + 4 * ((f0 >> 2) ^ xzr)) = dz[tb][kt];
     }
 #pragma unroll
-    for (int s = 0; s < K / 32; ++s) *(v8bf*)(SA + row * (K + PAD) + 32 * s + 8 * h) = a[tb][s];
+    for (int s = 0; s < K / 32; ++s) *(v8bf*)(SA + row * (K + PAD) + 4 * ((8 * s + 2 * h) ^ xar)) = a[tb][s];
   }
 }
 
@@ -232,18 +299,20 @@ __device__ __forceinline__ void dw_phase(v4f (&acc)[NTW * KTW], const uint16_t* 
   const uint16_t* SZ = S;
   const uint16_t* SA = S + T * (N + PAD);
   const int q = r >> 2, p = r & 3;
+  constexpr Swz szw = sswz<N>(), saw = sswz<K>();
+  const int rl = 8 * h + q, xz = xmask(szw, rl), xa = xmask(saw, rl);
 #pragma unroll
   for (int ts = 0; ts < T / 32; ++ts) {
     v8bf fa[NTW], fb[KTW];
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
-      const uint16_t* pa = SZ + (32 * ts + 8 * h + q) * (N + PAD) + 16 * (nt0 + i * ntS) + 4 * p;
-      fa[i] = cat8(tr_read(pa), tr_read(pa + 4 * (N + PAD)));
+      const int col = 16 * (nt0 + i * ntS) + 4 * p;
+      fa[i] = cat8(tr_read(SZ + soff<N + PAD>(szw, xz, rl, 32 * ts, col)), tr_read(SZ + soff<N + PAD>(szw, xz, rl, 32 * ts + 4, col)));
     }
 #pragma unroll
     for (int j = 0; j < KTW; ++j) {
-      const uint16_t* pb = SA + (32 * ts + 8 * h + q) * (K + PAD) + 16 * (kt0 + j * ktS) + 4 * p;
-      fb[j] = cat8(tr_read(pb), tr_read(pb + 4 * (K + PAD)));
+      const int col = 16 * (kt0 + j * ktS) + 4 * p;
+      fb[j] = cat8(tr_read(SA + soff<K + PAD>(saw, xa, rl, 32 * ts, col)), tr_read(SA + soff<K + PAD>(saw, xa, rl, 32 * ts + 4, col)));
     }
 #pragma unroll
     for (int i = 0; i < NTW; ++i)
@@ -272,8 +341,8 @@ __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], c
   }
 }
 
-template <bool TRAIN>
-__global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ data, long long n_data, long long batch,
+template <bool TRAIN, int TBN>
+__global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint4* __restrict__ data, long long n_data, long long batch,
                                                      long long start_fixed, const long long* __restrict__ step_ctr,
                                                      const uint4* __restrict__ wimg, const float* __restrict__ wide,
                                                      float* __restrict__ slab, float* __restrict__ slab_loss,
@@ -283,7 +352,11 @@ __global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ d
   float* wgrad = (float*)(lds + LSEND);
   float* red = wgrad + WIDE_PAD;
   int* wgi = (int*)wgrad;
+  constexpr int NWAVE = T / (16 * TBN), NTHR = 64 * NWAVE, EPW = 16 * TBN;  // waves, threads, examples per wave
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
+  bool stamp_on = true;
+  (void)stamp_on;
+  STAMP(0);
 
   {  // stage the bf16 weight image (already in LDS layout): all global loads, then all LDS stores
     constexpr int NCH = LWEND / 8, PER = (NCH + NTHR - 1) / NTHR;
@@ -306,53 +379,67 @@ __global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ d
   const float qinv = 1.f / qscale;
   const float qmax = 1073741824.f / (float)(max(my_iters, 1) * T);
 
-  // dW tile ownership (wave w): L1 nt {2w, 2w+1} x kt 0 (kt 1 holds only padding columns);
-  // L2 nt 0..5 x kt {2w, 2w+1}; L3 nt w x kt 0..5; L4 nt w x kt 0..3; L5 nt 0 x kt w
-  v4f acc1[2], acc2[12], acc3[6], acc4[4], acc5[1];
-  int ct1[2], ct2[12], ct3[6], ct4[4], ct5[1];
+  // dW tile ownership (wave w); 4 waves: L1 nt {2w, 2w+1} x kt 0 (kt 1 holds only padding columns);
+  // L2 nt 0..5 x kt {2w, 2w+1}; L3 nt w x kt 0..5; L4 nt w x kt 0..3; L5 nt 0 x kt w.
+  // 8 waves: L1 nt w x kt 0; L2 nt 0..5 x kt w; L3 nt w%4 x kt 3(w/4)..+2; L4 nt w%4 x kt 2(w/4)..+1;
+  // L5 nt 0 x kt w (waves 0..3)
+  constexpr int O1N = TBN == 2 ? 2 : 1, O2K = TBN == 2 ? 2 : 1, O3K = TBN == 2 ? 6 : 3,
+                O4K = TBN == 2 ? 4 : 2;
+  const int n1 = TBN == 2 ? 2 * w : w, k2 = TBN == 2 ? 2 * w : w, n3 = w & 3, k3 = TBN == 2 ? 0 : 3 * (w >> 2),
+            n4 = w & 3, k4 = TBN == 2 ? 0 : 2 * (w >> 2);
+  const bool l5 = w < 4;
+  v4f acc1[O1N], acc2[6 * O2K], acc3[O3K], acc4[O4K], acc5[1];
+  int ct1[O1N], ct2[6 * O2K], ct3[O3K], ct4[O4K], ct5[1];
   if (TRAIN) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) acc1[i] = kZero4;
+    for (int i = 0; i < O1N; ++i) acc1[i] = kZero4;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) acc2[i] = kZero4;
+    for (int i = 0; i < 6 * O2K; ++i) acc2[i] = kZero4;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) acc3[i] = kZero4;
+    for (int i = 0; i < O3K; ++i) acc3[i] = kZero4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc4[i] = kZero4;
+    for (int i = 0; i < O4K; ++i) acc4[i] = kZero4;
     acc5[0] = kZero4;
-    load_ct<K1, 2, 1>(ct1, TB1, 2 * w, 1, 0, 0, tmap);
-    load_ct<K2, 6, 2>(ct2, TB2, 0, 1, 2 * w, 1, tmap);
-    load_ct<K3, 1, 6>(ct3, TB3, w, 0, 0, 1, tmap);
-    load_ct<K4, 1, 4>(ct4, TB4, w, 0, 0, 1, tmap);
-    load_ct<K5, 1, 1>(ct5, TB5, 0, 0, w, 0, tmap);
+    load_ct<K1, O1N, 1>(ct1, TB1, n1, 1, 0, 0, tmap);
+    load_ct<K2, 6, O2K>(ct2, TB2, 0, 1, k2, 1, tmap);
+    load_ct<K3, 1, O3K>(ct3, TB3, n3, 0, k3, 1, tmap);
+    load_ct<K4, 1, O4K>(ct4, TB4, n4, 0, k4, 1, tmap);
+    load_ct<K5, 1, 1>(ct5, TB5, 0, 0, w & 3, 0, tmap);
+    if (!l5) ct5[0] = -1;
   }
   float loss_sum = 0.f, dl_sum = 0.f;
-  const int mtb = h & 1;  // the column block whose wide part / loss this lane computes (lanes h < 2 own it)
+  // the column block whose wide part / loss this lane computes (lanes h < TBN own one each)
+  const int mtb = TBN == 2 ? (h & 1) : 0;
 
-  auto fetch = [&](int it, uint4 (&u)[2][2]) {
+  auto fetch = [&](int it, uint4 (&u)[TBN][2]) {
 #pragma unroll
-    for (int tb = 0; tb < 2; ++tb) {
-      const long long row = min((long long)it * T + 32 * w + 16 * tb + r, batch - 1);
+    for (int tb = 0; tb < TBN; ++tb) {
+      const long long row = min((long long)it * T + EPW * w + 16 * tb + r, batch - 1);
       long long di = start + row;
       if (di >= n_data) di -= n_data;  // host guarantees batch <= n_data
       u[tb][0] = data[2 * di];
       u[tb][1] = data[2 * di + 1];
     }
   };
-  uint4 nu[2][2];
+  uint4 nu[TBN][2];
   fetch(blockIdx.x, nu);
 
+  STAMP(1);
   for (int it = blockIdx.x; it < niters; it += gridDim.x) {
-    uint4 u[2][2];
+#ifdef WDC_STAMPS
+    stamp_on = niters > (int)gridDim.x ? it == (int)(blockIdx.x + gridDim.x) : it == (int)blockIdx.x;
+#endif
+    STAMP(2);
+    uint4 u[TBN][2];
 #pragma unroll
-    for (int tb = 0; tb < 2; ++tb) {
+    for (int tb = 0; tb < TBN; ++tb) {
       u[tb][0] = nu[tb][0];
       u[tb][1] = nu[tb][1];
     }
     fetch(it + gridDim.x, nu);  // next iteration's records
 
     // wide gather for the lane's column block (issued before the forward: its latency hides under MFMAs)
-    const uint4 m0 = mtb ? u[1][0] : u[0][0], m1 = mtb ? u[1][1] : u[0][1];
+    const uint4 m0 = mtb ? u[TBN - 1][0] : u[0][0], m1 = mtb ? u[TBN - 1][1] : u[0][1];
     const uint32_t idw[5] = {m0.w, m1.x, m1.y, m1.z, m1.w};
     int ids[9];
     float wv[9];
@@ -366,45 +453,46 @@ __global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ d
     const float wbias = wide[WIDE_BIAS];
 
     // ---- forward, in registers
-    v8bf a0[2][1];
+    v8bf a0[TBN][1];
 #pragma unroll
-    for (int tb = 0; tb < 2; ++tb) {
+    for (int tb = 0; tb < TBN; ++tb) {
       const v8bf x = {(bf16)__uint_as_float(u[tb][0].x), (bf16)__uint_as_float(u[tb][0].y),
                       (bf16)__uint_as_float(u[tb][0].z), (bf16)1.0f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
       a0[tb][0] = h == 0 ? x : (v8bf){};
     }
-    v8bf a1[2][N1 / 32], a2[2][N2 / 32], a3[2][N3 / 32], a4[2][N4 / 32];
-    v4f z5[2][1];
+    v8bf a1[TBN][N1 / 32], a2[TBN][N2 / 32], a3[TBN][N3 / 32], a4[TBN][N4 / 32];
+    v4f z5[TBN][1];
     {
-      v4f acc[2][N1 / 16];
-      fwd<K1, N1>(lds + LW1, a0, acc, r, h);
-      relu_pack<N1>(acc, a1);
+      v4f acc[TBN][N1 / 16];
+      fwd<K1, N1, TBN>(lds + LW1, a0, acc, r, h);
+      relu_pack<N1, TBN>(acc, a1);
     }
     {
-      v4f acc[2][N2 / 16];
-      fwd<K2, N2>(lds + LW2, a1, acc, r, h);
-      relu_pack<N2>(acc, a2);
+      v4f acc[TBN][N2 / 16];
+      fwd<K2, N2, TBN>(lds + LW2, a1, acc, r, h);
+      relu_pack<N2, TBN>(acc, a2);
     }
     {
-      v4f acc[2][N3 / 16];
-      fwd<K3, N3>(lds + LW3, a2, acc, r, h);
-      relu_pack<N3>(acc, a3);
+      v4f acc[TBN][N3 / 16];
+      fwd<K3, N3, TBN>(lds + LW3, a2, acc, r, h);
+      relu_pack<N3, TBN>(acc, a3);
     }
     {
-      v4f acc[2][N4 / 16];
-      fwd<K4, N4>(lds + LW4, a3, acc, r, h);
-      relu_pack<N4>(acc, a4);
+      v4f acc[TBN][N4 / 16];
+      fwd<K4, N4, TBN>(lds + LW4, a3, acc, r, h);
+      relu_pack<N4, TBN>(acc, a4);
     }
-    fwd<K5, N5>(lds + LW5, a4, z5, r, h);
+    fwd<K5, N5, TBN>(lds + LW5, a4, z5, r, h);
 
+    STAMP(3);
     // ---- logit = deep (row 0 of the layer-5 tile: lane (r, h = 0)) + wide; loss and dlogit
-    const float zd0 = __shfl(z5[0][0][0], r), zd1 = __shfl(z5[1][0][0], r);
+    const float zd0 = __shfl(z5[0][0][0], r), zd1 = __shfl(z5[TBN - 1][0][0], r);
     float wl = wbias;
 #pragma unroll
     for (int f = 0; f < 9; ++f) wl += wv[f];
     const float x = (mtb ? zd1 : zd0) + wl;
-    const long long grow = (long long)it * T + 32 * w + 16 * mtb + r;
-    const bool own = h < 2 && grow < batch;
+    const long long grow = (long long)it * T + EPW * w + 16 * mtb + r;
+    const bool own = h < TBN && grow < batch;
     const float y = (float)(idw[4] >> 16);
     const float lossv = fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
     if (!TRAIN) {
@@ -420,93 +508,114 @@ __global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ d
       dl_sum += dl;
     }
     // dlogit of the lane's example in both column blocks, rounded to bf16 like the staged dZ5 the dW5 MFMA reads
-    const float dlb[2] = {(float)(bf16)__shfl(dl, r), (float)(bf16)__shfl(dl, 16 + r)};
+    float dlb[TBN];
+#pragma unroll
+    for (int tb = 0; tb < TBN; ++tb) dlb[tb] = (float)(bf16)__shfl(dl, 16 * tb + r);
 
     // ---- layer 5: stage (dZ5, A4); dW5; dA4 = w5 (x) dl on the VALU, masked
+    STAMP(4);
     uint16_t* S = lds + LS;
     block_sync_lds();  // previous iteration's dW1 reads of the staging area are done
+    STAMP(5);
     if (own) {
       const int q = __float2int_rn(fminf(fmaxf(dl * qscale, -qmax), qmax));
 #pragma unroll
       for (int f = 0; f < 9; ++f) atomicAdd(&wgi[ids[f]], q);
     }
     {
-      v4bf d5[2][1];
+      v4bf d5[TBN][1];
 #pragma unroll
-      for (int tb = 0; tb < 2; ++tb) {
+      for (int tb = 0; tb < TBN; ++tb) {
         v4bf o = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
         if (h == 0) o[0] = (bf16)dlb[tb];
         d5[tb][0] = o;
       }
       // dZ5 has one natural-order tile (N5 = 16): stage it directly (row t: [dl, 0 ... 0])
 #pragma unroll
-      for (int tb = 0; tb < 2; ++tb) {
-        const int row = 32 * w + 16 * tb + r;
-        *(v4bf*)(S + row * (N5 + PAD) + 4 * h) = d5[tb][0];
+      for (int tb = 0; tb < TBN; ++tb) {
+        const int row = EPW * w + 16 * tb + r;
+        constexpr Swz saw = sswz<K5>();
+        const int xar = xmask(saw, row);
+        *(v4bf*)(S + row * (N5 + PAD) + 4 * (h ^ xmask(sswz<N5>(), row))) = d5[tb][0];
 #pragma unroll
-        for (int s = 0; s < K5 / 32; ++s) *(v8bf*)(S + T * (N5 + PAD) + row * (K5 + PAD) + 32 * s + 8 * h) = a4[tb][s];
+        for (int s = 0; s < K5 / 32; ++s)
+          *(v8bf*)(S + T * (N5 + PAD) + row * (K5 + PAD) + 4 * ((8 * s + 2 * h) ^ xar)) = a4[tb][s];
       }
     }
     block_sync_lds();
-    dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w, 0, r, h);
-    v4bf dz4[2][K5 / 16];
+    STAMP(6);
+    if (l5) dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w & 3, 0, r, h);
+    v4bf dz4[TBN][K5 / 16];
     {
-      v4f g[2][K5 / 16];
+      v4f g[TBN][K5 / 16];
 #pragma unroll
       for (int kt = 0; kt < K5 / 16; ++kt) {
-        const uint2 wv2 = *(const uint2*)(lds + LW5 + 16 * kt + 4 * h);  // W5 row 0 (the logit row), C order
+        const uint2 wv2 = *(const uint2*)(lds + LW5 + 16 * kt + 4 * h);  // W5 row 0 (the logit row; X(0) = 0)
         const float w5[4] = {__uint_as_float(wv2.x << 16), __uint_as_float(wv2.x & 0xffff0000u),
                              __uint_as_float(wv2.y << 16), __uint_as_float(wv2.y & 0xffff0000u)};
 #pragma unroll
-        for (int tb = 0; tb < 2; ++tb)
+        for (int tb = 0; tb < TBN; ++tb)
 #pragma unroll
           for (int e = 0; e < 4; ++e) g[tb][kt][e] = w5[e] * dlb[tb];
       }
-      mask_grad<K5>(g, S + T * (N5 + PAD), w, r, h, dz4);
+      mask_grad<K5, TBN>(g, S + T * (N5 + PAD), w, r, h, dz4);
     }
     block_sync_lds();
 
     // ---- layer 4
-    stage<K4, N4>(S, dz4, a3, w, r, h);
+    STAMP(7);
+    stage<K4, N4, TBN>(S, dz4, a3, w, r, h);
     block_sync_lds();
-    dw_phase<K4, N4, 1, 4>(acc4, S, w, 0, 0, 1, r, h);
-    v4bf dz3[2][K4 / 16];
+    STAMP(8);
+    dw_phase<K4, N4, 1, O4K>(acc4, S, n4, 0, k4, 1, r, h);
+    v4bf dz3[TBN][K4 / 16];
     {
-      v4f g[2][K4 / 16];
-      bwd_dA<K4, N4>(lds + LW4, dz4, g, r, h);
-      mask_grad<K4>(g, S + T * (N4 + PAD), w, r, h, dz3);
+      v4f g[TBN][K4 / 16];
+      bwd_dA<K4, N4, TBN>(lds + LW4, dz4, g, r, h);
+      mask_grad<K4, TBN>(g, S + T * (N4 + PAD), w, r, h, dz3);
     }
     block_sync_lds();
 
     // ---- layer 3
-    stage<K3, N3>(S, dz3, a2, w, r, h);
+    STAMP(9);
+    stage<K3, N3, TBN>(S, dz3, a2, w, r, h);
     block_sync_lds();
-    dw_phase<K3, N3, 1, 6>(acc3, S, w, 0, 0, 1, r, h);
-    v4bf dz2[2][K3 / 16];
+    STAMP(10);
+    dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
+    v4bf dz2[TBN][K3 / 16];
     {
-      v4f g[2][K3 / 16];
-      bwd_dA<K3, N3>(lds + LW3, dz3, g, r, h);
-      mask_grad<K3>(g, S + T * (N3 + PAD), w, r, h, dz2);
+      v4f g[TBN][K3 / 16];
+      bwd_dA<K3, N3, TBN>(lds + LW3, dz3, g, r, h);
+      mask_grad<K3, TBN>(g, S + T * (N3 + PAD), w, r, h, dz2);
     }
     block_sync_lds();
 
     // ---- layer 2
-    stage<K2, N2>(S, dz2, a1, w, r, h);
+    STAMP(11);
+    stage<K2, N2, TBN>(S, dz2, a1, w, r, h);
     block_sync_lds();
-    dw_phase<K2, N2, 6, 2>(acc2, S, 0, 1, 2 * w, 1, r, h);
-    v4bf dz1[2][K2 / 16];
+    STAMP(12);
+    dw_phase<K2, N2, 6, O2K>(acc2, S, 0, 1, k2, 1, r, h);
+    v4bf dz1[TBN][K2 / 16];
     {
-      v4f g[2][K2 / 16];
-      bwd_dA<K2, N2>(lds + LW2, dz2, g, r, h);
-      mask_grad<K2>(g, S + T * (N2 + PAD), w, r, h, dz1);
+      v4f g[TBN][K2 / 16];
+      bwd_dA<K2, N2, TBN>(lds + LW2, dz2, g, r, h);
+      mask_grad<K2, TBN>(g, S + T * (N2 + PAD), w, r, h, dz1);
     }
     block_sync_lds();
 
     // ---- layer 1
-    stage<K1, N1>(S, dz1, a0, w, r, h);
+    STAMP(13);
+    stage<K1, N1, TBN>(S, dz1, a0, w, r, h);
     block_sync_lds();
-    dw_phase<K1, N1, 2, 1>(acc1, S, 2 * w, 1, 0, 0, r, h);
+    STAMP(14);
+    dw_phase<K1, N1, O1N, 1>(acc1, S, n1, 1, 0, 0, r, h);
+    STAMP(15);
   }
+#ifdef WDC_STAMPS
+  stamp_on = true;
+#endif
+  STAMP(16);
 
   // ---- epilogue: per-workgroup slab (same layout as wd_fused)
   for (int o = 32; o > 0; o >>= 1) {
@@ -520,10 +629,10 @@ __global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ d
   }
   if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * stride;
-    store_tiles<2>(my, acc1, ct1, lane);
-    store_tiles<12>(my, acc2, ct2, lane);
-    store_tiles<6>(my, acc3, ct3, lane);
-    store_tiles<4>(my, acc4, ct4, lane);
+    store_tiles<O1N>(my, acc1, ct1, lane);
+    store_tiles<6 * O2K>(my, acc2, ct2, lane);
+    store_tiles<O3K>(my, acc3, ct3, lane);
+    store_tiles<O4K>(my, acc4, ct4, lane);
     store_tiles<1>(my, acc5, ct5, lane);
   }
   __syncthreads();
@@ -544,46 +653,66 @@ __global__ __launch_bounds__(NTHR, 1) void wdc_fused(const uint4* __restrict__ d
     for (int i = 0; i < NWAVE; ++i) l += red[i];
     slab_loss[blockIdx.x] = l;
   }
+  STAMP(17);
+}
+
+template <bool TRAIN, int TBN>
+void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
+            const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
+            float* logits_out, float grad_scale, const int* tmap, int stride) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)wdc_fused<TRAIN, TBN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((wdc_fused<TRAIN, TBN>), grid, dim3(64 * (T / (16 * TBN))), LDS_BYTES, stream, (const uint4*)data,
+                     n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out,
+                     grad_scale, tmap, stride);
 }
 
 }  // namespace
 
 extern "C" {
 
-// T, LWEND (weight image elements), LDS_BYTES, PAD, NTILE, WIDE_PAD
+// T, LWEND (weight image elements), LDS_BYTES, WPAD (weight-image row pad), NTILE, WIDE_PAD
 int mifx_wdc_constants(int* out, int n) {
-  const int v[] = {T, LWEND, LDS_BYTES, PAD, NTILE, WIDE_PAD, LW1, LW2, LW3, LW4, LW5};
+  const int v[] = {T, LWEND, LDS_BYTES, WPAD, NTILE, WIDE_PAD, LW1, LW2, LW3, LW4, LW5};
   const int m = (int)(sizeof(v) / sizeof(int));
   for (int i = 0; i < n && i < m; ++i) out[i] = v[i];
   return m;
 }
 
 // One launch = forward (+ loss) [+ backward into the per-workgroup slab] over `batch` records starting at
+// waves: 4 (4 waves x 32 examples, one wave per SIMD) or 8 (8 waves x 16 examples, two waves per SIMD).
 // (step_ctr[0] * batch) % n_data (or start_fixed when step_ctr is null). wimg: the bf16 weight image in LDS
 // layout (LWEND elements, C-ordered columns, see models.wide_deep.chain_image).
 int mifx_wdc_fused(const void* data, long long n_data, long long batch, long long start_fixed,
                    const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
                    float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
-                   hipStream_t stream) {
-  static bool attr_done = false;
-  if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wdc_fused<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)wdc_fused<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    attr_done = true;
-  }
+                   int waves, hipStream_t stream) {
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
   if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;
   if (!train && logits_out == nullptr) return -1;
-  if (train)
-    hipLaunchKernelGGL(wdc_fused<true>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
-                       start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out, grad_scale, tmap,
-                       stride);
-  else
-    hipLaunchKernelGGL(wdc_fused<false>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
-                       start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out, grad_scale, tmap,
-                       stride);
+  if (waves != 4 && waves != 8) return -1;
+  const dim3 g(grid);
+  if (train && waves == 4)
+    launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                    grad_scale, tmap, stride);
+  else if (train)
+    launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                    grad_scale, tmap, stride);
+  else  // eval / predict: the 4-wave shape for either request (forward only, no dW phases to overlap)
+    launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                     grad_scale, tmap, stride);
   return (int)hipGetLastError();
 }
+
+#ifdef WDC_STAMPS
+int mifx_wdc_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wdc_stamps), sizeof(g_wdc_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // extern "C"

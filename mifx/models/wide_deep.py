@@ -314,17 +314,36 @@ def tensors_to_records(dense, ids, label) -> np.ndarray:
 # ---- register-chained kernel layout (csrc/wd_chain.hip) ---------------------------------------
 # The chained kernel feeds layer l's MFMA output tiles straight into layer l+1 as its B operand, so layer
 # l+1's k axis is consumed in "C order": inside every 32-block, position 8H + E holds feature
-# 16 (E // 4) + 4 H + E % 4. Its LDS weight image W_l^T [N][K + PAD] therefore has natural rows and
-# C-ordered columns; dW tiles come out in the same image coordinates.
-CHAIN_PAD = 8
+# 16 (E // 4) + 4 H + E % 4. Its LDS weight image W_l^T [N][K] therefore has natural rows and C-ordered
+# columns; dW tiles come out in the same image coordinates. Rows are padded by CHAIN_PAD elements (the kernel's
+# WPAD) for conflict-free forward reads; CHAIN_WSWZ mirrors wswz<K>() (per-row XOR of 8-byte granules, all zero:
+# see the kernel's WPAD note).
+CHAIN_PAD = 16
 CHAIN_LW = [int(v) for v in np.cumsum([0] + [n * (k + CHAIN_PAD) for k, n in LAYER_KN])[:-1]]
-CHAIN_LWEND = sum(n * (k + CHAIN_PAD) for k, n in LAYER_KN)  # 30592
+CHAIN_LWEND = sum(n * (k + CHAIN_PAD) for k, n in LAYER_KN)  # 33536
+CHAIN_WSWZ = {32: (0,) * 7, 128: (0,) * 7, 96: (0,) * 7, 64: (0,) * 7}
 
 
 def chain_perm(K: int) -> np.ndarray:
     """f[c] = natural feature held at C-order position c of a K-wide (K % 32 == 0) chained input axis."""
     c = np.arange(K)
     return 32 * (c // 32) + 16 * ((c % 8) // 4) + 4 * ((c % 32) // 8) + c % 4
+
+
+def _xmask(masks, rows: np.ndarray) -> np.ndarray:
+    x = np.zeros_like(rows)
+    for b, m in enumerate(masks):
+        x ^= np.where((rows >> b) & 1, m, 0)
+    return x
+
+
+def chain_image_offsets(li: int) -> np.ndarray:
+    """[N, K] element offsets in the chained kernel's weight image of layer li's entry (row n, C position c)."""
+    K, N = LAYER_KN[li]
+    n = np.arange(N)[:, None]
+    c = np.arange(K)[None, :]
+    g = (c >> 2) ^ _xmask(CHAIN_WSWZ[K], n)
+    return CHAIN_LW[li] + n * (K + CHAIN_PAD) + 4 * g + (c & 3)
 
 
 def chain_image(param) -> np.ndarray:
@@ -334,9 +353,7 @@ def chain_image(param) -> np.ndarray:
     img = np.zeros(CHAIN_LWEND, np.float32)
     for li, (K, N) in enumerate(LAYER_KN):
         w = p[LAYER_OFF[li]:LAYER_OFF[li] + K * N].reshape(N, K)
-        blk = np.zeros((N, K + CHAIN_PAD), np.float32)
-        blk[:, :K] = w[:, chain_perm(K)]
-        img[CHAIN_LW[li]:CHAIN_LW[li] + N * (K + CHAIN_PAD)] = blk.reshape(-1)
+        img[chain_image_offsets(li)] = w[:, chain_perm(K)]
     return img
 
 
@@ -373,7 +390,7 @@ def chain_maps(cfg: WideDeepConfig | None = None):
         assert (ct[m] >= 0).all()
         gidx[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = idx.reshape(-1)
         mask[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = m.reshape(-1)
-        wmap[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = (CHAIN_LW[li] + n * (K + CHAIN_PAD) + col).reshape(-1)
+        wmap[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = chain_image_offsets(li)[n, col].reshape(-1)
     gidx[WTOT:] = stride - WIDE_PAD + np.arange(NWIDE)
     mask[WTOT:] = 1
     return tmap, stride, gidx, mask, wmap

@@ -15,7 +15,8 @@ def _fns():
     lib = _lib.load("wd_chain")
     return {
         "constants": sig(lib, "mifx_wdc_constants", [VP, I32]),
-        "fused": sig(lib, "mifx_wdc_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP]),
+        "fused": sig(lib, "mifx_wdc_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, I32,
+                                             VP]),
     }
 
 
@@ -30,9 +31,12 @@ def constants() -> dict[str, int]:
 def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
           wimg_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
           logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
-          tmap: torch.Tensor | None = None) -> None:
+          tmap: torch.Tensor | None = None, waves: int = 8) -> None:
     """One chained-kernel launch. wimg_bf16: [LWEND] bf16 (or int16) weight image in the kernel's LDS layout
-    (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout."""
+    (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout.
+    waves: 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each)."""
+    if waves not in (4, 8):
+        raise ValueError("waves must be 4 or 8")
     c = constants()
     if wimg_bf16.numel() != c["LWEND"] or wimg_bf16.element_size() != 2 or not wimg_bf16.is_contiguous():
         raise ValueError("weight image must be a contiguous 16-bit [LWEND] tensor")
@@ -50,5 +54,5 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
         raise ValueError("eval launch needs logits_out with >= batch floats")
     rc = _fns()["fused"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide), ptr(slab),
                          ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train), ptr(tmap), stride,
-                         stream_handle(records.device))
+                         int(waves), stream_handle(records.device))
     check(rc, "mifx_wdc_fused")

@@ -58,13 +58,14 @@ class FusedWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
-                 live_staging: bool = False, fused_update: bool = True, kernel: str = "chain"):
+                 live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
         if kernel not in ("chain", "tile"):
             raise ValueError("kernel must be 'chain' or 'tile'")
         self.kernel = kernel
+        self.waves = int(waves)  # chained kernel: 8 (2 waves / SIMD x 16 examples) or 4 (1 wave / SIMD x 32)
         c = wdk.constants()
         assert c["WTOT"] == wdm.WTOT and c["STRIDE"] == wdm.STRIDE and c["NWIDE"] == wdm.NWIDE
         if kernel == "chain":
@@ -141,7 +142,7 @@ class FusedWideDeepTrainer:
             from ..ops import wd_chain as wdc
 
             wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.param[wdm.WTOT:], slab, slab_loss,
-                      logits, self.grad_scale, grid, train, self.tmap if train else None)
+                      logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves)
         else:
             wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.param[wdm.WTOT:], slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,

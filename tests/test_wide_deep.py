@@ -144,7 +144,7 @@ def _emulated_grads(vec, rec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["chain", "tile"])
+@pytest.mark.parametrize("kernel", ["chain", "chain4", "tile"])
 @pytest.mark.parametrize("batch", [40, 64, 1000, 8192])
 def test_fused_gradients_match_torch(batch, kernel):
     torch.manual_seed(batch)
@@ -158,7 +158,8 @@ def test_fused_gradients_match_torch(batch, kernel):
         for lin in m.dnn:
             lin.bias.normal_(0, 0.1)
     rec = synthetic_records(batch, seed=7)
-    tr = FusedWideDeepTrainer(m, batch=batch, device=dev, kernel=kernel)
+    kw = {"kernel": "chain", "waves": 4} if kernel == "chain4" else {"kernel": kernel}
+    tr = FusedWideDeepTrainer(m, batch=batch, device=dev, **kw)
     tr.set_data(rec.to(dev))
     g_tn = tr.gradients_once()
     torch.cuda.synchronize()

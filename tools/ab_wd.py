@@ -17,7 +17,7 @@ from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernels", default="chain,tile")
+    ap.add_argument("--kernels", default="chain8,chain4,tile", help="chain8 / chain4 (waves) or tile")
     ap.add_argument("--batches", default="65536,131072,40")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
@@ -28,7 +28,8 @@ def main():
         steps = 3000 if batch <= 1024 else 300
         trs = {}
         for k in a.kernels.split(","):
-            tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=dev, kernel=k)
+            kw = {"kernel": "tile"} if k == "tile" else {"kernel": "chain", "waves": int(k[5:] or 8)}
+            tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=dev, **kw)
             tr.set_data(data)
             tr.capture()
             trs[k] = tr

@@ -1,0 +1,44 @@
+"""Phase breakdown of wdc_fused<true> (csrc/wd_chain.hip) block 0 via the s_memtime diagnostic build.
+
+Build: bash tools/build_stamps.sh (CPU) -> tools/bin/libwdc_stamps.so; run on the GPU: python tools/stamps_wdc.py
+Read SHARES, not absolute lengths (stamps fence the schedule)."""
+import ctypes
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+import mifx.ops._lib as L  # noqa: E402
+
+diag = ctypes.CDLL("tools/bin/libwdc_stamps.so", mode=ctypes.RTLD_GLOBAL)
+L.load.cache_clear()
+_orig = L.load.__wrapped__
+
+
+def _load(name):
+    return diag if name == "wd_chain" else _orig(name)
+
+
+L.load = _load
+from mifx.data.synthetic import synthetic_records  # noqa: E402
+from mifx.models.wide_deep import WideDeepModel  # noqa: E402
+from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
+
+NAMES = {1: "prologue", 2: "loop->iter", 3: "gather+fwd", 4: "loss", 5: "B0", 6: "stage5+B", 7: "dW5+dA4",
+         8: "B+stage4+B", 9: "dW4+dA3", 10: "B+stage3+B", 11: "dW3+dA2", 12: "B+stage2+B", 13: "dW2+dA1",
+         14: "B+stage1+B", 15: "dW1", 16: "->epi", 17: "epilogue"}
+for NW, batch in ((4, 65536), (8, 128), (8, 65536)):
+    tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device="cuda", kernel="chain", waves=NW)
+    tr.set_data(synthetic_records(1 << 17, device="cuda", seed=0))
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+
+    buf = (ctypes.c_ulonglong * (32 * 8))()  # g_wdc_stamps is [MAXW = 8][32]
+    assert diag.mifx_wdc_stamps(buf) == 0
+    st = [[buf[w * 32 + i] for i in range(32)] for w in range(NW)]
+    print(f"== batch {batch} grid {tr.grid}: cycles per phase (block 0; the 2nd iteration when there is one)")
+    for i in range(1, 18):
+        d = [st[w][i] - st[w][i - 1] for w in range(NW)]
+        print(f"  {NAMES[i]:>11}: " + " ".join(f"{x:8d}" for x in d))
+    print(f"  iteration (stamp 2 -> 15), wave 0: {st[0][15] - st[0][2]}; kernel (0 -> 17): {st[0][17] - st[0][0]}")
