@@ -39,8 +39,11 @@ def run(trainer, steps: int, warmup: int, device) -> float:
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        trainer.step()
+    if hasattr(trainer, "run"):
+        trainer.run(steps)  # exactly `steps` steps (multi-step graph replays + one-step remainder)
+    else:
+        for _ in range(steps):
+            trainer.step()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     mdist.barrier()
@@ -59,7 +62,8 @@ def _ranks_agree(tr) -> bool:
     return bool(torch.equal(hi, lo)) and bool(torch.isfinite(chk).all())
 
 
-def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, capture_collective: bool = False):
+def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, capture_collective: bool = False,
+                 steps_per_graph: int = 10):
     def build():
         model = WideDeepModel(seed=0)
         if device.type == "cuda":
@@ -84,7 +88,7 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, ca
     # to validate it); its guard: after two replays every rank must hold bit-identical weights, else the
     # trainer (and its HBM-resident data) is released and a split-phase one is built instead.
     captured = pg is not None and capture_collective and torch.distributed.get_backend(pg) == "nccl"
-    tr.capture(include_collective=captured)
+    tr.capture(include_collective=captured, steps_per_graph=steps_per_graph)
     tr.collective_in_graph = captured
     if captured:
         for _ in range(2):
@@ -113,6 +117,8 @@ def main(argv=None) -> int:
     ap.add_argument("--ref-steps", type=int, default=2000)
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--steps-per-graph", type=int, default=10,
+                    help="consecutive training steps captured in one hipGraph (single rank / captured collective)")
     ap.add_argument("--capture-collective", action="store_true",
                     help="multi-rank: capture the RCCL all-reduce inside the step's hipGraph (default: split-phase, "
                          "eager all-reduce between two graphs)")
@@ -131,8 +137,9 @@ def main(argv=None) -> int:
     n = env.world_size
 
     tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph,
-                      a.capture_collective)
+                      a.capture_collective, a.steps_per_graph)
     collective_in_graph = bool(getattr(tr, "collective_in_graph", False))
+    spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
     dt = mdist.max_over_ranks(run(tr, a.steps, a.warmup, device), device if use_cuda else None)
     loss = tr.last_loss() / a.batch_per_gpu
     value = a.batch_per_gpu * n * a.steps / dt
@@ -143,7 +150,8 @@ def main(argv=None) -> int:
         if use_cuda:
             torch.cuda.synchronize(device)
             torch.cuda.empty_cache()
-        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.capture_collective)
+        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.capture_collective,
+                           a.steps_per_graph)
         dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
                "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps}
@@ -168,6 +176,8 @@ def main(argv=None) -> int:
                        "precision": "bf16 MFMA compute, fp32 master weights/optimizer state",
                        "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
                        "hipgraph": bool(use_cuda and not a.no_graph),
+                       "steps_per_graph": spg,
+                       "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
                        "collective_in_graph": collective_in_graph},
             "final_mean_loss": loss,
             "reference_batch": ref,

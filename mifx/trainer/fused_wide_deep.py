@@ -128,6 +128,7 @@ class FusedWideDeepTrainer:
         self.n_data = 0
         self.graph = None
         self._graphs = None
+        self.graph_multi, self.graph_multi_steps = None, 1
 
     def _weight_image(self) -> torch.Tensor:
         """bf16 (as int16) weight image the fused kernel stages: canonical order (tile kernel) or the chained
@@ -156,6 +157,7 @@ class FusedWideDeepTrainer:
         self.records = records.to(self.device).contiguous()
         self.n_data = self.records.shape[0]
         self.graph, self._graphs = None, None
+        self.graph_multi, self.graph_multi_steps = None, 1
 
     @property
     def grad_scale(self) -> float:
@@ -214,7 +216,20 @@ class FusedWideDeepTrainer:
         else:
             self._step_impl()
 
-    def capture(self, warmup: int = 2, include_collective: bool = False) -> None:
+    def run(self, n: int) -> None:
+        """n training steps. With a multi-step graph (capture(steps_per_graph=S)) this replays it n // S times and
+        the one-step graph n % S times: every step still runs its own kernels (the data offset and optimizer
+        step advance through the device-side step counter), the host just launches once per S steps. Replaying
+        one graph per step left ~8.7 us of idle GPU between steps on MI355X (the host-side launch of a replay
+        costs more than the step's ~35 us of GPU work): tools/timeline.py, profiles/wd_step_timeline_r2.txt."""
+        if self.graph_multi is not None and n >= self.graph_multi_steps:
+            reps, n = divmod(n, self.graph_multi_steps)
+            for _ in range(reps):
+                self.graph_multi.replay()
+        for _ in range(n):
+            self.step()
+
+    def capture(self, warmup: int = 2, include_collective: bool = False, steps_per_graph: int = 1) -> None:
         """Capture the step as hipGraph(s) after `warmup` eager steps on a side stream.
 
         Single rank: one graph. Multi-rank: by default two graphs (local grad, optimizer) with the
@@ -229,11 +244,18 @@ class FusedWideDeepTrainer:
                 self._step_impl()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graph, self._graphs = None, None
+        self.graph_multi, self.graph_multi_steps = None, 1
         if self.world == 1 or include_collective:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._step_impl()
             self.graph = g
+            if steps_per_graph > 1:  # S consecutive steps in one graph (see run())
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm):
+                    for _ in range(steps_per_graph):
+                        self._step_impl()
+                self.graph_multi, self.graph_multi_steps = gm, int(steps_per_graph)
             return
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):

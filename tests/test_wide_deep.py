@@ -378,3 +378,23 @@ def test_chain_maps_cover_trainable_parameters():
     img = wdm.chain_image(vec)
     np.testing.assert_array_equal(img[wmap], vec[:wdm.WTOT])
     assert np.count_nonzero(img) == np.count_nonzero(vec[:wdm.WTOT])
+
+
+@pytest.mark.gpu
+def test_multi_step_graph_matches_single_step_replays():
+    """run(n) with a 7-step graph (2 multi-step replays + 3 one-step replays) must give exactly the parameters
+    of 17 one-step replays: the data offset and optimizer step advance through the device-side step counter."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(1 << 16, device=dev, seed=12)
+    out = []
+    for spg in (1, 7):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=2048, device=dev)
+        tr.set_data(rec)
+        tr.capture(steps_per_graph=spg)
+        tr.run(17)
+        torch.cuda.synchronize()
+        assert tr.steps_done == 17 + 2  # + the capture's warmup steps
+        out.append(tr.param.clone())
+    assert torch.equal(out[0], out[1])
