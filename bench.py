@@ -80,16 +80,20 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, ca
     tr = build()
     if not (graph and device.type == "cuda"):
         return tr
-    # Multi-rank over RCCL, default: split-phase step (graph: fused fwd/bwd + slab reduce; eager RCCL all-reduce
-    # of the flat gradient; graph: optimizer). --capture-collective captures the all-reduce INTO the step's
-    # hipGraph (one replay per step). Measured on one MI355X with the DP code path forced
-    # (tools/dp_step_overhead.py): split-phase 67.4 us at B=65536 vs 51.2 us captured; B=40: 37.7 vs 22.5 us.
+    # Multi-rank over RCCL, default: the direct path -- fused fwd/bwd, slab reduce and optimizer launched eagerly
+    # from prebuilt arguments with the flat-gradient ncclAllReduce enqueued between them on the same stream
+    # through torch's communicator (mifx.parallel.rccl_direct); no graph-launch bubbles, no extra stream hops.
+    # --capture-collective captures the all-reduce INTO the step's hipGraph instead. Measured on one MI355X with
+    # the DP code path forced (tools/dp_step_overhead.py, profiles/dp_step_overhead_r2.jsonl).
     # The captured variant stays opt-in until it has run on a multi-GPU node (only 1-GPU boxes were available
     # to validate it); its guard: after two replays every rank must hold bit-identical weights, else the
     # trainer (and its HBM-resident data) is released and a split-phase one is built instead.
     captured = pg is not None and capture_collective and torch.distributed.get_backend(pg) == "nccl"
     tr.capture(include_collective=captured, steps_per_graph=steps_per_graph)
     tr.collective_in_graph = captured
+    tr.dp_path = ("captured-in-graph" if captured else
+                  "rccl-direct (eager launches + ncclAllReduce on the compute stream)" if tr._fast is not None else
+                  "split-phase graphs + torch all_reduce") if pg is not None else None
     if captured:
         for _ in range(2):
             tr.step()
@@ -139,6 +143,8 @@ def main(argv=None) -> int:
     tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph,
                       a.capture_collective, a.steps_per_graph)
     collective_in_graph = bool(getattr(tr, "collective_in_graph", False))
+    dp_path = getattr(tr, "dp_path", None)
+    ranks_agree = _ranks_agree(tr) if (n > 1 and use_cuda) else None  # replicas must hold identical weights
     spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
     dt = mdist.max_over_ranks(run(tr, a.steps, a.warmup, device), device if use_cuda else None)
     loss = tr.last_loss() / a.batch_per_gpu
@@ -178,7 +184,8 @@ def main(argv=None) -> int:
                        "hipgraph": bool(use_cuda and not a.no_graph),
                        "steps_per_graph": spg,
                        "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
-                       "collective_in_graph": collective_in_graph},
+                       "collective_in_graph": collective_in_graph, "dp_allreduce": dp_path,
+                       "replicas_bit_identical": ranks_agree},
             "final_mean_loss": loss,
             "reference_batch": ref,
         }

@@ -128,6 +128,8 @@ class FusedWideDeepTrainer:
         self.n_data = 0
         self.graph = None
         self._graphs = None
+        self._fast = None
+        self._direct = None
         self.graph_multi, self.graph_multi_steps = None, 1
 
     def _weight_image(self) -> torch.Tensor:
@@ -156,7 +158,7 @@ class FusedWideDeepTrainer:
             raise ValueError("records must be uint8 [N, 32]")
         self.records = records.to(self.device).contiguous()
         self.n_data = self.records.shape[0]
-        self.graph, self._graphs = None, None
+        self.graph, self._graphs, self._fast = None, None, None
         self.graph_multi, self.graph_multi_steps = None, 1
 
     @property
@@ -197,7 +199,52 @@ class FusedWideDeepTrainer:
 
     def _allreduce(self) -> None:
         if self.world > 1:
-            torch.distributed.all_reduce(self.grad, group=self.pg)
+            if self._direct is not None:
+                self._direct()
+            else:
+                torch.distributed.all_reduce(self.grad, group=self.pg)
+
+    # ---------------------------------------------------------------- eager data-parallel fast path
+    def _prepare_direct(self) -> None:
+        """Data-parallel step without graphs: the three kernel launches with their ctypes arguments built once
+        and the all-reduce issued straight to RCCL on the same stream (mifx.parallel.rccl_direct). Stream order
+        is the only synchronisation; no graph-launch bubbles, no ProcessGroupNCCL stream hops."""
+        import ctypes
+
+        from ..ops import wd_chain as wdc
+        from ..parallel.rccl_direct import DirectAllReduce
+        from ..ops._lib import ptr
+
+        if self.kernel != "chain" or not self.fused_update:
+            raise ValueError("the direct DP path needs the chained kernel and the fused update")
+        self._direct = DirectAllReduce(self.grad, self.pg)
+        stream = torch.cuda.current_stream(self.device)
+        sh = ctypes.c_void_p(stream.cuda_stream)
+        fused = (wdc._fns()["fused"], (ptr(self.records), self.n_data, self.batch, 0, ptr(self.step_ctr), ptr(self.wt),
+                                       ptr(self.param[wdm.WTOT:]), ptr(self.slab), ptr(self.slab_loss), None,
+                                       float(self.grad_scale), int(self.grid), 1, ptr(self.tmap), int(self.stride),
+                                       int(self.waves), sh))
+        ro = wdk._fns()["reduce_opt"]
+        red = (ro, (ptr(self.slab), int(self.grid), int(self.stride), ptr(self.grad), None, None, None, None, None, None,
+                    None, None, None, sh))
+        hd = self.h_dnn.contiguous()
+        hw = self.h_wide.contiguous()
+        app = (ro, (ptr(self.grad), 1, int(self.stride), None, ptr(self.inv), ptr(self.param), ptr(self.s0),
+                    ptr(self.s1), ptr(self.wt), ptr(self.wmap), ptr(self.step_ctr), ptr(hd), ptr(hw), sh))
+        wdk._check_step_ctr(self.step_ctr)
+        self._fast = (stream, fused, red, app, hd, hw)
+
+    def _step_direct(self) -> None:
+        stream, fused, red, app = self._fast[:4]
+        if torch.cuda.current_stream(self.device) != stream:
+            self._prepare_direct()
+            stream, fused, red, app = self._fast[:4]
+        for fn, args in (fused, red):
+            if fn(*args) != 0:
+                raise RuntimeError("W&D kernel launch failed")
+        self._direct(stream)
+        if app[0](*app[1]) != 0:
+            raise RuntimeError("W&D optimizer launch failed")
 
     def _step_impl(self) -> None:
         self._local_grad()
@@ -209,6 +256,8 @@ class FusedWideDeepTrainer:
             raise RuntimeError("call set_data() first")
         if self.graph is not None:
             self.graph.replay()
+        elif self._fast is not None:  # data-parallel eager path with the direct RCCL all-reduce
+            self._step_direct()
         elif self._graphs is not None:  # split capture: eager collective between two graphs
             self._graphs[0].replay()
             self._allreduce()
@@ -229,11 +278,15 @@ class FusedWideDeepTrainer:
         for _ in range(n):
             self.step()
 
-    def capture(self, warmup: int = 2, include_collective: bool = False, steps_per_graph: int = 1) -> None:
+    def capture(self, warmup: int = 2, include_collective: bool = False, steps_per_graph: int = 1,
+                dp_mode: str = "direct") -> None:
         """Capture the step as hipGraph(s) after `warmup` eager steps on a side stream.
 
-        Single rank: one graph. Multi-rank: by default two graphs (local grad, optimizer) with the
-        all-reduce issued eagerly between them (works with any backend, e.g. gloo); `include_collective=True`
+        Single rank: one graph (plus an S-step graph when steps_per_graph > 1). Multi-rank over RCCL, default
+        (dp_mode="direct"): no graphs -- the fused, reduce and optimizer kernels launched eagerly from prebuilt
+        ctypes arguments with the gradient all-reduce issued directly to RCCL in between, on the same stream
+        (tools/dp_step_overhead.py). dp_mode="split": two graphs (local grad, optimizer) with the all-reduce
+        issued eagerly between them (works with any backend, e.g. gloo); `include_collective=True`
         captures the RCCL all-reduce too -- one graph launch per step (bench.py --capture-collective; opt-in
         until validated on a multi-GPU node). On one MI355X with the DP path forced (tools/dp_step_overhead.py)
         the split-phase step costs 67.4 us vs 51.2 us captured at B=65536 (host 41.6 vs 11.4 us per step)."""
@@ -243,7 +296,7 @@ class FusedWideDeepTrainer:
             for _ in range(warmup):
                 self._step_impl()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self.graph, self._graphs = None, None
+        self.graph, self._graphs, self._fast = None, None, None
         self.graph_multi, self.graph_multi_steps = None, 1
         if self.world == 1 or include_collective:
             g = torch.cuda.CUDAGraph()
@@ -256,6 +309,10 @@ class FusedWideDeepTrainer:
                     for _ in range(steps_per_graph):
                         self._step_impl()
                 self.graph_multi, self.graph_multi_steps = gm, int(steps_per_graph)
+            return
+        if dp_mode == "direct" and self.kernel == "chain" and self.fused_update \
+                and torch.distributed.get_backend(self.pg) == "nccl":
+            self._prepare_direct()  # no graphs: eager launches + direct RCCL in stream order
             return
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):

@@ -80,11 +80,47 @@ def test_captured_rccl_allreduce_step_matches_split_phase():
                                       process_group=dist.group.WORLD)
             tr.world = 2  # take the DP code path (reduce_full -> all-reduce -> optimizer) on one rank
             tr.set_data(recs)
-            tr.capture(include_collective=captured)
+            tr.capture(include_collective=captured, dp_mode="split")
             assert (tr.graph is not None) == captured and (tr._graphs is not None) != captured
             for _ in range(6):
                 tr.step()
             torch.cuda.synchronize()
+            out.append(tr.param.clone())
+        assert torch.equal(out[0], out[1])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_direct_rccl_dp_step_matches_split_phase():
+    """The default multi-rank W&D path (eager launches + ncclAllReduce on the compute stream through torch's
+    communicator, mifx.parallel.rccl_direct) must give exactly the weights of the split-phase graph path, on a
+    1-rank RCCL group with the trainer forced onto its data-parallel code path."""
+    from mifx.data.synthetic import synthetic_records
+    from mifx.models import wide_deep as wdm
+    from mifx.parallel.rccl_direct import DirectAllReduce
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        x = torch.arange(1000, device="cuda", dtype=torch.float32)
+        ar = DirectAllReduce(x)
+        ar()
+        torch.cuda.synchronize()
+        assert torch.equal(x, torch.arange(1000, device="cuda", dtype=torch.float32))  # sum over one rank
+        recs = synthetic_records(1 << 16, device="cuda", seed=4)
+        out = []
+        for mode in ("split", "direct"):
+            tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=2), batch=4096, device="cuda",
+                                      process_group=dist.group.WORLD)
+            tr.world = 2
+            tr.set_data(recs)
+            tr.capture(dp_mode=mode)
+            assert (tr._fast is not None) == (mode == "direct")
+            tr.run(6)
+            torch.cuda.synchronize()
+            assert tr.steps_done == 8
             out.append(tr.param.clone())
         assert torch.equal(out[0], out[1])
     finally:

@@ -1,6 +1,7 @@
 """Host/GPU cost of the data-parallel W&D step paths on ONE GPU with a 1-rank RCCL group: the split-phase
-step (graph, eager RCCL all-reduce, graph) that bench.py uses at N>1, and the single graph with the
-all-reduce captured (include_collective=True). The trainer is told world=2 so it takes the DP code path."""
+step (graph, eager RCCL all-reduce, graph), the direct path bench.py uses at N>1 (eager kernel launches from
+prebuilt arguments + ncclAllReduce on the same stream), and the single graph with the all-reduce captured
+(include_collective=True). The trainer is told world=2 so it takes the DP code path."""
 import json
 import os
 import sys
@@ -16,11 +17,11 @@ from mifx.models.wide_deep import WideDeepModel  # noqa: E402
 from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
 
 
-def run(batch, include_collective, steps=300):
+def run(batch, include_collective, steps=300, dp_mode="split"):
     tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device="cuda", process_group=dist.group.WORLD)
     tr.world = 2  # force the DP path (reduce_full -> all_reduce -> optimizer) on a 1-rank group
     tr.set_data(synthetic_records(1 << 20, device="cuda", seed=1))
-    tr.capture(include_collective=include_collective)
+    tr.capture(include_collective=include_collective, dp_mode=dp_mode)
     for _ in range(20):
         tr.step()
     torch.cuda.synchronize()
@@ -30,7 +31,8 @@ def run(batch, include_collective, steps=300):
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     t_all = time.perf_counter() - t0
-    return {"batch": batch, "captured_collective": include_collective, "host_us_per_step": round(t_host / steps * 1e6, 2),
+    return {"batch": batch, "captured_collective": include_collective, "dp_mode": dp_mode,
+            "host_us_per_step": round(t_host / steps * 1e6, 2),
             "us_per_step": round(t_all / steps * 1e6, 2), "finite": bool(torch.isfinite(tr.param).all())}
 
 
@@ -40,7 +42,9 @@ if __name__ == "__main__":
     dist.init_process_group("nccl", rank=0, world_size=1)
     torch.cuda.set_device(0)
     for b in (65536, 40):
-        print(json.dumps(run(b, False)), flush=True)
+        print(json.dumps(run(b, False, dp_mode="split")), flush=True)
+    for b in (65536, 40):
+        print(json.dumps(run(b, False, dp_mode="direct")), flush=True)
     for b in (65536, 40):
         print(json.dumps(run(b, True)), flush=True)
     dist.destroy_process_group()
