@@ -1,0 +1,353 @@
+// Fused multi-head self-attention for BERT (BASELINE config 4) on gfx950: forward and backward, key-padding
+// mask, counter-based attention-probability dropout. Replaces scaled_dot_product_attention, whose ROCm
+// backends are Triton-generated (AOTriton attn_fwd / bwd_kernel_fuse: 0.96 ms of a 7.4 ms BERT-base step,
+// profiles/bert_base_steady_kernels_s3b.md).
+//
+// One workgroup per (batch, local head): the whole S x S problem of a BERT sequence (S = 64 or 128, head dim 64)
+// lives in one CU. S/16 waves, wave w owns queries 16w .. 16w+15 and works in the TRANSPOSED orientation so the
+// MFMA outputs chain (same idiom as csrc/wd_chain.hip):
+//  * S^T = K Q^T (16x16x32 bf16 MFMA, K rows from LDS, Q^T fragments = the wave's own query rows): lane = query,
+//    4 consecutive keys per lane per key tile. Softmax statistics per query reduce over the lane's registers and
+//    across the 4 lane groups with two xor shuffles.
+//  * O^T = V^T P^T: the P^T tiles 2s, 2s+1 ARE the B operand of k-step s (keys in the chained order
+//    32s + 16(e/4) + 4h + e%4), so the V^T operand is read with ds_read_b64_tr_b16 at those key rows.
+//  * backward: S^T and dP_d^T = V dO^T recomputed per wave; dS^T = P^T (dP^T - D), D = rowsum(dO o O);
+//    dQ^T = K^T dS^T chained the same way; P_d and dS are staged once in LDS ([query][key]) and each wave then
+//    owns 16 keys for dV^T = dO^T P_d and dK^T = Q^T dS, reading both operands with transposed LDS reads.
+// qkv is the fused projection output [B, S, 3, H, 64] (this rank's H heads), out / dout are [B, S, H, 64]; no
+// transposes around the kernels. Dropout element (b, global head, i, j) uses the flat index
+// ((b Htot + h0 + h) S + i) S + j into the counter-based mask of csrc/counter_rng.h, so the mask does not depend
+// on how heads are split over tensor-parallel ranks.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "counter_rng.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int D = 64;        // head dim
+constexpr int LD = D + 8;    // LDS row of a [token][d] image (elements): 144 B rows
+constexpr v4f kZero4 = {0.f, 0.f, 0.f, 0.f};
+
+__device__ __forceinline__ v4s tr_read(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+}
+__device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
+  v8s r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
+__device__ __forceinline__ v8bf ld8(const bf16* p) { return *(const v8bf*)p; }
+__device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ v8bf pack8(v4f a, v4f b) {
+  v8bf o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[i] = (bf16)a[i];
+    o[4 + i] = (bf16)b[i];
+  }
+  return o;
+}
+__device__ __forceinline__ v4bf pack4(v4f a) {
+  v4bf o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = (bf16)a[i];
+  return o;
+}
+
+struct Drop {
+  const int64_t* rng;
+  int site;
+  uint32_t thr;  // 0: no dropout
+  float scale;   // 1 / (1 - p)
+};
+
+// load S rows x 64 of one [B, S, *, 64]-strided tensor into an LDS [S][LD] image (16-B chunks)
+template <int S, int NTHR>
+__device__ __forceinline__ void load_rows(bf16* dst, const bf16* src, size_t row_stride) {
+  for (int c = threadIdx.x; c < S * 8; c += NTHR) {
+    const int row = c >> 3, ch = c & 7;
+    *(uint4*)(dst + row * LD + ch * 8) = *(const uint4*)(src + (size_t)row * row_stride + ch * 8);
+  }
+}
+
+// scores S^T for the wave's 16 queries: acc[kt][e] = q_i . k_{16kt + 4h + e}, q_i = query 16w + r
+template <int S>
+__device__ __forceinline__ void scores(const bf16* Ks, const v8bf (&qf)[2], v4f (&acc)[S / 16], int r, int h) {
+#pragma unroll
+  for (int kt = 0; kt < S / 16; ++kt) {
+    v4f a = kZero4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Ks + (16 * kt + r) * LD + 32 * ks + 8 * h), qf[ks], a);
+    acc[kt] = a;
+  }
+}
+
+// P^T (probabilities, before dropout) from the scores, the key bias and the per-query logsumexp
+template <int S>
+__device__ __forceinline__ void probs(v4f (&p)[S / 16], float scale, const float* kb, float lse, int h) {
+#pragma unroll
+  for (int kt = 0; kt < S / 16; ++kt) {
+    const float4 b = kb ? *(const float4*)(kb + 16 * kt + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+    p[kt][0] = __expf(p[kt][0] * scale + b.x - lse);
+    p[kt][1] = __expf(p[kt][1] * scale + b.y - lse);
+    p[kt][2] = __expf(p[kt][2] * scale + b.z - lse);
+    p[kt][3] = __expf(p[kt][3] * scale + b.w - lse);
+  }
+}
+
+// dropout keep bits of the lane's 4 keys of tile kt for query i: flat index ((bh_global) S + i) S + 16kt + 4h
+template <int S>
+__device__ __forceinline__ uint32_t keep_bits(const Drop& dp, uint64_t key, uint64_t row_base, int kt, int h) {
+  if (!dp.thr) return 0xf;
+  return mifx_rng::keep4(key, (row_base + 16 * kt + 4 * h) >> 2, dp.thr);
+}
+
+template <int S>
+__global__ __launch_bounds__(64 * (S / 16)) void attn_fwd(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
+                                                         float scale, Drop dp, int H, int h0, int Htot,
+                                                         bf16* __restrict__ out, float* __restrict__ lse_out) {
+  constexpr int NTHR = 64 * (S / 16), KT = S / 16, KS = S / 32;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[S * LD];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[S * LD];
+  const int b = blockIdx.x / H, hh = blockIdx.x % H;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
+  const size_t tok = (size_t)3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * tok;
+  load_rows<S, NTHR>(Ks, base + (size_t)(H + hh) * D, tok);
+  load_rows<S, NTHR>(Vs, base + (size_t)(2 * H + hh) * D, tok);
+  const int qi = 16 * w + r;
+  v8bf qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const v8bf*)(base + (size_t)qi * tok + (size_t)hh * D + 32 * ks + 8 * h);
+  __syncthreads();
+
+  v4f s[KT];
+  scores<S>(Ks, qf, s, r, h);
+  const float* kb = kbias ? kbias + (size_t)b * S : nullptr;
+  float m = -3.0e38f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const float4 bb = kb ? *(const float4*)(kb + 16 * kt + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s[kt][0] = s[kt][0] * scale + bb.x;
+    s[kt][1] = s[kt][1] * scale + bb.y;
+    s[kt][2] = s[kt][2] * scale + bb.z;
+    s[kt][3] = s[kt][3] * scale + bb.w;
+    m = fmaxf(m, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+  }
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s[kt][e] = __expf(s[kt][e] - m);
+      l += s[kt][e];
+    }
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  const float inv = 1.f / l;
+  const uint64_t key = dp.thr ? mifx_rng::drop_key(dp.rng, dp.site) : 0;
+  const uint64_t row_base = (((uint64_t)b * Htot + h0 + hh) * S + qi) * S;
+  v8bf pb[KS];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const uint32_t k = keep_bits<S>(dp, key, row_base, kt, h);
+    const float sc = dp.thr ? inv * dp.scale : inv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[kt][e] = (k >> e) & 1 ? s[kt][e] * sc : 0.f;
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) pb[ks] = pack8(s[2 * ks], s[2 * ks + 1]);
+  // O^T = V^T P^T (V^T rows read transposed at the chained key order)
+  const int q = r >> 2, p = r & 3;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    v4f o = kZero4;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16* pa = Vs + (32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
+      o = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), pb[ks], o);
+    }
+    *(v4bf*)(out + ((size_t)b * S + qi) * H * D + (size_t)hh * D + 16 * dt + 4 * h) = pack4(o);
+  }
+  if (h == 0) lse_out[((size_t)b * H + hh) * S + qi] = m + __logf(l);
+}
+
+template <int S>
+__global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
+                                                         const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                                         const float* __restrict__ lse, float scale, Drop dp, int H,
+                                                         int h0, int Htot, bf16* __restrict__ dqkv) {
+  constexpr int NTHR = 64 * (S / 16), KT = S / 16, KS = S / 32, LP = S + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  bf16* Qs = smem;
+  bf16* Ks = Qs + S * LD;
+  bf16* Vs = Ks + S * LD;
+  bf16* dOs = Vs + S * LD;
+  bf16* PT = dOs + S * LD;  // P_d [query][key]
+  bf16* dST = PT + S * LP;  // dS * scale [query][key]
+  const int b = blockIdx.x / H, hh = blockIdx.x % H;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
+  const size_t tok = (size_t)3 * H * D, otok = (size_t)H * D;
+  const bf16* base = qkv + (size_t)b * S * tok;
+  load_rows<S, NTHR>(Qs, base + (size_t)hh * D, tok);
+  load_rows<S, NTHR>(Ks, base + (size_t)(H + hh) * D, tok);
+  load_rows<S, NTHR>(Vs, base + (size_t)(2 * H + hh) * D, tok);
+  load_rows<S, NTHR>(dOs, dout + (size_t)b * S * otok + (size_t)hh * D, otok);
+  const int qi = 16 * w + r;
+  // D_i = sum_d dO o O over the lane group's 16 d values, reduced over the 4 groups
+  float di;
+  {
+    const bf16* po = o + ((size_t)b * S + qi) * otok + (size_t)hh * D + 16 * h;
+    const bf16* pd = dout + ((size_t)b * S + qi) * otok + (size_t)hh * D + 16 * h;
+    const v8bf o0 = ld8(po), o1 = ld8(po + 8), d0 = ld8(pd), d1 = ld8(pd + 8);
+    di = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) di += (float)o0[e] * (float)d0[e] + (float)o1[e] * (float)d1[e];
+    di += __shfl_xor(di, 16);
+    di += __shfl_xor(di, 32);
+  }
+  const float lq = lse[((size_t)b * H + hh) * S + qi];
+  __syncthreads();
+
+  v8bf qf[2], dof[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    qf[ks] = ld8(Qs + qi * LD + 32 * ks + 8 * h);
+    dof[ks] = ld8(dOs + qi * LD + 32 * ks + 8 * h);
+  }
+  v4f pp[KT];
+  scores<S>(Ks, qf, pp, r, h);
+  probs<S>(pp, scale, kbias ? kbias + (size_t)b * S : nullptr, lq, h);
+  // dP_d^T = V dO^T
+  v4f dp_[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    v4f a = kZero4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Vs + (16 * kt + r) * LD + 32 * ks + 8 * h), dof[ks], a);
+    dp_[kt] = a;
+  }
+  const uint64_t key = dp.thr ? mifx_rng::drop_key(dp.rng, dp.site) : 0;
+  const uint64_t row_base = (((uint64_t)b * Htot + h0 + hh) * S + qi) * S;
+  v8bf dsb[KS];
+  v4f ds[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const uint32_t k = keep_bits<S>(dp, key, row_base, kt, h);
+    const float dsc = dp.thr ? dp.scale : 1.f;
+    v4f pd;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool kept = (k >> e) & 1;
+      const float dpv = kept ? dp_[kt][e] * dsc : 0.f;  // dP = dP_d o M / (1 - p)
+      ds[kt][e] = pp[kt][e] * (dpv - di) * scale;        // dS (with the score scale folded in)
+      pd[e] = kept ? pp[kt][e] * dsc : 0.f;              // P_d
+    }
+    *(v4bf*)(PT + qi * LP + 16 * kt + 4 * h) = pack4(pd);
+    *(v4bf*)(dST + qi * LP + 16 * kt + 4 * h) = pack4(ds[kt]);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) dsb[ks] = pack8(ds[2 * ks], ds[2 * ks + 1]);
+  // dQ^T = K^T dS^T (K rows read transposed at the chained key order)
+  const int q = r >> 2, p = r & 3;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    v4f a = kZero4;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16* pa = Ks + (32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
+      a = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), dsb[ks], a);
+    }
+    *(v4bf*)(dqkv + ((size_t)b * S + qi) * tok + (size_t)hh * D + 16 * dt + 4 * h) = pack4(a);
+  }
+  __syncthreads();  // P_d and dS images complete
+  // wave w owns keys 16w .. 16w+15: dV^T = dO^T P_d, dK^T = Q^T dS (queries are the reduction, natural order)
+  const int kj = 16 * w;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    v4f av = kZero4, ak = kZero4;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int row = 32 * s + 8 * h + q;
+      const bf16* pdo = dOs + row * LD + 16 * dt + 4 * p;
+      const bf16* pq = Qs + row * LD + 16 * dt + 4 * p;
+      const bf16* ppd = PT + row * LP + kj + 4 * p;
+      const bf16* pds = dST + row * LP + kj + 4 * p;
+      av = mfma(cat8(tr_read(pdo), tr_read(pdo + 4 * LD)), cat8(tr_read(ppd), tr_read(ppd + 4 * LP)), av);
+      ak = mfma(cat8(tr_read(pq), tr_read(pq + 4 * LD)), cat8(tr_read(pds), tr_read(pds + 4 * LP)), ak);
+    }
+    const size_t kr = ((size_t)b * S + kj + r) * tok;
+    *(v4bf*)(dqkv + kr + (size_t)(H + hh) * D + 16 * dt + 4 * h) = pack4(ak);
+    *(v4bf*)(dqkv + kr + (size_t)(2 * H + hh) * D + 16 * dt + 4 * h) = pack4(av);
+  }
+}
+
+uint32_t drop_threshold(float p) {
+  if (!(p > 0.f)) return 0;
+  const float t = p * 65536.f + 0.5f;
+  return t >= 65536.f ? 65536u : (uint32_t)t;
+}
+
+template <int S>
+constexpr int bwd_lds() {
+  return (4 * S * LD + 2 * S * (S + 8)) * 2;
+}
+
+}  // namespace
+
+extern "C" {
+
+// qkv [B, S, 3, H, 64] bf16 (contiguous), kbias [B, S] fp32 additive key bias or null, out [B, S, H, 64] bf16,
+// lse [B, H, S] fp32. p: attention-probability dropout (rng: device int64 [seed, counter]; site per layer).
+// h0 / Htot: this rank's first global head and the model's head count (dropout indexing only).
+int mifx_attn_fwd(const void* qkv, const float* kbias, int B, int S, int H, int h0, int Htot, float scale, float p,
+                  const int64_t* rng, int site, void* out, float* lse, hipStream_t st) {
+  if (B <= 0 || H <= 0 || (S != 64 && S != 128) || p < 0.f || p >= 1.f || (p > 0.f && rng == nullptr)) return -1;
+  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)kbias) % 16 != 0) return -1;
+  const Drop dp{rng, site, drop_threshold(p), 1.f / (1.f - p)};
+  const dim3 grid(B * H);
+  if (S == 128)
+    hipLaunchKernelGGL(attn_fwd<128>, grid, dim3(512), 0, st, (const bf16*)qkv, kbias, scale, dp, H, h0, Htot,
+                       (bf16*)out, lse);
+  else
+    hipLaunchKernelGGL(attn_fwd<64>, grid, dim3(256), 0, st, (const bf16*)qkv, kbias, scale, dp, H, h0, Htot,
+                       (bf16*)out, lse);
+  return (int)hipGetLastError();
+}
+
+// dqkv [B, S, 3, H, 64] bf16 (every element written)
+int mifx_attn_bwd(const void* qkv, const float* kbias, const void* out, const void* dout, const float* lse, int B,
+                  int S, int H, int h0, int Htot, float scale, float p, const int64_t* rng, int site, void* dqkv,
+                  hipStream_t st) {
+  if (B <= 0 || H <= 0 || (S != 64 && S != 128) || p < 0.f || p >= 1.f || (p > 0.f && rng == nullptr)) return -1;
+  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)dout | (uintptr_t)dqkv | (uintptr_t)kbias) % 16 != 0) return -1;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd<128>, hipFuncAttributeMaxDynamicSharedMemorySize, bwd_lds<128>());
+    (void)hipFuncSetAttribute((const void*)attn_bwd<64>, hipFuncAttributeMaxDynamicSharedMemorySize, bwd_lds<64>());
+    attr = true;
+  }
+  const Drop dp{rng, site, drop_threshold(p), 1.f / (1.f - p)};
+  const dim3 grid(B * H);
+  if (S == 128)
+    hipLaunchKernelGGL(attn_bwd<128>, grid, dim3(512), bwd_lds<128>(), st, (const bf16*)qkv, kbias, (const bf16*)out,
+                       (const bf16*)dout, lse, scale, dp, H, h0, Htot, (bf16*)dqkv);
+  else
+    hipLaunchKernelGGL(attn_bwd<64>, grid, dim3(256), bwd_lds<64>(), st, (const bf16*)qkv, kbias, (const bf16*)out,
+                       (const bf16*)dout, lse, scale, dp, H, h0, Htot, (bf16*)dqkv);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

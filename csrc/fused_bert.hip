@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "counter_rng.h"
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -75,32 +77,10 @@ __device__ __forceinline__ void stv(T* p, const float* v) {
   *(Pack<T, N>*)p = pk;
 }
 
-// ---- dropout mask: counter-based, recomputed in the backward (nothing stored) and hipGraph-replay safe.
-// rng points at device int64 [seed, step counter]; the counter is advanced by an in-graph op once per step,
-// so replays draw fresh masks without any host-side state. A 64-bit finaliser (murmur3 fmix64) of
-// (seed, counter, site) gives the per-call key; each group of 4 consecutive elements (flat index 4g..4g+3)
-// takes the four 16-bit lanes of mix64(key + g * golden) and keeps element e iff lane_e >= thr
-// (thr = round(p * 65536)). The same bits are produced by mifx.ops.fused_bert._keep_mask_cpu, so CPU and GPU
-// runs of a model draw identical masks, and every tensor-parallel rank (same seed) draws the same mask for a
-// replicated activation.
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z ^= z >> 33;
-  z *= 0xff51afd7ed558ccdULL;
-  z ^= z >> 33;
-  z *= 0xc4ceb9fe1a85ec53ULL;
-  z ^= z >> 33;
-  return z;
-}
-constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
-
-__device__ __forceinline__ uint64_t drop_key(const int64_t* rng, int site) {
-  return mix64((uint64_t)rng[0] ^ mix64((uint64_t)rng[1] * kGolden + (uint64_t)site));
-}
-__device__ __forceinline__ uint32_t keep4(uint64_t key, uint64_t g, uint32_t thr) {
-  const uint64_t h = mix64(key + g * kGolden);
-  return (uint32_t)((h & 0xffff) >= thr) | ((uint32_t)(((h >> 16) & 0xffff) >= thr) << 1) |
-         ((uint32_t)(((h >> 32) & 0xffff) >= thr) << 2) | ((uint32_t)((h >> 48) >= thr) << 3);
-}
+// ---- dropout mask: counter-based, recomputed in the backward (nothing stored), hipGraph-replay safe; identical
+// on every TP rank for a replicated activation (same seed). Definition: csrc/counter_rng.h.
+using mifx_rng::drop_key;
+using mifx_rng::keep4;
 
 // Drop: the optional (bias, dropout) prologue of the fused LayerNorm: s = keep ? (a + bias) * scale : 0, + r.
 // thr == 0 disables dropout (no hashing); bias == nullptr disables the bias.

@@ -32,7 +32,8 @@ class BertConfig:
     type_vocab: int = 2
     dropout: float = 0.1
     attn_dropout: float | None = None  # attention-probability dropout (None: same as dropout)
-    dropout_seed: int = 1234  # hidden-dropout mask seed (identical on every TP rank)
+    dropout_seed: int = 1234  # dropout mask seed (identical on every TP rank)
+    fused_attention: bool = True  # csrc/attention.hip (False: torch scaled_dot_product_attention)
     num_labels: int = 2
     ln_eps: float = 1e-12
     init_std: float = 0.02
@@ -76,22 +77,29 @@ class BertLayer(nn.Module):
             getattr(self, n).load_state_dict({"weight": sd[f"{prefix}{n}.weight"], "bias": sd[f"{prefix}{n}.bias"]})
 
     def forward(self, x, mask, rng=None, site=0):
-        """Dropout RNG: attention-probability dropout runs inside SDPA on this rank's own heads with the torch
-        generator (per-rank stream: its offset use differs with the uneven head split and never reaches the
-        replicated activations); the hidden dropouts act on REPLICATED activations (every TP rank holds the
-        same [B, S, H] tensor) and use the counter-based mask of fb.bias_dropout_add_layernorm keyed by
-        (model seed, step counter, site) — identical on all TP ranks by construction, fused with the row-parallel
-        bias, the residual add and the LayerNorm. Sites `site` and `site + 1`."""
+        """Dropout RNG: every mask is counter-based (model seed, step counter, site; csrc/counter_rng.h), never the
+        torch generator. The hidden dropouts act on REPLICATED activations (every TP rank holds the same [B, S, H]
+        tensor) and are fused with the row-parallel bias, the residual add and the LayerNorm
+        (fb.bias_dropout_add_layernorm, sites `site` and `site + 1`); the attention-probability dropout indexes
+        its mask by the global head (fb.attention, site 1000 + site), so both are identical for every TP split.
+        (With fused_attention=False the attention dropout is SDPA's, on the torch generator.)"""
         B, S, _ = x.shape
         h, d = self.local_heads, self.head_dim
-        # q/k/v as [B, h, S, d] views of the fused QKV output; unbind (not indexing a permuted view) so the
-        # backward assembles dq/dk/dv with ONE stack copy instead of a zero-fill plus three slice copies
-        q, k, v = (t.transpose(1, 2) for t in self.qkv(x).view(B, S, 3, h, d).unbind(2))
         c = self.cfg
         drop = c.dropout if self.training else 0.0
         adrop = (c.dropout if c.attn_dropout is None else c.attn_dropout) if self.training else 0.0
-        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=adrop)
-        ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
+        qkv = self.qkv(x).view(B, S, 3, h, d)
+        if c.fused_attention:
+            # fused attention straight on the projection output (no q/k/v transposes); its dropout mask is keyed
+            # by the GLOBAL head index, so it is identical for any TP split (site: this layer's attention)
+            h0 = sum(self.heads_per_rank[:self.tp.rank])
+            ctx = fb.attention(qkv, mask, 1.0 / d ** 0.5, adrop, rng, 1000 + site, h0, c.heads).reshape(B, S, h * d)
+        else:
+            # q/k/v as [B, h, S, d] views; unbind so the backward assembles dq/dk/dv with ONE stack copy
+            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+            amask = None if mask is None else mask[:, None, None, :].to(q.dtype)
+            ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, dropout_p=adrop)
+            ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
         x = fb.bias_dropout_add_layernorm(self.attn_out(ctx, add_bias=False), self.attn_out.bias, x, self.ln1.weight,
                                           self.ln1.bias, c.ln_eps, drop, rng, site)
         f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
@@ -139,8 +147,8 @@ class BertForSequenceClassification(nn.Module):
             self.drop_rng[1:].add_(1)  # new masks every step (captured into the step's hipGraph)
         x = fb.dropout(self.ln_emb(x), drop, self.drop_rng, 0)
         mask = None
-        if attention_mask is not None:  # additive mask [B, 1, 1, S]
-            mask = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * torch.finfo(x.dtype).min
+        if attention_mask is not None:  # additive key bias [B, S] (fp32; -1e30 on padding keys)
+            mask = ((1.0 - attention_mask.float()) * -1e30).contiguous()
         for i, layer in enumerate(self.layers):
             x = layer(x, mask, self.drop_rng, 1 + 2 * i)
         pooled = torch.tanh(self.pooler(x[:, 0]))

@@ -328,3 +328,75 @@ def bias_gelu(x: torch.Tensor, bias) -> torch.Tensor:
     if x.is_cuda and not _TORCH_OPS:
         return _BiasGelu.apply(x, bias)
     return F.gelu(x + bias)
+
+
+# ---- fused attention (csrc/attention.hip) ----------------------------------------------------------------------
+@functools.lru_cache(maxsize=None)
+def _attn_fns():
+    lib = _lib.load("attention")
+    return {
+        "fwd": sig(lib, "mifx_attn_fwd", [VP, VP, I32, I32, I32, I32, I32, F32, F32, VP, I32, VP, VP, VP]),
+        "bwd": sig(lib, "mifx_attn_bwd", [VP, VP, VP, VP, VP, I32, I32, I32, I32, I32, F32, F32, VP, I32, VP, VP]),
+    }
+
+
+ATTN_SEQ = (64, 128)  # sequence lengths of the fused kernels (head dim 64)
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, kbias, scale, p, rng, site, h0, htot):
+        B, S, _, H, Dh = qkv.shape
+        qkv = qkv.contiguous()
+        out = torch.empty(B, S, H, Dh, device=qkv.device, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, S, device=qkv.device, dtype=torch.float32)
+        kb = None if kbias is None else kbias.float().contiguous()
+        check(_attn_fns()["fwd"](ptr(qkv), ptr(kb), B, S, H, int(h0), int(htot), float(scale), float(p),
+                                 ptr(rng if p > 0 else None), int(site), ptr(out), ptr(lse), stream_handle(qkv.device)),
+              "mifx_attn_fwd")
+        ctx.save_for_backward(qkv, kb, out, lse)
+        ctx.args = (float(scale), float(p), rng, int(site), int(h0), int(htot))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, kb, out, lse = ctx.saved_tensors
+        scale, p, rng, site, h0, htot = ctx.args
+        B, S, _, H, Dh = qkv.shape
+        dout = dout.to(torch.bfloat16).contiguous()
+        dqkv = torch.empty_like(qkv)
+        check(_attn_fns()["bwd"](ptr(qkv), ptr(kb), ptr(out), ptr(dout), ptr(lse), B, S, H, h0, htot, scale, p,
+                                 ptr(rng if p > 0 else None), site, ptr(dqkv), stream_handle(qkv.device)),
+              "mifx_attn_bwd")
+        return dqkv, None, None, None, None, None, None, None
+
+
+def attention_reference(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, rng=None, site: int = 0, h0: int = 0,
+                        htot: int | None = None) -> torch.Tensor:
+    """PyTorch reference of the fused attention: qkv [B, S, 3, H, Dh] -> [B, S, H, Dh]; kbias [B, S] additive
+    key bias; dropout mask element (b, global head, i, j) = keep_mask at flat index ((b Htot + h0 + h) S + i) S + j
+    (the kernel's indexing, so any head split over TP ranks draws the same mask)."""
+    B, S, _, H, Dh = qkv.shape
+    htot = H if htot is None else htot
+    q, k, v = (t.float() for t in qkv.unbind(2))
+    s = torch.einsum("bihd,bjhd->bhij", q, k) * scale
+    if kbias is not None:
+        s = s + kbias.float()[:, None, None, :]
+    pr = torch.softmax(s, -1)
+    if p > 0:
+        keep = keep_mask(B * htot * S * S, rng, site, p).view(B, htot, S, S)[:, h0:h0 + H].to(pr.device)
+        pr = torch.where(keep, pr * _drop_scale(p), torch.zeros((), dtype=pr.dtype, device=pr.device))
+    return torch.einsum("bhij,bjhd->bihd", pr, v.float()).to(qkv.dtype)
+
+
+def attention(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, rng=None, site: int = 0, h0: int = 0,
+              htot: int | None = None) -> torch.Tensor:
+    """Multi-head self-attention over the fused projection output qkv [B, S, 3, H, Dh] -> [B, S, H, Dh].
+    GPU (bf16, Dh 64, S 64 or 128): csrc/attention.hip fwd/bwd; elsewhere the reference composition (same mask)."""
+    if p > 0 and rng is None:
+        raise ValueError("attention dropout p > 0 needs an rng state tensor [seed, counter]")
+    htot = qkv.shape[3] if htot is None else htot
+    if (qkv.is_cuda and not _TORCH_OPS and qkv.shape[1] in ATTN_SEQ and qkv.shape[4] == 64
+            and qkv.dtype == torch.bfloat16):
+        return _Attention.apply(qkv, kbias, scale, p, rng, site, h0, htot)
+    return attention_reference(qkv, kbias, scale, p, rng, site, h0, htot)

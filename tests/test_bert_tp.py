@@ -107,14 +107,41 @@ def test_tp_dropout_replicated_params_identical_and_match_tp1():
 
 
 def test_tp_attention_dropout_keeps_replicated_params_identical():
-    """With attention-probability dropout on too (per-rank torch generator on the local heads, uneven split at
-    TP=3), the replicated parameters still stay bit-identical across ranks."""
+    """With attention-probability dropout on too (uneven head split at TP=3): its mask is indexed by the GLOBAL
+    head, so replicated parameters stay bit-identical across ranks AND the TP=3 trajectory equals TP=1."""
+    cfg = BertConfig.tiny(dropout=0.1)
+    ref = BertForSequenceClassification(cfg, None, seed=1)
+    for _ in range(2):
+        ref_logits = _step(ref, cfg)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
         mp.start_processes(_worker, args=(3, _port(), out, {"dropout": 0.1}, 2), nprocs=3, start_method="spawn")
         reps = [torch.load(f"{out}.repl{r}", weights_only=True) for r in range(3)]
+        got = torch.load(out, weights_only=True)
     for k in reps[0]:
         assert torch.equal(reps[0][k], reps[1][k]) and torch.equal(reps[0][k], reps[2][k]), k
+    torch.testing.assert_close(got["logits"], ref_logits, rtol=1e-4, atol=1e-5)
+
+
+def test_attention_reference_matches_sdpa_and_masks():
+    from mifx.ops import fused_bert as fb
+
+    torch.manual_seed(4)
+    B, S, H, Dh = 2, 16, 3, 8
+    qkv = torch.randn(B, S, 3, H, Dh)
+    am = torch.ones(B, S)
+    am[1, 11:] = 0
+    kb = (1.0 - am) * -1e30
+    got = fb.attention(qkv, kb, Dh ** -0.5)
+    q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=(kb[:, None, None, :] > -1))
+    torch.testing.assert_close(got, ref.transpose(1, 2), rtol=1e-5, atol=1e-5)
+    rng = torch.tensor([3, 9])
+    d1 = fb.attention(qkv, kb, Dh ** -0.5, 0.2, rng, 7)
+    assert not torch.allclose(d1, got)
+    # a head slice with its global offset draws the same mask as the full model (TP invariance)
+    part = fb.attention(qkv[:, :, :, 1:3].contiguous(), kb, Dh ** -0.5, 0.2, rng, 7, h0=1, htot=3)
+    torch.testing.assert_close(part, d1[:, :, 1:3])
 
 
 def test_counter_dropout_mask_cpu():
@@ -135,6 +162,35 @@ def test_counter_dropout_mask_cpu():
     x = torch.randn(5, 9)
     torch.testing.assert_close(fb.dropout(x, 0.5, rng, 1), torch.where(fb.keep_mask(45, rng, 1, 0.5).view(5, 9),
                                                                       x * 2, 0.0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,H", [(128, 12), (64, 5)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fused_attention_gpu(S, H, p):
+    """csrc/attention.hip forward/backward against the fp32 PyTorch reference with the same key mask and the same
+    counter-based dropout mask (h0 / Htot: a TP shard of a larger head set)."""
+    from mifx.ops import fused_bert as fb
+
+    torch.manual_seed(S + H)
+    B, Dh, h0, htot = 3, 64, 2, H + 4
+    qkv = (torch.randn(B, S, 3, H, Dh, device="cuda") * 0.7).bfloat16().requires_grad_()
+    am = torch.ones(B, S, device="cuda")
+    am[1, S - 9:] = 0
+    am[2, S // 2:] = 0
+    kb = ((1.0 - am) * -1e30).contiguous()
+    rng = torch.tensor([5, 17], dtype=torch.int64, device="cuda")
+    out = fb.attention(qkv, kb, Dh ** -0.5, p, rng, 3, h0, htot)
+    q32 = qkv.detach().float().requires_grad_()
+    ref = fb.attention_reference(q32, kb, Dh ** -0.5, p, rng, 3, h0, htot)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g)
+    got, want = qkv.grad.float(), q32.grad
+    for i, name in enumerate("qkv"):
+        err = (got[:, :, i] - want[:, :, i]).norm() / want[:, :, i].norm()
+        assert err < 2e-2, f"d{name}: relative error {err:.4f}"
 
 
 @pytest.mark.gpu
