@@ -381,27 +381,27 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 
   // dW tile ownership (wave w); 4 waves: L1 nt {2w, 2w+1} x kt 0 (kt 1 holds only padding columns);
   // L2 nt 0..5 x kt {2w, 2w+1}; L3 nt w x kt 0..5; L4 nt w x kt 0..3; L5 nt 0 x kt w.
-  // 8 waves: L1 nt w x kt 0; L2 nt 0..5 x kt w; L3 nt w%4 x kt 3(w/4)..+2; L4 nt w%4 x kt 2(w/4)..+1;
-  // L5 nt 0 x kt w (waves 0..3)
-  constexpr int O1N = TBN == 2 ? 2 : 1, O2K = TBN == 2 ? 2 : 1, O3K = TBN == 2 ? 6 : 3,
+  // 8 waves: L1 nt w x kt 0; L2 nt 3(w%2)..+2 x kt 2(w/2)..+1 (3 x 2 blocks: 5 operand fragments per k-step
+  // instead of 7 for 6 x 1); L3 nt w%4 x kt 3(w/4)..+2; L4 nt w%4 x kt 2(w/4)..+1; L5 nt 0 x kt w (waves 0..3)
+  constexpr int O1N = TBN == 2 ? 2 : 1, O2N = TBN == 2 ? 6 : 3, O2K = 2, O3K = TBN == 2 ? 6 : 3,
                 O4K = TBN == 2 ? 4 : 2;
-  const int n1 = TBN == 2 ? 2 * w : w, k2 = TBN == 2 ? 2 * w : w, n3 = w & 3, k3 = TBN == 2 ? 0 : 3 * (w >> 2),
-            n4 = w & 3, k4 = TBN == 2 ? 0 : 2 * (w >> 2);
+  const int n1 = TBN == 2 ? 2 * w : w, n2 = TBN == 2 ? 0 : 3 * (w & 1), k2 = TBN == 2 ? 2 * w : 2 * (w >> 1),
+            n3 = w & 3, k3 = TBN == 2 ? 0 : 3 * (w >> 2), n4 = w & 3, k4 = TBN == 2 ? 0 : 2 * (w >> 2);
   const bool l5 = w < 4;
-  v4f acc1[O1N], acc2[6 * O2K], acc3[O3K], acc4[O4K], acc5[1];
-  int ct1[O1N], ct2[6 * O2K], ct3[O3K], ct4[O4K], ct5[1];
+  v4f acc1[O1N], acc2[O2N * O2K], acc3[O3K], acc4[O4K], acc5[1];
+  int ct1[O1N], ct2[O2N * O2K], ct3[O3K], ct4[O4K], ct5[1];
   if (TRAIN) {
 #pragma unroll
     for (int i = 0; i < O1N; ++i) acc1[i] = kZero4;
 #pragma unroll
-    for (int i = 0; i < 6 * O2K; ++i) acc2[i] = kZero4;
+    for (int i = 0; i < O2N * O2K; ++i) acc2[i] = kZero4;
 #pragma unroll
     for (int i = 0; i < O3K; ++i) acc3[i] = kZero4;
 #pragma unroll
     for (int i = 0; i < O4K; ++i) acc4[i] = kZero4;
     acc5[0] = kZero4;
     load_ct<K1, O1N, 1>(ct1, TB1, n1, 1, 0, 0, tmap);
-    load_ct<K2, 6, O2K>(ct2, TB2, 0, 1, k2, 1, tmap);
+    load_ct<K2, O2N, O2K>(ct2, TB2, n2, 1, k2, 1, tmap);
     load_ct<K3, 1, O3K>(ct3, TB3, n3, 0, k3, 1, tmap);
     load_ct<K4, 1, O4K>(ct4, TB4, n4, 0, k4, 1, tmap);
     load_ct<K5, 1, 1>(ct5, TB5, 0, 0, w & 3, 0, tmap);
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     stage<K2, N2, TBN>(S, dz2, a1, w, r, h);
     block_sync_lds();
     STAMP(12);
-    dw_phase<K2, N2, 6, O2K>(acc2, S, 0, 1, k2, 1, r, h);
+    dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
     v4bf dz1[TBN][K2 / 16];
     {
       v4f g[TBN][K2 / 16];
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * stride;
     store_tiles<O1N>(my, acc1, ct1, lane);
-    store_tiles<6 * O2K>(my, acc2, ct2, lane);
+    store_tiles<O2N * O2K>(my, acc2, ct2, lane);
     store_tiles<O3K>(my, acc3, ct3, lane);
     store_tiles<O4K>(my, acc4, ct4, lane);
     store_tiles<1>(my, acc5, ct5, lane);

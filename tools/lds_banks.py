@@ -226,3 +226,33 @@ def optimise():
 
 if __name__ == "__main__" and __import__("sys").argv[1:] == ["opt"]:
     optimise()
+
+
+def rowbit3_swz(mask_gran):
+    """XOR the granule index with mask_gran on rows whose bit 3 is set (cheap: bit 3 of the row is lane-dependent
+    in every staging access, so at most two address variants per access pattern)."""
+    def f(row, g, ngran):
+        return g ^ (mask_gran if (row >> 3) & 1 else 0)
+    return f
+
+
+def staging_candidates():
+    print("== staging: pad + (row bit 3 -> granule XOR 16) candidates")
+    for cols in (64, 96, 128):
+        base = staging_cost(Layout(cols, 8), cols, True, True, True)
+        res = []
+        for pad in (8, 16, 24, 32):
+            for m in (0, 16):
+                if m >= cols // 4:
+                    continue
+                L = Layout(cols, pad, rowbit3_swz(m) if m else None)
+                res.append((staging_cost(L, cols, True, True, True), pad, m,
+                            sum(dw_read(L, cols)), sum(stage_writes(L, L, cols, cols)[0]),
+                            sum(stage_writes(L, L, cols, cols)[1]), sum(mask_read(L, cols))))
+        res.sort()
+        print(f"   cols {cols}: current (pad 8) {base}; best: " + "; ".join(
+            f"cost {c} pad {p} xor {m} (dW {a} dZw {b} Aw {c2} mask {d})" for c, p, m, a, b, c2, d in res[:3]))
+
+
+if __name__ == "__main__" and __import__("sys").argv[1:] == ["stage"]:
+    staging_candidates()
