@@ -12,8 +12,9 @@
 //  * O^T = V^T P^T: the P^T tiles 2s, 2s+1 ARE the B operand of k-step s (keys in the chained order
 //    32s + 16(e/4) + 4h + e%4), so the V^T operand is read with ds_read_b64_tr_b16 at those key rows.
 //  * backward: S^T and dP_d^T = V dO^T recomputed per wave; dS^T = P^T (dP^T - D), D = rowsum(dO o O);
-//    dQ^T = K^T dS^T chained the same way; P_d and dS are staged once in LDS ([query][key]) and each wave then
-//    owns 16 keys for dV^T = dO^T P_d and dK^T = Q^T dS, reading both operands with transposed LDS reads.
+//    dQ^T = K^T dS^T chained the same way; P_d, then dS, are staged in LDS ([query][key], over the no longer
+//    needed K / V images: 74 KB per workgroup, two workgroups per CU) and each wave then owns 16 keys for
+//    dV^T = dO^T P_d and dK^T = Q^T dS, reading both operands with transposed LDS reads.
 // qkv is the fused projection output [B, S, 3, H, 64] (this rank's H heads), out / dout are [B, S, H, 64]; no
 // transposes around the kernels. Dropout element (b, global head, i, j) uses the flat index
 // ((b Htot + h0 + h) S + i) S + j into the counter-based mask of csrc/counter_rng.h, so the mask does not depend
@@ -195,8 +196,9 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
   bf16* Ks = Qs + S * LD;
   bf16* Vs = Ks + S * LD;
   bf16* dOs = Vs + S * LD;
-  bf16* PT = dOs + S * LD;  // P_d [query][key]
-  bf16* dST = PT + S * LP;  // dS * scale [query][key]
+  // P_d and dS are staged, one after the other, over the K / V images once those are no longer read
+  // ([query][key] rows of S + 8: 17 KB <= the 18 KB of K + V at S = 128): 74 KB of LDS -> two workgroups per CU
+  bf16* KV = Ks;
   const int b = blockIdx.x / H, hh = blockIdx.x % H;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
   const size_t tok = (size_t)3 * H * D, otok = (size_t)H * D;
@@ -243,6 +245,7 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
   const uint64_t row_base = (((uint64_t)b * Htot + h0 + hh) * S + qi) * S;
   v8bf dsb[KS];
   v4f ds[KT];
+  v4bf pdv[KT], dsv[KT];
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     const uint32_t k = keep_bits<S>(dp, key, row_base, kt, h);
@@ -255,8 +258,8 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
       ds[kt][e] = pp[kt][e] * (dpv - di) * scale;        // dS (with the score scale folded in)
       pd[e] = kept ? pp[kt][e] * dsc : 0.f;              // P_d
     }
-    *(v4bf*)(PT + qi * LP + 16 * kt + 4 * h) = pack4(pd);
-    *(v4bf*)(dST + qi * LP + 16 * kt + 4 * h) = pack4(ds[kt]);
+    pdv[kt] = pack4(pd);
+    dsv[kt] = pack4(ds[kt]);
   }
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) dsb[ks] = pack8(ds[2 * ks], ds[2 * ks + 1]);
@@ -272,25 +275,40 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
     }
     *(v4bf*)(dqkv + ((size_t)b * S + qi) * tok + (size_t)hh * D + 16 * dt + 4 * h) = pack4(a);
   }
-  __syncthreads();  // P_d and dS images complete
-  // wave w owns keys 16w .. 16w+15: dV^T = dO^T P_d, dK^T = Q^T dS (queries are the reduction, natural order)
+  // wave w owns keys 16w .. 16w+15: dV^T = dO^T P_d, then dK^T = Q^T dS (queries are the reduction, natural
+  // order); each staged over K / V once every wave is past its reads of them
   const int kj = 16 * w;
+  __syncthreads();  // K / V reads (scores, dP, dQ) done
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) *(v4bf*)(KV + qi * LP + 16 * kt + 4 * h) = pdv[kt];
+  __syncthreads();
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
-    v4f av = kZero4, ak = kZero4;
+    v4f av = kZero4;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int row = 32 * s + 8 * h + q;
       const bf16* pdo = dOs + row * LD + 16 * dt + 4 * p;
-      const bf16* pq = Qs + row * LD + 16 * dt + 4 * p;
-      const bf16* ppd = PT + row * LP + kj + 4 * p;
-      const bf16* pds = dST + row * LP + kj + 4 * p;
+      const bf16* ppd = KV + row * LP + kj + 4 * p;
       av = mfma(cat8(tr_read(pdo), tr_read(pdo + 4 * LD)), cat8(tr_read(ppd), tr_read(ppd + 4 * LP)), av);
+    }
+    *(v4bf*)(dqkv + ((size_t)b * S + kj + r) * tok + (size_t)(2 * H + hh) * D + 16 * dt + 4 * h) = pack4(av);
+  }
+  __syncthreads();  // P_d reads done
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) *(v4bf*)(KV + qi * LP + 16 * kt + 4 * h) = dsv[kt];
+  __syncthreads();
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    v4f ak = kZero4;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int row = 32 * s + 8 * h + q;
+      const bf16* pq = Qs + row * LD + 16 * dt + 4 * p;
+      const bf16* pds = KV + row * LP + kj + 4 * p;
       ak = mfma(cat8(tr_read(pq), tr_read(pq + 4 * LD)), cat8(tr_read(pds), tr_read(pds + 4 * LP)), ak);
     }
-    const size_t kr = ((size_t)b * S + kj + r) * tok;
-    *(v4bf*)(dqkv + kr + (size_t)(H + hh) * D + 16 * dt + 4 * h) = pack4(ak);
-    *(v4bf*)(dqkv + kr + (size_t)(2 * H + hh) * D + 16 * dt + 4 * h) = pack4(av);
+    *(v4bf*)(dqkv + ((size_t)b * S + kj + r) * tok + (size_t)(H + hh) * D + 16 * dt + 4 * h) = pack4(ak);
   }
 }
 
@@ -302,7 +320,8 @@ uint32_t drop_threshold(float p) {
 
 template <int S>
 constexpr int bwd_lds() {
-  return (4 * S * LD + 2 * S * (S + 8)) * 2;
+  static_assert(S * (S + 8) <= 2 * S * LD, "P_d / dS staging must fit over the K and V images");
+  return 4 * S * LD * 2;
 }
 
 }  // namespace
