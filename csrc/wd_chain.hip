@@ -42,12 +42,10 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 constexpr int T = 128;  // examples per workgroup iteration
 constexpr int MAXW = 8;  // waves per workgroup: T / (16 TBN), TBN = 16-example column blocks per wave (1 or 2)
-// Row padding (elements): WPAD for the weight images, PAD for the staging images. With the per-row XOR swizzles
-// below set to zero these are the bank-conflict controls: tools/lds_banks.py models every access site; WPAD 16
-// makes the forward row reads conflict-free and halves the transposed-read conflicts of the activation-gradient
-// product (3.1x -> 2x of the ideal LDS cycles); PAD 8 is the best plain pad for the staging images. (Non-zero
-// swizzle masks remove the remaining conflicts in the model, but their per-lane XORs defeat the compiler's
-// immediate-offset addressing and the 4- and 8-wave kernels then spill: measured, not adopted.)
+// Row padding (elements): WPAD for the weight images, PAD for the staging images; with the row permutations below
+// (wperm, sperm16) every LDS access site is conflict-free in the bank model (tools/lds_banks.py). (XOR swizzles
+// of 8-byte granules reach the same in the model, but their per-lane XORs defeat the compiler's immediate-offset
+// addressing and the kernels then spill: measured, not adopted.)
 constexpr int WPAD = 16;
 constexpr int PAD = 8;
 
@@ -128,38 +126,18 @@ __device__ __forceinline__ void block_sync_lds() {
 }
 constexpr v4f kZero4 = {0.f, 0.f, 0.f, 0.f};
 
-// ---- LDS image swizzles: element (row, col) of a [rows][C] bf16 image lives at row * C + 4 * (col / 4 ^ X(row)) +
-// col % 4, X(row) = XOR of m[b] over the set bits b of row (8-byte granules; masks even, so the 16-byte pairs
-// that ds_read_b128 / ds_write_b128 move stay contiguous). Masks chosen by tools/lds_banks.py (bank model of
-// every access site in this kernel): weight images -> conflict-free forward row reads and activation-gradient
-// transposed reads; staging images -> near conflict-free dW transposed reads, stores and mask reads.
-// models.wide_deep.CHAIN_WSWZ mirrors WSwz for the host-built image.
-struct Swz {
-  int m[7];
-};
-// conflict-free in the bank model but not adopted (register cost, see WPAD): weight K=128 {4, 8, 16, 0, 16, 0, 0},
-// K=64 {0, 4, 8, 0, 8, 0, 0}, K=32/96 {0, 0, 4, 0, 4, 0, 0}; staging C=128 {4, 8, 2, 16}, C=64 {2, 4, 8, 10},
-// C=32/96 {0, 2, 4, 6}
-template <int K>
-__host__ __device__ constexpr Swz wswz() {
-  return Swz{{0, 0, 0, 0, 0, 0, 0}};
-}
-template <int C>
-__host__ __device__ constexpr Swz sswz() {
-  return Swz{{0, 0, 0, 0, 0, 0, 0}};
-}
-__host__ __device__ constexpr int xmask(const Swz& s, int row) {
-  int x = 0;
-  for (int b = 0; b < 7; ++b)
-    if ((row >> b) & 1) x ^= s.m[b];
-  return x;
-}
-// element offset of (row_lane + row_c, col) in an image with rows of RL elements, where row_lane and row_c have
-// disjoint bits (so the row mask is xmask(row_lane) ^ xmask(row_c): the constant part folds at compile time)
-template <int RL>
-__device__ __forceinline__ int soff(const Swz& s, int xl, int row_lane, int row_c, int col) {
-  return (row_lane + row_c) * RL + 4 * ((col >> 2) ^ xl ^ xmask(s, row_c)) + (col & 3);
-}
+// ---- LDS row permutations (bank-conflict control; tools/lds_banks.py models every access site of this kernel and
+// finds all of them conflict-free with these layouts, padding alone leaves 2x on the transposed reads):
+//  * weight images: physical row wperm(n) = n ^ (bit 4 of n) << 2. The activation-gradient transposed reads of a
+//    32-lane half touch rows q and 16 + q (+8); with 8 + 16 k dword rows (WPAD 16) rows 16 + q would share banks
+//    with rows q, as rows 20 + q they do not. The lane part of every permuted row is known per lane (bit 4 of the
+//    row is lane-dependent in the transposed read, one of two constants in the forward read).
+//  * staging images: inside every 16-row block, row bits (b3 b2 b1 b0) -> (b3 b1 b0 b2): the 8 rows a 32-lane half
+//    of a dW transposed read touches (q, 8 + q) become physical rows of one parity, which with 4 mod 8 dword rows
+//    (PAD 8) are 8 dwords apart mod 64; the 16-byte stores and 8-byte mask reads of 16 consecutive rows stay
+//    conflict-free. models.wide_deep.chain_image_offsets applies wperm on the host.
+__host__ __device__ constexpr int wperm(int n) { return n ^ (((n >> 4) & 1) << 2); }
+__host__ __device__ constexpr int sperm16(int t) { return (t & 8) | ((t & 3) << 1) | ((t >> 2) & 1); }
 
 #ifdef WDC_STAMPS  // diagnostic build only (tools/build_stamps.sh): per-wave shader-clock stamps of block 0
 __device__ unsigned long long g_wdc_stamps[MAXW][32];
@@ -169,7 +147,18 @@ __device__ unsigned long long g_wdc_stamps[MAXW][32];
     if (blockIdx.x == 0 && lane == 0 && stamp_on) g_wdc_stamps[w][i] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                            \
   } while (0)
+// per-block 100 MHz global clock: [block][0] start, [1] prologue done, [2] end (wave 0)
+__device__ unsigned long long g_wdc_blk[4096][3];
+#define BSTAMP(i)                                                                                       \
+  do {                                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+    if (w == 0 && lane == 0 && blockIdx.x < 4096) g_wdc_blk[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+  } while (0)
 #else
+#define BSTAMP(i) \
+  do {            \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -185,16 +174,15 @@ __device__ __forceinline__ void fwd(const uint16_t* W, const v8bf (&B)[TBN][K / 
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int tb = 0; tb < TBN; ++tb) acc[tb][nt] = kZero4;
-  constexpr Swz sw = wswz<K>();
-  const int xl = xmask(sw, r);
+  const int rw[2] = {r, r ^ 4};  // physical row in a 32-row block: 16 nt + rw[nt & 1]
   v8bf wa[2][NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) wa[0][nt] = ld8(W + soff<K + WPAD>(sw, xl, r, 16 * nt, 8 * h));
+  for (int nt = 0; nt < NT; ++nt) wa[0][nt] = ld8(W + (16 * nt + rw[nt & 1]) * (K + WPAD) + 8 * h);
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (s + 1 < KS) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) wa[(s + 1) & 1][nt] = ld8(W + soff<K + WPAD>(sw, xl, r, 16 * nt, 32 * (s + 1) + 8 * h));
+      for (int nt = 0; nt < NT; ++nt) wa[(s + 1) & 1][nt] = ld8(W + (16 * nt + rw[nt & 1]) * (K + WPAD) + 32 * (s + 1) + 8 * h);
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -219,9 +207,7 @@ __device__ __forceinline__ void bwd_dA(const uint16_t* W, const v4bf (&dz)[TBN][
                                        int h) {
   constexpr int NS = N / 32, KT = K / 16;
   const int q = r >> 2, p = r & 3;
-  const int rb = 16 * (h & 1) + 4 * (h >> 1) + q;
-  constexpr Swz sw = wswz<K>();
-  const int xl = xmask(sw, rb);
+  const int rb = wperm(16 * (h & 1) + 4 * (h >> 1) + q);  // + 32 s (+8): bits 3, 5, 6 untouched by wperm
   v8bf b[TBN][NS];
 #pragma unroll
   for (int tb = 0; tb < TBN; ++tb)
@@ -236,8 +222,8 @@ __device__ __forceinline__ void bwd_dA(const uint16_t* W, const v4bf (&dz)[TBN][
     v8bf a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      a[s] = cat8(tr_read(W + soff<K + WPAD>(sw, xl, rb, 32 * s, 16 * kt + 4 * p)),
-                  tr_read(W + soff<K + WPAD>(sw, xl, rb, 32 * s + 8, 16 * kt + 4 * p)));
+      const uint16_t* pa = W + (32 * s + rb) * (K + WPAD) + 16 * kt + 4 * p;
+      a[s] = cat8(tr_read(pa), tr_read(pa + 8 * (K + WPAD)));
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s)
@@ -250,15 +236,13 @@ __device__ __forceinline__ void bwd_dA(const uint16_t* W, const v4bf (&dz)[TBN][
 template <int K, int TBN>
 __device__ __forceinline__ void mask_grad(const v4f (&g)[TBN][K / 16], const uint16_t* SA, int w, int r, int h,
                                           v4bf (&dz)[TBN][K / 16]) {
-  constexpr Swz sw = sswz<K>();
-  const int xl = xmask(sw, r);
+  const int rp = sperm16(r);
 #pragma unroll
   for (int tb = 0; tb < TBN; ++tb)
 #pragma unroll
     for (int kt = 0; kt < K / 16; ++kt) {
-      // row 16 TBN w + 16 tb + r: the wave part is not a compile-time constant, fold it at run time
-      const int rc = 16 * TBN * w + 16 * tb;
-      const uint2 m = *(const uint2*)(SA + (rc + r) * (K + PAD) + 4 * ((4 * kt + h) ^ xl ^ xmask(sw, rc)));
+      const int row = 16 * TBN * w + 16 * tb + rp;
+      const uint2 m = *(const uint2*)(SA + row * (K + PAD) + 16 * kt + 4 * h);
       v4bf o;
       o[0] = (bf16)((m.x & 0xffffu) ? g[tb][kt][0] : 0.f);
       o[1] = (bf16)((m.x >> 16) ? g[tb][kt][1] : 0.f);
@@ -268,26 +252,22 @@ __device__ __forceinline__ void mask_grad(const v4f (&g)[TBN][K / 16], const uin
     }
 }
 
-// stage dZ (gradient tiles in C order of the layer above -> natural order columns) and the layer's input
-// activation fragments (C order) for the dW product of a layer with dims K x N
+// stage dZ (gradient tiles, C order of the layer above: tiles 2m, 2m+1 = the 16-byte fragment of C positions
+// 32 m + 8 h, as bwd_dA consumes them) and the layer's input activation fragments (C order) for the dW product
+// of a layer with dims K x N; rows permuted by sperm16 inside each 16-row block
 template <int K, int N, int TBN>
 __device__ __forceinline__ void stage(uint16_t* S, const v4bf (&dz)[TBN][N / 16], const v8bf (&a)[TBN][K / 32], int w,
                                       int r, int h) {
   uint16_t* SZ = S;
   uint16_t* SA = S + T * (N + PAD);
-  constexpr Swz szw = sswz<N>(), saw = sswz<K>();
-  const int xz = xmask(szw, r), xa = xmask(saw, r);
+  const int rp = sperm16(r);
 #pragma unroll
   for (int tb = 0; tb < TBN; ++tb) {
-    const int rc = 16 * TBN * w + 16 * tb, row = rc + r;
-    const int xzr = xz ^ xmask(szw, rc), xar = xa ^ xmask(saw, rc);
+    const int row = 16 * TBN * w + 16 * tb + rp;
 #pragma unroll
-    for (int kt = 0; kt < N / 16; ++kt) {
-      const int f0 = 32 * (kt >> 1) + 16 * (h & 1) + 8 * (kt & 1) + 4 * (h >> 1);
-      *(v4bf*)(SZ + row * (N + PAD) + 4 * ((f0 >> 2) ^ xzr)) = dz[tb][kt];
-    }
+    for (int m = 0; m < N / 32; ++m) *(v8bf*)(SZ + row * (N + PAD) + 32 * m + 8 * h) = cat_bf(dz[tb][2 * m], dz[tb][2 * m + 1]);
 #pragma unroll
-    for (int s = 0; s < K / 32; ++s) *(v8bf*)(SA + row * (K + PAD) + 4 * ((8 * s + 2 * h) ^ xar)) = a[tb][s];
+    for (int s = 0; s < K / 32; ++s) *(v8bf*)(SA + row * (K + PAD) + 32 * s + 8 * h) = a[tb][s];
   }
 }
 
@@ -299,20 +279,21 @@ __device__ __forceinline__ void dw_phase(v4f (&acc)[NTW * KTW], const uint16_t* 
   const uint16_t* SZ = S;
   const uint16_t* SA = S + T * (N + PAD);
   const int q = r >> 2, p = r & 3;
-  constexpr Swz szw = sswz<N>(), saw = sswz<K>();
-  const int rl = 8 * h + q, xz = xmask(szw, rl), xa = xmask(saw, rl);
+  // example rows 32 ts + 8 h + q (first read) and + 4 (second): inside the 16-row block 16 (h >> 1) they are
+  // rows 8 (h & 1) + q and + 4, physical sperm16() = 8 (h & 1) + 2 q and + 1
+  const int rl = 16 * (h >> 1) + 8 * (h & 1) + 2 * q;
 #pragma unroll
   for (int ts = 0; ts < T / 32; ++ts) {
     v8bf fa[NTW], fb[KTW];
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
-      const int col = 16 * (nt0 + i * ntS) + 4 * p;
-      fa[i] = cat8(tr_read(SZ + soff<N + PAD>(szw, xz, rl, 32 * ts, col)), tr_read(SZ + soff<N + PAD>(szw, xz, rl, 32 * ts + 4, col)));
+      const uint16_t* pa = SZ + (32 * ts + rl) * (N + PAD) + 16 * (nt0 + i * ntS) + 4 * p;
+      fa[i] = cat8(tr_read(pa), tr_read(pa + (N + PAD)));
     }
 #pragma unroll
     for (int j = 0; j < KTW; ++j) {
-      const int col = 16 * (kt0 + j * ktS) + 4 * p;
-      fb[j] = cat8(tr_read(SA + soff<K + PAD>(saw, xa, rl, 32 * ts, col)), tr_read(SA + soff<K + PAD>(saw, xa, rl, 32 * ts + 4, col)));
+      const uint16_t* pb = SA + (32 * ts + rl) * (K + PAD) + 16 * (kt0 + j * ktS) + 4 * p;
+      fb[j] = cat8(tr_read(pb), tr_read(pb + (K + PAD)));
     }
 #pragma unroll
     for (int i = 0; i < NTW; ++i)
@@ -330,6 +311,14 @@ __device__ __forceinline__ void load_ct(int (&ct)[NTW * KTW], int tbase, int nt0
     for (int j = 0; j < KTW; ++j) ct[i * KTW + j] = tmap[tbase + (nt0 + i * ntS) * (K / 16) + kt0 + j * ktS];
 }
 
+// WDC_NT_SLAB (A/B builds only): nontemporal slab stores shorten this kernel by ~1 us but lengthen the reduce
+// that reads the slab by as much (profiles/wd_ab_r2s.txt)
+#ifdef WDC_NT_SLAB
+#define SLAB_STORE(dst, v) __builtin_nontemporal_store((v), &(dst))
+#else
+#define SLAB_STORE(dst, v) ((dst) = (v))
+#endif
+
 template <int NT>
 __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], const int (&ct)[NT], int lane) {
 #pragma unroll
@@ -337,7 +326,7 @@ __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], c
     if (ct[i] < 0) continue;
     float* dst = slab + (size_t)ct[i] * 256 + lane;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dst[e * 64] = acc[i][e];
+    for (int e = 0; e < 4; ++e) SLAB_STORE(dst[e * 64], acc[i][e]);
   }
 }
 
@@ -357,6 +346,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   bool stamp_on = true;
   (void)stamp_on;
   STAMP(0);
+  BSTAMP(0);
 
   {  // stage the bf16 weight image (already in LDS layout): all global loads, then all LDS stores
     constexpr int NCH = LWEND / 8, PER = (NCH + NTHR - 1) / NTHR;
@@ -425,6 +415,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   fetch(blockIdx.x, nu);
 
   STAMP(1);
+  BSTAMP(1);
   for (int it = blockIdx.x; it < niters; it += gridDim.x) {
 #ifdef WDC_STAMPS
     stamp_on = niters > (int)gridDim.x ? it == (int)(blockIdx.x + gridDim.x) : it == (int)blockIdx.x;
@@ -533,13 +524,11 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       // dZ5 has one natural-order tile (N5 = 16): stage it directly (row t: [dl, 0 ... 0])
 #pragma unroll
       for (int tb = 0; tb < TBN; ++tb) {
-        const int row = EPW * w + 16 * tb + r;
-        constexpr Swz saw = sswz<K5>();
-        const int xar = xmask(saw, row);
-        *(v4bf*)(S + row * (N5 + PAD) + 4 * (h ^ xmask(sswz<N5>(), row))) = d5[tb][0];
+        const int row = EPW * w + 16 * tb + sperm16(r);
+        *(v4bf*)(S + row * (N5 + PAD) + 4 * h) = d5[tb][0];
 #pragma unroll
         for (int s = 0; s < K5 / 32; ++s)
-          *(v8bf*)(S + T * (N5 + PAD) + row * (K5 + PAD) + 4 * ((8 * s + 2 * h) ^ xar)) = a4[tb][s];
+          *(v8bf*)(S + T * (N5 + PAD) + row * (K5 + PAD) + 32 * s + 8 * h) = a4[tb][s];
       }
     }
     block_sync_lds();
@@ -644,7 +633,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 #pragma unroll
         for (int i = 0; i < NWAVE; ++i) v += red[NWAVE + i];
       }
-      my[c] = v;
+      SLAB_STORE(my[c], v);
     }
   }
   if (tid == 0 && slab_loss) {
@@ -654,6 +643,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     slab_loss[blockIdx.x] = l;
   }
   STAMP(17);
+  BSTAMP(2);
 }
 
 template <bool TRAIN, int TBN>
@@ -712,6 +702,9 @@ int mifx_wdc_fused(const void* data, long long n_data, long long batch, long lon
 #ifdef WDC_STAMPS
 int mifx_wdc_stamps(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wdc_stamps), sizeof(g_wdc_stamps), 0, hipMemcpyDeviceToHost);
+}
+int mifx_wdc_blk_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wdc_blk), sizeof(g_wdc_blk), 0, hipMemcpyDeviceToHost);
 }
 #endif
 

@@ -705,8 +705,12 @@ __global__ __launch_bounds__(256) void wd_optimizer(
 // full reduction feeding the DP all-reduce.
 constexpr int RQ = 16;               // float4 columns per workgroup
 constexpr int RG = 256 / RQ;         // row groups
-constexpr int RU = 8;                // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
-                                     // 8 x 16 B = the whole 21 MB slab requested in two rounds)
+#ifndef WD_RU
+#define WD_RU 8
+#endif
+constexpr int RU = WD_RU;            // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
+                                     // 8 x 16 B = the whole 21 MB slab requested in two rounds; RU 16, all of
+                                     // it in one round, measured 2 us slower per step: profiles/wd_ab_r2s.txt)
 template <bool OPT>
 __global__ __launch_bounds__(256) void wd_reduce_opt(
     const float4* __restrict__ slab, int G, int stride, float4* __restrict__ out, const int* __restrict__ inv,

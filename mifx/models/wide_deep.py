@@ -315,13 +315,13 @@ def tensors_to_records(dense, ids, label) -> np.ndarray:
 # The chained kernel feeds layer l's MFMA output tiles straight into layer l+1 as its B operand, so layer
 # l+1's k axis is consumed in "C order": inside every 32-block, position 8H + E holds feature
 # 16 (E // 4) + 4 H + E % 4. Its LDS weight image W_l^T [N][K] therefore has natural rows and C-ordered
-# columns; dW tiles come out in the same image coordinates. Rows are padded by CHAIN_PAD elements (the kernel's
-# WPAD) for conflict-free forward reads; CHAIN_WSWZ mirrors wswz<K>() (per-row XOR of 8-byte granules, all zero:
-# see the kernel's WPAD note).
+# columns. Image row n sits at physical row wperm(n) (bit 4 of n flips bit 2) and rows are padded by CHAIN_PAD
+# elements (the kernel's WPAD) -- together conflict-free LDS reads (see the kernel's wperm note). dW tiles come
+# out with C-order k columns and, for layers 1-4, an n axis in "C o C" order: the kernel stages the dZ fragments
+# it holds (C positions of the layer above's k axis) as 16-byte pairs, which applies chain_perm once more.
 CHAIN_PAD = 16
 CHAIN_LW = [int(v) for v in np.cumsum([0] + [n * (k + CHAIN_PAD) for k, n in LAYER_KN])[:-1]]
 CHAIN_LWEND = sum(n * (k + CHAIN_PAD) for k, n in LAYER_KN)  # 33536
-CHAIN_WSWZ = {32: (0,) * 7, 128: (0,) * 7, 96: (0,) * 7, 64: (0,) * 7}
 
 
 def chain_perm(K: int) -> np.ndarray:
@@ -330,11 +330,18 @@ def chain_perm(K: int) -> np.ndarray:
     return 32 * (c // 32) + 16 * ((c % 8) // 4) + 4 * ((c % 32) // 8) + c % 4
 
 
-def _xmask(masks, rows: np.ndarray) -> np.ndarray:
-    x = np.zeros_like(rows)
-    for b, m in enumerate(masks):
-        x ^= np.where((rows >> b) & 1, m, 0)
-    return x
+def chain_wperm(n: np.ndarray) -> np.ndarray:
+    """Physical LDS row of weight-image row n (the kernel's wperm)."""
+    return n ^ (((n >> 4) & 1) << 2)
+
+
+def chain_dw_rows(li: int) -> np.ndarray:
+    """f[j] = natural output feature on row j of layer li's dW tiles."""
+    N = LAYER_KN[li][1]
+    if li == len(LAYER_KN) - 1:
+        return np.arange(N)  # dZ5 is staged in natural order
+    c = chain_perm(N)
+    return c[c]
 
 
 def chain_image_offsets(li: int) -> np.ndarray:
@@ -342,8 +349,7 @@ def chain_image_offsets(li: int) -> np.ndarray:
     K, N = LAYER_KN[li]
     n = np.arange(N)[:, None]
     c = np.arange(K)[None, :]
-    g = (c >> 2) ^ _xmask(CHAIN_WSWZ[K], n)
-    return CHAIN_LW[li] + n * (K + CHAIN_PAD) + 4 * g + (c & 3)
+    return CHAIN_LW[li] + chain_wperm(n) * (K + CHAIN_PAD) + c
 
 
 def chain_image(param) -> np.ndarray:
@@ -361,7 +367,7 @@ def chain_maps(cfg: WideDeepConfig | None = None):
     """Index maps of the chained kernel: (tmap int32 [NTILE], stride, gidx int32 [WTOT+NWIDE],
     mask uint8 [WTOT+NWIDE], wmap int32 [WTOT]).
 
-    tmap: dW tile (image coordinates, id TILE_BASE + nt * K/16 + kt) -> compact slab position (-1: only
+    tmap: dW tile (rows chain_dw_rows, C-order columns; id TILE_BASE + nt * K/16 + kt) -> compact slab position (-1: only
     padding); gidx: canonical parameter -> slab position (tile-native order inside a tile, as wd_fused);
     wmap: canonical DNN parameter -> offset in the bf16 image the optimizer re-emits."""
     cfg = cfg or WideDeepConfig()
@@ -370,7 +376,7 @@ def chain_maps(cfg: WideDeepConfig | None = None):
     tmap = np.full(NTILE, -1, np.int32)
     c = 0
     for li, ((K, N), m) in enumerate(zip(LAYER_KN, masks)):
-        mi = m[:, chain_perm(K)]  # image coordinates
+        mi = m[chain_dw_rows(li)][:, chain_perm(K)]  # dW tile coordinates
         for nt in range(N // 16):
             for kt in range(K // 16):
                 if mi[16 * nt:16 * nt + 16, 16 * kt:16 * kt + 16].any():
@@ -384,9 +390,10 @@ def chain_maps(cfg: WideDeepConfig | None = None):
         cinv = np.argsort(chain_perm(K))  # natural k -> image column
         n = np.arange(N)[:, None]
         col = cinv[None, :].repeat(N, 0)
-        ct = tmap[TILE_BASE[li] + (n // 16) * (K // 16) + col // 16]
-        lane = 16 * ((n % 16) // 4) + col % 16
-        idx = np.where(ct >= 0, ct * 256 + (n % 4) * 64 + lane, 0)
+        j = np.argsort(chain_dw_rows(li))[n]  # natural n -> dW tile row
+        ct = tmap[TILE_BASE[li] + (j // 16) * (K // 16) + col // 16]
+        lane = 16 * ((j % 16) // 4) + col % 16
+        idx = np.where(ct >= 0, ct * 256 + (j % 4) * 64 + lane, 0)
         assert (ct[m] >= 0).all()
         gidx[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = idx.reshape(-1)
         mask[LAYER_OFF[li]:LAYER_OFF[li] + K * N] = m.reshape(-1)

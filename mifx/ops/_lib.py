@@ -26,6 +26,9 @@ def gpu_available() -> bool:
 
 @functools.lru_cache(maxsize=None)
 def load(name: str) -> ctypes.CDLL:
+    override = os.environ.get(f"MIFX_LIB_{name.upper()}")  # A/B of diagnostic / variant builds (tools/)
+    if override:
+        return ctypes.CDLL(override, mode=ctypes.RTLD_GLOBAL)
     path = LIBDIR / f"libmifx_{name}.so"
     if not path.exists():
         if os.environ.get("MIFX_AUTOBUILD", "1") == "1":

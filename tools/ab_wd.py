@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--kernels", default="chain8,chain4,tile", help="chain8 / chain4 (waves) or tile")
     ap.add_argument("--batches", default="65536,131072,40")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps-per-graph", type=int, default=10, help="as bench.py; 1 = launch-bound replays")
     a = ap.parse_args()
     dev = torch.device("cuda")
     data = synthetic_records(1 << 22, device=dev, seed=1)
@@ -31,14 +32,13 @@ def main():
             kw = {"kernel": "tile"} if k == "tile" else {"kernel": "chain", "waves": int(k[5:] or 8)}
             tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=dev, **kw)
             tr.set_data(data)
-            tr.capture()
+            tr.capture(steps_per_graph=a.steps_per_graph)
             trs[k] = tr
         for _ in range(a.rounds):
             for key, tr in trs.items():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                for _ in range(steps):
-                    tr.step()
+                tr.run(steps)
                 torch.cuda.synchronize()
                 us = 1e6 * (time.perf_counter() - t0) / steps
                 res.setdefault(f"B={batch} kernel={key}", []).append(round(us, 2))

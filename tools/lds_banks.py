@@ -256,3 +256,86 @@ def staging_candidates():
 
 if __name__ == "__main__" and __import__("sys").argv[1:] == ["stage"]:
     staging_candidates()
+
+
+class PermLayout(Layout):
+    """row-major image with row stride cols + pad and a physical row permutation perm(row)."""
+
+    def __init__(self, cols, pad, perm):
+        super().__init__(cols, pad)
+        self.perm = perm
+
+    def addr(self, row, col):
+        return super().addr(self.perm(row), col)
+
+
+def wperm(n):
+    return n ^ (((n >> 4) & 1) << 2)
+
+
+def sperm(t):
+    return t ^ (((t >> 3) & 1) << 2)
+
+
+def perm_report():
+    print("== row-permuted layouts (weights: pad 16 + rows 16-31 of each 32-block XOR 4; staging: pad 16 + rows "
+          "8-15 of each 16-block XOR 4)")
+    report("pad 16 / pad 8 (current)", lambda K: Layout(K, 16), lambda c: Layout(c, 8))
+    report("permuted", lambda K: PermLayout(K, 16, wperm), lambda c: PermLayout(c, 16, sperm))
+
+
+if __name__ == "__main__" and __import__("sys").argv[1:] == ["perm"]:
+    perm_report()
+
+
+def sperm2(t):
+    """staging row permutation: inside each 16-row block, row bits (b3 b2 b1 b0) -> (b3 b1 b0 b2), so the 8 rows a
+    32-lane half of a dW transposed read touches (q, 8+q) land on physical rows of one parity."""
+    return (t & ~15) | (t & 8) | ((t & 3) << 1) | ((t >> 2) & 1)
+
+
+def stage_writes_c(LZ, LA, K, N, epw=16):
+    """dZ staged in C order with 16-byte writes (cat of tiles 2m, 2m+1 at C position 32m + 8h)."""
+    outz, outa = [], []
+    for m in range(N // 32):
+        a = [LZ.addr(epw * 0 + (l & 15), 32 * m + 8 * (l >> 4)) for l in range(64)]
+        outz.append(cycles(a, "w128"))
+    for s in range(K // 32):
+        a = [LA.addr(epw * 0 + (l & 15), 32 * s + 8 * (l >> 4)) for l in range(64)]
+        outa.append(cycles(a, "w128"))
+    return outz, outa
+
+
+def perm2_report():
+    wl = lambda K: PermLayout(K, 16, wperm)  # noqa: E731
+    sl = lambda c: PermLayout(c, 8, sperm2)  # noqa: E731
+    tot = defaultdict(lambda: [0, 0])
+    for li, (K, N) in enumerate(LAYERS):
+        f = fwd_read(wl(K), K, N)
+        tot["fwd b128"][0] += sum(f)
+        tot["fwd b128"][1] += 4 * len(f)
+        if li > 0 and N >= 32:
+            d = dA_read(wl(K), K, N)
+            tot["dA tr"][0] += sum(d)
+            tot["dA tr"][1] += 2 * len(d)
+        for cols in (N, K):
+            if cols >= 16:
+                d = dw_read(sl(cols), cols)
+                tot["dW tr"][0] += sum(d)
+                tot["dW tr"][1] += 2 * len(d)
+        if N >= 32:
+            z, a = stage_writes_c(sl(N), sl(K), K, N)
+            tot["stage dZ w128"][0] += sum(z)
+            tot["stage dZ w128"][1] += 8 * len(z)
+            tot["stage A w128"][0] += sum(a)
+            tot["stage A w128"][1] += 8 * len(a)
+        m = mask_read(sl(K), K)
+        tot["mask b64"][0] += sum(m)
+        tot["mask b64"][1] += 2 * len(m)
+    print("== weights pad 16 + wperm; staging pad 8 + sperm2, dZ in C order (16-B writes)")
+    for k, (c, ideal) in tot.items():
+        print(f"   {k:>14}: {c:6d} cycles (ideal {ideal:6d}, x{c / ideal:.2f})")
+
+
+if __name__ == "__main__" and __import__("sys").argv[1:] == ["perm2"]:
+    perm2_report()

@@ -42,3 +42,23 @@ for NW, batch in ((4, 65536), (8, 128), (8, 65536)):
         d = [st[w][i] - st[w][i - 1] for w in range(NW)]
         print(f"  {NAMES[i]:>11}: " + " ".join(f"{x:8d}" for x in d))
     print(f"  iteration (stamp 2 -> 15), wave 0: {st[0][15] - st[0][2]}; kernel (0 -> 17): {st[0][17] - st[0][0]}")
+
+# per-block global clock (100 MHz) of the last launch (the 8-wave B=65536 trainer above): dispatch stagger and
+# block imbalance
+import numpy as np  # noqa: E402
+
+bb = (ctypes.c_ulonglong * (4096 * 3))()
+assert diag.mifx_wdc_blk_stamps(bb) == 0
+a = np.array(bb, dtype=np.int64).reshape(4096, 3)[:tr.grid]
+t0 = a[:, 0].min()
+st, pro, end = (a[:, 0] - t0) / 100.0, (a[:, 1] - a[:, 0]) / 100.0, (a[:, 2] - t0) / 100.0  # us
+q = lambda v: " ".join(f"{x:7.2f}" for x in np.percentile(v, [0, 10, 50, 90, 100]))  # noqa: E731
+print(f"== per-block (grid {tr.grid}), us, percentiles 0/10/50/90/100")
+print(f"  start offset: {q(st)}")
+print(f"  prologue:     {q(pro)}")
+print(f"  duration:     {q(end - st)}")
+print(f"  end offset:   {q(end)}   kernel span {end.max():.2f} us")
+order = np.argsort(st)
+print("  slowest 8 blocks (id, start, dur):", [(int(i), round(float(st[i]), 2), round(float(end[i] - st[i]), 2))
+                                              for i in np.argsort(-(end - st))[:8]])
+print("  first 16 by start:", [int(i) for i in order[:16]])
