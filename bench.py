@@ -62,7 +62,7 @@ def _ranks_agree(tr) -> bool:
     return bool(torch.equal(hi, lo)) and bool(torch.isfinite(chk).all())
 
 
-def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, capture_collective: bool = False,
+def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, dp: str = "xgmi",
                  steps_per_graph: int = 10):
     def build():
         model = WideDeepModel(seed=0)
@@ -80,20 +80,49 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, ca
     tr = build()
     if not (graph and device.type == "cuda"):
         return tr
-    # Multi-rank over RCCL, default: the direct path -- fused fwd/bwd, slab reduce and optimizer launched eagerly
-    # from prebuilt arguments with the flat-gradient ncclAllReduce enqueued between them on the same stream
-    # through torch's communicator (mifx.parallel.rccl_direct); no graph-launch bubbles, no extra stream hops.
-    # --capture-collective captures the all-reduce INTO the step's hipGraph instead. Measured on one MI355X with
-    # the DP code path forced (tools/dp_step_overhead.py, profiles/dp_step_overhead_r2.jsonl).
-    # The captured variant stays opt-in until it has run on a multi-GPU node (only 1-GPU boxes were available
-    # to validate it); its guard: after two replays every rank must hold bit-identical weights, else the
-    # trainer (and its HBM-resident data) is released and a split-phase one is built instead.
-    captured = pg is not None and capture_collective and torch.distributed.get_backend(pg) == "nccl"
-    tr.capture(include_collective=captured, steps_per_graph=steps_per_graph)
-    tr.collective_in_graph = captured
+    if pg is None:
+        tr.capture(steps_per_graph=steps_per_graph)
+        tr.dp_path = None
+        return tr
+    # Multi-rank data parallelism, default "xgmi": the one-shot xGMI gradient exchange (mifx.parallel.xgmi) --
+    # every rank reads its peers' 82 KB local gradients straight from their HBM and sums + applies the optimizer
+    # in one kernel, device-side epoch flags keep the ranks in lock-step, so the whole step (and 10 of them) is
+    # one hipGraph with no host collective. Guard: its setup self-test, then 2 graph replays after which every
+    # rank must hold bit-identical weights with no timed-out wait; otherwise (agreed by all ranks) the trainer is
+    # released and the "direct" path is built: eager launches + ncclAllReduce enqueued on the compute stream
+    # through torch's RCCL communicator (mifx.parallel.rccl_direct). "captured" puts the RCCL all-reduce inside
+    # the step's graph, "split" issues torch's all_reduce between two graphs.
+    if dp == "xgmi":
+        ok = True
+        try:
+            tr.capture(steps_per_graph=steps_per_graph, dp_mode="xgmi")
+            tr.run(2 * max(1, steps_per_graph))
+            torch.cuda.synchronize(device)
+            tr._xg.check()
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            print(f"[bench] xGMI exchange unavailable: {e}", file=sys.stderr, flush=True)
+            ok = False
+        flag = torch.tensor([0.0 if ok else 1.0], device=device)
+        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+        ok = flag.item() == 0.0 and _ranks_agree(tr)
+        if ok:
+            tr.dp_path = "xgmi one-shot exchange (IPC peer reads + epoch flags, whole step in hipGraphs)"
+            return tr
+        print("[bench] xGMI step failed validation on some rank: falling back to direct RCCL", file=sys.stderr,
+              flush=True)
+        if tr._xg is not None:
+            tr.disable_xgmi()
+        del tr
+        torch.cuda.synchronize(device)
+        torch.cuda.empty_cache()
+        tr = build()
+        dp = "direct"
+    captured = dp == "captured" and torch.distributed.get_backend(pg) == "nccl"
+    tr.capture(include_collective=captured, steps_per_graph=steps_per_graph,
+               dp_mode="split" if dp == "split" else "direct")
     tr.dp_path = ("captured-in-graph" if captured else
                   "rccl-direct (eager launches + ncclAllReduce on the compute stream)" if tr._fast is not None else
-                  "split-phase graphs + torch all_reduce") if pg is not None else None
+                  "split-phase graphs + torch all_reduce")
     if captured:
         for _ in range(2):
             tr.step()
@@ -105,8 +134,8 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, ca
             torch.cuda.synchronize(device)
             torch.cuda.empty_cache()
             tr = build()
-            tr.capture(include_collective=False)
-            tr.collective_in_graph = False
+            tr.capture(dp_mode="split")
+            tr.dp_path = "split-phase graphs + torch all_reduce"
     return tr
 
 
@@ -123,9 +152,11 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--steps-per-graph", type=int, default=10,
                     help="consecutive training steps captured in one hipGraph (single rank / captured collective)")
-    ap.add_argument("--capture-collective", action="store_true",
-                    help="multi-rank: capture the RCCL all-reduce inside the step's hipGraph (default: split-phase, "
-                         "eager all-reduce between two graphs)")
+    ap.add_argument("--dp", choices=("xgmi", "direct", "captured", "split"), default="xgmi",
+                    help="multi-rank gradient exchange: xgmi (one-shot peer reads, whole step in hipGraphs; falls "
+                         "back to direct if its validation fails), direct (eager + ncclAllReduce on the compute "
+                         "stream), captured (RCCL all-reduce inside the graph), split (torch all_reduce between "
+                         "two graphs)")
     a = ap.parse_args(argv)
 
     env = mdist.init()
@@ -140,9 +171,8 @@ def main(argv=None) -> int:
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     n = env.world_size
 
-    tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph,
-                      a.capture_collective, a.steps_per_graph)
-    collective_in_graph = bool(getattr(tr, "collective_in_graph", False))
+    tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph, a.dp,
+                      a.steps_per_graph)
     dp_path = getattr(tr, "dp_path", None)
     ranks_agree = _ranks_agree(tr) if (n > 1 and use_cuda) else None  # replicas must hold identical weights
     spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
@@ -152,11 +182,13 @@ def main(argv=None) -> int:
 
     ref = None
     if a.ref_batch:
+        if getattr(tr, "_xg", None) is not None:
+            tr.disable_xgmi()
         del tr
         if use_cuda:
             torch.cuda.synchronize(device)
             torch.cuda.empty_cache()
-        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.capture_collective,
+        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.dp,
                            a.steps_per_graph)
         dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
@@ -184,7 +216,7 @@ def main(argv=None) -> int:
                        "hipgraph": bool(use_cuda and not a.no_graph),
                        "steps_per_graph": spg,
                        "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
-                       "collective_in_graph": collective_in_graph, "dp_allreduce": dp_path,
+                       "dp_exchange": dp_path,
                        "replicas_bit_identical": ranks_agree},
             "final_mean_loss": loss,
             "reference_batch": ref,

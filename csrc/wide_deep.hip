@@ -784,6 +784,168 @@ __global__ __launch_bounds__(256) void wd_reduce_opt(
   if (threadIdx.x == 0) step_ctr[blockIdx.x] = step;
 }
 
+// ---- data parallelism over xGMI: one-shot cross-GPU exchange of the local gradient, no host collective
+// (mifx/parallel/xgmi.py). Two kernels per step after the fused fwd/bwd:
+//   A wd_reduce_xgmi_publish (322 workgroups): workgroup c sums its RQ float4 columns ("chunk c") over the G slab
+//     rows (as wd_reduce_opt, fixed order), stores the chunk into half (epoch & 1) of this rank's IPC-shared
+//     partial buffer with system-scope (write-through) stores, waits for their completion and publishes epoch e
+//     for chunk c into every peer's flag array (uncached memory): sig[c][rank] = e. No waiting.
+//   B wd_xgmi_gather_opt (81 one-wave workgroups, 4 chunks each): waits until all ranks published e for its
+//     chunks (bounded spin: a peer that never arrives sets err, no wave can hang), loads the world partials from
+//     the peers' HBM over xGMI with system-scope loads, sums them in rank order -- identical on every rank, so
+//     the replicas stay bit-identical -- and runs the optimizer on its columns.
+// No cache-wide writeback or invalidate anywhere. The waiting kernel is small on purpose: it never holds the CUs
+// another rank's fused kernel needs (ranks sharing a GPU in tests, or anything else running on the node).
+// Double buffering by epoch parity makes one flag per epoch enough: rank r rewrites half e & 1 of chunk c only in
+// epoch e + 2, after its epoch e + 1 kernel B saw every peer's e + 1 flag for chunk c, which that peer published
+// after its epoch-e kernel B (its reads of chunk c) completed. The W&D gradient is one 82 KB bucket: every GPU
+// reads 7 x 82 KB over 7 point-to-point xGMI links in one round.
+constexpr int XG_MAXW = 8;
+constexpr int XB_THR = 64;               // kernel B: one wave, one float4 column per thread
+constexpr int XB_CHUNKS = XB_THR / RQ;   // chunks per kernel-B workgroup
+struct XgPeers {
+  const float* part[XG_MAXW];  // peer p's [2][stride] partial buffer (p == rank: our own)
+  unsigned int* sig[XG_MAXW];   // peer p's flag array [chunks][XG_MAXW] (uncached)
+};
+
+__device__ __forceinline__ void st_sys(float* p, float v) {
+  __hip_atomic_store((unsigned int*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys(const float* p) {
+  return __uint_as_float(__hip_atomic_load((const unsigned int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+// epoch of the coming exchange: xctr holds the last completed one (per-workgroup slots of kernel B; kernel A
+// reads slot 0, written by kernel B's workgroup 0 of the previous step)
+__global__ __launch_bounds__(256) void wd_reduce_xgmi_publish(const float4* __restrict__ slab, int G, int stride,
+                                                              XgPeers peers, int world, int rank,
+                                                              const long long* __restrict__ xctr) {
+  __shared__ float4 part[RG][RQ];
+  const int S4 = stride / 4;
+  const int lq = threadIdx.x % RQ, r = threadIdx.x / RQ;
+  const int q = blockIdx.x * RQ + lq;
+  const long long e = xctr[0] + 1;
+  float4 acc[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) acc[u] = make_float4(0, 0, 0, 0);
+  if (q < S4) {
+    int g = r;
+    for (; g + (RU - 1) * RG < G; g += RU * RG) {
+      float4 v[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) v[u] = slab[(size_t)(g + u * RG) * S4 + q];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
+    }
+    for (; g < G; g += RG) {
+      const float4 v = slab[(size_t)g * S4 + q];
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+  }
+#pragma unroll
+  for (int h = RU / 2; h >= 1; h /= 2)
+#pragma unroll
+    for (int u = 0; u < h; ++u) {
+      acc[u].x += acc[u + h].x; acc[u].y += acc[u + h].y; acc[u].z += acc[u + h].z; acc[u].w += acc[u + h].w;
+    }
+  part[r][lq] = acc[0];
+  __syncthreads();
+  if (threadIdx.x < RQ && q < S4) {
+    float4 s = part[0][lq];
+#pragma unroll
+    for (int k = 1; k < RG; ++k) {
+      const float4 v = part[k][lq];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float* dst = (float*)peers.part[rank] + (size_t)(e & 1) * stride + 4 * q;
+    st_sys(dst + 0, s.x);
+    st_sys(dst + 1, s.y);
+    st_sys(dst + 2, s.z);
+    st_sys(dst + 3, s.w);
+    __builtin_amdgcn_s_waitcnt(0);  // the chunk's stores acknowledged before the flag below
+  }
+  __syncthreads();
+  if (threadIdx.x < world)
+    __hip_atomic_store(peers.sig[threadIdx.x] + blockIdx.x * XG_MAXW + rank, (unsigned int)e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool OPT>
+__global__ __launch_bounds__(XB_THR) void wd_xgmi_gather_opt(
+    int stride, XgPeers peers, int world, const unsigned int* __restrict__ my_sig, int* __restrict__ err,
+    long long* __restrict__ xctr, float4* __restrict__ out, const int* __restrict__ inv, float* __restrict__ param,
+    float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out, const int* __restrict__ wmap,
+    long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+  const int t = threadIdx.x;
+  const long long e = xctr[blockIdx.x] + 1;  // one wave: every lane reads the slot, no LDS broadcast needed
+  const long long step = OPT ? step_ctr[blockIdx.x] + 1 : 0;
+  const unsigned int ue = (unsigned int)e;
+  const int nchunks = (stride / 4 + RQ - 1) / RQ;
+  {  // lane t waits for flag (chunk XB_CHUNKS * blockIdx.x + t / world, rank t % world)
+    const int c = XB_CHUNKS * blockIdx.x + t / max(world, 1);
+    if (t < XB_CHUNKS * world && c < nchunks) {
+      long long spins = 0;
+      const unsigned int* f = my_sig + c * XG_MAXW + t % world;
+      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ue) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1ll << 26)) {  // seconds: a peer is gone; record it and finish (results are garbage)
+          err[0] = 1;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int S4 = stride / 4;
+  const int q = blockIdx.x * XB_THR + t;
+  if (q < S4) {
+    const size_t off = (size_t)(e & 1) * stride + 4 * q;
+    float v[XG_MAXW][4];
+#pragma unroll
+    for (int p = 0; p < XG_MAXW; ++p)
+      if (p < world) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[p][j] = ld_sys(peers.part[p] + off + j);
+      }
+    float g4[4] = {v[0][0], v[0][1], v[0][2], v[0][3]};
+#pragma unroll
+    for (int p = 1; p < XG_MAXW; ++p)
+      if (p < world) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g4[j] += v[p][j];
+      }
+    if (!OPT) {
+      out[q] = make_float4(g4[0], g4[1], g4[2], g4[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = inv[4 * q + j];
+        if (c < 0) continue;
+        const bool dnn = c < WTOT;
+        float a0 = s0[c], a1 = s1[c];
+        const float w = opt_update(dnn ? hd : hw, param[c], g4[j], a0, a1, step);
+        s0[c] = a0;
+        s1[c] = a1;
+        param[c] = w;
+        if (dnn) wt_out[wmap != nullptr ? wmap[c] : c] = __builtin_bit_cast(uint16_t, (bf16)w);
+      }
+    }
+  }
+  __syncthreads();  // every lane read its slots before lane 0 moves them on
+  if (t == 0) {
+    xctr[blockIdx.x] = e;
+    if (OPT) step_ctr[blockIdx.x] = step;
+  }
+  // keep the slots no workgroup of this grid owns equal to the canonical values
+  if (blockIdx.x == 0)
+    for (int i = gridDim.x + t; i < STEP_SLOTS; i += XB_THR) {
+      xctr[i] = e;
+      if (OPT) step_ctr[i] = step;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -873,6 +1035,50 @@ int mifx_wd_reduce_opt(const float* slab, int G, int stride, float* out, const i
               hyper_wide[6], hyper_wide[7]};
   hipLaunchKernelGGL(wd_reduce_opt<true>, grid, dim3(256), 0, stream, (const float4*)slab, G, stride, nullptr, inv,
                      param, s0, s1, (uint16_t*)wt_out, wmap, step_ctr, hd, hw);
+  return (int)hipGetLastError();
+}
+
+// slab [G, stride] -> local sum -> xGMI exchange over `world` ranks -> optimizer (inv != null) or the plain
+// global sum into out [stride] (inv == null; self-test). Two launches (A publish, B gather). parts / sigs: host
+// arrays of world device pointers (peer buffers opened through IPC; [rank] = our own; parts [2][stride] fp32,
+// sigs [chunks][8] uint32 uncached). xctr: STEP_SLOTS int64 epoch slots (all equal), err: device int set to 1
+// if a peer never published.
+int mifx_wd_xgmi_chunks(int stride) { return (stride / 4 + RQ - 1) / RQ; }
+
+int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* const* parts, void* const* sigs,
+                            int world, int rank, const unsigned int* my_sig, int* err, long long* xctr, float* out,
+                            const int* inv, float* param, float* s0, float* s1, void* wt_out, const int* wmap,
+                            long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
+                            hipStream_t stream) {
+  if (G <= 0 || world < 1 || world > XG_MAXW || rank < 0 || rank >= world || stride <= 0 || stride > STRIDE ||
+      stride % 4 != 0 || my_sig == nullptr || err == nullptr || xctr == nullptr)
+    return -1;
+  XgPeers pe{};
+  for (int p = 0; p < world; ++p) {
+    if (parts[p] == nullptr || sigs[p] == nullptr) return -1;
+    pe.part[p] = (const float*)parts[p];
+    pe.sig[p] = (unsigned int*)sigs[p];
+  }
+  const dim3 ga(mifx_wd_xgmi_chunks(stride)), gb((stride / 4 + XB_THR - 1) / XB_THR);
+  if ((int)gb.x > STEP_SLOTS) return -1;
+  if (inv == nullptr && out == nullptr) return -1;
+  if (inv != nullptr && (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
+                         step_ctr == nullptr))
+    return -1;
+  hipLaunchKernelGGL(wd_reduce_xgmi_publish, ga, dim3(256), 0, stream, (const float4*)slab, G, stride, pe, world, rank,
+                     xctr);
+  if (inv == nullptr) {
+    hipLaunchKernelGGL(wd_xgmi_gather_opt<false>, gb, dim3(XB_THR), 0, stream, stride, pe, world, my_sig, err, xctr,
+                       (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{},
+                       OptHyper{});
+    return (int)hipGetLastError();
+  }
+  OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5], hyper_dnn[6],
+              hyper_dnn[7]};
+  OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+              hyper_wide[6], hyper_wide[7]};
+  hipLaunchKernelGGL(wd_xgmi_gather_opt<true>, gb, dim3(XB_THR), 0, stream, stride, pe, world, my_sig, err, xctr,
+                     nullptr, inv, param, s0, s1, (uint16_t*)wt_out, wmap, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
 

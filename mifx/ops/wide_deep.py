@@ -19,6 +19,9 @@ def _fns():
         "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, I32, VP]),
         "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
         "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
+        "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
+                                                                VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 

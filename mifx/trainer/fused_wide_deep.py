@@ -130,6 +130,7 @@ class FusedWideDeepTrainer:
         self._graphs = None
         self._fast = None
         self._direct = None
+        self._xg = None  # xGMI gradient exchange (enable_xgmi)
         self.graph_multi, self.graph_multi_steps = None, 1
 
     def _weight_image(self) -> torch.Tensor:
@@ -247,9 +248,51 @@ class FusedWideDeepTrainer:
             raise RuntimeError("W&D optimizer launch failed")
 
     def _step_impl(self) -> None:
+        if self._xg is not None:  # data parallel over xGMI: no host collective, graph-capturable
+            self._launch(self.records, self.n_data, self.batch, 0, self.step_ctr, self.slab, self.slab_loss, None,
+                         self.grid, True)
+            self._xg.reduce_apply(self)
+            return
         self._local_grad()
         self._allreduce()
         self._apply()
+
+    # ---------------------------------------------------------------- data parallel over xGMI
+    def enable_xgmi(self) -> None:
+        """Switch the data-parallel step to the one-shot xGMI gradient exchange (mifx.parallel.xgmi): the
+        peers' local gradients are read straight from their HBM and summed with the optimizer in one kernel,
+        so the whole step (all ranks in lock-step through device-side epoch flags) captures into hipGraphs.
+        Runs the exchange self-test first; raises if it fails."""
+        if self.world <= 1:
+            raise ValueError("enable_xgmi needs a process group with more than one rank")
+        if self.kernel != "chain" or not self.fused_update:
+            raise ValueError("the xGMI step needs the chained kernel and the fused update")
+        from ..parallel.xgmi import XgmiExchange
+
+        self.disable_xgmi()
+        xg = XgmiExchange(self.stride, self.pg, self.device)
+        try:
+            xg.selftest()
+        except Exception:
+            xg.close()
+            raise
+        self._xg = xg
+        self.graph, self._graphs, self._fast = None, None, None
+        self.graph_multi, self.graph_multi_steps = None, 1
+
+    def disable_xgmi(self) -> None:
+        if self._xg is not None:
+            self._xg.close()
+            self._xg = None
+            self.graph, self.graph_multi, self.graph_multi_steps = None, None, 1
+
+    @property
+    def dp_exchange(self) -> str | None:
+        if self.world <= 1:
+            return None
+        if self._xg is not None:
+            return "xgmi"
+        return "rccl-direct" if self._fast is not None else "collective"
 
     def step(self) -> None:
         if self.records is None:
@@ -290,6 +333,8 @@ class FusedWideDeepTrainer:
         captures the RCCL all-reduce too -- one graph launch per step (bench.py --capture-collective; opt-in
         until validated on a multi-GPU node). On one MI355X with the DP path forced (tools/dp_step_overhead.py)
         the split-phase step costs 67.4 us vs 51.2 us captured at B=65536 (host 41.6 vs 11.4 us per step)."""
+        if dp_mode == "xgmi" and self.world > 1 and self._xg is None:
+            self.enable_xgmi()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -298,7 +343,7 @@ class FusedWideDeepTrainer:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graph, self._graphs, self._fast = None, None, None
         self.graph_multi, self.graph_multi_steps = None, 1
-        if self.world == 1 or include_collective:
+        if self.world == 1 or include_collective or self._xg is not None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._step_impl()

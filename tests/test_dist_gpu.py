@@ -125,3 +125,56 @@ def test_direct_rccl_dp_step_matches_split_phase():
         assert torch.equal(out[0], out[1])
     finally:
         dist.destroy_process_group()
+
+
+def _xgmi_worker(rank, world, port, out_dir, steps, batch, spg):
+    from mifx.data.synthetic import synthetic_records
+    from mifx.models import wide_deep as wdm
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        recs = synthetic_records(batch * world * steps, device="cpu", seed=11)
+        shard = recs.view(steps, world, batch, 32)[:, rank].reshape(-1, 32).contiguous().cuda()
+        out = {}
+        for mode in ("split", "xgmi"):
+            tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device="cuda:0",
+                                      process_group=dist.group.WORLD)
+            tr.set_data(shard)
+            tr.step()  # one step on the collective path first
+            tr.capture(warmup=1, steps_per_graph=spg, dp_mode=mode)
+            if mode == "xgmi":
+                assert tr.dp_exchange == "xgmi" and tr.graph is not None and tr.graph_multi is not None
+            tr.run(steps - 2)
+            torch.cuda.synchronize()
+            assert tr.steps_done == steps
+            if mode == "xgmi":
+                tr._xg.check()
+                tr.disable_xgmi()
+            out[mode] = tr.param.cpu()
+        torch.save(out, os.path.join(out_dir, f"xgmi{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_dp_step_matches_split_phase(world):
+    """Data parallelism over the one-shot xGMI exchange (IPC-shared HBM partials + epoch flags, csrc/xgmi.hip,
+    wd_xgmi_opt): `world` processes share cuda:0 (the IPC path is the same as across GPUs) and run the step in
+    multi-step hipGraphs with no host collective. Every replica must hold bit-identical weights, equal to the
+    split-phase DP path (graph, all-reduce, graph): bit-exact at 2 ranks (a + b has one order), to fp32 summation
+    order at 4. (Against one process on the global batch both DP paths drift after ~6 steps on this data: FTRL's L1
+    threshold flips wide weights on last-bit differences -- tools/xgmi_probe.py.)"""
+    steps, batch = 8, 512
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_xgmi_worker, args=(world, _free_port(), d, steps, batch, 3), nprocs=world,
+                           start_method="spawn")
+        got = [torch.load(os.path.join(d, f"xgmi{r}.pt"), weights_only=True) for r in range(world)]
+    for g in got[1:]:
+        assert torch.equal(g["xgmi"], got[0]["xgmi"])
+    if world == 2:
+        assert torch.equal(got[0]["xgmi"], got[0]["split"])
+    else:
+        np.testing.assert_allclose(got[0]["xgmi"].numpy(), got[0]["split"].numpy(), rtol=1e-4, atol=2e-6)

@@ -1,7 +1,9 @@
 """Host/GPU cost of the data-parallel W&D step paths on ONE GPU with a 1-rank RCCL group: the split-phase
 step (graph, eager RCCL all-reduce, graph), the direct path bench.py uses at N>1 (eager kernel launches from
 prebuilt arguments + ncclAllReduce on the same stream), and the single graph with the all-reduce captured
-(include_collective=True). The trainer is told world=2 so it takes the DP code path."""
+(include_collective=True), and the xGMI one-shot exchange (its 1-rank exchange still publishes/waits on the
+epoch flag and reads the partial back; whole step in 10-step graphs). The trainer is told world=2 so it takes
+the DP code path."""
 import json
 import os
 import sys
@@ -21,19 +23,19 @@ def run(batch, include_collective, steps=300, dp_mode="split"):
     tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device="cuda", process_group=dist.group.WORLD)
     tr.world = 2  # force the DP path (reduce_full -> all_reduce -> optimizer) on a 1-rank group
     tr.set_data(synthetic_records(1 << 20, device="cuda", seed=1))
-    tr.capture(include_collective=include_collective, dp_mode=dp_mode)
-    for _ in range(20):
-        tr.step()
+    tr.capture(include_collective=include_collective, dp_mode=dp_mode,
+               steps_per_graph=10 if dp_mode == "xgmi" else 1)
+    tr.run(20)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.step()
+    tr.run(steps)
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     t_all = time.perf_counter() - t0
     return {"batch": batch, "captured_collective": include_collective, "dp_mode": dp_mode,
             "host_us_per_step": round(t_host / steps * 1e6, 2),
-            "us_per_step": round(t_all / steps * 1e6, 2), "finite": bool(torch.isfinite(tr.param).all())}
+            "us_per_step": round(t_all / steps * 1e6, 2), "finite": bool(torch.isfinite(tr.param).all()),
+            "xgmi_err": int(tr._xg.err.item()) if tr._xg is not None else None}
 
 
 if __name__ == "__main__":
@@ -47,4 +49,6 @@ if __name__ == "__main__":
         print(json.dumps(run(b, False, dp_mode="direct")), flush=True)
     for b in (65536, 40):
         print(json.dumps(run(b, True)), flush=True)
+    for b in (65536, 40):
+        print(json.dumps(run(b, False, dp_mode="xgmi")), flush=True)
     dist.destroy_process_group()
