@@ -711,34 +711,31 @@ constexpr int RG = 256 / RQ;         // row groups
 constexpr int RU = WD_RU;            // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
                                      // 8 x 16 B = the whole 21 MB slab requested in two rounds; RU 16, all of
                                      // it in one round, measured 2 us slower per step: profiles/wd_ab_r2s.txt)
-template <bool OPT>
-__global__ __launch_bounds__(256) void wd_reduce_opt(
-    const float4* __restrict__ slab, int G, int stride, float4* __restrict__ out, const int* __restrict__ inv,
-    float* __restrict__ param, float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
-    const int* __restrict__ wmap, long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
-  __shared__ float4 part[RG][RQ];
-  __shared__ float gsum[4 * RQ];
-  __shared__ long long s_step;
-  if (OPT && threadIdx.x == 0) s_step = step_ctr[blockIdx.x] + 1;  // slot read and written by thread 0 only
-  const int S4 = stride / 4;
+// Column sums of the slab: float4 column q = blockIdx.x * RQ + threadIdx.x % RQ over rows [0, G), row groups of
+// RG threads, fixed order (deterministic). The full sum is returned to threads threadIdx.x < RQ. (A chunk-major
+// slab layout -- this workgroup's columns one contiguous [G][RQ] block -- measured no faster: profiles/wd_ab_r2s.txt)
+__device__ __forceinline__ float4 slab_column_sum(const float4* __restrict__ slab, int G, int S4,
+                                                  float4 (&part)[RG][RQ]) {
   const int lq = threadIdx.x % RQ, r = threadIdx.x / RQ;
   const int q = blockIdx.x * RQ + lq;
   float4 acc[RU];
 #pragma unroll
   for (int u = 0; u < RU; ++u) acc[u] = make_float4(0, 0, 0, 0);
   if (q < S4) {
+    const float4* base = slab + q;
+    const size_t rs = S4;
     int g = r;
     for (; g + (RU - 1) * RG < G; g += RU * RG) {
       float4 v[RU];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) v[u] = slab[(size_t)(g + u * RG) * S4 + q];
+      for (int u = 0; u < RU; ++u) v[u] = base[(size_t)(g + u * RG) * rs];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
       }
     }
     for (; g < G; g += RG) {
-      const float4 v = slab[(size_t)g * S4 + q];
+      const float4 v = base[(size_t)g * rs];
       acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
     }
   }
@@ -750,13 +747,32 @@ __global__ __launch_bounds__(256) void wd_reduce_opt(
     }
   part[r][lq] = acc[0];
   __syncthreads();
+  float4 s = make_float4(0, 0, 0, 0);
   if (threadIdx.x < RQ) {
-    float4 s = part[0][lq];
+    s = part[0][lq];
 #pragma unroll
     for (int k = 1; k < RG; ++k) {
       const float4 v = part[k][lq];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
+  }
+  return s;
+}
+
+template <bool OPT>
+__global__ __launch_bounds__(256) void wd_reduce_opt(
+    const float4* __restrict__ slab, int G, int stride, float4* __restrict__ out, const int* __restrict__ inv,
+    float* __restrict__ param, float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
+    const int* __restrict__ wmap, long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+  __shared__ float4 part[RG][RQ];
+  __shared__ float gsum[4 * RQ];
+  __shared__ long long s_step;
+  if (OPT && threadIdx.x == 0) s_step = step_ctr[blockIdx.x] + 1;  // slot read and written by thread 0 only
+  const int S4 = stride / 4;
+  const int lq = threadIdx.x % RQ;
+  const int q = blockIdx.x * RQ + lq;
+  const float4 s = slab_column_sum(slab, G, S4, part);
+  if (threadIdx.x < RQ) {
     if (!OPT) {
       if (q < S4) out[q] = s;
     } else {
@@ -782,6 +798,59 @@ __global__ __launch_bounds__(256) void wd_reduce_opt(
     }
   }
   if (threadIdx.x == 0) step_ctr[blockIdx.x] = step;
+}
+
+// Slab-column-order optimizer state (the register-chained trainer): param / s0 / s1 are indexed by slab column and
+// wsc[col] says what the column is (-1 padding, -2 wide weight, >= 0 DNN weight with that bf16 weight-image offset).
+// No indirection: a thread's state is loaded before the slab reduction starts and is in registers when the summed
+// gradient arrives (the canonical-order kernel above must wait for the gradient's inv[] entry, then for param/s0/s1
+// at that index, then for wmap).
+struct ScState {
+  int w;           // wsc entry
+  float p, a0, a1;
+};
+__device__ __forceinline__ ScState sc_load(int gi, int stride, const int* __restrict__ wsc, const float* __restrict__ param,
+                                           const float* __restrict__ s0, const float* __restrict__ s1) {
+  ScState st{-1, 0.f, 0.f, 0.f};
+  if (gi < stride) {
+    st.w = wsc[gi];
+    st.p = param[gi];
+    st.a0 = s0[gi];
+    st.a1 = s1[gi];
+  }
+  return st;
+}
+__device__ __forceinline__ void sc_update(int gi, ScState st, float g, const OptHyper& hd, const OptHyper& hw,
+                                          long long step, float* __restrict__ param, float* __restrict__ s0,
+                                          float* __restrict__ s1, uint16_t* __restrict__ wt_out) {
+  if (st.w == -1) return;
+  const float w = opt_update(st.w >= 0 ? hd : hw, st.p, g, st.a0, st.a1, step);
+  s0[gi] = st.a0;
+  s1[gi] = st.a1;
+  param[gi] = w;
+  if (st.w >= 0) wt_out[st.w] = __builtin_bit_cast(uint16_t, (bf16)w);
+}
+
+__global__ __launch_bounds__(256) void wd_reduce_opt_sc(const float4* __restrict__ slab, int G, int stride,
+                                                        const int* __restrict__ wsc, float* __restrict__ param,
+                                                        float* __restrict__ s0, float* __restrict__ s1,
+                                                        uint16_t* __restrict__ wt_out, long long* __restrict__ step_ctr,
+                                                        OptHyper hd, OptHyper hw) {
+  __shared__ float4 part[RG][RQ];
+  __shared__ float gsum[4 * RQ];
+  __shared__ long long s_step;
+  if (threadIdx.x == 0) s_step = step_ctr[blockIdx.x] + 1;
+  const int gi = blockIdx.x * 4 * RQ + threadIdx.x;
+  ScState st{-1, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 4 * RQ) st = sc_load(gi, stride, wsc, param, s0, s1);  // in flight during the reduction
+  const int lq = threadIdx.x % RQ;
+  const float4 s = slab_column_sum(slab, G, stride / 4, part);
+  if (threadIdx.x < RQ) {
+    gsum[4 * lq + 0] = s.x; gsum[4 * lq + 1] = s.y; gsum[4 * lq + 2] = s.z; gsum[4 * lq + 3] = s.w;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 * RQ) sc_update(gi, st, gsum[threadIdx.x], hd, hw, s_step, param, s0, s1, wt_out);
+  if (threadIdx.x == 0) step_ctr[blockIdx.x] = s_step;
 }
 
 // ---- data parallelism over xGMI: one-shot cross-GPU exchange of the local gradient, no host collective
@@ -822,43 +891,10 @@ __global__ __launch_bounds__(256) void wd_reduce_xgmi_publish(const float4* __re
                                                               const long long* __restrict__ xctr) {
   __shared__ float4 part[RG][RQ];
   const int S4 = stride / 4;
-  const int lq = threadIdx.x % RQ, r = threadIdx.x / RQ;
-  const int q = blockIdx.x * RQ + lq;
+  const int q = blockIdx.x * RQ + threadIdx.x % RQ;
   const long long e = xctr[0] + 1;
-  float4 acc[RU];
-#pragma unroll
-  for (int u = 0; u < RU; ++u) acc[u] = make_float4(0, 0, 0, 0);
-  if (q < S4) {
-    int g = r;
-    for (; g + (RU - 1) * RG < G; g += RU * RG) {
-      float4 v[RU];
-#pragma unroll
-      for (int u = 0; u < RU; ++u) v[u] = slab[(size_t)(g + u * RG) * S4 + q];
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
-      }
-    }
-    for (; g < G; g += RG) {
-      const float4 v = slab[(size_t)g * S4 + q];
-      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
-    }
-  }
-#pragma unroll
-  for (int h = RU / 2; h >= 1; h /= 2)
-#pragma unroll
-    for (int u = 0; u < h; ++u) {
-      acc[u].x += acc[u + h].x; acc[u].y += acc[u + h].y; acc[u].z += acc[u + h].z; acc[u].w += acc[u + h].w;
-    }
-  part[r][lq] = acc[0];
-  __syncthreads();
+  const float4 s = slab_column_sum(slab, G, S4, part);
   if (threadIdx.x < RQ && q < S4) {
-    float4 s = part[0][lq];
-#pragma unroll
-    for (int k = 1; k < RG; ++k) {
-      const float4 v = part[k][lq];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
     float* dst = (float*)peers.part[rank] + (size_t)(e & 1) * stride + 4 * q;
     st_sys(dst + 0, s.x);
     st_sys(dst + 1, s.y);
@@ -875,10 +911,16 @@ __global__ __launch_bounds__(256) void wd_reduce_xgmi_publish(const float4* __re
 template <bool OPT>
 __global__ __launch_bounds__(XB_THR) void wd_xgmi_gather_opt(
     int stride, XgPeers peers, int world, const unsigned int* __restrict__ my_sig, int* __restrict__ err,
-    long long* __restrict__ xctr, float4* __restrict__ out, const int* __restrict__ inv, float* __restrict__ param,
-    float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out, const int* __restrict__ wmap,
+    long long* __restrict__ xctr, float4* __restrict__ out, const int* __restrict__ wsc, float* __restrict__ param,
+    float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
     long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
   const int t = threadIdx.x;
+  const int q0 = blockIdx.x * XB_THR + t;
+  ScState st[4];
+  if (OPT) {  // slab-order optimizer state, in flight during the wait
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[j] = sc_load(4 * q0 + j, stride, wsc, param, s0, s1);
+  }
   const long long e = xctr[blockIdx.x] + 1;  // one wave: every lane reads the slot, no LDS broadcast needed
   const long long step = OPT ? step_ctr[blockIdx.x] + 1 : 0;
   const unsigned int ue = (unsigned int)e;
@@ -920,17 +962,7 @@ __global__ __launch_bounds__(XB_THR) void wd_xgmi_gather_opt(
       out[q] = make_float4(g4[0], g4[1], g4[2], g4[3]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = inv[4 * q + j];
-        if (c < 0) continue;
-        const bool dnn = c < WTOT;
-        float a0 = s0[c], a1 = s1[c];
-        const float w = opt_update(dnn ? hd : hw, param[c], g4[j], a0, a1, step);
-        s0[c] = a0;
-        s1[c] = a1;
-        param[c] = w;
-        if (dnn) wt_out[wmap != nullptr ? wmap[c] : c] = __builtin_bit_cast(uint16_t, (bf16)w);
-      }
+      for (int j = 0; j < 4; ++j) sc_update(4 * q + j, st[j], g4[j], hd, hw, step, param, s0, s1, wt_out);
     }
   }
   __syncthreads();  // every lane read its slots before lane 0 moves them on
@@ -1047,7 +1079,7 @@ int mifx_wd_xgmi_chunks(int stride) { return (stride / 4 + RQ - 1) / RQ; }
 
 int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* const* parts, void* const* sigs,
                             int world, int rank, const unsigned int* my_sig, int* err, long long* xctr, float* out,
-                            const int* inv, float* param, float* s0, float* s1, void* wt_out, const int* wmap,
+                            const int* wsc, float* param, float* s0, float* s1, void* wt_out,
                             long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
                             hipStream_t stream) {
   if (G <= 0 || world < 1 || world > XG_MAXW || rank < 0 || rank >= world || stride <= 0 || stride > STRIDE ||
@@ -1061,16 +1093,15 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
   }
   const dim3 ga(mifx_wd_xgmi_chunks(stride)), gb((stride / 4 + XB_THR - 1) / XB_THR);
   if ((int)gb.x > STEP_SLOTS) return -1;
-  if (inv == nullptr && out == nullptr) return -1;
-  if (inv != nullptr && (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
+  if (wsc == nullptr && out == nullptr) return -1;
+  if (wsc != nullptr && (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
                          step_ctr == nullptr))
     return -1;
   hipLaunchKernelGGL(wd_reduce_xgmi_publish, ga, dim3(256), 0, stream, (const float4*)slab, G, stride, pe, world, rank,
                      xctr);
-  if (inv == nullptr) {
+  if (wsc == nullptr) {  // plain sum into out
     hipLaunchKernelGGL(wd_xgmi_gather_opt<false>, gb, dim3(XB_THR), 0, stream, stride, pe, world, my_sig, err, xctr,
-                       (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{},
-                       OptHyper{});
+                       (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{}, OptHyper{});
     return (int)hipGetLastError();
   }
   OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5], hyper_dnn[6],
@@ -1078,7 +1109,26 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
   OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
               hyper_wide[6], hyper_wide[7]};
   hipLaunchKernelGGL(wd_xgmi_gather_opt<true>, gb, dim3(XB_THR), 0, stream, stride, pe, world, my_sig, err, xctr,
-                     nullptr, inv, param, s0, s1, (uint16_t*)wt_out, wmap, step_ctr, hd, hw);
+                     nullptr, wsc, param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
+  return (int)hipGetLastError();
+}
+
+// slab [G, stride] -> sum -> optimizer on slab-column-order state (param/s0/s1 [stride], wsc [stride]: -1 padding,
+// -2 wide, >= 0 DNN weight-image offset). step_ctr: STEP_SLOTS per-workgroup step slots.
+int mifx_wd_reduce_opt_sc(const float* slab, int G, int stride, const int* wsc, float* param, float* s0, float* s1,
+                          void* wt_out, long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
+                          hipStream_t stream) {
+  if (G <= 0 || stride <= 0 || stride > STRIDE || stride % 4 != 0 || wsc == nullptr || param == nullptr ||
+      s0 == nullptr || s1 == nullptr || wt_out == nullptr || step_ctr == nullptr)
+    return -1;
+  const dim3 grid((stride / 4 + RQ - 1) / RQ);
+  if (grid.x > STEP_SLOTS) return -1;
+  OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5], hyper_dnn[6],
+              hyper_dnn[7]};
+  OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+              hyper_wide[6], hyper_wide[7]};
+  hipLaunchKernelGGL(wd_reduce_opt_sc, grid, dim3(256), 0, stream, (const float4*)slab, G, stride, wsc, param, s0, s1,
+                     (uint16_t*)wt_out, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
 

@@ -19,9 +19,10 @@ def _fns():
         "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, I32, VP]),
         "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
         "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "reduce_opt_sc": sig(lib, "mifx_wd_reduce_opt_sc", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
         "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
         "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
-                                                                VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+                                                                VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -100,6 +101,21 @@ def reduce_apply(slab: torch.Tensor, groups: int, inv: torch.Tensor, param: torc
                               ptr(wt_out), ptr(wmap), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
                               stream_handle(param.device))
     check(rc, "mifx_wd_reduce_opt")
+
+
+def reduce_apply_sc(slab: torch.Tensor, groups: int, wsc: torch.Tensor, param_sc: torch.Tensor, s0_sc: torch.Tensor,
+                    s1_sc: torch.Tensor, wt_out: torch.Tensor, step_ctr: torch.Tensor, hyper_dnn: torch.Tensor,
+                    hyper_wide: torch.Tensor) -> None:
+    """Slab [groups, stride] -> sum -> optimizer on slab-column-order state (csrc/wide_deep.hip wd_reduce_opt_sc)."""
+    stride = slab.shape[-1]
+    for t in (wsc, param_sc, s0_sc, s1_sc):
+        if t.numel() != stride or not t.is_contiguous():
+            raise ValueError("slab-order state must be contiguous [stride]")
+    _check_step_ctr(step_ctr)
+    rc = _fns()["reduce_opt_sc"](ptr(slab), int(groups), stride, ptr(wsc), ptr(param_sc), ptr(s0_sc), ptr(s1_sc),
+                                 ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
+                                 stream_handle(param_sc.device))
+    check(rc, "mifx_wd_reduce_opt_sc")
 
 
 def optimizer(partial: torch.Tensor, nparts: int, gidx: torch.Tensor, mask: torch.Tensor, param: torch.Tensor,

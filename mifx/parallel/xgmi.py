@@ -123,8 +123,8 @@ class XgmiExchange:
         from ..ops import wide_deep as wdk
 
         rc = wdk._fns()["reduce_xgmi_opt"](ptr(tr.slab), int(tr.grid), self.stride, self.parts, self.sigs, self.world,
-                                           self.rank, self.sig, ptr(self.err), ptr(self.xctr), None, ptr(tr.inv),
-                                           ptr(tr.param), ptr(tr.s0), ptr(tr.s1), ptr(tr.wt), ptr(tr.wmap),
+                                           self.rank, self.sig, ptr(self.err), ptr(self.xctr), None, ptr(tr.wsc),
+                                           ptr(tr.param_sc), ptr(tr.s0_sc), ptr(tr.s1_sc), ptr(tr.wt),
                                            ptr(tr.step_ctr), ptr(tr.h_dnn), ptr(tr.h_wide), stream_handle(self.device))
         check(rc, "mifx_wd_reduce_xgmi_opt")
 
@@ -134,8 +134,7 @@ class XgmiExchange:
 
         rc = wdk._fns()["reduce_xgmi_opt"](ptr(slab), int(slab.shape[0]), self.stride, self.parts, self.sigs,
                                            self.world, self.rank, self.sig, ptr(self.err), ptr(self.xctr), ptr(out),
-                                           None, None, None, None, None, None, None, None, None,
-                                           stream_handle(self.device))
+                                           None, None, None, None, None, None, None, None, stream_handle(self.device))
         check(rc, "mifx_wd_reduce_xgmi_opt(sum)")
 
     # ------------------------------------------------------------------ validation

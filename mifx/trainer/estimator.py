@@ -163,8 +163,7 @@ class WideDeepEstimator:
             tr = FusedWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
                                       loss_reduction=self.loss_reduction)
             if getattr(self, "_opt_state", None):
-                tr.s0.copy_(self._opt_state["s0"])
-                tr.s1.copy_(self._opt_state["s1"])
+                tr.set_master_state(s0=self._opt_state["s0"], s1=self._opt_state["s1"])
             tr.set_step(self.global_step)
         else:
             tr = TorchWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,

@@ -101,19 +101,36 @@ class FusedWideDeepTrainer:
         self.tmap = torch.from_numpy(tmap).to(dev)
         self.gidx = torch.from_numpy(gidx).to(dev)
         self.mask = torch.from_numpy(mask).to(dev)
-        self.param = torch.from_numpy(wdm.pack_canonical(self.model)).to(dev)
+        param = torch.from_numpy(wdm.pack_canonical(self.model)).to(dev)
         n = wdm.WTOT + wdm.NWIDE
-        self.s0 = torch.zeros(n, device=dev)
-        self.s1 = torch.zeros(n, device=dev)
+        s0 = torch.zeros(n, device=dev)
+        s1 = torch.zeros(n, device=dev)
         for sl, spec in ((slice(0, wdm.WTOT), self.dnn_opt), (slice(wdm.WTOT, n), self.wide_opt)):
             if spec.kind in ("adagrad", "ftrl"):
-                self.s0[sl] = spec.initial_accumulator_value
-        self.wt = self._weight_image()
+                s0[sl] = spec.initial_accumulator_value
         # inverse of the (bijective on live entries) canonical -> slab-column map, -1 on padding columns
         inv = np.full(self.stride, -1, dtype=np.int32)
         live = np.nonzero(mask)[0]
         inv[gidx[live]] = live.astype(np.int32)
         self.inv = torch.from_numpy(inv).to(dev)
+        # Chained kernel: the master weights and optimizer state live in SLAB-COLUMN order (param_sc / s0_sc /
+        # s1_sc [stride]) so the optimizer kernels index them by the gradient's own column (no inv[] -> state ->
+        # wmap chain of dependent loads; csrc/wide_deep.hip wd_reduce_opt_sc). wsc[col]: -1 padding, -2 wide
+        # weight, >= 0 DNN weight with its bf16 weight-image offset. `param` / `s0` / `s1` are canonical views.
+        self._sc = kernel == "chain"
+        self._gidx_l = self.gidx.long()
+        self._mask_b = self.mask.bool()
+        if self._sc:
+            wsc = np.full(self.stride, -1, dtype=np.int32)
+            dnn_live = live[live < wdm.WTOT]
+            wsc[gidx[dnn_live]] = wmap[dnn_live]
+            wsc[gidx[live[live >= wdm.WTOT]]] = -2
+            self.wsc = torch.from_numpy(wsc).to(dev)
+            self._frozen = tuple(torch.where(self._mask_b, torch.zeros_like(v), v) for v in (param, s0, s1))
+            self.param_sc, self.s0_sc, self.s1_sc = (self._to_sc(v) for v in (param, s0, s1))
+        else:
+            self._param, self._s0, self._s1 = param, s0, s1
+        self.wt = self._weight_image()
         self.fused_update = bool(fused_update)
         # per-optimizer-workgroup step slots (slot 0 = the step; see csrc/wide_deep.hip STEP_SLOTS)
         self.step_ctr = torch.zeros(wdk.STEP_SLOTS, dtype=torch.int64, device=dev)
@@ -133,6 +150,52 @@ class FusedWideDeepTrainer:
         self._xg = None  # xGMI gradient exchange (enable_xgmi)
         self.graph_multi, self.graph_multi_steps = None, 1
 
+    # ---------------------------------------------------------------- master state views
+    def _to_sc(self, v: torch.Tensor) -> torch.Tensor:
+        out = torch.zeros(self.stride, device=self.device)
+        out[self._gidx_l[self._mask_b]] = v.to(self.device)[self._mask_b]
+        return out
+
+    def _canon(self, v_sc: torch.Tensor, frozen: torch.Tensor) -> torch.Tensor:
+        return torch.where(self._mask_b, v_sc[self._gidx_l], frozen)
+
+    @property
+    def param(self) -> torch.Tensor:
+        """fp32 master weights in canonical order [WTOT + NWIDE] (a copy for the chained kernel)."""
+        return self._canon(self.param_sc, self._frozen[0]) if self._sc else self._param
+
+    @property
+    def s0(self) -> torch.Tensor:
+        return self._canon(self.s0_sc, self._frozen[1]) if self._sc else self._s0
+
+    @property
+    def s1(self) -> torch.Tensor:
+        return self._canon(self.s1_sc, self._frozen[2]) if self._sc else self._s1
+
+    def set_master_state(self, param=None, s0=None, s1=None) -> None:
+        """Overwrite weights / optimizer state (canonical order); re-emits the bf16 weight image."""
+        for i, (name, v) in enumerate((("param", param), ("s0", s0), ("s1", s1))):
+            if v is None:
+                continue
+            v = torch.as_tensor(v, dtype=torch.float32).to(self.device)
+            if self._sc:
+                getattr(self, name + "_sc").copy_(self._to_sc(v))
+                fr = list(self._frozen)
+                fr[i] = torch.where(self._mask_b, torch.zeros_like(v), v)
+                self._frozen = tuple(fr)
+            else:
+                getattr(self, "_" + name).copy_(v)
+        if param is not None:
+            self.wt.copy_(self._weight_image())
+
+    @property
+    def wide_weights(self) -> torch.Tensor:
+        """The wide (linear) weights the fused kernel reads, canonical order [NWIDE] (a view)."""
+        if self._sc:
+            w0 = self.stride - wdm.WIDE_PAD
+            return self.param_sc[w0:w0 + wdm.NWIDE]
+        return self._param[wdm.WTOT:]
+
     def _weight_image(self) -> torch.Tensor:
         """bf16 (as int16) weight image the fused kernel stages: canonical order (tile kernel) or the chained
         kernel's C-ordered LDS layout."""
@@ -145,10 +208,10 @@ class FusedWideDeepTrainer:
         if self.kernel == "chain":
             from ..ops import wd_chain as wdc
 
-            wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.param[wdm.WTOT:], slab, slab_loss,
+            wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves)
         else:
-            wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.param[wdm.WTOT:], slab, slab_loss,
+            wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
                       self.stage_dims)
 
@@ -188,14 +251,18 @@ class FusedWideDeepTrainer:
     def _apply(self) -> None:
         if self.fused_update:
             src, groups = (self.slab, self.grid) if self.world == 1 else (self.grad, 1)
-            wdk.reduce_apply(src, groups, self.inv, self.param, self.s0, self.s1, self.wt, self.step_ctr,
-                             self.h_dnn, self.h_wide, self.wmap)
+            if self._sc:
+                wdk.reduce_apply_sc(src, groups, self.wsc, self.param_sc, self.s0_sc, self.s1_sc, self.wt,
+                                    self.step_ctr, self.h_dnn, self.h_wide)
+            else:
+                wdk.reduce_apply(src, groups, self.inv, self._param, self._s0, self._s1, self.wt, self.step_ctr,
+                                 self.h_dnn, self.h_wide, self.wmap)
             return
         if self.world == 1:
             src, nparts = (self.slab, 1) if self.grid == 1 else (self.partial, self.nsplit)
         else:
             src, nparts = self.grad, 1
-        wdk.optimizer(src, nparts, self.gidx, self.mask, self.param, self.s0, self.s1, self.wt, self.step_ctr,
+        wdk.optimizer(src, nparts, self.gidx, self.mask, self._param, self._s0, self._s1, self.wt, self.step_ctr,
                       self.h_dnn, self.h_wide)
 
     def _allreduce(self) -> None:
@@ -222,7 +289,7 @@ class FusedWideDeepTrainer:
         stream = torch.cuda.current_stream(self.device)
         sh = ctypes.c_void_p(stream.cuda_stream)
         fused = (wdc._fns()["fused"], (ptr(self.records), self.n_data, self.batch, 0, ptr(self.step_ctr), ptr(self.wt),
-                                       ptr(self.param[wdm.WTOT:]), ptr(self.slab), ptr(self.slab_loss), None,
+                                       ptr(self.wide_weights), ptr(self.slab), ptr(self.slab_loss), None,
                                        float(self.grad_scale), int(self.grid), 1, ptr(self.tmap), int(self.stride),
                                        int(self.waves), sh))
         ro = wdk._fns()["reduce_opt"]
@@ -230,8 +297,9 @@ class FusedWideDeepTrainer:
                     None, None, None, sh))
         hd = self.h_dnn.contiguous()
         hw = self.h_wide.contiguous()
-        app = (ro, (ptr(self.grad), 1, int(self.stride), None, ptr(self.inv), ptr(self.param), ptr(self.s0),
-                    ptr(self.s1), ptr(self.wt), ptr(self.wmap), ptr(self.step_ctr), ptr(hd), ptr(hw), sh))
+        app = (wdk._fns()["reduce_opt_sc"], (ptr(self.grad), 1, int(self.stride), ptr(self.wsc), ptr(self.param_sc),
+                                             ptr(self.s0_sc), ptr(self.s1_sc), ptr(self.wt), ptr(self.step_ctr),
+                                             ptr(hd), ptr(hw), sh))
         wdk._check_step_ctr(self.step_ctr)
         self._fast = (stream, fused, red, app, hd, hw)
 
@@ -404,8 +472,5 @@ class FusedWideDeepTrainer:
         return {"param": self.param.cpu(), "s0": self.s0.cpu(), "s1": self.s1.cpu(), "step": self.step_ctr[:1].cpu()}
 
     def load_state_dict(self, sd: dict) -> None:
-        self.param.copy_(sd["param"])
-        self.s0.copy_(sd["s0"])
-        self.s1.copy_(sd["s1"])
+        self.set_master_state(sd["param"], sd["s0"], sd["s1"])
         self.set_step(int(sd["step"].reshape(-1)[0]))
-        self.wt.copy_(self._weight_image())

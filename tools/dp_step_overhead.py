@@ -43,6 +43,10 @@ if __name__ == "__main__":
     os.environ.setdefault("MASTER_PORT", "29533")
     dist.init_process_group("nccl", rank=0, world_size=1)
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1:  # e.g. `xgmi` (one mode, B=65536; for kernel traces)
+        print(json.dumps(run(65536, False, dp_mode=sys.argv[1])), flush=True)
+        dist.destroy_process_group()
+        sys.exit(0)
     for b in (65536, 40):
         print(json.dumps(run(b, False, dp_mode="split")), flush=True)
     for b in (65536, 40):
