@@ -28,6 +28,7 @@
 //
 // MIFX_HIPCC_FLAGS: -fno-honor-nans -fno-honor-infinities
 #include <hip/hip_runtime.h>
+#include "xcd.h"
 #include <stdint.h>
 
 namespace {
@@ -336,7 +337,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
                                                      const uint4* __restrict__ wimg, const float* __restrict__ wide,
                                                      float* __restrict__ slab, float* __restrict__ slab_loss,
                                                      float* __restrict__ logits_out, float grad_scale,
-                                                     const int* __restrict__ tmap, int stride) {
+                                                     const int* __restrict__ tmap, int stride,
+                                                     int* __restrict__ xcd_of) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LSEND);
   float* red = wgrad + WIDE_PAD;
@@ -347,6 +349,9 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   (void)stamp_on;
   STAMP(0);
   BSTAMP(0);
+  // the XCD this workgroup's slab row is written from (its L2 holds the row for the XCD-local reduction,
+  // csrc/wide_deep.hip wd_reduce_xcd)
+  if (TRAIN && xcd_of != nullptr && tid == 0) xcd_of[blockIdx.x] = mifx_xcc_id();
 
   {  // stage the bf16 weight image (already in LDS layout): all global loads, then all LDS stores
     constexpr int NCH = LWEND / 8, PER = (NCH + NTHR - 1) / NTHR;
@@ -649,7 +654,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 template <bool TRAIN, int TBN>
 void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
             const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
-            float* logits_out, float grad_scale, const int* tmap, int stride) {
+            float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of) {
   static bool attr_done = false;
   if (!attr_done) {
     (void)hipFuncSetAttribute((const void*)wdc_fused<TRAIN, TBN>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -658,7 +663,7 @@ void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, l
   }
   hipLaunchKernelGGL((wdc_fused<TRAIN, TBN>), grid, dim3(64 * (T / (16 * TBN))), LDS_BYTES, stream, (const uint4*)data,
                      n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out,
-                     grad_scale, tmap, stride);
+                     grad_scale, tmap, stride, xcd_of);
 }
 
 }  // namespace
@@ -677,10 +682,11 @@ int mifx_wdc_constants(int* out, int n) {
 // waves: 4 (4 waves x 32 examples, one wave per SIMD) or 8 (8 waves x 16 examples, two waves per SIMD).
 // (step_ctr[0] * batch) % n_data (or start_fixed when step_ctr is null). wimg: the bf16 weight image in LDS
 // layout (LWEND elements, C-ordered columns, see models.wide_deep.chain_image).
-int mifx_wdc_fused(const void* data, long long n_data, long long batch, long long start_fixed,
-                   const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
-                   float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
-                   int waves, hipStream_t stream) {
+// xcd_of (nullable, >= grid ints): receives the XCD each workgroup ran on (training only).
+int mifx_wdc_fused_x(const void* data, long long n_data, long long batch, long long start_fixed,
+                     const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
+                     float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
+                     int waves, int* xcd_of, hipStream_t stream) {
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
   if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;
@@ -689,14 +695,22 @@ int mifx_wdc_fused(const void* data, long long n_data, long long batch, long lon
   const dim3 g(grid);
   if (train && waves == 4)
     launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride);
+                    grad_scale, tmap, stride, xcd_of);
   else if (train)
     launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride);
+                    grad_scale, tmap, stride, xcd_of);
   else  // eval / predict: the 4-wave shape for either request (forward only, no dW phases to overlap)
     launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                     grad_scale, tmap, stride);
+                     grad_scale, tmap, stride, nullptr);
   return (int)hipGetLastError();
+}
+
+int mifx_wdc_fused(const void* data, long long n_data, long long batch, long long start_fixed,
+                   const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
+                   float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
+                   int waves, hipStream_t stream) {
+  return mifx_wdc_fused_x(data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                          grad_scale, grid, train, tmap, stride, waves, nullptr, stream);
 }
 
 #ifdef WDC_STAMPS

@@ -36,6 +36,7 @@
 // (no NaN canonicalisation v_max before every ReLU; MFMA results in VGPRs instead of
 //  AGPR->VGPR copies feeding the epilogues)
 #include <hip/hip_runtime.h>
+#include "xcd.h"
 #include <stdint.h>
 
 namespace {
@@ -711,6 +712,27 @@ constexpr int RG = 256 / RQ;         // row groups
 constexpr int RU = WD_RU;            // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
                                      // 8 x 16 B = the whole 21 MB slab requested in two rounds; RU 16, all of
                                      // it in one round, measured 2 us slower per step: profiles/wd_ab_r2s.txt)
+// Slab loads of the one-pass reductions. A/B builds only: WD_SLAB_LOAD=1 nontemporal, 2 agent-scope.
+#ifndef WD_SLAB_LOAD
+#define WD_SLAB_LOAD 0
+#endif
+__device__ __forceinline__ float4 slab_load(const float4* p) {
+  if (WD_SLAB_LOAD == 1) {
+    const float* f = (const float*)p;
+    return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1),
+                       __builtin_nontemporal_load(f + 2), __builtin_nontemporal_load(f + 3));
+  }
+  if (WD_SLAB_LOAD == 2) {
+    const unsigned int* u = (const unsigned int*)p;
+    return make_float4(__uint_as_float(__hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                       __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                       __uint_as_float(__hip_atomic_load(u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                       __uint_as_float(__hip_atomic_load(u + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+  }
+  return *p;
+}
+#define SLAB_LOAD(p) slab_load(p)
+
 // Column sums of the slab: float4 column q = blockIdx.x * RQ + threadIdx.x % RQ over rows [0, G), row groups of
 // RG threads, fixed order (deterministic). The full sum is returned to threads threadIdx.x < RQ. (A chunk-major
 // slab layout -- this workgroup's columns one contiguous [G][RQ] block -- measured no faster: profiles/wd_ab_r2s.txt)
@@ -728,14 +750,14 @@ __device__ __forceinline__ float4 slab_column_sum(const float4* __restrict__ sla
     for (; g + (RU - 1) * RG < G; g += RU * RG) {
       float4 v[RU];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) v[u] = base[(size_t)(g + u * RG) * rs];
+      for (int u = 0; u < RU; ++u) v[u] = SLAB_LOAD(base + (size_t)(g + u * RG) * rs);
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
       }
     }
     for (; g < G; g += RG) {
-      const float4 v = base[(size_t)g * rs];
+      const float4 v = SLAB_LOAD(base + (size_t)g * rs);
       acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
     }
   }
@@ -853,6 +875,166 @@ __global__ __launch_bounds__(256) void wd_reduce_opt_sc(const float4* __restrict
   if (threadIdx.x == 0) step_ctr[blockIdx.x] = s_step;
 }
 
+// system-scope (write-through / cache-bypassing) 32-bit stores and loads, for data another XCD or GPU reads
+__device__ __forceinline__ void st_sys(float* p, float v) {
+  __hip_atomic_store((unsigned int*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys(const float* p) {
+  return __uint_as_float(__hip_atomic_load((const unsigned int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+// ---- XCD-local slab reduction + optimizer (the register-chained trainer's step on one GPU).
+// The fused kernel's workgroups write their 82 KB slab rows into the L2 of the XCD they run on (8 XCDs, 4 MB L2
+// each; 32 rows per XCD at grid 256). A one-pass reduction reads every row from every XCD: measured, the fused
+// kernel then runs 29-30 us instead of 23 us (its slab writes pay for the lines the previous reduction pulled
+// across XCDs), whatever cache policy the reduction's loads use (plain, nontemporal or agent-scope:
+// profiles/wd_ab_r2s.txt), and a standalone write + read-back of 21 MB costs 12 us against 3.6 us for re-reading
+// a clean slab (tools/micro/launch_floor.hip). So:
+//   level 1 (wd_reduce_xcd, 8 x 81 workgroups): workgroup (chunk c = blockIdx / 8) sums, for its 256 columns, only
+//     the rows written on ITS OWN XCD (the fused kernel records each workgroup's XCD in xcd_of), ascending -- L2
+//     hits -- into the per-XCD partial part[xcd], and stamps ok[xcd][c] with the epoch;
+//   level 2 (wd_xcd_opt_sc, one thread per column): sums the per-XCD partials and runs the optimizer.
+// Determinism: the dispatcher hands out workgroups round-robin over the XCDs but the starting XCD rotates with
+// launch history, so level 2 adds the partials in the order of each XCD's FIRST row, not of XCD id: the same
+// association for every rotation. Completeness: an XCD holding rows that no level-1 workgroup of a chunk ran on
+// (another placement; XCC ids >= 8) is seen through the epoch stamps and summed from the slab by level 2 itself.
+// (One kernel with a last-arriver finalizer measured slower, 12.9 us vs 5.0 + 6.0: its chain of write-through
+// stores, counter atomic and partial loads is longer than a kernel boundary.)
+constexpr int XMAX = 16;  // XCC_ID range
+constexpr int X1C = 64;   // float4 columns per level-1 workgroup (1 KB of each slab row)
+
+__global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ slab, int G, int stride,
+                                                     const int* __restrict__ xcd_of, float4* __restrict__ part,
+                                                     int* __restrict__ ok, const long long* __restrict__ xep) {
+  __shared__ int rows[256];
+  __shared__ int wcnt[4];
+  __shared__ float4 red[4][X1C];
+  const int x = mifx_xcc_id();
+  const int S4 = stride / 4, nc1 = (S4 + X1C - 1) / X1C;
+  const int c = blockIdx.x / 8;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // ascending list of the rows written on this XCD
+  const bool sel = t < G && xcd_of[t] == x;
+  const unsigned long long m = __ballot(sel);
+  if (lane == 0) wcnt[w] = __popcll(m);
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < w; ++i) base += wcnt[i];
+  if (sel) rows[base + __popcll(m & ((1ull << lane) - 1))] = t;
+  const int n = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+  __syncthreads();
+  if (c >= nc1) return;
+  const int q = c * X1C + lane;
+  float4 a = make_float4(0, 0, 0, 0);
+  if (q < S4) {  // rows w, w + 4, ... of the list, 8 loads in flight (32 rows per XCD at grid 256: one round)
+    constexpr int U = 8;
+    for (int i0 = w; i0 < n; i0 += 4 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + 4 * u;
+        v[u] = i < n ? slab[(size_t)rows[i] * S4 + q] : make_float4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+  }
+  red[w][lane] = a;
+  __syncthreads();
+  if (w == 0 && q < S4) {
+    float4 sm = red[0][lane];
+#pragma unroll
+    for (int k2 = 1; k2 < 4; ++k2) {
+      sm.x += red[k2][lane].x; sm.y += red[k2][lane].y; sm.z += red[k2][lane].z; sm.w += red[k2][lane].w;
+    }
+    part[(size_t)x * S4 + q] = sm;
+  }
+  if (t == 0) ok[x * nc1 + c] = (int)(xep[0] + 1);
+}
+
+// level 2: one thread per slab column; wsc == nullptr: plain sum into out (no optimizer)
+__global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ part, const int* __restrict__ ok,
+                                                     const float* __restrict__ slab, int G, int stride,
+                                                     const int* __restrict__ xcd_of, long long* __restrict__ xep,
+                                                     float* __restrict__ out, const int* __restrict__ wsc,
+                                                     float* __restrict__ param, float* __restrict__ s0,
+                                                     float* __restrict__ s1, uint16_t* __restrict__ wt_out,
+                                                     long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+  __shared__ int first[XMAX];
+  __shared__ int order[XMAX];
+  __shared__ int nord;
+  __shared__ long long s_e, s_step;
+  const int t = threadIdx.x;
+  const bool opt = wsc != nullptr;
+  if (t < XMAX) first[t] = 1 << 30;
+  if (t == 0) {
+    s_e = xep[blockIdx.x] + 1;
+    if (opt) s_step = step_ctr[blockIdx.x] + 1;
+  }
+  const int gi = blockIdx.x * 256 + t;
+  const int S4 = stride / 4, nc1 = (S4 + X1C - 1) / X1C;
+  const int c1 = min(gi, stride - 1) / 4 / X1C;
+  // everything in flight at once: the row XCDs, the 8 stamps and 8 partials of this column, the optimizer state
+  const int xo = t < G ? xcd_of[t] : -1;
+  int okv[8];
+  float pv[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    okv[x] = ok[x * nc1 + c1];
+    pv[x] = gi < stride ? part[(size_t)x * stride + gi] : 0.f;
+  }
+  ScState st{-1, 0.f, 0.f, 0.f};
+  if (opt) st = sc_load(gi, stride, wsc, param, s0, s1);
+  __syncthreads();
+  if (xo >= 0) atomicMin(&first[xo], t);
+  __syncthreads();
+  if (t == 0) {  // XCDs holding rows, by first row (insertion sort of <= 16 LDS values)
+    int k2 = 0;
+    for (int xx = 0; xx < XMAX; ++xx) {
+      if (first[xx] >= (1 << 30)) continue;
+      int j = k2++;
+      while (j > 0 && first[order[j - 1]] > first[xx]) {
+        order[j] = order[j - 1];
+        --j;
+      }
+      order[j] = xx;
+    }
+    nord = k2;
+  }
+  __syncthreads();
+  const int e = (int)s_e;
+  float g = 0.f;
+  if (gi < stride) {
+    for (int k2 = 0; k2 < nord; ++k2) {
+      const int xx = order[k2];
+      float v = 0.f;
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+        if (x == xx) v = pv[x];
+      if (!(xx < 8 && okv[xx & 7] == e)) {  // no level-1 workgroup ran on XCD xx for this chunk: its rows, here
+        v = 0.f;
+        for (int r = 0; r < G; ++r)
+          if (xcd_of[r] == xx) v += slab[(size_t)r * stride + gi];
+      }
+      g += v;
+    }
+    if (!opt) out[gi] = g;
+    else sc_update(gi, st, g, hd, hw, s_step, param, s0, s1, wt_out);
+  }
+  __syncthreads();
+  if (t == 0) {
+    xep[blockIdx.x] = s_e;
+    if (opt) step_ctr[blockIdx.x] = s_step;
+  }
+  if (blockIdx.x == 0)
+    for (int i = gridDim.x + t; i < STEP_SLOTS; i += 256) {
+      xep[i] = s_e;
+      if (opt) step_ctr[i] = s_step;
+    }
+}
+
 // ---- data parallelism over xGMI: one-shot cross-GPU exchange of the local gradient, no host collective
 // (mifx/parallel/xgmi.py). Two kernels per step after the fused fwd/bwd:
 //   A wd_reduce_xgmi_publish (322 workgroups): workgroup c sums its RQ float4 columns ("chunk c") over the G slab
@@ -877,12 +1059,6 @@ struct XgPeers {
   unsigned int* sig[XG_MAXW];   // peer p's flag array [chunks][XG_MAXW] (uncached)
 };
 
-__device__ __forceinline__ void st_sys(float* p, float v) {
-  __hip_atomic_store((unsigned int*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ float ld_sys(const float* p) {
-  return __uint_as_float(__hip_atomic_load((const unsigned int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-}
 
 // epoch of the coming exchange: xctr holds the last completed one (per-workgroup slots of kernel B; kernel A
 // reads slot 0, written by kernel B's workgroup 0 of the previous step)
@@ -1129,6 +1305,39 @@ int mifx_wd_reduce_opt_sc(const float* slab, int G, int stride, const int* wsc, 
               hyper_wide[6], hyper_wide[7]};
   hipLaunchKernelGGL(wd_reduce_opt_sc, grid, dim3(256), 0, stream, (const float4*)slab, G, stride, wsc, param, s0, s1,
                      (uint16_t*)wt_out, step_ctr, hd, hw);
+  return (int)hipGetLastError();
+}
+
+// XCD-local slab reduction [+ optimizer on slab-column-order state] (see wd_reduce_xcd). xcd_of [G] from the fused
+// kernel (mifx_wdc_fused_x); part [16][stride] fp32 and ok [16][chunks] int scratch; xep: STEP_SLOTS int64 epoch
+// slots (all equal). wsc == null: plain sum into out [stride].
+int mifx_wd_xcd_chunks(int stride) { return (stride / 4 + X1C - 1) / X1C; }
+
+int mifx_wd_reduce_xcd_opt(const float* slab, int G, int stride, const int* xcd_of, float* part, int* ok,
+                           long long* xep, float* out, const int* wsc, float* param, float* s0, float* s1,
+                           void* wt_out, long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
+                           hipStream_t stream) {
+  if (G <= 0 || G > 256 || stride <= 0 || stride > STRIDE || stride % 4 != 0 || xcd_of == nullptr ||
+      part == nullptr || ok == nullptr || xep == nullptr)
+    return -1;
+  if (wsc == nullptr && out == nullptr) return -1;
+  if (wsc != nullptr && (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
+                         step_ctr == nullptr))
+    return -1;
+  const int nc1 = mifx_wd_xcd_chunks(stride);
+  const dim3 g2((stride + 255) / 256);
+  if ((int)g2.x > STEP_SLOTS) return -1;
+  OptHyper hd{}, hw{};
+  if (wsc != nullptr) {
+    hd = OptHyper{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                  hyper_dnn[6], hyper_dnn[7]};
+    hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                  hyper_wide[6], hyper_wide[7]};
+  }
+  hipLaunchKernelGGL(wd_reduce_xcd, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, xcd_of,
+                     (float4*)part, ok, xep);
+  hipLaunchKernelGGL(wd_xcd_opt_sc, g2, dim3(256), 0, stream, part, ok, slab, G, stride, xcd_of, xep, out, wsc, param,
+                     s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
 

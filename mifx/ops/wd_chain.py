@@ -17,6 +17,8 @@ def _fns():
         "constants": sig(lib, "mifx_wdc_constants", [VP, I32]),
         "fused": sig(lib, "mifx_wdc_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, I32,
                                              VP]),
+        "fused_x": sig(lib, "mifx_wdc_fused_x", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
+                                                 I32, VP, VP]),
     }
 
 
@@ -31,10 +33,11 @@ def constants() -> dict[str, int]:
 def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
           wimg_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
           logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
-          tmap: torch.Tensor | None = None, waves: int = 8) -> None:
+          tmap: torch.Tensor | None = None, waves: int = 8, xcd_of: torch.Tensor | None = None) -> None:
     """One chained-kernel launch. wimg_bf16: [LWEND] bf16 (or int16) weight image in the kernel's LDS layout
     (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout.
-    waves: 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each)."""
+    waves: 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each). xcd_of: int32
+    [>= grid], receives the XCD each workgroup ran on (for the XCD-local slab reduction)."""
     if waves not in (4, 8):
         raise ValueError("waves must be 4 or 8")
     c = constants()
@@ -52,7 +55,9 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
             raise ValueError("slab_loss must hold >= grid floats")
     elif logits_out is None or logits_out.numel() < batch:
         raise ValueError("eval launch needs logits_out with >= batch floats")
-    rc = _fns()["fused"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide), ptr(slab),
-                         ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train), ptr(tmap), stride,
-                         int(waves), stream_handle(records.device))
+    if xcd_of is not None and (xcd_of.dtype != torch.int32 or xcd_of.numel() < grid):
+        raise ValueError("xcd_of must be int32 [>= grid]")
+    rc = _fns()["fused_x"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
+                           ptr(slab), ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
+                           ptr(tmap), stride, int(waves), ptr(xcd_of), stream_handle(records.device))
     check(rc, "mifx_wdc_fused")

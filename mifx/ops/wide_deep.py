@@ -20,6 +20,9 @@ def _fns():
         "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
         "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
         "reduce_opt_sc": sig(lib, "mifx_wd_reduce_opt_sc", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "xcd_chunks": sig(lib, "mifx_wd_xcd_chunks", [I32]),
+        "reduce_xcd_opt": sig(lib, "mifx_wd_reduce_xcd_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP,
+                                                              VP, VP, VP, VP]),
         "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
         "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
                                                                 VP, VP, VP, VP, VP, VP, VP, VP]),
@@ -116,6 +119,35 @@ def reduce_apply_sc(slab: torch.Tensor, groups: int, wsc: torch.Tensor, param_sc
                                  ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
                                  stream_handle(param_sc.device))
     check(rc, "mifx_wd_reduce_opt_sc")
+
+
+class XcdReduce:
+    """Scratch for the XCD-local two-level slab reduction + optimizer (csrc/wide_deep.hip wd_reduce_xcd /
+    wd_xcd_opt_sc): xcd_of [256] (filled by the chained kernel), per-XCD partials [16, stride], epoch stamps and
+    epoch slots."""
+
+    def __init__(self, stride: int, device):
+        nc1 = _fns()["xcd_chunks"](int(stride))
+        self.stride = int(stride)
+        self.xcd_of = torch.zeros(256, dtype=torch.int32, device=device)
+        self.part = torch.zeros(16 * stride, device=device)
+        self.ok = torch.zeros(16 * nc1, dtype=torch.int32, device=device)
+        self.xep = torch.zeros(STEP_SLOTS, dtype=torch.int64, device=device)
+
+    def _call(self, slab, groups, out, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide):
+        rc = _fns()["reduce_xcd_opt"](ptr(slab), int(groups), self.stride, ptr(self.xcd_of), ptr(self.part),
+                                      ptr(self.ok), ptr(self.xep), ptr(out), ptr(wsc), ptr(param_sc), ptr(s0_sc),
+                                      ptr(s1_sc), ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
+                                      stream_handle(slab.device))
+        check(rc, "mifx_wd_reduce_xcd_opt")
+
+    def apply_sc(self, slab: torch.Tensor, groups: int, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn,
+                 hyper_wide) -> None:
+        _check_step_ctr(step_ctr)
+        self._call(slab, groups, None, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide)
+
+    def sum_into(self, slab: torch.Tensor, groups: int, out: torch.Tensor) -> None:
+        self._call(slab, groups, out, None, None, None, None, None, None, None, None)
 
 
 def optimizer(partial: torch.Tensor, nparts: int, gidx: torch.Tensor, mask: torch.Tensor, param: torch.Tensor,

@@ -16,6 +16,8 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 import torch
 
@@ -135,6 +137,11 @@ class FusedWideDeepTrainer:
         # per-optimizer-workgroup step slots (slot 0 = the step; see csrc/wide_deep.hip STEP_SLOTS)
         self.step_ctr = torch.zeros(wdk.STEP_SLOTS, dtype=torch.int64, device=dev)
         self.slab = torch.empty(self.grid, self.stride, device=dev)
+        # chained kernel, one rank: XCD-local two-level slab reduction (each XCD's slab rows summed where its L2
+        # holds them; csrc/wide_deep.hip wd_reduce_xcd)
+        # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
+        use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
+        self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
         self.partial = torch.empty(self.nsplit, self.stride, device=dev)
@@ -209,7 +216,8 @@ class FusedWideDeepTrainer:
             from ..ops import wd_chain as wdc
 
             wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
-                      logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves)
+                      logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves,
+                      self._xcd.xcd_of if (train and self._xcd is not None and slab is self.slab) else None)
         else:
             wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
@@ -251,7 +259,10 @@ class FusedWideDeepTrainer:
     def _apply(self) -> None:
         if self.fused_update:
             src, groups = (self.slab, self.grid) if self.world == 1 else (self.grad, 1)
-            if self._sc:
+            if self._sc and self.world == 1 and self._xcd is not None:
+                self._xcd.apply_sc(self.slab, self.grid, self.wsc, self.param_sc, self.s0_sc, self.s1_sc, self.wt,
+                                   self.step_ctr, self.h_dnn, self.h_wide)
+            elif self._sc:
                 wdk.reduce_apply_sc(src, groups, self.wsc, self.param_sc, self.s0_sc, self.s1_sc, self.wt,
                                     self.step_ctr, self.h_dnn, self.h_wide)
             else:

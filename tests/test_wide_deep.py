@@ -339,6 +339,50 @@ def test_reduce_full_matches_fp64_sum():
 
 
 @pytest.mark.gpu
+def test_xcd_local_reduce_matches_fp64_sum():
+    """XCD-local two-level slab reduction (wd_reduce_xcd + wd_xcd_opt_sc): whatever XCD labels the rows carry --
+    the real placement, labels no level-1 workgroup can match (XCD 13: the level-2 fallback sums them from the
+    slab), or a random mix -- the result is the full column sum."""
+    from mifx.ops import wide_deep as wdk
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    stride = 20608
+    xr = wdk.XcdReduce(stride, "cuda")
+    for groups in (256, 37, 1):
+        slab = torch.randn(groups, stride, generator=g).mul_(10).cuda()
+        ref = slab.double().sum(0)
+        tol = 1e-6 * slab.abs().sum(0).max().item()
+        for labels in (torch.arange(groups) % 8, torch.full((groups,), 13), torch.randint(0, 16, (groups,),
+                                                                                            generator=g)):
+            xr.xcd_of[:groups] = labels.to(torch.int32).cuda()
+            out = torch.empty(stride, device="cuda")
+            xr.sum_into(slab, groups, out)
+            err = (out.double() - ref).abs().max().item()
+            assert err <= tol, (groups, labels[:4].tolist(), err)
+
+
+@pytest.mark.gpu
+def test_chain_trainer_xcd_reduce_matches_plain_reduce():
+    """The chained trainer's default single-GPU step (XCD-local reduction) against the plain slab reduction."""
+    from mifx.data.synthetic import synthetic_records
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    recs = synthetic_records(1 << 16, device="cuda", seed=9)
+    out = []
+    for xcd in (True, False):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=16384, device="cuda")
+        assert tr._xcd is not None  # grid 128
+        if not xcd:
+            tr._xcd = None
+        tr.set_data(recs)
+        for _ in range(4):
+            tr.step()
+        torch.cuda.synchronize()
+        out.append(tr.param.clone())
+    np.testing.assert_allclose(out[0].cpu().numpy(), out[1].cpu().numpy(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("batch", [40, 16384])
 def test_chain_kernel_step_matches_tile_kernel(batch):
     """The register-chained kernel against the LDS-tile kernel: same data, same init, one fused step each
