@@ -883,6 +883,15 @@ __device__ __forceinline__ float ld_sys(const float* p) {
   return __uint_as_float(__hip_atomic_load((const unsigned int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 
+// xGMI exchange peers (see the data-parallel section below)
+constexpr int XG_MAXW = 8;
+constexpr int XB_THR = 64;               // kernel B: one wave, one float4 column per thread
+constexpr int XB_CHUNKS = XB_THR / RQ;   // chunks per kernel-B workgroup
+struct XgPeers {
+  const float* part[XG_MAXW];  // peer p's [2][stride] partial buffer (p == rank: our own)
+  unsigned int* sig[XG_MAXW];   // peer p's flag array [chunks][XG_MAXW] (uncached)
+};
+
 // ---- XCD-local slab reduction + optimizer (the register-chained trainer's step on one GPU).
 // The fused kernel's workgroups write their 82 KB slab rows into the L2 of the XCD they run on (8 XCDs, 4 MB L2
 // each; 32 rows per XCD at grid 256). A one-pass reduction reads every row from every XCD: measured, the fused
@@ -954,20 +963,30 @@ __global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ 
   if (t == 0) ok[x * nc1 + c] = (int)(xep[0] + 1);
 }
 
-// level 2: one thread per slab column; wsc == nullptr: plain sum into out (no optimizer)
+// level 2: one thread per slab column. MODE 0: plain sum into out; 1: optimizer on slab-order state; 3: xGMI
+// data parallelism -- publish the local sum (store into half (epoch & 1) of this rank's IPC buffer, stamp the 4
+// RQ-float4 chunks' flags in every peer), wait for every peer's stamps on the SAME 4 chunks (bounded spin), load
+// the peers' partials of these 256 columns over xGMI, sum in rank order and run the optimizer. Only same-block
+// workgroups of different ranks wait on each other and a rank's 81 waiting workgroups leave the other CUs free,
+// so ranks sharing one GPU (tests) still make progress.
+template <int MODE>
 __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ part, const int* __restrict__ ok,
                                                      const float* __restrict__ slab, int G, int stride,
                                                      const int* __restrict__ xcd_of, long long* __restrict__ xep,
                                                      float* __restrict__ out, const int* __restrict__ wsc,
                                                      float* __restrict__ param, float* __restrict__ s0,
                                                      float* __restrict__ s1, uint16_t* __restrict__ wt_out,
-                                                     long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+                                                     long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw,
+                                                     XgPeers peers, int world, int rank,
+                                                     long long* __restrict__ xctr,
+                                                     const unsigned int* __restrict__ my_sig,
+                                                     int* __restrict__ err) {
   __shared__ int first[XMAX];
   __shared__ int order[XMAX];
   __shared__ int nord;
   __shared__ long long s_e, s_step;
   const int t = threadIdx.x;
-  const bool opt = wsc != nullptr;
+  constexpr bool opt = MODE == 1 || MODE == 3;
   if (t < XMAX) first[t] = 1 << 30;
   if (t == 0) {
     s_e = xep[blockIdx.x] + 1;
@@ -1020,8 +1039,50 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
       }
       g += v;
     }
-    if (!opt) out[gi] = g;
-    else sc_update(gi, st, g, hd, hw, s_step, param, s0, s1, wt_out);
+    if (MODE == 0) out[gi] = g;
+    if (MODE == 1) sc_update(gi, st, g, hd, hw, s_step, param, s0, s1, wt_out);
+  }
+  if (MODE == 3) {
+    const long long ex = xctr[blockIdx.x] + 1;  // exchange epoch (own slot)
+    const unsigned int uex = (unsigned int)ex;
+    const size_t hoff = (size_t)(ex & 1) * stride;
+    if (gi < stride) {
+      st_sys((float*)peers.part[rank] + hoff + gi, g);
+      __builtin_amdgcn_s_waitcnt(0);  // acknowledged before the chunk flags below
+    }
+    __syncthreads();
+    // the 256 columns are 4 exchange chunks of RQ float4: stamp each in every peer, then wait for every peer's
+    const int nch = (stride / 4 + RQ - 1) / RQ;
+    if (t < 4 * world) {
+      const int cc = 4 * blockIdx.x + t / world, p = t % world;
+      if (cc < nch) {
+        __hip_atomic_store(peers.sig[p] + cc * XG_MAXW + rank, uex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        long long spins = 0;
+        const unsigned int* f = my_sig + cc * XG_MAXW + p;
+        while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - uex) < 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1ll << 26)) {  // seconds: a peer is gone; record it and finish (results are garbage)
+            err[0] = 1;
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (gi < stride) {
+      float pv2[XG_MAXW];
+#pragma unroll
+      for (int p = 0; p < XG_MAXW; ++p) pv2[p] = p < world ? ld_sys(peers.part[p] + hoff + gi) : 0.f;
+      float gs = pv2[0];
+#pragma unroll
+      for (int p = 1; p < XG_MAXW; ++p)
+        if (p < world) gs += pv2[p];
+      sc_update(gi, st, gs, hd, hw, s_step, param, s0, s1, wt_out);
+    }
+    __syncthreads();
+    if (t == 0) xctr[blockIdx.x] = ex;
+    if (blockIdx.x == 0)
+      for (int i = gridDim.x + t; i < STEP_SLOTS; i += 256) xctr[i] = ex;
   }
   __syncthreads();
   if (t == 0) {
@@ -1051,13 +1112,6 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
 // epoch e + 2, after its epoch e + 1 kernel B saw every peer's e + 1 flag for chunk c, which that peer published
 // after its epoch-e kernel B (its reads of chunk c) completed. The W&D gradient is one 82 KB bucket: every GPU
 // reads 7 x 82 KB over 7 point-to-point xGMI links in one round.
-constexpr int XG_MAXW = 8;
-constexpr int XB_THR = 64;               // kernel B: one wave, one float4 column per thread
-constexpr int XB_CHUNKS = XB_THR / RQ;   // chunks per kernel-B workgroup
-struct XgPeers {
-  const float* part[XG_MAXW];  // peer p's [2][stride] partial buffer (p == rank: our own)
-  unsigned int* sig[XG_MAXW];   // peer p's flag array [chunks][XG_MAXW] (uncached)
-};
 
 
 // epoch of the coming exchange: xctr holds the last completed one (per-workgroup slots of kernel B; kernel A
@@ -1257,7 +1311,7 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
                             int world, int rank, const unsigned int* my_sig, int* err, long long* xctr, float* out,
                             const int* wsc, float* param, float* s0, float* s1, void* wt_out,
                             long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
-                            hipStream_t stream) {
+                            const int* xcd_of, float* xpart, int* xok, long long* xep, hipStream_t stream) {
   if (G <= 0 || world < 1 || world > XG_MAXW || rank < 0 || rank >= world || stride <= 0 || stride > STRIDE ||
       stride % 4 != 0 || my_sig == nullptr || err == nullptr || xctr == nullptr)
     return -1;
@@ -1273,6 +1327,21 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
   if (wsc != nullptr && (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
                          step_ctr == nullptr))
     return -1;
+  if (wsc != nullptr && xcd_of != nullptr && xpart != nullptr && xok != nullptr && xep != nullptr && G <= 256) {
+    // XCD-local level 1, then level 2 publishes, waits, gathers and applies the optimizer (wd_xcd_opt_sc<3>)
+    const int nc1 = (stride / 4 + X1C - 1) / X1C;
+    const dim3 g2((stride + 255) / 256);
+    if ((int)g2.x != (int)gb.x) return -1;  // both paths keep the same number of xctr slots
+    OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                hyper_dnn[6], hyper_dnn[7]};
+    OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                hyper_wide[6], hyper_wide[7]};
+    hipLaunchKernelGGL(wd_reduce_xcd, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, xcd_of,
+                       (float4*)xpart, xok, xep);
+    hipLaunchKernelGGL(wd_xcd_opt_sc<3>, g2, dim3(256), 0, stream, xpart, xok, slab, G, stride, xcd_of, xep, nullptr,
+                       wsc, param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, pe, world, rank, xctr, my_sig, err);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(wd_reduce_xgmi_publish, ga, dim3(256), 0, stream, (const float4*)slab, G, stride, pe, world, rank,
                      xctr);
   if (wsc == nullptr) {  // plain sum into out
@@ -1336,8 +1405,12 @@ int mifx_wd_reduce_xcd_opt(const float* slab, int G, int stride, const int* xcd_
   }
   hipLaunchKernelGGL(wd_reduce_xcd, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, xcd_of,
                      (float4*)part, ok, xep);
-  hipLaunchKernelGGL(wd_xcd_opt_sc, g2, dim3(256), 0, stream, part, ok, slab, G, stride, xcd_of, xep, out, wsc, param,
-                     s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
+  if (wsc == nullptr)
+    hipLaunchKernelGGL(wd_xcd_opt_sc<0>, g2, dim3(256), 0, stream, part, ok, slab, G, stride, xcd_of, xep, out, wsc,
+                       param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, XgPeers{}, 0, 0, nullptr, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL(wd_xcd_opt_sc<1>, g2, dim3(256), 0, stream, part, ok, slab, G, stride, xcd_of, xep, out, wsc,
+                       param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, XgPeers{}, 0, 0, nullptr, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 

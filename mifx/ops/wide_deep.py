@@ -25,7 +25,7 @@ def _fns():
                                                               VP, VP, VP, VP]),
         "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
         "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
-                                                                VP, VP, VP, VP, VP, VP, VP, VP]),
+                                                                VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 

@@ -119,13 +119,18 @@ class XgmiExchange:
 
     # ------------------------------------------------------------------ step (stream ordered)
     def reduce_apply(self, tr) -> None:
-        """Slab reduction + exchange + optimizer of FusedWideDeepTrainer `tr` (one kernel)."""
+        """Slab reduction + exchange + optimizer of FusedWideDeepTrainer `tr`: local sum (XCD-local when the trainer
+        has the XcdReduce scratch and the kernel recorded workgroup XCDs) published to the peers, then gather +
+        optimizer."""
         from ..ops import wide_deep as wdk
 
+        xr = getattr(tr, "_xcd", None)
+        xa = (ptr(xr.xcd_of), ptr(xr.part), ptr(xr.ok), ptr(xr.xep)) if xr is not None else (None,) * 4
         rc = wdk._fns()["reduce_xgmi_opt"](ptr(tr.slab), int(tr.grid), self.stride, self.parts, self.sigs, self.world,
                                            self.rank, self.sig, ptr(self.err), ptr(self.xctr), None, ptr(tr.wsc),
                                            ptr(tr.param_sc), ptr(tr.s0_sc), ptr(tr.s1_sc), ptr(tr.wt),
-                                           ptr(tr.step_ctr), ptr(tr.h_dnn), ptr(tr.h_wide), stream_handle(self.device))
+                                           ptr(tr.step_ctr), ptr(tr.h_dnn), ptr(tr.h_wide), *xa,
+                                           stream_handle(self.device))
         check(rc, "mifx_wd_reduce_xgmi_opt")
 
     def sum_into(self, slab: torch.Tensor, out: torch.Tensor) -> None:
@@ -134,7 +139,8 @@ class XgmiExchange:
 
         rc = wdk._fns()["reduce_xgmi_opt"](ptr(slab), int(slab.shape[0]), self.stride, self.parts, self.sigs,
                                            self.world, self.rank, self.sig, ptr(self.err), ptr(self.xctr), ptr(out),
-                                           None, None, None, None, None, None, None, None, stream_handle(self.device))
+                                           None, None, None, None, None, None, None, None, None, None, None, None,
+                                           stream_handle(self.device))
         check(rc, "mifx_wd_reduce_xgmi_opt(sum)")
 
     # ------------------------------------------------------------------ validation

@@ -159,22 +159,23 @@ def _xgmi_worker(rank, world, port, out_dir, steps, batch, spg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_xgmi_dp_step_matches_split_phase(world):
+@pytest.mark.parametrize("world,batch", [(2, 512), (4, 512), (2, 8192)])
+def test_xgmi_dp_step_matches_split_phase(world, batch):
     """Data parallelism over the one-shot xGMI exchange (IPC-shared HBM partials + epoch flags, csrc/xgmi.hip,
     wd_xgmi_opt): `world` processes share cuda:0 (the IPC path is the same as across GPUs) and run the step in
     multi-step hipGraphs with no host collective. Every replica must hold bit-identical weights, equal to the
     split-phase DP path (graph, all-reduce, graph): bit-exact at 2 ranks (a + b has one order), to fp32 summation
-    order at 4. (Against one process on the global batch both DP paths drift after ~6 steps on this data: FTRL's L1
+    order at 4. Batch 8192 (grid 64) takes the XCD-local local sum (wd_reduce_xcd + publish), 512 the one-pass one.
+    (Against one process on the global batch both DP paths drift after ~6 steps on this data: FTRL's L1
     threshold flips wide weights on last-bit differences -- tools/xgmi_probe.py.)"""
-    steps, batch = 8, 512
+    steps = 8
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_xgmi_worker, args=(world, _free_port(), d, steps, batch, 3), nprocs=world,
                            start_method="spawn")
         got = [torch.load(os.path.join(d, f"xgmi{r}.pt"), weights_only=True) for r in range(world)]
     for g in got[1:]:
         assert torch.equal(g["xgmi"], got[0]["xgmi"])
-    if world == 2:
+    if world == 2 and batch < 8192:
         assert torch.equal(got[0]["xgmi"], got[0]["split"])
-    else:
+    else:  # 4 ranks / XCD-local local sums: same math, other fp32 association
         np.testing.assert_allclose(got[0]["xgmi"].numpy(), got[0]["split"].numpy(), rtol=1e-4, atol=2e-6)
