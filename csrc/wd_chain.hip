@@ -36,6 +36,7 @@ namespace {
 typedef __bf16 bf16;
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -96,14 +97,30 @@ __device__ __forceinline__ v8bf ld8(const uint16_t* p) { return *(const v8bf*)p;
 __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// Packed-bf16 activation math: 2 values per 32-bit lane op instead of a compare/select or max per value.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned int cvt_pk(float lo, float hi) {  // v_cvt_pk_bf16_f32 (round to nearest even)
+  return __builtin_bit_cast(unsigned int, (v2bf){(bf16)lo, (bf16)hi});
+}
+// relu on two packed bf16: as signed 16-bit integers negative bf16 values (and -0) are negative, non-negative ones
+// order like their floats, so max(x, 0) in int16 is relu(x) (= relu before rounding: rounding keeps the sign)
+__device__ __forceinline__ unsigned int relu_pk(unsigned int x) {
+  return __builtin_bit_cast(unsigned int, __builtin_elementwise_max(__builtin_bit_cast(s16x2, x), (s16x2){0, 0}));
+}
+// zero the bf16 halves of g whose activation half in a is zero (a >= 0 after relu): g * min(a, 1) in u16
+// (asm: written as u16 vector math the compiler turns it back into a compare + select per half)
+__device__ __forceinline__ unsigned int mask_pk(unsigned int g, unsigned int a) {
+  unsigned int m, r;
+  // the (1, 1) operand from a register: a packed op's inline constant only fills the low half
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(a), "v"(0x00010001u));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(g), "v"(m));
+  return r;
+}
 __device__ __forceinline__ v8bf pack_relu(v4f a, v4f b) {
-  v8bf o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    o[i] = (bf16)fmaxf(a[i], 0.f);
-    o[4 + i] = (bf16)fmaxf(b[i], 0.f);
-  }
-  return o;
+  const unsigned int u[4] = {relu_pk(cvt_pk(a[0], a[1])), relu_pk(cvt_pk(a[2], a[3])), relu_pk(cvt_pk(b[0], b[1])),
+                             relu_pk(cvt_pk(b[2], b[3]))};
+  return __builtin_bit_cast(v8bf, u);
 }
 __device__ __forceinline__ v4bf to_bf4(v4f a) {
   v4bf o;
@@ -244,12 +261,9 @@ __device__ __forceinline__ void mask_grad(const v4f (&g)[TBN][K / 16], const uin
     for (int kt = 0; kt < K / 16; ++kt) {
       const int row = 16 * TBN * w + 16 * tb + rp;
       const uint2 m = *(const uint2*)(SA + row * (K + PAD) + 16 * kt + 4 * h);
-      v4bf o;
-      o[0] = (bf16)((m.x & 0xffffu) ? g[tb][kt][0] : 0.f);
-      o[1] = (bf16)((m.x >> 16) ? g[tb][kt][1] : 0.f);
-      o[2] = (bf16)((m.y & 0xffffu) ? g[tb][kt][2] : 0.f);
-      o[3] = (bf16)((m.y >> 16) ? g[tb][kt][3] : 0.f);
-      dz[tb][kt] = o;
+      const unsigned int u[2] = {mask_pk(cvt_pk(g[tb][kt][0], g[tb][kt][1]), m.x),
+                                 mask_pk(cvt_pk(g[tb][kt][2], g[tb][kt][3]), m.y)};
+      dz[tb][kt] = __builtin_bit_cast(v4bf, u);
     }
 }
 
@@ -536,11 +550,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
           *(v8bf*)(S + T * (N5 + PAD) + row * (K5 + PAD) + 32 * s + 8 * h) = a4[tb][s];
       }
     }
-    block_sync_lds();
-    STAMP(6);
-    if (l5) dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w & 3, 0, r, h);
     v4bf dz4[TBN][K5 / 16];
-    {
+    {  // dA4 (VALU) + mask: own rows only, before the barrier (see layer 4)
       v4f g[TBN][K5 / 16];
 #pragma unroll
       for (int kt = 0; kt < K5 / 16; ++kt) {
@@ -555,13 +566,15 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       mask_grad<K5, TBN>(g, S + T * (N5 + PAD), w, r, h, dz4);
     }
     block_sync_lds();
+    STAMP(6);
+    if (l5) dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w & 3, 0, r, h);
+    block_sync_lds();
 
     // ---- layer 4
     STAMP(7);
     stage<K4, N4, TBN>(S, dz4, a3, w, r, h);
-    block_sync_lds();
-    STAMP(8);
-    dw_phase<K4, N4, 1, O4K>(acc4, S, n4, 0, k4, 1, r, h);
+    // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
+    // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
     v4bf dz3[TBN][K4 / 16];
     {
       v4f g[TBN][K4 / 16];
@@ -569,13 +582,15 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       mask_grad<K4, TBN>(g, S + T * (N4 + PAD), w, r, h, dz3);
     }
     block_sync_lds();
+    STAMP(8);
+    dw_phase<K4, N4, 1, O4K>(acc4, S, n4, 0, k4, 1, r, h);
+    block_sync_lds();
 
     // ---- layer 3
     STAMP(9);
     stage<K3, N3, TBN>(S, dz3, a2, w, r, h);
-    block_sync_lds();
-    STAMP(10);
-    dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
+    // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
+    // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
     v4bf dz2[TBN][K3 / 16];
     {
       v4f g[TBN][K3 / 16];
@@ -583,19 +598,24 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       mask_grad<K3, TBN>(g, S + T * (N3 + PAD), w, r, h, dz2);
     }
     block_sync_lds();
+    STAMP(10);
+    dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
+    block_sync_lds();
 
     // ---- layer 2
     STAMP(11);
     stage<K2, N2, TBN>(S, dz2, a1, w, r, h);
-    block_sync_lds();
-    STAMP(12);
-    dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
+    // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
+    // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
     v4bf dz1[TBN][K2 / 16];
     {
       v4f g[TBN][K2 / 16];
       bwd_dA<K2, N2, TBN>(lds + LW2, dz2, g, r, h);
       mask_grad<K2, TBN>(g, S + T * (N2 + PAD), w, r, h, dz1);
     }
+    block_sync_lds();
+    STAMP(12);
+    dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
     block_sync_lds();
 
     // ---- layer 1
