@@ -161,7 +161,10 @@ def main(argv=None) -> int:
 
     env = mdist.init()
     use_cuda = torch.cuda.is_available()
-    device = torch.device("cuda", env.local_rank) if use_cuda else torch.device("cpu")
+    # MIFX_SHARED_GPU=1 (rehearsal of the multi-rank flow on a 1-GPU box, with MIFX_DIST_BACKEND=gloo): every
+    # rank on cuda:0 -- functional only, the timings of ranks sharing a GPU mean nothing
+    shared = os.environ.get("MIFX_SHARED_GPU") == "1"
+    device = torch.device("cuda", 0 if shared else env.local_rank) if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
     else:  # CPU dev fallback: keep it quick
@@ -192,7 +195,10 @@ def main(argv=None) -> int:
                            a.steps_per_graph)
         dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
-               "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps}
+               "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps,
+               "dp_exchange": getattr(tr2, "dp_path", None)}
+        if getattr(tr2, "_xg", None) is not None:
+            tr2.disable_xgmi()
 
     if env.is_main:
         out = {

@@ -36,8 +36,8 @@ def init(backend: str | None = None, timeout_s: int = 600) -> DistEnv:
     if dist.is_initialized():
         env.backend = dist.get_backend()
         return env
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # MIFX_DIST_BACKEND: rehearsal override (e.g. gloo ranks sharing one GPU)
+        backend = os.environ.get("MIFX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if backend == "nccl":
