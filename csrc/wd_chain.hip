@@ -440,6 +440,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     stamp_on = niters > (int)gridDim.x ? it == (int)(blockIdx.x + gridDim.x) : it == (int)blockIdx.x;
 #endif
     STAMP(2);
+    const bool last = it + (int)gridDim.x >= niters;  // this workgroup's final iteration: dW tiles are final
+    float* my_slab = TRAIN ? slab + (size_t)blockIdx.x * stride : nullptr;
     uint4 u[TBN][2];
 #pragma unroll
     for (int tb = 0; tb < TBN; ++tb) {
@@ -568,6 +570,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(6);
     if (l5) dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w & 3, 0, r, h);
+    if (last) store_tiles<1>(my_slab, acc5, ct5, lane);
     block_sync_lds();
 
     // ---- layer 4
@@ -584,6 +587,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(8);
     dw_phase<K4, N4, 1, O4K>(acc4, S, n4, 0, k4, 1, r, h);
+    if (last) store_tiles<O4K>(my_slab, acc4, ct4, lane);
     block_sync_lds();
 
     // ---- layer 3
@@ -600,6 +604,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(10);
     dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
+    if (last) store_tiles<O3K>(my_slab, acc3, ct3, lane);
     block_sync_lds();
 
     // ---- layer 2
@@ -616,6 +621,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(12);
     dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
+    if (last) store_tiles<O2N * O2K>(my_slab, acc2, ct2, lane);
     block_sync_lds();
 
     // ---- layer 1
@@ -624,6 +630,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(14);
     dw_phase<K1, N1, O1N, 1>(acc1, S, n1, 1, 0, 0, r, h);
+    if (last) store_tiles<O1N>(my_slab, acc1, ct1, lane);
     STAMP(15);
   }
 #ifdef WDC_STAMPS
@@ -641,14 +648,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     red[w] = loss_sum;
     red[NWAVE + w] = dl_sum;
   }
-  if (TRAIN) {
-    float* my = slab + (size_t)blockIdx.x * stride;
-    store_tiles<O1N>(my, acc1, ct1, lane);
-    store_tiles<O2N * O2K>(my, acc2, ct2, lane);
-    store_tiles<O3K>(my, acc3, ct3, lane);
-    store_tiles<O4K>(my, acc4, ct4, lane);
-    store_tiles<1>(my, acc5, ct5, lane);
-  }
+  // (the dW tiles went out in the last iteration, each right after its layer's dW phase: their stores drain
+  // under the remaining layers' compute instead of here)
   __syncthreads();
   if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD);
