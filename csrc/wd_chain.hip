@@ -367,14 +367,18 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   // csrc/wide_deep.hip wd_reduce_xcd)
   if (TRAIN && xcd_of != nullptr && tid == 0) xcd_of[blockIdx.x] = mifx_xcc_id();
 
-  {  // stage the bf16 weight image (already in LDS layout): all global loads, then all LDS stores
+  {  // stage the bf16 weight image (already in LDS layout) with direct-to-LDS loads: no VGPR round trip, no
+     // ds_write transfer cycles. Wave w's lanes fill 16-byte chunks i * NTHR + 64 w + lane; the last wave's
+     // lanes past the image end re-read its last chunk and land in the staging area, written before any read.
     constexpr int NCH = LWEND / 8, PER = (NCH + NTHR - 1) / NTHR;
-    uint4 v[PER];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = wimg[min(tid + i * NTHR, NCH - 1)];
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-      if (tid + i * NTHR < NCH) *(uint4*)(lds + (tid + i * NTHR) * 8) = v[i];
+    for (int i = 0; i < PER; ++i) {
+      const int c0 = i * NTHR + 64 * w;  // wave-uniform
+      if (c0 < NCH)
+        __builtin_amdgcn_global_load_lds((const void*)(wimg + min(c0 + lane, NCH - 1)),
+                                         (__attribute__((address_space(3))) void*)(lds + c0 * 8), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (TRAIN)
     for (int c = tid; c < WIDE_PAD; c += NTHR) wgrad[c] = 0.f;
