@@ -326,13 +326,6 @@ __device__ __forceinline__ void load_ct(int (&ct)[NTW * KTW], int tbase, int nt0
     for (int j = 0; j < KTW; ++j) ct[i * KTW + j] = tmap[tbase + (nt0 + i * ntS) * (K / 16) + kt0 + j * ktS];
 }
 
-// WDC_NT_SLAB (A/B builds only): nontemporal slab stores shorten this kernel by ~1 us but lengthen the reduce
-// that reads the slab by as much (profiles/wd_ab_r2s.txt)
-#ifdef WDC_NT_SLAB
-#define SLAB_STORE(dst, v) __builtin_nontemporal_store((v), &(dst))
-#else
-#define SLAB_STORE(dst, v) ((dst) = (v))
-#endif
 
 template <int NT>
 __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], const int (&ct)[NT], int lane) {
@@ -341,7 +334,7 @@ __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], c
     if (ct[i] < 0) continue;
     float* dst = slab + (size_t)ct[i] * 256 + lane;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) SLAB_STORE(dst[e * 64], acc[i][e]);
+    for (int e = 0; e < 4; ++e) dst[e * 64] = acc[i][e];
   }
 }
 
@@ -663,7 +656,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 #pragma unroll
         for (int i = 0; i < NWAVE; ++i) v += red[NWAVE + i];
       }
-      SLAB_STORE(my[c], v);
+      my[c] = v;
     }
   }
   if (tid == 0 && slab_loss) {

@@ -706,32 +706,9 @@ __global__ __launch_bounds__(256) void wd_optimizer(
 // full reduction feeding the DP all-reduce.
 constexpr int RQ = 16;               // float4 columns per workgroup
 constexpr int RG = 256 / RQ;         // row groups
-#ifndef WD_RU
-#define WD_RU 8
-#endif
-constexpr int RU = WD_RU;            // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
+constexpr int RU = 8;            // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
                                      // 8 x 16 B = the whole 21 MB slab requested in two rounds; RU 16, all of
                                      // it in one round, measured 2 us slower per step: profiles/wd_ab_r2s.txt)
-// Slab loads of the one-pass reductions. A/B builds only: WD_SLAB_LOAD=1 nontemporal, 2 agent-scope.
-#ifndef WD_SLAB_LOAD
-#define WD_SLAB_LOAD 0
-#endif
-__device__ __forceinline__ float4 slab_load(const float4* p) {
-  if (WD_SLAB_LOAD == 1) {
-    const float* f = (const float*)p;
-    return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1),
-                       __builtin_nontemporal_load(f + 2), __builtin_nontemporal_load(f + 3));
-  }
-  if (WD_SLAB_LOAD == 2) {
-    const unsigned int* u = (const unsigned int*)p;
-    return make_float4(__uint_as_float(__hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                       __uint_as_float(__hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                       __uint_as_float(__hip_atomic_load(u + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                       __uint_as_float(__hip_atomic_load(u + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-  }
-  return *p;
-}
-#define SLAB_LOAD(p) slab_load(p)
 
 // Column sums of the slab: float4 column q = blockIdx.x * RQ + threadIdx.x % RQ over rows [0, G), row groups of
 // RG threads, fixed order (deterministic). The full sum is returned to threads threadIdx.x < RQ. (A chunk-major
@@ -750,14 +727,14 @@ __device__ __forceinline__ float4 slab_column_sum(const float4* __restrict__ sla
     for (; g + (RU - 1) * RG < G; g += RU * RG) {
       float4 v[RU];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) v[u] = SLAB_LOAD(base + (size_t)(g + u * RG) * rs);
+      for (int u = 0; u < RU; ++u) v[u] = base[(size_t)(g + u * RG) * rs];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
       }
     }
     for (; g < G; g += RG) {
-      const float4 v = SLAB_LOAD(base + (size_t)g * rs);
+      const float4 v = base[(size_t)g * rs];
       acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
     }
   }
