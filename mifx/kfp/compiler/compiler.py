@@ -273,7 +273,7 @@ class Compiler:
 
     def _compile(self, pipeline_func) -> dict:
         spec = inspect.getfullargspec(pipeline_func)
-        meta = _extract_pipeline_metadata(pipeline_func, validate=_config.TYPE_CHECK)
+        meta = _extract_pipeline_metadata(pipeline_func, validate=_config.type_check_enabled())
         pname = sanitize_k8s_name(meta.name)
         args_list = []
         for arg in spec.args:
@@ -310,12 +310,11 @@ class Compiler:
         return self._create_pipeline_workflow(with_defaults, p, p.conf.op_transformers)
 
     def compile_to_workflow(self, pipeline_func, type_check: bool = True) -> dict:
-        old = _config.TYPE_CHECK
+        old = _config.set_type_check(type_check)
         try:
-            _config.TYPE_CHECK = type_check
             return self._compile(pipeline_func)
         finally:
-            _config.TYPE_CHECK = old
+            _config.set_type_check(old)
 
     def compile(self, pipeline_func, package_path: str, type_check: bool = True) -> None:
         wf = self.compile_to_workflow(pipeline_func, type_check)

@@ -47,6 +47,8 @@ def load_component(filename=None, url=None, text=None):
 
 def load_component_from_url(url: str):
     """Fetch component.yaml over HTTP(S) (or file://) and create a task factory."""
+    if url is None:
+        raise TypeError("url must not be None")
     if url.startswith("file://"):
         return load_component_from_file(url[len("file://"):])
     import requests
@@ -59,6 +61,8 @@ def load_component_from_url(url: str):
 
 
 def load_component_from_file(filename: str):
+    if filename is None:
+        raise TypeError("filename must not be None")
     if filename.endswith(".zip"):
         with zipfile.ZipFile(filename) as z:
             with z.open("component.yaml") as f:
@@ -69,7 +73,7 @@ def load_component_from_file(filename: str):
 
 def load_component_from_text(text: str):
     if text is None:
-        raise TypeError
+        raise TypeError("text must not be None")
     return _create_task_factory_from_component_text(text, None)
 
 
@@ -110,7 +114,7 @@ def _create_task_factory_from_component_spec(component_spec: ComponentSpec, comp
                      if v is not None}
         for key, val in list(arguments.items()):
             if isinstance(val, PipelineParam):
-                if _config.TYPE_CHECK:
+                if _config.type_check_enabled():
                     spec = next(i for i in inputs if i.name == key)
                     if val.param_type is not None and not check_types(val.param_type.to_dict_or_str(),
                                                                       "" if spec.type is None else spec.type):

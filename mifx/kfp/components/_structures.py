@@ -11,6 +11,7 @@ from collections import OrderedDict
 from typing import Any, Dict, List, Mapping, Optional, Union
 
 from .modelbase import ModelBase
+from .structures.kubernetes import v1 as k8s_v1
 
 PrimitiveTypes = Union[str, int, float, bool]
 PrimitiveTypesIncludingNone = Optional[PrimitiveTypes]
@@ -250,14 +251,19 @@ class ComponentReference(ModelBase):
 
 class TaskSpec(ModelBase):
     _serialized_names = {"component_ref": "componentRef", "is_enabled": "isEnabled",
-                         "execution_options": "executionOptions"}
+                         "execution_options": "executionOptions", "k8s_container_options": "k8sContainerOptions",
+                         "k8s_pod_options": "k8sPodOptions"}
 
     def __init__(self, component_ref: ComponentReference, arguments: Optional[Mapping[str, ArgumentType]] = None,
-                 is_enabled: Optional[PredicateType] = None, execution_options: Optional[ExecutionOptionsSpec] = None):
+                 is_enabled: Optional[PredicateType] = None, execution_options: Optional[ExecutionOptionsSpec] = None,
+                 k8s_container_options: Optional[k8s_v1.Container] = None,
+                 k8s_pod_options: Optional[k8s_v1.PodArgoSubset] = None):
         self.component_ref = component_ref
         self.arguments = arguments
         self.is_enabled = is_enabled
         self.execution_options = execution_options
+        self.k8s_container_options = k8s_container_options
+        self.k8s_pod_options = k8s_pod_options
 
 
 class GraphSpec(ModelBase):

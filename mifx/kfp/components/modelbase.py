@@ -75,6 +75,45 @@ def parse_object_from_struct_based_on_type(struct: Any, typ) -> Any:
     raise TypeError(f"cannot parse {struct!r} as {typ}")
 
 
+def _verify(obj, typ) -> None:
+    """Checks an already-constructed object (not a wire struct) against a type hint."""
+    if typ is Any or typ is inspect.Parameter.empty:
+        return
+    if typ is None or typ is _NONE:
+        if obj is not None:
+            raise TypeError(f"expected None, got {type(obj).__name__}")
+        return
+    if isinstance(typ, type) and issubclass(typ, ModelBase):
+        if not isinstance(obj, typ):
+            raise TypeError(f"expected {typ.__name__}, got {type(obj).__name__}")
+        return
+    origin = _origin(typ)
+    args = getattr(typ, "__args__", ()) or ()
+    if origin is Union:
+        for member in args:
+            try:
+                _verify(obj, member)
+                return
+            except TypeError:
+                continue
+        raise TypeError(f"{obj!r} matches none of {args}")
+    if origin in (list, List, typing.Sequence, collections.abc.Sequence):
+        if not isinstance(obj, list):
+            raise TypeError(f"expected list, got {type(obj).__name__}")
+        for x in obj:
+            _verify(x, args[0] if args else Any)
+        return
+    if origin in (dict, Dict, Mapping, typing.Mapping, collections.abc.Mapping):
+        if not isinstance(obj, dict):
+            raise TypeError(f"expected dict, got {type(obj).__name__}")
+        kt, vt = (args + (Any, Any))[:2] if args else (Any, Any)
+        for k, v in obj.items():
+            _verify(k, kt)
+            _verify(v, vt)
+        return
+    parse_object_from_struct_based_on_type(obj, typ)
+
+
 def convert_object_to_struct(obj, serialized_names: dict | None = None):
     if isinstance(obj, ModelBase):
         return obj.to_dict()
@@ -88,11 +127,29 @@ def convert_object_to_struct(obj, serialized_names: dict | None = None):
 class ModelBase:
     _serialized_names: dict = {}
 
+    def __init__(self, args: dict | None = None):
+        """Subclasses call `super().__init__(locals())`: every argument is checked against the
+        subclass constructor's type hints (TypeError on mismatch) and stored as a field."""
+        if args is None:
+            return
+        _, hints = self._signature()
+        fields = {k: v for k, v in args.items() if k != "self" and not k.startswith("_")}
+        for k, v in fields.items():
+            t = hints.get(k)
+            if t is None:
+                continue
+            try:
+                _verify(v, t)
+            except (TypeError, ValueError, KeyError, AttributeError) as e:
+                raise TypeError(f'Argument for {k} is not compatible with type "{t}": {e}') from None
+        self.__dict__.update(fields)
+
     @classmethod
     def _signature(cls):
         sig = inspect.signature(cls.__init__)
         try:
-            hints = typing.get_type_hints(cls.__init__, globalns=vars(__import__(cls.__module__, fromlist=["*"])))
+            hints = typing.get_type_hints(cls.__init__, globalns=vars(__import__(cls.__module__, fromlist=["*"])),
+                                          localns={cls.__name__: cls})
         except Exception:  # noqa: BLE001 - fall back to raw annotations
             hints = {}
         params = [p for p in sig.parameters.values() if p.name != "self" and p.kind in
@@ -125,6 +182,10 @@ class ModelBase:
         for p in params:
             v = getattr(self, p.name, None)
             if v is None:
+                continue
+            # scalars equal to the constructor default are omitted (reference modelbase.py:178-200)
+            if not isinstance(v, (ModelBase, list, dict)) and p.default is not inspect.Parameter.empty \
+                    and type(v) is type(p.default) and v == p.default:
                 continue
             out[self._serialized_names.get(p.name, p.name)] = convert_object_to_struct(v)
         return out

@@ -22,18 +22,19 @@ class ArtifactLocation:
             access_key_secret=_dict_to_secret(access_key_secret), secret_key_secret=_dict_to_secret(secret_key_secret)))
 
     @staticmethod
-    def create_artifact_for_s3(artifact_location, name: str, path: str, key: str) -> V1alpha1Artifact:
+    def create_artifact_for_s3(artifact_location, name: str, path: str, key: str, **kwargs) -> V1alpha1Artifact:
         if isinstance(artifact_location, dict):  # already converted to JSON by param substitution
             s3 = artifact_location.get("s3")
             if not s3:
-                return V1alpha1Artifact(name=name, path=path)
+                return V1alpha1Artifact(name=name, path=path, **kwargs)
             s3 = V1alpha1S3Artifact(bucket=s3.get("bucket"), endpoint=s3.get("endpoint"), insecure=s3.get("insecure"),
-                                    region=s3.get("region"), access_key_secret=s3.get("accessKeySecret"),
-                                    secret_key_secret=s3.get("secretKeySecret"))
+                                    region=s3.get("region"),
+                                    access_key_secret=_dict_to_secret(s3.get("accessKeySecret")),
+                                    secret_key_secret=_dict_to_secret(s3.get("secretKeySecret")))
         elif not artifact_location or not getattr(artifact_location, "s3", None):
-            return V1alpha1Artifact(name=name, path=path)
+            return V1alpha1Artifact(name=name, path=path, **kwargs)
         else:
             s3 = artifact_location.s3
         return V1alpha1Artifact(name=name, path=path, s3=V1alpha1S3Artifact(
             bucket=s3.bucket, endpoint=s3.endpoint, insecure=s3.insecure, region=s3.region,
-            access_key_secret=s3.access_key_secret, secret_key_secret=s3.secret_key_secret, key=key))
+            access_key_secret=s3.access_key_secret, secret_key_secret=s3.secret_key_secret, key=key), **kwargs)

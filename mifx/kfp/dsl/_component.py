@@ -34,7 +34,7 @@ def component(func):
     def _component(*args, **kwargs):
         from .. import _config
 
-        if not _config.TYPE_CHECK:
+        if not _config.type_check_enabled():
             op = func(*args, **kwargs)
             op._set_metadata(_extract_component_metadata(func))
             return op

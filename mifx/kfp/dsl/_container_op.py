@@ -345,6 +345,31 @@ class ContainerOp(BaseOp):
     def container(self) -> Container:
         return self._container
 
+    # deprecated property proxies onto the container (reference `_container_op.py:51-83`: image, env_variables)
+    def _deprecated(self, prop: str, target: str):
+        warnings.warn(f"`dsl.ContainerOp.{prop}` will be removed in future releases. "
+                      f"Use `dsl.ContainerOp.container.{target}` instead.", PendingDeprecationWarning, stacklevel=3)
+
+    @property
+    def image(self):
+        self._deprecated("image", "image")
+        return self._container.image
+
+    @image.setter
+    def image(self, value):
+        self._deprecated("image", "image")
+        self._container.image = value
+
+    @property
+    def env_variables(self):
+        self._deprecated("env_variables", "env")
+        return self._container.env
+
+    @env_variables.setter
+    def env_variables(self, value):
+        self._deprecated("env_variables", "env")
+        self._container.env = value
+
     def _set_metadata(self, metadata: ComponentMeta):
         if not isinstance(metadata, ComponentMeta):
             raise ValueError("_set_metadata is expecting ComponentMeta.")

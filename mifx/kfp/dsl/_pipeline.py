@@ -21,7 +21,7 @@ def pipeline(name: str | None = None, description: str | None = None):
             func._pipeline_description = description
         from .. import _config
 
-        if _config.TYPE_CHECK:
+        if _config.type_check_enabled():
             func._pipeline_meta = _extract_pipeline_metadata(func, validate=False)
         from . import _pipeline as me
 

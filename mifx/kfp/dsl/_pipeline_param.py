@@ -129,4 +129,6 @@ class PipelineParam:
         return hash((self.op_name, self.name))
 
     def ignore_type(self):
+        """Drops the type so type checking passes for this argument (chainable)."""
         self.param_type = TypeMeta()
+        return self

@@ -22,6 +22,7 @@ import re
 import subprocess
 import threading
 import time
+import hashlib
 import uuid
 from dataclasses import dataclass, field
 
@@ -276,6 +277,8 @@ class LocalWorkflowExecutor:
 
     def _exec_container(self, tmpl: dict, scope: dict, display: str, node: NodeStatus) -> dict:
         pod = re.sub(r"[^A-Za-z0-9_.-]+", "_", display) + f"-{node.attempts}"
+        if len(pod) > 120:  # deep recursion grows the display path past the file-name limit: keep it unique
+            pod = pod[:48] + "-" + hashlib.sha1(pod.encode()).hexdigest()[:16] + pod[-48:]
         scope = dict(scope, **{"pod.name": pod})
         c = _substitute(tmpl["container"], scope)
         sandbox = os.path.join(self.run_dir, "steps", pod)

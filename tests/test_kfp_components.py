@@ -5,6 +5,7 @@ as a subprocess with outputs redirected to a temp dir), `test_components.py` (co
 loading, placeholders), `tests/dsl/*` (ops, params). Execution of compiled workflows has no
 reference counterpart (the reference relies on an Argo cluster); here it runs on the host."""
 import json
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -356,3 +357,32 @@ def test_pipelines_api_server_with_rest_client(tmp_path):
     finally:
         server.should_exit = True
         th.join(timeout=10)
+
+
+def test_local_executor_deep_recursion_keeps_step_dirs_short(tmp_path):
+    """A graph component recursing 12 levels: the nested display path outgrows the file-name limit,
+    so step sandboxes are named by a bounded prefix/digest/suffix (executor._exec_container)."""
+    from mifx.kfp import compiler, dsl
+    from mifx.kfp.local import LocalWorkflowExecutor
+
+    def dec_op(n):
+        return dsl.ContainerOp(name="decrement-counter-step", image="python:3.10-alpine", command=["sh", "-c"],
+                               arguments=['python3 -c "import sys; print(int(sys.argv[1]) - 1)" $0 | tee $1', n,
+                                          "/tmp/output"], file_outputs={"output": "/tmp/output"})
+
+    @dsl.graph_component
+    def count_down(n):
+        nxt = dec_op(n)
+        with dsl.Condition(nxt.output > 0):
+            count_down(nxt.output)
+
+    @dsl.pipeline(name="deep recursion")
+    def deep(start=12):
+        count_down(start)
+
+    wf = compiler.Compiler().compile_to_workflow(deep)
+    st = LocalWorkflowExecutor(wf, str(tmp_path), {"start": "12"}, timeout=300).run()
+    assert st["phase"] == "Succeeded", st
+    steps = os.listdir(tmp_path / "steps")
+    assert len([s for s in steps if "decrement" in s]) == 12
+    assert max(len(s) for s in steps) <= 120
