@@ -107,17 +107,31 @@ class DPOptimizer:
         return loss
 
 
-def make_optimizer_class(kind: str):
-    """DP counterpart of an optimizer kind ('sgd', 'adagrad', 'adam') — the reference's
-    `make_optimizer_class(tf.train.XOptimizer)`."""
+def make_optimizer_class(kind):
+    """DP counterpart of an optimizer — the reference's `make_optimizer_class(tf.train.XOptimizer)`
+    (`dp_optimizer.py:25-94`): `kind` is an optimizer name ('sgd', 'adagrad', 'adam', 'ftrl') or any
+    `torch.optim.Optimizer` subclass (constructed as `cls(params, lr=learning_rate, **kw)`)."""
+    if isinstance(kind, type) and issubclass(kind, torch.optim.Optimizer):
+        def build(params, lr, **kw):
+            return kind(params, lr=lr, **kw)
+
+        label = kind.__name__
+    elif isinstance(kind, str):
+        def build(params, lr, **kw):
+            return make_optimizer(kind, params, lr, **kw)
+
+        label = kind.capitalize()
+    else:
+        raise TypeError(f"make_optimizer_class expects an optimizer name or torch.optim.Optimizer subclass, got "
+                        f"{kind!r}")
 
     class _DP(DPOptimizer):
         def __init__(self, l2_norm_clip, noise_multiplier, num_microbatches, params, learning_rate, seed=None,
                      **kw):
-            super().__init__(make_optimizer(kind, params, learning_rate, **kw), l2_norm_clip, noise_multiplier,
-                             num_microbatches, seed)
+            super().__init__(build(params, learning_rate, **kw), l2_norm_clip, noise_multiplier, num_microbatches,
+                             seed)
 
-    _DP.__name__ = f"DP{kind.capitalize()}Optimizer"
+    _DP.__name__ = _DP.__qualname__ = f"DP{label}Optimizer"
     return _DP
 
 

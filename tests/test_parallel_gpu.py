@@ -1,0 +1,126 @@
+"""Tensor- and data-parallel trainers on the GPU, multi-rank on one device.
+
+RCCL refuses two ranks on one GPU, so these rehearse the 8-GPU runs (BASELINE configs 4 and 5) with 2 processes
+sharing cuda:0 over gloo: every kernel of the step (fused attention, bias+dropout+residual+LayerNorm, flat AdamW,
+hipBLASLt GEMMs; MIOpen convs + fused BN/ReLU + the bucketed all-reduce engine) runs as it does on the node, only
+the collectives go through host memory.
+
+* BERT TP=2 (Megatron column/row-parallel layers, counter-based dropout on): the replicated parameters must stay
+  bit-identical across the TP ranks (per-rank RNG streams would let them drift) and the loss curve must
+  match the TP=1 trainer on the same batch.
+* ResNet-50 DP=2, both ranks fed the same batch: the averaged gradient equals each rank's own, so the replicas'
+  parameters must be bit-identical and track the single-process trainer (BN running statistics are per-replica
+  buffers; MIOpen's convolutions are not bit-reproducible across processes, so those only agree closely).
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+_BERT = dict(vocab_size=4096, hidden=128, heads=4, layers=2, intermediate=256, max_position=64, dropout=0.1)
+_BERT_STEPS = 4
+
+
+def _bert_run(world: int, rank: int, out: str) -> None:
+    from mifx.models.bert import BertConfig, gather_full_state
+    from mifx.parallel.tensor_parallel import TPGroup
+    from mifx.trainer.bert_trainer import BertTrainer
+
+    torch.manual_seed(100 + rank)  # per-rank default generators differ: masks must not depend on them
+    tp = TPGroup(dist.group.WORLD if world > 1 else None)
+    tr = BertTrainer(BertConfig.tiny(**_BERT), batch=8, seq=64, device="cuda:0", tp=tp, lr=1e-3, graph=False)
+    losses = [float(tr.step()) for _ in range(_BERT_STEPS)]
+    torch.cuda.synchronize()
+    repl = {n: p.detach().float().cpu() for n, p in tr.model.named_parameters()
+            if not any(s in n for s in ("qkv.", "ffn_in.", "word.")) and not n.endswith(("attn_out.weight",
+                                                                                        "ffn_out.weight"))}
+    full = {k: v.float().cpu() for k, v in gather_full_state(tr.model).items()} if world > 1 or rank == 0 else None
+    torch.save({"losses": losses, "repl": repl, "full": full}, f"{out}.{world}.{rank}")
+
+
+def _bert_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _bert_run(world, rank, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bert_tp2_on_gpu_matches_tp1_and_keeps_replicas_identical():
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "bert")
+        mp.start_processes(_bert_worker, args=(2, _port(), out), nprocs=2, start_method="spawn")
+        mp.start_processes(_bert_worker, args=(1, _port(), out), nprocs=1, start_method="spawn")
+        r0, r1 = (torch.load(f"{out}.2.{r}", weights_only=True) for r in range(2))
+        one = torch.load(f"{out}.1.0", weights_only=True)
+    assert r0["repl"].keys() == r1["repl"].keys() and len(r0["repl"]) > 10
+    for n in r0["repl"]:
+        assert torch.equal(r0["repl"][n], r1["repl"][n]), f"replicated {n} drifted across TP ranks"
+    assert r0["losses"] == r1["losses"]
+    # TP=2 sums the row-parallel partial products in another order than TP=1: bf16-level differences only
+    for a, b in zip(r0["losses"], one["losses"]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r0["losses"], one["losses"])
+    for k, v in one["full"].items():
+        w = r0["full"][k]
+        assert w.shape == v.shape, k
+        assert torch.allclose(w, v, rtol=5e-2, atol=5e-3), (k, (w - v).abs().max().item())
+
+
+_RES_STEPS = 3
+
+
+def _resnet_run(world: int, rank: int, out: str) -> None:
+    from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
+
+    imgs, labels = synthetic_imagenet(64, size=72, classes=10, seed=0)  # same data on every rank
+    tr = ResNetTrainer(4, "cuda:0", imgs, labels, num_classes=10, lr=0.05, warmup_steps=1, crop=64,
+                       process_group=dist.group.WORLD if world > 1 else None, seed=3)
+    torch.backends.cudnn.benchmark = False  # no solver search in a test (and the same solvers in every process)
+    losses = [float(tr.step()) for _ in range(_RES_STEPS)]
+    torch.cuda.synchronize()
+    params = {k: v.detach().float().cpu() for k, v in tr.model.named_parameters()}
+    stats = {k: v.detach().float().cpu() for k, v in tr.model.named_buffers() if v.is_floating_point()}
+    torch.save({"losses": losses, "state": params, "stats": stats}, f"{out}.{world}.{rank}")
+
+
+def _resnet_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _resnet_run(world, rank, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single():
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.start_processes(_resnet_worker, args=(2, _port(), out), nprocs=2, start_method="spawn")
+        mp.start_processes(_resnet_worker, args=(1, _port(), out), nprocs=1, start_method="spawn")
+        r0, r1 = (torch.load(f"{out}.2.{r}", weights_only=True) for r in range(2))
+        one = torch.load(f"{out}.1.0", weights_only=True)
+    assert all(torch.isfinite(torch.tensor(r0["losses"])))
+    for k in r0["state"]:  # parameters: every rank applies the same all-reduced gradient
+        assert torch.equal(r0["state"][k], r1["state"][k]), f"DP replicas disagree on {k}"
+    for k in r0["stats"]:  # BN running statistics are per-replica buffers (same data here -> ~equal at bf16 level)
+        a, b = r0["stats"][k], r1["stats"][k]
+        assert (a - b).abs().max().item() <= 2e-2 * (b.abs().max().item() + 1e-3), k
+    for a, b in zip(r0["losses"], one["losses"]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (r0["losses"], one["losses"])
+    worst = max((r0["state"][k] - v).abs().max().item() / (v.abs().max().item() + 1e-6)
+                for k, v in one["state"].items())
+    assert worst < 5e-2, worst

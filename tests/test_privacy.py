@@ -371,3 +371,79 @@ def test_dp_sgd_mnist_cnn_gpu_step():
     y = torch.randint(0, 10, (256,), device="cuda")
     loss = opt.step(m, lambda out, t: torch.nn.functional.cross_entropy(out, t, reduction="none"), x, y)
     assert math.isfinite(loss) and opt.last_norms.shape == (256,)
+
+
+# ---------------------------------------------------------------- more query / optimizer behaviour
+# (reference: gaussian_query_test.py test_incompatible_records, nested_query_test.py test_complex_nested_query /
+#  test_nested_query_with_noise, no_privacy_query_test.py, dp_optimizer_test.py testEstimator)
+
+
+@pytest.mark.parametrize("query", [Q.GaussianSumQuery(10.0, 0.0), Q.NoPrivacySumQuery(),
+                                   Q.GaussianAverageQuery(10.0, 0.0, 1.0), Q.NoPrivacyAverageQuery()])
+@pytest.mark.parametrize("rec1,rec2", [
+    (torch.zeros(2), torch.zeros(3)),                       # shape mismatch
+    ([torch.zeros(2), torch.zeros(1)], [torch.zeros(2)]),   # structure mismatch
+])
+def test_incompatible_records_raise(query, rec1, rec2):
+    with pytest.raises((ValueError, TypeError, RuntimeError)):
+        _run_query(query, [rec1, rec2])
+
+
+def test_no_privacy_sum_and_average_exact():
+    r = [torch.tensor([1.0, 2.0]), torch.tensor([3.0, 5.0]), torch.tensor([-1.0, 2.0])]
+    s, _ = _run_query(Q.NoPrivacySumQuery(), r)
+    a, _ = _run_query(Q.NoPrivacyAverageQuery(), r)
+    torch.testing.assert_close(s, torch.tensor([3.0, 9.0]))
+    torch.testing.assert_close(a, torch.tensor([1.0, 3.0]))
+
+
+def test_complex_nested_query():
+    """Sums and averages at several nesting depths, each clipping its own sub-record."""
+    q = Q.NestedQuery({"a": Q.GaussianSumQuery(1.0, 0.0),
+                       "b": [Q.GaussianAverageQuery(10.0, 0.0, 2.0), (Q.NoPrivacySumQuery(),
+                                                                      Q.GaussianSumQuery(5.0, 0.0))]})
+    recs = [{"a": torch.tensor([3.0, 4.0]), "b": [torch.tensor([2.0]), (torch.tensor([1.0]), torch.tensor([6.0, 8.0]))]},
+            {"a": torch.tensor([0.3, 0.4]), "b": [torch.tensor([4.0]), (torch.tensor([2.0]), torch.tensor([0.0, 1.0]))]}]
+    out, _ = _run_query(q, recs)
+    torch.testing.assert_close(out["a"], torch.tensor([0.6 + 0.3, 0.8 + 0.4]))   # first record clipped to norm 1
+    torch.testing.assert_close(out["b"][0], torch.tensor([3.0]))                  # (2 + 4) / 2
+    torch.testing.assert_close(out["b"][1][0], torch.tensor([3.0]))
+    torch.testing.assert_close(out["b"][1][1], torch.tensor([3.0, 5.0]))          # [6,8] clipped to [3,4] + [0,1]
+
+
+def test_nested_query_noise_std_per_leaf():
+    g = torch.Generator().manual_seed(7)
+    q = Q.NestedQuery([Q.GaussianSumQuery(1.0, 1.0, generator=g), Q.GaussianSumQuery(1.0, 3.0, generator=g)])
+    draws = np.array([[float(x) for x in _run_query(q, [[torch.zeros(1), torch.zeros(1)]])[0]] for _ in range(1500)])
+    assert draws[:, 0].std() == pytest.approx(1.0, abs=0.1)
+    assert draws[:, 1].std() == pytest.approx(3.0, abs=0.25)
+
+
+def test_make_optimizer_class_wraps_any_torch_optimizer():
+    from mifx.privacy.optimizers import make_optimizer_class
+
+    DPRMSprop = make_optimizer_class(torch.optim.RMSprop)
+    assert DPRMSprop.__name__ == "DPRMSpropOptimizer"
+    model = _Var([1.0, 2.0])
+    opt = DPRMSprop(l2_norm_clip=1.0e9, noise_multiplier=0.0, num_microbatches=2, params=model.parameters(),
+                    learning_rate=0.01)
+    opt.compute_gradients(model, _half_sq, torch.tensor([[3.0, 4.0], [5.0, 6.0]]), torch.zeros(2))
+    torch.testing.assert_close(model.v.grad, torch.tensor([-3.0, -3.0]))
+    with pytest.raises(TypeError):
+        make_optimizer_class(42)
+
+
+def test_dp_sgd_linear_regression_converges():
+    """The reference's estimator integration test: DP-SGD with clipping + noise fits y = X w* + b*."""
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(2000, 4, generator=g)
+    w_true, b_true = torch.tensor([-6.0, -3.0, 2.0, 5.0]), 1.0
+    y = X @ w_true + b_true
+    model = torch.nn.Linear(4, 1)
+    opt = DPGradientDescentOptimizer(l2_norm_clip=100.0, noise_multiplier=0.1, num_microbatches=20,
+                                     params=model.parameters(), learning_rate=0.5, seed=5)
+    for step in range(150):
+        i = torch.randint(0, 2000, (20,), generator=g)
+        opt.step(model, lambda out, t: 0.5 * (out.squeeze(-1) - t) ** 2, X[i], y[i])
+    torch.testing.assert_close(model.weight.detach().squeeze(0), w_true, atol=1.0, rtol=0)
+    assert abs(float(model.bias) - b_true) < 1.0
