@@ -94,7 +94,13 @@ def main(argv=None):
     ap.add_argument("--images", type=int, default=2048, help="HBM-resident images per GPU")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--deterministic", action="store_true",
+                    help="MIOpen deterministic convolution solvers: bit-reproducible steps (the default bf16 solvers "
+                         "are not run-to-run reproducible, tools/diag/resnet_determinism.py). Diagnostic only: "
+                         "measured 13.7 s/step at B=256 on one MI355X vs 26.5 ms with the default solvers")
     a = ap.parse_args(argv)
+    if a.deterministic:
+        torch.backends.cudnn.deterministic = True
     env = mdist.init()
     dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     imgs, labels = synthetic_imagenet(a.images, seed=env.rank, device=dev)
@@ -124,7 +130,8 @@ def main(argv=None):
                           "value": a.batch * env.world_size * a.steps / dt, "unit": "images/s",
                           "n_gpus": env.world_size, "batch_per_gpu": a.batch, "ms_per_step": 1e3 * dt / a.steps,
                           "loss": float(loss), "dtype": "bf16", "data": "synthetic ImageNet-shaped (HBM-resident)",
-                          "parallelism": f"dp{env.world_size}"}), flush=True)
+                          "parallelism": f"dp{env.world_size}",
+                          "deterministic": bool(torch.backends.cudnn.deterministic)}), flush=True)
     mdist.shutdown()
 
 
