@@ -178,8 +178,7 @@ def dnntrainer(a) -> None:
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
     tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=0), batch=a.batch_size, lr=a.learning_rate, device=dev)
     tr.set_data(ids, dense, y)
-    for _ in range(a.steps):
-        tr.step()
+    tr.run(a.steps)  # GPU: hipGraph replays of 50 steps (CPU: eager steps)
     ecols = dataset.table_to_numpy(dataset.read_split(os.path.join(a.transformed_data_dir, "eval")))
     eids, edense, ey = columns_to_tensors(ecols, cfg)
     logits = tr.predict_logits(eids, edense)

@@ -10,14 +10,18 @@ from . import _lib
 from ._lib import F32, I32, VP, check, ptr, sig, stream_handle
 
 
+I64 = ctypes.c_longlong
+
+
 @functools.lru_cache(maxsize=None)
 def _fns():
     lib = _lib.load("embag_mlp")
     return {
         "limits": sig(lib, "mifx_tdnn_limits", [VP]),
-        "fwd_bwd": sig(lib, "mifx_tdnn_fwd_bwd", [VP, VP, VP, VP, VP, I32, VP, I32, I32, VP, I32, I32, F32, I32,
-                                                  VP, VP, VP, VP, VP, VP, VP]),
-        "adagrad": sig(lib, "mifx_tdnn_adagrad", [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, I32, VP, I32, I32,
+        "max_batch": sig(lib, "mifx_tdnn_max_batch", []),
+        "fwd_bwd": sig(lib, "mifx_tdnn_fwd_bwd", [VP, VP, VP, VP, VP, I32, VP, I32, I32, VP, I64, VP, I64, I32, I32,
+                                                  F32, I32, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "adagrad": sig(lib, "mifx_tdnn_adagrad", [VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP, I32, I32, I64, VP, I64,
                                                   VP, VP, VP, I32, I32, F32, VP, VP]),
         "chunks": sig(lib, "mifx_tdnn_chunks", [I32]),
     }
@@ -26,7 +30,7 @@ def _fns():
 def limits() -> dict:
     out = (ctypes.c_int * 3)()
     _fns()["limits"](out)
-    return {"max_hidden": out[0], "max_fields": out[1], "max_dense": out[2]}
+    return {"max_hidden": out[0], "max_fields": out[1], "max_dense": out[2], "max_batch": _fns()["max_batch"]()}
 
 
 def make_buffers(B: int, H: int, D: int, device) -> dict:
@@ -38,30 +42,32 @@ def make_buffers(B: int, H: int, D: int, device) -> dict:
             "dpart": torch.empty(_fns()["chunks"](B) * (D + 2) * H, device=device)}
 
 
-def fwd_bwd(W1, b1, w2, b2, rows, xd, y, dense_row0: int, grad_scale: float, train: bool, bufs: dict):
-    """rows int32 [B, F] (global W1 rows), xd float [B, D], y float [B] -> fills bufs (a, dz, logit, dlogit, loss)."""
-    B, F = rows.shape
+def fwd_bwd(W1, b1, w2, b2, rows, xd, y, dense_row0: int, grad_scale: float, train: bool, bufs: dict,
+            batch: int | None = None, step_ctr: torch.Tensor | None = None, start: int = 0):
+    """rows int32 [n, F] (global W1 rows), xd float [n, D], y float [n]: the resident records (n = batch for one
+    batch). Example b of the step is record (start + b) % n, start = step_ctr * batch % n when `step_ctr` (int64
+    device scalar) is given. Fills bufs (a, dz, logit, dlogit, loss) for `batch` examples."""
+    n, F = rows.shape
+    B = n if batch is None else int(batch)
     D = xd.shape[1]
     H = W1.shape[1]
     check(_fns()["fwd_bwd"](ptr(W1), ptr(b1), ptr(w2), ptr(b2), ptr(rows), F, ptr(xd), D, dense_row0,
-                            ptr(y), B, H, float(grad_scale), int(train), ptr(bufs["a"]), ptr(bufs["part"]),
-                            ptr(bufs.get("dz")),
-                            ptr(bufs["logit"]), ptr(bufs.get("dlogit")), ptr(bufs.get("loss")),
-                            stream_handle(W1.device)), "mifx_tdnn_fwd_bwd")
+                            ptr(y), n, ptr(step_ctr), int(start), B, H, float(grad_scale), int(train),
+                            ptr(bufs["a"]), ptr(bufs["part"]), ptr(bufs.get("dz")), ptr(bufs["logit"]),
+                            ptr(bufs.get("dlogit")), ptr(bufs.get("loss")), ptr(bufs.get("dpart") if train else None),
+                            stream_handle(W1.device)),
+          "mifx_tdnn_fwd_bwd")
 
 
-def adagrad(params: dict, accs: dict, rows: torch.Tensor, xd, dense_row0: int, bufs: dict, lr: float) -> None:
-    """Sparse-row + dense Adagrad (TF semantics) from the buffers of `fwd_bwd`."""
-    B, F = rows.shape
-    flat = rows.reshape(-1)
-    srt, order = torch.sort(flat, stable=True)
-    urows, counts = torch.unique_consecutive(srt, return_counts=True)
-    seg = torch.zeros(urows.numel() + 1, dtype=torch.int32, device=rows.device)
-    seg[1:] = torch.cumsum(counts, 0)
+def adagrad(params: dict, accs: dict, rows: torch.Tensor, xd, dense_row0: int, bufs: dict, lr: float,
+            batch: int | None = None, step_ctr: torch.Tensor | None = None, start: int = 0) -> None:
+    """Sparse-row + dense Adagrad (TF semantics) from the buffers of `fwd_bwd` (same record selection); advances
+    `step_ctr` by one at the end of the update. No host synchronisation: graph-capturable."""
+    n, F = rows.shape
+    B = n if batch is None else int(batch)
     H = params["W1"].shape[1]
-    urows32, order32 = urows.to(torch.int32), order.to(torch.int32)  # keep alive across the launch
     check(_fns()["adagrad"](ptr(params["W1"]), ptr(accs["W1"]), ptr(params["b1"]), ptr(accs["b1"]),
                             ptr(params["w2"]), ptr(accs["w2"]), ptr(params["b2"]), ptr(accs["b2"]),
-                            ptr(urows32), ptr(seg), ptr(order32), urows.numel(), F,
-                            ptr(xd), xd.shape[1], dense_row0, ptr(bufs["a"]), ptr(bufs["dz"]), ptr(bufs["dlogit"]),
-                            B, H, float(lr), ptr(bufs["dpart"]), stream_handle(rows.device)), "mifx_tdnn_adagrad")
+                            ptr(rows), F, ptr(xd), xd.shape[1], dense_row0, n, ptr(step_ctr), int(start),
+                            ptr(bufs["a"]), ptr(bufs["dz"]), ptr(bufs["dlogit"]), B, H, float(lr),
+                            ptr(bufs["dpart"]), stream_handle(rows.device)), "mifx_tdnn_adagrad")

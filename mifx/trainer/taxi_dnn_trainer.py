@@ -13,17 +13,30 @@ from .optim import TFAdagrad
 
 
 class TaxiDNNTrainer:
+    """On the GPU a step is 5 HIP launches with no host work: the batch is selected on the device from the
+    HBM-resident records through a device step counter (advanced by the optimizer kernel), and the sparse Adagrad
+    deduplicates rows in-kernel (no sort/unique, whose dynamic output size synchronised the host every step). So
+    the step is captured once into hipGraphs -- one step and `steps_per_graph` consecutive steps -- and replayed
+    (`graph=False`: eager launches of the same kernels)."""
+
     def __init__(self, model: TaxiDNN | None = None, batch: int = 32, lr: float = 0.1, device="cpu",
-                 initial_accumulator_value: float = 0.1, loss_reduction: str = "sum", native: bool | None = None):
+                 initial_accumulator_value: float = 0.1, loss_reduction: str = "sum", native: bool | None = None,
+                 graph: bool = True, steps_per_graph: int = 50):
         self.device = torch.device(device)
         self.model = (model or TaxiDNN()).to(self.device)
         self.batch, self.lr, self.loss_reduction = batch, lr, loss_reduction
         self.native = (self.device.type == "cuda") if native is None else native
         self.dense_row0 = self.model.cfg.sparse_rows
+        self.use_graph = bool(graph and self.native)
+        self.steps_per_graph = max(1, int(steps_per_graph))
+        self.graph, self.graph_multi = None, None
         if self.native:
             from ..ops import embag_mlp
 
             self._k = embag_mlp
+            if batch > embag_mlp.limits()["max_batch"]:
+                raise ValueError(f"batch {batch} > {embag_mlp.limits()['max_batch']} (csrc/embag_mlp.hip kMaxList)")
+            self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
             p = {n: getattr(self.model, n) for n in ("W1", "b1", "w2", "b2")}
             self.params = {n: t.data for n, t in p.items()}
             self.accs = {n: torch.full_like(t, initial_accumulator_value) for n, t in self.params.items()}
@@ -38,21 +51,64 @@ class TaxiDNNTrainer:
         self.dense = dense.to(self.device).float().contiguous()
         self.label = label.to(self.device).float().contiguous()
         self.n = len(self.label)
+        if self.n < self.batch:
+            raise ValueError(f"{self.n} records < batch {self.batch}")
+        if self.native:  # the device counter continues from the host's step count (graphs read the same tensors)
+            self.step_ctr.fill_(self.step_idx)
 
     def _idx(self):
         s = (self.step_idx * self.batch) % self.n
         return (torch.arange(self.batch, device=self.device) + s) % self.n
 
+    def _native_step(self) -> None:
+        scale = 1.0 if self.loss_reduction == "sum" else 1.0 / self.batch
+        p = self.params
+        self._k.fwd_bwd(p["W1"], p["b1"], p["w2"], p["b2"], self.rows, self.dense, self.label, self.dense_row0, scale,
+                        True, self.bufs, batch=self.batch, step_ctr=self.step_ctr)
+        self._k.adagrad(p, self.accs, self.rows, self.dense, self.dense_row0, self.bufs, self.lr, batch=self.batch,
+                        step_ctr=self.step_ctr)
+
+    def capture(self) -> None:
+        """Capture one step and `steps_per_graph` consecutive steps as hipGraphs (every captured step reads the
+        device counter, so replays walk through the data and the optimizer state like eager steps)."""
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._native_step()
+        gm = None
+        if self.steps_per_graph > 1:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm):
+                for _ in range(self.steps_per_graph):
+                    self._native_step()
+        self.graph, self.graph_multi = g, gm
+
+    def run(self, n: int) -> None:
+        """n training steps: the first eagerly (lazy library/kernel initialisation), then multi-step graph replays
+        and single-step replays for the remainder."""
+        while n > 0 and self.use_graph and self.graph is None:
+            self.step()  # step() captures once a first eager step has run
+            n -= 1
+        if self.graph_multi is not None:
+            reps, n = divmod(n, self.steps_per_graph)
+            for _ in range(reps):
+                self.graph_multi.replay()
+                self.step_idx += self.steps_per_graph
+        for _ in range(n):
+            self.step()
+
     def step(self) -> None:
-        idx = self._idx()
-        rows, xd, y = self.rows[idx].contiguous(), self.dense[idx].contiguous(), self.label[idx].contiguous()
         if self.native:
-            scale = 1.0 if self.loss_reduction == "sum" else 1.0 / self.batch
-            self._k.fwd_bwd(self.params["W1"], self.params["b1"], self.params["w2"], self.params["b2"], rows, xd, y,
-                            self.dense_row0, scale, True, self.bufs)
-            self._k.adagrad(self.params, self.accs, rows, xd, self.dense_row0, self.bufs, self.lr)
+            if self.use_graph and self.graph is None and self.step_idx >= 1:  # first step eager (lazy init), then
+                self.capture()
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._native_step()
             self._last_t = self.bufs["loss"]
         else:
+            idx = self._idx()
+            rows, xd, y = self.rows[idx].contiguous(), self.dense[idx].contiguous(), self.label[idx].contiguous()
             logit = self._forward_rows(rows, xd)
             loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, y, reduction=self.loss_reduction)
             self.opt.zero_grad(set_to_none=True)
@@ -63,7 +119,7 @@ class TaxiDNNTrainer:
 
     def last_loss(self) -> float:
         if self.native:
-            return float(self._last_t.sum())
+            return float(self.bufs["loss"].sum())
         return self._last
 
     @torch.no_grad()

@@ -63,3 +63,24 @@ def test_hip_step_matches_cpu_oracle():
         torch.testing.assert_close(getattr(gpu.model, n).detach().cpu(), getattr(cpu.model, n).detach(),
                                    rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(gpu.predict_logits(ids, dense), cpu.predict_logits(ids, dense), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,steps,spg", [(32, 23, 5), (1024, 7, 3)])
+def test_hip_graph_run_matches_cpu_oracle(batch, steps, spg):
+    """run(): one eager step, then multi-step hipGraph replays + single-step replays; the device step counter walks
+    the resident records exactly as the host oracle does (wrap-around included), and heavily repeated rows (field 0
+    takes 5 values) exercise the in-kernel row dedup of the sparse Adagrad."""
+    cfg = TaxiDNNConfig()
+    ids, dense, y = _data(batch * 3 + 17, cfg, seed=7)  # not a multiple of the batch: batches wrap around
+    cpu = TaxiDNNTrainer(TaxiDNN(cfg, seed=3), batch=batch, lr=0.1, device="cpu")
+    gpu = TaxiDNNTrainer(TaxiDNN(cfg, seed=3), batch=batch, lr=0.1, device="cuda", steps_per_graph=spg)
+    for tr in (cpu, gpu):
+        tr.set_data(ids, dense, y)
+    cpu.run(steps)
+    gpu.run(steps)
+    assert gpu.graph_multi is not None and gpu.step_idx == steps and int(gpu.step_ctr.item()) == steps
+    assert gpu.last_loss() == pytest.approx(cpu.last_loss(), rel=2e-4)
+    for n in ("W1", "b1", "w2", "b2"):
+        torch.testing.assert_close(getattr(gpu.model, n).detach().cpu(), getattr(cpu.model, n).detach(),
+                                   rtol=2e-4, atol=2e-5)

@@ -22,18 +22,17 @@ def run(device, batch, steps, warmup):
     y = (torch.rand(n, generator=g) < 0.3).float()
     tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=0), batch=batch, device=device)
     tr.set_data(ids, dense, y)
-    for _ in range(warmup):
-        tr.step()
+    tr.run(warmup)
     if device != "cpu":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.step()
+    tr.run(steps)  # GPU: 50-step hipGraph replays
     if device != "cpu":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"device": device, "batch": batch, "steps": steps, "ms_per_step": 1e3 * dt / steps,
-            "examples_per_sec": batch * steps / dt, "final_loss": tr.last_loss()}
+            "examples_per_sec": batch * steps / dt, "final_loss": tr.last_loss(),
+            "hipgraph": getattr(tr, "graph_multi", None) is not None}
 
 
 if __name__ == "__main__":
