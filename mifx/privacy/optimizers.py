@@ -17,9 +17,21 @@ import math
 import torch
 from torch.func import functional_call, grad_and_value, vmap
 
+from ..ops import dpsgd_mnist
 from ..ops.dp import clip_sum_noise
 from ..trainer.optim import make_optimizer
 from .queries import GaussianAverageQuery
+
+_MAX_FUSED_ROWS = 4096  # clip_sum_noise's row bound
+
+
+def sparse_softmax_ce(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Per-example `tf.nn.sparse_softmax_cross_entropy_with_logits` (the tutorial's vector loss). Passing
+    this function as `vector_loss_fn` lets models with a fused per-microbatch gradient kernel use it."""
+    return torch.nn.functional.cross_entropy(logits, labels, reduction="none")
+
+
+sparse_softmax_ce.mifx_kind = "sparse_softmax_ce"
 
 
 class DPOptimizer:
@@ -60,6 +72,9 @@ class DPOptimizer:
         M = self.num_microbatches or B
         if B % M:
             raise ValueError("Number of microbatches should divide evenly batch_size")
+        if (getattr(vector_loss_fn, "mifx_kind", None) == "sparse_softmax_ce" and len(batch) == 2
+                and M <= _MAX_FUSED_ROWS and dpsgd_mnist.supported(model, batch[0])):
+            return self._fused_mnist(model, *batch, M)
         names = [n for n, p in model.named_parameters() if p.requires_grad]
         params = {n: p.detach() for n, p in model.named_parameters() if p.requires_grad}
         buffers = {n: b.detach() for n, b in model.named_buffers()}
@@ -89,6 +104,11 @@ class DPOptimizer:
             acc = clip_sum_noise(acc[None, :], math.inf, self.l2_norm_clip * self.noise_multiplier, M, self.seed,
                                  self.steps)
         self.last_norms = torch.cat(norms)
+        self._assign_grads(model, names, acc)
+        return total_loss / B
+
+    @staticmethod
+    def _assign_grads(model, names, acc) -> None:
         off = 0
         named = dict(model.named_parameters())
         for n in names:
@@ -97,7 +117,15 @@ class DPOptimizer:
             g = acc[off:off + k].view_as(p).to(p.dtype)
             p.grad = g.clone() if p.grad is None else p.grad.copy_(g)
             off += k
-        return total_loss / B
+
+    def _fused_mnist(self, model, x, y, M) -> float:
+        """MNIST tutorial CNN on the GPU: all M microbatch gradients from one kernel (csrc/dpsgd_mnist.hip),
+        then the same fused clip / sum / noise pass as the generic path."""
+        G, losses = dpsgd_mnist.per_microbatch_grads(model, x, y, M)
+        acc, self.last_norms = clip_sum_noise(G, self.l2_norm_clip, self.l2_norm_clip * self.noise_multiplier, M,
+                                              self.seed, self.steps, return_norms=True)
+        self._assign_grads(model, [n for n, _ in model.named_parameters()], acc)
+        return float(losses.sum()) / x.shape[0]
 
     def step(self, model: torch.nn.Module, vector_loss_fn, *batch) -> float:
         self.optimizer.zero_grad(set_to_none=True)

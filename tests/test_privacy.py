@@ -373,6 +373,65 @@ def test_dp_sgd_mnist_cnn_gpu_step():
     assert math.isfinite(loss) and opt.last_norms.shape == (256,)
 
 
+def _vmap_microbatch_grads(model, x, y, M):
+    """fp32 reference: torch.func per-microbatch gradients of the summed CE loss, [M, P] in parameter order."""
+    from torch.func import functional_call, grad, vmap
+
+    params = {n: p.detach() for n, p in model.named_parameters()}
+
+    def f(p, xb, yb):
+        return torch.nn.functional.cross_entropy(functional_call(model, p, (xb,)), yb, reduction="sum")
+
+    g = vmap(grad(f), in_dims=(None, 0, 0))(params, x.reshape(M, -1, *x.shape[1:]), y.reshape(M, -1))
+    return torch.cat([g[n].reshape(M, -1) for n in params], 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,M", [(64, 64), (64, 16), (96, 1)])
+def test_dpsgd_mnist_fused_grads_match_vmap(B, M):
+    """csrc/dpsgd_mnist.hip: whole-network per-microbatch gradients == vmap(grad) of the torch model (fp32)."""
+    from mifx.models.cnn import MnistDPCNN
+    from mifx.ops import dpsgd_mnist
+
+    torch.manual_seed(1)
+    m = MnistDPCNN().cuda()
+    x = torch.rand(B, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (B,), device="cuda")
+    y[3] = -100  # ignored label: zero loss and gradient, as F.cross_entropy
+    G, loss = dpsgd_mnist.per_microbatch_grads(m, x, y, M)
+    torch.cuda.synchronize()
+    assert G.shape == (M, dpsgd_mnist.LD) and bool((G[:, dpsgd_mnist.NUM_PARAMS:] == 0).all())
+    ref = _vmap_microbatch_grads(m, x, y, M)
+    scale = ref.abs().amax(1, keepdim=True).clamp_min(1e-6)  # (row of the ignored label is all zero)
+    torch.testing.assert_close(G[:, :dpsgd_mnist.NUM_PARAMS] / scale, ref / scale, rtol=0, atol=2e-5)
+    ref_loss = torch.nn.functional.cross_entropy(m(x), y, reduction="none")
+    torch.testing.assert_close(loss, ref_loss, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_dpsgd_mnist_fused_step_matches_generic_path():
+    """The DP optimizer's fused MNIST path (sparse_softmax_ce) and its generic vmap path take the same step
+    (same clip, same Philox noise stream)."""
+    from mifx.models.cnn import MnistDPCNN
+    from mifx.privacy import sparse_softmax_ce
+
+    torch.manual_seed(2)
+    ma = MnistDPCNN().cuda()
+    mb = MnistDPCNN().cuda()
+    mb.load_state_dict(ma.state_dict())
+    oa = DPGradientDescentOptimizer(1.0, 1.12, 32, ma.parameters(), 0.08, seed=7)
+    ob = DPGradientDescentOptimizer(1.0, 1.12, 32, mb.parameters(), 0.08, seed=7)
+    for it in range(3):
+        x = torch.rand(128, 28, 28, device="cuda")
+        y = torch.randint(0, 10, (128,), device="cuda")
+        la = oa.step(ma, sparse_softmax_ce, x, y)
+        lb = ob.step(mb, lambda out, t: torch.nn.functional.cross_entropy(out, t, reduction="none"), x, y)
+        assert abs(la - lb) < 1e-4 * max(1.0, abs(lb))
+        torch.testing.assert_close(oa.last_norms, ob.last_norms, rtol=1e-4, atol=1e-6)
+    for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5, msg=n)
+
+
 # ---------------------------------------------------------------- more query / optimizer behaviour
 # (reference: gaussian_query_test.py test_incompatible_records, nested_query_test.py test_complex_nested_query /
 #  test_nested_query_with_noise, no_privacy_query_test.py, dp_optimizer_test.py testEstimator)
