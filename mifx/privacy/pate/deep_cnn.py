@@ -125,7 +125,9 @@ def train(images: np.ndarray, labels: np.ndarray, ckpt_path: str, cfg: DeepCNNCo
     model = build_model(cfg, dropout).to(dev)
     if dev.type == "cuda":
         model = model.to(memory_format=torch.channels_last)
-    x, y = _to_nchw(np.asarray(images, np.float32), dev), torch.as_tensor(np.asarray(labels), device=dev).long()
+    pdt = next(model.parameters()).dtype  # fp32 (fp64 in the ensemble-equivalence test)
+    x = _to_nchw(np.asarray(images, np.float32), dev).to(pdt)
+    y = torch.as_tensor(np.asarray(labels), device=dev).long()
     params = [p for p in model.parameters() if p.requires_grad]
     nb_ex_per_epoch = int(60000 / cfg.nb_teachers)
     decay_steps = max(1, int(nb_ex_per_epoch / cfg.batch_size * cfg.epochs_per_decay))
@@ -176,7 +178,7 @@ def softmax_preds(images: np.ndarray, ckpt_path: str, cfg: DeepCNNConfig | None 
     if dev.type == "cuda":
         model = model.to(memory_format=torch.channels_last)
     model.eval()
-    x = _to_nchw(np.asarray(images, np.float32), dev)
+    x = _to_nchw(np.asarray(images, np.float32), dev).to(next(model.parameters()).dtype)
     outs = []
     bs = max(cfg.batch_size, 4096)
     for i in range(0, len(x), bs):

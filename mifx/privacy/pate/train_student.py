@@ -16,13 +16,18 @@ from . import aggregation, deep_cnn
 from .train_teachers import add_common_flags, config_from, teacher_ckpt
 
 
-def ensemble_preds(a, nb_teachers: int, stdnt_data: np.ndarray) -> np.ndarray:
+def ensemble_preds(a, nb_teachers: int, stdnt_data: np.ndarray, chunk: int = 64) -> np.ndarray:
+    """[nb_teachers, N, labels] teacher softmax predictions; `chunk` teachers per grouped forward
+    (`ensemble.ensemble_softmax_preds`) instead of one restore + inference per teacher."""
+    from .ensemble import ensemble_softmax_preds
+
     out = np.zeros((nb_teachers, len(stdnt_data), a.nb_labels), dtype=np.float32)
     cfg = config_from(a, nb_teachers)
-    for t in range(nb_teachers):
-        ck = teacher_ckpt(a.teachers_dir, a.dataset, nb_teachers, t, a.deeper) + f"-{a.teachers_max_steps - 1}"
-        out[t] = deep_cnn.softmax_preds(stdnt_data, ck, cfg, device=a.device)
-        print("Computed Teacher " + str(t) + " softmax predictions")
+    ckpts = [teacher_ckpt(a.teachers_dir, a.dataset, nb_teachers, t, a.deeper) + f"-{a.teachers_max_steps - 1}"
+             for t in range(nb_teachers)]
+    for t0 in range(0, nb_teachers, chunk):
+        out[t0:t0 + chunk] = ensemble_softmax_preds(stdnt_data, ckpts[t0:t0 + chunk], cfg, device=a.device)
+        print(f"Computed Teachers {t0}..{min(nb_teachers, t0 + chunk) - 1} softmax predictions")
     return out
 
 

@@ -53,12 +53,45 @@ def train_teacher(a, nb_teachers: int, teacher_id: int) -> float:
     return precision
 
 
-def main(argv=None) -> float:
+def train_all_teachers(a, nb_teachers: int, teacher_ids=None) -> list[float]:
+    """Every teacher (or `teacher_ids`) in ONE grouped-network training run (`ensemble.train_ensemble`): same
+    shards, batches, optimizer and checkpoint files as `train_teacher` per id. Under a multi-process launch
+    (WORLD_SIZE > 1) rank r takes teachers r, r + WORLD_SIZE, ... (no communication)."""
+    from . import ensemble
+
+    os.makedirs(a.data_dir, exist_ok=True)
+    os.makedirs(a.train_dir, exist_ok=True)
+    if teacher_ids is None:
+        rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+        teacher_ids = list(range(rank, nb_teachers, world))
+        if world > 1 and (a.device is None or a.device == "cuda"):
+            import torch
+
+            if torch.cuda.is_available():
+                a.device = f"cuda:{int(os.environ.get('LOCAL_RANK', rank)) % torch.cuda.device_count()}"
+    if not teacher_ids:
+        return []
+    xtr, ytr, xte, yte = deep_cnn.load_dataset(a.dataset, train_size=a.train_size, test_size=a.test_size)
+    shards = [deep_cnn.partition_dataset(xtr, ytr, nb_teachers, t) for t in teacher_ids]
+    print(f"Training {len(teacher_ids)} teachers together; length of training data per teacher: {len(shards[0][1])}")
+    cfg = config_from(a, nb_teachers)
+    ckpts = [teacher_ckpt(a.train_dir, a.dataset, nb_teachers, t, a.deeper) for t in teacher_ids]
+    assert ensemble.train_ensemble([s[0] for s in shards], [s[1] for s in shards], ckpts, cfg, device=a.device)
+    preds = ensemble.ensemble_softmax_preds(xte, [f"{c}-{a.max_steps - 1}" for c in ckpts], cfg, device=a.device)
+    precisions = [accuracy(p, yte) for p in preds]
+    for t, p in zip(teacher_ids, precisions):
+        print(f"Precision of teacher {t} after training: {p}")
+    return precisions
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser(prog="python -m mifx.privacy.pate.train_teachers")
     add_common_flags(ap)
     ap.add_argument("--nb_teachers", type=int, default=50)
-    ap.add_argument("--teacher_id", type=int, default=0)
+    ap.add_argument("--teacher_id", type=int, default=0, help="-1: train every teacher at once (grouped ensemble)")
     a = ap.parse_args(argv)
+    if a.teacher_id < 0:
+        return train_all_teachers(a, a.nb_teachers)
     return train_teacher(a, a.nb_teachers, a.teacher_id)
 
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# PATE teacher ensemble (grouped network): GPU tests, throughput vs the sequential recipe, kernel trace
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_pate_training.py -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pate_tests.log 2>&1
+rc=$?
+grep -E "PASSED|FAILED|^E " gpurun_out/pate_tests.log | head -30
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u tools/bench_pate.py --steps 30 > gpurun_out/pate_bench.jsonl 2> gpurun_out/pate_bench.err || { tail -20 gpurun_out/pate_bench.err; exit 1; }
+cat gpurun_out/pate_bench.jsonl
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pate_prof -o pate -- python3 tools/bench_pate.py --steps 12 --teachers 250 > gpurun_out/pate_prof.log 2>&1 || { echo "prof failed"; tail -5 gpurun_out/pate_prof.log; exit 1; }
+echo done
