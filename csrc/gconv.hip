@@ -1,0 +1,295 @@
+// Grouped stride-1 convolution as an implicit GEMM on bf16 MFMA (NHWC), forward and input gradient.
+//
+// Reference workload: the PATE-2017 `deep_cnn.inference` CNN (5x5 convs 64/128 channels,
+// `research/pate_2017/deep_cnn.py:84-191`) trained for every teacher of the ensemble
+// (`train_teachers.py:44-96`). `mifx/privacy/pate/ensemble.py` trains all teachers at once as ONE grouped
+// network (group g = teacher g), and MIOpen's grouped NHWC solvers run those shapes (G = 250 groups of
+// 64 -> 128 channels, 5x5, 14x14, B = 128) at 20-40 TFLOP/s. Here each group is an implicit GEMM:
+//   y[m = (n,p,q), g*K + k] = b[g*K + k] + sum_{r,s,c} x[n, p+r-pad, q+s-pad, g*C + c] * w[g][k][r][s][c]
+// with M = N*Ho*Wo output pixels, N_gemm = K output channels, reduction = R*S*C ordered tap-major, so a
+// 32-wide reduction chunk is 32 contiguous channels of one input pixel (one 64-byte row).
+//
+//  * Tiles: 128 pixels x BN channels (BN = 128 or 64) per 256-thread workgroup; 4 waves, each 64 x BN/2, on
+//    v_mfma_f32_16x16x32_bf16 with fp32 accumulators. A (pixel rows, zero-filled outside the image) and B
+//    (weight rows [k][tap][c]) chunks are staged global -> registers -> LDS, double-buffered (one barrier
+//    per 32-wide chunk); LDS rows are padded to 80 bytes so the 16-byte fragment reads are conflict-free.
+//  * Grid (pixel tiles, K / BN, G): tiles of one group are consecutive, so a group's weights and its input
+//    halo rows are reused from L2 while they are hot.
+//  * The input gradient of a stride-1 convolution is the same operation on dy with the weight flipped
+//    spatially and transposed ([g][c][R-1-r][S-1-s][k]) and pad' = R-1-pad, so one kernel serves both.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int BM = 128, BK = 32, LDR = 40;  // LDS row: 32 bf16 + 8 pad (80 B)
+
+__device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+struct Geo {
+  int N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad;
+};
+
+template <int BN>
+__global__ __launch_bounds__(kThreads) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                      const float* __restrict__ bias, bf16* __restrict__ y, Geo d) {
+  constexpr int BCH = BN * 4 / kThreads;  // 16-byte weight chunks per thread per step (2 or 1)
+  __shared__ __attribute__((aligned(16))) bf16 As[2][BM * LDR];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * LDR];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = blockIdx.z, n0 = blockIdx.y * BN;
+  const long long M = (long long)d.N * d.Ho * d.Wo;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int CT = d.G * d.C;  // input row stride (channels)
+  const int chunks_c = d.C / BK, nsteps = d.R * d.S * chunks_c;
+
+  // this thread's two A chunks: pixel rows ap[j] = (t >> 2) + 64 j, 16-byte part (t & 3)
+  int an[2], ah[2], aw[2];
+  bool am[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const long long m = m0 + (t >> 2) + 64 * j;
+    am[j] = m < M;
+    const long long mm = am[j] ? m : 0;
+    aw[j] = (int)(mm % d.Wo);
+    ah[j] = (int)((mm / d.Wo) % d.Ho);
+    an[j] = (int)(mm / ((long long)d.Wo * d.Ho));
+  }
+  const int apart = (t & 3) * 8;
+  const bf16* wg = w + (size_t)g * d.K * d.R * d.S * d.C;
+
+  u4 ra[2], rb[BCH];
+  auto load = [&](int step) {
+    const int tap = step / chunks_c, c0 = (step - tap * chunks_c) * BK;
+    const int r = tap / d.S, s = tap - r * d.S;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int hh = ah[j] + r - d.pad, ww = aw[j] + s - d.pad;
+      if (am[j] && hh >= 0 && hh < d.Hi && ww >= 0 && ww < d.Wi) {
+        const bf16* src = x + ((size_t)(an[j] * d.Hi + hh) * d.Wi + ww) * CT + g * d.C + c0 + apart;
+        ra[j] = *(const u4*)src;
+      } else {
+        ra[j] = u4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      const int c = t + kThreads * j, k = c >> 2, part = (c & 3) * 8;
+      rb[j] = *(const u4*)(wg + ((size_t)(n0 + k) * d.R * d.S + tap) * d.C + c0 + part);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *(u4*)(&As[buf][((t >> 2) + 64 * j) * LDR + apart]) = ra[j];
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      const int c = t + kThreads * j;
+      *(u4*)(&Bs[buf][(c >> 2) * LDR + (c & 3) * 8]) = rb[j];
+    }
+  };
+
+  constexpr int TN = BN / 32;  // 16-wide column tiles per wave (wave owns BN/2 columns)
+  v4f acc[4][TN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int wm = (wv >> 1) * 64, wn = (wv & 1) * (BN / 2);
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    if (step + 1 < nsteps) load(step + 1);
+    v8bf af[4], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const v8bf*)(&As[buf][(wm + 16 * i + fr) * LDR + fk]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = *(const v8bf*)(&Bs[buf][(wn + 16 * j + fr) * LDR + fk]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+    if (step + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][e] = y[pixel m0 + wm + 16 i + 4 (lane >> 4) + e][channel n0 + wn + 16 j + (lane & 15)]
+  const int KT = d.G * d.K;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int k = n0 + wn + 16 * j + fr;
+    const float b = bias ? bias[g * d.K + k] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long long m = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
+        if (m < M) y[m * KT + g * d.K + k] = (bf16)(acc[i][j][e] + b);
+      }
+  }
+}
+
+// ---- weight gradient ------------------------------------------------------------------------------------
+// dw[g*K + k][c][r][s] = sum_m dy[m][g*K + k] * x[pixel(m) + (r - pad, s - pad)][g*C + c]: a GEMM of
+// 128 k-rows x 128 (tap, c) columns per workgroup (128 / C taps of C channels), reduced over output pixels m in
+// chunks of 32. Both operands arrive pixel-major (channels contiguous), so the chunks are staged as
+// [32 pixels][128] bf16 images (rows padded to 288 B) and the MFMA fragments, which need 8 consecutive reduction
+// elements per lane, come from ds_read_b64_tr_b16 transposed reads. The reduction order inside a 32-chunk is
+// permuted identically for both operands (element j of lane group g <-> pixel row 4g + j for j < 4,
+// 16 + 4g + j - 4 for j >= 4), which makes every transposed read conflict-free.
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+constexpr int WLD = 144;  // LDS row (bf16 elements): 128 + 16 pad = 288 B
+
+__device__ __forceinline__ v4s tr_read(const bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p); }
+__device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
+  const v4s r0 = a, r1 = b;
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s r = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
+
+__global__ __launch_bounds__(kThreads) void gconv_wgrad(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        float* __restrict__ dw, Geo d) {
+  __shared__ __attribute__((aligned(16))) bf16 As[2][32 * WLD];  // dy chunk [pixel][k]
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][32 * WLD];  // x chunk [pixel][(tap, c)]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = blockIdx.z, k0 = blockIdx.y * 128;
+  const int tpb = 128 / d.C, tap0 = blockIdx.x * tpb, RS = d.R * d.S;
+  const long long M = (long long)d.N * d.Ho * d.Wo;
+  const int KT = d.G * d.K, CT = d.G * d.C;
+  const int nsteps = (int)((M + 31) / 32);
+  // this thread's chunks: pixel rows pr[j] = (t >> 4) + 16 j, 16-byte chunk (t & 15) of the 256-byte row
+  const int ch = t & 15;
+  const int btap = tap0 + (ch * 8) / d.C, bc = (ch * 8) % d.C;
+  const int br = btap / d.S, bs = btap - br * d.S;
+  const bool btap_ok = btap < RS;
+
+  u4 ra[2], rb[2];
+  auto load = [&](int step) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long long m = (long long)step * 32 + (t >> 4) + 16 * j;
+      ra[j] = u4{0, 0, 0, 0};
+      rb[j] = u4{0, 0, 0, 0};
+      if (m < M) {
+        if (k0 + ch * 8 < d.K) ra[j] = *(const u4*)(dy + m * KT + g * d.K + k0 + ch * 8);
+        const int q = (int)(m % d.Wo), p = (int)((m / d.Wo) % d.Ho), n = (int)(m / ((long long)d.Wo * d.Ho));
+        const int hh = p + br - d.pad, ww = q + bs - d.pad;
+        if (btap_ok && hh >= 0 && hh < d.Hi && ww >= 0 && ww < d.Wi)
+          rb[j] = *(const u4*)(x + ((size_t)(n * d.Hi + hh) * d.Wi + ww) * CT + g * d.C + bc);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (t >> 4) + 16 * j;
+      *(u4*)(&As[buf][row * WLD + ch * 8]) = ra[j];
+      *(u4*)(&Bs[buf][row * WLD + ch * 8]) = rb[j];
+    }
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+  // transposed-read address of lane 4q + p of its 16-lane group G: rows 4G + q (and 16 + 4G + q), cols 4p..4p+3
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int rd_row = 4 * grp + q, rd_col = 4 * p;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    if (step + 1 < nsteps) load(step + 1);
+    v8bf af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16* pa = &As[buf][rd_row * WLD + wm + 16 * i + rd_col];
+      af[i] = cat8(tr_read(pa), tr_read(pa + 16 * WLD));
+      const bf16* pb = &Bs[buf][rd_row * WLD + wn + 16 * i + rd_col];
+      bfr[i] = cat8(tr_read(pb), tr_read(pb + 16 * WLD));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+    if (step + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // acc[i][j][e]: k = k0 + wm + 16 i + 4 (lane >> 4) + e, column wn + 16 j + (lane & 15) = (tap, c)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = wn + 16 * j + (lane & 15);
+    const int tap = tap0 + col / d.C, c = col % d.C;
+    if (tap >= RS) continue;
+    const int r = tap / d.S, s = tap - r * d.S;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm + 16 * i + 4 * (lane >> 4) + e;
+        if (k < d.K) dw[(((size_t)(g * d.K + k) * d.C + c) * d.R + r) * d.S + s] = acc[i][j][e];
+      }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// dw [G*K][C][R][S] fp32 (PyTorch layout) from x [N, Hi, Wi, G*C] and dy [N, Ho, Wo, G*K] bf16 (NHWC).
+// Needs C in {32, 64, 128} and K % 8 == 0 (k-tiles of 128; a partial last tile is masked).
+int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, int Wi, int G, int C, int K, int R,
+                     int S, int pad, hipStream_t st) {
+  const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
+  if (N <= 0 || G <= 0 || G > 65535 || (C != 32 && C != 64 && C != 128) || K <= 0 || K % 8 != 0 || Ho <= 0 ||
+      Wo <= 0 || pad < 0 || pad >= R || pad >= S)
+    return -1;
+  if ((long long)N * Ho * Wo > 0x3fffffffLL) return -1;
+  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad};
+  const int tpb = 128 / C;
+  hipLaunchKernelGGL(gconv_wgrad, dim3((R * S + tpb - 1) / tpb, (K + 127) / 128, G), dim3(kThreads), 0, st,
+                     (const bf16*)x, (const bf16*)dy, dw, d);
+  return (int)hipGetLastError();
+}
+
+// x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
+// stride 1, zero padding `pad` on every side, Ho = Hi + 2 pad - R + 1. Needs C % 32 == 0 and K % 64 == 0.
+int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
+                   int K, int R, int S, int pad, hipStream_t st) {
+  const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
+  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 64 != 0 || Ho <= 0 || Wo <= 0 ||
+      pad < 0 || pad >= R || pad >= S)
+    return -1;
+  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad};
+  const long long M = (long long)N * Ho * Wo;
+  const long long mt = (M + BM - 1) / BM;
+  if (mt > 0x7fffffffLL) return -1;
+  if (K % 128 == 0) {
+    hipLaunchKernelGGL(gconv_fwd<128>, dim3((unsigned)mt, K / 128, G), dim3(kThreads), 0, st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, d);
+  } else {
+    hipLaunchKernelGGL(gconv_fwd<64>, dim3((unsigned)mt, K / 64, G), dim3(kThreads), 0, st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, d);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+"""Grouped stride-1 NHWC convolution on hand-written bf16 MFMA implicit-GEMM kernels (csrc/gconv.hip).
+
+`conv2d(x, weight, bias, padding, groups)` == `F.conv2d(x, weight, bias, stride=1, padding=padding,
+groups=groups)` for channels-last bf16 activations: the forward and the input gradient run one HIP kernel (the
+input gradient of a stride-1 conv is the same kernel on dy with the weight flipped and transposed), the weight
+gradient a second one (transposed LDS reads). `eligible()` says when a call can take this path
+(GPU, C/group % 32 == 0, K/group % 64 == 0; the input gradient needs C/group % 64 == 0 and the weight gradient
+C/group in {32, 64, 128}, else those parts run on MIOpen); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
+ensemble (`mifx/privacy/pate/ensemble.py`)."""
+from __future__ import annotations
+
+import functools
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import I32, VP, check, ptr, sig, stream_handle
+
+
+@functools.lru_cache(maxsize=None)
+def _fns():
+    lib = _lib.load("gconv")
+    return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 9 + [VP]),
+            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 9 + [VP])}
+
+
+def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and weight.dim() == 4):
+        return False
+    GK, C, R, S = weight.shape
+    if x.shape[1] != C * groups or GK % groups:
+        return False
+    K = GK // groups
+    Ho, Wo = x.shape[2] + 2 * padding - R + 1, x.shape[3] + 2 * padding - S + 1
+    return C % 32 == 0 and K % 64 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
+
+
+def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad) -> torch.Tensor:
+    Ho, Wo = Hi + 2 * pad - R + 1, Wi + 2 * pad - S + 1
+    y = torch.empty(N, G * K, Ho, Wo, device=x_nhwc.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+    check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad,
+                        stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
+    return y
+
+
+class _GConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, pad, groups):
+        N, _, Hi, Wi = x.shape
+        GK, C, R, S = weight.shape
+        G, K = groups, GK // groups
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wb = weight.to(torch.bfloat16)
+        w_fwd = wb.view(G, K, C, R, S).permute(0, 1, 3, 4, 2).contiguous()  # [G][K][R][S][C]
+        b = bias.float().contiguous() if bias is not None else None
+        y = _launch(xb, w_fwd, b, N, Hi, Wi, G, C, K, R, S, pad)
+        ctx.save_for_backward(xb, wb)
+        ctx.geo = (N, Hi, Wi, G, C, K, R, S, pad, bias is not None, weight.dtype,
+                   bias.dtype if bias is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        N, Hi, Wi, G, C, K, R, S, pad, has_bias, wdt, bdt = ctx.geo
+        dyb = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        Ho, Wo = dyb.shape[2], dyb.shape[3]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if C % 64 == 0 and R == S:
+                # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
+                w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
+                dx = _launch(dyb, w_bwd, None, N, Ho, Wo, G, K, C, R, S, R - 1 - pad)
+            else:
+                dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=1, padding=pad, groups=G)
+        if ctx.needs_input_grad[1]:
+            if C in (32, 64, 128):  # hand-written weight gradient (fp32 out, PyTorch layout)
+                dw = torch.empty(G * K, C, R, S, device=dyb.device, dtype=torch.float32)
+                check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad,
+                                      stream_handle(dyb.device)), "mifx_gconv_wgrad")
+                dw = dw.to(wdt)
+            else:
+                dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=1, padding=pad,
+                                                 groups=G).to(wdt)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dyb.float().sum((0, 2, 3)).to(bdt)
+        return dx, dw, db, None, None
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0,
+           groups: int = 1) -> torch.Tensor:
+    """Stride-1 (grouped) convolution; the HIP kernels when `eligible`, else F.conv2d. Output bf16 channels-last
+    on the kernel path (the dtype F.conv2d gives under bf16 autocast)."""
+    if eligible(x, weight, groups, padding) and _lib.gpu_available():
+        return _GConv.apply(x, weight, bias, int(padding), int(groups))
+    return F.conv2d(x, weight, bias, stride=1, padding=padding, groups=groups)

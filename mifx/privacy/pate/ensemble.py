@@ -28,8 +28,11 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...models.cnn import _same_pad, same_maxpool
-from ...ops import cnn_ops
+from ...ops import cnn_ops, gconv
 from . import deep_cnn
+
+
+USE_HIP_CONV = True  # csrc/gconv.hip for the eligible stride-1 layers (False: F.conv2d, for A/B and exact tests)
 
 
 def _conv_specs(model: nn.Module):
@@ -68,8 +71,45 @@ class PateEnsemble(nn.Module):
         self.kernels = [template.get_submodule(n).kernel_size[0] for n, _ in self.conv_specs]
 
     # -------------------------------------------------------------------------------- forward
+    @property
+    def col_input(self) -> bool:
+        """First layer as a 1x1 grouped GEMM over an im2col image (Cin * k * k <= 32 taps padded to 32 channels per
+        teacher): the Cin = 1 layer has no 32-channel reduction of its own, and the image of the resident dataset is
+        built once (`conv_input`), not per step."""
+        w = self.conv_w[0]
+        return (USE_HIP_CONV and not self.deeper and self.conv_specs[0][1] == 1 and self.kernels[0] % 2 == 1
+                and w.shape[1] * self.kernels[0] ** 2 <= 32)
+
+    def conv_input(self, x: torch.Tensor, chunk: int = 256) -> torch.Tensor:
+        """[n, T*Cin, H, W] images -> [n, T*32, H, W] SAME-padded im2col image (channels-last storage; bf16 on the
+        GPU), channel t*32 + (c*k + r)*k + s = x[t*Cin + c] at offset (r - k//2, s - k//2), zero-padded to 32."""
+        if not self.col_input:
+            return x
+        n, TC, H, W = x.shape
+        k, T = self.kernels[0], self.T
+        cin, p = TC // T, self.kernels[0] // 2
+        dt = torch.bfloat16 if x.is_cuda else x.dtype
+        out = torch.empty(n, H, W, T, 32, device=x.device, dtype=dt)
+        for i in range(0, n, chunk):
+            xb = F.pad(x[i:i + chunk].to(dt), (p, p, p, p))
+            cols = xb.unfold(2, k, 1).unfold(3, k, 1)  # [b, T*Cin, H, W, k, k]
+            b = cols.shape[0]
+            cols = cols.reshape(b, T, cin, H, W, k * k).permute(0, 3, 4, 1, 2, 5).reshape(b, H, W, T, cin * k * k)
+            out[i:i + chunk, ..., :cin * k * k] = cols
+            out[i:i + chunk, ..., cin * k * k:] = 0
+        t = out.view(n, H, W, T * 32).permute(0, 3, 1, 2)
+        return t if x.is_cuda else t.contiguous()
+
+    def _conv0_col(self, xcol: torch.Tensor) -> torch.Tensor:
+        w = self.conv_w[0]
+        taps = w.shape[1] * self.kernels[0] ** 2
+        wc = F.pad(w.reshape(w.shape[0], taps), (0, 32 - taps)).view(w.shape[0], 32, 1, 1)
+        return gconv.conv2d(xcol, wc, self.conv_b[0], padding=0, groups=self.T)
+
     def _conv(self, i: int, x: torch.Tensor) -> torch.Tensor:
         k, s = self.kernels[i], self.conv_specs[i][1]
+        if USE_HIP_CONV and s == 1 and k % 2 == 1:  # SAME = symmetric pad k//2: grouped MFMA conv when eligible
+            return gconv.conv2d(x, self.conv_w[i], self.conv_b[i], padding=k // 2, groups=self.T)
         return F.conv2d(_same_pad(x, k, s), self.conv_w[i], self.conv_b[i], stride=s, groups=self.T)
 
     def _lrn(self, y: torch.Tensor) -> torch.Tensor:
@@ -83,9 +123,10 @@ class PateEnsemble(nn.Module):
         out = cnn_ops.lrn(v, depth_radius=4, bias=1.0, alpha=0.001 / 9.0, beta=0.75)
         return out.reshape(B, h, w, TC).permute(0, 3, 1, 2)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, col: bool = False) -> torch.Tensor:
+        """`col=True`: x is `conv_input(images)` (the first layer runs as a 1x1 grouped GEMM)."""
         if not self.deeper:
-            y = F.relu(self._conv(0, x))
+            y = F.relu(self._conv0_col(x) if col else self._conv(0, x))
             y = self._lrn(same_maxpool(y, 3, 2))
             y = F.relu(self._conv(1, y))
             y = same_maxpool(self._lrn(y), 3, 2)
@@ -165,6 +206,9 @@ def train_ensemble(shards_x: list[np.ndarray], shards_y: list[np.ndarray], ckpt_
     template = deep_cnn.build_model(cfg)
     ens = PateEnsemble(template, T).to(dev)
     x = _interleave(shards_x, dev).to(ens.conv_w[0].dtype)
+    col = ens.col_input
+    if col:  # im2col image of the resident dataset, built once
+        x = ens.conv_input(x)
     y = torch.as_tensor(np.stack([np.asarray(s) for s in shards_y])).to(dev).long()  # [T, n]
     params = list(ens.parameters())
     nb_ex_per_epoch = int(60000 / cfg.nb_teachers)
@@ -179,7 +223,7 @@ def train_ensemble(shards_x: list[np.ndarray], shards_y: list[np.ndarray], ckpt_
         s, e = deep_cnn.batch_indices(step % nb_batches, n, cfg.batch_size)
         opt.zero_grad()
         with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=amp):
-            logits = ens(x[s:e])  # [T, B, classes]
+            logits = ens(x[s:e], col=col)  # [T, B, classes]
         B = e - s
         # sum over teachers of each teacher's mean loss: teacher t's gradient is its own mean-loss gradient
         loss = cnn_ops.softmax_cross_entropy(logits.float().reshape(T * B, -1), y[:, s:e].reshape(-1),
@@ -235,6 +279,6 @@ def ensemble_softmax_preds(images: np.ndarray, ckpt_paths: list[str], cfg: deep_
         if dev.type != "cuda":
             xb = xb.contiguous()
         with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=dev.type == "cuda"):
-            o = ens(xb).float()
+            o = (ens(ens.conv_input(xb), col=True) if ens.col_input else ens(xb)).float()
         outs.append(F.softmax(o, -1))
     return torch.cat(outs, 1).cpu().numpy().astype(np.float32)

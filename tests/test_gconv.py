@@ -1,0 +1,46 @@
+"""Grouped stride-1 NHWC implicit-GEMM convolution (csrc/gconv.hip) vs an fp32 PyTorch reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mifx.ops import gconv
+
+
+def test_eligibility_rules():
+    x = torch.empty(2, 3 * 64, 8, 8)
+    assert not gconv.eligible(x, torch.empty(3 * 128, 64, 5, 5), 3, 2)  # CPU tensor
+    w = torch.empty(3 * 128, 32, 5, 5)
+    assert not gconv.eligible(torch.empty(2, 96, 8, 8), w, 3, 2)
+
+
+def test_cpu_falls_back_to_f_conv2d():
+    torch.manual_seed(0)
+    x, w, b = torch.randn(2, 6, 7, 7), torch.randn(8, 3, 3, 3), torch.randn(8)
+    torch.testing.assert_close(gconv.conv2d(x, w, b, padding=1, groups=2), F.conv2d(x, w, b, padding=1, groups=2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,G,C,K,R,pad", [(4, 14, 3, 64, 128, 5, 2), (3, 7, 2, 64, 64, 3, 1),
+                                             (2, 9, 1, 64, 64, 3, 0), (5, 6, 4, 128, 64, 5, 2),
+                                             (3, 7, 2, 32, 128, 3, 1), (2, 5, 1, 128, 256, 3, 0),
+                                             (6, 8, 5, 32, 64, 1, 0)])
+def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad):
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(N, G * C, H, H + 1, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (0.05 * torch.randn(G * K, C, R, R, device=dev)).to(torch.bfloat16).float()
+    b = torch.randn(G * K, device=dev)
+    xr, wr, br = x.float().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = F.conv2d(xr, wr, br, padding=pad, groups=G)
+    xk, wk, bk = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    assert gconv.eligible(xk, wk, G, pad)
+    out = gconv.conv2d(xk, wk, bk, padding=pad, groups=G)
+    assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=torch.channels_last)
+    s = ref.abs().max()
+    torch.testing.assert_close(out.float() / s, ref / s, rtol=0, atol=1e-2)
+    dy = torch.randn_like(ref).to(torch.bfloat16)
+    ref.backward(dy.float())
+    out.backward(dy)
+    for got, want in ((xk.grad, xr.grad), (wk.grad, wr.grad), (bk.grad, br.grad)):
+        sc = want.abs().max()
+        torch.testing.assert_close(got.float() / sc, want / sc, rtol=0, atol=1.5e-2)

@@ -114,13 +114,16 @@ def test_all_teachers_cli_and_student(tmp_path):
 
 
 @pytest.mark.gpu
-def test_ensemble_gpu_grads_match_per_teacher_models():
-    """On the GPU (MIOpen grouped NHWC convs, HIP LRN kernel on per-teacher channel blocks, batched dense layers)
-    the ensemble's fp32 logits and gradients equal each teacher's own PateCNN."""
+@pytest.mark.parametrize("hip_conv", [False, True])
+def test_ensemble_gpu_grads_match_per_teacher_models(monkeypatch, hip_conv):
+    """On the GPU (grouped convs, HIP LRN kernel on per-teacher channel blocks, batched dense layers) the ensemble's
+    fp32 logits and gradients equal each teacher's own PateCNN. With the hand-written bf16 grouped MFMA conv
+    (csrc/gconv.hip, checked against fp32 in tests/test_gconv.py) the logits agree to bf16 accuracy."""
     import torch.nn.functional as F
 
     from mifx.privacy.pate import ensemble
 
+    monkeypatch.setattr(ensemble, "USE_HIP_CONV", hip_conv)
     T, B = 5, 16
     cfg = deep_cnn.DeepCNNConfig(nb_teachers=T)
     torch.manual_seed(0)
@@ -140,7 +143,10 @@ def test_ensemble_gpu_grads_match_per_teacher_models():
         m.load_state_dict(states[t])
         m.zero_grad()
         out = m(deep_cnn._to_nchw(xs[t], torch.device("cuda")))
-        torch.testing.assert_close(lo[t], out, rtol=1e-4, atol=1e-4)
+        sc = out.abs().max()
+        torch.testing.assert_close(lo[t].float() / sc, out / sc, rtol=0, atol=2e-2 if hip_conv else 1e-4)
+        if hip_conv:
+            continue
         F.cross_entropy(out, ys[t], reduction="sum").backward()
         gt = ens.teacher_state(t, grads)
         for k, p in m.named_parameters():
