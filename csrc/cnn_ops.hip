@@ -118,6 +118,98 @@ __global__ __launch_bounds__(256) void lrn_bwd(const T* __restrict__ x, const T*
   }
 }
 
+// ---- bf16 rows of C = 8 * LPR channels, radius 4: LPR lanes per row, 8 channels (one 16-byte load) per lane.
+// The 9-channel window needs the 4 nearest channels of each neighbouring lane (8 shuffles); the backward pass
+// recomputes the normaliser from x instead of reading a stored fp32 copy, so forward moves 4 B per element
+// and backward 6 B (the generic kernels above: 8 and 10 B).
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void unpack8(u4v p, float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(p[i] << 16);
+    v[2 * i + 1] = __uint_as_float(p[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ unsigned int bf16_bits(float f) {  // round to nearest even (finite inputs)
+  const unsigned int u = __float_as_uint(f);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ u4v pack8(const float (&v)[8]) {
+  u4v p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) p[i] = bf16_bits(v[2 * i]) | (bf16_bits(v[2 * i + 1]) << 16);
+  return p;
+}
+
+// window sums over [c-4, c+4] of a per-channel quantity q (8 per lane), neighbours' values by shuffle
+template <int LPR>
+__device__ __forceinline__ void window9(const float (&q)[8], int j, float (&out)[8]) {
+  const int lane = threadIdx.x & 63;
+  float ext[16];  // channels 8j-4 .. 8j+11
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float l = __shfl(q[4 + i], lane - 1 < 0 ? 0 : lane - 1);
+    const float r = __shfl(q[i], lane + 1 > 63 ? 63 : lane + 1);
+    ext[i] = j > 0 ? l : 0.f;
+    ext[12 + i] = j < LPR - 1 ? r : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ext[4 + i] = q[i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a += ext[i + k];
+    out[i] = a;
+  }
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void lrn_fwd_v8(const u4v* __restrict__ x, long long M, float bias, float alpha,
+                                                  float beta, u4v* __restrict__ y) {
+  const long long gl = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long row = gl / LPR;
+  const int j = (int)(gl % LPR);
+  const bool live = row < M;
+  float v[8], sq[8], w[8];
+  unpack8(live ? x[gl] : u4v{0, 0, 0, 0}, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sq[i] = v[i] * v[i];
+  window9<LPR>(sq, j, w);
+  float o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = v[i] * __powf(bias + alpha * w[i], -beta);
+  if (live) y[gl] = pack8(o);
+}
+
+// dx_c = dy_c N_c^-beta - 2 alpha beta x_c sum_{|j-c|<=4} dy_j x_j N_j^(-beta-1)
+template <int LPR>
+__global__ __launch_bounds__(256) void lrn_bwd_v8(const u4v* __restrict__ x, const u4v* __restrict__ dy, long long M,
+                                                  float bias, float alpha, float beta, u4v* __restrict__ dx) {
+  const long long gl = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long row = gl / LPR;
+  const int j = (int)(gl % LPR);
+  const bool live = row < M;
+  float v[8], g[8], sq[8], w[8], p[8], t[8], ts[8];
+  unpack8(live ? x[gl] : u4v{0, 0, 0, 0}, v);
+  unpack8(live ? dy[gl] : u4v{0, 0, 0, 0}, g);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sq[i] = v[i] * v[i];
+  window9<LPR>(sq, j, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float N = bias + alpha * w[i];
+    p[i] = __powf(N, -beta);
+    t[i] = g[i] * v[i] * p[i] / N;
+  }
+  window9<LPR>(t, j, ts);
+  float o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = g[i] * p[i] - 2.f * alpha * beta * v[i] * ts[i];
+  if (live) dx[gl] = pack8(o);
+}
+
 // ------------------------------------------------------------------------- SGD + EMA
 struct TensorRef {
   float* w;
@@ -206,6 +298,35 @@ int mifx_cnn_lrn_bwd(int dtype, const void* x, const void* dy, const float* nrm,
   else
     hipLaunchKernelGGL(lrn_bwd<float>, dim3(grid), dim3(256), lds, st, (const float*)x, (const float*)dy, nrm, M, C, r,
                        alpha, beta, (float*)dx);
+  return (int)hipGetLastError();
+}
+
+// bf16, depth radius 4, C in {64, 128}, 16-byte aligned rows: vectorised kernels without a stored normaliser
+int mifx_cnn_lrn_v8_ok(int C, int r) { return (r == 4 && (C == 64 || C == 128)) ? 1 : 0; }
+
+int mifx_cnn_lrn_fwd_v8(const void* x, long long M, int C, float bias, float alpha, float beta, void* y,
+                        hipStream_t st) {
+  if (M < 0 || !mifx_cnn_lrn_v8_ok(C, 4)) return -1;
+  if (M == 0) return 0;
+  const int grid = blocks_for(M * (C / 8), 256);
+  if (C == 64)
+    hipLaunchKernelGGL(lrn_fwd_v8<8>, dim3(grid), dim3(256), 0, st, (const u4v*)x, M, bias, alpha, beta, (u4v*)y);
+  else
+    hipLaunchKernelGGL(lrn_fwd_v8<16>, dim3(grid), dim3(256), 0, st, (const u4v*)x, M, bias, alpha, beta, (u4v*)y);
+  return (int)hipGetLastError();
+}
+
+int mifx_cnn_lrn_bwd_v8(const void* x, const void* dy, long long M, int C, float bias, float alpha, float beta,
+                        void* dx, hipStream_t st) {
+  if (M < 0 || !mifx_cnn_lrn_v8_ok(C, 4)) return -1;
+  if (M == 0) return 0;
+  const int grid = blocks_for(M * (C / 8), 256);
+  if (C == 64)
+    hipLaunchKernelGGL(lrn_bwd_v8<8>, dim3(grid), dim3(256), 0, st, (const u4v*)x, (const u4v*)dy, M, bias, alpha,
+                       beta, (u4v*)dx);
+  else
+    hipLaunchKernelGGL(lrn_bwd_v8<16>, dim3(grid), dim3(256), 0, st, (const u4v*)x, (const u4v*)dy, M, bias, alpha,
+                       beta, (u4v*)dx);
   return (int)hipGetLastError();
 }
 

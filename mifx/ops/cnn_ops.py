@@ -24,6 +24,9 @@ def _fns():
         "lrn_bwd": sig(lib, "mifx_cnn_lrn_bwd", [I32, VP, VP, VP, I64, I32, I32, F32, F32, VP, VP]),
         "chunk": sig(lib, "mifx_cnn_chunk_elems", []),
         "sgd_ema": sig(lib, "mifx_cnn_sgd_ema", [VP, VP, VP, I32, F32, F32, F32, VP]),
+        "lrn_v8_ok": sig(lib, "mifx_cnn_lrn_v8_ok", [I32, I32]),
+        "lrn_fwd_v8": sig(lib, "mifx_cnn_lrn_fwd_v8", [VP, I64, I32, F32, F32, F32, VP, VP]),
+        "lrn_bwd_v8": sig(lib, "mifx_cnn_lrn_bwd_v8", [VP, VP, I64, I32, F32, F32, F32, VP, VP]),
         "tref": sig(lib, "mifx_cnn_tensor_ref_bytes", []),
     }
 
@@ -87,17 +90,32 @@ class _LRN(torch.autograd.Function):
         v = _nhwc(x)
         M, C = v.shape
         y = torch.empty_like(x)
+        if x.dtype == torch.bfloat16 and x.data_ptr() % 16 == 0 and _fns()["lrn_v8_ok"](C, r):
+            # vectorised bf16 kernels; backward recomputes the normaliser (nothing but x is saved)
+            check(_fns()["lrn_fwd_v8"](ptr(v), M, C, bias, alpha, beta, ptr(_nhwc(y)), stream_handle(x.device)),
+                  "mifx_cnn_lrn_fwd_v8")
+            ctx.save_for_backward(x)
+            ctx.args = (r, alpha, beta, bias, True)
+            return y
         nrm = torch.empty(M, C, device=x.device, dtype=torch.float32)
         check(_fns()["lrn_fwd"](_dt(x), ptr(v), M, C, r, bias, alpha, beta, ptr(_nhwc(y)), ptr(nrm),
                                 stream_handle(x.device)), "mifx_cnn_lrn_fwd")
         ctx.save_for_backward(x, nrm)
-        ctx.args = (r, alpha, beta)
+        ctx.args = (r, alpha, beta, bias, False)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        r, alpha, beta, bias, v8 = ctx.args
+        if v8:
+            (x,) = ctx.saved_tensors
+            dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+            dx = torch.empty_like(x)
+            M, C = _nhwc(x).shape
+            check(_fns()["lrn_bwd_v8"](ptr(_nhwc(x)), ptr(_nhwc(dy)), M, C, bias, alpha, beta, ptr(_nhwc(dx)),
+                                       stream_handle(x.device)), "mifx_cnn_lrn_bwd_v8")
+            return dx, None, None, None, None
         x, nrm = ctx.saved_tensors
-        r, alpha, beta = ctx.args
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         M, C = nrm.shape
         dx = torch.empty_like(x)
