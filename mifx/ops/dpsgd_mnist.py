@@ -54,8 +54,12 @@ def per_microbatch_grads(model: torch.nn.Module, x: torch.Tensor, y: torch.Tenso
     ps = [p.detach().contiguous() for _, p in model.named_parameters()]
     xc = x.detach().contiguous()
     yc = y.detach().to(torch.int64).contiguous()
-    G = torch.empty(M, LD, dtype=torch.float32, device=x.device)
+    # One workgroup per example (B workgroups fill the chip even when M is small), then the microbatch sums.
+    rows = B if M < B and B <= 65536 else M
+    G = torch.empty(rows, LD, dtype=torch.float32, device=x.device)
     loss = torch.empty(B, dtype=torch.float32, device=x.device)
-    check(_fns()["grads"](ptr(xc), ptr(yc), B, M, *[ptr(p) for p in ps], ptr(G), LD, ptr(loss),
+    check(_fns()["grads"](ptr(xc), ptr(yc), B, rows, *[ptr(p) for p in ps], ptr(G), LD, ptr(loss),
                           stream_handle(x.device)), "mifx_dpmnist_grads")
+    if rows != M:
+        G = G.view(M, B // M, LD).sum(1)
     return G, loss
