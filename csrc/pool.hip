@@ -1,4 +1,5 @@
-// 3x3 / stride 2 / pad 1 max pooling for NHWC bf16 activations (ResNet-50 stem, BASELINE config 5).
+// 3x3 / stride 2 max pooling for NHWC bf16 activations: the ResNet-50 stem (pad 1, BASELINE config 5) and the
+// PATE CNN's TF-SAME pooling (`deep_cnn.py:123,151`: top/left pad = total // 2, the rest at the bottom/right).
 //
 // PyTorch's NHWC max-pool saves an int64 argmax per OUTPUT element and scatters the backward through it
 // (profiles/resnet50_steady_kernels_s3.md: 252 us fwd + 620 us bwd per step at B=256, 112x112x64). Here:
@@ -25,7 +26,7 @@ struct alignas(8) U8x8 {
 };
 
 __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __restrict__ x, int N, int H, int W, int C,
-                                                       int OH, int OW, __hip_bfloat16* __restrict__ y,
+                                                       int OH, int OW, int pt, int pl, __hip_bfloat16* __restrict__ y,
                                                        uint8_t* __restrict__ idx) {
   const int cg = C / kVec;
   const long long total = (long long)N * OH * OW * cg;
@@ -46,11 +47,11 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __
     bool first = true;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
-      const int ih = 2 * oh - 1 + kh;
+      const int ih = 2 * oh - pt + kh;
       if (ih < 0 || ih >= H) continue;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int iw = 2 * ow - 1 + kw;
+        const int iw = 2 * ow - pl + kw;
         if (iw < 0 || iw >= W) continue;
         const Bf8 v8 = *(const Bf8*)(x + (((size_t)n * H + ih) * W + iw) * C + g * kVec);
 #pragma unroll
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __
 
 __global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __restrict__ dy,
                                                        const uint8_t* __restrict__ idx, int N, int H, int W, int C,
-                                                       int OH, int OW, __hip_bfloat16* __restrict__ dx) {
+                                                       int OH, int OW, int pt, int pl, __hip_bfloat16* __restrict__ dx) {
   const int cg = C / kVec;
   const long long total = (long long)N * H * W * cg;
   for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
@@ -85,9 +86,10 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __
     p /= W;
     const int ih = (int)(p % H);
     const int n = (int)(p / H);
-    // output windows containing ih: 2 oh - 1 <= ih <= 2 oh + 1
-    const int oh0 = ih >> 1, oh1 = (ih & 1) ? oh0 + 1 : oh0;
-    const int ow0 = iw >> 1, ow1 = (iw & 1) ? ow0 + 1 : ow0;
+    // output windows containing ih: 2 oh - pt <= ih <= 2 oh - pt + 2, i.e. oh in [ceil((u - 2) / 2), u / 2], u = ih + pt
+    const int uh = ih + pt, uw = iw + pl;
+    const int oh1 = uh >> 1, oh0 = max(0, (uh - 1) >> 1);
+    const int ow1 = uw >> 1, ow0 = max(0, (uw - 1) >> 1);
     float acc[kVec];
 #pragma unroll
     for (int e = 0; e < kVec; ++e) acc[e] = 0.f;
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __
       for (int b = 0; b < 2; ++b) {
         const int ow = b ? ow1 : ow0;
         if ((b && ow1 == ow0) || ow >= OW) continue;
-        const uint8_t k = (uint8_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+        const uint8_t k = (uint8_t)((ih - (2 * oh - pt)) * 3 + (iw - (2 * ow - pl)));
         const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + g * kVec;
         const U8x8 k8 = *(const U8x8*)(idx + off);
         const Bf8 d8 = *(const Bf8*)(dy + off);
@@ -125,21 +127,36 @@ int grid_for(long long total) {
 
 extern "C" {
 
-// x, y, dx: NHWC bf16 (channels_last), C % 8 == 0, 16-byte aligned; idx: [N, OH, OW, C] uint8
-int mifx_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* y, void* idx, hipStream_t st) {
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec) return -1;
-  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+// x, y, dx: NHWC bf16 (channels_last), C % 8 == 0, 16-byte aligned; idx: [N, OH, OW, C] uint8. Window (oh, ow)
+// covers rows 2 oh - pt .. 2 oh - pt + 2 (columns likewise with pl); taps outside the image never win, and every
+// window must hold at least one tap of the image.
+int mifx_maxpool3s2p_fwd(const void* x, int N, int H, int W, int C, int pt, int pl, int OH, int OW, void* y, void* idx,
+                         hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec || pt < 0 || pt > 2 || pl < 0 || pl > 2 || OH <= 0 ||
+      OW <= 0 || 2 * (OH - 1) - pt >= H || 2 * (OW - 1) - pl >= W)
+    return -1;
   hipLaunchKernelGGL(maxpool_fwd, dim3(grid_for((long long)N * OH * OW * (C / kVec))), dim3(kThreads), 0, st,
-                     (const __hip_bfloat16*)x, N, H, W, C, OH, OW, (__hip_bfloat16*)y, (uint8_t*)idx);
+                     (const __hip_bfloat16*)x, N, H, W, C, OH, OW, pt, pl, (__hip_bfloat16*)y, (uint8_t*)idx);
   return (int)hipGetLastError();
 }
 
-int mifx_maxpool3s2_bwd(const void* dy, const void* idx, int N, int H, int W, int C, void* dx, hipStream_t st) {
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec) return -1;
-  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+int mifx_maxpool3s2p_bwd(const void* dy, const void* idx, int N, int H, int W, int C, int pt, int pl, int OH, int OW,
+                         void* dx, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec || pt < 0 || pt > 2 || pl < 0 || pl > 2 || OH <= 0 ||
+      OW <= 0)
+    return -1;
   hipLaunchKernelGGL(maxpool_bwd, dim3(grid_for((long long)N * H * W * (C / kVec))), dim3(kThreads), 0, st,
-                     (const __hip_bfloat16*)dy, (const uint8_t*)idx, N, H, W, C, OH, OW, (__hip_bfloat16*)dx);
+                     (const __hip_bfloat16*)dy, (const uint8_t*)idx, N, H, W, C, OH, OW, pt, pl, (__hip_bfloat16*)dx);
   return (int)hipGetLastError();
+}
+
+// ResNet stem: pad 1, OH = (H - 1) / 2 + 1
+int mifx_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* y, void* idx, hipStream_t st) {
+  return mifx_maxpool3s2p_fwd(x, N, H, W, C, 1, 1, (H - 1) / 2 + 1, (W - 1) / 2 + 1, y, idx, st);
+}
+
+int mifx_maxpool3s2_bwd(const void* dy, const void* idx, int N, int H, int W, int C, void* dx, hipStream_t st) {
+  return mifx_maxpool3s2p_bwd(dy, idx, N, H, W, C, 1, 1, (H - 1) / 2 + 1, (W - 1) / 2 + 1, dx, st);
 }
 
 }  // extern "C"

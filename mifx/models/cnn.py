@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops import cnn_ops
+from ..ops import cnn_ops, pool
 
 
 def _same_pad(x: torch.Tensor, k: int, s: int, value: float = 0.0) -> torch.Tensor:
@@ -40,6 +40,10 @@ class SameConv2d(nn.Conv2d):
 
 
 def same_maxpool(x, k, s):
+    if k == 3 and s == 2:  # NHWC bf16 on the GPU: HIP kernels (csrc/pool.hip), 1-byte argmax
+        y = pool.max_pool3s2_same(x)
+        if y is not None:
+            return y
     return F.max_pool2d(_same_pad(x, k, s, value=-math.inf), k, s)
 
 

@@ -183,7 +183,7 @@ def test_resnet_fused_blocks_match_fp64_reference():
 def test_maxpool3s2_matches_pytorch(shape):
     """HIP 3x3/s2/p1 NHWC max-pool (1-byte argmax, gather backward) vs F.max_pool2d: identical forward, and
     the backward equal to PyTorch's (ties are avoided by distinct values so both pick the same position)."""
-    from mifx.ops.pool import _MaxPool3s2, native_ok
+    from mifx.ops.pool import max_pool3s2, native_ok
 
     torch.manual_seed(0)
     N, C, H, W = shape
@@ -193,7 +193,7 @@ def test_maxpool3s2_matches_pytorch(shape):
     assert native_ok(x)
     xa = x.detach().requires_grad_()
     xb = x.detach().float().requires_grad_()
-    ya = _MaxPool3s2.apply(xa)
+    ya = max_pool3s2(xa)
     yb = torch.nn.functional.max_pool2d(xb, 3, 2, 1)
     assert ya.shape == yb.shape and ya.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(ya.float(), yb, rtol=0, atol=0)
@@ -230,7 +230,7 @@ def test_fused_bn_large_mean_variance_vs_fp64():
 @pytest.mark.gpu
 def test_maxpool3s2_nan_routing_matches_pytorch():
     """Several NaNs in one window: forward NaN and the gradient routed to the LAST NaN (PyTorch's rule)."""
-    from mifx.ops.pool import _MaxPool3s2
+    from mifx.ops.pool import max_pool3s2
 
     x = torch.randn(1, 8, 6, 6, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     x[0, :, 1, 1] = float("nan")
@@ -238,10 +238,37 @@ def test_maxpool3s2_nan_routing_matches_pytorch():
     x[0, :, 4, 3] = float("nan")
     xa = x.detach().requires_grad_()
     xb = x.detach().float().requires_grad_()
-    ya = _MaxPool3s2.apply(xa)
+    ya = max_pool3s2(xa)
     yb = torch.nn.functional.max_pool2d(xb, 3, 2, 1)
     assert torch.equal(torch.isnan(ya.float()), torch.isnan(yb))
     g = torch.ones_like(yb)
     ya.backward(g.bfloat16().contiguous(memory_format=torch.channels_last))
     yb.backward(g)
     torch.testing.assert_close(xa.grad.float(), xb.grad, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 64, 28, 28), (3, 16, 14, 14), (2, 8, 7, 9)])
+def test_maxpool3s2_tf_same_matches_padded_pytorch(shape):
+    """TF-SAME 3x3/2 pooling of the PATE CNN (asymmetric padding) on the HIP kernels == F.max_pool2d over the
+    -inf-padded input, forward and backward."""
+    import math
+
+    from mifx.models.cnn import _same_pad
+    from mifx.ops.pool import max_pool3s2_same
+
+    torch.manual_seed(1)
+    N, C, H, W = shape
+    vals = torch.randperm(N * C * H * W, device="cuda").float() / (N * C * H * W)
+    x = (vals.view(N, C, H, W) * 256).round().bfloat16().contiguous(memory_format=torch.channels_last)
+    xa = x.detach().requires_grad_()
+    xb = x.detach().float().requires_grad_()
+    ya = max_pool3s2_same(xa)
+    yb = torch.nn.functional.max_pool2d(_same_pad(xb, 3, 2, value=-math.inf), 3, 2)
+    assert ya is not None and ya.shape == yb.shape
+    torch.testing.assert_close(ya.float(), yb, rtol=0, atol=0)
+    g = torch.randn_like(yb).bfloat16().float()
+    ya.backward(g.bfloat16().contiguous(memory_format=torch.channels_last))
+    yb.backward(g)
+    same = xa.grad.float() == xb.grad.bfloat16().float()
+    assert same.float().mean() > 0.999
