@@ -165,6 +165,10 @@ __device__ __forceinline__ void window9(const float (&q)[8], int j, float (&out)
   }
 }
 
+// N^-beta with the native v_log_f32 / v_exp_f32 (N >= bias > 0); __powf lowers to the full-precision
+// library pow here (~1600 instructions per 8 channels), which made these kernels instruction-bound
+__device__ __forceinline__ float npow(float N, float nb) { return __builtin_amdgcn_exp2f(nb * __builtin_amdgcn_logf(N)); }
+
 template <int LPR>
 __global__ __launch_bounds__(256) void lrn_fwd_v8(const u4v* __restrict__ x, long long M, float bias, float alpha,
                                                   float beta, u4v* __restrict__ y) {
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(256) void lrn_fwd_v8(const u4v* __restrict__ x, lon
   window9<LPR>(sq, j, w);
   float o[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = v[i] * __powf(bias + alpha * w[i], -beta);
+  for (int i = 0; i < 8; ++i) o[i] = v[i] * npow(bias + alpha * w[i], -beta);
   if (live) y[gl] = pack8(o);
 }
 
@@ -200,8 +204,8 @@ __global__ __launch_bounds__(256) void lrn_bwd_v8(const u4v* __restrict__ x, con
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const float N = bias + alpha * w[i];
-    p[i] = __powf(N, -beta);
-    t[i] = g[i] * v[i] * p[i] / N;
+    p[i] = npow(N, -beta);
+    t[i] = g[i] * v[i] * p[i] * __builtin_amdgcn_rcpf(N);
   }
   window9<LPR>(t, j, ts);
   float o[8];

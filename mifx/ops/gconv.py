@@ -75,7 +75,12 @@ class _GConv(torch.autograd.Function):
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=1, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
-            if C in (32, 64, 128):  # hand-written weight gradient (fp32 out, PyTorch layout)
+            if R == 1 and S == 1 and pad == 0:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
+                M = N * Ho * Wo
+                dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
+                xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
+                dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
+            elif C in (32, 64, 128):  # hand-written weight gradient (fp32 out, PyTorch layout)
                 dw = torch.empty(G * K, C, R, S, device=dyb.device, dtype=torch.float32)
                 check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad,
                                       stream_handle(dyb.device)), "mifx_gconv_wgrad")
@@ -84,7 +89,7 @@ class _GConv(torch.autograd.Function):
                 dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=1, padding=pad,
                                                  groups=G).to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
-            db = dyb.float().sum((0, 2, 3)).to(bdt)
+            db = torch.sum(dyb, dim=(0, 2, 3), dtype=torch.float32).to(bdt)
         return dx, dw, db, None, None
 
 

@@ -52,8 +52,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--teachers", default="10,50,250")
+    ap.add_argument("--no-sequential", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
-    print(json.dumps(run_sequential(a.steps, dev)), flush=True)
+    if not a.no_sequential:
+        print(json.dumps(run_sequential(a.steps, dev)), flush=True)
     for T in [int(t) for t in a.teachers.split(",")]:
         print(json.dumps(run(T, a.steps, dev)), flush=True)
