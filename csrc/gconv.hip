@@ -40,10 +40,13 @@ struct Geo {
 
 template <int BN>
 __global__ __launch_bounds__(kThreads) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                      const float* __restrict__ bias, bf16* __restrict__ y, Geo d) {
+                                                      const float* __restrict__ bias, bf16* __restrict__ y, Geo d,
+                                                      int relu) {
   constexpr int BCH = BN * 4 / kThreads;  // 16-byte weight chunks per thread per step (2 or 1)
-  __shared__ __attribute__((aligned(16))) bf16 As[2][BM * LDR];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * LDR];
+  // one LDS block: double-buffered A and B staging, reused as the epilogue's output tile
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BM * LDR + 2 * BN * LDR];
+  bf16(*As)[BM * LDR] = reinterpret_cast<bf16(*)[BM * LDR]>(smem);
+  bf16(*Bs)[BN * LDR] = reinterpret_cast<bf16(*)[BN * LDR]>(smem + 2 * BM * LDR);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = blockIdx.z, n0 = blockIdx.y * BN;
   const long long M = (long long)d.N * d.Ho * d.Wo;
@@ -124,19 +127,32 @@ __global__ __launch_bounds__(kThreads) void gconv_fwd(const bf16* __restrict__ x
     __syncthreads();
   }
 
-  // epilogue: acc[i][j][e] = y[pixel m0 + wm + 16 i + 4 (lane >> 4) + e][channel n0 + wn + 16 j + (lane & 15)]
-  const int KT = d.G * d.K;
+  // epilogue: acc[i][j][e] = y[pixel m0 + wm + 16 i + 4 (lane >> 4) + e][channel n0 + wn + 16 j + (lane & 15)].
+  // (+ bias, optional ReLU) -> bf16 tile in LDS (the staging buffers are free after the last barrier), then
+  // 16-byte coalesced row stores: a pixel's BN channels are contiguous in y.
+  constexpr int CLD = BN + 8;
+  static_assert(BM * CLD <= 2 * BM * LDR + 2 * BN * LDR, "epilogue tile fits the staging buffers");
+  bf16* Cs = smem;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int k = n0 + wn + 16 * j + fr;
-    const float b = bias ? bias[g * d.K + k] : 0.f;
+    const int cl = wn + 16 * j + fr;
+    const float b = bias ? bias[g * d.K + n0 + cl] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const long long m = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
-        if (m < M) y[m * KT + g * d.K + k] = (bf16)(acc[i][j][e] + b);
+        float v = acc[i][j][e] + b;
+        if (relu) v = fmaxf(v, 0.f);
+        Cs[(wm + 16 * i + 4 * (lane >> 4) + e) * CLD + cl] = (bf16)v;
       }
+  }
+  __syncthreads();
+  const int KT = d.G * d.K;
+  constexpr int CPR = BN / 8;  // 16-byte chunks per pixel row
+  for (int c = t; c < BM * CPR; c += kThreads) {
+    const int row = c / CPR, part = (c % CPR) * 8;
+    const long long m = m0 + row;
+    if (m < M) *(u4*)(y + m * KT + g * d.K + n0 + part) = *(const u4*)(&Cs[row * CLD + part]);
   }
 }
 
@@ -271,9 +287,10 @@ int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, in
 }
 
 // x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
-// stride 1, zero padding `pad` on every side, Ho = Hi + 2 pad - R + 1. Needs C % 32 == 0 and K % 64 == 0.
+// stride 1, zero padding `pad` on every side, Ho = Hi + 2 pad - R + 1, relu != 0: y = max(y, 0).
+// Needs C % 32 == 0 and K % 64 == 0.
 int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
-                   int K, int R, int S, int pad, hipStream_t st) {
+                   int K, int R, int S, int pad, int relu, hipStream_t st) {
   const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
   if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 64 != 0 || Ho <= 0 || Wo <= 0 ||
       pad < 0 || pad >= R || pad >= S)
@@ -284,10 +301,10 @@ int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int
   if (mt > 0x7fffffffLL) return -1;
   if (K % 128 == 0) {
     hipLaunchKernelGGL(gconv_fwd<128>, dim3((unsigned)mt, K / 128, G), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d);
+                       (const bf16*)w, bias, (bf16*)y, d, relu);
   } else {
     hipLaunchKernelGGL(gconv_fwd<64>, dim3((unsigned)mt, K / 64, G), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d);
+                       (const bf16*)w, bias, (bf16*)y, d, relu);
   }
   return (int)hipGetLastError();
 }

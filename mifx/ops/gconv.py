@@ -21,7 +21,7 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 @functools.lru_cache(maxsize=None)
 def _fns():
     lib = _lib.load("gconv")
-    return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 9 + [VP]),
+    return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 10 + [VP]),
             "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 9 + [VP])}
 
 
@@ -36,17 +36,18 @@ def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int) -
     return C % 32 == 0 and K % 64 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
 
 
-def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad) -> torch.Tensor:
+def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad,
+            relu: bool = False) -> torch.Tensor:
     Ho, Wo = Hi + 2 * pad - R + 1, Wi + 2 * pad - S + 1
     y = torch.empty(N, G * K, Ho, Wo, device=x_nhwc.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
-    check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad,
+    check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(relu),
                         stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
     return y
 
 
 class _GConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, pad, groups):
+    def forward(ctx, x, weight, bias, pad, groups, relu):
         N, _, Hi, Wi = x.shape
         GK, C, R, S = weight.shape
         G, K = groups, GK // groups
@@ -54,17 +55,20 @@ class _GConv(torch.autograd.Function):
         wb = weight.to(torch.bfloat16)
         w_fwd = wb.view(G, K, C, R, S).permute(0, 1, 3, 4, 2).contiguous()  # [G][K][R][S][C]
         b = bias.float().contiguous() if bias is not None else None
-        y = _launch(xb, w_fwd, b, N, Hi, Wi, G, C, K, R, S, pad)
-        ctx.save_for_backward(xb, wb)
+        y = _launch(xb, w_fwd, b, N, Hi, Wi, G, C, K, R, S, pad, relu)
+        ctx.save_for_backward(xb, wb, y if relu else None)
         ctx.geo = (N, Hi, Wi, G, C, K, R, S, pad, bias is not None, weight.dtype,
                    bias.dtype if bias is not None else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xb, wb = ctx.saved_tensors
+        xb, wb, y = ctx.saved_tensors
         N, Hi, Wi, G, C, K, R, S, pad, has_bias, wdt, bdt = ctx.geo
-        dyb = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dyb = dy.to(torch.bfloat16)
+        if y is not None:  # fused ReLU: gradient through max(., 0)
+            dyb = torch.ops.aten.threshold_backward(dyb, y, 0)
+        dyb = dyb.contiguous(memory_format=torch.channels_last)
         Ho, Wo = dyb.shape[2], dyb.shape[3]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -90,13 +94,15 @@ class _GConv(torch.autograd.Function):
                                                  groups=G).to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = torch.sum(dyb, dim=(0, 2, 3), dtype=torch.float32).to(bdt)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0,
-           groups: int = 1) -> torch.Tensor:
-    """Stride-1 (grouped) convolution; the HIP kernels when `eligible`, else F.conv2d. Output bf16 channels-last
-    on the kernel path (the dtype F.conv2d gives under bf16 autocast)."""
+           groups: int = 1, relu: bool = False) -> torch.Tensor:
+    """Stride-1 (grouped) convolution (`relu=True`: followed by ReLU, fused into the kernel's epilogue); the HIP
+    kernels when `eligible`, else F.conv2d. Output bf16 channels-last on the kernel path (the dtype F.conv2d gives
+    under bf16 autocast)."""
     if eligible(x, weight, groups, padding) and _lib.gpu_available():
-        return _GConv.apply(x, weight, bias, int(padding), int(groups))
-    return F.conv2d(x, weight, bias, stride=1, padding=padding, groups=groups)
+        return _GConv.apply(x, weight, bias, int(padding), int(groups), bool(relu))
+    y = F.conv2d(x, weight, bias, stride=1, padding=padding, groups=groups)
+    return F.relu(y) if relu else y

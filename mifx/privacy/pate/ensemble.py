@@ -100,17 +100,18 @@ class PateEnsemble(nn.Module):
         t = out.view(n, H, W, T * 32).permute(0, 3, 1, 2)
         return t if x.is_cuda else t.contiguous()
 
-    def _conv0_col(self, xcol: torch.Tensor) -> torch.Tensor:
+    def _conv0_col(self, xcol: torch.Tensor, relu: bool = False) -> torch.Tensor:
         w = self.conv_w[0]
         taps = w.shape[1] * self.kernels[0] ** 2
         wc = F.pad(w.reshape(w.shape[0], taps), (0, 32 - taps)).view(w.shape[0], 32, 1, 1)
-        return gconv.conv2d(xcol, wc, self.conv_b[0], padding=0, groups=self.T)
+        return gconv.conv2d(xcol, wc, self.conv_b[0], padding=0, groups=self.T, relu=relu)
 
-    def _conv(self, i: int, x: torch.Tensor) -> torch.Tensor:
+    def _conv(self, i: int, x: torch.Tensor, relu: bool = False) -> torch.Tensor:
         k, s = self.kernels[i], self.conv_specs[i][1]
         if USE_HIP_CONV and s == 1 and k % 2 == 1:  # SAME = symmetric pad k//2: grouped MFMA conv when eligible
-            return gconv.conv2d(x, self.conv_w[i], self.conv_b[i], padding=k // 2, groups=self.T)
-        return F.conv2d(_same_pad(x, k, s), self.conv_w[i], self.conv_b[i], stride=s, groups=self.T)
+            return gconv.conv2d(x, self.conv_w[i], self.conv_b[i], padding=k // 2, groups=self.T, relu=relu)
+        y = F.conv2d(_same_pad(x, k, s), self.conv_w[i], self.conv_b[i], stride=s, groups=self.T)
+        return F.relu(y) if relu else y
 
     def _lrn(self, y: torch.Tensor) -> torch.Tensor:
         """tf.nn.lrn(4, 1, 0.001/9, 0.75) over each teacher's own channel block: the NHWC rows of every
@@ -126,14 +127,14 @@ class PateEnsemble(nn.Module):
     def forward(self, x: torch.Tensor, col: bool = False) -> torch.Tensor:
         """`col=True`: x is `conv_input(images)` (the first layer runs as a 1x1 grouped GEMM)."""
         if not self.deeper:
-            y = F.relu(self._conv0_col(x) if col else self._conv(0, x))
+            y = self._conv0_col(x, relu=True) if col else self._conv(0, x, relu=True)
             y = self._lrn(same_maxpool(y, 3, 2))
-            y = F.relu(self._conv(1, y))
+            y = self._conv(1, y, relu=True)
             y = same_maxpool(self._lrn(y), 3, 2)
         else:
             y = x
             for i in range(len(self.conv_specs)):
-                y = F.relu(self._conv(i, y))
+                y = self._conv(i, y, relu=True)
         B, TC, h, w = y.shape
         z = y.reshape(B, self.T, (TC // self.T) * h * w).transpose(0, 1)  # per-teacher NCHW flatten
         n = len(self.fc_w)

@@ -20,11 +20,12 @@ def test_cpu_falls_back_to_f_conv2d():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("N,H,G,C,K,R,pad", [(4, 14, 3, 64, 128, 5, 2), (3, 7, 2, 64, 64, 3, 1),
                                              (2, 9, 1, 64, 64, 3, 0), (5, 6, 4, 128, 64, 5, 2),
                                              (3, 7, 2, 32, 128, 3, 1), (2, 5, 1, 128, 256, 3, 0),
                                              (6, 8, 5, 32, 64, 1, 0)])
-def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad):
+def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad, relu):
     torch.manual_seed(0)
     dev = "cuda"
     x = torch.randn(N, G * C, H, H + 1, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -32,9 +33,11 @@ def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad):
     b = torch.randn(G * K, device=dev)
     xr, wr, br = x.float().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
     ref = F.conv2d(xr, wr, br, padding=pad, groups=G)
+    if relu:
+        ref = F.relu(ref)
     xk, wk, bk = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
     assert gconv.eligible(xk, wk, G, pad)
-    out = gconv.conv2d(xk, wk, bk, padding=pad, groups=G)
+    out = gconv.conv2d(xk, wk, bk, padding=pad, groups=G, relu=relu)
     assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=torch.channels_last)
     s = ref.abs().max()
     torch.testing.assert_close(out.float() / s, ref / s, rtol=0, atol=1e-2)
