@@ -168,3 +168,15 @@ def test_ensemble_gpu_training_learns(tmp_path):
     preds = ensemble.ensemble_softmax_preds(xte, [f"{c}-59" for c in ck], cfg, device="cuda")
     assert preds.shape == (T, 256, 10)
     assert min(float((p.argmax(1) == yte).mean()) for p in preds) > 0.5
+
+
+def test_all_teachers_split_across_ranks(tmp_path, monkeypatch):
+    """Under a multi-process launch rank r trains teachers r, r + W, ... and writes exactly their checkpoints."""
+    common = ["--dataset", "mnist", "--train_dir", str(tmp_path), "--train_size", "400", "--test_size", "64",
+              "--max_steps", "3", "--device", "cpu", "--batch_size", "32"]
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    precisions = train_teachers.main(common + ["--nb_teachers", "4", "--teacher_id", "-1"])
+    assert len(precisions) == 2
+    names = sorted(p.name for p in tmp_path.glob("mnist_4_teachers_*.ckpt-2"))
+    assert names == ["mnist_4_teachers_1.ckpt-2", "mnist_4_teachers_3.ckpt-2"]
