@@ -38,8 +38,10 @@ struct Geo {
   int N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad;
 };
 
+// amdgpu_waves_per_eu(4): 4 workgroups per CU (40 KB LDS each) -- the loop is latency-bound, occupancy pays
+// (profiles/gconv_bk_ab_r2.txt, gconv_prefetch_ab_r2.txt: deeper prefetch / wider chunks that cost occupancy lose)
 template <int BN>
-__global__ __launch_bounds__(kThreads) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                       const float* __restrict__ bias, bf16* __restrict__ y, Geo d,
                                                       int relu) {
   constexpr int BCH = BN * 4 / kThreads;  // 16-byte weight chunks per thread per step (2 or 1)
