@@ -178,7 +178,7 @@ __device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
   return __builtin_bit_cast(v8bf, r);
 }
 
-__global__ __launch_bounds__(kThreads) void gconv_wgrad(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_wgrad(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                         float* __restrict__ dw, Geo d) {
   __shared__ __attribute__((aligned(16))) bf16 As[2][32 * WLD];  // dy chunk [pixel][k]
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][32 * WLD];  // x chunk [pixel][(tap, c)]
