@@ -71,20 +71,25 @@ class _GConv(torch.autograd.Function):
         dyb = dyb.contiguous(memory_format=torch.channels_last)
         Ho, Wo = dyb.shape[2], dyb.shape[3]
         dx = dw = db = None
+        M = N * Ho * Wo
         if ctx.needs_input_grad[0]:
-            if C % 64 == 0 and R == S:
+            # HIP input gradient for grouped / large-image convs; MIOpen's is as fast or faster on small
+            # single-group images (profiles/gconv_resnet_r2.jsonl)
+            if C % 64 == 0 and R == S and (G > 1 or M >= 100_000):
                 # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
                 w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
                 dx = _launch(dyb, w_bwd, None, N, Ho, Wo, G, K, C, R, S, R - 1 - pad)
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=1, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
+            tpb = 128 // C if C in (32, 64, 128) else 0
+            wg_blocks = ((R * S + tpb - 1) // tpb) * ((K + 127) // 128) * G if tpb else 0
             if R == 1 and S == 1 and pad == 0:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
-                M = N * Ho * Wo
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
                 dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
-            elif C in (32, 64, 128):  # hand-written weight gradient (fp32 out, PyTorch layout)
+            elif wg_blocks >= 256:  # hand-written weight gradient (fp32 out, PyTorch layout); it has no split over
+                # pixels, so it needs many (tap, k, group) tiles to fill the chip -- else MIOpen's
                 dw = torch.empty(G * K, C, R, S, device=dyb.device, dtype=torch.float32)
                 check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad,
                                       stream_handle(dyb.device)), "mifx_gconv_wgrad")
