@@ -17,6 +17,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kVec = 8;  // channels per thread (16 bytes of bf16)
+constexpr uint8_t kNone = 255;  // window position of a window that passes no gradient (fused ReLU)
 
 struct alignas(16) Bf8 {
   __hip_bfloat16 v[kVec];
@@ -26,8 +27,8 @@ struct alignas(8) U8x8 {
 };
 
 __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __restrict__ x, int N, int H, int W, int C,
-                                                       int OH, int OW, int pt, int pl, __hip_bfloat16* __restrict__ y,
-                                                       uint8_t* __restrict__ idx) {
+                                                       int OH, int OW, int pt, int pl, int relu,
+                                                       __hip_bfloat16* __restrict__ y, uint8_t* __restrict__ idx) {
   const int cg = C / kVec;
   const long long total = (long long)N * OH * OW * cg;
   for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
@@ -63,6 +64,15 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __
           }
         }
         first = false;
+      }
+    }
+    if (relu) {  // relu(max) == max(relu): windows whose max is <= 0 (or NaN) pass no gradient (idx kNone)
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        if (!(m[e] > 0.f)) {
+          k8.v[e] = kNone;
+          if (m[e] == m[e]) m[e] = 0.f;
+        }
       }
     }
     Bf8 o;
@@ -127,16 +137,17 @@ int grid_for(long long total) {
 
 extern "C" {
 
-// x, y, dx: NHWC bf16 (channels_last), C % 8 == 0, 16-byte aligned; idx: [N, OH, OW, C] uint8. Window (oh, ow)
+// x, y, dx: NHWC bf16 (channels_last), C % 8 == 0, 16-byte aligned; idx: [N, OH, OW, C] uint8. relu != 0: the pool
+// of relu(x) (y = max(window max, 0); a window whose max is <= 0 routes no gradient). Window (oh, ow)
 // covers rows 2 oh - pt .. 2 oh - pt + 2 (columns likewise with pl); taps outside the image never win, and every
 // window must hold at least one tap of the image.
-int mifx_maxpool3s2p_fwd(const void* x, int N, int H, int W, int C, int pt, int pl, int OH, int OW, void* y, void* idx,
-                         hipStream_t st) {
+int mifx_maxpool3s2p_fwd(const void* x, int N, int H, int W, int C, int pt, int pl, int OH, int OW, int relu, void* y,
+                         void* idx, hipStream_t st) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec || pt < 0 || pt > 2 || pl < 0 || pl > 2 || OH <= 0 ||
       OW <= 0 || 2 * (OH - 1) - pt >= H || 2 * (OW - 1) - pl >= W)
     return -1;
   hipLaunchKernelGGL(maxpool_fwd, dim3(grid_for((long long)N * OH * OW * (C / kVec))), dim3(kThreads), 0, st,
-                     (const __hip_bfloat16*)x, N, H, W, C, OH, OW, pt, pl, (__hip_bfloat16*)y, (uint8_t*)idx);
+                     (const __hip_bfloat16*)x, N, H, W, C, OH, OW, pt, pl, relu, (__hip_bfloat16*)y, (uint8_t*)idx);
   return (int)hipGetLastError();
 }
 
@@ -152,7 +163,7 @@ int mifx_maxpool3s2p_bwd(const void* dy, const void* idx, int N, int H, int W, i
 
 // ResNet stem: pad 1, OH = (H - 1) / 2 + 1
 int mifx_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* y, void* idx, hipStream_t st) {
-  return mifx_maxpool3s2p_fwd(x, N, H, W, C, 1, 1, (H - 1) / 2 + 1, (W - 1) / 2 + 1, y, idx, st);
+  return mifx_maxpool3s2p_fwd(x, N, H, W, C, 1, 1, (H - 1) / 2 + 1, (W - 1) / 2 + 1, 0, y, idx, st);
 }
 
 int mifx_maxpool3s2_bwd(const void* dy, const void* idx, int N, int H, int W, int C, void* dx, hipStream_t st) {

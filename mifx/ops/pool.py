@@ -15,7 +15,7 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 @functools.lru_cache(maxsize=None)
 def _fns():
     lib = _lib.load("pool")
-    return {"fwd": sig(lib, "mifx_maxpool3s2p_fwd", [VP] + [I32] * 8 + [VP, VP, VP]),
+    return {"fwd": sig(lib, "mifx_maxpool3s2p_fwd", [VP] + [I32] * 9 + [VP, VP, VP]),
             "bwd": sig(lib, "mifx_maxpool3s2p_bwd", [VP, VP] + [I32] * 8 + [VP, VP])}
 
 
@@ -30,11 +30,11 @@ def _out_hw(H: int, W: int) -> tuple[int, int]:
 
 class _MaxPool3s2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, pt, pl, OH, OW):
+    def forward(ctx, x, pt, pl, OH, OW, relu=False):
         N, C, H, W = x.shape
         y = torch.empty((N, C, OH, OW), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
         idx = torch.empty((N, OH, OW, C), device=x.device, dtype=torch.uint8)
-        check(_fns()["fwd"](ptr(x), N, H, W, C, pt, pl, OH, OW, ptr(y), ptr(idx), stream_handle(x.device)),
+        check(_fns()["fwd"](ptr(x), N, H, W, C, pt, pl, OH, OW, int(relu), ptr(y), ptr(idx), stream_handle(x.device)),
               "mifx_maxpool3s2p_fwd")
         ctx.save_for_backward(idx)
         ctx.shape = (N, C, H, W, pt, pl, OH, OW)
@@ -48,7 +48,7 @@ class _MaxPool3s2(torch.autograd.Function):
         dx = torch.empty((N, C, H, W), device=dy.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
         check(_fns()["bwd"](ptr(dy), ptr(idx), N, H, W, C, pt, pl, OH, OW, ptr(dx), stream_handle(dy.device)),
               "mifx_maxpool3s2p_bwd")
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
 def max_pool3s2(x: torch.Tensor) -> torch.Tensor:
@@ -65,9 +65,10 @@ def same_pads(H: int) -> tuple[int, int]:
     return out, max((out - 1) * 2 + 3 - H, 0) // 2
 
 
-def max_pool3s2_same(x: torch.Tensor) -> torch.Tensor | None:
-    """TF-SAME 3x3/2 max pool (padding never wins) on the HIP kernels for NHWC bf16; None when not applicable."""
+def max_pool3s2_same(x: torch.Tensor, relu: bool = False) -> torch.Tensor | None:
+    """TF-SAME 3x3/2 max pool (padding never wins) of x, or of relu(x) with `relu` (one pass each way: the ReLU's
+    backward mask comes free from the window max), on the HIP kernels for NHWC bf16; None when not applicable."""
     if not native_ok(x):
         return None
     (OH, pt), (OW, pl) = same_pads(x.shape[2]), same_pads(x.shape[3])
-    return _MaxPool3s2.apply(x, pt, pl, OH, OW)
+    return _MaxPool3s2.apply(x, pt, pl, OH, OW, bool(relu))

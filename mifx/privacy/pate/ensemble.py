@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...models.cnn import _same_pad, same_maxpool
-from ...ops import cnn_ops, gconv
+from ...ops import cnn_ops, gconv, pool
 from . import deep_cnn
 
 
@@ -127,8 +127,9 @@ class PateEnsemble(nn.Module):
     def forward(self, x: torch.Tensor, col: bool = False) -> torch.Tensor:
         """`col=True`: x is `conv_input(images)` (the first layer runs as a 1x1 grouped GEMM)."""
         if not self.deeper:
-            y = self._conv0_col(x, relu=True) if col else self._conv(0, x, relu=True)
-            y = self._lrn(same_maxpool(y, 3, 2))
+            y = self._conv0_col(x) if col else self._conv(0, x)
+            p = pool.max_pool3s2_same(y, relu=True)  # relu + SAME max-pool in one HIP pass each way
+            y = self._lrn(p if p is not None else same_maxpool(F.relu(y), 3, 2))
             y = self._conv(1, y, relu=True)
             y = same_maxpool(self._lrn(y), 3, 2)
         else:

@@ -272,3 +272,27 @@ def test_maxpool3s2_tf_same_matches_padded_pytorch(shape):
     yb.backward(g)
     same = xa.grad.float() == xb.grad.bfloat16().float()
     assert same.float().mean() > 0.999
+
+
+@pytest.mark.gpu
+def test_maxpool3s2_same_fused_relu_matches_relu_then_pool():
+    """relu + TF-SAME 3x3/2 pool in one kernel == F.relu then the padded F.max_pool2d, forward and backward
+    (negative-only windows pass no gradient)."""
+    import math
+
+    from mifx.models.cnn import _same_pad
+    from mifx.ops.pool import max_pool3s2_same
+
+    torch.manual_seed(2)
+    N, C, H, W = 2, 16, 28, 28
+    vals = torch.randperm(N * C * H * W, device="cuda").float() / (N * C * H * W) - 0.7  # mostly negative
+    x = (vals.view(N, C, H, W) * 256).round().bfloat16().contiguous(memory_format=torch.channels_last)
+    xa = x.detach().requires_grad_()
+    xb = x.detach().float().requires_grad_()
+    ya = max_pool3s2_same(xa, relu=True)
+    yb = torch.nn.functional.max_pool2d(_same_pad(torch.relu(xb), 3, 2, value=-math.inf), 3, 2)
+    torch.testing.assert_close(ya.float(), yb, rtol=0, atol=0)
+    g = torch.randn_like(yb).bfloat16().float()
+    ya.backward(g.bfloat16().contiguous(memory_format=torch.channels_last))
+    yb.backward(g)
+    torch.testing.assert_close(xa.grad.float(), xb.grad.bfloat16().float(), rtol=0, atol=0)
