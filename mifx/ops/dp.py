@@ -75,8 +75,9 @@ def _pad4(G: torch.Tensor) -> torch.Tensor:
 
 
 def clip_sum_noise(G: torch.Tensor, l2_norm_clip: float, stddev: float, denominator: float = 1.0, seed: int = 0,
-                   offset: int = 0, return_norms: bool = False):
-    """sum_m min(1, C/||G_m||) G_m + stddev * N(0, I), divided by `denominator`.
+                   offset: int = 0, return_norms: bool = False, out: torch.Tensor | None = None):
+    """sum_m min(1, C/||G_m||) G_m + stddev * N(0, I), divided by `denominator` (GPU: written into `out` when
+    given).
 
     G: [M, P] float32 per-microbatch (flattened, concatenated) gradients."""
     if G.dim() != 2:
@@ -98,7 +99,10 @@ def clip_sum_noise(G: torch.Tensor, l2_norm_clip: float, stddev: float, denomina
     ld = Gp.shape[1]
     nchunk = (ld + fns["chunk"]() - 1) // fns["chunk"]()
     partial = torch.empty(M * nchunk, dtype=torch.float32, device=G.device)
-    out = torch.empty(P, dtype=torch.float32, device=G.device)
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=G.device)
+    elif out.dtype != torch.float32 or out.numel() != P or not out.is_contiguous() or out.device != G.device:
+        raise ValueError("out must be a contiguous float32 tensor of G.shape[1] elements on G's device")
     norms = torch.empty(M, dtype=torch.float32, device=G.device) if return_norms else None
     check(fns["clip"](ptr(Gp), M, ld, P, float(l2_norm_clip), float(stddev), float(denominator), seed, offset,
                       ptr(partial), ptr(out), ptr(norms), stream_handle(G.device)), "mifx_dp_clip_sum_noise")

@@ -41,7 +41,7 @@ class DPOptimizer:
 
         opt = DPOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), l2_norm_clip=1.0,
                           noise_multiplier=1.1, num_microbatches=256)
-        loss = opt.step(model, vector_loss_fn, x, y)   # vector_loss_fn(logits, y) -> [B]
+        loss = opt.step(model, vector_loss_fn, x, y)   # vector_loss_fn(logits, y) -> [B]; 0-dim loss tensor
     """
 
     def __init__(self, optimizer: torch.optim.Optimizer, l2_norm_clip: float, noise_multiplier: float,
@@ -67,7 +67,8 @@ class DPOptimizer:
         return GaussianAverageQuery(self.l2_norm_clip, self.l2_norm_clip * self.noise_multiplier, m)
 
     def compute_gradients(self, model: torch.nn.Module, vector_loss_fn, *batch) -> torch.Tensor:
-        """Fill `p.grad` with the noised, clipped microbatch average; returns the mean example loss."""
+        """Fill `p.grad` with the noised, clipped microbatch average; returns the mean example loss as a 0-dim
+        tensor (read it with float(); no host synchronisation per step)."""
         B = batch[0].shape[0]
         M = self.num_microbatches or B
         if B % M:
@@ -87,11 +88,12 @@ class DPOptimizer:
         split = [t.reshape(M, B // M, *t.shape[1:]) for t in batch]
         numel = sum(params[n].numel() for n in names)
         rows = max(1, min(M, self.max_g_bytes // max(1, numel * 4)))
-        acc, total_loss, norms = None, 0.0, []
+        acc, total_loss, norms = None, None, []
         for r0 in range(0, M, rows):
             grads, losses = per_mb(params, *[t[r0:r0 + rows] for t in split])
             G = torch.cat([grads[n].reshape(grads[n].shape[0], -1).float() for n in names], dim=1)
-            total_loss += float(losses.detach().sum())
+            lsum = losses.detach().sum()
+            total_loss = lsum if total_loss is None else total_loss + lsum
             if rows == M:  # whole batch in one fused pass: clip + sum + noise + /M
                 acc, nrm = clip_sum_noise(G, self.l2_norm_clip, self.l2_norm_clip * self.noise_multiplier, M,
                                           self.seed, self.steps, return_norms=True)
@@ -118,16 +120,23 @@ class DPOptimizer:
             p.grad = g.clone() if p.grad is None else p.grad.copy_(g)
             off += k
 
-    def _fused_mnist(self, model, x, y, M) -> float:
+    def _fused_mnist(self, model, x, y, M) -> torch.Tensor:
         """MNIST tutorial CNN on the GPU: all M microbatch gradients from one kernel (csrc/dpsgd_mnist.hip),
-        then the same fused clip / sum / noise pass as the generic path."""
+        then the same fused clip / sum / noise pass as the generic path, written straight into one flat gradient
+        buffer whose slices become the parameters' .grad (no per-parameter copies, no host sync)."""
         G, losses = dpsgd_mnist.per_microbatch_grads(model, x, y, M)
-        acc, self.last_norms = clip_sum_noise(G, self.l2_norm_clip, self.l2_norm_clip * self.noise_multiplier, M,
-                                              self.seed, self.steps, return_norms=True)
-        self._assign_grads(model, [n for n, _ in model.named_parameters()], acc)
-        return float(losses.sum()) / x.shape[0]
+        flat = getattr(self, "_flat_grad", None)
+        if flat is None or flat.device != G.device:
+            flat = self._flat_grad = torch.empty(G.shape[1], dtype=torch.float32, device=G.device)
+        _, self.last_norms = clip_sum_noise(G, self.l2_norm_clip, self.l2_norm_clip * self.noise_multiplier, M,
+                                            self.seed, self.steps, return_norms=True, out=flat)
+        off = 0
+        for p in model.parameters():
+            p.grad = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        return losses.sum() / x.shape[0]
 
-    def step(self, model: torch.nn.Module, vector_loss_fn, *batch) -> float:
+    def step(self, model: torch.nn.Module, vector_loss_fn, *batch) -> torch.Tensor:
         self.optimizer.zero_grad(set_to_none=True)
         loss = self.compute_gradients(model, vector_loss_fn, *batch)
         self.optimizer.step()

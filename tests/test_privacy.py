@@ -220,7 +220,7 @@ def test_dp_optimizer_chunked_equals_fused():
         x = torch.randn(16, 28, 28, generator=torch.Generator().manual_seed(2))
         y = torch.randint(0, 10, (16,), generator=torch.Generator().manual_seed(3))
         loss = opt.step(m, lambda out, t: torch.nn.functional.cross_entropy(out, t, reduction="none"), x, y)
-        return loss, [p.detach().clone() for p in m.parameters()]
+        return float(loss), [p.detach().clone() for p in m.parameters()]
 
     l1, p1 = run(8 << 30)
     l2, p2 = run(26010 * 4 * 3)  # 3 microbatches per chunk
@@ -424,8 +424,8 @@ def test_dpsgd_mnist_fused_step_matches_generic_path():
     for it in range(3):
         x = torch.rand(128, 28, 28, device="cuda")
         y = torch.randint(0, 10, (128,), device="cuda")
-        la = oa.step(ma, sparse_softmax_ce, x, y)
-        lb = ob.step(mb, lambda out, t: torch.nn.functional.cross_entropy(out, t, reduction="none"), x, y)
+        la = float(oa.step(ma, sparse_softmax_ce, x, y))
+        lb = float(ob.step(mb, lambda out, t: torch.nn.functional.cross_entropy(out, t, reduction="none"), x, y))
         assert abs(la - lb) < 1e-4 * max(1.0, abs(lb))
         torch.testing.assert_close(oa.last_norms, ob.last_norms, rtol=1e-4, atol=1e-6)
     for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
