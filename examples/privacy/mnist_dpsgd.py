@@ -17,6 +17,7 @@ import torch.nn.functional as F  # noqa: E402
 
 from mifx.data.synthetic import synthetic_images
 from mifx.models.cnn import MnistDPCNN
+from mifx.ops import dpsgd_mnist
 from mifx.privacy import DPGradientDescentOptimizer, compute_dp_sgd_privacy, sparse_softmax_ce
 
 
@@ -47,6 +48,7 @@ def main(argv=None):
     else:
         opt = torch.optim.SGD(model.parameters(), lr=a.learning_rate)
     steps_per_epoch = a.train_size // a.batch_size
+    fused_plain = not a.dpsgd and dpsgd_mnist.supported(model, xtr)
     for epoch in range(1, a.epochs + 1):
         t0 = time.time()
         perm = torch.randperm(a.train_size, device=dev)
@@ -54,6 +56,9 @@ def main(argv=None):
             idx = perm[s * a.batch_size:(s + 1) * a.batch_size]
             if a.dpsgd:
                 opt.step(model, vloss, xtr[idx], ytr[idx])
+            elif fused_plain:  # same network, non-private: per-example gradient kernel + mean (csrc/dpsgd_mnist.hip)
+                dpsgd_mnist.assign_mean_grads(model, xtr[idx], ytr[idx])
+                opt.step()
             else:
                 opt.zero_grad()
                 F.cross_entropy(model(xtr[idx]), ytr[idx]).backward()

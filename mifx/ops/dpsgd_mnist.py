@@ -63,3 +63,16 @@ def per_microbatch_grads(model: torch.nn.Module, x: torch.Tensor, y: torch.Tenso
     if rows != M:
         G = G.view(M, B // M, LD).sum(1)
     return G, loss
+
+
+def assign_mean_grads(model: torch.nn.Module, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Non-private step of the same network (the tutorial's `--dpsgd=False`): p.grad = gradient of the mean
+    softmax cross-entropy, from the per-example kernel (one workgroup per example) and one column sum; returns
+    the mean loss as a 0-dim tensor. GPU only (see `supported`)."""
+    G, loss = per_microbatch_grads(model, x, y, 1)
+    g = G[0] / x.shape[0]
+    off = 0
+    for p in model.parameters():
+        p.grad = g[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    return loss.mean()

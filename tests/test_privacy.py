@@ -506,3 +506,24 @@ def test_dp_sgd_linear_regression_converges():
         opt.step(model, lambda out, t: 0.5 * (out.squeeze(-1) - t) ** 2, X[i], y[i])
     torch.testing.assert_close(model.weight.detach().squeeze(0), w_true, atol=1.0, rtol=0)
     assert abs(float(model.bias) - b_true) < 1.0
+
+
+@pytest.mark.gpu
+def test_mnist_fused_mean_grads_match_autograd():
+    """Non-private step on the per-example kernel: p.grad == autograd of the mean cross-entropy (fp32)."""
+    from mifx.models.cnn import MnistDPCNN
+    from mifx.ops import dpsgd_mnist
+
+    torch.manual_seed(3)
+    m = MnistDPCNN().cuda()
+    x = torch.rand(48, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (48,), device="cuda")
+    loss = dpsgd_mnist.assign_mean_grads(m, x, y)
+    got = [p.grad.clone() for p in m.parameters()]
+    m.zero_grad()
+    ref_loss = torch.nn.functional.cross_entropy(m(x), y)
+    ref_loss.backward()
+    assert abs(float(loss) - float(ref_loss)) < 1e-5
+    for g, p in zip(got, m.parameters()):
+        s = p.grad.abs().max().clamp_min(1e-8)
+        torch.testing.assert_close(g / s, p.grad / s, rtol=0, atol=2e-5)

@@ -14,6 +14,7 @@ import torch.nn.functional as F  # noqa: E402
 
 from mifx.data.synthetic import synthetic_images  # noqa: E402
 from mifx.models import cnn  # noqa: E402
+from mifx.ops import dpsgd_mnist  # noqa: E402
 from mifx.privacy import DPGradientDescentOptimizer, sparse_softmax_ce  # noqa: E402
 
 
@@ -49,13 +50,16 @@ def bench_dpsgd(dev, steps, warmup, dp=True, B=256, M=256, fused=True):
         xb, yb = x[i * B:(i + 1) * B], y[i * B:(i + 1) * B]
         if dp:
             opt.step(model, vloss, xb, yb)
+        elif fused and dev.type == "cuda":  # non-private step on the per-example gradient kernel
+            dpsgd_mnist.assign_mean_grads(model, xb, yb)
+            opt.step()
         else:
             opt.zero_grad()
             F.cross_entropy(model(xb), yb).backward()
             opt.step()
 
     dt = _time(step, steps, warmup, dev)
-    name = ("dpsgd_mnist" + ("" if fused else "_vmap")) if dp else "sgd_mnist"
+    name = ("dpsgd_mnist" + ("" if fused else "_vmap")) if dp else ("sgd_mnist" + ("_fused" if fused else ""))
     return {"workload": name, "batch": B, "microbatches": M if dp else None,
             "ms_per_step": 1e3 * dt, "examples_per_sec": B / dt}
 
@@ -91,7 +95,8 @@ if __name__ == "__main__":
         "dpsgd": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=True),
         "dpsgd_vmap": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=True, fused=False),
         "dpsgd_m32": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=True, M=32),
-        "sgd": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=False),
+        "sgd": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=False, fused=False),
+        "sgd_fused": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=False),
         "pate": lambda: bench_model(dev, a.steps, a.warmup, "pate_teacher", cnn.PateCNN(), 128, (28, 28)),
         "tpu": lambda: bench_model(dev, a.steps, a.warmup, "tpu_mnist_cnn", cnn.TpuMnistCNN(), 1024, (28, 28)),
     }
