@@ -44,7 +44,7 @@ template <int BN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                       const float* __restrict__ bias, bf16* __restrict__ y, Geo d,
                                                       int relu) {
-  constexpr int BCH = BN * 4 / kThreads;  // 16-byte weight chunks per thread per step (2 or 1)
+  constexpr int BCH = (BN * 4 + kThreads - 1) / kThreads;  // 16-byte weight chunks per thread per step (2, 1, 1)
   // one LDS block: double-buffered A and B staging, reused as the epilogue's output tile
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * BM * LDR + 2 * BN * LDR];
   bf16(*As)[BM * LDR] = reinterpret_cast<bf16(*)[BM * LDR]>(smem);
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
       const int c = t + kThreads * j, k = c >> 2, part = (c & 3) * 8;
-      rb[j] = *(const u4*)(wg + ((size_t)(n0 + k) * d.R * d.S + tap) * d.C + c0 + part);
+      if ((BN * 4) % kThreads == 0 || c < BN * 4) rb[j] = *(const u4*)(wg + ((size_t)(n0 + k) * d.R * d.S + tap) * d.C + c0 + part);
     }
   };
   auto store = [&](int buf) {
@@ -97,11 +97,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
       const int c = t + kThreads * j;
-      *(u4*)(&Bs[buf][(c >> 2) * LDR + (c & 3) * 8]) = rb[j];
+      if ((BN * 4) % kThreads == 0 || c < BN * 4) *(u4*)(&Bs[buf][(c >> 2) * LDR + (c & 3) * 8]) = rb[j];
     }
   };
 
-  constexpr int TN = BN / 32;  // 16-wide column tiles per wave (wave owns BN/2 columns)
+  constexpr int TN = BN / 32;  // 16-wide column tiles per wave (wave owns BN/2 columns; BN = 32: one tile)
   v4f acc[4][TN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -290,11 +290,11 @@ int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, in
 
 // x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
 // stride 1, zero padding `pad` on every side, Ho = Hi + 2 pad - R + 1, relu != 0: y = max(y, 0).
-// Needs C % 32 == 0 and K % 64 == 0.
+// Needs C % 32 == 0 and K % 32 == 0.
 int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
                    int K, int R, int S, int pad, int relu, hipStream_t st) {
   const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
-  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 64 != 0 || Ho <= 0 || Wo <= 0 ||
+  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 32 != 0 || Ho <= 0 || Wo <= 0 ||
       pad < 0 || pad >= R || pad >= S)
     return -1;
   const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad};
@@ -304,8 +304,11 @@ int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int
   if (K % 128 == 0) {
     hipLaunchKernelGGL(gconv_fwd<128>, dim3((unsigned)mt, K / 128, G), dim3(kThreads), 0, st, (const bf16*)x,
                        (const bf16*)w, bias, (bf16*)y, d, relu);
-  } else {
+  } else if (K % 64 == 0) {
     hipLaunchKernelGGL(gconv_fwd<64>, dim3((unsigned)mt, K / 64, G), dim3(kThreads), 0, st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, d, relu);
+  } else {  // e.g. the 96-channel layers of PATE's inference_deeper
+    hipLaunchKernelGGL(gconv_fwd<32>, dim3((unsigned)mt, K / 32, G), dim3(kThreads), 0, st, (const bf16*)x,
                        (const bf16*)w, bias, (bf16*)y, d, relu);
   }
   return (int)hipGetLastError();

@@ -4,7 +4,7 @@
 groups=groups)` for channels-last bf16 activations: the forward and the input gradient run one HIP kernel (the
 input gradient of a stride-1 conv is the same kernel on dy with the weight flipped and transposed), the weight
 gradient a second one (transposed LDS reads). `eligible()` says when a call can take this path
-(GPU, C/group % 32 == 0, K/group % 64 == 0; the input gradient needs C/group % 64 == 0 and the weight gradient
+(GPU, C/group % 32 == 0, K/group % 32 == 0 (the input gradient likewise, with the roles of C and K swapped); the weight gradient needs
 C/group in {32, 64, 128}, else those parts run on MIOpen); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
 ensemble (`mifx/privacy/pate/ensemble.py`)."""
 from __future__ import annotations
@@ -33,7 +33,7 @@ def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int) -
         return False
     K = GK // groups
     Ho, Wo = x.shape[2] + 2 * padding - R + 1, x.shape[3] + 2 * padding - S + 1
-    return C % 32 == 0 and K % 64 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
+    return C % 32 == 0 and K % 32 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
 
 
 def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad,
@@ -75,7 +75,7 @@ class _GConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # HIP input gradient for grouped / large-image convs; MIOpen's is as fast or faster on small
             # single-group images (profiles/gconv_resnet_r2.jsonl)
-            if C % 64 == 0 and R == S and (G > 1 or M >= 100_000):
+            if C % 32 == 0 and R == S and (G > 1 or M >= 100_000):
                 # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
                 w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
                 dx = _launch(dyb, w_bwd, None, N, Ho, Wo, G, K, C, R, S, R - 1 - pad)

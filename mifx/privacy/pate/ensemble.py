@@ -77,7 +77,7 @@ class PateEnsemble(nn.Module):
         teacher): the Cin = 1 layer has no 32-channel reduction of its own, and the image of the resident dataset is
         built once (`conv_input`), not per step."""
         w = self.conv_w[0]
-        return (USE_HIP_CONV and not self.deeper and self.conv_specs[0][1] == 1 and self.kernels[0] % 2 == 1
+        return (USE_HIP_CONV and self.conv_specs[0][1] == 1 and self.kernels[0] % 2 == 1
                 and w.shape[1] * self.kernels[0] ** 2 <= 32)
 
     def conv_input(self, x: torch.Tensor, chunk: int = 256) -> torch.Tensor:
@@ -110,7 +110,9 @@ class PateEnsemble(nn.Module):
         k, s = self.kernels[i], self.conv_specs[i][1]
         if USE_HIP_CONV and s == 1 and k % 2 == 1:  # SAME = symmetric pad k//2: grouped MFMA conv when eligible
             return gconv.conv2d(x, self.conv_w[i], self.conv_b[i], padding=k // 2, groups=self.T, relu=relu)
-        y = F.conv2d(_same_pad(x, k, s), self.conv_w[i], self.conv_b[i], stride=s, groups=self.T)
+        # (weights in the activations' dtype: the HIP layers hand bf16 activations on even outside autocast)
+        y = F.conv2d(_same_pad(x, k, s), self.conv_w[i].to(x.dtype), self.conv_b[i].to(x.dtype), stride=s,
+                     groups=self.T)
         return F.relu(y) if relu else y
 
     def _lrn(self, y: torch.Tensor) -> torch.Tensor:
@@ -133,8 +135,8 @@ class PateEnsemble(nn.Module):
             y = self._conv(1, y, relu=True)
             y = same_maxpool(self._lrn(y), 3, 2)
         else:
-            y = x
-            for i in range(len(self.conv_specs)):
+            y = self._conv0_col(x, relu=True) if col else self._conv(0, x, relu=True)
+            for i in range(1, len(self.conv_specs)):
                 y = self._conv(i, y, relu=True)
         B, TC, h, w = y.shape
         z = y.reshape(B, self.T, (TC // self.T) * h * w).transpose(0, 1)  # per-teacher NCHW flatten

@@ -53,9 +53,10 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--teachers", default="10,50,250")
     ap.add_argument("--no-sequential", action="store_true")
+    ap.add_argument("--deeper", action="store_true", help="inference_deeper (3x3 convs 96/192)")
     a = ap.parse_args()
     dev = "cuda"
     if not a.no_sequential:
-        print(json.dumps(run_sequential(a.steps, dev)), flush=True)
+        print(json.dumps(run_sequential(a.steps, dev, a.deeper)), flush=True)
     for T in [int(t) for t in a.teachers.split(",")]:
-        print(json.dumps(run(T, a.steps, dev)), flush=True)
+        print(json.dumps(run(T, a.steps, dev, a.deeper)), flush=True)
