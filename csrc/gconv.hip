@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
 
 // ---- weight gradient ------------------------------------------------------------------------------------
 // dw[g*K + k][c][r][s] = sum_m dy[m][g*K + k] * x[pixel(m) + (r - pad, s - pad)][g*C + c]: a GEMM of
-// 128 k-rows x 128 (tap, c) columns per workgroup (128 / C taps of C channels), reduced over output pixels m in
+// 128 k-rows x 128 (tap, c) columns per workgroup (the flattened tap-major column space), reduced over output pixels m in
 // chunks of 32. Both operands arrive pixel-major (channels contiguous), so the chunks are staged as
 // [32 pixels][128] bf16 images (rows padded to 288 B) and the MFMA fragments, which need 8 consecutive reduction
 // elements per lane, come from ds_read_b64_tr_b16 transposed reads. The reduction order inside a 32-chunk is
@@ -184,15 +184,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][32 * WLD];  // x chunk [pixel][(tap, c)]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = blockIdx.z, k0 = blockIdx.y * 128;
-  const int tpb = 128 / d.C, tap0 = blockIdx.x * tpb, RS = d.R * d.S;
+  const int RS = d.R * d.S, col0 = blockIdx.x * 128;  // 128 columns of the flattened (tap, c) space
   const long long M = (long long)d.N * d.Ho * d.Wo;
   const int KT = d.G * d.K, CT = d.G * d.C;
   const int nsteps = (int)((M + 31) / 32);
   // this thread's chunks: pixel rows pr[j] = (t >> 4) + 16 j, 16-byte chunk (t & 15) of the 256-byte row
   const int ch = t & 15;
-  const int btap = tap0 + (ch * 8) / d.C, bc = (ch * 8) % d.C;
+  const int bcol = col0 + ch * 8;  // C % 8 == 0: an 8-channel chunk never straddles two taps
+  const bool btap_ok = bcol < RS * d.C;
+  const int btap = bcol / d.C, bc = bcol - btap * d.C;
   const int br = btap / d.S, bs = btap - br * d.S;
-  const bool btap_ok = btap < RS;
 
   u4 ra[2], rb[2];
   auto load = [&](int step) {
@@ -254,9 +255,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   // acc[i][j][e]: k = k0 + wm + 16 i + 4 (lane >> 4) + e, column wn + 16 j + (lane & 15) = (tap, c)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = wn + 16 * j + (lane & 15);
-    const int tap = tap0 + col / d.C, c = col % d.C;
-    if (tap >= RS) continue;
+    const int col = col0 + wn + 16 * j + (lane & 15);
+    if (col >= RS * d.C) continue;
+    const int tap = col / d.C, c = col - tap * d.C;
     const int r = tap / d.S, s = tap - r * d.S;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -273,17 +274,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
 extern "C" {
 
 // dw [G*K][C][R][S] fp32 (PyTorch layout) from x [N, Hi, Wi, G*C] and dy [N, Ho, Wo, G*K] bf16 (NHWC).
-// Needs C in {32, 64, 128} and K % 8 == 0 (k-tiles of 128; a partial last tile is masked).
+// Needs C % 8 == 0 and K % 8 == 0 (tiles of 128 k x 128 (tap, c) columns; partial last tiles are masked).
 int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, int Wi, int G, int C, int K, int R,
                      int S, int pad, hipStream_t st) {
   const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
-  if (N <= 0 || G <= 0 || G > 65535 || (C != 32 && C != 64 && C != 128) || K <= 0 || K % 8 != 0 || Ho <= 0 ||
+  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % 8 != 0 || K <= 0 || K % 8 != 0 || Ho <= 0 ||
       Wo <= 0 || pad < 0 || pad >= R || pad >= S)
     return -1;
   if ((long long)N * Ho * Wo > 0x3fffffffLL) return -1;
   const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad};
-  const int tpb = 128 / C;
-  hipLaunchKernelGGL(gconv_wgrad, dim3((R * S + tpb - 1) / tpb, (K + 127) / 128, G), dim3(kThreads), 0, st,
+  hipLaunchKernelGGL(gconv_wgrad, dim3((R * S * C + 127) / 128, (K + 127) / 128, G), dim3(kThreads), 0, st,
                      (const bf16*)x, (const bf16*)dy, dw, d);
   return (int)hipGetLastError();
 }

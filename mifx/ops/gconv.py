@@ -5,7 +5,7 @@ groups=groups)` for channels-last bf16 activations: the forward and the input gr
 input gradient of a stride-1 conv is the same kernel on dy with the weight flipped and transposed), the weight
 gradient a second one (transposed LDS reads). `eligible()` says when a call can take this path
 (GPU, C/group % 32 == 0, K/group % 32 == 0 (the input gradient likewise, with the roles of C and K swapped); the weight gradient needs
-C/group in {32, 64, 128}, else those parts run on MIOpen); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
+C/group % 8 == 0 and enough (tap, k, group) tiles, else those parts run on MIOpen); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
 ensemble (`mifx/privacy/pate/ensemble.py`)."""
 from __future__ import annotations
 
@@ -82,8 +82,7 @@ class _GConv(torch.autograd.Function):
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=1, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
-            tpb = 128 // C if C in (32, 64, 128) else 0
-            wg_blocks = ((R * S + tpb - 1) // tpb) * ((K + 127) // 128) * G if tpb else 0
+            wg_blocks = ((R * S * C + 127) // 128) * ((K + 127) // 128) * G if C % 8 == 0 else 0
             if R == 1 and S == 1 and pad == 0:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)

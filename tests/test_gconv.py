@@ -28,7 +28,9 @@ def test_cpu_falls_back_to_f_conv2d():
                                              # enough (tap, k, group) tiles for the HIP weight-gradient kernel
                                              (2, 6, 32, 64, 128, 5, 2), (2, 5, 96, 32, 128, 3, 1),
                                              # 32-channel output tiles (PATE inference_deeper's 96-channel layers)
-                                             (3, 8, 4, 96, 96, 3, 1), (2, 7, 3, 96, 192, 3, 1)])
+                                             (3, 8, 4, 96, 96, 3, 1), (2, 7, 3, 96, 192, 3, 1),
+                                             # HIP weight gradient over a tap-straddling (tap, c) column space
+                                             (2, 5, 48, 96, 96, 3, 1), (2, 4, 24, 192, 192, 3, 1)])
 def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad, relu):
     torch.manual_seed(0)
     dev = "cuda"
