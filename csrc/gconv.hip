@@ -1,4 +1,5 @@
-// Grouped stride-1 convolution as an implicit GEMM on bf16 MFMA (NHWC), forward and input gradient.
+// Grouped convolution as an implicit GEMM on bf16 MFMA (NHWC): forward (any stride), stride-1 input gradient,
+// weight gradient (any stride).
 //
 // Reference workload: the PATE-2017 `deep_cnn.inference` CNN (5x5 convs 64/128 channels,
 // `research/pate_2017/deep_cnn.py:84-191`) trained for every teacher of the ensemble
@@ -35,7 +36,7 @@ __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
 }
 
 struct Geo {
-  int N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad;
+  int N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride;
 };
 
 // amdgpu_waves_per_eu(4): 4 workgroups per CU (40 KB LDS each) -- the loop is latency-bound, occupancy pays
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int r = tap / d.S, s = tap - r * d.S;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int hh = ah[j] + r - d.pad, ww = aw[j] + s - d.pad;
+      const int hh = ah[j] * d.stride + r - d.pad, ww = aw[j] * d.stride + s - d.pad;
       if (am[j] && hh >= 0 && hh < d.Hi && ww >= 0 && ww < d.Wi) {
         const bf16* src = x + ((size_t)(an[j] * d.Hi + hh) * d.Wi + ww) * CT + g * d.C + c0 + apart;
         ra[j] = *(const u4*)src;
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
       if (m < M) {
         if (k0 + ch * 8 < d.K) ra[j] = *(const u4*)(dy + m * KT + g * d.K + k0 + ch * 8);
         const int q = (int)(m % d.Wo), p = (int)((m / d.Wo) % d.Ho), n = (int)(m / ((long long)d.Wo * d.Ho));
-        const int hh = p + br - d.pad, ww = q + bs - d.pad;
+        const int hh = p * d.stride + br - d.pad, ww = q * d.stride + bs - d.pad;
         if (btap_ok && hh >= 0 && hh < d.Hi && ww >= 0 && ww < d.Wi)
           rb[j] = *(const u4*)(x + ((size_t)(n * d.Hi + hh) * d.Wi + ww) * CT + g * d.C + bc);
       }
@@ -276,28 +277,30 @@ extern "C" {
 // dw [G*K][C][R][S] fp32 (PyTorch layout) from x [N, Hi, Wi, G*C] and dy [N, Ho, Wo, G*K] bf16 (NHWC).
 // Needs C % 8 == 0 and K % 8 == 0 (tiles of 128 k x 128 (tap, c) columns; partial last tiles are masked).
 int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, int Wi, int G, int C, int K, int R,
-                     int S, int pad, hipStream_t st) {
-  const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
-  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % 8 != 0 || K <= 0 || K % 8 != 0 || Ho <= 0 ||
-      Wo <= 0 || pad < 0 || pad >= R || pad >= S)
+                     int S, int pad, int stride, hipStream_t st) {
+  if (stride <= 0) return -1;
+  const int Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
+  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % 8 != 0 || K <= 0 || K % 8 != 0 || Hi + 2 * pad < R ||
+      Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S)
     return -1;
   if ((long long)N * Ho * Wo > 0x3fffffffLL) return -1;
-  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad};
+  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride};
   hipLaunchKernelGGL(gconv_wgrad, dim3((R * S * C + 127) / 128, (K + 127) / 128, G), dim3(kThreads), 0, st,
                      (const bf16*)x, (const bf16*)dy, dw, d);
   return (int)hipGetLastError();
 }
 
 // x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
-// stride 1, zero padding `pad` on every side, Ho = Hi + 2 pad - R + 1, relu != 0: y = max(y, 0).
+// zero padding `pad` on every side, Ho = (Hi + 2 pad - R) / stride + 1, relu != 0: y = max(y, 0).
 // Needs C % 32 == 0 and K % 32 == 0.
 int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
-                   int K, int R, int S, int pad, int relu, hipStream_t st) {
-  const int Ho = Hi + 2 * pad - R + 1, Wo = Wi + 2 * pad - S + 1;
-  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 32 != 0 || Ho <= 0 || Wo <= 0 ||
-      pad < 0 || pad >= R || pad >= S)
+                   int K, int R, int S, int pad, int stride, int relu, hipStream_t st) {
+  if (stride <= 0) return -1;
+  const int Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
+  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 32 != 0 || Hi + 2 * pad < R ||
+      Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S)
     return -1;
-  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad};
+  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride};
   const long long M = (long long)N * Ho * Wo;
   const long long mt = (M + BM - 1) / BM;
   if (mt > 0x7fffffffLL) return -1;

@@ -21,11 +21,11 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 @functools.lru_cache(maxsize=None)
 def _fns():
     lib = _lib.load("gconv")
-    return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 10 + [VP]),
-            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 9 + [VP])}
+    return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 11 + [VP]),
+            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 10 + [VP])}
 
 
-def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int) -> bool:
+def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int, stride: int = 1) -> bool:
     if not (x.is_cuda and x.dim() == 4 and weight.dim() == 4):
         return False
     GK, C, R, S = weight.shape
@@ -33,21 +33,21 @@ def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int) -
         return False
     K = GK // groups
     Ho, Wo = x.shape[2] + 2 * padding - R + 1, x.shape[3] + 2 * padding - S + 1
-    return C % 32 == 0 and K % 32 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
+    return stride >= 1 and C % 32 == 0 and K % 32 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
 
 
 def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad,
-            relu: bool = False) -> torch.Tensor:
-    Ho, Wo = Hi + 2 * pad - R + 1, Wi + 2 * pad - S + 1
+            relu: bool = False, stride: int = 1) -> torch.Tensor:
+    Ho, Wo = (Hi + 2 * pad - R) // stride + 1, (Wi + 2 * pad - S) // stride + 1
     y = torch.empty(N, G * K, Ho, Wo, device=x_nhwc.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
-    check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(relu),
-                        stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
+    check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
+                        int(relu), stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
     return y
 
 
 class _GConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, pad, groups, relu):
+    def forward(ctx, x, weight, bias, pad, groups, relu, stride):
         N, _, Hi, Wi = x.shape
         GK, C, R, S = weight.shape
         G, K = groups, GK // groups
@@ -55,16 +55,16 @@ class _GConv(torch.autograd.Function):
         wb = weight.to(torch.bfloat16)
         w_fwd = wb.view(G, K, C, R, S).permute(0, 1, 3, 4, 2).contiguous()  # [G][K][R][S][C]
         b = bias.float().contiguous() if bias is not None else None
-        y = _launch(xb, w_fwd, b, N, Hi, Wi, G, C, K, R, S, pad, relu)
+        y = _launch(xb, w_fwd, b, N, Hi, Wi, G, C, K, R, S, pad, relu, stride)
         ctx.save_for_backward(xb, wb, y if relu else None)
         ctx.geo = (N, Hi, Wi, G, C, K, R, S, pad, bias is not None, weight.dtype,
-                   bias.dtype if bias is not None else None)
+                   bias.dtype if bias is not None else None, stride)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xb, wb, y = ctx.saved_tensors
-        N, Hi, Wi, G, C, K, R, S, pad, has_bias, wdt, bdt = ctx.geo
+        N, Hi, Wi, G, C, K, R, S, pad, has_bias, wdt, bdt, stride = ctx.geo
         dyb = dy.to(torch.bfloat16)
         if y is not None:  # fused ReLU: gradient through max(., 0)
             dyb = torch.ops.aten.threshold_backward(dyb, y, 0)
@@ -75,38 +75,38 @@ class _GConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # HIP input gradient for grouped / large-image convs; MIOpen's is as fast or faster on small
             # single-group images (profiles/gconv_resnet_r2.jsonl)
-            if C % 32 == 0 and R == S and (G > 1 or M >= 100_000):
+            if stride == 1 and C % 32 == 0 and R == S and (G > 1 or M >= 100_000):
                 # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
                 w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
                 dx = _launch(dyb, w_bwd, None, N, Ho, Wo, G, K, C, R, S, R - 1 - pad)
             else:
-                dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=1, padding=pad, groups=G)
+                dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
             wg_blocks = ((R * S * C + 127) // 128) * ((K + 127) // 128) * G if C % 8 == 0 else 0
-            if R == 1 and S == 1 and pad == 0:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
+            if R == 1 and S == 1 and pad == 0 and stride == 1:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
                 dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
             elif wg_blocks >= 256:  # hand-written weight gradient (fp32 out, PyTorch layout); it has no split over
                 # pixels, so it needs many (tap, k, group) tiles to fill the chip -- else MIOpen's
                 dw = torch.empty(G * K, C, R, S, device=dyb.device, dtype=torch.float32)
-                check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad,
+                check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
                                       stream_handle(dyb.device)), "mifx_gconv_wgrad")
                 dw = dw.to(wdt)
             else:
-                dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=1, padding=pad,
+                dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
                                                  groups=G).to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = torch.sum(dyb, dim=(0, 2, 3), dtype=torch.float32).to(bdt)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0,
-           groups: int = 1, relu: bool = False) -> torch.Tensor:
+           groups: int = 1, relu: bool = False, stride: int = 1) -> torch.Tensor:
     """Stride-1 (grouped) convolution (`relu=True`: followed by ReLU, fused into the kernel's epilogue); the HIP
     kernels when `eligible`, else F.conv2d. Output bf16 channels-last on the kernel path (the dtype F.conv2d gives
     under bf16 autocast)."""
-    if eligible(x, weight, groups, padding) and _lib.gpu_available():
-        return _GConv.apply(x, weight, bias, int(padding), int(groups), bool(relu))
-    y = F.conv2d(x, weight, bias, stride=1, padding=padding, groups=groups)
+    if eligible(x, weight, groups, padding, stride) and _lib.gpu_available():
+        return _GConv.apply(x, weight, bias, int(padding), int(groups), bool(relu), int(stride))
+    y = F.conv2d(x, weight, bias, stride=stride, padding=padding, groups=groups)
     return F.relu(y) if relu else y

@@ -110,6 +110,9 @@ class PateEnsemble(nn.Module):
         k, s = self.kernels[i], self.conv_specs[i][1]
         if USE_HIP_CONV and s == 1 and k % 2 == 1:  # SAME = symmetric pad k//2: grouped MFMA conv when eligible
             return gconv.conv2d(x, self.conv_w[i], self.conv_b[i], padding=k // 2, groups=self.T, relu=relu)
+        if USE_HIP_CONV and x.is_cuda:  # strided SAME: explicit (asymmetric) pad, then the strided kernel
+            return gconv.conv2d(_same_pad(x, k, s), self.conv_w[i], self.conv_b[i], padding=0, groups=self.T,
+                                relu=relu, stride=s)
         # (weights in the activations' dtype: the HIP layers hand bf16 activations on even outside autocast)
         y = F.conv2d(_same_pad(x, k, s), self.conv_w[i].to(x.dtype), self.conv_b[i].to(x.dtype), stride=s,
                      groups=self.T)

@@ -32,18 +32,31 @@ def test_cpu_falls_back_to_f_conv2d():
                                              # HIP weight gradient over a tap-straddling (tap, c) column space
                                              (2, 5, 48, 96, 96, 3, 1), (2, 4, 24, 192, 192, 3, 1)])
 def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad, relu):
+    _check_against_reference(N, H, G, C, K, R, pad, relu, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,G,C,K,R,pad", [(2, 9, 3, 96, 96, 3, 0), (2, 15, 24, 192, 192, 3, 0),
+                                             (3, 8, 2, 64, 128, 3, 1)])
+def test_gconv_stride2_matches_fp32_reference(N, H, G, C, K, R, pad):
+    """Strided forward + weight gradient on the HIP kernels (input gradient on MIOpen) -- PATE inference_deeper's
+    stride-2 layers."""
+    _check_against_reference(N, H, G, C, K, R, pad, False, 2)
+
+
+def _check_against_reference(N, H, G, C, K, R, pad, relu, stride):
     torch.manual_seed(0)
     dev = "cuda"
     x = torch.randn(N, G * C, H, H + 1, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (0.05 * torch.randn(G * K, C, R, R, device=dev)).to(torch.bfloat16).float()
     b = torch.randn(G * K, device=dev)
     xr, wr, br = x.float().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
-    ref = F.conv2d(xr, wr, br, padding=pad, groups=G)
+    ref = F.conv2d(xr, wr, br, padding=pad, groups=G, stride=stride)
     if relu:
         ref = F.relu(ref)
     xk, wk, bk = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
-    assert gconv.eligible(xk, wk, G, pad)
-    out = gconv.conv2d(xk, wk, bk, padding=pad, groups=G, relu=relu)
+    assert gconv.eligible(xk, wk, G, pad, stride)
+    out = gconv.conv2d(xk, wk, bk, padding=pad, groups=G, relu=relu, stride=stride)
     assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=torch.channels_last)
     s = ref.abs().max()
     torch.testing.assert_close(out.float() / s, ref / s, rtol=0, atol=1e-2)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# gconv weight gradient over any C % 8 (tap-straddling column tiles): tests, deeper + standard PATE benches
+# gconv strided forward + weight gradient (deeper ensemble stride-2 layers): tests, deeper + standard PATE benches
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
