@@ -62,6 +62,24 @@ def _ranks_agree(tr) -> bool:
     return bool(torch.equal(hi, lo)) and bool(torch.isfinite(chk).all())
 
 
+def _post_run_ok(tr, n: int, use_cuda: bool) -> tuple[bool, bool | None]:
+    """After the timed region (outside it): the exchange must not have timed out on any rank and every replica
+    must hold bit-identical weights. Returns (ok on every rank, replicas_bit_identical or None at one rank)."""
+    if n == 1 or not use_cuda:
+        return True, None
+    bad = 0.0
+    try:
+        if getattr(tr, "_xg", None) is not None:
+            tr._xg.check()
+    except RuntimeError as e:
+        print(f"[bench] {e}", file=sys.stderr, flush=True)
+        bad = 1.0
+    flag = torch.tensor([bad], device=tr.device)
+    torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+    agree = _ranks_agree(tr)
+    return flag.item() == 0.0 and agree, agree
+
+
 def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, dp: str = "xgmi",
                  steps_per_graph: int = 10):
     def build():
@@ -174,31 +192,42 @@ def main(argv=None) -> int:
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     n = env.world_size
 
-    tr = make_trainer(a.batch_per_gpu, device, pg, 1234 + env.rank, a.data_per_gpu, not a.no_graph, a.dp,
-                      a.steps_per_graph)
-    dp_path = getattr(tr, "dp_path", None)
-    ranks_agree = _ranks_agree(tr) if (n > 1 and use_cuda) else None  # replicas must hold identical weights
-    spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
-    dt = mdist.max_over_ranks(run(tr, a.steps, a.warmup, device), device if use_cuda else None)
-    loss = tr.last_loss() / a.batch_per_gpu
+    def measure(batch, seed, n_data, steps, warmup):
+        """Build, time `steps` steps, validate after the timed region. A multi-rank xGMI run that fails the
+        post-run validation (a timed-out wait, replicas that differ) is discarded and re-measured on the direct
+        RCCL path; a failing direct run fails the benchmark (no number from a broken step)."""
+        dp = a.dp
+        while True:
+            tr = make_trainer(batch, device, pg, seed, n_data, not a.no_graph, dp, a.steps_per_graph)
+            spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
+            dt = mdist.max_over_ranks(run(tr, steps, warmup, device), device if use_cuda else None)
+            ok, agree = _post_run_ok(tr, n, use_cuda)
+            res = {"dt": dt, "dp_path": getattr(tr, "dp_path", None), "spg": spg, "agree": agree,
+                   "loss": tr.last_loss() / batch if ok else float("nan")}
+            if getattr(tr, "_xg", None) is not None:
+                tr.disable_xgmi()
+            del tr
+            if use_cuda:
+                torch.cuda.synchronize(device)
+                torch.cuda.empty_cache()
+            if ok:
+                return res
+            if dp == "direct":
+                raise SystemExit("[bench] the direct RCCL step failed post-run validation")
+            print("[bench] post-run validation failed: re-measuring on the direct RCCL path", file=sys.stderr,
+                  flush=True)
+            dp = "direct"
+
+    r = measure(a.batch_per_gpu, 1234 + env.rank, a.data_per_gpu, a.steps, a.warmup)
+    dt, dp_path, spg, ranks_agree, loss = r["dt"], r["dp_path"], r["spg"], r["agree"], r["loss"]
     value = a.batch_per_gpu * n * a.steps / dt
 
     ref = None
     if a.ref_batch:
-        if getattr(tr, "_xg", None) is not None:
-            tr.disable_xgmi()
-        del tr
-        if use_cuda:
-            torch.cuda.synchronize(device)
-            torch.cuda.empty_cache()
-        tr2 = make_trainer(a.ref_batch, device, pg, 99 + env.rank, 1 << 16, not a.no_graph, a.dp,
-                           a.steps_per_graph)
-        dt2 = mdist.max_over_ranks(run(tr2, a.ref_steps, max(10, a.warmup), device), device if use_cuda else None)
-        ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / dt2,
-               "ms_per_step": 1e3 * dt2 / a.ref_steps, "steps": a.ref_steps,
-               "dp_exchange": getattr(tr2, "dp_path", None)}
-        if getattr(tr2, "_xg", None) is not None:
-            tr2.disable_xgmi()
+        r2 = measure(a.ref_batch, 99 + env.rank, 1 << 16, a.ref_steps, max(10, a.warmup))
+        ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / r2["dt"],
+               "ms_per_step": 1e3 * r2["dt"] / a.ref_steps, "steps": a.ref_steps,
+               "dp_exchange": r2["dp_path"], "replicas_bit_identical": r2["agree"]}
 
     if env.is_main:
         out = {
@@ -223,7 +252,7 @@ def main(argv=None) -> int:
                        "steps_per_graph": spg,
                        "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
                        "dp_exchange": dp_path,
-                       "replicas_bit_identical": ranks_agree},
+                       "replicas_bit_identical": ranks_agree, "validated_after_timed_region": True},
             "final_mean_loss": loss,
             "reference_batch": ref,
         }

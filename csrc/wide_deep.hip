@@ -879,6 +879,39 @@ __device__ __forceinline__ float ld_sys(const float* p) {
   return __uint_as_float(__hip_atomic_load((const unsigned int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 
+// ---- xGMI exchange synchronisation (release / acquire at system scope; bounded, sticky failure)
+// A rank publishes epoch e for a chunk with a RELEASE store of the flag (its partial stores are ordered before it:
+// they are write-through system-scope stores, drained by the s_waitcnt before the workgroup barrier, and the
+// release orders everything the workgroup did before the barrier), and a waiter re-reads the flag with relaxed
+// loads and then issues an ACQUIRE fence before loading the partials. The wait is bounded by WALL-CLOCK time
+// (s_memrealtime, 100 MHz): a peer that never arrives sets the rank's sticky err flag instead of hanging the
+// GPU; every exchange kernel reads err first and does nothing once it is set (no publish, no parameter update,
+// no counter advance) -- the peers then time out too, so every rank stops with its weights untouched by
+// garbage and the host raises at its next check (FusedWideDeepTrainer._check_exchange).
+constexpr long long XG_TIMEOUT_TICKS = 1000ll * 1000 * 1000;  // 10 s at the 100 MHz real-time clock
+
+__device__ __forceinline__ bool xg_failed(const int* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+__device__ __forceinline__ void xg_publish(unsigned int* flag, unsigned int e) {
+  __hip_atomic_store(flag, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// wait until *f reaches epoch e (wrapping compare); false on timeout or when another workgroup already failed
+__device__ __forceinline__ bool xg_wait(const unsigned int* f, unsigned int e, int* err) {
+  const long long t0 = wall_clock64();
+  while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+    __builtin_amdgcn_s_sleep(2);
+    if (xg_failed(err)) return false;
+    if (wall_clock64() - t0 > XG_TIMEOUT_TICKS) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+  return true;
+}
+
 // xGMI exchange peers (see the data-parallel section below)
 constexpr int XG_MAXW = 8;
 constexpr int XB_THR = 64;               // kernel B: one wave, one float4 column per thread
@@ -981,8 +1014,14 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
   __shared__ int order[XMAX];
   __shared__ int nord;
   __shared__ long long s_e, s_step;
+  __shared__ int s_bad;
   const int t = threadIdx.x;
   constexpr bool opt = MODE == 1 || MODE == 3;
+  if (MODE == 3) {  // the exchange already failed on this rank: touch nothing (see xg_wait)
+    if (t == 0) s_bad = xg_failed(err) ? 1 : 0;
+    __syncthreads();
+    if (s_bad) return;
+  }
   if (t < XMAX) first[t] = 1 << 30;
   if (t == 0) {
     s_e = xep[blockIdx.x] + 1;
@@ -1052,19 +1091,13 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
     if (t < 4 * world) {
       const int cc = 4 * blockIdx.x + t / world, p = t % world;
       if (cc < nch) {
-        __hip_atomic_store(peers.sig[p] + cc * XG_MAXW + rank, uex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        long long spins = 0;
-        const unsigned int* f = my_sig + cc * XG_MAXW + p;
-        while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - uex) < 0) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1ll << 26)) {  // seconds: a peer is gone; record it and finish (results are garbage)
-            err[0] = 1;
-            break;
-          }
-        }
+        xg_publish(peers.sig[p] + cc * XG_MAXW + rank, uex);
+        if (!xg_wait(my_sig + cc * XG_MAXW + p, uex, err)) s_bad = 1;
       }
     }
     __syncthreads();
+    if (s_bad) return;  // a peer never arrived: no update, no counter advance (err is set)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the peers' partials published before their flags
     if (gi < stride) {
       float pv2[XG_MAXW];
 #pragma unroll
@@ -1114,8 +1147,13 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
 // reads slot 0, written by kernel B's workgroup 0 of the previous step)
 __global__ __launch_bounds__(256) void wd_reduce_xgmi_publish(const float4* __restrict__ slab, int G, int stride,
                                                               XgPeers peers, int world, int rank,
-                                                              const long long* __restrict__ xctr) {
+                                                              const long long* __restrict__ xctr,
+                                                              const int* __restrict__ err) {
   __shared__ float4 part[RG][RQ];
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = xg_failed(err) ? 1 : 0;
+  __syncthreads();
+  if (s_bad) return;  // failed exchange: publish nothing (the peers time out and stop too)
   const int S4 = stride / 4;
   const int q = blockIdx.x * RQ + threadIdx.x % RQ;
   const long long e = xctr[0] + 1;
@@ -1129,9 +1167,7 @@ __global__ __launch_bounds__(256) void wd_reduce_xgmi_publish(const float4* __re
     __builtin_amdgcn_s_waitcnt(0);  // the chunk's stores acknowledged before the flag below
   }
   __syncthreads();
-  if (threadIdx.x < world)
-    __hip_atomic_store(peers.sig[threadIdx.x] + blockIdx.x * XG_MAXW + rank, (unsigned int)e, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x < world) xg_publish(peers.sig[threadIdx.x] + blockIdx.x * XG_MAXW + rank, (unsigned int)e);
 }
 
 template <bool OPT>
@@ -1141,6 +1177,8 @@ __global__ __launch_bounds__(XB_THR) void wd_xgmi_gather_opt(
     float* __restrict__ s0, float* __restrict__ s1, uint16_t* __restrict__ wt_out,
     long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
   const int t = threadIdx.x;
+  // one wave: a lane-uniform early exit needs no barrier
+  if (xg_failed(err)) return;
   const int q0 = blockIdx.x * XB_THR + t;
   ScState st[4];
   if (OPT) {  // slab-order optimizer state, in flight during the wait
@@ -1151,21 +1189,14 @@ __global__ __launch_bounds__(XB_THR) void wd_xgmi_gather_opt(
   const long long step = OPT ? step_ctr[blockIdx.x] + 1 : 0;
   const unsigned int ue = (unsigned int)e;
   const int nchunks = (stride / 4 + RQ - 1) / RQ;
+  bool ok = true;
   {  // lane t waits for flag (chunk XB_CHUNKS * blockIdx.x + t / world, rank t % world)
     const int c = XB_CHUNKS * blockIdx.x + t / max(world, 1);
-    if (t < XB_CHUNKS * world && c < nchunks) {
-      long long spins = 0;
-      const unsigned int* f = my_sig + c * XG_MAXW + t % world;
-      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ue) < 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1ll << 26)) {  // seconds: a peer is gone; record it and finish (results are garbage)
-          err[0] = 1;
-          break;
-        }
-      }
-    }
+    if (t < XB_CHUNKS * world && c < nchunks) ok = xg_wait(my_sig + c * XG_MAXW + t % world, ue, err);
   }
-  __syncthreads();
+  // any lane's timeout stops the whole wave: no update, no counter advance (err is set)
+  if (__ballot(!ok) != 0ull) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the peers' partials published before their flags
   const int S4 = stride / 4;
   const int q = blockIdx.x * XB_THR + t;
   if (q < S4) {
@@ -1339,7 +1370,7 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(wd_reduce_xgmi_publish, ga, dim3(256), 0, stream, (const float4*)slab, G, stride, pe, world, rank,
-                     xctr);
+                     xctr, err);
   if (wsc == nullptr) {  // plain sum into out
     hipLaunchKernelGGL(wd_xgmi_gather_opt<false>, gb, dim3(XB_THR), 0, stream, stride, pe, world, my_sig, err, xctr,
                        (float4*)out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, OptHyper{}, OptHyper{});

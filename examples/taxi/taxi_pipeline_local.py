@@ -24,7 +24,9 @@ MODULE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "taxi_mod
 
 def create_pipeline(pipeline_name: str, pipeline_root: str, data_root: str, serving_model_dir: str,
                     train_steps: int = 10000, eval_steps: int = 5000, enable_cache: bool = True,
-                    metadata_db_root: str | None = None, batch_size: int = 40, log_root: str | None = None) -> Pipeline:
+                    metadata_db_root: str | None = None, batch_size: int = 40, log_root: str | None = None,
+                    num_gpus: int = 1) -> Pipeline:
+    """num_gpus > 1: the Trainer runs data-parallel, one rank per GPU, batch_size examples per rank per step."""
     examples = csv_input(data_root)
     example_gen = CsvExampleGen(input_base=examples)
     statistics_gen = StatisticsGen(input_data=example_gen.outputs.examples)
@@ -35,7 +37,7 @@ def create_pipeline(pipeline_name: str, pipeline_root: str, data_root: str, serv
     trainer = Trainer(module_file=MODULE_FILE, transformed_examples=transform.outputs.transformed_examples,
                       schema=infer_schema.outputs.output, transform_output=transform.outputs.transform_output,
                       train_args=TrainArgs(num_steps=train_steps), eval_args=EvalArgs(num_steps=eval_steps),
-                      custom_config={"batch_size": batch_size})
+                      custom_config={"batch_size": batch_size, "num_gpus": num_gpus})
     model_analyzer = Evaluator(examples=example_gen.outputs.examples, model_exports=trainer.outputs.output,
                                feature_slicing_spec=FeatureSlicingSpec(
                                    specs=[SingleSlicingSpec(column_for_slicing=["trip_start_hour"])]))
@@ -58,10 +60,11 @@ def main(argv=None):
     ap.add_argument("--eval-steps", type=int, default=5000)
     ap.add_argument("--batch-size", type=int, default=40)
     ap.add_argument("--parallel", type=int, default=2)
+    ap.add_argument("--num-gpus", type=int, default=1, help="data-parallel Trainer ranks (one per GPU)")
     a = ap.parse_args(argv)
     p = create_pipeline("taxi", os.path.join(a.root, "pipelines"), a.data, os.path.join(a.root, "serving_model", "taxi"),
                         a.train_steps, a.eval_steps, metadata_db_root=os.path.join(a.root, "metadata"),
-                        batch_size=a.batch_size)
+                        batch_size=a.batch_size, num_gpus=a.num_gpus)
     res = LocalDagRunner(max_parallel=a.parallel).run(p)
     for cid, r in res.components.items():
         print(f"{cid:>20}: {r.state:9s} exec={r.execution_id} {r.seconds:.2f}s")

@@ -23,7 +23,6 @@ from ..io import dataset
 from ..orchestration import artifact as A
 from ..orchestration.component import BaseComponent, BaseExecutor, ChannelParameter, ComponentSpec, ExecutionParameter
 from ..serving import saved_model
-from ..transform import import_module_file
 from . import proto
 from .statistics import load_schema_from_artifact
 from .transform import table_to_inputs
@@ -43,30 +42,41 @@ class TrainerSpec(ComponentSpec):
 
 
 class TrainerExecutor(BaseExecutor):
-    def Do(self, input_dict, output_dict, exec_properties):  # noqa: N802
-        from ..trainer.estimator import HParams, train_and_evaluate
+    """custom_config["num_gpus"] = N > 1 trains data-parallel: N ranks (one per GPU; gloo processes on a CPU
+    host) launched by mifx.trainer.distributed, each running the same trainer_fn on its shard of every global
+    batch; rank 0 evaluates and exports. Otherwise trainer_fn runs in this process."""
 
-        trainer_fn = import_module_file(exec_properties["module_file"], "trainer_fn")
+    def Do(self, input_dict, output_dict, exec_properties):  # noqa: N802
         ex = {a.split: a.uri for a in input_dict["transformed_examples"]}
         out = output_dict["output"][0]
         targs = proto.from_dict(proto.TrainArgs, exec_properties["train_args"])
         eargs = proto.from_dict(proto.EvalArgs, exec_properties["eval_args"])
-        hp = HParams(train_files=[ex.get("train", next(iter(ex.values())))], eval_files=[ex.get("eval", "")],
-                     transform_output=input_dict["transform_output"][0].uri if input_dict.get("transform_output")
-                     else None, train_steps=targs.num_steps, eval_steps=eargs.num_steps,
-                     serving_model_dir=os.path.join(out.uri, SERVING_DIR),
-                     eval_model_dir=os.path.join(out.uri, EVAL_DIR), warm_start_from=None,
-                     device=self.context.device, custom_config=exec_properties.get("custom_config") or {})
-        schema = load_schema_from_artifact(input_dict["schema"][0].uri)
-        spec = trainer_fn(hp, schema)
-        est = spec["estimator"]
-        metrics, exports = train_and_evaluate(est, spec["train_spec"], spec["eval_spec"])
-        if spec.get("eval_input_receiver_fn") is not None:
-            est.export_saved_model(hp.eval_model_dir, spec["eval_input_receiver_fn"])
+        custom = dict(exec_properties.get("custom_config") or {})
+        hp = dict(train_files=[ex.get("train", next(iter(ex.values())))], eval_files=[ex.get("eval", "")],
+                  transform_output=input_dict["transform_output"][0].uri if input_dict.get("transform_output")
+                  else None, train_steps=targs.num_steps, eval_steps=eargs.num_steps,
+                  serving_model_dir=os.path.join(out.uri, SERVING_DIR),
+                  eval_model_dir=os.path.join(out.uri, EVAL_DIR), warm_start_from=custom.get("warm_start_from"),
+                  device=self.context.device, custom_config=custom)
+        module_file, schema_uri = exec_properties["module_file"], input_dict["schema"][0].uri
+        n = int(custom.get("num_gpus", 1) or 1)
+        if n > 1:
+            from ..trainer import distributed
+
+            res = distributed.launch({"module_file": module_file, "hparams": hp, "schema_uri": schema_uri,
+                                      "out_dir": out.uri, "work_dir": os.path.join(out.uri, "dp_run")},
+                                     n, os.path.join(out.uri, "dp_run"), timeout=custom.get("timeout_s"))
+        else:
+            from ..trainer.distributed import run_trainer_fn
+
+            res = run_trainer_fn(module_file, hp, schema_uri, out.uri)
+        metrics = res["eval"]
         with open(os.path.join(out.uri, "metrics.json"), "w") as f:
-            json.dump({"eval": metrics, "exports": exports,
-                       "train_examples_per_sec": getattr(est, "examples_per_sec", None)}, f, default=float)
+            json.dump(res, f, default=float)
         out.custom_properties["train_steps"] = int(targs.num_steps)
+        out.custom_properties["num_replicas"] = int(res.get("world_size") or 1)
+        if res.get("train_examples_per_sec"):
+            out.custom_properties["train_examples_per_sec"] = float(res["train_examples_per_sec"])
         for k in ("accuracy", "auc", "average_loss"):
             if k in metrics and metrics[k] == metrics[k]:
                 out.custom_properties[f"eval_{k}"] = float(metrics[k])
@@ -121,7 +131,7 @@ class EvaluatorExecutor(BaseExecutor):
         fss = proto.from_dict(proto.FeatureSlicingSpec, exec_properties.get("feature_slicing_spec")) or \
             proto.FeatureSlicingSpec()
         specs = [em.SliceSpec(columns=list(s.column_for_slicing)) for s in fss.specs]
-        res = em.compute_sliced_metrics(y, p, raw, specs)
+        res = em.compute_sliced_metrics(y, p, raw, specs, device=self.context.device)
         res.model_location, res.data_location = model_uri, ex.get("eval", "")
         out = output_dict["output"][0]
         em.save_eval_result(res, out.uri)
@@ -166,14 +176,19 @@ class ModelValidatorExecutor(BaseExecutor):
         cand = input_dict["model"][0]
         metric = exec_properties.get("metric") or "auc"
         tol = float(exec_properties.get("tolerance") or 0.0)
+        dev = self.context.device
+
+        def score(y, p):  # overall metric: one GPU segmented reduction on a device, else the host pass
+            return em.compute_sliced_metrics(y, p, {}, None, device=dev).overall()[metric]
+
         y, p, _ = _eval_predictions(cand.uri, eval_uri)
-        cur = em.binary_metrics(y, p)[metric]
+        cur = score(y, p)
         out = output_dict["blessing"][0]
         prev = self._last_blessed()
         blessed, base = True, None
         if prev is not None and os.path.exists(prev[0]):
             yb, pb, _ = _eval_predictions(prev[0], eval_uri)
-            base = em.binary_metrics(yb, pb)[metric]
+            base = score(yb, pb)
             lower_is_better = metric in ("average_loss", "loss")
             blessed = cur <= base + tol if lower_is_better else cur >= base - tol
         with open(os.path.join(out.uri, "BLESSED" if blessed else "NOT_BLESSED"), "w") as f:

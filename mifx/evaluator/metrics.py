@@ -47,6 +47,28 @@ def binary_metrics(y: np.ndarray, p: np.ndarray, weights: np.ndarray | None = No
             "calibration": float(p.mean() / y.mean()) if y.mean() > 0 else float("nan")}
 
 
+HIST_BUCKETS = 10000  # TFMA's AUC: confusion matrices at 10000 thresholds (num_buckets of tfma's auc metric)
+
+
+def binary_metrics_from_hist(sums: np.ndarray, hist: np.ndarray) -> dict:
+    """Slice metrics from the GPU segmented reduction (mifx.ops.analyzers.segment_hist): sums = [count, label
+    sum, prediction sum, loss sum, correct], hist = [buckets, (neg, pos)] of clipped probabilities. AUC is the
+    bucketed (TFMA-style) one; precision / recall count predictions in buckets above one half."""
+    from ..ops.analyzers import auc_from_hist
+
+    n = float(sums[0])
+    if n == 0:
+        return {"example_count": 0}
+    nb = hist.shape[0]
+    tp, fp = float(hist[nb // 2:, 1].sum()), float(hist[nb // 2:, 0].sum())
+    fn = float(hist[:nb // 2, 1].sum())
+    ym, pm = sums[1] / n, sums[2] / n
+    return {"example_count": int(n), "accuracy": float(sums[4] / n), "auc": auc_from_hist(hist),
+            "average_loss": float(sums[3] / n), "precision": tp / (tp + fp) if tp + fp else float("nan"),
+            "recall": tp / (tp + fn) if tp + fn else float("nan"), "label/mean": float(ym),
+            "prediction/mean": float(pm), "calibration": float(pm / ym) if ym > 0 else float("nan")}
+
+
 @dataclass
 class SliceSpec:
     columns: list = field(default_factory=list)
@@ -86,8 +108,12 @@ class EvalResult:
 
 
 def compute_sliced_metrics(labels, preds, features: dict, specs: list[SliceSpec] | None = None,
-                           min_slice_size: int = 1) -> EvalResult:
+                           min_slice_size: int = 1, device=None) -> EvalResult:
+    """device = a GPU: every slice spec is ONE segmented reduction (csrc/analyzers.hip segment_hist: per-slice
+    sums + label-split prediction histograms) instead of a host pass per slice value; AUC is then bucketed."""
     y, p = np.asarray(labels), np.asarray(preds)
+    if device is not None and str(device).startswith("cuda"):
+        return _sliced_metrics_gpu(y, p, features, specs, min_slice_size, device)
     res = EvalResult()
     specs = specs or [SliceSpec()]
     if not any(not s.columns and not s.feature_values for s in specs):
@@ -108,6 +134,37 @@ def compute_sliced_metrics(labels, preds, features: dict, specs: list[SliceSpec]
                 continue
             sl = [[c, (None if (isinstance(v, float) and np.isnan(v)) else v)] for c, v in zip(spec.columns, vals)]
             res.slices.append({"slice": sl + fixed, "spec": spec.key(), "metrics": binary_metrics(y[rows], p[rows])})
+    return res
+
+
+def _sliced_metrics_gpu(y, p, features, specs, min_slice_size, device) -> EvalResult:
+    from ..ops.analyzers import segment_hist
+
+    res = EvalResult()
+    specs = specs or [SliceSpec()]
+    if not any(not s.columns and not s.feature_values for s in specs):
+        specs = [SliceSpec()] + list(specs)
+    for spec in specs:
+        mask = np.ones(len(y), bool)
+        for k, v in spec.feature_values.items():
+            mask &= np.asarray([str(x) == str(v) for x in features[k]])
+        fixed = [[k, v] for k, v in sorted(spec.feature_values.items())]
+        if spec.columns:
+            keys = pd.DataFrame({c: np.asarray(features[c], dtype=object) for c in spec.columns})
+            codes, uniq = pd.MultiIndex.from_frame(keys).factorize(sort=True)
+            seg = np.where(mask, codes, -1).astype(np.int32)
+            values = list(uniq)
+        else:
+            seg = np.where(mask, 0, -1).astype(np.int32)
+            values = [()]
+        sums, hist = segment_hist(seg, y, p, max(1, len(values)), HIST_BUCKETS, device=device)
+        for i, vals in enumerate(values):
+            if spec.columns and sums[i, 0] < max(1, min_slice_size):
+                continue
+            vals = vals if isinstance(vals, tuple) else (vals,)
+            sl = [[c, (None if (isinstance(v, float) and np.isnan(v)) else v)] for c, v in zip(spec.columns, vals)]
+            res.slices.append({"slice": sl + fixed, "spec": spec.key(), "metrics": binary_metrics_from_hist(
+                sums[i], hist[i])})
     return res
 
 

@@ -44,7 +44,10 @@ def supported(model: torch.nn.Module, x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.float32 and x.shape[-2:] == (28, 28) and x.numel() == x.shape[0] * 784
 
 
-def per_microbatch_grads(model: torch.nn.Module, x: torch.Tensor, y: torch.Tensor, num_microbatches: int):
+def per_microbatch_grads(model: torch.nn.Module, x: torch.Tensor, y: torch.Tensor, num_microbatches: int,
+                         max_bytes: int | None = None):
+    """max_bytes bounds the per-example scratch [B, LD] fp32: above it the kernel writes the M microbatch rows
+    directly (one workgroup per microbatch) instead of one row per example."""
     B = x.shape[0]
     M = int(num_microbatches)
     if B % M:
@@ -56,6 +59,8 @@ def per_microbatch_grads(model: torch.nn.Module, x: torch.Tensor, y: torch.Tenso
     yc = y.detach().to(torch.int64).contiguous()
     # One workgroup per example (B workgroups fill the chip even when M is small), then the microbatch sums.
     rows = B if M < B and B <= 65536 else M
+    if max_bytes is not None and rows != M and rows * LD * 4 > max_bytes:
+        rows = M
     G = torch.empty(rows, LD, dtype=torch.float32, device=x.device)
     loss = torch.empty(B, dtype=torch.float32, device=x.device)
     check(_fns()["grads"](ptr(xc), ptr(yc), B, rows, *[ptr(p) for p in ps], ptr(G), LD, ptr(loss),

@@ -83,6 +83,26 @@ def keep_mask(n: int, rng: torch.Tensor, site: int, p: float) -> torch.Tensor:
     return torch.from_numpy(keep)
 
 
+def _snap(rng, p) -> torch.Tensor | None:
+    """Device copy of the dropout RNG state taken when the forward runs (None without dropout)."""
+    return rng.detach().clone() if (rng is not None and p > 0) else None
+
+
+def device_keep_mask(n: int, rng: torch.Tensor, site: int, p: float, device) -> torch.Tensor:
+    """keep_mask computed on the GPU (no host sync; graph-capturable): the dropout kernel applied to ones."""
+    ones = torch.ones(n, device=device, dtype=torch.float32)
+    y = torch.empty_like(ones)
+    check(_fns()["dropout"](_dt(ones), ptr(ones), n, float(p), ptr(rng), int(site), ptr(y), stream_handle(device)),
+          "mifx_bert_dropout(mask)")
+    return y != 0
+
+
+def _mask(n: int, rng, site: int, p: float, device) -> torch.Tensor:
+    if torch.device(device).type == "cuda" and rng is not None and rng.is_cuda and not _TORCH_OPS:
+        return device_keep_mask(n, rng, site, p, device)
+    return keep_mask(n, rng, site, p).to(device)
+
+
 def _drop_scale(p: float) -> float:
     return float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
 
@@ -106,7 +126,9 @@ class _BiasDropAddLN(torch.autograd.Function):
                                float(p), ptr(rng if p > 0 else None), int(site), ptr(y), ptr(mean), ptr(rstd),
                                stream_handle(a.device)), "mifx_bert_bdaln_fwd")
         ctx.save_for_backward(a, r, wp, biasp, mean, rstd)
-        ctx.rng, ctx.p, ctx.site = rng, float(p), int(site)  # rng is advanced only between steps
+        # snapshot of [seed, counter] at forward time (a device copy, graph-capturable): the backward recomputes
+        # the forward's mask even if the live counter advanced in between (activation re-forward, 2 forwards)
+        ctx.rng, ctx.p, ctx.site = _snap(rng, p), float(p), int(site)
         ctx.wdtype = w.dtype
         ctx.bdtype = None if bias is None else bias.dtype
         return y
@@ -141,7 +163,7 @@ class _Dropout(torch.autograd.Function):
         y = torch.empty_like(x)
         check(_fns()["dropout"](_dt(x), ptr(x), x.numel(), float(p), ptr(rng), int(site), ptr(y),
                                 stream_handle(x.device)), "mifx_bert_dropout")
-        ctx.rng, ctx.p, ctx.site = rng, float(p), int(site)
+        ctx.rng, ctx.p, ctx.site = _snap(rng, p), float(p), int(site)
         return y
 
     @staticmethod
@@ -303,7 +325,7 @@ def bias_dropout_add_layernorm(a: torch.Tensor, bias, r: torch.Tensor, weight, l
         return _BiasDropAddLN.apply(a, bias, r, weight, ln_bias, eps, p, rng, site)
     x = a if bias is None else a + bias.to(a.dtype)
     if p > 0:
-        keep = keep_mask(x.numel(), rng, site, p).to(x.device).view(x.shape)
+        keep = _mask(x.numel(), rng, site, p, x.device).view(x.shape)
         x = torch.where(keep, x * _drop_scale(p), torch.zeros((), dtype=x.dtype, device=x.device))
     return F.layer_norm(x + r, (a.shape[-1],), weight, ln_bias, eps)
 
@@ -355,7 +377,7 @@ class _Attention(torch.autograd.Function):
                                  ptr(rng if p > 0 else None), int(site), ptr(out), ptr(lse), stream_handle(qkv.device)),
               "mifx_attn_fwd")
         ctx.save_for_backward(qkv, kb, out, lse)
-        ctx.args = (float(scale), float(p), rng, int(site), int(h0), int(htot))
+        ctx.args = (float(scale), float(p), _snap(rng, p), int(site), int(h0), int(htot))
         return out
 
     @staticmethod
@@ -384,7 +406,7 @@ def attention_reference(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, 
         s = s + kbias.float()[:, None, None, :]
     pr = torch.softmax(s, -1)
     if p > 0:
-        keep = keep_mask(B * htot * S * S, rng, site, p).view(B, htot, S, S)[:, h0:h0 + H].to(pr.device)
+        keep = _mask(B * htot * S * S, rng, site, p, pr.device).view(B, htot, S, S)[:, h0:h0 + H]
         pr = torch.where(keep, pr * _drop_scale(p), torch.zeros((), dtype=pr.dtype, device=pr.device))
     return torch.einsum("bhij,bjhd->bihd", pr, v.float()).to(qkv.dtype)
 
@@ -399,4 +421,9 @@ def attention(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, rng=None, 
     if (qkv.is_cuda and not _TORCH_OPS and qkv.shape[1] in ATTN_SEQ and qkv.shape[4] == 64
             and qkv.dtype == torch.bfloat16):
         return _Attention.apply(qkv, kbias, scale, p, rng, site, h0, htot)
+    if qkv.is_cuda and not p > 0:  # other shapes without dropout: the library flash kernel, no S x S tensor
+        q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+        am = None if kbias is None else kbias[:, None, None, :].to(q.dtype)
+        return F.scaled_dot_product_attention(q, k, v, attn_mask=am, scale=scale).transpose(1, 2)
+    # with dropout: the reference composition, its counter-based mask drawn on the device (graph-capturable)
     return attention_reference(qkv, kbias, scale, p, rng, site, h0, htot)

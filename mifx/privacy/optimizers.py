@@ -124,7 +124,7 @@ class DPOptimizer:
         """MNIST tutorial CNN on the GPU: all M microbatch gradients from one kernel (csrc/dpsgd_mnist.hip),
         then the same fused clip / sum / noise pass as the generic path, written straight into one flat gradient
         buffer whose slices become the parameters' .grad (no per-parameter copies, no host sync)."""
-        G, losses = dpsgd_mnist.per_microbatch_grads(model, x, y, M)
+        G, losses = dpsgd_mnist.per_microbatch_grads(model, x, y, M, max_bytes=self.max_g_bytes)
         flat = getattr(self, "_flat_grad", None)
         if flat is None or flat.device != G.device:
             flat = self._flat_grad = torch.empty(G.shape[1], dtype=torch.float32, device=G.device)

@@ -67,10 +67,35 @@ class HParams:
         return dict(self.__dict__)
 
 
+def _dist_info() -> tuple[object, int, int]:
+    """(process group, rank, world) when this process is one rank of a data-parallel Trainer
+    (mifx.trainer.distributed), else (None, 0, 1)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.group.WORLD, dist.get_rank(), dist.get_world_size()
+    return None, 0, 1
+
+
 def _default_device(cfg: RunConfig) -> torch.device:
-    if cfg.device:
-        return torch.device(cfg.device)
-    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device(cfg.device) if cfg.device else \
+        (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    if dev.type == "cuda" and dev.index is None:  # one process per GPU: this rank's device
+        shared = os.environ.get("MIFX_SHARED_GPU") == "1"  # multi-rank rehearsal on one GPU
+        dev = torch.device("cuda", 0 if shared else int(os.environ.get("LOCAL_RANK", 0)))
+    return dev
+
+
+def shard_records(records: torch.Tensor, rank: int, world: int, batch: int) -> torch.Tensor:
+    """Rank `rank`'s shard for data parallelism with per-replica batch `batch`: the records are cut into global
+    batches of world * batch (remainder dropped) and rank r takes slice r of every global batch, so step i of
+    the DP job trains on exactly the examples of step i of one process at batch world * batch."""
+    g = world * batch
+    n = records.shape[0] // g * g
+    if n == 0:
+        raise ValueError(f"{records.shape[0]} records < one global batch ({world} x {batch})")
+    return records[:n].reshape(n // g, world, batch, *records.shape[1:])[:, rank].reshape(-1, *records.shape[1:]) \
+        .contiguous()
 
 
 def _auc(labels: np.ndarray, scores: np.ndarray) -> float:
@@ -98,8 +123,14 @@ class WideDeepEstimator:
     """DNNLinearCombinedClassifier equivalent for the taxi feature set."""
 
     def __init__(self, config: RunConfig, hidden_units: list[int] | None = None, warm_start_from: str | None = None,
-                 batch_size: int = 40, loss_reduction: str = "sum", dnn_optimizer=None, linear_optimizer=None):
+                 batch_size: int = 40, loss_reduction: str = "sum", dnn_optimizer=None, linear_optimizer=None,
+                 steps_per_graph: int = 100):
+        """batch_size is per replica: a data-parallel Trainer with N ranks trains on N x batch_size examples per
+        step (TF distributed Estimator semantics). steps_per_graph: training steps per hipGraph replay on the
+        GPU (checkpoint boundaries and max_steps are honoured exactly; remainders replay a one-step graph)."""
         self.config = config
+        self.pg, self.rank, self.world = _dist_info()
+        self.steps_per_graph = int(steps_per_graph)
         self.cfg = wdm.WideDeepConfig(hidden_units=list(hidden_units or wdm.dnn_hidden_units()))
         self.device = _default_device(config)
         self.batch_size = batch_size
@@ -122,6 +153,7 @@ class WideDeepEstimator:
         return c[-1] if c else None
 
     def _restore(self, path: str) -> None:
+        """Model weights, the optimizer slots (canonical s0 / s1, either trainer's) and the global step."""
         sd = load_file(path)
         self.global_step = int(sd.pop("global_step").item()) if "global_step" in sd else 0
         self.model.load_state_dict({k: v for k, v in sd.items() if not k.startswith("opt.")}, strict=False)
@@ -136,16 +168,26 @@ class WideDeepEstimator:
         self.model.load_state_dict({k: v for k, v in sd.items() if k in self.model.state_dict()}, strict=False)
 
     def _save_checkpoint(self) -> None:
+        """Rank 0 writes ckpt-<step>.safetensors (weights, canonical optimizer slots, global step); every rank of
+        a data-parallel job meets at a host barrier afterwards, so no replica waits on the device meanwhile."""
         d = self.config.model_dir
-        if not d:
-            return
-        os.makedirs(d, exist_ok=True)
-        sd = {k: v.detach().cpu().contiguous() for k, v in self.model.state_dict().items()}
-        sd["global_step"] = torch.tensor([self.global_step], dtype=torch.int64)
         tr = self._trainer
-        if tr is not None and hasattr(tr, "s0"):
-            sd["opt.s0"], sd["opt.s1"] = tr.s0.cpu(), tr.s1.cpu()
-        save_file(sd, os.path.join(d, f"ckpt-{self.global_step}.safetensors"))
+        if d and self.rank == 0:
+            os.makedirs(d, exist_ok=True)
+            sd = {k: v.detach().cpu().contiguous() for k, v in self.model.state_dict().items()}
+            sd["global_step"] = torch.tensor([self.global_step], dtype=torch.int64)
+            if tr is not None:
+                st = tr.state_dict()
+                sd["opt.s0"], sd["opt.s1"] = st["s0"].cpu().contiguous(), st["s1"].cpu().contiguous()
+            save_file(sd, os.path.join(d, f"ckpt-{self.global_step}.safetensors"))
+            self._prune_checkpoints(d)
+        self._barrier()
+
+    def _barrier(self) -> None:
+        if self.pg is not None:
+            torch.distributed.barrier(group=self.pg)
+
+    def _prune_checkpoints(self, d: str) -> None:
         ck = sorted(glob.glob(os.path.join(d, "ckpt-*.safetensors")),
                     key=lambda p: int(p.rsplit("-", 1)[1].split(".")[0]))
         for old in ck[:-max(1, self.config.keep_checkpoint_max)]:
@@ -158,40 +200,89 @@ class WideDeepEstimator:
 
         dopt = self.dnn_optimizer or default_dnn_opt()
         wopt = self.linear_optimizer or default_wide_opt(len(self.cfg.wide))
+        if self.pg is not None:
+            records = shard_records(records, self.rank, self.world, self.batch_size)
         bs = min(self.batch_size, records.shape[0])
         if self.device.type == "cuda":
             tr = FusedWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
-                                      loss_reduction=self.loss_reduction)
-            if getattr(self, "_opt_state", None):
-                tr.set_master_state(s0=self._opt_state["s0"], s1=self._opt_state["s1"])
-            tr.set_step(self.global_step)
+                                      loss_reduction=self.loss_reduction, process_group=self.pg)
         else:
             tr = TorchWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
-                                      loss_reduction=self.loss_reduction)
-            tr.step_idx = self.global_step
+                                      loss_reduction=self.loss_reduction, process_group=self.pg)
+        st = getattr(self, "_opt_state", None) or {}
+        tr.load_state_dict({"param": None, "s0": st.get("s0"), "s1": st.get("s1"),
+                            "step": torch.tensor([self.global_step])})
         tr.set_data(records)
         return tr
 
+    def _graph_setup(self, tr) -> None:
+        """GPU: capture S-step hipGraphs (data-parallel: the xGMI exchange inside the graph, the direct RCCL
+        path if its validation fails on any rank). The first steps already ran eagerly (lazy kernel / module
+        initialisation), so capture runs no warmup steps of its own."""
+        if self.pg is None:
+            tr.capture(warmup=0, steps_per_graph=self.steps_per_graph)
+            return
+        ok = True
+        try:
+            tr.capture(warmup=0, steps_per_graph=self.steps_per_graph, dp_mode="xgmi")
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            import sys
+
+            print(f"[estimator] xGMI exchange unavailable ({e}); using the RCCL path", file=sys.stderr)
+            ok = False
+        fdev = self.device if torch.distributed.get_backend(self.pg) == "nccl" else torch.device("cpu")
+        flag = torch.tensor([0.0 if ok else 1.0], device=fdev)
+        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX, group=self.pg)
+        if flag.item() != 0.0:
+            tr.disable_xgmi()
+            tr.capture(warmup=0, steps_per_graph=self.steps_per_graph, dp_mode="direct")
+
     def train(self, input_fn: Callable, max_steps: int, hooks: list | None = None) -> "WideDeepEstimator":
+        """Train to global step `max_steps` (resuming from the latest checkpoint in model_dir), checkpointing
+        every save_checkpoints_steps. On the GPU the steps between checkpoints run as multi-step hipGraph
+        replays (per-step `hooks` force one host step at a time)."""
         records = input_fn()
         self._trainer = tr = self._make_trainer(records)
         every = self.config.save_checkpoints_steps or 0
+        cuda = self.device.type == "cuda"
         t0, n0 = time.time(), self.global_step
+        eager_first = 2  # lazy initialisation before any capture
+        graphs = cuda and not hooks
         while self.global_step < max_steps:
-            tr.step()
-            self.global_step += 1
+            nxt = max_steps
+            if every:
+                nxt = min(nxt, (self.global_step // every + 1) * every)
+            if hooks or (graphs and eager_first > 0):
+                tr.step()
+                self.global_step += 1
+                eager_first -= 1
+                for h in hooks or []:
+                    h(self.global_step, tr)
+                if graphs and eager_first == 0 and getattr(tr, "graph", None) is None:
+                    self._graph_setup(tr)
+            else:
+                tr.run(nxt - self.global_step)
+                self.global_step = nxt
             if every and self.global_step % every == 0:
                 tr.sync_to_model()
                 self._save_checkpoint()
-            for h in hooks or []:
-                h(self.global_step, tr)
-        if self.device.type == "cuda":
+        if cuda:
             torch.cuda.synchronize(self.device)
         self.train_seconds = time.time() - t0
-        self.examples_per_sec = (self.global_step - n0) * tr.batch / max(self.train_seconds, 1e-9)
+        # whole-job rate: every replica trains batch examples per step
+        self.examples_per_sec = (self.global_step - n0) * tr.batch * self.world / max(self.train_seconds, 1e-9)
         tr.sync_to_model()
-        self._save_checkpoint()
+        if not (every and self.global_step % every == 0):
+            self._save_checkpoint()
+        if hasattr(tr, "steps_done"):
+            assert tr.steps_done == self.global_step, (tr.steps_done, self.global_step)
         return self
+
+    def close(self) -> None:
+        """Release the data-parallel exchange (collective: every rank calls it after train_and_evaluate)."""
+        tr = self._trainer
+        if tr is not None and getattr(tr, "_xg", None) is not None:
+            tr.disable_xgmi()
 
     def predict_logits(self, records: torch.Tensor) -> np.ndarray:
         if self.device.type == "cuda":
@@ -204,7 +295,8 @@ class WideDeepEstimator:
 
     def evaluate(self, input_fn: Callable, steps: int | None = None, name: str | None = None) -> dict:
         records = input_fn()
-        n = records.shape[0] if not steps else min(records.shape[0], steps * self.batch_size)
+        # `steps` batches of the global batch (a data-parallel job's rank 0 evaluates what all ranks would)
+        n = records.shape[0] if not steps else min(records.shape[0], steps * self.batch_size * self.world)
         records = records[:n]
         logits = self.predict_logits(records)
         _, _, label = wdm.records_to_tensors(records.cpu())
@@ -237,7 +329,10 @@ class WideDeepEstimator:
 
 
 def train_and_evaluate(estimator, train_spec: TrainSpec, eval_spec: EvalSpec) -> tuple[dict, list[str]]:
+    """Data-parallel ranks all train; rank 0 alone evaluates and exports (the others return ({}, []))."""
     estimator.train(train_spec.input_fn, max_steps=train_spec.max_steps)
+    if getattr(estimator, "rank", 0) != 0:
+        return {}, []
     metrics = estimator.evaluate(eval_spec.input_fn, steps=eval_spec.steps, name=eval_spec.name)
     exports = []
     for ex in eval_spec.exporters:
@@ -247,4 +342,4 @@ def train_and_evaluate(estimator, train_spec: TrainSpec, eval_spec: EvalSpec) ->
 
 
 __all__ = ["RunConfig", "TrainSpec", "EvalSpec", "FinalExporter", "HParams", "WideDeepEstimator",
-           "train_and_evaluate", "Any"]
+           "train_and_evaluate", "shard_records", "Any"]

@@ -53,8 +53,10 @@ class TaxiDNNTrainer:
         self.n = len(self.label)
         if self.n < self.batch:
             raise ValueError(f"{self.n} records < batch {self.batch}")
-        if self.native:  # the device counter continues from the host's step count (graphs read the same tensors)
+        if self.native:  # the device counter continues from the host's step count
             self.step_ctr.fill_(self.step_idx)
+        # captured graphs hold the previous tensors' addresses and record count: recapture on the next step
+        self.graph, self.graph_multi = None, None
 
     def _idx(self):
         s = (self.step_idx * self.batch) % self.n

@@ -389,3 +389,41 @@ def test_bert_trainer_main_default_config_stays_finite(capsys):
     assert out["hipgraph"] is True
     assert np.isfinite(out["loss"]), out
     assert out["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bert_seq256_dropout_hipgraph_stays_finite():
+    """S=256 is outside the fused attention kernel's shapes: with dropout on, the fallback draws its mask on the
+    device (no host sync), so the whole step still captures into a hipGraph (regression: the host mask broke
+    capture)."""
+    from mifx.trainer.bert_trainer import BertTrainer
+
+    cfg = BertConfig(layers=2, dropout=0.1)
+    tr = BertTrainer(cfg, 4, 256, "cuda", graph=True)
+    losses = [float(tr.step()) for _ in range(4)]
+    assert tr.graph is not None
+    assert all(np.isfinite(losses)), losses
+
+
+@pytest.mark.gpu
+def test_attention_fallback_device_mask_matches_host_mask():
+    import mifx.ops.fused_bert as fb
+
+    rng = torch.tensor([7, 3], dtype=torch.int64, device="cuda")
+    dev = fb.device_keep_mask(4 * 2 * 256 * 256, rng, 1005, 0.1, torch.device("cuda")).cpu()
+    host = fb.keep_mask(4 * 2 * 256 * 256, rng, 1005, 0.1)
+    assert torch.equal(dev, host)
+
+
+@pytest.mark.gpu
+def test_dropout_backward_uses_forward_time_rng_snapshot():
+    """Advancing the live counter between forward and backward must not change the backward's mask."""
+    import mifx.ops.fused_bert as fb
+
+    x = torch.randn(64, 256, device="cuda", requires_grad=True)
+    rng = torch.tensor([11, 0], dtype=torch.int64, device="cuda")
+    y = fb.dropout(x, 0.3, rng, 2)
+    rng[1:].add_(5)  # e.g. a second training forward before this backward
+    y.backward(torch.ones_like(y))
+    keep = (y.detach() != 0).float()
+    torch.testing.assert_close(x.grad, keep / 0.7, rtol=1e-6, atol=1e-6)

@@ -159,7 +159,7 @@ def _xgmi_worker(rank, world, port, out_dir, steps, batch, spg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,batch", [(2, 512), (4, 512), (2, 8192)])
+@pytest.mark.parametrize("world,batch", [(2, 512), (4, 512), (2, 8192), (2, 65536), (4, 65536)])
 def test_xgmi_dp_step_matches_split_phase(world, batch):
     """Data parallelism over the one-shot xGMI exchange (IPC-shared HBM partials + epoch flags, csrc/xgmi.hip,
     wd_xgmi_opt): `world` processes share cuda:0 (the IPC path is the same as across GPUs) and run the step in
@@ -179,3 +179,47 @@ def test_xgmi_dp_step_matches_split_phase(world, batch):
         assert torch.equal(got[0]["xgmi"], got[0]["split"])
     else:  # 4 ranks / XCD-local local sums: same math, other fp32 association
         np.testing.assert_allclose(got[0]["xgmi"].numpy(), got[0]["split"].numpy(), rtol=1e-4, atol=2e-6)
+
+
+def _xgmi_timeout_worker(rank, world, port, out_dir, batch):
+    from mifx.data.synthetic import synthetic_records
+    from mifx.models import wide_deep as wdm
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device="cuda:0",
+                                  process_group=dist.group.WORLD)
+        tr.set_data(synthetic_records(batch * 2, device="cuda:0", seed=3))
+        tr.enable_xgmi()  # collective self-test: both ranks healthy so far
+        res = {}
+        if rank == 0:  # rank 1 never joins the step: rank 0's wait must time out and leave the weights alone
+            p0, s0 = tr.param.clone(), tr.s0.clone()
+            tr._step_impl()
+            tr._step_impl()  # the sticky error: a second exchange step does nothing at once
+            torch.cuda.synchronize()
+            res["err"] = int(tr._xg.err.item())
+            res["param_unchanged"] = bool(torch.equal(tr.param, p0) and torch.equal(tr.s0, s0))
+            try:
+                tr.last_loss()
+                res["raised"] = False
+            except RuntimeError:
+                res["raised"] = True
+        dist.barrier()
+        tr.disable_xgmi()
+        torch.save(res, os.path.join(out_dir, f"to{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [512, 65536])
+def test_xgmi_timeout_sets_err_skips_update_and_raises(batch):
+    """A peer that never publishes: the bounded wall-clock wait (10 s) sets the sticky err flag, the exchange
+    kernels then skip the parameter update and the counter advance, and the trainer raises at its next host sync
+    instead of training on garbage (one-pass path at 512, XCD-local path at 65536)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_xgmi_timeout_worker, args=(2, _free_port(), d, batch), nprocs=2, start_method="spawn")
+        r = torch.load(os.path.join(d, "to0.pt"), weights_only=True)
+    assert r == {"err": 1, "param_unchanged": True, "raised": True}

@@ -84,3 +84,23 @@ def test_hip_graph_run_matches_cpu_oracle(batch, steps, spg):
     for n in ("W1", "b1", "w2", "b2"):
         torch.testing.assert_close(getattr(gpu.model, n).detach().cpu(), getattr(cpu.model, n).detach(),
                                    rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_set_data_twice_recaptures_graphs():
+    """set_data after graph replays must drop the captured graphs (they hold the old tensors' addresses and
+    record count); training on the new data then matches the CPU oracle fed the same two data sets."""
+    cfg = TaxiDNNConfig()
+    a = _data(32 * 4 + 5, cfg, seed=11)
+    b = _data(32 * 2 + 3, cfg, seed=12)
+    cpu = TaxiDNNTrainer(TaxiDNN(cfg, seed=5), batch=32, lr=0.1, device="cpu")
+    gpu = TaxiDNNTrainer(TaxiDNN(cfg, seed=5), batch=32, lr=0.1, device="cuda", steps_per_graph=3)
+    for d in (a, b):
+        for tr in (cpu, gpu):
+            tr.set_data(*d)
+            tr.run(8)
+        assert gpu.graph is not None
+    assert gpu.last_loss() == pytest.approx(cpu.last_loss(), rel=2e-4)
+    for n in ("W1", "b1", "w2", "b2"):
+        torch.testing.assert_close(getattr(gpu.model, n).detach().cpu(), getattr(cpu.model, n).detach(),
+                                   rtol=2e-4, atol=2e-5)
