@@ -44,7 +44,7 @@ def load_gemm_table(path: str = GEMM_TABLE) -> bool:
 def synthetic_batch(cfg: BertConfig, batch: int, seq: int, device, seed: int = 0):
     """Same tokens on every TP rank (TP ranks consume one replicated batch)."""
     g = torch.Generator().manual_seed(seed)
-    ids = torch.randint(1000, cfg.vocab_size, (batch, seq), generator=g)
+    ids = torch.randint(min(1000, cfg.vocab_size // 4), cfg.vocab_size, (batch, seq), generator=g)
     ids[:, 0] = 101  # [CLS]
     tt = torch.zeros(batch, seq, dtype=torch.long)
     tt[:, seq // 2:] = 1
@@ -87,6 +87,22 @@ class BertTrainer:
         self.sdpa = sdpa  # None = PyTorch's choice; "math" / "efficient" / "flash" pins the SDPA backend
         self.graph = None
         self.static_loss = None
+
+    def set_batch(self, ids, tt, am, y) -> None:
+        """Next training batch, copied INTO the step's input tensors (a captured hipGraph reads these same
+        buffers on every replay)."""
+        for dst, src in zip(self.data, (ids, tt, am, y)):
+            dst.copy_(src.to(dst.dtype), non_blocking=True)
+
+    @torch.no_grad()
+    def predict(self, ids, tt, am) -> torch.Tensor:
+        """Eval-mode logits (every TP rank must call it: the forward all-reduces)."""
+        self.model.eval()
+        try:
+            with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
+                return self.model(ids.to(self.device), tt.to(self.device), am.to(self.device).float()).float()
+        finally:
+            self.model.train()
 
     def _eager_step(self) -> torch.Tensor:
         ids, tt, am, y = self.data

@@ -97,6 +97,13 @@ def run_trainer_fn(module_file: str, hp_values: dict, schema_uri: str, out_dir: 
         metrics, exports = train_and_evaluate(est, spec["train_spec"], spec["eval_spec"])
         if getattr(est, "rank", 0) == 0 and spec.get("eval_input_receiver_fn") is not None:
             est.export_saved_model(hp.eval_model_dir, spec["eval_input_receiver_fn"])
+        dump = (hp_values.get("custom_config") or {}).get("dump_replicas_dir")
+        if dump:  # every rank's final weights (replica-agreement checks)
+            import torch
+
+            os.makedirs(dump, exist_ok=True)
+            torch.save({k: v.detach().cpu() for k, v in est.model.state_dict().items()},
+                       os.path.join(dump, f"replica{getattr(est, 'rank', 0)}.pt"))
     finally:
         if hasattr(est, "close"):
             est.close()
@@ -111,13 +118,21 @@ def worker_main(spec_path: str) -> int:
 
     from ..parallel import dist as mdist
 
+    spec.setdefault("hparams", {})
     cpu = spec["hparams"].get("device") == "cpu" or not torch.cuda.is_available()
     env = mdist.init("gloo" if cpu else None)
     try:
         hp = dict(spec["hparams"])
         if hp.get("device") in (None, "cuda") and torch.cuda.is_available():
             hp["device"] = "cuda"  # the estimator picks cuda:LOCAL_RANK (cuda:0 under MIFX_SHARED_GPU)
-        res = run_trainer_fn(spec["module_file"], hp, spec["schema_uri"], spec["out_dir"])
+        target = spec.get("target")
+        if target:  # another per-rank entry point (e.g. the BERT tensor-parallel Trainer): module:function(spec)
+            import importlib
+
+            mod, _, fn = target.partition(":")
+            res = getattr(importlib.import_module(mod), fn)(spec)
+        else:
+            res = run_trainer_fn(spec["module_file"], hp, spec["schema_uri"], spec["out_dir"])
         if env.rank == 0:
             with open(os.path.join(spec["work_dir"], RESULT), "w") as f:
                 json.dump(res, f, default=float)

@@ -50,7 +50,7 @@ def test_launch_local_ranks(tmp_path, kind, key, roles):
 
 
 def test_render_indexed_job(tmp_path):
-    spec = JobSpec.from_yaml("deploy/k8s/wide-deep-dp8-job.yaml")
+    spec = JobSpec.from_yaml("deploy/k8s/wide-deep-bench-dp8-job.yaml")
     job = to_indexed_job(spec)
     c = job["spec"]["template"]["spec"]["containers"][0]
     assert "--nproc-per-node=8" in c["command"] and c["resources"]["limits"]["amd.com/gpu"] == "8"
@@ -75,3 +75,15 @@ def test_notebook10_distributed_training_job_runs_three_workers(tmp_path):
     codes = launch_local(spec, num_gpus=0, timeout=500, cwd=root, log_dir=str(tmp_path))
     assert set(codes.values()) == {0}, codes
     assert (tmp_path / "w.safetensors").exists()
+
+
+def test_dp8_pipeline_job_runs_the_trainer_component():
+    """The 8-GPU deployment runs the pipeline whose Trainer component trains data-parallel (not bench.py)."""
+    import os
+
+    job = yaml.safe_load(open("deploy/k8s/wide-deep-dp8-job.yaml"))
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert c["resources"]["limits"]["amd.com/gpu"] == 8
+    cmd = c["command"]
+    assert cmd[1] == "examples/taxi/taxi_pipeline_local.py" and os.path.exists(cmd[1])
+    assert cmd[cmd.index("--num-gpus") + 1] == "8" and "bench.py" not in cmd

@@ -60,3 +60,32 @@ def test_dp_trainer_component_equals_single_process_global_batch(tmp_path):
     for k in one:  # same examples per step, gradients summed across ranks: fp32 summation order only
         np.testing.assert_allclose(dp[k].numpy(), one[k].numpy(), rtol=2e-4, atol=2e-5, err_msg=k)
     assert abs(tr2.custom_properties["eval_auc"] - tr1.custom_properties["eval_auc"]) < 1e-3
+
+
+@pytest.mark.gpu
+def test_dp_trainer_component_gpu_shared_rehearsal(tmp_path, monkeypatch):
+    """2 ranks sharing cuda:0 (the multi-GPU flow on a 1-GPU box): the fused W&D step with the xGMI exchange in
+    multi-step hipGraphs, launched by the component. The replicas must end bit-identical, and match one
+    process on the global batch to fp32 summation order."""
+    monkeypatch.setenv("MIFX_SHARED_GPU", "1")
+    monkeypatch.setenv("MIFX_DIST_BACKEND", "gloo")
+    import taxi_pipeline_local as tp
+
+    data = _csv(tmp_path)
+    one_tr, _ = _run(tmp_path, data, "single", 1, 40, "cuda", steps=300)
+    p = tp.create_pipeline("dp2", str(tmp_path / "dp2"), str(data), str(tmp_path / "serving_dp2"), train_steps=300,
+                           eval_steps=10, metadata_db_root=str(tmp_path / "md_dp2"), batch_size=20, num_gpus=2)
+    trainer = next(c for c in p.components if c.id == "Trainer")
+    trainer.exec_properties["custom_config"]["dump_replicas_dir"] = str(tmp_path / "replicas")
+    res = LocalDagRunner(device="cuda").run(p)
+    assert res.succeeded
+    r0 = torch.load(tmp_path / "replicas" / "replica0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "replicas" / "replica1.pt", weights_only=True)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    tr = res.components["Trainer"].outputs["output"][0]
+    # (weights: bf16 MFMA + another fp32 association of the gradient sum; FTRL's threshold makes single weights
+    # flip on last-bit differences, so the two runs are compared on their evaluation)
+    assert abs(tr.custom_properties["eval_auc"] - one_tr.custom_properties["eval_auc"]) < 5e-3
+    log = open(os.path.join(tr.uri, "dp_run", "rank0.log")).read()
+    assert "xGMI exchange unavailable" not in log
