@@ -26,6 +26,10 @@ roc_op = kfp_components.load("roc")
 deploy_op = kfp_components.load("deployer")
 
 
+# data-parallel dnntrainer ranks (one per GPU of the trainer pod); set by --num-gpus before compiling
+NUM_GPUS = 1
+
+
 @dsl.pipeline(name="TFX Taxi Cab Classification Pipeline Example",
               description="Example pipeline that does classification with model analysis.")
 def taxi_cab_classification(output="/mnt", project="taxi-cab-classification-pipeline",
@@ -46,7 +50,8 @@ def taxi_cab_classification(output="/mnt", project="taxi-cab-classification-pipe
                         preprocessing_module=preprocess_module, transformed_data_dir=output_template)
     training = train_op(transformed_data_dir=preprocess.output, schema=validation.outputs["schema"],
                         learning_rate=learning_rate, hidden_layer_size=hidden_layer_size, steps=steps, target="tips",
-                        preprocessing_module=preprocess_module, training_output_dir=output_template)
+                        preprocessing_module=preprocess_module, training_output_dir=output_template,
+                        num_gpus=NUM_GPUS)
     analysis = tfma_op(model=training.output, evaluation_data=evaluation, schema=validation.outputs["schema"],
                        project=project, mode=mode, slice_columns=analyze_slice_column,
                        analysis_results_dir=output_template)
@@ -57,7 +62,7 @@ def taxi_cab_classification(output="/mnt", project="taxi-cab-classification-pipe
     deploy = deploy_op(model_dir=str(training.output) + "/export/export", server_name=server_name,
                        cluster_name=project, pvc_name="users-pvc", service_type="NodePort",
                        output_dir=output_template)
-    training.apply(amd.use_amd_gpus(1))
+    training.apply(amd.use_amd_gpus(NUM_GPUS))
     for step in (validation, preprocess, training, analysis, prediction, cm, roc, deploy):
         step.apply(onprem.mount_pvc("users-pvc", "local-storage", output))
 
@@ -70,7 +75,10 @@ def main(argv=None):
     ap.add_argument("--work-dir", default="/tmp/mifx_kfp_taxi")
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--hidden", default="1500")
+    ap.add_argument("--num-gpus", type=int, default=1, help="data-parallel dnntrainer ranks (GPUs of its pod)")
     a = ap.parse_args(argv)
+    global NUM_GPUS
+    NUM_GPUS = a.num_gpus
     compiler.Compiler().compile(taxi_cab_classification, a.output)
     print(f"compiled -> {a.output}")
     if not a.run_local:

@@ -28,7 +28,7 @@ _TAXI = {
                     ("learning_rate", "Float", "0.1"), ("hidden_layer_size", "String", "1500"),
                     ("steps", "Integer", "3000"), ("target", "String", "tips"),
                     ("preprocessing_module", "String", ""), ("training_output_dir", "String", None),
-                    ("batch_size", "Integer", "32")],
+                    ("batch_size", "Integer", "32"), ("num_gpus", "Integer", "1")],
                    [("training_output_dir", "String")]),
     "tfma": ("Model analysis (TFMA-equivalent): overall + sliced accuracy/AUC/loss",
              [("model", "String", None), ("evaluation_data", "String", None), ("schema", "String", None),

@@ -171,14 +171,31 @@ def dnntrainer(a) -> None:
     from ..serving.saved_model import save_module
     from ..trainer.taxi_dnn_trainer import TaxiDNNTrainer
 
+    n_gpus = int(a.num_gpus or 1)
+    if n_gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # data parallel: this container step launches one rank per GPU of itself (rank 0 exports)
+        from ..trainer.distributed import run_ranks
+
+        run_ranks(["-m", "mifx.kfp_components.taxi"] + list(a._argv), n_gpus,
+                  os.path.join(a.training_output_dir, "dp_run"))
+        return
+    from ..parallel import dist as mdist
+
+    env = mdist.init("gloo" if a.device == "cpu" else None)
+    pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     hidden = [int(x) for x in str(a.hidden_layer_size).split(",") if x.strip()]
     cfg = TaxiDNNConfig(hidden=hidden[0], label=a.target)
     cols = dataset.table_to_numpy(dataset.read_split(os.path.join(a.transformed_data_dir, "train")))
     ids, dense, y = columns_to_tensors(cols, cfg)
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=0), batch=a.batch_size, lr=a.learning_rate, device=dev)
+    if dev == "cuda" and env.world_size > 1:
+        dev = f"cuda:{0 if os.environ.get('MIFX_SHARED_GPU') == '1' else env.local_rank}"
+    tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=0), batch=a.batch_size, lr=a.learning_rate, device=dev, process_group=pg)
     tr.set_data(ids, dense, y)
-    tr.run(a.steps)  # GPU: hipGraph replays of 50 steps (CPU: eager steps)
+    tr.run(a.steps)  # GPU: hipGraph replays of 50 steps (CPU: eager steps); DP: one all-gather per step
+    if env.rank != 0:
+        mdist.shutdown()
+        return
     ecols = dataset.table_to_numpy(dataset.read_split(os.path.join(a.transformed_data_dir, "eval")))
     eids, edense, ey = columns_to_tensors(ecols, cfg)
     logits = tr.predict_logits(eids, edense)
@@ -190,7 +207,8 @@ def dnntrainer(a) -> None:
         f.write(os.path.abspath(a.transformed_data_dir))
     _metrics(a.training_output_dir, [("accuracy", acc)])
     _write_output(a.training_output_dir_out, a.training_output_dir)
-    print(f"trained {a.steps} steps on {dev}: eval accuracy {acc:.4f}")
+    print(f"trained {a.steps} steps on {dev} x {env.world_size}: eval accuracy {acc:.4f}")
+    mdist.shutdown()
 
 
 def _load_model_and_transform(model_dir: str):
@@ -430,7 +448,8 @@ def build_parser() -> argparse.ArgumentParser:
                                    ("hidden_layer_size", {"default": "1500"}),
                                    ("steps", {"type": int, "default": 3000}), ("target", {"default": "tips"}),
                                    "preprocessing_module", "training_output_dir",
-                                   ("batch_size", {"type": int, "default": 32}), "device", "training_output_dir_out"])
+                                   ("batch_size", {"type": int, "default": 32}), "device", "training_output_dir_out",
+                                   ("num_gpus", {"type": int, "default": 1})])
     add("tfma", tfma, ["model", "evaluation_data", "schema", "project", ("mode", {"default": "local"}),
                        ("slice_columns", {"default": ""}), "analysis_results_dir", "analysis_results_dir_out"])
     add("predict", predict, ["data_file_pattern", "schema", ("target_column", {"default": "tips"}), "model",
@@ -449,7 +468,9 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv=None) -> None:
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = build_parser().parse_args(argv)
+    a._argv = argv
     a.fn(a)
 
 

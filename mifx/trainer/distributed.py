@@ -41,6 +41,15 @@ def launch(spec: dict, num_procs: int, work_dir: str, timeout: float | None = No
     path = os.path.join(work_dir, "dp_spec.json")
     with open(path, "w") as f:
         json.dump(spec, f, default=str)
+    run_ranks(["-m", "mifx.trainer.distributed", path], num_procs, work_dir, timeout)
+    with open(os.path.join(work_dir, RESULT)) as f:
+        return json.load(f)
+
+
+def run_ranks(args: list, num_procs: int, work_dir: str, timeout: float | None = None) -> None:
+    """Start `python <args>` once per rank (torchrun-style env, logs in work_dir/rank<r>.log) and wait; a failing
+    rank kills the others and raises with every rank's log tail."""
+    os.makedirs(work_dir, exist_ok=True)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     port = _free_port()
     procs = []
@@ -51,8 +60,8 @@ def launch(spec: dict, num_procs: int, work_dir: str, timeout: float | None = No
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0",
                     "PYTHONPATH": os.pathsep.join([root, env.get("PYTHONPATH", "")]).rstrip(os.pathsep)})
         log = open(os.path.join(work_dir, f"rank{r}.log"), "w")
-        procs.append((subprocess.Popen([sys.executable, "-m", "mifx.trainer.distributed", path], env=env,
-                                       stdout=log, stderr=subprocess.STDOUT), log))
+        procs.append((subprocess.Popen([sys.executable] + list(args), env=env, stdout=log,
+                                       stderr=subprocess.STDOUT), log))
     deadline = time.time() + timeout if timeout else None
     codes = [None] * num_procs
     try:
@@ -78,8 +87,6 @@ def launch(spec: dict, num_procs: int, work_dir: str, timeout: float | None = No
             with open(os.path.join(work_dir, f"rank{r}.log")) as f:
                 tails.append(f"--- rank {r} (exit {codes[r]}) ---\n" + "".join(f.readlines()[-25:]))
         raise RuntimeError("data-parallel Trainer failed:\n" + "\n".join(tails))
-    with open(os.path.join(work_dir, RESULT)) as f:
-        return json.load(f)
 
 
 def run_trainer_fn(module_file: str, hp_values: dict, schema_uri: str, out_dir: str) -> dict:

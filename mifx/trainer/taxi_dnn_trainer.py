@@ -17,17 +17,34 @@ class TaxiDNNTrainer:
     HBM-resident records through a device step counter (advanced by the optimizer kernel), and the sparse Adagrad
     deduplicates rows in-kernel (no sort/unique, whose dynamic output size synchronised the host every step). So
     the step is captured once into hipGraphs -- one step and `steps_per_graph` consecutive steps -- and replayed
-    (`graph=False`: eager launches of the same kernels)."""
+    (`graph=False`: eager launches of the same kernels).
+
+    Data parallel (`process_group`, one rank per GPU): the 6170 x 1500 first layer makes the DENSE gradient 37 MB
+    (the bandwidth-relevant case), but a step touches only batch x 13 of its 6,167 sparse rows. So
+    the ranks exchange the step's per-example backward state instead -- activations, hidden-layer gradient dz,
+    dense inputs, dlogit and the W1 row ids: B x (2H + D + 1 + F) floats, ~0.4 MB per rank at B=32 -- with ONE
+    all-gather, and every rank runs the sparse + dense Adagrad kernels over the gathered global batch (rank-major =
+    the global batch's example order). That is bit-identical to one process at batch world x B (same kernels, same
+    summation order) for ~1/100 of the bytes a dense all-reduce would move over xGMI. The CPU path all-reduces
+    dense gradients (mifx.parallel.ddp; TF-Adagrad leaves untouched rows unchanged under a zero gradient)."""
 
     def __init__(self, model: TaxiDNN | None = None, batch: int = 32, lr: float = 0.1, device="cpu",
                  initial_accumulator_value: float = 0.1, loss_reduction: str = "sum", native: bool | None = None,
-                 graph: bool = True, steps_per_graph: int = 50):
+                 graph: bool = True, steps_per_graph: int = 50, process_group=None):
         self.device = torch.device(device)
         self.model = (model or TaxiDNN()).to(self.device)
         self.batch, self.lr, self.loss_reduction = batch, lr, loss_reduction
         self.native = (self.device.type == "cuda") if native is None else native
         self.dense_row0 = self.model.cfg.sparse_rows
-        self.use_graph = bool(graph and self.native)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.rank = torch.distributed.get_rank(process_group) if process_group is not None else 0
+        if self.world > 1:
+            for p in self.model.parameters():  # identical initial replicas
+                torch.distributed.broadcast(p.data, src=torch.distributed.get_global_rank(process_group, 0)
+                                            if process_group is not torch.distributed.group.WORLD else 0,
+                                            group=process_group)
+        self.use_graph = bool(graph and self.native and self.world == 1)
         self.steps_per_graph = max(1, int(steps_per_graph))
         self.graph, self.graph_multi = None, None
         if self.native:
@@ -41,12 +58,84 @@ class TaxiDNNTrainer:
             self.params = {n: t.data for n, t in p.items()}
             self.accs = {n: torch.full_like(t, initial_accumulator_value) for n, t in self.params.items()}
             self.bufs = embag_mlp.make_buffers(batch, self.model.cfg.hidden, len(self.model.cfg.dense), self.device)
+            if self.world > 1:
+                self._init_exchange()
         else:
             self.opt = TFAdagrad(self.model.parameters(), lr=lr, initial_accumulator_value=initial_accumulator_value)
+            if self.world > 1:
+                from ..parallel.ddp import DataParallel
+
+                self.dp = DataParallel(self.model, process_group, average=(loss_reduction == "mean"),
+                                       broadcast_init=False)
         self.step_idx = 0
         self._last = float("nan")
 
+    # ---------------------------------------------------------------- data parallel (sparse exchange)
+    def _init_exchange(self) -> None:
+        from ..ops import embag_mlp
+
+        B, W = self.batch, self.world
+        H, D, F = self.model.cfg.hidden, len(self.model.cfg.dense), len(self.model.cfg.sparse)
+        Bg = B * W
+        if Bg > embag_mlp.limits()["max_batch"]:
+            raise ValueError(f"global batch {Bg} > {embag_mlp.limits()['max_batch']}")
+        self.H, self.D, self.F, self.Bg = H, D, F, Bg
+        self.gbufs = embag_mlp.make_buffers(Bg, H, D, self.device)
+        self.g_rows = torch.empty(Bg, F, dtype=torch.int32, device=self.device)
+        self.g_xd = torch.empty(Bg, D, device=self.device)
+        self.C = 2 * H + D + 1 + F
+        # global batches of <= 64 take the kernels' per-example dense chunks (written by the forward/backward
+        # launch): those travel too, so the update stays the single-process one
+        self.direct = Bg <= 64
+        self.L = B * self.C + (B * (D + 2) * H if self.direct else 0)
+        self.send = torch.empty(self.L, device=self.device)
+        self.recv = torch.empty(W * self.L, device=self.device)
+        self._ar = torch.arange(B, device=self.device)
+
+    def _all_gather(self) -> None:
+        dist = torch.distributed
+        if dist.get_backend(self.pg) == "nccl":
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.pg)
+        else:  # gloo (CPU collectives; ranks sharing one GPU in rehearsals)
+            parts = [torch.empty(self.L) for _ in range(self.world)]
+            dist.all_gather(parts, self.send.cpu(), group=self.pg)
+            self.recv.copy_(torch.cat(parts))
+
+    def _native_step_dp(self) -> None:
+        B, H, D, W = self.batch, self.H, self.D, self.world
+        scale = 1.0 if self.loss_reduction == "sum" else 1.0 / (B * W)
+        p = self.params
+        self._k.fwd_bwd(p["W1"], p["b1"], p["w2"], p["b2"], self.rows, self.dense, self.label, self.dense_row0, scale,
+                        True, self.bufs, batch=B, step_ctr=self.step_ctr)
+        idx = (self.step_ctr * B + self._ar) % self.n
+        seg = self.send[:B * self.C].view(B, self.C)
+        seg[:, :H] = self.bufs["a"]
+        seg[:, H:2 * H] = self.bufs["dz"]
+        seg[:, 2 * H:2 * H + D] = self.dense[idx]
+        seg[:, 2 * H + D] = self.bufs["dlogit"]
+        seg[:, 2 * H + D + 1:] = self.rows[idx].view(torch.float32)  # the ids' bits travel unchanged
+        if self.direct:
+            self.send[B * self.C:] = self.bufs["dpart"][:B * (D + 2) * H]
+        self._all_gather()
+        rv = self.recv.view(W, self.L)
+        g = rv[:, :B * self.C].reshape(W * B, self.C)
+        self.gbufs["a"].copy_(g[:, :H])
+        self.gbufs["dz"].copy_(g[:, H:2 * H])
+        self.g_xd.copy_(g[:, 2 * H:2 * H + D])
+        self.gbufs["dlogit"].copy_(g[:, 2 * H + D])
+        self.g_rows.copy_(g[:, 2 * H + D + 1:].contiguous().view(torch.int32))
+        if self.direct:
+            self.gbufs["dpart"][:W * B * (D + 2) * H].view(W, -1).copy_(rv[:, B * self.C:])
+        self._k.adagrad(p, self.accs, self.g_rows, self.g_xd, self.dense_row0, self.gbufs, self.lr, batch=W * B)
+        self.step_ctr.add_(1)
+
     def set_data(self, ids: torch.Tensor, dense: torch.Tensor, label: torch.Tensor) -> None:
+        """The training records (all of them: with a process group each rank keeps its shard of every global
+        batch, `mifx.trainer.estimator.shard_records`)."""
+        if self.world > 1:
+            from .estimator import shard_records
+
+            ids, dense, label = (shard_records(t, self.rank, self.world, self.batch) for t in (ids, dense, label))
         self.rows = self.model.rows(ids.to(self.device)).to(torch.int32).contiguous()
         self.dense = dense.to(self.device).float().contiguous()
         self.label = label.to(self.device).float().contiguous()
@@ -63,6 +152,9 @@ class TaxiDNNTrainer:
         return (torch.arange(self.batch, device=self.device) + s) % self.n
 
     def _native_step(self) -> None:
+        if self.world > 1:
+            self._native_step_dp()
+            return
         scale = 1.0 if self.loss_reduction == "sum" else 1.0 / self.batch
         p = self.params
         self._k.fwd_bwd(p["W1"], p["b1"], p["w2"], p["b2"], self.rows, self.dense, self.label, self.dense_row0, scale,
@@ -115,6 +207,8 @@ class TaxiDNNTrainer:
             loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, y, reduction=self.loss_reduction)
             self.opt.zero_grad(set_to_none=True)
             loss.backward()
+            if self.world > 1:
+                self.dp.finish()
             self.opt.step()
             self._last = float(loss.detach()) * (self.batch if self.loss_reduction == "mean" else 1.0)
         self.step_idx += 1

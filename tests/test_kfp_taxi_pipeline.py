@@ -49,10 +49,11 @@ def test_taxi_pipeline_compiles_with_amd_gpu_and_pvc(tmp_path):
     assert any(v["name"] == "local-storage" for v in wf["spec"]["volumes"])
 
 
-def _run(tmp_path, data_dir, steps, hidden):
+def _run(tmp_path, data_dir, steps, hidden, num_gpus=1):
     mod = _load_example()
     return mod.main(["--output", str(tmp_path / "p.yaml"), "--run-local", "--data-dir", data_dir,
-                     "--work-dir", str(tmp_path / "work"), "--steps", str(steps), "--hidden", hidden])
+                     "--work-dir", str(tmp_path / "work"), "--steps", str(steps), "--hidden", hidden,
+                     "--num-gpus", str(num_gpus)])
 
 
 def _outputs(st, template):
@@ -73,6 +74,25 @@ def test_taxi_pipeline_runs_locally_on_synthetic_csv(tmp_path):
     manifest = _outputs(st, "deployer")[0]["value"]
     docs = list(yaml.safe_load_all(open(manifest)))
     assert docs[0]["kind"] == "Deployment" and docs[1]["spec"]["type"] == "NodePort"
+
+
+def test_taxi_pipeline_dnntrainer_data_parallel_two_ranks(tmp_path, monkeypatch):
+    """--num-gpus 2: the dnntrainer step launches two ranks of itself (gloo on this CPU host; on GPUs: one
+    per device, sparse backward-state all-gather) and the rest of the pipeline consumes rank 0's export."""
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")
+    data = tmp_path / "data"
+    data.mkdir()
+    _write_csv(data / "train.csv", synthetic_taxi_csv_rows(1200, seed=1))
+    _write_csv(data / "eval.csv", synthetic_taxi_csv_rows(400, seed=2))
+    (data / "column-names.json").write_text(json.dumps(TAXI_COLUMNS))
+    st = _run(tmp_path, str(data), 30, "64", num_gpus=2)
+    assert st["phase"] == "Succeeded", st["message"]
+    wf = yaml.safe_load(open(tmp_path / "p.yaml"))
+    t = {x["name"]: x for x in wf["spec"]["templates"]}
+    assert t["dnntrainer"]["container"]["resources"]["limits"]["amd.com/gpu"] == "2"
+    logs = [p for p in (tmp_path / "work").rglob("rank1.log")]
+    assert logs, "no rank logs"
+    assert 0.5 < float(_outputs(st, "roc")[0]["value"]) <= 1.0
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(REF_TAXI, "train.csv")), reason="reference data not present")

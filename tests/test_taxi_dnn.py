@@ -104,3 +104,62 @@ def test_set_data_twice_recaptures_graphs():
     for n in ("W1", "b1", "w2", "b2"):
         torch.testing.assert_close(getattr(gpu.model, n).detach().cpu(), getattr(cpu.model, n).detach(),
                                    rtol=2e-4, atol=2e-5)
+
+
+def _dp_worker(rank, world, port, out, device, batch, steps, hidden):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = TaxiDNNConfig(hidden=hidden)
+        ids, dense, y = _data(batch * world * steps + 7, cfg, seed=21)
+        tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=rank + 1), batch=batch, lr=0.1, device=device,  # rank 0's init wins
+                            process_group=dist.group.WORLD)
+        tr.set_data(ids, dense, y)
+        tr.run(steps)
+        torch.save({n: getattr(tr.model, n).detach().cpu() for n in ("W1", "b1", "w2", "b2")}, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def _dp_case(tmp_path, device, batch, steps, hidden):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "dp")
+    mp.start_processes(_dp_worker, args=(2, port, out, device, batch, steps, hidden), nprocs=2, start_method="spawn")
+    r0, r1 = (torch.load(f"{out}.{r}", weights_only=True) for r in (0, 1))
+    cfg = TaxiDNNConfig(hidden=hidden)
+    ids, dense, y = _data(batch * 2 * steps + 7, cfg, seed=21)
+    n = batch * 2 * steps  # the DP shards drop the last partial global batch
+    one = TaxiDNNTrainer(TaxiDNN(cfg, seed=1), batch=2 * batch, lr=0.1, device=device)
+    one.set_data(ids[:n], dense[:n], y[:n])
+    one.run(steps)
+    ref = {k: getattr(one.model, k).detach().cpu() for k in ("W1", "b1", "w2", "b2")}
+    return r0, r1, ref
+
+
+def test_dp_cpu_two_ranks_equal_one_process_global_batch(tmp_path):
+    r0, r1, ref = _dp_case(tmp_path, "cpu", 16, 6, 64)
+    for k in ref:
+        assert torch.equal(r0[k], r1[k]), k
+        torch.testing.assert_close(r0[k], ref[k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [32, 48])
+def test_dp_gpu_sparse_exchange_bit_identical_to_global_batch(tmp_path, batch):
+    """Two ranks sharing cuda:0 exchange per-example backward state (one all-gather) and run the sparse + dense
+    Adagrad kernels over the global batch: bit-identical to one process at batch 2B (2B = 64: per-example dense
+    chunks travel too; 96: the chunked reduction path)."""
+    r0, r1, ref = _dp_case(tmp_path, "cuda", batch, 5, 1500)
+    for k in ref:
+        assert torch.equal(r0[k], r1[k]), k
+        assert torch.equal(r0[k], ref[k]), k
