@@ -49,11 +49,36 @@ def _file_flags(src: Path) -> list[str]:
     return []
 
 
+def source_hash(src: Path) -> str:
+    """sha256 (16 hex) of what a library is built from: its source, every csrc header, the compiler flags."""
+    import hashlib
+
+    h = hashlib.sha256()
+    flags = (HIP_FLAGS + _file_flags(src)) if src.suffix == ".hip" else CXX_FLAGS
+    h.update(" ".join(flags).encode())
+    for d in [src] + sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("include/*.h")):
+        if d.exists() and d.name != HASH_HEADER.name:
+            h.update(d.name.encode())
+            h.update(d.read_bytes())
+    return h.hexdigest()[:16]
+
+
+# force-included into every translation unit: the library reports the source hash it was built from, and
+# mifx.ops._lib.load refuses a library whose hash does not match the sources next to it (no stale binaries)
+HASH_HEADER = CSRC / "mifx_srchash.h"
+
+
 def _needs_build(src: Path, out: Path) -> bool:
     if not out.exists():
         return True
-    deps = [src] + sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("include/*.h"))
-    return any(d.stat().st_mtime > out.stat().st_mtime for d in deps if d.exists())
+    return embedded_hash(out) != source_hash(src)
+
+
+def embedded_hash(lib: Path) -> str | None:
+    """The hash string compiled into a library (read from the file, without loading it)."""
+    data = lib.read_bytes()
+    i = data.find(b"MIFX_SRC_HASH=")
+    return data[i + 14:i + 30].decode(errors="replace") if i >= 0 else None
 
 
 def _build_one(src: Path, force: bool) -> tuple[str, str]:
@@ -61,10 +86,11 @@ def _build_one(src: Path, force: bool) -> tuple[str, str]:
     if not force and not _needs_build(src, out):
         return src.name, "up-to-date"
     tmp = out.with_suffix(".so.tmp")
+    hd = ["-include", str(HASH_HEADER), f"-DMIFX_SRC_HASH_VALUE=\"{source_hash(src)}\""]
     if src.suffix == ".hip":
-        cmd = [hipcc()] + HIP_FLAGS + _file_flags(src) + ["-I", str(CSRC), str(src), "-o", str(tmp)]
+        cmd = [hipcc()] + HIP_FLAGS + _file_flags(src) + hd + ["-I", str(CSRC), str(src), "-o", str(tmp)]
     else:
-        cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + ["-I", str(CSRC), str(src), "-o", str(tmp)]
+        cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + hd + ["-I", str(CSRC), str(src), "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"build of {src.name} failed:\n{' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
