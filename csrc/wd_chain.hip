@@ -42,6 +42,8 @@ typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
+#include "wd_opt.h"
+
 constexpr int T = 128;  // examples per workgroup iteration
 constexpr int MAXW = 8;  // waves per workgroup: T / (16 TBN), TBN = 16-example column blocks per wave (1 or 2)
 // Row padding (elements): WPAD for the weight images, PAD for the staging images; with the row permutations below
@@ -338,14 +340,76 @@ __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], c
   }
 }
 
-template <bool TRAIN, int TBN>
+// ---- in-kernel step tail (TAIL = true): slab reduction + optimizer inside the training kernel itself.
+// With one workgroup per CU and grid <= #CUs every workgroup of the launch is resident, so the launch can
+// synchronise grid-wide. After its last iteration every workgroup has written its slab row (into the L2 of the
+// XCD it runs on); then
+//   barrier 1 -> level 1: the workgroups of each XCD split the columns and sum the rows written on THAT XCD
+//                (ascending row order, L2 hits), storing the per-XCD partials write-through (system scope);
+//   barrier 2 -> level 2: workgroup b sums the per-XCD partials of its ~stride/G columns (XCDs in the order of
+//                their first row: the same association for any rotation of the round-robin dispatch, so the
+//                step is run-to-run deterministic) and applies the optimizer (wd_opt.h sc_update) in place.
+// This replaces the two tail kernels (csrc/wide_deep.hip wd_reduce_xcd + wd_xcd_opt_sc, 11.8 us per step at
+// B=65536, profiles/bench_r2_final_kernels.md) and their launch ramps; the slab never has to leave its XCD.
+// Barrier: a monotonic 64-bit arrival counter (no reset, no generation flag): the workgroup whose arrival
+// returned `old` waits until the counter reaches (old / G + 1) G. The wait is bounded by wall-clock time: on a
+// timeout (a workgroup never arrived: not co-resident) it sets the sticky `err` flag, and the tail then skips
+// the update and the step-counter advance (the host raises at its next check).
+struct TailArgs {
+  float* xpart;                  // [XMAX][stride] per-XCD partial column sums
+  unsigned long long* bar;       // arrival counter (monotonic)
+  int* err;                      // sticky failure flag
+  const int* wsc;                // slab column -> -1 padding / -2 wide / >= 0 bf16 image offset
+  float* param;
+  float* s0;
+  float* s1;
+  uint16_t* wt_out;              // the bf16 weight image (the kernel's own staging source)
+  long long* step_slots;         // STEP_SLOTS per-workgroup optimizer step slots (slot 0 = the data offset step)
+  OptHyper hd, hw;
+};
+constexpr int XMAXT = 16;  // XCC_ID range
+constexpr long long TAIL_TIMEOUT_TICKS = 200ll * 1000 * 1000;  // 2 s at the 100 MHz real-time clock
+
+__device__ __forceinline__ void st_sys4(float* p, float4 v) {
+  __hip_atomic_store((unsigned int*)p + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store((unsigned int*)p + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store((unsigned int*)p + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store((unsigned int*)p + 3, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys1(const float* p) {
+  return __uint_as_float(__hip_atomic_load((const unsigned int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+// every thread's outstanding stores acknowledged, then one arrival per workgroup; false on timeout / earlier error
+__device__ __forceinline__ bool grid_sync(unsigned long long* bar, int* err, int G, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    const unsigned long long old = __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = (old / (unsigned long long)G + 1ull) * (unsigned long long)G;
+    const long long t0 = wall_clock64();
+    while (ok && __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > TAIL_TIMEOUT_TICKS) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+      }
+    }
+    *s_flag = ok;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+template <bool TRAIN, int TBN, bool TAIL>
 __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint4* __restrict__ data, long long n_data, long long batch,
                                                      long long start_fixed, const long long* __restrict__ step_ctr,
                                                      const uint4* __restrict__ wimg, const float* __restrict__ wide,
                                                      float* __restrict__ slab, float* __restrict__ slab_loss,
                                                      float* __restrict__ logits_out, float grad_scale,
                                                      const int* __restrict__ tmap, int stride,
-                                                     int* __restrict__ xcd_of) {
+                                                     int* __restrict__ xcd_of, TailArgs ta) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LSEND);
   float* red = wgrad + WIDE_PAD;
@@ -358,7 +422,12 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   BSTAMP(0);
   // the XCD this workgroup's slab row is written from (its L2 holds the row for the XCD-local reduction,
   // csrc/wide_deep.hip wd_reduce_xcd)
-  if (TRAIN && xcd_of != nullptr && tid == 0) xcd_of[blockIdx.x] = mifx_xcc_id();
+  if (TRAIN && xcd_of != nullptr && tid == 0) {
+    if (TAIL)  // read by workgroups on every XCD after the first barrier: write-through
+      __hip_atomic_store(xcd_of + blockIdx.x, mifx_xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      xcd_of[blockIdx.x] = mifx_xcc_id();
+  }
 
   {  // stage the bf16 weight image (already in LDS layout) with direct-to-LDS loads: no VGPR round trip, no
      // ds_write transfer cycles. Wave w's lanes fill 16-byte chunks i * NTHR + 64 w + lane; the last wave's
@@ -667,21 +736,119 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   }
   STAMP(17);
   BSTAMP(2);
+  if constexpr (TRAIN && TAIL) {
+    const int G = gridDim.x, b = blockIdx.x, S4 = stride / 4;
+    int* tl = (int*)(lds + LS);  // the staging area is free now
+    int* rows = tl;              // [256] rows written on this XCD, ascending
+    int* first = tl + 256;       // [XMAXT] first row per XCD
+    int* order = tl + 256 + XMAXT;
+    int* misc = tl + 256 + 2 * XMAXT;  // [0] barrier flag, [1] nrows, [2] my index, [3] nord, [4..7] wave counts
+    float4* rsum = (float4*)(tl + 512);  // [4][128] level-1 row-group partials
+    // optimizer state of this workgroup's level-2 columns: in flight across both barriers
+    const int per = (stride + G - 1) / G;
+    const int gi = b * per + tid;
+    ScState st{-1, 0.f, 0.f, 0.f};
+    if (tid < per) st = sc_load(gi, stride, ta.wsc, ta.param, ta.s0, ta.s1);
+    const long long step = ta.step_slots[b] + 1;
+    if (!grid_sync(ta.bar, ta.err, G, misc)) return;
+    // ---- level 1
+    const int x = mifx_xcc_id();
+    if (tid < XMAXT) first[tid] = 1 << 30;
+    const int xo = tid < G ? __hip_atomic_load(xcd_of + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : -1;
+    const bool sel = tid < G && xo == x;
+    const unsigned long long m = __ballot(sel);
+    if (lane == 0 && w < 4) misc[4 + w] = __popcll(m);
+    __syncthreads();
+    if (tid < G) atomicMin(&first[xo & (XMAXT - 1)], tid);
+    int base = 0;
+    for (int i = 0; i < w && i < 4; ++i) base += misc[4 + i];
+    if (sel) {
+      const int pos = base + __popcll(m & ((1ull << lane) - 1));
+      rows[pos] = tid;
+      if (tid == b) misc[2] = pos;
+    }
+    if (tid == 0) misc[1] = misc[4] + misc[5] + misc[6] + misc[7];
+    __syncthreads();
+    if (tid == 0) {  // XCDs holding rows, ordered by their first row
+      int k2 = 0;
+      for (int xx = 0; xx < XMAXT; ++xx) {
+        if (first[xx] >= (1 << 30)) continue;
+        int j = k2++;
+        while (j > 0 && first[order[j - 1]] > first[xx]) {
+          order[j] = order[j - 1];
+          --j;
+        }
+        order[j] = xx;
+      }
+      misc[3] = k2;
+    }
+    const int nr = misc[1], me = misc[2];
+    const int q0 = (int)((long long)me * S4 / nr), q1 = (int)((long long)(me + 1) * S4 / nr);
+    const float4* slab4 = (const float4*)slab;
+    for (int qb = q0; qb < q1; qb += 128) {
+      const int lq = tid & 127, rg = tid >> 7;  // 4 row groups (NTHR = 512)
+      const int q = qb + lq;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < q1) {
+        constexpr int U = 8;
+        for (int i0 = rg; i0 < nr; i0 += 4 * U) {
+          float4 v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int i = i0 + 4 * u;
+            v[u] = i < nr ? slab4[(size_t)rows[i] * S4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+          }
+        }
+      }
+      rsum[rg * 128 + lq] = a;
+      __syncthreads();
+      if (rg == 0 && q < q1) {
+        float4 sm = rsum[lq];
+#pragma unroll
+        for (int k2 = 1; k2 < 4; ++k2) {
+          const float4 v = rsum[k2 * 128 + lq];
+          sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
+        }
+        st_sys4(ta.xpart + (size_t)x * stride + 4 * q, sm);
+      }
+      __syncthreads();
+    }
+    if (!grid_sync(ta.bar, ta.err, G, misc)) return;
+    // ---- level 2 + optimizer
+    if (tid < per && gi < stride) {
+      const int nord = misc[3];
+      float pv[XMAXT];
+#pragma unroll
+      for (int k2 = 0; k2 < XMAXT; ++k2) pv[k2] = k2 < nord ? ld_sys1(ta.xpart + (size_t)order[k2] * stride + gi) : 0.f;
+      float g = pv[0];
+#pragma unroll
+      for (int k2 = 1; k2 < XMAXT; ++k2)
+        if (k2 < nord) g += pv[k2];
+      sc_update(gi, st, g, ta.hd, ta.hw, step, ta.param, ta.s0, ta.s1, ta.wt_out);
+    }
+    if (tid == 0) ta.step_slots[b] = step;
+    if (b == 0)
+      for (int i = G + tid; i < STEP_SLOTS; i += NTHR) ta.step_slots[i] = step;
+  }
 }
 
-template <bool TRAIN, int TBN>
+template <bool TRAIN, int TBN, bool TAIL = false>
 void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
             const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
-            float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of) {
+            float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of, TailArgs ta = TailArgs{}) {
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wdc_fused<TRAIN, TBN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)wdc_fused<TRAIN, TBN, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     attr_done = true;
   }
-  hipLaunchKernelGGL((wdc_fused<TRAIN, TBN>), grid, dim3(64 * (T / (16 * TBN))), LDS_BYTES, stream, (const uint4*)data,
-                     n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab, slab_loss, logits_out,
-                     grad_scale, tmap, stride, xcd_of);
+  hipLaunchKernelGGL((wdc_fused<TRAIN, TBN, TAIL>), grid, dim3(64 * (T / (16 * TBN))), LDS_BYTES, stream,
+                     (const uint4*)data, n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab,
+                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta);
 }
 
 }  // namespace
@@ -729,6 +896,46 @@ int mifx_wdc_fused(const void* data, long long n_data, long long batch, long lon
                    int waves, hipStream_t stream) {
   return mifx_wdc_fused_x(data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                           grad_scale, grid, train, tmap, stride, waves, nullptr, stream);
+}
+
+// Training step with the in-kernel tail (slab reduction + optimizer inside the launch; see TailArgs): 8-wave
+// shape, grid <= the number of CUs (every workgroup must be resident), the whole step in ONE launch.
+// xpart: [16][stride] fp32 scratch; bar: one uint64 arrival counter (zero at creation, never reset while the
+// trainer lives); err: sticky int flag; wsc / param / s0 / s1 / wt (the kernel's own weight image) / step_ctr
+// (STEP_SLOTS slots): the slab-column-order optimizer state of csrc/wide_deep.hip wd_reduce_opt_sc.
+int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, long long* step_ctr, void* wimg,
+                        float* wide, float* slab, float* slab_loss, float grad_scale, int grid, const int* tmap,
+                        int stride, int* xcd_of, float* xpart, unsigned long long* bar, int* err, const int* wsc,
+                        float* param, float* s0, float* s1, const float* hyper_dnn, const float* hyper_wide,
+                        hipStream_t stream) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess)
+    return -1;
+  if (grid <= 0 || grid > ncu || grid > 256 || grid > STEP_SLOTS || n_data <= 0 || batch <= 0 || batch > n_data)
+    return -1;
+  if (wimg == nullptr || wide == nullptr || slab == nullptr || tmap == nullptr || xcd_of == nullptr ||
+      xpart == nullptr || bar == nullptr || err == nullptr || wsc == nullptr || param == nullptr || s0 == nullptr ||
+      s1 == nullptr || step_ctr == nullptr)
+    return -1;
+  if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0 || stride < WIDE_PAD || stride % 4 != 0) return -1;
+  TailArgs ta;
+  ta.xpart = xpart;
+  ta.bar = bar;
+  ta.err = err;
+  ta.wsc = wsc;
+  ta.param = param;
+  ta.s0 = s0;
+  ta.s1 = s1;
+  ta.wt_out = (uint16_t*)wimg;
+  ta.step_slots = step_ctr;
+  ta.hd = OptHyper{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                   hyper_dnn[6], hyper_dnn[7]};
+  ta.hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                   hyper_wide[6], hyper_wide[7]};
+  launch<true, 1, true>(dim3(grid), stream, data, n_data, batch, 0, step_ctr, wimg, wide, slab, slab_loss, nullptr,
+                        grad_scale, tmap, stride, xcd_of, ta);
+  return (int)hipGetLastError();
 }
 
 #ifdef WDC_STAMPS

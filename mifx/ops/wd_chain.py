@@ -19,6 +19,8 @@ def _fns():
                                              VP]),
         "fused_x": sig(lib, "mifx_wdc_fused_x", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
                                                  I32, VP, VP]),
+        "fused_tail": sig(lib, "mifx_wdc_fused_tail", [VP, I64, I64, VP, VP, VP, VP, VP, F32, I32, VP, I32, VP, VP, VP,
+                                                       VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -61,3 +63,36 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
                            ptr(slab), ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
                            ptr(tmap), stride, int(waves), ptr(xcd_of), stream_handle(records.device))
     check(rc, "mifx_wdc_fused")
+
+
+class InKernelTail:
+    """Scratch of the one-launch training step (csrc/wd_chain.hip TailArgs): the slab reduction and the optimizer
+    run inside the fused kernel after two grid-wide barriers. xcd_of [256], per-XCD partials [16, stride], the
+    monotonic barrier counter and the sticky error flag (set when a barrier wait timed out: the step then skipped
+    its update; `check()` raises)."""
+
+    def __init__(self, stride: int, device):
+        self.stride = int(stride)
+        self.xcd_of = torch.zeros(256, dtype=torch.int32, device=device)
+        self.xpart = torch.zeros(16 * self.stride, device=device)
+        self.bar = torch.zeros(1, dtype=torch.int64, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def step(self, tr) -> None:
+        """One training step of FusedWideDeepTrainer `tr` (chained kernel, slab-column-order state)."""
+        c = constants()
+        if tr.wt.numel() != c["LWEND"] or tr.tmap.numel() != c["NTILE"] or tr.slab.shape[0] < tr.grid:
+            raise ValueError("trainer buffers do not match the chained kernel")
+        if tr.grid > 256 or tr.stride != self.stride:
+            raise ValueError("in-kernel tail: grid <= 256 and the trainer's slab stride")
+        rc = _fns()["fused_tail"](ptr(tr.records), tr.n_data, tr.batch, ptr(tr.step_ctr), ptr(tr.wt),
+                                  ptr(tr.wide_weights), ptr(tr.slab), ptr(tr.slab_loss), float(tr.grad_scale),
+                                  int(tr.grid), ptr(tr.tmap), int(tr.stride), ptr(self.xcd_of), ptr(self.xpart),
+                                  ptr(self.bar), ptr(self.err), ptr(tr.wsc), ptr(tr.param_sc), ptr(tr.s0_sc),
+                                  ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide), stream_handle(tr.records.device))
+        check(rc, "mifx_wdc_fused_tail")
+
+    def check(self) -> None:
+        if int(self.err.item()) != 0:
+            raise RuntimeError("W&D in-kernel tail: a grid barrier timed out (workgroups not co-resident); the "
+                               "step skipped its update")

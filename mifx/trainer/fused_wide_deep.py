@@ -60,7 +60,8 @@ class FusedWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cuda",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
-                 live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8):
+                 live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8,
+                 in_kernel_tail: bool | None = None):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
@@ -142,6 +143,17 @@ class FusedWideDeepTrainer:
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
         self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
+        # one rank, large batch: the whole step in ONE launch -- slab reduction + optimizer inside the fused kernel
+        # after grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident: grid <= #CUs, one
+        # workgroup per CU by its LDS). in_kernel_tail=False (or MIFX_WD_TAIL=0) keeps the three-launch step.
+        if in_kernel_tail is None:
+            in_kernel_tail = os.environ.get("MIFX_WD_TAIL", "1") != "0"
+        self._ktail = None
+        if in_kernel_tail and self._sc and self.world == 1 and 64 <= self.grid <= 256 and self.waves == 8 \
+                and self.device.type == "cuda" and self.grid <= torch.cuda.get_device_properties(dev).multi_processor_count:
+            from ..ops import wd_chain as wdc
+
+            self._ktail = wdc.InKernelTail(self.stride, dev)
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
         self.partial = torch.empty(self.nsplit, self.stride, device=dev)
@@ -327,6 +339,9 @@ class FusedWideDeepTrainer:
             raise RuntimeError("W&D optimizer launch failed")
 
     def _step_impl(self) -> None:
+        if self._ktail is not None:  # one launch: fwd/bwd + slab reduction + optimizer
+            self._ktail.step(self)
+            return
         if self._xg is not None:  # data parallel over xGMI: no host collective, graph-capturable
             self._launch(self.records, self.n_data, self.batch, 0, self.step_ctr, self.slab, self.slab_loss, None,
                          self.grid, True)
@@ -372,6 +387,8 @@ class FusedWideDeepTrainer:
         csrc/wide_deep.hip xg_wait). Called at every host synchronisation point."""
         if self._xg is not None:
             self._xg.check()
+        if self._ktail is not None:
+            self._ktail.check()
 
     def disable_xgmi(self) -> None:
         if self._xg is not None:

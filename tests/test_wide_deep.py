@@ -370,7 +370,7 @@ def test_chain_trainer_xcd_reduce_matches_plain_reduce():
     recs = synthetic_records(1 << 16, device="cuda", seed=9)
     out = []
     for xcd in (True, False):
-        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=16384, device="cuda")
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=16384, device="cuda", in_kernel_tail=False)
         assert tr._xcd is not None  # grid 128
         if not xcd:
             tr._xcd = None
@@ -442,3 +442,50 @@ def test_multi_step_graph_matches_single_step_replays():
         assert tr.steps_done == 17 + 2  # + the capture's warmup steps
         out.append(tr.param.clone())
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,opt", [(65536, "adagrad_ftrl"), (16384, "adam"), (8192, "sgd")])
+def test_in_kernel_tail_step_matches_three_launch_step(batch, opt):
+    """The one-launch step (slab reduction + optimizer inside the fused kernel after two grid barriers) against the
+    three-launch step (fused, XCD-local reduce, reduce + optimizer) over 12 steps with multi-step hipGraph replays:
+    same math, another fp32 association of the slab sum -> allclose; no barrier may time out."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    recs = synthetic_records(1 << 18, device="cuda", seed=13)
+    kw = {} if opt == "adagrad_ftrl" else {"dnn_opt": OptSpec(opt, lr=1e-3 if opt == "adam" else 0.01),
+                                           "wide_opt": OptSpec(opt, lr=1e-3 if opt == "adam" else 0.01)}
+    out = []
+    for tail in (True, False):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=batch, device="cuda", in_kernel_tail=tail, **kw)
+        assert (tr._ktail is not None) == tail
+        tr.set_data(recs)
+        tr.capture(steps_per_graph=5)
+        tr.run(12)
+        torch.cuda.synchronize()
+        assert tr.steps_done == 14  # 2 capture warmup steps + 12
+        if tail:
+            assert int(tr._ktail.err.item()) == 0
+        out.append((tr.param.clone(), tr.s0.clone(), tr.s1.clone(), tr.last_loss()))
+    for a, b in zip(out[0][:3], out[1][:3]):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=2e-4, atol=2e-6)
+    assert out[0][3] == pytest.approx(out[1][3], rel=1e-3)
+
+
+@pytest.mark.gpu
+def test_in_kernel_tail_is_run_to_run_deterministic_and_image_consistent():
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    recs = synthetic_records(1 << 18, device="cuda", seed=17)
+    res = []
+    for _ in range(2):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=4), batch=65536, device="cuda")
+        assert tr._ktail is not None
+        tr.set_data(recs)
+        for _ in range(6):
+            tr.step()
+        torch.cuda.synchronize()
+        res.append(tr.param.clone())
+        # the bf16 weight image the kernel re-emitted == the image built from its own fp32 master weights
+        assert torch.equal(tr.wt, tr._weight_image())
+    assert torch.equal(res[0], res[1])
