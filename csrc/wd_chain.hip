@@ -366,7 +366,12 @@ struct TailArgs {
   uint16_t* wt_out;              // the bf16 weight image (the kernel's own staging source)
   long long* step_slots;         // STEP_SLOTS per-workgroup optimizer step slots (slot 0 = the data offset step)
   OptHyper hd, hw;
+  long long* dbg;                // optional [grid][8] real-time stamps (tools/tail_stamps.py); null = off
 };
+#define TSTAMP(i)                                                                      \
+  do {                                                                                 \
+    if (ta.dbg != nullptr && threadIdx.x == 0) ta.dbg[blockIdx.x * 8 + (i)] = wall_clock64(); \
+  } while (0)
 constexpr int XMAXT = 16;  // XCC_ID range
 constexpr long long TAIL_TIMEOUT_TICKS = 200ll * 1000 * 1000;  // 2 s at the 100 MHz real-time clock
 
@@ -422,6 +427,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   BSTAMP(0);
   // the XCD this workgroup's slab row is written from (its L2 holds the row for the XCD-local reduction,
   // csrc/wide_deep.hip wd_reduce_xcd)
+  if constexpr (TAIL) TSTAMP(0);
   if (TRAIN && xcd_of != nullptr && tid == 0) {
     if (TAIL)  // read by workgroups on every XCD after the first barrier: write-through
       __hip_atomic_store(xcd_of + blockIdx.x, mifx_xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -750,7 +756,9 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     ScState st{-1, 0.f, 0.f, 0.f};
     if (tid < per) st = sc_load(gi, stride, ta.wsc, ta.param, ta.s0, ta.s1);
     const long long step = ta.step_slots[b] + 1;
+    TSTAMP(1);
     if (!grid_sync(ta.bar, ta.err, G, misc)) return;
+    TSTAMP(2);
     // ---- level 1
     const int x = mifx_xcc_id();
     if (tid < XMAXT) first[tid] = 1 << 30;
@@ -817,7 +825,9 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       }
       __syncthreads();
     }
+    TSTAMP(3);
     if (!grid_sync(ta.bar, ta.err, G, misc)) return;
+    TSTAMP(4);
     // ---- level 2 + optimizer
     if (tid < per && gi < stride) {
       const int nord = misc[3];
@@ -833,6 +843,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     if (tid == 0) ta.step_slots[b] = step;
     if (b == 0)
       for (int i = G + tid; i < STEP_SLOTS; i += NTHR) ta.step_slots[i] = step;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    TSTAMP(5);
   }
 }
 
@@ -907,7 +919,7 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
                         float* wide, float* slab, float* slab_loss, float grad_scale, int grid, const int* tmap,
                         int stride, int* xcd_of, float* xpart, unsigned long long* bar, int* err, const int* wsc,
                         float* param, float* s0, float* s1, const float* hyper_dnn, const float* hyper_wide,
-                        hipStream_t stream) {
+                        long long* dbg, hipStream_t stream) {
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
                                               hipSuccess)
@@ -929,6 +941,7 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
   ta.s1 = s1;
   ta.wt_out = (uint16_t*)wimg;
   ta.step_slots = step_ctr;
+  ta.dbg = dbg;
   ta.hd = OptHyper{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
                    hyper_dnn[6], hyper_dnn[7]};
   ta.hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],

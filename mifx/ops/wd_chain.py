@@ -20,7 +20,7 @@ def _fns():
         "fused_x": sig(lib, "mifx_wdc_fused_x", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
                                                  I32, VP, VP]),
         "fused_tail": sig(lib, "mifx_wdc_fused_tail", [VP, I64, I64, VP, VP, VP, VP, VP, F32, I32, VP, I32, VP, VP, VP,
-                                                       VP, VP, VP, VP, VP, VP, VP, VP]),
+                                                       VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -77,6 +77,7 @@ class InKernelTail:
         self.xpart = torch.zeros(16 * self.stride, device=device)
         self.bar = torch.zeros(1, dtype=torch.int64, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.dbg = None  # [256, 8] int64 real-time stamps when set (tools/tail_stamps.py)
 
     def step(self, tr) -> None:
         """One training step of FusedWideDeepTrainer `tr` (chained kernel, slab-column-order state)."""
@@ -89,7 +90,8 @@ class InKernelTail:
                                   ptr(tr.wide_weights), ptr(tr.slab), ptr(tr.slab_loss), float(tr.grad_scale),
                                   int(tr.grid), ptr(tr.tmap), int(tr.stride), ptr(self.xcd_of), ptr(self.xpart),
                                   ptr(self.bar), ptr(self.err), ptr(tr.wsc), ptr(tr.param_sc), ptr(tr.s0_sc),
-                                  ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide), stream_handle(tr.records.device))
+                                  ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide), ptr(self.dbg),
+                                  stream_handle(tr.records.device))
         check(rc, "mifx_wdc_fused_tail")
 
     def check(self) -> None:

@@ -143,11 +143,14 @@ class FusedWideDeepTrainer:
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
         self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
-        # one rank, large batch: the whole step in ONE launch -- slab reduction + optimizer inside the fused kernel
-        # after grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident: grid <= #CUs, one
-        # workgroup per CU by its LDS). in_kernel_tail=False (or MIFX_WD_TAIL=0) keeps the three-launch step.
+        # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
+        # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
+        # grid <= #CUs, one workgroup per CU by its LDS). Measured SLOWER on MI355X and therefore off by default:
+        # 40.8 vs 33.6 us per step at B=65536 (profiles/wd_tail_ab_r3.md): each cross-XCD grid barrier costs ~3 us
+        # (arrival atomic + polling through the fabric) and the write-through per-XCD partials ~7 us more before
+        # the second barrier, against ~11.6 us for the two tail kernels they replace.
         if in_kernel_tail is None:
-            in_kernel_tail = os.environ.get("MIFX_WD_TAIL", "1") != "0"
+            in_kernel_tail = os.environ.get("MIFX_WD_TAIL", "0") == "1"
         self._ktail = None
         if in_kernel_tail and self._sc and self.world == 1 and 64 <= self.grid <= 256 and self.waves == 8 \
                 and self.device.type == "cuda" and self.grid <= torch.cuda.get_device_properties(dev).multi_processor_count:
