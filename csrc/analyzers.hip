@@ -11,6 +11,10 @@
 //  * segment_hist: per-slice (count, label sum, pred sum, loss sum, correct) + a NB-bucket prediction
 //    histogram split by label, accumulated in LDS with ds_add then flushed with one global atomic
 //    per non-zero bin (host turns the histograms into AUC / precision / recall).
+//  * hist / select: equal-width or explicit-edge histograms (TFDV), and the exact order-statistic selection behind
+//    tft.quantiles / bucketize boundaries and TFDV quantiles / median: a uniform histogram narrows every wanted
+//    rank to one bin, the few values of those bins are gathered and ordered on the host (repeated on a bin that is
+//    too full) -- exact np.quantile results without a device sort.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -144,9 +148,99 @@ __global__ __launch_bounds__(256) void segment_hist_k(const int* __restrict__ se
   }
 }
 
+// ---- histograms (TFDV equal-width histograms, integer value counts, quantile narrowing)
+// mode 0 (edges): bin = searchsorted(edges, x, right) - 1 over nb + 1 sorted edges, the last bin closed --
+//   np.histogram's binning exactly (values outside [e0, e_nb] dropped); nb <= 4096.
+// mode 1 (uniform): bin = floor((x - lo) * inv), values with bin outside [0, nb) dropped; monotone in x (IEEE
+//   subtraction / multiplication by a positive constant), which is all the exact quantile selection needs;
+//   integer unit bins (inv = 1) are exact for integer-valued doubles.
+// Counts in LDS (ds_add) when nb <= 16384, one global atomic per non-zero bin per block; global atomics beyond.
+constexpr int HIST_LDS_BINS = 16384;
+
+__global__ __launch_bounds__(256) void hist_k(const double* __restrict__ x, long long n, int mode,
+                                              const double* __restrict__ edges, double lo, double inv, int nb,
+                                              unsigned long long* __restrict__ counts) {
+  extern __shared__ unsigned int lh[];
+  __shared__ double se[4097];
+  const bool use_lds = nb <= HIST_LDS_BINS;
+  if (use_lds)
+    for (int i = threadIdx.x; i < nb; i += 256) lh[i] = 0;
+  if (mode == 0)
+    for (int i = threadIdx.x; i <= nb; i += 256) se[i] = edges[i];
+  __syncthreads();
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double v = x[i];
+    if (v != v) continue;
+    int b;
+    if (mode == 0) {
+      if (v < se[0] || v > se[nb]) continue;
+      int l = 0, h = nb + 1;  // number of edges <= v
+      while (l < h) {
+        const int mid = (l + h) >> 1;
+        const bool le = se[mid] <= v;
+        l = le ? mid + 1 : l;
+        h = le ? h : mid;
+      }
+      b = l - 1;
+      if (b >= nb) b = nb - 1;  // v == last edge: the closed last bin
+    } else {
+      const double f = (v - lo) * inv;
+      if (!(f >= 0.0) || f >= (double)nb) continue;
+      b = (int)f;
+    }
+    if (use_lds)
+      atomicAdd(&lh[b], 1u);
+    else
+      atomicAdd(&counts[b], 1ull);
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += 256)
+      if (lh[i]) atomicAdd(&counts[i], (unsigned long long)lh[i]);
+  }
+}
+
+// candidate gather of the exact quantile selection: values whose uniform bin b has slot[b] >= 0 are appended to
+// out[slot * cap + pos] (pos from a per-slot counter; counts past cap are still counted, the host then narrows)
+__global__ __launch_bounds__(256) void select_k(const double* __restrict__ x, long long n, double lo, double inv,
+                                                int nb, const int* __restrict__ slot, int cap,
+                                                unsigned int* __restrict__ cnt, double* __restrict__ out) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double v = x[i];
+    if (v != v) continue;
+    const double f = (v - lo) * inv;
+    if (!(f >= 0.0) || f >= (double)nb) continue;
+    const int s = slot[(int)f];
+    if (s < 0) continue;
+    const unsigned int p = atomicAdd(&cnt[s], 1u);
+    if (p < (unsigned int)cap) out[(size_t)s * cap + p] = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int mifx_an_histogram(const double* x, long long n, int mode, const double* edges, double lo, double inv, int nb,
+                      unsigned long long* counts, hipStream_t st) {
+  if (nb <= 0 || (mode == 0 && (edges == nullptr || nb > 4096)) || mode < 0 || mode > 1) return -1;
+  const long long blocks = (n + 1023) / 1024;
+  const int grid = (int)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024);
+  const size_t lds = nb <= HIST_LDS_BINS ? (size_t)nb * 4 : 0;
+  if (lds > 32768) (void)hipFuncSetAttribute((const void*)hist_k, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  hipLaunchKernelGGL(hist_k, dim3(grid), dim3(256), lds, st, x, n, mode, edges, lo, inv, nb, counts);
+  return (int)hipGetLastError();
+}
+
+int mifx_an_select(const double* x, long long n, double lo, double inv, int nb, const int* slot, int cap,
+                   unsigned int* cnt, double* out, hipStream_t st) {
+  if (nb <= 0 || cap <= 0) return -1;
+  const long long blocks = (n + 1023) / 1024;
+  const int grid = (int)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024);
+  hipLaunchKernelGGL(select_k, dim3(grid), dim3(256), 0, st, x, n, lo, inv, nb, slot, cap, cnt, out);
+  return (int)hipGetLastError();
+}
+
 
 int mifx_an_moments(const double* x, long long n, void* partial, int grid, double* out, hipStream_t st) {
   if (grid <= 0 || grid > 4096) return -1;

@@ -32,8 +32,7 @@ def preprocessing_fn(inputs):
         out[xf(key)] = mt.bucketize(mt.fill_in_missing(inputs[key]), wdm.FEATURE_BUCKET_COUNT)
     for key in CATEGORICAL_FEATURE_KEYS:
         out[xf(key)] = mt.fill_in_missing(inputs[key]).astype(np.int64)
-    fare = np.asarray(inputs[FARE_KEY], dtype=object)
-    fare = np.array([np.nan if v is None else float(v) for v in fare])
+    fare = mt.to_float(inputs[FARE_KEY])  # missing -> NaN (vectorised)
     tips = mt.fill_in_missing(inputs[LABEL_KEY]).astype(np.float64)
     out[xf(LABEL_KEY)] = np.where(np.isnan(fare), 0, tips > 0.2 * np.nan_to_num(fare)).astype(np.int64)
     return out

@@ -26,25 +26,38 @@ def _common(n: int, present: int) -> dict:
             "tot_num_values": int(present)}
 
 
+def _gpu(device) -> bool:
+    return device is not None and str(device).startswith("cuda")
+
+
 def _num_stats(vals: np.ndarray, n: int, device=None) -> dict:
+    """On a GPU the column goes to the device ONCE and every statistic is a kernel there: moments (fp64 Welford),
+    the equal-width histogram (hist_k with np.histogram's edges), quantiles + median (exact order statistics by
+    histogram narrowing) -- bit-identical to the numpy path (tests/test_analyzers_quantiles.py)."""
+    from ..ops import analyzers
+
     present = vals.size
     st = {"common_stats": _common(n, present)}
     if present == 0:
         return st
-    if device is not None:
-        from ..ops import analyzers
+    x = vals.astype(np.float64)
+    if _gpu(device):
+        import torch
 
-        mom = analyzers.column_moments(vals, device=device)
+        x = torch.from_numpy(np.ascontiguousarray(x)).to(device)
+        mom = analyzers.column_moments(x, device=device)
     else:
-        v64 = vals.astype(np.float64)
-        mom = {"mean": float(v64.mean()), "std": float(v64.std()), "min": float(v64.min()), "max": float(v64.max()),
-               "zeros": int((v64 == 0).sum())}
+        mom = {"mean": float(x.mean()), "std": float(x.std()), "min": float(x.min()), "max": float(x.max()),
+               "zeros": int((x == 0).sum())}
+    dev = device if _gpu(device) else None
     lo, hi = mom["min"], mom["max"]
     edges = np.linspace(lo, hi, NUM_HIST_BUCKETS + 1) if hi > lo else np.array([lo, hi])
-    counts, _ = np.histogram(vals, bins=edges)
-    qs = np.quantile(vals.astype(np.float64), np.linspace(0, 1, NUM_QUANTILE_BUCKETS + 1))
+    counts = analyzers.histogram(x, edges, device=dev)
+    qgrid = np.linspace(0, 1, NUM_QUANTILE_BUCKETS + 1)
+    qv = analyzers.quantiles(x, np.concatenate([qgrid, [0.5]]), method="linear", device=dev)
+    qs, median = qv[:-1], float(qv[-1])
     st.update(mean=mom["mean"], std_dev=mom["std"], num_zeros=mom["zeros"], min=lo, max=hi,
-              median=float(np.median(vals)),
+              median=median,
               histograms=[
                   {"type": "STANDARD", "num_nan": 0, "buckets": [
                       {"low_value": float(edges[i]), "high_value": float(edges[i + 1]), "sample_count": float(c)}
@@ -55,14 +68,27 @@ def _num_stats(vals: np.ndarray, n: int, device=None) -> dict:
     return st
 
 
-def _string_stats(vals: np.ndarray, n: int) -> dict:
-    st = {"common_stats": _common(n, vals.size)}
-    if vals.size == 0:
+def _string_stats(vals, n: int, device=None) -> dict:
+    """vals: object array of str, or (GPU) the Arrow column itself -- the device hash-table count
+    (csrc/vocab.hip, exact with collision fallback) reads its buffers without a per-row Python pass."""
+    size = len(vals)
+    st = {"common_stats": _common(n, size)}
+    if size == 0:
         return st
-    s = pd.Series(vals.astype(str))
-    vc = s.value_counts()
+    if _gpu(device) and not isinstance(vals, np.ndarray):
+        import pyarrow.compute as pc
+
+        from ..ops import vocab as V
+
+        got = V.count_unique(vals, device=device) or V.count_unique(vals, device=None)
+        vc = pd.Series(got[1], index=got[0], dtype=np.int64)
+        avg_len = float(pc.mean(pc.utf8_length(vals)).as_py())
+    else:
+        s = pd.Series(np.asarray(vals, dtype=object).astype(str))
+        vc = s.value_counts()
+        avg_len = float(s.str.len().mean())
     vc = vc.sort_index(kind="stable").sort_values(ascending=False, kind="stable")
-    st.update(unique=int(vc.size), avg_length=float(s.str.len().mean()),
+    st.update(unique=int(vc.size), avg_length=avg_len,
               top_values=[{"value": str(k), "frequency": float(v)} for k, v in vc.head(TOP_K).items()],
               rank_histogram={"buckets": [{"low_rank": i, "high_rank": i, "label": str(k), "sample_count": float(v)}
                                           for i, (k, v) in enumerate(vc.head(50).items())]},
@@ -70,10 +96,12 @@ def _string_stats(vals: np.ndarray, n: int) -> dict:
     return st
 
 
-def _column(col: pa.ChunkedArray):
+def _column(col: pa.ChunkedArray, device=None):
     col = col.combine_chunks() if isinstance(col, pa.ChunkedArray) else col
     valid = col.drop_null()
     if pa.types.is_string(col.type) or pa.types.is_large_string(col.type) or pa.types.is_binary(col.type):
+        if _gpu(device):
+            return "STRING", valid
         return "STRING", np.array(valid.to_pylist(), dtype=object)
     if pa.types.is_integer(col.type) or pa.types.is_boolean(col.type):
         return "INT", valid.to_numpy(zero_copy_only=False).astype(np.int64)
@@ -89,14 +117,16 @@ def generate_statistics_from_table(table: pa.Table, name: str = "", device=None)
     n = table.num_rows
     feats = []
     for cname in table.column_names:
-        kind, vals = _column(table.column(cname))
+        kind, vals = _column(table.column(cname), device)
         f = {"name": cname, "type": kind}
         if kind == "STRING":
-            f["string_stats"] = _string_stats(vals, n)
+            f["string_stats"] = _string_stats(vals, n, device)
         else:
             f["num_stats"] = _num_stats(vals, n, device)
             if kind == "INT":  # categorical view for skew/drift comparators on int features
-                u, c = np.unique(vals, return_counts=True)
+                from ..ops.analyzers import int_value_counts
+
+                u, c = int_value_counts(vals, device=device if _gpu(device) else None)
                 if u.size <= 10000:
                     f["num_stats"]["value_counts"] = {str(int(a)): int(b) for a, b in zip(u, c)}
         feats.append(f)

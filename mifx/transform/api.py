@@ -121,10 +121,25 @@ def _np(x):
 
 
 def _num(x) -> np.ndarray:
-    a = np.asarray(_np(x))
+    """Numeric column as float64, missing -> NaN (Arrow columns converted without a per-row Python pass)."""
+    if _is_arrow(x):
+        import pyarrow as pa
+
+        a = x.combine_chunks() if isinstance(x, pa.ChunkedArray) else x
+        if pa.types.is_integer(a.type) or pa.types.is_floating(a.type) or pa.types.is_boolean(a.type):
+            return a.cast(pa.float64()).to_numpy(zero_copy_only=False)
+        x = _np(x)
+    a = np.asarray(x)
     if a.dtype == object:
-        a = np.array([np.nan if v is None else v for v in a], dtype=np.float64)
+        import pandas as pd
+
+        a = pd.to_numeric(pd.Series(a, dtype=object), errors="coerce").to_numpy(dtype=np.float64, na_value=np.nan)
     return a.astype(np.float64)
+
+
+def to_float(x) -> np.ndarray:
+    """Public: a column as float64 with missing values as NaN (e.g. the taxi label rule's NaN fare test)."""
+    return _num(x)
 
 
 def _str(x) -> np.ndarray:
@@ -146,14 +161,22 @@ def fill_in_missing(x, default=None) -> np.ndarray:
             return pc.fill_null(x, "" if default is None else default) if x.null_count else x
         x = _np(x)
     a = np.asarray(x, dtype=object) if not isinstance(x, np.ndarray) else x
-    if a.dtype == object:
-        is_str = any(isinstance(v, (str, bytes)) for v in a if v is not None)
+    if a.dtype == object:  # vectorised: pandas missing mask + dtype inference, no per-row Python loop
+        import pandas as pd
+
+        ser = pd.Series(a, dtype=object)
+        miss = ser.isna().to_numpy()
+        kind = pd.api.types.infer_dtype(ser[~miss], skipna=True) if (~miss).any() else "empty"
+        is_str = kind in ("string", "bytes", "mixed")
         d = ("" if is_str else 0) if default is None else default
-        out = np.array([d if v is None or (isinstance(v, float) and np.isnan(v)) else v for v in a], dtype=object)
-        if not is_str:
-            out = out.astype(np.float64)
-            if all(float(v).is_integer() for v in out):
-                out = out.astype(np.int64)
+        if is_str:
+            out = a.copy()
+            out[miss] = d
+            return out
+        out = pd.to_numeric(ser, errors="coerce").to_numpy(dtype=np.float64, na_value=np.nan)
+        out[miss] = d
+        if np.all(np.mod(out, 1) == 0):
+            out = out.astype(np.int64)
         return out
     if np.issubdtype(a.dtype, np.floating):
         return np.where(np.isnan(a), 0.0 if default is None else default, a)
@@ -220,10 +243,21 @@ def quantiles(x, num_buckets: int) -> list[float]:
     a = _num(x)
 
     def compute():
+        """Boundaries = the exact order statistics np.quantile(method="higher") picks at q = 1/nb .. (nb-1)/nb,
+        deduplicated. tft's quantiles analyzer is an epsilon-approximate sketch of the same order statistics
+        (`taxi_utils.py:128-130`); without TF the exact variant is the pinned definition here. On a GPU: a
+        histogram-narrowed selection (csrc/analyzers.hip hist_k / select_k), no sort of the column."""
         if a.size == 0:
             return []
-        qs = np.quantile(a, np.arange(1, num_buckets) / num_buckets, method="higher")
-        return sorted(set(float(q) for q in qs))
+        q = np.arange(1, num_buckets) / num_buckets
+        dev = _gpu_ctx(a.size)
+        if dev is not None:
+            from ..ops import analyzers
+
+            qs = analyzers.quantiles(a, q, method="higher", device=dev)
+        else:
+            qs = np.quantile(a[~np.isnan(a)], q, method="higher")
+        return sorted(set(float(v) for v in qs))
 
     return _analyzer("quantiles", {"num_buckets": num_buckets}, compute)
 

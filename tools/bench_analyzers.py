@@ -75,6 +75,35 @@ def main():
     tc, bc = _t(lambda: analyzers.bucketize(lat, bnd, device=None))
     assert np.array_equal(bg, bc)
     res.append({"op": "bucketize(10)", "rows": n, "gpu_ms": 1e3 * tg, "cpu_ms": 1e3 * tc})
+
+    qs = np.arange(1, 10) / 10
+    if dev:
+        tl = torch.from_numpy(lat).to(dev)  # column already on the device (Transform / TFDV GPU path)
+        tg, qg = _t(lambda: analyzers.quantiles(tl, qs, method="higher", device=dev))
+    else:
+        tg, qg = _t(lambda: analyzers.quantiles(lat, qs, method="higher"))
+    tc, qc = _t(lambda: np.quantile(lat, qs, method="higher"))
+    assert np.array_equal(qg, qc)
+    res.append({"op": "quantiles(10, method=higher) exact", "rows": n, "gpu_ms": 1e3 * tg, "cpu_ms": 1e3 * tc})
+    dup = rng.integers(0, 7, n).astype(np.float64)  # heavy duplicates: crowded bins
+    tg, qg = _t(lambda: analyzers.quantiles(dup, np.linspace(0, 1, 11), device=dev))
+    tc, qc = _t(lambda: np.quantile(dup, np.linspace(0, 1, 11)))
+    assert np.array_equal(qg, qc)
+    res.append({"op": "quantiles(linspace 11) duplicates", "rows": n, "gpu_ms": 1e3 * tg, "cpu_ms": 1e3 * tc})
+    edges = np.linspace(fare.min(), fare.max(), 11)
+    tg, hg = _t(lambda: analyzers.histogram(fare, edges, device=dev))
+    tc, hc = _t(lambda: np.histogram(fare, bins=edges)[0])
+    assert np.array_equal(hg, hc)
+    res.append({"op": "histogram(10 equal-width)", "rows": n, "gpu_ms": 1e3 * tg, "cpu_ms": 1e3 * tc})
+
+    from mifx.data_validation import stats as S
+
+    tbl = pa.table({"fare": fare, "pickup_latitude": lat, "trip_start_hour": rng.integers(0, 24, n),
+                    "company": arr})
+    tg, sg = _t(lambda: S.generate_statistics_from_table(tbl, device=dev), reps=2)
+    tc, sc = _t(lambda: S.generate_statistics_from_table(tbl, device=None), reps=1)
+    assert sg == sc
+    res.append({"op": "TFDV generate_statistics (4 columns)", "rows": n, "gpu_ms": 1e3 * tg, "cpu_ms": 1e3 * tc})
     for r in res:
         print(json.dumps(r), flush=True)
 
