@@ -1,5 +1,5 @@
-// Grouped convolution as an implicit GEMM on bf16 MFMA (NHWC): forward (any stride), stride-1 input gradient,
-// weight gradient (any stride).
+// Grouped convolution as an implicit GEMM on bf16 MFMA (NHWC): forward (any stride), input gradient (stride 1:
+// the forward kernel on the flipped weight; stride > 1: a phase-split kernel), weight gradient (any stride).
 //
 // Reference workload: the PATE-2017 `deep_cnn.inference` CNN (5x5 convs 64/128 channels,
 // `research/pate_2017/deep_cnn.py:84-191`) trained for every teacher of the ensemble
@@ -159,6 +159,136 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
+// ---- input gradient of a STRIDED convolution -----------------------------------------------------------
+// dx[n, h, w, g*C + c] = sum over taps (r, s) with (h + pad - r) % st == 0 and (w + pad - s) % st == 0 of
+//   dy[n, (h + pad - r) / st, (w + pad - s) / st, g*K + k] * w[g][k][c][r][s].
+// Split by output phase (h % st, w % st): inside a phase every pixel takes the SAME taps
+// (r = r0 + st a, r0 = (ph + pad) % st; likewise s), and the dy row of tap a is p = i - a + bh for dx row
+// h = ph + st i (bh = (ph + pad - r0) / st) -- a stride-1 implicit GEMM per phase with no wasted (zero) taps.
+// blockIdx.z = g * st^2 + phase, pixel tiles are phase-major (pixels of one tile share the phase), reduction =
+// (phase taps) x K in 32-wide chunks; same tile / LDS / MFMA structure as gconv_fwd. Weight image: the transposed
+// (unflipped) [G][C][R][S][K] layout; dx rows are scattered back to (n, h, w) in the epilogue.
+template <int BN>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_dgrad_s(
+    const bf16* __restrict__ dy, const bf16* __restrict__ wt, bf16* __restrict__ dx, Geo d) {
+  constexpr int BCH = (BN * 4 + kThreads - 1) / kThreads;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BM * LDR + 2 * BN * LDR];
+  bf16(*As)[BM * LDR] = reinterpret_cast<bf16(*)[BM * LDR]>(smem);
+  bf16(*Bs)[BN * LDR] = reinterpret_cast<bf16(*)[BN * LDR]>(smem + 2 * BM * LDR);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int st = d.stride, nph = st * st;
+  const int g = blockIdx.z / nph, ph = (blockIdx.z % nph) / st, pw = blockIdx.z % st;
+  const int n0 = blockIdx.y * BN;
+  const int Hp = (d.Hi - ph + st - 1) / st, Wp = (d.Wi - pw + st - 1) / st;  // dx rows / cols of this phase
+  const long long Mp = (long long)d.N * Hp * Wp;
+  const long long m0 = (long long)blockIdx.x * BM;
+  if (Hp <= 0 || Wp <= 0 || m0 >= Mp) return;
+  const int r0 = (ph + d.pad) % st, s0 = (pw + d.pad) % st;
+  const int Ra = r0 < d.R ? (d.R - r0 + st - 1) / st : 0, Sa = s0 < d.S ? (d.S - s0 + st - 1) / st : 0;
+  const int bh = (ph + d.pad - r0) / st, bw = (pw + d.pad - s0) / st;
+  const int KT = d.G * d.K;  // dy row stride (channels)
+  const int chunks_k = d.K / BK, nsteps = Ra * Sa * chunks_k;
+
+  int an[2], ai[2], aj[2];
+  bool am[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const long long m = m0 + (t >> 2) + 64 * j;
+    am[j] = m < Mp;
+    const long long mm = am[j] ? m : 0;
+    aj[j] = (int)(mm % Wp);
+    ai[j] = (int)((mm / Wp) % Hp);
+    an[j] = (int)(mm / ((long long)Wp * Hp));
+  }
+  const int apart = (t & 3) * 8;
+  const bf16* wg = wt + (size_t)g * d.C * d.R * d.S * d.K;
+
+  u4 ra[2], rb[BCH];
+  auto load = [&](int step) {
+    const int tap = step / chunks_k, k0 = (step - tap * chunks_k) * BK;
+    const int a = tap / Sa, b = tap - a * Sa;
+    const int r = r0 + st * a, s = s0 + st * b;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = ai[j] - a + bh, q = aj[j] - b + bw;
+      if (am[j] && p >= 0 && p < d.Ho && q >= 0 && q < d.Wo) {
+        ra[j] = *(const u4*)(dy + ((size_t)(an[j] * d.Ho + p) * d.Wo + q) * KT + g * d.K + k0 + apart);
+      } else {
+        ra[j] = u4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      const int c = t + kThreads * j, cr = c >> 2, part = (c & 3) * 8;
+      if ((BN * 4) % kThreads == 0 || c < BN * 4)
+        rb[j] = *(const u4*)(wg + (((size_t)(n0 + cr) * d.R + r) * d.S + s) * d.K + k0 + part);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *(u4*)(&As[buf][((t >> 2) + 64 * j) * LDR + apart]) = ra[j];
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) {
+      const int c = t + kThreads * j;
+      if ((BN * 4) % kThreads == 0 || c < BN * 4) *(u4*)(&Bs[buf][(c >> 2) * LDR + (c & 3) * 8]) = rb[j];
+    }
+  };
+
+  constexpr int TN = BN / 32;
+  v4f acc[4][TN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int wm = (wv >> 1) * 64, wn = (wv & 1) * (BN / 2);
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+
+  if (nsteps > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    if (step + 1 < nsteps) load(step + 1);
+    v8bf af[4], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const v8bf*)(&As[buf][(wm + 16 * i + fr) * LDR + fk]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = *(const v8bf*)(&Bs[buf][(wn + 16 * j + fr) * LDR + fk]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
+    if (step + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  constexpr int CLD = BN + 8;
+  static_assert(BM * CLD <= 2 * BM * LDR + 2 * BN * LDR, "epilogue tile fits the staging buffers");
+  bf16* Cs = smem;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl = wn + 16 * j + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[(wm + 16 * i + 4 * (lane >> 4) + e) * CLD + cl] = (bf16)acc[i][j][e];
+  }
+  __syncthreads();
+  const int CT = d.G * d.C;
+  constexpr int CPR = BN / 8;
+  for (int c = t; c < BM * CPR; c += kThreads) {
+    const int row = c / CPR, part = (c % CPR) * 8;
+    const long long m = m0 + row;
+    if (m < Mp) {
+      const int jj = (int)(m % Wp), ii = (int)((m / Wp) % Hp), nn = (int)(m / ((long long)Wp * Hp));
+      const int h = ph + st * ii, w = pw + st * jj;
+      *(u4*)(dx + ((size_t)(nn * d.Hi + h) * d.Wi + w) * CT + g * d.C + n0 + part) = *(const u4*)(&Cs[row * CLD + part]);
+    }
+  }
+}
+
 // ---- weight gradient ------------------------------------------------------------------------------------
 // dw[g*K + k][c][r][s] = sum_m dy[m][g*K + k] * x[pixel(m) + (r - pad, s - pad)][g*C + c]: a GEMM of
 // 128 k-rows x 128 (tap, c) columns per workgroup (the flattened tap-major column space), reduced over output pixels m in
@@ -287,6 +417,33 @@ int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, in
   const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride};
   hipLaunchKernelGGL(gconv_wgrad, dim3((R * S * C + 127) / 128, (K + 127) / 128, G), dim3(kThreads), 0, st,
                      (const bf16*)x, (const bf16*)dy, dw, d);
+  return (int)hipGetLastError();
+}
+
+// Input gradient of a convolution with stride >= 1: dy [N, Ho, Wo, G*K] bf16, wt [G][C][R][S][K] bf16 (the weight
+// transposed, NOT flipped), dx [N, Hi, Wi, G*C] bf16 (every element written). Needs C % 32 == 0, K % 32 == 0.
+int mifx_gconv_dgrad_strided(const void* dy, const void* wt, void* dx, int N, int Hi, int Wi, int G, int C, int K,
+                             int R, int S, int pad, int stride, hipStream_t st) {
+  if (stride <= 0 || stride > 8) return -1;
+  const int Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
+  if (N <= 0 || G <= 0 || C <= 0 || C % 32 != 0 || K <= 0 || K % BK != 0 || Hi + 2 * pad < R || Wi + 2 * pad < S ||
+      pad < 0 || pad >= R || pad >= S || Ho <= 0 || Wo <= 0)
+    return -1;
+  if ((long long)G * stride * stride > 65535) return -1;
+  const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride};
+  const long long Hp = (Hi + stride - 1) / stride, Wp = (Wi + stride - 1) / stride;  // the largest phase
+  const long long mt = ((long long)N * Hp * Wp + BM - 1) / BM;
+  if (mt > 0x7fffffffLL) return -1;
+  const dim3 z((unsigned)mt, 1, (unsigned)(G * stride * stride));
+  if (C % 128 == 0)
+    hipLaunchKernelGGL(gconv_dgrad_s<128>, dim3(z.x, C / 128, z.z), dim3(kThreads), 0, st, (const bf16*)dy,
+                       (const bf16*)wt, (bf16*)dx, d);
+  else if (C % 64 == 0)
+    hipLaunchKernelGGL(gconv_dgrad_s<64>, dim3(z.x, C / 64, z.z), dim3(kThreads), 0, st, (const bf16*)dy,
+                       (const bf16*)wt, (bf16*)dx, d);
+  else
+    hipLaunchKernelGGL(gconv_dgrad_s<32>, dim3(z.x, C / 32, z.z), dim3(kThreads), 0, st, (const bf16*)dy,
+                       (const bf16*)wt, (bf16*)dx, d);
   return (int)hipGetLastError();
 }
 

@@ -1,9 +1,9 @@
 """Grouped stride-1 NHWC convolution on hand-written bf16 MFMA implicit-GEMM kernels (csrc/gconv.hip).
 
-`conv2d(x, weight, bias, padding, groups)` == `F.conv2d(x, weight, bias, stride=1, padding=padding,
-groups=groups)` for channels-last bf16 activations: the forward and the input gradient run one HIP kernel (the
-input gradient of a stride-1 conv is the same kernel on dy with the weight flipped and transposed), the weight
-gradient a second one (transposed LDS reads). `eligible()` says when a call can take this path
+`conv2d(x, weight, bias, padding, groups, stride=...)` == `F.conv2d(...)` for channels-last bf16 activations: the
+forward and the stride-1 input gradient run one HIP kernel (the input gradient of a stride-1 conv is the same
+kernel on dy with the weight flipped and transposed), a strided conv's input gradient a phase-split kernel
+(`dgrad_strided`), the weight gradient a third one (transposed LDS reads). `eligible()` says when a call can take this path
 (GPU, C/group % 32 == 0, K/group % 32 == 0 (the input gradient likewise, with the roles of C and K swapped); the weight gradient needs
 C/group % 8 == 0 and enough (tap, k, group) tiles, else those parts run on MIOpen); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
 ensemble (`mifx/privacy/pate/ensemble.py`)."""
@@ -22,7 +22,18 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 def _fns():
     lib = _lib.load("gconv")
     return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 11 + [VP]),
-            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 10 + [VP])}
+            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 10 + [VP]),
+            "dgrad_s": sig(lib, "mifx_gconv_dgrad_strided", [VP, VP, VP] + [I32] * 10 + [VP])}
+
+
+def dgrad_strided(dyb: torch.Tensor, wb: torch.Tensor, N, Hi, Wi, G, C, K, R, S, pad, stride) -> torch.Tensor:
+    """Input gradient of a strided (grouped) convolution on the phase-split HIP kernel: dy bf16 channels-last
+    [N, G*K, Ho, Wo], weight bf16 [G*K, C, R, S] -> dx bf16 channels-last [N, G*C, Hi, Wi]."""
+    wt = wb.view(G, K, C, R, S).permute(0, 2, 3, 4, 1).contiguous()  # [G][C][R][S][K], not flipped
+    dx = torch.empty(N, G * C, Hi, Wi, device=dyb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+    check(_fns()["dgrad_s"](ptr(dyb), ptr(wt), ptr(dx), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
+                            stream_handle(dyb.device)), "mifx_gconv_dgrad_strided")
+    return dx
 
 
 def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int, stride: int = 1) -> bool:
@@ -79,6 +90,8 @@ class _GConv(torch.autograd.Function):
                 # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
                 w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
                 dx = _launch(dyb, w_bwd, None, N, Ho, Wo, G, K, C, R, S, R - 1 - pad)
+            elif stride > 1 and C % 32 == 0 and K % 32 == 0:  # phase-split strided input gradient
+                dx = dgrad_strided(dyb, wb, N, Hi, Wi, G, C, K, R, S, pad, stride)
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:

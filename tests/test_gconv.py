@@ -1,4 +1,4 @@
-"""Grouped stride-1 NHWC implicit-GEMM convolution (csrc/gconv.hip) vs an fp32 PyTorch reference."""
+"""Grouped NHWC implicit-GEMM convolution (csrc/gconv.hip) vs an fp32 PyTorch reference."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -39,9 +39,29 @@ def test_gconv_fwd_bwd_match_fp32_reference(N, H, G, C, K, R, pad, relu):
 @pytest.mark.parametrize("N,H,G,C,K,R,pad", [(2, 9, 3, 96, 96, 3, 0), (2, 15, 24, 192, 192, 3, 0),
                                              (3, 8, 2, 64, 128, 3, 1)])
 def test_gconv_stride2_matches_fp32_reference(N, H, G, C, K, R, pad):
-    """Strided forward + weight gradient on the HIP kernels (input gradient on MIOpen) -- PATE inference_deeper's
-    stride-2 layers."""
+    """Strided forward, phase-split input gradient and weight gradient, all on the HIP kernels -- PATE
+    inference_deeper's stride-2 layers."""
     _check_against_reference(N, H, G, C, K, R, pad, False, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,G,C,K,R,pad,stride", [(2, 9, 3, 96, 96, 3, 0, 2), (2, 10, 2, 64, 32, 3, 1, 2),
+                                                    (3, 11, 1, 128, 64, 5, 2, 2), (2, 13, 4, 32, 96, 3, 1, 3),
+                                                    (2, 7, 2, 32, 32, 1, 0, 2), (1, 16, 250, 96, 96, 3, 0, 2)])
+def test_gconv_strided_input_gradient_kernel(N, H, G, C, K, R, pad, stride):
+    """The phase-split input gradient (csrc/gconv.hip gconv_dgrad_s) alone against the fp32 reference: odd and
+    even sizes (phases with fewer rows), strides 2 and 3, 1x1 taps (phases without taps: zero rows), 250 groups."""
+    torch.manual_seed(1)
+    dev = "cuda"
+    W = H + 1
+    Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1
+    w = (0.05 * torch.randn(G * K, C, R, R, device=dev)).to(torch.bfloat16)
+    dy = torch.randn(N, G * K, Ho, Wo, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_input((N, G * C, H, W), w.float(), dy.float(), stride=stride, padding=pad, groups=G)
+    got = gconv.dgrad_strided(dy, w, N, H, W, G, C, K, R, R, pad, stride)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    sc = ref.abs().max()
+    torch.testing.assert_close(got.float() / sc, ref / sc, rtol=0, atol=1e-2)
 
 
 def _check_against_reference(N, H, G, C, K, R, pad, relu, stride):
