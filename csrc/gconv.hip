@@ -309,16 +309,22 @@ __device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
   return __builtin_bit_cast(v8bf, r);
 }
 
+// Split over output pixels (splits > 1, blockIdx.z = g * splits + split): few (tap, k, group) tiles -- a single
+// group, e.g. ResNet-50's convs -- would leave most CUs idle, so the pixel reduction is cut into `splits` ranges of
+// whole 32-pixel chunks; each writes its partial dW into part[split] and gconv_wgrad_sum adds the splits in split
+// order (deterministic: no atomics).
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_wgrad(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                        float* __restrict__ dw, Geo d) {
+                                                        float* __restrict__ dw, Geo d, int splits) {
   __shared__ __attribute__((aligned(16))) bf16 As[2][32 * WLD];  // dy chunk [pixel][k]
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][32 * WLD];  // x chunk [pixel][(tap, c)]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int g = blockIdx.z, k0 = blockIdx.y * 128;
+  const int g = blockIdx.z / splits, sp = blockIdx.z - g * splits, k0 = blockIdx.y * 128;
   const int RS = d.R * d.S, col0 = blockIdx.x * 128;  // 128 columns of the flattened (tap, c) space
   const long long M = (long long)d.N * d.Ho * d.Wo;
   const int KT = d.G * d.K, CT = d.G * d.C;
-  const int nsteps = (int)((M + 31) / 32);
+  const int total = (int)((M + 31) / 32), per = (total + splits - 1) / splits;
+  const int s_begin = sp * per, nsteps = max(0, min(total, s_begin + per) - s_begin);
+  if (splits > 1) dw += (size_t)sp * d.G * d.K * d.C * RS;  // this split's partial
   // this thread's chunks: pixel rows pr[j] = (t >> 4) + 16 j, 16-byte chunk (t & 15) of the 256-byte row
   const int ch = t & 15;
   const int bcol = col0 + ch * 8;  // C % 8 == 0: an 8-channel chunk never straddles two taps
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   auto load = [&](int step) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const long long m = (long long)step * 32 + (t >> 4) + 16 * j;
+      const long long m = (long long)(s_begin + step) * 32 + (t >> 4) + 16 * j;
       ra[j] = u4{0, 0, 0, 0};
       rb[j] = u4{0, 0, 0, 0};
       if (m < M) {
@@ -361,8 +367,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int rd_row = 4 * grp + q, rd_col = 4 * p;
 
-  load(0);
-  store(0);
+  if (nsteps > 0) {
+    load(0);
+    store(0);
+  }
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int buf = step & 1;
@@ -400,23 +408,56 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
+// dw[i] = sum over splits (in split order) of part[split][i]
+__global__ __launch_bounds__(256) void gconv_wgrad_sum(const float4* __restrict__ part, long long n4, int splits,
+                                                       float4* __restrict__ dw) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 a = part[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 v = part[(size_t)s * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    dw[i] = a;
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
+// pixel splits the weight gradient takes for a shape (>= 2 x 256 workgroups when the pixel count allows, every
+// split >= 16 chunks of 32 pixels); the caller provides splits x |dw| floats of scratch when it is > 1
+int mifx_gconv_wgrad_splits(int N, int Hi, int Wi, int G, int C, int K, int R, int S, int pad, int stride) {
+  if (stride <= 0) return 1;
+  const long long Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
+  const long long tiles = (long long)((R * S * C + 127) / 128) * ((K + 127) / 128) * G;
+  const long long chunks = ((long long)N * Ho * Wo + 31) / 32;
+  long long sp = (512 + tiles - 1) / tiles;
+  sp = sp < chunks / 16 ? sp : chunks / 16;
+  sp = sp < 32 ? sp : 32;
+  return (int)(sp > 1 ? sp : 1);
+}
+
 // dw [G*K][C][R][S] fp32 (PyTorch layout) from x [N, Hi, Wi, G*C] and dy [N, Ho, Wo, G*K] bf16 (NHWC).
 // Needs C % 8 == 0 and K % 8 == 0 (tiles of 128 k x 128 (tap, c) columns; partial last tiles are masked).
+// splits / part: mifx_gconv_wgrad_splits(...) and its scratch (part may be null when splits == 1).
 int mifx_gconv_wgrad(const void* x, const void* dy, float* dw, int N, int Hi, int Wi, int G, int C, int K, int R,
-                     int S, int pad, int stride, hipStream_t st) {
+                     int S, int pad, int stride, int splits, float* part, hipStream_t st) {
   if (stride <= 0) return -1;
   const int Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
-  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % 8 != 0 || K <= 0 || K % 8 != 0 || Hi + 2 * pad < R ||
-      Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S)
+  if (N <= 0 || G <= 0 || C <= 0 || C % 8 != 0 || K <= 0 || K % 8 != 0 || Hi + 2 * pad < R ||
+      Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S || splits < 1 || (splits > 1 && part == nullptr))
     return -1;
-  if ((long long)N * Ho * Wo > 0x3fffffffLL) return -1;
+  if ((long long)N * Ho * Wo > 0x3fffffffLL || (long long)G * splits > 65535) return -1;
   const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride};
-  hipLaunchKernelGGL(gconv_wgrad, dim3((R * S * C + 127) / 128, (K + 127) / 128, G), dim3(kThreads), 0, st,
-                     (const bf16*)x, (const bf16*)dy, dw, d);
+  hipLaunchKernelGGL(gconv_wgrad, dim3((R * S * C + 127) / 128, (K + 127) / 128, G * splits), dim3(kThreads), 0, st,
+                     (const bf16*)x, (const bf16*)dy, splits > 1 ? part : dw, d, splits);
+  if (splits > 1) {
+    const long long n4 = (long long)G * K * C * R * S / 4;  // C % 8 == 0: divisible
+    const long long blocks = (n4 + 255) / 256;
+    hipLaunchKernelGGL(gconv_wgrad_sum, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, st,
+                       (const float4*)part, n4, splits, (float4*)dw);
+  }
   return (int)hipGetLastError();
 }
 

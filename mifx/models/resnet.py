@@ -7,8 +7,32 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import os
+
+from ..ops import gconv
 from ..ops.bn_relu import BatchNormReLU2d
 from ..ops.pool import max_pool3s2
+
+# MIFX_RESNET_HIP_CONV=1: the block convolutions (1x1 and 3x3, any stride) on the hand-written MFMA implicit-GEMM
+# kernels (csrc/gconv.hip: forward, stride-1 / phase-split strided input gradient, pixel-split weight gradient);
+# 0 (default until the whole-step A/B says otherwise, profiles/resnet_gconv_ab_r3.txt): MIOpen.
+USE_HIP_CONV = os.environ.get("MIFX_RESNET_HIP_CONV", "0") == "1"
+
+
+class HipConv2d(nn.Conv2d):
+    """nn.Conv2d whose CUDA forward / backward run csrc/gconv.hip when the shape is eligible (channels % 32,
+    symmetric padding < kernel); bf16 channels-last output like F.conv2d under bf16 autocast."""
+
+    def forward(self, x):
+        if x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.padding[0] == self.padding[1] \
+                and self.stride[0] == self.stride[1] and self.kernel_size[0] == self.kernel_size[1] \
+                and gconv.eligible(x, self.weight, 1, self.padding[0], self.stride[0]):
+            return gconv.conv2d(x, self.weight, self.bias, padding=self.padding[0], stride=self.stride[0])
+        return super().forward(x)
+
+
+def _conv(*a, **kw):
+    return (HipConv2d if USE_HIP_CONV else nn.Conv2d)(*a, **kw)
 
 
 class PreActBottleneck(nn.Module):
@@ -18,12 +42,12 @@ class PreActBottleneck(nn.Module):
         super().__init__()
         cout = width * self.expansion
         self.bn0 = BatchNormReLU2d(cin)  # every BN of the pre-activation net feeds a ReLU: fused
-        self.shortcut = nn.Conv2d(cin, cout, 1, stride=stride, bias=False) if (stride != 1 or cin != cout) else None
-        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.shortcut = _conv(cin, cout, 1, stride=stride, bias=False) if (stride != 1 or cin != cout) else None
+        self.conv1 = _conv(cin, width, 1, bias=False)
         self.bn1 = BatchNormReLU2d(width)
-        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.conv2 = _conv(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNormReLU2d(width)
-        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.conv3 = _conv(width, cout, 1, bias=False)
 
     def forward(self, x):
         """x: a tensor, or the (branch, shortcut) pair of the previous block whose sum is this block's

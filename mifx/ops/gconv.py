@@ -4,8 +4,8 @@
 forward and the stride-1 input gradient run one HIP kernel (the input gradient of a stride-1 conv is the same
 kernel on dy with the weight flipped and transposed), a strided conv's input gradient a phase-split kernel
 (`dgrad_strided`), the weight gradient a third one (transposed LDS reads). `eligible()` says when a call can take this path
-(GPU, C/group % 32 == 0, K/group % 32 == 0 (the input gradient likewise, with the roles of C and K swapped); the weight gradient needs
-C/group % 8 == 0 and enough (tap, k, group) tiles, else those parts run on MIOpen); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
+(GPU, C/group % 32 == 0, K/group % 32 == 0 (the input gradient likewise, with the roles of C and K swapped); the weight
+gradient needs C/group % 8 == 0 and splits over output pixels when there are few (tap, k, group) tiles); otherwise callers use F.conv2d. SURVEY KN14; used by the PATE teacher
 ensemble (`mifx/privacy/pate/ensemble.py`)."""
 from __future__ import annotations
 
@@ -22,7 +22,8 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 def _fns():
     lib = _lib.load("gconv")
     return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 11 + [VP]),
-            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 10 + [VP]),
+            "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 11 + [VP, VP]),
+            "wsplits": sig(lib, "mifx_gconv_wgrad_splits", [I32] * 10),
             "dgrad_s": sig(lib, "mifx_gconv_dgrad_strided", [VP, VP, VP] + [I32] * 10 + [VP])}
 
 
@@ -54,6 +55,17 @@ def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, 
     check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
                         int(relu), stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
     return y
+
+
+def wgrad(xb: torch.Tensor, dyb: torch.Tensor, N, Hi, Wi, G, C, K, R, S, pad, stride) -> torch.Tensor:
+    """Weight gradient [G*K, C, R, S] fp32 of a (grouped, strided) conv on the HIP kernel: x / dy bf16
+    channels-last; split over output pixels when the (tap, k, group) tiles alone cannot fill the chip."""
+    sp = int(_fns()["wsplits"](N, Hi, Wi, G, C, K, R, S, pad, int(stride)))
+    dw = torch.empty(G * K, C, R, S, device=dyb.device, dtype=torch.float32)
+    part = torch.empty(sp * dw.numel(), device=dyb.device, dtype=torch.float32) if sp > 1 else None
+    check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad, int(stride), sp, ptr(part),
+                          stream_handle(dyb.device)), "mifx_gconv_wgrad")
+    return dw
 
 
 class _GConv(torch.autograd.Function):
@@ -95,17 +107,13 @@ class _GConv(torch.autograd.Function):
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
-            wg_blocks = ((R * S * C + 127) // 128) * ((K + 127) // 128) * G if C % 8 == 0 else 0
             if R == 1 and S == 1 and pad == 0 and stride == 1:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
                 dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
-            elif wg_blocks >= 256:  # hand-written weight gradient (fp32 out, PyTorch layout); it has no split over
-                # pixels, so it needs many (tap, k, group) tiles to fill the chip -- else MIOpen's
-                dw = torch.empty(G * K, C, R, S, device=dyb.device, dtype=torch.float32)
-                check(_fns()["wgrad"](ptr(xb), ptr(dyb), ptr(dw), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
-                                      stream_handle(dyb.device)), "mifx_gconv_wgrad")
-                dw = dw.to(wdt)
+            elif C % 8 == 0 and K % 8 == 0:  # hand-written weight gradient (fp32 out, PyTorch layout); few
+                # (tap, k, group) tiles (one group) -> split over output pixels + a deterministic split sum
+                dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
             else:
                 dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
                                                  groups=G).to(wdt)

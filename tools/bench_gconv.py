@@ -27,7 +27,10 @@ def timeit(fn, it=10):
 SHAPES = {"pate": [(250, 128, 14, 64, 128, 5), (50, 128, 14, 64, 128, 5), (1, 128, 14, 64, 128, 5)],
           # ResNet-50 3x3 stride-1 convs at B=256 (config 5)
           "resnet": [(1, 256, 56, 64, 64, 3), (1, 256, 28, 128, 128, 3), (1, 256, 14, 256, 256, 3),
-                     (1, 256, 7, 512, 512, 3)]}
+                     (1, 256, 7, 512, 512, 3)],
+          # ResNet-50 1x1 convs (B=256): expand / reduce of each stage
+          "resnet1x1": [(1, 256, 56, 64, 256, 1), (1, 256, 56, 256, 64, 1), (1, 256, 28, 512, 128, 1),
+                        (1, 256, 14, 1024, 256, 1), (1, 256, 7, 2048, 512, 1)]}
 which = sys.argv[1] if len(sys.argv) > 1 else "pate"
 for G, B, H, C, K, R in SHAPES[which]:
     x = torch.randn(B, G * C, H, H, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
