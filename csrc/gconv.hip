@@ -425,16 +425,19 @@ __global__ __launch_bounds__(256) void gconv_wgrad_sum(const float4* __restrict_
 
 extern "C" {
 
-// pixel splits the weight gradient takes for a shape (>= 2 x 256 workgroups when the pixel count allows, every
-// split >= 16 chunks of 32 pixels); the caller provides splits x |dw| floats of scratch when it is > 1
+// pixel splits the weight gradient takes for a shape: ~1024 workgroups (4 per CU: the kernel's occupancy) when the
+// pixel count allows, every split >= 16 chunks of 32 pixels, at most 256 splits and 64 M floats of partials; the
+// caller provides splits x |dw| floats of scratch when it is > 1
 int mifx_gconv_wgrad_splits(int N, int Hi, int Wi, int G, int C, int K, int R, int S, int pad, int stride) {
   if (stride <= 0) return 1;
   const long long Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
   const long long tiles = (long long)((R * S * C + 127) / 128) * ((K + 127) / 128) * G;
   const long long chunks = ((long long)N * Ho * Wo + 31) / 32;
-  long long sp = (512 + tiles - 1) / tiles;
+  const long long dwn = (long long)G * K * C * R * S;
+  long long sp = (1024 + tiles - 1) / tiles;
   sp = sp < chunks / 16 ? sp : chunks / 16;
-  sp = sp < 32 ? sp : 32;
+  sp = sp < 256 ? sp : 256;
+  while (sp > 1 && sp * dwn > (64ll << 20)) --sp;
   return (int)(sp > 1 ? sp : 1);
 }
 

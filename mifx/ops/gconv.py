@@ -107,13 +107,13 @@ class _GConv(torch.autograd.Function):
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
-            if R == 1 and S == 1 and pad == 0 and stride == 1:  # 1x1: dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
+            if C % 8 == 0 and K % 8 == 0:  # hand-written weight gradient (fp32 out, PyTorch layout); few
+                # (tap, k, group) tiles (one group) -> split over output pixels + a deterministic split sum
+                dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
+            elif R == 1 and S == 1 and pad == 0 and stride == 1:  # 1x1: dw[g] = dy_g^T x_g, one batched GEMM
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
                 dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
-            elif C % 8 == 0 and K % 8 == 0:  # hand-written weight gradient (fp32 out, PyTorch layout); few
-                # (tap, k, group) tiles (one group) -> split over output pixels + a deterministic split sum
-                dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
             else:
                 dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
                                                  groups=G).to(wdt)
