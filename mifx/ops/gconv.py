@@ -57,6 +57,9 @@ def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, 
     return y
 
 
+WGRAD_HIP_SINGLE_GROUP = False  # single-group weight gradients on the HIP kernel too (A/B switch)
+
+
 def wgrad(xb: torch.Tensor, dyb: torch.Tensor, N, Hi, Wi, G, C, K, R, S, pad, stride) -> torch.Tensor:
     """Weight gradient [G*K, C, R, S] fp32 of a (grouped, strided) conv on the HIP kernel: x / dy bf16
     channels-last; split over output pixels when the (tap, k, group) tiles alone cannot fill the chip."""
@@ -107,13 +110,18 @@ class _GConv(torch.autograd.Function):
             else:
                 dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
         if ctx.needs_input_grad[1]:
-            if C % 8 == 0 and K % 8 == 0:  # hand-written weight gradient (fp32 out, PyTorch layout); few
-                # (tap, k, group) tiles (one group) -> split over output pixels + a deterministic split sum
-                dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
-            elif R == 1 and S == 1 and pad == 0 and stride == 1:  # 1x1: dw[g] = dy_g^T x_g, one batched GEMM
+            # Weight-gradient policy from measurements (profiles/gconv_resnet_shapes_r3.jsonl,
+            # pate_ensemble_bench_r3*.jsonl): grouped 1x1 -> one batched GEMM; other grouped convs -> the HIP kernel;
+            # a single group (ResNet-50) -> MIOpen, which beats the pixel-split kernel on 7 of the 9 ResNet shapes.
+            one_by_one = R == 1 and S == 1 and pad == 0 and stride == 1
+            if G > 1 and one_by_one:  # dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
                 dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
+            elif (G > 1 or WGRAD_HIP_SINGLE_GROUP) and C % 8 == 0 and K % 8 == 0:
+                # hand-written weight gradient (fp32 out, PyTorch layout), split over output pixels when the
+                # (tap, k, group) tiles alone cannot fill the chip (deterministic split sum)
+                dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
             else:
                 dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
                                                  groups=G).to(wdt)

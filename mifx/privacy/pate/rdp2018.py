@@ -53,29 +53,43 @@ def rdp_data_independent_gaussian(sigma: float, orders):
 
 
 def rdp_gaussian(logq: float, sigma: float, orders):
-    """Data-dependent RDP of GNMax given logq (Theorem 6); falls back to the data-independent bound."""
+    """Data-dependent RDP of GNMax (Papernot et al. 2018, Theorem 6), the data-independent lambda / sigma^2
+    wherever the theorem gives nothing better.
+
+    Derivation used here. GNMax with noise N(0, sigma^2) is (lambda, lambda / sigma^2)-RDP for every order. Let
+    q >= Pr[GNMax(D) != the plurality class] (logq = ln q, Proposition 7). Theorem 6 picks two higher orders
+    mu1 = mu2 + 1 > lambda with eps_i = mu_i / sigma^2 and bounds, for lambda < mu1,
+
+        RDP(lambda) <= 1 / (lambda - 1) * ln[(1 - q) A^(lambda - 1) + q B^(lambda - 1)],
+        A = (1 - q) / (1 - (q e^eps2)^((mu2 - 1) / mu2)),      B = e^eps1 / q^(1 / (mu1 - 1)),
+
+    valid when q <= e^((mu2 - 1) eps2) / [(mu1 / (mu1 - 1)) (mu2 / (mu2 - 1))]^mu2 and q e^eps2 < 1. The free
+    parameter mu2 is set to sqrt(sigma^2 ln(1/q)) (the choice that minimises the bound to first order). Everything
+    is evaluated in log space (q can be ~1e-300), and the minimum with the data-independent bound is taken."""
     if logq > 0 or sigma < 0 or np.any(np.asarray(orders) <= 1):
         raise ValueError("Inputs are malformed.")
-    scalar = np.isscalar(orders)
-    if np.isneginf(logq):
-        return 0.0 if scalar else np.zeros(len(np.atleast_1d(orders)))
-    var = sigma ** 2
-    mu2 = math.sqrt(var * -logq)
-    mu1 = mu2 + 1
-    ov = np.atleast_1d(np.asarray(orders, dtype=np.float64))
-    ret = ov / var
-    mask = np.logical_and(mu1 > ov, mu2 > 1)
-    eps1, eps2 = mu1 / var, mu2 / var
-    log_a2 = (mu2 - 1) * eps2
-    if (np.any(mask) and logq <= log_a2 - mu2 * (math.log(1 + 1 / (mu1 - 1)) + math.log(1 + 1 / (mu2 - 1)))
-            and -logq > eps2):
-        log1q = log1mexp(logq)
-        log_a = (ov - 1) * (log1q - log1mexp((logq + eps2) * (1 - 1 / mu2)))
-        log_b = (ov - 1) * (eps1 - logq / (mu1 - 1))
-        log_s = np.logaddexp(log1q + log_a, logq + log_b)
-        ret[mask] = np.minimum(ret, log_s / (ov - 1))[mask]
-    assert np.all(ret >= 0)
-    return float(ret[0]) if scalar else ret
+    lam = np.atleast_1d(np.asarray(orders, dtype=np.float64))
+    data_ind = lam / sigma ** 2
+    if np.isneginf(logq):  # q = 0: the answer never changes
+        out = np.zeros_like(lam)
+        return float(out[0]) if np.isscalar(orders) else out
+    mu2 = math.sqrt(sigma ** 2 * -logq)
+    mu1 = mu2 + 1.0
+    eps1, eps2 = mu1 / sigma ** 2, mu2 / sigma ** 2
+    applicable = (lam < mu1) & (mu2 > 1)
+    # the theorem's conditions on q, in log form: ln q <= (mu2 - 1) eps2 - mu2 ln[(mu1/(mu1-1)) (mu2/(mu2-1))]
+    # and ln q + eps2 < 0
+    q_small_enough = logq <= (mu2 - 1) * eps2 - mu2 * (math.log(mu1 / (mu1 - 1)) + math.log(mu2 / (mu2 - 1)))
+    bound = data_ind.copy()
+    if applicable.any() and q_small_enough and logq + eps2 < 0:
+        log_1mq = log1mexp(logq)                                        # ln(1 - q)
+        log_A = log_1mq - log1mexp((logq + eps2) * (mu2 - 1) / mu2)     # ln A
+        log_B = eps1 - logq / (mu1 - 1)                                  # ln B
+        log_mix = np.logaddexp(log_1mq + (lam - 1) * log_A, logq + (lam - 1) * log_B)
+        dep = log_mix / (lam - 1)
+        bound = np.where(applicable, np.minimum(data_ind, dep), data_ind)
+    assert np.all(bound >= 0)
+    return float(bound[0]) if np.isscalar(orders) else bound
 
 
 def is_data_independent_always_opt_gaussian(num_teachers: int, num_classes: int, sigma: float, orders):

@@ -527,3 +527,33 @@ def test_mnist_fused_mean_grads_match_autograd():
     for g, p in zip(got, m.parameters()):
         s = p.grad.abs().max().clamp_min(1e-8)
         torch.testing.assert_close(g / s, p.grad / s, rtol=0, atol=2e-5)
+
+
+def test_rdp_gaussian_theorem6_direct_evaluation():
+    """Own goldens for the GNMax data-dependent bound (Theorem 6): at moderate q the log-space implementation must
+    equal the theorem's formula evaluated directly, stay below the data-independent lambda / sigma^2, and grow
+    with q."""
+    import math
+
+    import numpy as np
+
+    from mifx.privacy.pate import rdp2018 as core
+
+    sigma = 40.0
+    lam = np.array([2.0, 5.0, 10.0, 20.0])
+    prev = None
+    for q in (1e-6, 1e-5, 1e-4):
+        got = core.rdp_gaussian(math.log(q), sigma, lam)
+        mu2 = math.sqrt(sigma ** 2 * math.log(1 / q))
+        mu1 = mu2 + 1
+        e1, e2 = mu1 / sigma ** 2, mu2 / sigma ** 2
+        A = (1 - q) / (1 - (q * math.exp(e2)) ** ((mu2 - 1) / mu2))
+        B = math.exp(e1) / q ** (1 / (mu1 - 1))
+        direct = np.log((1 - q) * A ** (lam - 1) + q * B ** (lam - 1)) / (lam - 1)
+        want = np.where(lam < mu1, np.minimum(lam / sigma ** 2, direct), lam / sigma ** 2)
+        np.testing.assert_allclose(got, want, rtol=1e-8, atol=1e-15)
+        assert np.all(got <= lam / sigma ** 2 + 1e-15)
+        if prev is not None:
+            assert np.all(got >= prev - 1e-15)
+        prev = got
+    assert core.rdp_gaussian(-math.inf, sigma, 7.0) == 0.0
