@@ -367,6 +367,7 @@ struct TailArgs {
   long long* step_slots;         // STEP_SLOTS per-workgroup optimizer step slots (slot 0 = the data offset step)
   OptHyper hd, hw;
   long long* dbg;                // optional [grid][8] real-time stamps (tools/tail_stamps.py); null = off
+  int nsteps;                    // PERSIST: training steps per launch
 };
 #define TSTAMP(i)                                                                      \
   do {                                                                                 \
@@ -407,7 +408,67 @@ __device__ __forceinline__ bool grid_sync(unsigned long long* bar, int* err, int
   return *s_flag != 0;
 }
 
-template <bool TRAIN, int TBN, bool TAIL>
+// ---- persistent small-batch training (PERSIST = true): ONE workgroup runs `nsteps` whole training steps of a
+// batch <= T in one launch. Its dW tiles are the whole gradient (no slab, no reduction): right after a layer's dW
+// phase every lane applies the optimizer to the columns its accumulators hold (column ct * 256 + 64 e + lane of
+// the compact layout) and writes the new bf16 weight straight into the LDS weight image -- that layer's weights are
+// not read again in the step (its activation gradient ran before the dW barrier). The wide weights stay in LDS as
+// fp32 and are updated from the LDS histogram at the end of the step. The weight image is staged once per launch;
+// the fp32 master weights / optimizer state stay in global memory (L2-resident, each column read and written by
+// the one lane that owns it). Bit-identical to the slab path with grid 1 (same fp32 gradient, same update).
+constexpr int LDS_BYTES_P = LDS_BYTES + WIDE_PAD * 4;
+static_assert(LDS_BYTES_P <= 163840, "LDS budget (persistent)");
+
+// The optimizer over the lane's own dW columns (column ct[i] * 256 + 64 e + lane of the compact layout, which
+// this lane stored to the slab row earlier in the step -- same lane, same addresses, so program order suffices):
+// the 4-column tiles are processed GS at a time with their loads batched. Run at the end of the step, where no
+// accumulators are live (applying each layer's update right after its dW phase instead spills the kernel).
+template <int NT>
+__device__ __forceinline__ void opt_tiles(const int (&ct)[NT], int lane, const TailArgs& ta, long long step,
+                                          bool last_step, uint16_t* img, const float* slab_row) {
+  constexpr int GS = 3;  // 4+ spills the persistent kernel (tiles of 4 columns x 5 loads each)
+  const bool s1_live = ta.hd.kind >= 2;
+#pragma unroll
+  for (int i0 = 0; i0 < NT; i0 += GS) {
+    int wo[GS][4];
+    float p[GS][4], a0[GS][4], a1[GS][4], g[GS][4];
+#pragma unroll
+    for (int j = 0; j < GS; ++j) {
+      const int i = i0 + j;
+      if (i >= NT || ct[i] < 0) continue;
+      const unsigned g0 = (unsigned)ct[i] * 256u + (unsigned)lane;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned gi = g0 + 64u * e;
+        wo[j][e] = ta.wsc[gi];
+        p[j][e] = ta.param[gi];
+        a0[j][e] = ta.s0[gi];
+        a1[j][e] = s1_live ? ta.s1[gi] : 0.f;
+        g[j][e] = slab_row[gi];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GS; ++j) {
+      const int i = i0 + j;
+      if (i >= NT || ct[i] < 0) continue;
+      const unsigned g0 = (unsigned)ct[i] * 256u + (unsigned)lane;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (wo[j][e] < 0) continue;  // padding column
+        const unsigned gi = g0 + 64u * e;
+        const float w = opt_update(ta.hd, p[j][e], g[j][e], a0[j][e], a1[j][e], step);
+        ta.param[gi] = w;
+        ta.s0[gi] = a0[j][e];
+        if (s1_live) ta.s1[gi] = a1[j][e];
+        const uint16_t wb = __builtin_bit_cast(uint16_t, (bf16)w);
+        img[wo[j][e]] = wb;
+        if (last_step) ta.wt_out[wo[j][e]] = wb;
+      }
+    }
+  }
+}
+
+template <bool TRAIN, int TBN, bool TAIL, bool PERSIST = false>
 __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint4* __restrict__ data, long long n_data, long long batch,
                                                      long long start_fixed, const long long* __restrict__ step_ctr,
                                                      const uint4* __restrict__ wimg, const float* __restrict__ wide,
@@ -448,11 +509,18 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  float* wlds = red + 64;  // PERSIST: the fp32 wide weights [WIDE_PAD], resident for the launch
   if (TRAIN)
     for (int c = tid; c < WIDE_PAD; c += NTHR) wgrad[c] = 0.f;
+  if constexpr (PERSIST)
+    for (int c = tid; c < WIDE_PAD; c += NTHR) wlds[c] = wide[c];
   __syncthreads();
 
-  const long long start = step_ctr ? (step_ctr[0] * batch) % n_data : start_fixed;
+  const long long step0 = step_ctr ? step_ctr[0] : 0;
+  constexpr bool kPersist = PERSIST;
+  const int nsteps = kPersist ? ta.nsteps : 1;
+  for (int ps = 0; ps < nsteps; ++ps) {
+  const long long start = step_ctr ? ((step0 + ps) * batch) % n_data : start_fixed;
   const int niters = (int)((batch + T - 1) / T);
   const int my_iters = (niters - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   const float qbound = fmaxf(fabsf(grad_scale) * (float)(max(my_iters, 1) * T), 1e-30f);
@@ -507,20 +575,29 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 
   STAMP(1);
   BSTAMP(1);
-  for (int it = blockIdx.x; it < niters; it += gridDim.x) {
+  // PERSIST (grid 1, batch <= T): exactly one iteration, known at compile time, so the dW accumulators die at
+  // their layer's emission instead of living across a loop back-edge
+  const int it_end = PERSIST ? 1 : niters, it_inc = PERSIST ? 1 : (int)gridDim.x;
+  for (int it = PERSIST ? 0 : (int)blockIdx.x; it < it_end; it += it_inc) {
 #ifdef WDC_STAMPS
     stamp_on = niters > (int)gridDim.x ? it == (int)(blockIdx.x + gridDim.x) : it == (int)blockIdx.x;
 #endif
     STAMP(2);
-    const bool last = it + (int)gridDim.x >= niters;  // this workgroup's final iteration: dW tiles are final
+    const bool last = PERSIST || it + (int)gridDim.x >= niters;  // this workgroup's final iteration: dW final
     float* my_slab = TRAIN ? slab + (size_t)blockIdx.x * stride : nullptr;
+    const long long pstep = step0 + ps + 1;  // PERSIST: the optimizer step (Adam bias correction)
+    const bool plast = ps + 1 == nsteps;
+#define WDC_EMIT(NT, ACC, CT)                          \
+  do {                                                 \
+    if (last) store_tiles<NT>(my_slab, ACC, CT, lane); \
+  } while (0)
     uint4 u[TBN][2];
 #pragma unroll
     for (int tb = 0; tb < TBN; ++tb) {
       u[tb][0] = nu[tb][0];
       u[tb][1] = nu[tb][1];
     }
-    fetch(it + gridDim.x, nu);  // next iteration's records
+    if constexpr (!PERSIST) fetch(it + gridDim.x, nu);  // next iteration's records
 
     // wide gather for the lane's column block (issued before the forward: its latency hides under MFMAs)
     const uint4 m0 = mtb ? u[TBN - 1][0] : u[0][0], m1 = mtb ? u[TBN - 1][1] : u[0][1];
@@ -532,9 +609,9 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       int id = (f & 1) ? (idw[f >> 1] >> 16) : (idw[f >> 1] & 0xffff);
       id = id < kWideNb[f] ? id : 0;
       ids[f] = kWideOff[f] + id;
-      wv[f] = wide[ids[f]];
+      wv[f] = PERSIST ? wlds[ids[f]] : wide[ids[f]];
     }
-    const float wbias = wide[WIDE_BIAS];
+    const float wbias = PERSIST ? wlds[WIDE_BIAS] : wide[WIDE_BIAS];
 
     // ---- forward, in registers
     v8bf a0[TBN][1];
@@ -642,7 +719,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(6);
     if (l5) dw_phase<K5, N5, 1, 1>(acc5, S, 0, 0, w & 3, 0, r, h);
-    if (last) store_tiles<1>(my_slab, acc5, ct5, lane);
+    WDC_EMIT(1, acc5, ct5);
     block_sync_lds();
 
     // ---- layer 4
@@ -659,7 +736,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(8);
     dw_phase<K4, N4, 1, O4K>(acc4, S, n4, 0, k4, 1, r, h);
-    if (last) store_tiles<O4K>(my_slab, acc4, ct4, lane);
+    WDC_EMIT(O4K, acc4, ct4);
     block_sync_lds();
 
     // ---- layer 3
@@ -676,7 +753,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(10);
     dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
-    if (last) store_tiles<O3K>(my_slab, acc3, ct3, lane);
+    WDC_EMIT(O3K, acc3, ct3);
     block_sync_lds();
 
     // ---- layer 2
@@ -693,7 +770,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(12);
     dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
-    if (last) store_tiles<O2N * O2K>(my_slab, acc2, ct2, lane);
+    WDC_EMIT(O2N * O2K, acc2, ct2);
     block_sync_lds();
 
     // ---- layer 1
@@ -702,7 +779,21 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     block_sync_lds();
     STAMP(14);
     dw_phase<K1, N1, O1N, 1>(acc1, S, n1, 1, 0, 0, r, h);
-    if (last) store_tiles<O1N>(my_slab, acc1, ct1, lane);
+    WDC_EMIT(O1N, acc1, ct1);
+    if constexpr (PERSIST) {  // the whole DNN update of this lane's columns (see opt_tiles)
+      constexpr int NA = O1N + O2N * O2K + O3K + O4K + 1;
+      int cta[NA];
+#pragma unroll
+      for (int i = 0; i < O1N; ++i) cta[i] = ct1[i];
+#pragma unroll
+      for (int i = 0; i < O2N * O2K; ++i) cta[O1N + i] = ct2[i];
+#pragma unroll
+      for (int i = 0; i < O3K; ++i) cta[O1N + O2N * O2K + i] = ct3[i];
+#pragma unroll
+      for (int i = 0; i < O4K; ++i) cta[O1N + O2N * O2K + O3K + i] = ct4[i];
+      cta[NA - 1] = ct5[0];
+      opt_tiles<NA>(cta, lane, ta, pstep, plast, lds, my_slab);
+    }
     STAMP(15);
   }
 #ifdef WDC_STAMPS
@@ -723,7 +814,25 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   // (the dW tiles went out in the last iteration, each right after its layer's dW phase: their stores drain
   // under the remaining layers' compute instead of here)
   __syncthreads();
-  if (TRAIN) {
+  if constexpr (TRAIN && PERSIST) {  // wide weights: optimizer on the histogram gradient, in LDS + master copy
+    const bool s1_live = ta.hw.kind >= 2;
+    const int w0 = stride - WIDE_PAD;
+    for (int c = tid; c < WIDE_PAD; c += NTHR) {
+      float v = (float)wgi[c] * qinv;
+      wgi[c] = 0;  // next step's histogram (read back only after the step-end barrier)
+      if (c == WIDE_BIAS) {
+#pragma unroll
+        for (int i = 0; i < NWAVE; ++i) v += red[NWAVE + i];
+      }
+      if (ta.wsc[w0 + c] == -1) continue;  // padding
+      float a0 = ta.s0[w0 + c], a1 = s1_live ? ta.s1[w0 + c] : 0.f;
+      const float nw = opt_update(ta.hw, wlds[c], v, a0, a1, step0 + ps + 1);
+      wlds[c] = nw;
+      ta.param[w0 + c] = nw;
+      ta.s0[w0 + c] = a0;
+      if (s1_live) ta.s1[w0 + c] = a1;
+    }
+  } else if (TRAIN) {
     float* my = slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD);
     for (int c = tid; c < WIDE_PAD; c += NTHR) {
       float v = (float)wgi[c] * qinv;
@@ -739,6 +848,18 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 #pragma unroll
     for (int i = 0; i < NWAVE; ++i) l += red[i];
     slab_loss[blockIdx.x] = l;
+  }
+  if constexpr (PERSIST) {
+    // the step's LDS weight / wide updates and histogram reset before the next step's forward; the master
+    // state's stores acknowledged and the vector L1 invalidated before the owning lanes read it back
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  }  // step loop
+  if constexpr (PERSIST) {
+    for (int i = tid; i < STEP_SLOTS; i += NTHR) ta.step_slots[i] = step0 + nsteps;
   }
   STAMP(17);
   BSTAMP(2);
@@ -848,17 +969,18 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   }
 }
 
-template <bool TRAIN, int TBN, bool TAIL = false>
+template <bool TRAIN, int TBN, bool TAIL = false, bool PERSIST = false>
 void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
             const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
             float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of, TailArgs ta = TailArgs{}) {
+  constexpr int lds_bytes = PERSIST ? LDS_BYTES_P : LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wdc_fused<TRAIN, TBN, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)wdc_fused<TRAIN, TBN, TAIL, PERSIST>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
     attr_done = true;
   }
-  hipLaunchKernelGGL((wdc_fused<TRAIN, TBN, TAIL>), grid, dim3(64 * (T / (16 * TBN))), LDS_BYTES, stream,
+  hipLaunchKernelGGL((wdc_fused<TRAIN, TBN, TAIL, PERSIST>), grid, dim3(64 * (T / (16 * TBN))), lds_bytes, stream,
                      (const uint4*)data, n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab,
                      slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta);
 }
@@ -948,6 +1070,36 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
                    hyper_wide[6], hyper_wide[7]};
   launch<true, 1, true>(dim3(grid), stream, data, n_data, batch, 0, step_ctr, wimg, wide, slab, slab_loss, nullptr,
                         grad_scale, tmap, stride, xcd_of, ta);
+  return (int)hipGetLastError();
+}
+
+// Persistent small-batch training (see opt_tiles): `nsteps` whole training steps of a batch <= T in ONE launch of
+// one 8-wave workgroup -- forward, backward, Adagrad/FTRL/Adam/SGD update of every weight, step counter advance.
+// State in slab-column order as mifx_wdc_fused_tail (wsc / param / s0 / s1, STEP_SLOTS step slots; wimg is the
+// global bf16 image, rewritten at the last step). Bit-identical to nsteps grid-1 slab steps + wd_reduce_opt_sc.
+int mifx_wdc_persist(const void* data, long long n_data, long long batch, long long* step_ctr, void* wimg,
+                     float* wide, float* slab, float* slab_loss, float grad_scale, const int* tmap, int stride, const int* wsc,
+                     float* param, float* s0, float* s1, const float* hyper_dnn, const float* hyper_wide, int nsteps,
+                     hipStream_t stream) {
+  if (nsteps <= 0 || n_data <= 0 || batch <= 0 || batch > T || batch > n_data) return -1;
+  if (wimg == nullptr || wide == nullptr || tmap == nullptr || wsc == nullptr || param == nullptr || s0 == nullptr ||
+      s1 == nullptr || step_ctr == nullptr || hyper_dnn == nullptr || hyper_wide == nullptr || slab == nullptr)
+    return -1;
+  if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0 || stride < WIDE_PAD || stride % 4 != 0) return -1;
+  TailArgs ta{};
+  ta.wsc = wsc;
+  ta.param = param;
+  ta.s0 = s0;
+  ta.s1 = s1;
+  ta.wt_out = (uint16_t*)wimg;
+  ta.step_slots = step_ctr;
+  ta.nsteps = nsteps;
+  ta.hd = OptHyper{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                   hyper_dnn[6], hyper_dnn[7]};
+  ta.hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                   hyper_wide[6], hyper_wide[7]};
+  launch<true, 1, false, true>(dim3(1), stream, data, n_data, batch, 0, step_ctr, wimg, wide, slab, slab_loss,
+                               nullptr, grad_scale, tmap, stride, nullptr, ta);
   return (int)hipGetLastError();
 }
 

@@ -25,15 +25,17 @@ MODULE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "taxi_mod
 def create_pipeline(pipeline_name: str, pipeline_root: str, data_root: str, serving_model_dir: str,
                     train_steps: int = 10000, eval_steps: int = 5000, enable_cache: bool = True,
                     metadata_db_root: str | None = None, batch_size: int = 40, log_root: str | None = None,
-                    num_gpus: int = 1) -> Pipeline:
-    """num_gpus > 1: the Trainer runs data-parallel, one rank per GPU, batch_size examples per rank per step."""
+                    num_gpus: int = 1, transform_workers: int = 0) -> Pipeline:
+    """num_gpus > 1: the Trainer runs data-parallel, one rank per GPU, batch_size examples per rank per step.
+    transform_workers > 1: Transform analyzes and transforms sharded over that many worker processes (the
+    reference's Beam DirectRunner workers; mifx.transform.parallel)."""
     examples = csv_input(data_root)
     example_gen = CsvExampleGen(input_base=examples)
     statistics_gen = StatisticsGen(input_data=example_gen.outputs.examples)
     infer_schema = SchemaGen(stats=statistics_gen.outputs.output)
     validate_stats = ExampleValidator(stats=statistics_gen.outputs.output, schema=infer_schema.outputs.output)
     transform = Transform(input_data=example_gen.outputs.examples, schema=infer_schema.outputs.output,
-                          module_file=MODULE_FILE)
+                          module_file=MODULE_FILE, num_workers=transform_workers)
     trainer = Trainer(module_file=MODULE_FILE, transformed_examples=transform.outputs.transformed_examples,
                       schema=infer_schema.outputs.output, transform_output=transform.outputs.transform_output,
                       train_args=TrainArgs(num_steps=train_steps), eval_args=EvalArgs(num_steps=eval_steps),
@@ -61,10 +63,11 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=40)
     ap.add_argument("--parallel", type=int, default=2)
     ap.add_argument("--num-gpus", type=int, default=1, help="data-parallel Trainer ranks (one per GPU)")
+    ap.add_argument("--transform-workers", type=int, default=0, help="sharded Transform worker processes")
     a = ap.parse_args(argv)
     p = create_pipeline("taxi", os.path.join(a.root, "pipelines"), a.data, os.path.join(a.root, "serving_model", "taxi"),
                         a.train_steps, a.eval_steps, metadata_db_root=os.path.join(a.root, "metadata"),
-                        batch_size=a.batch_size, num_gpus=a.num_gpus)
+                        batch_size=a.batch_size, num_gpus=a.num_gpus, transform_workers=a.transform_workers)
     res = LocalDagRunner(max_parallel=a.parallel).run(p)
     for cid, r in res.components.items():
         print(f"{cid:>20}: {r.state:9s} exec={r.execution_id} {r.seconds:.2f}s")

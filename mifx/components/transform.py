@@ -52,7 +52,7 @@ def outputs_to_table(cols: dict) -> pa.Table:
 
 class TransformSpec(ComponentSpec):
     PARAMETERS = {"module_file": ExecutionParameter(), "preprocessing_fn_name": ExecutionParameter(
-        optional=True, default="preprocessing_fn")}
+        optional=True, default="preprocessing_fn"), "num_workers": ExecutionParameter(optional=True, default=0)}
     INPUTS = {"input_data": ChannelParameter(A.EXAMPLES), "schema": ChannelParameter(A.SCHEMA)}
     OUTPUTS = {"transform_output": ChannelParameter(A.TRANSFORM),
                "transformed_examples": ChannelParameter(A.EXAMPLES)}
@@ -69,13 +69,13 @@ class TransformExecutor(BaseExecutor):
         dev = self.context.device
         gpu = dev is not None and str(dev).startswith("cuda")
         table = dataset.read_split(train.uri)
-        try:
-            cols, state = mt.analyze(fn, table_to_inputs(table, arrow_strings=gpu), device=dev)
-        except (TypeError, AttributeError, ValueError):
-            if not gpu:
-                raise
-            # user code that needs numpy string columns: same analysis on the numpy form
-            cols, state = mt.analyze(fn, table_to_inputs(table), device=dev)
+        workers = int(exec_properties.get("num_workers") or 0)
+        if workers > 1:  # Beam-style: shards on worker processes, merged accumulators (mifx.transform.parallel)
+            from ..transform import parallel as tpar
+
+            cols, state = tpar.analyze_sharded(fn, table_to_inputs(table), num_workers=workers)
+        else:
+            cols, state = self._analyze_local(fn, table, dev, gpu)
         t_stats = dv.generate_statistics_from_table(outputs_to_table(cols), name="train")
         t_schema = dv.infer_schema(t_stats)
         out = output_dict["transform_output"][0]
@@ -83,10 +83,24 @@ class TransformExecutor(BaseExecutor):
         for art in output_dict["transformed_examples"]:
             if art.split == train.split:
                 res = cols
+            elif workers > 1:
+                res = tpar.transform_sharded(fn, table_to_inputs(dataset.read_split(splits[art.split].uri)), state,
+                                             num_workers=workers)
             else:
                 res = mt.apply(fn, table_to_inputs(dataset.read_split(splits[art.split].uri)), state, device=dev)
             dataset.write_split(art.uri, outputs_to_table(res))
             art.custom_properties["num_examples"] = int(len(next(iter(res.values()))))
+
+    @staticmethod
+    def _analyze_local(fn, table, dev, gpu):
+        try:
+            cols, state = mt.analyze(fn, table_to_inputs(table, arrow_strings=gpu), device=dev)
+        except (TypeError, AttributeError, ValueError):
+            if not gpu:
+                raise
+            # user code that needs numpy string columns: same analysis on the numpy form
+            cols, state = mt.analyze(fn, table_to_inputs(table), device=dev)
+        return cols, state
 
 
 class Transform(BaseComponent):
@@ -95,9 +109,12 @@ class Transform(BaseComponent):
     EXECUTION_TYPE = "transform"
 
     def __init__(self, input_data, schema, module_file: str, preprocessing_fn_name: str = "preprocessing_fn",
-                 name: str | None = None, transform_output=None, transformed_examples=None):
+                 name: str | None = None, transform_output=None, transformed_examples=None, num_workers: int = 0):
+        """num_workers > 1: analyze + transform sharded over that many worker processes (the reference's Beam
+        DirectRunner with `--direct_num_workers`; mifx.transform.parallel)."""
         super().__init__(TransformSpec(input_data=input_data, schema=schema, module_file=os.path.abspath(module_file),
-                                       preprocessing_fn_name=preprocessing_fn_name, transform_output=transform_output,
+                                       preprocessing_fn_name=preprocessing_fn_name, num_workers=int(num_workers),
+                                       transform_output=transform_output,
                                        transformed_examples=transformed_examples), name=name)
 
     def output_splits(self, key, input_dict):

@@ -21,6 +21,8 @@ def _fns():
                                                  I32, VP, VP]),
         "fused_tail": sig(lib, "mifx_wdc_fused_tail", [VP, I64, I64, VP, VP, VP, VP, VP, F32, I32, VP, I32, VP, VP, VP,
                                                        VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "persist": sig(lib, "mifx_wdc_persist", [VP, I64, I64, VP, VP, VP, VP, VP, F32, VP, I32, VP, VP, VP, VP, VP, VP,
+                                                 I32, VP]),
     }
 
 
@@ -98,3 +100,19 @@ class InKernelTail:
         if int(self.err.item()) != 0:
             raise RuntimeError("W&D in-kernel tail: a grid barrier timed out (workgroups not co-resident); the "
                                "step skipped its update")
+
+
+def persist_steps(tr, nsteps: int) -> None:
+    """`nsteps` training steps of FusedWideDeepTrainer `tr` (chained kernel, one rank, batch <= T) in ONE launch of
+    the persistent single-workgroup kernel (csrc/wd_chain.hip opt_tiles / mifx_wdc_persist): the weight image stays
+    in LDS across the steps and the optimizer runs inside the workgroup."""
+    c = constants()
+    if tr.wt.numel() != c["LWEND"] or tr.tmap.numel() != c["NTILE"]:
+        raise ValueError("trainer buffers do not match the chained kernel")
+    if tr.batch > c["T"] or nsteps <= 0:
+        raise ValueError(f"persistent step: batch <= {c['T']} and nsteps >= 1")
+    rc = _fns()["persist"](ptr(tr.records), tr.n_data, tr.batch, ptr(tr.step_ctr), ptr(tr.wt), ptr(tr.wide_weights),
+                           ptr(tr.slab), ptr(tr.slab_loss), float(tr.grad_scale), ptr(tr.tmap), int(tr.stride), ptr(tr.wsc),
+                           ptr(tr.param_sc), ptr(tr.s0_sc), ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide),
+                           int(nsteps), stream_handle(tr.records.device))
+    check(rc, "mifx_wdc_persist")

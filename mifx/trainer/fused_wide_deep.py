@@ -61,7 +61,7 @@ class FusedWideDeepTrainer:
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
                  live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8,
-                 in_kernel_tail: bool | None = None):
+                 in_kernel_tail: bool | None = None, persistent: bool | None = None):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
@@ -157,6 +157,13 @@ class FusedWideDeepTrainer:
             from ..ops import wd_chain as wdc
 
             self._ktail = wdc.InKernelTail(self.stride, dev)
+        # persistent (default for one rank and batch <= T, or MIFX_WD_PERSIST=0 to disable): run(n) is ONE launch
+        # of one workgroup doing n whole steps -- the weight image stays in LDS across them and the optimizer runs
+        # in the workgroup (csrc/wd_chain.hip opt_tiles / mifx_wdc_persist); bit-identical to the slab path.
+        if persistent is None:
+            persistent = os.environ.get("MIFX_WD_PERSIST", "1") != "0"
+        self._persist = bool(persistent and self._sc and self.world == 1 and self.grid == 1 and self.batch <= self.T
+                             and self.waves == 8 and self._ktail is None and self.device.type == "cuda")
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
         self.partial = torch.empty(self.nsplit, self.stride, device=dev)
@@ -342,6 +349,11 @@ class FusedWideDeepTrainer:
             raise RuntimeError("W&D optimizer launch failed")
 
     def _step_impl(self) -> None:
+        if self._persist:
+            from ..ops import wd_chain as wdc
+
+            wdc.persist_steps(self, 1)
+            return
         if self._ktail is not None:  # one launch: fwd/bwd + slab reduction + optimizer
             self._ktail.step(self)
             return
@@ -427,6 +439,14 @@ class FusedWideDeepTrainer:
         step advance through the device-side step counter), the host just launches once per S steps. Replaying
         one graph per step left ~8.7 us of idle GPU between steps on MI355X (the host-side launch of a replay
         costs more than the step's ~35 us of GPU work): tools/timeline.py, profiles/wd_step_timeline_r2.txt."""
+        if self._persist:  # all n steps in one launch of the persistent kernel
+            if n > 0:
+                if self.records is None:
+                    raise RuntimeError("call set_data() first")
+                from ..ops import wd_chain as wdc
+
+                wdc.persist_steps(self, n)
+            return
         if self.graph_multi is not None and n >= self.graph_multi_steps:
             reps, n = divmod(n, self.graph_multi_steps)
             for _ in range(reps):
@@ -463,7 +483,7 @@ class FusedWideDeepTrainer:
             with torch.cuda.graph(g):
                 self._step_impl()
             self.graph = g
-            if steps_per_graph > 1:  # S consecutive steps in one graph (see run())
+            if steps_per_graph > 1 and not self._persist:  # S consecutive steps in one graph (see run())
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm):
                     for _ in range(steps_per_graph):

@@ -67,8 +67,27 @@ def _phase(mode: str, state: TransformState, device=None):
         _LOCAL.ctx = prev
 
 
-def _analyzer(kind: str, params: dict, compute):
+class ShardStop(Exception):
+    """Raised in the SHARD phase (mifx.transform.parallel) at the analyzer being accumulated: carries its kind,
+    parameters and this shard's input to it; the rest of preprocessing_fn is not run."""
+
+    def __init__(self, kind: str, params: dict, data):
+        super().__init__(kind)
+        self.kind, self.params, self.data = kind, params, data
+
+
+def _analyzer(kind: str, params: dict, compute, data=None):
+    """One full-pass analyzer call. `data`: its input (the column; the row count for size), which the sharded
+    analyze (mifx.transform.parallel) accumulates per shard and merges instead of calling `compute`."""
     c = _ctx()
+    if c.mode == "shard":  # analyzers before the target replay their merged values; the target stops the fn
+        if c.cursor < len(c.state.entries):
+            e = c.state.entries[c.cursor]
+            c.cursor += 1
+            if e["kind"] != kind:
+                raise RuntimeError(f"analyzer order changed: recorded {e['kind']}, now {kind}")
+            return e["values"]
+        raise ShardStop(kind, params, data)
     if c.mode == "analyze":
         values = compute()
         c.state.entries.append({"kind": kind, "params": params, "values": values})
@@ -211,32 +230,32 @@ def _moments(a: np.ndarray) -> dict:
 # ------------------------------------------------------------------------------ analyzers
 def mean(x) -> float:
     a = _num(x)
-    return _analyzer("moments", {}, lambda: _moments(a))["mean"]
+    return _analyzer("moments", {}, lambda: _moments(a), a)["mean"]
 
 
 def var(x) -> float:
     a = _num(x)
-    return _analyzer("moments", {}, lambda: _moments(a))["var"]
+    return _analyzer("moments", {}, lambda: _moments(a), a)["var"]
 
 
 def min(x) -> float:  # noqa: A001
     a = _num(x)
-    return _analyzer("moments", {}, lambda: _moments(a))["min"]
+    return _analyzer("moments", {}, lambda: _moments(a), a)["min"]
 
 
 def max(x) -> float:  # noqa: A001
     a = _num(x)
-    return _analyzer("moments", {}, lambda: _moments(a))["max"]
+    return _analyzer("moments", {}, lambda: _moments(a), a)["max"]
 
 
 def size(x) -> int:
     n = len(x) if _is_arrow(x) else int(np.asarray(x).size)
-    return _analyzer("size", {}, lambda: n)
+    return _analyzer("size", {}, lambda: n, n)
 
 
 def sum(x) -> float:  # noqa: A001
     a = _num(x)
-    return _analyzer("sum", {}, lambda: float(a.sum()))
+    return _analyzer("sum", {}, lambda: float(a.sum()), a)
 
 
 def quantiles(x, num_buckets: int) -> list[float]:
@@ -259,7 +278,7 @@ def quantiles(x, num_buckets: int) -> list[float]:
             qs = np.quantile(a[~np.isnan(a)], q, method="higher")
         return sorted(set(float(v) for v in qs))
 
-    return _analyzer("quantiles", {"num_buckets": num_buckets}, compute)
+    return _analyzer("quantiles", {"num_buckets": num_buckets}, compute, a)
 
 
 def vocabulary(x, top_k: int | None = None, frequency_threshold: int | None = None,
@@ -282,20 +301,21 @@ def vocabulary(x, top_k: int | None = None, frequency_threshold: int | None = No
             order = order[:top_k]
         return [v for _, v in order]
 
-    return _analyzer("vocabulary", {"top_k": top_k, "vocab_filename": vocab_filename}, compute)
+    return _analyzer("vocabulary", {"top_k": top_k, "frequency_threshold": frequency_threshold,
+                                    "vocab_filename": vocab_filename}, compute, s)
 
 
 # -------------------------------------------------------------------------------- mappers
 def scale_to_z_score(x) -> np.ndarray:
     a = _num(x)
-    m = _analyzer("moments", {}, lambda: _moments(a))
+    m = _analyzer("moments", {}, lambda: _moments(a), a)
     sd = np.sqrt(m["var"])
     return (a - m["mean"]) / sd if sd > 0 else a - m["mean"]
 
 
 def scale_to_0_1(x) -> np.ndarray:
     a = _num(x)
-    m = _analyzer("moments", {}, lambda: _moments(a))
+    m = _analyzer("moments", {}, lambda: _moments(a), a)
     rng = m["max"] - m["min"]
     return (a - m["min"]) / rng if rng > 0 else np.full_like(a, 0.5)
 

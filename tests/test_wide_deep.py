@@ -489,3 +489,43 @@ def test_in_kernel_tail_is_run_to_run_deterministic_and_image_consistent():
         # the bf16 weight image the kernel re-emitted == the image built from its own fp32 master weights
         assert torch.equal(tr.wt, tr._weight_image())
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,opt", [(40, "adagrad_ftrl"), (128, "adagrad_ftrl"), (1, "adagrad_ftrl"),
+                                       (40, "adam"), (77, "sgd"), (40, "ftrl")])
+def test_persistent_small_batch_matches_slab_path(batch, opt):
+    """The persistent single-workgroup kernel (n whole steps in one launch, weight image resident in LDS, optimizer
+    in the workgroup) against the grid-1 slab path (fused kernel + reduce/optimizer kernel per step): the same fp32
+    gradient and update, so parameters, optimizer state, the bf16 image and the loss must be BIT-identical. The data
+    (300 records) wraps around several times over the 23 steps; run(n) split 1 + 20 + 2 checks the step counter
+    carries the data offset and Adam's bias-correction step across launches."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    recs = synthetic_records(300, device="cuda", seed=21)
+    lr = 1e-3 if opt == "adam" else 1e-4 if opt == "sgd" else None
+    kw = {} if opt == "adagrad_ftrl" else {"dnn_opt": OptSpec(opt, lr=lr) if lr else OptSpec(opt, lr=0.05),
+                                             "wide_opt": OptSpec(opt, lr=lr) if lr else OptSpec(opt, lr=0.2)}
+    out = []
+    for persistent in (True, False):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device="cuda", persistent=persistent, **kw)
+        assert tr._persist == persistent
+        tr.set_data(recs)
+        tr.step()
+        tr.run(20)
+        tr.run(2)
+        torch.cuda.synchronize()
+        assert tr.steps_done == 23
+        out.append((tr.param.clone(), tr.s0.clone(), tr.s1.clone(), tr.wt.clone(), tr.last_loss()))
+        if persistent:  # the image the kernel left behind == the image of its own fp32 master weights
+            assert torch.equal(tr.wt, tr._weight_image())
+    if opt == "adam":  # Adam's powf bias corrections: the two kernels' translation units are compiled with
+        # different fp flags and may round powf differently in the last ulp -> tight allclose (a step off by one
+        # would be ~1e-4 relative after 23 steps)
+        for a, b in zip(out[0][:3], out[1][:3]):
+            np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-8)
+        assert out[0][4] == pytest.approx(out[1][4], rel=1e-6)
+        return
+    for a, b in zip(out[0][:4], out[1][:4]):
+        assert torch.equal(a, b)
+    assert np.isfinite(out[0][4]) and out[0][4] == out[1][4]
