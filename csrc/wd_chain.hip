@@ -416,6 +416,9 @@ __device__ __forceinline__ bool grid_sync(unsigned long long* bar, int* err, int
 // fp32 and are updated from the LDS histogram at the end of the step. The weight image is staged once per launch;
 // the fp32 master weights / optimizer state stay in global memory (L2-resident, each column read and written by
 // the one lane that owns it). Bit-identical to the slab path with grid 1 (same fp32 gradient, same update).
+// Measured on MI355X at B=40: 25.6 us/step against 14.8 us for the grid-1 fused kernel + 370-workgroup optimizer
+// launch -- the ~750 KB of per-step optimizer traffic (slab, master weights, accumulators, column map) through one
+// CU's memory path outweighs the staging and launch it saves -- so the trainer keeps it opt-in.
 constexpr int LDS_BYTES_P = LDS_BYTES + WIDE_PAD * 4;
 static_assert(LDS_BYTES_P <= 163840, "LDS budget (persistent)");
 

@@ -15,7 +15,9 @@ from ..ops.pool import max_pool3s2
 
 # MIFX_RESNET_HIP_CONV=1: the block convolutions (1x1 and 3x3, any stride) on the hand-written MFMA implicit-GEMM
 # kernels (csrc/gconv.hip: forward, stride-1 / phase-split strided input gradient, pixel-split weight gradient);
-# 0 (default until the whole-step A/B says otherwise, profiles/resnet_gconv_ab_r3.txt): MIOpen.
+# 0 (default): MIOpen. Whole-step A/B on MI355X, batch 256 (profiles/resnet_gconv_ab_r3b_hybrid.jsonl): HIP forward +
+# HIP strided input gradient + MIOpen single-group weight gradient 27.4-27.6 ms/step vs MIOpen 26.5-27.0 (the
+# forward wins per shape, profiles/gconv_resnet_shapes_r3.jsonl, but not by enough to carry the backward).
 USE_HIP_CONV = os.environ.get("MIFX_RESNET_HIP_CONV", "0") == "1"
 
 

@@ -157,11 +157,14 @@ class FusedWideDeepTrainer:
             from ..ops import wd_chain as wdc
 
             self._ktail = wdc.InKernelTail(self.stride, dev)
-        # persistent (default for one rank and batch <= T, or MIFX_WD_PERSIST=0 to disable): run(n) is ONE launch
-        # of one workgroup doing n whole steps -- the weight image stays in LDS across them and the optimizer runs
-        # in the workgroup (csrc/wd_chain.hip opt_tiles / mifx_wdc_persist); bit-identical to the slab path.
+        # persistent (opt-in: persistent=True or MIFX_WD_PERSIST=1; one rank, batch <= T): run(n) is ONE launch of
+        # one workgroup doing n whole steps -- the weight image stays in LDS across them and the optimizer runs in
+        # the workgroup (csrc/wd_chain.hip opt_tiles / mifx_wdc_persist); bit-identical to the slab path. Measured
+        # SLOWER on MI355X at B=40: 25.6 us/step vs 14.8 us for the two-kernel graph step (profiles/
+        # wd_persist_ab_r3.md): the optimizer's ~750 KB of master-state traffic per step through ONE CU's memory
+        # path costs more than the 370-workgroup optimizer launch plus the weight re-staging it saves.
         if persistent is None:
-            persistent = os.environ.get("MIFX_WD_PERSIST", "1") != "0"
+            persistent = os.environ.get("MIFX_WD_PERSIST", "0") == "1"
         self._persist = bool(persistent and self._sc and self.world == 1 and self.grid == 1 and self.batch <= self.T
                              and self.waves == 8 and self._ktail is None and self.device.type == "cuda")
         self.slab_loss = torch.zeros(self.grid, device=dev)
