@@ -10,6 +10,7 @@ all-reduce), fused residual-add + LayerNorm (HIP), column-parallel FFN-in with f
 (HIP), row-parallel FFN-out (+1 all-reduce), fused residual-add + LayerNorm."""
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -17,8 +18,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import fused_bert as fb
+from ..ops import gemm as hg
 from ..parallel.tensor_parallel import (ColumnParallelLinear, RowParallelLinear, TPGroup, VocabParallelEmbedding,
-                                        copy_to_tp, head_partition, split_sizes)
+                                        copy_to_tp, head_partition, reduce_from_tp, split_sizes)
 
 
 @dataclass
@@ -34,6 +36,9 @@ class BertConfig:
     attn_dropout: float | None = None  # attention-probability dropout (None: same as dropout)
     dropout_seed: int = 1234  # dropout mask seed (identical on every TP rank)
     fused_attention: bool = True  # csrc/attention.hip (False: torch scaled_dot_product_attention)
+    # forward projections on the hand-written MFMA GEMM (csrc/gemm.hip; FFN-in with bias + GELU fused into its
+    # epilogue); None: MIFX_BERT_HIP_GEMM=1 enables it (A/B in profiles/gemm_hip_r3.jsonl)
+    hip_gemm: bool | None = None
     num_labels: int = 2
     ln_eps: float = 1e-12
     init_std: float = 0.02
@@ -88,7 +93,12 @@ class BertLayer(nn.Module):
         c = self.cfg
         drop = c.dropout if self.training else 0.0
         adrop = (c.dropout if c.attn_dropout is None else c.attn_dropout) if self.training else 0.0
-        qkv = self.qkv(x).view(B, S, 3, h, d)
+        hip = c.hip_gemm if c.hip_gemm is not None else os.environ.get("MIFX_BERT_HIP_GEMM", "0") == "1"
+        hip = hip and x.is_cuda
+        if hip:
+            qkv = hg.linear(copy_to_tp(x, self.tp), self.qkv.weight, self.qkv.bias).view(B, S, 3, h, d)
+        else:
+            qkv = self.qkv(x).view(B, S, 3, h, d)
         if c.fused_attention:
             # fused attention straight on the projection output (no q/k/v transposes); its dropout mask is keyed
             # by the GLOBAL head index, so it is identical for any TP split (site: this layer's attention)
@@ -100,11 +110,18 @@ class BertLayer(nn.Module):
             amask = None if mask is None else mask[:, None, None, :].to(q.dtype)
             ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, dropout_p=adrop)
             ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
-        x = fb.bias_dropout_add_layernorm(self.attn_out(ctx, add_bias=False), self.attn_out.bias, x, self.ln1.weight,
-                                          self.ln1.bias, c.ln_eps, drop, rng, site)
-        f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
-        return fb.bias_dropout_add_layernorm(self.ffn_out(f, add_bias=False), self.ffn_out.bias, x, self.ln2.weight,
-                                             self.ln2.bias, c.ln_eps, drop, rng, site + 1)
+        a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) if hip else \
+            self.attn_out(ctx, add_bias=False)
+        x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
+                                          rng, site)
+        if hip:
+            f = hg.linear_bias_gelu(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias)
+            o = reduce_from_tp(hg.linear(f, self.ffn_out.weight), self.tp)
+        else:
+            f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
+            o = self.ffn_out(f, add_bias=False)
+        return fb.bias_dropout_add_layernorm(o, self.ffn_out.bias, x, self.ln2.weight, self.ln2.bias, c.ln_eps, drop,
+                                             rng, site + 1)
 
 
 class BertForSequenceClassification(nn.Module):
