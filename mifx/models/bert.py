@@ -37,7 +37,7 @@ class BertConfig:
     dropout_seed: int = 1234  # dropout mask seed (identical on every TP rank)
     fused_attention: bool = True  # csrc/attention.hip (False: torch scaled_dot_product_attention)
     # forward projections on the hand-written MFMA GEMM (csrc/gemm.hip; FFN-in with bias + GELU fused into its
-    # epilogue); None: MIFX_BERT_HIP_GEMM=1 enables it (A/B in profiles/gemm_hip_r3.jsonl)
+    # epilogue) for the shapes where it measured faster (mifx.ops.gemm.TUNED); None: on unless MIFX_BERT_HIP_GEMM=0
     hip_gemm: bool | None = None
     num_labels: int = 2
     ln_eps: float = 1e-12
@@ -93,9 +93,10 @@ class BertLayer(nn.Module):
         c = self.cfg
         drop = c.dropout if self.training else 0.0
         adrop = (c.dropout if c.attn_dropout is None else c.attn_dropout) if self.training else 0.0
-        hip = c.hip_gemm if c.hip_gemm is not None else os.environ.get("MIFX_BERT_HIP_GEMM", "0") == "1"
+        # hand-written GEMM per projection only where it measured faster than hipBLASLt (mifx.ops.gemm.TUNED)
+        hip = c.hip_gemm if c.hip_gemm is not None else os.environ.get("MIFX_BERT_HIP_GEMM", "1") == "1"
         hip = hip and x.is_cuda
-        if hip:
+        if hip and hg.preferred(x, self.qkv.weight):
             qkv = hg.linear(copy_to_tp(x, self.tp), self.qkv.weight, self.qkv.bias).view(B, S, 3, h, d)
         else:
             qkv = self.qkv(x).view(B, S, 3, h, d)
@@ -110,15 +111,17 @@ class BertLayer(nn.Module):
             amask = None if mask is None else mask[:, None, None, :].to(q.dtype)
             ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, dropout_p=adrop)
             ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
-        a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) if hip else \
-            self.attn_out(ctx, add_bias=False)
+        a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) \
+            if hip and hg.preferred(ctx, self.attn_out.weight) else self.attn_out(ctx, add_bias=False)
         x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
                                           rng, site)
-        if hip:
+        if hip and hg.preferred(x, self.ffn_in.weight):
             f = hg.linear_bias_gelu(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias)
-            o = reduce_from_tp(hg.linear(f, self.ffn_out.weight), self.tp)
         else:
             f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
+        if hip and hg.preferred(f, self.ffn_out.weight):
+            o = reduce_from_tp(hg.linear(f, self.ffn_out.weight), self.tp)
+        else:
             o = self.ffn_out(f, add_bias=False)
         return fb.bias_dropout_add_layernorm(o, self.ffn_out.bias, x, self.ln2.weight, self.ln2.bias, c.ln_eps, drop,
                                              rng, site + 1)
