@@ -48,7 +48,9 @@ def config_details() -> tuple[tuple[int, int, int], ...]:
 # products it measured faster than hipBLASLt on MI355X, with the winning configuration (tools/bench_gemm_hip.py,
 # profiles/gemm_hip_r3b.jsonl; BERT-base, 4096 tokens): attention-out 4096x768x768 10.7 us vs 20.5 us. Measured
 # slower there and left on hipBLASLt: QKV 22.9 vs 21.6 us, FFN-in 25.3 vs 23.3 us (with the bias + GELU epilogue
-# 37.5 vs 34.9 us for GEMM + separate bias_gelu), FFN-out 28.9 vs 25.1 us. MIFX_HIP_GEMM=all routes every
+# 37.5 vs 34.9 us for GEMM + separate bias_gelu: the epilogue's second 25 MB output (the pre-bias product the
+# backward needs) is written after the last K-tile by every workgroup at once, un-overlapped, and a branch-free erf
+# did not change that: profiles/gemm_hip_r3c_fasterf.jsonl), FFN-out 28.9 vs 25.1 us. MIFX_HIP_GEMM=all routes every
 # eligible shape to the kernel (heuristic configuration) for A/B runs.
 TUNED: dict[tuple[int, int, int], int] = {(4096, 768, 768): 13}
 

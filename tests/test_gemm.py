@@ -39,10 +39,13 @@ def test_gemm_nt_matches_fp32_reference(cfg, epi, bias_dtype):
     assert (y.float() - ref).abs().max().item() <= tol
     if epi == 2:
         assert (z.float() - zref).abs().max().item() <= 2e-2 * zref.abs().max().item()
-        # the epilogue == the unfused bias_gelu kernel applied to the stored product z
+        # the epilogue == the unfused bias_gelu kernel applied to the stored product z, up to one bf16 rounding step
+        # (branch-free erf, |error| <= 1.5e-7, against the library erff)
         from mifx.ops import fused_bert as fb
 
-        assert torch.equal(y, fb.bias_gelu(z, b))
+        ref_y = fb.bias_gelu(z, b).float()
+        assert (y.float() - ref_y).abs().max().item() <= 2 ** -8 * ref_y.abs().max().item()
+        assert (y != fb.bias_gelu(z, b)).float().mean().item() < 0.01
 
 
 @pytest.mark.gpu
