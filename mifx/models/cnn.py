@@ -9,7 +9,9 @@ so MIOpen picks its NHWC implicit-GEMM (MFMA) convolution kernels on gfx950).
 * `FashionCNN` — serving notebook model (`serving/Predict_Fashion_MNIST.ipynb`): Conv8 3x3 s2 + Dense10.
 * `TpuMnistCNN` — TPU notebook model (`tpu/Keras_MNIST_TPU.ipynb`): Conv32-Pool-Conv64-Pool-Conv64-
   Dense64-Dropout-Dense10.
-TF "SAME" padding is reproduced exactly (asymmetric when needed) so shapes match the reference."""
+TF "SAME" padding is reproduced exactly (asymmetric when needed) so shapes match the reference. Convolutions with
+few channels (weights <= mifx.ops.conv_small.MAX_WEIGHTS) run on the direct fp32 HIP kernels on the GPU
+(csrc/conv_small.hip); the PATE ensembles use the grouped MFMA kernel (csrc/gconv.hip)."""
 from __future__ import annotations
 
 import math
@@ -19,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import cnn_ops, pool
+from ..ops.conv_small import SmallConv2d
 
 
 def _same_pad(x: torch.Tensor, k: int, s: int, value: float = 0.0) -> torch.Tensor:
@@ -31,12 +34,11 @@ def _same_pad(x: torch.Tensor, k: int, s: int, value: float = 0.0) -> torch.Tens
     return F.pad(x, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2), value=value)
 
 
-class SameConv2d(nn.Conv2d):
-    def __init__(self, cin, cout, k, stride=1):
-        super().__init__(cin, cout, k, stride=stride, padding=0)
+class SameConv2d(SmallConv2d):
+    """TF "SAME" conv: few-channel layers on the direct HIP kernels (csrc/conv_small.hip), the rest nn.Conv2d."""
 
-    def forward(self, x):
-        return super().forward(_same_pad(x, self.kernel_size[0], self.stride[0]))
+    def __init__(self, cin, cout, k, stride=1):
+        super().__init__(cin, cout, k, stride=stride, same=True)
 
 
 def same_maxpool(x, k, s):
@@ -58,7 +60,7 @@ class MnistDPCNN(nn.Module):
     def __init__(self, num_classes: int = 10):
         super().__init__()
         self.conv1 = SameConv2d(1, 16, 8, stride=2)
-        self.conv2 = nn.Conv2d(16, 32, 4, stride=2)
+        self.conv2 = SmallConv2d(16, 32, 4, stride=2)
         self.fc1 = nn.Linear(32 * 4 * 4, 32)
         self.fc2 = nn.Linear(32, num_classes)
         _he_normal_(self)
@@ -130,7 +132,7 @@ class FashionCNN(nn.Module):
 
     def __init__(self, num_classes: int = 10):
         super().__init__()
-        self.conv = nn.Conv2d(1, 8, 3, stride=2)
+        self.conv = SmallConv2d(1, 8, 3, stride=2)
         self.fc = nn.Linear(8 * 13 * 13, num_classes)
 
     def logits(self, x):
@@ -145,9 +147,9 @@ class FashionCNN(nn.Module):
 class TpuMnistCNN(nn.Module):
     def __init__(self, num_classes: int = 10, dropout: float = 0.5):
         super().__init__()
-        self.c1 = nn.Conv2d(1, 32, 3)
-        self.c2 = nn.Conv2d(32, 64, 3)
-        self.c3 = nn.Conv2d(64, 64, 3)
+        self.c1 = SmallConv2d(1, 32, 3)
+        self.c2 = SmallConv2d(32, 64, 3)
+        self.c3 = SmallConv2d(64, 64, 3)
         self.fc = nn.Linear(64 * 3 * 3, 64)
         self.out = nn.Linear(64, num_classes)
         self.p = dropout

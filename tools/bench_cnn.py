@@ -82,6 +82,17 @@ def bench_model(dev, steps, warmup, name, model, B, shape, channels=1, lr=1e-3):
     return {"workload": name, "batch": B, "ms_per_step": 1e3 * dt, "examples_per_sec": B / dt}
 
 
+class _Logits(torch.nn.Module):
+    """FashionCNN trains on its logits (forward() returns the served softmax)."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = m
+
+    def forward(self, x):
+        return self.m.logits(x)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
@@ -99,8 +110,11 @@ if __name__ == "__main__":
         "sgd_fused": lambda: bench_dpsgd(dev, a.steps, a.warmup, dp=False),
         "pate": lambda: bench_model(dev, a.steps, a.warmup, "pate_teacher", cnn.PateCNN(), 128, (28, 28)),
         "tpu": lambda: bench_model(dev, a.steps, a.warmup, "tpu_mnist_cnn", cnn.TpuMnistCNN(), 1024, (28, 28)),
+        "fashion": lambda: bench_model(dev, a.steps, a.warmup, "fashion_cnn", _Logits(cnn.FashionCNN()), 256, (28, 28)),
     }
     for k, fn in jobs.items():
         if (a.only and k not in a.only.split(",")) or (dev.type == "cpu" and k == "dpsgd_vmap"):
             continue
-        print(json.dumps(fn()), flush=True)
+        r = fn()
+        r["small_conv"] = os.environ.get("MIFX_SMALL_CONV", "1") != "0"
+        print(json.dumps(r), flush=True)
