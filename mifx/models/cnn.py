@@ -9,9 +9,9 @@ so MIOpen picks its NHWC implicit-GEMM (MFMA) convolution kernels on gfx950).
 * `FashionCNN` — serving notebook model (`serving/Predict_Fashion_MNIST.ipynb`): Conv8 3x3 s2 + Dense10.
 * `TpuMnistCNN` — TPU notebook model (`tpu/Keras_MNIST_TPU.ipynb`): Conv32-Pool-Conv64-Pool-Conv64-
   Dense64-Dropout-Dense10.
-TF "SAME" padding is reproduced exactly (asymmetric when needed) so shapes match the reference. Convolutions with
-few channels (weights <= mifx.ops.conv_small.MAX_WEIGHTS) run on the direct fp32 HIP kernels on the GPU
-(csrc/conv_small.hip); the PATE ensembles use the grouped MFMA kernel (csrc/gconv.hip)."""
+TF "SAME" padding is reproduced exactly (asymmetric when needed) so shapes match the reference. With
+MIFX_SMALL_CONV=1 the few-channel first layers run on the direct fp32 HIP kernels (csrc/conv_small.hip; opt-in:
+MIOpen measured faster, mifx/ops/conv_small.py); the PATE ensembles use the grouped MFMA kernel (csrc/gconv.hip)."""
 from __future__ import annotations
 
 import math
@@ -35,7 +35,7 @@ def _same_pad(x: torch.Tensor, k: int, s: int, value: float = 0.0) -> torch.Tens
 
 
 class SameConv2d(SmallConv2d):
-    """TF "SAME" conv: few-channel layers on the direct HIP kernels (csrc/conv_small.hip), the rest nn.Conv2d."""
+    """TF "SAME" conv (few-channel layers on the direct HIP kernels when MIFX_SMALL_CONV=1, else nn.Conv2d)."""
 
     def __init__(self, cin, cout, k, stride=1):
         super().__init__(cin, cout, k, stride=stride, same=True)

@@ -19,9 +19,10 @@ from . import _lib
 from ._lib import I32, VP, check, ptr, sig, stream_handle
 
 # Input channels up to which the VALU direct conv is used: the first layers (1 or 3 channels) of these CNNs, where
-# an MFMA tile has nothing to reduce over. Measured on MI355X (tools/bench_cnn.py, profiles/cnn_small_conv_r3.jsonl):
-# with every conv of the TPU CNN direct (C_in 1 / 32 / 64) the step took 6.8 ms against 1.29 ms on MIOpen, so the
-# deeper layers stay on the library.
+# an MFMA tile has nothing to reduce over. OPT-IN (MIFX_SMALL_CONV=1): measured on MI355X (tools/bench_cnn.py,
+# profiles/cnn_small_conv_r3.jsonl) MIOpen is faster on all but the Fashion CNN -- TPU CNN 1.46 ms/step with its
+# first layer direct (6.8 with every layer direct) vs 1.29, DP-SGD tutorial SGD step 0.67 vs 0.60, PATE teacher 1.75
+# vs 1.60; Fashion 0.43-0.49 vs 0.54.
 MAX_CIN = 4
 MAX_WEIGHTS = 40_000
 
@@ -45,8 +46,8 @@ def _in_functorch_transform() -> bool:
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor, groups: int = 1, dilation=(1, 1)) -> bool:
-    """MIFX_SMALL_CONV=0 turns the direct kernels off (library convolutions; A/B runs)."""
-    return (os.environ.get("MIFX_SMALL_CONV", "1") != "0" and x.is_cuda and x.dtype == torch.float32
+    """MIFX_SMALL_CONV=1 turns the direct kernels on (default: library convolutions, measured faster)."""
+    return (os.environ.get("MIFX_SMALL_CONV", "0") == "1" and x.is_cuda and x.dtype == torch.float32
             and w.dtype == torch.float32 and x.dim() == 4 and groups == 1 and tuple(dilation) == (1, 1)
             and w.shape[1] <= MAX_CIN and w.shape[2] * w.shape[3] <= 64 and w.numel() <= MAX_WEIGHTS
             and not _in_functorch_transform())

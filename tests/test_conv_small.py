@@ -45,9 +45,10 @@ def test_direct_conv_matches_fp32_reference(N, C, H, K, R, stride, pad):
 
 
 @pytest.mark.gpu
-def test_small_cnn_models_match_cpu():
+def test_small_cnn_models_match_cpu(monkeypatch):
     from mifx.models.cnn import FashionCNN, MnistDPCNN, TpuMnistCNN
 
+    monkeypatch.setenv("MIFX_SMALL_CONV", "1")
     for cls in (FashionCNN, TpuMnistCNN, MnistDPCNN):
         torch.manual_seed(0)
         m = cls().eval()

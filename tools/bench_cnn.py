@@ -116,5 +116,5 @@ if __name__ == "__main__":
         if (a.only and k not in a.only.split(",")) or (dev.type == "cpu" and k == "dpsgd_vmap"):
             continue
         r = fn()
-        r["small_conv"] = os.environ.get("MIFX_SMALL_CONV", "1") != "0"
+        r["small_conv"] = os.environ.get("MIFX_SMALL_CONV", "0") == "1"
         print(json.dumps(r), flush=True)
