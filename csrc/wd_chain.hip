@@ -44,7 +44,13 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 #include "wd_opt.h"
 
-constexpr int T = 128;  // examples per workgroup iteration
+#ifndef WDC_T
+#define WDC_T 128
+#endif
+// examples per workgroup iteration: 128 (this file's library), or 64 (csrc/wd_chain64.hip: the same kernel built
+// for one 4-wave workgroup of 4 x 16 examples, the small-batch shape)
+constexpr int T = WDC_T;
+static_assert(T == 128 || T == 64, "T");
 constexpr int MAXW = 8;  // waves per workgroup: T / (16 TBN), TBN = 16-example column blocks per wave (1 or 2)
 // Row padding (elements): WPAD for the weight images, PAD for the staging images; with the row permutations below
 // (wperm, sperm16) every LDS access site is conflict-free in the bank model (tools/lds_banks.py). (XOR swizzles
@@ -535,10 +541,11 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   // L2 nt 0..5 x kt {2w, 2w+1}; L3 nt w x kt 0..5; L4 nt w x kt 0..3; L5 nt 0 x kt w.
   // 8 waves: L1 nt w x kt 0; L2 nt 3(w%2)..+2 x kt 2(w/2)..+1 (3 x 2 blocks: 5 operand fragments per k-step
   // instead of 7 for 6 x 1); L3 nt w%4 x kt 3(w/4)..+2; L4 nt w%4 x kt 2(w/4)..+1; L5 nt 0 x kt w (waves 0..3)
-  constexpr int O1N = TBN == 2 ? 2 : 1, O2N = TBN == 2 ? 6 : 3, O2K = 2, O3K = TBN == 2 ? 6 : 3,
-                O4K = TBN == 2 ? 4 : 2;
-  const int n1 = TBN == 2 ? 2 * w : w, n2 = TBN == 2 ? 0 : 3 * (w & 1), k2 = TBN == 2 ? 2 * w : 2 * (w >> 1),
-            n3 = w & 3, k3 = TBN == 2 ? 0 : 3 * (w >> 2), n4 = w & 3, k4 = TBN == 2 ? 0 : 2 * (w >> 2);
+  constexpr bool W4 = NWAVE == 4;  // 4-wave shapes (TBN 2 at T 128, TBN 1 at T 64) share one tile ownership
+  static_assert(NWAVE == 4 || NWAVE == 8, "waves");
+  constexpr int O1N = W4 ? 2 : 1, O2N = W4 ? 6 : 3, O2K = 2, O3K = W4 ? 6 : 3, O4K = W4 ? 4 : 2;
+  const int n1 = W4 ? 2 * w : w, n2 = W4 ? 0 : 3 * (w & 1), k2 = W4 ? 2 * w : 2 * (w >> 1),
+            n3 = w & 3, k3 = W4 ? 0 : 3 * (w >> 2), n4 = w & 3, k4 = W4 ? 0 : 2 * (w >> 2);
   const bool l5 = w < 4;
   v4f acc1[O1N], acc2[O2N * O2K], acc3[O3K], acc4[O4K], acc5[1];
   int ct1[O1N], ct2[O2N * O2K], ct3[O3K], ct4[O4K], ct5[1];
@@ -901,18 +908,15 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     }
     if (tid == 0) misc[1] = misc[4] + misc[5] + misc[6] + misc[7];
     __syncthreads();
-    if (tid == 0) {  // XCDs holding rows, ordered by their first row
-      int k2 = 0;
-      for (int xx = 0; xx < XMAXT; ++xx) {
-        if (first[xx] >= (1 << 30)) continue;
-        int j = k2++;
-        while (j > 0 && first[order[j - 1]] > first[xx]) {
-          order[j] = order[j - 1];
-          --j;
-        }
-        order[j] = xx;
-      }
-      misc[3] = k2;
+    if (tid < XMAXT) {  // XCDs holding rows, ordered by their first row (lane tid's rank among the valid ones)
+      const int f = first[tid];
+      const bool valid = f < (1 << 30);
+      int rank = 0;
+#pragma unroll
+      for (int y = 0; y < XMAXT; ++y) rank += first[y] < f ? 1 : 0;
+      if (valid) order[rank] = tid;
+      const unsigned long long vm = __ballot(valid);
+      if (tid == 0) misc[3] = __popcll(vm);
     }
     const int nr = misc[1], me = misc[2];
     const int q0 = (int)((long long)me * S4 / nr), q1 = (int)((long long)(me + 1) * S4 / nr);
@@ -990,10 +994,18 @@ void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, l
 
 }  // namespace
 
+// exported names: the T = 64 build (csrc/wd_chain64.hip) suffixes them, so neither library's calls can bind to the
+// other's definitions when both are loaded RTLD_GLOBAL
+#if WDC_T == 128
+#define WDC_SYM(n) n
+#else
+#define WDC_SYM(n) n##_t64
+#endif
+
 extern "C" {
 
 // T, LWEND (weight image elements), LDS_BYTES, WPAD (weight-image row pad), NTILE, WIDE_PAD
-int mifx_wdc_constants(int* out, int n) {
+int WDC_SYM(mifx_wdc_constants)(int* out, int n) {
   const int v[] = {T, LWEND, LDS_BYTES, WPAD, NTILE, WIDE_PAD, LW1, LW2, LW3, LW4, LW5};
   const int m = (int)(sizeof(v) / sizeof(int));
   for (int i = 0; i < n && i < m; ++i) out[i] = v[i];
@@ -1005,16 +1017,27 @@ int mifx_wdc_constants(int* out, int n) {
 // (step_ctr[0] * batch) % n_data (or start_fixed when step_ctr is null). wimg: the bf16 weight image in LDS
 // layout (LWEND elements, C-ordered columns, see models.wide_deep.chain_image).
 // xcd_of (nullable, >= grid ints): receives the XCD each workgroup ran on (training only).
-int mifx_wdc_fused_x(const void* data, long long n_data, long long batch, long long start_fixed,
-                     const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
-                     float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
-                     int waves, int* xcd_of, hipStream_t stream) {
+// (T = 64 build: waves must be 4, 4 x 16 examples)
+int WDC_SYM(mifx_wdc_fused_x)(const void* data, long long n_data, long long batch, long long start_fixed,
+                              const long long* step_ctr, const void* wimg, const float* wide, float* slab,
+                              float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
+                              const int* tmap, int stride, int waves, int* xcd_of, hipStream_t stream) {
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
   if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;
   if (!train && logits_out == nullptr) return -1;
-  if (waves != 4 && waves != 8) return -1;
   const dim3 g(grid);
+#if WDC_T == 64
+  if (waves != 4) return -1;
+  if (train)
+    launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                    grad_scale, tmap, stride, xcd_of);
+  else
+    launch<false, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                     grad_scale, tmap, stride, nullptr);
+  return (int)hipGetLastError();
+#else
+  if (waves != 4 && waves != 8) return -1;
   if (train && waves == 4)
     launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                     grad_scale, tmap, stride, xcd_of);
@@ -1025,15 +1048,18 @@ int mifx_wdc_fused_x(const void* data, long long n_data, long long batch, long l
     launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                      grad_scale, tmap, stride, nullptr);
   return (int)hipGetLastError();
+#endif
 }
 
-int mifx_wdc_fused(const void* data, long long n_data, long long batch, long long start_fixed,
-                   const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
-                   float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
-                   int waves, hipStream_t stream) {
-  return mifx_wdc_fused_x(data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                          grad_scale, grid, train, tmap, stride, waves, nullptr, stream);
+int WDC_SYM(mifx_wdc_fused)(const void* data, long long n_data, long long batch, long long start_fixed,
+                            const long long* step_ctr, const void* wimg, const float* wide, float* slab,
+                            float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
+                            const int* tmap, int stride, int waves, hipStream_t stream) {
+  return WDC_SYM(mifx_wdc_fused_x)(data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss,
+                                   logits_out, grad_scale, grid, train, tmap, stride, waves, nullptr, stream);
 }
+
+#if WDC_T == 128  // the in-kernel tail and the persistent kernel exist for the 8-wave T = 128 shape only
 
 // Training step with the in-kernel tail (slab reduction + optimizer inside the launch; see TailArgs): 8-wave
 // shape, grid <= the number of CUs (every workgroup must be resident), the whole step in ONE launch.
@@ -1105,6 +1131,8 @@ int mifx_wdc_persist(const void* data, long long n_data, long long batch, long l
                                nullptr, grad_scale, tmap, stride, nullptr, ta);
   return (int)hipGetLastError();
 }
+
+#endif  // WDC_T == 128
 
 #ifdef WDC_STAMPS
 int mifx_wdc_stamps(unsigned long long* out) {

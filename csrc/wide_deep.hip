@@ -985,18 +985,16 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
   __syncthreads();
   if (xo >= 0) atomicMin(&first[xo], t);
   __syncthreads();
-  if (t == 0) {  // XCDs holding rows, by first row (insertion sort of <= 16 LDS values)
-    int k2 = 0;
-    for (int xx = 0; xx < XMAX; ++xx) {
-      if (first[xx] >= (1 << 30)) continue;
-      int j = k2++;
-      while (j > 0 && first[order[j - 1]] > first[xx]) {
-        order[j] = order[j - 1];
-        --j;
-      }
-      order[j] = xx;
-    }
-    nord = k2;
+  if (t < XMAX) {  // XCDs holding rows, by first row: lane t's rank among the distinct valid first rows (a serial
+                   // insertion sort by one lane cost ~1.5 us of dependent LDS round trips per workgroup)
+    const int f = first[t];
+    const bool valid = f < (1 << 30);
+    int rank = 0;
+#pragma unroll
+    for (int y = 0; y < XMAX; ++y) rank += first[y] < f ? 1 : 0;
+    if (valid) order[rank] = t;
+    const unsigned long long vm = __ballot(valid);
+    if (t == 0) nord = __popcll(vm);
   }
   __syncthreads();
   const int e = (int)s_e;

@@ -56,7 +56,10 @@ def source_hash(src: Path) -> str:
     h = hashlib.sha256()
     flags = (HIP_FLAGS + _file_flags(src)) if src.suffix == ".hip" else CXX_FLAGS
     h.update(" ".join(flags).encode())
-    for d in [src] + sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("include/*.h")):
+    # sources a source includes by name (csrc/wd_chain64.hip builds csrc/wd_chain.hip with another tile size)
+    incl = [CSRC / ln.split('"')[1] for ln in src.read_text().splitlines()
+            if ln.startswith('#include "') and ln.split('"')[1].endswith(".hip")]
+    for d in [src] + incl + sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("include/*.h")):
         if d.exists() and d.name != HASH_HEADER.name:
             h.update(d.name.encode())
             h.update(d.read_bytes())

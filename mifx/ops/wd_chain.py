@@ -27,6 +27,26 @@ def _fns():
 
 
 @functools.lru_cache(maxsize=None)
+def _fns64():
+    """csrc/wd_chain64.hip: the same kernel at 64 examples per iteration (4 waves x 16), the small-batch shape."""
+    lib = _lib.load("wd_chain64")
+    return {
+        "constants": sig(lib, "mifx_wdc_constants_t64", [VP, I32]),
+        "fused": sig(lib, "mifx_wdc_fused_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
+                                                 I32, VP]),
+        "fused_x": sig(lib, "mifx_wdc_fused_x_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
+                                                     I32, I32, VP, VP]),
+    }
+
+
+def fns_for(tile: int) -> dict:
+    """Bindings of the T = tile build (128: csrc/wd_chain.hip, 64: csrc/wd_chain64.hip)."""
+    if tile not in (64, 128):
+        raise ValueError("tile must be 64 or 128")
+    return _fns() if tile == 128 else _fns64()
+
+
+@functools.lru_cache(maxsize=None)
 def constants() -> dict[str, int]:
     buf = (ctypes.c_int * 16)()
     n = _fns()["constants"](buf, 16)
@@ -37,13 +57,15 @@ def constants() -> dict[str, int]:
 def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
           wimg_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
           logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
-          tmap: torch.Tensor | None = None, waves: int = 8, xcd_of: torch.Tensor | None = None) -> None:
+          tmap: torch.Tensor | None = None, waves: int = 8, xcd_of: torch.Tensor | None = None,
+          tile: int = 128) -> None:
     """One chained-kernel launch. wimg_bf16: [LWEND] bf16 (or int16) weight image in the kernel's LDS layout
     (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout.
-    waves: 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each). xcd_of: int32
+    tile 128: waves 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each);
+    tile 64 (64 examples per workgroup iteration): waves 4 (one wave per SIMD, 16 examples each). xcd_of: int32
     [>= grid], receives the XCD each workgroup ran on (for the XCD-local slab reduction)."""
-    if waves not in (4, 8):
-        raise ValueError("waves must be 4 or 8")
+    if waves not in ((4, 8) if tile == 128 else (4,)):
+        raise ValueError("waves must be 4 or 8 (tile 128) / 4 (tile 64)")
     c = constants()
     if wimg_bf16.numel() != c["LWEND"] or wimg_bf16.element_size() != 2 or not wimg_bf16.is_contiguous():
         raise ValueError("weight image must be a contiguous 16-bit [LWEND] tensor")
@@ -61,7 +83,7 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
         raise ValueError("eval launch needs logits_out with >= batch floats")
     if xcd_of is not None and (xcd_of.dtype != torch.int32 or xcd_of.numel() < grid):
         raise ValueError("xcd_of must be int32 [>= grid]")
-    rc = _fns()["fused_x"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
+    rc = fns_for(tile)["fused_x"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
                            ptr(slab), ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
                            ptr(tmap), stride, int(waves), ptr(xcd_of), stream_handle(records.device))
     check(rc, "mifx_wdc_fused")

@@ -61,7 +61,8 @@ class FusedWideDeepTrainer:
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
                  live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8,
-                 in_kernel_tail: bool | None = None, persistent: bool | None = None):
+                 in_kernel_tail: bool | None = None, persistent: bool | None = None,
+                 small_tile: bool | None = None):
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
@@ -167,6 +168,15 @@ class FusedWideDeepTrainer:
             persistent = os.environ.get("MIFX_WD_PERSIST", "0") == "1"
         self._persist = bool(persistent and self._sc and self.world == 1 and self.grid == 1 and self.batch <= self.T
                              and self.waves == 8 and self._ktail is None and self.device.type == "cuda")
+        # small_tile (default on; small_tile=False or MIFX_WD_T64=0 turns it off): a batch of <= 64 examples trains
+        # on the T = 64 build of the chained kernel (csrc/wd_chain64.hip: one 4-wave workgroup, one wave per SIMD)
+        # instead of one 8-wave T = 128 iteration that is mostly padding at the reference batch of 40
+        if small_tile is None:
+            small_tile = os.environ.get("MIFX_WD_T64", "1") == "1"
+        self.tile = 64 if (small_tile and kernel == "chain" and self.batch <= 64 and self.grid == 1
+                           and not self._persist and self._ktail is None) else 128
+        if self.tile == 64:
+            self.waves = 4
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
         self.partial = torch.empty(self.nsplit, self.stride, device=dev)
@@ -242,7 +252,8 @@ class FusedWideDeepTrainer:
 
             wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves,
-                      self._xcd.xcd_of if (train and self._xcd is not None and slab is self.slab) else None)
+                      self._xcd.xcd_of if (train and self._xcd is not None and slab is self.slab) else None,
+                      tile=self.tile if train else 128)
         else:
             wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
@@ -324,7 +335,7 @@ class FusedWideDeepTrainer:
         self._direct = DirectAllReduce(self.grad, self.pg)
         stream = torch.cuda.current_stream(self.device)
         sh = ctypes.c_void_p(stream.cuda_stream)
-        fused = (wdc._fns()["fused"], (ptr(self.records), self.n_data, self.batch, 0, ptr(self.step_ctr), ptr(self.wt),
+        fused = (wdc.fns_for(self.tile)["fused"], (ptr(self.records), self.n_data, self.batch, 0, ptr(self.step_ctr), ptr(self.wt),
                                        ptr(self.wide_weights), ptr(self.slab), ptr(self.slab_loss), None,
                                        float(self.grad_scale), int(self.grid), 1, ptr(self.tmap), int(self.stride),
                                        int(self.waves), sh))

@@ -144,7 +144,7 @@ def _emulated_grads(vec, rec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["chain", "chain4", "tile"])
+@pytest.mark.parametrize("kernel", ["chain", "chain4", "chain128", "tile"])
 @pytest.mark.parametrize("batch", [40, 64, 1000, 8192])
 def test_fused_gradients_match_torch(batch, kernel):
     torch.manual_seed(batch)
@@ -159,7 +159,15 @@ def test_fused_gradients_match_torch(batch, kernel):
             lin.bias.normal_(0, 0.1)
     rec = synthetic_records(batch, seed=7)
     kw = {"kernel": "chain", "waves": 4} if kernel == "chain4" else {"kernel": kernel}
+    if kernel == "chain128":  # small batches on the T = 128 build (the default trains them on T = 64)
+        if batch > 64:
+            pytest.skip("same launch as 'chain' above 64 examples")
+        kw = {"kernel": "chain", "small_tile": False}
     tr = FusedWideDeepTrainer(m, batch=batch, device=dev, **kw)
+    if kernel == "chain" and batch <= 64:
+        assert tr.tile == 64 and tr.waves == 4
+    if kernel == "chain128":
+        assert tr.tile == 128
     tr.set_data(rec.to(dev))
     g_tn = tr.gradients_once()
     torch.cuda.synchronize()
@@ -425,6 +433,36 @@ def test_chain_maps_cover_trainable_parameters():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 40, 64])
+def test_small_tile_training_matches_t128(batch):
+    """The T = 64 build (csrc/wd_chain64.hip, 4 waves x 16 examples) against the T = 128 build on the same small
+    batches: the dense dW tiles accumulate the same 32-example k-steps in the same order (bit-identical), the wide
+    fixed-point histogram uses a finer scale at T = 64 (2^k / (iterations x T)), so whole training runs agree to
+    rounding. Also run-to-run bit-identical, through multi-step graphs."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(4096, device=dev, seed=21)
+    grads, params = {}, {}
+    for small in (True, False, True):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device=dev, small_tile=small)
+        assert tr.tile == (64 if small else 128)
+        tr.set_data(rec)
+        g = tr.gradients_once()
+        tr.capture(steps_per_graph=10)
+        tr.run(200)
+        torch.cuda.synchronize()
+        if small in grads:
+            np.testing.assert_array_equal(g, grads[small])
+            assert torch.equal(tr.param, params[small])
+        grads[small], params[small] = g, tr.param.clone()
+    dense = tr.stride - wdm.WIDE_PAD  # the wide histogram is the last WIDE_PAD slab columns
+    np.testing.assert_array_equal(grads[True][:dense], grads[False][:dense])
+    np.testing.assert_allclose(grads[True][dense:], grads[False][dense:], rtol=0, atol=1e-5)
+    assert torch.allclose(params[True], params[False], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.gpu
 def test_multi_step_graph_matches_single_step_replays():
     """run(n) with a 7-step graph (2 multi-step replays + 3 one-step replays) must give exactly the parameters
     of 17 one-step replays: the data offset and optimizer step advance through the device-side step counter."""
@@ -508,7 +546,8 @@ def test_persistent_small_batch_matches_slab_path(batch, opt):
                                              "wide_opt": OptSpec(opt, lr=lr) if lr else OptSpec(opt, lr=0.2)}
     out = []
     for persistent in (True, False):
-        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device="cuda", persistent=persistent, **kw)
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device="cuda", persistent=persistent,
+                                  small_tile=False, **kw)  # the T = 128 slab path it is bit-identical to
         assert tr._persist == persistent
         tr.set_data(recs)
         tr.step()

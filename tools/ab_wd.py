@@ -18,7 +18,8 @@ from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernels", default="chain8,chain4,tile",
-                    help="chain8 / chain4 (waves), tile, or chain8tail / chain8notail (in-kernel step tail on / off)")
+                    help="chain8 / chain4 (waves), tile, t64 (T = 64 build, batch <= 64), or chain8tail / chain8notail "
+                         "(in-kernel step tail on / off)")
     ap.add_argument("--batches", default="65536,131072,40")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps-per-graph", type=int, default=10, help="as bench.py; 1 = launch-bound replays")
@@ -32,9 +33,11 @@ def main():
         for k in a.kernels.split(","):
             if k == "tile":
                 kw = {"kernel": "tile"}
+            elif k == "t64":  # the T = 64 build (csrc/wd_chain64.hip), batches <= 64
+                kw = {"kernel": "chain", "small_tile": True}
             else:
                 tail = None if not k.endswith("tail") else (not k.endswith("notail"))
-                kw = {"kernel": "chain", "waves": int(k[5:6] or 8), "in_kernel_tail": tail}
+                kw = {"kernel": "chain", "waves": int(k[5:6] or 8), "in_kernel_tail": tail, "small_tile": False}
             tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=dev, **kw)
             tr.set_data(data)
             tr.capture(steps_per_graph=a.steps_per_graph)
