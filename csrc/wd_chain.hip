@@ -516,14 +516,17 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
         __builtin_amdgcn_global_load_lds((const void*)(wimg + min(c0 + lane, NCH - 1)),
                                          (__attribute__((address_space(3))) void*)(lds + c0 * 8), 16, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (one launch = one step: the wait for the image and the block barrier come after the first iteration's
+    // record fetch below, so the step-counter -> records latency chain runs under the staging instead of after it)
+    if constexpr (PERSIST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   float* wlds = red + 64;  // PERSIST: the fp32 wide weights [WIDE_PAD], resident for the launch
   if (TRAIN)
     for (int c = tid; c < WIDE_PAD; c += NTHR) wgrad[c] = 0.f;
-  if constexpr (PERSIST)
+  if constexpr (PERSIST) {
     for (int c = tid; c < WIDE_PAD; c += NTHR) wlds[c] = wide[c];
-  __syncthreads();
+    __syncthreads();
+  }
 
   const long long step0 = step_ctr ? step_ctr[0] : 0;
   constexpr bool kPersist = PERSIST;
@@ -582,6 +585,10 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   };
   uint4 nu[TBN][2];
   fetch(blockIdx.x, nu);
+  if constexpr (!PERSIST) {  // weight image (LDS-DMA) and the first records landed; wgrad zeroed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 
   STAMP(1);
   BSTAMP(1);

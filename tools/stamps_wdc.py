@@ -11,12 +11,13 @@ sys.path.insert(0, ".")
 import mifx.ops._lib as L  # noqa: E402
 
 diag = ctypes.CDLL("tools/bin/libwdc_stamps.so", mode=ctypes.RTLD_GLOBAL)
+diag64 = ctypes.CDLL("tools/bin/libwdc64_stamps.so", mode=ctypes.RTLD_GLOBAL)
 L.load.cache_clear()
 _orig = L.load.__wrapped__
 
 
 def _load(name):
-    return diag if name == "wd_chain" else _orig(name)
+    return {"wd_chain": diag, "wd_chain64": diag64}.get(name) or _orig(name)
 
 
 L.load = _load
@@ -27,17 +28,20 @@ from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
 NAMES = {1: "prologue", 2: "loop->iter", 3: "gather+fwd", 4: "loss", 5: "B0", 6: "stage5+B", 7: "dW5+dA4",
          8: "B+stage4+B", 9: "dW4+dA3", 10: "B+stage3+B", 11: "dW3+dA2", 12: "B+stage2+B", 13: "dW2+dA1",
          14: "B+stage1+B", 15: "dW1", 16: "->epi", 17: "epilogue"}
-for NW, batch in ((4, 65536), (8, 128), (8, 65536)):
-    tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device="cuda", kernel="chain", waves=NW)
+for NW, batch in ((4, 40), (8, 40), (4, 65536), (8, 128), (8, 65536)):
+    t64 = NW == 4 and batch <= 64  # the T = 64 build (csrc/wd_chain64.hip)
+    tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device="cuda", kernel="chain", waves=NW,
+                              small_tile=t64)
+    lib = diag64 if t64 else diag
     tr.set_data(synthetic_records(1 << 17, device="cuda", seed=0))
     for _ in range(3):
         tr.step()
     torch.cuda.synchronize()
 
     buf = (ctypes.c_ulonglong * (32 * 8))()  # g_wdc_stamps is [MAXW = 8][32]
-    assert diag.mifx_wdc_stamps(buf) == 0
+    assert lib.mifx_wdc_stamps(buf) == 0
     st = [[buf[w * 32 + i] for i in range(32)] for w in range(NW)]
-    print(f"== batch {batch} grid {tr.grid}: cycles per phase (block 0; the 2nd iteration when there is one)")
+    print(f"== batch {batch} grid {tr.grid} T {tr.tile}: cycles per phase (block 0; the 2nd iteration when there is one)")
     for i in range(1, 18):
         d = [st[w][i] - st[w][i - 1] for w in range(NW)]
         print(f"  {NAMES[i]:>11}: " + " ".join(f"{x:8d}" for x in d))
