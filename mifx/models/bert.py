@@ -96,7 +96,8 @@ class BertLayer(nn.Module):
         # hand-written GEMM per projection only where it measured faster than hipBLASLt (mifx.ops.gemm.TUNED)
         hip = c.hip_gemm if c.hip_gemm is not None else os.environ.get("MIFX_BERT_HIP_GEMM", "1") == "1"
         hip = hip and x.is_cuda
-        if hip and hg.preferred(x, self.qkv.weight):
+        # (hg.linear: forward and weight gradient each on the hand-written kernel where it measured faster)
+        if hip:
             qkv = hg.linear(copy_to_tp(x, self.tp), self.qkv.weight, self.qkv.bias).view(B, S, 3, h, d)
         else:
             qkv = self.qkv(x).view(B, S, 3, h, d)
@@ -111,15 +112,14 @@ class BertLayer(nn.Module):
             amask = None if mask is None else mask[:, None, None, :].to(q.dtype)
             ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, dropout_p=adrop)
             ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
-        a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) \
-            if hip and hg.preferred(ctx, self.attn_out.weight) else self.attn_out(ctx, add_bias=False)
+        a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) if hip else self.attn_out(ctx, add_bias=False)
         x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
                                           rng, site)
-        if hip and hg.preferred(x, self.ffn_in.weight):
+        if hip:
             f = hg.linear_bias_gelu(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias)
         else:
             f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
-        if hip and hg.preferred(f, self.ffn_out.weight):
+        if hip:
             o = reduce_from_tp(hg.linear(f, self.ffn_out.weight), self.tp)
         else:
             o = self.ffn_out(f, add_bias=False)

@@ -1,9 +1,9 @@
 """Hand-written gfx950 MFMA GEMM (csrc/gemm.hip): Y = X W^T [+ bias] [-> GELU] for nn.Linear-shaped products.
 
 `linear(x, w, bias)` and `linear_bias_gelu(x, w, bias)` are autograd functions whose FORWARD runs the HIP kernel
-(with the bias / bias + GELU epilogue fused) and whose backward uses the library GEMMs for dX = dY W and
-dW = dY^T X (plus, for GELU, the existing fused bias-GELU backward kernel: the forward saves exactly what
-mifx.ops.fused_bert._BiasGelu saves). Shapes the kernel does not tile (M % BM, N % BN, K % 64) take F.linear.
+(with the bias / bias + GELU epilogue fused) where preferred, and whose backward takes dX = dY W from the library and
+dW = dY^T X from the hand-written TN kernel (csrc/gemm_tn.hip) where that is preferred (plus, for GELU, the existing
+fused bias-GELU backward kernel: the forward saves exactly what mifx.ops.fused_bert._BiasGelu saves). Shapes the kernel does not tile (M % BM, N % BN, K % 64) take F.linear.
 
 Tile configuration per (M, N, K): the one with the best measured time on MI355X (tools/bench_gemm_hip.py,
 profiles/gemm_hip_r3.jsonl) where known, else the heuristic below (fill >= ~1 wave of workgroups on 256 CUs).
@@ -112,12 +112,26 @@ def gemm_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
     return y, z
 
 
+def _dw(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """Weight gradient dY^T X: the hand-written TN kernel where it measured faster (TN_TUNED), else hipBLASLt."""
+    if tn_preferred(dy2.shape[1], x2.shape[1], dy2.shape[0]) and tn_eligible(dy2, x2):
+        return gemm_tn(dy2, x2)
+    return dy2.t() @ x2
+
+
+def tn_preferred(n_out: int, k_in: int, tokens: int) -> bool:
+    return (n_out, k_in, tokens) in TN_TUNED and os.environ.get("MIFX_HIP_GEMM_TN", "1") != "0"
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias):
+    def forward(ctx, x, w, bias, hip_fwd=True):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        y, _ = gemm_nt(x2, w, bias, 1 if bias is not None else 0)
+        if hip_fwd:
+            y, _ = gemm_nt(x2, w, bias, 1 if bias is not None else 0)
+        else:
+            y = F.linear(x2, w, bias)
         ctx.save_for_backward(x2, w)
         ctx.has_bias = bias is not None
         ctx.bdtype = bias.dtype if bias is not None else None
@@ -128,13 +142,13 @@ class _Linear(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype)
         dx = (dy2 @ w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = dy2.t() @ x2 if ctx.needs_input_grad[1] else None
+        dw = _dw(dy2.contiguous(), x2) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             from .fused_bert import col_sum
 
             db = col_sum(dy2, ctx.bdtype if ctx.bdtype in (torch.float32, torch.bfloat16) else torch.float32)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _LinearBiasGelu(torch.autograd.Function):
@@ -162,15 +176,18 @@ class _LinearBiasGelu(torch.autograd.Function):
         check(fb_fns()["gelu"](_dt(z), _dt(bp), 0, ptr(dy2), ptr(z), ptr(bp), M, N, ptr(dz), ptr(part), ptr(db),
                                stream_handle(z.device)), "mifx_bert_bias_gelu")
         dx = (dz @ w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = dz.t() @ x2 if ctx.needs_input_grad[1] else None
+        dw = _dw(dz, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, db if bp.dtype == ctx.bdtype else db.to(ctx.bdtype)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, force: bool = False) -> torch.Tensor:
     """F.linear with the forward on the hand-written kernel (bias fused) where it is preferred (or, force=True,
-    wherever it tiles the shape)."""
-    if eligible(x, w) if force else preferred(x, w):
-        return _Linear.apply(x, w, bias)
+    wherever it tiles the shape), and the weight gradient on the hand-written TN kernel where that is preferred."""
+    fwd = eligible(x, w) if force else preferred(x, w)
+    bwd = (x.is_cuda and x.dtype == torch.bfloat16 and w.requires_grad and torch.is_grad_enabled()
+           and tn_preferred(w.shape[0], w.shape[1], x.numel() // x.shape[-1]))
+    if fwd or bwd:
+        return _Linear.apply(x, w, bias, fwd)
     return F.linear(x, w, bias)
 
 
@@ -181,4 +198,78 @@ def linear_bias_gelu(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, force
         return _LinearBiasGelu.apply(x, w, bias)
     from .fused_bert import bias_gelu
 
-    return bias_gelu(F.linear(x, w), bias)
+    return bias_gelu(linear(x, w), bias)
+
+
+# ---------------------------------------------------------------- weight-gradient GEMM (csrc/gemm_tn.hip)
+@functools.lru_cache(maxsize=None)
+def _tn_fns():
+    lib = _lib.load("gemm_tn")
+    return {
+        "configs": sig(lib, "mifx_gemm_tn_configs", [VP, I32]),
+        "tn": sig(lib, "mifx_gemm_tn", [I32, VP, VP, VP, VP, I32, I32, I32, I32, VP]),
+    }
+
+
+@functools.lru_cache(maxsize=None)
+def tn_configs() -> tuple[tuple[int, int, int], ...]:
+    """(BM, BN, OPT bits) of every compiled TN tile configuration, by index."""
+    buf = (ctypes.c_int * 96)()
+    n = _tn_fns()["configs"](buf, 96)
+    return tuple((buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(n))
+
+
+# measured per-shape choices (M, N, T) -> (cfg, splits); tools/bench_gemm_tn.py, profiles/gemm_tn_r3.jsonl
+# BERT-base at 4096 tokens (B = 32, S = 128), us vs hipBLASLt `dy.t() @ x`: QKV 30.7 vs 36.2, attention-out 18.3 vs
+# 27.6, FFN-in 38.0 vs 41.8, FFN-out 37.7 vs 42.6 (configs with 2-3 workgroups per CU and a token split; the one-
+# workgroup-per-CU deep-ring configurations measured slower: the per-CU operand stream, not DMA latency, bounds a
+# 96 x 96 tile at ~30 GB/s per workgroup; profiles/gemm_tn_r3.jsonl)
+TN_TUNED: dict[tuple[int, int, int], tuple[int, int]] = {(2304, 768, 4096): (10, 4), (768, 768, 4096): (9, 8),
+                                                         (3072, 768, 4096): (9, 2), (768, 3072, 4096): (9, 2)}
+
+
+def pick_tn(M: int, N: int, T: int, cus: int = 256) -> tuple[int, int] | None:
+    """(config index, token splits) for C[M, N] = A[T, M]^T B[T, N]; None if no configuration tiles it. Splits: the
+    largest power of two that keeps tiles x splits within one wave of workgroups (T % (64 splits) == 0)."""
+    if (M, N, T) in TN_TUNED:
+        return TN_TUNED[(M, N, T)]
+    best, best_score = None, None
+    for i, (bm, bn, opt) in enumerate(tn_configs()):
+        if M % bm or N % bn or T % 64 or opt % 16:
+            continue
+        tiles = (M // bm) * (N // bn)
+        s = 1
+        while tiles * s * 2 <= cus and T % (64 * s * 2) == 0 and T // (s * 2) >= 512:
+            s *= 2
+        wgs = tiles * s
+        fill = wgs / (-(-wgs // cus) * cus)
+        score = (round(fill, 3), -abs(bm * bn - 96 * 96))  # full waves first, then the 96 x 96 tile
+        if best_score is None or score > best_score:
+            best, best_score = (i, s), score
+    return best
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int | None = None, splits: int | None = None) -> torch.Tensor:
+    """a [T, M] bf16, b [T, N] bf16 (row-major) -> a^T b [M, N] bf16 with fp32 accumulation (the weight gradient
+    dY^T X of a linear layer)."""
+    T, M = a.shape
+    N = b.shape[1]
+    if b.shape[0] != T:
+        raise ValueError("a and b must have the same number of rows")
+    if cfg is None or splits is None:
+        pk = pick_tn(M, N, T)
+        if pk is None:
+            raise ValueError(f"no TN tile configuration for {M}x{N} over {T} rows")
+        cfg = pk[0] if cfg is None else cfg
+        splits = pk[1] if splits is None else splits
+    a, b = a.contiguous(), b.contiguous()
+    c = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    part = torch.empty(splits, M, N, device=a.device, dtype=torch.float32) if splits > 1 else None
+    check(_tn_fns()["tn"](int(cfg), ptr(a), ptr(b), ptr(c), ptr(part), M, N, T, int(splits),
+                          stream_handle(a.device)), "mifx_gemm_tn")
+    return c
+
+
+def tn_eligible(a2: torch.Tensor, b2: torch.Tensor) -> bool:
+    return (a2.is_cuda and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.dim() == 2
+            and b2.dim() == 2 and pick_tn(a2.shape[1], b2.shape[1], a2.shape[0]) is not None)
