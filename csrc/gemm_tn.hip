@@ -40,9 +40,10 @@ constexpr int BK = 64;
 // chunk rotation of token row t for a row of CPA 16-byte chunks (conflict-free transposed fragment reads)
 template <int CPA>
 __device__ __forceinline__ int rot(int t) {
-  static_assert(CPA == 8 || CPA == 12 || CPA == 16, "chunks per row");
+  static_assert(CPA == 8 || CPA == 12 || CPA == 16 || CPA == 24, "chunks per row");
   if constexpr (CPA == 8) return ((t & 3) + 4 * ((t >> 3) & 3)) & 7;
   if constexpr (CPA == 12) return (2 * ((t >> 3) & 3)) % 12;
+  if constexpr (CPA == 24) return (6 * (t & 3) + 6 * ((t >> 3) & 3)) % 24;
   return (2 * (t & 3) + 8 * ((t >> 3) & 3)) & 15;
 }
 template <int CPA>
@@ -240,7 +241,8 @@ struct Cfg {
 };
 constexpr Cfg kCfgs[] = {{96, 96, 0, 0},  {96, 96, 1, 0},   {128, 128, 0, 0}, {128, 96, 0, 0}, {96, 128, 0, 0},
                          {64, 64, 0, 0},  {128, 64, 0, 0},  {64, 128, 0, 0},  {96, 96, 0, 3},  {96, 96, 0, 2},
-                         {128, 128, 0, 2}, {128, 128, 0, 3}, {64, 64, 0, 3},   {128, 64, 0, 3}, {64, 128, 0, 3}};
+                         {128, 128, 0, 2}, {128, 128, 0, 3}, {64, 64, 0, 3},   {128, 64, 0, 3}, {64, 128, 0, 3},
+                         {192, 192, 0, 3}, {192, 96, 0, 3},  {96, 192, 0, 3}};
 
 template <int BM, int BN, int OPT, int NS0 = 0>
 int dispatch(const void* A, const void* B, void* C, float* P, int M, int N, int T, int S, hipStream_t st) {
@@ -296,7 +298,10 @@ int mifx_gemm_tn(int cfg, const void* A, const void* B, void* C, float* P, int M
     case 11: return dispatch<128, 128, 0, 3>(A, B, C, P, M, N, T, S, st);
     case 12: return dispatch<64, 64, 0, 3>(A, B, C, P, M, N, T, S, st);
     case 13: return dispatch<128, 64, 0, 3>(A, B, C, P, M, N, T, S, st);
-    default: return dispatch<64, 128, 0, 3>(A, B, C, P, M, N, T, S, st);
+    case 14: return dispatch<64, 128, 0, 3>(A, B, C, P, M, N, T, S, st);
+    case 15: return dispatch<192, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
+    case 16: return dispatch<192, 96, 0, 3>(A, B, C, P, M, N, T, S, st);
+    default: return dispatch<96, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
   }
 }
 

@@ -505,16 +505,29 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       xcd_of[blockIdx.x] = mifx_xcc_id();
   }
 
+#ifndef WDC_REG_STAGE
+#define WDC_REG_STAGE 0
+#endif
+  // WDC_REG_STAGE (diagnostic builds): stage the weight image through registers (global_load_dwordx4 +
+  // ds_write_b128) instead of LDS-DMA
+  constexpr bool REG_STAGE = WDC_REG_STAGE && !PERSIST;
+  constexpr int NCH_STAGE = LWEND / 8, PER_STAGE = (NCH_STAGE + NTHR - 1) / NTHR;
+  uint4 wst[REG_STAGE ? PER_STAGE : 1];
+  (void)wst;
   {  // stage the bf16 weight image (already in LDS layout) with direct-to-LDS loads: no VGPR round trip, no
      // ds_write transfer cycles. Wave w's lanes fill 16-byte chunks i * NTHR + 64 w + lane; the last wave's
      // lanes past the image end re-read its last chunk and land in the staging area, written before any read.
-    constexpr int NCH = LWEND / 8, PER = (NCH + NTHR - 1) / NTHR;
+    if constexpr (!REG_STAGE) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c0 = i * NTHR + 64 * w;  // wave-uniform
-      if (c0 < NCH)
-        __builtin_amdgcn_global_load_lds((const void*)(wimg + min(c0 + lane, NCH - 1)),
-                                         (__attribute__((address_space(3))) void*)(lds + c0 * 8), 16, 0, 0);
+      for (int i = 0; i < PER_STAGE; ++i) {
+        const int c0 = i * NTHR + 64 * w;  // wave-uniform
+        if (c0 < NCH_STAGE)
+          __builtin_amdgcn_global_load_lds((const void*)(wimg + min(c0 + lane, NCH_STAGE - 1)),
+                                           (__attribute__((address_space(3))) void*)(lds + c0 * 8), 16, 0, 0);
+      }
+    } else {  // register staging: loads now, ds_write_b128 after the first record fetch (below)
+#pragma unroll
+      for (int i = 0; i < PER_STAGE; ++i) wst[i] = wimg[min(i * NTHR + tid, NCH_STAGE - 1)];
     }
     // (one launch = one step: the wait for the image and the block barrier come after the first iteration's
     // record fetch below, so the step-counter -> records latency chain runs under the staging instead of after it)
@@ -585,6 +598,11 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   };
   uint4 nu[TBN][2];
   fetch(blockIdx.x, nu);
+  if constexpr (REG_STAGE) {
+#pragma unroll
+    for (int i = 0; i < PER_STAGE; ++i)
+      if (i * NTHR + tid < NCH_STAGE) *(uint4*)(lds + (i * NTHR + tid) * 8) = wst[i];
+  }
   if constexpr (!PERSIST) {  // weight image (LDS-DMA) and the first records landed; wgrad zeroed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -163,16 +163,18 @@ class BertForSequenceClassification(nn.Module):
         tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
         x = self.word(input_ids) + fb.embedding(pos, self.pos.weight)[None] + fb.embedding(tt, self.tok_type.weight)
         drop = self.cfg.dropout if self.training else 0.0
+        rng = self.drop_rng
         if drop > 0:
             self.drop_rng[1:].add_(1)  # new masks every step (captured into the step's hipGraph)
-        x = fb.dropout(self.ln_emb(x), drop, self.drop_rng, 0)
+            rng = fb.rng_snapshot(self.drop_rng)  # this forward's state, shared by all its dropout sites
+        x = fb.dropout(self.ln_emb(x), drop, rng, 0)
         mask = None
         if attention_mask is not None:  # additive key bias [B, S] (fp32; -1e30 on padding keys)
             mask = ((1.0 - attention_mask.float()) * -1e30).contiguous()
         for i, layer in enumerate(self.layers):
-            x = layer(x, mask, self.drop_rng, 1 + 2 * i)
+            x = layer(x, mask, rng, 1 + 2 * i)
         pooled = torch.tanh(self.pooler(x[:, 0]))
-        return self.classifier(fb.dropout(pooled, drop, self.drop_rng, 1 + 2 * len(self.layers)))
+        return self.classifier(fb.dropout(pooled, drop, rng, 1 + 2 * len(self.layers)))
 
 
 def full_init_state(cfg: BertConfig, seed: int) -> dict:

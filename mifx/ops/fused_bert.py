@@ -83,9 +83,22 @@ def keep_mask(n: int, rng: torch.Tensor, site: int, p: float) -> torch.Tensor:
     return torch.from_numpy(keep)
 
 
+def rng_snapshot(rng: torch.Tensor) -> torch.Tensor:
+    """A frozen copy of the [seed, counter] state for one model forward: every dropout site of that forward reads it
+    (forward and recomputed-mask backward), so no site needs its own copy. One device copy per forward instead of
+    one per site (each a ~4.6 us copy node in the captured BERT step: 45 per step)."""
+    snap = rng.detach().clone()
+    snap._mifx_frozen = True
+    return snap
+
+
 def _snap(rng, p) -> torch.Tensor | None:
-    """Device copy of the dropout RNG state taken when the forward runs (None without dropout)."""
-    return rng.detach().clone() if (rng is not None and p > 0) else None
+    """The dropout RNG state as it is when the forward runs (None without dropout): the tensor itself when it is a
+    frozen per-forward snapshot (rng_snapshot), else a device copy (the live counter may advance before the
+    backward: two training forwards before one backward, activation checkpointing)."""
+    if rng is None or p <= 0:
+        return None
+    return rng if getattr(rng, "_mifx_frozen", False) else rng.detach().clone()
 
 
 def device_keep_mask(n: int, rng: torch.Tensor, site: int, p: float, device) -> torch.Tensor:

@@ -17,7 +17,7 @@ def ok(CPA, rot, xor=False):
                             slots.add((t*CPA+cp)%16)
                     if len(slots)<16: return False
     return True
-for CPA in (6,8,12,16):
+for CPA in (6, 8, 12, 16, 24):
     found=None
     for x1,x2,x3 in itertools.product(range(CPA),repeat=3):
         rot=lambda t: (x1*(t&3)+x2*((t>>2)&1)+x3*((t>>3)&3))
