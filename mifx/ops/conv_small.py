@@ -19,10 +19,11 @@ from . import _lib
 from ._lib import I32, VP, check, ptr, sig, stream_handle
 
 # Input channels up to which the VALU direct conv is used: the first layers (1 or 3 channels) of these CNNs, where
-# an MFMA tile has nothing to reduce over. OPT-IN (MIFX_SMALL_CONV=1): measured on MI355X (tools/bench_cnn.py,
-# profiles/cnn_small_conv_r3.jsonl) MIOpen is faster on all but the Fashion CNN -- TPU CNN 1.46 ms/step with its
+# an MFMA tile has nothing to reduce over. Per model by measurement (tools/bench_cnn.py,
+# profiles/cnn_small_conv_r3.jsonl): MIOpen is faster on all but the Fashion CNN -- TPU CNN 1.46 ms/step with its
 # first layer direct (6.8 with every layer direct) vs 1.29, DP-SGD tutorial SGD step 0.67 vs 0.60, PATE teacher 1.75
-# vs 1.60; Fashion 0.43-0.49 vs 0.54.
+# vs 1.60; Fashion 0.43-0.49 vs 0.54, so FashionCNN's conv runs here by default (prefer=True) and the others only
+# with MIFX_SMALL_CONV=1 (MIFX_SMALL_CONV=0 turns every direct conv off).
 MAX_CIN = 4
 MAX_WEIGHTS = 40_000
 
@@ -45,9 +46,12 @@ def _in_functorch_transform() -> bool:
         return False
 
 
-def eligible(x: torch.Tensor, w: torch.Tensor, groups: int = 1, dilation=(1, 1)) -> bool:
-    """MIFX_SMALL_CONV=1 turns the direct kernels on (default: library convolutions, measured faster)."""
-    return (os.environ.get("MIFX_SMALL_CONV", "0") == "1" and x.is_cuda and x.dtype == torch.float32
+def eligible(x: torch.Tensor, w: torch.Tensor, groups: int = 1, dilation=(1, 1), prefer: bool = False) -> bool:
+    """MIFX_SMALL_CONV=1 turns the direct kernels on (default: library convolutions, measured faster), =0 off;
+    unset: on only for layers whose model measured faster on them (prefer=True)."""
+    env = os.environ.get("MIFX_SMALL_CONV")
+    on = env == "1" if env is not None else prefer
+    return (on and x.is_cuda and x.dtype == torch.float32
             and w.dtype == torch.float32 and x.dim() == 4 and groups == 1 and tuple(dilation) == (1, 1)
             and w.shape[1] <= MAX_CIN and w.shape[2] * w.shape[3] <= 64 and w.numel() <= MAX_WEIGHTS
             and not _in_functorch_transform())
@@ -106,13 +110,14 @@ def same_split(h: int, w: int, k: int, s: int) -> tuple[int, int, tuple[int, int
 class SmallConv2d(nn.Conv2d):
     """nn.Conv2d (stride s, symmetric `padding`, or TF SAME with same=True) on the direct HIP kernels for CUDA fp32."""
 
-    def __init__(self, cin, cout, k, stride=1, padding=0, same: bool = False):
+    def __init__(self, cin, cout, k, stride=1, padding=0, same: bool = False, prefer: bool = False):
         super().__init__(cin, cout, k, stride=stride, padding=0 if same else padding)
         self.same = same
+        self.prefer = prefer  # the model measured faster with this layer on the direct kernels (default on)
 
     def forward(self, x):
         s = self.stride[0]
-        if not (eligible(x, self.weight, self.groups, self.dilation) and self.stride[0] == self.stride[1]):
+        if not (eligible(x, self.weight, self.groups, self.dilation, self.prefer) and self.stride[0] == self.stride[1]):
             if self.same:  # the library path exactly as before: explicit SAME pad, unpadded conv
                 ph, pw, extra = same_split(x.shape[-2], x.shape[-1], self.kernel_size[0], s)
                 x = F.pad(x, (pw, pw + extra[1], ph, ph + extra[3]))

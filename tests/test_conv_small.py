@@ -58,3 +58,31 @@ def test_small_cnn_models_match_cpu(monkeypatch):
         ref = m(x)
         got = m.cuda()(x.cuda()).cpu()
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_fashion_prefers_direct_conv_by_default(monkeypatch):
+    """Per-model policy: FashionCNN's conv is on the direct kernels unless MIFX_SMALL_CONV=0; the others opt in."""
+    from mifx.models.cnn import FashionCNN, MnistDPCNN
+    from mifx.ops import conv_small
+
+    monkeypatch.delenv("MIFX_SMALL_CONV", raising=False)
+    assert FashionCNN().conv.prefer and not MnistDPCNN().conv1.prefer
+    x = torch.zeros(2, 1, 28, 28)
+    w = torch.zeros(8, 1, 3, 3)
+    # (CPU tensors are never eligible; the switch logic is what is checked here)
+    assert not conv_small.eligible(x, w, prefer=True)
+    monkeypatch.setenv("MIFX_SMALL_CONV", "0")
+    assert not conv_small.eligible(x, w, prefer=True)
+
+
+@pytest.mark.gpu
+def test_fashion_default_runs_direct_kernel(monkeypatch):
+    from mifx.models.cnn import FashionCNN
+    from mifx.ops import conv_small
+
+    monkeypatch.delenv("MIFX_SMALL_CONV", raising=False)
+    m = FashionCNN().cuda()
+    x = torch.rand(4, 1, 28, 28, device="cuda")
+    assert conv_small.eligible(x, m.conv.weight, prefer=m.conv.prefer)
+    ref = torch.nn.functional.conv2d(x, m.conv.weight, m.conv.bias, 2)
+    torch.testing.assert_close(m.conv(x), ref, rtol=1e-4, atol=1e-4)
