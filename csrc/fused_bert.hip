@@ -625,6 +625,39 @@ __global__ __launch_bounds__(kThreads) void col_reduce2(const float* __restrict_
   if (o1 != nullptr) st(o1 + col, b);
 }
 
+// the same reduction for up to three (partials, output) pairs in ONE launch: blockIdx.y picks the pair (the
+// LayerNorm backward's dw, db and bias-gradient partials; one launch instead of two per LayerNorm backward, and
+// three times the workgroups of the two-buffer form)
+template <typename PO>
+__global__ __launch_bounds__(kThreads) void col_reduce_y(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                        const float* __restrict__ p2, int rows, int N,
+                                                        PO* __restrict__ o0, PO* __restrict__ o1,
+                                                        PO* __restrict__ o2) {
+  __shared__ float sa[kRedSlices][kRedCols];
+  const float* __restrict__ p = blockIdx.y == 0 ? p0 : (blockIdx.y == 1 ? p1 : p2);
+  PO* __restrict__ o = blockIdx.y == 0 ? o0 : (blockIdx.y == 1 ? o1 : o2);
+  const int cx = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int col = blockIdx.x * kRedCols + cx;
+  float a = 0.f;
+  if (col < N) {
+    int r = sl;
+    for (; r + (kRedU - 1) * kRedSlices < rows; r += kRedU * kRedSlices) {
+      float va[kRedU];
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) va[u] = p[(size_t)(r + u * kRedSlices) * N + col];
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) a += va[u];
+    }
+    for (; r < rows; r += kRedSlices) a += p[(size_t)r * N + col];
+  }
+  sa[sl][cx] = a;
+  __syncthreads();
+  if (sl != 0 || col >= N) return;
+  a = 0.f;
+  for (int i = 0; i < kRedSlices; ++i) a += sa[i][cx];
+  st(o + col, a);
+}
+
 // one launch description for the fused [bias +] [dropout +] residual-add + LayerNorm, forward or backward
 struct LnArgs {
   int fwd;
@@ -818,20 +851,14 @@ int mifx_bert_bdaln_bwd(int dtype, int pdt, const void* dy, const void* a, const
   x.st = st;
   const int rc = dispatch_add_ln_any(dtype, pdt, x);
   if (rc) return rc;
-  const dim3 g((H + kRedCols - 1) / kRedCols);
+  const dim3 g((H + kRedCols - 1) / kRedCols, bias != nullptr ? 3 : 2);
   typedef __hip_bfloat16 bf;
-  if (pdt) {
-    hipLaunchKernelGGL(col_reduce2<bf>, g, dim3(kThreads), 0, st, x.dw_part, x.db_part, blocks, H, (bf*)dw, (bf*)db);
-    if (bias != nullptr)
-      hipLaunchKernelGGL(col_reduce2<bf>, g, dim3(kThreads), 0, st, x.dbias_part, nullptr, blocks, H, (bf*)dbias,
-                         (bf*)nullptr);
-  } else {
-    hipLaunchKernelGGL(col_reduce2<float>, g, dim3(kThreads), 0, st, x.dw_part, x.db_part, blocks, H, (float*)dw,
-                       (float*)db);
-    if (bias != nullptr)
-      hipLaunchKernelGGL(col_reduce2<float>, g, dim3(kThreads), 0, st, x.dbias_part, nullptr, blocks, H,
-                         (float*)dbias, (float*)nullptr);
-  }
+  if (pdt)
+    hipLaunchKernelGGL(col_reduce_y<bf>, g, dim3(kThreads), 0, st, x.dw_part, x.db_part, x.dbias_part, blocks, H,
+                       (bf*)dw, (bf*)db, (bf*)dbias);
+  else
+    hipLaunchKernelGGL(col_reduce_y<float>, g, dim3(kThreads), 0, st, x.dw_part, x.db_part, x.dbias_part, blocks, H,
+                       (float*)dw, (float*)db, (float*)dbias);
   return (int)hipGetLastError();
 }
 
