@@ -167,4 +167,21 @@ int mifx_adamw_chunks(void* param, const unsigned long long* gptr, const long lo
   return (int)hipGetLastError();
 }
 
+// the chunk kernel WITHOUT the step advance (a step split into several launches, e.g. per gradient bucket overlapped
+// with the backward: every launch reads the same step, mifx_adamw_advance runs once after all of them)
+int mifx_adamw_chunks_noadv(void* param, const unsigned long long* gptr, const long long* poff, const int* bp,
+                            const int* bo, const int* bn, int nblocks, float* master, float* m, float* v, int* step,
+                            float lr, float beta1, float beta2, float eps, float wd, float grad_scale,
+                            hipStream_t st) {
+  if (nblocks <= 0) return -1;
+  hipLaunchKernelGGL(adamw_chunks, dim3((unsigned)nblocks), dim3(kThreads), 0, st, (__hip_bfloat16*)param, gptr, poff,
+                     bp, bo, bn, master, m, v, step, lr, beta1, beta2, eps, wd, grad_scale);
+  return (int)hipGetLastError();
+}
+
+int mifx_adamw_advance(int* step, hipStream_t st) {
+  hipLaunchKernelGGL(advance_step, dim3(1), dim3(1), 0, st, step);
+  return (int)hipGetLastError();
+}
+
 }  // extern "C"

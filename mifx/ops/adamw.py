@@ -21,7 +21,10 @@ def _fns_chunks():
     lib = _lib.load("adamw")
     return {"chunk": sig(lib, "mifx_adamw_chunk_size", []),
             "run": sig(lib, "mifx_adamw_chunks", [VP, VP, VP, VP, VP, VP, I32, VP, VP, VP, VP, F32, F32, F32, F32,
-                                                  F32, F32, VP])}
+                                                  F32, F32, VP]),
+            "run_noadv": sig(lib, "mifx_adamw_chunks_noadv", [VP, VP, VP, VP, VP, VP, I32, VP, VP, VP, VP, F32, F32,
+                                                              F32, F32, F32, F32, VP]),
+            "advance": sig(lib, "mifx_adamw_advance", [VP, VP])}
 
 
 def chunk_size() -> int:
@@ -31,14 +34,15 @@ def chunk_size() -> int:
 def adamw_chunks_(param: torch.Tensor, gptr: torch.Tensor, poff: torch.Tensor, bp: torch.Tensor, bo: torch.Tensor,
                   bn: torch.Tensor, master: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: torch.Tensor,
                   lr: float, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0,
-                  grad_scale: float = 1.0) -> None:
+                  grad_scale: float = 1.0, advance: bool = True) -> None:
     """AdamW over flat bf16 weights / fp32 master+moments with each parameter's gradient read from its own
     tensor: gptr [P] uint64 device addresses (0 = no grad), poff [P] int64 flat offsets (multiples of 8),
-    bp/bo/bn [nblocks] int32 chunk -> (parameter, element offset, length). See FlatAdamW."""
+    bp/bo/bn [nblocks] int32 chunk -> (parameter, element offset, length). See FlatAdamW. advance=False leaves the
+    step counter (adamw_advance_ once after all launches of a split step)."""
     assert param.dtype == torch.bfloat16 and master.dtype == m.dtype == v.dtype == torch.float32
     assert gptr.dtype == torch.int64 and poff.dtype == torch.int64 and step.dtype == torch.int32
     assert bp.dtype == bo.dtype == bn.dtype == torch.int32 and bp.numel() == bo.numel() == bn.numel()
-    check(_fns_chunks()["run"](ptr(param), ptr(gptr), ptr(poff), ptr(bp), ptr(bo), ptr(bn), int(bp.numel()),
+    check(_fns_chunks()["run" if advance else "run_noadv"](ptr(param), ptr(gptr), ptr(poff), ptr(bp), ptr(bo), ptr(bn), int(bp.numel()),
                                ptr(master), ptr(m), ptr(v), ptr(step), float(lr), float(beta1), float(beta2),
                                float(eps), float(weight_decay), float(grad_scale), stream_handle(param.device)),
           "mifx_adamw_chunks")
@@ -64,3 +68,7 @@ def adamw_flat_(param: torch.Tensor, grad: torch.Tensor, master: torch.Tensor, m
     master.mul_(1 - lr * weight_decay).addcdiv_(m, v.sqrt() / bc2 ** 0.5 + eps, value=-lr / bc1)
     param.copy_(master.to(param.dtype))
     step.add_(1)
+
+
+def adamw_advance_(step: torch.Tensor) -> None:
+    check(_fns_chunks()["advance"](ptr(step), stream_handle(step.device)), "mifx_adamw_advance")

@@ -136,6 +136,8 @@ class BertTrainer:
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
+        if hasattr(self.opt, "begin_capture"):  # FlatAdamW: bucket updates overlapped with the backward
+            self.opt.begin_capture()
         with torch.cuda.graph(self.graph):
             self.static_loss = self._eager_step()
 

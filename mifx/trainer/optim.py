@@ -7,6 +7,9 @@ exactly (no epsilon), as does the fused HIP optimizer in csrc/wide_deep.hip.
 """
 from __future__ import annotations
 
+import functools
+import os
+
 import torch
 
 
@@ -80,7 +83,8 @@ class FlatAdamW:
         per `zero_grad()`); the flat kernel is then hipGraph-capturable (device-side step counter)."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 dtype: torch.dtype = torch.bfloat16, grads: str | None = None):
+                 dtype: torch.dtype = torch.bfloat16, grads: str | None = None, overlap: bool | None = None,
+                 bucket_elems: int = 8 << 20):
         self.params = [p for p in params if p.requires_grad]
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         dev = self.params[0].device
@@ -126,6 +130,82 @@ class FlatAdamW:
             self._capture_host = torch.zeros(len(self.params), dtype=torch.int64).pin_memory()
             self._addr = None
             self.bp, self.bo, self.bn = (torch.tensor(x, dtype=torch.int32, device=dev) for x in (bp, bo, bn))
+            # overlap (opt-in: overlap=True or MIFX_ADAMW_OVERLAP=1): in a CAPTURED step, the update of each bucket of
+            # ~bucket_elems consecutive parameters is launched on a side stream as soon as autograd has accumulated
+            # the last gradient of the bucket (post-accumulate-grad hooks), so the memory-bound update of layer L
+            # runs under the compute-bound backward of layers < L; step() launches what is left, joins the side
+            # stream and advances the step counter once. Every bucket reads the same step value, so the update is
+            # the single-launch update, bucket by bucket (same kernel, same per-element math). Measured SLOWER in the
+            # BERT-base step (7.18 vs 6.38 ms on MI355X, profiles/bert_adamw_overlap_r3.txt): the bucket launches fill
+            # every CU with memory-bound blocks beside the backward's one-workgroup-per-CU GEMMs, which lose more
+            # than the ~0.5 ms update that is hidden.
+            if overlap is None:
+                overlap = os.environ.get("MIFX_ADAMW_OVERLAP", "0") == "1"
+            self.overlap = bool(overlap)
+            if self.overlap:
+                self._buckets, cur, acc = [], [], 0
+                for i, p in enumerate(self.params):
+                    cur.append(i)
+                    acc += p.numel()
+                    if acc >= bucket_elems:
+                        self._buckets.append(cur)
+                        cur, acc = [], 0
+                if cur:
+                    self._buckets.append(cur)
+                self._bucket_of = {i: b for b, idx in enumerate(self._buckets) for i in idx}
+                self._bchunks = []
+                for idx in self._buckets:
+                    sel = [k for k, pi in enumerate(bp) if idx[0] <= pi <= idx[-1]]
+                    self._bchunks.append(tuple(torch.tensor([x[k] for k in sel], dtype=torch.int32, device=dev)
+                                               for x in (bp, bo, bn)))
+                self._ov_host = torch.zeros(len(self.params), dtype=torch.int64).pin_memory()
+                self._ov_side = torch.cuda.Stream(dev)
+                self._ov_ready = [0] * len(self._buckets)
+                self._ov_launched = [False] * len(self._buckets)
+                self._ov_active = False
+                self._ov_captured = False
+                for i, p in enumerate(self.params):
+                    p.register_post_accumulate_grad_hook(functools.partial(self._on_grad, i))
+
+    # ---------------------------------------------------------------- overlapped update (captured steps)
+    def _on_grad(self, i: int, p: torch.Tensor) -> None:
+        if not (self._ov_active and torch.cuda.is_current_stream_capturing()):
+            return
+        b = self._bucket_of[i]
+        self._ov_ready[b] += 1
+        if self._ov_ready[b] == len(self._buckets[b]) and not self._ov_launched[b]:
+            self._launch_bucket(b)
+
+    def _launch_bucket(self, b: int) -> None:
+        from ..ops.adamw import adamw_chunks_
+
+        idx = self._buckets[b]
+        i0, i1 = idx[0], idx[-1] + 1
+        host = self._ov_host.numpy()
+        for i in idx:
+            g = self.params[i].grad
+            if g is not None and (g.dtype != torch.bfloat16 or not g.is_contiguous() or g.device != self.flat.device):
+                raise RuntimeError("FlatAdamW(grads='own') needs contiguous bf16 gradients on the parameter's device")
+            host[i] = 0 if g is None else g.data_ptr()
+        cur = torch.cuda.current_stream(self.flat.device)
+        self._ov_side.wait_stream(cur)  # the bucket's gradients (and the backward kernels that read its weights)
+        with torch.cuda.stream(self._ov_side):
+            # captured H2D copy: reads the pinned table on every replay (the captured gradients keep their
+            # addresses, so the table is written once, here)
+            self._gptr[i0:i1].copy_(self._ov_host[i0:i1], non_blocking=True)
+            bpb, bob, bnb = self._bchunks[b]
+            adamw_chunks_(self.flat, self._gptr, self.poff, bpb, bob, bnb, self.master, self.m, self.v,
+                          self.step_count, self.lr, self.betas[0], self.betas[1], self.eps, self.wd, advance=False)
+        self._ov_launched[b] = True
+
+    def begin_capture(self) -> None:
+        """Arm the overlapped update for the step about to be captured (one captured step per optimizer)."""
+        if self.mode == "own" and self.overlap:
+            if self._ov_captured:
+                raise RuntimeError("FlatAdamW overlap: one captured step per optimizer")
+            self._ov_ready = [0] * len(self._buckets)
+            self._ov_launched = [False] * len(self._buckets)
+            self._ov_active = True
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         if self.mode == "own":
@@ -148,6 +228,17 @@ class FlatAdamW:
                 raise RuntimeError("FlatAdamW(grads='own') needs contiguous bf16 gradients on the parameter's device")
             addr.append(0 if g is None else g.data_ptr())
         addr = tuple(addr)
+        if self.overlap and self._ov_active and torch.cuda.is_current_stream_capturing():
+            from ..ops.adamw import adamw_advance_
+
+            for b in range(len(self._buckets)):  # buckets whose last gradient never arrived (unused parameters)
+                if not self._ov_launched[b]:
+                    self._launch_bucket(b)
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._ov_side)
+            adamw_advance_(self.step_count)
+            self._ov_active, self._ov_captured = False, True
+            self._capture_host = None
+            return
         if torch.cuda.is_current_stream_capturing():
             # hipGraph capture: no pinned allocation is allowed here, so the table goes through the pinned
             # buffer reserved at construction; the captured copy reads it on every replay, so it is never

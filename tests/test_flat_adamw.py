@@ -74,3 +74,49 @@ def test_flat_adamw_own_grads_matches_views_mode():
     assert int(ob.step_count) == 4 and all(p.grad is not None for p in mb.parameters())
     ob.zero_grad()
     assert all(p.grad is None for p in mb.parameters())
+
+
+@pytest.mark.gpu
+def test_overlapped_bucket_update_in_captured_step_is_bit_identical():
+    """grads='own' with overlap: in a captured step each parameter bucket's update is launched on a side stream from
+    the post-accumulate-grad hook of its last gradient (under the rest of the backward), the step counter advanced
+    once at the end. After graph replays the weights must equal the single-launch update bit for bit; an unused
+    parameter (never gets a gradient) is left untouched."""
+    def make():
+        torch.manual_seed(1)
+        return torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.GELU(), torch.nn.Linear(7, 20000),
+                                   torch.nn.Linear(20000, 3), torch.nn.Linear(3, 9)).cuda().bfloat16()
+
+    x = torch.randn(64, 5, device="cuda", dtype=torch.bfloat16)
+    out = []
+    for overlap in (False, True):
+        m = make()
+        unused = torch.nn.Parameter(torch.ones(13, device="cuda", dtype=torch.bfloat16))
+        o = FlatAdamW(list(m.parameters()) + [unused], lr=1e-3, weight_decay=0.01, grads="own", overlap=overlap,
+                      bucket_elems=4096)  # several buckets of whole parameters
+        if overlap:
+            assert len(o._buckets) > 2
+
+        def step():
+            o.zero_grad()
+            m(x).float().pow(2).mean().backward()
+            o.step()
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        o.zero_grad()
+        o.begin_capture()
+        with torch.cuda.graph(g):
+            step()
+        for _ in range(5):
+            g.replay()
+        torch.cuda.synchronize()
+        assert int(o.step_count) == 2 + 5  # (capturing records the step, it does not run it)
+        assert torch.equal(unused.detach(), torch.ones_like(unused))
+        out.append(o.flat.clone())
+    assert torch.equal(out[0], out[1])
