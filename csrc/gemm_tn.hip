@@ -61,7 +61,7 @@ __device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
 }
 
 // OUT_F32: store the fp32 partial of split blockIdx.y at P + blockIdx.y * M * N (else bf16 C directly).
-// OPT bit 0: raise the wave priority around each MFMA block.
+// OPT bit 0: raise the wave priority around each MFMA block (bit 1 in the config table: the 8-wave gemm_tn_k2).
 template <int BM, int BN, bool OUT_F32, int OPT, int NS>
 __global__ __launch_bounds__(256) void gemm_tn(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                   bf16* __restrict__ C, float* __restrict__ P, int M, int N, int T,
@@ -205,6 +205,132 @@ __global__ __launch_bounds__(256) void gemm_tn(const bf16* __restrict__ A, const
   }
 }
 
+// Measured (profiles/gemm_tn_r3b_k2.jsonl): 50 us on FFN-in's dW at S = 1 against 54 for the 4-wave deep ring and
+// 38 for two 4-wave workgroups per CU with a 2-way token split -- two independent barrier pipelines per CU beat one
+// 8-wave pipeline, so the tuned table keeps the split; this form stays selectable (config 18).
+// 8-wave form of the 96 x 96 tile (one workgroup per CU, two waves per SIMD, no token split across workgroups):
+// waves w and w + 4 own the same 48 x 48 quadrant and take the two 32-token k-steps of every K-tile, so each SIMD
+// runs two independent MFMA chains (the one-wave-per-SIMD 4-wave form idles at every barrier and fragment read);
+// the k-step-1 waves hand their accumulators to the k-step-0 waves through LDS at the end (fixed order: k-step 0
+// + k-step 1). DMA: each K-tile's 12 + 12 wave-instructions are dealt 2 + 1 / 1 + 2 to waves 0-3 / 4-7 (3 each, so
+// the counted vmcnt is the same for every wave).
+template <bool OUT_F32, int NS>
+__global__ __launch_bounds__(512) void gemm_tn_k2(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                 bf16* __restrict__ C, float* __restrict__ P, int M, int N, int T,
+                                                 int tps) {
+  constexpr int BM = 96, BN = 96, TM = 48, TN = 48, MR = 3, NR = 3, CPA = 12, CPB = 12;
+  constexpr int ABYTES = BK * BM * 2, BBYTES = BK * BN * 2, BUF = ABYTES + BBYTES;
+  constexpr int G = 3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int qd = w & 3, kg = w >> 2, wm = qd >> 1, wn = qd & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  constexpr int GM = 4;
+  const int nb_m = M / BM, nb_n = N / BN, per_group = GM * nb_n;
+  const int group = tile / per_group, first_m = group * GM, gsz = min(GM, nb_m - first_m);
+  const int wi = tile - group * per_group;
+  const int m0 = (first_m + wi % gsz) * BM, n0 = (wi / gsz) * BN;
+  const int t_begin = blockIdx.y * tps, KT = tps / BK;
+  // this wave's 3 DMA wave-instructions: (operand, instruction index) -> LDS slots [64 i, 64 i + 64)
+  int doff[G], dslot[G];
+  bool dis_a[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    // waves 0-3: A {w, w + 8}, B {w + 4}; waves 4-7: A {w}, B {w - 4, w + 4}
+    const bool isa = kg == 0 ? j < 2 : j == 0;
+    const int i = isa ? w + 8 * j : (kg == 0 ? w + 4 : (w - 4) + 8 * (j - 1));
+    const int sl = 64 * i + lane, t = sl / 12, pp = sl % 12;
+    int c = pp - rot<12>(t);
+    c = c < 0 ? c + 12 : c;
+    dis_a[j] = isa;
+    dslot[j] = 64 * i;
+    doff[j] = isa ? t * M + m0 + 8 * c : t * N + n0 + 8 * c;
+  }
+  auto issue = [&](int kt, int buf) {
+    unsigned char* ba = lds + buf * BUF;
+    const size_t t0 = (size_t)(t_begin + kt * BK);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const bf16* src = dis_a[j] ? A + t0 * M + doff[j] : B + t0 * N + doff[j];
+      unsigned char* dst = dis_a[j] ? ba + dslot[j] * 16 : ba + ABYTES + dslot[j] * 16;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  v4f acc[MR][NR];
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b) acc[a][b] = (v4f){0.f, 0.f, 0.f, 0.f};
+  const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+  const int t1 = 32 * kg + 8 * h + q, t2 = t1 + 4;
+  int ao1[MR], ao2[MR], bo1[NR], bo2[NR];  // byte offsets of this lane's fragment reads inside a buffer
+#pragma unroll
+  for (int a = 0; a < MR; ++a) {
+    const int c = (wm * TM + 16 * a) / 8 + (p >> 1);
+    ao1[a] = (t1 * CPA + slot_of<CPA>(t1, c)) * 16 + 8 * (p & 1);
+    ao2[a] = (t2 * CPA + slot_of<CPA>(t2, c)) * 16 + 8 * (p & 1);
+  }
+#pragma unroll
+  for (int b = 0; b < NR; ++b) {
+    const int c = (wn * TN + 16 * b) / 8 + (p >> 1);
+    bo1[b] = ABYTES + (t1 * CPB + slot_of<CPB>(t1, c)) * 16 + 8 * (p & 1);
+    bo2[b] = ABYTES + (t2 * CPB + slot_of<CPB>(t2, c)) * 16 + 8 * (p & 1);
+  }
+  constexpr int INFL = (NS - 2) * G;
+  constexpr int WAIT_STEADY = (INFL & 15) | (7 << 4) | (15 << 8) | ((INFL >> 4) << 14);
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < KT) issue(i, i);
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + NS - 2 <= KT - 1)
+      __builtin_amdgcn_s_waitcnt(WAIT_STEADY);
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const unsigned char* bf = lds + (kt % NS) * BUF;
+    v8bf af[MR], bfr[NR];
+#pragma unroll
+    for (int a = 0; a < MR; ++a) af[a] = cat8(tr_read(bf + ao1[a]), tr_read(bf + ao2[a]));
+#pragma unroll
+    for (int b = 0; b < NR; ++b) bfr[b] = cat8(tr_read(bf + bo1[b]), tr_read(bf + bo2[b]));
+#pragma unroll
+    for (int a = 0; a < MR; ++a)
+#pragma unroll
+      for (int b = 0; b < NR; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+  }
+  // k-step-1 waves -> LDS -> k-step-0 waves add (every buffer is free once all waves passed this barrier)
+  __syncthreads();
+  v4f* red = (v4f*)lds;
+  if (kg == 1) {
+#pragma unroll
+    for (int a = 0; a < MR; ++a)
+#pragma unroll
+      for (int b = 0; b < NR; ++b) red[((qd * MR + a) * NR + b) * 64 + lane] = acc[a][b];
+  }
+  __syncthreads();
+  if (kg == 1) return;
+#pragma unroll
+  for (int a = 0; a < MR; ++a) {
+    const int m = m0 + wm * TM + 16 * a + r;
+#pragma unroll
+    for (int b = 0; b < NR; ++b) {
+      const v4f o4 = acc[a][b] + red[((qd * MR + a) * NR + b) * 64 + lane];
+      const int n = n0 + wn * TN + 16 * b + 4 * h;
+      if constexpr (OUT_F32) {
+        *(v4f*)(P + (size_t)blockIdx.y * M * N + (size_t)m * N + n) = o4;
+      } else {
+        v4bf o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)o4[i];
+        *(v4bf*)(C + (size_t)m * N + n) = o;
+      }
+    }
+  }
+}
+
 // C = bf16(sum over s of P[s]) in split order; 8 elements per thread
 __global__ __launch_bounds__(256) void splits_sum(const float4* __restrict__ P, int S, long long n8, v8bf* __restrict__ C) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -236,13 +362,36 @@ int launch(const void* A, const void* B, void* C, float* P, int M, int N, int T,
   return (int)hipGetLastError();
 }
 
+template <bool OUT_F32>
+int launch_k2(const void* A, const void* B, void* C, float* P, int M, int N, int T, int S, hipStream_t st) {
+  constexpr int BUF = 2 * 96 * BK * 2, NS = 6, LDS = NS * BUF;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_tn_k2<OUT_F32, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_tn_k2<OUT_F32, NS>), dim3((M / 96) * (N / 96), S), dim3(512), LDS, st, (const bf16*)A,
+                     (const bf16*)B, (bf16*)C, P, M, N, T, T / S);
+  return (int)hipGetLastError();
+}
+
+int dispatch_k2(const void* A, const void* B, void* C, float* P, int M, int N, int T, int S, hipStream_t st) {
+  if (S == 1) return launch_k2<false>(A, B, C, nullptr, M, N, T, 1, st);
+  const int rc = launch_k2<true>(A, B, nullptr, P, M, N, T, S, st);
+  if (rc != 0) return rc;
+  const long long n8 = (long long)M * N / 8;
+  hipLaunchKernelGGL(splits_sum, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, (const float4*)P, S, n8,
+                     (v8bf*)C);
+  return (int)hipGetLastError();
+}
+
 struct Cfg {
   int bm, bn, opt, ns;
 };
 constexpr Cfg kCfgs[] = {{96, 96, 0, 0},  {96, 96, 1, 0},   {128, 128, 0, 0}, {128, 96, 0, 0}, {96, 128, 0, 0},
                          {64, 64, 0, 0},  {128, 64, 0, 0},  {64, 128, 0, 0},  {96, 96, 0, 3},  {96, 96, 0, 2},
                          {128, 128, 0, 2}, {128, 128, 0, 3}, {64, 64, 0, 3},   {128, 64, 0, 3}, {64, 128, 0, 3},
-                         {192, 192, 0, 3}, {192, 96, 0, 3},  {96, 192, 0, 3}};
+                         {192, 192, 0, 3}, {192, 96, 0, 3},  {96, 192, 0, 3},  {96, 96, 2, 6}};
 
 template <int BM, int BN, int OPT, int NS0 = 0>
 int dispatch(const void* A, const void* B, void* C, float* P, int M, int N, int T, int S, hipStream_t st) {
@@ -301,7 +450,8 @@ int mifx_gemm_tn(int cfg, const void* A, const void* B, void* C, float* P, int M
     case 14: return dispatch<64, 128, 0, 3>(A, B, C, P, M, N, T, S, st);
     case 15: return dispatch<192, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
     case 16: return dispatch<192, 96, 0, 3>(A, B, C, P, M, N, T, S, st);
-    default: return dispatch<96, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
+    case 17: return dispatch<96, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
+    default: return dispatch_k2(A, B, C, P, M, N, T, S, st);  // 18: 8 waves, k-steps split over wave pairs
   }
 }
 

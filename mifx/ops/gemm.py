@@ -235,7 +235,7 @@ def pick_tn(M: int, N: int, T: int, cus: int = 256) -> tuple[int, int] | None:
         return TN_TUNED[(M, N, T)]
     best, best_score = None, None
     for i, (bm, bn, opt) in enumerate(tn_configs()):
-        if M % bm or N % bn or T % 64 or opt % 16:
+        if M % bm or N % bn or T % 64 or opt % 16:  # (the heuristic picks among the plain 4-wave forms)
             continue
         tiles = (M // bm) * (N // bn)
         s = 1
