@@ -868,14 +868,19 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       if (s1_live) ta.s1[w0 + c] = a1;
     }
   } else if (TRAIN) {
-    float* my = slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD);
-    for (int c = tid; c < WIDE_PAD; c += NTHR) {
-      float v = (float)wgi[c] * qinv;
-      if (c == WIDE_BIAS) {
+    // 16-byte stores (stride and WIDE_PAD are multiples of 4 floats; the histogram sits 16-B aligned in LDS)
+    static_assert(WIDE_PAD % 4 == 0 && (LSEND * 2) % 16 == 0, "vector wide-gradient epilogue");
+    float4* my4 = (float4*)(slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD));
+    const int4* wgi4 = (const int4*)wgi;
+    for (int c4 = tid; c4 < WIDE_PAD / 4; c4 += NTHR) {
+      const int4 qv = wgi4[c4];
+      float4 v = make_float4((float)qv.x * qinv, (float)qv.y * qinv, (float)qv.z * qinv, (float)qv.w * qinv);
+      static_assert(WIDE_BIAS % 4 == 3, "bias column is the .w lane of its float4");
+      if (c4 == WIDE_BIAS / 4) {  // the wave sums added one by one onto the bias column, in wave order
 #pragma unroll
-        for (int i = 0; i < NWAVE; ++i) v += red[NWAVE + i];
+        for (int i = 0; i < NWAVE; ++i) v.w += red[NWAVE + i];
       }
-      my[c] = v;
+      my4[c4] = v;
     }
   }
   if (tid == 0 && slab_loss) {
