@@ -168,8 +168,9 @@ def main(argv=None) -> int:
     ap.add_argument("--ref-steps", type=int, default=2000)
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--steps-per-graph", type=int, default=10,
-                    help="consecutive training steps captured in one hipGraph (single rank / captured collective)")
+    ap.add_argument("--steps-per-graph", type=int, default=20,
+                    help="consecutive training steps captured in one hipGraph (single rank / captured collective); "
+                         "20 measured best at the driver's 20 timed steps (profiles/bench_spg_sweep_r3.txt)")
     ap.add_argument("--dp", choices=("xgmi", "direct", "captured", "split"), default="xgmi",
                     help="multi-rank gradient exchange: xgmi (one-shot peer reads, whole step in hipGraphs; falls "
                          "back to direct if its validation fails), direct (eager + ncclAllReduce on the compute "
