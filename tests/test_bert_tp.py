@@ -11,6 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from mifx.models.bert import BertConfig, BertForSequenceClassification, full_init_state, gather_full_state, num_params
+from mifx.ops import fused_bert as fb_mod
 from mifx.parallel.tensor_parallel import TPGroup, head_partition, split_sizes
 
 
@@ -427,3 +428,40 @@ def test_dropout_backward_uses_forward_time_rng_snapshot():
     y.backward(torch.ones_like(y))
     keep = (y.detach() != 0).float()
     torch.testing.assert_close(x.grad, keep / 0.7, rtol=1e-6, atol=1e-6)
+
+
+def test_rng_snapshot_shared_by_the_sites_of_one_forward():
+    """One frozen [seed, counter] snapshot per model forward: every dropout site keeps that tensor (no per-site copy),
+    a live (mutable) state tensor is still copied at forward time, and advancing the live counter afterwards does not
+    change what the snapshot holds (the masks recomputed in backward stay the forward's)."""
+    from mifx.ops import fused_bert as fb
+
+    live = torch.tensor([1234, 7], dtype=torch.int64)
+    snap = fb.rng_snapshot(live)
+    assert fb._snap(snap, 0.1) is snap
+    copy = fb._snap(live, 0.1)
+    assert copy is not live and torch.equal(copy, live)
+    assert fb._snap(live, 0.0) is None and fb._snap(None, 0.1) is None
+    live[1:].add_(1)
+    assert int(snap[1]) == 7 and int(copy[1]) == 7
+
+
+def test_model_forward_uses_one_snapshot_per_step():
+    cfg = BertConfig.tiny(dropout=0.1)
+    m = BertForSequenceClassification(cfg, seed=0)
+    m.train()
+    ids = torch.randint(0, cfg.vocab_size, (2, 8))
+    seen = []
+    orig = fb_mod.dropout
+
+    def spy(x, p, rng, site):
+        seen.append(rng)
+        return orig(x, p, rng, site)
+
+    fb_mod.dropout = spy
+    try:
+        m(ids)
+    finally:
+        fb_mod.dropout = orig
+    assert len(seen) == 2 and seen[0] is seen[1] and getattr(seen[0], "_mifx_frozen", False)
+    assert int(seen[0][1]) == int(m.drop_rng[1]) == 1
