@@ -1,6 +1,8 @@
 #!/bin/bash
 # Same-box A/B of the W&D bench between this tree and a built copy of another revision in ./ab_old (git archive +
-# build), alternating processes; prints us/step at B=65536 and at the reference batch.
+# build: mkdir ab_old && git archive REV | tar -x -C ab_old && (cd ab_old && python -c "import __graft_entry__ as g; g.build()"));
+# alternating processes; prints us/step at B=65536 and at the reference batch. Delete ab_old afterwards (it is
+# git-ignored but travels with every gpurun call while it exists).
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
