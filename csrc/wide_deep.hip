@@ -880,7 +880,8 @@ struct XgPeers {
 // (One kernel with a last-arriver finalizer measured slower, 12.9 us vs 5.0 + 6.0: its chain of write-through
 // stores, counter atomic and partial loads is longer than a kernel boundary.)
 constexpr int XMAX = 16;  // XCC_ID range
-constexpr int X1C = 64;   // float4 columns per level-1 workgroup (1 KB of each slab row)
+constexpr int X1C = 64;   // float4 columns per level-1 workgroup (1 KB of each slab row): one per lane of a wave
+static_assert(X1C == 64, "wd_reduce_xcd maps lane -> float4 column of its chunk");
 
 __global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ slab, int G, int stride,
                                                      const int* __restrict__ xcd_of, float4* __restrict__ part,
