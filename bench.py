@@ -80,6 +80,39 @@ def _post_run_ok(tr, n: int, use_cuda: bool) -> tuple[bool, bool | None]:
     return flag.item() == 0.0 and agree, agree
 
 
+def gradient_check(batch: int, device, seed: int) -> float:
+    """Outside the timed region: ONE training step through the same kernels the benchmark times (fused fwd/bwd,
+    XCD-local slab reduction, slab-order optimizer) with plain SGD at lr 1, so the weight change IS the summed
+    gradient, against fp32 PyTorch autograd of the same model on the same records. Returns the largest relative
+    Frobenius error over the parameter tensors: the bf16 data path costs a few % (tests/test_wide_deep.py); a
+    broken reduction, exchange or optimizer shows up as O(1)."""
+    import numpy as np
+
+    from mifx.models import wide_deep as wdm
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer, OptSpec
+
+    recs = synthetic_records(batch, device=device, seed=seed)
+    tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device=device, dnn_opt=OptSpec("sgd", lr=1.0),
+                              wide_opt=OptSpec("sgd", lr=1.0))
+    tr.set_data(recs)
+    before = tr.param.double().cpu()
+    tr.step()
+    torch.cuda.synchronize(device)
+    g = (before - tr.param.double().cpu()).float().numpy()
+    got = wdm.canonical_grad_to_torch(g, tr.model, np.arange(g.size))
+    ref_model = wdm.unpack_canonical(before.float(), WideDeepModel(seed=0))
+    dense, ids, label = wdm.records_to_tensors(recs.cpu())
+    ref_model.zero_grad()
+    ref_model.loss(dense, ids, label, reduction="sum").backward()
+    worst = 0.0
+    for name, prm in ref_model.named_parameters():
+        r = prm.grad.detach().numpy()
+        gk = np.asarray(got[name]).reshape(r.shape)
+        worst = max(worst, float(np.linalg.norm(gk - r) / (np.linalg.norm(r) + 1e-8)))
+    del tr
+    return worst
+
+
 def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, dp: str = "xgmi",
                  steps_per_graph: int = 10):
     def build():
@@ -222,6 +255,11 @@ def main(argv=None) -> int:
     r = measure(a.batch_per_gpu, 1234 + env.rank, a.data_per_gpu, a.steps, a.warmup)
     dt, dp_path, spg, ranks_agree, loss = r["dt"], r["dp_path"], r["spg"], r["agree"], r["loss"]
     value = a.batch_per_gpu * n * a.steps / dt
+    grad_err = None
+    if use_cuda and env.is_main:  # after the timed region: the kernel's gradient vs fp32 autograd on one batch
+        grad_err = gradient_check(a.batch_per_gpu, device, 4321)
+        if not grad_err < 0.1:
+            raise SystemExit(f"[bench] gradient check failed: relative error {grad_err:.3g} vs fp32 autograd")
 
     ref = None
     if a.ref_batch:
@@ -253,7 +291,8 @@ def main(argv=None) -> int:
                        "steps_per_graph": spg,
                        "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
                        "dp_exchange": dp_path,
-                       "replicas_bit_identical": ranks_agree, "validated_after_timed_region": True},
+                       "replicas_bit_identical": ranks_agree, "validated_after_timed_region": True,
+                       "grad_check_max_rel_err_vs_fp32": grad_err},
             "final_mean_loss": loss,
             "reference_batch": ref,
         }
