@@ -391,7 +391,8 @@ struct Cfg {
 constexpr Cfg kCfgs[] = {{96, 96, 0, 0},  {96, 96, 1, 0},   {128, 128, 0, 0}, {128, 96, 0, 0}, {96, 128, 0, 0},
                          {64, 64, 0, 0},  {128, 64, 0, 0},  {64, 128, 0, 0},  {96, 96, 0, 3},  {96, 96, 0, 2},
                          {128, 128, 0, 2}, {128, 128, 0, 3}, {64, 64, 0, 3},   {128, 64, 0, 3}, {64, 128, 0, 3},
-                         {192, 192, 0, 3}, {192, 96, 0, 3},  {96, 192, 0, 3},  {96, 96, 2, 6}};
+                         {192, 192, 0, 3}, {192, 96, 0, 3},  {96, 192, 0, 3},  {96, 96, 2, 6},  {96, 96, 1, 2},
+                         {128, 128, 1, 2}};
 
 template <int BM, int BN, int OPT, int NS0 = 0>
 int dispatch(const void* A, const void* B, void* C, float* P, int M, int N, int T, int S, hipStream_t st) {
@@ -451,7 +452,9 @@ int mifx_gemm_tn(int cfg, const void* A, const void* B, void* C, float* P, int M
     case 15: return dispatch<192, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
     case 16: return dispatch<192, 96, 0, 3>(A, B, C, P, M, N, T, S, st);
     case 17: return dispatch<96, 192, 0, 3>(A, B, C, P, M, N, T, S, st);
-    default: return dispatch_k2(A, B, C, P, M, N, T, S, st);  // 18: 8 waves, k-steps split over wave pairs
+    case 18: return dispatch_k2(A, B, C, P, M, N, T, S, st);  // 8 waves, k-steps split over wave pairs
+    case 19: return dispatch<96, 96, 1, 2>(A, B, C, P, M, N, T, S, st);
+    default: return dispatch<128, 128, 1, 2>(A, B, C, P, M, N, T, S, st);
   }
 }
 

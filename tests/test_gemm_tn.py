@@ -21,7 +21,7 @@ def _check(T, M, N, cfg=None, splits=None, seed=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", range(19))
+@pytest.mark.parametrize("cfg", range(21))
 def test_every_config(cfg):
     bm, bn, _ = gemm.tn_configs()[cfg]
     _check(512, 2 * bm, 3 * bn, cfg, 1)

@@ -53,7 +53,7 @@ def main():
             if M % bm or N % bn:
                 continue
             for s in (1, 2, 4, 8):
-                if T % (64 * s) or (M // bm) * (N // bn) * s > 1024 or (opt & 1):
+                if T % (64 * s) or (M // bm) * (N // bn) * s > 1024 or (opt & 2):
                     continue
                 out = gemm.gemm_tn(dy, x, cfg, s)
                 err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
