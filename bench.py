@@ -199,6 +199,9 @@ def main(argv=None) -> int:
                     help="throughput batch per replica (BASELINE.md protocol: 8K-64K); 40 = reference batch")
     ap.add_argument("--ref-batch", type=int, default=40, help="also time the reference batch (0 = skip)")
     ap.add_argument("--ref-steps", type=int, default=2000)
+    ap.add_argument("--ref-steps-per-graph", type=int, default=100,
+                    help="steps per hipGraph for the reference-batch run (its 2000 steps amortise graph boundaries; "
+                         "profiles/bench_ref_spg_sweep_r3.txt)")
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--steps-per-graph", type=int, default=20,
@@ -226,13 +229,13 @@ def main(argv=None) -> int:
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     n = env.world_size
 
-    def measure(batch, seed, n_data, steps, warmup):
+    def measure(batch, seed, n_data, steps, warmup, spg_req=None):
         """Build, time `steps` steps, validate after the timed region. A multi-rank xGMI run that fails the
         post-run validation (a timed-out wait, replicas that differ) is discarded and re-measured on the direct
         RCCL path; a failing direct run fails the benchmark (no number from a broken step)."""
         dp = a.dp
         while True:
-            tr = make_trainer(batch, device, pg, seed, n_data, not a.no_graph, dp, a.steps_per_graph)
+            tr = make_trainer(batch, device, pg, seed, n_data, not a.no_graph, dp, spg_req or a.steps_per_graph)
             spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
             dt = mdist.max_over_ranks(run(tr, steps, warmup, device), device if use_cuda else None)
             ok, agree = _post_run_ok(tr, n, use_cuda)
@@ -263,7 +266,8 @@ def main(argv=None) -> int:
 
     ref = None
     if a.ref_batch:
-        r2 = measure(a.ref_batch, 99 + env.rank, 1 << 16, a.ref_steps, max(10, a.warmup))
+        r2 = measure(a.ref_batch, 99 + env.rank, 1 << 16, a.ref_steps, max(10, a.warmup),
+                     min(a.ref_steps_per_graph, max(1, a.ref_steps)))
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / r2["dt"],
                "ms_per_step": 1e3 * r2["dt"] / a.ref_steps, "steps": a.ref_steps,
                "dp_exchange": r2["dp_path"], "replicas_bit_identical": r2["agree"]}
