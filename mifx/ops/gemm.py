@@ -112,11 +112,55 @@ def gemm_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
     return y, z
 
 
-def _dw(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    """Weight gradient dY^T X: the hand-written TN kernel where it measured faster (TN_TUNED), else hipBLASLt."""
+# Asynchronous weight gradients (opt-in, `async_weight_grads()` context): dW is off the backward's critical path
+# (nothing in the backward reads it), so its GEMM is issued on a side stream that forks from the backward stream
+# and runs beside the following dX / attention / elementwise kernels; `join_weight_grads()` (before the optimizer)
+# joins it. The operands are kept referenced until the join, so the allocator cannot hand their memory to the main
+# stream while the side stream still reads them; the dW tensors come from the side stream's pool. Measured SLOWER in
+# the BERT-base step (6.75 vs 6.41 ms, identical loss: profiles/bert_async_dw_ab_r3.txt) -- the side-stream GEMMs take
+# CUs from the dX GEMMs and attention kernels rather than filling idle ones -- so BertTrainer keeps it off
+# (MIFX_BERT_ASYNC_DW=1 turns it on).
+_ASYNC = {"on": False, "side": {}, "pending": {}}
+
+
+class async_weight_grads:
+    def __enter__(self):
+        self.prev = _ASYNC["on"]
+        _ASYNC["on"] = True
+        return self
+
+    def __exit__(self, *exc):
+        _ASYNC["on"] = self.prev
+        return False
+
+
+def join_weight_grads(device) -> None:
+    """The current stream waits for every asynchronous weight gradient issued on `device`."""
+    dev = torch.device(device)
+    if _ASYNC["pending"].pop(dev, None) is not None:
+        torch.cuda.current_stream(dev).wait_stream(_ASYNC["side"][dev])
+
+
+def _dw_tensor(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     if tn_preferred(dy2.shape[1], x2.shape[1], dy2.shape[0]) and tn_eligible(dy2, x2):
         return gemm_tn(dy2, x2)
     return dy2.t() @ x2
+
+
+def _dw(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """Weight gradient dY^T X: the hand-written TN kernel where it measured faster (TN_TUNED), else hipBLASLt; on a
+    side stream inside `async_weight_grads()`."""
+    if not (_ASYNC["on"] and dy2.is_cuda):
+        return _dw_tensor(dy2, x2)
+    dev = dy2.device
+    side = _ASYNC["side"].get(dev)
+    if side is None:
+        side = _ASYNC["side"][dev] = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        dw = _dw_tensor(dy2, x2)
+    _ASYNC["pending"].setdefault(dev, []).append((dy2, x2))
+    return dw
 
 
 def tn_preferred(n_out: int, k_in: int, tokens: int) -> bool:

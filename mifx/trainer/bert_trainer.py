@@ -87,6 +87,8 @@ class BertTrainer:
         self.sdpa = sdpa  # None = PyTorch's choice; "math" / "efficient" / "flash" pins the SDPA backend
         self.graph = None
         self.static_loss = None
+        # MIFX_BERT_ASYNC_DW=1: weight gradients on a side stream (mifx.ops.gemm.async_weight_grads)
+        self.async_dw = cuda and os.environ.get("MIFX_BERT_ASYNC_DW", "0") == "1"
 
     def set_batch(self, ids, tt, am, y) -> None:
         """Next training batch, copied INTO the step's input tensors (a captured hipGraph reads these same
@@ -114,7 +116,14 @@ class BertTrainer:
                             cache_enabled=not self.use_graph), self._sdpa_ctx():
             logits = self.model(ids, tt, am)
         loss = F.cross_entropy(logits.float(), y)
-        loss.backward()
+        if self.async_dw:  # weight-gradient GEMMs on a side stream beside the backward's dX chain
+            from ..ops import gemm as hg
+
+            with hg.async_weight_grads():
+                loss.backward()
+            hg.join_weight_grads(self.device)
+        else:
+            loss.backward()
         self.opt.step()
         return loss.detach()
 
