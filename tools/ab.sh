@@ -52,7 +52,7 @@ for run in $(seq 1 "$rounds"); do
     echo "[ab] $label run $run: ${envs[*]} (cwd $dir)"
     (cd "$dir" && env "${envs[@]}" timeout -k 10 "$limit" "$@" > "$log.log" 2> "$log.err") \
       || { echo "[ab] $label run $run failed"; tail -20 "$log.err"; exit 1; }
-    python - "$log.log" "$label" "$run" "$root/gpurun_out/ab_${name}.jsonl" <<'EOF'
+    python - "$log.log" "$label" "$run" "$root/gpurun_out/ab_${name}.jsonl" <<'EOF' || exit 1
 import json, sys
 path, label, run, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
 lines = [l for l in open(path).read().splitlines() if l.startswith("{")]
