@@ -335,6 +335,17 @@ __device__ __forceinline__ void load_ct(int (&ct)[NTW * KTW], int tbase, int nt0
 }
 
 
+// WDC_NT_SLAB (diagnostic builds): slab stores with the non-temporal hint, so the 24 MB of per-step partials
+// stream out of L2 during the kernel instead of sitting dirty until the end-of-kernel write-back
+#ifndef WDC_NT_SLAB
+#define WDC_NT_SLAB 0
+#endif
+template <class V>
+__device__ __forceinline__ void slab_store(V* p, V v) {
+  if constexpr (WDC_NT_SLAB) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <int NT>
 __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], const int (&ct)[NT], int lane) {
 #pragma unroll
@@ -342,7 +353,7 @@ __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], c
     if (ct[i] < 0) continue;
     float* dst = slab + (size_t)ct[i] * 256 + lane;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dst[e * 64] = acc[i][e];
+    for (int e = 0; e < 4; ++e) slab_store(dst + e * 64, acc[i][e]);
   }
 }
 
@@ -870,7 +881,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   } else if (TRAIN) {
     // 16-byte stores (stride and WIDE_PAD are multiples of 4 floats; the histogram sits 16-B aligned in LDS)
     static_assert(WIDE_PAD % 4 == 0 && (LSEND * 2) % 16 == 0, "vector wide-gradient epilogue");
-    float4* my4 = (float4*)(slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD));
+    v4f* my4 = (v4f*)(slab + (size_t)blockIdx.x * stride + (stride - WIDE_PAD));
     const int4* wgi4 = (const int4*)wgi;
     for (int c4 = tid; c4 < WIDE_PAD / 4; c4 += NTHR) {
       const int4 qv = wgi4[c4];
@@ -880,7 +891,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 #pragma unroll
         for (int i = 0; i < NWAVE; ++i) v.w += red[NWAVE + i];
       }
-      my4[c4] = v;
+      slab_store(my4 + c4, v4f{v.x, v.y, v.z, v.w});
     }
   }
   if (tid == 0 && slab_loss) {
