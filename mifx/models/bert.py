@@ -11,7 +11,7 @@ all-reduce), fused residual-add + LayerNorm (HIP), column-parallel FFN-in with f
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 import torch.nn as nn
@@ -39,6 +39,10 @@ class BertConfig:
     # forward projections on the hand-written MFMA GEMM (csrc/gemm.hip; FFN-in with bias + GELU fused into its
     # epilogue) for the shapes where it measured faster (mifx.ops.gemm.TUNED); None: on unless MIFX_BERT_HIP_GEMM=0
     hip_gemm: bool | None = None
+    # residual gradients folded into the projections' input-gradient GEMMs (mifx.ops.gemm.GradSlot); off with
+    # MIFX_BERT_FOLD_RESIDUAL=0
+    fold_residual_grad: bool = field(
+        default_factory=lambda: os.environ.get("MIFX_BERT_FOLD_RESIDUAL", "1") != "0")
     num_labels: int = 2
     ln_eps: float = 1e-12
     init_std: float = 0.02
@@ -97,8 +101,14 @@ class BertLayer(nn.Module):
         hip = c.hip_gemm if c.hip_gemm is not None else os.environ.get("MIFX_BERT_HIP_GEMM", "1") == "1"
         hip = hip and x.is_cuda
         # (hg.linear: forward and weight gradient each on the hand-written kernel where it measured faster)
+        # residual gradients folded into the input-gradient GEMMs of the projections reading the same activation
+        # (hg.GradSlot: no separate gradient-sum kernel per activation); single TP rank, fused path only
+        fold = (hip and self.tp.size == 1 and c.fold_residual_grad and torch.is_grad_enabled() and x.requires_grad
+                and x.dtype == torch.bfloat16 and self.qkv.weight.dtype == torch.bfloat16)
+        slot_a = hg.GradSlot() if fold else None
+        slot_f = hg.GradSlot() if fold else None
         if hip:
-            qkv = hg.linear(copy_to_tp(x, self.tp), self.qkv.weight, self.qkv.bias).view(B, S, 3, h, d)
+            qkv = hg.linear(copy_to_tp(x, self.tp), self.qkv.weight, self.qkv.bias, slot=slot_a).view(B, S, 3, h, d)
         else:
             qkv = self.qkv(x).view(B, S, 3, h, d)
         if c.fused_attention:
@@ -114,9 +124,9 @@ class BertLayer(nn.Module):
             ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
         a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) if hip else self.attn_out(ctx, add_bias=False)
         x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
-                                          rng, site)
+                                          rng, site, slot=slot_a)
         if hip:
-            f = hg.linear_bias_gelu(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias)
+            f = hg.linear_bias_gelu(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias, slot=slot_f)
         else:
             f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
         if hip:
@@ -124,7 +134,7 @@ class BertLayer(nn.Module):
         else:
             o = self.ffn_out(f, add_bias=False)
         return fb.bias_dropout_add_layernorm(o, self.ffn_out.bias, x, self.ln2.weight, self.ln2.bias, c.ln_eps, drop,
-                                             rng, site + 1)
+                                             rng, site + 1, slot=slot_f)
 
 
 class BertForSequenceClassification(nn.Module):

@@ -125,7 +125,7 @@ class _BiasDropAddLN(torch.autograd.Function):
     dr, da and the gamma / beta / bias gradients); the dropout mask is recomputed in the backward."""
 
     @staticmethod
-    def forward(ctx, a, bias, r, w, b, eps, p, rng, site):
+    def forward(ctx, a, bias, r, w, b, eps, p, rng, site, slot=None):
         a, r = a.contiguous(), r.contiguous().to(a.dtype)
         H = a.shape[-1]
         R = a.numel() // H
@@ -144,6 +144,7 @@ class _BiasDropAddLN(torch.autograd.Function):
         ctx.rng, ctx.p, ctx.site = _snap(rng, p), float(p), int(site)
         ctx.wdtype = w.dtype
         ctx.bdtype = None if bias is None else bias.dtype
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -166,7 +167,9 @@ class _BiasDropAddLN(torch.autograd.Function):
             dw, db = dw.to(ctx.wdtype), db.to(ctx.wdtype)
         if dbias is not None and dbias.dtype != ctx.bdtype:
             dbias = dbias.to(ctx.bdtype)
-        return da, dbias, dr, dw, db, None, None, None, None
+        if ctx.slot is not None:  # the residual's other consumer folds dr into its input-gradient GEMM
+            ctx.slot.g, dr = dr, None
+        return da, dbias, dr, dw, db, None, None, None, None, None
 
 
 class _Dropout(torch.autograd.Function):
@@ -327,15 +330,19 @@ _TORCH_OPS = os.environ.get("MIFX_BERT_TORCH_OPS") == "1"
 
 
 def bias_dropout_add_layernorm(a: torch.Tensor, bias, r: torch.Tensor, weight, ln_bias, eps: float = 1e-12,
-                               p: float = 0.0, rng: torch.Tensor | None = None, site: int = 0) -> torch.Tensor:
+                               p: float = 0.0, rng: torch.Tensor | None = None, site: int = 0,
+                               slot=None) -> torch.Tensor:
     """LayerNorm(dropout_p(a + bias) + r) * weight + ln_bias (bias optional; p > 0 needs rng = device int64
     [seed, counter]). The mask depends only on (seed, counter, site, element index): every tensor-parallel rank
     with the same seed drops the same elements of a replicated activation, and a captured hipGraph draws a new
-    mask per replay once the counter is advanced in-graph."""
+    mask per replay once the counter is advanced in-graph. slot (mifx.ops.gemm.GradSlot, GPU path only): the
+    residual's gradient is handed to the projection that also reads r instead of being returned to autograd."""
     if p > 0 and rng is None:
         raise ValueError("dropout p > 0 needs an rng state tensor [seed, counter]")
     if a.is_cuda and not _TORCH_OPS:
-        return _BiasDropAddLN.apply(a, bias, r, weight, ln_bias, eps, p, rng, site)
+        return _BiasDropAddLN.apply(a, bias, r, weight, ln_bias, eps, p, rng, site, slot)
+    if slot is not None:
+        raise ValueError("a residual-gradient slot needs the fused GPU path")
     x = a if bias is None else a + bias.to(a.dtype)
     if p > 0:
         keep = _mask(x.numel(), rng, site, p, x.device).view(x.shape)

@@ -167,9 +167,32 @@ def tn_preferred(n_out: int, k_in: int, tokens: int) -> bool:
     return (n_out, k_in, tokens) in TN_TUNED and os.environ.get("MIFX_HIP_GEMM_TN", "1") != "0"
 
 
+class GradSlot:
+    """Hand-off of a residual branch's input gradient into the input-gradient GEMM of the other consumer of the
+    same activation. In a BERT layer h feeds both a projection and the residual of the next add+LayerNorm; autograd
+    would sum the two gradients with one extra elementwise kernel per activation (2 per layer). Instead the
+    add+LayerNorm backward (which always runs first: the projection's output gradient flows through it) parks its
+    residual gradient here and returns none, and the projection's backward folds it in as the GEMM's C operand
+    (dX = dY W + dR, one addmm). Single tensor-parallel rank only (with TP the dX GEMM output is a partial sum)."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
+def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tensor:
+    if slot is None:
+        return dy2 @ w
+    g, slot.g = slot.g, None
+    if g is None:
+        raise RuntimeError("GradSlot empty: the residual gradient did not arrive before the projection's backward")
+    return torch.addmm(g.reshape(-1, w.shape[1]).to(dy2.dtype), dy2, w)
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, hip_fwd=True):
+    def forward(ctx, x, w, bias, hip_fwd=True, slot=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if hip_fwd:
@@ -177,6 +200,7 @@ class _Linear(torch.autograd.Function):
         else:
             y = F.linear(x2, w, bias)
         ctx.save_for_backward(x2, w)
+        ctx.slot = slot
         ctx.has_bias = bias is not None
         ctx.bdtype = bias.dtype if bias is not None else None
         return y.view(*shp[:-1], w.shape[0])
@@ -185,22 +209,23 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype)
-        dx = (dy2 @ w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dx = _dx(dy2, w, ctx.slot).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         dw = _dw(dy2.contiguous(), x2) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             from .fused_bert import col_sum
 
             db = col_sum(dy2, ctx.bdtype if ctx.bdtype in (torch.float32, torch.bfloat16) else torch.float32)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class _LinearBiasGelu(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias):
+    def forward(ctx, x, w, bias, slot=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         y, z = gemm_nt(x2, w, bias, 2)
+        ctx.slot = slot
         from .fused_bert import _param
 
         ctx.save_for_backward(x2, w, z, _param(bias))
@@ -219,30 +244,33 @@ class _LinearBiasGelu(torch.autograd.Function):
         db = torch.empty(N, device=z.device, dtype=bp.dtype)
         check(fb_fns()["gelu"](_dt(z), _dt(bp), 0, ptr(dy2), ptr(z), ptr(bp), M, N, ptr(dz), ptr(part), ptr(db),
                                stream_handle(z.device)), "mifx_bert_bias_gelu")
-        dx = (dz @ w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dx = _dx(dz, w, ctx.slot).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         dw = _dw(dz, x2) if ctx.needs_input_grad[1] else None
-        return dx, dw, db if bp.dtype == ctx.bdtype else db.to(ctx.bdtype)
+        return dx, dw, db if bp.dtype == ctx.bdtype else db.to(ctx.bdtype), None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, force: bool = False) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, force: bool = False,
+           slot: GradSlot | None = None) -> torch.Tensor:
     """F.linear with the forward on the hand-written kernel (bias fused) where it is preferred (or, force=True,
-    wherever it tiles the shape), and the weight gradient on the hand-written TN kernel where that is preferred."""
+    wherever it tiles the shape), and the weight gradient on the hand-written TN kernel where that is preferred.
+    slot: the input gradient also carries the residual gradient parked there (GradSlot)."""
     fwd = eligible(x, w) if force else preferred(x, w)
     bwd = (x.is_cuda and x.dtype == torch.bfloat16 and w.requires_grad and torch.is_grad_enabled()
            and tn_preferred(w.shape[0], w.shape[1], x.numel() // x.shape[-1]))
-    if fwd or bwd:
-        return _Linear.apply(x, w, bias, fwd)
+    if fwd or bwd or slot is not None:
+        return _Linear.apply(x, w, bias, fwd, slot)
     return F.linear(x, w, bias)
 
 
-def linear_bias_gelu(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, force: bool = False) -> torch.Tensor:
+def linear_bias_gelu(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, force: bool = False,
+                     slot: GradSlot | None = None) -> torch.Tensor:
     """GELU(x w^T + bias) with the bias + GELU fused into the GEMM epilogue where preferred (force: wherever it
     tiles)."""
     if eligible(x, w) if force else preferred(x, w):
-        return _LinearBiasGelu.apply(x, w, bias)
+        return _LinearBiasGelu.apply(x, w, bias, slot)
     from .fused_bert import bias_gelu
 
-    return bias_gelu(linear(x, w), bias)
+    return bias_gelu(linear(x, w, slot=slot), bias)
 
 
 # ---------------------------------------------------------------- weight-gradient GEMM (csrc/gemm_tn.hip)
