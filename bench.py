@@ -9,13 +9,23 @@ real CSV); random-init weights. Weak scaling: fixed batch per GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-gpu B]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` (N > 1, no torchrun env) starts its own N ranks -- one process per GPU with
+torchrun-style env, spawned before this process touches the GPU -- relays rank 0's JSON line and exits with the
+worst rank's code (a failing rank takes the job down), like the job-owned replicas of the reference's
+`notebooks/training-jobs/distributed-tensorflow-training-job.yaml:8-18`. Under torchrun, WORLD_SIZE must equal
+--gpus: a mismatch exits non-zero instead of timing a different number of GPUs than was asked for.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import torch
@@ -55,7 +65,8 @@ def run(trainer, steps: int, warmup: int, device) -> float:
 def _ranks_agree(tr) -> bool:
     """All ranks apply the same all-reduced gradient to the same initial weights: their parameters must be
     bit-identical. Eager MAX/MIN all-reduce of a checksum, outside any graph."""
-    chk = torch.stack([tr.param.double().sum(), tr.param.double().abs().sum()])
+    prm = tr.param if hasattr(tr, "param") else torch.cat([p.detach().flatten() for p in tr.model.parameters()])
+    chk = torch.stack([prm.double().sum(), prm.double().abs().sum()])
     hi, lo = chk.clone(), chk.clone()
     torch.distributed.all_reduce(hi, op=torch.distributed.ReduceOp.MAX)
     torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
@@ -65,8 +76,11 @@ def _ranks_agree(tr) -> bool:
 def _post_run_ok(tr, n: int, use_cuda: bool) -> tuple[bool, bool | None]:
     """After the timed region (outside it): the exchange must not have timed out on any rank and every replica
     must hold bit-identical weights. Returns (ok on every rank, replicas_bit_identical or None at one rank)."""
-    if n == 1 or not use_cuda:
+    if n == 1:
         return True, None
+    if not use_cuda:
+        agree = _ranks_agree(tr)
+        return agree, agree
     bad = 0.0
     try:
         if getattr(tr, "_xg", None) is not None:
@@ -124,7 +138,8 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, dp
         else:
             from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
 
-            t = TorchWideDeepTrainer(model, batch=batch, device=device)
+            t = TorchWideDeepTrainer(model, batch=batch, device=device, process_group=pg)
+            t.dp_path = "gloo bucketed all-reduce (mifx.parallel.ddp)" if pg is not None else None
         t.set_data(synthetic_records(n_data, device=device, seed=seed))
         return t
 
@@ -190,7 +205,69 @@ def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, dp
     return tr
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Run this script as N ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), one per
+    GPU. Nothing here touches the GPU (no torch.cuda call): the native libraries are checked (and rebuilt if stale)
+    once, under the build lock, before any rank starts. Rank 0's stdout is relayed line by line; every rank's
+    stderr goes to ours. The first rank that fails kills the others and its exit code is the job's."""
+    try:
+        from mifx.ops import build
+
+        build.build_all(verbose=False)
+    except Exception as e:  # noqa: BLE001 -- no hipcc / read-only tree: the ranks' own load() reports it
+        print(f"[bench] native prebuild skipped: {e}", file=sys.stderr, flush=True)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   MIFX_AUTOBUILD="0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, start_new_session=True))
+
+    def relay():
+        for line in procs[0].stdout:  # the result line to stdout; library chatter (gloo, RCCL) to stderr
+            txt = line.decode()
+            out = sys.stdout if txt.lstrip().startswith("{") else sys.stderr
+            out.write(txt)
+            out.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    codes = [None] * n
+    first_bad = None
+    try:
+        while any(c is None for c in codes):
+            codes = [p.poll() for p in procs]
+            if any(c not in (None, 0) for c in codes):
+                bad = next(r for r, c in enumerate(codes) if c not in (None, 0))
+                first_bad = codes[bad]
+                print(f"[bench] rank {bad} exited with {codes[bad]}: stopping the job", file=sys.stderr, flush=True)
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+            p.wait()
+        t.join(timeout=5)
+    codes = [(c if c >= 0 else 128 - c) for c in (p.returncode for p in procs)]  # signal death -> 128+sig
+    if first_bad is not None:  # the rank that failed first is the cause; the ones killed after it are not
+        return first_bad if first_bad >= 0 else 128 - first_bad
+    return max(codes)
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -214,7 +291,17 @@ def main(argv=None) -> int:
                          "two graphs)")
     a = ap.parse_args(argv)
 
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and a.gpus > 1:
+        return spawn_ranks(a.gpus, argv)
+    if int(ws or 1) != a.gpus:
+        print(f"[bench] WORLD_SIZE={ws} but --gpus {a.gpus}: refusing to time a different number of GPUs",
+              file=sys.stderr, flush=True)
+        return 2
     env = mdist.init()
+    if os.environ.get("MIFX_BENCH_FAIL_RANK") == str(env.rank):  # fault injection (tests): this rank dies
+        print(f"[bench] rank {env.rank}: injected failure", file=sys.stderr, flush=True)
+        os._exit(3)
     use_cuda = torch.cuda.is_available()
     # MIFX_SHARED_GPU=1 (rehearsal of the multi-rank flow on a 1-GPU box, with MIFX_DIST_BACKEND=gloo): every
     # rank on cuda:0 -- functional only, the timings of ranks sharing a GPU mean nothing
@@ -228,6 +315,9 @@ def main(argv=None) -> int:
         a.steps, a.warmup, a.ref_steps = min(a.steps, 20), min(a.warmup, 2), min(a.ref_steps, 50)
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
     n = env.world_size
+    seen = torch.distributed.get_world_size() if pg is not None else 1
+    if seen != a.gpus:
+        raise SystemExit(f"[bench] process group has {seen} ranks, --gpus {a.gpus}")
 
     def measure(batch, seed, n_data, steps, warmup, spg_req=None):
         """Build, time `steps` steps, validate after the timed region. A multi-rank xGMI run that fails the
@@ -241,6 +331,10 @@ def main(argv=None) -> int:
             ok, agree = _post_run_ok(tr, n, use_cuda)
             res = {"dt": dt, "dp_path": getattr(tr, "dp_path", None), "spg": spg, "agree": agree,
                    "loss": tr.last_loss() / batch if ok else float("nan")}
+            if pg is not None:  # which exchange every rank actually timed
+                paths = [None] * n
+                torch.distributed.all_gather_object(paths, res["dp_path"])
+                res["dp_per_rank"] = paths
             if getattr(tr, "_xg", None) is not None:
                 tr.disable_xgmi()
             del tr
@@ -257,6 +351,7 @@ def main(argv=None) -> int:
 
     r = measure(a.batch_per_gpu, 1234 + env.rank, a.data_per_gpu, a.steps, a.warmup)
     dt, dp_path, spg, ranks_agree, loss = r["dt"], r["dp_path"], r["spg"], r["agree"], r["loss"]
+    dp_per_rank = r.get("dp_per_rank")
     value = a.batch_per_gpu * n * a.steps / dt
     grad_err = None
     if use_cuda and env.is_main:  # after the timed region: the kernel's gradient vs fp32 autograd on one batch
@@ -270,7 +365,8 @@ def main(argv=None) -> int:
                      min(a.ref_steps_per_graph, max(1, a.ref_steps)))
         ref = {"batch_per_gpu": a.ref_batch, "examples_per_sec": a.ref_batch * n * a.ref_steps / r2["dt"],
                "ms_per_step": 1e3 * r2["dt"] / a.ref_steps, "steps": a.ref_steps,
-               "dp_exchange": r2["dp_path"], "replicas_bit_identical": r2["agree"]}
+               "dp_exchange": r2["dp_path"], "dp_exchange_per_rank": r2.get("dp_per_rank"),
+               "replicas_bit_identical": r2["agree"]}
 
     if env.is_main:
         out = {
@@ -278,13 +374,15 @@ def main(argv=None) -> int:
             "value": value,
             "unit": "examples/s",
             "n_gpus": n,
+            "world_size_seen_by_backend": seen,
+            "backend": torch.distributed.get_backend(pg) if pg is not None else None,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": 1e3 * dt / a.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if use_cuda else "fp32",
             "data": "synthetic (transformed Chicago-Taxi-shaped records, HBM-resident); random-init weights",
             "config": {"model": MODEL, "global_batch": a.batch_per_gpu * n, "seq_len": None,
                        "parallelism": f"dp{n}", "batch_per_gpu": a.batch_per_gpu,
@@ -294,7 +392,7 @@ def main(argv=None) -> int:
                        "hipgraph": bool(use_cuda and not a.no_graph),
                        "steps_per_graph": spg,
                        "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
-                       "dp_exchange": dp_path,
+                       "dp_exchange": dp_path, "dp_exchange_per_rank": dp_per_rank,
                        "replicas_bit_identical": ranks_agree, "validated_after_timed_region": True,
                        "grad_check_max_rel_err_vs_fp32": grad_err},
             "final_mean_loss": loss,

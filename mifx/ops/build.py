@@ -15,6 +15,7 @@ import os
 import shutil
 import subprocess
 import sys
+import threading
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[2]
@@ -88,7 +89,7 @@ def _build_one(src: Path, force: bool) -> tuple[str, str]:
     out = LIBDIR / f"libmifx_{src.stem}.so"
     if not force and not _needs_build(src, out):
         return src.name, "up-to-date"
-    tmp = out.with_suffix(".so.tmp")
+    tmp = out.with_suffix(f".so.tmp.{os.getpid()}.{threading.get_ident()}")
     hd = ["-include", str(HASH_HEADER), f"-DMIFX_SRC_HASH_VALUE=\"{source_hash(src)}\""]
     if src.suffix == ".hip":
         cmd = [hipcc()] + HIP_FLAGS + _file_flags(src) + hd + ["-I", str(CSRC), str(src), "-o", str(tmp)]
@@ -96,19 +97,39 @@ def _build_one(src: Path, force: bool) -> tuple[str, str]:
         cmd = [os.environ.get("CXX", "g++")] + CXX_FLAGS + hd + ["-I", str(CSRC), str(src), "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
+        tmp.unlink(missing_ok=True)
         raise RuntimeError(f"build of {src.name} failed:\n{' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
-    tmp.replace(out)
+    tmp.replace(out)  # atomic: a concurrent loader sees the old or the new library, never a partial one
     return src.name, "built"
 
 
+class build_lock:
+    """Exclusive fcntl lock on LIBDIR/.build.lock: the N ranks of a data-parallel job that all find the libraries
+    stale build them once (the first holder builds; the others wait, then find every library up to date)."""
+
+    def __enter__(self):
+        import fcntl
+
+        LIBDIR.mkdir(parents=True, exist_ok=True)
+        self._f = open(LIBDIR / ".build.lock", "w")
+        fcntl.flock(self._f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+
+        fcntl.flock(self._f, fcntl.LOCK_UN)
+        self._f.close()
+
+
 def build_all(force: bool = False, jobs: int | None = None, verbose: bool = True) -> list[Path]:
-    LIBDIR.mkdir(parents=True, exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
     jobs = jobs or min(8, max(1, len(srcs)))
-    with cf.ThreadPoolExecutor(jobs) as ex:
-        for name, status in ex.map(lambda s: _build_one(s, force), srcs):
-            if verbose:
-                print(f"[mifx.build] {name}: {status}", file=sys.stderr)
+    with build_lock():  # staleness is re-checked per library under the lock (_build_one -> _needs_build)
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            for name, status in ex.map(lambda s: _build_one(s, force), srcs):
+                if verbose:
+                    print(f"[mifx.build] {name}: {status}", file=sys.stderr)
     return [LIBDIR / f"libmifx_{s.stem}.so" for s in srcs]
 
 
