@@ -128,17 +128,17 @@ def gradient_check(batch: int, device, seed: int) -> float:
 
 
 def make_trainer(batch: int, device, pg, seed: int, n_data: int, graph: bool, dp: str = "xgmi",
-                 steps_per_graph: int = 10):
+                 steps_per_graph: int = 10, shuffle_seed: int = 0):
     def build():
         model = WideDeepModel(seed=0)
         if device.type == "cuda":
             from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
 
-            t = FusedWideDeepTrainer(model, batch=batch, device=device, process_group=pg)
+            t = FusedWideDeepTrainer(model, batch=batch, device=device, process_group=pg, shuffle_seed=shuffle_seed)
         else:
             from mifx.trainer.torch_wide_deep import TorchWideDeepTrainer
 
-            t = TorchWideDeepTrainer(model, batch=batch, device=device, process_group=pg)
+            t = TorchWideDeepTrainer(model, batch=batch, device=device, process_group=pg, shuffle_seed=shuffle_seed)
             t.dp_path = "gloo bucketed all-reduce (mifx.parallel.ddp)" if pg is not None else None
         t.set_data(synthetic_records(n_data, device=device, seed=seed))
         return t
@@ -281,6 +281,9 @@ def main(argv=None) -> int:
                          "profiles/bench_ref_spg_sweep_r3.txt)")
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--shuffle-seed", type=int, default=0x5EED,
+                    help="per-epoch shuffle of the resident records inside the kernel's record fetch (csrc/feed.h; "
+                         "the reference's read_batch_features(randomize_input=True)); 0 = stored order")
     ap.add_argument("--steps-per-graph", type=int, default=20,
                     help="consecutive training steps captured in one hipGraph (single rank / captured collective); "
                          "20 measured best at the driver's 20 timed steps (profiles/bench_spg_sweep_r3.txt)")
@@ -325,7 +328,8 @@ def main(argv=None) -> int:
         RCCL path; a failing direct run fails the benchmark (no number from a broken step)."""
         dp = a.dp
         while True:
-            tr = make_trainer(batch, device, pg, seed, n_data, not a.no_graph, dp, spg_req or a.steps_per_graph)
+            tr = make_trainer(batch, device, pg, seed, n_data, not a.no_graph, dp, spg_req or a.steps_per_graph,
+                              a.shuffle_seed)
             spg = int(getattr(tr, "graph_multi_steps", 1)) if getattr(tr, "graph_multi", None) is not None else 1
             dt = mdist.max_over_ranks(run(tr, steps, warmup, device), device if use_cuda else None)
             ok, agree = _post_run_ok(tr, n, use_cuda)
@@ -383,13 +387,16 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if use_cuda else "fp32",
-            "data": "synthetic (transformed Chicago-Taxi-shaped records, HBM-resident); random-init weights",
+            "data": "synthetic (transformed Chicago-Taxi-shaped records, HBM-resident, "
+                    + ("reshuffled every epoch in-kernel" if a.shuffle_seed else "stored order")
+                    + "); random-init weights",
             "config": {"model": MODEL, "global_batch": a.batch_per_gpu * n, "seq_len": None,
                        "parallelism": f"dp{n}", "batch_per_gpu": a.batch_per_gpu,
                        "optimizer": "adagrad(dnn,lr=0.05)+ftrl(linear,lr=0.2)",
                        "precision": "bf16 MFMA compute, fp32 master weights/optimizer state",
                        "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
                        "hipgraph": bool(use_cuda and not a.no_graph),
+                       "input_shuffle_seed": a.shuffle_seed,
                        "steps_per_graph": spg,
                        "kernel": "wd_chain (register-chained, 8 waves)" if use_cuda else "torch-cpu",
                        "dp_exchange": dp_path, "dp_exchange_per_rank": dp_per_rank,

@@ -19,13 +19,15 @@
 //    (deterministic, no atomics, no sort) and applies acc += g^2; w -= lr * g * rsqrt(acc); the other
 //    pairs exit. No host-side sort/unique (whose dynamic output size forced a device->host sync per
 //    step), so the whole step is hipGraph-capturable.
-//  * Batch selection on the device: example b of a step is record (start + b) % n of the resident
-//    dataset with start = step_ctr[0] * B % n (or a fixed start), and tdnn_dense_apply advances
-//    step_ctr at the end of the step -- replayed graphs walk through the data with no host work.
+//  * Batch selection on the device: example b of a step is the record the feed of csrc/feed.h gives for stream
+//    position step_ctr[0] * stride + offset + b of the resident dataset (optionally shuffled per epoch; or a fixed
+//    start, stored order), and tdnn_dense_apply advances step_ctr at the end of the step -- replayed graphs walk
+//    through the data with no host work.
 //  * tdnn_dense_partial + tdnn_dense_apply: batch-chunked reductions for the dense W1 rows, b1, w2
 //    (grid H/256 x chunks), then a fixed-order combine and the same update; block 0 updates b2. Up to
 //    64 examples tdnn_head_bwd writes one chunk per example itself (no tdnn_dense_partial launch).
 #include <hip/hip_runtime.h>
+#include "feed.h"
 #include <stdint.h>
 
 namespace {
@@ -48,16 +50,29 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-// record of example b of this step (see the header): start = step_ctr[0] * B % n, or start_fixed
+// record of example b of this step (see the header): the record feed of csrc/feed.h at step step_ctr[0] (global
+// stream stride / offset, optional per-epoch shuffle), or records start_fixed.. in stored order
 struct BatchSel {
   long long n;
   const long long* ctr;
   long long start_fixed;
   int B;
-  __device__ __forceinline__ long long start() const { return ctr ? (ctr[0] * (long long)B) % n : start_fixed; }
-  __device__ __forceinline__ long long rec(long long st, int b) const {
-    const long long e = st + b;
-    return e >= n ? e - n : e;  // host guarantees B <= n
+  MifxFeed feed;
+  long long* rec_out;  // nullable: tdnn_head_bwd records which record each example of the step was
+  __device__ __forceinline__ MifxFeedStep start() const {
+    if (ctr) return mifx_feed_step(feed, ctr[0], n);
+    MifxFeedStep s;
+    s.e0 = 0;
+    s.i0 = start_fixed;
+    s.h = 1;
+    return s;
+  }
+  __device__ __forceinline__ long long rec(const MifxFeedStep& st, int b) const {
+    if (!ctr) {
+      const long long e = st.i0 + b;
+      return e >= n ? e - n : e;  // host guarantees B <= n
+    }
+    return mifx_feed_record(feed, st, b, n);
   }
 };
 
@@ -106,7 +121,9 @@ __global__ __launch_bounds__(kThreads) void tdnn_head_bwd(const float* __restric
   for (int c = 0; c < nh; ++c) logit += part[(size_t)b * nh + c];
   if (blockIdx.y == 0 && threadIdx.x == 0) logit_out[b] = logit;
   if (!train) return;
-  const float yy = y[sel.rec(sel.start(), b)];
+  const long long rec = sel.rec(sel.start(), b);
+  if (sel.rec_out != nullptr && blockIdx.y == 0 && threadIdx.x == 0) sel.rec_out[b] = rec;
+  const float yy = y[rec];
   const float dl = (1.f / (1.f + expf(-logit)) - yy) * grad_scale;
   if (blockIdx.y == 0 && threadIdx.x == 0) {
     // stable BCE with logits: max(l,0) - l*y + log1p(exp(-|l|))
@@ -140,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void tdnn_sparse_adagrad(float* __restric
   __shared__ int s_n, s_earlier;
   const int B = sel.B;
   const int b = blockIdx.x / F, f = blockIdx.x % F;
-  const long long st = sel.start();
+  const MifxFeedStep st = sel.start();
   const int r = rows[(size_t)sel.rec(st, b) * F + f];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (t == 0) {
@@ -187,7 +204,7 @@ __global__ __launch_bounds__(kThreads) void tdnn_dense_partial(const float* __re
                                                               float* __restrict__ part) {
   const int h = blockIdx.x * kThreads + threadIdx.x;
   if (h >= H) return;
-  const long long st = sel.start();
+  const MifxFeedStep st = sel.start();
   const int nchunk = gridDim.y, c = blockIdx.y;
   const int b0 = (int)((long long)B * c / nchunk), b1e = (int)((long long)B * (c + 1) / nchunk);
   float gd[kMaxDense];
@@ -279,17 +296,19 @@ constexpr int kDirectChunks = 64;
 int mifx_tdnn_chunks(int B) { return B <= kDirectChunks ? B : (B / 32 < 64 ? B / 32 : 64); }
 
 // rows [n, F] int32 global W1 rows, xd [n, D], y [n]: the resident dataset (or one batch with n = B). Example b
-// of the step is record (start + b) % n, start = step_ctr[0] * B % n when step_ctr is set, else start_fixed.
+// of the step is the feed's record (csrc/feed.h) when step_ctr is set, else record (start_fixed + b) % n.
+// rec_out (nullable, int64 [B]): receives the record index of every example.
 // scratch: part_logit [B * ceil(H/256)]
 int mifx_tdnn_fwd_bwd(const float* W1, const float* b1, const float* w2, const float* b2, const int* rows, int F,
                       const float* xd, int D, int dense_row0, const float* y, long long n, const long long* step_ctr,
                       long long start_fixed, int B, int H, float grad_scale, int train, float* a_out,
                       float* part_logit, float* dz_out, float* logit_out, float* dlogit_out, float* loss_out,
-                      float* dense_part, hipStream_t st) {
+                      float* dense_part, long long feed_stride, long long feed_offset, unsigned long long shuffle_key,
+                      long long* rec_out, hipStream_t st) {
   if (H <= 0 || H > kMaxH || F > kMaxFields || D > kMaxDense || B <= 0 || n < B || start_fixed < 0 ||
-      start_fixed >= n)
+      start_fixed >= n || feed_stride < B || feed_offset < 0 || feed_offset + B > feed_stride)
     return -1;
-  const BatchSel sel{n, step_ctr, start_fixed, B};
+  const BatchSel sel{n, step_ctr, start_fixed, B, MifxFeed{feed_stride, feed_offset, shuffle_key}, rec_out};
   const dim3 grid(B, (H + kThreads - 1) / kThreads);
   hipLaunchKernelGGL(tdnn_fwd, grid, dim3(kThreads), 0, st, W1, b1, w2, rows, F, xd, D, dense_row0, H, sel, a_out,
                      part_logit);
@@ -306,11 +325,12 @@ int mifx_tdnn_max_batch() { return kMaxList; }
 int mifx_tdnn_adagrad(float* W1, float* acc1, float* b1, float* accb1, float* w2, float* accw2, float* b2,
                       float* accb2, const int* rows, int F, const float* xd, int D, int dense_row0, long long n,
                       long long* step_ctr, long long start_fixed, const float* a, const float* dz,
-                      const float* dlogit, int B, int H, float lr, float* dense_part, hipStream_t st) {
+                      const float* dlogit, int B, int H, float lr, float* dense_part, long long feed_stride,
+                      long long feed_offset, unsigned long long shuffle_key, hipStream_t st) {
   if (H <= 0 || H > kMaxH || D > kMaxDense || F > kMaxFields || B <= 0 || B > kMaxList || n < B ||
-      start_fixed < 0 || start_fixed >= n)
+      start_fixed < 0 || start_fixed >= n || feed_stride < B || feed_offset < 0 || feed_offset + B > feed_stride)
     return -1;
-  const BatchSel sel{n, step_ctr, start_fixed, B};
+  const BatchSel sel{n, step_ctr, start_fixed, B, MifxFeed{feed_stride, feed_offset, shuffle_key}, nullptr};
   hipLaunchKernelGGL(tdnn_sparse_adagrad, dim3(B * F), dim3(kThreads), 0, st, W1, acc1, rows, F, sel, dz, H, lr);
   const int nchunk = mifx_tdnn_chunks(B);
   const int hb = (H + kThreads - 1) / kThreads;

@@ -1,0 +1,96 @@
+// Record feed of the fused Wide&Deep training kernels: which resident record a batch row trains on.
+//
+// The reference reads its training files through `read_batch_features(..., randomize_input=True)`
+// (`airflow-dags/taxi_utils.py:275-276`): a fresh shuffle of the records every epoch. Here the records stay
+// resident in HBM and the shuffle is a pseudo-random PERMUTATION of [0, n) per epoch, evaluated per record in the
+// kernel's own fetch (no index array, no host work, nothing re-uploaded between epochs):
+//
+//   position p = step * gstride + goff + row          (the global stream: a data-parallel rank r with per-replica
+//                                                      batch B and world W uses gstride = W B, goff = r B, so the
+//                                                      ranks read disjoint rows of ONE global stream and the job
+//                                                      equals one process at batch W B)
+//   epoch e = p / n,  i = p mod n
+//   record  = key == 0 ? i : feistel_perm(i, n, epoch_key(key, e))
+//
+// feistel_perm: a 4-round balanced Feistel network on [0, 2^(2h)) (2^(2h) >= n, h >= 1) with cycle walking down to
+// [0, n) -- a bijection of [0, n) for every n and key (each walk follows the permutation's cycle from i until it
+// re-enters [0, n), which it must: at the latest back at i). Expected walk length < 4 (2^(2h) < 4n).
+// mifx/data/shuffle.py is the bit-exact host implementation (tests and the CPU trainer).
+#pragma once
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define MIFX_HD __host__ __device__ __forceinline__
+#else
+#define MIFX_HD inline
+#endif
+
+MIFX_HD uint32_t mifx_mix32(uint32_t x) {  // "lowbias32" integer hash
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+MIFX_HD uint64_t mifx_epoch_key(uint64_t key, uint64_t epoch) {
+  const uint32_t a = mifx_mix32((uint32_t)key ^ mifx_mix32((uint32_t)epoch + 0x9e3779b9u));
+  const uint32_t b = mifx_mix32((uint32_t)(key >> 32) ^ mifx_mix32((uint32_t)(epoch >> 32) + 0x85ebca6bu) ^ a);
+  return ((uint64_t)b << 32) | a;
+}
+
+// half width h (bits) of the Feistel domain for n records: the smallest h >= 1 with 4^h >= n
+MIFX_HD int mifx_feistel_half(uint64_t n) {
+  int h = 1;
+  while (h < 32 && (uint64_t(1) << (2 * h)) < n) ++h;
+  return h;
+}
+
+MIFX_HD uint64_t mifx_feistel_perm(uint64_t i, uint64_t n, uint64_t ekey, int h) {
+  const uint64_t mask = (uint64_t(1) << h) - 1;
+  const uint32_t k0 = (uint32_t)ekey, k1 = (uint32_t)(ekey >> 32);
+  const uint32_t rk[4] = {k0, k1, k0 ^ 0x68e31da4u, k1 ^ 0xb5297a4du};
+  uint64_t x = i;
+  do {
+    uint64_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t t = L ^ ((uint64_t)mifx_mix32((uint32_t)R ^ rk[r] ^ (uint32_t)(R >> 32)) & mask);
+      L = R;
+      R = t;
+    }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+
+struct MifxFeed {
+  long long gstride;   // stream positions per training step (the global batch)
+  long long goff;      // this replica's offset inside the global batch
+  unsigned long long key;  // 0: no shuffle (records in stored order); else the shuffle seed
+};
+
+// per step: the epoch and in-epoch index of this replica's first row
+struct MifxFeedStep {
+  long long e0, i0;
+  int h;
+};
+MIFX_HD MifxFeedStep mifx_feed_step(const MifxFeed& f, long long step, long long n) {
+  const long long p = step * f.gstride + f.goff;
+  MifxFeedStep s;
+  s.e0 = p / n;
+  s.i0 = p - s.e0 * n;
+  s.h = mifx_feistel_half((uint64_t)n);
+  return s;
+}
+// record of batch row `row` (0 <= row < batch <= n)
+MIFX_HD long long mifx_feed_record(const MifxFeed& f, const MifxFeedStep& s, long long row, long long n) {
+  long long i = s.i0 + row, e = s.e0;
+  if (i >= n) {
+    i -= n;
+    e += 1;
+  }
+  if (f.key == 0) return i;
+  return (long long)mifx_feistel_perm((uint64_t)i, (uint64_t)n, mifx_epoch_key(f.key, (uint64_t)e), s.h);
+}

@@ -29,6 +29,7 @@
 // MIFX_HIPCC_FLAGS: -fno-honor-nans -fno-honor-infinities
 #include <hip/hip_runtime.h>
 #include "xcd.h"
+#include "feed.h"
 #include <stdint.h>
 
 namespace {
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
                                                      float* __restrict__ slab, float* __restrict__ slab_loss,
                                                      float* __restrict__ logits_out, float grad_scale,
                                                      const int* __restrict__ tmap, int stride,
-                                                     int* __restrict__ xcd_of, TailArgs ta) {
+                                                     int* __restrict__ xcd_of, TailArgs ta, MifxFeed feed) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LSEND);
   float* red = wgrad + WIDE_PAD;
@@ -556,7 +557,18 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   constexpr bool kPersist = PERSIST;
   const int nsteps = kPersist ? ta.nsteps : 1;
   for (int ps = 0; ps < nsteps; ++ps) {
-  const long long start = step_ctr ? ((step0 + ps) * batch) % n_data : start_fixed;
+  // record feed (csrc/feed.h): the step's place in the (optionally shuffled) global record stream; a fixed start
+  // (eval / predict) reads records start_fixed.. in stored order
+  MifxFeed fd = feed;
+  MifxFeedStep fs;
+  if (step_ctr) {
+    fs = mifx_feed_step(fd, step0 + ps, n_data);
+  } else {
+    fd.key = 0;
+    fs.e0 = 0;
+    fs.i0 = start_fixed;
+    fs.h = 1;
+  }
   const int niters = (int)((batch + T - 1) / T);
   const int my_iters = (niters - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   const float qbound = fmaxf(fabsf(grad_scale) * (float)(max(my_iters, 1) * T), 1e-30f);
@@ -601,8 +613,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 #pragma unroll
     for (int tb = 0; tb < TBN; ++tb) {
       const long long row = min((long long)it * T + EPW * w + 16 * tb + r, batch - 1);
-      long long di = start + row;
-      if (di >= n_data) di -= n_data;  // host guarantees batch <= n_data
+      const long long di = mifx_feed_record(fd, fs, row, n_data);  // host guarantees batch <= n_data
       u[tb][0] = data[2 * di];
       u[tb][1] = data[2 * di + 1];
     }
@@ -1020,7 +1031,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 template <bool TRAIN, int TBN, bool TAIL = false, bool PERSIST = false>
 void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
             const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
-            float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of, TailArgs ta = TailArgs{}) {
+            float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of, MifxFeed feed,
+            TailArgs ta = TailArgs{}) {
   constexpr int lds_bytes = PERSIST ? LDS_BYTES_P : LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
@@ -1030,7 +1042,7 @@ void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, l
   }
   hipLaunchKernelGGL((wdc_fused<TRAIN, TBN, TAIL, PERSIST>), grid, dim3(64 * (T / (16 * TBN))), lds_bytes, stream,
                      (const uint4*)data, n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab,
-                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta);
+                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta, feed);
 }
 
 }  // namespace
@@ -1059,37 +1071,50 @@ int WDC_SYM(mifx_wdc_constants)(int* out, int n) {
 // layout (LWEND elements, C-ordered columns, see models.wide_deep.chain_image).
 // xcd_of (nullable, >= grid ints): receives the XCD each workgroup ran on (training only).
 // (T = 64 build: waves must be 4, 4 x 16 examples)
-int WDC_SYM(mifx_wdc_fused_x)(const void* data, long long n_data, long long batch, long long start_fixed,
+int WDC_SYM(mifx_wdc_fused_f)(const void* data, long long n_data, long long batch, long long start_fixed,
                               const long long* step_ctr, const void* wimg, const float* wide, float* slab,
                               float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
-                              const int* tmap, int stride, int waves, int* xcd_of, hipStream_t stream) {
+                              const int* tmap, int stride, int waves, int* xcd_of, long long feed_stride,
+                              long long feed_offset, unsigned long long shuffle_key, hipStream_t stream) {
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
   if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;
   if (!train && logits_out == nullptr) return -1;
+  if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
+  const MifxFeed fd{feed_stride, feed_offset, shuffle_key};
   const dim3 g(grid);
 #if WDC_T == 64
   if (waves != 4) return -1;
   if (train)
     launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else
     launch<false, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                     grad_scale, tmap, stride, nullptr);
+                     grad_scale, tmap, stride, nullptr, fd);
   return (int)hipGetLastError();
 #else
   if (waves != 4 && waves != 8) return -1;
   if (train && waves == 4)
     launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else if (train)
     launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else  // eval / predict: the 4-wave shape for either request (forward only, no dW phases to overlap)
     launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                     grad_scale, tmap, stride, nullptr);
+                     grad_scale, tmap, stride, nullptr, fd);
   return (int)hipGetLastError();
 #endif
+}
+
+// the same launch with the records in stored order, one replica (feed stride = batch, offset 0, no shuffle)
+int WDC_SYM(mifx_wdc_fused_x)(const void* data, long long n_data, long long batch, long long start_fixed,
+                              const long long* step_ctr, const void* wimg, const float* wide, float* slab,
+                              float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
+                              const int* tmap, int stride, int waves, int* xcd_of, hipStream_t stream) {
+  return WDC_SYM(mifx_wdc_fused_f)(data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss,
+                                   logits_out, grad_scale, grid, train, tmap, stride, waves, xcd_of, batch, 0, 0,
+                                   stream);
 }
 
 int WDC_SYM(mifx_wdc_fused)(const void* data, long long n_data, long long batch, long long start_fixed,
@@ -1111,7 +1136,8 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
                         float* wide, float* slab, float* slab_loss, float grad_scale, int grid, const int* tmap,
                         int stride, int* xcd_of, float* xpart, unsigned long long* bar, int* err, const int* wsc,
                         float* param, float* s0, float* s1, const float* hyper_dnn, const float* hyper_wide,
-                        long long* dbg, hipStream_t stream) {
+                        long long* dbg, long long feed_stride, long long feed_offset, unsigned long long shuffle_key,
+                        hipStream_t stream) {
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
                                               hipSuccess)
@@ -1123,6 +1149,7 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
       s1 == nullptr || step_ctr == nullptr)
     return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0 || stride < WIDE_PAD || stride % 4 != 0) return -1;
+  if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
   TailArgs ta;
   ta.xpart = xpart;
   ta.bar = bar;
@@ -1139,7 +1166,7 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
   ta.hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
                    hyper_wide[6], hyper_wide[7]};
   launch<true, 1, true>(dim3(grid), stream, data, n_data, batch, 0, step_ctr, wimg, wide, slab, slab_loss, nullptr,
-                        grad_scale, tmap, stride, xcd_of, ta);
+                        grad_scale, tmap, stride, xcd_of, MifxFeed{feed_stride, feed_offset, shuffle_key}, ta);
   return (int)hipGetLastError();
 }
 
@@ -1150,12 +1177,13 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
 int mifx_wdc_persist(const void* data, long long n_data, long long batch, long long* step_ctr, void* wimg,
                      float* wide, float* slab, float* slab_loss, float grad_scale, const int* tmap, int stride, const int* wsc,
                      float* param, float* s0, float* s1, const float* hyper_dnn, const float* hyper_wide, int nsteps,
-                     hipStream_t stream) {
+                     long long feed_stride, long long feed_offset, unsigned long long shuffle_key, hipStream_t stream) {
   if (nsteps <= 0 || n_data <= 0 || batch <= 0 || batch > T || batch > n_data) return -1;
   if (wimg == nullptr || wide == nullptr || tmap == nullptr || wsc == nullptr || param == nullptr || s0 == nullptr ||
       s1 == nullptr || step_ctr == nullptr || hyper_dnn == nullptr || hyper_wide == nullptr || slab == nullptr)
     return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0 || stride < WIDE_PAD || stride % 4 != 0) return -1;
+  if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
   TailArgs ta{};
   ta.wsc = wsc;
   ta.param = param;
@@ -1169,7 +1197,8 @@ int mifx_wdc_persist(const void* data, long long n_data, long long batch, long l
   ta.hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
                    hyper_wide[6], hyper_wide[7]};
   launch<true, 1, false, true>(dim3(1), stream, data, n_data, batch, 0, step_ctr, wimg, wide, slab, slab_loss,
-                               nullptr, grad_scale, tmap, stride, nullptr, ta);
+                               nullptr, grad_scale, tmap, stride, nullptr, MifxFeed{feed_stride, feed_offset, shuffle_key},
+                               ta);
   return (int)hipGetLastError();
 }
 

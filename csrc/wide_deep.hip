@@ -36,6 +36,7 @@
 // (no NaN canonicalisation v_max before every ReLU; MFMA results in VGPRs instead of
 //  AGPR->VGPR copies feeding the epilogues)
 #include <hip/hip_runtime.h>
+#include "feed.h"
 #include "xcd.h"
 #include <stdint.h>
 
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
     const uint4* __restrict__ data, long long n_data, long long batch, long long start_fixed,
     const long long* __restrict__ step_ctr, const uint16_t* __restrict__ wt, const float* __restrict__ wide,
     float* __restrict__ slab, float* __restrict__ slab_loss, float* __restrict__ logits_out, float grad_scale,
-    const int* __restrict__ tmap, int stride, StageDims sd) {
+    const int* __restrict__ tmap, int stride, StageDims sd, MifxFeed feed) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LEND);
   float* red = wgrad + WIDE_PAD;
@@ -395,7 +396,17 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   (void)stamp_on;
   STAMP(1);
 
-  const long long start = step_ctr ? (step_ctr[0] * batch) % n_data : start_fixed;
+  // record feed (csrc/feed.h); a fixed start (eval / predict) reads records start_fixed.. in stored order
+  MifxFeed fd = feed;
+  MifxFeedStep fs;
+  if (step_ctr) {
+    fs = mifx_feed_step(fd, step_ctr[0], n_data);
+  } else {
+    fd.key = 0;
+    fs.e0 = 0;
+    fs.i0 = start_fixed;
+    fs.h = 1;
+  }
   const int ntiles = (int)((batch + T - 1) / T);
   // Wide-part gradient: LDS histogram in 32-bit fixed point, so the result does not depend on the
   // order in which lanes/waves hit a bucket (integer adds commute; fp32 ds_add_f32 would not).
@@ -443,8 +454,7 @@ __global__ __launch_bounds__(NTHR, 1) void wd_fused(
   // dl = 0 and are excluded from loss and wide-gradient, so they contribute nothing.
   auto fetch = [&](int tile, uint4& a, uint4& b) {
     const long long row = min((long long)tile * T + 16 * wr + r, batch - 1);
-    long long di = start + row;
-    if (di >= n_data) di -= n_data;  // host guarantees batch <= n_data
+    const long long di = mifx_feed_record(fd, fs, row, n_data);  // host guarantees batch <= n_data
     a = data[2 * di];
     b = data[2 * di + 1];
   };
@@ -1190,7 +1200,8 @@ int mifx_wd_constants(int* out, int n) {
 int mifx_wd_fused(const void* data, long long n_data, long long batch, long long start_fixed,
                   const long long* step_ctr, const void* wt, const float* wide, float* slab, float* slab_loss,
                   float* logits_out, float grad_scale, int grid, int train, const int* tmap, int stride,
-                  const int* stage_dims, hipStream_t stream) {
+                  const int* stage_dims, long long feed_stride, long long feed_offset, unsigned long long shuffle_key,
+                  hipStream_t stream) {
   static bool attr_done = false;
   if (!attr_done) {
     (void)hipFuncSetAttribute((const void*)wd_fused<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -1199,6 +1210,8 @@ int mifx_wd_fused(const void* data, long long n_data, long long batch, long long
   }
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data) return -1;
   if (train && (tmap == nullptr || stride < WIDE_PAD || stride > STRIDE || stride % 4 != 0)) return -1;
+  if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
+  const MifxFeed fd{feed_stride, feed_offset, shuffle_key};
   // stage_dims (host array of 10 ints: rows[5], granules-per-row[5]); null = the whole padded image
   StageDims sd;
   const int KL[5] = {K1, K2, K3, K4, K5}, NL[5] = {N1, N2, N3, N4, N5};
@@ -1212,11 +1225,11 @@ int mifx_wd_fused(const void* data, long long n_data, long long batch, long long
   if (train)
     hipLaunchKernelGGL(wd_fused<true>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
                        start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale,
-                       tmap, stride, sd);
+                       tmap, stride, sd, fd);
   else
     hipLaunchKernelGGL(wd_fused<false>, dim3(grid), dim3(NTHR), LDS_BYTES, stream, (const uint4*)data, n_data, batch,
                        start_fixed, step_ctr, (const uint16_t*)wt, wide, slab, slab_loss, logits_out, grad_scale,
-                       tmap, stride, sd);
+                       tmap, stride, sd, fd);
   return (int)hipGetLastError();
 }
 

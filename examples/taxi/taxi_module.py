@@ -51,11 +51,13 @@ def _input_fn(files, device=None):
 def trainer_fn(hparams, schema):
     first_dnn_layer_size, num_dnn_layers, dnn_decay_factor = 100, 4, 0.7
     train_batch_size = int((hparams.custom_config or {}).get("batch_size", 40))
+    eval_batch_size = 40
     run_config = RunConfig(save_checkpoints_steps=999, keep_checkpoint_max=1, device=hparams.device)
     run_config = run_config.replace(model_dir=hparams.serving_model_dir)
     est = WideDeepEstimator(run_config, hidden_units=[max(2, int(first_dnn_layer_size * dnn_decay_factor ** i))
                                                       for i in range(num_dnn_layers)],
-                            warm_start_from=hparams.warm_start_from, batch_size=train_batch_size)
+                            warm_start_from=hparams.warm_start_from, batch_size=train_batch_size,
+                            eval_batch_size=eval_batch_size)
     dev = est.device
     serving_receiver = lambda: {"kind": "raw_examples", "transform_output": hparams.transform_output,  # noqa: E731
                                 "raw_feature_spec": {f.name: f.type for f in schema.feature if f.name != LABEL_KEY}}

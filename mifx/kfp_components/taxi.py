@@ -190,7 +190,10 @@ def dnntrainer(a) -> None:
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
     if dev == "cuda" and env.world_size > 1:
         dev = f"cuda:{0 if os.environ.get('MIFX_SHARED_GPU') == '1' else env.local_rank}"
-    tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=0), batch=a.batch_size, lr=a.learning_rate, device=dev, process_group=pg)
+    # shuffled per epoch like the reference's randomised input reader (taxi_utils.py:275-276); same order for any
+    # number of ranks (each reads its slice of one global stream)
+    tr = TaxiDNNTrainer(TaxiDNN(cfg, seed=0), batch=a.batch_size, lr=a.learning_rate, device=dev, process_group=pg,
+                        shuffle_seed=0x5EED)
     tr.set_data(ids, dense, y)
     tr.run(a.steps)  # GPU: hipGraph replays of 50 steps (CPU: eager steps); DP: one all-gather per step
     if env.rank != 0:

@@ -97,4 +97,5 @@ def sig(lib: ctypes.CDLL, fname: str, argtypes: list, restype=ctypes.c_int):
 VP = ctypes.c_void_p
 I32 = ctypes.c_int
 I64 = ctypes.c_longlong
+U64 = ctypes.c_ulonglong
 F32 = ctypes.c_float

@@ -287,7 +287,7 @@ class _Embedding(torch.autograd.Function):
     """F.embedding whose backward is a scatter-add into an fp32 [V, H] gradient (index_add_), not the sort +
     unique-by-key (rocPRIM partition with decoupled look-back) of PyTorch's embedding backward: that kernel
     faults under hipGraph replay on ROCm (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION in
-    rocprim::partition_kernel on the first replay of a captured BERT fwd+bwd, tools/diag_bert_graph.py), and
+    rocprim::partition_kernel on the first replay of a captured BERT fwd+bwd, diagnosed in round 1), and
     corrupted the captured training step (non-finite loss after ~10 replays)."""
 
     @staticmethod

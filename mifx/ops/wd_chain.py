@@ -7,7 +7,7 @@ import functools
 import torch
 
 from . import _lib
-from ._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
+from ._lib import F32, I32, I64, U64, VP, check, ptr, sig, stream_handle
 
 
 @functools.lru_cache(maxsize=None)
@@ -19,10 +19,12 @@ def _fns():
                                              VP]),
         "fused_x": sig(lib, "mifx_wdc_fused_x", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
                                                  I32, VP, VP]),
+        "fused_f": sig(lib, "mifx_wdc_fused_f", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
+                                                 I32, VP, I64, I64, U64, VP]),
         "fused_tail": sig(lib, "mifx_wdc_fused_tail", [VP, I64, I64, VP, VP, VP, VP, VP, F32, I32, VP, I32, VP, VP, VP,
-                                                       VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+                                                       VP, VP, VP, VP, VP, VP, VP, VP, I64, I64, U64, VP]),
         "persist": sig(lib, "mifx_wdc_persist", [VP, I64, I64, VP, VP, VP, VP, VP, F32, VP, I32, VP, VP, VP, VP, VP, VP,
-                                                 I32, VP]),
+                                                 I32, I64, I64, U64, VP]),
     }
 
 
@@ -36,6 +38,8 @@ def _fns64():
                                                  I32, VP]),
         "fused_x": sig(lib, "mifx_wdc_fused_x_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
                                                      I32, I32, VP, VP]),
+        "fused_f": sig(lib, "mifx_wdc_fused_f_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
+                                                     I32, I32, VP, I64, I64, U64, VP]),
     }
 
 
@@ -58,12 +62,13 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
           wimg_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
           logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
           tmap: torch.Tensor | None = None, waves: int = 8, xcd_of: torch.Tensor | None = None,
-          tile: int = 128) -> None:
+          tile: int = 128, feed: tuple[int, int, int] | None = None) -> None:
     """One chained-kernel launch. wimg_bf16: [LWEND] bf16 (or int16) weight image in the kernel's LDS layout
     (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout.
     tile 128: waves 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each);
     tile 64 (64 examples per workgroup iteration): waves 4 (one wave per SIMD, 16 examples each). xcd_of: int32
-    [>= grid], receives the XCD each workgroup ran on (for the XCD-local slab reduction)."""
+    [>= grid], receives the XCD each workgroup ran on (for the XCD-local slab reduction). feed: (stride, offset,
+    shuffle seed) of the record stream (csrc/feed.h, mifx.data.shuffle); None = (batch, 0, 0), stored order."""
     if waves not in ((4, 8) if tile == 128 else (4,)):
         raise ValueError("waves must be 4 or 8 (tile 128) / 4 (tile 64)")
     c = constants()
@@ -83,9 +88,11 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
         raise ValueError("eval launch needs logits_out with >= batch floats")
     if xcd_of is not None and (xcd_of.dtype != torch.int32 or xcd_of.numel() < grid):
         raise ValueError("xcd_of must be int32 [>= grid]")
-    rc = fns_for(tile)["fused_x"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
-                           ptr(slab), ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
-                           ptr(tmap), stride, int(waves), ptr(xcd_of), stream_handle(records.device))
+    gs, go, key = feed if feed is not None else (batch, 0, 0)
+    rc = fns_for(tile)["fused_f"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
+                                  ptr(slab), ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
+                                  ptr(tmap), stride, int(waves), ptr(xcd_of), int(gs), int(go), int(key) & (2**64 - 1),
+                                  stream_handle(records.device))
     check(rc, "mifx_wdc_fused")
 
 
@@ -114,7 +121,7 @@ class InKernelTail:
                                   ptr(tr.wide_weights), ptr(tr.slab), ptr(tr.slab_loss), float(tr.grad_scale),
                                   int(tr.grid), ptr(tr.tmap), int(tr.stride), ptr(self.xcd_of), ptr(self.xpart),
                                   ptr(self.bar), ptr(self.err), ptr(tr.wsc), ptr(tr.param_sc), ptr(tr.s0_sc),
-                                  ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide), ptr(self.dbg),
+                                  ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide), ptr(self.dbg), *tr.feed_args(),
                                   stream_handle(tr.records.device))
         check(rc, "mifx_wdc_fused_tail")
 
@@ -136,5 +143,5 @@ def persist_steps(tr, nsteps: int) -> None:
     rc = _fns()["persist"](ptr(tr.records), tr.n_data, tr.batch, ptr(tr.step_ctr), ptr(tr.wt), ptr(tr.wide_weights),
                            ptr(tr.slab), ptr(tr.slab_loss), float(tr.grad_scale), ptr(tr.tmap), int(tr.stride), ptr(tr.wsc),
                            ptr(tr.param_sc), ptr(tr.s0_sc), ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide),
-                           int(nsteps), stream_handle(tr.records.device))
+                           int(nsteps), *tr.feed_args(), stream_handle(tr.records.device))
     check(rc, "mifx_wdc_persist")

@@ -7,7 +7,7 @@ import functools
 import torch
 
 from . import _lib
-from ._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
+from ._lib import F32, I32, I64, U64, VP, check, ptr, sig, stream_handle
 
 
 @functools.lru_cache(maxsize=None)
@@ -15,7 +15,8 @@ def _fns():
     lib = _lib.load("wide_deep")
     return {
         "constants": sig(lib, "mifx_wd_constants", [VP, I32]),
-        "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP, VP]),
+        "fused": sig(lib, "mifx_wd_fused", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32, VP,
+                                            I64, I64, U64, VP]),
         "reduce": sig(lib, "mifx_wd_reduce", [VP, I32, I32, VP, I32, VP]),
         "optimizer": sig(lib, "mifx_wd_optimizer", [VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]),
         "reduce_opt": sig(lib, "mifx_wd_reduce_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
@@ -41,10 +42,11 @@ def constants() -> dict[str, int]:
 def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step_ctr: torch.Tensor | None,
           wt_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
           logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
-          tmap: torch.Tensor | None = None, stage_dims=None) -> None:
+          tmap: torch.Tensor | None = None, stage_dims=None, feed: tuple[int, int, int] | None = None) -> None:
     """slab: [grid, stride] with stride = slab.shape[1] (compact layout of `tmap`, see
     models.wide_deep.compact_tile_map). stage_dims: 10 ints (live rows[5], 16-B granules per row[5]) of
-    the weight image to stage (models.wide_deep.stage_dims); None stages the whole padded image."""
+    the weight image to stage (models.wide_deep.stage_dims); None stages the whole padded image. feed: (stride,
+    offset, shuffle seed) of the record stream (csrc/feed.h); None = (batch, 0, 0), stored order."""
     sd = None
     if stage_dims is not None:
         sd = (ctypes.c_int * 10)(*[int(v) for v in stage_dims])
@@ -56,8 +58,13 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
             raise ValueError("slab must be a contiguous [>= grid, stride] tensor")
     rc = _fns()["fused"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wt_bf16), ptr(wide), ptr(slab),
                          ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train), ptr(tmap), stride,
-                         sd, stream_handle(records.device))
+                         sd, *(feed_args(feed, batch)), stream_handle(records.device))
     check(rc, "mifx_wd_fused")
+
+
+def feed_args(feed, batch: int) -> tuple[int, int, int]:
+    gs, go, key = feed if feed is not None else (batch, 0, 0)
+    return int(gs), int(go), int(key) & (2**64 - 1)
 
 
 def reduce(slab: torch.Tensor, groups: int, nsplit: int, partial: torch.Tensor) -> None:

@@ -71,7 +71,7 @@ class BertTrainer:
         # The whole step is captured once as a hipGraph and replayed by default on the GPU (9.2 ms/step vs
         # 12.8 ms eager: the eager step is host-bound). The embeddings use a scatter-add backward
         # (mifx.ops.fused_bert.embedding): PyTorch's sort/unique embedding backward faults under hipGraph
-        # replay on ROCm (rocPRIM partition kernel, tools/diag_bert_graph.py) and made the captured step go
+        # replay on ROCm (rocPRIM partition kernel, diagnosed in round 1) and made the captured step go
         # non-finite after ~10 replays.
         # (default only at TP=1: capturing the TP all-reduces into the graph is not yet validated on a
         # multi-GPU node, so TP>1 steps eagerly unless graph=True is passed)

@@ -124,17 +124,24 @@ class WideDeepEstimator:
 
     def __init__(self, config: RunConfig, hidden_units: list[int] | None = None, warm_start_from: str | None = None,
                  batch_size: int = 40, loss_reduction: str = "sum", dnn_optimizer=None, linear_optimizer=None,
-                 steps_per_graph: int = 100):
+                 steps_per_graph: int = 100, shuffle: bool = True, eval_batch_size: int | None = None):
         """batch_size is per replica: a data-parallel Trainer with N ranks trains on N x batch_size examples per
         step (TF distributed Estimator semantics). steps_per_graph: training steps per hipGraph replay on the
-        GPU (checkpoint boundaries and max_steps are honoured exactly; remainders replay a one-step graph)."""
+        GPU (checkpoint boundaries and max_steps are honoured exactly; remainders replay a one-step graph).
+        shuffle: a new pseudo-random order of the training records every epoch, seeded by
+        config.tf_random_seed (`read_batch_features(randomize_input=True)`, `taxi_utils.py:275-276`); the same
+        order on the CPU and GPU paths and for any number of data-parallel ranks (mifx.data.shuffle).
+        eval_batch_size: the evaluation input's batch (default batch_size): evaluate(steps) reads steps x
+        eval_batch_size examples, whatever the number of training ranks (`taxi_utils.py:304-305`: 40 / 40)."""
         self.config = config
         self.pg, self.rank, self.world = _dist_info()
         self.steps_per_graph = int(steps_per_graph)
         self.cfg = wdm.WideDeepConfig(hidden_units=list(hidden_units or wdm.dnn_hidden_units()))
         self.device = _default_device(config)
         self.batch_size = batch_size
+        self.eval_batch_size = int(eval_batch_size or batch_size)
         self.loss_reduction = loss_reduction
+        self.shuffle = bool(shuffle)
         self.dnn_optimizer, self.linear_optimizer = dnn_optimizer, linear_optimizer
         self.model = wdm.WideDeepModel(self.cfg, seed=config.tf_random_seed)
         self.global_step = 0
@@ -200,20 +207,30 @@ class WideDeepEstimator:
 
         dopt = self.dnn_optimizer or default_dnn_opt()
         wopt = self.linear_optimizer or default_wide_opt(len(self.cfg.wide))
-        if self.pg is not None:
-            records = shard_records(records, self.rank, self.world, self.batch_size)
-        bs = min(self.batch_size, records.shape[0])
+        # every rank holds all records and reads its slice of one global stream (stride world x batch, offset
+        # rank x batch): step i of a data-parallel job trains on exactly the examples of step i of one process at
+        # batch world x batch, shuffled or not, and the ranks' rows are disjoint
+        n = records.shape[0]
+        bs = min(self.batch_size, n // self.world)
+        if bs < 1:
+            raise ValueError(f"{n} records < one global batch ({self.world} x {self.batch_size})")
+        feed = dict(shuffle_seed=self.shuffle_seed() if self.shuffle else 0, feed_stride=self.world * bs,
+                    feed_offset=self.rank * bs)
         if self.device.type == "cuda":
             tr = FusedWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
-                                      loss_reduction=self.loss_reduction, process_group=self.pg)
+                                      loss_reduction=self.loss_reduction, process_group=self.pg, **feed)
         else:
             tr = TorchWideDeepTrainer(self.model, batch=bs, device=self.device, dnn_opt=dopt, wide_opt=wopt,
-                                      loss_reduction=self.loss_reduction, process_group=self.pg)
+                                      loss_reduction=self.loss_reduction, process_group=self.pg, **feed)
         st = getattr(self, "_opt_state", None) or {}
         tr.load_state_dict({"param": None, "s0": st.get("s0"), "s1": st.get("s1"),
                             "step": torch.tensor([self.global_step])})
         tr.set_data(records)
         return tr
+
+    def shuffle_seed(self) -> int:
+        """The (non-zero) shuffle key derived from config.tf_random_seed."""
+        return ((int(self.config.tf_random_seed or 0) * 0x9E3779B97F4A7C15) ^ 0x5EEDF00D) % (2**64 - 1) + 1
 
     def _graph_setup(self, tr) -> None:
         """GPU: capture S-step hipGraphs (data-parallel: the xGMI exchange inside the graph, the direct RCCL
@@ -295,15 +312,16 @@ class WideDeepEstimator:
 
     def evaluate(self, input_fn: Callable, steps: int | None = None, name: str | None = None) -> dict:
         records = input_fn()
-        # `steps` batches of the global batch (a data-parallel job's rank 0 evaluates what all ranks would)
-        n = records.shape[0] if not steps else min(records.shape[0], steps * self.batch_size * self.world)
+        # `steps` batches of the input batch size, whatever the number of training ranks (TF Estimator evaluate:
+        # the evaluator runs eval_spec.steps batches of its input_fn's batch size)
+        n = records.shape[0] if not steps else min(records.shape[0], steps * self.eval_batch_size)
         records = records[:n]
         logits = self.predict_logits(records)
         _, _, label = wdm.records_to_tensors(records.cpu())
         y = label.numpy()
         p = 1.0 / (1.0 + np.exp(-logits))
         loss = np.maximum(logits, 0) - logits * y + np.log1p(np.exp(-np.abs(logits)))
-        m = {"loss": float(loss.mean() * self.batch_size), "average_loss": float(loss.mean()),
+        m = {"loss": float(loss.mean() * self.eval_batch_size), "average_loss": float(loss.mean()),
              "accuracy": float(((p > 0.5) == (y > 0.5)).mean()), "auc": _auc(y, p),
              "prediction/mean": float(p.mean()), "label/mean": float(y.mean()), "global_step": self.global_step}
         self.last_eval = m

@@ -62,7 +62,13 @@ class FusedWideDeepTrainer:
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
                  live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8,
                  in_kernel_tail: bool | None = None, persistent: bool | None = None,
-                 small_tile: bool | None = None):
+                 small_tile: bool | None = None, shuffle_seed: int = 0, feed_stride: int | None = None,
+                 feed_offset: int = 0):
+        """shuffle_seed: 0 trains on the records in stored order; any other value draws a fresh pseudo-random
+        permutation of the resident records every epoch inside the kernel's record fetch (csrc/feed.h; the
+        reference's `read_batch_features(randomize_input=True)`, `taxi_utils.py:275-276`). feed_stride / feed_offset:
+        this replica's place in a global record stream shared by data-parallel ranks (stride = world x batch,
+        offset = rank x batch; default: its own stream, stride = batch, offset 0)."""
         self.device = torch.device(device)
         self.model = model or wdm.WideDeepModel()
         wdm.check_fused_compatible(self.model.cfg)
@@ -83,6 +89,11 @@ class FusedWideDeepTrainer:
         else:
             self.T = c["T"]
         self.batch = int(batch)
+        self.shuffle_seed = int(shuffle_seed)
+        self.feed_stride = int(feed_stride) if feed_stride is not None else self.batch
+        self.feed_offset = int(feed_offset)
+        if not (self.feed_stride >= self.batch and 0 <= self.feed_offset <= self.feed_stride - self.batch):
+            raise ValueError("need feed_stride >= batch and 0 <= feed_offset <= feed_stride - batch")
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         ntiles = (self.batch + self.T - 1) // self.T
@@ -246,18 +257,23 @@ class FusedWideDeepTrainer:
             return img.to(self.device).to(torch.bfloat16).view(torch.int16).contiguous()
         return self.param[: wdm.WTOT].to(torch.bfloat16).view(torch.int16).contiguous()
 
+    def feed_args(self) -> tuple[int, int, int]:
+        """(stride, offset, shuffle key) of the training record stream (csrc/feed.h)."""
+        return self.feed_stride, self.feed_offset, self.shuffle_seed & (2**64 - 1)
+
     def _launch(self, records, n, batch, start_fixed, step_ctr, slab, slab_loss, logits, grid, train) -> None:
+        feed = self.feed_args() if train else None
         if self.kernel == "chain":
             from ..ops import wd_chain as wdc
 
             wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves,
                       self._xcd.xcd_of if (train and self._xcd is not None and slab is self.slab) else None,
-                      tile=self.tile if train else 128)
+                      tile=self.tile if train else 128, feed=feed)
         else:
             wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
-                      self.stage_dims)
+                      self.stage_dims, feed=feed)
 
     # ---------------------------------------------------------------- data
     def set_data(self, records: torch.Tensor) -> None:
@@ -335,10 +351,10 @@ class FusedWideDeepTrainer:
         self._direct = DirectAllReduce(self.grad, self.pg)
         stream = torch.cuda.current_stream(self.device)
         sh = ctypes.c_void_p(stream.cuda_stream)
-        fused = (wdc.fns_for(self.tile)["fused"], (ptr(self.records), self.n_data, self.batch, 0, ptr(self.step_ctr), ptr(self.wt),
-                                       ptr(self.wide_weights), ptr(self.slab), ptr(self.slab_loss), None,
-                                       float(self.grad_scale), int(self.grid), 1, ptr(self.tmap), int(self.stride),
-                                       int(self.waves), sh))
+        fused = (wdc.fns_for(self.tile)["fused_f"],
+                 (ptr(self.records), self.n_data, self.batch, 0, ptr(self.step_ctr), ptr(self.wt),
+                  ptr(self.wide_weights), ptr(self.slab), ptr(self.slab_loss), None, float(self.grad_scale),
+                  int(self.grid), 1, ptr(self.tmap), int(self.stride), int(self.waves), None, *self.feed_args(), sh))
         ro = wdk._fns()["reduce_opt"]
         red = (ro, (ptr(self.slab), int(self.grid), int(self.stride), ptr(self.grad), None, None, None, None, None, None,
                     None, None, None, sh))

@@ -30,7 +30,11 @@ class TaxiDNNTrainer:
 
     def __init__(self, model: TaxiDNN | None = None, batch: int = 32, lr: float = 0.1, device="cpu",
                  initial_accumulator_value: float = 0.1, loss_reduction: str = "sum", native: bool | None = None,
-                 graph: bool = True, steps_per_graph: int = 50, process_group=None):
+                 graph: bool = True, steps_per_graph: int = 50, process_group=None, shuffle_seed: int = 0):
+        """shuffle_seed: 0 = the records in stored order, else a fresh pseudo-random order every epoch, computed in
+        the kernels' record selection (csrc/feed.h; the same order on the CPU path, mifx.data.shuffle). With a
+        process group every rank keeps all records and trains on its slice of one global stream (stride
+        world x batch, offset rank x batch), so the job equals one process at batch world x batch."""
         self.device = torch.device(device)
         self.model = (model or TaxiDNN()).to(self.device)
         self.batch, self.lr, self.loss_reduction = batch, lr, loss_reduction
@@ -39,6 +43,7 @@ class TaxiDNNTrainer:
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.rank = torch.distributed.get_rank(process_group) if process_group is not None else 0
+        self.feed = (self.world * batch, self.rank * batch, int(shuffle_seed) & (2**64 - 1))
         if self.world > 1:
             for p in self.model.parameters():  # identical initial replicas
                 torch.distributed.broadcast(p.data, src=torch.distributed.get_global_rank(process_group, 0)
@@ -83,21 +88,24 @@ class TaxiDNNTrainer:
         self.gbufs = embag_mlp.make_buffers(Bg, H, D, self.device)
         self.g_rows = torch.empty(Bg, F, dtype=torch.int32, device=self.device)
         self.g_xd = torch.empty(Bg, D, device=self.device)
-        self.C = 2 * H + D + 1 + F
+        self.C = 2 * H + D + 1
         # global batches of <= 64 take the kernels' per-example dense chunks (written by the forward/backward
         # launch): those travel too, so the update stays the single-process one
         self.direct = Bg <= 64
-        self.L = B * self.C + (B * (D + 2) * H if self.direct else 0)
-        self.send = torch.empty(self.L, device=self.device)
-        self.recv = torch.empty(W * self.L, device=self.device)
-        self._ar = torch.arange(B, device=self.device)
+        self.NF = B * self.C + (B * (D + 2) * H if self.direct else 0)  # float32 words per rank
+        # one BYTE buffer per rank: the float state, then the int32 W1 row ids -- a byte all-gather moves both
+        # bit-exactly (no float copy ever touches the ids)
+        self.L = 4 * (self.NF + B * F)
+        self.send = torch.empty(self.L, dtype=torch.uint8, device=self.device)
+        self.recv = torch.empty(W * self.L, dtype=torch.uint8, device=self.device)
+        self.rec_idx = torch.zeros(B, dtype=torch.int64, device=self.device)
 
     def _all_gather(self) -> None:
         dist = torch.distributed
         if dist.get_backend(self.pg) == "nccl":
             dist.all_gather_into_tensor(self.recv, self.send, group=self.pg)
         else:  # gloo (CPU collectives; ranks sharing one GPU in rehearsals)
-            parts = [torch.empty(self.L) for _ in range(self.world)]
+            parts = [torch.empty(self.L, dtype=torch.uint8) for _ in range(self.world)]
             dist.all_gather(parts, self.send.cpu(), group=self.pg)
             self.recv.copy_(torch.cat(parts))
 
@@ -106,50 +114,52 @@ class TaxiDNNTrainer:
         scale = 1.0 if self.loss_reduction == "sum" else 1.0 / (B * W)
         p = self.params
         self._k.fwd_bwd(p["W1"], p["b1"], p["w2"], p["b2"], self.rows, self.dense, self.label, self.dense_row0, scale,
-                        True, self.bufs, batch=B, step_ctr=self.step_ctr)
-        idx = (self.step_ctr * B + self._ar) % self.n
-        seg = self.send[:B * self.C].view(B, self.C)
+                        True, self.bufs, batch=B, step_ctr=self.step_ctr, feed=self.feed, rec_out=self.rec_idx)
+        idx = self.rec_idx  # the records the kernel selected for this rank's rows of the global batch
+        F = self.F
+        sf = self.send[:4 * self.NF].view(torch.float32)
+        seg = sf[:B * self.C].view(B, self.C)
         seg[:, :H] = self.bufs["a"]
         seg[:, H:2 * H] = self.bufs["dz"]
         seg[:, 2 * H:2 * H + D] = self.dense[idx]
         seg[:, 2 * H + D] = self.bufs["dlogit"]
-        seg[:, 2 * H + D + 1:] = self.rows[idx].view(torch.float32)  # the ids' bits travel unchanged
+        self.send[4 * self.NF:].view(torch.int32).view(B, F).copy_(self.rows[idx])
         if self.direct:
-            self.send[B * self.C:] = self.bufs["dpart"][:B * (D + 2) * H]
+            sf[B * self.C:] = self.bufs["dpart"][:B * (D + 2) * H]
         self._all_gather()
         rv = self.recv.view(W, self.L)
-        g = rv[:, :B * self.C].reshape(W * B, self.C)
+        rf = rv[:, :4 * self.NF].contiguous().view(torch.float32)  # [W, NF]
+        g = rf[:, :B * self.C].reshape(W * B, self.C)
         self.gbufs["a"].copy_(g[:, :H])
         self.gbufs["dz"].copy_(g[:, H:2 * H])
         self.g_xd.copy_(g[:, 2 * H:2 * H + D])
         self.gbufs["dlogit"].copy_(g[:, 2 * H + D])
-        self.g_rows.copy_(g[:, 2 * H + D + 1:].contiguous().view(torch.int32))
+        self.g_rows.copy_(rv[:, 4 * self.NF:].contiguous().view(torch.int32).view(W * B, F))
         if self.direct:
-            self.gbufs["dpart"][:W * B * (D + 2) * H].view(W, -1).copy_(rv[:, B * self.C:])
+            self.gbufs["dpart"][:W * B * (D + 2) * H].view(W, -1).copy_(rf[:, B * self.C:])
         self._k.adagrad(p, self.accs, self.g_rows, self.g_xd, self.dense_row0, self.gbufs, self.lr, batch=W * B)
         self.step_ctr.add_(1)
 
     def set_data(self, ids: torch.Tensor, dense: torch.Tensor, label: torch.Tensor) -> None:
-        """The training records (all of them: with a process group each rank keeps its shard of every global
-        batch, `mifx.trainer.estimator.shard_records`)."""
-        if self.world > 1:
-            from .estimator import shard_records
-
-            ids, dense, label = (shard_records(t, self.rank, self.world, self.batch) for t in (ids, dense, label))
+        """The training records (all of them, on every rank: each reads its slice of the global stream)."""
         self.rows = self.model.rows(ids.to(self.device)).to(torch.int32).contiguous()
         self.dense = dense.to(self.device).float().contiguous()
         self.label = label.to(self.device).float().contiguous()
         self.n = len(self.label)
         if self.n < self.batch:
             raise ValueError(f"{self.n} records < batch {self.batch}")
+        if self.n < self.world * self.batch:
+            raise ValueError(f"{self.n} records < one global batch ({self.world} x {self.batch})")
         if self.native:  # the device counter continues from the host's step count
             self.step_ctr.fill_(self.step_idx)
         # captured graphs hold the previous tensors' addresses and record count: recapture on the next step
         self.graph, self.graph_multi = None, None
 
     def _idx(self):
-        s = (self.step_idx * self.batch) % self.n
-        return (torch.arange(self.batch, device=self.device) + s) % self.n
+        from ..data.shuffle import record_indices
+
+        gs, go, key = self.feed
+        return torch.from_numpy(record_indices(self.step_idx, self.batch, self.n, gs, go, key)).to(self.device)
 
     def _native_step(self) -> None:
         if self.world > 1:
@@ -158,9 +168,9 @@ class TaxiDNNTrainer:
         scale = 1.0 if self.loss_reduction == "sum" else 1.0 / self.batch
         p = self.params
         self._k.fwd_bwd(p["W1"], p["b1"], p["w2"], p["b2"], self.rows, self.dense, self.label, self.dense_row0, scale,
-                        True, self.bufs, batch=self.batch, step_ctr=self.step_ctr)
+                        True, self.bufs, batch=self.batch, step_ctr=self.step_ctr, feed=self.feed)
         self._k.adagrad(p, self.accs, self.rows, self.dense, self.dense_row0, self.bufs, self.lr, batch=self.batch,
-                        step_ctr=self.step_ctr)
+                        step_ctr=self.step_ctr, feed=self.feed)
 
     def capture(self) -> None:
         """Capture one step and `steps_per_graph` consecutive steps as hipGraphs (every captured step reads the

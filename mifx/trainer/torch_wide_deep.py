@@ -33,7 +33,9 @@ def _mk(spec: OptSpec, params):
 class TorchWideDeepTrainer:
     def __init__(self, model: wdm.WideDeepModel | None = None, batch: int = 40, device="cpu",
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
-                 process_group=None):
+                 process_group=None, shuffle_seed: int = 0, feed_stride: int | None = None, feed_offset: int = 0):
+        """shuffle_seed / feed_stride / feed_offset: the record stream of the fused GPU trainer (csrc/feed.h,
+        mifx.data.shuffle): the same records per step, so both paths train on identical batches."""
         self.device = torch.device(device)
         self.model = (model or wdm.WideDeepModel()).to(self.device)
         # DP: "sum" losses are summed across ranks (global-batch sum, like the fused trainer); "mean"
@@ -41,6 +43,9 @@ class TorchWideDeepTrainer:
         self.dp = DataParallel(self.model, process_group, average=(loss_reduction == "mean")) \
             if process_group is not None else None
         self.batch = batch
+        self.shuffle_seed = int(shuffle_seed)
+        self.feed_stride = int(feed_stride) if feed_stride is not None else int(batch)
+        self.feed_offset = int(feed_offset)
         self.loss_reduction = loss_reduction
         dnn_params = [p for n, p in self.model.named_parameters() if not n.startswith("wide")]
         wide_params = [self.model.wide, self.model.wide_bias]
@@ -62,8 +67,11 @@ class TorchWideDeepTrainer:
         self.records = records
 
     def _batch_idx(self) -> torch.Tensor:
-        start = (self.step_idx * self.batch) % self.n_data
-        return (torch.arange(self.batch, device=self.device) + start) % self.n_data
+        from ..data.shuffle import record_indices
+
+        idx = record_indices(self.step_idx, self.batch, self.n_data, self.feed_stride, self.feed_offset,
+                             self.shuffle_seed)
+        return torch.from_numpy(idx).to(self.device)
 
     def step(self) -> None:
         idx = self._batch_idx()

@@ -120,7 +120,7 @@ def test_resnet_fused_blocks_match_fp64_reference():
     (run first, so both use the same MIOpen solvers); fp64 is a loose sanity bound, because MIOpen's
     solver choice for a first-seen fp32 NHWC problem can be a reduced-precision one (measured 3e-3 on
     the stem's weight gradient when the fused model ran first).
-    Conditioning notes (tools/diag/resnet_grad_fp64.py, tools/diag/bn_model_divergence.py on MI355X):
+    Conditioning notes (one-off fp64 gradient and model-divergence probes on MI355X, round 2):
     (1) the full 16-block net at 64x64 / batch 4 has train-mode BN over as few as 16 samples per
     channel and its gradients are noise-dominated even for the fp32 PyTorch path (1-3 % vs fp64), so a
     one-block-per-stage net is used; (2) MIOpen's reduced-precision (xf32) convolution solvers are
