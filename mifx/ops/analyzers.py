@@ -172,6 +172,16 @@ def order_statistics(x, ks, device=None) -> np.ndarray:
         return np.zeros(0)
     if ks.min() < 0 or ks.max() >= n:
         raise IndexError("rank out of range")
+    # +-inf: ranks in the infinite tails resolve directly; the histogram selection runs over the finite values
+    ninf, pinf = int((t == -np.inf).sum()), int((t == np.inf).sum())
+    if ninf or pinf:
+        res = np.empty(ks.size)
+        lo_tail, hi_tail = ks < ninf, ks >= n - pinf
+        res[lo_tail], res[hi_tail] = -np.inf, np.inf
+        mid = ~(lo_tail | hi_tail)
+        if mid.any():
+            res[mid] = order_statistics(t[torch.isfinite(t)], ks[mid] - ninf, device)
+        return res
     lo, hi = (float(v) for v in torch.aminmax(t))
     if hi == lo:
         return np.full(ks.size, lo)

@@ -186,7 +186,8 @@ def fill_in_missing(x, default=None) -> np.ndarray:
         ser = pd.Series(a, dtype=object)
         miss = ser.isna().to_numpy()
         kind = pd.api.types.infer_dtype(ser[~miss], skipna=True) if (~miss).any() else "empty"
-        is_str = kind in ("string", "bytes", "mixed")
+        # any column holding a str / bytes value stays a string column ("mixed-integer": ints mixed with strings)
+        is_str = kind in ("string", "bytes", "mixed", "mixed-integer", "mixed-integer-float")
         d = ("" if is_str else 0) if default is None else default
         if is_str:
             out = a.copy()

@@ -123,8 +123,13 @@ def _vocab_merge(accs: list[dict], params: dict) -> list[str]:
 
 # worker-side quantile rounds: the analyzer's input (non-NaN) is cached per analyzer index
 def _q_init(a: np.ndarray) -> dict:
+    """Count, FINITE min / max and the +-inf counts of the non-NaN input: the selection rounds bin the finite range
+    only (linspace over an infinite interval is NaN everywhere); ranks in the infinite tails resolve directly."""
     a = a[~np.isnan(a)]
-    return {"n": int(a.size), "min": float(a.min()) if a.size else np.inf, "max": float(a.max()) if a.size else -np.inf}
+    fin = a[np.isfinite(a)]
+    return {"n": int(a.size), "min": float(fin.min()) if fin.size else np.inf,
+            "max": float(fin.max()) if fin.size else -np.inf,
+            "ninf": int(np.count_nonzero(a == -np.inf)), "pinf": int(np.count_nonzero(a == np.inf))}
 
 
 def _q_hist(a: np.ndarray, intervals: list) -> list:
@@ -262,9 +267,19 @@ def _ranks_higher(n: int, num_buckets: int) -> np.ndarray:
 def _distributed_order_stats(workers: ShardWorkers, idx: int, inits: list[dict], ranks: np.ndarray) -> np.ndarray:
     lo = min(a["min"] for a in inits)
     hi = max(a["max"] for a in inits)
+    n = sum(a["n"] for a in inits)
+    ninf = sum(a.get("ninf", 0) for a in inits)
+    pinf = sum(a.get("pinf", 0) for a in inits)
     out = np.full(ranks.size, np.nan)
-    # per pending rank: [lo, hi] (closed) holds it; `below` values lie under lo
-    state = {j: [lo, hi, 0] for j in range(ranks.size)}
+    # ranks in the infinite tails need no selection; the rest select among the finite values in [lo, hi]
+    state = {}
+    for j in range(ranks.size):
+        if ranks[j] < ninf:
+            out[j] = -np.inf
+        elif ranks[j] >= n - pinf:
+            out[j] = np.inf
+        else:  # per pending rank: [lo, hi] (closed) holds it; `below` values (the -inf ones first) lie under lo
+            state[j] = [lo, hi, ninf]
     while state:
         pend = sorted(state)
         done = [j for j in pend if state[j][0] == state[j][1]]

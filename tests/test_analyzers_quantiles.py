@@ -114,3 +114,34 @@ def test_transform_bucketize_boundaries_on_gpu_equal_host(monkeypatch):
     out_c, st_c = mt.analyze(fn, {"lat": lat}, device=None)
     assert np.array_equal(out_g["b"], out_c["b"])
     assert st_g.to_dict() == st_c.to_dict() if hasattr(st_g, "to_dict") else True
+
+
+def _inf_case(rng):
+    a = np.concatenate([rng.normal(size=700), [np.inf] * 3, [-np.inf] * 5, [np.nan] * 2])
+    rng.shuffle(a)
+    return a
+
+
+def test_host_order_statistics_with_infinities():
+    rng = np.random.default_rng(11)
+    a = _inf_case(rng)
+    v = np.sort(a[~np.isnan(a)])
+    ks = np.array([0, 4, 5, 6, 300, 704, 705, 707])
+    assert np.array_equal(A.order_statistics(a, ks), v[ks])
+    q = np.linspace(0, 1, 11)
+    assert np.array_equal(A.quantiles(a, q, "higher"), np.quantile(v, q, method="higher"))
+
+
+@pytest.mark.gpu
+def test_gpu_order_statistics_with_infinities():
+    """+-inf values: the tails resolve directly, the histogram selection runs over the finite values (an infinite
+    range would make every bin edge NaN)."""
+    rng = np.random.default_rng(11)
+    a = _inf_case(rng)
+    v = np.sort(a[~np.isnan(a)])
+    ks = np.array([0, 4, 5, 6, 300, 704, 705, 707])
+    assert np.array_equal(A.order_statistics(a, ks, device="cuda"), v[ks])
+    q = np.linspace(0, 1, 11)
+    assert np.array_equal(A.quantiles(a, q, "higher", device="cuda"), np.quantile(v, q, method="higher"))
+    allinf = np.array([np.inf, -np.inf, np.inf])
+    assert np.array_equal(A.order_statistics(allinf, np.array([0, 1, 2]), device="cuda"), np.sort(allinf))

@@ -82,6 +82,9 @@ def test_fill_in_missing():
     assert mt.fill_in_missing(np.array([None, "x"], object)).tolist() == ["", "x"]
     assert mt.fill_in_missing(np.array([1.0, np.nan])).tolist() == [1.0, 0.0]
     assert mt.fill_in_missing(np.array([None, 3], object)).tolist() == [0, 3]
+    # ints mixed with strings stay a string column (pandas infers "mixed-integer"): no value is coerced to NaN
+    assert mt.fill_in_missing(np.array([None, 3, "a"], object)).tolist() == ["", 3, "a"]
+    assert mt.fill_in_missing(np.array([1.5, None, "b"], object)).tolist() == [1.5, "", "b"]
 
 
 def test_tfrecord_roundtrip_and_corruption(tmp_path):

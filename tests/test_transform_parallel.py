@@ -139,3 +139,25 @@ def test_transform_component_num_workers(tmp_path):
                 np.testing.assert_allclose(b[c].to_numpy(), a[c].to_numpy(), rtol=1e-9, atol=1e-12)
             else:
                 assert (a[c].to_numpy() == b[c].to_numpy()).all(), c
+
+
+def test_sharded_quantiles_with_infinities_terminate_and_match():
+    """A column with +-inf: the sharded selection bins the finite range only and resolves the infinite tails
+    directly (before, linspace over [-inf, hi] made every edge NaN and a crowded bin never narrowed)."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.normal(0, 1, 4000), [np.inf] * 300, [-np.inf] * 700])
+    rng.shuffle(x)
+    parts = np.array_split(x, 3)
+    inits = [tpar._q_init(p) for p in parts]
+
+    class _Local:
+        def call(self, msg):
+            op, _, iv = msg
+            f = tpar._q_hist if op == "qhist" else tpar._q_gather
+            return [f(p, iv) for p in parts]
+
+    n = sum(i["n"] for i in inits)
+    ranks = tpar._ranks_higher(n, 20)
+    qs = tpar._distributed_order_stats(_Local(), 0, inits, ranks)
+    assert np.array_equal(qs, np.sort(x)[ranks])
+    assert qs[0] == -np.inf and qs[-1] == np.inf
