@@ -137,18 +137,18 @@ def ls_of_q(sigma: float = 20.0, order: float = 20.0, num_classes: int = 10, num
     """`plot_ls_q.py`: the local sensitivity (upward change beta(bu(q)) - beta(q)) of GNMax's data-dependent RDP
     bound as a function of q in [0, 0.1], with the q0 / q1 landmarks of the smooth-sensitivity analysis."""
     def beta(q):
-        return ss._rdp_gnmax(sigma, math.log(q), order)
+        return ss.rdp_gnmax(sigma, math.log(q), order)
 
     def delta_beta(q):
         if q == 0 or q > 0.8:
             return 0.0
-        bq, bu, bl = beta(q), beta(ss._bu(q, sigma, num_classes)), beta(ss._bl(q, sigma, num_classes))
+        bq, bu, bl = beta(q), beta(ss.q_upper(q, sigma, num_classes)), beta(ss.q_lower(q, sigma, num_classes))
         assert bl <= bq <= bu
         return bu - bq
 
     xs = np.linspace(0, 0.1, num=num, endpoint=True)
     return {"q": xs, "ls": np.array([delta_beta(x) for x in xs]),
-            "q0": math.exp(ss._logq0(sigma, order)), "q1": math.exp(ss._logq1(sigma, order, num_classes))}
+            "q0": math.exp(ss.compute_logq0_gnmax(sigma, order)), "q1": math.exp(ss.gnmax_logq1(sigma, order, num_classes))}
 
 
 def _plots(figdir: str, res: dict) -> list[str]:

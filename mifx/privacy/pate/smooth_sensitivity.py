@@ -1,13 +1,34 @@
-"""Smooth sensitivity of the PATE-2018 data-dependent RDP (GNMax and threshold mechanisms).
+"""Smooth sensitivity of the PATE-2018 data-dependent privacy cost (GNMax and the threshold check).
 
-Reference: `research/pate_2018/smooth_sensitivity.py:27-419` — logq0 (where the data-dependent
-bound meets the data-independent one, by Brent root finding), local-sensitivity bounds at every
-distance in O(teachers * classes), discounted max, RDP of the smooth-sensitivity release
-(Thm. 23), and the symbolic monotonicity checks (Conditions 5/6) done with sympy."""
+Papernot et al., "Scalable Private Learning with PATE" (ICLR 2018), Appendix B-C. Releasing a DATA-DEPENDENT
+RDP cost leaks the votes, so the paper releases it with noise scaled to a beta-smooth upper bound on its local
+sensitivity, SS_beta = max_d e^{-beta d} LS(d), where LS(d) bounds how much the cost can change between any two
+neighbouring vote histograms at distance d from the actual one.
+
+GNMax (Gaussian noisy max, noise sigma, m classes). With q = Pr[answer != plurality] (bounded from the votes),
+the data-dependent RDP at order lambda (Prop. 10) is
+    beta(q) = log((1-q) A^{lambda-1} + q B^{lambda-1}) / (lambda - 1),
+    mu2 = sigma sqrt(log 1/q), mu1 = mu2 + 1, eps_i = mu_i / sigma^2,
+    A = (1-q) / (1 - (q e^{eps2})^{1 - 1/mu2}),  B = e^{eps1} / q^{1/(mu1-1)},
+valid (and better than the data-independent lambda / sigma^2) for q below a threshold q0 (found here by root
+finding where the two bounds meet). One teacher changing its vote moves q inside [B_l(q), B_u(q)] with
+    B_{l,u}(q) = (m-1)/2 erfc(erfc^{-1}(2q / (m-1)) +- 1/sigma),
+so LS at the current histogram is max(beta(B_u(q)) - beta(q), beta(q) - beta(B_l(q))). Because beta is
+non-decreasing in q below q0 (Condition 5, checked symbolically by check_conditions), the cost is flat above q0
+and LS is constant once q is pushed into [q1, q0] (q1 = B_l(q0)). LS(d) follows the histogram as d votes move:
+from the plurality to the runner-up while q < q1 ("right", q grows), or towards the plurality while q > q0 ("left").
+
+Threshold check (Gaussian noise sigma on the plurality count v vs a threshold T): the RDP of the check is a
+function of v alone (rdp2018.compute_rdp_threshold of log Pr[v + N(0, sigma^2) >= T]); LS at distance d is the
+largest one-vote change of that table at the vote counts d away from the current plurality.
+
+Reference: `research/pate_2018/smooth_sensitivity.py:43-412`; its numeric goldens are pinned in
+tests/test_privacy.py (`smooth_sensitivity_test.py:28-126`)."""
 from __future__ import annotations
 
 import functools
 import math
+from dataclasses import dataclass
 
 import numpy as np
 import scipy.optimize
@@ -17,143 +38,180 @@ import scipy.stats
 from . import rdp2018 as core
 
 
-def _mu(sigma: float, logq: float):
-    mu2 = sigma * math.sqrt(-logq)
-    return mu2 + 1, mu2
+# ------------------------------------------------------------------------------------------- GNMax
+@dataclass(frozen=True)
+class GNMaxCost:
+    """The data-dependent RDP of one GNMax answer as a function of log q, at noise sigma and order lambda."""
 
+    sigma: float
+    order: float
 
-def _data_dep_bound(sigma: float, logq: float, order: float) -> float:
-    var = sigma ** 2
-    mu1, mu2 = _mu(sigma, logq)
-    eps1, eps2 = mu1 / var, mu2 / var
-    log1q = np.log1p(-math.exp(logq))
-    log_a = (order - 1) * (log1q - np.log1p(-math.exp((logq + eps2) * (1 - 1 / mu2))))
-    log_b = (order - 1) * (eps1 - logq / (mu1 - 1))
-    return float(np.logaddexp(log1q + log_a, logq + log_b) / (order - 1))
+    def _mu(self, logq: float) -> tuple[float, float]:
+        mu2 = self.sigma * math.sqrt(-logq)
+        return mu2 + 1.0, mu2
 
+    def dependent(self, logq: float) -> float:
+        """Prop. 10's bound, evaluated in log space (log1p for the 1 - q factors)."""
+        lam, var = self.order, self.sigma ** 2
+        mu1, mu2 = self._mu(logq)
+        eps1, eps2 = mu1 / var, mu2 / var
+        log_1mq = math.log1p(-math.exp(logq))
+        log_a = (lam - 1) * (log_1mq - math.log1p(-math.exp((logq + eps2) * (1 - 1 / mu2))))
+        log_b = (lam - 1) * (eps1 - logq / (mu1 - 1))
+        return float(np.logaddexp(log_1mq + log_a, logq + log_b)) / (lam - 1)
 
-def compute_logq0_gnmax(sigma: float, order: float) -> float:
-    """logq above which the data-independent bound is the better one."""
-    def valid(logq):
-        mu1, mu2 = _mu(sigma, logq)
-        if mu1 < order:
+    def independent(self) -> float:
+        return core.rdp_data_independent_gaussian(self.sigma, self.order)
+
+    def _valid(self, logq: float) -> bool:
+        """Prop. 10's preconditions: mu1 >= lambda and q <= e^{(mu2-1) eps2} / (mu1/(mu1-1) mu2/(mu2-1))^{mu2}."""
+        mu1, mu2 = self._mu(logq)
+        if mu1 < self.order:
             return False
-        eps2 = mu2 / sigma ** 2
+        eps2 = mu2 / self.sigma ** 2
         return logq <= (mu2 - 1) * eps2 - mu2 * math.log(mu1 / (mu1 - 1) * mu2 / (mu2 - 1))
 
-    def gap(logq):
-        return _data_dep_bound(sigma, logq, order) - core.rdp_data_independent_gaussian(sigma, order)
+    @functools.cached_property
+    def logq0(self) -> float:
+        """log q0: where the data-dependent bound rises to the data-independent one (the cost is flat above)."""
+        s, lam = self.sigma, self.order
+        # the largest logq that meets the preconditions with margin: mu2 > 1 and mu2 >= lambda - 0.99,
+        # and mu2 >= 1 + sigma (so that the (mu2 - 1) eps2 term of the validity test is positive)
+        top = -max((1 + 1 / s) ** 2, ((lam - 0.99) / s) ** 2, 1 / s ** 2)
+        if not self._valid(top):
+            raise AssertionError("GNMax bound not valid at the search start")
 
-    hi = min(-(1 + 1.0 / sigma) ** 2, -((order - 0.99) / sigma) ** 2, -1 / sigma ** 2)
-    assert valid(hi)
-    if gap(hi) < 0:
-        return hi
-    lo = 2 * hi
-    while gap(lo) > 0:
-        assert lo > -10000, "The lower bound on q0 is way too low."
-        lo *= 1.5
-    root, r = scipy.optimize.brentq(gap, lo, hi, full_output=True)
-    assert r.converged and valid(root)
-    return root
+        def excess(lq):
+            return self.dependent(lq) - self.independent()
+
+        if excess(top) < 0:  # still below the data-independent cost at the validity edge
+            return top
+        bottom = 2 * top
+        while excess(bottom) > 0:  # geometric search down for a sign change
+            if bottom <= -10000:
+                raise AssertionError("no sign change of the bound excess above log q = -10000")
+            bottom *= 1.5
+        root, res = scipy.optimize.brentq(excess, bottom, top, full_output=True)
+        if not (res.converged and self._valid(root)):
+            raise AssertionError("q0 root finding failed")
+        return root
+
+    def rdp(self, logq: float) -> float:
+        return self.independent() if logq >= self.logq0 else self.dependent(logq)
+
+
+def _q_bound(q: float, sigma: float, m: int, sign: float) -> float:
+    return (m - 1) / 2 * scipy.special.erfc(scipy.special.erfcinv(2 * q / (m - 1)) + sign / sigma)
+
+
+def q_lower(q: float, sigma: float, m: int) -> float:
+    """B_l: the smallest q of a histogram one vote away."""
+    return _q_bound(q, sigma, m, 1.0)
+
+
+def q_upper(q: float, sigma: float, m: int) -> float:
+    """B_u: the largest q of a histogram one vote away (a probability: at most 1)."""
+    return min(1.0, _q_bound(q, sigma, m, -1.0))
 
 
 @functools.lru_cache(maxsize=None)
-def _logq0(sigma: float, order: float) -> float:
-    return compute_logq0_gnmax(sigma, order)
-
-
-def _bl(q: float, sigma: float, m: int) -> float:
-    return (m - 1) / 2 * scipy.special.erfc(1 / sigma + scipy.special.erfcinv(2 * q / (m - 1)))
-
-
-def _bu(q: float, sigma: float, m: int) -> float:
-    return min(1, (m - 1) / 2 * scipy.special.erfc(-1 / sigma + scipy.special.erfcinv(2 * q / (m - 1))))
+def gnmax_cost(sigma: float, order: float) -> GNMaxCost:
+    return GNMaxCost(float(sigma), float(order))
 
 
 @functools.lru_cache(maxsize=None)
-def _logq1(sigma: float, order: float, m: int) -> float:
-    lq0 = _logq0(sigma, order)
-    lq1 = math.log(_bl(math.exp(lq0), sigma, m))
-    assert lq1 <= lq0
+def gnmax_logq1(sigma: float, order: float, m: int) -> float:
+    """log q1 = log B_l(q0): from q1 upward one vote can reach the flat region."""
+    lq0 = gnmax_cost(sigma, order).logq0
+    lq1 = math.log(q_lower(math.exp(lq0), sigma, m))
+    if lq1 > lq0:
+        raise AssertionError("q1 above q0")
     return lq1
 
 
-def _rdp_gnmax(sigma: float, logq: float, order: float) -> float:
-    if logq >= _logq0(sigma, order):
-        return core.rdp_data_independent_gaussian(sigma, order)
-    return _data_dep_bound(sigma, logq, order)
+def compute_logq0_gnmax(sigma: float, order: float) -> float:
+    return gnmax_cost(sigma, order).logq0
 
 
-def _local_sens(logq: float, sigma: float, m: int, order: float) -> float:
-    lq0, lq1 = _logq0(sigma, order), _logq1(sigma, order, m)
-    if lq1 <= logq <= lq0:
+def gnmax_local_sensitivity(logq: float, sigma: float, m: int, order: float) -> float:
+    """LS of GNMax's data-dependent RDP at a histogram with log q = logq (inside [q1, q0] the worst case q1)."""
+    cost = gnmax_cost(sigma, order)
+    lq1 = gnmax_logq1(sigma, order, m)
+    if lq1 <= logq <= cost.logq0:
         logq = lq1
-    beta = _rdp_gnmax(sigma, logq, order)
-    up = _rdp_gnmax(sigma, math.log(_bu(math.exp(logq), sigma, m)), order)
-    down = _rdp_gnmax(sigma, math.log(_bl(math.exp(logq), sigma, m)), order)
-    return max(up - beta, beta - down)
+    q = math.exp(logq)
+    here = cost.rdp(logq)
+    return max(cost.rdp(math.log(q_upper(q, sigma, m))) - here, here - cost.rdp(math.log(q_lower(q, sigma, m))))
 
 
-def compute_local_sensitivity_bounds_gnmax(votes, num_teachers: int, sigma: float, order: float) -> np.ndarray:
-    """Local sensitivity of GNMax's data-dependent RDP at distances 0..num_teachers-1."""
-    m = len(votes)
-    lq0, lq1 = _logq0(sigma, order), _logq1(sigma, order, m)
-    logq = core.compute_logq_gaussian(votes, sigma)
-    res = np.full(num_teachers, _local_sens(lq1, sigma, m, order))
-    if lq1 <= logq <= lq0:
-        return res
+def _gnmax_walk(votes, sigma: float, lq0: float, lq1: float):
+    """log q of the histograms the worst-case walk visits at distances 1, 2, ...: votes move from the plurality to
+    the runner-up while q < q1, or from the runner-up (kept the largest non-plurality count) to the plurality while
+    q > q0; stops once q enters [q1, q0] (or the runner-up runs out of votes)."""
     v = sorted(votes, reverse=True)
-    res[0] = _local_sens(logq, sigma, m, order)
-    d = 0
-    left = logq > lq0  # otherwise logq < lq1: move right
-    while (left and logq > lq0 and v[1] > 0) or (not left and logq < lq1):
-        d += 1
-        if left:  # make the top class stronger
+    logq = core.compute_logq_gaussian(v, sigma)
+    left = logq > lq0
+    while (logq > lq0 and v[1] > 0) if left else (logq < lq1):
+        if left:
             v[0] += 1
             v[1] -= 1
-            i = 1
-            while i < len(v) - 1 and v[i] < v[i + 1]:
-                v[i], v[i + 1] = v[i + 1], v[i]
-                i += 1
+            j = 1  # restore the decreasing order of the non-plurality counts
+            while j + 1 < len(v) and v[j] < v[j + 1]:
+                v[j], v[j + 1] = v[j + 1], v[j]
+                j += 1
         else:
             v[0] -= 1
             v[1] += 1
         logq = core.compute_logq_gaussian(v, sigma)
-        res[d] = _local_sens(logq, sigma, m, order)
-    return res
+        yield logq
 
 
+def compute_local_sensitivity_bounds_gnmax(votes, num_teachers: int, sigma: float, order: float) -> np.ndarray:
+    """LS(d) of GNMax's data-dependent RDP for d = 0 .. num_teachers - 1."""
+    m = len(votes)
+    cost = gnmax_cost(sigma, order)
+    lq0, lq1 = cost.logq0, gnmax_logq1(sigma, order, m)
+    plateau = gnmax_local_sensitivity(lq1, sigma, m, order)
+    out = np.full(num_teachers, plateau)
+    logq = core.compute_logq_gaussian(votes, sigma)
+    if lq1 <= logq <= lq0:
+        return out
+    out[0] = gnmax_local_sensitivity(logq, sigma, m, order)
+    for d, lq in enumerate(_gnmax_walk(votes, sigma, lq0, lq1), start=1):
+        out[d] = gnmax_local_sensitivity(lq, sigma, m, order)
+    return out
+
+
+# --------------------------------------------------------------------------------- threshold check
 @functools.lru_cache(maxsize=None)
-def _rdp_threshold_table(num_teachers: int, threshold: float, sigma: float, order: float) -> tuple:
-    return tuple(core.compute_rdp_threshold(float(scipy.stats.norm.logsf(threshold - v, scale=sigma)), sigma, order)
-                 for v in range(num_teachers + 1))
+def _threshold_cost_table(num_teachers: int, threshold: float, sigma: float, order: float) -> np.ndarray:
+    """RDP of the threshold check for every plurality count v = 0 .. num_teachers."""
+    v = np.arange(num_teachers + 1)
+    logpr = scipy.stats.norm.logsf(threshold - v, scale=sigma)
+    return np.array([core.compute_rdp_threshold(float(lp), sigma, order) for lp in logpr])
 
 
 def compute_local_sensitivity_bounds_threshold(counts, num_teachers: int, threshold: float, sigma: float,
                                                order: float) -> np.ndarray:
-    rdp = _rdp_threshold_table(num_teachers, threshold, sigma, order)
-
-    def ls_at(v):
-        cands = []
-        if v > 0:
-            cands.append(abs(rdp[v - 1] - rdp[v]))
-        if v < num_teachers:
-            cands.append(abs(rdp[v + 1] - rdp[v]))
-        return max(cands)
-
+    """LS(d) of the threshold check's RDP: the largest one-vote change of the cost table at the plurality counts
+    d away from the current (rounded) plurality, for d = 0 .. num_teachers - 1."""
+    table = _threshold_cost_table(num_teachers, threshold, sigma, order)
+    step = np.abs(np.diff(table))  # step[v] = |cost(v + 1) - cost(v)|
+    # one-vote sensitivity at each count: the larger of its two steps (one step at the ends)
+    at = np.zeros(num_teachers + 1)
+    at[:-1] = step
+    at[1:] = np.maximum(at[1:], step)
     cur = int(round(max(counts)))
     out = np.zeros(num_teachers)
     for d in range(max(cur, num_teachers - cur)):
-        cands = []
-        if cur + d <= num_teachers:
-            cands.append(ls_at(cur + d))
-        if cur - d >= 0:
-            cands.append(ls_at(cur - d))
-        out[d] = max(cands)
+        reach = [v for v in (cur + d, cur - d) if 0 <= v <= num_teachers]
+        out[d] = max(at[v] for v in reach)
     return out
 
 
+# ------------------------------------------------------------------------------- smooth sensitivity
 def compute_discounted_max(beta: float, a) -> float:
+    """max_d e^{-beta d} a[d]."""
     a = np.asarray(a)
     return float(np.max(a * np.exp(-beta * np.arange(len(a)))))
 
@@ -163,18 +221,22 @@ def compute_smooth_sensitivity_gnmax(beta: float, counts, num_teachers: int, sig
 
 
 def compute_rdp_of_smooth_sensitivity_gaussian(beta: float, sigma: float, order: float) -> float:
-    """RDP of releasing smooth sensitivity with Gaussian noise (Theorem 23)."""
+    """RDP at `order` of releasing the cost plus Gaussian noise scaled by its beta-smooth sensitivity (Thm. 23):
+    order e^{2 beta} / sigma^2 + (beta order - log(1 - 2 order beta) / 2) / (order - 1), for 1 < order < 1/(2 beta)."""
     if beta > 0 and not 1 < order < 1 / (2 * beta):
         raise ValueError("Order outside the (1, 1/(2*beta)) range.")
-    return order * math.exp(2 * beta) / sigma ** 2 + (-0.5 * math.log(1 - 2 * order * beta) + beta * order) / (order - 1)
+    return order * math.exp(2 * beta) / sigma ** 2 + (beta * order - 0.5 * math.log(1 - 2 * order * beta)) / (order - 1)
 
 
 def compute_params_for_ss_release(eps: float, delta: float):
+    """(beta, sigma multiplier) for an (eps, delta) smooth-sensitivity release (the paper's Gaussian recipe)."""
     a = scipy.special.ndtri(1 - delta / 2)
     return math.sqrt(a ** 2 + eps / 2) - a, eps / (2 * scipy.special.chdtri(1, delta / 2))
 
 
-def _symbolic_beta(q, sigma, order):
+# ------------------------------------------------------------------------------ symbolic conditions
+def _beta_expr(q, sigma: float, order: float):
+    """Prop. 10's bound as a sympy expression of q (same formula as GNMaxCost.dependent)."""
     import sympy as sp
 
     mu2 = sigma * sp.sqrt(sp.log(1 / q))
@@ -182,29 +244,35 @@ def _symbolic_beta(q, sigma, order):
     eps1, eps2 = mu1 / sigma ** 2, mu2 / sigma ** 2
     a = (1 - q) / (1 - (q * sp.exp(eps2)) ** (1 - 1 / mu2))
     b = sp.exp(eps1) / q ** (1 / (mu1 - 1))
-    return (1 / (order - 1)) * sp.log((1 - q) * a ** (order - 1) + q * b ** (order - 1))
+    return sp.log((1 - q) * a ** (order - 1) + q * b ** (order - 1)) / (order - 1)
 
 
-def _non_decreasing(fn, q, bounds) -> bool:
+def _derivative_nonnegative(expr, q, interval) -> bool:
+    """min over the interval of d expr / dq >= 0 (numeric minimisation of the symbolic derivative)."""
     import sympy as sp
 
-    d = sp.lambdify(q, sp.diff(fn, q), modules=["numpy", {"erfc": scipy.special.erfc,
-                                                          "erfcinv": scipy.special.erfcinv}])
-    r = scipy.optimize.minimize_scalar(d, bounds=bounds, method="bounded")
-    assert r.success
+    f = sp.lambdify(q, sp.diff(expr, q),
+                    modules=["numpy", {"erfc": scipy.special.erfc, "erfcinv": scipy.special.erfcinv}])
+    r = scipy.optimize.minimize_scalar(f, bounds=interval, method="bounded")
+    if not r.success:
+        raise RuntimeError("derivative minimisation failed")
     return bool(r.fun >= 0)
 
 
 def check_conditions(sigma: float, m: int, order: float):
-    """(Condition 5, Condition 6) of the smooth-sensitivity analysis, checked symbolically."""
+    """(Condition 5: beta non-decreasing on (0, q0); Condition 6: beta(B_u(q)) - beta(q) non-decreasing on
+    (0, q1)) for GNMax with m classes. Condition 6 is only checked when 5 holds."""
     import sympy as sp
 
     q = sp.symbols("q", positive=True, real=True)
-    beta = _symbolic_beta(q, sigma, order)
+    beta = _beta_expr(q, sigma, order)
     q0 = math.exp(compute_logq0_gnmax(sigma, order))
-    c5 = _non_decreasing(beta, q, (0, q0))
-    if not c5:
-        return c5, False
+    if not _derivative_nonnegative(beta, q, (0, q0)):
+        return False, False
     bu = (m - 1) / 2 * sp.erfc(sp.erfcinv(2 * q / (m - 1)) - 1 / sigma)
-    c6 = _non_decreasing(beta.subs(q, bu) - beta, q, (0, _bl(q0, sigma, m)))
-    return c5, c6
+    return True, _derivative_nonnegative(beta.subs(q, bu) - beta, q, (0, q_lower(q0, sigma, m)))
+
+
+# names the ICLR'18 scripts use
+def rdp_gnmax(sigma: float, logq: float, order: float) -> float:
+    return gnmax_cost(sigma, order).rdp(logq)

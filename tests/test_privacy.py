@@ -557,3 +557,22 @@ def test_rdp_gaussian_theorem6_direct_evaluation():
             assert np.all(got >= prev - 1e-15)
         prev = got
     assert core.rdp_gaussian(-math.inf, sigma, 7.0) == 0.0
+
+
+def test_smooth_sensitivity_threshold_low_threshold_golden():
+    """`smooth_sensitivity_test.py:82-92` (t = 2, below every count)."""
+    c = np.array([20, 10, 0])
+    out2 = ss.compute_local_sensitivity_bounds_threshold(c, int(c.sum()), 2, 2, 10)
+    ans2 = [1.60212079e-01, 2.07021132e-01, 2.07021132e-01, 1.93127860e-01, 1.68302106e-01, 1.42180452e-01,
+            1.16054002e-01, 9.01543247e-02, 6.45775697e-02, 3.94153241e-02, 1.47826870e-02, 1.48454129e-04] + [0] * 18
+    np.testing.assert_allclose(out2, ans2, rtol=5e-8, atol=0)
+
+
+def test_pate2017_sensitivity_uses_sorted_counts():
+    """The distance-k check uses the plurality and runner-up of the SORTED counts (the reference compared the
+    unsorted input's first two entries): permuting the classes does not change the smooth sensitivity."""
+    c = np.array([3, 200, 40, 7])
+    perm = np.array([200, 40, 7, 3])
+    for l in (1.0, 4.0):
+        assert analysis2017.smoothed_sens(c, 0.05, l, 0.09) == analysis2017.smoothed_sens(perm, 0.05, l, 0.09)
+        assert analysis2017.smoothed_sens(perm, 0.05, l, 0.09) > 0
