@@ -42,9 +42,32 @@ MIFX_HD uint64_t mifx_epoch_key(uint64_t key, uint64_t epoch) {
 
 // half width h (bits) of the Feistel domain for n records: the smallest h >= 1 with 4^h >= n
 MIFX_HD int mifx_feistel_half(uint64_t n) {
-  int h = 1;
-  while (h < 32 && (uint64_t(1) << (2 * h)) < n) ++h;
-  return h;
+  if (n <= 4) return 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int b = 64 - __clzll((long long)(n - 1));  // bits of n - 1
+#else
+  const int b = 64 - __builtin_clzll(n - 1);
+#endif
+  return (b + 1) >> 1;  // the smallest h with 4^h >= n
+}
+
+// the same network in 32-bit arithmetic (n <= 2^32, h <= 16): identical values, half the instructions
+MIFX_HD uint32_t mifx_feistel_perm32(uint32_t i, uint64_t n, uint64_t ekey, int h) {
+  const uint32_t mask = (1u << h) - 1u;
+  const uint32_t k0 = (uint32_t)ekey, k1 = (uint32_t)(ekey >> 32);
+  const uint32_t rk[4] = {k0, k1, k0 ^ 0x68e31da4u, k1 ^ 0xb5297a4du};
+  uint32_t x = i;
+  do {
+    uint32_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t t = L ^ (mifx_mix32(R ^ rk[r]) & mask);
+      L = R;
+      R = t;
+    }
+    x = (L << h) | R;
+  } while ((uint64_t)x >= n);
+  return x;
 }
 
 MIFX_HD uint64_t mifx_feistel_perm(uint64_t i, uint64_t n, uint64_t ekey, int h) {
@@ -79,8 +102,19 @@ struct MifxFeedStep {
 MIFX_HD MifxFeedStep mifx_feed_step(const MifxFeed& f, long long step, long long n) {
   const long long p = step * f.gstride + f.goff;
   MifxFeedStep s;
-  s.e0 = p / n;
-  s.i0 = p - s.e0 * n;
+  // p / n through a double quotient (exact to +-1 below 2^53) and an integer correction: no 64-bit divide
+  long long e = (long long)((double)p / (double)n);
+  long long i = p - e * n;
+  while (i < 0) {
+    i += n;
+    --e;
+  }
+  while (i >= n) {
+    i -= n;
+    ++e;
+  }
+  s.e0 = e;
+  s.i0 = i;
   s.h = mifx_feistel_half((uint64_t)n);
   return s;
 }
@@ -92,5 +126,7 @@ MIFX_HD long long mifx_feed_record(const MifxFeed& f, const MifxFeedStep& s, lon
     e += 1;
   }
   if (f.key == 0) return i;
-  return (long long)mifx_feistel_perm((uint64_t)i, (uint64_t)n, mifx_epoch_key(f.key, (uint64_t)e), s.h);
+  const uint64_t ek = mifx_epoch_key(f.key, (uint64_t)e);
+  if (s.h <= 16) return (long long)mifx_feistel_perm32((uint32_t)i, (uint64_t)n, ek, s.h);
+  return (long long)mifx_feistel_perm((uint64_t)i, (uint64_t)n, ek, s.h);
 }

@@ -57,14 +57,32 @@ def source_hash(src: Path) -> str:
     h = hashlib.sha256()
     flags = (HIP_FLAGS + _file_flags(src)) if src.suffix == ".hip" else CXX_FLAGS
     h.update(" ".join(flags).encode())
-    # sources a source includes by name (csrc/wd_chain64.hip builds csrc/wd_chain.hip with another tile size)
-    incl = [CSRC / ln.split('"')[1] for ln in src.read_text().splitlines()
-            if ln.startswith('#include "') and ln.split('"')[1].endswith(".hip")]
-    for d in [src] + incl + sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("include/*.h")):
-        if d.exists() and d.name != HASH_HEADER.name:
+    # the source and everything it #includes by quoted name, transitively (csrc/wd_chain64.hip builds
+    # csrc/wd_chain.hip with another tile size; headers such as feed.h): a header edit rebuilds only its users
+    for d in _quoted_includes(src):
+        if d.name != HASH_HEADER.name:
             h.update(d.name.encode())
             h.update(d.read_bytes())
     return h.hexdigest()[:16]
+
+
+def _quoted_includes(src: Path) -> list[Path]:
+    seen: dict[Path, None] = {}
+    todo = [src]
+    while todo:
+        f = todo.pop()
+        if f in seen or not f.exists():
+            continue
+        seen[f] = None
+        for ln in f.read_text().splitlines():
+            t = ln.strip()
+            if t.startswith('#include "'):
+                name = t.split('"')[1]
+                for base in (f.parent, CSRC, CSRC / "include"):
+                    if (base / name).exists():
+                        todo.append((base / name).resolve())
+                        break
+    return sorted(seen, key=lambda p: (p != src.resolve(), str(p)))
 
 
 # force-included into every translation unit: the library reports the source hash it was built from, and
