@@ -37,6 +37,7 @@
 //  AGPR->VGPR copies feeding the epilogues)
 #include <hip/hip_runtime.h>
 #include "feed.h"
+#include <stdlib.h>
 #include "xcd.h"
 #include <stdint.h>
 
@@ -944,12 +945,11 @@ __global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ 
   if (t == 0) ok[x * nc1 + c] = (int)(xep[0] + 1);
 }
 
-// level 2: one thread per slab column. MODE 0: plain sum into out; 1: optimizer on slab-order state; 3: xGMI
-// data parallelism -- publish the local sum (store into half (epoch & 1) of this rank's IPC buffer, stamp the 4
-// RQ-float4 chunks' flags in every peer), wait for every peer's stamps on the SAME 4 chunks (bounded spin), load
-// the peers' partials of these 256 columns over xGMI, sum in rank order and run the optimizer. Only same-block
-// workgroups of different ranks wait on each other and a rank's 81 waiting workgroups leave the other CUs free,
-// so ranks sharing one GPU (tests) still make progress.
+// level 2: one thread per slab column. MODE 0: plain sum into out; 1: optimizer on slab-order state; 2: xGMI data
+// parallelism, publish half -- store the local sum into half (epoch & 1) of this rank's IPC buffer and stamp the 4
+// RQ-float4 chunks' flags in every peer, no wait (wd_xgmi_gather_opt waits, gathers and applies the optimizer in
+// one-wave workgroups); 3: the same with the wait, the gather over xGMI and the optimizer in this kernel (opt-in,
+// MIFX_XGMI_FUSED_WAIT=1: one launch fewer, but 256-thread workgroups spin on the peers).
 template <int MODE>
 __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ part, const int* __restrict__ ok,
                                                      const float* __restrict__ slab, int G, int stride,
@@ -969,7 +969,7 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
   __shared__ int s_bad;
   const int t = threadIdx.x;
   constexpr bool opt = MODE == 1 || MODE == 3;
-  if (MODE == 3) {  // the exchange already failed on this rank: touch nothing (see xg_wait)
+  if (MODE >= 2) {  // the exchange already failed on this rank: touch nothing (see xg_wait)
     if (t == 0) s_bad = xg_failed(err) ? 1 : 0;
     __syncthreads();
     if (s_bad) return;
@@ -1026,6 +1026,20 @@ __global__ __launch_bounds__(256) void wd_xcd_opt_sc(const float* __restrict__ p
     }
     if (MODE == 0) out[gi] = g;
     if (MODE == 1) sc_update(gi, st, g, hd, hw, s_step, param, s0, s1, wt_out);
+  }
+  if (MODE == 2) {  // publish only: the wait, gather and optimizer run in wd_xgmi_gather_opt (one-wave waiters)
+    const long long ex = xctr[blockIdx.x] + 1;  // exchange epoch: slot b is advanced by the gather kernel's block b
+    const size_t hoff = (size_t)(ex & 1) * stride;
+    if (gi < stride) {
+      st_sys((float*)peers.part[rank] + hoff + gi, g);
+      __builtin_amdgcn_s_waitcnt(0);  // acknowledged before the chunk flags below
+    }
+    __syncthreads();
+    const int nch = (stride / 4 + RQ - 1) / RQ;
+    if (t < 4 * world) {
+      const int cc = 4 * blockIdx.x + t / world, p = t % world;
+      if (cc < nch) xg_publish(peers.sig[p] + cc * XG_MAXW + rank, (unsigned int)ex);
+    }
   }
   if (MODE == 3) {
     const long long ex = xctr[blockIdx.x] + 1;  // exchange epoch (own slot)
@@ -1318,8 +1332,21 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
                 hyper_wide[6], hyper_wide[7]};
     hipLaunchKernelGGL(wd_reduce_xcd, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, xcd_of,
                        (float4*)xpart, xok, xep);
-    hipLaunchKernelGGL(wd_xcd_opt_sc<3>, g2, dim3(256), 0, stream, xpart, xok, slab, G, stride, xcd_of, xep, nullptr,
+    static const bool fused_wait = getenv("MIFX_XGMI_FUSED_WAIT") != nullptr && getenv("MIFX_XGMI_FUSED_WAIT")[0] == '1';
+    if (fused_wait) {  // (opt-in) publish + wait + gather + optimizer in the 256-thread level-2 workgroups
+      hipLaunchKernelGGL(wd_xcd_opt_sc<3>, g2, dim3(256), 0, stream, xpart, xok, slab, G, stride, xcd_of, xep,
+                         nullptr, wsc, param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, pe, world, rank, xctr,
+                         my_sig, err);
+      return (int)hipGetLastError();
+    }
+    // default: the level-2 workgroups sum the XCD partials and PUBLISH, and never wait; the wait runs in the
+    // one-wave workgroups of wd_xgmi_gather_opt (as on the non-XCD path), so no 256-thread workgroup ever spins
+    // on a peer: a rank's waiting kernel cannot hold the CU slots a peer's fused kernel needs when ranks share a
+    // GPU, and on separate GPUs each spinner is one wave
+    hipLaunchKernelGGL(wd_xcd_opt_sc<2>, g2, dim3(256), 0, stream, xpart, xok, slab, G, stride, xcd_of, xep, nullptr,
                        wsc, param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, pe, world, rank, xctr, my_sig, err);
+    hipLaunchKernelGGL(wd_xgmi_gather_opt<true>, gb, dim3(XB_THR), 0, stream, stride, pe, world, my_sig, err, xctr,
+                       nullptr, wsc, param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(wd_reduce_xgmi_publish, ga, dim3(256), 0, stream, (const float4*)slab, G, stride, pe, world, rank,

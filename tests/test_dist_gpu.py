@@ -127,7 +127,9 @@ def test_direct_rccl_dp_step_matches_split_phase():
         dist.destroy_process_group()
 
 
-def _xgmi_worker(rank, world, port, out_dir, steps, batch, spg):
+def _xgmi_worker(rank, world, port, out_dir, steps, batch, spg, fused_wait=False):
+    if fused_wait:  # read once by the library (csrc/wide_deep.hip): set before it loads
+        os.environ["MIFX_XGMI_FUSED_WAIT"] = "1"
     from mifx.data.synthetic import synthetic_records
     from mifx.models import wide_deep as wdm
     from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
@@ -159,18 +161,21 @@ def _xgmi_worker(rank, world, port, out_dir, steps, batch, spg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,batch", [(2, 512), (4, 512), (2, 8192), (2, 65536), (4, 65536)])
-def test_xgmi_dp_step_matches_split_phase(world, batch):
+@pytest.mark.parametrize("world,batch,fused_wait", [(2, 512, False), (4, 512, False), (2, 8192, False),
+                                                    (2, 65536, False), (4, 65536, False), (2, 65536, True)])
+def test_xgmi_dp_step_matches_split_phase(world, batch, fused_wait):
     """Data parallelism over the one-shot xGMI exchange (IPC-shared HBM partials + epoch flags, csrc/xgmi.hip,
     wd_xgmi_opt): `world` processes share cuda:0 (the IPC path is the same as across GPUs) and run the step in
     multi-step hipGraphs with no host collective. Every replica must hold bit-identical weights, equal to the
     split-phase DP path (graph, all-reduce, graph): bit-exact at 2 ranks (a + b has one order), to fp32 summation
     order at 4. Batch 8192 (grid 64) takes the XCD-local local sum (wd_reduce_xcd + publish), 512 the one-pass one.
+    Every rank's waits run in one-wave workgroups (wd_xgmi_gather_opt) on both paths, so ranks sharing one GPU
+    always make progress; fused_wait=True is the opt-in variant whose 256-thread level-2 workgroups wait.
     (Against one process on the global batch both DP paths drift after ~6 steps on this data: FTRL's L1
     threshold flips wide weights on last-bit differences -- tools/xgmi_probe.py.)"""
     steps = 8
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_xgmi_worker, args=(world, _free_port(), d, steps, batch, 3), nprocs=world,
+        mp.start_processes(_xgmi_worker, args=(world, _free_port(), d, steps, batch, 3, fused_wait), nprocs=world,
                            start_method="spawn")
         got = [torch.load(os.path.join(d, f"xgmi{r}.pt"), weights_only=True) for r in range(world)]
     for g in got[1:]:
