@@ -121,37 +121,104 @@ class ImageTrainerSpec(ComponentSpec):
     PARAMETERS = {"train_steps": ExecutionParameter(optional=True, default=100),
                   "batch_size": ExecutionParameter(optional=True, default=64),
                   "learning_rate": ExecutionParameter(optional=True, default=0.1),
-                  "num_classes": ExecutionParameter(optional=True, default=1000)}
+                  "num_classes": ExecutionParameter(optional=True, default=1000),
+                  "custom_config": ExecutionParameter(optional=True)}
+
+
+def run_image_rank(spec: dict) -> dict:
+    """One rank (or the only process) of the image Trainer: ResNet-50 v2 on the examples of `spec`, resuming
+    from the latest checkpoint in <out>/serving_model_dir, checkpointing every `checkpoint_every` steps (rank 0
+    writes, every rank resumes from the same file), evaluating and exporting on rank 0. `batch_size` is per
+    replica (W ranks train W x batch_size images per step); `accum_steps` micro-batches per replica and step."""
+    import numpy as np
+    import torch
+
+    from ..serving.saved_model import save_module
+    from ..trainer.resnet_trainer import ResNetTrainer
+
+    pg = torch.distributed.group.WORLD if torch.distributed.is_initialized() else None
+    rank = torch.distributed.get_rank() if pg is not None else 0
+    world = torch.distributed.get_world_size() if pg is not None else 1
+    cc = spec.get("custom_config") or {}
+    with open(os.path.join(spec["transform_uri"], "image_transform.json")) as f:
+        tf = json.load(f)
+    # every rank maps the whole split; each step's global sample is drawn from (seed, step) (ResNetTrainer)
+    imgs = torch.from_numpy(np.load(os.path.join(spec["train_uri"], "images.npy"), allow_pickle=False))
+    labels = torch.from_numpy(np.load(os.path.join(spec["train_uri"], "labels.npy"), allow_pickle=False))
+    dev = spec.get("device") or ("cuda" if torch.cuda.is_available() else "cpu")
+    if dev == "cuda" and world > 1:
+        dev = f"cuda:{0 if os.environ.get('MIFX_SHARED_GPU') == '1' else int(os.environ.get('LOCAL_RANK', 0))}"
+    steps = int(spec["train_steps"])
+    tr = ResNetTrainer(int(spec["batch_size"]), dev, imgs, labels, num_classes=int(spec["num_classes"]),
+                       lr=float(spec["learning_rate"]), warmup_steps=max(1, steps // 10), mean=tuple(tf["mean"]),
+                       std=tuple(tf["std"]), crop=int(tf["crop"]), process_group=pg, seed=int(cc.get("seed", 0)),
+                       accum_steps=int(cc.get("accum_steps", 1)))
+    model_dir = os.path.join(spec["out_dir"], "serving_model_dir")
+    ck = ResNetTrainer.latest_checkpoint(model_dir)
+    if ck:
+        tr.restore(ck)
+    every = int(cc.get("checkpoint_every", 0) or 0)
+    loss = torch.tensor(float("nan"))
+    import time
+
+    t0, s0 = time.time(), tr.step_idx
+    while tr.step_idx < steps:
+        loss = tr.step()
+        if every and tr.step_idx % every == 0 and tr.step_idx < steps:
+            if rank == 0:
+                tr.save_checkpoint(model_dir)
+            if pg is not None:
+                torch.distributed.barrier()
+    if tr.device.type == "cuda":
+        torch.cuda.synchronize(tr.device)
+    secs = time.time() - t0
+    res = {"final_loss": float(loss), "world": world, "steps": tr.step_idx, "resumed_from": ck,
+           "train_images_per_sec": (tr.step_idx - s0) * tr.batch * tr.accum * world / max(secs, 1e-9)}
+    if rank == 0:
+        tr.save_checkpoint(model_dir)
+        ev_imgs = torch.from_numpy(np.load(os.path.join(spec["eval_uri"], "images.npy"), allow_pickle=False))
+        ev_labels = torch.from_numpy(np.load(os.path.join(spec["eval_uri"], "labels.npy"), allow_pickle=False))
+        res["eval_accuracy"] = tr.evaluate(ev_imgs, ev_labels)
+        save_module(os.path.join(model_dir, "export", "1"), tr.model.cpu().float(), "mifx.models.resnet:ResNetV2",
+                    {"num_classes": int(spec["num_classes"])}, [3, tf["crop"], tf["crop"]])
+    if pg is not None:
+        torch.distributed.barrier()
+    return res
 
 
 class ImageTrainerExecutor(BaseExecutor):
+    """custom_config: num_gpus (> 1: one rank per GPU launched by the component itself, mifx.trainer.distributed;
+    the reference runs its ResNet-50 workers as a hand-written TFJob, `tf-job-simple-v1beta2.jsonnet:22-40`),
+    checkpoint_every (steps; resume from the latest checkpoint like the reference's Saver,
+    `research/pate_2017/deep_cnn.py:489,541-542`), accum_steps, seed, timeout_s."""
+
     def Do(self, input_dict, output_dict, exec_properties):  # noqa: N802
-        import torch
-
-        from ..serving.saved_model import save_module
-        from ..trainer.resnet_trainer import ResNetTrainer
-
         ex = {a.split: a.uri for a in input_dict["examples"]}
-        with open(os.path.join(input_dict["transform_output"][0].uri, "image_transform.json")) as f:
-            tf = json.load(f)
-        imgs = torch.from_numpy(np.load(os.path.join(ex["train"], "images.npy"), allow_pickle=False))
-        labels = torch.from_numpy(np.load(os.path.join(ex["train"], "labels.npy"), allow_pickle=False))
-        dev = self.context.extra.get("device") or ("cuda" if torch.cuda.is_available() else "cpu")
-        tr = ResNetTrainer(int(exec_properties["batch_size"]), dev, imgs, labels,
-                           num_classes=int(exec_properties["num_classes"]), lr=float(exec_properties["learning_rate"]),
-                           warmup_steps=max(1, int(exec_properties["train_steps"]) // 10), mean=tuple(tf["mean"]),
-                           std=tuple(tf["std"]), crop=int(tf["crop"]))
-        for _ in range(int(exec_properties["train_steps"])):
-            loss = tr.step()
-        ev_imgs = torch.from_numpy(np.load(os.path.join(ex["eval"], "images.npy"), allow_pickle=False))
-        ev_labels = torch.from_numpy(np.load(os.path.join(ex["eval"], "labels.npy"), allow_pickle=False))
-        acc = tr.evaluate(ev_imgs, ev_labels)
         out = output_dict["output"][0]
-        save_module(os.path.join(out.uri, "serving_model_dir", "export", "1"), tr.model.cpu().float(),
-                    "mifx.models.resnet:ResNetV2", {"num_classes": int(exec_properties["num_classes"])},
-                    [3, tf["crop"], tf["crop"]])
-        out.custom_properties.update({"eval_accuracy": acc, "final_loss": float(loss)})
-        self.context.logger.info("ImageTrainer: loss %.4f eval accuracy %.4f", float(loss), acc)
+        cc = dict(exec_properties.get("custom_config") or {})
+        spec = {"train_uri": ex["train"], "eval_uri": ex.get("eval", ex["train"]), "out_dir": out.uri,
+                "transform_uri": input_dict["transform_output"][0].uri,
+                "train_steps": int(exec_properties["train_steps"]), "batch_size": int(exec_properties["batch_size"]),
+                "learning_rate": float(exec_properties["learning_rate"]),
+                "num_classes": int(exec_properties["num_classes"]), "custom_config": cc,
+                "device": self.context.device or self.context.extra.get("device"),
+                "hparams": {"device": self.context.device or self.context.extra.get("device")}}
+        n = int(cc.get("num_gpus", 1) or 1)
+        if n > 1:
+            from ..trainer import distributed
+
+            work = os.path.join(out.uri, "dp_run")
+            res = distributed.launch(dict(spec, target="mifx.components.image:run_image_rank", work_dir=work), n, work,
+                                     timeout=cc.get("timeout_s"))
+        else:
+            res = run_image_rank(spec)
+        with open(os.path.join(out.uri, "metrics.json"), "w") as f:
+            json.dump(res, f, default=float)
+        out.custom_properties.update({"eval_accuracy": float(res["eval_accuracy"]),
+                                      "final_loss": float(res["final_loss"]), "num_replicas": int(res["world"]),
+                                      "train_images_per_sec": float(res["train_images_per_sec"])})
+        self.context.logger.info("ImageTrainer: %d replica(s), loss %.4f eval accuracy %.4f", res["world"],
+                                 res["final_loss"], res["eval_accuracy"])
 
 
 class ImageTrainer(_KwComponent):

@@ -16,7 +16,11 @@ all-reduce, PyTorchJob DDP (`tf-job-simple-v1beta2.jsonnet:22-74`
   receiving side is RCCL's; the master gradient stays fp32).
 
 `DataParallel.finish()` (or `step_ready()`) waits for outstanding work and writes averaged gradients
-back into `param.grad`. Works unchanged on gloo/CPU, which is how the tests exercise it."""
+back into `param.grad`. With `grad_as_bucket_view=True` there is nothing to write back: every `param.grad` IS a
+view of its bucket (same strides as the parameter, channels_last included), autograd accumulates straight into
+the bucket, the all-reduce runs in place and the average is one scale per bucket -- no copy into or out of the
+buckets (call `zero_grad()` instead of the optimizer's). Works unchanged on gloo/CPU, which is how the tests
+exercise it."""
 from __future__ import annotations
 
 import contextlib
@@ -41,8 +45,12 @@ class DataParallel:
     """Wraps a module; call `finish()` after `loss.backward()` and before `optimizer.step()`."""
 
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
-                 wire_dtype: torch.dtype | None = None, broadcast_init: bool = True, average: bool = True):
+                 wire_dtype: torch.dtype | None = None, broadcast_init: bool = True, average: bool = True,
+                 grad_as_bucket_view: bool = False):
+        if grad_as_bucket_view and wire_dtype is not None:
+            raise ValueError("gradients as bucket views need the parameters' own dtype on the wire")
         self.module = module
+        self.views = bool(grad_as_bucket_view)
         self.pg = process_group if process_group is not None else (dist.group.WORLD if dist.is_initialized()
                                                                     else None)
         self.world = dist.get_world_size(self.pg) if self.pg is not None else 1
@@ -74,6 +82,21 @@ class DataParallel:
         dev = params[0].device if params else torch.device("cpu")
         self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if self.world > 1 else []
+        if self.views:
+            self.zero_grad()
+
+    def _view(self, b: _Bucket, pi: int) -> torch.Tensor:
+        p, off = b.params[pi], b.offsets[pi]
+        return b.buf[off:off + p.numel()].as_strided(p.shape, p.stride())
+
+    def zero_grad(self) -> None:
+        """(grad_as_bucket_view) zero every bucket and (re)attach each param.grad as its bucket view."""
+        for b in self.buckets:
+            b.buf.zero_()
+            for pi, p in enumerate(b.params):
+                g = p.grad
+                if g is None or g.data_ptr() != b.buf.data_ptr() + b.offsets[pi] * b.buf.element_size():
+                    p.grad = self._view(b, pi)
 
     def _add_bucket(self, params: list) -> None:
         n = sum(p.numel() for p in params)
@@ -95,8 +118,9 @@ class DataParallel:
         if pi in b.ready:
             return
         b.ready.add(pi)
-        off = b.offsets[pi]
-        b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        if not self.views:
+            off = b.offsets[pi]
+            b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
         if len(b.ready) == len(b.params):
             self._launch(b)
 
@@ -127,7 +151,9 @@ class DataParallel:
         if self.world == 1 or not self._sync:
             return
         for b in self.buckets:
-            if b.work is None:  # unused params this step: contribute zeros for them
+            if b.work is None and self.views:  # unused params: their bucket views are still zero
+                self._launch(b)
+            elif b.work is None:  # unused params this step: contribute zeros for them
                 for pi, p in enumerate(b.params):
                     if pi not in b.ready:
                         off = b.offsets[pi]
@@ -142,6 +168,11 @@ class DataParallel:
             b.work.wait()
             if cur is not None:
                 cur.wait_stream(self._comm_stream)
+            if self.views:  # param.grad are views of the bucket: average in place, nothing to copy back
+                if scale != 1.0:
+                    b.buf.mul_(scale)
+                b.work, b.ready = None, set()
+                continue
             for pi, p in enumerate(b.params):
                 off = b.offsets[pi]
                 g = b.buf[off:off + p.numel()].view_as(p).to(p.dtype)

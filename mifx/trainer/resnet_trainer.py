@@ -34,12 +34,22 @@ def synthetic_imagenet(n: int, size: int = 256, classes: int = 1000, seed: int =
 class ResNetTrainer:
     def __init__(self, batch: int, device, images: torch.Tensor, labels: torch.Tensor, num_classes: int = 1000,
                  lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 5e-5, warmup_steps: int = 100,
-                 process_group=None, mean=IMAGENET_MEAN, std=IMAGENET_STD, seed: int = 0, crop: int = 224):
+                 process_group=None, mean=IMAGENET_MEAN, std=IMAGENET_STD, seed: int = 0, crop: int = 224,
+                 accum_steps: int = 1):
+        """batch: examples per micro-batch per replica; accum_steps micro-batches (each with its own BatchNorm
+        statistics) are summed into one update. A data-parallel step over W ranks trains on W x accum_steps x batch
+        examples: the global sample of the step is drawn from (seed, step) and rank r takes micro-batches
+        r accum_steps .. (r + 1) accum_steps - 1 of it, so W ranks at accum 1 compute the same update as one
+        process at accum W (up to fp32 summation order)."""
         self.device = torch.device(device)
         self.batch, self.crop, self.seed = batch, crop, seed
+        self.accum = max(1, int(accum_steps))
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.rank = torch.distributed.get_rank(process_group) if process_group is not None else 0
         torch.manual_seed(seed)
         self.model = resnet50_v2(num_classes).to(self.device).to(memory_format=torch.channels_last)
-        self.dp = DataParallel(self.model, process_group) if process_group is not None else None
+        self.dp = DataParallel(self.model, process_group, grad_as_bucket_view=True) \
+            if process_group is not None else None
         decay = [p for n, p in self.model.named_parameters() if p.ndim > 1]
         no_decay = [p for n, p in self.model.named_parameters() if p.ndim <= 1]
         self.opt = torch.optim.SGD([{"params": decay, "weight_decay": weight_decay},
@@ -56,23 +66,90 @@ class ResNetTrainer:
     def _lr(self) -> float:
         return self.base_lr * min(1.0, (self.step_idx + 1) / max(1, self.warmup))
 
+    def _step_indices(self) -> torch.Tensor:
+        """The global sample of this step ([world * accum * batch], from (seed, step) on a host generator: the same
+        on every rank and device)."""
+        g = torch.Generator().manual_seed(self.seed * 1000003 + self.step_idx)
+        return torch.randint(0, len(self.labels), (self.world * self.accum * self.batch,), generator=g)
+
     def step(self) -> torch.Tensor:
-        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + self.step_idx)
-        idx = torch.randint(0, len(self.labels), (self.batch,), generator=g, device=self.device)
-        x = crop_flip_normalize(self.images, idx, (self.crop, self.crop), True, self.seed, self.step_idx, self.mean,
-                                self.std, torch.bfloat16 if self.amp else torch.float32)
-        y = self.labels[idx]
+        glob = self._step_indices()
         for pg in self.opt.param_groups:
             pg["lr"] = self._lr()
-        self.opt.zero_grad(set_to_none=True)
-        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
-            loss = F.cross_entropy(self.model(x).float(), y)
-        loss.backward()
+        if self.dp is not None:
+            self.dp.zero_grad()  # the bucket buffers ARE the gradients (views): one memset per bucket
+        else:
+            self.opt.zero_grad(set_to_none=True)
+        total = 0.0
+        for m in range(self.accum):
+            mb = self.rank * self.accum + m
+            idx = glob[mb * self.batch:(mb + 1) * self.batch].to(self.device)
+            x = crop_flip_normalize(self.images, idx, (self.crop, self.crop), True, self.seed, self.step_idx,
+                                    self.mean, self.std, torch.bfloat16 if self.amp else torch.float32)
+            y = self.labels[idx]
+            with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
+                loss = F.cross_entropy(self.model(x).float(), y) / self.accum
+            last = m == self.accum - 1
+            if self.dp is not None and not last:
+                with self.dp.no_sync():
+                    loss.backward()
+            else:
+                loss.backward()
+            total = total + loss.detach()
         if self.dp is not None:
             self.dp.finish()
         self.opt.step()
         self.step_idx += 1
-        return loss.detach()
+        return total
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    def state_dict(self) -> dict:
+        """Weights, BatchNorm running statistics, the SGD momentum buffers and the step (flat tensor dict)."""
+        sd = {f"model.{k}": v.detach().contiguous() for k, v in self.model.state_dict().items()}
+        for i, p in enumerate(self.model.parameters()):
+            buf = self.opt.state.get(p, {}).get("momentum_buffer")
+            if buf is not None:
+                sd[f"opt.momentum.{i}"] = buf.detach().contiguous()
+        sd["step"] = torch.tensor([self.step_idx], dtype=torch.int64)
+        return sd
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.model.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")})
+        for i, p in enumerate(self.model.parameters()):
+            v = sd.get(f"opt.momentum.{i}")
+            if v is not None:
+                self.opt.state[p]["momentum_buffer"] = v.to(device=p.device, dtype=p.dtype).clone() \
+                    .contiguous(memory_format=torch.channels_last if p.ndim == 4 else torch.contiguous_format)
+        self.step_idx = int(sd["step"][0])
+
+    def save_checkpoint(self, model_dir: str, keep: int = 1) -> str:
+        import glob as _glob
+        import os
+
+        from safetensors.torch import save_file
+
+        os.makedirs(model_dir, exist_ok=True)
+        path = os.path.join(model_dir, f"ckpt-{self.step_idx}.safetensors")
+        save_file({k: v.cpu().contiguous() for k, v in self.state_dict().items()}, path)
+        old = sorted(_glob.glob(os.path.join(model_dir, "ckpt-*.safetensors")),
+                     key=lambda q: int(q.rsplit("-", 1)[1].split(".")[0]))
+        for q in old[:-max(1, keep)]:
+            os.remove(q)
+        return path
+
+    @staticmethod
+    def latest_checkpoint(model_dir: str) -> str | None:
+        import glob as _glob
+        import os
+
+        c = sorted(_glob.glob(os.path.join(model_dir, "ckpt-*.safetensors")),
+                   key=lambda q: int(q.rsplit("-", 1)[1].split(".")[0]))
+        return c[-1] if c else None
+
+    def restore(self, path: str) -> None:
+        from safetensors.torch import load_file
+
+        self.load_state_dict(load_file(path))
 
     @torch.no_grad()
     def evaluate(self, images: torch.Tensor, labels: torch.Tensor, batch: int = 256) -> float:

@@ -5,6 +5,7 @@ import socket
 import tempfile
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -60,27 +61,36 @@ def test_wide_deep_dp_matches_single_process():
 class _Net(torch.nn.Module):
     def __init__(self):
         super().__init__()
+        self.conv = torch.nn.Conv2d(1, 4, 3, padding=1)  # a 4-D weight: channels_last strides below
         self.a = torch.nn.Linear(16, 64)
         self.b = torch.nn.Linear(64, 64)
         self.unused = torch.nn.Linear(4, 4)
         self.c = torch.nn.Linear(64, 3)
 
     def forward(self, x):
+        x = x + self.conv(x.view(-1, 1, 4, 4)).mean(1).reshape(-1, 16)
         return self.c(torch.relu(self.b(torch.relu(self.a(x)))))
 
 
-def _ddp_worker(rank, world, port, out_dir):
+def _ddp_worker(rank, world, port, out_dir, views=False):
     _init(rank, world, port)
     torch.manual_seed(100 + rank)  # different init per rank: DataParallel must broadcast rank 0's
-    net = _Net()
-    dp = DataParallel(net, bucket_cap_mb=0.01)  # tiny buckets -> several overlapped all-reduces
+    net = _Net().to(memory_format=torch.channels_last)
+    dp = DataParallel(net, bucket_cap_mb=0.01, grad_as_bucket_view=views)  # tiny buckets -> several all-reduces
     assert len(dp.buckets) > 2
+    if views:
+        assert net.conv.weight.grad.stride() == net.conv.weight.stride()
+        st = net.conv.weight.grad.untyped_storage().data_ptr()
+        assert any(st == b.buf.untyped_storage().data_ptr() for b in dp.buckets)  # a view of a bucket
     g = torch.Generator().manual_seed(5)
     x = torch.randn(world * 8, 16, generator=g)
     y = torch.randint(0, 3, (world * 8,), generator=g)
     opt = torch.optim.SGD(net.parameters(), lr=0.1)
     for _ in range(2):
-        opt.zero_grad()
+        if views:
+            dp.zero_grad()  # the bucket buffers are the gradients
+        else:
+            opt.zero_grad()
         with dp.no_sync():  # two micro-batches accumulated locally
             torch.nn.functional.cross_entropy(net(x[rank * 8:rank * 8 + 4]), y[rank * 8:rank * 8 + 4],
                                               reduction="sum").backward()
@@ -93,10 +103,12 @@ def _ddp_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_bucketed_ddp_matches_single_process():
+@pytest.mark.parametrize("views", [False, True])
+def test_bucketed_ddp_matches_single_process(views):
+    """Copy-in/copy-out buckets and gradients-as-bucket-views (no copies) give the single-process weights."""
     world, port = 2, _free_port()
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_ddp_worker, args=(world, port, d), nprocs=world, start_method="spawn")
+        mp.start_processes(_ddp_worker, args=(world, port, d, views), nprocs=world, start_method="spawn")
         got = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
     torch.manual_seed(100)
     net = _Net()
