@@ -48,10 +48,13 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 #ifndef WDC_T
 #define WDC_T 128
 #endif
-// examples per workgroup iteration: 128 (this file's library), or 64 (csrc/wd_chain64.hip: the same kernel built
-// for one 4-wave workgroup of 4 x 16 examples, the small-batch shape)
+// examples per workgroup iteration: 128 (this file's library), 64 (csrc/wd_chain64.hip: the same kernel built
+// for one 4-wave workgroup of 4 x 16 examples, the small-batch shape) or 256 (csrc/wd_chain256.hip: 8 waves x 32
+// examples, two column blocks per wave -- the large-batch shape: one iteration per workgroup at B = 65536 on 256
+// workgroups, the forward and activation-gradient chains of both blocks interleaved in one wave)
 constexpr int T = WDC_T;
-static_assert(T == 128 || T == 64, "T");
+static_assert(T == 128 || T == 64 || T == 256, "T");
+constexpr bool ONE_ITER = T == 256;  // see the iteration loop of wdc_fused
 constexpr int MAXW = 8;  // waves per workgroup: T / (16 TBN), TBN = 16-example column blocks per wave (1 or 2)
 // Row padding (elements): WPAD for the weight images, PAD for the staging images; with the row permutations below
 // (wperm, sperm16) every LDS access site is conflict-free in the bank model (tools/lds_banks.py). (XOR swizzles
@@ -76,13 +79,23 @@ constexpr int LWEND = LW5 + N5 * (K5 + WPAD);  // 33536
 // dW staging: dZ_l [T][N_l + PAD] (natural order) followed by A_{l-1} [T][K_l + PAD] (C order)
 constexpr int stage_len(int K, int N) { return T * (N + PAD) + T * (K + PAD); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int LSLEN = cmax(cmax(cmax(stage_len(K1, N1), stage_len(K2, N2)), cmax(stage_len(K3, N3), stage_len(K4, N4))),
-                           stage_len(K5, N5));
+// LDS left for staging next to the weight image and the wide histogram. A layer whose full staging (T rows of dZ
+// and A) does not fit is staged and reduced in two passes of T / 2 rows -- column block 0 of every wave, then
+// block 1 (T = 256: layers 1-3; never at T <= 128)
+constexpr int WIDE_PAD = 2176;  // the wide (linear) weights / histogram, padded
+constexpr int LDS_FIXED_B = LWEND * 2 + WIDE_PAD * 4 + 64 * 4;
+constexpr int STAGE_MAX = ((163840 - LDS_FIXED_B) / 2) & ~7;
+constexpr bool split_stage(int K, int N) { return stage_len(K, N) > STAGE_MAX; }
+constexpr int stage_eff(int K, int N) { return split_stage(K, N) ? stage_len(K, N) / 2 : stage_len(K, N); }
+constexpr int LSLEN = cmax(cmax(cmax(stage_eff(K1, N1), stage_eff(K2, N2)), cmax(stage_eff(K3, N3), stage_eff(K4, N4))),
+                           stage_eff(K5, N5));
+static_assert(T == 256 || !(split_stage(K1, N1) || split_stage(K2, N2) || split_stage(K3, N3) ||
+                            split_stage(K4, N4) || split_stage(K5, N5)), "split staging is the T = 256 shape's");
+static_assert(!split_stage(K4, N4) && !split_stage(K5, N5), "layers 4-5 stage whole");
 constexpr int LS = LWEND;
 constexpr int LSEND = LS + LSLEN;
 constexpr int NWIDE = 2128;
 constexpr int WIDE_BIAS = 2127;
-constexpr int WIDE_PAD = 2176;
 constexpr int NTILE = 108;
 constexpr int LDS_BYTES = LSEND * 2 + WIDE_PAD * 4 + 64 * 4;
 static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -295,19 +308,63 @@ __device__ __forceinline__ void stage(uint16_t* S, const v4bf (&dz)[TBN][N / 16]
   }
 }
 
+// ---- split staging (T = 256, layers 1-3): pass `tb` stages column block tb of every wave (rows 16 w + sperm16(r) of
+// a T / 2-row image), the activation gradient waits as unmasked bf16 tiles until its pass's A rows give the mask
+template <int K, int N, int TBN>
+__device__ __forceinline__ void stage_half(uint16_t* S, const v4bf (&dz)[TBN][N / 16], const v8bf (&a)[TBN][K / 32],
+                                           int w, int r, int h, int tb) {
+  constexpr int R = T / 2;
+  uint16_t* SZ = S;
+  uint16_t* SA = S + R * (N + PAD);
+  const int row = 16 * w + sperm16(r);
+#pragma unroll
+  for (int t = 0; t < TBN; ++t) {
+    if (t != tb) continue;
+#pragma unroll
+    for (int m = 0; m < N / 32; ++m) *(v8bf*)(SZ + row * (N + PAD) + 32 * m + 8 * h) = cat_bf(dz[t][2 * m], dz[t][2 * m + 1]);
+#pragma unroll
+    for (int s2 = 0; s2 < K / 32; ++s2) *(v8bf*)(SA + row * (K + PAD) + 32 * s2 + 8 * h) = a[t][s2];
+  }
+}
+template <int K, int TBN>
+__device__ __forceinline__ void to_bf_tiles(const v4f (&g)[TBN][K / 16], unsigned int (&gb)[TBN][K / 16][2]) {
+#pragma unroll
+  for (int tb = 0; tb < TBN; ++tb)
+#pragma unroll
+    for (int kt = 0; kt < K / 16; ++kt) {
+      gb[tb][kt][0] = cvt_pk(g[tb][kt][0], g[tb][kt][1]);
+      gb[tb][kt][1] = cvt_pk(g[tb][kt][2], g[tb][kt][3]);
+    }
+}
+template <int K, int TBN>
+__device__ __forceinline__ void mask_half(const unsigned int (&gb)[TBN][K / 16][2], const uint16_t* SA, int w, int r,
+                                          int h, v4bf (&dz)[TBN][K / 16], int tb) {
+  const int row = 16 * w + sperm16(r);
+#pragma unroll
+  for (int t = 0; t < TBN; ++t) {
+    if (t != tb) continue;
+#pragma unroll
+    for (int kt = 0; kt < K / 16; ++kt) {
+      const uint2 m = *(const uint2*)(SA + row * (K + PAD) + 16 * kt + 4 * h);
+      const unsigned int u[2] = {mask_pk(gb[t][kt][0], m.x), mask_pk(gb[t][kt][1], m.y)};
+      dz[t][kt] = __builtin_bit_cast(v4bf, u);
+    }
+  }
+}
+
 // ---- weight gradient: the wave's NTW x KTW tiles (nt = nt0 + i ntS, kt = kt0 + j ktS) accumulate
 // dW^T[n][k] += sum_t dZ[t][n] A[t][k] over the T staged rows (4 k-steps of 32 examples)
-template <int K, int N, int NTW, int KTW>
+template <int K, int N, int NTW, int KTW, int ROWS = T>
 __device__ __forceinline__ void dw_phase(v4f (&acc)[NTW * KTW], const uint16_t* S, int nt0, int ntS, int kt0, int ktS,
                                          int r, int h) {
   const uint16_t* SZ = S;
-  const uint16_t* SA = S + T * (N + PAD);
+  const uint16_t* SA = S + ROWS * (N + PAD);
   const int q = r >> 2, p = r & 3;
   // example rows 32 ts + 8 h + q (first read) and + 4 (second): inside the 16-row block 16 (h >> 1) they are
   // rows 8 (h & 1) + q and + 4, physical sperm16() = 8 (h & 1) + 2 q and + 1
   const int rl = 16 * (h >> 1) + 8 * (h & 1) + 2 * q;
 #pragma unroll
-  for (int ts = 0; ts < T / 32; ++ts) {
+  for (int ts = 0; ts < ROWS / 32; ++ts) {
     v8bf fa[NTW], fb[KTW];
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
@@ -634,13 +691,17 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   BSTAMP(1);
   // PERSIST (grid 1, batch <= T): exactly one iteration, known at compile time, so the dW accumulators die at
   // their layer's emission instead of living across a loop back-edge
-  const int it_end = PERSIST ? 1 : niters, it_inc = PERSIST ? 1 : (int)gridDim.x;
-  for (int it = PERSIST ? 0 : (int)blockIdx.x; it < it_end; it += it_inc) {
+  // ONE_ITER (T = 256: the host launches grid >= ceil(batch / T)): every workgroup runs exactly its own iteration,
+  // also known at compile time -- the dW accumulators live only through their layer's phase, and no prefetch
+  constexpr bool SINGLE = PERSIST || ONE_ITER;
+  const int it_end = SINGLE ? 1 : niters, it_inc = SINGLE ? 1 : (int)gridDim.x;
+  for (int itv = SINGLE ? 0 : (int)blockIdx.x; itv < it_end; itv += it_inc) {
+    const int it = ONE_ITER ? (int)blockIdx.x : itv;
 #ifdef WDC_STAMPS
     stamp_on = niters > (int)gridDim.x ? it == (int)(blockIdx.x + gridDim.x) : it == (int)blockIdx.x;
 #endif
     STAMP(2);
-    const bool last = PERSIST || it + (int)gridDim.x >= niters;  // this workgroup's final iteration: dW final
+    const bool last = SINGLE || it + (int)gridDim.x >= niters;  // this workgroup's final iteration: dW final
     float* my_slab = TRAIN ? slab + (size_t)blockIdx.x * stride : nullptr;
     const long long pstep = step0 + ps + 1;  // PERSIST: the optimizer step (Adam bias correction)
     const bool plast = ps + 1 == nsteps;
@@ -654,7 +715,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       u[tb][0] = nu[tb][0];
       u[tb][1] = nu[tb][1];
     }
-    if constexpr (!PERSIST) fetch(it + gridDim.x, nu);  // next iteration's records
+    if constexpr (!SINGLE) fetch(it + gridDim.x, nu);  // next iteration's records
 
     // wide gather for the lane's column block (issued before the forward: its latency hides under MFMAs)
     const uint4 m0 = mtb ? u[TBN - 1][0] : u[0][0], m1 = mtb ? u[TBN - 1][1] : u[0][1];
@@ -798,44 +859,93 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 
     // ---- layer 3
     STAMP(9);
-    stage<K3, N3, TBN>(S, dz3, a2, w, r, h);
-    // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
-    // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
     v4bf dz2[TBN][K3 / 16];
-    {
-      v4f g[TBN][K3 / 16];
-      bwd_dA<K3, N3, TBN>(lds + LW3, dz3, g, r, h);
-      mask_grad<K3, TBN>(g, S + T * (N3 + PAD), w, r, h, dz2);
+    if constexpr (split_stage(K3, N3)) {  // two passes of T / 2 staged rows (column block 0, then 1)
+      unsigned int gb[TBN][K3 / 16][2];
+      {
+        stage_half<K3, N3, TBN>(S, dz3, a2, w, r, h, 0);
+        v4f g[TBN][K3 / 16];
+        bwd_dA<K3, N3, TBN>(lds + LW3, dz3, g, r, h);
+        to_bf_tiles<K3, TBN>(g, gb);
+      }
+      mask_half<K3, TBN>(gb, S + (T / 2) * (N3 + PAD), w, r, h, dz2, 0);
+      block_sync_lds();
+      dw_phase<K3, N3, 1, O3K, T / 2>(acc3, S, n3, 0, k3, 1, r, h);
+      block_sync_lds();
+      stage_half<K3, N3, TBN>(S, dz3, a2, w, r, h, 1);
+      mask_half<K3, TBN>(gb, S + (T / 2) * (N3 + PAD), w, r, h, dz2, 1);
+      block_sync_lds();
+      STAMP(10);
+      dw_phase<K3, N3, 1, O3K, T / 2>(acc3, S, n3, 0, k3, 1, r, h);
+    } else {
+      stage<K3, N3, TBN>(S, dz3, a2, w, r, h);
+      // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
+      // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
+      {
+        v4f g[TBN][K3 / 16];
+        bwd_dA<K3, N3, TBN>(lds + LW3, dz3, g, r, h);
+        mask_grad<K3, TBN>(g, S + T * (N3 + PAD), w, r, h, dz2);
+      }
+      block_sync_lds();
+      STAMP(10);
+      dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
     }
-    block_sync_lds();
-    STAMP(10);
-    dw_phase<K3, N3, 1, O3K>(acc3, S, n3, 0, k3, 1, r, h);
     WDC_EMIT(O3K, acc3, ct3);
     block_sync_lds();
 
     // ---- layer 2
     STAMP(11);
-    stage<K2, N2, TBN>(S, dz2, a1, w, r, h);
-    // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
-    // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
     v4bf dz1[TBN][K2 / 16];
-    {
-      v4f g[TBN][K2 / 16];
-      bwd_dA<K2, N2, TBN>(lds + LW2, dz2, g, r, h);
-      mask_grad<K2, TBN>(g, S + T * (N2 + PAD), w, r, h, dz1);
+    if constexpr (split_stage(K2, N2)) {  // two passes of T / 2 staged rows (column block 0, then 1)
+      unsigned int gb[TBN][K2 / 16][2];
+      {
+        stage_half<K2, N2, TBN>(S, dz2, a1, w, r, h, 0);
+        v4f g[TBN][K2 / 16];
+        bwd_dA<K2, N2, TBN>(lds + LW2, dz2, g, r, h);
+        to_bf_tiles<K2, TBN>(g, gb);
+      }
+      mask_half<K2, TBN>(gb, S + (T / 2) * (N2 + PAD), w, r, h, dz1, 0);
+      block_sync_lds();
+      dw_phase<K2, N2, O2N, O2K, T / 2>(acc2, S, n2, 1, k2, 1, r, h);
+      block_sync_lds();
+      stage_half<K2, N2, TBN>(S, dz2, a1, w, r, h, 1);
+      mask_half<K2, TBN>(gb, S + (T / 2) * (N2 + PAD), w, r, h, dz1, 1);
+      block_sync_lds();
+      STAMP(12);
+      dw_phase<K2, N2, O2N, O2K, T / 2>(acc2, S, n2, 1, k2, 1, r, h);
+    } else {
+      stage<K2, N2, TBN>(S, dz2, a1, w, r, h);
+      // the activation gradient needs only the weights, this wave's dZ and its own staged rows (the relu mask):
+      // issued before the barrier so its MFMAs and weight reads overlap the other waves' staging
+      {
+        v4f g[TBN][K2 / 16];
+        bwd_dA<K2, N2, TBN>(lds + LW2, dz2, g, r, h);
+        mask_grad<K2, TBN>(g, S + T * (N2 + PAD), w, r, h, dz1);
+      }
+      block_sync_lds();
+      STAMP(12);
+      dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
     }
-    block_sync_lds();
-    STAMP(12);
-    dw_phase<K2, N2, O2N, O2K>(acc2, S, n2, 1, k2, 1, r, h);
     WDC_EMIT(O2N * O2K, acc2, ct2);
     block_sync_lds();
 
     // ---- layer 1
     STAMP(13);
-    stage<K1, N1, TBN>(S, dz1, a0, w, r, h);
-    block_sync_lds();
-    STAMP(14);
-    dw_phase<K1, N1, O1N, 1>(acc1, S, n1, 1, 0, 0, r, h);
+    if constexpr (split_stage(K1, N1)) {  // two passes of T / 2 staged rows
+      stage_half<K1, N1, TBN>(S, dz1, a0, w, r, h, 0);
+      block_sync_lds();
+      dw_phase<K1, N1, O1N, 1, T / 2>(acc1, S, n1, 1, 0, 0, r, h);
+      block_sync_lds();
+      stage_half<K1, N1, TBN>(S, dz1, a0, w, r, h, 1);
+      block_sync_lds();
+      STAMP(14);
+      dw_phase<K1, N1, O1N, 1, T / 2>(acc1, S, n1, 1, 0, 0, r, h);
+    } else {
+      stage<K1, N1, TBN>(S, dz1, a0, w, r, h);
+      block_sync_lds();
+      STAMP(14);
+      dw_phase<K1, N1, O1N, 1>(acc1, S, n1, 1, 0, 0, r, h);
+    }
     WDC_EMIT(O1N, acc1, ct1);
     if constexpr (PERSIST) {  // the whole DNN update of this lane's columns (see opt_tiles)
       constexpr int NA = O1N + O2N * O2K + O3K + O4K + 1;
@@ -1051,8 +1161,10 @@ void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, l
 // other's definitions when both are loaded RTLD_GLOBAL
 #if WDC_T == 128
 #define WDC_SYM(n) n
-#else
+#elif WDC_T == 64
 #define WDC_SYM(n) n##_t64
+#else
+#define WDC_SYM(n) n##_t256
 #endif
 
 extern "C" {
@@ -1090,6 +1202,16 @@ int WDC_SYM(mifx_wdc_fused_f)(const void* data, long long n_data, long long batc
                     grad_scale, tmap, stride, xcd_of, fd);
   else
     launch<false, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                     grad_scale, tmap, stride, nullptr, fd);
+  return (int)hipGetLastError();
+#elif WDC_T == 256
+  if (waves != 8) return -1;  // 8 waves x 2 column blocks of 16 examples
+  if ((long long)grid * T < batch) return -1;  // ONE_ITER: one iteration per workgroup
+  if (train)
+    launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
+                    grad_scale, tmap, stride, xcd_of, fd);
+  else
+    launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                      grad_scale, tmap, stride, nullptr, fd);
   return (int)hipGetLastError();
 #else

@@ -43,11 +43,23 @@ def _fns64():
     }
 
 
+@functools.lru_cache(maxsize=None)
+def _fns256():
+    """csrc/wd_chain256.hip: 256 examples per iteration (8 waves x 32), ONE iteration per workgroup (grid * 256 >=
+    batch), layers 1-3 staged in two passes: the large-batch shape."""
+    lib = _lib.load("wd_chain256")
+    return {
+        "constants": sig(lib, "mifx_wdc_constants_t256", [VP, I32]),
+        "fused_f": sig(lib, "mifx_wdc_fused_f_t256", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
+                                                      I32, I32, VP, I64, I64, U64, VP]),
+    }
+
+
 def fns_for(tile: int) -> dict:
-    """Bindings of the T = tile build (128: csrc/wd_chain.hip, 64: csrc/wd_chain64.hip)."""
-    if tile not in (64, 128):
-        raise ValueError("tile must be 64 or 128")
-    return _fns() if tile == 128 else _fns64()
+    """Bindings of the T = tile build (128: csrc/wd_chain.hip, 64: csrc/wd_chain64.hip, 256: csrc/wd_chain256.hip)."""
+    if tile not in (64, 128, 256):
+        raise ValueError("tile must be 64, 128 or 256")
+    return {128: _fns, 64: _fns64, 256: _fns256}[tile]()
 
 
 @functools.lru_cache(maxsize=None)
@@ -69,8 +81,10 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
     tile 64 (64 examples per workgroup iteration): waves 4 (one wave per SIMD, 16 examples each). xcd_of: int32
     [>= grid], receives the XCD each workgroup ran on (for the XCD-local slab reduction). feed: (stride, offset,
     shuffle seed) of the record stream (csrc/feed.h, mifx.data.shuffle); None = (batch, 0, 0), stored order."""
-    if waves not in ((4, 8) if tile == 128 else (4,)):
-        raise ValueError("waves must be 4 or 8 (tile 128) / 4 (tile 64)")
+    if waves not in {128: (4, 8), 64: (4,), 256: (8,)}[tile]:
+        raise ValueError("waves must be 4 or 8 (tile 128) / 4 (tile 64) / 8 (tile 256)")
+    if tile == 256 and train and grid * 256 < batch:
+        raise ValueError("tile 256 runs one iteration per workgroup: grid * 256 >= batch")
     c = constants()
     if wimg_bf16.numel() != c["LWEND"] or wimg_bf16.element_size() != 2 or not wimg_bf16.is_contiguous():
         raise ValueError("weight image must be a contiguous 16-bit [LWEND] tensor")

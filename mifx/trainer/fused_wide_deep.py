@@ -63,7 +63,7 @@ class FusedWideDeepTrainer:
                  live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8,
                  in_kernel_tail: bool | None = None, persistent: bool | None = None,
                  small_tile: bool | None = None, shuffle_seed: int = 0, feed_stride: int | None = None,
-                 feed_offset: int = 0):
+                 feed_offset: int = 0, large_tile: bool | None = None):
         """shuffle_seed: 0 trains on the records in stored order; any other value draws a fresh pseudo-random
         permutation of the resident records every epoch inside the kernel's record fetch (csrc/feed.h; the
         reference's `read_batch_features(randomize_input=True)`, `taxi_utils.py:275-276`). feed_stride / feed_offset:
@@ -98,6 +98,15 @@ class FusedWideDeepTrainer:
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         ntiles = (self.batch + self.T - 1) // self.T
         self.grid = int(grid or min(ntiles, max_grid))
+        # large batches (more than one T = 128 iteration per workgroup): the T = 256 build, one iteration of 256
+        # examples per workgroup (csrc/wd_chain256.hip; MIFX_WD_T256=0 or large_tile=False turns it off)
+        if large_tile is None:
+            large_tile = os.environ.get("MIFX_WD_T256", "1") == "1"
+        tail_req = in_kernel_tail if in_kernel_tail is not None else os.environ.get("MIFX_WD_TAIL", "0") == "1"
+        self._t256 = bool(large_tile and kernel == "chain" and self.waves == 8 and grid is None and not tail_req
+                          and ntiles > max_grid and (self.batch + 255) // 256 <= max_grid)
+        if self._t256:
+            self.grid = (self.batch + 255) // 256
         self.dnn_opt = dnn_opt or default_dnn_opt()
         self.wide_opt = wide_opt or default_wide_opt(len(self.model.cfg.wide))
         self.loss_reduction = loss_reduction
@@ -184,8 +193,8 @@ class FusedWideDeepTrainer:
         # instead of one 8-wave T = 128 iteration that is mostly padding at the reference batch of 40
         if small_tile is None:
             small_tile = os.environ.get("MIFX_WD_T64", "1") == "1"
-        self.tile = 64 if (small_tile and kernel == "chain" and self.batch <= 64 and self.grid == 1
-                           and not self._persist and self._ktail is None) else 128
+        self.tile = 256 if self._t256 else 64 if (small_tile and kernel == "chain" and self.batch <= 64 and self.grid == 1
+                                                  and not self._persist and self._ktail is None) else 128
         if self.tile == 64:
             self.waves = 4
         self.slab_loss = torch.zeros(self.grid, device=dev)

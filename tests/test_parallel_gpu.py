@@ -87,8 +87,10 @@ def _resnet_run(world: int, rank: int, out: str) -> None:
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
 
     imgs, labels = synthetic_imagenet(64, size=72, classes=10, seed=0)  # same data on every rank
+    # one process accumulates the 2 micro-batches that the 2 ranks train on (ResNetTrainer's global sample)
     tr = ResNetTrainer(4, "cuda:0", imgs, labels, num_classes=10, lr=0.05, warmup_steps=1, crop=64,
-                       process_group=dist.group.WORLD if world > 1 else None, seed=3)
+                       process_group=dist.group.WORLD if world > 1 else None, seed=3,
+                       accum_steps=1 if world > 1 else 2)
     torch.backends.cudnn.benchmark = False  # no solver search in a test (and the same solvers in every process)
     # MIOpen's default bf16 convolution solvers are not run-to-run reproducible (profiles/resnet_determinism_r2s3.txt:
     # the same fwd+bwd twice in one process differs); its deterministic solvers are, which makes this exact
@@ -117,10 +119,11 @@ def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single():
         r0, r1 = (torch.load(f"{out}.2.{r}", weights_only=True) for r in range(2))
         one = torch.load(f"{out}.1.0", weights_only=True)
     assert all(torch.isfinite(torch.tensor(r0["losses"])))
-    # both ranks see the same batch: (g + g) / 2 == g exactly, so with deterministic kernels DP=2 IS the
-    # single-process run, bit for bit -- parameters, BN running statistics and losses
-    assert r0["losses"] == r1["losses"] == one["losses"], (r0["losses"], one["losses"])
+    # rank r trains micro-batch r of every step's global sample; the single process accumulates both micro-batches
+    # (loss / 2 each): the averaged DP gradient (g0 + g1) / 2 and the accumulated g0 / 2 + g1 / 2 are the same
+    # numbers up to the summation order of the halves, so the replicas are bit-identical and match the single run
+    for a, b, c in zip(r0["losses"], r1["losses"], one["losses"]):
+        assert abs((a + b) / 2 - c) < 1e-4 * max(1.0, abs(c)), (r0["losses"], r1["losses"], one["losses"])
     for k in one["state"]:
-        assert torch.equal(r0["state"][k], one["state"][k]) and torch.equal(r1["state"][k], one["state"][k]), k
-    for k in one["stats"]:
-        assert torch.equal(r0["stats"][k], one["stats"][k]) and torch.equal(r1["stats"][k], one["stats"][k]), k
+        assert torch.equal(r0["state"][k], r1["state"][k]), k
+        torch.testing.assert_close(r0["state"][k], one["state"][k], rtol=1e-5, atol=1e-6, msg=k)

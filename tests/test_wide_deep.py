@@ -568,3 +568,39 @@ def test_persistent_small_batch_matches_slab_path(batch, opt):
     for a, b in zip(out[0][:4], out[1][:4]):
         assert torch.equal(a, b)
     assert np.isfinite(out[0][4]) and out[0][4] == out[1][4]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [4096, 65536])
+def test_large_tile_matches_t128(batch):
+    """The T = 256 build (csrc/wd_chain256.hip: 8 waves x 32 examples, one iteration per workgroup, layers 1-3
+    staged in two 128-row passes) against the T = 128 build running two iterations per workgroup on the same
+    batch: the same gradient up to the fp32 order of the per-workgroup sums (the examples land in other
+    workgroups), the fp32 autograd gradient within the bf16 data path's error, and run-to-run bit-identical."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(batch * 3, device=dev, seed=33)
+    G = batch // 256
+    grads, params = {}, {}
+    for large in (True, False, True):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device=dev, max_grid=G, large_tile=large)
+        assert (tr.tile, tr.grid) == ((256, G) if large else (128, G))
+        tr.set_data(rec)
+        g = tr.gradients_once()
+        tr.capture(steps_per_graph=5)
+        tr.run(10)
+        torch.cuda.synchronize()
+        if large in grads:
+            np.testing.assert_array_equal(g, grads[large])
+            assert torch.equal(tr.param, params[large])
+        grads[large], params[large] = g, tr.param.clone()
+    scale = np.abs(grads[False]).max()
+    np.testing.assert_allclose(grads[True], grads[False], rtol=0, atol=2e-5 * scale)
+    assert torch.allclose(params[True], params[False], rtol=2e-3, atol=2e-4)
+    # the fp32 model's gradient on the first batch (the T = 256 step's own check)
+    named = wdm.canonical_grad_to_torch(grads[True], wdm.WideDeepModel(seed=5), tr.gidx_np)
+    _, ref = _torch_grads(wdm.WideDeepModel(seed=5), rec[:batch].cpu())
+    for name, r in ref.items():
+        rel = np.linalg.norm(named[name].reshape(r.shape) - r) / (np.linalg.norm(r) + 1e-8)
+        assert rel < 0.06, f"{name}: relative Frobenius err {rel:.4f}"
