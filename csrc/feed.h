@@ -12,12 +12,22 @@
 //   epoch e = p / n,  i = p mod n
 //   record  = key == 0 ? i : feistel_perm(i, n, epoch_key(key, e))
 //
+// The permutation moves GROUPS of 2^MIFX_SHUFFLE_GLOG2 = 4 consecutive records (one 128-byte cache line of 32-byte
+// records): a fresh random order of the record groups every epoch, records inside a group kept together (the
+// n mod 4 records past the last whole group keep their place). A batch of B rows then reads B / 4 random lines
+// instead of B random half-lines: the per-record shuffle cost 1.4 us of a 35 us step at B = 65536 (the wave's 16
+// distinct records per load instruction each a separate line), this one ~0 (profiles/wd_shuffle_ab_r4.txt).
+//
 // feistel_perm: a 4-round balanced Feistel network on [0, 2^(2h)) (2^(2h) >= n, h >= 1) with cycle walking down to
 // [0, n) -- a bijection of [0, n) for every n and key (each walk follows the permutation's cycle from i until it
 // re-enters [0, n), which it must: at the latest back at i). Expected walk length < 4 (2^(2h) < 4n).
 // mifx/data/shuffle.py is the bit-exact host implementation (tests and the CPU trainer).
 #pragma once
 #include <stdint.h>
+
+#ifndef MIFX_SHUFFLE_GLOG2
+#define MIFX_SHUFFLE_GLOG2 2
+#endif
 
 #ifdef __HIPCC__
 #define MIFX_HD __host__ __device__ __forceinline__
@@ -94,10 +104,13 @@ struct MifxFeed {
   unsigned long long key;  // 0: no shuffle (records in stored order); else the shuffle seed
 };
 
-// per step: the epoch and in-epoch index of this replica's first row
+// per step: the epoch and in-epoch index of this replica's first row, the group count and Feistel half width, and
+// the epoch keys of the step's epoch and the next (a batch spans at most one epoch boundary)
 struct MifxFeedStep {
   long long e0, i0;
+  long long ng;
   int h;
+  uint64_t ek0, ek1;
 };
 MIFX_HD MifxFeedStep mifx_feed_step(const MifxFeed& f, long long step, long long n) {
   const long long p = step * f.gstride + f.goff;
@@ -115,7 +128,10 @@ MIFX_HD MifxFeedStep mifx_feed_step(const MifxFeed& f, long long step, long long
   }
   s.e0 = e;
   s.i0 = i;
-  s.h = mifx_feistel_half((uint64_t)n);
+  s.ng = n >> MIFX_SHUFFLE_GLOG2;
+  s.h = mifx_feistel_half((uint64_t)(s.ng > 0 ? s.ng : 1));
+  s.ek0 = f.key ? mifx_epoch_key(f.key, (uint64_t)e) : 0;
+  s.ek1 = f.key ? mifx_epoch_key(f.key, (uint64_t)e + 1) : 0;
   return s;
 }
 // record of batch row `row` (0 <= row < batch <= n)
@@ -126,7 +142,11 @@ MIFX_HD long long mifx_feed_record(const MifxFeed& f, const MifxFeedStep& s, lon
     e += 1;
   }
   if (f.key == 0) return i;
-  const uint64_t ek = mifx_epoch_key(f.key, (uint64_t)e);
-  if (s.h <= 16) return (long long)mifx_feistel_perm32((uint32_t)i, (uint64_t)n, ek, s.h);
-  return (long long)mifx_feistel_perm((uint64_t)i, (uint64_t)n, ek, s.h);
+  constexpr int GL = MIFX_SHUFFLE_GLOG2;
+  if (i >= (s.ng << GL)) return i;  // the records past the last whole group
+  const uint64_t ek = e == s.e0 ? s.ek0 : s.ek1;
+  const long long g = i >> GL, in = i & ((1ll << GL) - 1);
+  const long long pg = s.h <= 16 ? (long long)mifx_feistel_perm32((uint32_t)g, (uint64_t)s.ng, ek, s.h)
+                                 : (long long)mifx_feistel_perm((uint64_t)g, (uint64_t)s.ng, ek, s.h);
+  return (pg << GL) | in;
 }

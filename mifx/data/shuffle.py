@@ -6,16 +6,20 @@ resident and evaluate a per-epoch pseudo-random permutation of [0, n) per record
 CPU trainer and the tests use these functions to compute the same record indices:
 
     p = step * gstride + goff + row;  e = p // n;  i = p % n
-    record = i                                   (seed 0: stored order)
-             feistel_perm(i, n, epoch_key(seed, e))   (otherwise)
+    record = i                                               (seed 0: stored order)
+             4 feistel_perm(i // 4, n // 4, epoch_key(seed, e)) + i % 4     (otherwise; i < 4 (n // 4))
+             i                                               (the n % 4 records past the last whole group)
 
-feistel_perm is a bijection of [0, n) for every n >= 1 and key: a 4-round balanced Feistel network on
-[0, 4^h) (4^h >= n) with cycle walking."""
+The shuffle permutes GROUPS of GROUP = 4 consecutive records (one 128-byte line of 32-byte records) -- see
+csrc/feed.h. feistel_perm is a bijection of [0, m) for every m >= 1 and key: a 4-round balanced Feistel network on
+[0, 4^h) (4^h >= m) with cycle walking."""
 from __future__ import annotations
 
 import numpy as np
 
 _M32 = np.uint64(0xFFFFFFFF)
+GROUP_LOG2 = 2  # csrc/feed.h MIFX_SHUFFLE_GLOG2
+GROUP = 1 << GROUP_LOG2
 
 
 def _mix32(x: np.ndarray) -> np.ndarray:
@@ -82,9 +86,12 @@ def record_indices(step: int, batch: int, n: int, gstride: int | None = None, go
     e[wrap] += 1
     if seed == 0:
         return i
-    out = np.empty(batch, dtype=np.int64)
-    h = feistel_half(n)
+    ng = n >> GROUP_LOG2
+    out = i.copy()  # records past the last whole group keep their place
+    h = feistel_half(max(ng, 1))
     for ep in np.unique(e):
-        sel = e == ep
-        out[sel] = feistel_perm(i[sel], n, epoch_key(int(seed), int(ep)), h)
+        sel = (e == ep) & (i < ng * GROUP)
+        if sel.any():
+            g = feistel_perm(i[sel] >> GROUP_LOG2, ng, epoch_key(int(seed), int(ep)), h)
+            out[sel] = (g << GROUP_LOG2) | (i[sel] & (GROUP - 1))
     return out

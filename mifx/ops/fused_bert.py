@@ -438,9 +438,14 @@ def attention(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, rng=None, 
     if p > 0 and rng is None:
         raise ValueError("attention dropout p > 0 needs an rng state tensor [seed, counter]")
     htot = qkv.shape[3] if htot is None else htot
+    from . import native_stats
+
     if (qkv.is_cuda and not _TORCH_OPS and qkv.shape[1] in ATTN_SEQ and qkv.shape[4] == 64
             and qkv.dtype == torch.bfloat16):
+        native_stats.count("attention", True)
         return _Attention.apply(qkv, kbias, scale, p, rng, site, h0, htot)
+    if qkv.is_cuda:
+        native_stats.count("attention", False)
     if qkv.is_cuda and not p > 0:  # other shapes without dropout: the library flash kernel, no S x S tensor
         q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
         am = None if kbias is None else kbias[:, None, None, :].to(q.dtype)

@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import native_stats
 from ._lib import I32, VP, check, ptr, sig, stream_handle
 
 
@@ -143,7 +144,9 @@ def join_weight_grads(device) -> None:
 
 def _dw_tensor(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     if tn_preferred(dy2.shape[1], x2.shape[1], dy2.shape[0]) and tn_eligible(dy2, x2):
+        native_stats.count("gemm_dW", True)
         return gemm_tn(dy2, x2)
+    native_stats.count("gemm_dW", False)
     return dy2.t() @ x2
 
 
@@ -182,6 +185,7 @@ class GradSlot:
 
 
 def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tensor:
+    native_stats.count("gemm_dX", False)  # dX = dY W on hipBLASLt (with the residual gradient as its C operand)
     if slot is None:
         return dy2 @ w
     g, slot.g = slot.g, None
@@ -255,6 +259,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, f
     wherever it tiles the shape), and the weight gradient on the hand-written TN kernel where that is preferred.
     slot: the input gradient also carries the residual gradient parked there (GradSlot)."""
     fwd = eligible(x, w) if force else preferred(x, w)
+    if x.is_cuda:
+        native_stats.count("gemm_fwd", fwd)
     bwd = (x.is_cuda and x.dtype == torch.bfloat16 and w.requires_grad and torch.is_grad_enabled()
            and tn_preferred(w.shape[0], w.shape[1], x.numel() // x.shape[-1]))
     if fwd or bwd or slot is not None:
@@ -267,7 +273,10 @@ def linear_bias_gelu(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, force
     """GELU(x w^T + bias) with the bias + GELU fused into the GEMM epilogue where preferred (force: wherever it
     tiles)."""
     if eligible(x, w) if force else preferred(x, w):
+        native_stats.count("gemm_fwd_bias_gelu", True)
         return _LinearBiasGelu.apply(x, w, bias, slot)
+    if x.is_cuda:
+        native_stats.count("gemm_fwd_bias_gelu", False)
     from .fused_bert import bias_gelu
 
     return bias_gelu(linear(x, w, slot=slot), bias)

@@ -198,9 +198,16 @@ def main(argv=None):
     tr = BertTrainer(BertConfig(layers=a.layers, dropout=a.dropout), a.batch, a.seq, dev, tp,
                      graph=False if a.no_graph else (True if a.graph else None),
                      flat_adamw=False if a.no_flat_adamw else None, sdpa=a.sdpa)
+    from ..ops import native_stats
+
+    per_step = None
     with heartbeat("bert warmup"):
-        for _ in range(a.warmup):
+        for i in range(a.warmup):
+            if i == 0:
+                native_stats.reset()
             tr.step()
+            if i == 0:  # the first step runs every dispatch in Python: which path each GEMM / attention call took
+                per_step = native_stats.snapshot()
         if dev.type == "cuda":
             torch.cuda.synchronize()
     mdist.barrier()
@@ -225,6 +232,7 @@ def main(argv=None):
                           "seq_len": a.seq, "ms_per_step": 1e3 * dt / a.steps, "loss": float(loss),
                           "dtype": "bf16", "data": "synthetic", "layers": a.layers,
                           "hipgraph": tr.graph is not None,
+                          "calls_per_step_native_vs_fallback": per_step,
                           "optimizer": "flat bf16 AdamW (fp32 master)" if tr.flat else "torch fused AdamW"}),
               flush=True)
     mdist.shutdown()
