@@ -54,7 +54,7 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 // workgroups, the forward and activation-gradient chains of both blocks interleaved in one wave)
 constexpr int T = WDC_T;
 static_assert(T == 128 || T == 64 || T == 256, "T");
-constexpr bool ONE_ITER = T == 256;  // see the iteration loop of wdc_fused
+constexpr bool ONE_ITER = T == 256 || T == 64;  // see the iteration loop of wdc_fused
 constexpr int MAXW = 8;  // waves per workgroup: T / (16 TBN), TBN = 16-example column blocks per wave (1 or 2)
 // Row padding (elements): WPAD for the weight images, PAD for the staging images; with the row permutations below
 // (wperm, sperm16) every LDS access site is conflict-free in the bank model (tools/lds_banks.py). (XOR swizzles
@@ -1197,6 +1197,7 @@ int WDC_SYM(mifx_wdc_fused_f)(const void* data, long long n_data, long long batc
   const dim3 g(grid);
 #if WDC_T == 64
   if (waves != 4) return -1;
+  if ((long long)grid * T < batch) return -1;  // ONE_ITER: one iteration per workgroup
   if (train)
     launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                     grad_scale, tmap, stride, xcd_of, fd);
