@@ -95,8 +95,9 @@ def _read_varint(buf: bytes, i: int):
         shift += 7
 
 
-def read_scalars(path_or_dir: str) -> dict[str, list[tuple[int, float]]]:
-    """{tag: [(step, value), ...]} from one events file or every events file in a directory."""
+def read_scalars(path_or_dir: str, with_wall_time: bool = False) -> dict[str, list[tuple]]:
+    """{tag: [(step, value), ...]} from one events file or every events file in a directory
+    ([(wall_time, step, value), ...] with with_wall_time)."""
     files = [path_or_dir] if os.path.isfile(path_or_dir) else sorted(
         os.path.join(path_or_dir, f) for f in os.listdir(path_or_dir) if f.startswith("events.out.tfevents"))
     out: dict[str, list] = {}
@@ -109,5 +110,6 @@ def read_scalars(path_or_dir: str) -> dict[str, list[tuple[int, float]]]:
                 if f != 1:
                     continue
                 d = dict(_fields(val))
-                out.setdefault(d[1].decode(), []).append((int(ev.get(2, 0)), float(d.get(2, 0.0))))
+                row = (int(ev.get(2, 0)), float(d.get(2, 0.0)))
+                out.setdefault(d[1].decode(), []).append((float(ev.get(1, 0.0)),) + row if with_wall_time else row)
     return out
