@@ -495,7 +495,9 @@ def test_in_kernel_tail_step_matches_three_launch_step(batch, opt):
     kw = {} if opt == "adagrad_ftrl" else {"dnn_opt": OptSpec(opt, lr=lr), "wide_opt": OptSpec(opt, lr=lr)}
     out = []
     for tail in (True, False):
-        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=batch, device="cuda", in_kernel_tail=tail, **kw)
+        # (the three-launch side on the same T = 128 build: large_tile=False)
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=3), batch=batch, device="cuda", in_kernel_tail=tail,
+                                  large_tile=False, **kw)
         assert (tr._ktail is not None) == tail
         tr.set_data(recs)
         tr.capture(steps_per_graph=5)

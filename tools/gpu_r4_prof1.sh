@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_wide_deep.py tests/test_shuffle.py > gpurun_out/r4_t4.log 2>&1 || { tail -40 gpurun_out/r4_t4.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_wide_deep.py tests/test_shuffle.py tests/test_dist_gpu.py tests/test_bench_launch.py > gpurun_out/r4_t4.log 2>&1 || { tail -40 gpurun_out/r4_t4.log; exit 1; }
 tail -2 gpurun_out/r4_t4.log
 for r in 1 2; do
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r4_b4.json 2>/dev/null || exit 1
