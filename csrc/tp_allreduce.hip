@@ -1,0 +1,199 @@
+// Two-shot all-reduce of bf16 activations over xGMI peer memory, for tensor parallelism (BERT, BASELINE config 4).
+//
+// Megatron-style TP reduces a [tokens, hidden] activation after every row-parallel projection (attention out, FFN
+// out) and every column-parallel input gradient: 2 + 2 per transformer block per step, 6.3 MB each at B = 32,
+// S = 128. Issued through torch.distributed they are host-side collectives between kernels (no hipGraph capture of
+// the TP step, a host round trip each). Here each rank's partial is exchanged through IPC-mapped HBM with device-side
+// epoch flags, in three stream-ordered kernels that capture into a graph:
+//
+//   A  tpar_publish   (one workgroup per 8 KB chunk): copy the partial into this rank's IPC buffer half (epoch & 1)
+//                     with system-scope stores, then stamp flag[0][chunk][rank] = epoch in every peer;
+//   B  tpar_reduce    (chunks c with c % world == rank): wait for every peer's stamp of c, sum the world partials
+//                     of c in rank order in fp32 (identical bits on every rank), round to bf16 into this rank's
+//                     reduced buffer half, stamp flag[1][c][rank] in every peer (the reduce-scatter);
+//   C  tpar_gather    (every chunk): wait for the owner's phase-1 stamp, copy its reduced chunk into the output (the
+//                     all-gather); the last workgroup advances the epoch counter.
+//
+// Bytes over xGMI per rank: (world - 1) / world of the tensor twice (the two shots), instead of (world - 1) x the
+// tensor for a one-shot sum; point-to-point links to every peer at once (xGMI full mesh, no ring hops).
+// Double buffering by epoch parity makes one flag per chunk and phase enough (a rank rewrites half (e & 1) only in
+// epoch e + 2, after every peer's epoch e + 1 kernel A stamp, which that peer issued after its epoch e kernels B and
+// C had read the half). Waits run in one-wave workgroups and are bounded by wall-clock time: a peer that never
+// arrives sets the sticky err flag; every later kernel of this group then does nothing (the host raises at its
+// next check) instead of hanging the GPU. Data moves as 8-byte system-scope accesses (write-through stores, L2-
+// bypassing loads), so no cache maintenance is needed anywhere.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int MAXW = 8;
+constexpr int CHUNK = 4096;          // bf16 elements per chunk (8 KB)
+constexpr int WG = 64;               // one wave per workgroup
+constexpr int PER_LANE = CHUNK / 4 / WG;  // uint64 (4 x bf16) per lane per chunk = 16
+constexpr long long TIMEOUT_TICKS = 1000ll * 1000 * 1000;  // 10 s at the 100 MHz real-time clock
+
+struct Peers {
+  uint64_t* buf[MAXW];     // peer p's partial buffer [2][npad / 4] (uint64 = 4 bf16)
+  uint64_t* red[MAXW];     // peer p's reduced buffer [2][npad / 4]
+  unsigned int* flag[MAXW];  // peer p's flags [2][nchunks][MAXW] (uncached)
+};
+
+__device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool failed(const int* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+__device__ __forceinline__ void publish(unsigned int* f, unsigned int e) {
+  __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// wait until *f reaches epoch e (wrapping compare); false on timeout or an earlier failure
+__device__ __forceinline__ bool wait_flag(const unsigned int* f, unsigned int e, int* err) {
+  const long long t0 = wall_clock64();
+  while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+    __builtin_amdgcn_s_sleep(2);
+    if (failed(err)) return false;
+    if (wall_clock64() - t0 > TIMEOUT_TICKS) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ float2 bf2f(uint32_t u) {
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+}
+__device__ __forceinline__ uint32_t f2bf(float a, float b) {  // round to nearest even, NaN kept a NaN
+  typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, (v2bf){(__bf16)a, (__bf16)b});
+}
+
+// A: partial -> own buffer half, stamp phase 0
+__global__ __launch_bounds__(WG) void tpar_publish(const uint64_t* __restrict__ x, long long n4, Peers pe, int world,
+                                                   int rank, long long npad4, const long long* __restrict__ ep,
+                                                   const int* __restrict__ err, int nchunks) {
+  if (failed(err)) return;  // one wave: a uniform exit
+  const long long e = ep[0] + 1;
+  const int c = blockIdx.x;
+  uint64_t* dst = pe.buf[rank] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+  const long long base = (long long)c * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const long long q = base + i * WG + threadIdx.x;
+    st_sys64(dst + i * WG + threadIdx.x, q < n4 ? x[q] : 0ull);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave acknowledged before the stamps
+  if (threadIdx.x < world)
+    publish(pe.flag[threadIdx.x] + ((size_t)0 * nchunks + c) * MAXW + rank, (unsigned int)e);
+}
+
+// B: reduce-scatter of the chunks this rank owns (c = rank + world k)
+__global__ __launch_bounds__(WG) void tpar_reduce(Peers pe, int world, int rank, long long npad4,
+                                                  const long long* __restrict__ ep, int* __restrict__ err,
+                                                  int nchunks, int nch) {
+  if (failed(err)) return;
+  const int c = rank + world * blockIdx.x;
+  if (c >= nch) return;  // (nch: chunks holding data; nchunks: the flag array's chunk dimension)
+  const long long e = ep[0] + 1;
+  const unsigned int* my = pe.flag[rank];
+  bool ok = true;
+  if (threadIdx.x < world) ok = wait_flag(my + ((size_t)0 * nchunks + c) * MAXW + threadIdx.x, (unsigned int)e, err);
+  if (__ballot(!ok) != 0ull) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the peers' partials were stored before their stamps
+  const size_t off = (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+  uint64_t* dst = pe.red[rank] + off;
+#pragma unroll 4
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int q = i * WG + threadIdx.x;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    uint64_t v[MAXW];
+#pragma unroll
+    for (int p = 0; p < MAXW; ++p) v[p] = p < world ? ld_sys64(pe.buf[p] + off + q) : 0ull;
+#pragma unroll
+    for (int p = 0; p < MAXW; ++p)  // rank order: the same fp32 sum on every rank
+      if (p < world) {
+        const float2 a = bf2f((uint32_t)v[p]), b = bf2f((uint32_t)(v[p] >> 32));
+        s[0] += a.x;
+        s[1] += a.y;
+        s[2] += b.x;
+        s[3] += b.y;
+      }
+    st_sys64(dst + q, (uint64_t)f2bf(s[0], s[1]) | ((uint64_t)f2bf(s[2], s[3]) << 32));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x < world)
+    publish(pe.flag[threadIdx.x] + ((size_t)1 * nchunks + c) * MAXW + rank, (unsigned int)e);
+}
+
+// C: all-gather of the reduced chunks into the output; the last workgroup advances the epoch
+__global__ __launch_bounds__(WG) void tpar_gather(uint64_t* __restrict__ y, long long n4, Peers pe, int world, int rank,
+                                                  long long npad4, long long* __restrict__ ep, int* __restrict__ err,
+                                                  int nchunks, unsigned int* __restrict__ done) {
+  if (failed(err)) return;
+  const long long e = ep[0] + 1;
+  const int c = blockIdx.x, owner = c % world;
+  bool ok = true;
+  if (threadIdx.x == 0)  // (own chunks too: uniform code; their stamp is already there)
+    ok = wait_flag(pe.flag[rank] + ((size_t)1 * nchunks + c) * MAXW + owner, (unsigned int)e, err);
+  if (__ballot(!ok) != 0ull) return;  // no epoch advance: the error is sticky, the host raises
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const uint64_t* src = pe.red[owner] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+  const long long base = (long long)c * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const long long q = base + i * WG + threadIdx.x;
+    const uint64_t v = ld_sys64(src + i * WG + threadIdx.x);
+    if (q < n4) y[q] = v;
+  }
+  // every workgroup read ep before its arrival: the last one to arrive advances it for the next call
+  if (threadIdx.x == 0) {
+    const unsigned int old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned int)gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ep[0] = e;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mifx_tpar_chunk() { return CHUNK; }
+
+// x, y: bf16 [n] (n % 4 == 0, 8-byte aligned; y may equal x); bufs / reds / flags: host arrays of `world` device
+// pointers (IPC-opened peer buffers, [rank] = own): bufs / reds [2][npad] bf16 with npad = nchunks * CHUNK >= n,
+// flags [2][nchunks][8] uint32 (uncached). ep: int64 epoch counter (device), done: uint32 arrival counter (device,
+// zero), err: sticky int flag (device). Three kernels on `stream`.
+int mifx_tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, void* const* reds, void* const* flags,
+                        int world, int rank, long long npad, long long* ep, unsigned int* done, int* err,
+                        hipStream_t stream) {
+  if (world < 1 || world > MAXW || rank < 0 || rank >= world || n <= 0 || n % 4 != 0 || npad % CHUNK != 0 ||
+      n > npad || x == nullptr || y == nullptr || ep == nullptr || done == nullptr || err == nullptr)
+    return -1;
+  if ((uintptr_t)x % 8 != 0 || (uintptr_t)y % 8 != 0) return -1;
+  Peers pe{};
+  for (int p = 0; p < world; ++p) {
+    if (bufs[p] == nullptr || reds[p] == nullptr || flags[p] == nullptr) return -1;
+    pe.buf[p] = (uint64_t*)bufs[p];
+    pe.red[p] = (uint64_t*)reds[p];
+    pe.flag[p] = (unsigned int*)flags[p];
+  }
+  const int nchunks = (int)((n + CHUNK - 1) / CHUNK);
+  const int nchunks_all = (int)(npad / CHUNK);  // the flag array's chunk dimension
+  const long long n4 = n / 4, npad4 = npad / 4;
+  hipLaunchKernelGGL(tpar_publish, dim3(nchunks), dim3(WG), 0, stream, (const uint64_t*)x, n4, pe, world, rank, npad4,
+                     ep, err, nchunks_all);
+  hipLaunchKernelGGL(tpar_reduce, dim3((nchunks + world - 1) / world), dim3(WG), 0, stream, pe, world, rank, npad4, ep,
+                     err, nchunks_all, nchunks);
+  hipLaunchKernelGGL(tpar_gather, dim3(nchunks), dim3(WG), 0, stream, (uint64_t*)y, n4, pe, world, rank, npad4, ep,
+                     err, nchunks_all, done);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -14,7 +14,11 @@ BERT-base fine-tune at TP=8, so this module provides the standard column/row spl
 
 Two all-reduces per transformer block (after attention-out and FFN-out), each of
 [tokens, hidden] activations — on MI355X the 8-GPU xGMI ring is ~7 links x ~150 GB/s, so a
-[32*128, 768] bf16 block reduction (6.3 MB) is ~10-15 us."""
+[32*128, 768] bf16 block reduction (6.3 MB) is ~10-15 us.
+
+`TPGroup.enable_ipc(max_elems, device)` moves every bf16 TP all-reduce onto the two-shot peer-memory kernels of
+mifx.parallel.tp_ipc (no host collective: the TP step captures into a hipGraph); otherwise torch.distributed's
+all-reduce runs in place on the fresh GEMM output / gradient (no defensive copies either way)."""
 from __future__ import annotations
 
 import torch
@@ -32,11 +36,35 @@ class TPGroup:
         self.group = group if group is not None else (dist.group.WORLD if dist.is_initialized() else None)
         self.size = dist.get_world_size(self.group) if self.group is not None else 1
         self.rank = dist.get_rank(self.group) if self.group is not None else 0
+        self.ipc = None
+
+    def enable_ipc(self, max_elems: int, device) -> None:
+        """Route bf16 all-reduces of up to max_elems elements through the peer-memory kernels (collective)."""
+        if self.size > 1 and self.ipc is None:
+            from .tp_ipc import IpcAllReduce
+
+            self.ipc = IpcAllReduce(self.group, device, max_elems)
+
+    def disable_ipc(self) -> None:
+        if self.ipc is not None:
+            self.ipc.close()
+            self.ipc = None
+
+    def check(self) -> None:
+        if self.ipc is not None:
+            self.ipc.check()
 
 
 def _all_reduce(x: torch.Tensor, tp: TPGroup) -> torch.Tensor:
-    if tp.size > 1:
-        dist.all_reduce(x, group=tp.group)
+    """Sum over the TP ranks. x must be a fresh tensor nobody else reads (a GEMM output or an incoming gradient):
+    the torch path reduces it in place, the IPC path returns a new tensor."""
+    if tp.size == 1:
+        return x
+    x = x.contiguous()
+    if tp.ipc is not None and x.dtype == torch.bfloat16 and x.is_cuda and x.numel() % 4 == 0 \
+            and x.numel() <= tp.ipc.npad:
+        return tp.ipc.all_reduce(x)
+    dist.all_reduce(x, group=tp.group)
     return x
 
 
@@ -50,7 +78,11 @@ class _CopyToTP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return _all_reduce(g.contiguous().clone(), ctx.tp), None
+        # (the incoming gradient may be shared by other consumers of the graph: reduce a private copy on the
+        # torch path; the IPC path writes a new tensor anyway)
+        if ctx.tp.ipc is None:
+            g = g.clone()
+        return _all_reduce(g, ctx.tp), None
 
 
 class _ReduceFromTP(torch.autograd.Function):
@@ -58,7 +90,12 @@ class _ReduceFromTP(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, tp):
-        return _all_reduce(x.contiguous().clone(), tp)
+        # x is the row-parallel GEMM's fresh output (F.linear saves its input and weight, not its output): the
+        # torch path reduces it in place (marked dirty for autograd), the IPC path writes a new tensor
+        y = _all_reduce(x, tp)
+        if y is x:
+            ctx.mark_dirty(x)
+        return y
 
     @staticmethod
     def backward(ctx, g):

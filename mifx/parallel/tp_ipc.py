@@ -1,0 +1,120 @@
+"""Graph-capturable tensor-parallel all-reduce over xGMI peer memory (csrc/tp_allreduce.hip).
+
+Every rank of the TP group allocates three IPC-exportable buffers -- its partial-sum buffer and its reduced-slice
+buffer ([2][npad] bf16 each, double-buffered by epoch parity) and an uncached flag array -- and opens its peers'
+(handles all-gathered over the process group once, as mifx.parallel.xgmi does for the W&D gradient). An all-reduce
+is then three kernels on the current stream (publish, reduce-scatter, all-gather) synchronised by device-side
+epoch flags: no host collective, so a TP step captures into a hipGraph like a single-GPU step, and the result lands
+in a fresh tensor (no defensive `.clone()` of the input). The reduction is a rank-order fp32 sum rounded once to
+bf16: every rank gets the same bits. A peer that never arrives sets a sticky error flag after a bounded wait;
+`check()` raises. Used by mifx.parallel.tensor_parallel when `TPGroup.enable_ipc()` was called."""
+from __future__ import annotations
+
+import ctypes
+import functools
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+from ..ops._lib import I32, I64, VP, check, ptr, sig, stream_handle
+from .xgmi import MAX_WORLD, _fns as _xg_fns
+
+
+@functools.lru_cache(maxsize=None)
+def _fns():
+    lib = _lib.load("tp_allreduce")
+    return {"chunk": sig(lib, "mifx_tpar_chunk", []),
+            "ar": sig(lib, "mifx_tpar_allreduce", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, VP])}
+
+
+class IpcAllReduce:
+    """All-reduce (sum) of bf16 tensors of up to `max_elems` elements over the ranks of `pg`, one GPU each (or
+    ranks sharing one GPU in rehearsals: the IPC path is the same)."""
+
+    def __init__(self, pg, device, max_elems: int):
+        self.pg, self.device = pg, torch.device(device)
+        self.rank, self.world = dist.get_rank(pg), dist.get_world_size(pg)
+        if not 1 <= self.world <= MAX_WORLD:
+            raise ValueError(f"IPC all-reduce supports 1..{MAX_WORLD} ranks")
+        chunk = _fns()["chunk"]()
+        self.npad = -(-int(max_elems) // chunk) * chunk
+        self.nchunks = self.npad // chunk
+        xf = _xg_fns()
+        self._own, self._opened = [], []
+        mine, err = None, ""
+        bufs = [VP(), VP(), VP()]
+        try:
+            with torch.cuda.device(self.device):
+                sizes = (2 * self.npad * 2, 2 * self.npad * 2, 2 * self.nchunks * MAX_WORLD * 4)
+                for b, nbytes, unc in zip(bufs, sizes, (0, 0, 1)):
+                    check(xf["malloc"](nbytes, unc, ctypes.byref(b)), "tp ipc malloc")
+                    self._own.append(b)
+                hs = xf["hsize"]()
+                hdl = []
+                for b in bufs:
+                    h = (ctypes.c_char * hs)()
+                    check(xf["export"](b, h), "hipIpcGetMemHandle")
+                    hdl.append(bytes(h))
+                mine = tuple(hdl)
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            err = f"rank {self.rank}: {e}"
+        handles = [None] * self.world
+        dist.all_gather_object(handles, (mine, err), group=pg)
+        self._agree([e for _, e in handles])
+        cols = [[], [], []]
+        try:
+            with torch.cuda.device(self.device):
+                for p, (hs_, _) in enumerate(handles):
+                    for k in range(3):
+                        if p == self.rank:
+                            cols[k].append(bufs[k].value)
+                            continue
+                        q = VP()
+                        check(xf["open"](hs_[k], ctypes.byref(q)), f"hipIpcOpenMemHandle (rank {p})")
+                        self._opened.append(q)
+                        cols[k].append(q.value)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {e}"
+        errs = [None] * self.world
+        dist.all_gather_object(errs, err, group=pg)
+        self._agree(errs)
+        self.bufs, self.reds, self.flags = ((VP * self.world)(*c) for c in cols)
+        self.ep = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.done = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        dist.barrier(group=pg)  # every rank's buffers exist (zeroed) before any flag can be stored
+
+    def _agree(self, errs) -> None:
+        bad = [e for e in errs if e]
+        if bad:
+            self.close()
+            raise RuntimeError("TP IPC all-reduce setup failed: " + "; ".join(bad))
+
+    def close(self) -> None:
+        xf = _xg_fns()
+        for p in self._opened:
+            xf["close"](p)
+        self._opened = []
+        for p in self._own:
+            xf["free"](p)
+        self._own = []
+
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum of `x` over the ranks (bf16, any shape, numel % 4 == 0, <= max_elems) into `out` (default: a new
+        tensor; `out=x` reduces in place). Stream-ordered and graph-capturable."""
+        if x.dtype != torch.bfloat16 or x.device != self.device:
+            raise ValueError("IPC all-reduce takes bf16 tensors on the group's device")
+        x = x.contiguous()
+        n = x.numel()
+        if n % 4 or n > self.npad:
+            raise ValueError(f"{n} elements: need a multiple of 4 and <= {self.npad}")
+        y = torch.empty_like(x) if out is None else out
+        check(_fns()["ar"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank, self.npad,
+                           ptr(self.ep), ptr(self.done), ptr(self.err), stream_handle(self.device)),
+              "mifx_tpar_allreduce")
+        return y
+
+    def check(self) -> None:
+        if int(self.err.item()) != 0:
+            raise RuntimeError("TP IPC all-reduce: a peer never published (wait timed out); results since are invalid")

@@ -63,19 +63,28 @@ class BertTrainer:
     per-parameter accumulate kernels."""
 
     def __init__(self, cfg: BertConfig, batch: int, seq: int, device, tp: TPGroup | None = None, lr: float = 2e-5,
-                 graph: bool | None = None, flat_adamw: bool | None = None, sdpa: str | None = None):
+                 graph: bool | None = None, flat_adamw: bool | None = None, sdpa: str | None = None,
+                 tp_ipc: bool | None = None):
+        """tp_ipc (TP > 1 on the GPU; default on, MIFX_TP_IPC=0 turns it off): the TP all-reduces run on the
+        peer-memory kernels of mifx.parallel.tp_ipc, so the TP step is captured into a hipGraph like the TP=1
+        step (otherwise they are torch.distributed collectives and TP > 1 steps eagerly)."""
         self.cfg, self.batch, self.seq, self.device = cfg, batch, seq, torch.device(device)
         self.tp = tp or TPGroup(None)
         self.model = BertForSequenceClassification(cfg, self.tp, seed=0).to(self.device)
         cuda = self.device.type == "cuda"
+        if tp_ipc is None:
+            tp_ipc = os.environ.get("MIFX_TP_IPC", "1") != "0"
+        if cuda and self.tp.size > 1 and tp_ipc:
+            self.tp.enable_ipc(batch * seq * cfg.hidden, self.device)
         # The whole step is captured once as a hipGraph and replayed by default on the GPU (9.2 ms/step vs
         # 12.8 ms eager: the eager step is host-bound). The embeddings use a scatter-add backward
         # (mifx.ops.fused_bert.embedding): PyTorch's sort/unique embedding backward faults under hipGraph
         # replay on ROCm (rocPRIM partition kernel, diagnosed in round 1) and made the captured step go
         # non-finite after ~10 replays.
-        # (default only at TP=1: capturing the TP all-reduces into the graph is not yet validated on a
-        # multi-GPU node, so TP>1 steps eagerly unless graph=True is passed)
-        self.use_graph = (cuda and self.tp.size == 1) if graph is None else (graph and cuda)
+        # At TP > 1 the step is captured when the all-reduces are the peer-memory kernels (tp_ipc); over
+        # torch.distributed collectives it steps eagerly unless graph=True is passed.
+        self.use_graph = (cuda and (self.tp.size == 1 or self.tp.ipc is not None)) if graph is None \
+            else (graph and cuda)
         self.flat = cuda if flat_adamw is None else (flat_adamw and cuda)
         if self.flat:  # bf16 weights/grads as flat-buffer views + fp32 master, one fused HIP update
             self.opt = FlatAdamW(self.model.parameters(), lr=lr, weight_decay=0.01)

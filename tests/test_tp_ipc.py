@@ -1,0 +1,134 @@
+"""Tensor-parallel all-reduce over peer memory (csrc/tp_allreduce.hip, mifx.parallel.tp_ipc): ranks share cuda:0
+over gloo in these tests (the IPC mapping path is the one used across GPUs). The sum must equal the rank-order
+fp32 sum rounded once to bf16, identically on every rank, through repeated epochs, in place, and replayed from a
+captured hipGraph; a BERT TP step captured into a graph must be bit-identical to the same step run eagerly."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ar_worker(rank, world, port, out):
+    from mifx.parallel.tp_ipc import IpcAllReduce
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        ar = IpcAllReduce(dist.group.WORLD, dev, 1 << 20)
+        res = {}
+        for i, n in enumerate((4, 4096 * 3 + 8, 1 << 20, 100000)):
+            g = torch.Generator().manual_seed(1000 * i + rank)
+            x = (torch.randn(n, generator=g) * (rank + 1)).to(torch.bfloat16).to(dev)
+            res[f"y{i}"] = ar.all_reduce(x).cpu()
+            res[f"x{i}"] = x.cpu()
+        x = torch.full((8192,), float(rank + 1), dtype=torch.bfloat16, device=dev)
+        ar.all_reduce(x, out=x)  # in place
+        res["inplace"] = x.cpu()
+        # captured: three all-reduces in one graph, replayed
+        a = torch.zeros(65536, dtype=torch.bfloat16, device=dev)
+        b = torch.zeros(65536, dtype=torch.bfloat16, device=dev)
+        ya = torch.empty_like(a)
+        yb = torch.empty_like(b)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.synchronize(dev)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            ar.all_reduce(a, out=ya)
+            ar.all_reduce(b, out=yb)
+            ar.all_reduce(ya, out=ya)
+        outs = []
+        for k in range(5):
+            a.fill_(float(rank + k))
+            b.fill_(float(2 * rank - k))
+            gr.replay()
+            torch.cuda.synchronize(dev)
+            outs.append((ya[:4].cpu().clone(), yb[:4].cpu().clone()))
+        res["graph"] = outs
+        ar.check()
+        res["err"] = int(ar.err.item())
+        dist.barrier()
+        ar.close()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_allreduce_exact_rank_order_sum(world):
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "ar")
+        mp.start_processes(_ar_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for i in range(4):
+        want = res[0][f"x{i}"].float()
+        for r in range(1, world):
+            want = want + res[r][f"x{i}"].float()
+        want = want.to(torch.bfloat16)
+        for r in range(world):
+            assert torch.equal(res[r][f"y{i}"], want), (i, r)
+    tri = sum(range(1, world + 1))
+    for r in range(world):
+        assert torch.equal(res[r]["inplace"], torch.full((8192,), float(tri), dtype=torch.bfloat16))
+        assert res[r]["err"] == 0
+        for k, (ya, yb) in enumerate(res[r]["graph"]):
+            sa = sum(float(q + k) for q in range(world))
+            sb = sum(float(2 * q - k) for q in range(world))
+            assert torch.equal(ya, torch.full((4,), world * sa, dtype=torch.bfloat16)), (r, k)
+            assert torch.equal(yb, torch.full((4,), sb, dtype=torch.bfloat16)), (r, k)
+
+
+def _bert_worker(rank, world, port, out):
+    from mifx.models.bert import BertConfig
+    from mifx.parallel.tensor_parallel import TPGroup
+    from mifx.trainer.bert_trainer import BertTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        res = {}
+        for graph in (False, True):
+            tp = TPGroup()
+            torch.manual_seed(0)
+            tr = BertTrainer(BertConfig(layers=2, dropout=0.1), 4, 128, dev, tp, graph=graph, tp_ipc=True)
+            assert tp.ipc is not None and tr.use_graph == graph
+            losses = [float(tr.step()) for _ in range(6)]
+            torch.cuda.synchronize(dev)
+            tp.check()
+            res[graph] = (losses, {n: p.detach().float().cpu() for n, p in tr.model.named_parameters()})
+            dist.barrier()
+            tp.disable_ipc()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bert_tp_step_captured_with_ipc_allreduce_bit_identical_to_eager(world):
+    """BertTrainer at TP=world with the peer-memory all-reduces: the step captured into one hipGraph (the TP>1
+    default now) and the same step run eagerly give bit-identical losses and weights."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "bt")
+        mp.start_processes(_bert_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for r in range(world):
+        (le, pe), (lg, pg) = res[r][False], res[r][True]
+        assert all(torch.isfinite(torch.tensor(le)))
+        assert le == lg, (r, le, lg)
+        for n in pe:
+            assert torch.equal(pe[n], pg[n]), (r, n)
+    assert res[0][True][0] == res[1][True][0]  # every TP rank reports the same loss
