@@ -44,7 +44,12 @@ def main(iters: int = 50) -> dict:
     if torch.cuda.is_available():
         xg = x.cuda()
         sync = torch.cuda.synchronize
-        out["gpu_fp32_ms"] = _time(lambda: xg @ xg, iters, sync)
+        out["gpu_fp32_ms"] = _time(lambda: xg @ xg, iters, sync)  # hipBLASLt
+        from mifx.ops.gemm import matmul_f32  # the same fp32 op on the hand-written MFMA kernel (edge tiles)
+
+        out["gpu_fp32_hip_ms"] = _time(lambda: matmul_f32(xg, xg), iters, sync)
+        out["gpu_fp32_hip_max_abs_err"] = float((matmul_f32(xg, xg) - (x.double() @ x.double()).float().cuda())
+                                                .abs().max())
         xb = xg.bfloat16()
         out["gpu_bf16_ms"] = _time(lambda: xb @ xb, iters, sync)
         out["gpu_bf16_tflops"] = 2e9 / (out["gpu_bf16_ms"] * 1e-3) / 1e12

@@ -354,3 +354,27 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int | None = None, splits: in
 def tn_eligible(a2: torch.Tensor, b2: torch.Tensor) -> bool:
     return (a2.is_cuda and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.dim() == 2
             and b2.dim() == 2 and pick_tn(a2.shape[1], b2.shape[1], a2.shape[0]) is not None)
+
+
+# ---------------------------------------------------------------- exact fp32 GEMM with edge tiles (csrc/gemm_f32.hip)
+@functools.lru_cache(maxsize=None)
+def _f32_fns():
+    lib = _lib.load("gemm_f32")
+    return {"nn": sig(lib, "mifx_gemm_f32_nn", [VP, VP, VP, I32, I32, I32, I32, I32, I32, VP])}
+
+
+def matmul_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [M, K] @ b [K, N] in fp32 on the f32 matrix cores (exact fp32 products and accumulation), any shape:
+    ragged edges are zero-filled in the kernel's tile loads. The KN18 anchor (the reference's 1000 x 1000 eager
+    matmul) on a hand-written kernel; CPU tensors take torch.matmul."""
+    if not a.is_cuda:
+        return a @ b
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[0] or a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise ValueError("matmul_f32 takes fp32 [M, K] and [K, N] CUDA tensors")
+    a, b = a.contiguous(), b.contiguous()
+    M, K = a.shape
+    N = b.shape[1]
+    c = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    native_stats.count("gemm_f32", True)
+    check(_f32_fns()["nn"](ptr(a), ptr(b), ptr(c), M, N, K, K, N, N, stream_handle(a.device)), "mifx_gemm_f32_nn")
+    return c
