@@ -32,7 +32,7 @@ HIP_FLAGS = [
     "-Wno-unused-result",
     "-Wno-unused-value",
 ]
-CXX_FLAGS = ["-O3", "-shared", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
+CXX_FLAGS = ["-O3", "-shared", "-fPIC", "-std=c++17", "-pthread", "-Wall", "-Wno-unused-function"]
 
 
 def hipcc() -> str:

@@ -51,7 +51,8 @@ def test_xgb_regressor_early_stopping():
     y = 3 * X[:, 0] + np.sin(X[:, 1]) + r.normal(0, 0.3, 800)
     m = XGBRegressor(n_estimators=500, learning_rate=0.1).fit(X[:600], y[:600], eval_set=[(X[600:], y[600:])],
                                                               early_stopping_rounds=10)
-    assert m.best_iteration + 1 == m.n_trees_ < 500
+    # XGBoost semantics: training stops early_stopping_rounds after the best round; predict uses the best round
+    assert m.best_iteration + 1 + 10 == m.n_trees_ < 500
     rmse = float(np.sqrt(np.mean((m.predict(X[600:]) - y[600:]) ** 2)))
     assert rmse == pytest.approx(m.best_score, rel=1e-9) and rmse < 0.6
     assert len(m.evals_result_["validation_0"]["rmse"]) > m.best_iteration
@@ -63,6 +64,79 @@ def test_xgb_classifier():
     y = (X[:, 0] + X[:, 1] > 0).astype(int)
     m = XGBClassifier(n_estimators=50, learning_rate=0.3).fit(X[:400], y[:400], eval_set=[(X[400:], y[400:])])
     assert (m.predict(X[400:]) == y[400:]).mean() > 0.85 and m.predict_proba(X[:3]).shape == (3, 2)
+
+
+def _ref_tree(X, g, h, depth, lam, mcw, eta):
+    """Brute-force second-order tree (every distinct value as a cut, missing rows tried on both sides) -- the
+    oracle for csrc/gbdt.cpp on data with at most max_bins distinct values per feature."""
+    def leaf(idx):
+        return ("leaf", -eta * g[idx].sum() / (h[idx].sum() + lam))
+
+    def grow(idx, d):
+        if d == depth or len(idx) < 2:
+            return leaf(idx)
+        G, H = g[idx].sum(), h[idx].sum()
+        best = (1e-6, None)
+        for j in range(X.shape[1]):
+            col = X[idx, j]
+            miss = np.isnan(col)
+            for c in np.unique(col[~miss])[1:]:
+                lm = (~miss) & (col < c)
+                for ml in (False, True):
+                    L = lm | (miss & ml)
+                    GL, HL = g[idx][L].sum(), h[idx][L].sum()
+                    GR, HR = G - GL, H - HL
+                    if HL < mcw or HR < mcw:
+                        continue
+                    gain = 0.5 * (GL ** 2 / (HL + lam) + GR ** 2 / (HR + lam) - G ** 2 / (H + lam))
+                    if gain > best[0] + 1e-9:
+                        best = (gain, (j, c, ml, L))
+        if best[1] is None:
+            return leaf(idx)
+        j, c, ml, L = best[1]
+        return ("split", j, c, ml, grow(idx[L], d + 1), grow(idx[~L], d + 1))
+
+    return grow(np.arange(len(g)), 0)
+
+
+def _ref_predict(t, x):
+    while t[0] == "split":
+        _, j, c, ml, lt, rt = t
+        t = lt if (ml if np.isnan(x[j]) else x[j] < c) else rt
+    return t[1]
+
+
+def test_gbdt_native_matches_bruteforce_learner():
+    """csrc/gbdt.cpp vs an exhaustive Python learner: same trees (hence predictions) for squared error on data with
+    missing values, when every distinct value is its own bin."""
+    r = np.random.default_rng(3)
+    X = np.round(r.normal(size=(300, 4)), 1)  # few distinct values -> one bin each
+    X[r.random(X.shape) < 0.1] = np.nan
+    y = 2 * np.nan_to_num(X[:, 0]) - np.nan_to_num(X[:, 2]) ** 2 + r.normal(0, 0.1, 300)
+    m = XGBRegressor(n_estimators=3, learning_rate=0.5, max_depth=3, max_bins=256, min_child_weight=1.0).fit(X, y)
+    margin = np.full(len(y), y.mean())
+    trees = []
+    for _ in range(3):
+        t = _ref_tree(X, margin - y, np.ones(len(y)), 3, 1.0, 1.0, 0.5)
+        trees.append(t)
+        margin = margin + np.array([_ref_predict(t, x) for x in X])
+    Xt = np.round(r.normal(size=(50, 4)), 1)
+    Xt[r.random(Xt.shape) < 0.1] = np.nan
+    want = y.mean() + np.array([sum(_ref_predict(t, x) for t in trees) for x in Xt])
+    np.testing.assert_allclose(m.predict(Xt), want, rtol=1e-6, atol=1e-6)  # (float32 gradients)
+    np.testing.assert_allclose(m.predict(X), margin, rtol=1e-6, atol=1e-6)  # (float32 gradients)
+
+
+def test_gbdt_deterministic_across_threads_and_binned():
+    r = np.random.default_rng(5)
+    X = r.normal(size=(30000, 12))
+    y = X[:, 0] * X[:, 1] + np.abs(X[:, 2]) + r.normal(0, 0.1, 30000)
+    a = XGBRegressor(n_estimators=20, max_bins=64, n_jobs=1).fit(X, y)
+    b = XGBRegressor(n_estimators=20, max_bins=64, n_jobs=8).fit(X, y)
+    assert np.array_equal(a.predict(X[:1000]), b.predict(X[:1000]))  # bit-identical for any thread count
+    assert all(len(c) <= 63 for c in a._cuts)  # quantile thinning to max_bins bins
+    rmse = float(np.sqrt(np.mean((a.predict(X) - y) ** 2)))
+    assert rmse < 0.35 * y.std()
 
 
 def _square_sum(n):
