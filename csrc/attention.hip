@@ -3,7 +3,7 @@
 // backends are Triton-generated (AOTriton attn_fwd / bwd_kernel_fuse: 0.96 ms of a 7.4 ms BERT-base step,
 // profiles/bert_base_steady_kernels_s3b.md).
 //
-// One workgroup per (batch, local head): the whole S x S problem of a BERT sequence (S = 64 or 128, head dim 64)
+// S = 64 / 128: one workgroup per (batch, local head): the whole S x S problem of a BERT sequence (head dim 64)
 // lives in one CU. S/16 waves, wave w owns queries 16w .. 16w+15 and works in the TRANSPOSED orientation so the
 // MFMA outputs chain (same idiom as csrc/wd_chain.hip):
 //  * S^T = K Q^T (16x16x32 bf16 MFMA, K rows from LDS, Q^T fragments = the wave's own query rows): lane = query,
@@ -16,7 +16,8 @@
 //    needed K / V images: 74 KB per workgroup, two workgroups per CU) and each wave then owns 16 keys for
 //    dV^T = dO^T P_d and dK^T = Q^T dS, reading both operands with transposed LDS reads.
 // qkv is the fused projection output [B, S, 3, H, 64] (this rank's H heads), out / dout are [B, S, H, 64]; no
-// transposes around the kernels. Dropout element (b, global head, i, j) uses the flat index
+// transposes around the kernels. Longer sequences (S % 64 == 0, <= 512) take the chunked kernels described further
+// down. Dropout element (b, global head, i, j) uses the flat index
 // ((b Htot + h0 + h) S + i) S + j into the counter-based mask of csrc/counter_rng.h, so the mask does not depend
 // on how heads are split over tensor-parallel ranks.
 #include <hip/hip_runtime.h>
@@ -312,6 +313,280 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
   }
 }
 
+// ---- sequences of 192 .. 512 tokens (S % 64 == 0) -------------------------------------------------------------
+// The whole S x S problem no longer fits one CU's registers and LDS, so the long kernels tile it flash-style while
+// keeping the chained MFMA orientation of the S <= 128 kernels:
+//  * forward: a workgroup owns 128 queries of one (batch, head) (8 waves x 16), the head's K and V rows resident in
+//    LDS (S x 144 B each: 147 KB at S = 512); keys stream in chunks of 64 with an online softmax (running max and
+//    row sum per query lane, the O^T accumulators rescaled per chunk), the dropout mask drawn per chunk.
+//  * backward, dQ: the same partition; with the forward's logsumexp the probabilities of a key chunk need nothing
+//    from other chunks, so dS^T is formed chunk by chunk and dQ^T = K^T dS^T accumulates in registers. It also
+//    writes D_i = rowsum(dO o O) for the second kernel.
+//  * backward, dK / dV: a workgroup owns 128 keys (wave = 16 keys), Q and dO resident; query chunks of 64 give
+//    S = Q K^T and dP_d = dO V^T in the [query][key] orientation, so P_d and dS chain straight into
+//    dV^T = dO^T P_d and dK^T = Q^T dS with dO / Q read transposed -- the forward's structure with the roles of
+//    queries and keys exchanged. The lane holds 4 query rows of one key column; the dropout bits come from one
+//    mask draw per lane (row 4h + lane % 4, its quad's 4 keys) exchanged within the quad.
+constexpr int LQB = 128, LNT = 512, LKC = 64, LMAXS = 512;
+
+constexpr int long_lds(int S) { return 2 * S * LD * 2; }
+
+// the query (key) blocks of one head are consecutive logical blocks: keep them on one XCD (dispatch round-robins
+// consecutive workgroups over the 8 XCDs), so the head's K / V (Q / dO) rows are fetched into one L2
+__device__ __forceinline__ int xcd_block(int bid, int nwg) { return (nwg & 7) ? bid : (bid & 7) * (nwg >> 3) + (bid >> 3); }
+
+__device__ __forceinline__ void load_rows_n(bf16* dst, const bf16* src, size_t row_stride, int rows) {
+#pragma unroll 4
+  for (int c = threadIdx.x; c < rows * 8; c += LNT) {
+    const int row = c >> 3, ch = c & 7;
+    *(uint4*)(dst + row * LD + ch * 8) = *(const uint4*)(src + (size_t)row * row_stride + ch * 8);
+  }
+}
+
+__global__ __launch_bounds__(LNT) void attn_fwd_long(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
+                                                     int S, float scale, Drop dp, int H, int h0, int Htot,
+                                                     bf16* __restrict__ out, float* __restrict__ lse_out) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  bf16* Ks = smem;
+  bf16* Vs = smem + S * LD;
+  const int nqb = (S + LQB - 1) / LQB, lb = xcd_block(blockIdx.x, gridDim.x);
+  const int qb = lb % nqb, bh = lb / nqb, b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+  const size_t tok = (size_t)3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * tok;
+  load_rows_n(Ks, base + (size_t)(H + hh) * D, tok, S);
+  load_rows_n(Vs, base + (size_t)(2 * H + hh) * D, tok, S);
+  const bool live = qb * LQB + 16 * w < S;
+  const int qi = qb * LQB + 16 * w + r;
+  v8bf qf[2];
+  if (live)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = ld8(base + (size_t)qi * tok + (size_t)hh * D + 32 * ks + 8 * h);
+  __syncthreads();
+  if (!live) return;  // no barrier follows
+
+  const float* kb = kbias ? kbias + (size_t)b * S : nullptr;
+  const uint64_t key = dp.thr ? mifx_rng::drop_key(dp.rng, dp.site) : 0;
+  const uint64_t row_base = (((uint64_t)b * Htot + h0 + hh) * S + qi) * S;
+  float m = -3.0e38f, l = 0.f;
+  v4f o[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) o[dt] = kZero4;
+  for (int c = 0; c < S; c += LKC) {
+    v4f s[LKC / 16];
+    float mc = m;
+#pragma unroll
+    for (int kt = 0; kt < LKC / 16; ++kt) {
+      v4f a = kZero4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Ks + (c + 16 * kt + r) * LD + 32 * ks + 8 * h), qf[ks], a);
+      const float4 bb = kb ? *(const float4*)(kb + c + 16 * kt + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[0] = a[0] * scale + bb.x;
+      a[1] = a[1] * scale + bb.y;
+      a[2] = a[2] * scale + bb.z;
+      a[3] = a[3] * scale + bb.w;
+      mc = fmaxf(mc, fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])));
+      s[kt] = a;
+    }
+    mc = fmaxf(mc, __shfl_xor(mc, 16));
+    mc = fmaxf(mc, __shfl_xor(mc, 32));
+    const float alpha = __expf(m - mc);
+    m = mc;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < LKC / 16; ++kt) {
+      const uint32_t kbits = dp.thr ? mifx_rng::keep4(key, (row_base + c + 16 * kt + 4 * h) >> 2, dp.thr) : 0xf;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pe = __expf(s[kt][e] - m);
+        l += pe;
+        s[kt][e] = (kbits >> e) & 1 ? pe : 0.f;
+      }
+    }
+    const v8bf pb[2] = {pack8(s[0], s[1]), pack8(s[2], s[3])};
+    // O^T += V^T P^T over this chunk (V rows read transposed at the chained key order)
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16* pa = Vs + (c + 32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
+        o[dt] = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), pb[ks], o[dt]);
+      }
+  }
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  const float inv = (dp.thr ? dp.scale : 1.f) / l;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+    *(v4bf*)(out + ((size_t)b * S + qi) * H * D + (size_t)hh * D + 16 * dt + 4 * h) = pack4(o[dt] * inv);
+  if (h == 0) lse_out[(size_t)bh * S + qi] = m + __logf(l);
+}
+
+__global__ __launch_bounds__(LNT) void attn_bwd_dq_long(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
+                                                        const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                                        const float* __restrict__ lse, int S, float scale, Drop dp,
+                                                        int H, int h0, int Htot, bf16* __restrict__ dqkv,
+                                                        float* __restrict__ dsum) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  bf16* Ks = smem;
+  bf16* Vs = smem + S * LD;
+  const int nqb = (S + LQB - 1) / LQB, lb = xcd_block(blockIdx.x, gridDim.x);
+  const int qb = lb % nqb, bh = lb / nqb, b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+  const size_t tok = (size_t)3 * H * D, otok = (size_t)H * D;
+  const bf16* base = qkv + (size_t)b * S * tok;
+  load_rows_n(Ks, base + (size_t)(H + hh) * D, tok, S);
+  load_rows_n(Vs, base + (size_t)(2 * H + hh) * D, tok, S);
+  const bool live = qb * LQB + 16 * w < S;
+  const int qi = qb * LQB + 16 * w + r;
+  v8bf qf[2], dof[2];
+  float di = 0.f, lq = 0.f;
+  if (live) {
+    const bf16* pdo = dout + ((size_t)b * S + qi) * otok + (size_t)hh * D;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[ks] = ld8(base + (size_t)qi * tok + (size_t)hh * D + 32 * ks + 8 * h);
+      dof[ks] = ld8(pdo + 32 * ks + 8 * h);
+    }
+    const bf16* po = o + ((size_t)b * S + qi) * otok + (size_t)hh * D + 16 * h;
+    const v8bf o0 = ld8(po), o1 = ld8(po + 8), d0 = ld8(pdo + 16 * h), d1 = ld8(pdo + 16 * h + 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) di += (float)o0[e] * (float)d0[e] + (float)o1[e] * (float)d1[e];
+    di += __shfl_xor(di, 16);
+    di += __shfl_xor(di, 32);
+    if (h == 0) dsum[(size_t)bh * S + qi] = di;
+    lq = lse[(size_t)bh * S + qi];
+  }
+  __syncthreads();
+  if (!live) return;
+
+  const float* kb = kbias ? kbias + (size_t)b * S : nullptr;
+  const uint64_t key = dp.thr ? mifx_rng::drop_key(dp.rng, dp.site) : 0;
+  const uint64_t row_base = (((uint64_t)b * Htot + h0 + hh) * S + qi) * S;
+  const float dsc = dp.thr ? dp.scale : 1.f;
+  v4f dq[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) dq[dt] = kZero4;
+  for (int c = 0; c < S; c += LKC) {
+    v4f ds[LKC / 16];
+#pragma unroll
+    for (int kt = 0; kt < LKC / 16; ++kt) {
+      v4f sc = kZero4, dpd = kZero4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        sc = mfma(ld8(Ks + (c + 16 * kt + r) * LD + 32 * ks + 8 * h), qf[ks], sc);
+        dpd = mfma(ld8(Vs + (c + 16 * kt + r) * LD + 32 * ks + 8 * h), dof[ks], dpd);
+      }
+      const float4 bb = kb ? *(const float4*)(kb + c + 16 * kt + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      const uint32_t kbits = dp.thr ? mifx_rng::keep4(key, (row_base + c + 16 * kt + 4 * h) >> 2, dp.thr) : 0xf;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pe = __expf(sc[e] * scale + bv[e] - lq);
+        const float dpv = (kbits >> e) & 1 ? dpd[e] * dsc : 0.f;
+        ds[kt][e] = pe * (dpv - di) * scale;
+      }
+    }
+    const v8bf dsb[2] = {pack8(ds[0], ds[1]), pack8(ds[2], ds[3])};
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16* pa = Ks + (c + 32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
+        dq[dt] = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), dsb[ks], dq[dt]);
+      }
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+    *(v4bf*)(dqkv + ((size_t)b * S + qi) * tok + (size_t)hh * D + 16 * dt + 4 * h) = pack4(dq[dt]);
+}
+
+__global__ __launch_bounds__(LNT) void attn_bwd_dkv_long(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
+                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                         const float* __restrict__ dsum, int S, float scale, Drop dp,
+                                                         int H, int h0, int Htot, bf16* __restrict__ dqkv) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  bf16* Qs = smem;
+  bf16* dOs = smem + S * LD;
+  const int nkb = (S + LQB - 1) / LQB, lb = xcd_block(blockIdx.x, gridDim.x);
+  const int kb_ = lb % nkb, bh = lb / nkb, b = bh / H, hh = bh % H;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+  const size_t tok = (size_t)3 * H * D, otok = (size_t)H * D;
+  const bf16* base = qkv + (size_t)b * S * tok;
+  load_rows_n(Qs, base + (size_t)hh * D, tok, S);
+  load_rows_n(dOs, dout + (size_t)b * S * otok + (size_t)hh * D, otok, S);
+  const bool live = kb_ * LQB + 16 * w < S;
+  const int kj = kb_ * LQB + 16 * w + r;
+  v8bf kf[2], vf[2];
+  float bj = 0.f;
+  if (live) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = ld8(base + (size_t)kj * tok + (size_t)(H + hh) * D + 32 * ks + 8 * h);
+      vf[ks] = ld8(base + (size_t)kj * tok + (size_t)(2 * H + hh) * D + 32 * ks + 8 * h);
+    }
+    if (kbias) bj = kbias[(size_t)b * S + kj];
+  }
+  __syncthreads();
+  if (!live) return;
+
+  const float* lq = lse + (size_t)bh * S;
+  const float* dd = dsum + (size_t)bh * S;
+  const uint64_t key = dp.thr ? mifx_rng::drop_key(dp.rng, dp.site) : 0;
+  const uint64_t mrow = ((uint64_t)b * Htot + h0 + hh) * S;
+  const float dsc = dp.thr ? dp.scale : 1.f;
+  v4f dk[D / 16], dv[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) dk[dt] = dv[dt] = kZero4;
+  for (int c = 0; c < S; c += LKC) {
+    v4f pd[LKC / 16], ds[LKC / 16];
+#pragma unroll
+    for (int it = 0; it < LKC / 16; ++it) {
+      // lane: S[i][j], i = c + 16 it + 4h + e, j = kj
+      v4f sc = kZero4, dpd = kZero4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        sc = mfma(ld8(Qs + (c + 16 * it + r) * LD + 32 * ks + 8 * h), kf[ks], sc);
+        dpd = mfma(ld8(dOs + (c + 16 * it + r) * LD + 32 * ks + 8 * h), vf[ks], dpd);
+      }
+      const int i0 = c + 16 * it + 4 * h;
+      const float4 L = *(const float4*)(lq + i0);
+      const float4 Dq = *(const float4*)(dd + i0);
+      const float lv[4] = {L.x, L.y, L.z, L.w}, dv4[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
+      uint32_t nib = 0xf;
+      if (dp.thr) nib = mifx_rng::keep4(key, ((mrow + i0 + p) * S + (kj & ~3)) >> 2, dp.thr);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool kept = dp.thr ? ((__shfl(nib, (lane & ~3) | e) >> p) & 1) : true;
+        const float pe = __expf(sc[e] * scale + bj - lv[e]);
+        pd[it][e] = kept ? pe * dsc : 0.f;
+        ds[it][e] = pe * ((kept ? dpd[e] * dsc : 0.f) - dv4[e]) * scale;
+      }
+    }
+    const v8bf pdb[2] = {pack8(pd[0], pd[1]), pack8(pd[2], pd[3])};
+    const v8bf dsb[2] = {pack8(ds[0], ds[1]), pack8(ds[2], ds[3])};
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16* pa = dOs + (c + 32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
+        dv[dt] = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), pdb[ks], dv[dt]);
+        const bf16* pq = Qs + (c + 32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
+        dk[dt] = mfma(cat8(tr_read(pq), tr_read(pq + 16 * LD)), dsb[ks], dk[dt]);
+      }
+  }
+  bf16* dst = dqkv + ((size_t)b * S + kj) * tok;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    *(v4bf*)(dst + (size_t)(H + hh) * D + 16 * dt + 4 * h) = pack4(dk[dt]);
+    *(v4bf*)(dst + (size_t)(2 * H + hh) * D + 16 * dt + 4 * h) = pack4(dv[dt]);
+  }
+}
+
+bool long_seq(int S) { return S > 128 && S <= LMAXS && S % LKC == 0; }
+
 uint32_t drop_threshold(float p) {
   if (!(p > 0.f)) return 0;
   const float t = p * 65536.f + 0.5f;
@@ -333,11 +608,21 @@ extern "C" {
 // h0 / Htot: this rank's first global head and the model's head count (dropout indexing only).
 int mifx_attn_fwd(const void* qkv, const float* kbias, int B, int S, int H, int h0, int Htot, float scale, float p,
                   const int64_t* rng, int site, void* out, float* lse, hipStream_t st) {
-  if (B <= 0 || H <= 0 || (S != 64 && S != 128) || p < 0.f || p >= 1.f || (p > 0.f && rng == nullptr)) return -1;
+  if (B <= 0 || H <= 0 || (S != 64 && S != 128 && !long_seq(S)) || p < 0.f || p >= 1.f || (p > 0.f && rng == nullptr))
+    return -1;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)kbias) % 16 != 0) return -1;
   const Drop dp{rng, site, drop_threshold(p), 1.f / (1.f - p)};
   const dim3 grid(B * H);
-  if (S == 128)
+  if (long_seq(S)) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)attn_fwd_long, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                long_lds(LMAXS));
+      attr = true;
+    }
+    hipLaunchKernelGGL(attn_fwd_long, dim3(B * H * ((S + LQB - 1) / LQB)), dim3(LNT), long_lds(S), st,
+                       (const bf16*)qkv, kbias, S, scale, dp, H, h0, Htot, (bf16*)out, lse);
+  } else if (S == 128)
     hipLaunchKernelGGL(attn_fwd<128>, grid, dim3(512), 0, st, (const bf16*)qkv, kbias, scale, dp, H, h0, Htot,
                        (bf16*)out, lse);
   else
@@ -346,11 +631,13 @@ int mifx_attn_fwd(const void* qkv, const float* kbias, int B, int S, int H, int 
   return (int)hipGetLastError();
 }
 
-// dqkv [B, S, 3, H, 64] bf16 (every element written)
+// dqkv [B, S, 3, H, 64] bf16 (every element written); dsum: fp32 [B, H, S] workspace for S > 128 (else unused)
 int mifx_attn_bwd(const void* qkv, const float* kbias, const void* out, const void* dout, const float* lse, int B,
                   int S, int H, int h0, int Htot, float scale, float p, const int64_t* rng, int site, void* dqkv,
-                  hipStream_t st) {
-  if (B <= 0 || H <= 0 || (S != 64 && S != 128) || p < 0.f || p >= 1.f || (p > 0.f && rng == nullptr)) return -1;
+                  float* dsum, hipStream_t st) {
+  if (B <= 0 || H <= 0 || (S != 64 && S != 128 && !long_seq(S)) || p < 0.f || p >= 1.f || (p > 0.f && rng == nullptr))
+    return -1;
+  if (long_seq(S) && dsum == nullptr) return -1;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)dout | (uintptr_t)dqkv | (uintptr_t)kbias) % 16 != 0) return -1;
   static bool attr = false;
   if (!attr) {
@@ -360,7 +647,21 @@ int mifx_attn_bwd(const void* qkv, const float* kbias, const void* out, const vo
   }
   const Drop dp{rng, site, drop_threshold(p), 1.f / (1.f - p)};
   const dim3 grid(B * H);
-  if (S == 128)
+  if (long_seq(S)) {
+    static bool lattr = false;
+    if (!lattr) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dq_long, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                long_lds(LMAXS));
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_long, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                long_lds(LMAXS));
+      lattr = true;
+    }
+    const dim3 lgrid(B * H * ((S + LQB - 1) / LQB));
+    hipLaunchKernelGGL(attn_bwd_dq_long, lgrid, dim3(LNT), long_lds(S), st, (const bf16*)qkv, kbias, (const bf16*)out,
+                       (const bf16*)dout, lse, S, scale, dp, H, h0, Htot, (bf16*)dqkv, dsum);
+    hipLaunchKernelGGL(attn_bwd_dkv_long, lgrid, dim3(LNT), long_lds(S), st, (const bf16*)qkv, kbias,
+                       (const bf16*)dout, lse, (const float*)dsum, S, scale, dp, H, h0, Htot, (bf16*)dqkv);
+  } else if (S == 128)
     hipLaunchKernelGGL(attn_bwd<128>, grid, dim3(512), bwd_lds<128>(), st, (const bf16*)qkv, kbias, (const bf16*)out,
                        (const bf16*)dout, lse, scale, dp, H, h0, Htot, (bf16*)dqkv);
   else

@@ -108,7 +108,12 @@ class BertLayer(nn.Module):
         slot_a = hg.GradSlot() if fold else None
         slot_f = hg.GradSlot() if fold else None
         if hip:
-            qkv = hg.linear(copy_to_tp(x, self.tp), self.qkv.weight, self.qkv.bias, slot=slot_a).view(B, S, 3, h, d)
+            # the projection computes in the weight dtype anyway (autocast's cast of x); casting before the TP copy
+            # makes its backward all-reduce a bf16 one (the peer-memory kernels: no host collective in the captured
+            # step) -- the first layer's input is the fp32 embedding LayerNorm output
+            cdt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else self.qkv.weight.dtype
+            xin = x if x.dtype == cdt or self.tp.size == 1 else x.to(cdt)
+            qkv = hg.linear(copy_to_tp(xin, self.tp), self.qkv.weight, self.qkv.bias, slot=slot_a).view(B, S, 3, h, d)
         else:
             qkv = self.qkv(x).view(B, S, 3, h, d)
         if c.fused_attention:

@@ -378,11 +378,17 @@ def _attn_fns():
     lib = _lib.load("attention")
     return {
         "fwd": sig(lib, "mifx_attn_fwd", [VP, VP, I32, I32, I32, I32, I32, F32, F32, VP, I32, VP, VP, VP]),
-        "bwd": sig(lib, "mifx_attn_bwd", [VP, VP, VP, VP, VP, I32, I32, I32, I32, I32, F32, F32, VP, I32, VP, VP]),
+        "bwd": sig(lib, "mifx_attn_bwd", [VP, VP, VP, VP, VP, I32, I32, I32, I32, I32, F32, F32, VP, I32, VP, VP,
+                                          VP]),
     }
 
 
-ATTN_SEQ = (64, 128)  # sequence lengths of the fused kernels (head dim 64)
+ATTN_SEQ = (64, 128)  # sequence lengths of the one-workgroup-per-head kernels (head dim 64)
+ATTN_MAX_SEQ = 512  # longer S (multiple of 64, up to this) run the chunked kernels of the same file
+
+
+def attn_native_seq(S: int) -> bool:
+    return S in ATTN_SEQ or (128 < S <= ATTN_MAX_SEQ and S % 64 == 0)
 
 
 class _Attention(torch.autograd.Function):
@@ -407,8 +413,9 @@ class _Attention(torch.autograd.Function):
         B, S, _, H, Dh = qkv.shape
         dout = dout.to(torch.bfloat16).contiguous()
         dqkv = torch.empty_like(qkv)
+        dsum = torch.empty(B, H, S, device=qkv.device, dtype=torch.float32) if S > 128 else None
         check(_attn_fns()["bwd"](ptr(qkv), ptr(kb), ptr(out), ptr(dout), ptr(lse), B, S, H, h0, htot, scale, p,
-                                 ptr(rng if p > 0 else None), site, ptr(dqkv), stream_handle(qkv.device)),
+                                 ptr(rng if p > 0 else None), site, ptr(dqkv), ptr(dsum), stream_handle(qkv.device)),
               "mifx_attn_bwd")
         return dqkv, None, None, None, None, None, None, None
 
@@ -434,13 +441,14 @@ def attention_reference(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, 
 def attention(qkv: torch.Tensor, kbias, scale: float, p: float = 0.0, rng=None, site: int = 0, h0: int = 0,
               htot: int | None = None) -> torch.Tensor:
     """Multi-head self-attention over the fused projection output qkv [B, S, 3, H, Dh] -> [B, S, H, Dh].
-    GPU (bf16, Dh 64, S 64 or 128): csrc/attention.hip fwd/bwd; elsewhere the reference composition (same mask)."""
+    GPU (bf16, Dh 64, S 64 / 128, or a multiple of 64 up to 512): csrc/attention.hip fwd/bwd; elsewhere the
+    reference composition (same mask)."""
     if p > 0 and rng is None:
         raise ValueError("attention dropout p > 0 needs an rng state tensor [seed, counter]")
     htot = qkv.shape[3] if htot is None else htot
     from . import native_stats
 
-    if (qkv.is_cuda and not _TORCH_OPS and qkv.shape[1] in ATTN_SEQ and qkv.shape[4] == 64
+    if (qkv.is_cuda and not _TORCH_OPS and attn_native_seq(qkv.shape[1]) and qkv.shape[4] == 64
             and qkv.dtype == torch.bfloat16):
         native_stats.count("attention", True)
         return _Attention.apply(qkv, kbias, scale, p, rng, site, h0, htot)

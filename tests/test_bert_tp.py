@@ -166,11 +166,13 @@ def test_counter_dropout_mask_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S,H", [(128, 12), (64, 5)])
+@pytest.mark.parametrize("S,H", [(128, 12), (64, 5), (192, 3), (256, 4), (384, 3), (512, 2)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_fused_attention_gpu(S, H, p):
     """csrc/attention.hip forward/backward against the fp32 PyTorch reference with the same key mask and the same
-    counter-based dropout mask (h0 / Htot: a TP shard of a larger head set)."""
+    counter-based dropout mask (h0 / Htot: a TP shard of a larger head set). S > 128: the chunked kernels (online
+    softmax forward, dQ and dK/dV backward passes; 192 leaves half of the last 128-query block idle)."""
+    from mifx.ops import native_stats
     from mifx.ops import fused_bert as fb
 
     torch.manual_seed(S + H)
@@ -181,7 +183,9 @@ def test_fused_attention_gpu(S, H, p):
     am[2, S // 2:] = 0
     kb = ((1.0 - am) * -1e30).contiguous()
     rng = torch.tensor([5, 17], dtype=torch.int64, device="cuda")
+    native_stats.reset()
     out = fb.attention(qkv, kb, Dh ** -0.5, p, rng, 3, h0, htot)
+    assert native_stats.snapshot()["attention"] == {"native": 1, "fallback": 0}  # the HIP kernel ran
     q32 = qkv.detach().float().requires_grad_()
     ref = fb.attention_reference(q32, kb, Dh ** -0.5, p, rng, 3, h0, htot)
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)

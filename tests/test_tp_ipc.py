@@ -106,7 +106,9 @@ def _bert_worker(rank, world, port, out):
             torch.manual_seed(0)
             tr = BertTrainer(BertConfig(layers=2, dropout=0.1), 4, 128, dev, tp, graph=graph, tp_ipc=True)
             assert tp.ipc is not None and tr.use_graph == graph
-            losses = [float(tr.step()) for _ in range(6)]
+            # the graph trainer's capture runs 3 eager warm-up steps first: the eager run takes 9 steps, so both
+            # end after 9 updates and eager steps 3..8 line up with replays 0..5
+            losses = [float(tr.step()) for _ in range(6 if graph else 9)]
             torch.cuda.synchronize(dev)
             tp.check()
             res[graph] = (losses, {n: p.detach().float().cpu() for n, p in tr.model.named_parameters()})
@@ -128,7 +130,7 @@ def test_bert_tp_step_captured_with_ipc_allreduce_bit_identical_to_eager(world):
     for r in range(world):
         (le, pe), (lg, pg) = res[r][False], res[r][True]
         assert all(torch.isfinite(torch.tensor(le)))
-        assert le == lg, (r, le, lg)
+        assert le[3:] == lg, (r, le, lg)
         for n in pe:
             assert torch.equal(pe[n], pg[n]), (r, n)
     assert res[0][True][0] == res[1][True][0]  # every TP rank reports the same loss
