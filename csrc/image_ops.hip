@@ -49,12 +49,14 @@ template <typename TOut>
 __global__ __launch_bounds__(kThreads) void crop_flip_norm(const uint8_t* __restrict__ src, const int* __restrict__ idx,
                                                           int Hin, int Win, int C, int Hout, int Wout, int train,
                                                           uint32_t seed_lo, uint32_t seed_hi, uint32_t step,
+                                                          const long long* __restrict__ step_dev,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ inv_std,
                                                           TOut* __restrict__ out) {
   const int b = blockIdx.z, y = blockIdx.y;
   int oy, ox, flip;
   if (train) {
+    if (step_dev) step = (uint32_t)step_dev[0];  // device step counter (captured hipGraph steps)
     const U4 r = philox(U4{(uint32_t)b, step, 0x1234u, 0u}, seed_lo, seed_hi);
     oy = (int)(r.x % (uint32_t)(Hin - Hout + 1));
     ox = (int)(r.y % (uint32_t)(Win - Wout + 1));
@@ -84,18 +86,20 @@ __global__ __launch_bounds__(kThreads) void crop_flip_norm(const uint8_t* __rest
 
 extern "C" {
 
-// src: [N, Hin, Win, C] uint8; idx: [B] int32 image ids; out: [B, Hout, Wout, C] (dtype 0 fp32, 1 bf16)
+// src: [N, Hin, Win, C] uint8; idx: [B] int32 image ids; out: [B, Hout, Wout, C] (dtype 0 fp32, 1 bf16).
+// step_dev (optional): device int64 read by the kernel in place of `step` (a graph replayed every step)
 int mifx_img_crop_flip_norm(const uint8_t* src, const int* idx, int B, int Hin, int Win, int C, int Hout, int Wout,
-                            int train, unsigned long long seed, unsigned int step, const float* mean,
+                            int train, unsigned long long seed, unsigned int step, const long long* step_dev,
+                            const float* mean,
                             const float* inv_std, int dtype, void* out, hipStream_t st) {
   if (B <= 0 || Hout > Hin || Wout > Win || C <= 0 || C > 4) return -1;
   const dim3 grid((Wout * C + kThreads * kVec - 1) / (kThreads * kVec), Hout, B);
   if (dtype)
     hipLaunchKernelGGL(crop_flip_norm<__hip_bfloat16>, grid, dim3(kThreads), 0, st, src, idx, Hin, Win, C, Hout, Wout,
-                       train, (uint32_t)seed, (uint32_t)(seed >> 32), step, mean, inv_std, (__hip_bfloat16*)out);
+                       train, (uint32_t)seed, (uint32_t)(seed >> 32), step, step_dev, mean, inv_std, (__hip_bfloat16*)out);
   else
     hipLaunchKernelGGL(crop_flip_norm<float>, grid, dim3(kThreads), 0, st, src, idx, Hin, Win, C, Hout, Wout, train,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), step, mean, inv_std, (float*)out);
+                       (uint32_t)seed, (uint32_t)(seed >> 32), step, step_dev, mean, inv_std, (float*)out);
   return (int)hipGetLastError();
 }
 

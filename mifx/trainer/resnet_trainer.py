@@ -3,10 +3,17 @@
 dataset with the fused crop/flip/normalize HIP kernel, bf16 autocast in channels_last
 (MIOpen NHWC MFMA convolutions), SGD + Nesterov momentum with linear warmup.
 
+On the GPU the step is captured into hipGraphs after `graph_warmup` eager steps (graph=True, the default there):
+graph A = gradient zeroing + every micro-batch's input kernel, forward and backward (the step counter, learning rate
+and sample indices are device tensors written before each replay), then -- data-parallel -- the bucket all-reduces
+run eagerly on RCCL (collectives stay outside the graphs) and graph B applies SGD; one graph when there is no
+data parallelism.
+
 `python -m torch.distributed.run --nproc-per-node 8 -m mifx.trainer.resnet_trainer` prints images/sec."""
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import sys
 import time
@@ -35,7 +42,7 @@ class ResNetTrainer:
     def __init__(self, batch: int, device, images: torch.Tensor, labels: torch.Tensor, num_classes: int = 1000,
                  lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 5e-5, warmup_steps: int = 100,
                  process_group=None, mean=IMAGENET_MEAN, std=IMAGENET_STD, seed: int = 0, crop: int = 224,
-                 accum_steps: int = 1):
+                 accum_steps: int = 1, graph: bool | None = None, graph_warmup: int = 2):
         """batch: examples per micro-batch per replica; accum_steps micro-batches (each with its own BatchNorm
         statistics) are summed into one update. A data-parallel step over W ranks trains on W x accum_steps x batch
         examples: the global sample of the step is drawn from (seed, step) and rank r takes micro-batches
@@ -62,6 +69,16 @@ class ResNetTrainer:
         self.amp = self.device.type == "cuda"
         if self.amp:  # MIOpen find: benchmark the solvers once per conv shape, then reuse (+12% measured)
             torch.backends.cudnn.benchmark = True
+        # captured steps (GPU): eager for the first graph_warmup steps (MIOpen find, momentum buffers), then graphs
+        self.use_graph = (self.device.type == "cuda") if graph is None else (bool(graph) and self.device.type == "cuda")
+        self.graph_warmup = max(1, int(graph_warmup))
+        self._gA = self._gB = None
+        self._eager_done = 0  # eager steps since construction / restore (the capture needs warm MIOpen solvers)
+        if self.use_graph:
+            n = self.world * self.accum * self.batch
+            self._idx_dev = torch.zeros(n, dtype=torch.int64, device=self.device)
+            self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._neg_lr = torch.zeros(1, dtype=torch.float32, device=self.device)
 
     def _lr(self) -> float:
         return self.base_lr * min(1.0, (self.step_idx + 1) / max(1, self.warmup))
@@ -73,6 +90,12 @@ class ResNetTrainer:
         return torch.randint(0, len(self.labels), (self.world * self.accum * self.batch,), generator=g)
 
     def step(self) -> torch.Tensor:
+        if self.use_graph and self._eager_done >= self.graph_warmup:
+            return self._graph_step()
+        self._eager_done += 1
+        return self._eager_step()
+
+    def _eager_step(self) -> torch.Tensor:
         glob = self._step_indices()
         for pg in self.opt.param_groups:
             pg["lr"] = self._lr()
@@ -102,6 +125,82 @@ class ResNetTrainer:
         self.step_idx += 1
         return total
 
+    # ---------------------------------------------------------------- captured step
+    def _graph_step(self) -> torch.Tensor:
+        glob = self._step_indices()
+        if self._gA is None:
+            self._capture()
+        self._idx_dev.copy_(glob)
+        self._step_dev.fill_(self.step_idx)
+        self._neg_lr.fill_(-self._lr())
+        for pg in self.opt.param_groups:
+            pg["lr"] = self._lr()  # (kept current for checkpoints / eager fallbacks)
+        self._gA.replay()
+        if self.dp is not None:
+            self.dp.finish()  # bucket all-reduces (RCCL) in place on the gradient views, averaged
+            self._gB.replay()
+        self.step_idx += 1
+        return self._static_loss
+
+    def _fwd_bwd_captured(self) -> torch.Tensor:
+        if self.dp is not None:
+            for b in self.dp.buckets:  # param.grad are views of these
+                b.buf.zero_()
+        else:
+            torch._foreach_zero_([p.grad for p in self.model.parameters() if p.grad is not None])
+        total = None
+        ctx = self.dp.no_sync() if self.dp is not None else contextlib.nullcontext()
+        with ctx:
+            for m in range(self.accum):
+                mb = self.rank * self.accum + m
+                idx = self._idx_dev[mb * self.batch:(mb + 1) * self.batch]
+                x = crop_flip_normalize(self.images, idx, (self.crop, self.crop), True, self.seed, 0, self.mean,
+                                        self.std, torch.bfloat16 if self.amp else torch.float32,
+                                        step_dev=self._step_dev)
+                y = self.labels[idx]
+                with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
+                    loss = F.cross_entropy(self.model(x).float(), y) / self.accum
+                loss.backward()
+                total = loss.detach() if total is None else total + loss.detach()
+        return total
+
+    @torch.no_grad()
+    def _sgd_captured(self) -> None:
+        """torch.optim.SGD's update (weight decay, momentum, Nesterov; its own momentum buffers) with the learning
+        rate read from a device tensor, so a replayed graph follows the warmup schedule."""
+        for group in self.opt.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            grads = [p.grad for p in params]
+            bufs = [self.opt.state[p]["momentum_buffer"] for p in params]
+            wd, mom, damp = group["weight_decay"], group["momentum"], group["dampening"]
+            if wd:
+                grads = torch._foreach_add(grads, params, alpha=wd)
+            torch._foreach_mul_(bufs, mom)
+            torch._foreach_add_(bufs, grads, alpha=1 - damp)
+            if group["nesterov"]:
+                upd = torch._foreach_add(grads, bufs, alpha=mom)
+            else:
+                upd = [b.clone() for b in bufs]
+            torch._foreach_mul_(upd, self._neg_lr)
+            torch._foreach_add_(params, upd)
+
+    def _capture(self) -> None:
+        if any("momentum_buffer" not in self.opt.state.get(p, {}) for p in self.model.parameters()
+               if p.requires_grad):
+            raise RuntimeError("capture needs the SGD momentum buffers of an eager step first")
+        torch.cuda.synchronize(self.device)
+        self._gA = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._gA):
+            self._static_loss = self._fwd_bwd_captured()
+            if self.dp is None:
+                self._sgd_captured()
+        if self.dp is not None:
+            self._gB = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._gB):
+                self._sgd_captured()
+
     # ---------------------------------------------------------------- checkpoint / resume
     def state_dict(self) -> dict:
         """Weights, BatchNorm running statistics, the SGD momentum buffers and the step (flat tensor dict)."""
@@ -121,6 +220,8 @@ class ResNetTrainer:
                 self.opt.state[p]["momentum_buffer"] = v.to(device=p.device, dtype=p.dtype).clone() \
                     .contiguous(memory_format=torch.channels_last if p.ndim == 4 else torch.contiguous_format)
         self.step_idx = int(sd["step"][0])
+        self._gA = self._gB = None  # the graphs captured the old momentum buffers: re-capture after warm steps
+        self._eager_done = 0
 
     def save_checkpoint(self, model_dir: str, keep: int = 1) -> str:
         import glob as _glob
@@ -175,6 +276,7 @@ def main(argv=None):
                     help="MIOpen deterministic convolution solvers: bit-reproducible steps (the default bf16 solvers "
                          "are not run-to-run reproducible, measured in round 2, profiles/resnet_determinism_r2s3.txt). Diagnostic only: "
                          "measured 13.7 s/step at B=256 on one MI355X vs 26.5 ms with the default solvers")
+    ap.add_argument("--no-graph", action="store_true", help="eager steps instead of the captured hipGraph step")
     a = ap.parse_args(argv)
     if a.deterministic:
         torch.backends.cudnn.deterministic = True
@@ -182,7 +284,7 @@ def main(argv=None):
     dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     imgs, labels = synthetic_imagenet(a.images, seed=env.rank, device=dev)
     pg = torch.distributed.group.WORLD if env.world_size > 1 else None
-    tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=pg, warmup_steps=10)
+    tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=pg, warmup_steps=10, graph=not a.no_graph)
     for i in range(a.warmup):  # first steps include MIOpen solver search/compile: report progress
         t1 = time.perf_counter()
         with heartbeat("resnet warmup"):
@@ -207,7 +309,7 @@ def main(argv=None):
                           "value": a.batch * env.world_size * a.steps / dt, "unit": "images/s",
                           "n_gpus": env.world_size, "batch_per_gpu": a.batch, "ms_per_step": 1e3 * dt / a.steps,
                           "loss": float(loss), "dtype": "bf16", "data": "synthetic ImageNet-shaped (HBM-resident)",
-                          "parallelism": f"dp{env.world_size}",
+                          "parallelism": f"dp{env.world_size}", "hipgraph": tr.use_graph,
                           "deterministic": bool(torch.backends.cudnn.deterministic)}), flush=True)
     mdist.shutdown()
 

@@ -127,3 +127,36 @@ def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single():
     for k in one["state"]:
         assert torch.equal(r0["state"][k], r1["state"][k]), k
         torch.testing.assert_close(r0["state"][k], one["state"][k], rtol=1e-5, atol=1e-6, msg=k)
+
+def test_resnet_captured_step_matches_eager():
+    """ResNetTrainer's hipGraph step (graph A: input kernel + forward + backward with device-side step, indices and
+    learning rate; SGD captured with the learning rate read from a device tensor) follows the eager trainer: same
+    losses and weights up to the update's rounding (lr * g formed before the add), with MIOpen's deterministic
+    solvers. Includes a checkpoint restore in the middle (the graphs are re-captured after fresh eager steps)."""
+    import tempfile as _tf
+
+    from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
+
+    imgs, labels = synthetic_imagenet(48, size=72, classes=10, seed=1)
+
+    def run(graph, restore_at=None):
+        tr = ResNetTrainer(6, "cuda:0", imgs, labels, num_classes=10, lr=0.05, warmup_steps=4, crop=64, seed=5,
+                           graph=graph, graph_warmup=2)
+        torch.backends.cudnn.benchmark = False
+        torch.backends.cudnn.deterministic = True
+        losses = []
+        with _tf.TemporaryDirectory() as d:
+            for i in range(7):
+                if restore_at is not None and i == restore_at:
+                    path = tr.save_checkpoint(d)
+                    tr.restore(path)
+                losses.append(float(tr.step()))
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().float().cpu() for k, v in tr.model.named_parameters()}, tr
+
+    le, pe, _ = run(False)
+    lg, pg, trg = run(True, restore_at=4)
+    assert trg._gA is not None and trg._eager_done == 2  # re-captured after the restore's 2 eager steps
+    torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-3, atol=1e-3)
+    for k in pe:
+        torch.testing.assert_close(pg[k], pe[k], rtol=1e-3, atol=1e-4, msg=k)

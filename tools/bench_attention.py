@@ -64,9 +64,30 @@ def run_fused(B=32, H=12, S=128, D=64, mask=True, drop=0.1, iters=50):
     return {"backend": "mifx fused (csrc/attention.hip)", "mask": mask, "us_fwd_bwd": (time.perf_counter() - t0) / iters * 1e6}
 
 
+def _tflops(r, B, H, S, D):
+    # fwd 2 GEMMs (4 B H S^2 D FLOP) + bwd 5 (S recompute, dP, dQ, dK, dV: 10 B H S^2 D)
+    if "us_fwd_bwd" in r:
+        r["tflops"] = round(14 * B * H * S * S * D / (r["us_fwd_bwd"] * 1e-6) / 1e12, 1)
+    r.update(B=B, S=S, H=H)
+    return r
+
+
 if __name__ == "__main__":
-    for mask in (True, False):
-        print(json.dumps(run_fused(mask=mask)), flush=True)
-    for be in (SDPBackend.FLASH_ATTENTION, SDPBackend.EFFICIENT_ATTENTION, SDPBackend.MATH):
-        for mask in (True, False):
-            print(json.dumps(run(be, mask=mask)), flush=True)
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seq", type=int, nargs="*", default=[128])
+    ap.add_argument("--tokens", type=int, default=4096, help="batch = tokens // seq")
+    ap.add_argument("--drop", type=float, nargs="*", default=[0.1])
+    ap.add_argument("--sdpa", action="store_true", help="also time the SDPA backends")
+    a = ap.parse_args()
+    for S in a.seq:
+        B = max(1, a.tokens // S)
+        for drop in a.drop:
+            for mask in (True, False):
+                print(json.dumps(_tflops(run_fused(B=B, S=S, mask=mask, drop=drop), B, 12, S, 64) | {"drop": drop}),
+                      flush=True)
+            if a.sdpa:
+                for be in (SDPBackend.FLASH_ATTENTION, SDPBackend.EFFICIENT_ATTENTION, SDPBackend.MATH):
+                    print(json.dumps(_tflops(run(be, B=B, S=S, mask=True, drop=drop), B, 12, S, 64) | {"drop": drop}),
+                          flush=True)

@@ -20,7 +20,7 @@ def make_step(model: str, batch: int, seq: int):
         from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
 
         imgs, labels = synthetic_imagenet(1024, device=dev)
-        tr = ResNetTrainer(batch, dev, imgs, labels, warmup_steps=10)
+        tr = ResNetTrainer(batch, dev, imgs, labels, warmup_steps=10, graph=False)  # same kernels, visible
         return tr.step
     if model == "bert":
         from mifx.models.bert import BertConfig
