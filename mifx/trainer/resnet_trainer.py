@@ -78,7 +78,7 @@ class ResNetTrainer:
             n = self.world * self.accum * self.batch
             self._idx_dev = torch.zeros(n, dtype=torch.int64, device=self.device)
             self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
-            self._neg_lr = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._neg_lr = torch.zeros((), dtype=torch.float32, device=self.device)  # 0-dim: a foreach scalar
 
     def _lr(self) -> float:
         return self.base_lr * min(1.0, (self.step_idx + 1) / max(1, self.warmup))

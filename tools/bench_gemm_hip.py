@@ -34,13 +34,22 @@ def main():
     torch.manual_seed(0)
     dev = "cuda"
     cfgs = gemm.config_details()
-    for name, (k, n) in SHAPES.items():
+    # --dx: the backward's input-gradient products dX[M, in] = dY[M, out] . W[out, in], run as NT products against a
+    # transposed weight copy (W^T [in, out], K-contiguous) vs the library's dY @ W (what the backward runs today)
+    dx = "--dx" in sys.argv
+    shapes = {nm: (n, k) for nm, (k, n) in SHAPES.items()} if dx else SHAPES
+    for name, (k, n) in shapes.items():
         x = (torch.rand(M, k, device=dev) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(n, k, device=dev) * 2 - 1) * k ** -0.5).to(torch.bfloat16)
         b = (torch.rand(n, device=dev) * 0.2 - 0.1).to(torch.bfloat16)
         flop = 2.0 * M * k * n
-        rows = [("hipblaslt F.linear(x, w)", lambda: F.linear(x, w)),
-                ("hipblaslt F.linear(x, w, b)", lambda: F.linear(x, w, b))]
+        if dx:
+            wt = w.t().contiguous()  # [k, n]: the layer's weight [out = k, in = n]
+            rows = [("hipblaslt dY @ W (NN)", lambda: x @ wt), ("transpose W (per step)", lambda: w.t().contiguous())]
+            name = name + "_dx"
+        else:
+            rows = [("hipblaslt F.linear(x, w)", lambda: F.linear(x, w)),
+                    ("hipblaslt F.linear(x, w, b)", lambda: F.linear(x, w, b))]
         if name == "ffn1":
             rows.append(("hipblaslt F.linear + bias_gelu kernel", lambda: fb.bias_gelu(F.linear(x, w), b)))
         for i, (bm, bn, opt) in enumerate(cfgs):
@@ -48,6 +57,8 @@ def main():
                 continue
             tag = f"hip cfg{i} {bm}x{bn} opt{opt}"
             rows.append((f"{tag} none", lambda i=i: gemm.gemm_nt(x, w, None, 0, cfg=i)))
+            if dx:
+                continue
             rows.append((f"{tag} +bias", lambda i=i: gemm.gemm_nt(x, w, b, 1, cfg=i)))
             if name == "ffn1":
                 rows.append((f"{tag} +bias+gelu (y and z)", lambda i=i: gemm.gemm_nt(x, w, b, 2, cfg=i)))

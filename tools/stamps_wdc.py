@@ -12,12 +12,13 @@ import mifx.ops._lib as L  # noqa: E402
 
 diag = ctypes.CDLL("tools/bin/libwdc_stamps.so", mode=ctypes.RTLD_GLOBAL)
 diag64 = ctypes.CDLL("tools/bin/libwdc64_stamps.so", mode=ctypes.RTLD_GLOBAL)
+diag256 = ctypes.CDLL("tools/bin/libwdc256_stamps.so", mode=ctypes.RTLD_GLOBAL)
 L.load.cache_clear()
 _orig = L.load.__wrapped__
 
 
 def _load(name):
-    return {"wd_chain": diag, "wd_chain64": diag64}.get(name) or _orig(name)
+    return {"wd_chain": diag, "wd_chain64": diag64, "wd_chain256": diag256}.get(name) or _orig(name)
 
 
 L.load = _load
@@ -28,11 +29,13 @@ from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer  # noqa: E402
 NAMES = {1: "prologue", 2: "loop->iter", 3: "gather+fwd", 4: "loss", 5: "B0", 6: "stage5+B", 7: "dW5+dA4",
          8: "B+stage4+B", 9: "dW4+dA3", 10: "B+stage3+B", 11: "dW3+dA2", 12: "B+stage2+B", 13: "dW2+dA1",
          14: "B+stage1+B", 15: "dW1", 16: "->epi", 17: "epilogue"}
-for NW, batch in ((4, 40), (8, 40), (4, 65536), (8, 128), (8, 65536)):
+CFGS = [(4, 40, False), (8, 65536, False), (8, 65536, True)] if "--quick" in sys.argv else \
+    [(4, 40, False), (8, 40, False), (4, 65536, False), (8, 128, False), (8, 65536, False), (8, 65536, True)]
+for NW, batch, big in CFGS:
     t64 = NW == 4 and batch <= 64  # the T = 64 build (csrc/wd_chain64.hip)
     tr = FusedWideDeepTrainer(WideDeepModel(seed=0), batch=batch, device="cuda", kernel="chain", waves=NW,
-                              small_tile=t64)
-    lib = diag64 if t64 else diag
+                              small_tile=t64, large_tile=big, shuffle_seed=0x5EED)
+    lib = diag64 if t64 else diag256 if big else diag
     tr.set_data(synthetic_records(1 << 17, device="cuda", seed=0))
     for _ in range(3):
         tr.step()
@@ -52,7 +55,7 @@ for NW, batch in ((4, 40), (8, 40), (4, 65536), (8, 128), (8, 65536)):
 import numpy as np  # noqa: E402
 
 bb = (ctypes.c_ulonglong * (4096 * 3))()
-assert diag.mifx_wdc_blk_stamps(bb) == 0
+assert lib.mifx_wdc_blk_stamps(bb) == 0
 a = np.array(bb, dtype=np.int64).reshape(4096, 3)[:tr.grid]
 t0 = a[:, 0].min()
 st, pro, end = (a[:, 0] - t0) / 100.0, (a[:, 1] - a[:, 0]) / 100.0, (a[:, 2] - t0) / 100.0  # us

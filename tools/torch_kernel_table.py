@@ -26,7 +26,7 @@ def make_step(model: str, batch: int, seq: int):
         from mifx.models.bert import BertConfig
         from mifx.trainer.bert_trainer import BertTrainer
 
-        return BertTrainer(BertConfig(), batch, seq, dev).step
+        return BertTrainer(BertConfig(), batch, seq, dev, graph=False).step  # same kernels as the graph, visible
     raise ValueError(model)
 
 
@@ -39,10 +39,14 @@ def main():
     ap.add_argument("--active", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
+    from mifx.utils.meter import heartbeat
+
     step = make_step(a.model, a.batch, a.seq)
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
+    with heartbeat(f"{a.model} warmup"):  # first steps: MIOpen solver search can run for minutes on a fresh box
+        for i in range(a.warmup):
+            step()
+            torch.cuda.synchronize()
+            print(f"[{a.model}] warmup step {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
     from torch.profiler import ProfilerActivity, profile
 
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
