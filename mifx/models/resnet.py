@@ -13,23 +13,35 @@ from ..ops import gconv
 from ..ops.bn_relu import BatchNormReLU2d
 from ..ops.pool import max_pool3s2
 
-# MIFX_RESNET_HIP_CONV=1: the block convolutions (1x1 and 3x3, any stride) on the hand-written MFMA implicit-GEMM
-# kernels (csrc/gconv.hip: forward, stride-1 / phase-split strided input gradient, pixel-split weight gradient);
-# 0 (default): MIOpen. Whole-step A/B on MI355X, batch 256 (profiles/resnet_gconv_ab_r3b_hybrid.jsonl): HIP forward +
-# HIP strided input gradient + MIOpen single-group weight gradient 27.4-27.6 ms/step vs MIOpen 26.5-27.0 (the
-# forward wins per shape, profiles/gconv_resnet_shapes_r3.jsonl, but not by enough to carry the backward).
-USE_HIP_CONV = os.environ.get("MIFX_RESNET_HIP_CONV", "0") == "1"
+# Convolution backends (MIFX_RESNET_HIP_CONV): "routed" -- per shape and pass, the faster of the hand-written MFMA
+# implicit-GEMM kernels (csrc/gconv.hip: forward, stride-1 / phase-split strided input gradient, pixel-split weight
+# gradient) and MIOpen, from the measurement of every ResNet-50 convolution at B = 256 (CONV_ROUTES below,
+# tools/bench_resnet_convs.py); "1" -- every eligible pass on the HIP kernels (gconv's own policy); "0" -- MIOpen.
+_MODE = os.environ.get("MIFX_RESNET_HIP_CONV", "0")
+USE_HIP_CONV = _MODE != "0"
+
+# (input H, C in, K out, kernel, stride) -> (forward, input gradient, weight gradient) backend; shapes not listed
+# (e.g. the 3-channel stem) stay on MIOpen
+CONV_ROUTES: dict[tuple[int, int, int, int, int], tuple[str, str, str]] = {}
 
 
 class HipConv2d(nn.Conv2d):
     """nn.Conv2d whose CUDA forward / backward run csrc/gconv.hip when the shape is eligible (channels % 32,
-    symmetric padding < kernel); bf16 channels-last output like F.conv2d under bf16 autocast."""
+    symmetric padding < kernel) and routed there; bf16 channels-last output like F.conv2d under bf16 autocast."""
 
     def forward(self, x):
         if x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.padding[0] == self.padding[1] \
                 and self.stride[0] == self.stride[1] and self.kernel_size[0] == self.kernel_size[1] \
                 and gconv.eligible(x, self.weight, 1, self.padding[0], self.stride[0]):
-            return gconv.conv2d(x, self.weight, self.bias, padding=self.padding[0], stride=self.stride[0])
+            route = None
+            if _MODE == "routed":
+                r = CONV_ROUTES.get((x.shape[2], self.in_channels, self.out_channels, self.kernel_size[0],
+                                     self.stride[0]))
+                if r is None or r[0] != "hip":
+                    return super().forward(x)
+                route = (r[1], r[2])
+            return gconv.conv2d(x, self.weight, self.bias, padding=self.padding[0], stride=self.stride[0],
+                                route=route)
         return super().forward(x)
 
 

@@ -73,7 +73,7 @@ def wgrad(xb: torch.Tensor, dyb: torch.Tensor, N, Hi, Wi, G, C, K, R, S, pad, st
 
 class _GConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, pad, groups, relu, stride):
+    def forward(ctx, x, weight, bias, pad, groups, relu, stride, route=None):
         N, _, Hi, Wi = x.shape
         GK, C, R, S = weight.shape
         G, K = groups, GK // groups
@@ -85,6 +85,7 @@ class _GConv(torch.autograd.Function):
         ctx.save_for_backward(xb, wb, y if relu else None)
         ctx.geo = (N, Hi, Wi, G, C, K, R, S, pad, bias is not None, weight.dtype,
                    bias.dtype if bias is not None else None, stride)
+        ctx.route = route or (None, None)
         return y
 
     @staticmethod
@@ -98,10 +99,14 @@ class _GConv(torch.autograd.Function):
         Ho, Wo = dyb.shape[2], dyb.shape[3]
         dx = dw = db = None
         M = N * Ho * Wo
+        r_dgrad, r_wgrad = ctx.route
         if ctx.needs_input_grad[0]:
             # HIP input gradient for grouped / large-image convs; MIOpen's is as fast or faster on small
-            # single-group images (profiles/gconv_resnet_r2.jsonl)
-            if stride == 1 and C % 32 == 0 and R == S and (G > 1 or M >= 100_000):
+            # single-group images (profiles/gconv_resnet_r2.jsonl); a per-shape route overrides the policy
+            hip_ok = C % 32 == 0 and K % 32 == 0 and R == S
+            if r_dgrad == "miopen" or (r_dgrad == "hip" and not hip_ok):
+                dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
+            elif stride == 1 and C % 32 == 0 and R == S and (G > 1 or M >= 100_000 or r_dgrad == "hip"):
                 # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
                 w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
                 dx = _launch(dyb, w_bwd, None, N, Ho, Wo, G, K, C, R, S, R - 1 - pad)
@@ -114,7 +119,12 @@ class _GConv(torch.autograd.Function):
             # pate_ensemble_bench_r3*.jsonl): grouped 1x1 -> one batched GEMM; other grouped convs -> the HIP kernel;
             # a single group (ResNet-50) -> MIOpen, which beats the pixel-split kernel on 7 of the 9 ResNet shapes.
             one_by_one = R == 1 and S == 1 and pad == 0 and stride == 1
-            if G > 1 and one_by_one:  # dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
+            if r_wgrad == "miopen" or (r_wgrad == "hip" and not (C % 8 == 0 and K % 8 == 0)):
+                dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
+                                                 groups=G).to(wdt)
+            elif r_wgrad == "hip":
+                dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
+            elif G > 1 and one_by_one:  # dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
                 dyv = dyb.permute(0, 2, 3, 1).reshape(M, G, K).permute(1, 2, 0)
                 xv = xb.permute(0, 2, 3, 1).reshape(M, G, C).permute(1, 0, 2)
                 dw = torch.bmm(dyv, xv, out_dtype=torch.float32).reshape(G * K, C, 1, 1).to(wdt)
@@ -127,15 +137,16 @@ class _GConv(torch.autograd.Function):
                                                  groups=G).to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = torch.sum(dyb, dim=(0, 2, 3), dtype=torch.float32).to(bdt)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0,
-           groups: int = 1, relu: bool = False, stride: int = 1) -> torch.Tensor:
-    """Stride-1 (grouped) convolution (`relu=True`: followed by ReLU, fused into the kernel's epilogue); the HIP
+           groups: int = 1, relu: bool = False, stride: int = 1, route: tuple | None = None) -> torch.Tensor:
+    """(Grouped, strided) convolution (`relu=True`: followed by ReLU, fused into the kernel's epilogue); the HIP
     kernels when `eligible`, else F.conv2d. Output bf16 channels-last on the kernel path (the dtype F.conv2d gives
-    under bf16 autocast)."""
+    under bf16 autocast). route = (input-gradient backend, weight-gradient backend), each "hip", "miopen" or None
+    (the built-in policy): a per-shape choice from measurements (mifx.models.resnet.CONV_ROUTES)."""
     if eligible(x, weight, groups, padding, stride) and _lib.gpu_available():
-        return _GConv.apply(x, weight, bias, int(padding), int(groups), bool(relu), int(stride))
+        return _GConv.apply(x, weight, bias, int(padding), int(groups), bool(relu), int(stride), route)
     y = F.conv2d(x, weight, bias, stride=stride, padding=padding, groups=groups)
     return F.relu(y) if relu else y

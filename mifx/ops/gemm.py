@@ -184,13 +184,81 @@ class GradSlot:
         self.g = None
 
 
+# ---------------------------------------------------------------- input-gradient GEMM (csrc/gemm_nn.hip)
+@functools.lru_cache(maxsize=None)
+def _nn_fns():
+    lib = _lib.load("gemm_nn")
+    return {"configs": sig(lib, "mifx_gemm_nn_configs", [VP, I32]),
+            "nn": sig(lib, "mifx_gemm_nn", [I32, VP, VP, VP, VP, I32, I32, I32, VP])}
+
+
+@functools.lru_cache(maxsize=None)
+def nn_configs() -> tuple[tuple[int, int, int], ...]:
+    """(BM, BN, ring depth) of every compiled NN configuration, by index."""
+    buf = (ctypes.c_int * 96)()
+    n = _nn_fns()["configs"](buf, 96)
+    return tuple((buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(n))
+
+
+# (M, N, K) of dX = dY[M, K] W[K, N] -> configuration, where the NN kernel measured faster than hipBLASLt
+# (tools/bench_gemm_hip.py --dx); other shapes stay on the library
+NN_TUNED: dict[tuple[int, int, int], int] = {}
+
+
+def nn_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
+    if (M, N, K) in NN_TUNED:
+        return NN_TUNED[(M, N, K)]
+    best, best_score = None, None
+    for i, (bm, bn, _) in enumerate(nn_configs()):
+        if M % bm or N % bn or K % 64:
+            continue
+        tiles = (M // bm) * (N // bn)
+        fill = tiles / (-(-tiles // cus) * cus)
+        score = (fill * (bm * bn) ** 0.25, bm * bn)
+        if best_score is None or score > best_score:
+            best, best_score = i, score
+    return best
+
+
+def gemm_nn(a: torch.Tensor, b: torch.Tensor, r: torch.Tensor | None = None, cfg: int | None = None) -> torch.Tensor:
+    """a [M, K] bf16, b [K, N] bf16 (row-major) -> a @ b (+ r [M, N]) bf16 on csrc/gemm_nn.hip (fp32 accumulation,
+    r added before the single rounding: torch.addmm(r, a, b)'s contract)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if cfg is None:
+        cfg = nn_pick(M, N, K)
+    if cfg is None:
+        raise ValueError(f"no NN tile configuration for {M}x{N}x{K}")
+    a, b = a.contiguous(), b.contiguous()
+    if r is not None:
+        r = r.reshape(M, N).to(torch.bfloat16).contiguous()
+    c = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    check(_nn_fns()["nn"](int(cfg), ptr(a), ptr(b), ptr(r), ptr(c), M, N, K, stream_handle(a.device)), "mifx_gemm_nn")
+    return c
+
+
+def nn_preferred(M: int, N: int, K: int) -> bool:
+    if os.environ.get("MIFX_HIP_GEMM_NN", "1") == "0":
+        return False
+    return (M, N, K) in NN_TUNED or (os.environ.get("MIFX_HIP_GEMM") == "all" and nn_pick(M, N, K) is not None)
+
+
 def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tensor:
-    native_stats.count("gemm_dX", False)  # dX = dY W on hipBLASLt (with the residual gradient as its C operand)
-    if slot is None:
-        return dy2 @ w
-    g, slot.g = slot.g, None
+    """dX = dY W (+ the residual gradient parked in `slot` as the C operand): the hand-written NN kernel where it
+    measured faster (NN_TUNED), else hipBLASLt."""
+    g = None
+    if slot is not None:
+        g, slot.g = slot.g, None
+        if g is None:
+            raise RuntimeError("GradSlot empty: the residual gradient did not arrive before the projection's backward")
+    M, K = dy2.shape
+    N = w.shape[1]
+    native = (dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and nn_preferred(M, N, K))
+    native_stats.count("gemm_dX", native)
+    if native:
+        return gemm_nn(dy2, w, g)
     if g is None:
-        raise RuntimeError("GradSlot empty: the residual gradient did not arrive before the projection's backward")
+        return dy2 @ w
     return torch.addmm(g.reshape(-1, w.shape[1]).to(dy2.dtype), dy2, w)
 
 

@@ -62,6 +62,14 @@ def main():
             rows.append((f"{tag} +bias", lambda i=i: gemm.gemm_nt(x, w, b, 1, cfg=i)))
             if name == "ffn1":
                 rows.append((f"{tag} +bias+gelu (y and z)", lambda i=i: gemm.gemm_nt(x, w, b, 2, cfg=i)))
+        if dx:  # the NN kernel on dY [M, k] x W [k, n] (no transposed copy)
+            for i, (bm, bn, ns) in enumerate(gemm.nn_configs()):
+                if M % bm or n % bn or k % 64:
+                    continue
+                rows.append((f"nn cfg{i} {bm}x{bn} ring{ns}", lambda i=i: gemm.gemm_nn(x, wt, None, cfg=i)))
+                rows.append((f"nn cfg{i} {bm}x{bn} ring{ns} +R", lambda i=i: gemm.gemm_nn(x, wt, rr, cfg=i)))
+            rr = torch.randn(M, n, device=dev).to(torch.bfloat16)
+            rows.append(("hipblaslt addmm(R, dY, W)", lambda: torch.addmm(rr, x, wt)))
         for label, fn in rows:
             us = timeit(fn)
             print(json.dumps({"gemm": name, "M": M, "N": n, "K": k, "impl": label, "us": round(us, 2),
