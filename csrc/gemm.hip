@@ -33,7 +33,9 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64;
 
-enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2 };
+// EPI_ADD_R: Y = X W^T + R (R bf16 [M, N], passed as `bias`): the input-gradient GEMM dX = dY W computed as an NT
+// product against a transposed weight copy, with the residual gradient folded in (mifx.ops.gemm.GradSlot)
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3 };
 
 // GELU(erf) with a branch-free erf (Abramowitz & Stegun 7.1.26: |error| <= 1.5e-7, far below the bf16 output's
 // 2^-9 relative step): the library erff evaluates piecewise polynomials selected per |x|, which diverge inside a
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt(const bf16* __restric
   for (int a = 0; a < NR; ++a) {
     const int n = n0 + wn * TN + 16 * a + 4 * fc;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (EPI != EPI_NONE) {
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n + r];
     }
@@ -196,6 +198,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt(const bf16* __restric
           o[r] = (bf16)gelu_f((float)z[r] + bv[r]);   // bias_gelu_fwd on that stored value
         }
         *(v4bf*)(Z + (size_t)m * N + n) = z;
+      } else if (EPI == EPI_ADD_R) {
+        const v4bf rv = *(const v4bf*)((const bf16*)bias + (size_t)m * N + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[a][b][r] + (float)rv[r]);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[a][b][r] + bv[r]);
@@ -223,6 +229,7 @@ template <int BM, int BN, int WM, int WN, int OPT>
 int dispatch_epi(int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N,
                  int K, hipStream_t st) {
   if (epi == EPI_NONE) return launch<BM, BN, WM, WN, EPI_NONE, bf16, OPT>(X, W, nullptr, Y, nullptr, M, N, K, st);
+  if (epi == EPI_ADD_R) return launch<BM, BN, WM, WN, EPI_ADD_R, bf16, OPT>(X, W, bias, Y, nullptr, M, N, K, st);
   if (epi == EPI_BIAS)
     return bias_f32 ? launch<BM, BN, WM, WN, EPI_BIAS, float, OPT>(X, W, bias, Y, nullptr, M, N, K, st)
                     : launch<BM, BN, WM, WN, EPI_BIAS, bf16, OPT>(X, W, bias, Y, nullptr, M, N, K, st);
@@ -241,9 +248,40 @@ constexpr Cfg kCfgs[] = {{256, 256, 0}, {256, 128, 0}, {128, 128, 0}, {128, 256,
                          {128, 96, 1}, {128, 96, 5}, {128, 128, 5}, {256, 128, 5}, {128, 96, 7}, {128, 128, 7},
                          {256, 128, 7}, {256, 144, 7}};
 
+// dst[C][R] = src[R][C] (bf16), 64 x 64 tiles through LDS: 16-byte loads along src rows, 16-byte stores along dst
+// rows (8 consecutive src rows of one column gathered from LDS). The transposed weight copy of the dX GEMMs.
+__global__ __launch_bounds__(256) void transpose_bf16(const bf16* __restrict__ src, bf16* __restrict__ dst, int R,
+                                                      int C) {
+  __shared__ bf16 t[64][64 + 2];
+  const int nbc = C / 64, r0 = (blockIdx.x / nbc) * 64, c0 = (blockIdx.x % nbc) * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = i * 256 + threadIdx.x, row = q >> 3, ch = q & 7;
+    const v8bf v = *(const v8bf*)(src + (size_t)(r0 + row) * C + c0 + 8 * ch);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[row][8 * ch + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = i * 256 + threadIdx.x, col = q >> 3, ch = q & 7;  // dst row = src column col
+    v8bf v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = t[8 * ch + e][col];
+    *(v8bf*)(dst + (size_t)(c0 + col) * R + r0 + 8 * ch) = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// dst [C, R] = src [R, C]^T, bf16; R % 64 == 0, C % 64 == 0, 16-byte aligned
+int mifx_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t st) {
+  if (R <= 0 || C <= 0 || R % 64 || C % 64 || (uintptr_t)src % 16 || (uintptr_t)dst % 16) return -1;
+  hipLaunchKernelGGL(transpose_bf16, dim3((R / 64) * (C / 64)), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, R, C);
+  return (int)hipGetLastError();
+}
 
 // tile configurations: out[3 * i] = BM, out[3 * i + 1] = BN, out[3 * i + 2] = OPT bits
 int mifx_gemm_configs(int* out, int n) {
@@ -265,7 +303,8 @@ int mifx_gemm_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, c
   if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || X == nullptr || W == nullptr || Y == nullptr) return -1;
   const Cfg c = kCfgs[cfg];
   if (M % c.bm || N % c.bn || K % BK) return -1;
-  if (epi < 0 || epi > 2 || (epi > 0 && bias == nullptr) || (epi == 2 && Z == nullptr)) return -1;
+  if (epi < 0 || epi > 3 || (epi > 0 && bias == nullptr) || (epi == 2 && Z == nullptr)) return -1;
+  if (epi == 3 && (uintptr_t)bias % 8) return -1;
   if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 8 || (Z != nullptr && (uintptr_t)Z % 8)) return -1;
   if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;  // 32-bit element offsets
   switch (cfg) {

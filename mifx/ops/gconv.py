@@ -71,6 +71,15 @@ def wgrad(xb: torch.Tensor, dyb: torch.Tensor, N, Hi, Wi, G, C, K, R, S, pad, st
     return dw
 
 
+def _lib_bwd(xb, wb, dyb, stride: int, pad: int, groups: int, dgrad: bool, wgrad: bool):
+    """MIOpen's backward through the op autograd itself uses (aten.convolution_backward): torch.nn.grad.conv2d_input
+    / conv2d_weight take a different, much slower path on channels-last bf16 (4x on ResNet-50's input gradients,
+    profiles/resnet_conv_routes_r4.jsonl)."""
+    dx, dw, _ = torch.ops.aten.convolution_backward(dyb, xb, wb, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                    [0, 0], groups, [dgrad, wgrad, False])
+    return dx, dw
+
+
 class _GConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, pad, groups, relu, stride, route=None):
@@ -105,7 +114,7 @@ class _GConv(torch.autograd.Function):
             # single-group images (profiles/gconv_resnet_r2.jsonl); a per-shape route overrides the policy
             hip_ok = C % 32 == 0 and K % 32 == 0 and R == S
             if r_dgrad == "miopen" or (r_dgrad == "hip" and not hip_ok):
-                dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
+                dx = _lib_bwd(xb, wb, dyb, stride, pad, G, True, False)[0]
             elif stride == 1 and C % 32 == 0 and R == S and (G > 1 or M >= 100_000 or r_dgrad == "hip"):
                 # dx = conv(dy, flip(w) transposed), pad' = R - 1 - pad: [G][C][R][S][K] weight image
                 w_bwd = wb.view(G, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
@@ -113,15 +122,14 @@ class _GConv(torch.autograd.Function):
             elif stride > 1 and C % 32 == 0 and K % 32 == 0:  # phase-split strided input gradient
                 dx = dgrad_strided(dyb, wb, N, Hi, Wi, G, C, K, R, S, pad, stride)
             else:
-                dx = torch.nn.grad.conv2d_input((N, G * C, Hi, Wi), wb, dyb, stride=stride, padding=pad, groups=G)
+                dx = _lib_bwd(xb, wb, dyb, stride, pad, G, True, False)[0]
         if ctx.needs_input_grad[1]:
             # Weight-gradient policy from measurements (profiles/gconv_resnet_shapes_r3.jsonl,
             # pate_ensemble_bench_r3*.jsonl): grouped 1x1 -> one batched GEMM; other grouped convs -> the HIP kernel;
             # a single group (ResNet-50) -> MIOpen, which beats the pixel-split kernel on 7 of the 9 ResNet shapes.
             one_by_one = R == 1 and S == 1 and pad == 0 and stride == 1
             if r_wgrad == "miopen" or (r_wgrad == "hip" and not (C % 8 == 0 and K % 8 == 0)):
-                dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
-                                                 groups=G).to(wdt)
+                dw = _lib_bwd(xb, wb, dyb, stride, pad, G, False, True)[1].to(wdt)
             elif r_wgrad == "hip":
                 dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
             elif G > 1 and one_by_one:  # dw[g] = dy_g^T x_g, one strided batched GEMM (no copies)
@@ -133,8 +141,7 @@ class _GConv(torch.autograd.Function):
                 # (tap, k, group) tiles alone cannot fill the chip (deterministic split sum)
                 dw = wgrad(xb, dyb, N, Hi, Wi, G, C, K, R, S, pad, stride).to(wdt)
             else:
-                dw = torch.nn.grad.conv2d_weight(xb, (G * K, C, R, S), dyb, stride=stride, padding=pad,
-                                                 groups=G).to(wdt)
+                dw = _lib_bwd(xb, wb, dyb, stride, pad, G, False, True)[1].to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = torch.sum(dyb, dim=(0, 2, 3), dtype=torch.float32).to(bdt)
         return dx, dw, db, None, None, None, None, None

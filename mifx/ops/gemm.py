@@ -28,7 +28,19 @@ def _fns():
     return {
         "configs": sig(lib, "mifx_gemm_configs", [VP, I32]),
         "nt": sig(lib, "mifx_gemm_nt", [I32, I32, I32, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
+        "tr": sig(lib, "mifx_transpose_bf16", [VP, VP, I32, I32, VP]),
     }
+
+
+def transpose(w: torch.Tensor) -> torch.Tensor:
+    """w [R, C] bf16 -> w^T [C, R] contiguous (csrc/gemm.hip transpose_bf16 where R, C % 64 == 0)."""
+    R, C = w.shape
+    if not (w.is_cuda and w.dtype == torch.bfloat16 and R % 64 == 0 and C % 64 == 0):
+        return w.t().contiguous()
+    w = w.contiguous()
+    out = torch.empty(C, R, device=w.device, dtype=torch.bfloat16)
+    check(_fns()["tr"](ptr(w), ptr(out), R, C, stream_handle(w.device)), "mifx_transpose_bf16")
+    return out
 
 
 @functools.lru_cache(maxsize=None)
@@ -94,7 +106,8 @@ def preferred(x: torch.Tensor, w: torch.Tensor) -> bool:
 def gemm_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0,
             cfg: int | None = None) -> tuple[torch.Tensor, torch.Tensor | None]:
     """x2 [M, K] bf16, w [N, K] bf16 -> (Y [M, N] bf16, Z or None). epi 0: X W^T; 1: + bias; 2: GELU(X W^T + bias)
-    with Z = bf16(X W^T) (pre-bias)."""
+    with Z = bf16(X W^T) (pre-bias); 3: X W^T + bias where `bias` is a bf16 [M, N] matrix (added before the one
+    rounding)."""
     M, K = x2.shape
     N = w.shape[0]
     if cfg is None:
@@ -105,7 +118,9 @@ def gemm_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
     y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
     z = torch.empty_like(y) if epi == 2 else None
     b = None
-    if epi:
+    if epi == 3:
+        b = bias.reshape(M, N).to(torch.bfloat16).contiguous()
+    elif epi:
         b = bias if bias.dtype in (torch.float32, torch.bfloat16) else bias.float()
         b = b.contiguous()
     check(_fns()["nt"](int(cfg), int(epi), int(b is not None and b.dtype == torch.float32), ptr(x2), ptr(w), ptr(b),
@@ -243,9 +258,18 @@ def nn_preferred(M: int, N: int, K: int) -> bool:
     return (M, N, K) in NN_TUNED or (os.environ.get("MIFX_HIP_GEMM") == "all" and nn_pick(M, N, K) is not None)
 
 
+# dX = dY[M, K] W[K, N] as an NT product dY . (W^T)^T against a transposed weight copy (transpose_bf16, 1-3 us per
+# BERT weight) with the residual gradient folded into the epilogue: measured faster than hipBLASLt's NN kernels and
+# much faster than its addmm (the GradSlot fold) on BERT-base's shapes at 4096 tokens
+# (profiles/gemm_dx_r4.jsonl): QKV 23.5 vs 30.3 (addmm 35.2) us, attention-out 10.4 vs 19.4, FFN-in 29.7 vs 39.2
+# (addmm 70.2). FFN-out (N = 3072) ties and stays on the library. (M, N, K) -> NT configuration.
+DX_NT_TUNED: dict[tuple[int, int, int], int] = {(4096, 768, 2304): 13, (4096, 768, 768): 12, (4096, 768, 3072): 13}
+
+
 def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tensor:
-    """dX = dY W (+ the residual gradient parked in `slot` as the C operand): the hand-written NN kernel where it
-    measured faster (NN_TUNED), else hipBLASLt."""
+    """dX = dY W (+ the residual gradient parked in `slot` as the C operand): the hand-written NT kernel against a
+    transposed weight copy where it measured faster (DX_NT_TUNED), the NN kernel where tuned (NN_TUNED), else
+    hipBLASLt."""
     g = None
     if slot is not None:
         g, slot.g = slot.g, None
@@ -253,7 +277,12 @@ def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tens
             raise RuntimeError("GradSlot empty: the residual gradient did not arrive before the projection's backward")
     M, K = dy2.shape
     N = w.shape[1]
-    native = (dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and nn_preferred(M, N, K))
+    ok = dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+    if ok and (M, N, K) in DX_NT_TUNED and os.environ.get("MIFX_HIP_GEMM_DX", "1") != "0":
+        native_stats.count("gemm_dX", True)
+        y, _ = gemm_nt(dy2, transpose(w), g, 3 if g is not None else 0, cfg=DX_NT_TUNED[(M, N, K)])
+        return y
+    native = ok and nn_preferred(M, N, K)
     native_stats.count("gemm_dX", native)
     if native:
         return gemm_nn(dy2, w, g)

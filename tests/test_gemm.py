@@ -173,3 +173,42 @@ def test_dx_routes_to_nn_kernel_and_matches_library(monkeypatch):
     slot.g = res
     got2 = torch.autograd.grad(gemm.linear(x, w, force=True, slot=slot), x, dy)[0]
     torch.testing.assert_close(got2.float(), (ref.float() + res.float()), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_transpose_and_add_r_epilogue():
+    """transpose_bf16 is exact; the NT kernel's R epilogue (epi 3) adds R before the single rounding."""
+    torch.manual_seed(9)
+    w = torch.randn(192, 320, device="cuda").to(torch.bfloat16)
+    assert torch.equal(gemm.transpose(w), w.t().contiguous())
+    M, N, K = 256, 192, 384
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    wt = ((torch.rand(N, K, device="cuda") * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+    r = (torch.rand(M, N, device="cuda") - 0.5).to(torch.bfloat16)
+    y, _ = gemm.gemm_nt(x, wt, r, 3, cfg=12)
+    ref = x.float() @ wt.float().t() + r.float()
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_dx_on_transposed_nt_matches_library(monkeypatch):
+    """_Linear's input gradient through the transposed-weight NT path (DX_NT_TUNED) equals the library's, with and
+    without the GradSlot residual fold."""
+    from mifx.ops import native_stats
+
+    torch.manual_seed(6)
+    M, K, N = 512, 384, 192
+    x = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16).requires_grad_()
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    ref = torch.autograd.grad(torch.nn.functional.linear(x, w), x, dy)[0]
+    monkeypatch.setitem(gemm.DX_NT_TUNED, (M, K, N), 12)
+    native_stats.reset()
+    got = torch.autograd.grad(gemm.linear(x, w, force=True), x, dy)[0]
+    assert native_stats.snapshot()["gemm_dX"]["native"] == 1
+    torch.testing.assert_close(got.float(), ref.float(), rtol=2e-2, atol=2e-2)
+    slot = gemm.GradSlot()
+    res = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    slot.g = res
+    got2 = torch.autograd.grad(gemm.linear(x, w, force=True, slot=slot), x, dy)[0]
+    torch.testing.assert_close(got2.float(), ref.float() + res.float(), rtol=2e-2, atol=2e-2)

@@ -67,8 +67,15 @@ def main():
         hip_ok = gconv.eligible(x, w, 1, pad, st)
         t = {}
         t["fwd_miopen"] = timeit(lambda: F.conv2d(x, w, None, stride=st, padding=pad))
-        t["dgrad_miopen"] = timeit(lambda: torch.nn.grad.conv2d_input(x.shape, w, dy, stride=st, padding=pad))
-        t["wgrad_miopen"] = timeit(lambda: torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=st, padding=pad))
+        # MIOpen through aten.convolution_backward, the op autograd runs (torch.nn.grad.conv2d_input / _weight take
+        # a slower path on channels-last bf16)
+        def mbwd(dg, wg):
+            return torch.ops.aten.convolution_backward(dy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                       [dg, wg, False])
+
+        t["dgrad_miopen"] = timeit(lambda: mbwd(True, False))
+        t["wgrad_miopen"] = timeit(lambda: mbwd(False, True))
+        t["bwd_both_miopen"] = timeit(lambda: mbwd(True, True))
         if hip_ok:
             w_fwd = w.view(1, K, C, R, R).permute(0, 1, 3, 4, 2).contiguous()
             t["fwd_hip"] = timeit(lambda: gconv._launch(x, w_fwd, None, B, Hi, Wi, 1, C, K, R, R, pad, False, st))
