@@ -164,6 +164,10 @@ class FusedWideDeepTrainer:
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
         self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
+        # next-step record prefetch (csrc/feed.h MifxPrefetch): the XCD-local slab reduction of step s gathers step
+        # s + 1's records into one contiguous buffer, so the fused kernel's first loads need no step -> feed ->
+        # record-address chain (MIFX_WD_PREFETCH=0 turns it off)
+        self._pre = self._pre_tag = None
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
         # grid <= #CUs, one workgroup per CU by its LDS). Measured SLOWER on MI355X and therefore off by default:
@@ -278,7 +282,9 @@ class FusedWideDeepTrainer:
             wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves,
                       self._xcd.xcd_of if (train and self._xcd is not None and slab is self.slab) else None,
-                      tile=self.tile if train else 128, feed=feed)
+                      tile=self.tile if train else 128, feed=feed,
+                      prefetch=(self._pre, self._pre_tag) if (train and self._pre is not None and slab is self.slab)
+                      else None)
         else:
             wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
@@ -293,6 +299,17 @@ class FusedWideDeepTrainer:
         self.n_data = self.records.shape[0]
         self.graph, self._graphs, self._fast = None, None, None
         self.graph_multi, self.graph_multi_steps = None, 1
+        self._setup_prefetch()
+
+    def _setup_prefetch(self) -> None:
+        if self._xcd is None or self.kernel != "chain" or os.environ.get("MIFX_WD_PREFETCH", "1") == "0":
+            return
+        if self._pre is None:
+            self._pre = torch.empty(self.batch, 32, dtype=torch.uint8, device=self.device)
+            self._pre_tag = torch.empty(1, dtype=torch.int64, device=self.device)
+        self._pre_tag.fill_(-1)  # new records: nothing prefetched yet
+        self._xcd.set_prefetch(self.records, self.n_data, self.batch, self.feed_args(), self._pre, self._pre_tag,
+                               self.step_ctr)
 
     @property
     def grad_scale(self) -> float:
