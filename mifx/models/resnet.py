@@ -20,9 +20,29 @@ from ..ops.pool import max_pool3s2
 _MODE = os.environ.get("MIFX_RESNET_HIP_CONV", "0")
 USE_HIP_CONV = _MODE != "0"
 
-# (input H, C in, K out, kernel, stride) -> (forward, input gradient, weight gradient) backend; shapes not listed
-# (e.g. the 3-channel stem) stay on MIOpen
-CONV_ROUTES: dict[tuple[int, int, int, int, int], tuple[str, str, str]] = {}
+# (input H, C in, K out, kernel, stride) -> (forward, input gradient, weight gradient) backend, measured per pass at
+# B = 256 with MIOpen through aten.convolution_backward (profiles/resnet_conv_routes_r4.jsonl): MIOpen's forward and
+# weight gradient win on every shape; the hand-written input gradient wins on the 17 shapes below (0.55 ms of the
+# 17.9 ms of convolution per step). Shapes not listed (and the 3-channel stem) stay on MIOpen.
+CONV_ROUTES: dict[tuple[int, int, int, int, int], tuple[str, str, str]] = {
+    (7, 2048, 512, 1, 1): ('miopen', 'hip', 'miopen'),
+    (14, 1024, 256, 1, 1): ('miopen', 'hip', 'miopen'),
+    (14, 1024, 512, 1, 1): ('miopen', 'hip', 'miopen'),
+    (14, 1024, 2048, 1, 2): ('miopen', 'hip', 'miopen'),
+    (28, 128, 128, 3, 1): ('miopen', 'hip', 'miopen'),
+    (28, 128, 512, 1, 1): ('miopen', 'hip', 'miopen'),
+    (28, 256, 256, 3, 2): ('miopen', 'hip', 'miopen'),
+    (28, 512, 128, 1, 1): ('miopen', 'hip', 'miopen'),
+    (28, 512, 256, 1, 1): ('miopen', 'hip', 'miopen'),
+    (28, 512, 1024, 1, 2): ('miopen', 'hip', 'miopen'),
+    (56, 64, 64, 1, 1): ('miopen', 'hip', 'miopen'),
+    (56, 64, 64, 3, 1): ('miopen', 'hip', 'miopen'),
+    (56, 64, 256, 1, 1): ('miopen', 'hip', 'miopen'),
+    (56, 128, 128, 3, 2): ('miopen', 'hip', 'miopen'),
+    (56, 256, 64, 1, 1): ('miopen', 'hip', 'miopen'),
+    (56, 256, 128, 1, 1): ('miopen', 'hip', 'miopen'),
+    (56, 256, 512, 1, 2): ('miopen', 'hip', 'miopen'),
+}
 
 
 class HipConv2d(nn.Conv2d):
@@ -37,8 +57,10 @@ class HipConv2d(nn.Conv2d):
             if _MODE == "routed":
                 r = CONV_ROUTES.get((x.shape[2], self.in_channels, self.out_channels, self.kernel_size[0],
                                      self.stride[0]))
-                if r is None or r[0] != "hip":
+                if r is None or "hip" not in r:
                     return super().forward(x)
+                if r[0] != "hip":  # MIOpen forward / weight gradient, hand-written input gradient
+                    return gconv.conv2d_hip_dgrad(x, self.weight, self.padding[0], self.stride[0])
                 route = (r[1], r[2])
             return gconv.conv2d(x, self.weight, self.bias, padding=self.padding[0], stride=self.stride[0],
                                 route=route)

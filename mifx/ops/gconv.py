@@ -147,6 +147,46 @@ class _GConv(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None
 
 
+class _LibFwdHipDgrad(torch.autograd.Function):
+    """Single-group convolution with MIOpen's forward and weight gradient and the hand-written input gradient (the
+    per-shape route where only the input gradient measured faster: profiles/resnet_conv_routes_r4.jsonl)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, pad, stride):
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wb = weight.to(torch.bfloat16)
+        y = torch.ops.aten.convolution(xb, wb, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
+        ctx.save_for_backward(xb, wb)
+        ctx.geo = (pad, stride, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        pad, stride, wdt = ctx.geo
+        N, C, Hi, Wi = xb.shape
+        K, _, R, S = wb.shape
+        dyb = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if stride == 1:
+                w_bwd = wb.view(1, K, C, R, S).flip(3, 4).permute(0, 2, 3, 4, 1).contiguous()
+                dx = _launch(dyb, w_bwd, None, N, dyb.shape[2], dyb.shape[3], 1, K, C, R, S, R - 1 - pad)
+            else:
+                dx = dgrad_strided(dyb, wb, N, Hi, Wi, 1, C, K, R, S, pad, stride)
+        if ctx.needs_input_grad[1]:
+            dw = _lib_bwd(xb, wb, dyb, stride, pad, 1, False, True)[1].to(wdt)
+        return dx, dw, None, None
+
+
+def conv2d_hip_dgrad(x: torch.Tensor, weight: torch.Tensor, padding: int, stride: int) -> torch.Tensor:
+    """MIOpen forward / weight gradient, hand-written input gradient (single group, C and K % 32, square kernel)."""
+    K, C, R, S = weight.shape
+    if x.is_cuda and C % 32 == 0 and K % 32 == 0 and R == S and 0 <= padding < R and _lib.gpu_available():
+        return _LibFwdHipDgrad.apply(x, weight, int(padding), int(stride))
+    return F.conv2d(x, weight, None, stride=stride, padding=padding)
+
+
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, padding: int = 0,
            groups: int = 1, relu: bool = False, stride: int = 1, route: tuple | None = None) -> torch.Tensor:
     """(Grouped, strided) convolution (`relu=True`: followed by ReLU, fused into the kernel's epilogue); the HIP

@@ -164,9 +164,11 @@ class FusedWideDeepTrainer:
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
         self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
-        # next-step record prefetch (csrc/feed.h MifxPrefetch): the XCD-local slab reduction of step s gathers step
-        # s + 1's records into one contiguous buffer, so the fused kernel's first loads need no step -> feed ->
-        # record-address chain (MIFX_WD_PREFETCH=0 turns it off)
+        # next-step record prefetch (csrc/feed.h MifxPrefetch, opt-in MIFX_WD_PREFETCH=1): the XCD-local slab
+        # reduction of step s gathers step s + 1's records into one contiguous buffer, so the fused kernel's first
+        # loads need no step -> feed -> record-address chain. Measured SLOWER at B = 65536 (32.7-32.9 vs
+        # 32.0-32.1 us per step, profiles/wd_prefetch_ab_r4.txt): the gather lengthens the reduction kernel by more
+        # than the fused kernel's prologue loses (its 3.6 us prologue is bound by the weight-image staging too)
         self._pre = self._pre_tag = None
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
@@ -302,7 +304,7 @@ class FusedWideDeepTrainer:
         self._setup_prefetch()
 
     def _setup_prefetch(self) -> None:
-        if self._xcd is None or self.kernel != "chain" or os.environ.get("MIFX_WD_PREFETCH", "1") == "0":
+        if self._xcd is None or self.kernel != "chain" or os.environ.get("MIFX_WD_PREFETCH", "0") != "1":
             return
         if self._pre is None:
             self._pre = torch.empty(self.batch, 32, dtype=torch.uint8, device=self.device)

@@ -131,8 +131,10 @@ def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single():
 def test_resnet_captured_step_matches_eager():
     """ResNetTrainer's hipGraph step (graph A: input kernel + forward + backward with device-side step, indices and
     learning rate; SGD captured with the learning rate read from a device tensor) follows the eager trainer: same
-    losses and weights up to the update's rounding (lr * g formed before the add), with MIOpen's deterministic
-    solvers. Includes a checkpoint restore in the middle (the graphs are re-captured after fresh eager steps)."""
+    losses and weights up to the update's rounding (lr * g formed before the add, where torch's SGD fuses it), with
+    MIOpen's deterministic solvers, at a learning rate where training is stable (at lr 0.05 this tiny problem
+    diverges and amplifies the one-ulp update differences: profiles/resnet_graph_diag_r4.jsonl). Includes a checkpoint
+    restore in the middle (the graphs are re-captured after fresh eager steps)."""
     import tempfile as _tf
 
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
@@ -140,7 +142,7 @@ def test_resnet_captured_step_matches_eager():
     imgs, labels = synthetic_imagenet(48, size=72, classes=10, seed=1)
 
     def run(graph, restore_at=None):
-        tr = ResNetTrainer(6, "cuda:0", imgs, labels, num_classes=10, lr=0.05, warmup_steps=4, crop=64, seed=5,
+        tr = ResNetTrainer(6, "cuda:0", imgs, labels, num_classes=10, lr=0.005, warmup_steps=4, crop=64, seed=5,
                            graph=graph, graph_warmup=2)
         torch.backends.cudnn.benchmark = False
         torch.backends.cudnn.deterministic = True
@@ -160,3 +162,26 @@ def test_resnet_captured_step_matches_eager():
     torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-3, atol=1e-3)
     for k in pe:
         torch.testing.assert_close(pg[k], pe[k], rtol=1e-3, atol=1e-4, msg=k)
+
+
+@pytest.mark.parametrize("shape", [(56, 64, 64, 3, 1), (56, 256, 64, 1, 1), (56, 128, 128, 3, 2), (28, 512, 1024, 1, 2)])
+def test_resnet_routed_dgrad_matches_miopen(shape):
+    """The routed ResNet convolution (MIOpen forward and weight gradient, hand-written input gradient: stride 1 on
+    the flipped-weight forward kernel, stride 2 on the phase-split kernel) against F.conv2d's autograd."""
+    from mifx.ops import gconv
+
+    Hi, C, K, R, st = shape
+    torch.manual_seed(sum(shape))
+    x = torch.randn(4, C, Hi, Hi, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * (C * R * R) ** -0.5).contiguous(memory_format=torch.channels_last)
+    pad = R // 2
+    xa, wa = x.clone().requires_grad_(), w.clone().requires_grad_()
+    y = gconv.conv2d_hip_dgrad(xa, wa, pad, st)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr = x.float().requires_grad_(), w.clone().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, None, stride=st, padding=pad)
+    yr.backward(g.float())
+    assert (y.float() - yr).abs().max().item() <= 2e-2 * yr.abs().max().item()
+    assert (xa.grad.float() - xr.grad).abs().max().item() <= 2e-2 * xr.grad.abs().max().item()
+    assert (wa.grad - wr.grad).abs().max().item() <= 2e-2 * wr.grad.abs().max().item()
