@@ -16,8 +16,9 @@ from ..ops.pool import max_pool3s2
 # Convolution backends (MIFX_RESNET_HIP_CONV): "routed" -- per shape and pass, the faster of the hand-written MFMA
 # implicit-GEMM kernels (csrc/gconv.hip: forward, stride-1 / phase-split strided input gradient, pixel-split weight
 # gradient) and MIOpen, from the measurement of every ResNet-50 convolution at B = 256 (CONV_ROUTES below,
-# tools/bench_resnet_convs.py); "1" -- every eligible pass on the HIP kernels (gconv's own policy); "0" -- MIOpen.
-_MODE = os.environ.get("MIFX_RESNET_HIP_CONV", "0")
+# tools/bench_resnet_convs.py; the default: 25.8 vs 26.2 ms per step at B = 256, profiles/resnet_routed_ab_r4.txt);
+# "1" -- every eligible pass on the HIP kernels (gconv's own policy); "0" -- MIOpen.
+_MODE = os.environ.get("MIFX_RESNET_HIP_CONV", "routed")
 USE_HIP_CONV = _MODE != "0"
 
 # (input H, C in, K out, kernel, stride) -> (forward, input gradient, weight gradient) backend, measured per pass at
