@@ -35,7 +35,10 @@ constexpr int BK = 64;
 
 // EPI_ADD_R: Y = X W^T + R (R bf16 [M, N], passed as `bias`): the input-gradient GEMM dX = dY W computed as an NT
 // product against a transposed weight copy, with the residual gradient folded in (mifx.ops.gemm.GradSlot)
-enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3 };
+// EPI_GELU_BWD: Y = dZ = (X W^T) o GELU'(Z + bias) with Z the saved pre-bias product of the FFN-in GEMM (read), plus
+// per-workgroup column sums of the stored dZ (the bias gradient) into part[M / BM][N]: the FFN-out input gradient
+// and the bias-GELU backward in one pass (the unfused path writes dGELU [M, N] and reads it back)
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3, EPI_GELU_BWD = 4 };
 
 // GELU(erf) with a branch-free erf (Abramowitz & Stegun 7.1.26: |error| <= 1.5e-7, far below the bf16 output's
 // 2^-9 relative step): the library erff evaluates piecewise polynomials selected per |x|, which diverge inside a
@@ -48,6 +51,9 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(r, x);
 }
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erf_fast(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -59,7 +65,8 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 template <int BM, int BN, int WM, int WN, int EPI, typename P, int OPT>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                             const P* __restrict__ bias, bf16* __restrict__ Y,
-                                                            bf16* __restrict__ Z, int M, int N, int K) {
+                                                            bf16* __restrict__ Z, int M, int N, int K,
+                                                            float* __restrict__ part) {
   constexpr int NT = 64 * WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
   // 16-byte DMA rounds per K-tile (a partial last round is skipped wave by wave: BM * 8 and BN * 8 are multiples of 64)
@@ -178,6 +185,59 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt(const bf16* __restric
   }
 
   // ---- epilogue: lane holds Y[m][n .. n + 3]
+  if constexpr (EPI == EPI_GELU_BWD) {
+    float cs[NR][4];
+#pragma unroll
+    for (int a = 0; a < NR; ++a) {
+      const int n = n0 + wn * TN + 16 * a + 4 * fc;
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bv[r] = (float)bias[n + r];
+        cs[a][r] = 0.f;
+      }
+#pragma unroll
+      for (int b = 0; b < MR; ++b) {
+        const int m = m0 + wm * TM + 16 * b + fr;
+        const v4bf zv = *(const v4bf*)(Z + (size_t)m * N + n);
+        v4bf o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[r] = (bf16)(acc[a][b][r] * gelu_grad_f((float)zv[r] + bv[r]));
+          cs[a][r] += (float)o[r];  // the bias gradient of the value actually stored
+        }
+        *(v4bf*)(Y + (size_t)m * N + n) = o;
+      }
+    }
+    // column sums: over the 16 rows of a lane group (xor tree), then over the WM row-waves in order (LDS)
+#pragma unroll
+    for (int a = 0; a < NR; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cs[a][r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        cs[a][r] = v;
+      }
+    __syncthreads();  // every wave is past its last LDS fragment read
+    float* red = (float*)lds;  // [WM][BN]
+    if (fr == 0) {
+#pragma unroll
+      for (int a = 0; a < NR; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wm * BN + wn * TN + 16 * a + 4 * fc + r] = cs[a][r];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) t += red[i * BN + c];
+      part[(size_t)(m0 / BM) * N + n0 + c] = t;
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < NR; ++a) {
     const int n = n0 + wn * TN + 16 * a + 4 * fc;
@@ -212,7 +272,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt(const bf16* __restric
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, typename P, int OPT>
-int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, hipStream_t st) {
+int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, hipStream_t st,
+           float* part = nullptr) {
   constexpr int LDS = ((OPT & 4) ? 3 : 2) * (BM + BN) * BK * 2;
   static bool attr = false;
   if (!attr) {
@@ -221,13 +282,16 @@ int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int
     attr = true;
   }
   hipLaunchKernelGGL((gemm_nt<BM, BN, WM, WN, EPI, P, OPT>), dim3((M / BM) * (N / BN)), dim3(64 * WM * WN), LDS, st,
-                     (const bf16*)X, (const bf16*)W, (const P*)bias, (bf16*)Y, (bf16*)Z, M, N, K);
+                     (const bf16*)X, (const bf16*)W, (const P*)bias, (bf16*)Y, (bf16*)Z, M, N, K, part);
   return (int)hipGetLastError();
 }
 
 template <int BM, int BN, int WM, int WN, int OPT>
 int dispatch_epi(int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N,
-                 int K, hipStream_t st) {
+                 int K, hipStream_t st, float* part = nullptr) {
+  if (epi == EPI_GELU_BWD)
+    return bias_f32 ? launch<BM, BN, WM, WN, EPI_GELU_BWD, float, OPT>(X, W, bias, Y, Z, M, N, K, st, part)
+                    : launch<BM, BN, WM, WN, EPI_GELU_BWD, bf16, OPT>(X, W, bias, Y, Z, M, N, K, st, part);
   if (epi == EPI_NONE) return launch<BM, BN, WM, WN, EPI_NONE, bf16, OPT>(X, W, nullptr, Y, nullptr, M, N, K, st);
   if (epi == EPI_ADD_R) return launch<BM, BN, WM, WN, EPI_ADD_R, bf16, OPT>(X, W, bias, Y, nullptr, M, N, K, st);
   if (epi == EPI_BIAS)
@@ -275,6 +339,29 @@ __global__ __launch_bounds__(256) void transpose_bf16(const bf16* __restrict__ s
 }  // namespace
 
 extern "C" {
+
+// dZ[M, N] = (X[M, K] . W[N, K]^T) o GELU'(Z + bias) (bf16 out), part[M / BM][N] = per-tile column sums of the
+// stored dZ (fp32). Z: bf16 [M, N] (the saved pre-bias product), bias bf16 or fp32 [N]. cfg: index into
+// mifx_gemm_configs; M % BM == 0, N % BN == 0, K % 64 == 0.
+int mifx_gemm_nt_gelu_bwd(int cfg, int bias_f32, const void* X, const void* W, const void* bias, const void* Z,
+                          void* Y, float* part, int M, int N, int K, hipStream_t st) {
+  const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
+  if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || X == nullptr || W == nullptr || Y == nullptr ||
+      Z == nullptr || bias == nullptr || part == nullptr)
+    return -1;
+  const Cfg c = kCfgs[cfg];
+  if (M % c.bm || N % c.bn || K % BK) return -1;
+  if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 8 || (uintptr_t)Z % 8) return -1;
+  if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;
+  void* z = const_cast<void*>(Z);
+  switch (cfg) {
+    case 9: return dispatch_epi<256, 192, 2, 4, 3>(EPI_GELU_BWD, bias_f32, X, W, bias, Y, z, M, N, K, st, part);
+    case 11: return dispatch_epi<128, 96, 2, 2, 3>(EPI_GELU_BWD, bias_f32, X, W, bias, Y, z, M, N, K, st, part);
+    case 12: return dispatch_epi<128, 96, 2, 2, 1>(EPI_GELU_BWD, bias_f32, X, W, bias, Y, z, M, N, K, st, part);
+    case 7: return dispatch_epi<128, 128, 2, 2, 1>(EPI_GELU_BWD, bias_f32, X, W, bias, Y, z, M, N, K, st, part);
+    default: return -2;  // configuration without a GELU-backward build
+  }
+}
 
 // dst [C, R] = src [R, C]^T, bf16; R % 64 == 0, C % 64 == 0, 16-byte aligned
 int mifx_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t st) {

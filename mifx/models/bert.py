@@ -130,13 +130,11 @@ class BertLayer(nn.Module):
         a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) if hip else self.attn_out(ctx, add_bias=False)
         x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
                                           rng, site, slot=slot_a)
-        if hip:
-            f = hg.linear_bias_gelu(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias, slot=slot_f)
+        if hip:  # FFN-in + GELU + FFN-out as one autograd node (the dH GEMM and the GELU backward fused)
+            o = reduce_from_tp(hg.ffn(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias,
+                                      self.ffn_out.weight, slot=slot_f), self.tp)
         else:
             f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
-        if hip:
-            o = reduce_from_tp(hg.linear(f, self.ffn_out.weight), self.tp)
-        else:
             o = self.ffn_out(f, add_bias=False)
         return fb.bias_dropout_add_layernorm(o, self.ffn_out.bias, x, self.ln2.weight, self.ln2.bias, c.ln_eps, drop,
                                              rng, site + 1, slot=slot_f)

@@ -29,6 +29,7 @@ def _fns():
         "configs": sig(lib, "mifx_gemm_configs", [VP, I32]),
         "nt": sig(lib, "mifx_gemm_nt", [I32, I32, I32, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
         "tr": sig(lib, "mifx_transpose_bf16", [VP, VP, I32, I32, VP]),
+        "gelu_bwd": sig(lib, "mifx_gemm_nt_gelu_bwd", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
     }
 
 
@@ -475,3 +476,89 @@ def matmul_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     native_stats.count("gemm_f32", True)
     check(_f32_fns()["nn"](ptr(a), ptr(b), ptr(c), M, N, K, K, N, N, stream_handle(a.device)), "mifx_gemm_f32_nn")
     return c
+
+
+# ---------------------------------------------------------------- fused FFN block (BERT): one autograd node
+# FFN-out's input gradient dH = dOut W2 and FFN-in's bias-GELU backward dZ = dH o GELU'(Z + b1) in ONE GEMM
+# (csrc/gemm.hip EPI_GELU_BWD on the transposed W2 copy): the unfused path writes dH [tokens, 3072] and the
+# bias_gelu backward kernel reads it back with Z. (M, N, K) of the dH GEMM -> NT configuration.
+GELU_BWD_TUNED: dict[tuple[int, int, int], int] = {(4096, 3072, 768): 9}
+
+
+def _gelu_bwd_gemm(dout2: torch.Tensor, w2: torch.Tensor, z: torch.Tensor, b1: torch.Tensor, cfg: int):
+    """dZ = (dOut W2) o GELU'(Z + b1) and db1 = column sums of dZ: dout2 [M, K], w2 [K, N] (the FFN-out weight
+    [out, in]), z [M, N] bf16."""
+    M, K = dout2.shape
+    N = w2.shape[1]
+    bm = configs()[cfg][0]
+    bp = b1 if b1.dtype in (torch.float32, torch.bfloat16) else b1.float()
+    dz = torch.empty(M, N, device=dout2.device, dtype=torch.bfloat16)
+    part = torch.empty(M // bm, N, device=dout2.device, dtype=torch.float32)
+    check(_fns()["gelu_bwd"](int(cfg), int(bp.dtype == torch.float32), ptr(dout2.contiguous()), ptr(transpose(w2)),
+                             ptr(bp.contiguous()), ptr(z), ptr(dz), ptr(part), M, N, K,
+                             stream_handle(dout2.device)), "mifx_gemm_nt_gelu_bwd")
+    from .fused_bert import col_sum
+
+    return dz, col_sum(part, b1.dtype if b1.dtype in (torch.float32, torch.bfloat16) else torch.float32)
+
+
+class _FFN(torch.autograd.Function):
+    """out = GELU(x W1^T + b1) W2^T (no FFN-out bias: the caller fuses it into the next add + LayerNorm)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, slot=None):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        from .fused_bert import _fns as fb_fns, _dt, _param
+
+        if preferred(x2, w1):
+            y1, z = gemm_nt(x2, w1, b1, 2)
+        else:
+            z = F.linear(x2, w1)
+            bp = _param(b1)
+            y1 = torch.empty_like(z)
+            N = z.shape[-1]
+            check(fb_fns()["gelu"](_dt(z), _dt(bp), 1, None, ptr(z), ptr(bp), z.numel() // N, N, ptr(y1), None,
+                                   None, stream_handle(z.device)), "mifx_bert_bias_gelu")
+        native_stats.count("gemm_fwd_bias_gelu", preferred(x2, w1))
+        fwd2 = preferred(y1, w2)
+        native_stats.count("gemm_fwd", fwd2)
+        out = gemm_nt(y1, w2)[0] if fwd2 else F.linear(y1, w2)
+        ctx.save_for_backward(x2, w1, b1, z, y1, w2)
+        ctx.slot = slot
+        return out.view(*shp[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, w1, b1, z, y1, w2 = ctx.saved_tensors
+        dout2 = dout.reshape(-1, dout.shape[-1]).to(y1.dtype).contiguous()
+        dw2 = _dw(dout2, y1)
+        M, K = dout2.shape
+        N = w2.shape[1]
+        cfg = GELU_BWD_TUNED.get((M, N, K))
+        if cfg is not None and os.environ.get("MIFX_HIP_GELU_BWD", "1") != "0":
+            native_stats.count("gemm_dX_gelu_bwd", True)
+            dz, db1 = _gelu_bwd_gemm(dout2, w2, z, b1, cfg)
+        else:
+            native_stats.count("gemm_dX_gelu_bwd", False)
+            dh = _dx(dout2, w2, None)
+            from .fused_bert import _fns as fb_fns, _dt, _param
+
+            bp = _param(b1)
+            dz = torch.empty_like(z)
+            part = torch.empty(fb_fns()["gchunks"](M), N, device=z.device, dtype=torch.float32)
+            db1 = torch.empty(N, device=z.device, dtype=bp.dtype)
+            check(fb_fns()["gelu"](_dt(z), _dt(bp), 0, ptr(dh.to(z.dtype).contiguous()), ptr(z), ptr(bp), M, N,
+                                   ptr(dz), ptr(part), ptr(db1), stream_handle(z.device)), "mifx_bert_bias_gelu")
+        dw1 = _dw(dz, x2)
+        dx = _dx(dz, w1, ctx.slot).view(*dout.shape[:-1], w1.shape[1]) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1.to(b1.dtype), dw2, None
+
+
+def ffn(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+        slot: GradSlot | None = None) -> torch.Tensor:
+    """GELU(x W1^T + b1) W2^T as one autograd node on the GPU (bf16): the FFN-out input gradient and the bias-GELU
+    backward fused into one GEMM where tuned (GELU_BWD_TUNED); elsewhere the two-node composition."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16:
+        return _FFN.apply(x, w1, b1, w2, slot)
+    return linear(linear_bias_gelu(x, w1, b1, slot=slot), w2)

@@ -212,3 +212,39 @@ def test_dx_on_transposed_nt_matches_library(monkeypatch):
     slot.g = res
     got2 = torch.autograd.grad(gemm.linear(x, w, force=True, slot=slot), x, dy)[0]
     torch.testing.assert_close(got2.float(), ref.float() + res.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [True, False])
+def test_ffn_block_matches_fp32_reference(monkeypatch, fused):
+    """gemm.ffn (one autograd node: FFN-in + bias + GELU + FFN-out) against the fp32 composition: forward, the input
+    gradient (with a GradSlot residual), both weight gradients and the bias gradient; fused = the dH GEMM with the
+    GELU-backward epilogue and in-kernel bias-gradient partials, else dH then the bias_gelu backward kernel."""
+    from mifx.ops import native_stats
+
+    torch.manual_seed(11)
+    M, H, I = 512, 192, 384
+    if fused:
+        monkeypatch.setitem(gemm.GELU_BWD_TUNED, (M, I, H), 9)
+    else:
+        monkeypatch.setenv("MIFX_HIP_GELU_BWD", "0")
+    x = (torch.randn(M, H, device="cuda") * 0.7).to(torch.bfloat16).requires_grad_()
+    w1 = (torch.randn(I, H, device="cuda") * H ** -0.5).to(torch.bfloat16).requires_grad_()
+    b1 = (torch.randn(I, device="cuda") * 0.1).to(torch.bfloat16).requires_grad_()
+    w2 = (torch.randn(H, I, device="cuda") * I ** -0.5).to(torch.bfloat16).requires_grad_()
+    res = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+    slot = gemm.GradSlot()
+    native_stats.reset()
+    out = gemm.ffn(x, w1, b1, w2, slot=slot)
+    g = torch.randn_like(out)
+    slot.g = res
+    out.backward(g)
+    assert native_stats.snapshot()["gemm_dX_gelu_bwd"] == {"native": int(fused), "fallback": int(not fused)}
+    xr, w1r, b1r, w2r = (t.detach().float().requires_grad_() for t in (x, w1, b1, w2))
+    ref = torch.nn.functional.gelu(xr @ w1r.t() + b1r) @ w2r.t()
+    ref.backward(g.float())
+    torch.testing.assert_close(out.float(), ref, rtol=3e-2, atol=3e-2)
+    for got, want, name in ((x.grad.float(), xr.grad + res.float(), "dx"), (w1.grad.float(), w1r.grad, "dw1"),
+                            (b1.grad.float(), b1r.grad, "db1"), (w2.grad.float(), w2r.grad, "dw2")):
+        err = (got - want).norm() / want.norm()
+        assert err < 2e-2, f"{name}: relative error {err:.4f}"

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_rehearsal.log 2>&1 || { echo "pytest failed"; grep -E "Error|assert|FAILED|error" gpurun_out/pytest_rehearsal.log | tail -30; tail -5 gpurun_out/pytest_rehearsal.log; exit 1; }
+timeout -k 10 1050 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_rehearsal.log 2>&1 || { echo "pytest failed"; grep -E "Error|assert|FAILED|error" gpurun_out/pytest_rehearsal.log | tail -30; tail -5 gpurun_out/pytest_rehearsal.log; exit 1; }
 tail -1 gpurun_out/pytest_rehearsal.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_rehearsal.log 2>&1 || { tail -20 gpurun_out/smoke_rehearsal.log; exit 1; }
 tail -1 gpurun_out/smoke_rehearsal.log
