@@ -131,9 +131,8 @@ def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single():
 def test_resnet_captured_step_matches_eager():
     """ResNetTrainer's hipGraph step (graph A: input kernel + forward + backward with device-side step, indices and
     learning rate; SGD captured with the learning rate read from a device tensor) against ONE eager step from the
-    same state: the same loss and the same parameter update up to numerics (MIOpen may pick other bf16 solvers
-    under stream capture; trajectories of this tiny problem then drift apart, profiles/resnet_graph_diag_r4.jsonl,
-    so the check is per step). A checkpoint restore drops the graphs and re-captures them after fresh eager steps."""
+    same state: the same loss and the same parameter update up to the update's rounding (the check is per step:
+    trajectories of this tiny problem are chaotic, profiles/resnet_graph_diag_r4.jsonl). A checkpoint restore drops the graphs and re-captures them after fresh eager steps."""
     import tempfile as _tf
 
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
@@ -144,6 +143,9 @@ def test_resnet_captured_step_matches_eager():
         tr = ResNetTrainer(6, "cuda:0", imgs, labels, num_classes=10, lr=0.01, warmup_steps=4, crop=64, seed=5,
                            graph=graph, graph_warmup=2)
         torch.backends.cudnn.benchmark = False
+        # MIOpen's default bf16 solvers are not run-to-run reproducible; with its deterministic ones the captured and
+        # the eager update agree to ~2e-7 (profiles/resnet_graph_diag2_r4.jsonl)
+        torch.backends.cudnn.deterministic = True
         return tr
 
     trg = make(True)
@@ -158,10 +160,10 @@ def test_resnet_captured_step_matches_eager():
     tre.load_state_dict(ck)
     le = float(tre.step())  # the same step, eager, from the same state
     pe = {k: v.detach().float().clone() for k, v in tre.model.named_parameters()}
-    assert abs(lg - le) <= 1e-2 * abs(le), (lg, le)
+    assert abs(lg - le) <= 1e-4 * abs(le), (lg, le)
     num = sum(float((pg[k] - pe[k]).norm() ** 2) for k in p0) ** 0.5
     den = sum(float((pe[k] - p0[k]).norm() ** 2) for k in p0) ** 0.5
-    assert den > 0 and num <= 0.05 * den, (num, den)
+    assert den > 0 and num <= 1e-4 * den, (num, den)
     with _tf.TemporaryDirectory() as d:
         trg.restore(trg.save_checkpoint(d))
     assert trg._gA is None
