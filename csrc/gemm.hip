@@ -314,10 +314,9 @@ constexpr Cfg kCfgs[] = {{256, 256, 0}, {256, 128, 0}, {128, 128, 0}, {128, 256,
 
 // dst[C][R] = src[R][C] (bf16), 64 x 64 tiles through LDS: 16-byte loads along src rows, 16-byte stores along dst
 // rows (8 consecutive src rows of one column gathered from LDS). The transposed weight copy of the dX GEMMs.
-__global__ __launch_bounds__(256) void transpose_bf16(const bf16* __restrict__ src, bf16* __restrict__ dst, int R,
-                                                      int C) {
-  __shared__ bf16 t[64][64 + 2];
-  const int nbc = C / 64, r0 = (blockIdx.x / nbc) * 64, c0 = (blockIdx.x % nbc) * 64;
+__device__ __forceinline__ void transpose_tile(const bf16* __restrict__ src, bf16* __restrict__ dst, int R, int C,
+                                               int tile, bf16 (*t)[64 + 2]) {
+  const int nbc = C / 64, r0 = (tile / nbc) * 64, c0 = (tile % nbc) * 64;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = i * 256 + threadIdx.x, row = q >> 3, ch = q & 7;
@@ -334,6 +333,26 @@ __global__ __launch_bounds__(256) void transpose_bf16(const bf16* __restrict__ s
     for (int e = 0; e < 8; ++e) v[e] = t[8 * ch + e][col];
     *(v8bf*)(dst + (size_t)(c0 + col) * R + r0 + 8 * ch) = v;
   }
+}
+
+__global__ __launch_bounds__(256) void transpose_bf16(const bf16* __restrict__ src, bf16* __restrict__ dst, int R,
+                                                      int C) {
+  __shared__ bf16 t[64][64 + 2];
+  transpose_tile(src, dst, R, C, blockIdx.x, t);
+}
+
+// every weight of a model in one launch (mifx.ops.gemm.TransposeCache): entry e covers tiles [tile0, next tile0)
+struct TrEntry {
+  const bf16* src;
+  bf16* dst;
+  int R, C, tile0, pad;
+};
+__global__ __launch_bounds__(256) void transpose_batch(const TrEntry* __restrict__ ents, int n) {
+  __shared__ bf16 t[64][64 + 2];
+  int e = 0;
+  while (e + 1 < n && ents[e + 1].tile0 <= (int)blockIdx.x) ++e;
+  const TrEntry E = ents[e];
+  transpose_tile(E.src, E.dst, E.R, E.C, (int)blockIdx.x - E.tile0, t);
 }
 
 }  // namespace
@@ -361,6 +380,14 @@ int mifx_gemm_nt_gelu_bwd(int cfg, int bias_f32, const void* X, const void* W, c
     case 7: return dispatch_epi<128, 128, 2, 2, 1>(EPI_GELU_BWD, bias_f32, X, W, bias, Y, z, M, N, K, st, part);
     default: return -2;  // configuration without a GELU-backward build
   }
+}
+
+// n transposes in one launch: ents = device array of TrEntry {src, dst, R, C, tile0, 0} with tile0 the running sum
+// of (R / 64) (C / 64); every R, C % 64 == 0, 16-byte aligned
+int mifx_transpose_bf16_batch(const void* ents, int n, int total_tiles, hipStream_t st) {
+  if (ents == nullptr || n <= 0 || total_tiles <= 0) return -1;
+  hipLaunchKernelGGL(transpose_batch, dim3(total_tiles), dim3(256), 0, st, (const TrEntry*)ents, n);
+  return (int)hipGetLastError();
 }
 
 // dst [C, R] = src [R, C]^T, bf16; R % 64 == 0, C % 64 == 0, 16-byte aligned

@@ -30,7 +30,70 @@ def _fns():
         "nt": sig(lib, "mifx_gemm_nt", [I32, I32, I32, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
         "tr": sig(lib, "mifx_transpose_bf16", [VP, VP, I32, I32, VP]),
         "gelu_bwd": sig(lib, "mifx_gemm_nt_gelu_bwd", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
+        "tr_batch": sig(lib, "mifx_transpose_bf16_batch", [VP, I32, I32, VP]),
     }
+
+
+class TransposeCache:
+    """Transposed copies of a model's projection weights, refreshed in ONE launch after every optimizer step
+    (csrc/gemm.hip transpose_batch), for the dX GEMMs that run as NT products against W^T. Refreshing per step in
+    one kernel replaces a transpose launch per weight in the backward (47 per BERT-base step, ~200 us:
+    profiles/bert_steady_r4b.md). The owner (BertTrainer) calls refresh() after every update of the weights and runs
+    its backward inside `use_transposes(cache)`."""
+
+    def __init__(self, weights):
+        self.items = {}
+        rows, tile0 = [], 0
+        for w in weights:
+            R, C = w.shape
+            if not (w.is_cuda and w.dtype == torch.bfloat16 and w.is_contiguous() and R % 64 == 0 and C % 64 == 0):
+                continue
+            wt = torch.empty(C, R, device=w.device, dtype=torch.bfloat16)
+            self.items[w.data_ptr()] = (tuple(w.shape), wt, w)
+            rows.append([w.data_ptr(), wt.data_ptr(), R + (C << 32), tile0])
+            tile0 += (R // 64) * (C // 64)
+        self.n, self.tiles = len(rows), tile0
+        self.table = torch.tensor(rows, dtype=torch.int64).to(next(iter(self.items.values()))[1].device) \
+            if rows else None
+
+    def refresh(self) -> None:
+        if self.n:
+            check(_fns()["tr_batch"](ptr(self.table), self.n, self.tiles, stream_handle(self.table.device)),
+                  "mifx_transpose_bf16_batch")
+
+    def get(self, w: torch.Tensor) -> torch.Tensor | None:
+        e = self.items.get(w.data_ptr())
+        return e[1] if e is not None and e[0] == tuple(w.shape) else None
+
+
+class use_transposes:
+    """Context: _dx / the fused FFN backward take W^T from `cache` (None: no-op) while it is active -- the owner's
+    backward runs inside it, so a cache is never consulted for another model's weights."""
+
+    def __init__(self, cache: TransposeCache | None):
+        self.cache = cache
+
+    def __enter__(self):
+        if self.cache is not None:
+            _TCACHES.append(self.cache)
+        return self
+
+    def __exit__(self, *exc):
+        if self.cache is not None:
+            _TCACHES.remove(self.cache)
+        return False
+
+
+_TCACHES: list[TransposeCache] = []
+
+
+def transposed(w: torch.Tensor) -> torch.Tensor:
+    """W^T for an NT dX GEMM: the active TransposeCache's copy when it holds w, else a fresh transpose."""
+    for c in _TCACHES:
+        wt = c.get(w)
+        if wt is not None:
+            return wt
+    return transpose(w)
 
 
 def transpose(w: torch.Tensor) -> torch.Tensor:
@@ -281,7 +344,7 @@ def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tens
     ok = dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
     if ok and (M, N, K) in DX_NT_TUNED and os.environ.get("MIFX_HIP_GEMM_DX", "1") != "0":
         native_stats.count("gemm_dX", True)
-        y, _ = gemm_nt(dy2, transpose(w), g, 3 if g is not None else 0, cfg=DX_NT_TUNED[(M, N, K)])
+        y, _ = gemm_nt(dy2, transposed(w), g, 3 if g is not None else 0, cfg=DX_NT_TUNED[(M, N, K)])
         return y
     native = ok and nn_preferred(M, N, K)
     native_stats.count("gemm_dX", native)
@@ -494,7 +557,7 @@ def _gelu_bwd_gemm(dout2: torch.Tensor, w2: torch.Tensor, z: torch.Tensor, b1: t
     bp = b1 if b1.dtype in (torch.float32, torch.bfloat16) else b1.float()
     dz = torch.empty(M, N, device=dout2.device, dtype=torch.bfloat16)
     part = torch.empty(M // bm, N, device=dout2.device, dtype=torch.float32)
-    check(_fns()["gelu_bwd"](int(cfg), int(bp.dtype == torch.float32), ptr(dout2.contiguous()), ptr(transpose(w2)),
+    check(_fns()["gelu_bwd"](int(cfg), int(bp.dtype == torch.float32), ptr(dout2.contiguous()), ptr(transposed(w2)),
                              ptr(bp.contiguous()), ptr(z), ptr(dz), ptr(part), M, N, K,
                              stream_handle(dout2.device)), "mifx_gemm_nt_gelu_bwd")
     from .fused_bert import col_sum

@@ -91,6 +91,15 @@ class BertTrainer:
         else:
             self.opt = torch.optim.AdamW(self.model.parameters(), lr=lr, weight_decay=0.01, fused=cuda,
                                          capturable=self.use_graph)
+        # transposed copies of the projection weights for the dX GEMMs, refreshed in one launch after each update
+        self.tcache = None
+        if self.flat:
+            from ..ops import gemm as hg
+
+            ws = [m.weight for layer in self.model.layers for m in (layer.qkv, layer.attn_out, layer.ffn_in,
+                                                                      layer.ffn_out)]
+            self.tcache = hg.TransposeCache(ws)
+            self.tcache.refresh()
         self.data = synthetic_batch(cfg, batch, seq, self.device)
         self.amp = cuda
         self.sdpa = sdpa  # None = PyTorch's choice; "math" / "efficient" / "flash" pins the SDPA backend
@@ -125,15 +134,18 @@ class BertTrainer:
                             cache_enabled=not self.use_graph), self._sdpa_ctx():
             logits = self.model(ids, tt, am)
         loss = F.cross_entropy(logits.float(), y)
-        if self.async_dw:  # weight-gradient GEMMs on a side stream beside the backward's dX chain
-            from ..ops import gemm as hg
+        from ..ops import gemm as hg
 
-            with hg.async_weight_grads():
+        with hg.use_transposes(self.tcache):
+            if self.async_dw:  # weight-gradient GEMMs on a side stream beside the backward's dX chain
+                with hg.async_weight_grads():
+                    loss.backward()
+                hg.join_weight_grads(self.device)
+            else:
                 loss.backward()
-            hg.join_weight_grads(self.device)
-        else:
-            loss.backward()
         self.opt.step()
+        if self.tcache is not None:
+            self.tcache.refresh()
         return loss.detach()
 
     def _sdpa_ctx(self):

@@ -248,3 +248,22 @@ def test_ffn_block_matches_fp32_reference(monkeypatch, fused):
                             (b1.grad.float(), b1r.grad, "db1"), (w2.grad.float(), w2r.grad, "dw2")):
         err = (got - want).norm() / want.norm()
         assert err < 2e-2, f"{name}: relative error {err:.4f}"
+
+
+@pytest.mark.gpu
+def test_transpose_cache_batch_refresh():
+    """TransposeCache: every registered weight transposed in one launch; refresh() after an in-place update; used by
+    _dx only inside use_transposes()."""
+    torch.manual_seed(12)
+    ws = [torch.randn(r, c, device="cuda").to(torch.bfloat16) for r, c in ((192, 320), (64, 64), (768, 128))]
+    tc = gemm.TransposeCache(ws)
+    tc.refresh()
+    for w in ws:
+        assert torch.equal(tc.get(w), w.t().contiguous())
+    ws[0].mul_(2)
+    assert not torch.equal(tc.get(ws[0]), ws[0].t().contiguous())  # stale until refreshed
+    tc.refresh()
+    assert torch.equal(tc.get(ws[0]), ws[0].t().contiguous())
+    assert gemm.transposed(ws[1]) is not tc.get(ws[1])  # inactive: a fresh transpose
+    with gemm.use_transposes(tc):
+        assert gemm.transposed(ws[1]) is tc.get(ws[1])
