@@ -134,18 +134,6 @@ MIFX_HD MifxFeedStep mifx_feed_step(const MifxFeed& f, long long step, long long
   s.ek1 = f.key ? mifx_epoch_key(f.key, (uint64_t)e + 1) : 0;
   return s;
 }
-// Records of the NEXT training step gathered ahead of time (csrc/wide_deep.hip wd_reduce_xcd, the previous step's
-// slab reduction) into a contiguous [batch] buffer of 32-byte records, stamped with the step they belong to; the
-// fused kernel loads its rows from it beside the step counter instead of step -> feed -> record address -> load.
-struct MifxPrefetch {
-  const void* data;          // the resident records (uint4 pairs)
-  long long n_data, batch;
-  MifxFeed feed;
-  void* buf;                 // [batch] records (uint4 pairs); null: no prefetch
-  long long* tag;            // the step whose records buf holds (-1: none)
-  const long long* step_ctr;  // the trainer's step counter (slot 0)
-};
-
 // record of batch row `row` (0 <= row < batch <= n)
 MIFX_HD long long mifx_feed_record(const MifxFeed& f, const MifxFeedStep& s, long long row, long long n) {
   long long i = s.i0 + row, e = s.e0;

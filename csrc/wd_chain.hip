@@ -554,8 +554,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
                                                      float* __restrict__ logits_out, float grad_scale,
                                                      const int* __restrict__ tmap, int stride,
                                                      int* __restrict__ xcd_of, TailArgs ta, MifxFeed feed,
-                                                     const uint4* __restrict__ pre,
-                                                     const long long* __restrict__ pre_tag) {
+                                                     uint4* pre, long long* pre_tag) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LSEND);
   float* red = wgrad + WIDE_PAD;
@@ -612,11 +611,11 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     __syncthreads();
   }
 
-  // this step's records, gathered by the previous step's slab reduction (MifxPrefetch): loaded now, beside the step
+  // this step's records, gathered by this workgroup index in the previous step (below): loaded now, beside the step
   // counter and the buffer's tag, so the first records do not wait for step -> feed -> record address
   constexpr int EPW0 = 16 * TBN;
   const bool has_pre = TRAIN && !PERSIST && pre != nullptr && step_ctr != nullptr;
-  uint4 pu[TBN][2];
+  uint4 pu[TBN][2], nx[TBN][2];
   long long ptag = -1;
   if (has_pre) {
     ptag = *pre_tag;
@@ -688,18 +687,25 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
 #pragma unroll
     for (int tb = 0; tb < TBN; ++tb) {
       const long long row = min((long long)it * T + EPW * w + 16 * tb + r, batch - 1);
-      if (use_pre) {
-        u[tb][0] = pre[2 * row];
-        u[tb][1] = pre[2 * row + 1];
-      } else {
-        const long long di = mifx_feed_record(fd, fs, row, n_data);  // host guarantees batch <= n_data
-        u[tb][0] = data[2 * di];
-        u[tb][1] = data[2 * di + 1];
-      }
+      const long long di = mifx_feed_record(fd, fs, row, n_data);  // host guarantees batch <= n_data
+      u[tb][0] = data[2 * di];
+      u[tb][1] = data[2 * di + 1];
     }
   };
+  // the NEXT step's records for this workgroup's first rows: loaded now (their latency hides under the step) and
+  // stored to the prefetch buffer at the end, where the next step's workgroup of the same index reads them
+  if (has_pre) {
+    const MifxFeedStep fsn = mifx_feed_step(fd, step0 + 1, n_data);
+#pragma unroll
+    for (int tb = 0; tb < TBN; ++tb) {
+      const long long row = min((long long)blockIdx.x * T + EPW0 * w + 16 * tb + r, batch - 1);
+      const long long di = mifx_feed_record(fd, fsn, row, n_data);
+      nx[tb][0] = data[2 * di];
+      nx[tb][1] = data[2 * di + 1];
+    }
+  }
   uint4 nu[TBN][2];
-  if (use_pre) {
+  if (use_pre) {  // the first iteration's rows (later iterations of a multi-iteration workgroup use the feed)
 #pragma unroll
     for (int tb = 0; tb < TBN; ++tb) {
       nu[tb][0] = pu[tb][0];
@@ -1064,6 +1070,17 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   if constexpr (PERSIST) {
     for (int i = tid; i < STEP_SLOTS; i += NTHR) ta.step_slots[i] = step0 + nsteps;
   }
+  if (has_pre) {  // the next step's first records (rows of this workgroup index only: no other workgroup reads them)
+#pragma unroll
+    for (int tb = 0; tb < TBN; ++tb) {
+      const long long row = min((long long)blockIdx.x * T + EPW0 * w + 16 * tb + r, batch - 1);
+      pre[2 * row] = nx[tb][0];
+      pre[2 * row + 1] = nx[tb][1];
+    }
+    // read by the next launch (a workgroup of this launch that reads it late sees step0 + 1 != its step and takes
+    // the feed path: slower, never wrong)
+    if (blockIdx.x == 0 && tid == 0) *pre_tag = step0 + 1;
+  }
   STAMP(17);
   BSTAMP(2);
   if constexpr (TRAIN && TAIL) {
@@ -1173,7 +1190,7 @@ template <bool TRAIN, int TBN, bool TAIL = false, bool PERSIST = false>
 void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
             const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
             float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of, MifxFeed feed,
-            TailArgs ta = TailArgs{}, const void* pre = nullptr, const long long* pre_tag = nullptr) {
+            TailArgs ta = TailArgs{}, void* pre = nullptr, long long* pre_tag = nullptr) {
   constexpr int lds_bytes = PERSIST ? LDS_BYTES_P : LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
@@ -1183,7 +1200,7 @@ void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, l
   }
   hipLaunchKernelGGL((wdc_fused<TRAIN, TBN, TAIL, PERSIST>), grid, dim3(64 * (T / (16 * TBN))), lds_bytes, stream,
                      (const uint4*)data, n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab,
-                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta, feed, (const uint4*)pre, pre_tag);
+                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta, feed, (uint4*)pre, pre_tag);
 }
 
 }  // namespace
@@ -1218,8 +1235,8 @@ int WDC_SYM(mifx_wdc_fused_p)(const void* data, long long n_data, long long batc
                               const long long* step_ctr, const void* wimg, const float* wide, float* slab,
                               float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
                               const int* tmap, int stride, int waves, int* xcd_of, long long feed_stride,
-                              long long feed_offset, unsigned long long shuffle_key, const void* pre,
-                              const long long* pre_tag, hipStream_t stream) {
+                              long long feed_offset, unsigned long long shuffle_key, void* pre, long long* pre_tag,
+                              hipStream_t stream) {
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
   if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;

@@ -891,53 +891,15 @@ struct XgPeers {
 // (One kernel with a last-arriver finalizer measured slower, 12.9 us vs 5.0 + 6.0: its chain of write-through
 // stores, counter atomic and partial loads is longer than a kernel boundary.)
 constexpr int XMAX = 16;  // XCC_ID range
-
-// host-side prefetch request (mifx.ops.wide_deep.Prefetch, ctypes): null -> no prefetch
-struct WdPrefetchArgs {
-  const void* data;
-  long long n_data, batch, feed_stride, feed_offset;
-  unsigned long long key;
-  void* buf;
-  long long* tag;
-  const long long* step_ctr;
-};
-inline bool prefetch_of(const WdPrefetchArgs* a, MifxPrefetch* out) {
-  *out = MifxPrefetch{};
-  if (a == nullptr || a->buf == nullptr) return true;
-  if (a->data == nullptr || a->tag == nullptr || a->step_ctr == nullptr || a->n_data <= 0 || a->batch <= 0 ||
-      a->batch > a->n_data || a->feed_stride < a->batch || a->feed_offset < 0 ||
-      a->feed_offset + a->batch > a->feed_stride || (uintptr_t)a->buf % 16 || (uintptr_t)a->data % 16)
-    return false;
-  *out = MifxPrefetch{a->data, a->n_data, a->batch, MifxFeed{a->feed_stride, a->feed_offset, a->key}, a->buf, a->tag,
-                      a->step_ctr};
-  return true;
-}
 constexpr int X1C = 64;   // float4 columns per level-1 workgroup (1 KB of each slab row): one per lane of a wave
 static_assert(X1C == 64, "wd_reduce_xcd maps lane -> float4 column of its chunk");
 
 __global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ slab, int G, int stride,
                                                      const int* __restrict__ xcd_of, float4* __restrict__ part,
-                                                     int* __restrict__ ok, const long long* __restrict__ xep,
-                                                     MifxPrefetch pf) {
+                                                     int* __restrict__ ok, const long long* __restrict__ xep) {
   __shared__ int rows[256];
   __shared__ int wcnt[4];
   __shared__ float4 red[4][X1C];
-  // the NEXT step's records for the fused kernel (MifxPrefetch, csrc/feed.h): loads issued first, under this
-  // kernel's row-list and slab work; one record per thread (loop for batches beyond the grid)
-  const long long gthreads = (long long)gridDim.x * 256, gid0 = (long long)blockIdx.x * 256 + threadIdx.x;
-  long long s1 = 0;
-  MifxFeedStep pfs{};
-  uint4 pr0 = make_uint4(0, 0, 0, 0), pr1 = pr0;
-  const bool pf_on = pf.buf != nullptr;
-  if (pf_on) {
-    s1 = pf.step_ctr[0] + 1;
-    pfs = mifx_feed_step(pf.feed, s1, pf.n_data);
-    if (gid0 < pf.batch) {
-      const long long di = mifx_feed_record(pf.feed, pfs, gid0, pf.n_data);
-      pr0 = ((const uint4*)pf.data)[2 * di];
-      pr1 = ((const uint4*)pf.data)[2 * di + 1];
-    }
-  }
   const int x = mifx_xcc_id();
   const int S4 = stride / 4, nc1 = (S4 + X1C - 1) / X1C;
   const int c = blockIdx.x / 8;
@@ -952,19 +914,6 @@ __global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ 
   if (sel) rows[base + __popcll(m & ((1ull << lane) - 1))] = t;
   const int n = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
   __syncthreads();
-  if (pf_on) {
-    if (gid0 < pf.batch) {
-      ((uint4*)pf.buf)[2 * gid0] = pr0;
-      ((uint4*)pf.buf)[2 * gid0 + 1] = pr1;
-    }
-    for (long long g = gid0 + gthreads; g < pf.batch; g += gthreads) {
-      const long long di = mifx_feed_record(pf.feed, pfs, g, pf.n_data);
-      ((uint4*)pf.buf)[2 * g] = ((const uint4*)pf.data)[2 * di];
-      ((uint4*)pf.buf)[2 * g + 1] = ((const uint4*)pf.data)[2 * di + 1];
-    }
-    // read by the next step's fused kernel, after this kernel (and the optimizer) completed
-    if (blockIdx.x == 0 && threadIdx.x == 0) *pf.tag = s1;
-  }
   if (c >= nc1) return;
   const int q = c * X1C + lane;
   float4 a = make_float4(0, 0, 0, 0);
@@ -1356,10 +1305,7 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
                             int world, int rank, const unsigned int* my_sig, int* err, long long* xctr, float* out,
                             const int* wsc, float* param, float* s0, float* s1, void* wt_out,
                             long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
-                            const int* xcd_of, float* xpart, int* xok, long long* xep, const WdPrefetchArgs* pfa,
-                            hipStream_t stream) {
-  MifxPrefetch pf;
-  if (!prefetch_of(pfa, &pf)) return -1;
+                            const int* xcd_of, float* xpart, int* xok, long long* xep, hipStream_t stream) {
   if (G <= 0 || world < 1 || world > XG_MAXW || rank < 0 || rank >= world || stride <= 0 || stride > STRIDE ||
       stride % 4 != 0 || my_sig == nullptr || err == nullptr || xctr == nullptr)
     return -1;
@@ -1385,7 +1331,7 @@ int mifx_wd_reduce_xgmi_opt(const float* slab, int G, int stride, const void* co
     OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
                 hyper_wide[6], hyper_wide[7]};
     hipLaunchKernelGGL(wd_reduce_xcd, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, xcd_of,
-                       (float4*)xpart, xok, xep, pf);
+                       (float4*)xpart, xok, xep);
     static const bool fused_wait = getenv("MIFX_XGMI_FUSED_WAIT") != nullptr && getenv("MIFX_XGMI_FUSED_WAIT")[0] == '1';
     if (fused_wait) {  // (opt-in) publish + wait + gather + optimizer in the 256-thread level-2 workgroups
       hipLaunchKernelGGL(wd_xcd_opt_sc<3>, g2, dim3(256), 0, stream, xpart, xok, slab, G, stride, xcd_of, xep,
@@ -1450,9 +1396,7 @@ int mifx_wd_xcd_chunks(int stride) { return (stride / 4 + X1C - 1) / X1C; }
 int mifx_wd_reduce_xcd_opt(const float* slab, int G, int stride, const int* xcd_of, float* part, int* ok,
                            long long* xep, float* out, const int* wsc, float* param, float* s0, float* s1,
                            void* wt_out, long long* step_ctr, const float* hyper_dnn, const float* hyper_wide,
-                           const WdPrefetchArgs* pfa, hipStream_t stream) {
-  MifxPrefetch pf;
-  if (!prefetch_of(pfa, &pf)) return -1;
+                           hipStream_t stream) {
   if (G <= 0 || G > 256 || stride <= 0 || stride > STRIDE || stride % 4 != 0 || xcd_of == nullptr ||
       part == nullptr || ok == nullptr || xep == nullptr)
     return -1;
@@ -1471,7 +1415,7 @@ int mifx_wd_reduce_xcd_opt(const float* slab, int G, int stride, const int* xcd_
                   hyper_wide[6], hyper_wide[7]};
   }
   hipLaunchKernelGGL(wd_reduce_xcd, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, xcd_of,
-                     (float4*)part, ok, xep, pf);
+                     (float4*)part, ok, xep);
   if (wsc == nullptr)
     hipLaunchKernelGGL(wd_xcd_opt_sc<0>, g2, dim3(256), 0, stream, part, ok, slab, G, stride, xcd_of, xep, out, wsc,
                        param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, XgPeers{}, 0, 0, nullptr, nullptr, nullptr);

@@ -23,10 +23,10 @@ def _fns():
         "reduce_opt_sc": sig(lib, "mifx_wd_reduce_opt_sc", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
         "xcd_chunks": sig(lib, "mifx_wd_xcd_chunks", [I32]),
         "reduce_xcd_opt": sig(lib, "mifx_wd_reduce_xcd_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP,
-                                                              VP, VP, VP, VP, VP]),
+                                                              VP, VP, VP, VP]),
         "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
         "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
-                                                                VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+                                                                VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -128,14 +128,6 @@ def reduce_apply_sc(slab: torch.Tensor, groups: int, wsc: torch.Tensor, param_sc
     check(rc, "mifx_wd_reduce_opt_sc")
 
 
-class PrefetchArgs(ctypes.Structure):
-    """csrc/wide_deep.hip WdPrefetchArgs: the level-1 slab reduction gathers the NEXT step's records into `buf`
-    (csrc/feed.h MifxPrefetch) for the fused kernel."""
-    _fields_ = [("data", ctypes.c_void_p), ("n_data", ctypes.c_longlong), ("batch", ctypes.c_longlong),
-                ("feed_stride", ctypes.c_longlong), ("feed_offset", ctypes.c_longlong), ("key", ctypes.c_ulonglong),
-                ("buf", ctypes.c_void_p), ("tag", ctypes.c_void_p), ("step_ctr", ctypes.c_void_p)]
-
-
 class XcdReduce:
     """Scratch for the XCD-local two-level slab reduction + optimizer (csrc/wide_deep.hip wd_reduce_xcd /
     wd_xcd_opt_sc): xcd_of [256] (filled by the chained kernel), per-XCD partials [16, stride], epoch stamps and
@@ -148,26 +140,12 @@ class XcdReduce:
         self.part = torch.zeros(16 * stride, device=device)
         self.ok = torch.zeros(16 * nc1, dtype=torch.int32, device=device)
         self.xep = torch.zeros(STEP_SLOTS, dtype=torch.int64, device=device)
-        self.pf = None  # PrefetchArgs of the trainer's next-step record gather (set_prefetch)
-
-    def set_prefetch(self, records, n_data: int, batch: int, feed: tuple[int, int, int], buf, tag, step_ctr) -> None:
-        """Gather the next step's records into buf (uint8 [batch, 32]) in every optimizer step (tag <- its step);
-        records=None turns it off."""
-        if records is None:
-            self.pf = None
-            return
-        gs, go, key = feed
-        self.pf = PrefetchArgs(records.data_ptr(), int(n_data), int(batch), int(gs), int(go), int(key) & (2**64 - 1),
-                               buf.data_ptr(), tag.data_ptr(), step_ctr.data_ptr())
-
-    def pf_ref(self):
-        return ctypes.byref(self.pf) if self.pf is not None else None
 
     def _call(self, slab, groups, out, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide):
         rc = _fns()["reduce_xcd_opt"](ptr(slab), int(groups), self.stride, ptr(self.xcd_of), ptr(self.part),
                                       ptr(self.ok), ptr(self.xep), ptr(out), ptr(wsc), ptr(param_sc), ptr(s0_sc),
                                       ptr(s1_sc), ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
-                                      self.pf_ref() if wsc is not None else None, stream_handle(slab.device))
+                                      stream_handle(slab.device))
         check(rc, "mifx_wd_reduce_xcd_opt")
 
     def apply_sc(self, slab: torch.Tensor, groups: int, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn,

@@ -130,7 +130,7 @@ class XgmiExchange:
                                            self.rank, self.sig, ptr(self.err), ptr(self.xctr), None, ptr(tr.wsc),
                                            ptr(tr.param_sc), ptr(tr.s0_sc), ptr(tr.s1_sc), ptr(tr.wt),
                                            ptr(tr.step_ctr), ptr(tr.h_dnn), ptr(tr.h_wide), *xa,
-                                           xr.pf_ref() if xr is not None else None, stream_handle(self.device))
+                                           stream_handle(self.device))
         check(rc, "mifx_wd_reduce_xgmi_opt")
 
     def sum_into(self, slab: torch.Tensor, out: torch.Tensor) -> None:
@@ -140,7 +140,7 @@ class XgmiExchange:
         rc = wdk._fns()["reduce_xgmi_opt"](ptr(slab), int(slab.shape[0]), self.stride, self.parts, self.sigs,
                                            self.world, self.rank, self.sig, ptr(self.err), ptr(self.xctr), ptr(out),
                                            None, None, None, None, None, None, None, None, None, None, None, None,
-                                           None, stream_handle(self.device))
+                                           stream_handle(self.device))
         check(rc, "mifx_wd_reduce_xgmi_opt(sum)")
 
     # ------------------------------------------------------------------ validation

@@ -164,11 +164,11 @@ class FusedWideDeepTrainer:
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
         self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
-        # next-step record prefetch (csrc/feed.h MifxPrefetch, opt-in MIFX_WD_PREFETCH=1): the XCD-local slab
-        # reduction of step s gathers step s + 1's records into one contiguous buffer, so the fused kernel's first
-        # loads need no step -> feed -> record-address chain. Measured SLOWER at B = 65536 (32.7-32.9 vs
-        # 32.0-32.1 us per step, profiles/wd_prefetch_ab_r4.txt): the gather lengthens the reduction kernel by more
-        # than the fused kernel's prologue loses (its 3.6 us prologue is bound by the weight-image staging too)
+        # record prefetch (MIFX_WD_PREFETCH=1): every workgroup of the chained kernel loads the NEXT step's
+        # records for its first rows at its start and stores them to a buffer at its end; the next step's workgroup of
+        # the same index reads them beside the step counter (tag-checked), so its first records need no step -> feed
+        # -> record-address chain. (Gathering them in the slab reduction instead measured slower: 32.7-32.9 vs
+        # 32.0-32.1 us per step, profiles/wd_prefetch_ab_r4.txt.)
         self._pre = self._pre_tag = None
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
@@ -304,14 +304,12 @@ class FusedWideDeepTrainer:
         self._setup_prefetch()
 
     def _setup_prefetch(self) -> None:
-        if self._xcd is None or self.kernel != "chain" or os.environ.get("MIFX_WD_PREFETCH", "0") != "1":
+        if self.kernel != "chain" or os.environ.get("MIFX_WD_PREFETCH", "0") != "1":
             return
         if self._pre is None:
             self._pre = torch.empty(self.batch, 32, dtype=torch.uint8, device=self.device)
             self._pre_tag = torch.empty(1, dtype=torch.int64, device=self.device)
         self._pre_tag.fill_(-1)  # new records: nothing prefetched yet
-        self._xcd.set_prefetch(self.records, self.n_data, self.batch, self.feed_args(), self._pre, self._pre_tag,
-                               self.step_ctr)
 
     @property
     def grad_scale(self) -> float:

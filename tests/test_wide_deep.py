@@ -618,14 +618,13 @@ def test_record_prefetch_bit_identical(monkeypatch, large):
     from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
 
     dev = torch.device("cuda")
-    batch = 16384  # T = 256: grid 64 (the XCD-local reduction); T = 128: grid 128
     rec = synthetic_records(batch * 3 + 100, device=dev, seed=41)
     rec2 = synthetic_records(batch * 2 + 36, device=dev, seed=42)
     out = {}
     for pf in ("0", "1"):
         monkeypatch.setenv("MIFX_WD_PREFETCH", pf)
         tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=6), batch=batch, device=dev, large_tile=large,
-                                  shuffle_seed=0x5EED)
+                                  shuffle_seed=0x5EED, max_grid=max_grid)
         tr.set_data(rec)
         for _ in range(3):
             tr.step()
