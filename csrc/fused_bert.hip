@@ -774,6 +774,49 @@ int launch_col_sum(const void* x, int M, int N, float* part, void* out, int chun
   return (int)hipGetLastError();
 }
 
+// Deterministic embedding gradient g[V, H] (fp32, zero-filled by the caller) += dy[N, H] scattered by ids[N]: one
+// workgroup per token; the workgroup of the FIRST occurrence of an id collects every occurrence in token order
+// (ballot compaction into LDS) and writes the row as one ordered fp32 sum -- no atomics, so the gradient (and a
+// captured training step) is bit-reproducible, and no sort (PyTorch's sort + unique-by-key backward faults under
+// hipGraph replay on ROCm, see mifx.ops.fused_bert._Embedding).
+template <typename T>
+__global__ __launch_bounds__(256) void emb_bwd_det(const long long* __restrict__ ids, int N, const T* __restrict__ dy,
+                                                   int H, long long V, float* __restrict__ g) {
+  extern __shared__ int list[];  // [N]
+  __shared__ int earlier, cnt, wc[4];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long id = ids[n];
+  if (id < 0 || id >= V) return;  // (uniform) out-of-range ids contribute nothing
+  if (tid == 0) {
+    earlier = 0;
+    cnt = 0;
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += 256)
+    if (ids[j] == id) earlier = 1;
+  __syncthreads();
+  if (earlier) return;  // (uniform) a previous token's workgroup owns this row
+  for (int j0 = n; j0 < N; j0 += 256) {
+    const int j = j0 + tid;
+    const bool m = j < N && ids[j] == id;
+    const unsigned long long b = __ballot(m);
+    if (lane == 0) wc[w] = __popcll(b);
+    __syncthreads();
+    int pos = cnt;
+    for (int i = 0; i < w; ++i) pos += wc[i];
+    if (m) list[pos + __popcll(b & ((1ull << lane) - 1))] = j;
+    __syncthreads();
+    if (tid == 0) cnt += wc[0] + wc[1] + wc[2] + wc[3];
+    __syncthreads();
+  }
+  const int c = cnt;
+  for (int h = tid; h < H; h += 256) {
+    float a = 0.f;
+    for (int k = 0; k < c; ++k) a += ld(dy + (size_t)list[k] * H + h);
+    g[(size_t)id * H + h] += a;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -894,6 +937,27 @@ int mifx_bert_bias_gelu(int dtype, int pdt, int fwd, const void* dy, const void*
 }
 
 // out[N] (dtype pdt) = column sums of x [M, N] (dtype); scratch part [gelu_chunks(M), N] fp32
+// g [V, H] fp32 (zero-filled) += the embedding gradient of dy [N, H] (dtype 0 fp32, 1 bf16) at int64 ids [N],
+// deterministic (emb_bwd_det). N <= 32768 (the token list of one row lives in LDS).
+int mifx_bert_emb_bwd(int dtype, const long long* ids, int N, const void* dy, int H, long long V, float* g,
+                      hipStream_t st) {
+  if (N <= 0 || N > 32768 || H <= 0 || V <= 0 || ids == nullptr || dy == nullptr || g == nullptr) return -1;
+  const size_t lds = (size_t)N * sizeof(int);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)emb_bwd_det<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4);
+    (void)hipFuncSetAttribute((const void*)emb_bwd_det<__hip_bfloat16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              32768 * 4);
+    attr = true;
+  }
+  if (dtype == 1)
+    hipLaunchKernelGGL(emb_bwd_det<__hip_bfloat16>, dim3(N), dim3(256), lds, st, ids, N, (const __hip_bfloat16*)dy, H,
+                       V, g);
+  else
+    hipLaunchKernelGGL(emb_bwd_det<float>, dim3(N), dim3(256), lds, st, ids, N, (const float*)dy, H, V, g);
+  return (int)hipGetLastError();
+}
+
 int mifx_bert_col_sum(int dtype, int pdt, const void* x, int M, int N, float* part, void* out, hipStream_t st) {
   if (M <= 0 || N <= 0) return -1;
   const int chunks = mifx_bert_gelu_chunks(M);

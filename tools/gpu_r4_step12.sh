@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_wide_deep.py tests/test_shuffle.py tests/test_dist_gpu.py -k "prefetch or large_tile or shuffle or xgmi or dist" > gpurun_out/r4_t12a.log 2>&1; rc=$?; tail -3 gpurun_out/r4_t12a.log
+timeout -k 10 800 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/test_wide_deep.py tests/test_shuffle.py tests/test_dist_gpu.py tests/test_bert_tp.py tests/test_tp_ipc.py -k "prefetch or large_tile or shuffle or xgmi or dist or embedding or bert or ipc" > gpurun_out/r4_t12a.log 2>&1; rc=$?; tail -3 gpurun_out/r4_t12a.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for r in 1 2 3; do
 for pf in 1 0; do
