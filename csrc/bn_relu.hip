@@ -19,6 +19,7 @@
 // same fused multiply-add as forward, so it matches the forward output exactly.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 namespace {
@@ -387,10 +388,20 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ d
   }
 }
 
+// workgroups of the statistics / backward-reduction passes (>= 16 rows per thread, at most MIFX_BN_BLOCKS_CAP,
+// default 512)
+int blocks_cap() {
+  static const int cap = [] {
+    const char* e = getenv("MIFX_BN_BLOCKS_CAP");
+    const int v = e ? atoi(e) : 512;
+    return v < 64 ? 64 : (v > 8192 ? 8192 : v);
+  }();
+  return cap;
+}
 int blocks_for(long long M, int C) {
   const int rpb = kThreads / (C / kVec);
   long long nb = (M + (long long)rpb * 16 - 1) / ((long long)rpb * 16);  // >= 16 rows per thread
-  if (nb > 512) nb = 512;
+  if (nb > blocks_cap()) nb = blocks_cap();
   return nb < 1 ? 1 : (int)nb;
 }
 
