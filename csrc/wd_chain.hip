@@ -553,8 +553,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
                                                      float* __restrict__ slab, float* __restrict__ slab_loss,
                                                      float* __restrict__ logits_out, float grad_scale,
                                                      const int* __restrict__ tmap, int stride,
-                                                     int* __restrict__ xcd_of, TailArgs ta, MifxFeed feed,
-                                                     uint4* pre, long long* pre_tag) {
+                                                     int* __restrict__ xcd_of, TailArgs ta, MifxFeed feed) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   float* wgrad = (float*)(lds + LSEND);
   float* red = wgrad + WIDE_PAD;
@@ -611,23 +610,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     __syncthreads();
   }
 
-  // this step's records, gathered by this workgroup index in the previous step (below): loaded now, beside the step
-  // counter and the buffer's tag, so the first records do not wait for step -> feed -> record address
-  constexpr int EPW0 = 16 * TBN;
-  const bool has_pre = TRAIN && !PERSIST && pre != nullptr && step_ctr != nullptr;
-  uint4 pu[TBN][2], nx[TBN][2];
-  long long ptag = -1;
-  if (has_pre) {
-    ptag = *pre_tag;
-#pragma unroll
-    for (int tb = 0; tb < TBN; ++tb) {
-      const long long row = min((long long)blockIdx.x * T + EPW0 * w + 16 * tb + r, batch - 1);
-      pu[tb][0] = pre[2 * row];
-      pu[tb][1] = pre[2 * row + 1];
-    }
-  }
   const long long step0 = step_ctr ? step_ctr[0] : 0;
-  const bool use_pre = has_pre && ptag == step0;  // (uniform) stale or absent: the feed path below
   constexpr bool kPersist = PERSIST;
   const int nsteps = kPersist ? ta.nsteps : 1;
   for (int ps = 0; ps < nsteps; ++ps) {
@@ -692,28 +675,8 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
       u[tb][1] = data[2 * di + 1];
     }
   };
-  // the NEXT step's records for this workgroup's first rows: loaded now (their latency hides under the step) and
-  // stored to the prefetch buffer at the end, where the next step's workgroup of the same index reads them
-  if (has_pre) {
-    const MifxFeedStep fsn = mifx_feed_step(fd, step0 + 1, n_data);
-#pragma unroll
-    for (int tb = 0; tb < TBN; ++tb) {
-      const long long row = min((long long)blockIdx.x * T + EPW0 * w + 16 * tb + r, batch - 1);
-      const long long di = mifx_feed_record(fd, fsn, row, n_data);
-      nx[tb][0] = data[2 * di];
-      nx[tb][1] = data[2 * di + 1];
-    }
-  }
   uint4 nu[TBN][2];
-  if (use_pre) {  // the first iteration's rows (later iterations of a multi-iteration workgroup use the feed)
-#pragma unroll
-    for (int tb = 0; tb < TBN; ++tb) {
-      nu[tb][0] = pu[tb][0];
-      nu[tb][1] = pu[tb][1];
-    }
-  } else {
-    fetch(blockIdx.x, nu);
-  }
+  fetch(blockIdx.x, nu);
   if constexpr (REG_STAGE) {
 #pragma unroll
     for (int i = 0; i < PER_STAGE; ++i)
@@ -1070,17 +1033,6 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   if constexpr (PERSIST) {
     for (int i = tid; i < STEP_SLOTS; i += NTHR) ta.step_slots[i] = step0 + nsteps;
   }
-  if (has_pre) {  // the next step's first records (rows of this workgroup index only: no other workgroup reads them)
-#pragma unroll
-    for (int tb = 0; tb < TBN; ++tb) {
-      const long long row = min((long long)blockIdx.x * T + EPW0 * w + 16 * tb + r, batch - 1);
-      pre[2 * row] = nx[tb][0];
-      pre[2 * row + 1] = nx[tb][1];
-    }
-    // read by the next launch (a workgroup of this launch that reads it late sees step0 + 1 != its step and takes
-    // the feed path: slower, never wrong)
-    if (blockIdx.x == 0 && tid == 0) *pre_tag = step0 + 1;
-  }
   STAMP(17);
   BSTAMP(2);
   if constexpr (TRAIN && TAIL) {
@@ -1190,7 +1142,7 @@ template <bool TRAIN, int TBN, bool TAIL = false, bool PERSIST = false>
 void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, long long batch, long long start_fixed,
             const long long* step_ctr, const void* wimg, const float* wide, float* slab, float* slab_loss,
             float* logits_out, float grad_scale, const int* tmap, int stride, int* xcd_of, MifxFeed feed,
-            TailArgs ta = TailArgs{}, void* pre = nullptr, long long* pre_tag = nullptr) {
+            TailArgs ta = TailArgs{}) {
   constexpr int lds_bytes = PERSIST ? LDS_BYTES_P : LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
@@ -1200,7 +1152,7 @@ void launch(dim3 grid, hipStream_t stream, const void* data, long long n_data, l
   }
   hipLaunchKernelGGL((wdc_fused<TRAIN, TBN, TAIL, PERSIST>), grid, dim3(64 * (T / (16 * TBN))), lds_bytes, stream,
                      (const uint4*)data, n_data, batch, start_fixed, step_ctr, (const uint4*)wimg, wide, slab,
-                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta, feed, (uint4*)pre, pre_tag);
+                     slab_loss, logits_out, grad_scale, tmap, stride, xcd_of, ta, feed);
 }
 
 }  // namespace
@@ -1231,27 +1183,24 @@ int WDC_SYM(mifx_wdc_constants)(int* out, int n) {
 // layout (LWEND elements, C-ordered columns, see models.wide_deep.chain_image).
 // xcd_of (nullable, >= grid ints): receives the XCD each workgroup ran on (training only).
 // (T = 64 build: waves must be 4, 4 x 16 examples)
-int WDC_SYM(mifx_wdc_fused_p)(const void* data, long long n_data, long long batch, long long start_fixed,
+int WDC_SYM(mifx_wdc_fused_f)(const void* data, long long n_data, long long batch, long long start_fixed,
                               const long long* step_ctr, const void* wimg, const float* wide, float* slab,
                               float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
                               const int* tmap, int stride, int waves, int* xcd_of, long long feed_stride,
-                              long long feed_offset, unsigned long long shuffle_key, void* pre, long long* pre_tag,
-                              hipStream_t stream) {
+                              long long feed_offset, unsigned long long shuffle_key, hipStream_t stream) {
   if (grid <= 0 || n_data <= 0 || batch <= 0 || batch > n_data || wimg == nullptr || wide == nullptr) return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0) return -1;
   if (train && (tmap == nullptr || slab == nullptr || stride < WIDE_PAD || stride % 4 != 0)) return -1;
   if (!train && logits_out == nullptr) return -1;
   if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
   const MifxFeed fd{feed_stride, feed_offset, shuffle_key};
-  if (pre != nullptr && (pre_tag == nullptr || step_ctr == nullptr || (uintptr_t)pre % 16 != 0)) return -1;
-  if (!train) pre = nullptr, pre_tag = nullptr;
   const dim3 g(grid);
 #if WDC_T == 64
   if (waves != 4) return -1;
   if ((long long)grid * T < batch) return -1;  // ONE_ITER: one iteration per workgroup
   if (train)
     launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of, fd, TailArgs{}, pre, pre_tag);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else
     launch<false, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                      grad_scale, tmap, stride, nullptr, fd);
@@ -1261,7 +1210,7 @@ int WDC_SYM(mifx_wdc_fused_p)(const void* data, long long n_data, long long batc
   if ((long long)grid * T < batch) return -1;  // ONE_ITER: one iteration per workgroup
   if (train)
     launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of, fd, TailArgs{}, pre, pre_tag);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else
     launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                      grad_scale, tmap, stride, nullptr, fd);
@@ -1270,26 +1219,15 @@ int WDC_SYM(mifx_wdc_fused_p)(const void* data, long long n_data, long long batc
   if (waves != 4 && waves != 8) return -1;
   if (train && waves == 4)
     launch<true, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of, fd, TailArgs{}, pre, pre_tag);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else if (train)
     launch<true, 1>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
-                    grad_scale, tmap, stride, xcd_of, fd, TailArgs{}, pre, pre_tag);
+                    grad_scale, tmap, stride, xcd_of, fd);
   else  // eval / predict: the 4-wave shape for either request (forward only, no dW phases to overlap)
     launch<false, 2>(g, stream, data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss, logits_out,
                      grad_scale, tmap, stride, nullptr, fd);
   return (int)hipGetLastError();
 #endif
-}
-
-// (without the prefetch buffer: records through the feed)
-int WDC_SYM(mifx_wdc_fused_f)(const void* data, long long n_data, long long batch, long long start_fixed,
-                              const long long* step_ctr, const void* wimg, const float* wide, float* slab,
-                              float* slab_loss, float* logits_out, float grad_scale, int grid, int train,
-                              const int* tmap, int stride, int waves, int* xcd_of, long long feed_stride,
-                              long long feed_offset, unsigned long long shuffle_key, hipStream_t stream) {
-  return WDC_SYM(mifx_wdc_fused_p)(data, n_data, batch, start_fixed, step_ctr, wimg, wide, slab, slab_loss,
-                                   logits_out, grad_scale, grid, train, tmap, stride, waves, xcd_of, feed_stride,
-                                   feed_offset, shuffle_key, nullptr, nullptr, stream);
 }
 
 // the same launch with the records in stored order, one replica (feed stride = batch, offset 0, no shuffle)

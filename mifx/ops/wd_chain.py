@@ -21,8 +21,6 @@ def _fns():
                                                  I32, VP, VP]),
         "fused_f": sig(lib, "mifx_wdc_fused_f", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
                                                  I32, VP, I64, I64, U64, VP]),
-        "fused_p": sig(lib, "mifx_wdc_fused_p", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP, I32,
-                                                 I32, VP, I64, I64, U64, VP, VP, VP]),
         "fused_tail": sig(lib, "mifx_wdc_fused_tail", [VP, I64, I64, VP, VP, VP, VP, VP, F32, I32, VP, I32, VP, VP, VP,
                                                        VP, VP, VP, VP, VP, VP, VP, VP, I64, I64, U64, VP]),
         "persist": sig(lib, "mifx_wdc_persist", [VP, I64, I64, VP, VP, VP, VP, VP, F32, VP, I32, VP, VP, VP, VP, VP, VP,
@@ -42,8 +40,6 @@ def _fns64():
                                                      I32, I32, VP, VP]),
         "fused_f": sig(lib, "mifx_wdc_fused_f_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
                                                      I32, I32, VP, I64, I64, U64, VP]),
-        "fused_p": sig(lib, "mifx_wdc_fused_p_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
-                                                     I32, I32, VP, I64, I64, U64, VP, VP, VP]),
     }
 
 
@@ -56,8 +52,6 @@ def _fns256():
         "constants": sig(lib, "mifx_wdc_constants_t256", [VP, I32]),
         "fused_f": sig(lib, "mifx_wdc_fused_f_t256", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
                                                       I32, I32, VP, I64, I64, U64, VP]),
-        "fused_p": sig(lib, "mifx_wdc_fused_p_t256", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
-                                                      I32, I32, VP, I64, I64, U64, VP, VP, VP]),
     }
 
 
@@ -80,16 +74,13 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
           wimg_bf16: torch.Tensor, wide: torch.Tensor, slab: torch.Tensor | None, slab_loss: torch.Tensor | None,
           logits_out: torch.Tensor | None, grad_scale: float, grid: int, train: bool,
           tmap: torch.Tensor | None = None, waves: int = 8, xcd_of: torch.Tensor | None = None,
-          tile: int = 128, feed: tuple[int, int, int] | None = None,
-          prefetch: tuple[torch.Tensor, torch.Tensor] | None = None) -> None:
+          tile: int = 128, feed: tuple[int, int, int] | None = None) -> None:
     """One chained-kernel launch. wimg_bf16: [LWEND] bf16 (or int16) weight image in the kernel's LDS layout
     (models.wide_deep.chain_image); slab: [>= grid, stride] with the chain_maps() compact layout.
     tile 128: waves 8 (two waves per SIMD, 16 examples each) or 4 (one wave per SIMD, 32 examples each);
     tile 64 (64 examples per workgroup iteration): waves 4 (one wave per SIMD, 16 examples each). xcd_of: int32
     [>= grid], receives the XCD each workgroup ran on (for the XCD-local slab reduction). feed: (stride, offset,
-    shuffle seed) of the record stream (csrc/feed.h, mifx.data.shuffle); None = (batch, 0, 0), stored order.
-    prefetch (training): (buffer uint8 [batch, 32], tag int64 [1]) -- the step's records gathered by the previous
-    step's slab reduction (csrc/feed.h MifxPrefetch), used when the tag equals the step counter."""
+    shuffle seed) of the record stream (csrc/feed.h, mifx.data.shuffle); None = (batch, 0, 0), stored order."""
     if waves not in {128: (4, 8), 64: (4,), 256: (8,)}[tile]:
         raise ValueError("waves must be 4 or 8 (tile 128) / 4 (tile 64) / 8 (tile 256)")
     if tile == 256 and train and grid * 256 < batch:
@@ -112,13 +103,10 @@ def fused(records: torch.Tensor, n_data: int, batch: int, start_fixed: int, step
     if xcd_of is not None and (xcd_of.dtype != torch.int32 or xcd_of.numel() < grid):
         raise ValueError("xcd_of must be int32 [>= grid]")
     gs, go, key = feed if feed is not None else (batch, 0, 0)
-    pre, tag = prefetch if (prefetch is not None and train) else (None, None)
-    if pre is not None and (pre.numel() < 32 * batch or tag is None or step_ctr is None):
-        raise ValueError("prefetch buffer must hold batch records, with its tag and the step counter")
-    rc = fns_for(tile)["fused_p"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
+    rc = fns_for(tile)["fused_f"](ptr(records), n_data, batch, start_fixed, ptr(step_ctr), ptr(wimg_bf16), ptr(wide),
                                   ptr(slab), ptr(slab_loss), ptr(logits_out), float(grad_scale), int(grid), int(train),
                                   ptr(tmap), stride, int(waves), ptr(xcd_of), int(gs), int(go), int(key) & (2**64 - 1),
-                                  ptr(pre), ptr(tag), stream_handle(records.device))
+                                  stream_handle(records.device))
     check(rc, "mifx_wdc_fused")
 
 

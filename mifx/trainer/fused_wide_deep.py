@@ -164,12 +164,6 @@ class FusedWideDeepTrainer:
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
         self._xcd = wdk.XcdReduce(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
-        # record prefetch (MIFX_WD_PREFETCH=1): every workgroup of the chained kernel loads the NEXT step's
-        # records for its first rows at its start and stores them to a buffer at its end; the next step's workgroup of
-        # the same index reads them beside the step counter (tag-checked), so its first records need no step -> feed
-        # -> record-address chain. (Gathering them in the slab reduction instead measured slower: 32.7-32.9 vs
-        # 32.0-32.1 us per step, profiles/wd_prefetch_ab_r4.txt.)
-        self._pre = self._pre_tag = None
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
         # grid <= #CUs, one workgroup per CU by its LDS). Measured SLOWER on MI355X and therefore off by default:
@@ -284,9 +278,7 @@ class FusedWideDeepTrainer:
             wdc.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale, grid, train, self.tmap if train else None, self.waves,
                       self._xcd.xcd_of if (train and self._xcd is not None and slab is self.slab) else None,
-                      tile=self.tile if train else 128, feed=feed,
-                      prefetch=(self._pre, self._pre_tag) if (train and self._pre is not None and slab is self.slab)
-                      else None)
+                      tile=self.tile if train else 128, feed=feed)
         else:
             wdk.fused(records, n, batch, start_fixed, step_ctr, self.wt, self.wide_weights, slab, slab_loss,
                       logits, self.grad_scale if train else 1.0, grid, train, self.tmap if train else None,
@@ -301,15 +293,6 @@ class FusedWideDeepTrainer:
         self.n_data = self.records.shape[0]
         self.graph, self._graphs, self._fast = None, None, None
         self.graph_multi, self.graph_multi_steps = None, 1
-        self._setup_prefetch()
-
-    def _setup_prefetch(self) -> None:
-        if self.kernel != "chain" or os.environ.get("MIFX_WD_PREFETCH", "0") != "1":
-            return
-        if self._pre is None:
-            self._pre = torch.empty(self.batch, 32, dtype=torch.uint8, device=self.device)
-            self._pre_tag = torch.empty(1, dtype=torch.int64, device=self.device)
-        self._pre_tag.fill_(-1)  # new records: nothing prefetched yet
 
     @property
     def grad_scale(self) -> float:

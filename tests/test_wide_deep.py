@@ -606,38 +606,3 @@ def test_large_tile_matches_t128(batch):
     for name, r in ref.items():
         rel = np.linalg.norm(named[name].reshape(r.shape) - r) / (np.linalg.norm(r) + 1e-8)
         assert rel < 0.06, f"{name}: relative Frobenius err {rel:.4f}"
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("large", [True, False])
-def test_record_prefetch_bit_identical(monkeypatch, large):
-    """The next-step record prefetch (csrc/feed.h MifxPrefetch: the XCD-local slab reduction gathers step s + 1's
-    shuffled records, the fused kernel reads them when the tag matches its step) trains bit-identically to the feed
-    path, through eager steps, captured multi-step graphs (epoch boundaries included) and a set_data() in between
-    (which invalidates the buffer)."""
-    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
-
-    dev = torch.device("cuda")
-    rec = synthetic_records(batch * 3 + 100, device=dev, seed=41)
-    rec2 = synthetic_records(batch * 2 + 36, device=dev, seed=42)
-    out = {}
-    for pf in ("0", "1"):
-        monkeypatch.setenv("MIFX_WD_PREFETCH", pf)
-        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=6), batch=batch, device=dev, large_tile=large,
-                                  shuffle_seed=0x5EED, max_grid=max_grid)
-        tr.set_data(rec)
-        for _ in range(3):
-            tr.step()
-        tr.capture(steps_per_graph=4)
-        tr.run(8)
-        tag_mid = (int(tr._pre_tag.item()) if tr._pre is not None else None, tr.steps_done)
-        tr.set_data(rec2)
-        tr.capture(steps_per_graph=3)
-        tr.run(6)
-        torch.cuda.synchronize()
-        out[pf] = (tr.param.clone(), tr._pre is not None, tag_mid, tr.steps_done,
-                   int(tr._pre_tag.item()) if tr._pre is not None else None)
-    assert out["1"][1] and not out["0"][1]
-    # the buffer holds the coming step's records (the step counter's value after the last update)
-    assert out["1"][2][0] == out["1"][2][1] and out["1"][4] == out["1"][3]
-    assert torch.equal(out["0"][0], out["1"][0])
