@@ -586,7 +586,12 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   {  // stage the bf16 weight image (already in LDS layout) with direct-to-LDS loads: no VGPR round trip, no
      // ds_write transfer cycles. Wave w's lanes fill 16-byte chunks i * NTHR + 64 w + lane; the last wave's
      // lanes past the image end re-read its last chunk and land in the staging area, written before any read.
-    if constexpr (!REG_STAGE) {
+#ifndef WDC_DIAG_NOIMG
+#define WDC_DIAG_NOIMG 0
+#endif
+    // WDC_DIAG_NOIMG (stamp builds only, wrong results): skip the image load, so the prologue stamp times the
+    // step-counter -> feed -> record chain alone
+    if constexpr (!REG_STAGE && !WDC_DIAG_NOIMG) {
 #pragma unroll
       for (int i = 0; i < PER_STAGE; ++i) {
         const int c0 = i * NTHR + 64 * w;  // wave-uniform
@@ -594,7 +599,7 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
           __builtin_amdgcn_global_load_lds((const void*)(wimg + min(c0 + lane, NCH_STAGE - 1)),
                                            (__attribute__((address_space(3))) void*)(lds + c0 * 8), 16, 0, 0);
       }
-    } else {  // register staging: loads now, ds_write_b128 after the first record fetch (below)
+    } else if constexpr (REG_STAGE) {  // register staging: loads now, ds_write_b128 after the first record fetch
 #pragma unroll
       for (int i = 0; i < PER_STAGE; ++i) wst[i] = wimg[min(i * NTHR + tid, NCH_STAGE - 1)];
     }
