@@ -615,7 +615,11 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
     __syncthreads();
   }
 
-  const long long step0 = step_ctr ? step_ctr[0] : 0;
+#ifndef WDC_DIAG_NOSTEP
+#define WDC_DIAG_NOSTEP 0
+#endif
+  // WDC_DIAG_NOSTEP (stamp builds only, wrong record order): step 0's records, no step-counter load ahead of them
+  const long long step0 = (step_ctr && !WDC_DIAG_NOSTEP) ? step_ctr[0] : 0;
   constexpr bool kPersist = PERSIST;
   const int nsteps = kPersist ? ta.nsteps : 1;
   for (int ps = 0; ps < nsteps; ++ps) {

@@ -10,9 +10,9 @@ import torch
 sys.path.insert(0, ".")
 import mifx.ops._lib as L  # noqa: E402
 
-# --noimg: the builds without the weight-image load (bash tools/build_stamps.sh --noimg; wrong results), so the
-# prologue stamp times the step-counter -> feed -> record chain alone
-_sfx = "_noimg" if "--noimg" in sys.argv else ""
+# --noimg / --nostep: the builds without the weight-image load / the step-counter load (bash tools/build_stamps.sh
+# --noimg / --nostep; wrong results), to split the prologue
+_sfx = "_noimg" if "--noimg" in sys.argv else "_nostep" if "--nostep" in sys.argv else ""
 diag = ctypes.CDLL(f"tools/bin/libwdc{_sfx}_stamps.so", mode=ctypes.RTLD_GLOBAL)
 diag64 = ctypes.CDLL(f"tools/bin/libwdc64{_sfx}_stamps.so", mode=ctypes.RTLD_GLOBAL)
 diag256 = ctypes.CDLL(f"tools/bin/libwdc256{_sfx}_stamps.so", mode=ctypes.RTLD_GLOBAL)
