@@ -10,4 +10,4 @@ MIFX_RESNET_HIP_CONV=$m timeout -k 10 600 python -u -m mifx.trainer.resnet_train
 python -c "import json; d=[json.loads(l) for l in open('gpurun_out/resnet_ab.json') if l.startswith('{')][-1]; print('conv', '$m', round(d['value'],1), round(d['ms_per_step'],3))" | tee -a gpurun_out/resnet_routed_ab_r4.txt
 done
 done
-bash tools/gpu_r4_pmc.sh
+bash tools/gpu_batches/gpu_r4_pmc.sh
