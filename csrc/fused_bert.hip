@@ -103,9 +103,13 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
   constexpr int H = NC * 256;
   const int lane = threadIdx.x & 63;
   const int wpb = kThreads / 64;
-  float bias[NC][4];
+  // gamma / beta / bias loaded once, beside the first row's activations (loading gamma and beta after the row's
+  // two reductions put one more dependent L2 round trip on every row)
+  float bias[NC][4], wreg[NC][4], breg[NC][4];
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
+    ldv<P, 4>(w + 4 * (64 * j + lane), wreg[j]);
+    ldv<P, 4>(b + 4 * (64 * j + lane), breg[j]);
     if (dp.bias != nullptr)
       ldv<P, 4>(dp.bias + 4 * (64 * j + lane), bias[j]);
     else
@@ -143,9 +147,8 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       const int c = 4 * (64 * j + lane);
-      float wv[4], bv[4];
-      ldv<P, 4>(w + c, wv);
-      ldv<P, 4>(b + c, bv);
+      const float* wv = wreg[j];
+      const float* bv = breg[j];
       float o[4] = {(v[j][0] - mean) * rstd * wv[0] + bv[0], (v[j][1] - mean) * rstd * wv[1] + bv[1],
                     (v[j][2] - mean) * rstd * wv[2] + bv[2], (v[j][3] - mean) * rstd * wv[3] + bv[3]};
       stv<T, 4>(y + base + c, o);
@@ -774,46 +777,163 @@ int launch_col_sum(const void* x, int M, int N, float* part, void* out, int chun
   return (int)hipGetLastError();
 }
 
-// Deterministic embedding gradient g[V, H] (fp32, zero-filled by the caller) += dy[N, H] scattered by ids[N]: one
-// workgroup per token; the workgroup of the FIRST occurrence of an id collects every occurrence in token order
-// (ballot compaction into LDS) and writes the row as one ordered fp32 sum -- no atomics, so the gradient (and a
-// captured training step) is bit-reproducible, and no sort (PyTorch's sort + unique-by-key backward faults under
-// hipGraph replay on ROCm, see mifx.ops.fused_bert._Embedding).
-template <typename T>
-__global__ __launch_bounds__(256) void emb_bwd_det(const long long* __restrict__ ids, int N, const T* __restrict__ dy,
-                                                   int H, long long V, float* __restrict__ g) {
-  extern __shared__ int list[];  // [N]
-  __shared__ int earlier, cnt, wc[4];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long id = ids[n];
-  if (id < 0 || id >= V) return;  // (uniform) out-of-range ids contribute nothing
-  if (tid == 0) {
-    earlier = 0;
-    cnt = 0;
-  }
+// Deterministic embedding gradient g[V, H] (fp32, zero-filled by the caller) += dy[N, H] scattered by ids[N]. No
+// atomics (a captured training step stays bit-reproducible) and no sort (PyTorch's sort + unique-by-key backward
+// faults under hipGraph replay on ROCm, see mifx.ops.fused_bert._Embedding). An id's occurrences, in token order, are
+// cut into chunks of kEmbCh; the token at rank r % kEmbCh == 0 of its id leads a chunk and sums the chunk's rows in
+// order. An id with one chunk is written directly; a heavier one (e.g. the token-type ids: 2048 occurrences each)
+// leaves its chunk sums in `part` [N, H] (slot = the leader's token index) and emb_bwd_combine adds them in chunk
+// order -- a heavy row is spread over many workgroups instead of one CU walking thousands of rows (which cost ~0.5 ms
+// per BERT step).
+constexpr int kEmbCh = 64;
+
+// block-wide sum of an int (every thread gets the total)
+__device__ __forceinline__ int block_sum_i(int v, int* sred) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
   __syncthreads();
-  for (int j = tid; j < n; j += 256)
-    if (ids[j] == id) earlier = 1;
+  if ((threadIdx.x & 63) == 0) sred[w] = v;
   __syncthreads();
-  if (earlier) return;  // (uniform) a previous token's workgroup owns this row
-  for (int j0 = n; j0 < N; j0 += 256) {
-    const int j = j0 + tid;
+  return sred[0] + sred[1] + sred[2] + sred[3];
+}
+
+// compact, in token order, the occurrences of id at j >= j0 (ranks rank0, rank0 + 1, ... in that order) whose rank
+// satisfies keep(rank), at most cap of them, into list; returns how many (every thread of the block)
+template <typename Keep>
+__device__ int compact_occ(const long long* __restrict__ ids, int N, long long id, int j0, int rank0, int cap,
+                           Keep keep, int* list, int* wc) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int seen = 0, kept = 0;  // block-uniform
+  for (int jb = j0; jb < N && kept < cap; jb += 256) {
+    const int j = jb + tid;
     const bool m = j < N && ids[j] == id;
     const unsigned long long b = __ballot(m);
     if (lane == 0) wc[w] = __popcll(b);
     __syncthreads();
-    int pos = cnt;
-    for (int i = 0; i < w; ++i) pos += wc[i];
-    if (m) list[pos + __popcll(b & ((1ull << lane) - 1))] = j;
+    int before = 0;
+    for (int i = 0; i < w; ++i) before += wc[i];
+    const int tot = wc[0] + wc[1] + wc[2] + wc[3];
+    const bool k = m && keep(rank0 + seen + before + __popcll(b & ((1ull << lane) - 1)));
+    const unsigned long long bk = __ballot(k);
     __syncthreads();
-    if (tid == 0) cnt += wc[0] + wc[1] + wc[2] + wc[3];
+    if (lane == 0) wc[w] = __popcll(bk);
     __syncthreads();
+    int kb = 0;
+    for (int i = 0; i < w; ++i) kb += wc[i];
+    const int nk = wc[0] + wc[1] + wc[2] + wc[3];
+    const int slot = kept + kb + __popcll(bk & ((1ull << lane) - 1));
+    if (k && slot < cap) list[slot] = j;
+    __syncthreads();
+    kept += nk;
+    seen += tot;
   }
-  const int c = cnt;
+  return kept < cap ? kept : cap;
+}
+
+// rows list[0..m) of dy summed in list order for every column, fp32 -> out (H floats, global)
+template <typename T>
+__device__ void sum_rows(const T* __restrict__ dy, int H, const int* list, int m, float* __restrict__ out,
+                         float* sacc) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int tid = threadIdx.x;
+  const int NG = H / VEC;
+  if (H % VEC == 0 && NG <= 256) {
+    // thread -> (column group cg, row slice sl): slice sl sums rows sl, sl + S, ... in order, 8 loads in flight;
+    // slices are then added in slice order
+    const int S = 256 / NG, cg = tid % NG, sl = tid / NG;
+    float a[VEC] = {};
+    if (sl < S) {
+      for (int k0 = sl; k0 < m; k0 += 8 * S) {
+        Pack<T, VEC> v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * S;
+          if (k < m) v[u] = *(const Pack<T, VEC>*)(dy + (size_t)list[k] * H + (size_t)cg * VEC);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (k0 + u * S < m)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) a[e] += ld(&v[u].v[e]);
+      }
+    }
+    // slice partials through LDS [S][H], summed in slice order by slice 0
+    for (int sl2 = 1; sl2 < S; ++sl2) {
+      __syncthreads();
+      if (sl == sl2)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) sacc[cg * VEC + e] = a[e];
+      __syncthreads();
+      if (sl == 0)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) a[e] += sacc[cg * VEC + e];
+    }
+    if (sl == 0)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) out[cg * VEC + e] = a[e];
+  } else {
+    for (int h = tid; h < H; h += 256) {
+      float a = 0.f;
+      for (int k = 0; k < m; ++k) a += ld(dy + (size_t)list[k] * H + h);
+      out[h] = a;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void emb_bwd_chunks(const long long* __restrict__ ids, int N, const T* __restrict__ dy,
+                                                      int H, long long V, float* __restrict__ g,
+                                                      float* __restrict__ part, int* __restrict__ heavy) {
+  __shared__ int list[kEmbCh];
+  __shared__ int sred[4], wc[4];
+  __shared__ float sacc[2048];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const long long id = ids[n];
+  if (id < 0 || id >= V) {  // (uniform) out-of-range ids contribute nothing
+    if (tid == 0) heavy[n] = 0;
+    return;
+  }
+  // rank (earlier occurrences) and count of this id, 8 id loads in flight per thread
+  int rl = 0, cl = 0;
+  for (int j0 = tid; j0 < N; j0 += 8 * 256) {
+    long long v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = j0 + u * 256 < N ? ids[j0 + u * 256] : -1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (v[u] == id) {
+        ++cl;
+        rl += j0 + u * 256 < n ? 1 : 0;
+      }
+  }
+  const int r = block_sum_i(rl, sred);
+  const int c = block_sum_i(cl, sred);
+  if (tid == 0) heavy[n] = (r == 0 && c > kEmbCh) ? 1 : 0;
+  if (r % kEmbCh != 0) return;  // (uniform) not a chunk leader
+  const int m = min(kEmbCh, c - r);
+  const int got = compact_occ(ids, N, id, n, r, m, [](int) { return true; }, list, wc);
+  __syncthreads();
+  float* out = c <= kEmbCh ? g + (size_t)id * H : part + (size_t)n * H;
+  sum_rows<T>(dy, H, list, got, out, sacc);
+}
+
+// heavy ids (more than one chunk): the id's first token sums its chunks' partials in chunk order
+__global__ __launch_bounds__(256) void emb_bwd_combine(const long long* __restrict__ ids, int N, int H,
+                                                       const float* __restrict__ part, const int* __restrict__ heavy,
+                                                       float* __restrict__ g) {
+  __shared__ int leaders[32768 / kEmbCh + 1];
+  __shared__ int wc[4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  if (!heavy[n]) return;  // (uniform)
+  const long long id = ids[n];
+  const int K = compact_occ(ids, N, id, n, 0, N / kEmbCh + 1, [](int rank) { return rank % kEmbCh == 0; }, leaders,
+                            wc);
+  __syncthreads();
   for (int h = tid; h < H; h += 256) {
     float a = 0.f;
-    for (int k = 0; k < c; ++k) a += ld(dy + (size_t)list[k] * H + h);
-    g[(size_t)id * H + h] += a;
+    for (int k = 0; k < K; ++k) a += part[(size_t)leaders[k] * H + h];
+    g[(size_t)id * H + h] = a;
   }
 }
 
@@ -938,23 +1058,19 @@ int mifx_bert_bias_gelu(int dtype, int pdt, int fwd, const void* dy, const void*
 
 // out[N] (dtype pdt) = column sums of x [M, N] (dtype); scratch part [gelu_chunks(M), N] fp32
 // g [V, H] fp32 (zero-filled) += the embedding gradient of dy [N, H] (dtype 0 fp32, 1 bf16) at int64 ids [N],
-// deterministic (emb_bwd_det). N <= 32768 (the token list of one row lives in LDS).
+// deterministic (emb_bwd_chunks + emb_bwd_combine). N <= 32768. Scratch: part [N, H] fp32, heavy [N] int.
 int mifx_bert_emb_bwd(int dtype, const long long* ids, int N, const void* dy, int H, long long V, float* g,
-                      hipStream_t st) {
-  if (N <= 0 || N > 32768 || H <= 0 || V <= 0 || ids == nullptr || dy == nullptr || g == nullptr) return -1;
-  const size_t lds = (size_t)N * sizeof(int);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)emb_bwd_det<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4);
-    (void)hipFuncSetAttribute((const void*)emb_bwd_det<__hip_bfloat16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              32768 * 4);
-    attr = true;
-  }
+                      float* part, int* heavy, hipStream_t st) {
+  if (N <= 0 || N > 32768 || H <= 0 || V <= 0 || ids == nullptr || dy == nullptr || g == nullptr || part == nullptr ||
+      heavy == nullptr)
+    return -1;
   if (dtype == 1)
-    hipLaunchKernelGGL(emb_bwd_det<__hip_bfloat16>, dim3(N), dim3(256), lds, st, ids, N, (const __hip_bfloat16*)dy, H,
-                       V, g);
+    hipLaunchKernelGGL(emb_bwd_chunks<__hip_bfloat16>, dim3(N), dim3(256), 0, st, ids, N, (const __hip_bfloat16*)dy,
+                       H, V, g, part, heavy);
   else
-    hipLaunchKernelGGL(emb_bwd_det<float>, dim3(N), dim3(256), lds, st, ids, N, (const float*)dy, H, V, g);
+    hipLaunchKernelGGL(emb_bwd_chunks<float>, dim3(N), dim3(256), 0, st, ids, N, (const float*)dy, H, V, g, part,
+                       heavy);
+  hipLaunchKernelGGL(emb_bwd_combine, dim3(N), dim3(256), 0, st, ids, N, H, (const float*)part, (const int*)heavy, g);
   return (int)hipGetLastError();
 }
 

@@ -29,7 +29,7 @@ def _fns():
         "dropout": sig(lib, "mifx_bert_dropout", [I32, VP, I64, F32, VP, I32, VP, VP]),
         "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
         "colsum": sig(lib, "mifx_bert_col_sum", [I32, I32, VP, I32, I32, VP, VP, VP]),
-        "emb_bwd": sig(lib, "mifx_bert_emb_bwd", [I32, VP, I32, VP, I32, I64, VP, VP]),
+        "emb_bwd": sig(lib, "mifx_bert_emb_bwd", [I32, VP, I32, VP, I32, I64, VP, VP, VP, VP]),
     }
 
 
@@ -286,12 +286,15 @@ class _Linear(torch.autograd.Function):
 
 class _Embedding(torch.autograd.Function):
     """F.embedding whose backward is a deterministic scatter into an fp32 [V, H] gradient (csrc/fused_bert.hip
-    emb_bwd_det: each id's row summed by one workgroup in token order; index_add_ elsewhere), not the sort +
+    emb_bwd_chunks / emb_bwd_combine: an id's occurrences summed in token order, in chunks of 64 on separate
+    workgroups, the chunks added in order; index_add_ elsewhere), not the sort +
     unique-by-key (rocPRIM partition with decoupled look-back) of PyTorch's embedding backward: that kernel
     faults under hipGraph replay on ROCm (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION in
     rocprim::partition_kernel on the first replay of a captured BERT fwd+bwd, diagnosed in round 1), and
     corrupted the captured training step (non-finite loss after ~10 replays). index_add_'s float atomics made runs
-    differ in the last bits (repeated positions / tokens), which the emb_bwd_det kernel removes."""
+    differ in the last bits (repeated positions / tokens), which the deterministic kernels remove. (A first version
+    summed each id on ONE workgroup: the two token-type rows, 2048 occurrences each, cost ~0.5 ms per BERT-base step,
+    profiles/bert_steady_r4d.md.)"""
 
     @staticmethod
     def forward(ctx, ids, weight):
@@ -308,8 +311,10 @@ class _Embedding(torch.autograd.Function):
         if dy.is_cuda and flat.numel() <= 32768 and dy.dtype in (torch.float32, torch.bfloat16):
             idl = flat.to(torch.int64).contiguous()
             d2 = dy.reshape(-1, H).contiguous()
+            part = torch.empty(idl.numel(), H, device=dy.device, dtype=torch.float32)
+            heavy = torch.empty(idl.numel(), device=dy.device, dtype=torch.int32)
             check(_fns()["emb_bwd"](int(d2.dtype == torch.bfloat16), ptr(idl), idl.numel(), ptr(d2), H, V, ptr(g),
-                                    stream_handle(dy.device)), "mifx_bert_emb_bwd")
+                                    ptr(part), ptr(heavy), stream_handle(dy.device)), "mifx_bert_emb_bwd")
         else:
             g.index_add_(0, flat, dy.reshape(-1, H).float())
         return None, g.to(ctx.wdtype)
