@@ -14,5 +14,5 @@ for P in "$P1" "$P2"; do
   echo "pmc pass $i ok"
 done
 timeout -s KILL 180 rocprofv3 --kernel-trace --stats -d gpurun_out/pmcg_r4_t -o kt -- python3 tools/pmc_gemm_probe.py --reps 10 > gpurun_out/pmcg_r4_t.log 2>&1 || { tail -5 gpurun_out/pmcg_r4_t.log; exit 1; }
-f=$(find gpurun_out/pmcg_r4_t -name "*kernel_stats.csv" | head -1); cp "$f" gpurun_out/gemm_probe_kernel_stats_r4.csv; rm -rf gpurun_out/pmcg_r4_t
+true
 head -30 gpurun_out/gemm_pmc_r4_1.md
