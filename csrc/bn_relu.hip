@@ -237,8 +237,11 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restr
 
 // y = relu(x * scale + shift) (relu optional). Same [row slice x channel group] layout as the
 // reductions: a thread keeps its 8 channels' scale/shift in registers across all its rows.
+// x2 != null (inference over a residual sum): s = x + x2 rounded to T is written to s_out and normalised, as the
+// training forward's load_sum does
 template <typename T>
-__global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, long long M, int C,
+__global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, const T* __restrict__ x2,
+                                                    T* __restrict__ s_out, long long M, int C,
                                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                                     int relu, T* __restrict__ y) {
   const int tpr = C / kVec, rpb = kThreads / tpr;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, lo
   ld8f(shift + c0, sh);
   for (int r = r0 + slice; r < r1; r += rpb) {
     float u[kVec];
-    ldv(x + (size_t)r * C + c0, u);
+    load_sum(x, x2, s_out, (size_t)r * C + c0, u);
 #pragma unroll
     for (int e = 0; e < kVec; ++e) {
       const float t = fmaf(u[e], sc[e], sh[e]);
@@ -442,24 +445,33 @@ int mifx_bn_relu_fwd(int dtype, const void* x, const void* x2, void* sum_out, lo
                      stats + 2 * C, stats + 3 * C);
   if (dtype)
     hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
-                       (const __hip_bfloat16*)xa, M, C, stats + 2 * C, stats + 3 * C, relu, (__hip_bfloat16*)y);
+                       (const __hip_bfloat16*)xa, (const __hip_bfloat16*)nullptr, (__hip_bfloat16*)nullptr, M, C, stats + 2 * C, stats + 3 * C, relu, (__hip_bfloat16*)y);
   else
-    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)xa, M, C,
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)xa,
+                       (const float*)nullptr, (float*)nullptr, M, C,
                        stats + 2 * C, stats + 3 * C, relu, (float*)y);
   return (int)hipGetLastError();
 }
 
 // eval / inference: y = relu(x * scale + shift) with precomputed per-channel scale / shift
-int mifx_bn_relu_apply(int dtype, const void* x, long long M, int C, const float* scale, const float* shift, int relu,
-                       void* y, hipStream_t st) {
-  if (!shape_ok(M, C)) return -1;
+// inference BatchNorm (+ ReLU) with precomputed per-channel scale / shift; x2 / s_out non-null: over the residual
+// sum s = x + x2, also written to s_out (the identity shortcut of the next block reads it)
+int mifx_bn_add_relu_apply(int dtype, const void* x, const void* x2, void* s_out, long long M, int C,
+                           const float* scale, const float* shift, int relu, void* y, hipStream_t st) {
+  if (!shape_ok(M, C) || (x2 != nullptr) != (s_out != nullptr)) return -1;
   if (dtype)
     hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
-                       (const __hip_bfloat16*)x, M, C, scale, shift, relu, (__hip_bfloat16*)y);
+                       (const __hip_bfloat16*)x, (const __hip_bfloat16*)x2, (__hip_bfloat16*)s_out, M, C, scale, shift,
+                       relu, (__hip_bfloat16*)y);
   else
-    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)x, M, C, scale,
-                       shift, relu, (float*)y);
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)x,
+                       (const float*)x2, (float*)s_out, M, C, scale, shift, relu, (float*)y);
   return (int)hipGetLastError();
+}
+
+int mifx_bn_relu_apply(int dtype, const void* x, long long M, int C, const float* scale, const float* shift, int relu,
+                       void* y, hipStream_t st) {
+  return mifx_bn_add_relu_apply(dtype, x, nullptr, nullptr, M, C, scale, shift, relu, y, st);
 }
 
 // backward: stats = forward's [mean, rstd, scale, shift]; part = scratch [2, blocks, C];

@@ -20,6 +20,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from mifx.models.resnet import resnet50_v2  # noqa: E402
+from mifx.models.resnet_infer import FoldedResNetV2  # noqa: E402
 from mifx.serving.tensorstore import TensorStore  # noqa: E402
 
 SCRIPT = """
@@ -59,7 +60,7 @@ def main(repeats: int = 5) -> dict:
     model = resnet50_v2(1001)          # TF-Hub resnet_v2_50 has 1001 classes (0 = background)
     model = model.to(memory_format=torch.channels_last) if gpu else model
     rai.execute_command("AI.MODELSET", "imagenet_model", "TORCH", dev, "INPUTS", "images", "OUTPUTS", "output",
-                        _NHWCModel(model))
+                        _FoldedNHWCModel(model))
     rai.execute_command("AI.SCRIPTSET", "imagenet_script", dev, SCRIPT)
 
     lat = {}
@@ -82,20 +83,24 @@ def main(repeats: int = 5) -> dict:
     return lat
 
 
-class _NHWCModel(torch.nn.Module):
-    """Model wrapper taking the [1, H, W, 3] float image the TF-style script produces."""
+class _FoldedNHWCModel(torch.nn.Module):
+    """The served model, taking the [1, H, W, 3] float image the TF-style script produces. On the GPU the eval-mode
+    network runs folded (BatchNorms inside the convolutions, mifx.models.resnet_infer) and captured in one hipGraph
+    per input shape, built on the first call (after MODELSET moved the module to the device and set eval mode)."""
 
     def __init__(self, m):
         super().__init__()
         self.m = m
+        self._run, self._shape = None, None
 
     def forward(self, x):
         x = x.permute(0, 3, 1, 2)
-        if x.is_cuda:
-            x = x.contiguous(memory_format=torch.channels_last)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                return self.m(x).float()
-        return self.m(x)
+        if not x.is_cuda:
+            return self.m(x)
+        x = x.contiguous(memory_format=torch.channels_last)
+        if self._run is None or self._shape != tuple(x.shape):
+            self._run, self._shape = FoldedResNetV2(self.m.eval()).graphed(x), tuple(x.shape)
+        return self._run(x)
 
 
 if __name__ == "__main__":

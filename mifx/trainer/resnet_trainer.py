@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from ..models.resnet import resnet50_v2
+from ..ops.bn_relu import defer_batch_counts
 from ..ops.image_ops import IMAGENET_MEAN, IMAGENET_STD, crop_flip_normalize
 from ..parallel import dist as mdist
 from ..parallel.ddp import DataParallel
@@ -55,6 +56,7 @@ class ResNetTrainer:
         self.rank = torch.distributed.get_rank(process_group) if process_group is not None else 0
         torch.manual_seed(seed)
         self.model = resnet50_v2(num_classes).to(self.device).to(memory_format=torch.channels_last)
+        self._bn_count = defer_batch_counts(self.model)  # one counter kernel per forward, not one per BatchNorm
         self.dp = DataParallel(self.model, process_group, grad_as_bucket_view=True) \
             if process_group is not None else None
         decay = [p for n, p in self.model.named_parameters() if p.ndim > 1]
@@ -79,6 +81,10 @@ class ResNetTrainer:
             self._idx_dev = torch.zeros(n, dtype=torch.int64, device=self.device)
             self._step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._neg_lr = torch.zeros((), dtype=torch.float32, device=self.device)  # 0-dim: a foreach scalar
+
+    def _count_forward(self) -> None:
+        if self._bn_count is not None and self.model.training:
+            self._bn_count.add_(1)
 
     def _lr(self) -> float:
         return self.base_lr * min(1.0, (self.step_idx + 1) / max(1, self.warmup))
@@ -112,6 +118,7 @@ class ResNetTrainer:
             y = self.labels[idx]
             with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
                 loss = F.cross_entropy(self.model(x).float(), y) / self.accum
+            self._count_forward()
             last = m == self.accum - 1
             if self.dp is not None and not last:
                 with self.dp.no_sync():
@@ -160,6 +167,7 @@ class ResNetTrainer:
                 y = self.labels[idx]
                 with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
                     loss = F.cross_entropy(self.model(x).float(), y) / self.accum
+                self._count_forward()
                 loss.backward()
                 total = loss.detach() if total is None else total + loss.detach()
         return total
@@ -204,7 +212,8 @@ class ResNetTrainer:
     # ---------------------------------------------------------------- checkpoint / resume
     def state_dict(self) -> dict:
         """Weights, BatchNorm running statistics, the SGD momentum buffers and the step (flat tensor dict)."""
-        sd = {f"model.{k}": v.detach().contiguous() for k, v in self.model.state_dict().items()}
+        # (clone: the BatchNorm counters are views of one tensor, which safetensors would refuse as shared memory)
+        sd = {f"model.{k}": v.detach().clone() for k, v in self.model.state_dict().items()}
         for i, p in enumerate(self.model.parameters()):
             buf = self.opt.state.get(p, {}).get("momentum_buffer")
             if buf is not None:
