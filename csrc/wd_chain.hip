@@ -443,6 +443,7 @@ struct TailArgs {
   OptHyper hd, hw;
   long long* dbg;                // optional [grid][8] real-time stamps (tools/tail_stamps.py); null = off
   int nsteps;                    // PERSIST: training steps per launch
+  int helpers;                   // > 0: the one-row tail (help_update) with this many optimizer workgroups
 };
 #define TSTAMP(i)                                                                      \
   do {                                                                                 \
@@ -481,6 +482,44 @@ __device__ __forceinline__ bool grid_sync(unsigned long long* bar, int* err, int
   }
   __syncthreads();
   return *s_flag != 0;
+}
+
+// ---- one-row tail (TAIL with ta.helpers = H > 0), for batches ONE workgroup trains (the reference batch of 40):
+// the launch is 1 + H workgroups. Workgroup 0 runs the step and publishes its gradient row (ta.bar = the step);
+// workgroups 1..H are the optimizer -- one thread per slab column and step slot h - 1, exactly wd_opt1_sc's
+// workgroups (csrc/wide_deep.hip), so the update is bit-identical -- which load their columns' master weights and
+// optimizer state at launch, under workgroup 0's step, then wait for the row. This replaces the separate optimizer
+// launch: its ramp, kernel-argument and state loads no longer follow the step. The wait is bounded by wall-clock
+// time (a timeout sets ta.err and skips the update; the host raises). ta.bar holds the last published step and is
+// reset by the host whenever the step counters are rewritten (resume), so a stale value can never match.
+template <int NTHR>
+__device__ void help_update(const TailArgs& ta, const float* __restrict__ slab, int stride, int* s_flag) {
+  const int hb = (int)blockIdx.x - 1;
+  const int gi = hb * NTHR + (int)threadIdx.x;
+  const ScState st = sc_load(gi, stride, ta.wsc, ta.param, ta.s0, ta.s1);
+  const long long step = ta.step_slots[hb] + 1;
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    const long long t0 = wall_clock64();
+    // relaxed polls: an acquire load per poll would invalidate this XCD's L2 every time (workgroup 0 may share it);
+    // the row itself is read past the caches below
+    while ((long long)__hip_atomic_load(ta.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != step) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > TAIL_TIMEOUT_TICKS) {
+        __hip_atomic_store(ta.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *s_flag = ok;
+  }
+  __syncthreads();
+  if (!*s_flag) return;
+  if (gi < stride) {
+    const float g = ld_sys1(slab + gi);  // written by workgroup 0, possibly on another XCD: read past the caches
+    sc_update(gi, st, g, ta.hd, ta.hw, step, ta.param, ta.s0, ta.s1, ta.wt_out);
+  }
+  if (threadIdx.x == 0) ta.step_slots[hb] = step;
 }
 
 // ---- persistent small-batch training (PERSIST = true): ONE workgroup runs `nsteps` whole training steps of a
@@ -564,6 +603,12 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   (void)stamp_on;
   STAMP(0);
   BSTAMP(0);
+  if constexpr (TRAIN && TAIL) {
+    if (ta.helpers > 0 && blockIdx.x > 0) {  // one-row tail: an optimizer workgroup
+      help_update<NTHR>(ta, slab, stride, (int*)lds);
+      return;
+    }
+  }
   // the XCD this workgroup's slab row is written from (its L2 holds the row for the XCD-local reduction,
   // csrc/wide_deep.hip wd_reduce_xcd)
   if constexpr (TAIL) TSTAMP(0);
@@ -1045,6 +1090,15 @@ __global__ __launch_bounds__(64 * (T / (16 * TBN)), 1) void wdc_fused(const uint
   STAMP(17);
   BSTAMP(2);
   if constexpr (TRAIN && TAIL) {
+    if (ta.helpers > 0) {  // one-row tail: publish the gradient row (slab row 0) to the optimizer workgroups
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __threadfence();  // agent-scope release: this XCD's L2 written back, the row visible to every XCD
+        __hip_atomic_store(ta.bar, (unsigned long long)(step0 + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
     const int G = gridDim.x, b = blockIdx.x, S4 = stride / 4;
     int* tl = (int*)(lds + LS);  // the staging area is free now
     int* rows = tl;              // [256] rows written on this XCD, ascending
@@ -1257,6 +1311,50 @@ int WDC_SYM(mifx_wdc_fused)(const void* data, long long n_data, long long batch,
                                    logits_out, grad_scale, grid, train, tmap, stride, waves, nullptr, stream);
 }
 
+// One training step of a batch ONE workgroup trains, with the optimizer in the same launch (help_update): grid
+// 1 + helpers, helpers = ceil(stride / threads per workgroup) (wd_opt1_sc's workgroup count at 256 threads). State in
+// slab-column order (wsc / param / s0 / s1, step slots); bar / err as mifx_wdc_fused_tail. T = 64 build: 4 waves;
+// T = 128 build: 8 waves.
+int WDC_SYM(mifx_wdc_fused_help)(const void* data, long long n_data, long long batch, long long* step_ctr, void* wimg,
+                                 float* wide, float* slab, float* slab_loss, float grad_scale, const int* tmap,
+                                 int stride, unsigned long long* bar, int* err, const int* wsc, float* param,
+                                 float* s0, float* s1, const float* hyper_dnn, const float* hyper_wide, int helpers,
+                                 long long feed_stride, long long feed_offset, unsigned long long shuffle_key,
+                                 hipStream_t stream) {
+#if WDC_T == 256
+  return -1;
+#else
+  constexpr int NTHR_H = WDC_T == 64 ? 256 : 512;  // threads of the TBN = 1 shape (4 / 8 waves)
+  if (n_data <= 0 || batch <= 0 || batch > T || batch > n_data || helpers <= 0 || helpers + 1 > STEP_SLOTS ||
+      (long long)helpers * NTHR_H < stride)
+    return -1;
+  if (wimg == nullptr || wide == nullptr || slab == nullptr || tmap == nullptr || bar == nullptr || err == nullptr ||
+      wsc == nullptr || param == nullptr || s0 == nullptr || s1 == nullptr || step_ctr == nullptr ||
+      hyper_dnn == nullptr || hyper_wide == nullptr)
+    return -1;
+  if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0 || stride < WIDE_PAD || stride % 4 != 0) return -1;
+  if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
+  TailArgs ta{};
+  ta.bar = bar;
+  ta.err = err;
+  ta.wsc = wsc;
+  ta.param = param;
+  ta.s0 = s0;
+  ta.s1 = s1;
+  ta.wt_out = (uint16_t*)wimg;
+  ta.step_slots = step_ctr;
+  ta.helpers = helpers;
+  ta.hd = OptHyper{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                   hyper_dnn[6], hyper_dnn[7]};
+  ta.hw = OptHyper{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                   hyper_wide[6], hyper_wide[7]};
+  launch<true, 1, true>(dim3(1 + helpers), stream, data, n_data, batch, 0, step_ctr, wimg, wide, slab, slab_loss,
+                        nullptr, grad_scale, tmap, stride, nullptr, MifxFeed{feed_stride, feed_offset, shuffle_key},
+                        ta);
+  return (int)hipGetLastError();
+#endif
+}
+
 #if WDC_T == 128  // the in-kernel tail and the persistent kernel exist for the 8-wave T = 128 shape only
 
 // Training step with the in-kernel tail (slab reduction + optimizer inside the launch; see TailArgs): 8-wave
@@ -1282,7 +1380,7 @@ int mifx_wdc_fused_tail(const void* data, long long n_data, long long batch, lon
     return -1;
   if ((uintptr_t)wimg % 16 != 0 || (uintptr_t)data % 16 != 0 || stride < WIDE_PAD || stride % 4 != 0) return -1;
   if (feed_stride < batch || feed_offset < 0 || feed_offset + batch > feed_stride) return -1;
-  TailArgs ta;
+  TailArgs ta{};
   ta.xpart = xpart;
   ta.bar = bar;
   ta.err = err;

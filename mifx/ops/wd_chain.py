@@ -10,6 +10,11 @@ from . import _lib
 from ._lib import F32, I32, I64, U64, VP, check, ptr, sig, stream_handle
 
 
+# mifx_wdc_fused_help: records, n_data, batch, step slots, image, wide, slab, slab_loss, grad_scale, tile map, stride,
+# bar, err, wsc, param, s0, s1, hyper dnn / wide, helpers, feed stride / offset / key, stream
+HELP_SIG = [VP, I64, I64, VP, VP, VP, VP, VP, F32, VP, I32, VP, VP, VP, VP, VP, VP, VP, VP, I32, I64, I64, U64, VP]
+
+
 @functools.lru_cache(maxsize=None)
 def _fns():
     lib = _lib.load("wd_chain")
@@ -25,6 +30,7 @@ def _fns():
                                                        VP, VP, VP, VP, VP, VP, VP, VP, I64, I64, U64, VP]),
         "persist": sig(lib, "mifx_wdc_persist", [VP, I64, I64, VP, VP, VP, VP, VP, F32, VP, I32, VP, VP, VP, VP, VP, VP,
                                                  I32, I64, I64, U64, VP]),
+        "help": sig(lib, "mifx_wdc_fused_help", HELP_SIG),
     }
 
 
@@ -40,6 +46,7 @@ def _fns64():
                                                      I32, I32, VP, VP]),
         "fused_f": sig(lib, "mifx_wdc_fused_f_t64", [VP, I64, I64, I64, VP, VP, VP, VP, VP, VP, F32, I32, I32, VP,
                                                      I32, I32, VP, I64, I64, U64, VP]),
+        "help": sig(lib, "mifx_wdc_fused_help_t64", HELP_SIG),
     }
 
 
@@ -143,6 +150,41 @@ class InKernelTail:
         if int(self.err.item()) != 0:
             raise RuntimeError("W&D in-kernel tail: a grid barrier timed out (workgroups not co-resident); the "
                                "step skipped its update")
+
+
+class OneRowTail:
+    """One launch per step for a batch ONE workgroup trains (csrc/wd_chain.hip help_update): workgroup 0 runs the
+    fused step, `helpers` more workgroups run the optimizer over the slab columns (wd_opt1_sc's partition: one thread
+    per column, step slot per workgroup), loading their state during the step and updating once workgroup 0 has
+    published the gradient row. `bar` holds the last published step (reset whenever the step slots are rewritten);
+    `err` is the sticky timeout flag (`check()` raises)."""
+
+    def __init__(self, stride: int, tile: int, device):
+        self.stride, self.tile = int(stride), int(tile)
+        threads = 256 if self.tile == 64 else 512
+        self.helpers = -(-self.stride // threads)
+        self.bar = torch.empty(1, dtype=torch.int64, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.reset()
+
+    def reset(self) -> None:
+        self.bar.fill_(-1)  # matches no step
+
+    def step(self, tr) -> None:
+        c = constants()
+        if tr.wt.numel() != c["LWEND"] or tr.tmap.numel() != c["NTILE"] or tr.stride != self.stride:
+            raise ValueError("trainer buffers do not match the chained kernel")
+        rc = fns_for(self.tile)["help"](ptr(tr.records), tr.n_data, tr.batch, ptr(tr.step_ctr), ptr(tr.wt),
+                                        ptr(tr.wide_weights), ptr(tr.slab), ptr(tr.slab_loss), float(tr.grad_scale),
+                                        ptr(tr.tmap), int(tr.stride), ptr(self.bar), ptr(self.err), ptr(tr.wsc),
+                                        ptr(tr.param_sc), ptr(tr.s0_sc), ptr(tr.s1_sc), ptr(tr.h_dnn), ptr(tr.h_wide),
+                                        int(self.helpers), *tr.feed_args(), stream_handle(tr.records.device))
+        check(rc, "mifx_wdc_fused_help")
+
+    def check(self) -> None:
+        if int(self.err.item()) != 0:
+            raise RuntimeError("W&D one-launch step: the optimizer workgroups timed out waiting for the gradient row; "
+                               "the step skipped its update")
 
 
 def persist_steps(tr, nsteps: int) -> None:

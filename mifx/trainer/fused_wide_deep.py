@@ -61,7 +61,7 @@ class FusedWideDeepTrainer:
                  dnn_opt: OptSpec | None = None, wide_opt: OptSpec | None = None, loss_reduction: str = "sum",
                  grid: int | None = None, process_group=None, max_grid: int = 256, compact_slab: bool = True,
                  live_staging: bool = False, fused_update: bool = True, kernel: str = "chain", waves: int = 8,
-                 in_kernel_tail: bool | None = None, persistent: bool | None = None,
+                 in_kernel_tail: bool | None = None, persistent: bool | None = None, one_launch: bool | None = None,
                  small_tile: bool | None = None, shuffle_seed: int = 0, feed_stride: int | None = None,
                  feed_offset: int = 0, large_tile: bool | None = None):
         """shuffle_seed: 0 trains on the records in stored order; any other value draws a fresh pseudo-random
@@ -197,6 +197,22 @@ class FusedWideDeepTrainer:
                                                   and not self._persist and self._ktail is None) else 128
         if self.tile == 64:
             self.waves = 4
+        # one launch per step when ONE workgroup trains the batch (opt-in: one_launch=True or MIFX_WD_ONE_LAUNCH=1;
+        # grid 1, one rank): the optimizer runs in extra workgroups of the fused launch, which load their columns'
+        # state during the step and update once workgroup 0 has published the gradient row (csrc/wd_chain.hip
+        # help_update), instead of in a second kernel after it. Bit-identical to the two-kernel step (wd_opt1_sc's
+        # partition and step slots). Measured at the reference batch of 40: 13.55 vs 13.25 us per step
+        # (profiles/wd_one_launch_ab_r4.txt; 17.6 with acquire-ordered polls, which invalidate L2 on every poll) --
+        # the flag poll and the cache-bypassing read of the row after it cost what the saved launch did.
+        if one_launch is None:
+            one_launch = os.environ.get("MIFX_WD_ONE_LAUNCH", "0") == "1"
+        self._one = None
+        if one_launch and self._sc and self.world == 1 and self.grid == 1 and self.fused_update \
+                and not self._persist and self._ktail is None and self.device.type == "cuda" \
+                and (self.tile == 64 or (self.tile == 128 and self.waves == 8)):
+            from ..ops import wd_chain as wdc
+
+            self._one = wdc.OneRowTail(self.stride, self.tile, dev)
         self.slab_loss = torch.zeros(self.grid, device=dev)
         self.nsplit = max(1, min(16, self.grid // 8))
         self.partial = torch.empty(self.nsplit, self.stride, device=dev)
@@ -396,6 +412,9 @@ class FusedWideDeepTrainer:
         if self._ktail is not None:  # one launch: fwd/bwd + slab reduction + optimizer
             self._ktail.step(self)
             return
+        if self._one is not None:  # one launch: fwd/bwd of the one workgroup + the optimizer workgroups
+            self._one.step(self)
+            return
         if self._xg is not None:  # data parallel over xGMI: no host collective, graph-capturable
             self._launch(self.records, self.n_data, self.batch, 0, self.step_ctr, self.slab, self.slab_loss, None,
                          self.grid, True)
@@ -443,6 +462,8 @@ class FusedWideDeepTrainer:
             self._xg.check()
         if self._ktail is not None:
             self._ktail.check()
+        if getattr(self, "_one", None) is not None:
+            self._one.check()
 
     def disable_xgmi(self) -> None:
         if self._xg is not None:
@@ -555,6 +576,8 @@ class FusedWideDeepTrainer:
 
     def set_step(self, step: int) -> None:
         self.step_ctr.fill_(int(step))
+        if getattr(self, "_one", None) is not None:
+            self._one.reset()  # the published-step flag must not match a rewound step
 
     def gradients_once(self) -> np.ndarray:
         """Run fwd/bwd on the current batch WITHOUT updating; return the tile-native gradient (index it with

@@ -606,3 +606,35 @@ def test_large_tile_matches_t128(batch):
     for name, r in ref.items():
         rel = np.linalg.norm(named[name].reshape(r.shape) - r) / (np.linalg.norm(r) + 1e-8)
         assert rel < 0.06, f"{name}: relative Frobenius err {rel:.4f}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [40, 100])
+def test_one_launch_step_bit_identical(batch):
+    """The one-launch step (csrc/wd_chain.hip help_update: the optimizer in extra workgroups of the fused launch,
+    waiting for workgroup 0's gradient row) trains bit-identically to the fused kernel + wd_opt1_sc two-kernel step:
+    eager steps, captured multi-step graphs, and a checkpoint rewind in between (which resets the published-step
+    flag). Batch 40: the T = 64 build; 100: the 8-wave T = 128 build."""
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    dev = torch.device("cuda")
+    rec = synthetic_records(batch * 5 + 77, device=dev, seed=43)
+    out = {}
+    for one in (False, True):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=8), batch=batch, device=dev, one_launch=one,
+                                  shuffle_seed=0x5EED)
+        assert (tr._one is not None) == one
+        tr.set_data(rec)
+        for _ in range(3):
+            tr.step()
+        tr.capture(steps_per_graph=4)  # (its warm-up steps are real steps)
+        ck = tr.state_dict()
+        tr.run(8)
+        mid = tr.param.clone()
+        tr.load_state_dict(ck)  # rewind and train the same 8 steps again
+        tr.run(8)
+        torch.cuda.synchronize()
+        assert torch.equal(tr.param, mid)
+        out[one] = (tr.param.clone(), tr.s0.clone(), tr.steps_done, tr.last_loss())
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
+    assert out[True][2] == out[False][2] and out[True][3] == out[False][3]
