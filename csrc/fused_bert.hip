@@ -17,6 +17,7 @@
 // written in bf16 directly, no cast kernels around each call); statistics and reductions are fp32.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include "counter_rng.h"
@@ -941,9 +942,16 @@ __global__ __launch_bounds__(256) void emb_bwd_combine(const long long* __restri
 
 extern "C" {
 
-// partial-row count used by add_ln_bwd (fewer, fatter blocks: each wave walks many rows)
+// partial-row count used by add_ln_bwd (fewer, fatter blocks: each wave walks many rows). Rows per wave:
+// MIFX_BERT_LN_RPW, default 2 -- measured on the BERT-base step: 5199-5208 seq/s against 5139-5149 at 1 (twice the
+// partial rows for the column reduction) and 5192-5195 at 4 (profiles/bert_ln_rpw_ab_r4.txt)
 int mifx_bert_ln_blocks(int R) {
-  const int need = (R + 7) / 8;  // 2 rows per wave
+  static const int rpw = [] {
+    const char* e = getenv("MIFX_BERT_LN_RPW");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  const int need = (R + 4 * rpw - 1) / (4 * rpw);
   return need < 1024 ? (need > 0 ? need : 1) : 1024;
 }
 
