@@ -41,21 +41,26 @@ struct Geo {
 
 // amdgpu_waves_per_eu(4): 4 workgroups per CU (40 KB LDS each) -- the loop is latency-bound, occupancy pays
 // (profiles/gconv_bk_ab_r2.txt, gconv_prefetch_ab_r2.txt: deeper prefetch / wider chunks that cost occupancy lose)
+// ksplit > 1 (few pixel tiles, e.g. batch-1 inference): blockIdx.z = g * ksplit + split, the workgroup reduces
+// steps [nsteps split / ksplit, nsteps (split + 1) / ksplit) and writes its fp32 partial to part[split][M][G*K]
+// (gconv_splitk_finish adds the splits in order, + bias, ReLU)
 template <int BN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                       const float* __restrict__ bias, bf16* __restrict__ y, Geo d,
-                                                      int relu) {
+                                                      int relu, float* __restrict__ part, int ksplit) {
   constexpr int BCH = (BN * 4 + kThreads - 1) / kThreads;  // 16-byte weight chunks per thread per step (2, 1, 1)
   // one LDS block: double-buffered A and B staging, reused as the epilogue's output tile
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * BM * LDR + 2 * BN * LDR];
   bf16(*As)[BM * LDR] = reinterpret_cast<bf16(*)[BM * LDR]>(smem);
   bf16(*Bs)[BN * LDR] = reinterpret_cast<bf16(*)[BN * LDR]>(smem + 2 * BM * LDR);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int g = blockIdx.z, n0 = blockIdx.y * BN;
+  const int g = (int)blockIdx.z / ksplit, split = (int)blockIdx.z - g * ksplit, n0 = blockIdx.y * BN;
   const long long M = (long long)d.N * d.Ho * d.Wo;
   const long long m0 = (long long)blockIdx.x * BM;
   const int CT = d.G * d.C;  // input row stride (channels)
-  const int chunks_c = d.C / BK, nsteps = d.R * d.S * chunks_c;
+  const int chunks_c = d.C / BK, nsteps_all = d.R * d.S * chunks_c;
+  const int s_begin = (int)((long long)nsteps_all * split / ksplit);
+  const int s_end = (int)((long long)nsteps_all * (split + 1) / ksplit);
 
   // this thread's two A chunks: pixel rows ap[j] = (t >> 2) + 64 j, 16-byte part (t & 3)
   int an[2], ah[2], aw[2];
@@ -111,12 +116,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int wm = (wv >> 1) * 64, wn = (wv & 1) * (BN / 2);
   const int fr = lane & 15, fk = (lane >> 4) * 8;
 
-  load(0);
+  load(s_begin);
   store(0);
   __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
-    const int buf = step & 1;
-    if (step + 1 < nsteps) load(step + 1);
+  for (int step = s_begin; step < s_end; ++step) {
+    const int buf = (step - s_begin) & 1;
+    if (step + 1 < s_end) load(step + 1);
     v8bf af[4], bfr[TN];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *(const v8bf*)(&As[buf][(wm + 16 * i + fr) * LDR + fk]);
@@ -126,8 +131,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
-    if (step + 1 < nsteps) store(buf ^ 1);
+    if (step + 1 < s_end) store(buf ^ 1);
     __syncthreads();
+  }
+
+  if (part != nullptr) {  // split-K: this split's fp32 partial (bias / ReLU in gconv_splitk_finish)
+    const int KT = d.G * d.K;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int ch = g * d.K + n0 + wn + 16 * j + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long long m = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
+          if (m < M) part[((size_t)split * M + m) * KT + ch] = acc[i][j][e];
+        }
+    }
+    return;
   }
 
   // epilogue: acc[i][j][e] = y[pixel m0 + wm + 16 i + 4 (lane >> 4) + e][channel n0 + wn + 16 j + (lane & 15)].
@@ -157,6 +178,34 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
     const long long m = m0 + row;
     if (m < M) *(u4*)(y + m * KT + g * d.K + n0 + part) = *(const u4*)(&Cs[row * CLD + part]);
   }
+}
+
+// y = bf16(relu(sum over splits of part[s] + bias)), splits added in order; 8 channels per thread
+__global__ __launch_bounds__(kThreads) void gconv_splitk_finish(const float* __restrict__ part, int ksplit, long long M,
+                                                               int KT, const float* __restrict__ bias, int relu,
+                                                               bf16* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= M * KT / 8) return;
+  const size_t base = (size_t)i * 8;
+  float a[8];
+  {
+    const float4 lo = *(const float4*)(part + base), hi = *(const float4*)(part + base + 4);
+    a[0] = lo.x, a[1] = lo.y, a[2] = lo.z, a[3] = lo.w, a[4] = hi.x, a[5] = hi.y, a[6] = hi.z, a[7] = hi.w;
+  }
+  for (int s = 1; s < ksplit; ++s) {
+    const float* p = part + (size_t)s * M * KT + base;
+    const float4 lo = *(const float4*)p, hi = *(const float4*)(p + 4);
+    a[0] += lo.x, a[1] += lo.y, a[2] += lo.z, a[3] += lo.w, a[4] += hi.x, a[5] += hi.y, a[6] += hi.z, a[7] += hi.w;
+  }
+  const int c = (int)(base % KT);
+  v8bf o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = a[e] + (bias ? bias[c + e] : 0.f);
+    if (relu) v = fmaxf(v, 0.f);
+    o[e] = (bf16)v;
+  }
+  *(v8bf*)(y + base) = o;
 }
 
 // ---- input gradient of a STRIDED convolution -----------------------------------------------------------
@@ -494,28 +543,60 @@ int mifx_gconv_dgrad_strided(const void* dy, const void* wt, void* dx, int N, in
 // x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
 // zero padding `pad` on every side, Ho = (Hi + 2 pad - R) / stride + 1, relu != 0: y = max(y, 0).
 // Needs C % 32 == 0 and K % 32 == 0.
-int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
-                   int K, int R, int S, int pad, int stride, int relu, hipStream_t st) {
-  if (stride <= 0) return -1;
+int mifx_gconv_fwd_splitk(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G,
+                          int C, int K, int R, int S, int pad, int stride, int relu, float* part, int ksplit,
+                          hipStream_t st) {
+  if (stride <= 0 || ksplit <= 0 || (ksplit > 1 && part == nullptr)) return -1;
   const int Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
-  if (N <= 0 || G <= 0 || G > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 32 != 0 || Hi + 2 * pad < R ||
-      Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S)
+  if (N <= 0 || G <= 0 || (long long)G * ksplit > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 32 != 0 ||
+      Hi + 2 * pad < R || Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S || ksplit > R * S * (C / BK))
     return -1;
   const Geo d{N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride};
   const long long M = (long long)N * Ho * Wo;
   const long long mt = (M + BM - 1) / BM;
   if (mt > 0x7fffffffLL) return -1;
+  float* pp = ksplit > 1 ? part : nullptr;
+  const unsigned gz = (unsigned)(G * ksplit);
   if (K % 128 == 0) {
-    hipLaunchKernelGGL(gconv_fwd<128>, dim3((unsigned)mt, K / 128, G), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d, relu);
+    hipLaunchKernelGGL(gconv_fwd<128>, dim3((unsigned)mt, K / 128, gz), dim3(kThreads), 0, st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit);
   } else if (K % 64 == 0) {
-    hipLaunchKernelGGL(gconv_fwd<64>, dim3((unsigned)mt, K / 64, G), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d, relu);
+    hipLaunchKernelGGL(gconv_fwd<64>, dim3((unsigned)mt, K / 64, gz), dim3(kThreads), 0, st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit);
   } else {  // e.g. the 96-channel layers of PATE's inference_deeper
-    hipLaunchKernelGGL(gconv_fwd<32>, dim3((unsigned)mt, K / 32, G), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d, relu);
+    hipLaunchKernelGGL(gconv_fwd<32>, dim3((unsigned)mt, K / 32, gz), dim3(kThreads), 0, st, (const bf16*)x,
+                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit);
+  }
+  if (ksplit > 1) {
+    const long long n8 = M * G * K / 8;
+    hipLaunchKernelGGL(gconv_splitk_finish, dim3((unsigned)((n8 + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                       (const float*)part, ksplit, M, G * K, bias, relu, (bf16*)y);
   }
   return (int)hipGetLastError();
+}
+
+// x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
+// zero padding `pad` on every side, Ho = (Hi + 2 pad - R) / stride + 1, relu != 0: y = max(y, 0).
+// Needs C % 32 == 0 and K % 32 == 0.
+int mifx_gconv_fwd(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
+                   int K, int R, int S, int pad, int stride, int relu, hipStream_t st) {
+  return mifx_gconv_fwd_splitk(x, w, bias, y, N, Hi, Wi, G, C, K, R, S, pad, stride, relu, nullptr, 1, st);
+}
+
+// reduction splits for a forward whose pixel x channel tiles cannot fill the chip (batch-1 inference): enough
+// workgroups for ~all CUs, >= 4 reduction steps of 32 channels per split, at most 32 splits; 1 = no split
+int mifx_gconv_fwd_ksplit(int N, int Hi, int Wi, int G, int C, int K, int R, int S, int pad, int stride) {
+  if (stride <= 0 || C % BK != 0 || K % 32 != 0) return 1;
+  const long long Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
+  const long long M = (long long)N * Ho * Wo;
+  const int bn = K % 128 == 0 ? 128 : K % 64 == 0 ? 64 : 32;
+  const long long tiles = ((M + BM - 1) / BM) * (K / bn) * G;
+  const int nsteps = R * S * (C / BK);
+  if (tiles >= 128) return 1;
+  int ks = (int)((256 + tiles - 1) / tiles);
+  ks = ks < nsteps / 4 ? ks : nsteps / 4;
+  ks = ks < 32 ? ks : 32;
+  return ks > 1 ? ks : 1;
 }
 
 }  // extern "C"

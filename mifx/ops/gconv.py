@@ -22,6 +22,8 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 def _fns():
     lib = _lib.load("gconv")
     return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 11 + [VP]),
+            "fwd_sk": sig(lib, "mifx_gconv_fwd_splitk", [VP, VP, VP, VP] + [I32] * 11 + [VP, I32, VP]),
+            "ksplit": sig(lib, "mifx_gconv_fwd_ksplit", [I32] * 10),
             "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 11 + [VP, VP]),
             "wsplits": sig(lib, "mifx_gconv_wgrad_splits", [I32] * 10),
             "dgrad_s": sig(lib, "mifx_gconv_dgrad_strided", [VP, VP, VP] + [I32] * 10 + [VP])}
@@ -52,8 +54,12 @@ def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, 
             relu: bool = False, stride: int = 1) -> torch.Tensor:
     Ho, Wo = (Hi + 2 * pad - R) // stride + 1, (Wi + 2 * pad - S) // stride + 1
     y = torch.empty(N, G * K, Ho, Wo, device=x_nhwc.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
-    check(_fns()["fwd"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
-                        int(relu), stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
+    # few pixel x channel tiles (batch-1 inference): the reduction split over workgroups, fp32 partials summed in
+    # order by a second kernel (csrc/gconv.hip gconv_splitk_finish)
+    ks = int(_fns()["ksplit"](N, Hi, Wi, G, C, K, R, S, pad, int(stride)))
+    part = torch.empty(ks * N * Ho * Wo * G * K, device=x_nhwc.device, dtype=torch.float32) if ks > 1 else None
+    check(_fns()["fwd_sk"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(stride),
+                           int(relu), ptr(part), ks, stream_handle(x_nhwc.device)), "mifx_gconv_fwd")
     return y
 
 

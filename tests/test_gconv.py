@@ -135,3 +135,25 @@ def test_resnet_block_on_hip_convs_matches_miopen(monkeypatch):
         s = g.abs().max()
         torch.testing.assert_close(outs[1][1][n] / s, g / s, rtol=0, atol=3e-2, msg=n)
     _ = importlib
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,K,H,R,stride,pad", [(512, 512, 7, 3, 1, 1), (1024, 2048, 14, 1, 2, 0),
+                                                (256, 1024, 14, 1, 1, 0), (64, 64, 56, 3, 1, 1)])
+def test_split_reduction_forward_batch1(C, K, H, R, stride, pad):
+    """Batch-1 ResNet-50 shapes whose pixel x channel tiles cannot fill the chip: the forward splits its reduction
+    over workgroups (fp32 partials added in order by gconv_splitk_finish, + bias, ReLU); against the fp32 reference,
+    and deterministic run to run."""
+    torch.manual_seed(7)
+    x = torch.randn(1, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") / (C * R * R) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(K, device="cuda")
+    ks = int(gconv._fns()["ksplit"](1, H, H, 1, C, K, R, R, pad, stride))
+    if H <= 14:
+        assert ks > 1
+    wf = w.view(1, K, C, R, R).permute(0, 1, 3, 4, 2).contiguous()
+    y = gconv._launch(x, wf, b, 1, H, H, 1, C, K, R, R, pad, True, stride)
+    y2 = gconv._launch(x, wf, b, 1, H, H, 1, C, K, R, R, pad, True, stride)
+    assert torch.equal(y, y2)
+    ref = torch.relu(F.conv2d(x.float(), w.float(), b, stride=stride, padding=pad))
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
