@@ -39,6 +39,30 @@ struct Geo {
   int N, Hi, Wi, Ho, Wo, G, C, K, R, S, pad, stride;
 };
 
+// optional residual epilogue (inference of a pre-activation block): y = bf16(bf16(conv + bias) + res) and
+// y2 = bf16(relu(y * scale2 + shift2)) -- the residual sum and the next block's BatchNorm + ReLU, rounded exactly as
+// the separate add and csrc/bn_relu.hip apply kernels round them
+struct ResEpi {
+  const bf16* res;      // [M, G*K] like y, or null
+  const float* scale2;  // [G*K] (with y2)
+  const float* shift2;
+  bf16* y2;             // or null
+};
+
+// one 16-byte output chunk (8 channels from c) through the residual epilogue; returns the chunk for y
+__device__ __forceinline__ u4 res_epi(u4 v, const ResEpi& re, size_t off, int c) {
+  if (re.res == nullptr) return v;
+  const u4 r = *(const u4*)(re.res + off);
+  v8bf a = __builtin_bit_cast(v8bf, v), b = __builtin_bit_cast(v8bf, r), o2;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = (bf16)((float)a[e] + (float)b[e]);
+    if (re.y2 != nullptr) o2[e] = (bf16)fmaxf(fmaf((float)a[e], re.scale2[c + e], re.shift2[c + e]), 0.f);
+  }
+  if (re.y2 != nullptr) *(v8bf*)(re.y2 + off) = o2;
+  return __builtin_bit_cast(u4, a);
+}
+
 // amdgpu_waves_per_eu(4): 4 workgroups per CU (40 KB LDS each) -- the loop is latency-bound, occupancy pays
 // (profiles/gconv_bk_ab_r2.txt, gconv_prefetch_ab_r2.txt: deeper prefetch / wider chunks that cost occupancy lose)
 // ksplit > 1 (few pixel tiles, e.g. batch-1 inference): blockIdx.z = g * ksplit + split, the workgroup reduces
@@ -47,7 +71,7 @@ struct Geo {
 template <int BN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void gconv_fwd(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                       const float* __restrict__ bias, bf16* __restrict__ y, Geo d,
-                                                      int relu, float* __restrict__ part, int ksplit) {
+                                                      int relu, float* __restrict__ part, int ksplit, ResEpi re) {
   constexpr int BCH = (BN * 4 + kThreads - 1) / kThreads;  // 16-byte weight chunks per thread per step (2, 1, 1)
   // one LDS block: double-buffered A and B staging, reused as the epilogue's output tile
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * BM * LDR + 2 * BN * LDR];
@@ -176,14 +200,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8))
   for (int c = t; c < BM * CPR; c += kThreads) {
     const int row = c / CPR, part = (c % CPR) * 8;
     const long long m = m0 + row;
-    if (m < M) *(u4*)(y + m * KT + g * d.K + n0 + part) = *(const u4*)(&Cs[row * CLD + part]);
+    if (m < M) {
+      const size_t off = (size_t)m * KT + g * d.K + n0 + part;
+      *(u4*)(y + off) = res_epi(*(const u4*)(&Cs[row * CLD + part]), re, off, g * d.K + n0 + part);
+    }
   }
 }
 
 // y = bf16(relu(sum over splits of part[s] + bias)), splits added in order; 8 channels per thread
 __global__ __launch_bounds__(kThreads) void gconv_splitk_finish(const float* __restrict__ part, int ksplit, long long M,
                                                                int KT, const float* __restrict__ bias, int relu,
-                                                               bf16* __restrict__ y) {
+                                                               bf16* __restrict__ y, ResEpi re) {
   const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
   if (i >= M * KT / 8) return;
   const size_t base = (size_t)i * 8;
@@ -205,7 +232,7 @@ __global__ __launch_bounds__(kThreads) void gconv_splitk_finish(const float* __r
     if (relu) v = fmaxf(v, 0.f);
     o[e] = (bf16)v;
   }
-  *(v8bf*)(y + base) = o;
+  *(u4*)(y + base) = res_epi(__builtin_bit_cast(u4, o), re, base, c);
 }
 
 // ---- input gradient of a STRIDED convolution -----------------------------------------------------------
@@ -543,10 +570,14 @@ int mifx_gconv_dgrad_strided(const void* dy, const void* wt, void* dx, int N, in
 // x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;
 // zero padding `pad` on every side, Ho = (Hi + 2 pad - R) / stride + 1, relu != 0: y = max(y, 0).
 // Needs C % 32 == 0 and K % 32 == 0.
-int mifx_gconv_fwd_splitk(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G,
-                          int C, int K, int R, int S, int pad, int stride, int relu, float* part, int ksplit,
-                          hipStream_t st) {
+// res / scale2 / shift2 / y2 (nullable): the residual epilogue (ResEpi) -- y = conv (+ bias, ReLU) + res, and
+// y2 = relu(y * scale2 + shift2)
+int mifx_gconv_fwd_ex(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G, int C,
+                      int K, int R, int S, int pad, int stride, int relu, float* part, int ksplit, const void* res,
+                      const float* scale2, const float* shift2, void* y2, hipStream_t st) {
   if (stride <= 0 || ksplit <= 0 || (ksplit > 1 && part == nullptr)) return -1;
+  if (y2 != nullptr && (res == nullptr || scale2 == nullptr || shift2 == nullptr)) return -1;
+  const ResEpi re{(const bf16*)res, scale2, shift2, (bf16*)y2};
   const int Ho = (Hi + 2 * pad - R) / stride + 1, Wo = (Wi + 2 * pad - S) / stride + 1;
   if (N <= 0 || G <= 0 || (long long)G * ksplit > 65535 || C <= 0 || C % BK != 0 || K <= 0 || K % 32 != 0 ||
       Hi + 2 * pad < R || Wi + 2 * pad < S || pad < 0 || pad >= R || pad >= S || ksplit > R * S * (C / BK))
@@ -559,20 +590,27 @@ int mifx_gconv_fwd_splitk(const void* x, const void* w, const float* bias, void*
   const unsigned gz = (unsigned)(G * ksplit);
   if (K % 128 == 0) {
     hipLaunchKernelGGL(gconv_fwd<128>, dim3((unsigned)mt, K / 128, gz), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit);
+                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit, re);
   } else if (K % 64 == 0) {
     hipLaunchKernelGGL(gconv_fwd<64>, dim3((unsigned)mt, K / 64, gz), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit);
+                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit, re);
   } else {  // e.g. the 96-channel layers of PATE's inference_deeper
     hipLaunchKernelGGL(gconv_fwd<32>, dim3((unsigned)mt, K / 32, gz), dim3(kThreads), 0, st, (const bf16*)x,
-                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit);
+                       (const bf16*)w, bias, (bf16*)y, d, relu, pp, ksplit, re);
   }
   if (ksplit > 1) {
     const long long n8 = M * G * K / 8;
     hipLaunchKernelGGL(gconv_splitk_finish, dim3((unsigned)((n8 + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
-                       (const float*)part, ksplit, M, G * K, bias, relu, (bf16*)y);
+                       (const float*)part, ksplit, M, G * K, bias, relu, (bf16*)y, re);
   }
   return (int)hipGetLastError();
+}
+
+int mifx_gconv_fwd_splitk(const void* x, const void* w, const float* bias, void* y, int N, int Hi, int Wi, int G,
+                          int C, int K, int R, int S, int pad, int stride, int relu, float* part, int ksplit,
+                          hipStream_t st) {
+  return mifx_gconv_fwd_ex(x, w, bias, y, N, Hi, Wi, G, C, K, R, S, pad, stride, relu, part, ksplit, nullptr, nullptr,
+                           nullptr, nullptr, st);
 }
 
 // x [N, Hi, Wi, G*C] bf16, w [G][K][R][S][C] bf16, bias [G*K] fp32 or null, y [N, Ho, Wo, G*K] bf16;

@@ -6,11 +6,13 @@ In the pre-activation bottleneck every convolution but the last is followed by B
 statistics frozen, that BatchNorm is a per-output-channel affine map, so it folds into the convolution:
 w' = w * gamma / sqrt(var + eps) (per output channel), b' = beta - mean * gamma / sqrt(var + eps), and the ReLU runs in
 the convolution's epilogue (csrc/gconv.hip forward: bias + ReLU) -- conv1 and conv2 of every block are ONE kernel
-each, with no activation pass between them. The block-input BatchNorm + ReLU normalises the residual sum: one apply
-kernel reads branch and shortcut, writes the sum (the next identity shortcut) and relu(bn(sum))
-(csrc/bn_relu.hip `mifx_bn_add_relu_apply`). The 3-channel 7x7 stem stays on MIOpen (its channel count does not
-tile the MFMA kernel). `graphed()` captures the whole forward for a fixed input shape in one hipGraph (B = 1 serving
-is launch-bound: ~70 kernels).
+each, with no activation pass between them. The block-input BatchNorm + ReLU normalises the residual sum; it runs
+in the epilogue of the convolution that produces the branch (csrc/gconv.hip ResEpi: conv3 writes the sum -- the next
+identity shortcut -- and relu(bn(sum)) at once), and for the first block as one apply kernel (csrc/bn_relu.hip
+`mifx_bn_add_relu_apply`). At batch 1 the later stages have too few pixel x channel tiles for the chip, so their
+convolutions split the reduction over workgroups (ordered fp32 partials). The 3-channel 7x7 stem stays on MIOpen (its
+channel count does not tile the MFMA kernel). `graphed()` captures the whole forward for a fixed input shape in one
+hipGraph.
 
 Off the GPU (or for a shape the kernels do not take) the same folded weights run through F.conv2d, which is what
 the CPU test checks the folding against."""
@@ -58,9 +60,23 @@ class _FoldedConv:
         # the HIP kernel's layout [G = 1][K][R][S][C], bf16
         self.w_fwd = self.w.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous().view(1, self.K, self.R, self.S, self.C)
 
+    def hip_ok(self, x: torch.Tensor) -> bool:
+        return x.is_cuda and x.dtype == torch.bfloat16 and gconv.eligible(x, self.w, 1, self.pad, self.stride) \
+            and x.is_contiguous(memory_format=torch.channels_last)
+
+    def with_residual(self, x: torch.Tensor, res: torch.Tensor, scale2: torch.Tensor, shift2: torch.Tensor):
+        """(s, relu(s * scale2 + shift2)) with s = this conv(x) + res: on the GPU one kernel (the conv's residual
+        epilogue, csrc/gconv.hip ResEpi), else the separate ops."""
+        if self.hip_ok(x) and not self.relu and res.dtype == torch.bfloat16 \
+                and res.is_contiguous(memory_format=torch.channels_last):
+            N, _, Hi, Wi = x.shape
+            return gconv.launch_res(x, self.w_fwd, self.bias, N, Hi, Wi, 1, self.C, self.K, self.R, self.S, self.pad,
+                                    self.stride, res, scale2, shift2)
+        y, s = _bn_add_relu(self(x), res, scale2, shift2)
+        return s, y
+
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
-        if x.is_cuda and x.dtype == torch.bfloat16 and gconv.eligible(x, self.w, 1, self.pad, self.stride) \
-                and x.is_contiguous(memory_format=torch.channels_last):
+        if self.hip_ok(x):
             N, _, Hi, Wi = x.shape
             return gconv._launch(x, self.w_fwd, self.bias, N, Hi, Wi, 1, self.C, self.K, self.R, self.S, self.pad,
                                  self.relu, self.stride)
@@ -116,13 +132,13 @@ class FoldedResNetV2:
         if x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
         y = max_pool3s2(F.conv2d(x, self.stem_w, None, 2, 3))
-        branch, short = y, None
-        for b in self.blocks:
-            pre, s = _bn_add_relu(branch, short, *b["bn0"])
+        pre, s = _bn_add_relu(y, None, *self.blocks[0]["bn0"])
+        for i, b in enumerate(self.blocks):
             short = b["sc"](pre) if b["sc"] is not None else s
-            branch = b["c3"](b["c2"](b["c1"](pre)))
-        out, _ = _bn_add_relu(branch, short, *self.post)
-        return F.linear(out.float().mean(dim=(2, 3)), self.fc_w, self.fc_b)
+            # conv3 + residual sum + the next BatchNorm + ReLU (the next block's, or the final one) in one kernel
+            nxt = self.blocks[i + 1]["bn0"] if i + 1 < len(self.blocks) else self.post
+            s, pre = b["c3"].with_residual(b["c2"](b["c1"](pre)), short, *nxt)
+        return F.linear(pre.float().mean(dim=(2, 3)), self.fc_w, self.fc_b)
 
     def graphed(self, example: torch.Tensor):
         """The forward captured in one hipGraph for `example`'s shape: returns f(x) -> logits (a fresh tensor)."""

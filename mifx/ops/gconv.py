@@ -24,6 +24,7 @@ def _fns():
     return {"fwd": sig(lib, "mifx_gconv_fwd", [VP, VP, VP, VP] + [I32] * 11 + [VP]),
             "fwd_sk": sig(lib, "mifx_gconv_fwd_splitk", [VP, VP, VP, VP] + [I32] * 11 + [VP, I32, VP]),
             "ksplit": sig(lib, "mifx_gconv_fwd_ksplit", [I32] * 10),
+            "fwd_ex": sig(lib, "mifx_gconv_fwd_ex", [VP, VP, VP, VP] + [I32] * 11 + [VP, I32, VP, VP, VP, VP, VP]),
             "wgrad": sig(lib, "mifx_gconv_wgrad", [VP, VP, VP] + [I32] * 11 + [VP, VP]),
             "wsplits": sig(lib, "mifx_gconv_wgrad_splits", [I32] * 10),
             "dgrad_s": sig(lib, "mifx_gconv_dgrad_strided", [VP, VP, VP] + [I32] * 10 + [VP])}
@@ -48,6 +49,26 @@ def eligible(x: torch.Tensor, weight: torch.Tensor, groups: int, padding: int, s
     K = GK // groups
     Ho, Wo = x.shape[2] + 2 * padding - R + 1, x.shape[3] + 2 * padding - S + 1
     return stride >= 1 and C % 32 == 0 and K % 32 == 0 and Ho > 0 and Wo > 0 and 0 <= padding < min(R, S)
+
+
+def launch_res(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad, stride: int,
+               res: torch.Tensor, scale2: torch.Tensor, shift2: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Forward conv with the residual epilogue (inference of a pre-activation block): s = conv(x) (+ bias) + res,
+    y2 = relu(s * scale2 + shift2) -- the residual sum and the next block's BatchNorm + ReLU in the conv's epilogue,
+    rounded as the separate kernels round them. res: bf16 channels-last like the output; scale2 / shift2 fp32 [G*K].
+    Returns (s, y2)."""
+    Ho, Wo = (Hi + 2 * pad - R) // stride + 1, (Wi + 2 * pad - S) // stride + 1
+    if tuple(res.shape) != (N, G * K, Ho, Wo) or res.dtype != torch.bfloat16 or \
+            not res.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("residual must be a bf16 channels-last tensor shaped like the output")
+    y = torch.empty(N, G * K, Ho, Wo, device=x_nhwc.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+    y2 = torch.empty_like(y)
+    ks = int(_fns()["ksplit"](N, Hi, Wi, G, C, K, R, S, pad, int(stride)))
+    part = torch.empty(ks * N * Ho * Wo * G * K, device=x_nhwc.device, dtype=torch.float32) if ks > 1 else None
+    check(_fns()["fwd_ex"](ptr(x_nhwc), ptr(w_gkrsc), ptr(bias), ptr(y), N, Hi, Wi, G, C, K, R, S, pad, int(stride), 0,
+                           ptr(part), ks, ptr(res), ptr(scale2), ptr(shift2), ptr(y2), stream_handle(x_nhwc.device)),
+          "mifx_gconv_fwd_ex")
+    return y, y2
 
 
 def _launch(x_nhwc: torch.Tensor, w_gkrsc: torch.Tensor, bias, N, Hi, Wi, G, C, K, R, S, pad,

@@ -50,3 +50,24 @@ def test_folded_gpu_matches_fp32_and_graph_replays():
         out_g = run(x2)
         out_e = f(x2)
         torch.testing.assert_close(out_g, out_e, rtol=0, atol=1e-5 * float(out_e.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,C,K", [(1, 7, 512, 2048), (4, 28, 128, 512)])
+def test_residual_epilogue_matches_separate_kernels(N, H, C, K):
+    """csrc/gconv.hip ResEpi (conv + residual sum + the next BatchNorm + ReLU in the conv's epilogue) equals the
+    separate conv, add and BN-apply kernels bit for bit -- with a split reduction (batch 1) and without."""
+    from mifx.models.resnet_infer import _bn_add_relu
+    from mifx.ops import gconv
+
+    torch.manual_seed(3)
+    cl = torch.channels_last
+    x = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(K, C, 1, 1, device="cuda") / C ** 0.5).to(torch.bfloat16)
+    wf = w.view(1, K, C, 1, 1).permute(0, 1, 3, 4, 2).contiguous()
+    res = torch.randn(N, K, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    scale, shift = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.1
+    s, y2 = gconv.launch_res(x, wf, None, N, H, H, 1, C, K, 1, 1, 0, 1, res, scale, shift)
+    y = gconv._launch(x, wf, None, N, H, H, 1, C, K, 1, 1, 0, False, 1)
+    y2_ref, s_ref = _bn_add_relu(y, res, scale, shift)
+    assert torch.equal(s, s_ref) and torch.equal(y2, y2_ref)
