@@ -6,10 +6,12 @@ In the pre-activation bottleneck every convolution but the last is followed by B
 statistics frozen, that BatchNorm is a per-output-channel affine map, so it folds into the convolution:
 w' = w * gamma / sqrt(var + eps) (per output channel), b' = beta - mean * gamma / sqrt(var + eps), and the ReLU runs in
 the convolution's epilogue (csrc/gconv.hip forward: bias + ReLU) -- conv1 and conv2 of every block are ONE kernel
-each, with no activation pass between them. The block-input BatchNorm + ReLU normalises the residual sum; it runs
-in the epilogue of the convolution that produces the branch (csrc/gconv.hip ResEpi: conv3 writes the sum -- the next
-identity shortcut -- and relu(bn(sum)) at once), and for the first block as one apply kernel (csrc/bn_relu.hip
-`mifx_bn_add_relu_apply`). At batch 1 the later stages have too few pixel x channel tiles for the chip, so their
+each, with no activation pass between them. The block-input BatchNorm + ReLU normalises the residual sum: one apply
+kernel reads branch and shortcut and writes the sum (the next identity shortcut) and relu(bn(sum)) (csrc/bn_relu.hip
+`mifx_bn_add_relu_apply`). (Running it in conv3's epilogue instead -- csrc/gconv.hip ResEpi, opt-in
+MIFX_INFER_RES_EPI=1, bit-identical -- measured slower: 0.83 / 1.11 / 2.23 ms at B = 1 / 8 / 32 against 0.79 / 1.01 /
+1.76, profiles/resnet_infer_resepi_r4.jsonl: the conv's store loop turns into a dependent load-add-store chain with
+three times the traffic, on fewer workgroups than the standalone kernel.) At batch 1 the later stages have too few pixel x channel tiles for the chip, so their
 convolutions split the reduction over workgroups (ordered fp32 partials). The 3-channel 7x7 stem stays on MIOpen (its
 channel count does not tile the MFMA kernel). `graphed()` captures the whole forward for a fixed input shape in one
 hipGraph.
@@ -19,6 +21,7 @@ the CPU test checks the folding against."""
 from __future__ import annotations
 
 import functools
+import os
 
 import torch
 import torch.nn as nn
@@ -28,6 +31,9 @@ from ..ops import _lib, gconv
 from ..ops._lib import I32, I64, VP, check, ptr, sig, stream_handle
 from ..ops.pool import max_pool3s2
 from .resnet import ResNetV2
+
+
+_RES_EPI = os.environ.get("MIFX_INFER_RES_EPI", "0") == "1"  # residual + next BN in conv3's epilogue (see above)
 
 
 @functools.lru_cache(maxsize=None)
@@ -135,9 +141,13 @@ class FoldedResNetV2:
         pre, s = _bn_add_relu(y, None, *self.blocks[0]["bn0"])
         for i, b in enumerate(self.blocks):
             short = b["sc"](pre) if b["sc"] is not None else s
-            # conv3 + residual sum + the next BatchNorm + ReLU (the next block's, or the final one) in one kernel
+            # residual sum + the next BatchNorm + ReLU (the next block's, or the final one)
             nxt = self.blocks[i + 1]["bn0"] if i + 1 < len(self.blocks) else self.post
-            s, pre = b["c3"].with_residual(b["c2"](b["c1"](pre)), short, *nxt)
+            h = b["c2"](b["c1"](pre))
+            if _RES_EPI:
+                s, pre = b["c3"].with_residual(h, short, *nxt)
+            else:
+                pre, s = _bn_add_relu(b["c3"](h), short, *nxt)
         return F.linear(pre.float().mean(dim=(2, 3)), self.fc_w, self.fc_b)
 
     def graphed(self, example: torch.Tensor):
