@@ -80,6 +80,8 @@ __global__ __launch_bounds__(kThreads) void adamw_flat(__hip_bfloat16* __restric
 // Workgroup b updates chunk b: parameter bp[b], elements [bo[b], bo[b] + bn[b]) of it; gptr[param] is the
 // gradient's device address this step (0 = no gradient: the parameter is left untouched, as torch's
 // AdamW skips params whose .grad is None), poff[param] its (8-aligned) offset in the flat buffers.
+// (Non-temporal loads / stores of master / m / v measured slower on the BERT-base step: 5049-5070 vs 5193-5208
+// seq/s, profiles/bert_adamw_nt_ab_r4.txt.)
 constexpr int kChunk = kThreads * kVec;  // 2048 elements per workgroup: one 16-B vector per thread,
                                           // all loads in flight at once
 
