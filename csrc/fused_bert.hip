@@ -764,9 +764,37 @@ int launch_gelu(int fwd, const void* dy, const void* x, const void* bias, int M,
   return (int)hipGetLastError();
 }
 
+// few rows (e.g. the per-tile bias-gradient partials of the fused FFN backward, 32 rows): ONE pass, one thread per
+// VW columns summing every row in order (the two-pass partial + reduce launch pair cost ~8 us for ~0.4 MB)
+template <typename T, typename P, int VW>
+__global__ __launch_bounds__(kThreads) void col_sum_small(const T* __restrict__ x, int M, int N, P* __restrict__ out) {
+  const int c0 = (blockIdx.x * kThreads + threadIdx.x) * VW;
+  if (c0 >= N) return;
+  float a[VW] = {};
+  constexpr int U = 8;
+  for (int r0 = 0; r0 < M; r0 += U) {
+    Pack<T, VW> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (r0 + u < M) v[u] = *(const Pack<T, VW>*)(x + (size_t)(r0 + u) * N + c0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (r0 + u < M)
+#pragma unroll
+        for (int e = 0; e < VW; ++e) a[e] += ld(&v[u].v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < VW; ++e) st(out + c0 + e, a[e]);
+}
+
 template <typename T, typename P>
 int launch_col_sum(const void* x, int M, int N, float* part, void* out, int chunks, hipStream_t st) {
   constexpr int VW = 16 / sizeof(T);
+  if (M <= 64 && N % VW == 0 && (uintptr_t)x % 16 == 0) {
+    hipLaunchKernelGGL((col_sum_small<T, P, VW>), dim3((N / VW + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                       (const T*)x, M, N, (P*)out);
+    return (int)hipGetLastError();
+  }
   if (N % VW == 0 && (uintptr_t)x % 16 == 0)
     hipLaunchKernelGGL((col_sum_v<T, VW>), dim3((N / VW + kGCols - 1) / kGCols, chunks), dim3(kThreads), 0, st,
                        (const T*)x, M, N, part);

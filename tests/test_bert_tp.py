@@ -566,3 +566,20 @@ def test_embedding_backward_deterministic_gpu():
         ref = torch.zeros(V, H, device="cuda", dtype=torch.float64).index_add_(0, ids, g.double())
         tol = 1e-2 * max(1.0, float(ref.abs().max()) / 8) if dt == torch.bfloat16 else 1e-4 * float(ref.abs().max())
         torch.testing.assert_close(grads[0].double(), ref, rtol=1e-2, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(1, 768), (7, 3072), (32, 3072), (64, 2304), (65, 768), (4096, 2304)])
+def test_col_sum_matches_fp64(M, N):
+    """Bias-gradient column sums (csrc/fused_bert.hip: one-pass kernel up to 64 rows, partials + ordered reduce
+    above) against fp64, fp32 and bf16 inputs / outputs; run-to-run identical."""
+    from mifx.ops import fused_bert as fb
+
+    torch.manual_seed(M)
+    for dt, odt in ((torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32)):
+        x = torch.randn(M, N, device="cuda").to(dt)
+        a, b = fb.col_sum(x, odt), fb.col_sum(x, odt)
+        assert torch.equal(a, b) and a.dtype == odt
+        ref = x.double().sum(0)
+        tol = (2e-2 if odt == torch.bfloat16 else 1e-4) * (1 + float(ref.abs().max()))
+        torch.testing.assert_close(a.double(), ref, rtol=2e-2, atol=tol)
