@@ -582,7 +582,9 @@ __global__ __launch_bounds__(kThreads) void col_sum(const T* __restrict__ x, int
 // sum `rows` partial rows of width N (fixed order) for up to two buffers in one launch
 // block = kRedCols columns x kRedSlices row slices; each slice strides the rows with 8 loads per buffer in
 // flight (the partials are L2-resident: the kernel is latency-, not bandwidth-bound), slices combined in
-// LDS in a fixed order -> deterministic, N/16 workgroups
+// LDS in a fixed order -> deterministic, N/16 workgroups (8 columns x 32 slices -- twice the workgroups, half the
+// dependent load batches, but 32-byte row segments -- measured slower on the BERT step: 5137-5146 vs 5228-5234
+// seq/s, profiles/bert_redcols8_rejected_r4.txt)
 constexpr int kRedCols = 16, kRedSlices = kThreads / kRedCols, kRedU = 8;
 
 template <typename PO>
