@@ -584,7 +584,7 @@ __global__ __launch_bounds__(kThreads) void col_sum(const T* __restrict__ x, int
 // flight (the partials are L2-resident: the kernel is latency-, not bandwidth-bound), slices combined in
 // LDS in a fixed order -> deterministic, N/16 workgroups (8 columns x 32 slices -- twice the workgroups, half the
 // dependent load batches, but 32-byte row segments -- measured slower on the BERT step: 5137-5146 vs 5228-5234
-// seq/s, profiles/bert_redcols8_rejected_r4.txt)
+// seq/s, profiles/bert_redcols8_rejected_r4.txt; 32 columns x 8 slices: 5162-5172, bert_redcols32_rejected_r4.txt)
 constexpr int kRedCols = 16, kRedSlices = kThreads / kRedCols, kRedU = 8;
 
 template <typename PO>

@@ -5,5 +5,5 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 tail -1 gpurun_out/r4_t25a.log
 for r in 1 2 3; do
 timeout -k 10 400 python -u -m mifx.trainer.bert_trainer --steps 30 --warmup 5 > gpurun_out/bert_cs.json 2> gpurun_out/bert_cs.err || { tail -5 gpurun_out/bert_cs.err; exit 1; }
-python -c "import json; d=[json.loads(l) for l in open('gpurun_out/bert_cs.json') if l.startswith('{')][-1]; print('bert redcols8', round(d['value'],1), round(d['ms_per_step'],3))" | tee -a gpurun_out/bert_redcols_r4.txt
+python -c "import json; d=[json.loads(l) for l in open('gpurun_out/bert_cs.json') if l.startswith('{')][-1]; print('bert redcols32', round(d['value'],1), round(d['ms_per_step'],3))" | tee -a gpurun_out/bert_redcols32_r4.txt
 done
