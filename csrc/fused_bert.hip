@@ -863,8 +863,8 @@ __device__ int compact_occ(const long long* __restrict__ ids, int N, long long i
 }
 
 // rows list[0..m) of dy summed in list order for every column, fp32 -> out (H floats, global)
-template <typename T>
-__device__ void sum_rows(const T* __restrict__ dy, int H, const int* list, int m, float* __restrict__ out,
+template <typename T, typename O>
+__device__ void sum_rows(const T* __restrict__ dy, int H, const int* list, int m, O* __restrict__ out,
                          float* sacc) {
   constexpr int VEC = 16 / sizeof(T);
   const int tid = threadIdx.x;
@@ -902,19 +902,19 @@ __device__ void sum_rows(const T* __restrict__ dy, int H, const int* list, int m
     }
     if (sl == 0)
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) out[cg * VEC + e] = a[e];
+      for (int e = 0; e < VEC; ++e) st(out + cg * VEC + e, a[e]);
   } else {
     for (int h = tid; h < H; h += 256) {
       float a = 0.f;
       for (int k = 0; k < m; ++k) a += ld(dy + (size_t)list[k] * H + h);
-      out[h] = a;
+      st(out + h, a);
     }
   }
 }
 
-template <typename T>
+template <typename T, typename G>
 __global__ __launch_bounds__(256) void emb_bwd_chunks(const long long* __restrict__ ids, int N, const T* __restrict__ dy,
-                                                      int H, long long V, float* __restrict__ g,
+                                                      int H, long long V, G* __restrict__ g,
                                                       float* __restrict__ part, int* __restrict__ heavy) {
   __shared__ int list[kEmbCh];
   __shared__ int sred[4], wc[4];
@@ -945,14 +945,17 @@ __global__ __launch_bounds__(256) void emb_bwd_chunks(const long long* __restric
   const int m = min(kEmbCh, c - r);
   const int got = compact_occ(ids, N, id, n, r, m, [](int) { return true; }, list, wc);
   __syncthreads();
-  float* out = c <= kEmbCh ? g + (size_t)id * H : part + (size_t)n * H;
-  sum_rows<T>(dy, H, list, got, out, sacc);
+  if (c <= kEmbCh)
+    sum_rows<T, G>(dy, H, list, got, g + (size_t)id * H, sacc);
+  else
+    sum_rows<T, float>(dy, H, list, got, part + (size_t)n * H, sacc);
 }
 
 // heavy ids (more than one chunk): the id's first token sums its chunks' partials in chunk order
+template <typename G>
 __global__ __launch_bounds__(256) void emb_bwd_combine(const long long* __restrict__ ids, int N, int H,
                                                        const float* __restrict__ part, const int* __restrict__ heavy,
-                                                       float* __restrict__ g) {
+                                                       G* __restrict__ g) {
   __shared__ int leaders[32768 / kEmbCh + 1];
   __shared__ int wc[4];
   const int n = blockIdx.x, tid = threadIdx.x;
@@ -964,8 +967,17 @@ __global__ __launch_bounds__(256) void emb_bwd_combine(const long long* __restri
   for (int h = tid; h < H; h += 256) {
     float a = 0.f;
     for (int k = 0; k < K; ++k) a += part[(size_t)leaders[k] * H + h];
-    g[(size_t)id * H + h] = a;
+    st(g + (size_t)id * H + h, a);
   }
+}
+
+template <typename T, typename G>
+void launch_emb(const long long* ids, int N, const void* dy, int H, long long V, void* g, float* part, int* heavy,
+                hipStream_t st) {
+  hipLaunchKernelGGL((emb_bwd_chunks<T, G>), dim3(N), dim3(256), 0, st, ids, N, (const T*)dy, H, V, (G*)g, part,
+                     heavy);
+  hipLaunchKernelGGL(emb_bwd_combine<G>, dim3(N), dim3(256), 0, st, ids, N, H, (const float*)part, (const int*)heavy,
+                     (G*)g);
 }
 
 }  // namespace
@@ -1095,20 +1107,23 @@ int mifx_bert_bias_gelu(int dtype, int pdt, int fwd, const void* dy, const void*
 }
 
 // out[N] (dtype pdt) = column sums of x [M, N] (dtype); scratch part [gelu_chunks(M), N] fp32
-// g [V, H] fp32 (zero-filled) += the embedding gradient of dy [N, H] (dtype 0 fp32, 1 bf16) at int64 ids [N],
-// deterministic (emb_bwd_chunks + emb_bwd_combine). N <= 32768. Scratch: part [N, H] fp32, heavy [N] int.
-int mifx_bert_emb_bwd(int dtype, const long long* ids, int N, const void* dy, int H, long long V, float* g,
+// g [V, H] (gdtype 0 fp32, 1 bf16; zero-filled by the caller) = the embedding gradient of dy [N, H] (dtype 0 fp32,
+// 1 bf16) at int64 ids [N], deterministic (emb_bwd_chunks + emb_bwd_combine; written straight in the weight's dtype,
+// no fp32 image + cast). N <= 32768. Scratch: part [N, H] fp32, heavy [N] int.
+int mifx_bert_emb_bwd(int dtype, const long long* ids, int N, const void* dy, int H, long long V, void* g, int gdtype,
                       float* part, int* heavy, hipStream_t st) {
   if (N <= 0 || N > 32768 || H <= 0 || V <= 0 || ids == nullptr || dy == nullptr || g == nullptr || part == nullptr ||
       heavy == nullptr)
     return -1;
-  if (dtype == 1)
-    hipLaunchKernelGGL(emb_bwd_chunks<__hip_bfloat16>, dim3(N), dim3(256), 0, st, ids, N, (const __hip_bfloat16*)dy,
-                       H, V, g, part, heavy);
+  typedef __hip_bfloat16 bf;
+  if (dtype == 1 && gdtype == 1)
+    launch_emb<bf, bf>(ids, N, dy, H, V, g, part, heavy, st);
+  else if (dtype == 1)
+    launch_emb<bf, float>(ids, N, dy, H, V, g, part, heavy, st);
+  else if (gdtype == 1)
+    launch_emb<float, bf>(ids, N, dy, H, V, g, part, heavy, st);
   else
-    hipLaunchKernelGGL(emb_bwd_chunks<float>, dim3(N), dim3(256), 0, st, ids, N, (const float*)dy, H, V, g, part,
-                       heavy);
-  hipLaunchKernelGGL(emb_bwd_combine, dim3(N), dim3(256), 0, st, ids, N, H, (const float*)part, (const int*)heavy, g);
+    launch_emb<float, float>(ids, N, dy, H, V, g, part, heavy, st);
   return (int)hipGetLastError();
 }
 

@@ -29,7 +29,7 @@ def _fns():
         "dropout": sig(lib, "mifx_bert_dropout", [I32, VP, I64, F32, VP, I32, VP, VP]),
         "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
         "colsum": sig(lib, "mifx_bert_col_sum", [I32, I32, VP, I32, I32, VP, VP, VP]),
-        "emb_bwd": sig(lib, "mifx_bert_emb_bwd", [I32, VP, I32, VP, I32, I64, VP, VP, VP, VP]),
+        "emb_bwd": sig(lib, "mifx_bert_emb_bwd", [I32, VP, I32, VP, I32, I64, VP, I32, VP, VP, VP]),
     }
 
 
@@ -306,17 +306,21 @@ class _Embedding(torch.autograd.Function):
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
         V, H = ctx.wshape
-        g = torch.zeros(V, H, device=dy.device, dtype=torch.float32)
         flat = ids.reshape(-1)
-        if dy.is_cuda and flat.numel() <= 32768 and dy.dtype in (torch.float32, torch.bfloat16):
+        if dy.is_cuda and flat.numel() <= 32768 and dy.dtype in (torch.float32, torch.bfloat16) \
+                and ctx.wdtype in (torch.float32, torch.bfloat16):
+            # rows written in the weight's dtype: no fp32 [V, H] image and cast (the word embedding's is 94 MB)
+            g = torch.zeros(V, H, device=dy.device, dtype=ctx.wdtype)
             idl = flat.to(torch.int64).contiguous()
             d2 = dy.reshape(-1, H).contiguous()
             part = torch.empty(idl.numel(), H, device=dy.device, dtype=torch.float32)
             heavy = torch.empty(idl.numel(), device=dy.device, dtype=torch.int32)
             check(_fns()["emb_bwd"](int(d2.dtype == torch.bfloat16), ptr(idl), idl.numel(), ptr(d2), H, V, ptr(g),
-                                    ptr(part), ptr(heavy), stream_handle(dy.device)), "mifx_bert_emb_bwd")
-        else:
-            g.index_add_(0, flat, dy.reshape(-1, H).float())
+                                    int(g.dtype == torch.bfloat16), ptr(part), ptr(heavy), stream_handle(dy.device)),
+                  "mifx_bert_emb_bwd")
+            return None, g
+        g = torch.zeros(V, H, device=dy.device, dtype=torch.float32)
+        g.index_add_(0, flat, dy.reshape(-1, H).float())
         return None, g.to(ctx.wdtype)
 
 
