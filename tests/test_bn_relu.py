@@ -19,6 +19,28 @@ def test_cpu_reference_path_matches_batchnorm_relu():
     torch.testing.assert_close(m(x), F.relu(ref(x)))
 
 
+def test_deferred_batch_counts_one_tensor(tmp_path):
+    """defer_batch_counts: every BatchNormReLU2d's num_batches_tracked becomes an element of one tensor, forwards stop
+    advancing it, one add_(1) advances all; state_dict round trip and a safetensors save of cloned entries work."""
+    from safetensors.torch import load_file, save_file
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(BatchNormReLU2d(8), torch.nn.Conv2d(8, 8, 1), BatchNormReLU2d(8))
+    m(torch.randn(2, 8, 3, 3))  # one counted forward before deferring
+    flat = bnr.defer_batch_counts(m)
+    assert flat is not None and flat.tolist() == [1, 1]
+    m(torch.randn(2, 8, 3, 3))
+    assert flat.tolist() == [1, 1]  # forwards no longer count
+    flat.add_(1)
+    assert [int(b.num_batches_tracked) for b in (m[0], m[2])] == [2, 2]
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    save_file(sd, str(tmp_path / "m.safetensors"))
+    m[0].num_batches_tracked.fill_(7)  # in place: still a view of the shared tensor
+    assert flat.tolist() == [7, 2]
+    m.load_state_dict(load_file(str(tmp_path / "m.safetensors")))
+    assert flat.tolist() == [2, 2]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
 @pytest.mark.parametrize("shape", [(4, 64, 14, 14), (8, 256, 7, 7), (2, 2048, 3, 3), (3, 24, 5, 7)])
