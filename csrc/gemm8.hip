@@ -1,0 +1,420 @@
+// Ping-pong pipelined bf16 MFMA GEMM for gfx950: Y[M, N] = X[M, K] . W[N, K]^T (+ fused epilogues).
+//
+// The projection GEMMs of BERT-base (BASELINE config 4) and ResNet-50's 1x1 convolutions in NHWC (config 5) are all
+// "NT" products of a K-contiguous activation and a K-contiguous weight. csrc/gemm.hip runs them with ONE barrier and
+// a `vmcnt(0)` drain per 64-deep K-tile (the structure that tops out near 0.9 PFLOP/s, guide section 5 "step-3
+// structure"); its counters sat at 18-26 % MFMA busy on BERT's K = 768 shapes (profiles/gemm_pmc_r4.md). This kernel
+// is the multi-phase structure instead:
+//
+//  * 8 waves (512 threads), one workgroup per CU, tile BM x BN, BK = 64, two LDS K-tile buffers, each split into four
+//    HALF-tiles: A0 / A1 = X rows [0, BM/2) / [BM/2, BM), B0 / B1 = W rows [0, BN/2) / [BN/2, BN).
+//  * a K-tile is four PHASES, one C-quadrant each, in the order Q(A0,B0) Q(A1,B0) Q(A1,B1) Q(A0,B1): every phase
+//    each wave reads only what the quadrant needs that is not already in its registers (phase 0: A0 + B0 fragments,
+//    1: A1, 2: B1, 3: nothing) and runs (BM/64)*(BN/128)*2 MFMAs 16x16x32 on its (BM/4) x (BN/8) piece of the quadrant.
+//  * every phase also issues ONE half-tile of global->LDS DMA (`global_load_lds_dwordx4`, no VGPR round trip) into the
+//    slot the schedule has freed: phase j of K-tile t stages half (j + 2) % 4 of K-tile t + 1 (j < 2) or t + 2
+//    (j >= 2). A half is restaged two phases after its last read (the WAR margin of the guide's template) and first
+//    read at least five phases after it was issued, so one counted `s_waitcnt vmcnt(<one K-tile of DMAs>)` per phase,
+//    before the phase's first barrier, retires exactly what the next phase reads: four half-tiles (a whole K-tile,
+//    32-64 KB per CU) stay in flight across every barrier and the loop never drains to vmcnt(0) (guide T3+T4).
+//  * two raw `s_barrier`s per phase (no __syncthreads: its fence would drain the DMAs). Waves 4-7 run one barrier
+//    behind waves 0-3 (the guide's stagger): on each SIMD one wave runs its MFMA block while its partner issues LDS
+//    reads and DMAs, then they swap. `s_setprio(1)` around every MFMA block keeps the compiler from moving MFMAs
+//    across the barriers (guide T5).
+//  * LDS rows are 128 bytes with the 16-byte chunk index XOR-swizzled by (row >> 1) & 7 (conflict-free
+//    ds_read_b128 of the 16 rows of a fragment); the DMA destination is lane-linear, so the swizzle is applied to each
+//    lane's SOURCE address (guide rule 21) and to the fragment reads.
+//  * the weight fragment is the MFMA's A operand, so a lane's accumulator holds one output row and four CONSECUTIVE
+//    columns (8-byte stores, 4 consecutive bias values).
+//  * XCD-aware bijective tile order (consecutive workgroups land on different XCDs; each XCD walks a contiguous run of
+//    tiles that share X row panels in its L2).
+//
+// Epilogues: none / + bias[N] / bias + GELU(erf) also storing the pre-bias product Z (the FFN-in forward) / + R[M, N]
+// (dX = dY W + residual gradient) / GELU backward dZ = (X W^T) o GELU'(Z + bias) with per-tile column sums (the FFN-out
+// input gradient fused with FFN-in's bias-GELU backward) / per-tile column sum and sum of squares of the stored bf16
+// output (the BatchNorm statistics of a 1x1 convolution, folded into the GEMM that produces it).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;
+constexpr int NT = 512;
+
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3, EPI_GELU_BWD = 4, EPI_STATS = 5 };
+
+__device__ __forceinline__ float erf_fast(float x) {  // Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, branch-free
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.f - poly * __expf(-ax * ax), x);
+}
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erf_fast(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// s_waitcnt immediate (gfx9 encoding): vmcnt = n, expcnt / lgkmcnt not waited on
+constexpr int vm_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
+template <int BM, int BN, int EPI, typename P>
+__global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                  const P* __restrict__ bias, bf16* __restrict__ Y,
+                                                  bf16* __restrict__ Z, int M, int N, int K,
+                                                  float* __restrict__ part) {
+  constexpr int HA = BM / 2, HB = BN / 2;            // rows per half-tile
+  constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // 64 bf16 = 128 bytes per row
+  constexpr int XR = HA * 8 / NT, WR = HB * 8 / NT;    // DMAs per thread per half-tile
+  static_assert(HA * 8 % NT == 0 && HB * 8 % NT == 0, "whole DMA rounds per half-tile");
+  constexpr int MF = HA / 32, NF = HB / 64;  // 16-row fragments per wave per quadrant (2 x 4 waves)
+  static_assert(MF >= 1 && NF >= 1, "tile too small for 8 waves");
+  constexpr int BUF = 2 * (ABYTES + BBYTES);
+  constexpr int OFF_A0 = 0, OFF_B0 = ABYTES, OFF_A1 = ABYTES + BBYTES, OFF_B1 = 2 * ABYTES + BBYTES;
+  constexpr int KTILE_DMAS = 2 * (XR + WR);  // DMAs per thread per K-tile = per 4 consecutive phases
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wm = w >> 2, wn = w & 3;  // wave position inside a quadrant; wm is also the stagger group
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int nb_n = N / BN;
+  const int m0 = (tile / nb_n) * BM, n0 = (tile % nb_n) * BN;
+  const int KT = K / BK;
+
+  // per-lane DMA source offsets (elements, K-tile 0) of each half, pre-swizzled
+  int aoff[XR], boff[WR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int qq = i * NT + tid, row = qq >> 3;
+    aoff[i] = (m0 + row) * K + 8 * swz(row, qq & 7);
+  }
+#pragma unroll
+  for (int i = 0; i < WR; ++i) {
+    const int qq = i * NT + tid, row = qq >> 3;
+    boff[i] = (n0 + row) * K + 8 * swz(row, qq & 7);
+  }
+  // half h (0 A0, 1 B0, 2 A1, 3 B1) of K-tile t into LDS buffer t & 1
+  auto stage = [&](int h, int t) {
+    unsigned char* buf = lds + (t & 1) * BUF;
+    const int k0 = t * BK;
+    if (h == 0 || h == 2) {
+      unsigned char* dst = buf + (h == 0 ? OFF_A0 : OFF_A1);
+      const bf16* src = X + (h == 2 ? HA * K : 0) + k0;
+#pragma unroll
+      for (int i = 0; i < XR; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(src + aoff[i]),
+                                         (__attribute__((address_space(3))) void*)(dst + (i * NT + 64 * w) * 16), 16,
+                                         0, 0);
+    } else {
+      unsigned char* dst = buf + (h == 1 ? OFF_B0 : OFF_B1);
+      const bf16* src = W + (h == 3 ? HB * K : 0) + k0;
+#pragma unroll
+      for (int i = 0; i < WR; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(src + boff[i]),
+                                         (__attribute__((address_space(3))) void*)(dst + (i * NT + 64 * w) * 16), 16,
+                                         0, 0);
+    }
+  };
+
+  v4f acc[2][2][NF][MF];  // [mq][nq][n-frag][m-frag]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < NF; ++c)
+#pragma unroll
+        for (int d = 0; d < MF; ++d) acc[a][b][c][d] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  v8bf ra0[MF][2], ra1[MF][2], rb[NF][2];  // A0 / A1 / current-B fragments, [frag][k-step]
+  auto read_a = [&](const unsigned char* half, v8bf (&r)[MF][2]) {
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int row = wm * (HA / 2) + 16 * f + fr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) r[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+    }
+  };
+  auto read_b = [&](const unsigned char* half) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int row = wn * (HB / 4) + 16 * f + fr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) rb[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+    }
+  };
+  auto mma = [&](v4f (&c)[NF][MF], const v8bf (&ra)[MF][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < NF; ++a)
+#pragma unroll
+        for (int b = 0; b < MF; ++b) c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[a][ks], ra[b][ks], c[a][b], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: K-tile 0 whole, K-tile 1 halves A0 / B0; retire K-tile 0's A0 / B0 (phase 0 reads them)
+  stage(0, 0);
+  stage(1, 0);
+  stage(2, 0);
+  stage(3, 0);
+  if (KT > 1) {
+    stage(0, 1);
+    stage(1, 1);
+    __builtin_amdgcn_s_waitcnt(vm_wait(KTILE_DMAS));
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+  if (wm == 1) barrier();  // the stagger: waves 4-7 one barrier behind
+
+  for (int t = 0; t < KT; ++t) {
+    const unsigned char* buf = lds + (t & 1) * BUF;
+    const bool st1 = t + 1 < KT, st2 = t + 2 < KT;
+    auto phase = [&](auto J) {
+      constexpr int j = decltype(J)::value;
+      // LDS fragment reads of this phase's quadrant
+      if constexpr (j == 0) {
+        read_a(buf + OFF_A0, ra0);
+        read_b(buf + OFF_B0);
+      } else if constexpr (j == 1) {
+        read_a(buf + OFF_A1, ra1);
+      } else if constexpr (j == 2) {
+        read_b(buf + OFF_B1);
+      }
+      // one half-tile of DMA into the slot freed two phases ago
+      const bool issue = j < 2 ? st1 : st2;
+      if (issue) {
+        if constexpr (j < 2)
+          stage(j + 2, t + 1);
+        else
+          stage(j - 2, t + 2);
+        __builtin_amdgcn_s_waitcnt(vm_wait(KTILE_DMAS));  // everything issued >= 4 phases ago has landed
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail: nothing younger to count on
+      }
+      barrier();
+      if constexpr (j == 0) mma(acc[0][0], ra0);
+      if constexpr (j == 1) mma(acc[1][0], ra1);
+      if constexpr (j == 2) mma(acc[1][1], ra1);
+      if constexpr (j == 3) mma(acc[0][1], ra0);
+      barrier();
+    };
+    phase(std::integral_constant<int, 0>{});
+    phase(std::integral_constant<int, 1>{});
+    phase(std::integral_constant<int, 2>{});
+    phase(std::integral_constant<int, 3>{});
+  }
+  if (wm == 0) barrier();  // equal barrier counts for both groups
+
+  // ---- epilogue: acc[mq][nq][a][b][r] = Y[m0 + mq HA + wm HA/2 + 16 b + fr][n0 + nq HB + wn HB/4 + 16 a + 4 fc + r]
+  if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_STATS) {
+    // per-tile column sums of the stored values (GELU_BWD: dZ; STATS: y and y^2), over the rows of the 16-lane
+    // groups (xor tree), then over the two wave rows in order (LDS), written to part[m0 / BM][...]
+    constexpr int NS = EPI == EPI_STATS ? 2 : 1;
+    float cs[NS][2][NF][4];
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int a = 0; a < NF; ++a) {
+        const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_GELU_BWD) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n + r];
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[s][nq][a][r] = 0.f;
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int b = 0; b < MF; ++b) {
+            const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            v4bf o;
+            if constexpr (EPI == EPI_GELU_BWD) {
+              const v4bf zv = *(const v4bf*)(Z + (size_t)m * N + n);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                o[r] = (bf16)(acc[mq][nq][a][b][r] * gelu_grad_f((float)zv[r] + bv[r]));
+                cs[0][nq][a][r] += (float)o[r];
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                o[r] = (bf16)acc[mq][nq][a][b][r];
+                const float v = (float)o[r];
+                cs[0][nq][a][r] += v;
+                cs[NS - 1][nq][a][r] += v * v;
+              }
+            }
+            *(v4bf*)(Y + (size_t)m * N + n) = o;
+          }
+      }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int a = 0; a < NF; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = cs[s][nq][a][r];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            cs[s][nq][a][r] = v;
+          }
+    __syncthreads();  // all DMAs retired (vmcnt(0) in the tail) and every fragment read done: LDS reusable
+    float* red = (float*)lds;  // [NS][2 wave rows][BN]
+    if (fr == 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+          for (int a = 0; a < NF; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              red[(s * 2 + wm) * BN + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc + r] = cs[s][nq][a][r];
+    }
+    __syncthreads();
+    for (int c = tid; c < NS * BN; c += NT) {
+      const int s = c / BN, col = c % BN;
+      part[((size_t)s * (M / BM) + m0 / BM) * N + n0 + col] = red[(s * 2) * BN + col] + red[(s * 2 + 1) * BN + col];
+    }
+    return;
+  }
+#pragma unroll
+  for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+    for (int a = 0; a < NF; ++a) {
+      const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n + r];
+      }
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int b = 0; b < MF; ++b) {
+          const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+          v4bf o;
+          if constexpr (EPI == EPI_BIAS_GELU) {
+            v4bf z;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              z[r] = (bf16)acc[mq][nq][a][b][r];
+              o[r] = (bf16)gelu_f((float)z[r] + bv[r]);
+            }
+            *(v4bf*)(Z + (size_t)m * N + n) = z;
+          } else if constexpr (EPI == EPI_ADD_R) {
+            const v4bf rv = *(const v4bf*)((const bf16*)bias + (size_t)m * N + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mq][nq][a][b][r] + (float)rv[r]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mq][nq][a][b][r] + bv[r]);
+          }
+          *(v4bf*)(Y + (size_t)m * N + n) = o;
+        }
+    }
+}
+
+template <int BM, int BN, int EPI, typename P>
+int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, float* part,
+           hipStream_t st) {
+  constexpr int LDS = 2 * 2 * (BM / 2 + BN / 2) * 128;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8_nt<BM, BN, EPI, P>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm8_nt<BM, BN, EPI, P>), dim3((M / BM) * (N / BN)), dim3(NT), LDS, st, (const bf16*)X,
+                     (const bf16*)W, (const P*)bias, (bf16*)Y, (bf16*)Z, M, N, K, part);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN>
+int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N,
+             int K, float* part, hipStream_t st) {
+  switch (epi) {
+    case EPI_NONE: return launch<BM, BN, EPI_NONE, bf16>(X, W, nullptr, Y, nullptr, M, N, K, nullptr, st);
+    case EPI_BIAS:
+      return bias_f32 ? launch<BM, BN, EPI_BIAS, float>(X, W, bias, Y, nullptr, M, N, K, nullptr, st)
+                      : launch<BM, BN, EPI_BIAS, bf16>(X, W, bias, Y, nullptr, M, N, K, nullptr, st);
+    case EPI_BIAS_GELU:
+      return bias_f32 ? launch<BM, BN, EPI_BIAS_GELU, float>(X, W, bias, Y, Z, M, N, K, nullptr, st)
+                      : launch<BM, BN, EPI_BIAS_GELU, bf16>(X, W, bias, Y, Z, M, N, K, nullptr, st);
+    case EPI_ADD_R: return launch<BM, BN, EPI_ADD_R, bf16>(X, W, bias, Y, nullptr, M, N, K, nullptr, st);
+    case EPI_GELU_BWD:
+      return bias_f32 ? launch<BM, BN, EPI_GELU_BWD, float>(X, W, bias, Y, Z, M, N, K, part, st)
+                      : launch<BM, BN, EPI_GELU_BWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
+    case EPI_STATS: return launch<BM, BN, EPI_STATS, bf16>(X, W, nullptr, Y, nullptr, M, N, K, part, st);
+  }
+  return -1;
+}
+
+struct Cfg {
+  int bm, bn;
+};
+constexpr Cfg kCfgs[] = {{256, 256}, {256, 128}, {128, 256}, {128, 128}};
+
+}  // namespace
+
+extern "C" {
+
+int mifx_gemm8_configs(int* out, int n) {
+  const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
+  for (int i = 0; i < m && 2 * i + 1 < n; ++i) {
+    out[2 * i] = kCfgs[i].bm;
+    out[2 * i + 1] = kCfgs[i].bn;
+  }
+  return m;
+}
+
+// Y[M, N] = X[M, K] . W[N, K]^T, bf16 in / out, fp32 accumulation. epi: 0 none; 1 + bias[N]; 2 GELU(. + bias) with
+// Z = bf16(X W^T) (pre-bias); 3 + R (bias = bf16 [M, N]); 4 dZ = (X W^T) o GELU'(Z + bias) with part[M / BM][N] the
+// per-tile column sums of dZ; 5 part[2][M / BM][N] = per-tile column sum / sum of squares of the stored Y.
+// bias bf16 or fp32 (bias_f32). M % BM == 0, N % BN == 0, K % 64 == 0, 16-byte aligned operands.
+int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z,
+                  float* part, int M, int N, int K, hipStream_t st) {
+  const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
+  if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || X == nullptr || W == nullptr || Y == nullptr) return -1;
+  const Cfg c = kCfgs[cfg];
+  if (M % c.bm || N % c.bn || K % BK) return -1;
+  if (epi < 0 || epi > 5) return -1;
+  if ((epi == 1 || epi == 2 || epi == 3 || epi == 4) && bias == nullptr) return -1;
+  if ((epi == 2 || epi == 4) && Z == nullptr) return -1;
+  if ((epi == 4 || epi == 5) && part == nullptr) return -1;
+  if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 8 || (Z != nullptr && (uintptr_t)Z % 8)) return -1;
+  if (epi == 3 && (uintptr_t)bias % 8) return -1;
+  if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;  // 32-bit element offsets
+  switch (cfg) {
+    case 0: return dispatch<256, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
+    case 1: return dispatch<256, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
+    case 2: return dispatch<128, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
+    default: return dispatch<128, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
+  }
+}
+
+}  // extern "C"

@@ -131,16 +131,33 @@ __global__ __launch_bounds__(WG) void tpar_reduce(Peers pe, int world, int rank,
 }
 
 // C: all-gather of the reduced chunks into the output; the last workgroup advances the epoch
+// A failed group (sticky err) writes NaN into the output chunk instead of leaving it uninitialised: whatever consumes
+// the activation goes non-finite (the loss shows it) even before the host's next check() raises.
+__device__ __forceinline__ void poison(uint64_t* __restrict__ y, long long n4, int c) {
+  const long long base = (long long)c * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const long long q = base + i * WG + threadIdx.x;
+    if (q < n4) y[q] = 0x7FC07FC07FC07FC0ull;  // four bf16 quiet NaNs
+  }
+}
+
 __global__ __launch_bounds__(WG) void tpar_gather(uint64_t* __restrict__ y, long long n4, Peers pe, int world, int rank,
                                                   long long npad4, long long* __restrict__ ep, int* __restrict__ err,
                                                   int nchunks, unsigned int* __restrict__ done) {
-  if (failed(err)) return;
-  const long long e = ep[0] + 1;
   const int c = blockIdx.x, owner = c % world;
+  if (failed(err)) {
+    poison(y, n4, c);
+    return;
+  }
+  const long long e = ep[0] + 1;
   bool ok = true;
   if (threadIdx.x == 0)  // (own chunks too: uniform code; their stamp is already there)
     ok = wait_flag(pe.flag[rank] + ((size_t)1 * nchunks + c) * MAXW + owner, (unsigned int)e, err);
-  if (__ballot(!ok) != 0ull) return;  // no epoch advance: the error is sticky, the host raises
+  if (__ballot(!ok) != 0ull) {  // no epoch advance: the error is sticky, the host raises
+    poison(y, n4, c);
+    return;
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const uint64_t* src = pe.red[owner] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
   const long long base = (long long)c * (CHUNK / 4);

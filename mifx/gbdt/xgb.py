@@ -164,8 +164,10 @@ class _Base:
                     if early_stopping_rounds and since >= early_stopping_rounds:
                         break
         self.evals_result_ = {"validation_0": {self._metric_name(): hist}} if ev is not None else {}
-        if ev is not None:
-            self.best_score, self.best_iteration = best, best_it
+        # XGBoost's sklearn API sets best_iteration / best_score only under early stopping; without it predict uses
+        # every tree even when an eval_set was given
+        self.best_score, self.best_iteration = (best, best_it) if ev is not None and early_stopping_rounds else \
+            (None, None)
         return self
 
     @property

@@ -31,6 +31,7 @@ class JobSpec:
     kind: str
     name: str
     replicas: list  # [ReplicaSpec] in launch order
+    backoff_limit: int | None = None  # spec.runPolicy.backoffLimit (kubeflow v1) / spec.backoffLimit
 
     @property
     def world_size(self) -> int:
@@ -52,7 +53,9 @@ class JobSpec:
             env = {e["name"]: str(e.get("value", "")) for e in c.get("env", []) or []}
             out.append(ReplicaSpec(role, int(s.get("replicas", 1)), list(c.get("command", [])) + list(c.get("args", [])),
                                    env, gpus, c.get("image", ""), s.get("restartPolicy", "Never")))
-        spec = JobSpec(kind, d.get("metadata", {}).get("name", "job"), out)
+        sp = d.get("spec", {}) or {}
+        bl = (sp.get("runPolicy") or {}).get("backoffLimit", sp.get("backoffLimit"))
+        spec = JobSpec(kind, d.get("metadata", {}).get("name", "job"), out, None if bl is None else int(bl))
         validate(spec)
         return spec
 
@@ -71,6 +74,10 @@ def validate(spec: JobSpec) -> None:
             raise ValueError(f"{r.role}.replicas must be <= 1")
         if not r.command:
             raise ValueError(f"{r.role}: container command is required")
+        if r.restart_policy not in ("Never", "OnFailure", "Always", "ExitCode"):
+            raise ValueError(f"{r.role}.restartPolicy must be one of Never, OnFailure, Always, ExitCode")
+    if spec.backoff_limit is not None and spec.backoff_limit < 0:
+        raise ValueError("backoffLimit must be >= 0")
 
 
 def _free_port() -> int:
@@ -87,9 +94,45 @@ def _tf_config(spec: JobSpec, role: str, index: int, base_port: int) -> str:
     return json.dumps({"cluster": cluster, "task": {"type": role.lower(), "index": index}, "environment": "cloud"})
 
 
+# Exit codes the "ExitCode" restart policy treats as retryable (Kubeflow training-operator semantics: 128 + signal,
+# e.g. 137 OOM-kill / SIGKILL, 143 SIGTERM, 130 SIGINT; 1-127 are the program's own, permanent, failures)
+def _retryable(code: int) -> bool:
+    return code < 0 or code >= 128
+
+
+def _wants_restart(spec: JobSpec, codes: dict, roles: dict) -> bool:
+    """Does the failed replica set restart? Only when EVERY failing replica's policy allows it (a permanent failure of
+    any one replica ends the job)."""
+    failed = [(k, c) for k, c in codes.items() if c != 0]
+    if not failed:
+        return False
+    for k, c in failed:
+        pol = roles[k].restart_policy
+        if pol in ("OnFailure", "Always"):
+            continue
+        if pol == "ExitCode" and _retryable(c):
+            continue
+        return False
+    return True
+
+
 def launch_local(spec: JobSpec, num_gpus: int | None = None, timeout: float | None = None, cwd: str | None = None,
-                 log_dir: str | None = None) -> dict:
-    """Run every replica as a local process; returns {role-index: exit code} (and logs under log_dir)."""
+                 log_dir: str | None = None, isolate_gpus: bool = False, backoff_limit: int | None = None,
+                 backoff_s: float = 0.5, stats: dict | None = None) -> dict:
+    """Run every replica as a local process; returns {role-index: exit code} of the last attempt (logs under log_dir).
+
+    GPUs: every rank sees ALL of the node's GPUs and gets LOCAL_RANK = its rank on the node (torchrun's contract), so
+    a data-parallel job can map its peers' HBM over xGMI (IPC gradient exchange) and RCCL can use P2P; only
+    `isolate_gpus=True` (independent processes such as HPO trials) pins one device per process through
+    HIP_VISIBLE_DEVICES.
+
+    Failures: the first replica that exits non-zero takes the whole replica set down (torch.distributed ranks cannot
+    rejoin a group one at a time). With `restartPolicy: Never` (the reference's TFJob default) that ends the job. With
+    `OnFailure` / `Always` (or `ExitCode` and a retryable code >= 128) the whole set is relaunched as FRESH processes --
+    MIFX_RESTART_COUNT = the attempt number, same ports, same ranks -- after a bounded exponential backoff, at most
+    `backoff_limit` times (default: the spec's runPolicy.backoffLimit, else 3); the workload resumes from its latest
+    checkpoint (the estimator / Trainer components do that on start). `stats` (if given) receives {"restarts": n,
+    "attempts": [codes of every attempt]}."""
     if num_gpus is None:
         try:
             import torch
@@ -97,44 +140,77 @@ def launch_local(spec: JobSpec, num_gpus: int | None = None, timeout: float | No
             num_gpus = torch.cuda.device_count()
         except Exception:  # noqa: BLE001
             num_gpus = 0
-    port = _free_port()
-    tf_port = _free_port()
-    procs, rank = {}, 0
+    if backoff_limit is None:
+        backoff_limit = spec.backoff_limit if spec.backoff_limit is not None else 3
     log_dir = log_dir or os.path.join("/tmp", f"mifx_job_{spec.name}")
     os.makedirs(log_dir, exist_ok=True)
+    deadline = time.time() + timeout if timeout else None
+    attempts = []
+    attempt = 0
+    while True:
+        codes, roles = _run_once(spec, num_gpus, deadline, cwd, log_dir, isolate_gpus, attempt)
+        attempts.append(codes)
+        timed_out = any(c == -9 for c in codes.values()) and deadline is not None and time.time() >= deadline
+        if timed_out or attempt >= backoff_limit or not _wants_restart(spec, codes, roles):
+            break
+        attempt += 1
+        time.sleep(min(backoff_s * 2 ** (attempt - 1), 30.0))
+    if stats is not None:
+        stats["restarts"] = attempt
+        stats["attempts"] = attempts
+    return codes
+
+
+def _run_once(spec: JobSpec, num_gpus: int, deadline, cwd, log_dir, isolate_gpus: bool, attempt: int):
+    port = _free_port()
+    tf_port = _free_port()
+    procs, roles, rank = {}, {}, 0
     for r in spec.replicas:
         for i in range(r.replicas):
             env = dict(os.environ, **r.env)
             is_rank = r.role != "PS"
             env.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(spec.world_size),
-                        "HSA_ENABLE_IPC_MODE_LEGACY": "0", "JOB_ROLE": r.role, "JOB_INDEX": str(i)})
+                        "HSA_ENABLE_IPC_MODE_LEGACY": "0", "JOB_ROLE": r.role, "JOB_INDEX": str(i),
+                        "MIFX_RESTART_COUNT": str(attempt)})
             if is_rank:
                 env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "LOCAL_WORLD_SIZE": str(spec.world_size)})
                 if num_gpus:
-                    env["HIP_VISIBLE_DEVICES"] = str(rank % num_gpus)
-                    env["LOCAL_RANK"] = "0"  # one visible device per process
+                    if isolate_gpus:
+                        env["HIP_VISIBLE_DEVICES"] = str(rank % num_gpus)
+                        env["LOCAL_RANK"] = "0"  # one visible device per process
+                    else:  # (visibility left as inherited, like torchrun: every device, peers reachable over xGMI)
+                        env["LOCAL_RANK"] = str(rank % num_gpus)
             if spec.kind == "TFJob":
                 env["TF_CONFIG"] = _tf_config(spec, r.role, i, tf_port)
             cmd = [sys.executable if c in ("python", "python3") else c for c in r.command]
-            log = open(os.path.join(log_dir, f"{r.role.lower()}-{i}.log"), "w")
-            procs[f"{r.role.lower()}-{i}"] = (subprocess.Popen(cmd, env=env, cwd=cwd, stdout=log,
-                                                               stderr=subprocess.STDOUT), log)
+            key = f"{r.role.lower()}-{i}"
+            suffix = f".restart{attempt}" if attempt else ""
+            log = open(os.path.join(log_dir, f"{key}{suffix}.log"), "w")
+            procs[key] = (subprocess.Popen(cmd, env=env, cwd=cwd, stdout=log, stderr=subprocess.STDOUT), log)
+            roles[key] = r
             if is_rank:
                 rank += 1
-    deadline = time.time() + timeout if timeout else None
     codes = {}
-    for k, (p, log) in procs.items():
-        try:
-            codes[k] = p.wait(timeout=max(1.0, deadline - time.time()) if deadline else None)
-        except subprocess.TimeoutExpired:
-            p.kill()
-            codes[k] = -9
-        log.close()
-    if any(c != 0 for c in codes.values()):  # a failed rank takes the job down (restartPolicy Never)
-        for p, _ in procs.values():
-            if p.poll() is None:
+    # poll every process: the FIRST non-zero exit takes the set down at once (no rank left blocked in a collective
+    # waiting for a dead peer until its own timeout)
+    live = dict(procs)
+    while live:
+        for k in list(live):
+            c = live[k][0].poll()
+            if c is not None:
+                codes[k] = c
+                live.pop(k)
+        if any(c != 0 for c in codes.values()) or (deadline is not None and time.time() >= deadline):
+            for k, (p, _) in live.items():
                 p.kill()
-    return codes
+                p.wait()
+                codes[k] = -9
+            live = {}
+            break
+        time.sleep(0.05)
+    for _, log in procs.values():
+        log.close()
+    return codes, roles
 
 
 def to_indexed_job(spec: JobSpec, namespace: str = "kubeflow", image: str | None = None) -> dict:

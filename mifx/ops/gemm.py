@@ -35,11 +35,12 @@ def _fns():
 
 
 class TransposeCache:
-    """Transposed copies of a model's projection weights, refreshed in ONE launch after every optimizer step
-    (csrc/gemm.hip transpose_batch), for the dX GEMMs that run as NT products against W^T. Refreshing per step in
-    one kernel replaces a transpose launch per weight in the backward (47 per BERT-base step, ~200 us:
-    profiles/bert_steady_r4b.md). The owner (BertTrainer) calls refresh() after every update of the weights and runs
-    its backward inside `use_transposes(cache)`."""
+    """Transposed copies of a model's projection weights, refreshed in ONE launch per step (csrc/gemm.hip
+    transpose_batch), for the dX GEMMs that run as NT products against W^T. Refreshing per step in one kernel replaces
+    a transpose launch per weight in the backward (47 per BERT-base step, ~200 us: profiles/bert_steady_r4b.md). The
+    owner (BertTrainer) calls refresh() right before every backward -- from the weights as they are then, so a weight
+    change of any kind between steps (update, load_state_dict) is seen -- and runs the backward inside
+    `use_transposes(cache)`."""
 
     def __init__(self, weights):
         self.items = {}
@@ -515,6 +516,69 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, cfg: int | None = None, splits: in
 def tn_eligible(a2: torch.Tensor, b2: torch.Tensor) -> bool:
     return (a2.is_cuda and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and a2.dim() == 2
             and b2.dim() == 2 and pick_tn(a2.shape[1], b2.shape[1], a2.shape[0]) is not None)
+
+
+# ---------------------------------------------------------------- ping-pong pipelined NT GEMM (csrc/gemm8.hip)
+@functools.lru_cache(maxsize=None)
+def _g8_fns():
+    lib = _lib.load("gemm8")
+    return {"configs": sig(lib, "mifx_gemm8_configs", [VP, I32]),
+            "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP])}
+
+
+@functools.lru_cache(maxsize=None)
+def gemm8_configs() -> tuple[tuple[int, int], ...]:
+    """(BM, BN) of every compiled csrc/gemm8.hip configuration, by index."""
+    buf = (ctypes.c_int * 64)()
+    n = _g8_fns()["configs"](buf, 64)
+    return tuple((buf[2 * i], buf[2 * i + 1]) for i in range(n))
+
+
+def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
+    """The csrc/gemm8.hip configuration for an M x N x K product: fewest waves of workgroups, then the largest
+    tile (operand reuse per byte staged); None if none tiles the shape."""
+    best, best_score = None, None
+    for i, (bm, bn) in enumerate(gemm8_configs()):
+        if M % bm or N % bn or K % 64:
+            continue
+        tiles = (M // bm) * (N // bn)
+        waves = -(-tiles // cus)
+        score = (tiles / (waves * cus) * (bm * bn) ** 0.5, bm * bn)
+        if best_score is None or score > best_score:
+            best, best_score = i, score
+    return best
+
+
+def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0,
+             cfg: int | None = None, z: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """x2 [M, K] bf16, w [N, K] bf16 -> (Y [M, N] bf16, aux). epi 0: X W^T; 1: + bias; 2: GELU(X W^T + bias), aux
+    = Z = bf16(X W^T); 3: + bias as a bf16 [M, N] matrix; 4: dZ = (X W^T) o GELU'(z + bias), aux = per-tile column sums
+    [M / BM, N] fp32; 5: aux = per-tile column sums and sums of squares of Y [2, M / BM, N] fp32."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if cfg is None:
+        cfg = gemm8_pick(M, N, K)
+    if cfg is None:
+        raise ValueError(f"no gemm8 tile configuration for {M}x{N}x{K}")
+    bm = gemm8_configs()[cfg][0]
+    x2, w = x2.contiguous(), w.contiguous()
+    y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    aux, part = None, None
+    b = None
+    if epi == 2:
+        z = aux = torch.empty_like(y)
+    if epi == 3:
+        b = bias.reshape(M, N).to(torch.bfloat16).contiguous()
+    elif epi in (1, 2, 4):
+        b = bias if bias.dtype in (torch.float32, torch.bfloat16) else bias.float()
+        b = b.contiguous()
+    if epi == 4:
+        part = aux = torch.empty(M // bm, N, device=x2.device, dtype=torch.float32)
+    if epi == 5:
+        part = aux = torch.empty(2, M // bm, N, device=x2.device, dtype=torch.float32)
+    check(_g8_fns()["nt"](int(cfg), int(epi), int(b is not None and b.dtype == torch.float32), ptr(x2), ptr(w),
+                          ptr(b), ptr(y), ptr(z), ptr(part), M, N, K, stream_handle(x2.device)), "mifx_gemm8_nt")
+    return y, aux
 
 
 # ---------------------------------------------------------------- exact fp32 GEMM with edge tiles (csrc/gemm_f32.hip)

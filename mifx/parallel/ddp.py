@@ -118,9 +118,16 @@ class DataParallel:
         if pi in b.ready:
             return
         b.ready.add(pi)
+        off = b.offsets[pi]
+        view = b.buf[off:off + p.numel()]
         if not self.views:
-            off = b.offsets[pi]
-            b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
+            view.copy_(p.grad.reshape(-1))
+        elif p.grad.data_ptr() != view.data_ptr():
+            # views mode assumes p.grad IS the bucket view; something replaced it (optimizer.zero_grad() with
+            # set_to_none, a user assignment): copy the fresh gradient into the bucket and re-attach the view, so
+            # the all-reduced bucket and the gradient the optimizer reads stay the same memory
+            view.copy_(p.grad.reshape(-1))
+            p.grad = view.view_as(p)
         if len(b.ready) == len(b.params):
             self._launch(b)
 

@@ -60,14 +60,20 @@ class TPGroup:
             self.ipc.check()
 
 
+def ipc_eligible(x: torch.Tensor, tp: TPGroup) -> bool:
+    """The all-reduce of x runs on the peer-memory kernels (which write a NEW tensor); otherwise torch.distributed
+    reduces x IN PLACE."""
+    return (tp.ipc is not None and x.dtype == torch.bfloat16 and x.is_cuda and x.numel() % 4 == 0
+            and x.numel() <= tp.ipc.npad)
+
+
 def _all_reduce(x: torch.Tensor, tp: TPGroup) -> torch.Tensor:
     """Sum over the TP ranks. x must be a fresh tensor nobody else reads (a GEMM output or an incoming gradient):
     the torch path reduces it in place, the IPC path returns a new tensor."""
     if tp.size == 1:
         return x
     x = x.contiguous()
-    if tp.ipc is not None and x.dtype == torch.bfloat16 and x.is_cuda and x.numel() % 4 == 0 \
-            and x.numel() <= tp.ipc.npad:
+    if ipc_eligible(x, tp):
         return tp.ipc.all_reduce(x)
     dist.all_reduce(x, group=tp.group)
     return x
@@ -83,9 +89,10 @@ class _CopyToTP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        # (the incoming gradient may be shared by other consumers of the graph: reduce a private copy on the
-        # torch path; the IPC path writes a new tensor anyway)
-        if ctx.tp.ipc is None:
+        # (the incoming gradient may be shared by other consumers of the graph: reduce a private copy whenever the
+        # in-place torch path will run -- no IPC group, or a tensor the IPC kernels do not take; the IPC path writes
+        # a new tensor anyway)
+        if ctx.tp.size > 1 and not ipc_eligible(g.contiguous(), ctx.tp):
             g = g.clone()
         return _all_reduce(g, ctx.tp), None
 

@@ -91,7 +91,7 @@ class BertTrainer:
         else:
             self.opt = torch.optim.AdamW(self.model.parameters(), lr=lr, weight_decay=0.01, fused=cuda,
                                          capturable=self.use_graph)
-        # transposed copies of the projection weights for the dX GEMMs, refreshed in one launch after each update
+        # transposed copies of the projection weights for the dX GEMMs, refreshed in one launch before each backward
         self.tcache = None
         if self.flat:
             from ..ops import gemm as hg
@@ -99,7 +99,6 @@ class BertTrainer:
             ws = [m.weight for layer in self.model.layers for m in (layer.qkv, layer.attn_out, layer.ffn_in,
                                                                       layer.ffn_out)]
             self.tcache = hg.TransposeCache(ws)
-            self.tcache.refresh()
         self.data = synthetic_batch(cfg, batch, seq, self.device)
         self.amp = cuda
         self.sdpa = sdpa  # None = PyTorch's choice; "math" / "efficient" / "flash" pins the SDPA backend
@@ -136,6 +135,11 @@ class BertTrainer:
         loss = F.cross_entropy(logits.float(), y)
         from ..ops import gemm as hg
 
+        if self.tcache is not None:
+            # the transposed weight copies the dX GEMMs read, refreshed from the CURRENT weights right before the
+            # backward (once per step, inside the captured graph): a weight change between steps (an update, a
+            # load_state_dict, a warm start) can never leave the backward with stale transposes
+            self.tcache.refresh()
         with hg.use_transposes(self.tcache):
             if self.async_dw:  # weight-gradient GEMMs on a side stream beside the backward's dX chain
                 with hg.async_weight_grads():
@@ -144,8 +148,6 @@ class BertTrainer:
             else:
                 loss.backward()
         self.opt.step()
-        if self.tcache is not None:
-            self.tcache.refresh()
         return loss.detach()
 
     def _sdpa_ctx(self):
@@ -171,7 +173,18 @@ class BertTrainer:
         with torch.cuda.graph(self.graph):
             self.static_loss = self._eager_step()
 
+    # TP health check cadence: the peer-memory all-reduce reports a peer that never arrived through a sticky device
+    # flag (its later kernels then write NaN); reading it is a host sync, so step() reads it every CHECK_EVERY steps
+    CHECK_EVERY = 100
+
+    def check(self) -> None:
+        """Raise if a TP all-reduce of this trainer's group timed out (no-op at TP = 1 / without the IPC path)."""
+        self.tp.check()
+
     def step(self) -> torch.Tensor:
+        self.steps_done = getattr(self, "steps_done", 0) + 1
+        if self.tp.ipc is not None and self.steps_done % self.CHECK_EVERY == 0:
+            self.check()
         if self.use_graph:
             if self.graph is None:
                 self._capture()
@@ -179,6 +192,15 @@ class BertTrainer:
             return self.static_loss
         self.opt.zero_grad(set_to_none=True)
         return self._eager_step()
+
+    def load_weights(self, state: dict) -> None:
+        """Load a (full or TP-sharded) state dict into the model and refresh everything derived from the weights
+        (the transposed copies of the dX GEMMs). Use this instead of model.load_state_dict after construction."""
+        self.model.load_state_dict(state)
+        if self.flat and hasattr(self.opt, "reload_master"):
+            self.opt.reload_master()
+        if self.tcache is not None:
+            self.tcache.refresh()
 
 
 def main(argv=None):
@@ -231,6 +253,7 @@ def main(argv=None):
                 per_step = native_stats.snapshot()
         if dev.type == "cuda":
             torch.cuda.synchronize()
+    tr.check()  # a timed-out TP all-reduce during warmup fails the run here (outside the timed region)
     mdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -247,6 +270,7 @@ def main(argv=None):
         torch.cuda.synchronize()
     mdist.barrier()
     dt = mdist.max_over_ranks(time.perf_counter() - t0)
+    tr.check()  # ... and during the timed steps: never report a throughput of garbage activations
     if env.rank == 0:
         print(json.dumps({"metric": "BERT-base fine-tune sequences/sec (TP over the node)", "value": a.batch * a.steps / dt,
                           "unit": "sequences/s", "n_gpus": env.world_size, "tp": tp.size, "batch": a.batch,

@@ -167,6 +167,13 @@ class FlatAdamW:
                 for i, p in enumerate(self.params):
                     p.register_post_accumulate_grad_hook(functools.partial(self._on_grad, i))
 
+    @torch.no_grad()
+    def reload_master(self) -> None:
+        """Re-derive the fp32 master weights from the bf16 parameters after they were written from outside the
+        optimizer (load_state_dict into the flat views, a warm start): otherwise the next step would overwrite the
+        loaded weights with the stale master copy."""
+        self.master.copy_(self.flat.float())
+
     # ---------------------------------------------------------------- overlapped update (captured steps)
     def _on_grad(self, i: int, p: torch.Tensor) -> None:
         if not (self._ov_active and torch.cuda.is_current_stream_capturing()):

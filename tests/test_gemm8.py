@@ -1,0 +1,91 @@
+"""Ping-pong pipelined GEMM (csrc/gemm8.hip) against a plain PyTorch fp32 reference of the same op: every tile
+configuration, every epilogue (none / bias / bias + GELU with the saved pre-bias product / + R / GELU backward with
+column sums / BatchNorm statistics), bf16 and fp32 biases, K from one to many K-tiles (the prologue, steady state
+and tail of the DMA schedule)."""
+import pytest
+import torch
+
+from mifx.ops import gemm
+
+
+def test_gemm8_pick_prefers_full_waves(monkeypatch):
+    monkeypatch.setattr(gemm, "gemm8_configs", lambda: ((256, 256), (256, 128), (128, 256), (128, 128)))
+    assert gemm.gemm8_pick(4096, 4096, 4096) == 0
+    assert gemm.gemm8_pick(4096, 768, 768) in (1, 2, 3)  # 256x256 leaves 48 workgroups on 256 CUs
+    assert gemm.gemm8_pick(100, 768, 768) is None
+    assert gemm.gemm8_pick(4096, 768, 100) is None
+
+
+def _operands(M, N, K, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+    return x, w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("K", [64, 128, 192, 640])
+def test_gemm8_plain_matches_fp32(cfg, K):
+    bm, bn = gemm.gemm8_configs()[cfg]
+    M, N = 3 * bm, 2 * bn
+    x, w = _operands(M, N, K, cfg * 31 + K)
+    y, _ = gemm.gemm8_nt(x, w, cfg=cfg)
+    ref = x.float() @ w.float().t()
+    # bf16 output: one rounding of the fp32 accumulation
+    assert ((y.float() - ref).abs() <= 2 ** -8 * ref.abs() + 1e-3).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("bias_dtype", [torch.bfloat16, torch.float32])
+def test_gemm8_epilogues_match_fp32(cfg, bias_dtype):
+    bm, bn = gemm.gemm8_configs()[cfg]
+    M, N, K = 2 * bm, 3 * bn, 320
+    x, w = _operands(M, N, K, 7 + cfg)
+    b = (torch.rand(N, device="cuda") - 0.5).to(bias_dtype)
+    prod = x.float() @ w.float().t()
+    tol = 2e-2 * prod.abs().max().item()
+    y, _ = gemm.gemm8_nt(x, w, b, 1, cfg=cfg)
+    assert (y.float() - (prod + b.float())).abs().max().item() <= tol
+    y, z = gemm.gemm8_nt(x, w, b, 2, cfg=cfg)
+    assert (z.float() - prod).abs().max().item() <= tol
+    ref = torch.nn.functional.gelu(z.float() + b.float())
+    assert (y.float() - ref).abs().max().item() <= 2 ** -7 * ref.abs().max().item()
+    r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    y, _ = gemm.gemm8_nt(x, w, r, 3, cfg=cfg)
+    assert (y.float() - (prod + r.float())).abs().max().item() <= tol
+    # GELU backward: dZ = (X W^T) o GELU'(Z + b), per-tile column sums of the stored dZ
+    zz = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    dz, part = gemm.gemm8_nt(x, w, b, 4, cfg=cfg, z=zz)
+    u = (zz.float() + b.float()).requires_grad_()
+    gd, = torch.autograd.grad(torch.nn.functional.gelu(u), u, torch.ones_like(u))
+    ref = prod * gd
+    assert (dz.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    assert part.shape == (M // bm, N)
+    colref = dz.float().view(M // bm, bm, N).sum(1)
+    assert torch.allclose(part, colref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_gemm8_stats_epilogue(cfg):
+    """The BatchNorm-statistics epilogue: per-tile column sum and sum of squares of the STORED bf16 output."""
+    bm, bn = gemm.gemm8_configs()[cfg]
+    M, N, K = 4 * bm, bn, 256
+    x, w = _operands(M, N, K, 100 + cfg)
+    y, part = gemm.gemm8_nt(x, w, None, 5, cfg=cfg)
+    yf = y.float().view(M // bm, bm, N)
+    assert part.shape == (2, M // bm, N)
+    assert torch.allclose(part[0], yf.sum(1), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(part[1], (yf * yf).sum(1), rtol=1e-4, atol=1e-3)
+    ref = x.float() @ w.float().t()
+    assert ((y.float() - ref).abs() <= 2 ** -8 * ref.abs() + 1e-3).all()
+
+
+@pytest.mark.gpu
+def test_gemm8_deterministic():
+    x, w = _operands(512, 512, 1024, 5)
+    a, _ = gemm.gemm8_nt(x, w, cfg=0)
+    b, _ = gemm.gemm8_nt(x, w, cfg=0)
+    assert torch.equal(a, b)

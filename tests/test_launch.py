@@ -114,3 +114,114 @@ def test_deploy_stack_manifests_parse_and_point_at_real_entry_points():
                     assert os.path.exists(os.path.join(root, cmd[1])), cmd[1]
                     seen += 1
     assert seen >= 5
+
+
+# ---------------------------------------------------------------- restart policies and device visibility
+_CKPT_WORKER = """
+import os, sys, torch, torch.distributed as dist
+out, fail_at = sys.argv[1], int(sys.argv[2])
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+w, start = torch.zeros(8, dtype=torch.float64), 0
+ck = os.path.join(out, "ckpt.pt")
+if os.path.exists(ck):  # resume from the latest checkpoint (what a restarted replica set does)
+    st = torch.load(ck, weights_only=True)
+    w, start = st["w"], int(st["step"])
+for step in range(start, 10):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    x = torch.randn(16, 8, generator=g, dtype=torch.float64)
+    grad = 2 * x.t() @ (x @ w - x.sum(1)) / 16
+    dist.all_reduce(grad)
+    w = w - 0.05 * grad / world
+    if rank == 0:
+        torch.save({"w": w, "step": step + 1}, ck + ".tmp")
+        os.replace(ck + ".tmp", ck)
+    dist.barrier()
+    if step + 1 == fail_at and rank == 1 and os.environ["MIFX_RESTART_COUNT"] == "0":
+        os._exit(3)  # injected rank failure, first attempt only
+if rank == 0:
+    torch.save({"w": w, "restart": os.environ["MIFX_RESTART_COUNT"]}, os.path.join(out, "final.pt"))
+dist.destroy_process_group()
+"""
+
+
+def _ckpt_job(tmp_path, name, policy, fail_at, backoff=None):
+    worker = tmp_path / "ck.py"
+    worker.write_text(_CKPT_WORKER)
+    out = tmp_path / name
+    out.mkdir()
+    d = {"kind": "PyTorchJob", "metadata": {"name": name},
+         "spec": {"pytorchReplicaSpecs": {"Worker": {"replicas": 3, "restartPolicy": policy, "template": {"spec": {
+             "containers": [{"name": "c", "command": ["python", str(worker), str(out), str(fail_at)]}]}}}}}}
+    if backoff is not None:
+        d["spec"]["runPolicy"] = {"backoffLimit": backoff}
+    return JobSpec.from_dict(d), out
+
+
+@pytest.mark.timeout(300)
+def test_on_failure_restarts_from_checkpoint_bit_identical(tmp_path):
+    import torch
+
+    ref_spec, ref_out = _ckpt_job(tmp_path, "ref", "Never", -1)
+    assert set(launch_local(ref_spec, num_gpus=0, timeout=120, log_dir=str(tmp_path / "l0")).values()) == {0}
+    spec, out = _ckpt_job(tmp_path, "inj", "OnFailure", 4)
+    stats = {}
+    codes = launch_local(spec, num_gpus=0, timeout=200, log_dir=str(tmp_path / "l1"), backoff_s=0.05, stats=stats)
+    assert set(codes.values()) == {0}, codes
+    assert stats["restarts"] == 1 and stats["attempts"][0]["worker-1"] == 3
+    a = torch.load(ref_out / "final.pt", weights_only=True)
+    b = torch.load(out / "final.pt", weights_only=True)
+    assert b["restart"] == "1" and torch.equal(a["w"], b["w"])  # resumed run == uninterrupted run, bit for bit
+
+
+@pytest.mark.timeout(300)
+def test_never_fails_fast_and_backoff_limit_is_honoured(tmp_path):
+    spec, out = _ckpt_job(tmp_path, "never", "Never", 4)
+    stats = {}
+    codes = launch_local(spec, num_gpus=0, timeout=120, log_dir=str(tmp_path / "l"), stats=stats)
+    assert codes["worker-1"] == 3 and stats["restarts"] == 0 and not (out / "final.pt").exists()
+    # backoffLimit 0: OnFailure but no restart allowed
+    spec, out = _ckpt_job(tmp_path, "bl0", "OnFailure", 4, backoff=0)
+    assert spec.backoff_limit == 0
+    codes = launch_local(spec, num_gpus=0, timeout=120, log_dir=str(tmp_path / "l2"), stats=stats)
+    assert codes["worker-1"] == 3 and stats["restarts"] == 0
+
+
+def test_exit_code_policy_restarts_only_retryable_codes():
+    from mifx.launch.job import ReplicaSpec, _wants_restart
+
+    r = ReplicaSpec("Worker", 2, ["x"], restart_policy="ExitCode")
+    spec = JobSpec("PyTorchJob", "t", [r])
+    roles = {"worker-0": r, "worker-1": r}
+    assert _wants_restart(spec, {"worker-0": 0, "worker-1": 137}, roles)  # SIGKILL / OOM: retryable
+    assert not _wants_restart(spec, {"worker-0": 0, "worker-1": 1}, roles)  # the program's own failure
+    assert not _wants_restart(spec, {"worker-0": 0, "worker-1": 0}, roles)
+    with pytest.raises(ValueError):
+        validate(JobSpec("PyTorchJob", "t", [ReplicaSpec("Worker", 1, ["x"], restart_policy="Sometimes")]))
+
+
+_ENV_WORKER = """
+import json, os, sys
+keys = ("RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "HIP_VISIBLE_DEVICES")
+open(os.path.join(sys.argv[1], "env" + os.environ["RANK"] + ".json"), "w").write(
+    json.dumps({k: os.environ.get(k) for k in keys}))
+"""
+
+
+@pytest.mark.parametrize("isolate", [False, True])
+def test_data_parallel_ranks_see_every_gpu(tmp_path, monkeypatch, isolate):
+    """A DP job's ranks must see all the node's GPUs (xGMI peer mapping, RCCL P2P) and pick theirs by LOCAL_RANK;
+    one-device isolation is opt-in (independent trials)."""
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    worker = tmp_path / "env.py"
+    worker.write_text(_ENV_WORKER)
+    spec = JobSpec.from_dict(_job("PyTorchJob", "pytorchReplicaSpecs", [("Master", 1), ("Worker", 3)], worker,
+                                  tmp_path))
+    codes = launch_local(spec, num_gpus=8, timeout=60, log_dir=str(tmp_path / "logs"), isolate_gpus=isolate)
+    assert set(codes.values()) == {0}
+    envs = [json.loads((tmp_path / f"env{r}.json").read_text()) for r in range(4)]
+    for r, e in enumerate(envs):
+        if isolate:
+            assert e["HIP_VISIBLE_DEVICES"] == str(r) and e["LOCAL_RANK"] == "0"
+        else:
+            assert e["HIP_VISIBLE_DEVICES"] is None and e["LOCAL_RANK"] == str(r) and e["LOCAL_WORLD_SIZE"] == "4"

@@ -58,6 +58,20 @@ def test_xgb_regressor_early_stopping():
     assert len(m.evals_result_["validation_0"]["rmse"]) > m.best_iteration
 
 
+def test_xgb_eval_set_without_early_stopping_uses_every_tree():
+    """XGBoost's sklearn API: best_iteration / best_score exist only under early stopping; with an eval_set alone
+    predict uses all n_estimators trees."""
+    r = np.random.default_rng(2)
+    X = r.normal(size=(400, 6))
+    y = X[:, 0] - 2 * X[:, 2] + r.normal(0, 0.5, 400)
+    m = XGBRegressor(n_estimators=60, learning_rate=0.3).fit(X[:300], y[:300], eval_set=[(X[300:], y[300:])])
+    assert m.best_iteration is None and m.best_score is None and m.n_trees_ == 60
+    hist = m.evals_result_["validation_0"]["rmse"]
+    assert len(hist) == 60
+    rmse = float(np.sqrt(np.mean((m.predict(X[300:]) - y[300:]) ** 2)))
+    assert rmse == pytest.approx(hist[-1], rel=1e-9)  # the last tree's score, not the best one's
+
+
 def test_xgb_classifier():
     r = np.random.default_rng(1)
     X = r.normal(size=(600, 5))

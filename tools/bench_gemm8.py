@@ -1,0 +1,87 @@
+"""Ping-pong pipelined GEMM (csrc/gemm8.hip) vs the one-barrier kernel (csrc/gemm.hip) vs hipBLASLt (F.linear) on
+random bf16 operands: a 4096^3 calibration shape, BERT-base's projection shapes at 4096 tokens (forward and the NT
+input-gradient products) and ResNet-50's 1x1-convolution GEMMs at batch 256. Each measurement first checks the
+kernel against an fp32 reference, then times 50 back-to-back calls after 10 warmups (CUDA events). One JSON line per
+measurement.
+
+usage: python tools/bench_gemm8.py [--shapes calib,bert,dx,resnet] [--cfg i,j]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mifx.ops import gemm  # noqa: E402
+
+SHAPES = {
+    "calib": [("sq4096", 4096, 4096, 4096)],
+    "bert": [("qkv", 4096, 2304, 768), ("attn_out", 4096, 768, 768), ("ffn_in", 4096, 3072, 768),
+             ("ffn_out", 4096, 768, 3072)],
+    "dx": [("qkv_dx", 4096, 768, 2304), ("ffn_in_dx", 4096, 768, 3072), ("ffn_out_dx", 4096, 3072, 768)],
+    "resnet": [("s1_64_256", 802816, 256, 64), ("s1_256_64", 802816, 64, 256), ("s2_512_128", 200704, 128, 512),
+               ("s2_128_512", 200704, 512, 128), ("s3_1024_256", 50176, 256, 1024), ("s3_256_1024", 50176, 1024, 256),
+               ("s4_2048_512", 12544, 512, 2048), ("s4_512_2048", 12544, 2048, 512)],
+}
+
+
+def timeit(fn, iters=50):
+    for _ in range(10):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="calib,bert")
+    ap.add_argument("--cfg", default=None)
+    ap.add_argument("--old", action="store_true", help="also time csrc/gemm.hip configurations")
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    cfgs = gemm.gemm8_configs()
+    sel = [int(c) for c in a.cfg.split(",")] if a.cfg else range(len(cfgs))
+    for group in a.shapes.split(","):
+        for name, M, N, K in SHAPES[group]:
+            x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+            w = ((torch.rand(N, K, device="cuda") * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+            flop = 2.0 * M * N * K
+            rows = [("hipblaslt", lambda: F.linear(x, w))]
+            ref = None
+            if M * N <= 4096 * 4096:
+                ref = x.float() @ w.float().t()
+            for i in sel:
+                bm, bn = cfgs[i]
+                if M % bm or N % bn or K % 64:
+                    continue
+                if ref is not None:
+                    y, _ = gemm.gemm8_nt(x, w, cfg=i)
+                    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+                    if err > 2e-2:
+                        print(json.dumps({"gemm": name, "cfg": i, "ERROR_rel": err}), flush=True)
+                        continue
+                rows.append((f"gemm8 cfg{i} {bm}x{bn}", lambda i=i: gemm.gemm8_nt(x, w, cfg=i)))
+            if a.old:
+                for i, (bm, bn, opt) in enumerate(gemm.config_details()):
+                    if M % bm or N % bn or K % 64 or M * N > 4096 * 4096:
+                        continue
+                    rows.append((f"gemm cfg{i} {bm}x{bn} opt{opt}", lambda i=i: gemm.gemm_nt(x, w, cfg=i)))
+            for label, fn in rows:
+                us = timeit(fn)
+                print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "impl": label, "us": round(us, 2),
+                                  "tflops": round(flop / us / 1e6, 1)}), flush=True)
+            del x, w, ref
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
