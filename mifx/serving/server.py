@@ -1,7 +1,7 @@
 """Model server with the TF-Serving REST API, version management and GPU dynamic batching.
 
 Reference: the TF-Serving deployment (`tensorflow_model_server --port=9000 --rest_api_port=8500
---model_name --model_base_path`, ksonnet `tf-serving` prototypes, optional Prometheus monitoring
+--model_name --model_base_path`; the gRPC API on --port is mifx.serving.grpc_service, ksonnet `tf-serving` prototypes, optional Prometheus monitoring
 config) and the notebook's REST usage (`serving/Predict_Fashion_MNIST.ipynb`: POST
 `/v1/models/<name>:predict` and `/v1/models/<name>/versions/<v>:predict` with `{"instances": ...}`).
 
@@ -282,7 +282,8 @@ def create_app(models: dict[str, ModelManager]):
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="mifx-model-server")
     ap.add_argument("--rest_api_port", type=int, default=8500)
-    ap.add_argument("--port", type=int, default=9000, help="accepted for CLI compatibility (no gRPC endpoint)")
+    ap.add_argument("--port", type=int, default=9000,
+                    help="gRPC PredictionService / ModelService port (tensorflow_model_server --port); -1 disables")
     ap.add_argument("--model_name", required=True)
     ap.add_argument("--model_base_path", required=True)
     ap.add_argument("--version_policy", default="latest", choices=["latest", "all", "specific"])
@@ -295,7 +296,17 @@ def main(argv=None):
 
     mgr = ModelManager(a.model_name, a.model_base_path, a.version_policy, a.versions, a.device,
                        a.file_system_poll_wait_seconds, bool(a.enable_batching))
-    uvicorn.run(create_app({a.model_name: mgr}), host="0.0.0.0", port=a.rest_api_port, log_level="warning")
+    models = {a.model_name: mgr}
+    grpc_server = None
+    if a.port >= 0:  # the gRPC API beside REST, sharing the loaded versions and the dynamic batcher
+        from .grpc_service import serve
+
+        grpc_server, _ = serve(models, a.port)
+    try:
+        uvicorn.run(create_app(models), host="0.0.0.0", port=a.rest_api_port, log_level="warning")
+    finally:
+        if grpc_server is not None:
+            grpc_server.stop(grace=1.0)
 
 
 if __name__ == "__main__":

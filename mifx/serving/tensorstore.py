@@ -68,6 +68,14 @@ class TensorStore:
             return t
         return {"dtype": _DT_NAME[t.dtype], "shape": list(t.shape), "values": t.detach().cpu().reshape(-1).tolist()}
 
+    def exists(self, key: str) -> bool:
+        with self._lock:
+            return key in self._t or key in self._models or key in self._scripts
+
+    def keys(self) -> list:
+        with self._lock:
+            return sorted(set(self._t) | set(self._models) | set(self._scripts))
+
     def delete(self, key: str):
         with self._lock:
             for d in (self._t, self._models, self._scripts):
