@@ -1,0 +1,260 @@
+"""Training-job operator: reconciles MIFXJob / TFJob / PyTorchJob custom resources into running replica sets.
+
+Reference: the Kubeflow tf-job-operator / pytorch-operator the workshop installs (`install-kubeflow/app.yaml:15-27`,
+CRD `infrastructure/crd/tfjob-crd-v1.yaml`), which watch job CRs, create the replica pods, restart them per
+`restartPolicy` and report `status.conditions` (Created / Running / Restarting / Succeeded / Failed). Two backends:
+
+  * `KubeBackend` -- the Kubernetes REST API through the pod's service account (no client library needed): each new
+    CR becomes the single-node batch/v1 Job of `mifx.launch.job.to_indexed_job` (one pod, all GPUs of the node, one
+    rank per GPU under torch.distributed.run; restartPolicy OnFailure / Always / ExitCode -> the Job's backoffLimit,
+    Never -> 0), owned by the CR, and the Job's status is mirrored into the CR's status subresource.
+    Deployed by `deploy/k8s/mifxjob-operator.yaml` (ServiceAccount + RBAC + Deployment).
+  * `LocalBackend` -- CRs as YAML files in a directory (the single-node stand-in for the API server): each is run by
+    `launch_local` (restart semantics included) on a worker thread and its status written next to it as JSON.
+
+`python -m mifx.launch.operator --local DIR` / `--kube [--namespace NS]` runs the control loop."""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+
+import yaml
+
+from .job import JobSpec, launch_local, to_indexed_job
+
+KINDS = {"MIFXJob": ("mifx.amd.com", "v1", "mifxjobs"), "TFJob": ("kubeflow.org", "v1", "tfjobs"),
+         "PyTorchJob": ("kubeflow.org", "v1", "pytorchjobs")}
+TERMINAL = ("Succeeded", "Failed")
+
+
+def _now() -> str:
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+
+
+def _condition(status: dict, ctype: str, reason: str, message: str = "") -> dict:
+    """Append a condition (TFJob status convention: the last condition is the current phase)."""
+    conds = status.setdefault("conditions", [])
+    if not conds or conds[-1]["type"] != ctype:
+        conds.append({"type": ctype, "status": "True", "reason": reason, "message": message,
+                      "lastTransitionTime": _now()})
+    status["phase"] = ctype
+    return status
+
+
+def phase(status: dict | None) -> str | None:
+    return (status or {}).get("phase")
+
+
+# ---------------------------------------------------------------- local backend
+class LocalBackend:
+    """CRs are `<dir>/<name>.yaml`; status goes to `<dir>/<name>.status.json`; logs under `<dir>/logs/<name>/`."""
+
+    def __init__(self, root: str, num_gpus: int | None = None, cwd: str | None = None):
+        self.root, self.num_gpus, self.cwd = root, num_gpus, cwd
+        self._threads: dict[str, threading.Thread] = {}
+
+    def _status_path(self, name: str) -> str:
+        return os.path.join(self.root, f"{name}.status.json")
+
+    def list(self) -> list[tuple[str, dict, dict | None]]:
+        out = []
+        for fn in sorted(os.listdir(self.root)):
+            if not fn.endswith((".yaml", ".yml")):
+                continue
+            with open(os.path.join(self.root, fn)) as f:
+                cr = yaml.safe_load(f)
+            if not isinstance(cr, dict) or cr.get("kind") not in KINDS:
+                continue
+            name = cr.get("metadata", {}).get("name") or os.path.splitext(fn)[0]
+            st = None
+            if os.path.exists(self._status_path(name)):
+                with open(self._status_path(name)) as f:
+                    st = json.load(f)
+            out.append((name, cr, st))
+        return out
+
+    def set_status(self, name: str, status: dict) -> None:
+        tmp = self._status_path(name) + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(status, f, indent=1)
+        os.replace(tmp, self._status_path(name))
+
+    def reconcile(self, name: str, cr: dict, status: dict | None) -> None:
+        if phase(status) in TERMINAL or name in self._threads:
+            return
+        try:
+            spec = JobSpec.from_dict(cr)
+        except ValueError as e:
+            self.set_status(name, _condition({}, "Failed", "InvalidSpec", str(e)))
+            return
+        st = _condition(_condition({"startTime": _now()}, "Created", "JobCreated"), "Running", "JobRunning")
+        self.set_status(name, st)
+
+        def run():
+            stats: dict = {}
+            codes = launch_local(spec, num_gpus=self.num_gpus, cwd=self.cwd,
+                                 log_dir=os.path.join(self.root, "logs", name), stats=stats)
+            st2 = dict(st, restarts=stats.get("restarts", 0), exitCodes=codes, completionTime=_now())
+            if stats.get("restarts"):
+                _condition(st2, "Restarting", "JobRestarting", f"{stats['restarts']} restart(s) of the replica set")
+            ok = all(c == 0 for c in codes.values())
+            _condition(st2, "Succeeded" if ok else "Failed", "JobSucceeded" if ok else "JobFailed",
+                       "" if ok else f"replica exit codes {codes}")
+            self.set_status(name, st2)
+
+        t = threading.Thread(target=run, daemon=True)
+        self._threads[name] = t
+        t.start()
+
+    def idle(self) -> bool:
+        return all(not t.is_alive() for t in self._threads.values())
+
+
+# ---------------------------------------------------------------- Kubernetes backend
+class KubeApi:
+    """Minimal Kubernetes REST client: in-cluster service-account token + CA (or an explicit base URL / token)."""
+
+    SA = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+    def __init__(self, base: str | None = None, token: str | None = None, verify=None):
+        import requests
+
+        self.s = requests.Session()
+        if base is None:
+            base = f"https://{os.environ['KUBERNETES_SERVICE_HOST']}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}"
+        if token is None and os.path.exists(f"{self.SA}/token"):
+            with open(f"{self.SA}/token") as f:
+                token = f.read().strip()
+        if token:
+            self.s.headers["Authorization"] = f"Bearer {token}"
+        self.s.verify = verify if verify is not None else (f"{self.SA}/ca.crt" if os.path.exists(f"{self.SA}/ca.crt")
+                                                          else True)
+        self.base = base.rstrip("/")
+
+    def get(self, path: str):
+        r = self.s.get(self.base + path, timeout=30)
+        if r.status_code == 404:
+            return None
+        r.raise_for_status()
+        return r.json()
+
+    def post(self, path: str, body: dict):
+        r = self.s.post(self.base + path, json=body, timeout=30)
+        r.raise_for_status()
+        return r.json()
+
+    def patch_status(self, path: str, status: dict):
+        r = self.s.patch(self.base + path + "/status", data=json.dumps({"status": status}), timeout=30,
+                         headers={"Content-Type": "application/merge-patch+json"})
+        r.raise_for_status()
+        return r.json()
+
+
+class KubeBackend:
+    def __init__(self, api, namespace: str = "kubeflow", image: str | None = None):
+        self.api, self.ns, self.image = api, namespace, image
+
+    def _cr_path(self, kind: str, name: str | None = None) -> str:
+        g, v, plural = KINDS[kind]
+        p = f"/apis/{g}/{v}/namespaces/{self.ns}/{plural}"
+        return p + (f"/{name}" if name else "")
+
+    def list(self) -> list[tuple[str, dict, dict | None]]:
+        out = []
+        for kind in KINDS:
+            try:
+                lst = self.api.get(self._cr_path(kind))
+            except Exception:  # noqa: BLE001 -- a CRD that is not installed
+                lst = None
+            for cr in (lst or {}).get("items", []):
+                cr.setdefault("kind", kind)
+                out.append((cr["metadata"]["name"], cr, cr.get("status")))
+        return out
+
+    def set_status(self, name: str, status: dict, kind: str = "MIFXJob") -> None:
+        self.api.patch_status(self._cr_path(kind, name), status)
+
+    def reconcile(self, name: str, cr: dict, status: dict | None) -> None:
+        kind = cr.get("kind", "MIFXJob")
+        if phase(status) in TERMINAL:
+            return
+        try:
+            spec = JobSpec.from_dict(cr)
+        except ValueError as e:
+            self.set_status(name, _condition({}, "Failed", "InvalidSpec", str(e)), kind)
+            return
+        jpath = f"/apis/batch/v1/namespaces/{self.ns}/jobs"
+        job = self.api.get(f"{jpath}/{name}")
+        st = dict(status or {})
+        if job is None:
+            body = to_indexed_job(spec, self.ns, self.image)
+            body["metadata"]["name"] = name
+            body["metadata"]["ownerReferences"] = [{
+                "apiVersion": f"{KINDS[kind][0]}/{KINDS[kind][1]}", "kind": kind, "name": name,
+                "uid": cr["metadata"].get("uid", ""), "controller": True, "blockOwnerDeletion": True}]
+            policies = {r.restart_policy for r in spec.replicas}
+            restart = bool(policies & {"OnFailure", "Always", "ExitCode"})
+            body["spec"]["backoffLimit"] = (spec.backoff_limit if spec.backoff_limit is not None else 3) \
+                if restart else 0
+            self.api.post(jpath, body)
+            st.setdefault("startTime", _now())
+            self.set_status(name, _condition(st, "Created", "JobCreated", f"batch/v1 Job {name}"), kind)
+            return
+        js = job.get("status") or {}
+        if js.get("succeeded"):
+            _condition(st, "Succeeded", "JobSucceeded")
+            st["completionTime"] = _now()
+        elif any(c.get("type") == "Failed" and c.get("status") == "True" for c in js.get("conditions") or []):
+            _condition(st, "Failed", "JobFailed", f"{js.get('failed', 0)} failed pod(s)")
+            st["completionTime"] = _now()
+        elif js.get("failed"):
+            _condition(st, "Restarting", "JobRestarting", f"{js['failed']} failed attempt(s), retrying")
+            st["restarts"] = int(js["failed"])
+        elif js.get("active"):
+            _condition(st, "Running", "JobRunning")
+        else:
+            return
+        self.set_status(name, st, kind)
+
+
+# ---------------------------------------------------------------- control loop
+def reconcile_all(backend) -> int:
+    """One pass over every CR; returns how many are not yet terminal."""
+    pending = 0
+    for name, cr, st in backend.list():
+        try:
+            backend.reconcile(name, cr, st)
+        except Exception as e:  # noqa: BLE001 -- one bad CR never stops the loop
+            print(f"[mifx-operator] {name}: {e}", flush=True)
+        if phase(st) not in TERMINAL:
+            pending += 1
+    return pending
+
+
+def run(backend, interval_s: float = 2.0, stop: threading.Event | None = None) -> None:
+    stop = stop or threading.Event()
+    while not stop.is_set():
+        reconcile_all(backend)
+        stop.wait(interval_s)
+
+
+def main(argv=None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="python -m mifx.launch.operator", description=__doc__.split("\n")[0])
+    g = ap.add_mutually_exclusive_group(required=True)
+    g.add_argument("--local", metavar="DIR", help="watch CR YAML files in DIR and run them as local processes")
+    g.add_argument("--kube", action="store_true", help="reconcile CRs through the Kubernetes API (in-cluster)")
+    ap.add_argument("--namespace", default=os.environ.get("POD_NAMESPACE", "kubeflow"))
+    ap.add_argument("--image", default=None, help="container image for the rendered Jobs")
+    ap.add_argument("--interval", type=float, default=2.0)
+    a = ap.parse_args(argv)
+    backend = LocalBackend(a.local) if a.local else KubeBackend(KubeApi(), a.namespace, a.image)
+    run(backend, a.interval)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -225,3 +225,142 @@ def test_data_parallel_ranks_see_every_gpu(tmp_path, monkeypatch, isolate):
             assert e["HIP_VISIBLE_DEVICES"] == str(r) and e["LOCAL_RANK"] == "0"
         else:
             assert e["HIP_VISIBLE_DEVICES"] is None and e["LOCAL_RANK"] == str(r) and e["LOCAL_WORLD_SIZE"] == "4"
+
+
+# ---------------------------------------------------------------- job operator (CR -> replica set, status)
+def test_operator_local_backend_runs_crs_and_reports_status(tmp_path):
+    import time as _time
+
+    from mifx.launch import operator as op
+
+    worker = tmp_path / "w.py"
+    worker.write_text(_WORKER)
+    out = tmp_path / "out"
+    out.mkdir()
+    crs = tmp_path / "crs"
+    crs.mkdir()
+    ok = _job("PyTorchJob", "pytorchReplicaSpecs", [("Master", 1), ("Worker", 2)], worker, out)
+    ok["metadata"]["name"] = "good"
+    bad = {"kind": "MIFXJob", "metadata": {"name": "bad"}, "spec": {"replicaSpecs": {"Worker": {
+        "replicas": 2, "restartPolicy": "Never",
+        "template": {"spec": {"containers": [{"command": ["python", "-c", "import sys; sys.exit(4)"]}]}}}}}}
+    invalid = {"kind": "TFJob", "metadata": {"name": "invalid"}, "spec": {"tfReplicaSpecs": {"Chief": {
+        "replicas": 2, "template": {"spec": {"containers": [{"command": ["x"]}]}}}}}}
+    for cr in (ok, bad, invalid):
+        (crs / f"{cr['metadata']['name']}.yaml").write_text(yaml.safe_dump(cr))
+    be = op.LocalBackend(str(crs), num_gpus=0)
+    deadline = _time.time() + 120
+    while op.reconcile_all(be) and _time.time() < deadline:
+        _time.sleep(0.2)
+    st = {n: s for n, _, s in be.list()}
+    assert st["good"]["phase"] == "Succeeded" and [c["type"] for c in st["good"]["conditions"]] == \
+        ["Created", "Running", "Succeeded"]
+    assert st["bad"]["phase"] == "Failed" and set(st["bad"]["exitCodes"].values()) <= {4, -9}
+    assert st["invalid"]["phase"] == "Failed" and st["invalid"]["conditions"][-1]["reason"] == "InvalidSpec"
+    assert {json.loads((out / f"r{r}.json").read_text())["sum"] for r in range(3)} == {6.0}
+
+
+def test_operator_kube_backend_creates_job_and_mirrors_status():
+    from mifx.launch import operator as op
+
+    class FakeApi:
+        def __init__(self):
+            self.objs, self.status = {}, {}
+
+        def get(self, path):
+            if path.endswith("/mifxjobs"):
+                return {"items": [self.cr]}
+            if path.endswith(("/tfjobs", "/pytorchjobs")):
+                return None
+            return self.objs.get(path)
+
+        def post(self, path, body):
+            self.objs[f"{path}/{body['metadata']['name']}"] = body
+            return body
+
+        def patch_status(self, path, status):
+            self.status[path] = status
+            self.cr["status"] = status
+
+    api = FakeApi()
+    api.cr = {"kind": "MIFXJob", "metadata": {"name": "dp8", "uid": "u1"}, "spec": {
+        "runPolicy": {"backoffLimit": 2},
+        "replicaSpecs": {"Worker": {"replicas": 8, "restartPolicy": "OnFailure", "template": {"spec": {"containers": [
+            {"image": "img", "command": ["python3", "bench.py", "--gpus", "8"],
+             "resources": {"limits": {"amd.com/gpu": 1}}}]}}}}}}
+    be = op.KubeBackend(api, "kubeflow")
+    assert op.reconcile_all(be) == 1
+    job = api.objs["/apis/batch/v1/namespaces/kubeflow/jobs/dp8"]
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert "--nproc-per-node=8" in c["command"] and c["resources"]["limits"]["amd.com/gpu"] == "8"
+    assert job["spec"]["backoffLimit"] == 2 and job["metadata"]["ownerReferences"][0]["uid"] == "u1"
+    assert api.cr["status"]["phase"] == "Created"
+    op.reconcile_all(be)  # no Job status yet: nothing changes, no second Job
+    assert len(api.objs) == 1
+    job["status"] = {"active": 1}
+    op.reconcile_all(be)
+    assert api.cr["status"]["phase"] == "Running"
+    job["status"] = {"failed": 1, "active": 1}
+    op.reconcile_all(be)
+    assert api.cr["status"]["phase"] == "Restarting" and api.cr["status"]["restarts"] == 1
+    job["status"] = {"succeeded": 1, "failed": 1}
+    assert op.reconcile_all(be) == 1  # (the pass that observes success)
+    assert api.cr["status"]["phase"] == "Succeeded"
+    assert op.reconcile_all(be) == 0
+
+
+def test_central_dashboard_reports_live_services(tmp_path):
+    """The dashboard probes each service: one that answers is 'up', one that does not is 'down'."""
+    import threading
+
+    import uvicorn
+    from fastapi.testclient import TestClient
+
+    from mifx import dashboard
+    from mifx.board.server import create_app as board_app
+
+    import socket as _s
+    with _s.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    srv = uvicorn.Server(uvicorn.Config(board_app(str(tmp_path)), host="127.0.0.1", port=port, log_level="error"))
+    t = threading.Thread(target=srv.run, daemon=True)
+    t.start()
+    import time as _time
+    for _ in range(100):
+        if srv.started:
+            break
+        _time.sleep(0.05)
+    try:
+        services = [("board", "scalars", f"http://127.0.0.1:{port}/healthz", "/tensorboard/"),
+                    ("gone", "nothing listens", "http://127.0.0.1:9/healthz", "/gone/"),
+                    ("tracking", "files", None, "/tracking/")]
+        c = TestClient(dashboard.create_app(services))
+        st = {s["name"]: s["state"] for s in c.get("/api/services").json()["services"]}
+        assert st == {"board": "up", "gone": "down", "tracking": "static"}
+        assert "board" in c.get("/").text
+    finally:
+        srv.should_exit = True
+        t.join(5)
+
+
+def test_reverse_proxy_and_bootstrap_cover_every_service():
+    """deploy/nginx.conf routes every local service of the dashboard's list and the bootstrap script starts them
+    (and parses as bash)."""
+    import os
+    import re
+    import subprocess
+
+    from mifx import dashboard
+
+    root = os.path.join(os.path.dirname(__file__), "..")
+    conf = open(os.path.join(root, "deploy/nginx.conf")).read()
+    for _, _, _, link in dashboard.SERVICES:
+        assert re.search(r"location\s+" + re.escape(link) + r"\s", conf), link
+    boot = os.path.join(root, "deploy/scripts/bootstrap-node.sh")
+    subprocess.run(["bash", "-n", boot], check=True)
+    text = open(boot).read()
+    for mod in ("mifx.dashboard", "mifx.kfp.server", "mifx.metadata.server", "mifx.board", "mifx.notebook_server",
+                "mifx.launch.operator", "mifx.serving.resp_server", "mifx.serving.server"):
+        assert mod in text, mod
+    assert "kubectl apply -k" in text and "mifxjob-crd.yaml" in text
