@@ -29,6 +29,16 @@
 //  * XCD-aware bijective tile order (consecutive workgroups land on different XCDs; each XCD walks a contiguous run of
 //    tiles that share X row panels in its L2).
 //
+// TN layout (weight gradients, dW = dY^T X: both operands token-major, the reduction is their ROW index): the same
+// schedule with half-tiles of 64 tokens x BM/2 (BN/2) columns; an LDS row is a token's 256 (or 128) bytes with its
+// 16-byte chunks rotated per token (conflict-free transposed reads, csrc/gemm_tn.hip's rot<>), and the MFMA fragments
+// (8 consecutive tokens of one column per lane) come from two ds_read_b64_tr_b16. GROUPED launch: a table of up to
+// 64 problems in the kernel arguments, each workgroup finds its (problem, tile) by binary search over the per-problem
+// first-tile indices. A BERT step's 48 weight-gradient products are off the backward's critical path, so they are
+// deferred to the end of the backward and run as ONE launch of full 256 x 256 tiles over the whole 4096-token
+// reduction (no split-K partials, 1296 tiles = five waves of 256 CUs), instead of 48 small launches whose few output
+// tiles had to be split over tokens and summed by a second kernel.
+//
 // Epilogues: none / + bias[N] / bias + GELU(erf) also storing the pre-bias product Z (the FFN-in forward) / + R[M, N]
 // (dX = dY W + residual gradient) / GELU backward dZ = (X W^T) o GELU'(Z + bias) with per-tile column sums (the FFN-out
 // input gradient fused with FFN-in's bias-GELU backward) / per-tile column sum and sum of squares of the stored bf16
@@ -63,44 +73,91 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// TN images: chunk rotation of token row t for a row of CPR 16-byte chunks (every 32-lane half of a transposed
+// fragment read touches 64 distinct banks; tools/lds_banks_tn.py)
+template <int CPR>
+__device__ __forceinline__ int rot(int t) {
+  static_assert(CPR == 8 || CPR == 16, "chunks per token row");
+  if constexpr (CPR == 8) return ((t & 3) + 4 * ((t >> 3) & 3)) & 7;
+  return (2 * (t & 3) + 8 * ((t >> 3) & 3)) & 15;
+}
+__device__ __forceinline__ v8bf tr_frag(const unsigned char* p1, const unsigned char* p2) {
+  const v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p1);
+  const v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p2);
+  const v8s r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
+
+// grouped TN problems: C[M, N] (bf16, ldc N) = A[T, M]^T B[T, N]; tiles of problem i are [first[i], first[i + 1])
+constexpr int MAXP = 64;
+struct Prob {
+  const bf16* A;
+  const bf16* B;
+  bf16* C;
+  int M, N, T, pad;
+};
+struct Group {
+  Prob p[MAXP];
+  int first[MAXP + 1];
+  int n;
+};
+
 // s_waitcnt immediate (gfx9 encoding): vmcnt = n, expcnt / lgkmcnt not waited on
 constexpr int vm_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
 
-template <int BM, int BN, int EPI, typename P>
-__global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, const bf16* __restrict__ W,
-                                                  const P* __restrict__ bias, bf16* __restrict__ Y,
-                                                  bf16* __restrict__ Z, int M, int N, int K,
-                                                  float* __restrict__ part) {
-  constexpr int HA = BM / 2, HB = BN / 2;            // rows per half-tile
-  constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // 64 bf16 = 128 bytes per row
+// The body: one BM x BN tile of Y = X W^T (NT: X [M, K], W [N, K] row-major) or of C = A^T B (TN: A [K, M],
+// B [K, N] row-major; X := A, W := B, "K" = tokens), m0 / n0 its origin.
+template <int BM, int BN, int EPI, typename P, bool TN>
+__device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                           const P* __restrict__ bias, bf16* __restrict__ Y, bf16* __restrict__ Z,
+                                           int M, int N, int K, float* __restrict__ part, int m0, int n0,
+                                           unsigned char* lds) {
+  constexpr int HA = BM / 2, HB = BN / 2;            // rows (NT) / columns (TN) per half-tile
+  constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // NT: 64 bf16 per row; TN: 64 token rows of HA bf16
   constexpr int XR = HA * 8 / NT, WR = HB * 8 / NT;    // DMAs per thread per half-tile
+  constexpr int CPA = HA / 8, CPB = HB / 8;            // TN: 16-byte chunks per token row
   static_assert(HA * 8 % NT == 0 && HB * 8 % NT == 0, "whole DMA rounds per half-tile");
   constexpr int MF = HA / 32, NF = HB / 64;  // 16-row fragments per wave per quadrant (2 x 4 waves)
   static_assert(MF >= 1 && NF >= 1, "tile too small for 8 waves");
   constexpr int BUF = 2 * (ABYTES + BBYTES);
   constexpr int OFF_A0 = 0, OFF_B0 = ABYTES, OFF_A1 = ABYTES + BBYTES, OFF_B1 = 2 * ABYTES + BBYTES;
   constexpr int KTILE_DMAS = 2 * (XR + WR);  // DMAs per thread per K-tile = per 4 consecutive phases
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wm = w >> 2, wn = w & 3;  // wave position inside a quadrant; wm is also the stagger group
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
-  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-  const int nb_n = N / BN;
-  const int m0 = (tile / nb_n) * BM, n0 = (tile % nb_n) * BN;
   const int KT = K / BK;
 
-  // per-lane DMA source offsets (elements, K-tile 0) of each half, pre-swizzled
+  // per-lane DMA source offsets (elements, K-tile 0) of each half, pre-swizzled / pre-rotated
   int aoff[XR], boff[WR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
-    const int qq = i * NT + tid, row = qq >> 3;
-    aoff[i] = (m0 + row) * K + 8 * swz(row, qq & 7);
+    const int qq = i * NT + tid;
+    if constexpr (TN) {
+      const int t = qq / CPA, pc = qq % CPA;  // token row, physical chunk
+      int c = pc - rot<CPA>(t);
+      c = c < 0 ? c + CPA : c;
+      aoff[i] = t * M + m0 + 8 * c;
+    } else {
+      const int row = qq >> 3;
+      aoff[i] = (m0 + row) * K + 8 * swz(row, qq & 7);
+    }
   }
 #pragma unroll
   for (int i = 0; i < WR; ++i) {
-    const int qq = i * NT + tid, row = qq >> 3;
-    boff[i] = (n0 + row) * K + 8 * swz(row, qq & 7);
+    const int qq = i * NT + tid;
+    if constexpr (TN) {
+      const int t = qq / CPB, pc = qq % CPB;
+      int c = pc - rot<CPB>(t);
+      c = c < 0 ? c + CPB : c;
+      boff[i] = t * N + n0 + 8 * c;
+    } else {
+      const int row = qq >> 3;
+      boff[i] = (n0 + row) * K + 8 * swz(row, qq & 7);
+    }
   }
   // half h (0 A0, 1 B0, 2 A1, 3 B1) of K-tile t into LDS buffer t & 1
   auto stage = [&](int h, int t) {
@@ -108,7 +165,7 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
     const int k0 = t * BK;
     if (h == 0 || h == 2) {
       unsigned char* dst = buf + (h == 0 ? OFF_A0 : OFF_A1);
-      const bf16* src = X + (h == 2 ? HA * K : 0) + k0;
+      const bf16* src = TN ? X + (size_t)k0 * M + (h == 2 ? HA : 0) : X + (h == 2 ? HA * K : 0) + k0;
 #pragma unroll
       for (int i = 0; i < XR; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(src + aoff[i]),
@@ -116,7 +173,7 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
                                          0, 0);
     } else {
       unsigned char* dst = buf + (h == 1 ? OFF_B0 : OFF_B1);
-      const bf16* src = W + (h == 3 ? HB * K : 0) + k0;
+      const bf16* src = TN ? W + (size_t)k0 * N + (h == 3 ? HB : 0) : W + (h == 3 ? HB * K : 0) + k0;
 #pragma unroll
       for (int i = 0; i < WR; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(src + boff[i]),
@@ -137,12 +194,28 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
 
   const int fr = lane & 15, fc = lane >> 4;
   v8bf ra0[MF][2], ra1[MF][2], rb[NF][2];  // A0 / A1 / current-B fragments, [frag][k-step]
+  // TN fragment geometry: lane (r = lane & 15 -> token quad q = r >> 2, column quad p = r & 3; h = lane >> 4): the
+  // two transposed reads deliver tokens 32 ks + 8 h + q and + 4 of column 16 f + 4 p .. (4 consecutive per read)
+  const int tq = fr >> 2, tp = fr & 3;
+  auto tn_frag = [&](const unsigned char* half, int cpr_rot, int col0, int ks) -> v8bf {
+    const int t1 = 32 * ks + 8 * fc + tq, t2 = t1 + 4;
+    const int c = col0 / 8 + (tp >> 1);
+    int s1 = c + (cpr_rot == 16 ? rot<16>(t1) : rot<8>(t1)), s2 = c + (cpr_rot == 16 ? rot<16>(t2) : rot<8>(t2));
+    s1 = s1 >= cpr_rot ? s1 - cpr_rot : s1;
+    s2 = s2 >= cpr_rot ? s2 - cpr_rot : s2;
+    return tr_frag(half + (t1 * cpr_rot + s1) * 16 + 8 * (tp & 1), half + (t2 * cpr_rot + s2) * 16 + 8 * (tp & 1));
+  };
   auto read_a = [&](const unsigned char* half, v8bf (&r)[MF][2]) {
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
       const int row = wm * (HA / 2) + 16 * f + fr;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) r[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (TN)
+          r[f][ks] = tn_frag(half, CPA, wm * (HA / 2) + 16 * f, ks);
+        else
+          r[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+      }
     }
   };
   auto read_b = [&](const unsigned char* half) {
@@ -150,7 +223,12 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
     for (int f = 0; f < NF; ++f) {
       const int row = wn * (HB / 4) + 16 * f + fr;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) rb[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (TN)
+          rb[f][ks] = tn_frag(half, CPB, wn * (HB / 4) + 16 * f, ks);
+        else
+          rb[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+      }
     }
   };
   auto mma = [&](v4f (&c)[NF][MF], const v8bf (&ra)[MF][2]) {
@@ -340,6 +418,41 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
     }
 }
 
+__device__ __forceinline__ int xcd_tile() {  // bijective XCD-aware remap of blockIdx.x (guide section 5)
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+}
+
+template <int BM, int BN, int EPI, typename P>
+__global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                  const P* __restrict__ bias, bf16* __restrict__ Y,
+                                                  bf16* __restrict__ Z, int M, int N, int K,
+                                                  float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tile = xcd_tile(), nb_n = N / BN;
+  gemm8_tile<BM, BN, EPI, P, false>(X, W, bias, Y, Z, M, N, K, part, (tile / nb_n) * BM, (tile % nb_n) * BN, lds);
+}
+
+// grouped TN: each workgroup's (problem, tile) from the table; tiles of a problem run m-fastest in groups of 4
+// m-blocks (an XCD's consecutive tiles share B column strips in its L2)
+template <int BM, int BN>
+__global__ __launch_bounds__(NT, 1) void gemm8_tn_grouped(const Group g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tile = xcd_tile();
+  int lo = 0, hi = g.n - 1;  // largest i with first[i] <= tile
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (g.first[mid] <= tile) lo = mid; else hi = mid - 1;
+  }
+  const Prob& p = g.p[lo];
+  const int t = tile - g.first[lo];
+  constexpr int GM = 4;
+  const int nb_m = p.M / BM, nb_n = p.N / BN, per_group = GM * nb_n;
+  const int grp = t / per_group, first_m = grp * GM, gsz = min(GM, nb_m - first_m), wi = t - grp * per_group;
+  gemm8_tile<BM, BN, EPI_NONE, bf16, true>(p.A, p.B, nullptr, p.C, nullptr, p.M, p.N, p.T, nullptr,
+                                           (first_m + wi % gsz) * BM, (wi / gsz) * BN, lds);
+}
+
 template <int BM, int BN, int EPI, typename P>
 int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, float* part,
            hipStream_t st) {
@@ -415,6 +528,43 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
     case 2: return dispatch<128, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
     default: return dispatch<128, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
   }
+}
+
+// Grouped TN GEMM: for i < n, C_i[M_i, N_i] (bf16) = A_i[T_i, M_i]^T B_i[T_i, N_i] (bf16, row-major, fp32
+// accumulation), all in ONE launch. cfg 0: 256 x 256 tiles, 1: 128 x 128 (M_i % BM == 0, N_i % BN == 0, T_i % 64
+// == 0, 16-byte aligned operands). n <= 64. Returns the number of tiles launched (>0) or a negative error.
+int mifx_gemm8_tn_grouped(int cfg, int n, const void* const* A, const void* const* B, void* const* C, const int* M,
+                          const int* N, const int* T, hipStream_t st) {
+  if (n <= 0 || n > MAXP || (cfg != 0 && cfg != 1)) return -1;
+  const int bm = cfg == 0 ? 256 : 128;
+  Group g{};
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    if (A[i] == nullptr || B[i] == nullptr || C[i] == nullptr || M[i] <= 0 || N[i] <= 0 || T[i] <= 0) return -1;
+    if (M[i] % bm || N[i] % bm || T[i] % BK) return -1;
+    if ((uintptr_t)A[i] % 16 || (uintptr_t)B[i] % 16 || (uintptr_t)C[i] % 8) return -1;
+    if ((long long)T[i] * M[i] >= (1ll << 31) || (long long)T[i] * N[i] >= (1ll << 31)) return -1;
+    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], (bf16*)C[i], M[i], N[i], T[i], 0};
+    g.first[i] = tiles;
+    tiles += (M[i] / bm) * (N[i] / bm);
+  }
+  g.first[n] = tiles;
+  g.n = n;
+  if (cfg == 0) {
+    constexpr int LDS = 2 * 2 * (128 + 128) * 128;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm8_tn_grouped<256, 256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL((gemm8_tn_grouped<256, 256>), dim3(tiles), dim3(NT), LDS, st, g);
+  } else {
+    constexpr int LDS = 2 * 2 * (64 + 64) * 128;
+    hipLaunchKernelGGL((gemm8_tn_grouped<128, 128>), dim3(tiles), dim3(NT), LDS, st, g);
+  }
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : tiles;
 }
 
 }  // extern "C"

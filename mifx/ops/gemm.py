@@ -230,9 +230,62 @@ def _dw_tensor(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return dy2.t() @ x2
 
 
-def _dw(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    """Weight gradient dY^T X: the hand-written TN kernel where it measured faster (TN_TUNED), else hipBLASLt; on a
+# Deferred weight gradients (`deferred_weight_grads()` context + `flush_weight_grads()`): nothing in a backward reads
+# a weight gradient, so each dW = dY^T X is only RECORDED during the backward (its operands kept alive, an empty
+# gradient tensor returned to autograd) and all of them run at the end as ONE grouped launch of the pipelined TN
+# kernel (csrc/gemm8.hip gemm8_tn_grouped): full 256 x 256 tiles over the whole token reduction, no split-K partials
+# and no second summing kernel, instead of one small launch per weight (BERT-base: 48 per step). The flush writes each
+# result into the weight's .grad -- whatever tensor autograd ended up storing there -- so the gradients must be reset
+# (None or zero) before the backward and each weight may receive ONE recorded product per flush.
+_DEFER: dict = {"on": False, "pending": []}
+
+
+class deferred_weight_grads:
+    def __enter__(self):
+        self.prev = _DEFER["on"]
+        _DEFER["on"] = True
+        return self
+
+    def __exit__(self, *exc):
+        _DEFER["on"] = self.prev
+        return False
+
+
+def _defer_ok(dy2: torch.Tensor, x2: torch.Tensor, w) -> bool:
+    if not (_DEFER["on"] and w is not None and dy2.is_cuda and dy2.dtype == torch.bfloat16
+            and x2.dtype == torch.bfloat16 and os.environ.get("MIFX_DEFER_DW", "1") != "0"):
+        return False
+    T, N = dy2.shape
+    K = x2.shape[1]
+    return N % 256 == 0 and K % 256 == 0 and T % 64 == 0 and len(_DEFER["pending"]) < 64
+
+
+def flush_weight_grads() -> int:
+    """Run every recorded weight gradient as one grouped launch into the weights' .grad; returns how many."""
+    pend, _DEFER["pending"] = _DEFER["pending"], []
+    if not pend:
+        return 0
+    seen = set()
+    for _, _, w in pend:
+        if id(w) in seen:
+            raise RuntimeError("deferred weight gradients: a weight received two products in one flush")
+        seen.add(id(w))
+        g = w.grad
+        if g is None or g.dtype != torch.bfloat16 or not g.is_contiguous() or g.shape != w.shape:
+            raise RuntimeError("deferred weight gradients: the weight's .grad is not the bf16 tensor the backward "
+                               "returned (was it accumulated or replaced?)")
+    gemm8_tn_grouped([(dy, x, w.grad) for dy, x, w in pend])
+    return len(pend)
+
+
+def _dw(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor | None = None) -> torch.Tensor:
+    """Weight gradient dY^T X: recorded for the grouped flush inside `deferred_weight_grads()` (w: the weight whose
+    .grad receives it); else the hand-written TN kernel where it measured faster (TN_TUNED), else hipBLASLt; on a
     side stream inside `async_weight_grads()`."""
+    if _defer_ok(dy2, x2, w):
+        native_stats.count("gemm_dW", True)
+        _DEFER["pending"].append((dy2.contiguous(), x2.contiguous(), w))
+        return torch.empty(dy2.shape[1], x2.shape[1], device=dy2.device, dtype=torch.bfloat16)
     if not (_ASYNC["on"] and dy2.is_cuda):
         return _dw_tensor(dy2, x2)
     dev = dy2.device
@@ -376,7 +429,7 @@ class _Linear(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype)
         dx = _dx(dy2, w, ctx.slot).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = _dw(dy2.contiguous(), x2) if ctx.needs_input_grad[1] else None
+        dw = _dw(dy2.contiguous(), x2, w) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             from .fused_bert import col_sum
@@ -411,7 +464,7 @@ class _LinearBiasGelu(torch.autograd.Function):
         check(fb_fns()["gelu"](_dt(z), _dt(bp), 0, ptr(dy2), ptr(z), ptr(bp), M, N, ptr(dz), ptr(part), ptr(db),
                                stream_handle(z.device)), "mifx_bert_bias_gelu")
         dx = _dx(dz, w, ctx.slot).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = _dw(dz, x2) if ctx.needs_input_grad[1] else None
+        dw = _dw(dz, x2, w) if ctx.needs_input_grad[1] else None
         return dx, dw, db if bp.dtype == ctx.bdtype else db.to(ctx.bdtype), None
 
 
@@ -523,7 +576,8 @@ def tn_eligible(a2: torch.Tensor, b2: torch.Tensor) -> bool:
 def _g8_fns():
     lib = _lib.load("gemm8")
     return {"configs": sig(lib, "mifx_gemm8_configs", [VP, I32]),
-            "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP])}
+            "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
+            "tn": sig(lib, "mifx_gemm8_tn_grouped", [I32, I32, VP, VP, VP, VP, VP, VP, VP])}
 
 
 @functools.lru_cache(maxsize=None)
@@ -547,6 +601,28 @@ def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
         if best_score is None or score > best_score:
             best, best_score = i, score
     return best
+
+
+def gemm8_tn_grouped(problems, cfg: int = 0) -> int:
+    """problems: [(a [T, M], b [T, N], c [M, N]), ...] bf16 CUDA tensors on one device -> c = a^T b for all of them
+    in ONE launch (csrc/gemm8.hip; cfg 0: 256 x 256 tiles, 1: 128 x 128). Returns the number of tiles."""
+    n = len(problems)
+    if n == 0:
+        return 0
+    for a, b, c in problems:
+        if not (a.is_contiguous() and b.is_contiguous() and c.is_contiguous()) or a.shape[0] != b.shape[0] or \
+                tuple(c.shape) != (a.shape[1], b.shape[1]) or c.dtype != torch.bfloat16:
+            raise ValueError("gemm8_tn_grouped: need contiguous a [T, M], b [T, N], bf16 c [M, N]")
+    A = (VP * n)(*[a.data_ptr() for a, _, _ in problems])
+    B = (VP * n)(*[b.data_ptr() for _, b, _ in problems])
+    C = (VP * n)(*[c.data_ptr() for _, _, c in problems])
+    Ms = (ctypes.c_int * n)(*[a.shape[1] for a, _, _ in problems])
+    Ns = (ctypes.c_int * n)(*[b.shape[1] for _, b, _ in problems])
+    Ts = (ctypes.c_int * n)(*[a.shape[0] for a, _, _ in problems])
+    rc = _g8_fns()["tn"](int(cfg), n, A, B, C, Ms, Ns, Ts, stream_handle(problems[0][0].device))
+    if rc <= 0:
+        raise RuntimeError(f"mifx_gemm8_tn_grouped failed ({rc})")
+    return rc
 
 
 def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0,
@@ -659,7 +735,7 @@ class _FFN(torch.autograd.Function):
     def backward(ctx, dout):
         x2, w1, b1, z, y1, w2 = ctx.saved_tensors
         dout2 = dout.reshape(-1, dout.shape[-1]).to(y1.dtype).contiguous()
-        dw2 = _dw(dout2, y1)
+        dw2 = _dw(dout2, y1, w2)
         M, K = dout2.shape
         N = w2.shape[1]
         cfg = GELU_BWD_TUNED.get((M, N, K))
@@ -677,7 +753,7 @@ class _FFN(torch.autograd.Function):
             db1 = torch.empty(N, device=z.device, dtype=bp.dtype)
             check(fb_fns()["gelu"](_dt(z), _dt(bp), 0, ptr(dh.to(z.dtype).contiguous()), ptr(z), ptr(bp), M, N,
                                    ptr(dz), ptr(part), ptr(db1), stream_handle(z.device)), "mifx_bert_bias_gelu")
-        dw1 = _dw(dz, x2)
+        dw1 = _dw(dz, x2, w1)
         dx = _dx(dz, w1, ctx.slot).view(*dout.shape[:-1], w1.shape[1]) if ctx.needs_input_grad[0] else None
         return dx, dw1, db1.to(b1.dtype), dw2, None
 

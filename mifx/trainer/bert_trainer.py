@@ -106,6 +106,9 @@ class BertTrainer:
         self.static_loss = None
         # MIFX_BERT_ASYNC_DW=1: weight gradients on a side stream (mifx.ops.gemm.async_weight_grads)
         self.async_dw = cuda and os.environ.get("MIFX_BERT_ASYNC_DW", "0") == "1"
+        # deferred weight gradients (mifx.ops.gemm.deferred_weight_grads; MIFX_DEFER_DW=0 turns it off): the flat
+        # optimizer resets every gradient to None each step, which the flush relies on
+        self.defer_dw = cuda and self.flat and not self.async_dw and os.environ.get("MIFX_DEFER_DW", "1") != "0"
 
     def set_batch(self, ids, tt, am, y) -> None:
         """Next training batch, copied INTO the step's input tensors (a captured hipGraph reads these same
@@ -145,6 +148,10 @@ class BertTrainer:
                 with hg.async_weight_grads():
                     loss.backward()
                 hg.join_weight_grads(self.device)
+            elif self.defer_dw:  # every weight gradient in ONE grouped launch after the backward
+                with hg.deferred_weight_grads():
+                    loss.backward()
+                hg.flush_weight_grads()
             else:
                 loss.backward()
         self.opt.step()

@@ -89,3 +89,58 @@ def test_gemm8_deterministic():
     a, _ = gemm.gemm8_nt(x, w, cfg=0)
     b, _ = gemm.gemm8_nt(x, w, cfg=0)
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1])
+def test_gemm8_tn_grouped_matches_fp32(cfg):
+    """One grouped launch of several TN products C_i = A_i^T B_i (token-major operands, different shapes and token
+    counts) against fp32 references; prologue / steady state / tail of the DMA schedule (T from 64 to 1024)."""
+    bm = 256 if cfg == 0 else 128
+    g = torch.Generator(device="cuda").manual_seed(11 + cfg)
+    shapes = [(bm, bm, 64), (3 * bm, bm, 128), (bm, 2 * bm, 1024), (2 * bm, 3 * bm, 320), (bm, bm, 192)]
+    probs, refs = [], []
+    for M, N, T in shapes:
+        a = (torch.rand(T, M, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand(T, N, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        probs.append((a, b, c))
+        refs.append(a.float().t() @ b.float())
+    tiles = gemm.gemm8_tn_grouped(probs, cfg=cfg)
+    assert tiles == sum((M // bm) * (N // bm) for M, N, _ in shapes)
+    for (_, _, c), ref in zip(probs, refs):
+        assert ((c.float() - ref).abs() <= 2 ** -8 * ref.abs() + 1e-2).all()
+
+
+@pytest.mark.gpu
+def test_deferred_weight_grads_equal_reference():
+    """hg.linear / hg.ffn inside deferred_weight_grads(): the backward records the weight gradients, one grouped
+    flush writes them into .grad; they match the fp32 reference products, input gradients are unchanged."""
+    torch.manual_seed(3)
+    T, H, F_ = 512, 256, 768
+    x = (torch.rand(T, H, device="cuda") * 2 - 1).to(torch.bfloat16).requires_grad_()
+    w1 = ((torch.rand(H, H, device="cuda") * 2 - 1) / 16).to(torch.bfloat16).requires_grad_()
+    wi = ((torch.rand(F_, H, device="cuda") * 2 - 1) / 16).to(torch.bfloat16).requires_grad_()
+    bi = torch.zeros(F_, device="cuda", dtype=torch.bfloat16).requires_grad_()
+    wo = ((torch.rand(H, F_, device="cuda") * 2 - 1) / 16).to(torch.bfloat16).requires_grad_()
+
+    def run(defer):
+        for t in (x, w1, wi, bi, wo):
+            t.grad = None
+        h = gemm.linear(x, w1, force=True)
+        y = gemm.ffn(h, wi, bi, wo)
+        gy = torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y).to(y.dtype)
+        if defer:
+            with gemm.deferred_weight_grads():
+                y.backward(gy)
+            assert gemm.flush_weight_grads() == 3
+        else:
+            y.backward(gy)
+        return [t.grad.clone() for t in (x, w1, wi, wo)]
+
+    ref = run(False)
+    got = run(True)
+    assert torch.equal(got[0], ref[0])  # the input gradient does not depend on the deferral
+    for g_, r_ in zip(got[1:], ref[1:]):
+        err = ((g_.float() - r_.float()).abs().max() / r_.float().abs().max()).item()
+        assert err < 1e-2, err

@@ -51,6 +51,9 @@ def main():
     cfgs = gemm.gemm8_configs()
     sel = [int(c) for c in a.cfg.split(",")] if a.cfg else range(len(cfgs))
     for group in a.shapes.split(","):
+        if group == "bertdw":  # a BERT-base step's 48 weight gradients: one grouped launch vs 48 TN launches
+            bert_dw()
+            continue
         for name, M, N, K in SHAPES[group]:
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
             w = ((torch.rand(N, K, device="cuda") * 2 - 1) * K ** -0.5).to(torch.bfloat16)
@@ -81,6 +84,39 @@ def main():
                                   "tflops": round(flop / us / 1e6, 1)}), flush=True)
             del x, w, ref
             torch.cuda.empty_cache()
+
+
+def bert_dw(layers: int = 12, T: int = 4096):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]  # (out, in): QKV, attention-out, FFN-in, FFN-out
+    probs = []
+    for _ in range(layers):
+        for o, i in shapes:
+            dy = (torch.rand(T, o, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+            x = (torch.rand(T, i, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+            probs.append((dy, x, torch.empty(o, i, device="cuda", dtype=torch.bfloat16)))
+    flop = sum(2.0 * T * o * i for o, i in shapes) * layers
+    us = timeit(lambda: gemm.gemm8_tn_grouped(probs, cfg=0), iters=20)
+    print(json.dumps({"gemm": "bert_dw_grouped", "problems": len(probs), "impl": "gemm8 tn grouped 256x256",
+                      "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}), flush=True)
+    us = timeit(lambda: gemm.gemm8_tn_grouped(probs, cfg=1), iters=20)
+    print(json.dumps({"gemm": "bert_dw_grouped", "problems": len(probs), "impl": "gemm8 tn grouped 128x128",
+                      "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}), flush=True)
+
+    def per_gemm(fn):
+        for dy, x, _ in probs:
+            fn(dy, x)
+    us = timeit(lambda: per_gemm(gemm._dw_tensor), iters=5)
+    print(json.dumps({"gemm": "bert_dw_grouped", "problems": len(probs), "impl": "48 x TN_TUNED path (gemm_tn)",
+                      "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}), flush=True)
+    us = timeit(lambda: per_gemm(lambda dy, x: dy.t() @ x), iters=5)
+    print(json.dumps({"gemm": "bert_dw_grouped", "problems": len(probs), "impl": "48 x hipblaslt dy.t() @ x",
+                      "us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}), flush=True)
+    # numerics of one problem of each shape
+    for dy, x, c in probs[:4]:
+        ref = dy.float().t() @ x.float()
+        err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
+        print(json.dumps({"gemm": "bert_dw_check", "shape": list(c.shape), "max_rel_err": err}), flush=True)
 
 
 if __name__ == "__main__":
