@@ -235,6 +235,86 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_fwd(const float* __restr
   }
 }
 
+// Finalize from per-TILE statistics produced by the GEMM that wrote x (csrc/gemm8.hip EPI_STATS / EPI_ADD_STATS: the
+// BatchNorm statistics of a 1x1 convolution's output folded into its epilogue, so no statistics pass re-reads x):
+// pmean / pm2 [T][C] = each tile's column mean and sum of squared deviations over its rows (nt rows each, M = T nt).
+// Two launches: (1) grid (C / 64, G), 1024 threads = 64 channels x 16 tile slices: each thread combines its slice of
+// equal-count tiles in fp64 (mean of the means, then M2 = sum M2_t + nt sum (mean_t - mean_s)^2), thread 0 of each
+// channel merges the 16 slices by Chan's formula into ws[g] = (count, mean, M2); (2) one thread per channel merges the
+// G group results (Chan) and writes the same outputs as bn_finalize_fwd ([mean, rstd, scale, shift], running stats).
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& M2, double nk, double mk, double m2k) {
+  if (nk <= 0.0) return;
+  const double delta = mk - mean, nn = n + nk;
+  mean += delta * nk / nn;
+  M2 += m2k + delta * delta * n * nk / nn;
+  n = nn;
+}
+
+__global__ __launch_bounds__(1024) void bn_tiles_partial(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                        int T, int nt, int C, double* __restrict__ ws) {
+  __shared__ double sm[16][64], sq[16][64];
+  __shared__ int sk[16];
+  const int G = gridDim.y, g = blockIdx.y;
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const int gb = (int)((long long)T * g / G), ge = (int)((long long)T * (g + 1) / G);
+  const int t0 = gb + (int)((long long)(ge - gb) * sl / 16), t1 = gb + (int)((long long)(ge - gb) * (sl + 1) / 16);
+  double mu = 0.0, m2 = 0.0;
+  if (c < C && t1 > t0) {
+    double s = 0.0;
+    for (int t = t0; t < t1; ++t) s += (double)pmean[(size_t)t * C + c];
+    mu = s / (double)(t1 - t0);
+    double d2 = 0.0;
+    for (int t = t0; t < t1; ++t) {
+      const double d = (double)pmean[(size_t)t * C + c] - mu;
+      m2 += (double)pm2[(size_t)t * C + c];
+      d2 += d * d;
+    }
+    m2 += (double)nt * d2;
+  }
+  sm[sl][cl] = mu;
+  sq[sl][cl] = m2;
+  if (cl == 0) sk[sl] = t1 - t0;
+  __syncthreads();
+  if (sl != 0 || c >= C) return;
+  double n = 0.0, mean = 0.0, M2 = 0.0;
+  for (int k = 0; k < 16; ++k) chan_merge(n, mean, M2, (double)sk[k] * nt, sm[k][cl], sq[k][cl]);
+  double* o = ws + ((size_t)g * C + c) * 3;
+  o[0] = n;
+  o[1] = mean;
+  o[2] = M2;
+}
+
+__global__ __launch_bounds__(256) void bn_tiles_final(const double* __restrict__ ws, int G, int C,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     float eps, float momentum, float* __restrict__ run_mean,
+                                                     float* __restrict__ run_var, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, float* __restrict__ scale,
+                                                     float* __restrict__ shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double n = 0.0, mean = 0.0, M2 = 0.0;
+  for (int g = 0; g < G; ++g) {
+    const double* o = ws + ((size_t)g * C + c) * 3;
+    chan_merge(n, mean, M2, o[0], o[1], o[2]);
+  }
+  double var = M2 / n;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rstd;
+  const float sc = w[c] * rstd;
+  scale[c] = sc;
+  shift[c] = b[c] - (float)mean * sc;
+  if (run_mean != nullptr) {
+    const double unbiased = n > 1 ? M2 / (n - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+  }
+}
+
+// groups of tiles of the first finalize launch: ~12 tiles per thread (16 slices per group)
+int tile_groups(int T) { return T / 192 < 1 ? 1 : (T / 192 > 32 ? 32 : T / 192); }
+
 // y = relu(x * scale + shift) (relu optional). Same [row slice x channel group] layout as the
 // reductions: a thread keeps its 8 channels' scale/shift in registers across all its rows.
 // x2 != null (inference over a residual sum): s = x + x2 rounded to T is written to s_out and normalised, as the
@@ -450,6 +530,30 @@ int mifx_bn_relu_fwd(int dtype, const void* x, const void* x2, void* sum_out, lo
     hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)xa,
                        (const float*)nullptr, (float*)nullptr, M, C,
                        stats + 2 * C, stats + 3 * C, relu, (float*)y);
+  return (int)hipGetLastError();
+}
+
+// Training forward from per-tile statistics (see bn_tiles_partial): part = [2][T][C] (tile means, tile M2), nt rows
+// per tile, x [M = T nt, C]; ws = fp64 scratch of mifx_bn_tiles_ws(T, C) doubles; writes stats = [mean, rstd, scale,
+// shift] and y = relu(x * scale + shift).
+int mifx_bn_tiles_ws(int T, int C) { return tile_groups(T) * C * 3; }
+
+int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const float* part, int T, int nt,
+                           const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
+                           int relu, float* stats, double* ws, void* y, hipStream_t st) {
+  if (!shape_ok(M, C) || T <= 0 || nt <= 0 || (long long)T * nt != M || part == nullptr || ws == nullptr) return -1;
+  const int G = tile_groups(T);
+  hipLaunchKernelGGL(bn_tiles_partial, dim3((C + 63) / 64, G), dim3(1024), 0, st, part, part + (size_t)T * C, T, nt, C,
+                     ws);
+  hipLaunchKernelGGL(bn_tiles_final, dim3((C + 255) / 256), dim3(256), 0, st, ws, G, C, w, b, eps, momentum, run_mean,
+                     run_var, stats, stats + C, stats + 2 * C, stats + 3 * C);
+  if (dtype)
+    hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)x, (const __hip_bfloat16*)nullptr, (__hip_bfloat16*)nullptr, M, C,
+                       stats + 2 * C, stats + 3 * C, relu, (__hip_bfloat16*)y);
+  else
+    hipLaunchKernelGGL(bn_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)x,
+                       (const float*)nullptr, (float*)nullptr, M, C, stats + 2 * C, stats + 3 * C, relu, (float*)y);
   return (int)hipGetLastError();
 }
 

@@ -58,7 +58,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int BK = 64;
 constexpr int NT = 512;
 
-enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3, EPI_GELU_BWD = 4, EPI_STATS = 5 };
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3, EPI_GELU_BWD = 4, EPI_STATS = 5,
+           EPI_ADD_STATS = 6, EPI_F32 = 7 };
 
 __device__ __forceinline__ float erf_fast(float x) {  // Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, branch-free
   const float ax = fabsf(x);
@@ -94,16 +95,26 @@ __device__ __forceinline__ v8bf tr_frag(const unsigned char* p1, const unsigned 
 
 // grouped TN problems: C[M, N] (bf16, ldc N) = A[T, M]^T B[T, N]; tiles of problem i are [first[i], first[i + 1])
 constexpr int MAXP = 64;
+// Problem i: C_i[M, N] = A_i[T, M]^T B_i[T, N]. bf16 problems (F32 clear): C bf16, one token split, staged bf16
+// stores. fp32 problems (F32 set): the token range is cut into S chunks of `chunk` rows (the last shorter), each
+// (tile, chunk) item stores its fp32 partial into P[s][M][N]; gemm8_tn_reduce then ADDS sum_s P[s] (fixed order) into
+// the fp32 destination C -- the weight gradients of convolutions, whose token count (N H W = 12k-800k rows) is far
+// longer than their output is wide. TILE128: 128 x 128 tiles for this problem (dimensions % 256 != 0).
+constexpr int F32 = 1, TILE128 = 2, ACCUM = 4;  // ACCUM: C += sum of the partials (else C = the sum)
 struct Prob {
   const bf16* A;
   const bf16* B;
-  bf16* C;
-  int M, N, T, pad;
+  void* C;
+  float* P;
+  int M, N, T, chunk, S, flags;
 };
 struct Group {
   Prob p[MAXP];
-  int first[MAXP + 1];
+  int first[MAXP + 1];  // first work item (tile x chunk) of each problem
   int n;
+  int n_big;  // workgroups [0, n_big) run items [0, n_big); the rest run the (BM/2) x (BN/2) quadrants of items
+              // [n_big, first[n]) -- a last partial wave of quarter-size tiles instead of full ones (bf16 groups of
+              // uniform 256 x 256 tiles only)
 };
 
 // s_waitcnt immediate (gfx9 encoding): vmcnt = n, expcnt / lgkmcnt not waited on
@@ -302,120 +313,205 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   if (wm == 0) barrier();  // equal barrier counts for both groups
 
   // ---- epilogue: acc[mq][nq][a][b][r] = Y[m0 + mq HA + wm HA/2 + 16 b + fr][n0 + nq HB + wn HB/4 + 16 a + 4 fc + r]
-  if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_STATS) {
-    // per-tile column sums of the stored values (GELU_BWD: dZ; STATS: y and y^2), over the rows of the 16-lane
-    // groups (xor tree), then over the two wave rows in order (LDS), written to part[m0 / BM][...]
-    constexpr int NS = EPI == EPI_STATS ? 2 : 1;
-    float cs[NS][2][NF][4];
+  if constexpr (EPI == EPI_GELU_BWD) {
+    // per-tile column sums of the stored dZ, over the rows of the 16-lane groups (xor tree), then over the two
+    // wave rows in order (LDS), written to part[m0 / BM][...]
+    float cs[2][NF][4];
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
       for (int a = 0; a < NF; ++a) {
         const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_GELU_BWD) {
+        float bv[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n + r];
+        for (int r = 0; r < 4; ++r) {
+          bv[r] = (float)bias[n + r];
+          cs[nq][a][r] = 0.f;
         }
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cs[s][nq][a][r] = 0.f;
 #pragma unroll
         for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
           for (int b = 0; b < MF; ++b) {
             const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            const v4bf zv = *(const v4bf*)(Z + (size_t)m * N + n);
             v4bf o;
-            if constexpr (EPI == EPI_GELU_BWD) {
-              const v4bf zv = *(const v4bf*)(Z + (size_t)m * N + n);
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                o[r] = (bf16)(acc[mq][nq][a][b][r] * gelu_grad_f((float)zv[r] + bv[r]));
-                cs[0][nq][a][r] += (float)o[r];
-              }
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                o[r] = (bf16)acc[mq][nq][a][b][r];
-                const float v = (float)o[r];
-                cs[0][nq][a][r] += v;
-                cs[NS - 1][nq][a][r] += v * v;
-              }
+            for (int r = 0; r < 4; ++r) {
+              o[r] = (bf16)(acc[mq][nq][a][b][r] * gelu_grad_f((float)zv[r] + bv[r]));
+              cs[nq][a][r] += (float)o[r];
             }
             *(v4bf*)(Y + (size_t)m * N + n) = o;
           }
       }
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int a = 0; a < NF; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = cs[nq][a][r];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          cs[nq][a][r] = v;
+        }
+    __syncthreads();  // all DMAs retired (vmcnt(0) in the tail) and every fragment read done: LDS reusable
+    float* red = (float*)lds;  // [2 wave rows][BN]
+    if (fr == 0) {
 #pragma unroll
       for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
         for (int a = 0; a < NF; ++a)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = cs[s][nq][a][r];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            cs[s][nq][a][r] = v;
-          }
-    __syncthreads();  // all DMAs retired (vmcnt(0) in the tail) and every fragment read done: LDS reusable
-    float* red = (float*)lds;  // [NS][2 wave rows][BN]
-    if (fr == 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-          for (int a = 0; a < NF; ++a)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              red[(s * 2 + wm) * BN + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc + r] = cs[s][nq][a][r];
+          for (int r = 0; r < 4; ++r) red[wm * BN + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc + r] = cs[nq][a][r];
     }
     __syncthreads();
-    for (int c = tid; c < NS * BN; c += NT) {
-      const int s = c / BN, col = c % BN;
-      part[((size_t)s * (M / BM) + m0 / BM) * N + n0 + col] = red[(s * 2) * BN + col] + red[(s * 2 + 1) * BN + col];
-    }
+    for (int c = tid; c < BN; c += NT) part[(size_t)(m0 / BM) * N + n0 + c] = red[c] + red[BN + c];
     return;
   }
+  if constexpr (EPI == EPI_F32) {  // fp32 partial tile into part[M][N] (16-byte stores: 4 consecutive columns)
 #pragma unroll
-  for (int nq = 0; nq < 2; ++nq)
+    for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
-    for (int a = 0; a < NF; ++a) {
-      const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+      for (int a = 0; a < NF; ++a) {
+        const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int b = 0; b < MF; ++b) {
+            const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            *(v4f*)(part + (size_t)m * N + n) = acc[mq][nq][a][b];
+          }
+      }
+    return;
+  }
+  if constexpr (EPI == EPI_BIAS_GELU) {  // two outputs (Y and the pre-bias Z): direct 8-byte stores
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int a = 0; a < NF; ++a) {
+        const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+        float bv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n + r];
-      }
 #pragma unroll
-      for (int mq = 0; mq < 2; ++mq)
+        for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
-        for (int b = 0; b < MF; ++b) {
-          const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
-          v4bf o;
-          if constexpr (EPI == EPI_BIAS_GELU) {
-            v4bf z;
+          for (int b = 0; b < MF; ++b) {
+            const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            v4bf o, z;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               z[r] = (bf16)acc[mq][nq][a][b][r];
               o[r] = (bf16)gelu_f((float)z[r] + bv[r]);
             }
             *(v4bf*)(Z + (size_t)m * N + n) = z;
-          } else if constexpr (EPI == EPI_ADD_R) {
-            const v4bf rv = *(const v4bf*)((const bf16*)bias + (size_t)m * N + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mq][nq][a][b][r] + (float)rv[r]);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mq][nq][a][b][r] + bv[r]);
+            *(v4bf*)(Y + (size_t)m * N + n) = o;
           }
-          *(v4bf*)(Y + (size_t)m * N + n) = o;
+      }
+    return;
+  }
+  // Staged epilogue (none / bias / + R / statistics): the bf16 tile goes through LDS so that every global store and
+  // every R load is a whole 16-byte chunk of a row, consecutive lanes along the row (the fragment layout stores 8
+  // bytes per lane, 16 rows apart -- half-line writes that made small-K products output-bound). Chunk c of tile row r
+  // sits at physical chunk c ^ (r & (CPR_O - 1)): the 16 rows a fragment store writes land on 16 distinct 16-byte
+  // slots (conflict-free), and row reads stay conflict-free.
+  constexpr int CPR_O = BN / 8;  // 16-byte chunks per tile row
+  constexpr int RPI = NT / CPR_O;  // tile rows per store iteration
+  constexpr bool STATS = EPI == EPI_STATS || EPI == EPI_ADD_STATS;
+  constexpr bool ADD = EPI == EPI_ADD_R || EPI == EPI_ADD_STATS;
+  auto tslot = [&](int row, int c) -> unsigned char* {
+    return lds + (size_t)row * (BN * 2) + ((c ^ (row & (CPR_O - 1))) << 4);
+  };
+#pragma unroll
+  for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+    for (int a = 0; a < NF; ++a) {
+      const int col = nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n0 + col + r];
+      }
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int b = 0; b < MF; ++b) {
+          const int row = mq * HA + wm * (HA / 2) + 16 * b + fr;
+          v4bf o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mq][nq][a][b][r] + bv[r]);
+          *(v4bf*)(tslot(row, col >> 3) + ((col >> 2) & 1) * 8) = o;
         }
     }
+  __syncthreads();
+  const int cc = tid % CPR_O, rr0 = tid / CPR_O;
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+#pragma unroll 4
+  for (int i = 0; i < BM / RPI; ++i) {
+    const int row = rr0 + i * RPI;
+    v8bf v = *(const v8bf*)tslot(row, cc);
+    const size_t g = (size_t)(m0 + row) * N + n0 + 8 * cc;
+    if constexpr (ADD) {  // Y = X W^T + R, one rounding of the fp32-exact sum of two bf16 values
+      const v8bf rv = *(const v8bf*)((const bf16*)bias + g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[e]);
+      if constexpr (STATS) *(v8bf*)tslot(row, cc) = v;  // the stored sum, re-read by the second statistics pass
+    }
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
+    }
+    *(v8bf*)(Y + g) = v;
+  }
+  if constexpr (STATS) {
+    // per-tile BatchNorm statistics of the STORED values, two-pass (mean, then the sum of squared deviations from
+    // it): part[0][m0 / BM][n] = tile mean, part[1][m0 / BM][n] = M2 = sum (y - mean)^2 over the BM rows; combined
+    // across tiles by Chan's formula in fp64 (mifx_bn_relu_fwd_tiles), so no E[y^2] - E[y]^2 cancellation
+    float* red = (float*)(lds + (size_t)BM * BN * 2);  // [8 waves][BN]
+    float* meanv = red + 8 * BN;                       // [BN]
+    auto reduce_cols = [&](float (&v)[8], float* outc, float scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (CPR_O <= 16) v[e] += __shfl_xor(v[e], 16);
+        v[e] += __shfl_xor(v[e], 32);
+      }
+      if (lane < CPR_O) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[w * BN + 8 * lane + e] = v[e];
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += red[k * BN + c];
+        outc[c] = t * scale;
+      }
+      __syncthreads();
+    };
+    reduce_cols(cs, meanv, 1.f / BM);
+    float mu[8], m2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = meanv[8 * cc + e];
+      m2[e] = 0.f;
+    }
+#pragma unroll 4
+    for (int i = 0; i < BM / RPI; ++i) {
+      const v8bf v = *(const v8bf*)tslot(rr0 + i * RPI, cc);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (float)v[e] - mu[e];
+        m2[e] += d * d;
+      }
+    }
+    for (int c = tid; c < BN; c += NT) part[(size_t)(m0 / BM) * N + n0 + c] = meanv[c];
+    reduce_cols(m2, meanv, 1.f);  // (every thread has read its means: the barrier inside precedes the overwrite)
+    for (int c = tid; c < BN; c += NT) part[((size_t)(M / BM) + m0 / BM) * N + n0 + c] = meanv[c];
+  }
 }
 
 __device__ __forceinline__ int xcd_tile() {  // bijective XCD-aware remap of blockIdx.x (guide section 5)
@@ -433,30 +529,92 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
   gemm8_tile<BM, BN, EPI, P, false>(X, W, bias, Y, Z, M, N, K, part, (tile / nb_n) * BM, (tile % nb_n) * BN, lds);
 }
 
-// grouped TN: each workgroup's (problem, tile) from the table; tiles of a problem run m-fastest in groups of 4
-// m-blocks (an XCD's consecutive tiles share B column strips in its L2)
-template <int BM, int BN>
+// grouped TN: each workgroup's (problem, item) from the table by binary search; an item is (tile, token chunk); tiles
+// of a problem run m-fastest in groups of 4 m-blocks (an XCD's consecutive tiles share B column strips in its L2)
+template <int BM, int BN, bool TN>
+__device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, unsigned char* lds) {
+  constexpr int GM = 4;
+  const int bm = (p.flags & TILE128) ? BM / 2 : BM, bn = (p.flags & TILE128) ? BN / 2 : BN;
+  const int nb_m = p.M / bm, nb_n = p.N / bn, tiles = nb_m * nb_n;
+  const int sp = item / tiles, t = item - sp * tiles;
+  const int per_group = GM * nb_n, grp = t / per_group, first_m = grp * GM, gsz = min(GM, nb_m - first_m);
+  const int wi = t - grp * per_group;
+  const int m0 = (first_m + wi % gsz) * bm, n0 = (wi / gsz) * bn;
+  const int t0 = sp * p.chunk, len = min(p.chunk, p.T - t0);
+  const bf16* A = p.A + (size_t)t0 * p.M;
+  const bf16* B = p.B + (size_t)t0 * p.N;
+  if (p.flags & F32) {
+    float* P = p.P + (size_t)sp * p.M * p.N;
+    if (p.flags & TILE128)
+      gemm8_tile<BM / 2, BN / 2, EPI_F32, bf16, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds);
+    else
+      gemm8_tile<BM, BN, EPI_F32, bf16, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds);
+    return;
+  }
+  bf16* C = (bf16*)p.C;
+  if (quad >= 0 || (p.flags & TILE128)) {
+    const int mq = quad >= 0 ? m0 + (quad >> 1) * (BM / 2) : m0, nq = quad >= 0 ? n0 + (quad & 1) * (BN / 2) : n0;
+    gemm8_tile<BM / 2, BN / 2, EPI_NONE, bf16, true>(A, B, nullptr, C, nullptr, p.M, p.N, len, nullptr, mq, nq, lds);
+    return;
+  }
+  gemm8_tile<BM, BN, EPI_NONE, bf16, true>(A, B, nullptr, C, nullptr, p.M, p.N, len, nullptr, m0, n0, lds);
+}
+
 __global__ __launch_bounds__(NT, 1) void gemm8_tn_grouped(const Group g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int tile = xcd_tile();
-  int lo = 0, hi = g.n - 1;  // largest i with first[i] <= tile
+  int item, quad = -1;
+  if ((int)blockIdx.x < g.n_big) {  // bijective XCD-aware remap over the full-size items
+    const int nwg = g.n_big, bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    item = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  } else {
+    const int sidx = blockIdx.x - g.n_big;
+    item = g.n_big + sidx / 4;
+    quad = sidx % 4;
+  }
+  int lo = 0, hi = g.n - 1;  // largest i with first[i] <= item
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (g.first[mid] <= tile) lo = mid; else hi = mid - 1;
+    if (g.first[mid] <= item) lo = mid; else hi = mid - 1;
   }
-  const Prob& p = g.p[lo];
-  const int t = tile - g.first[lo];
-  constexpr int GM = 4;
-  const int nb_m = p.M / BM, nb_n = p.N / BN, per_group = GM * nb_n;
-  const int grp = t / per_group, first_m = grp * GM, gsz = min(GM, nb_m - first_m), wi = t - grp * per_group;
-  gemm8_tile<BM, BN, EPI_NONE, bf16, true>(p.A, p.B, nullptr, p.C, nullptr, p.M, p.N, p.T, nullptr,
-                                           (first_m + wi % gsz) * BM, (wi / gsz) * BN, lds);
+  grouped_item<256, 256, true>(g.p[lo], item - g.first[lo], quad, lds);
+}
+
+// C_i[M, N] (fp32) += sum over s of P_i[s][M][N], s in order; one thread per 4 elements, problems back to back
+struct RedProb {
+  const float* P;
+  float* C;
+  long long n4, first4;  // float4 count, first global float4 index
+  int S, accum;
+};
+struct RedGroup {
+  RedProb p[MAXP];
+  int n;
+};
+__global__ __launch_bounds__(256) void gemm8_tn_reduce(const RedGroup g, long long total4) {
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= total4) return;
+  int i = 0;
+  while (i + 1 < g.n && g.p[i + 1].first4 <= q) ++i;
+  const RedProb& r = g.p[i];
+  const long long k = q - r.first4;
+  v4f acc = ((const v4f*)r.P)[k];
+  for (int s = 1; s < r.S; ++s) acc += ((const v4f*)r.P)[(size_t)s * r.n4 + k];
+  if (r.accum) acc += ((v4f*)r.C)[k];
+  ((v4f*)r.C)[k] = acc;
+}
+
+// dynamic LDS: the main loop's two K-tile buffers, or the staged epilogue's bf16 tile (+ statistics scratch)
+template <int BM, int BN, int EPI>
+constexpr int lds_bytes() {
+  const int loop = 2 * 2 * (BM / 2 + BN / 2) * 128;
+  const int epi = BM * BN * 2 + ((EPI == EPI_STATS || EPI == EPI_ADD_STATS) ? 9 * BN * 4 : 0);
+  return loop > epi ? loop : epi;
 }
 
 template <int BM, int BN, int EPI, typename P>
 int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, float* part,
            hipStream_t st) {
-  constexpr int LDS = 2 * 2 * (BM / 2 + BN / 2) * 128;
+  constexpr int LDS = lds_bytes<BM, BN, EPI>();
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm8_nt<BM, BN, EPI, P>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -483,6 +641,7 @@ int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bi
       return bias_f32 ? launch<BM, BN, EPI_GELU_BWD, float>(X, W, bias, Y, Z, M, N, K, part, st)
                       : launch<BM, BN, EPI_GELU_BWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
     case EPI_STATS: return launch<BM, BN, EPI_STATS, bf16>(X, W, nullptr, Y, nullptr, M, N, K, part, st);
+    case EPI_ADD_STATS: return launch<BM, BN, EPI_ADD_STATS, bf16>(X, W, bias, Y, nullptr, M, N, K, part, st);
   }
   return -1;
 }
@@ -507,7 +666,8 @@ int mifx_gemm8_configs(int* out, int n) {
 
 // Y[M, N] = X[M, K] . W[N, K]^T, bf16 in / out, fp32 accumulation. epi: 0 none; 1 + bias[N]; 2 GELU(. + bias) with
 // Z = bf16(X W^T) (pre-bias); 3 + R (bias = bf16 [M, N]); 4 dZ = (X W^T) o GELU'(Z + bias) with part[M / BM][N] the
-// per-tile column sums of dZ; 5 part[2][M / BM][N] = per-tile column sum / sum of squares of the stored Y.
+// per-tile column sums of dZ; 5 part[2][M / BM][N] = per-tile column mean / sum of squared deviations (M2) of the
+// stored Y; 6 = 3 and 5: Y = X W^T + R with the statistics of the stored sum.
 // bias bf16 or fp32 (bias_f32). M % BM == 0, N % BN == 0, K % 64 == 0, 16-byte aligned operands.
 int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z,
                   float* part, int M, int N, int K, hipStream_t st) {
@@ -515,12 +675,14 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
   if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || X == nullptr || W == nullptr || Y == nullptr) return -1;
   const Cfg c = kCfgs[cfg];
   if (M % c.bm || N % c.bn || K % BK) return -1;
-  if (epi < 0 || epi > 5) return -1;
-  if ((epi == 1 || epi == 2 || epi == 3 || epi == 4) && bias == nullptr) return -1;
+  if (epi < 0 || epi > 6) return -1;
+  if ((epi >= 1 && epi <= 4) || epi == 6) {
+    if (bias == nullptr) return -1;
+  }
   if ((epi == 2 || epi == 4) && Z == nullptr) return -1;
-  if ((epi == 4 || epi == 5) && part == nullptr) return -1;
-  if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 8 || (Z != nullptr && (uintptr_t)Z % 8)) return -1;
-  if (epi == 3 && (uintptr_t)bias % 8) return -1;
+  if (epi >= 4 && part == nullptr) return -1;
+  if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 16 || (Z != nullptr && (uintptr_t)Z % 8)) return -1;
+  if ((epi == 3 || epi == 6) && (uintptr_t)bias % 16) return -1;
   if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;  // 32-bit element offsets
   switch (cfg) {
     case 0: return dispatch<256, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
@@ -530,41 +692,63 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
   }
 }
 
-// Grouped TN GEMM: for i < n, C_i[M_i, N_i] (bf16) = A_i[T_i, M_i]^T B_i[T_i, N_i] (bf16, row-major, fp32
-// accumulation), all in ONE launch. cfg 0: 256 x 256 tiles, 1: 128 x 128 (M_i % BM == 0, N_i % BN == 0, T_i % 64
-// == 0, 16-byte aligned operands). n <= 64. Returns the number of tiles launched (>0) or a negative error.
-int mifx_gemm8_tn_grouped(int cfg, int n, const void* const* A, const void* const* B, void* const* C, const int* M,
-                          const int* N, const int* T, hipStream_t st) {
-  if (n <= 0 || n > MAXP || (cfg != 0 && cfg != 1)) return -1;
-  const int bm = cfg == 0 ? 256 : 128;
+// Grouped TN GEMM: for i < n, C_i[M_i, N_i] = A_i[T_i, M_i]^T B_i[T_i, N_i] (bf16 row-major operands, fp32
+// accumulation), all in ONE launch. flags_i: bit 0 F32 -- C_i is fp32 and receives the product (+= with bit 2 ACCUM,
+// else =), computed in
+// token chunks of chunk_i rows (fp32 partials in ws, summed in order by a second launch); bit 1 TILE128 -- 128 x 128
+// tiles (M_i, N_i % 128) instead of 256 x 256 (% 256). bf16 problems need chunk_i = T_i. T_i % 64 == 0, chunk_i % 64
+// == 0, 16-byte aligned operands, n <= 64. ws: fp32 workspace of sum over F32 problems of S_i M_i N_i floats
+// (S_i = ceil(T_i / chunk_i)), may be null without F32 problems. Returns the number of work items (> 0) or < 0.
+int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, void* const* C, const int* M,
+                          const int* N, const int* T, const int* chunk, const int* flags, float* ws, hipStream_t st) {
+  if (n <= 0 || n > MAXP) return -1;
   Group g{};
-  int tiles = 0;
+  RedGroup rg{};
+  int items = 0, nred = 0;
+  bool uniform256 = true;
+  long long woff = 0, r4 = 0;
   for (int i = 0; i < n; ++i) {
+    const int fl = flags[i], tb = (fl & TILE128) ? 128 : 256;
     if (A[i] == nullptr || B[i] == nullptr || C[i] == nullptr || M[i] <= 0 || N[i] <= 0 || T[i] <= 0) return -1;
-    if (M[i] % bm || N[i] % bm || T[i] % BK) return -1;
-    if ((uintptr_t)A[i] % 16 || (uintptr_t)B[i] % 16 || (uintptr_t)C[i] % 8) return -1;
+    if (M[i] % tb || N[i] % tb || T[i] % BK || chunk[i] <= 0 || chunk[i] % BK) return -1;
+    if (!(fl & F32) && chunk[i] != T[i]) return -1;
+    if ((uintptr_t)A[i] % 16 || (uintptr_t)B[i] % 16 || (uintptr_t)C[i] % 16) return -1;
     if ((long long)T[i] * M[i] >= (1ll << 31) || (long long)T[i] * N[i] >= (1ll << 31)) return -1;
-    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], (bf16*)C[i], M[i], N[i], T[i], 0};
-    g.first[i] = tiles;
-    tiles += (M[i] / bm) * (N[i] / bm);
-  }
-  g.first[n] = tiles;
-  g.n = n;
-  if (cfg == 0) {
-    constexpr int LDS = 2 * 2 * (128 + 128) * 128;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm8_tn_grouped<256, 256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LDS);
-      attr = true;
+    const int S = (T[i] + chunk[i] - 1) / chunk[i];
+    float* P = nullptr;
+    if (fl & F32) {
+      if (ws == nullptr) return -1;
+      P = ws + woff;
+      const long long n4 = (long long)M[i] * N[i] / 4;
+      rg.p[nred++] = RedProb{P, (float*)C[i], n4, r4, S, (fl & ACCUM) ? 1 : 0};
+      r4 += n4;
+      woff += (long long)S * M[i] * N[i];
+      uniform256 = false;
     }
-    hipLaunchKernelGGL((gemm8_tn_grouped<256, 256>), dim3(tiles), dim3(NT), LDS, st, g);
-  } else {
-    constexpr int LDS = 2 * 2 * (64 + 64) * 128;
-    hipLaunchKernelGGL((gemm8_tn_grouped<128, 128>), dim3(tiles), dim3(NT), LDS, st, g);
+    if (fl & TILE128) uniform256 = false;
+    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], C[i], P, M[i], N[i], T[i], chunk[i], S, fl};
+    g.first[i] = items;
+    items += (M[i] / tb) * (N[i] / tb) * S;
+  }
+  g.first[n] = items;
+  g.n = n;
+  // a last partial wave of at most a quarter of the chip runs as quarter-size tiles (4x the workgroups, 1/4 the time)
+  const int cus = 256, rem = items % cus;
+  g.n_big = (uniform256 && items > cus && rem > 0 && rem <= cus / 4) ? items - rem : items;
+  const int grid = g.n_big + 4 * (items - g.n_big);
+  constexpr int LDS = lds_bytes<256, 256, EPI_NONE>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8_tn_grouped, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(gemm8_tn_grouped, dim3(grid), dim3(NT), LDS, st, g);
+  if (nred) {
+    rg.n = nred;
+    hipLaunchKernelGGL(gemm8_tn_reduce, dim3((unsigned)((r4 + 255) / 256)), dim3(256), 0, st, rg, r4);
   }
   const int rc = (int)hipGetLastError();
-  return rc ? -rc : tiles;
+  return rc ? -rc : items;
 }
 
 }  // extern "C"

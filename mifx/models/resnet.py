@@ -72,6 +72,29 @@ def _conv(*a, **kw):
     return (HipConv2d if USE_HIP_CONV else nn.Conv2d)(*a, **kw)
 
 
+# Stride-1 1x1 convolutions as GEMMs on csrc/gemm8.hip with the BatchNorm statistics -- and for conv3 the residual
+# add -- in the epilogue (mifx.ops.conv1x1): conv1 -> BN1 needs no statistics pass; conv3 + shortcut is written ALREADY
+# SUMMED with the per-tile statistics of the sum, which the next block's BN0 only finalizes and applies.
+# MIFX_RESNET_FUSED_1X1=0 keeps every convolution on the routed MIOpen / gconv path.
+FUSED_1X1 = os.environ.get("MIFX_RESNET_FUSED_1X1", "1") != "0"
+
+
+class Fused:
+    """A block output already summed with its shortcut, with the per-tile BatchNorm statistics of the sum."""
+
+    __slots__ = ("t", "part")
+
+    def __init__(self, t, part):
+        self.t, self.part = t, part
+
+
+def _fused_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    from ..ops import conv1x1
+
+    return FUSED_1X1 and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.bias is None \
+        and conv.groups == 1 and conv1x1.eligible(x, conv.weight)
+
+
 class PreActBottleneck(nn.Module):
     expansion = 4
 
@@ -87,18 +110,33 @@ class PreActBottleneck(nn.Module):
         self.conv3 = _conv(width, cout, 1, bias=False)
 
     def forward(self, x):
-        """x: a tensor, or the (branch, shortcut) pair of the previous block whose sum is this block's
-        input -- the residual add then happens inside bn0's fused kernels (fwd and bwd). Returns the
-        un-added (branch, shortcut) pair for the next block / the final BN."""
-        if isinstance(x, tuple):
+        """x: a tensor, the (branch, shortcut) pair of the previous block whose sum is this block's input -- the
+        residual add then happens inside bn0's fused kernels (fwd and bwd) -- or a `Fused` sum whose statistics the
+        producing GEMM already reduced. Returns the un-added (branch, shortcut) pair, or a `Fused` sum when conv3 ran
+        on the GEMM kernel, for the next block / the final BN."""
+        from ..ops.conv1x1 import conv1x1
+
+        if isinstance(x, Fused):
+            pre, s = self.bn0.forward_tiles(x.t, x.part)
+        elif isinstance(x, tuple):
             pre, s = self.bn0.forward_add(*x)
         else:
             pre, s = self.bn0(x), x
-        sc = self.shortcut(pre) if self.shortcut is not None else s
-        y = self.conv1(pre)
-        y = self.conv2(self.bn1(y))
-        y = self.conv3(self.bn2(y))
-        return y, sc
+        if self.shortcut is None:
+            sc = s
+        elif _fused_ok(self.shortcut, pre):
+            sc = conv1x1(pre, self.shortcut.weight)[0]
+        else:
+            sc = self.shortcut(pre)
+        if _fused_ok(self.conv1, pre):
+            y, part = conv1x1(pre, self.conv1.weight, stats=True)
+            h = self.bn1.forward_tiles(y, part)[0]
+        else:
+            h = self.bn1(self.conv1(pre))
+        h = self.bn2(self.conv2(h))
+        if _fused_ok(self.conv3, h) and sc.shape[1] == self.conv3.out_channels:
+            return Fused(*conv1x1(h, self.conv3.weight, residual=sc, stats=True))
+        return self.conv3(h), sc
 
 
 class ResNetV2(nn.Module):
@@ -117,7 +155,8 @@ class ResNetV2(nn.Module):
 
     def forward(self, x):  # x: [B, 3, H, W] in [0, 1] (NHWC memory format preferred)
         y = max_pool3s2(self.stem(x))  # HIP NHWC kernels (1-byte argmax) on the GPU, F.max_pool2d elsewhere
-        y, _ = self.post_bn.forward_add(*self.blocks(y))
+        out = self.blocks(y)
+        y, _ = self.post_bn.forward_tiles(out.t, out.part) if isinstance(out, Fused) else self.post_bn.forward_add(*out)
         # global average pool whose backward keeps the channels_last layout (a plain mean's backward
         # materialises an NCHW gradient, copied back to NHWC by the final BN backward)
         return self.fc(F.adaptive_avg_pool2d(y, 1).flatten(1))

@@ -26,6 +26,9 @@ def _fns():
                    [I32, VP, VP, VP, I64, I32, VP, VP, F32, F32, VP, VP, I32, VP, VP, VP, VP]),
         "apply": sig(lib, "mifx_bn_relu_apply", [I32, VP, I64, I32, VP, VP, I32, VP, VP]),
         "bwd": sig(lib, "mifx_bn_relu_bwd", [I32, VP, VP, VP, I64, I32, VP, VP, I32, VP, VP, VP, VP, VP, VP]),
+        "fwd_tiles": sig(lib, "mifx_bn_relu_fwd_tiles",
+                         [I32, VP, I64, I32, VP, I32, I32, VP, VP, F32, F32, VP, VP, I32, VP, VP, VP, VP]),
+        "tiles_ws": sig(lib, "mifx_bn_tiles_ws", [I32, I32]),
     }
 
 
@@ -95,6 +98,46 @@ def _bwd(dy, x, w32, stats, relu, dres):
                         ptr(stats), int(relu), ptr(part), ptr(kbuf), ptr(dx), ptr(dgb[0]), ptr(dgb[1]),
                         stream_handle(x.device)), "mifx_bn_relu_bwd")
     return dx, dgb
+
+
+def _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, relu):
+    """Forward from per-tile statistics computed by the GEMM that produced x (mifx.ops.conv1x1): no statistics pass
+    over x. part: [2, T, C] fp32 (tile means, tile M2), T tiles of M / T rows."""
+    v = _nhwc_view(x)
+    M, C = v.shape
+    T = part.shape[1]
+    w32, b32 = weight.float().contiguous(), bias.float().contiguous()
+    stats = torch.empty(4, C, device=x.device, dtype=torch.float32)
+    ws = torch.empty(_fns()["tiles_ws"](T, C), device=x.device, dtype=torch.float64)
+    y = torch.empty_like(x)
+    check(_fns()["fwd_tiles"](_dt(x), ptr(v), M, C, ptr(part), T, M // T, ptr(w32), ptr(b32), float(eps),
+                              float(momentum), ptr(run_mean), ptr(run_var if run_mean is not None else None),
+                              int(relu), ptr(stats), ptr(ws), ptr(y), stream_handle(x.device)), "mifx_bn_relu_fwd_tiles")
+    return y, w32, stats
+
+
+class _BNReLUTiles(torch.autograd.Function):
+    """(relu(bn(x)), x) with the batch statistics taken from the producing GEMM's per-tile partials. The second output
+    aliases x: its consumer (the next block's identity shortcut, i.e. the residual operand of the next fused conv)
+    sends its gradient back through here, and the BN backward kernel adds it in (its `dres` input), as _AddBNReLU
+    does -- no separate gradient-sum kernel."""
+
+    @staticmethod
+    def forward(ctx, x, part, weight, bias, run_mean, run_var, momentum, eps):
+        y, w32, stats = _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, True)
+        ctx.save_for_backward(x, w32, stats)
+        ctx.wdtype = weight.dtype
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(part)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dpass):
+        x, w32, stats = ctx.saved_tensors
+        if dy is None:
+            return dpass, None, None, None, None, None, None, None
+        dx, dgb = _bwd(dy, x, w32, stats, True, dpass)
+        return dx, None, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None
 
 
 class _BNReLU(torch.autograd.Function):
@@ -189,6 +232,14 @@ class BatchNormReLU2d(nn.BatchNorm2d):
     def forward_add(self, a, b):
         rm, rv, train = self._args()
         return add_bn_relu(a, b, self.weight, self.bias, rm, rv, train, self.momentum, self.eps)
+
+    def forward_tiles(self, x, part):
+        """(relu(bn(x)), x) in training mode with x's batch statistics already reduced per tile by the GEMM that
+        wrote it (part: [2, T, C], mifx.ops.conv1x1); other modes fall back to forward()."""
+        rm, rv, train = self._args()
+        if train and self.training and native_ok(x):
+            return _BNReLUTiles.apply(x, part, self.weight, self.bias, rm, rv, self.momentum, self.eps)
+        return bn_relu(x, self.weight, self.bias, rm, rv, train, self.momentum, self.eps, True), x
 
 
 def defer_batch_counts(model: nn.Module) -> torch.Tensor | None:

@@ -1,0 +1,94 @@
+"""1x1 convolutions of channels_last activations as GEMMs on the pipelined MFMA kernel, with the BatchNorm statistics
+(and the residual add) folded into the epilogue (csrc/gemm8.hip EPI_STATS / EPI_ADD_STATS).
+
+ResNet-50 v2 (BASELINE config 5) is pre-activation: conv1 (1x1) feeds BN1, and conv3 (1x1) plus the shortcut feeds the
+next block's BN0. With MIOpen convolutions every such BatchNorm re-read its input for a statistics pass, and the
+residual sum was recomputed by BN0's statistics AND apply passes (4 reads + 3 writes of the block output per block).
+Here the GEMM that writes the activation also writes it ALREADY SUMMED with the residual and the per-tile (mean, M2)
+of what it stored, so the BatchNorm only finalizes (a tiny kernel) and applies: 2 reads + 2 writes.
+
+In NHWC a 1x1 stride-1 convolution is exactly Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T with M = N H W. Backward: dX on
+MIOpen's backward-data convolution, dW = dY^T X deferred into one grouped split-K launch of the pipelined TN kernel
+when inside `mifx.ops.gemm.deferred_weight_grads()` (fp32, into .grad), else MIOpen's backward-weights -- and the
+residual's gradient is dY itself."""
+from __future__ import annotations
+
+import torch
+
+from . import gemm as hg
+from . import native_stats
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> the [N H W, C] storage view."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def eligible(x: torch.Tensor, w: torch.Tensor, stride: int = 1) -> bool:
+    """A stride-1 1x1 convolution the GEMM kernel tiles: bf16 channels_last CUDA input, Cout % 128, Cin % 64,
+    N H W % 128."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and stride == 1 and w.dim() == 4
+            and tuple(w.shape[2:]) == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    n, cin, h, ww = x.shape
+    return hg.gemm8_pick(n * h * ww, w.shape[0], cin) is not None
+
+
+class _Conv1x1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, r, stats):
+        cout, cin = w.shape[0], w.shape[1]
+        wb = w.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        x2 = _rows(x)
+        M = x2.shape[0]
+        cfg = hg.gemm8_pick(M, cout, cin)
+        out = torch.empty(x.shape[0], cout, x.shape[2], x.shape[3], device=x.device, dtype=torch.bfloat16,
+                          memory_format=torch.channels_last)
+        epi = (6 if r is not None else 5) if stats else (3 if r is not None else 0)
+        rr = _rows(r.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)) if r is not None else None
+        _, part = hg.gemm8_nt(x2, wb, rr, epi, cfg=cfg, out=_rows(out))
+        ctx.save_for_backward(x2, wb)
+        ctx.w = w
+        ctx.has_r = r is not None
+        ctx.shape = x.shape
+        if part is None:
+            part = torch.empty(0, device=x.device)
+        ctx.mark_non_differentiable(part)
+        return out, part
+
+    @staticmethod
+    def backward(ctx, dy, dpart):
+        x2, wb = ctx.saved_tensors
+        if dy is None:
+            return None, None, None, None
+        dyc = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+        dy2 = _rows(dyc)
+        w = ctx.w
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = hg.defer_weight_grad_f32(dy2, x2, w)
+        want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1] and dw is None
+        dx = None
+        if want_dx or want_dw:
+            # the input gradient (and a weight gradient the grouped flush does not take: Cin = 64) on MIOpen's NHWC
+            # backward convolutions, one call: measured faster than the library GEMMs on these skinny products
+            # (M = N H W up to 800k rows: hipBLASLt's dY^T X ran 1 ms on 16 workgroups)
+            n, cin, h, w_ = ctx.shape
+            xin = x2.view(n, h, w_, cin).permute(0, 3, 1, 2)
+            gx, gw, _ = torch.ops.aten.convolution_backward(dyc, xin, wb.view(wb.shape[0], cin, 1, 1), None, [1, 1],
+                                                            [0, 0], [1, 1], False, [0, 0], 1,
+                                                            [want_dx, want_dw, False])
+            dx = gx
+            if want_dw:
+                native_stats.count("conv1x1_dW", False)
+                dw = gw.to(w.dtype)
+        return dx, dw, (dyc if ctx.has_r else None), None
+
+
+def conv1x1(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None, stats: bool = False):
+    """(conv2d(x, w) [+ residual], part): a 1x1 stride-1 convolution of a bf16 channels_last tensor on the GEMM
+    kernel; with stats, part = [2, tiles, Cout] per-tile (mean, M2) of the stored output for
+    BatchNormReLU2d.forward_tiles (else an empty tensor)."""
+    native_stats.count("conv1x1_fwd", True)
+    return _Conv1x1.apply(x, w, residual, stats)

@@ -237,7 +237,7 @@ def _dw_tensor(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 # and no second summing kernel, instead of one small launch per weight (BERT-base: 48 per step). The flush writes each
 # result into the weight's .grad -- whatever tensor autograd ended up storing there -- so the gradients must be reset
 # (None or zero) before the backward and each weight may receive ONE recorded product per flush.
-_DEFER: dict = {"on": False, "pending": []}
+_DEFER: dict = {"on": False, "pending": [], "pending_f32": []}
 
 
 class deferred_weight_grads:
@@ -260,11 +260,48 @@ def _defer_ok(dy2: torch.Tensor, x2: torch.Tensor, w) -> bool:
     return N % 256 == 0 and K % 256 == 0 and T % 64 == 0 and len(_DEFER["pending"]) < 64
 
 
+def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor):
+    """Inside `deferred_weight_grads()`: record dW = dY^T X for the fp32-ACCUMULATING grouped flush (convolution
+    weights: fp32 parameters, token counts of 10^4-10^6 rows split into chunks) and return the ZERO placeholder
+    gradient for autograd (shape / dtype of w; whatever .grad ends up holding, the flush adds the product into it).
+    None when not deferring (or the shape does not tile)."""
+    if not (_DEFER["on"] and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and w.dtype == torch.float32 and os.environ.get("MIFX_DEFER_DW", "1") != "0"):
+        return None
+    T, N = dy2.shape
+    K = x2.shape[1]
+    if N % 128 or K % 128 or T % 64 or N * K != w.numel():
+        return None
+    native_stats.count("conv1x1_dW", True)
+    # w.grad None (the trainer zeroes with set_to_none): autograd stores the returned tensor as .grad untouched, so
+    # it may be uninitialised and the flush OVERWRITES it; otherwise autograd adds the placeholder into the existing
+    # gradient (micro-batch accumulation, bucket views): then it is zeros and the flush ADDS
+    overwrite = w.grad is None
+    ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
+    _DEFER["pending_f32"].append((dy2.contiguous(), x2.contiguous(), w, ph.data_ptr() if overwrite else None))
+    return ph
+
+
 def flush_weight_grads() -> int:
     """Run every recorded weight gradient as one grouped launch into the weights' .grad; returns how many."""
+    pf, _DEFER["pending_f32"] = _DEFER.get("pending_f32", []), []
+    nf = 0
+    if pf:
+        probs, acc = [], []
+        for dy, x, w, ph in pf:
+            g = w.grad
+            if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != w.shape:
+                raise RuntimeError("deferred weight gradients: the fp32 weight's .grad is missing or not contiguous")
+            if ph is not None and g.data_ptr() != ph:
+                raise RuntimeError("deferred weight gradients: autograd did not keep the uninitialised placeholder "
+                                   "as .grad (was the gradient accumulated?)")
+            probs.append((dy, x, g.view(dy.shape[1], x.shape[1])))
+            acc.append(ph is None)
+        gemm8_tn_grouped(probs, accumulate=acc)
+        nf = len(pf)
     pend, _DEFER["pending"] = _DEFER["pending"], []
     if not pend:
-        return 0
+        return nf
     seen = set()
     for _, _, w in pend:
         if id(w) in seen:
@@ -275,7 +312,7 @@ def flush_weight_grads() -> int:
             raise RuntimeError("deferred weight gradients: the weight's .grad is not the bf16 tensor the backward "
                                "returned (was it accumulated or replaced?)")
     gemm8_tn_grouped([(dy, x, w.grad) for dy, x, w in pend])
-    return len(pend)
+    return len(pend) + nf
 
 
 def _dw(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor | None = None) -> torch.Tensor:
@@ -577,7 +614,7 @@ def _g8_fns():
     lib = _lib.load("gemm8")
     return {"configs": sig(lib, "mifx_gemm8_configs", [VP, I32]),
             "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
-            "tn": sig(lib, "mifx_gemm8_tn_grouped", [I32, I32, VP, VP, VP, VP, VP, VP, VP])}
+            "tn": sig(lib, "mifx_gemm8_tn_grouped", [I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP])}
 
 
 @functools.lru_cache(maxsize=None)
@@ -603,23 +640,43 @@ def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
     return best
 
 
-def gemm8_tn_grouped(problems, cfg: int = 0) -> int:
-    """problems: [(a [T, M], b [T, N], c [M, N]), ...] bf16 CUDA tensors on one device -> c = a^T b for all of them
-    in ONE launch (csrc/gemm8.hip; cfg 0: 256 x 256 tiles, 1: 128 x 128). Returns the number of tiles."""
+def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, accumulate=True) -> int:
+    """problems: [(a [T, M], b [T, N], c [M, N]), ...] CUDA tensors on one device (a, b bf16) -> for every problem, in
+    ONE launch of csrc/gemm8.hip's pipelined TN kernel: c = a^T b when c is bf16; c += a^T b when c is fp32 (c = a^T b
+    where `accumulate` -- a bool or one per problem -- is False), the token range cut into `chunk`-row pieces whose
+    fp32 partials a second launch sums in order. 256 x 256 tiles where M and N allow (tile128=True forces 128 x 128).
+    Returns the number of work items."""
     n = len(problems)
     if n == 0:
         return 0
+    accs = list(accumulate) if isinstance(accumulate, (list, tuple)) else [bool(accumulate)] * n
+    if n > 64:
+        return sum(gemm8_tn_grouped(problems[i:i + 64], chunk, tile128, accs[i:i + 64]) for i in range(0, n, 64))
+    Ms, Ns, Ts, chunks, flags, ws_floats = [], [], [], [], [], 0
     for a, b, c in problems:
         if not (a.is_contiguous() and b.is_contiguous() and c.is_contiguous()) or a.shape[0] != b.shape[0] or \
-                tuple(c.shape) != (a.shape[1], b.shape[1]) or c.dtype != torch.bfloat16:
-            raise ValueError("gemm8_tn_grouped: need contiguous a [T, M], b [T, N], bf16 c [M, N]")
-    A = (VP * n)(*[a.data_ptr() for a, _, _ in problems])
-    B = (VP * n)(*[b.data_ptr() for _, b, _ in problems])
-    C = (VP * n)(*[c.data_ptr() for _, _, c in problems])
-    Ms = (ctypes.c_int * n)(*[a.shape[1] for a, _, _ in problems])
-    Ns = (ctypes.c_int * n)(*[b.shape[1] for _, b, _ in problems])
-    Ts = (ctypes.c_int * n)(*[a.shape[0] for a, _, _ in problems])
-    rc = _g8_fns()["tn"](int(cfg), n, A, B, C, Ms, Ns, Ts, stream_handle(problems[0][0].device))
+                c.numel() != a.shape[1] * b.shape[1] or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 \
+                or c.dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("gemm8_tn_grouped: need contiguous bf16 a [T, M], b [T, N] and c [M, N] (bf16 / fp32)")
+        T, M = a.shape
+        N = b.shape[1]
+        f32 = c.dtype == torch.float32
+        t128 = tile128 if tile128 is not None else (M % 256 or N % 256)
+        ck = chunk if f32 else T
+        Ms.append(M)
+        Ns.append(N)
+        Ts.append(T)
+        chunks.append(ck)
+        flags.append((1 if f32 else 0) | (2 if t128 else 0) | (4 if f32 and accs[len(flags)] else 0))
+        if f32:
+            ws_floats += -(-T // ck) * M * N
+    dev = problems[0][0].device
+    ws = torch.empty(ws_floats, device=dev, dtype=torch.float32) if ws_floats else None
+    arr = lambda xs, t=ctypes.c_int: (t * n)(*xs)  # noqa: E731
+    rc = _g8_fns()["tn"](n, arr([a.data_ptr() for a, _, _ in problems], VP),
+                         arr([b.data_ptr() for _, b, _ in problems], VP),
+                         arr([c.data_ptr() for _, _, c in problems], VP), arr(Ms), arr(Ns), arr(Ts), arr(chunks),
+                         arr(flags), ptr(ws), stream_handle(dev))
     if rc <= 0:
         raise RuntimeError(f"mifx_gemm8_tn_grouped failed ({rc})")
     return rc
@@ -629,7 +686,8 @@ def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None
              cfg: int | None = None, z: torch.Tensor | None = None, out: torch.Tensor | None = None):
     """x2 [M, K] bf16, w [N, K] bf16 -> (Y [M, N] bf16, aux). epi 0: X W^T; 1: + bias; 2: GELU(X W^T + bias), aux
     = Z = bf16(X W^T); 3: + bias as a bf16 [M, N] matrix; 4: dZ = (X W^T) o GELU'(z + bias), aux = per-tile column sums
-    [M / BM, N] fp32; 5: aux = per-tile column sums and sums of squares of Y [2, M / BM, N] fp32."""
+    [M / BM, N] fp32; 5: aux = per-tile BatchNorm statistics of the stored Y, [2, M / BM, N] fp32 = (tile column mean,
+    tile sum of squared deviations M2); 6: 3 and 5 (Y = X W^T + bias-matrix, statistics of the stored sum)."""
     M, K = x2.shape
     N = w.shape[0]
     if cfg is None:
@@ -643,14 +701,14 @@ def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None
     b = None
     if epi == 2:
         z = aux = torch.empty_like(y)
-    if epi == 3:
+    if epi in (3, 6):
         b = bias.reshape(M, N).to(torch.bfloat16).contiguous()
     elif epi in (1, 2, 4):
         b = bias if bias.dtype in (torch.float32, torch.bfloat16) else bias.float()
         b = b.contiguous()
     if epi == 4:
         part = aux = torch.empty(M // bm, N, device=x2.device, dtype=torch.float32)
-    if epi == 5:
+    if epi in (5, 6):
         part = aux = torch.empty(2, M // bm, N, device=x2.device, dtype=torch.float32)
     check(_g8_fns()["nt"](int(cfg), int(epi), int(b is not None and b.dtype == torch.float32), ptr(x2), ptr(w),
                           ptr(b), ptr(y), ptr(z), ptr(part), M, N, K, stream_handle(x2.device)), "mifx_gemm8_nt")

@@ -15,6 +15,7 @@ from __future__ import annotations
 import argparse
 import contextlib
 import json
+import os
 import sys
 import time
 
@@ -69,6 +70,7 @@ class ResNetTrainer:
         self.mean, self.std = mean, std
         self.step_idx = 0
         self.amp = self.device.type == "cuda"
+        self.defer_dw = self.amp and os.environ.get("MIFX_DEFER_DW", "1") != "0"
         if self.amp:  # MIOpen find: benchmark the solvers once per conv shape, then reuse (+12% measured)
             torch.backends.cudnn.benchmark = True
         # captured steps (GPU): eager for the first graph_warmup steps (MIOpen find, momentum buffers), then graphs
@@ -123,6 +125,15 @@ class ResNetTrainer:
             if self.dp is not None and not last:
                 with self.dp.no_sync():
                     loss.backward()
+            elif self.dp is None and self.defer_dw:
+                # the 1x1 convolutions' weight gradients in ONE grouped split-K launch after the backward (fp32,
+                # accumulated into .grad); not under data parallelism, whose bucket all-reduces fire during the
+                # backward as gradients complete
+                from ..ops import gemm as hg
+
+                with hg.deferred_weight_grads():
+                    loss.backward()
+                hg.flush_weight_grads()
             else:
                 loss.backward()
             total = total + loss.detach()
@@ -150,9 +161,15 @@ class ResNetTrainer:
         return self._static_loss
 
     def _fwd_bwd_captured(self) -> torch.Tensor:
+        defer = self.dp is None and self.defer_dw
         if self.dp is not None:
             for b in self.dp.buckets:  # param.grad are views of these
                 b.buf.zero_()
+        elif defer:
+            # gradients produced inside the graph (its private pool: the same addresses on every replay, which the
+            # captured SGD reads); the deferred weight-gradient flush then overwrites instead of zero-fill + add
+            for p in self.model.parameters():
+                p.grad = None
         else:
             torch._foreach_zero_([p.grad for p in self.model.parameters() if p.grad is not None])
         total = None
@@ -168,7 +185,14 @@ class ResNetTrainer:
                 with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
                     loss = F.cross_entropy(self.model(x).float(), y) / self.accum
                 self._count_forward()
-                loss.backward()
+                if defer:  # the same backward as the eager steps (deferred grouped weight gradients)
+                    from ..ops import gemm as hg
+
+                    with hg.deferred_weight_grads():
+                        loss.backward()
+                    hg.flush_weight_grads()
+                else:
+                    loss.backward()
                 total = loss.detach() if total is None else total + loss.detach()
         return total
 

@@ -1,0 +1,140 @@
+"""1x1 convolutions on the pipelined GEMM with BatchNorm statistics / residual add in the epilogue
+(mifx.ops.conv1x1, csrc/gemm8.hip), the BatchNorm that consumes those statistics (bn_relu forward_tiles), the deferred
+fp32 weight gradients, and the ResNet-50 v2 blocks built on them -- all against plain PyTorch fp32 references."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _x(n, c, h, w, seed, scale=1.0, shift=0.0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    t = (torch.randn(n, c, h, w, device="cuda", generator=g) * scale + shift).to(torch.bfloat16)
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("cin,cout,res", [(64, 256, False), (256, 128, True), (512, 512, True)])
+def test_conv1x1_forward_stats_backward(cin, cout, res):
+    from mifx.ops import gemm as hg
+    from mifx.ops.conv1x1 import conv1x1, eligible
+
+    x = _x(4, cin, 16, 8, 1).requires_grad_()
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") * cin ** -0.5).requires_grad_()
+    r = _x(4, cout, 16, 8, 2, 2.0, 5.0).requires_grad_() if res else None
+    assert eligible(x, w)
+    y, part = conv1x1(x, w, r, stats=True)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.dtype == torch.bfloat16
+    ref = F.conv2d(x.float(), w.float()) + (r.float() if res else 0)
+    assert ((y.float() - ref).abs() <= 2 ** -7 * ref.abs() + 2e-2).all()
+    # per-tile statistics of the stored output, combined: the batch mean / variance of y
+    M = 4 * 16 * 8
+    T = part.shape[1]
+    yf = y.float().permute(0, 2, 3, 1).reshape(M, cout)
+    tm, tm2 = part[0].double(), part[1].double()
+    mean = tm.mean(0)
+    var = (tm2.sum(0) + (M // T) * ((tm - mean) ** 2).sum(0)) / M
+    torch.testing.assert_close(mean, yf.double().mean(0), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(var, yf.double().var(0, unbiased=False), rtol=1e-4, atol=1e-5)
+    # backward: dX = dY W, dW = dY^T X (hipBLASLt and the deferred grouped TN flush), dR = dY
+    gy = _x(4, cout, 16, 8, 3)
+    y.backward(gy)
+    xr, wr = x.detach().float().requires_grad_(), w.detach().clone().requires_grad_()
+    F.conv2d(xr, wr.to(torch.bfloat16).float()).backward(gy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * wr.grad.abs().max().item())
+    if res:
+        assert torch.equal(r.grad, gy)
+    w2 = w.detach().clone().requires_grad_()
+    y2, _ = conv1x1(x.detach(), w2, r.detach() if res else None, stats=True)
+    with hg.deferred_weight_grads():
+        y2.backward(gy)
+    assert hg.flush_weight_grads() == (1 if cin % 128 == 0 else 0)  # K = 64 stays on the library
+    torch.testing.assert_close(w2.grad, wr.grad, rtol=2e-2, atol=2e-2 * wr.grad.abs().max().item())
+
+
+def test_bn_forward_tiles_matches_batchnorm():
+    """BatchNormReLU2d.forward_tiles (statistics from the GEMM epilogue) == the module's own forward (statistics
+    pass): outputs, running statistics, and the backward through the fused dres path."""
+    from mifx.ops.bn_relu import BatchNormReLU2d
+    from mifx.ops.conv1x1 import conv1x1
+
+    torch.manual_seed(0)
+    x = _x(8, 256, 16, 16, 4)
+    w = torch.randn(512, 256, 1, 1, device="cuda") * 256 ** -0.5
+    y, part = conv1x1(x, w, stats=True)
+    y = y.detach().requires_grad_()
+    bn_a, bn_b = BatchNormReLU2d(512).cuda(), BatchNormReLU2d(512).cuda()
+    bn_b.load_state_dict(bn_a.state_dict())
+    out_a, alias = bn_a.forward_tiles(y, part)
+    y2 = y.detach().clone().requires_grad_()
+    out_b = bn_b(y2)
+    torch.testing.assert_close(out_a.float(), out_b.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-4, atol=1e-5)
+    g = _x(8, 512, 16, 16, 5)
+    gp = _x(8, 512, 16, 16, 6)
+    torch.autograd.backward([out_a, alias], [g, gp])
+    out_b.backward(g)
+    torch.testing.assert_close(y.grad.float(), (y2.grad + gp).float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn_a.weight.grad, bn_b.weight.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_resnet_fused_1x1_matches_unfused_path():
+    """ResNet-50 v2 blocks (bf16 autocast, channels_last) with the fused 1x1 path vs the routed MIOpen path, both
+    against the fp32 network: logits, every parameter gradient (with and without the deferred grouped weight
+    gradients) and the running statistics. The bf16 paths differ from fp32 by bf16 rounding amplified through the
+    train-mode BatchNorms; the fused path must be as close to fp32 as the unfused one."""
+    import mifx.models.resnet as R
+    from mifx.ops import gemm as hg
+
+    torch.manual_seed(0)
+    base = R.ResNetV2((2, 2, 1, 1), 10).cuda().to(memory_format=torch.channels_last)
+    x = torch.rand(8, 3, 128, 128, device="cuda").contiguous(memory_format=torch.channels_last)
+    gout = torch.randn(8, 10, device="cuda")
+
+    def run(fused, defer, amp=True):
+        m = copy.deepcopy(base)
+        saved = R.FUSED_1X1
+        R.FUSED_1X1 = fused
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                out = m(x).float()
+            if defer:
+                with hg.deferred_weight_grads():
+                    out.backward(gout)
+                assert hg.flush_weight_grads() > 0
+            else:
+                out.backward(gout)
+        finally:
+            R.FUSED_1X1 = saved
+        return m, out
+
+    saved = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = False
+    try:
+        mr, orf = run(False, False, amp=False)  # fp32 reference (the fused path needs bf16: not taken)
+    finally:
+        torch.backends.cudnn.allow_tf32 = saved
+    m0, o0 = run(False, False)
+    m1, o1 = run(True, False)
+    m2, o2 = run(True, True)
+    e0 = (o0 - orf).abs().max().item()
+    assert (o1 - orf).abs().max().item() <= 2 * e0 + 1e-2
+    assert (o2 - orf).abs().max().item() <= 2 * e0 + 1e-2
+    pr, p0, p1, p2 = (dict(m.named_parameters()) for m in (mr, m0, m1, m2))
+
+    def rel(a, b):
+        return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+    rows = []
+    for n in pr:
+        r0, r1, r2 = rel(p0[n].grad, pr[n].grad), rel(p1[n].grad, pr[n].grad), rel(p2[n].grad, pr[n].grad)
+        rows.append(f"{n}: unfused {r0:.3e} fused {r1:.3e} fused+deferred {r2:.3e}")
+        assert r1 <= 2 * r0 + 2e-2 and r2 <= 2 * r0 + 2e-2, "\n".join(rows)
+    b0, b1, br = dict(m0.named_buffers()), dict(m1.named_buffers()), dict(mr.named_buffers())
+    for n in b0:
+        if n.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(b1[n], br[n], rtol=3e-2, atol=3e-3)

@@ -69,18 +69,24 @@ def test_gemm8_epilogues_match_fp32(cfg, bias_dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3])
-def test_gemm8_stats_epilogue(cfg):
-    """The BatchNorm-statistics epilogue: per-tile column sum and sum of squares of the STORED bf16 output."""
+@pytest.mark.parametrize("add", [False, True])
+def test_gemm8_stats_epilogue(cfg, add):
+    """The BatchNorm-statistics epilogue: per-tile column mean and sum of squared deviations (M2) of the STORED bf16
+    output (with add: of the stored Y = X W^T + R); the output itself through the staged 16-byte stores. A large
+    column offset checks the two-pass form does not cancel."""
     bm, bn = gemm.gemm8_configs()[cfg]
-    M, N, K = 4 * bm, bn, 256
+    M, N, K = 4 * bm, 2 * bn, 256
     x, w = _operands(M, N, K, 100 + cfg)
-    y, part = gemm.gemm8_nt(x, w, None, 5, cfg=cfg)
-    yf = y.float().view(M // bm, bm, N)
-    assert part.shape == (2, M // bm, N)
-    assert torch.allclose(part[0], yf.sum(1), rtol=1e-4, atol=1e-3)
-    assert torch.allclose(part[1], (yf * yf).sum(1), rtol=1e-4, atol=1e-3)
-    ref = x.float() @ w.float().t()
+    r = (torch.randn(M, N, device="cuda") + 40.0).to(torch.bfloat16) if add else None
+    y, part = gemm.gemm8_nt(x, w, r, 6 if add else 5, cfg=cfg)
+    ref = x.float() @ w.float().t() + (r.float() if add else 0)
     assert ((y.float() - ref).abs() <= 2 ** -8 * ref.abs() + 1e-3).all()
+    yf = y.float().view(M // bm, bm, N)
+    mean = yf.mean(1)
+    m2 = ((yf - mean[:, None, :]) ** 2).sum(1)
+    assert part.shape == (2, M // bm, N)
+    assert torch.allclose(part[0], mean, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(part[1], m2, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.gpu
@@ -97,6 +103,7 @@ def test_gemm8_tn_grouped_matches_fp32(cfg):
     """One grouped launch of several TN products C_i = A_i^T B_i (token-major operands, different shapes and token
     counts) against fp32 references; prologue / steady state / tail of the DMA schedule (T from 64 to 1024)."""
     bm = 256 if cfg == 0 else 128
+    tile128 = cfg == 1
     g = torch.Generator(device="cuda").manual_seed(11 + cfg)
     shapes = [(bm, bm, 64), (3 * bm, bm, 128), (bm, 2 * bm, 1024), (2 * bm, 3 * bm, 320), (bm, bm, 192)]
     probs, refs = [], []
@@ -106,7 +113,7 @@ def test_gemm8_tn_grouped_matches_fp32(cfg):
         c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
         probs.append((a, b, c))
         refs.append(a.float().t() @ b.float())
-    tiles = gemm.gemm8_tn_grouped(probs, cfg=cfg)
+    tiles = gemm.gemm8_tn_grouped(probs, tile128=tile128)
     assert tiles == sum((M // bm) * (N // bm) for M, N, _ in shapes)
     for (_, _, c), ref in zip(probs, refs):
         assert ((c.float() - ref).abs() <= 2 ** -8 * ref.abs() + 1e-2).all()
@@ -144,3 +151,38 @@ def test_deferred_weight_grads_equal_reference():
     for g_, r_ in zip(got[1:], ref[1:]):
         err = ((g_.float() - r_.float()).abs().max() / r_.float().abs().max()).item()
         assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+def test_gemm8_tn_grouped_quarter_tile_tail():
+    """260 full-size tiles: the 4 beyond the last whole wave of 256 run as 16 quarter-size tiles (the tail path)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    M, N, T = 256 * 20, 256 * 13, 128
+    a = (torch.rand(T, M, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    b = (torch.rand(T, N, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert gemm.gemm8_tn_grouped([(a, b, c)]) == 260
+    ref = a.float().t() @ b.float()
+    assert ((c.float() - ref).abs() <= 2 ** -8 * ref.abs() + 1e-2).all()
+
+
+@pytest.mark.gpu
+def test_gemm8_tn_grouped_fp32_split_accumulates():
+    """fp32 destinations: C += A^T B with the token range split into chunks (the last one short), mixed 256 / 128
+    tiles, bf16 and fp32 problems in one launch."""
+    g = torch.Generator(device="cuda").manual_seed(9)
+    shapes = [(128, 512, 12544, True), (512, 256, 4096 + 640, True), (256, 256, 1024, False)]
+    probs, refs = [], []
+    for M, N, T, f32 in shapes:
+        a = (torch.rand(T, M, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+        b = (torch.rand(T, N, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+        c0 = torch.randn(M, N, device="cuda") if f32 else None
+        c = c0.clone() if f32 else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        probs.append((a, b, c))
+        refs.append(a.float().t() @ b.float() + (c0 if f32 else 0))
+    items = gemm.gemm8_tn_grouped(probs, chunk=2048)
+    # 4 tiles of 128 x 128 x 7 chunks (the last 256 rows) + 2 tiles of 256 x 256 x 3 chunks + 1 bf16 tile
+    assert items == 4 * 7 + 2 * 3 + 1
+    for (_, _, c), ref in zip(probs, refs):
+        err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
+        assert err < (1e-5 if c.dtype == torch.float32 else 1e-2), err
