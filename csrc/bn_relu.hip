@@ -557,6 +557,25 @@ int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const f
   return (int)hipGetLastError();
 }
 
+// Backward from per-tile reductions computed by the GEMM that produced dy (csrc/gemm8.hip EPI_BNBWD): pg / pgx [T][C]
+// = per-tile sum g and sum g xhat; then the same finalize and apply as mifx_bn_relu_bwd (no reduction pass over dy, x).
+int mifx_bn_relu_bwd_tiles(int dtype, const void* dy, const void* x, const void* dres, long long M, int C,
+                           const float* w, const float* stats, int relu, const float* pg, const float* pgx, int T,
+                           float* kbuf, void* dx, float* dgamma, float* dbeta, hipStream_t st) {
+  if (!shape_ok(M, C) || T <= 0 || pg == nullptr || pgx == nullptr) return -1;
+  const float *mean = stats, *rstd = stats + C, *scale = stats + 2 * C, *shift = stats + 3 * C;
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kFinCols - 1) / kFinCols), dim3(kThreads), 0, st, pg, pgx, T, M, C, w,
+                     mean, rstd, dgamma, dbeta, kbuf);
+  if (dtype)
+    hipLaunchKernelGGL(bn_bwd_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
+                       (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, M, C, scale, shift, kbuf, relu,
+                       (const __hip_bfloat16*)dres, (__hip_bfloat16*)dx);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)dy,
+                       (const float*)x, M, C, scale, shift, kbuf, relu, (const float*)dres, (float*)dx);
+  return (int)hipGetLastError();
+}
+
 // eval / inference: y = relu(x * scale + shift) with precomputed per-channel scale / shift
 // inference BatchNorm (+ ReLU) with precomputed per-channel scale / shift; x2 / s_out non-null: over the residual
 // sum s = x + x2, also written to s_out (the identity shortcut of the next block reads it)

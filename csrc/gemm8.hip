@@ -59,7 +59,7 @@ constexpr int BK = 64;
 constexpr int NT = 512;
 
 enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3, EPI_GELU_BWD = 4, EPI_STATS = 5,
-           EPI_ADD_STATS = 6, EPI_F32 = 7 };
+           EPI_ADD_STATS = 6, EPI_F32 = 7, EPI_BNBWD = 8 };
 
 __device__ __forceinline__ float erf_fast(float x) {  // Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, branch-free
   const float ax = fabsf(x);
@@ -421,6 +421,12 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   constexpr int RPI = NT / CPR_O;  // tile rows per store iteration
   constexpr bool STATS = EPI == EPI_STATS || EPI == EPI_ADD_STATS;
   constexpr bool ADD = EPI == EPI_ADD_R || EPI == EPI_ADD_STATS;
+  // BNBWD: Y is the gradient dY of a BatchNorm + ReLU's OUTPUT (the input gradient of the 1x1 convolution it feeds);
+  // `bias` = that BatchNorm's input x (bf16 [M, N]), `Z` = its forward statistics (fp32 [4][N]: mean, rstd, scale,
+  // shift). Besides storing dY, the epilogue reduces the BatchNorm backward's per-tile sums over the tile rows:
+  // part[0][m0 / BM][n] = sum g, part[1][...] = sum g xhat, g = dY [x scale + shift > 0], xhat = (x - mean) rstd --
+  // what bn_bwd_reduce would otherwise re-read dY and x for.
+  constexpr bool BNB = EPI == EPI_BNBWD;
   auto tslot = [&](int row, int c) -> unsigned char* {
     return lds + (size_t)row * (BN * 2) + ((c ^ (row & (CPR_O - 1))) << 4);
   };
@@ -447,9 +453,20 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     }
   __syncthreads();
   const int cc = tid % CPR_O, rr0 = tid / CPR_O;
-  float cs[8];
+  float cs[8], cq[8], bsc[8], bsh[8], bmu[8], brs[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+  for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
+  if constexpr (BNB) {
+    const float* st = (const float*)(const void*)Z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = n0 + 8 * cc + e;
+      bmu[e] = st[c];
+      brs[e] = st[N + c];
+      bsc[e] = st[2 * N + c];
+      bsh[e] = st[3 * N + c];
+    }
+  }
 #pragma unroll 4
   for (int i = 0; i < BM / RPI; ++i) {
     const int row = rr0 + i * RPI;
@@ -465,9 +482,19 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
     }
+    if constexpr (BNB) {  // the BatchNorm backward's reduction, with its mask computed as the forward's fmaf
+      const v8bf xv = *(const v8bf*)((const bf16*)bias + g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float u = (float)xv[e];
+        const float gg = fmaf(u, bsc[e], bsh[e]) <= 0.f ? 0.f : (float)v[e];
+        cs[e] += gg;
+        cq[e] += gg * ((u - bmu[e]) * brs[e]);
+      }
+    }
     *(v8bf*)(Y + g) = v;
   }
-  if constexpr (STATS) {
+  if constexpr (STATS || BNB) {
     // per-tile BatchNorm statistics of the STORED values, two-pass (mean, then the sum of squared deviations from
     // it): part[0][m0 / BM][n] = tile mean, part[1][m0 / BM][n] = M2 = sum (y - mean)^2 over the BM rows; combined
     // across tiles by Chan's formula in fp64 (mifx_bn_relu_fwd_tiles), so no E[y^2] - E[y]^2 cancellation
@@ -492,6 +519,13 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       }
       __syncthreads();
     };
+    if constexpr (BNB) {
+      reduce_cols(cs, meanv, 1.f);
+      for (int c = tid; c < BN; c += NT) part[(size_t)(m0 / BM) * N + n0 + c] = meanv[c];
+      reduce_cols(cq, meanv, 1.f);  // (the barrier inside orders the reads of meanv above before the overwrite)
+      for (int c = tid; c < BN; c += NT) part[((size_t)(M / BM) + m0 / BM) * N + n0 + c] = meanv[c];
+      return;
+    }
     reduce_cols(cs, meanv, 1.f / BM);
     float mu[8], m2[8];
 #pragma unroll
@@ -607,7 +641,7 @@ __global__ __launch_bounds__(256) void gemm8_tn_reduce(const RedGroup g, long lo
 template <int BM, int BN, int EPI>
 constexpr int lds_bytes() {
   const int loop = 2 * 2 * (BM / 2 + BN / 2) * 128;
-  const int epi = BM * BN * 2 + ((EPI == EPI_STATS || EPI == EPI_ADD_STATS) ? 9 * BN * 4 : 0);
+  const int epi = BM * BN * 2 + ((EPI == EPI_STATS || EPI == EPI_ADD_STATS || EPI == EPI_BNBWD) ? 9 * BN * 4 : 0);
   return loop > epi ? loop : epi;
 }
 
@@ -642,6 +676,7 @@ int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bi
                       : launch<BM, BN, EPI_GELU_BWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
     case EPI_STATS: return launch<BM, BN, EPI_STATS, bf16>(X, W, nullptr, Y, nullptr, M, N, K, part, st);
     case EPI_ADD_STATS: return launch<BM, BN, EPI_ADD_STATS, bf16>(X, W, bias, Y, nullptr, M, N, K, part, st);
+    case EPI_BNBWD: return launch<BM, BN, EPI_BNBWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
   }
   return -1;
 }
@@ -667,7 +702,9 @@ int mifx_gemm8_configs(int* out, int n) {
 // Y[M, N] = X[M, K] . W[N, K]^T, bf16 in / out, fp32 accumulation. epi: 0 none; 1 + bias[N]; 2 GELU(. + bias) with
 // Z = bf16(X W^T) (pre-bias); 3 + R (bias = bf16 [M, N]); 4 dZ = (X W^T) o GELU'(Z + bias) with part[M / BM][N] the
 // per-tile column sums of dZ; 5 part[2][M / BM][N] = per-tile column mean / sum of squared deviations (M2) of the
-// stored Y; 6 = 3 and 5: Y = X W^T + R with the statistics of the stored sum.
+// stored Y; 6 = 3 and 5: Y = X W^T + R with the statistics of the stored sum; 8: Y = X W^T is the gradient of a
+// BatchNorm + ReLU output, bias = the BatchNorm's input (bf16 [M, N]), Z = its statistics (fp32 [4][N]: mean, rstd,
+// scale, shift), part[2][M / BM][N] = per-tile (sum g, sum g xhat) of the BatchNorm backward.
 // bias bf16 or fp32 (bias_f32). M % BM == 0, N % BN == 0, K % 64 == 0, 16-byte aligned operands.
 int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z,
                   float* part, int M, int N, int K, hipStream_t st) {
@@ -675,12 +712,13 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
   if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || X == nullptr || W == nullptr || Y == nullptr) return -1;
   const Cfg c = kCfgs[cfg];
   if (M % c.bm || N % c.bn || K % BK) return -1;
-  if (epi < 0 || epi > 6) return -1;
-  if ((epi >= 1 && epi <= 4) || epi == 6) {
+  if (epi < 0 || epi > 8 || epi == 7) return -1;
+  if ((epi >= 1 && epi <= 4) || epi == 6 || epi == 8) {
     if (bias == nullptr) return -1;
   }
-  if ((epi == 2 || epi == 4) && Z == nullptr) return -1;
+  if ((epi == 2 || epi == 4 || epi == 8) && Z == nullptr) return -1;
   if (epi >= 4 && part == nullptr) return -1;
+  if (epi == 8 && (uintptr_t)bias % 16) return -1;
   if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 16 || (Z != nullptr && (uintptr_t)Z % 8)) return -1;
   if ((epi == 3 || epi == 6) && (uintptr_t)bias % 16) return -1;
   if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;  // 32-bit element offsets

@@ -129,13 +129,14 @@ class PreActBottleneck(nn.Module):
         else:
             sc = self.shortcut(pre)
         if _fused_ok(self.conv1, pre):
-            y, part = conv1x1(pre, self.conv1.weight, stats=True)
+            # pre feeds only conv1 when the shortcut is the identity (the shortcut then takes bn0's alias output s)
+            y, part = conv1x1(pre, self.conv1.weight, stats=True, bn_input=self.shortcut is None)
             h = self.bn1.forward_tiles(y, part)[0]
         else:
             h = self.bn1(self.conv1(pre))
         h = self.bn2(self.conv2(h))
         if _fused_ok(self.conv3, h) and sc.shape[1] == self.conv3.out_channels:
-            return Fused(*conv1x1(h, self.conv3.weight, residual=sc, stats=True))
+            return Fused(*conv1x1(h, self.conv3.weight, residual=sc, stats=True, bn_input=True))
         return self.conv3(h), sc
 
 

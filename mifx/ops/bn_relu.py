@@ -29,6 +29,8 @@ def _fns():
         "fwd_tiles": sig(lib, "mifx_bn_relu_fwd_tiles",
                          [I32, VP, I64, I32, VP, I32, I32, VP, VP, F32, F32, VP, VP, I32, VP, VP, VP, VP]),
         "tiles_ws": sig(lib, "mifx_bn_tiles_ws", [I32, I32]),
+        "bwd_tiles": sig(lib, "mifx_bn_relu_bwd_tiles",
+                         [I32, VP, VP, VP, I64, I32, VP, VP, I32, VP, VP, I32, VP, VP, VP, VP, VP]),
     }
 
 
@@ -100,6 +102,50 @@ def _bwd(dy, x, w32, stats, relu, dres):
     return dx, dgb
 
 
+def offer_bwd_tiles(node, dy: torch.Tensor, part: torch.Tensor) -> None:
+    """Hand a BatchNorm + ReLU node (the grad_fn of its output) the per-tile backward sums (part: [2, T, C] = sum g,
+    sum g xhat) that the GEMM producing its output gradient `dy` reduced in its epilogue (mifx.ops.conv1x1). The node
+    uses them only if the gradient it then receives IS dy, unmodified (same storage, same version: no other consumer's
+    gradient was accumulated into it), else it runs its own reduction."""
+    node.mifx_bwd_tiles = (part, dy.data_ptr(), dy._version)
+
+
+def _take_tiles(ctx, dy):
+    t = getattr(ctx, "mifx_bwd_tiles", None)
+    if t is None:
+        return None
+    ctx.mifx_bwd_tiles = None
+    part, p, ver = t
+    if dy is None or dy.data_ptr() != p or dy._version != ver or dy.dtype != torch.bfloat16:
+        return None
+    return part
+
+
+def _bwd_tiles(dy, x, w32, stats, dres, part):
+    """Backward of relu(bn(x)) from the per-tile sums the producing GEMM reduced: finalize + apply only."""
+    if dres is not None:
+        if dres.dim() == 4 and not dres.is_contiguous(memory_format=torch.channels_last):
+            dres = dres.contiguous(memory_format=torch.channels_last)
+        dres = dres.to(x.dtype)
+    v, dv = _nhwc_view(x), _nhwc_view(dy)
+    M, C = v.shape
+    T = part.shape[1]
+    kbuf = torch.empty(3, C, device=x.device, dtype=torch.float32)
+    dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    dx = torch.empty_like(x)
+    check(_fns()["bwd_tiles"](_dt(x), ptr(dv), ptr(v), ptr(_nhwc_view(dres) if dres is not None else None), M, C,
+                              ptr(w32), ptr(stats), 1, ptr(part[0]), ptr(part[1]), T, ptr(kbuf), ptr(dx), ptr(dgb[0]),
+                              ptr(dgb[1]), stream_handle(x.device)), "mifx_bn_relu_bwd_tiles")
+    return dx, dgb
+
+
+def _bwd_any(ctx, dy, x, w32, stats, relu, dres):
+    part = _take_tiles(ctx, dy) if relu else None
+    if part is not None and x.dtype == torch.bfloat16 and _nhwc_view(dy) is not None:
+        return _bwd_tiles(dy, x, w32, stats, dres, part)
+    return _bwd(dy, x, w32, stats, relu, dres)
+
+
 def _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, relu):
     """Forward from per-tile statistics computed by the GEMM that produced x (mifx.ops.conv1x1): no statistics pass
     over x. part: [2, T, C] fp32 (tile means, tile M2), T tiles of M / T rows."""
@@ -126,7 +172,7 @@ class _BNReLUTiles(torch.autograd.Function):
     def forward(ctx, x, part, weight, bias, run_mean, run_var, momentum, eps):
         y, w32, stats = _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, True)
         ctx.save_for_backward(x, w32, stats)
-        ctx.wdtype = weight.dtype
+        ctx.wdtype, ctx.mifx_bn = weight.dtype, True
         ctx.set_materialize_grads(False)
         ctx.mark_non_differentiable(part)
         return y, x.view_as(x)
@@ -136,7 +182,7 @@ class _BNReLUTiles(torch.autograd.Function):
         x, w32, stats = ctx.saved_tensors
         if dy is None:
             return dpass, None, None, None, None, None, None, None
-        dx, dgb = _bwd(dy, x, w32, stats, True, dpass)
+        dx, dgb = _bwd_any(ctx, dy, x, w32, stats, True, dpass)
         return dx, None, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None
 
 
@@ -145,13 +191,13 @@ class _BNReLU(torch.autograd.Function):
     def forward(ctx, x, weight, bias, run_mean, run_var, momentum, eps, relu):
         y, _, w32, stats = _fwd(x, None, weight, bias, run_mean, run_var, momentum, eps, relu)
         ctx.save_for_backward(x, w32, stats)
-        ctx.relu, ctx.wdtype = relu, weight.dtype
+        ctx.relu, ctx.wdtype, ctx.mifx_bn = relu, weight.dtype, bool(relu)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w32, stats = ctx.saved_tensors
-        dx, dgb = _bwd(dy, x, w32, stats, ctx.relu, None)
+        dx, dgb = _bwd_any(ctx, dy, x, w32, stats, ctx.relu, None)
         return dx, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None, None
 
 
@@ -165,7 +211,7 @@ class _AddBNReLU(torch.autograd.Function):
     def forward(ctx, a, b, weight, bias, run_mean, run_var, momentum, eps):
         y, s, w32, stats = _fwd(a, b.to(a.dtype), weight, bias, run_mean, run_var, momentum, eps, True)
         ctx.save_for_backward(s, w32, stats)
-        ctx.wdtype = weight.dtype
+        ctx.wdtype, ctx.mifx_bn = weight.dtype, True
         # an unused output (s, when the next block has a projection shortcut) arrives as None instead of
         # a materialised zero tensor: autograd created those in NCHW, forcing a full channels_last copy
         # (plus a read of zeros) in the backward of the first block of every stage
@@ -179,7 +225,7 @@ class _AddBNReLU(torch.autograd.Function):
             if ds is None:
                 return None, None, None, None, None, None, None, None
             return ds, ds, None, None, None, None, None, None
-        dx, dgb = _bwd(dy, s, w32, stats, True, ds)
+        dx, dgb = _bwd_any(ctx, dy, s, w32, stats, True, ds)
         return dx, dx, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None
 
 

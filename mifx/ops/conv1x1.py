@@ -7,16 +7,27 @@ residual sum was recomputed by BN0's statistics AND apply passes (4 reads + 3 wr
 Here the GEMM that writes the activation also writes it ALREADY SUMMED with the residual and the per-tile (mean, M2)
 of what it stored, so the BatchNorm only finalizes (a tiny kernel) and applies: 2 reads + 2 writes.
 
-In NHWC a 1x1 stride-1 convolution is exactly Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T with M = N H W. Backward: dX on
-MIOpen's backward-data convolution, dW = dY^T X deferred into one grouped split-K launch of the pipelined TN kernel
-when inside `mifx.ops.gemm.deferred_weight_grads()` (fp32, into .grad), else MIOpen's backward-weights -- and the
-residual's gradient is dY itself."""
+In NHWC a 1x1 stride-1 convolution is exactly Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T with M = N H W. Backward:
+dX = dY W on the same kernel against W^T where it tiles (Cin % 128), else MIOpen's backward-data convolution;
+dW = dY^T X deferred into one grouped split-K launch of the pipelined TN kernel when inside
+`mifx.ops.gemm.deferred_weight_grads()` (fp32, into .grad), else MIOpen's backward-weights -- and the residual's
+gradient is dY itself.
+
+When the input is the output of a BatchNorm + ReLU that feeds ONLY this convolution (`bn_input=True`: conv3 after BN2;
+conv1 after BN0 in identity-shortcut blocks), the dX GEMM also reduces that BatchNorm's backward sums (sum g,
+sum g xhat per tile, csrc/gemm8.hip EPI_BNBWD) and hands them to its node: the BatchNorm backward skips its own
+reduction pass over dX and x (bn_relu.offer_bwd_tiles; it verifies the gradient it receives is that dX, unmodified)."""
 from __future__ import annotations
+
+import os
 
 import torch
 
 from . import gemm as hg
 from . import native_stats
+
+# dX backend for tileable shapes: "gemm8" (default) or "miopen" (A/B)
+DGRAD = os.environ.get("MIFX_CONV1X1_DGRAD", "gemm8")
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -37,7 +48,7 @@ def eligible(x: torch.Tensor, w: torch.Tensor, stride: int = 1) -> bool:
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, r, stats):
+    def forward(ctx, x, w, r, stats, bn):
         cout, cin = w.shape[0], w.shape[1]
         wb = w.reshape(cout, cin).to(torch.bfloat16).contiguous()
         x2 = _rows(x)
@@ -52,6 +63,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.w = w
         ctx.has_r = r is not None
         ctx.shape = x.shape
+        ctx.bn = bn
         if part is None:
             part = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(part)
@@ -61,7 +73,7 @@ class _Conv1x1(torch.autograd.Function):
     def backward(ctx, dy, dpart):
         x2, wb = ctx.saved_tensors
         if dy is None:
-            return None, None, None, None
+            return None, None, None, None, None
         dyc = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dyc)
         w = ctx.w
@@ -70,25 +82,47 @@ class _Conv1x1(torch.autograd.Function):
             dw = hg.defer_weight_grad_f32(dy2, x2, w)
         want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1] and dw is None
         dx = None
+        n, cin, h, w_ = ctx.shape
+        cfg = hg.gemm8_pick(dy2.shape[0], cin, wb.shape[0]) if want_dx and DGRAD == "gemm8" else None
+        if cfg is not None:
+            dx = torch.empty(n, cin, h, w_, device=dy.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+            bn, xbn, stats = ctx.bn, None, None
+            if bn is not None:
+                xbn, _, stats = bn.saved_tensors
+                if not (xbn.dtype == torch.bfloat16 and tuple(xbn.shape) == tuple(ctx.shape)
+                        and xbn.is_contiguous(memory_format=torch.channels_last)):
+                    xbn = None
+            if xbn is not None:
+                _, part = hg.gemm8_nt(dy2, hg.transpose(wb), _rows(xbn), 8, cfg=cfg, z=stats, out=_rows(dx))
+                from .bn_relu import offer_bwd_tiles
+                offer_bwd_tiles(bn, dx, part)
+            else:
+                hg.gemm8_nt(dy2, hg.transpose(wb), None, 0, cfg=cfg, out=_rows(dx))
+            want_dx = False
         if want_dx or want_dw:
             # the input gradient (and a weight gradient the grouped flush does not take: Cin = 64) on MIOpen's NHWC
             # backward convolutions, one call: measured faster than the library GEMMs on these skinny products
             # (M = N H W up to 800k rows: hipBLASLt's dY^T X ran 1 ms on 16 workgroups)
-            n, cin, h, w_ = ctx.shape
             xin = x2.view(n, h, w_, cin).permute(0, 3, 1, 2)
             gx, gw, _ = torch.ops.aten.convolution_backward(dyc, xin, wb.view(wb.shape[0], cin, 1, 1), None, [1, 1],
                                                             [0, 0], [1, 1], False, [0, 0], 1,
                                                             [want_dx, want_dw, False])
-            dx = gx
+            if want_dx:
+                dx = gx
             if want_dw:
                 native_stats.count("conv1x1_dW", False)
                 dw = gw.to(w.dtype)
-        return dx, dw, (dyc if ctx.has_r else None), None
+        return dx, dw, (dyc if ctx.has_r else None), None, None
 
 
-def conv1x1(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None, stats: bool = False):
+def conv1x1(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None, stats: bool = False,
+            bn_input: bool = False):
     """(conv2d(x, w) [+ residual], part): a 1x1 stride-1 convolution of a bf16 channels_last tensor on the GEMM
     kernel; with stats, part = [2, tiles, Cout] per-tile (mean, M2) of the stored output for
-    BatchNormReLU2d.forward_tiles (else an empty tensor)."""
+    BatchNormReLU2d.forward_tiles (else an empty tensor). bn_input: the caller guarantees x is a BatchNorm + ReLU
+    output consumed by nothing else, so the input-gradient GEMM may reduce that BatchNorm's backward sums."""
     native_stats.count("conv1x1_fwd", True)
-    return _Conv1x1.apply(x, w, residual, stats)
+    bn = x.grad_fn if bn_input else None
+    if bn is not None and not getattr(bn, "mifx_bn", False):
+        bn = None
+    return _Conv1x1.apply(x, w, residual, stats, bn)

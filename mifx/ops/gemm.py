@@ -687,7 +687,10 @@ def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None
     """x2 [M, K] bf16, w [N, K] bf16 -> (Y [M, N] bf16, aux). epi 0: X W^T; 1: + bias; 2: GELU(X W^T + bias), aux
     = Z = bf16(X W^T); 3: + bias as a bf16 [M, N] matrix; 4: dZ = (X W^T) o GELU'(z + bias), aux = per-tile column sums
     [M / BM, N] fp32; 5: aux = per-tile BatchNorm statistics of the stored Y, [2, M / BM, N] fp32 = (tile column mean,
-    tile sum of squared deviations M2); 6: 3 and 5 (Y = X W^T + bias-matrix, statistics of the stored sum)."""
+    tile sum of squared deviations M2); 6: 3 and 5 (Y = X W^T + bias-matrix, statistics of the stored sum); 8: Y = X W^T
+    is the output gradient of a BatchNorm + ReLU whose input is `bias` (bf16 [M, N]) and whose forward statistics are
+    `z` (fp32 [4, N]: mean, rstd, scale, shift): aux = [2, M / BM, N] fp32 per-tile (sum g, sum g xhat) of its
+    backward (csrc/bn_relu.hip mifx_bn_relu_bwd_tiles consumes them)."""
     M, K = x2.shape
     N = w.shape[0]
     if cfg is None:
@@ -708,8 +711,13 @@ def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None
         b = b.contiguous()
     if epi == 4:
         part = aux = torch.empty(M // bm, N, device=x2.device, dtype=torch.float32)
-    if epi in (5, 6):
+    if epi in (5, 6, 8):
         part = aux = torch.empty(2, M // bm, N, device=x2.device, dtype=torch.float32)
+    if epi == 8:
+        b = bias.reshape(M, N)
+        if not (b.dtype == torch.bfloat16 and b.is_contiguous() and z is not None and z.dtype == torch.float32
+                and z.numel() == 4 * N and z.is_contiguous()):
+            raise ValueError("gemm8_nt epi 8: need a contiguous bf16 [M, N] input and fp32 [4, N] statistics")
     check(_g8_fns()["nt"](int(cfg), int(epi), int(b is not None and b.dtype == torch.float32), ptr(x2), ptr(w),
                           ptr(b), ptr(y), ptr(z), ptr(part), M, N, K, stream_handle(x2.device)), "mifx_gemm8_nt")
     return y, aux

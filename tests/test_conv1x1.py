@@ -138,3 +138,75 @@ def test_resnet_fused_1x1_matches_unfused_path():
     for n in b0:
         if n.endswith(("running_mean", "running_var")):
             torch.testing.assert_close(b1[n], br[n], rtol=3e-2, atol=3e-3)
+
+
+def test_gemm8_bnbwd_epilogue_partials():
+    """EPI_BNBWD: the stored dY plus per-tile (sum g, sum g xhat) of the BatchNorm + ReLU backward, against fp32
+    sums of the same stored values."""
+    from mifx.ops import gemm as hg
+
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, N, K = 1024, 256, 512
+    a = (torch.randn(M, K, device="cuda", generator=g)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    xb = (torch.randn(M, N, device="cuda", generator=g) * 2 + 0.5).to(torch.bfloat16)
+    mean = torch.randn(N, device="cuda", generator=g) * 0.3
+    rstd = torch.rand(N, device="cuda", generator=g) + 0.5
+    gamma = torch.randn(N, device="cuda", generator=g)
+    beta = torch.randn(N, device="cuda", generator=g) * 0.2
+    stats = torch.stack([mean, rstd, gamma * rstd, beta - mean * gamma * rstd]).contiguous()
+    for cfg, (bm, bn) in enumerate(hg.gemm8_configs()):
+        y, part = hg.gemm8_nt(a, w, xb, 8, cfg=cfg, z=stats)
+        ref = a.float() @ w.float().t()
+        assert ((y.float() - ref).abs() <= 2 ** -7 * ref.abs() + 1e-2).all()
+        xf = xb.float()
+        mask = (xf * stats[2] + stats[3]) > 0
+        gg = torch.where(mask, y.float(), torch.zeros_like(ref))
+        xhat = (xf - mean) * rstd
+        T = M // bm
+        assert part.shape == (2, T, N)
+        torch.testing.assert_close(part[0], gg.view(T, bm, N).sum(1), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(part[1], (gg * xhat).view(T, bm, N).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("second_consumer", [False, True])
+def test_conv1x1_bn_coupled_backward(second_consumer):
+    """A BatchNorm + ReLU whose output feeds a 1x1 conv with bn_input=True takes its backward sums from the dX GEMM's
+    epilogue: gradients equal the uncoupled path's; when a second consumer's gradient is accumulated into the same
+    buffer (autograd's in-place accumulation) the node must notice and reduce itself."""
+    from mifx.ops.bn_relu import BatchNormReLU2d
+    from mifx.ops.conv1x1 import conv1x1
+
+    torch.manual_seed(1)
+    x0 = _x(4, 256, 16, 16, 11, 1.5, 0.3)
+    w = torch.randn(512, 256, 1, 1, device="cuda") * 256 ** -0.5
+    gy = _x(4, 512, 16, 16, 12)
+    bn_ref = BatchNormReLU2d(256).cuda()
+    with torch.no_grad():
+        bn_ref.weight.uniform_(0.5, 1.5)
+        bn_ref.bias.uniform_(-0.2, 0.2)
+    grads = []
+    for couple in (False, True):
+        bn = copy.deepcopy(bn_ref)
+        x = x0.detach().clone().requires_grad_()
+        wc = w.detach().clone().requires_grad_()
+        pre = bn(x)
+        y, _ = conv1x1(pre, wc, bn_input=couple)
+        loss = (y.float() * gy.float()).sum()
+        if second_consumer:
+            loss = loss + (pre.float() * 0.25).sum()
+        loss.backward()
+        grads.append((x.grad.float(), bn.weight.grad, bn.bias.grad, wc.grad))
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item())
+    # and against fp32
+    xr = x0.detach().float().requires_grad_()
+    wr = bn_ref.weight.detach().clone().requires_grad_()
+    br = bn_ref.bias.detach().clone().requires_grad_()
+    pre = F.relu(F.batch_norm(xr, None, None, wr, br, True, 0.1, 1e-5))
+    loss = (F.conv2d(pre, w) * gy.float()).sum()
+    if second_consumer:
+        loss = loss + (pre * 0.25).sum()
+    loss.backward()
+    for a, b in zip(grads[1][:3], (xr.grad, wr.grad, br.grad)):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2 * b.abs().max().item())
