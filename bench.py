@@ -278,7 +278,7 @@ def main(argv=None) -> int:
     ap.add_argument("--ref-steps", type=int, default=2000)
     ap.add_argument("--ref-steps-per-graph", type=int, default=100,
                     help="steps per hipGraph for the reference-batch run (its 2000 steps amortise graph boundaries; "
-                         "profiles/bench_ref_spg_sweep_r3.txt)")
+                         "profiles/archive/bench_ref_spg_sweep_r3.txt)")
     ap.add_argument("--data-per-gpu", type=int, default=1 << 24, help="resident records per GPU (32 B each)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--shuffle-seed", type=int, default=0x5EED,
@@ -286,7 +286,7 @@ def main(argv=None) -> int:
                          "the reference's read_batch_features(randomize_input=True)); 0 = stored order")
     ap.add_argument("--steps-per-graph", type=int, default=20,
                     help="consecutive training steps captured in one hipGraph (single rank / captured collective); "
-                         "20 measured best at the driver's 20 timed steps (profiles/bench_spg_sweep_r3.txt)")
+                         "20 measured best at the driver's 20 timed steps (profiles/archive/bench_spg_sweep_r3.txt)")
     ap.add_argument("--dp", choices=("xgmi", "direct", "captured", "split"), default="xgmi",
                     help="multi-rank gradient exchange: xgmi (one-shot peer reads, whole step in hipGraphs; falls "
                          "back to direct if its validation fails), direct (eager + ncclAllReduce on the compute "

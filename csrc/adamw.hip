@@ -1,7 +1,7 @@
 // Flat mixed-precision AdamW for gfx950: bf16 model weights + bf16 gradients in two flat buffers,
 // fp32 master weights and moments. One launch updates every parameter of the model.
 //
-// Why (profiles/bert_base_steady_kernels_r1.md, BERT-base B=32 S=128): with fp32 parameters under
+// Why (profiles/archive/bert_base_steady_kernels_r1.md, BERT-base B=32 S=128): with fp32 parameters under
 // bf16 autocast every step re-casts each weight to bf16 for the forward (103 copy kernels) and casts
 // each bf16 weight-gradient back to fp32 (91 kernels), ~0.8 ms, and torch's fused AdamW runs as 6
 // multi-tensor launches (~0.77 ms). Keeping the model itself in bf16 (views into one flat buffer)
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kThreads) void adamw_flat(__hip_bfloat16* __restric
 // Same update, but each parameter's gradient is read from its OWN tensor (the one autograd produced),
 // so the step needs neither a zero-fill of a flat gradient buffer nor the per-parameter in-place
 // accumulate (`grad += new`) autograd runs when .grad is a pre-existing view: on BERT-base that was
-// 201 add kernels (~1.0 ms) + a 220 MB fill per step (profiles/bert_base_steady_kernels_s3.md).
+// 201 add kernels (~1.0 ms) + a 220 MB fill per step (profiles/archive/bert_base_steady_kernels_s3.md).
 // Workgroup b updates chunk b: parameter bp[b], elements [bo[b], bo[b] + bn[b]) of it; gptr[param] is the
 // gradient's device address this step (0 = no gradient: the parameter is left untouched, as torch's
 // AdamW skips params whose .grad is None), poff[param] its (8-aligned) offset in the flat buffers.

@@ -1,7 +1,7 @@
 // Fused multi-head self-attention for BERT (BASELINE config 4) on gfx950: forward and backward, key-padding
 // mask, counter-based attention-probability dropout. Replaces scaled_dot_product_attention, whose ROCm
 // backends are Triton-generated (AOTriton attn_fwd / bwd_kernel_fuse: 0.96 ms of a 7.4 ms BERT-base step,
-// profiles/bert_base_steady_kernels_s3b.md).
+// profiles/archive/bert_base_steady_kernels_s3b.md).
 //
 // S = 64 / 128: one workgroup per (batch, local head): the whole S x S problem of a BERT sequence (head dim 64)
 // lives in one CU. S/16 waves, wave w owns queries 16w .. 16w+15 and works in the TRANSPOSED orientation so the

@@ -1,6 +1,6 @@
 // Fused BatchNorm(train) + ReLU for NHWC activations on gfx950 (ResNet-50 v2, BASELINE config 5).
 //
-// Profile that motivated it (profiles/resnet50_steady_kernels_r1.md, B=256 bf16 channels_last):
+// Profile that motivated it (profiles/archive/resnet50_steady_kernels_r1.md, B=256 bf16 channels_last):
 // MIOpen BatchNorm fwd/bwd kernels + the separate ReLU clamp / threshold-backward kernels were
 // ~16.5 ms of the 37.4 ms step — more than all convolutions. Pre-activation ResNet applies ReLU
 // right after every BatchNorm, so both directions fuse:

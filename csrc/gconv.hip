@@ -64,7 +64,7 @@ __device__ __forceinline__ u4 res_epi(u4 v, const ResEpi& re, size_t off, int c)
 }
 
 // amdgpu_waves_per_eu(4): 4 workgroups per CU (40 KB LDS each) -- the loop is latency-bound, occupancy pays
-// (profiles/gconv_bk_ab_r2.txt, gconv_prefetch_ab_r2.txt: deeper prefetch / wider chunks that cost occupancy lose)
+// (profiles/archive/gconv_bk_ab_r2.txt, gconv_prefetch_ab_r2.txt: deeper prefetch / wider chunks that cost occupancy lose)
 // ksplit > 1 (few pixel tiles, e.g. batch-1 inference): blockIdx.z = g * ksplit + split, the workgroup reduces
 // steps [nsteps split / ksplit, nsteps (split + 1) / ksplit) and writes its fp32 partial to part[split][M][G*K]
 // (gconv_splitk_finish adds the splits in order, + bias, ReLU)

@@ -3,7 +3,7 @@
 // BASELINE config 4 (BERT-base): the four projection GEMMs of a layer (QKV, attention out, FFN in, FFN out) are
 // "NT" products of a token-major activation and an nn.Linear weight, both K-contiguous. The FFN-in GEMM is followed
 // by bias + GELU(erf), which unfused costs a second pass over the [tokens, 3072] activation (bias_gelu_fwd_v,
-// 12 us per call at 4096 tokens: profiles/bert_base_steady_kernels_s3b.md); here it is the GEMM's epilogue, which
+// 12 us per call at 4096 tokens: profiles/archive/bert_base_steady_kernels_s3b.md); here it is the GEMM's epilogue, which
 // writes both the GELU output and the pre-bias product the backward needs (the saved-tensor contract of
 // mifx.ops.fused_bert._BiasGelu, so its backward kernel is reused as is).
 //

@@ -4,7 +4,7 @@
 // BASELINE config 4 (BERT-base, 4096 tokens): the four input-gradient GEMMs of a layer (dY of QKV 4096x2304, of
 // attention-out 4096x768, of FFN-in 4096x3072, of FFN-out 4096x768, against the nn.Linear weight [out, in]) ran on
 // hipBLASLt as 128x128-tile kernels on 192 workgroups (31 us for the 4096x768 outputs with K = 2304 / 3072:
-// profiles/bert_steady_kernels_r3_fold.md). The reduction index is the weight's ROW index, so the two operands sit
+// profiles/archive/bert_steady_kernels_r3_fold.md). The reduction index is the weight's ROW index, so the two operands sit
 // differently in memory:
 //  * A (dY, [M][K], K contiguous) is staged as in csrc/gemm.hip: [BM rows][64] bf16 per K-tile, 128-byte rows with
 //    the 16-byte chunk index XOR-swizzled by ((row >> 1) & 7), fragments read with ds_read_b128 (8 consecutive k);

@@ -4,7 +4,7 @@
 // BASELINE config 4 (BERT-base, 4096 tokens): the four weight-gradient GEMMs of a layer (QKV 2304x768, attention-out
 // 768x768, FFN-in 3072x768, FFN-out 768x3072, all with K = 4096 tokens) were hipBLASLt's slowest products in the
 // training step: 144-216 workgroups of 128x128 / 64x64 tiles on 256 CUs (one K-reduction per tile, no split), 30-46 us
-// each, 160-420 TFLOP/s (profiles/bert_steady_kernels_r3.md). Here every shape gets a whole wave of workgroups: the
+// each, 160-420 TFLOP/s (profiles/archive/bert_steady_kernels_r3.md). Here every shape gets a whole wave of workgroups: the
 // 96 x 96 tile puts 3072 x 768 (and 768 x 3072) on exactly 256 workgroups, and small outputs split the token range
 // over gridDim.y with an fp32 partial per split, summed in split order by a second kernel (deterministic).
 //
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void gemm_tn(const bf16* __restrict__ A, const
   }
 }
 
-// Measured (profiles/gemm_tn_r3b_k2.jsonl): 50 us on FFN-in's dW at S = 1 against 54 for the 4-wave deep ring and
+// Measured (profiles/archive/gemm_tn_r3b_k2.jsonl): 50 us on FFN-in's dW at S = 1 against 54 for the 4-wave deep ring and
 // 38 for two 4-wave workgroups per CU with a 2-way token split -- two independent barrier pipelines per CU beat one
 // 8-wave pipeline, so the tuned table keeps the split; this form stays selectable (config 18).
 // 8-wave form of the 96 x 96 tile (one workgroup per CU, two waves per SIMD, no token split across workgroups):

@@ -2,7 +2,7 @@
 // PATE CNN's TF-SAME pooling (`deep_cnn.py:123,151`: top/left pad = total // 2, the rest at the bottom/right).
 //
 // PyTorch's NHWC max-pool saves an int64 argmax per OUTPUT element and scatters the backward through it
-// (profiles/resnet50_steady_kernels_s3.md: 252 us fwd + 620 us bwd per step at B=256, 112x112x64). Here:
+// (profiles/archive/resnet50_steady_kernels_s3.md: 252 us fwd + 620 us bwd per step at B=256, 112x112x64). Here:
 //  * forward: one thread per (n, oh, ow, 8 channels): nine 16-byte window loads, per-channel max, and a
 //    1-byte window position (0..8) per channel -> the index traffic is 1/8 of int64 indices;
 //  * backward in gather form: one thread per (n, ih, iw, 8 channels) visits the (at most 2x2) output

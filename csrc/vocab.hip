@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void str_hash(const uint8_t* __restrict__ buf,
 }
 
 // Zipf-distributed columns (a few tokens carry most rows) make one global counter per hot token a
-// serialisation point: 1M rows spent 3 ms in vocab_count (profiles/analyzers_kernels_s2.md). Each
+// serialisation point: 1M rows spent 3 ms in vocab_count (profiles/archive/analyzers_kernels_s2.md). Each
 // block therefore pre-aggregates its rows in an LDS hash table (count + smallest row per key, LDS
 // atomics) and flushes one global insert per distinct key it saw; rows whose key finds no LDS slot
 // within kLdsProbe probes go straight to the global table.

@@ -425,7 +425,7 @@ __device__ __forceinline__ void store_tiles(float* slab, const v4f (&acc)[NT], c
 //                their first row: the same association for any rotation of the round-robin dispatch, so the
 //                step is run-to-run deterministic) and applies the optimizer (wd_opt.h sc_update) in place.
 // This replaces the two tail kernels (csrc/wide_deep.hip wd_reduce_xcd + wd_xcd_opt_sc, 11.8 us per step at
-// B=65536, profiles/bench_r2_final_kernels.md) and their launch ramps; the slab never has to leave its XCD.
+// B=65536, profiles/archive/bench_r2_final_kernels.md) and their launch ramps; the slab never has to leave its XCD.
 // Barrier: a monotonic 64-bit arrival counter (no reset, no generation flag): the workgroup whose arrival
 // returned `old` waits until the counter reaches (old / G + 1) G. The wait is bounded by wall-clock time: on a
 // timeout (a workgroup never arrived: not co-resident) it sets the sticky `err` flag, and the tail then skips

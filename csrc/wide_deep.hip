@@ -686,11 +686,11 @@ constexpr int RQ = 16;               // float4 columns per workgroup
 constexpr int RG = 256 / RQ;         // row groups
 constexpr int RU = 8;            // slab rows in flight per thread (G=256: 322 workgroups x 256 threads x
                                      // 8 x 16 B = the whole 21 MB slab requested in two rounds; RU 16, all of
-                                     // it in one round, measured 2 us slower per step: profiles/wd_ab_r2s.txt)
+                                     // it in one round, measured 2 us slower per step: profiles/archive/wd_ab_r2s.txt)
 
 // Column sums of the slab: float4 column q = blockIdx.x * RQ + threadIdx.x % RQ over rows [0, G), row groups of
 // RG threads, fixed order (deterministic). The full sum is returned to threads threadIdx.x < RQ. (A chunk-major
-// slab layout -- this workgroup's columns one contiguous [G][RQ] block -- measured no faster: profiles/wd_ab_r2s.txt)
+// slab layout -- this workgroup's columns one contiguous [G][RQ] block -- measured no faster: profiles/archive/wd_ab_r2s.txt)
 __device__ __forceinline__ float4 slab_column_sum(const float4* __restrict__ slab, int G, int S4,
                                                   float4 (&part)[RG][RQ]) {
   const int lq = threadIdx.x % RQ, r = threadIdx.x / RQ;
@@ -878,7 +878,7 @@ struct XgPeers {
 // each; 32 rows per XCD at grid 256). A one-pass reduction reads every row from every XCD: measured, the fused
 // kernel then runs 29-30 us instead of 23 us (its slab writes pay for the lines the previous reduction pulled
 // across XCDs), whatever cache policy the reduction's loads use (plain, nontemporal or agent-scope:
-// profiles/wd_ab_r2s.txt), and a standalone write + read-back of 21 MB costs 12 us against 3.6 us for re-reading
+// profiles/archive/wd_ab_r2s.txt), and a standalone write + read-back of 21 MB costs 12 us against 3.6 us for re-reading
 // a clean slab (tools/micro/launch_floor.hip). So:
 //   level 1 (wd_reduce_xcd, 8 x 81 workgroups): workgroup (chunk c = blockIdx / 8) sums, for its 256 columns, only
 //     the rows written on ITS OWN XCD (the fused kernel records each workgroup's XCD in xcd_of), ascending -- L2

@@ -133,7 +133,7 @@ class FashionCNN(nn.Module):
     def __init__(self, num_classes: int = 10):
         super().__init__()
         # the direct HIP conv by default here: the whole Fashion training step measured 0.43 vs 0.54 ms/step on
-        # MIOpen (profiles/cnn_small_conv_r3.jsonl; MIFX_SMALL_CONV=0 forces the library)
+        # MIOpen (profiles/archive/cnn_small_conv_r3.jsonl; MIFX_SMALL_CONV=0 forces the library)
         self.conv = SmallConv2d(1, 8, 3, stride=2, prefer=True)
         self.fc = nn.Linear(8 * 13 * 13, num_classes)
 

@@ -20,7 +20,7 @@ from ._lib import I32, VP, check, ptr, sig, stream_handle
 
 # Input channels up to which the VALU direct conv is used: the first layers (1 or 3 channels) of these CNNs, where
 # an MFMA tile has nothing to reduce over. Per model by measurement (tools/bench_cnn.py,
-# profiles/cnn_small_conv_r3.jsonl): MIOpen is faster on all but the Fashion CNN -- TPU CNN 1.46 ms/step with its
+# profiles/archive/cnn_small_conv_r3.jsonl): MIOpen is faster on all but the Fashion CNN -- TPU CNN 1.46 ms/step with its
 # first layer direct (6.8 with every layer direct) vs 1.29, DP-SGD tutorial SGD step 0.67 vs 0.60, PATE teacher 1.75
 # vs 1.60; Fashion 0.43-0.49 vs 0.54, so FashionCNN's conv runs here by default (prefer=True) and the others only
 # with MIFX_SMALL_CONV=1 (MIFX_SMALL_CONV=0 turns every direct conv off).

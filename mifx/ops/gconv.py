@@ -138,7 +138,7 @@ class _GConv(torch.autograd.Function):
         r_dgrad, r_wgrad = ctx.route
         if ctx.needs_input_grad[0]:
             # HIP input gradient for grouped / large-image convs; MIOpen's is as fast or faster on small
-            # single-group images (profiles/gconv_resnet_r2.jsonl); a per-shape route overrides the policy
+            # single-group images (profiles/archive/gconv_resnet_r2.jsonl); a per-shape route overrides the policy
             hip_ok = C % 32 == 0 and K % 32 == 0 and R == S
             if r_dgrad == "miopen" or (r_dgrad == "hip" and not hip_ok):
                 dx = _lib_bwd(xb, wb, dyb, stride, pad, G, True, False)[0]
@@ -151,7 +151,7 @@ class _GConv(torch.autograd.Function):
             else:
                 dx = _lib_bwd(xb, wb, dyb, stride, pad, G, True, False)[0]
         if ctx.needs_input_grad[1]:
-            # Weight-gradient policy from measurements (profiles/gconv_resnet_shapes_r3.jsonl,
+            # Weight-gradient policy from measurements (profiles/archive/gconv_resnet_shapes_r3.jsonl,
             # pate_ensemble_bench_r3*.jsonl): grouped 1x1 -> one batched GEMM; other grouped convs -> the HIP kernel;
             # a single group (ResNet-50) -> MIOpen, which beats the pixel-split kernel on 7 of the 9 ResNet shapes.
             one_by_one = R == 1 and S == 1 and pad == 0 and stride == 1

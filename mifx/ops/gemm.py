@@ -124,11 +124,11 @@ def config_details() -> tuple[tuple[int, int, int], ...]:
 
 # Where the hand-written kernel is USED by default (linear / linear_bias_gelu without force=True): the (M, N, K)
 # products it measured faster than hipBLASLt on MI355X, with the winning configuration (tools/bench_gemm_hip.py,
-# profiles/gemm_hip_r3b.jsonl; BERT-base, 4096 tokens): attention-out 4096x768x768 10.7 us vs 20.5 us. Measured
+# profiles/archive/gemm_hip_r3b.jsonl; BERT-base, 4096 tokens): attention-out 4096x768x768 10.7 us vs 20.5 us. Measured
 # slower there and left on hipBLASLt: QKV 22.9 vs 21.6 us, FFN-in 25.3 vs 23.3 us (with the bias + GELU epilogue
 # 37.5 vs 34.9 us for GEMM + separate bias_gelu: the epilogue's second 25 MB output (the pre-bias product the
 # backward needs) is written after the last K-tile by every workgroup at once, un-overlapped, and a branch-free erf
-# did not change that: profiles/gemm_hip_r3c_fasterf.jsonl), FFN-out 28.9 vs 25.1 us. MIFX_HIP_GEMM=all routes every
+# did not change that: profiles/archive/gemm_hip_r3c_fasterf.jsonl), FFN-out 28.9 vs 25.1 us. MIFX_HIP_GEMM=all routes every
 # eligible shape to the kernel (heuristic configuration) for A/B runs.
 TUNED: dict[tuple[int, int, int], int] = {(4096, 768, 768): 13}
 
@@ -198,7 +198,7 @@ def gemm_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
 # and runs beside the following dX / attention / elementwise kernels; `join_weight_grads()` (before the optimizer)
 # joins it. The operands are kept referenced until the join, so the allocator cannot hand their memory to the main
 # stream while the side stream still reads them; the dW tensors come from the side stream's pool. Measured SLOWER in
-# the BERT-base step (6.75 vs 6.41 ms, identical loss: profiles/bert_async_dw_ab_r3.txt) -- the side-stream GEMMs take
+# the BERT-base step (6.75 vs 6.41 ms, identical loss: profiles/archive/bert_async_dw_ab_r3.txt) -- the side-stream GEMMs take
 # CUs from the dX GEMMs and attention kernels rather than filling idle ones -- so BertTrainer keeps it off
 # (MIFX_BERT_ASYNC_DW=1 turns it on).
 _ASYNC = {"on": False, "side": {}, "pending": {}}
@@ -552,11 +552,11 @@ def tn_configs() -> tuple[tuple[int, int, int], ...]:
     return tuple((buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(n))
 
 
-# measured per-shape choices (M, N, T) -> (cfg, splits); tools/bench_gemm_tn.py, profiles/gemm_tn_r3.jsonl
+# measured per-shape choices (M, N, T) -> (cfg, splits); tools/bench_gemm_tn.py, profiles/archive/gemm_tn_r3.jsonl
 # BERT-base at 4096 tokens (B = 32, S = 128), us vs hipBLASLt `dy.t() @ x`: QKV 30.7 vs 36.2, attention-out 18.3 vs
 # 27.6, FFN-in 38.0 vs 41.8, FFN-out 37.7 vs 42.6 (configs with 2-3 workgroups per CU and a token split; the one-
 # workgroup-per-CU deep-ring configurations measured slower: the per-CU operand stream, not DMA latency, bounds a
-# 96 x 96 tile at ~30 GB/s per workgroup; profiles/gemm_tn_r3.jsonl)
+# 96 x 96 tile at ~30 GB/s per workgroup; profiles/archive/gemm_tn_r3.jsonl)
 TN_TUNED: dict[tuple[int, int, int], tuple[int, int]] = {(2304, 768, 4096): (10, 4), (768, 768, 4096): (9, 8),
                                                          (3072, 768, 4096): (9, 2), (768, 3072, 4096): (9, 2)}
 

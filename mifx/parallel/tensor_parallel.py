@@ -12,7 +12,7 @@ BERT-base fine-tune at TP=8, so this module provides the standard column/row spl
   partitioned as evenly as possible (2,2,2,2,1,1,1,1 at TP=8) and the QKV / output projections
   use the matching uneven column / row splits, so TP=8 is exact (not approximate). Cost of the imbalance: the
   fused attention kernels take 13.2 + 22.1 us per layer for all 12 heads at B = 32, S = 128
-  (profiles/bert_steady_kernels_r3_fold.md), so a 2-head rank spends ~5.9 us per layer where an even 1.5-head
+  (profiles/archive/bert_steady_kernels_r3_fold.md), so a 2-head rank spends ~5.9 us per layer where an even 1.5-head
   share would take ~4.4: ~1.5 us per layer, ~18 us per 12-layer step, while the GEMMs and LayerNorms split evenly
   (the FFN's 3072 columns and the 768-wide activations divide by 8). Rebalancing would need heads split across
   ranks (extra all-to-alls per layer), which costs more than it saves at this size.

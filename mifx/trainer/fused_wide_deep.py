@@ -167,7 +167,7 @@ class FusedWideDeepTrainer:
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
         # grid <= #CUs, one workgroup per CU by its LDS). Measured SLOWER on MI355X and therefore off by default:
-        # 40.8 vs 33.6 us per step at B=65536 (profiles/wd_tail_ab_r3.md): each cross-XCD grid barrier costs ~3 us
+        # 40.8 vs 33.6 us per step at B=65536 (profiles/archive/wd_tail_ab_r3.md): each cross-XCD grid barrier costs ~3 us
         # (arrival atomic + polling through the fabric) and the write-through per-XCD partials ~7 us more before
         # the second barrier, against ~11.6 us for the two tail kernels they replace.
         if in_kernel_tail is None:
@@ -498,7 +498,7 @@ class FusedWideDeepTrainer:
         the one-step graph n % S times: every step still runs its own kernels (the data offset and optimizer
         step advance through the device-side step counter), the host just launches once per S steps. Replaying
         one graph per step left ~8.7 us of idle GPU between steps on MI355X (the host-side launch of a replay
-        costs more than the step's ~35 us of GPU work): tools/timeline.py, profiles/wd_step_timeline_r2.txt."""
+        costs more than the step's ~35 us of GPU work): tools/timeline.py, profiles/archive/wd_step_timeline_r2.txt."""
         if self._persist:  # all n steps in one launch of the persistent kernel
             if n > 0:
                 if self.records is None:

@@ -136,7 +136,7 @@ class FlatAdamW:
             # runs under the compute-bound backward of layers < L; step() launches what is left, joins the side
             # stream and advances the step counter once. Every bucket reads the same step value, so the update is
             # the single-launch update, bucket by bucket (same kernel, same per-element math). Measured SLOWER in the
-            # BERT-base step (7.18 vs 6.38 ms on MI355X, profiles/bert_adamw_overlap_r3.txt): the bucket launches fill
+            # BERT-base step (7.18 vs 6.38 ms on MI355X, profiles/archive/bert_adamw_overlap_r3.txt): the bucket launches fill
             # every CU with memory-bound blocks beside the backward's one-workgroup-per-CU GEMMs, which lose more
             # than the ~0.5 ms update that is hidden.
             if overlap is None:

@@ -307,7 +307,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--deterministic", action="store_true",
                     help="MIOpen deterministic convolution solvers: bit-reproducible steps (the default bf16 solvers "
-                         "are not run-to-run reproducible, measured in round 2, profiles/resnet_determinism_r2s3.txt). Diagnostic only: "
+                         "are not run-to-run reproducible, measured in round 2, profiles/archive/resnet_determinism_r2s3.txt). Diagnostic only: "
                          "measured 13.7 s/step at B=256 on one MI355X vs 26.5 ms with the default solvers")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of the captured hipGraph step")
     a = ap.parse_args(argv)

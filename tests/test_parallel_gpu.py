@@ -92,7 +92,7 @@ def _resnet_run(world: int, rank: int, out: str) -> None:
                        process_group=dist.group.WORLD if world > 1 else None, seed=3,
                        accum_steps=1 if world > 1 else 2)
     torch.backends.cudnn.benchmark = False  # no solver search in a test (and the same solvers in every process)
-    # MIOpen's default bf16 convolution solvers are not run-to-run reproducible (profiles/resnet_determinism_r2s3.txt:
+    # MIOpen's default bf16 convolution solvers are not run-to-run reproducible (profiles/archive/resnet_determinism_r2s3.txt:
     # the same fwd+bwd twice in one process differs); its deterministic solvers are, which makes this exact
     torch.backends.cudnn.deterministic = True
     losses = [float(tr.step()) for _ in range(_RES_STEPS)]

@@ -3,7 +3,7 @@ steps at batch 40, checkpoints every 999 steps -- airflow-dags/taxi_pipeline.py:
 under LocalDagRunner on one device and write per-component times, the Trainer's examples/sec and the eval
 metrics as one JSON object.
 
-    python tools/pipeline_bench.py --device cuda --out profiles/pipeline_gpu_r3.json
+    python tools/pipeline_bench.py --device cuda --out profiles/archive/pipeline_gpu_r3.json
 """
 from __future__ import annotations
 
