@@ -73,6 +73,10 @@ __device__ __forceinline__ uint32_t f2bf(float a, float b) {  // round to neares
   return __builtin_bit_cast(uint32_t, (v2bf){(__bf16)a, (__bf16)b});
 }
 
+// DP gradient buckets (mifx.parallel.ddp exchange="ipc") take the same three kernels over fp32 data: F32 = the
+// 8-byte words hold 2 fp32 instead of 4 bf16, the rank-order sum stays fp32 and is scaled once (the 1 / world average)
+// before it is stored -- every rank gets the same bits, and the captured backward carries the exchange on a side stream.
+
 // A: partial -> own buffer half, stamp phase 0
 __global__ __launch_bounds__(WG) void tpar_publish(const uint64_t* __restrict__ x, long long n4, Peers pe, int world,
                                                    int rank, long long npad4, const long long* __restrict__ ep,
@@ -93,9 +97,10 @@ __global__ __launch_bounds__(WG) void tpar_publish(const uint64_t* __restrict__ 
 }
 
 // B: reduce-scatter of the chunks this rank owns (c = rank + world k)
+template <bool F32>
 __global__ __launch_bounds__(WG) void tpar_reduce(Peers pe, int world, int rank, long long npad4,
                                                   const long long* __restrict__ ep, int* __restrict__ err,
-                                                  int nchunks, int nch) {
+                                                  int nchunks, int nch, float scale) {
   if (failed(err)) return;
   const int c = rank + world * blockIdx.x;
   if (c >= nch) return;  // (nch: chunks holding data; nchunks: the flag array's chunk dimension)
@@ -110,20 +115,31 @@ __global__ __launch_bounds__(WG) void tpar_reduce(Peers pe, int world, int rank,
 #pragma unroll 4
   for (int i = 0; i < PER_LANE; ++i) {
     const int q = i * WG + threadIdx.x;
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
     uint64_t v[MAXW];
 #pragma unroll
     for (int p = 0; p < MAXW; ++p) v[p] = p < world ? ld_sys64(pe.buf[p] + off + q) : 0ull;
+    if constexpr (F32) {
+      float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-    for (int p = 0; p < MAXW; ++p)  // rank order: the same fp32 sum on every rank
-      if (p < world) {
-        const float2 a = bf2f((uint32_t)v[p]), b = bf2f((uint32_t)(v[p] >> 32));
-        s[0] += a.x;
-        s[1] += a.y;
-        s[2] += b.x;
-        s[3] += b.y;
-      }
-    st_sys64(dst + q, (uint64_t)f2bf(s[0], s[1]) | ((uint64_t)f2bf(s[2], s[3]) << 32));
+      for (int p = 0; p < MAXW; ++p)  // rank order: the same fp32 sum on every rank
+        if (p < world) {
+          s0 += __uint_as_float((uint32_t)v[p]);
+          s1 += __uint_as_float((uint32_t)(v[p] >> 32));
+        }
+      st_sys64(dst + q, (uint64_t)__float_as_uint(s0 * scale) | ((uint64_t)__float_as_uint(s1 * scale) << 32));
+    } else {
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < MAXW; ++p)  // rank order: the same fp32 sum on every rank
+        if (p < world) {
+          const float2 a = bf2f((uint32_t)v[p]), b = bf2f((uint32_t)(v[p] >> 32));
+          s[0] += a.x;
+          s[1] += a.y;
+          s[2] += b.x;
+          s[3] += b.y;
+        }
+      st_sys64(dst + q, (uint64_t)f2bf(s[0], s[1]) | ((uint64_t)f2bf(s[2], s[3]) << 32));
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x < world)
@@ -133,21 +149,21 @@ __global__ __launch_bounds__(WG) void tpar_reduce(Peers pe, int world, int rank,
 // C: all-gather of the reduced chunks into the output; the last workgroup advances the epoch
 // A failed group (sticky err) writes NaN into the output chunk instead of leaving it uninitialised: whatever consumes
 // the activation goes non-finite (the loss shows it) even before the host's next check() raises.
-__device__ __forceinline__ void poison(uint64_t* __restrict__ y, long long n4, int c) {
+__device__ __forceinline__ void poison(uint64_t* __restrict__ y, long long n4, int c, bool f32) {
   const long long base = (long long)c * (CHUNK / 4);
 #pragma unroll
   for (int i = 0; i < PER_LANE; ++i) {
     const long long q = base + i * WG + threadIdx.x;
-    if (q < n4) y[q] = 0x7FC07FC07FC07FC0ull;  // four bf16 quiet NaNs
+    if (q < n4) y[q] = f32 ? 0x7FC000007FC00000ull : 0x7FC07FC07FC07FC0ull;  // fp32 / bf16 quiet NaNs
   }
 }
 
 __global__ __launch_bounds__(WG) void tpar_gather(uint64_t* __restrict__ y, long long n4, Peers pe, int world, int rank,
                                                   long long npad4, long long* __restrict__ ep, int* __restrict__ err,
-                                                  int nchunks, unsigned int* __restrict__ done) {
+                                                  int nchunks, unsigned int* __restrict__ done, int f32) {
   const int c = blockIdx.x, owner = c % world;
   if (failed(err)) {
-    poison(y, n4, c);
+    poison(y, n4, c, f32);
     return;
   }
   const long long e = ep[0] + 1;
@@ -155,7 +171,7 @@ __global__ __launch_bounds__(WG) void tpar_gather(uint64_t* __restrict__ y, long
   if (threadIdx.x == 0)  // (own chunks too: uniform code; their stamp is already there)
     ok = wait_flag(pe.flag[rank] + ((size_t)1 * nchunks + c) * MAXW + owner, (unsigned int)e, err);
   if (__ballot(!ok) != 0ull) {  // no epoch advance: the error is sticky, the host raises
-    poison(y, n4, c);
+    poison(y, n4, c, f32);
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -187,9 +203,9 @@ int mifx_tpar_chunk() { return CHUNK; }
 // pointers (IPC-opened peer buffers, [rank] = own): bufs / reds [2][npad] bf16 with npad = nchunks * CHUNK >= n,
 // flags [2][nchunks][8] uint32 (uncached). ep: int64 epoch counter (device), done: uint32 arrival counter (device,
 // zero), err: sticky int flag (device). Three kernels on `stream`.
-int mifx_tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, void* const* reds, void* const* flags,
-                        int world, int rank, long long npad, long long* ep, unsigned int* done, int* err,
-                        hipStream_t stream) {
+static int tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, void* const* reds,
+                          void* const* flags, int world, int rank, long long npad, long long* ep, unsigned int* done,
+                          int* err, bool f32, float scale, hipStream_t stream) {
   if (world < 1 || world > MAXW || rank < 0 || rank >= world || n <= 0 || n % 4 != 0 || npad % CHUNK != 0 ||
       n > npad || x == nullptr || y == nullptr || ep == nullptr || done == nullptr || err == nullptr)
     return -1;
@@ -206,11 +222,30 @@ int mifx_tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, 
   const long long n4 = n / 4, npad4 = npad / 4;
   hipLaunchKernelGGL(tpar_publish, dim3(nchunks), dim3(WG), 0, stream, (const uint64_t*)x, n4, pe, world, rank, npad4,
                      ep, err, nchunks_all);
-  hipLaunchKernelGGL(tpar_reduce, dim3((nchunks + world - 1) / world), dim3(WG), 0, stream, pe, world, rank, npad4, ep,
-                     err, nchunks_all, nchunks);
+  if (f32)
+    hipLaunchKernelGGL(tpar_reduce<true>, dim3((nchunks + world - 1) / world), dim3(WG), 0, stream, pe, world, rank,
+                       npad4, ep, err, nchunks_all, nchunks, scale);
+  else
+    hipLaunchKernelGGL(tpar_reduce<false>, dim3((nchunks + world - 1) / world), dim3(WG), 0, stream, pe, world, rank,
+                       npad4, ep, err, nchunks_all, nchunks, 1.f);
   hipLaunchKernelGGL(tpar_gather, dim3(nchunks), dim3(WG), 0, stream, (uint64_t*)y, n4, pe, world, rank, npad4, ep,
-                     err, nchunks_all, done);
+                     err, nchunks_all, done, (int)f32);
   return (int)hipGetLastError();
+}
+
+int mifx_tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, void* const* reds, void* const* flags,
+                        int world, int rank, long long npad, long long* ep, unsigned int* done, int* err,
+                        hipStream_t stream) {
+  return tpar_allreduce(x, y, n, bufs, reds, flags, world, rank, npad, ep, done, err, false, 1.f, stream);
+}
+
+// fp32 variant (DP gradient buckets): n = fp32 elements (even), npad = the buffers' capacity in bf16-element units
+// as above (i.e. 2 x the fp32 capacity); the rank-order sum is multiplied by `scale` before it is stored.
+int mifx_tpar_allreduce_f32(const void* x, void* y, long long n, void* const* bufs, void* const* reds,
+                            void* const* flags, int world, int rank, long long npad, long long* ep, unsigned int* done,
+                            int* err, float scale, hipStream_t stream) {
+  if (n <= 0 || n % 2 != 0) return -1;
+  return tpar_allreduce(x, y, 2 * n, bufs, reds, flags, world, rank, npad, ep, done, err, true, scale, stream);
 }
 
 }  // extern "C"

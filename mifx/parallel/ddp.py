@@ -15,6 +15,15 @@ all-reduce, PyTorchJob DDP (`tf-job-simple-v1beta2.jsonnet:22-74`
 * optional bf16 wire format halves xGMI bytes for bandwidth-bound models (fp32 accumulate on the
   receiving side is RCCL's; the master gradient stays fp32).
 
+* buckets launch in bucket order on every rank (a bucket completing early waits for its predecessors), so the
+  collective sequence is the same on all ranks whatever order autograd finished them in;
+* exchange="ipc" replaces the RCCL collective by the peer-memory two-shot all-reduce of csrc/tp_allreduce.hip in fp32
+  (publish / reduce-scatter / all-gather kernels synchronised by device-side epoch flags, rank-order sum scaled by
+  1 / world in the kernel: identical bits on every rank): no host collective, so the whole data-parallel step --
+  forward, backward with the bucket exchanges overlapped on the side stream, optimizer -- captures into ONE hipGraph
+  (mifx.trainer.resnet_trainer). exchange="auto" takes it on CUDA when every rank can map its peers' memory (agreed
+  over the group; RCCL otherwise).
+
 `DataParallel.finish()` (or `step_ready()`) waits for outstanding work and writes averaged gradients
 back into `param.grad`. With `grad_as_bucket_view=True` there is nothing to write back: every `param.grad` IS a
 view of its bucket (same strides as the parameter, channels_last included), autograd accumulates straight into
@@ -46,14 +55,19 @@ class DataParallel:
 
     def __init__(self, module: torch.nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
                  wire_dtype: torch.dtype | None = None, broadcast_init: bool = True, average: bool = True,
-                 grad_as_bucket_view: bool = False):
+                 grad_as_bucket_view: bool = False, exchange: str = "rccl", force: bool = False):
+        """force: run the hooks and the exchange even on a one-rank group (a measurement of the data-parallel
+        machinery's own cost on one GPU: the exchange of a one-rank group is a copy through the peer buffers)."""
         if grad_as_bucket_view and wire_dtype is not None:
             raise ValueError("gradients as bucket views need the parameters' own dtype on the wire")
+        if exchange not in ("rccl", "ipc", "auto"):
+            raise ValueError(f"exchange: rccl, ipc or auto, not {exchange!r}")
         self.module = module
         self.views = bool(grad_as_bucket_view)
         self.pg = process_group if process_group is not None else (dist.group.WORLD if dist.is_initialized()
                                                                     else None)
         self.world = dist.get_world_size(self.pg) if self.pg is not None else 1
+        self.active = self.world > 1 or (force and self.pg is not None)
         self.average = average
         self.wire_dtype = wire_dtype
         self._sync = True
@@ -81,9 +95,34 @@ class DataParallel:
                 self._where[p] = (bi, pi)
         dev = params[0].device if params else torch.device("cpu")
         self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if self.world > 1 else []
+        self._next = 0  # the next bucket to launch (buckets launch in order)
+        self._ipc = None
+        if exchange != "rccl" and self.active:
+            self._ipc = self._open_ipc(dev, required=exchange == "ipc")
+        self.exchange = "ipc" if self._ipc is not None else ("rccl" if self.active else "none")
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if self.active else []
         if self.views:
             self.zero_grad()
+
+    def _open_ipc(self, dev, required: bool):
+        """The fp32 peer-memory all-reduce sized for the largest bucket, or None (auto: RCCL) when it cannot be set up
+        on every rank (the setup agrees over the group, so all ranks take the same exchange)."""
+        ok = dev.type == "cuda" and self.world <= 8 and all(b.buf.dtype == torch.float32 and b.numel % 2 == 0
+                                                             for b in self.buckets)
+        flags = [None] * self.world
+        dist.all_gather_object(flags, bool(ok), group=self.pg)
+        if not all(flags):
+            if required:
+                raise RuntimeError("DataParallel exchange='ipc' needs CUDA fp32 buckets of even size on <= 8 ranks")
+            return None
+        from .tp_ipc import IpcAllReduce
+
+        try:
+            return IpcAllReduce(self.pg, dev, max(b.numel for b in self.buckets), dtype=torch.float32)
+        except RuntimeError:
+            if required:
+                raise
+            return None
 
     def _view(self, b: _Bucket, pi: int) -> torch.Tensor:
         p, off = b.params[pi], b.offsets[pi]
@@ -129,13 +168,27 @@ class DataParallel:
             view.copy_(p.grad.reshape(-1))
             p.grad = view.view_as(p)
         if len(b.ready) == len(b.params):
+            self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        """Launch every complete bucket from the next one in bucket order on."""
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            if len(b.ready) != len(b.params):
+                return
             self._launch(b)
 
     def _launch(self, b: _Bucket) -> None:
+        assert b is self.buckets[self._next], "buckets launch in order"
+        self._next += 1
         if self._comm_stream is not None:
             self._comm_stream.wait_stream(torch.cuda.current_stream(b.buf.device))
             with torch.cuda.stream(self._comm_stream):
-                b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
+                if self._ipc is not None:  # averaged in the kernel; stream-ordered, graph-capturable
+                    self._ipc.all_reduce(b.buf, out=b.buf, scale=1.0 / self.world if self.average else 1.0)
+                    b.work = "ipc"
+                else:
+                    b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
         else:
             b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
 
@@ -155,12 +208,10 @@ class DataParallel:
     def finish(self) -> None:
         """Complete all bucket all-reduces (launching buckets whose params got no gradient) and write
         the averaged gradients back into `param.grad`."""
-        if self.world == 1 or not self._sync:
+        if not self.active or not self._sync:
             return
-        for b in self.buckets:
-            if b.work is None and self.views:  # unused params: their bucket views are still zero
-                self._launch(b)
-            elif b.work is None:  # unused params this step: contribute zeros for them
+        for b in self.buckets[self._next:]:  # (in order: an incomplete bucket holds back its successors)
+            if b.work is None and not self.views:  # unused params this step: contribute zeros for them
                 for pi, p in enumerate(b.params):
                     if pi not in b.ready:
                         off = b.offsets[pi]
@@ -168,9 +219,24 @@ class DataParallel:
                             b.buf[off:off + p.numel()].zero_()
                         else:
                             b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
-                self._launch(b)
+            # (views: unused params' bucket views are still zero)
+            self._launch(b)
+        self._next = 0
         cur = torch.cuda.current_stream(self.buckets[0].buf.device) if self._comm_stream is not None else None
         scale = 1.0 / self.world if self.average else 1.0
+        if self._ipc is not None:  # the kernels averaged in place; join the side stream
+            cur.wait_stream(self._comm_stream)
+            for b in self.buckets:
+                if not self.views:
+                    for pi, p in enumerate(b.params):
+                        off = b.offsets[pi]
+                        g = b.buf[off:off + p.numel()].view_as(p).to(p.dtype)
+                        if p.grad is None:
+                            p.grad = g.clone()
+                        else:
+                            p.grad.copy_(g)
+                b.work, b.ready = None, set()
+            return
         for b in self.buckets:
             b.work.wait()
             if cur is not None:

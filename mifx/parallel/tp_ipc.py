@@ -7,7 +7,9 @@ is then three kernels on the current stream (publish, reduce-scatter, all-gather
 epoch flags: no host collective, so a TP step captures into a hipGraph like a single-GPU step, and the result lands
 in a fresh tensor (no defensive `.clone()` of the input). The reduction is a rank-order fp32 sum rounded once to
 bf16: every rank gets the same bits. A peer that never arrives sets a sticky error flag after a bounded wait;
-`check()` raises. Used by mifx.parallel.tensor_parallel when `TPGroup.enable_ipc()` was called."""
+`check()` raises. Used by mifx.parallel.tensor_parallel when `TPGroup.enable_ipc()` was called, and -- with
+dtype=torch.float32 (rank-order fp32 sum, scaled once by the average) -- by mifx.parallel.ddp's exchange="ipc" for
+data-parallel gradient buckets inside the captured backward."""
 from __future__ import annotations
 
 import ctypes
@@ -17,7 +19,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _lib
-from ..ops._lib import I32, I64, VP, check, ptr, sig, stream_handle
+from ..ops._lib import F32, I32, I64, VP, check, ptr, sig, stream_handle
 from .xgmi import MAX_WORLD, _fns as _xg_fns
 
 
@@ -25,14 +27,20 @@ from .xgmi import MAX_WORLD, _fns as _xg_fns
 def _fns():
     lib = _lib.load("tp_allreduce")
     return {"chunk": sig(lib, "mifx_tpar_chunk", []),
-            "ar": sig(lib, "mifx_tpar_allreduce", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, VP])}
+            "ar": sig(lib, "mifx_tpar_allreduce", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, VP]),
+            "ar32": sig(lib, "mifx_tpar_allreduce_f32", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, F32, VP])}
 
 
 class IpcAllReduce:
-    """All-reduce (sum) of bf16 tensors of up to `max_elems` elements over the ranks of `pg`, one GPU each (or
-    ranks sharing one GPU in rehearsals: the IPC path is the same)."""
+    """All-reduce (sum) of bf16 (or fp32) tensors of up to `max_elems` elements over the ranks of `pg`, one GPU each
+    (or ranks sharing one GPU in rehearsals: the IPC path is the same)."""
 
-    def __init__(self, pg, device, max_elems: int):
+    def __init__(self, pg, device, max_elems: int, dtype: torch.dtype = torch.bfloat16):
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("IPC all-reduce: bf16 or fp32")
+        self.dtype = dtype
+        if dtype == torch.float32:
+            max_elems = 2 * int(max_elems)  # the buffers are sized in bf16-element units
         self.pg, self.device = pg, torch.device(device)
         self.rank, self.world = dist.get_rank(pg), dist.get_world_size(pg)
         if not 1 <= self.world <= MAX_WORLD:
@@ -100,16 +108,26 @@ class IpcAllReduce:
             xf["free"](p)
         self._own = []
 
-    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """Sum of `x` over the ranks (bf16, any shape, numel % 4 == 0, <= max_elems) into `out` (default: a new
-        tensor; `out=x` reduces in place). Stream-ordered and graph-capturable."""
-        if x.dtype != torch.bfloat16 or x.device != self.device:
-            raise ValueError("IPC all-reduce takes bf16 tensors on the group's device")
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None, scale: float = 1.0) -> torch.Tensor:
+        """Sum of `x` over the ranks (the group's dtype, any shape; bf16: numel % 4 == 0, fp32: even numel; <=
+        max_elems) into `out` (default: a new tensor; `out=x` reduces in place), times `scale` (fp32 only).
+        Stream-ordered and graph-capturable."""
+        if x.dtype != self.dtype or x.device != self.device:
+            raise ValueError(f"IPC all-reduce takes {self.dtype} tensors on the group's device")
         x = x.contiguous()
         n = x.numel()
+        y = torch.empty_like(x) if out is None else out
+        if self.dtype == torch.float32:
+            if n % 2 or 2 * n > self.npad:
+                raise ValueError(f"{n} fp32 elements: need an even count <= {self.npad // 2}")
+            check(_fns()["ar32"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank,
+                                 self.npad, ptr(self.ep), ptr(self.done), ptr(self.err), float(scale),
+                                 stream_handle(self.device)), "mifx_tpar_allreduce_f32")
+            return y
+        if scale != 1.0:
+            raise ValueError("scale is for the fp32 path")
         if n % 4 or n > self.npad:
             raise ValueError(f"{n} elements: need a multiple of 4 and <= {self.npad}")
-        y = torch.empty_like(x) if out is None else out
         check(_fns()["ar"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank, self.npad,
                            ptr(self.ep), ptr(self.done), ptr(self.err), stream_handle(self.device)),
               "mifx_tpar_allreduce")

@@ -5,9 +5,11 @@ dataset with the fused crop/flip/normalize HIP kernel, bf16 autocast in channels
 
 On the GPU the step is captured into hipGraphs after `graph_warmup` eager steps (graph=True, the default there):
 graph A = gradient zeroing + every micro-batch's input kernel, forward and backward (the step counter, learning rate
-and sample indices are device tensors written before each replay), then -- data-parallel -- the bucket all-reduces
-run eagerly on RCCL (collectives stay outside the graphs) and graph B applies SGD; one graph when there is no
-data parallelism.
+and sample indices are device tensors written before each replay). Data-parallel with the peer-memory exchange
+(DataParallel exchange="ipc", the default on the GPU: MIFX_DP_EXCHANGE=auto|ipc|rccl) the bucket all-reduces are
+kernels launched on the side stream as each bucket's gradients complete -- overlapped with the rest of the backward
+and captured with it -- and SGD follows in the same graph: ONE graph per step, nothing eager between. With the RCCL
+exchange the all-reduces run eagerly between graph A and graph B (SGD). One graph without data parallelism.
 
 `python -m torch.distributed.run --nproc-per-node 8 -m mifx.trainer.resnet_trainer` prints images/sec."""
 from __future__ import annotations
@@ -44,7 +46,7 @@ class ResNetTrainer:
     def __init__(self, batch: int, device, images: torch.Tensor, labels: torch.Tensor, num_classes: int = 1000,
                  lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 5e-5, warmup_steps: int = 100,
                  process_group=None, mean=IMAGENET_MEAN, std=IMAGENET_STD, seed: int = 0, crop: int = 224,
-                 accum_steps: int = 1, graph: bool | None = None, graph_warmup: int = 2):
+                 accum_steps: int = 1, graph: bool | None = None, graph_warmup: int = 2, force_dp: bool = False):
         """batch: examples per micro-batch per replica; accum_steps micro-batches (each with its own BatchNorm
         statistics) are summed into one update. A data-parallel step over W ranks trains on W x accum_steps x batch
         examples: the global sample of the step is drawn from (seed, step) and rank r takes micro-batches
@@ -58,7 +60,9 @@ class ResNetTrainer:
         torch.manual_seed(seed)
         self.model = resnet50_v2(num_classes).to(self.device).to(memory_format=torch.channels_last)
         self._bn_count = defer_batch_counts(self.model)  # one counter kernel per forward, not one per BatchNorm
-        self.dp = DataParallel(self.model, process_group, grad_as_bucket_view=True) \
+        exch = os.environ.get("MIFX_DP_EXCHANGE", "auto") if self.device.type == "cuda" else "rccl"
+        self.dp = DataParallel(self.model, process_group, grad_as_bucket_view=True, exchange=exch,
+                               bucket_cap_mb=float(os.environ.get("MIFX_DP_BUCKET_MB", "16")), force=force_dp) \
             if process_group is not None else None
         decay = [p for n, p in self.model.named_parameters() if p.ndim > 1]
         no_decay = [p for n, p in self.model.named_parameters() if p.ndim <= 1]
@@ -154,7 +158,7 @@ class ResNetTrainer:
         for pg in self.opt.param_groups:
             pg["lr"] = self._lr()  # (kept current for checkpoints / eager fallbacks)
         self._gA.replay()
-        if self.dp is not None:
+        if self._gB is not None:
             self.dp.finish()  # bucket all-reduces (RCCL) in place on the gradient views, averaged
             self._gB.replay()
         self.step_idx += 1
@@ -173,7 +177,8 @@ class ResNetTrainer:
         else:
             torch._foreach_zero_([p.grad for p in self.model.parameters() if p.grad is not None])
         total = None
-        ctx = self.dp.no_sync() if self.dp is not None else contextlib.nullcontext()
+        in_graph = self.dp is not None and self.dp.exchange == "ipc"  # the exchange captures with the backward
+        ctx = self.dp.no_sync() if self.dp is not None and not in_graph else contextlib.nullcontext()
         with ctx:
             for m in range(self.accum):
                 mb = self.rank * self.accum + m
@@ -191,9 +196,14 @@ class ResNetTrainer:
                     with hg.deferred_weight_grads():
                         loss.backward()
                     hg.flush_weight_grads()
+                elif in_graph and m < self.accum - 1:
+                    with self.dp.no_sync():
+                        loss.backward()
                 else:
                     loss.backward()
                 total = loss.detach() if total is None else total + loss.detach()
+        if in_graph:
+            self.dp.finish()  # joins the side stream: every bucket exchanged and averaged
         return total
 
     @torch.no_grad()
@@ -224,11 +234,12 @@ class ResNetTrainer:
             raise RuntimeError("capture needs the SGD momentum buffers of an eager step first")
         torch.cuda.synchronize(self.device)
         self._gA = torch.cuda.CUDAGraph()
+        one = self.dp is None or self.dp.exchange == "ipc"
         with torch.cuda.graph(self._gA):
             self._static_loss = self._fwd_bwd_captured()
-            if self.dp is None:
+            if one:
                 self._sgd_captured()
-        if self.dp is not None:
+        if not one:
             self._gB = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._gB):
                 self._sgd_captured()
@@ -316,8 +327,18 @@ def main(argv=None):
     env = mdist.init()
     dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     imgs, labels = synthetic_imagenet(a.images, seed=env.rank, device=dev)
-    pg = torch.distributed.group.WORLD if env.world_size > 1 else None
-    tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=pg, warmup_steps=10, graph=not a.no_graph)
+    force = os.environ.get("MIFX_DP_FORCE") == "1" and env.world_size == 1
+    if force:  # the data-parallel machinery on one rank (hooks, bucket exchange): its overhead, measured
+        import socket
+
+        with socket.socket() as s_:
+            s_.bind(("127.0.0.1", 0))
+            port = s_.getsockname()[1]
+        torch.distributed.init_process_group("nccl" if dev.type == "cuda" else "gloo",
+                                             init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    pg = torch.distributed.group.WORLD if env.world_size > 1 or force else None
+    tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=pg, warmup_steps=10, graph=not a.no_graph,
+                       force_dp=force)
     for i in range(a.warmup):  # first steps include MIOpen solver search/compile: report progress
         t1 = time.perf_counter()
         with heartbeat("resnet warmup"):
@@ -343,6 +364,8 @@ def main(argv=None):
                           "n_gpus": env.world_size, "batch_per_gpu": a.batch, "ms_per_step": 1e3 * dt / a.steps,
                           "loss": float(loss), "dtype": "bf16", "data": "synthetic ImageNet-shaped (HBM-resident)",
                           "parallelism": f"dp{env.world_size}", "hipgraph": tr.use_graph,
+                          "dp_exchange": tr.dp.exchange if tr.dp is not None else "none",
+                          "graphs_per_step": 0 if not tr.use_graph else (2 if tr._gB is not None else 1),
                           "deterministic": bool(torch.backends.cudnn.deterministic)}), flush=True)
     mdist.shutdown()
 

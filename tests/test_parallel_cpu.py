@@ -122,3 +122,47 @@ def test_bucketed_ddp_matches_single_process(views):
         opt.step()
     for k, v in net.state_dict().items():
         np.testing.assert_allclose(got[k].numpy(), v.numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def _order_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    torch.manual_seed(0)
+    net = _Net()
+    dp = DataParallel(net, bucket_cap_mb=0.01, grad_as_bucket_view=True, exchange="auto")
+    assert dp.exchange == "rccl"  # CPU: no peer memory, the agreed fallback
+    launched = []
+    orig = dp._launch
+
+    def rec(b):
+        launched.append(dp.buckets.index(b))
+        orig(b)
+
+    dp._launch = rec
+    params = [p for b in dp.buckets for p in b.params]
+    order = list(range(len(params)))
+    if rank == 1:
+        order.reverse()  # the last bucket completes first on this rank
+    for i in order:
+        p = params[i]
+        p.grad.fill_(float(rank + 1))
+        dp._on_grad(p)
+    dp.finish()
+    ok = all(bool((p.grad == 1.5).all()) for p in params)  # (1 + 2) / 2
+    torch.save({"launched": launched, "ok": ok, "n": len(dp.buckets)}, os.path.join(out_dir, f"order{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_buckets_launch_in_order_whatever_completes_first():
+    """Collectives must be issued in the same sequence on every rank: a bucket that completes before its
+    predecessors waits for them (rank 1 completes the buckets in reverse)."""
+    world, port = 2, _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_order_worker, args=(world, port, d), nprocs=world, start_method="spawn")
+        r = [torch.load(os.path.join(d, f"order{k}.pt"), weights_only=True) for k in range(world)]
+    for x in r:
+        assert x["ok"] and x["launched"] == list(range(x["n"])), x
+
+
+def test_ddp_ipc_exchange_needs_cuda():
+    with pytest.raises(ValueError):
+        DataParallel(_Net(), exchange="nope")

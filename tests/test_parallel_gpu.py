@@ -86,6 +86,8 @@ _RES_STEPS = 3
 def _resnet_run(world: int, rank: int, out: str) -> None:
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
 
+    os.environ["MIFX_DP_EXCHANGE"] = os.environ.get("MIFX_TEST_EXCHANGE", "auto")
+
     imgs, labels = synthetic_imagenet(64, size=72, classes=10, seed=0)  # same data on every rank
     # one process accumulates the 2 micro-batches that the 2 ranks train on (ResNetTrainer's global sample)
     tr = ResNetTrainer(4, "cuda:0", imgs, labels, num_classes=10, lr=0.05, warmup_steps=1, crop=64,
@@ -99,11 +101,15 @@ def _resnet_run(world: int, rank: int, out: str) -> None:
     torch.cuda.synchronize()
     params = {k: v.detach().float().cpu() for k, v in tr.model.named_parameters()}
     stats = {k: v.detach().float().cpu() for k, v in tr.model.named_buffers() if v.is_floating_point()}
-    torch.save({"losses": losses, "state": params, "stats": stats}, f"{out}.{world}.{rank}")
+    info = {"exchange": tr.dp.exchange if tr.dp is not None else "none", "graphs": (tr._gA is not None,
+                                                                                 tr._gB is not None)}
+    if tr.dp is not None and tr.dp._ipc is not None:
+        tr.dp._ipc.check()
+    torch.save({"losses": losses, "state": params, "stats": stats, "info": info}, f"{out}.{world}.{rank}")
 
 
-def _resnet_worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _resnet_worker(rank, world, port, out, exchange="auto"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MIFX_TEST_EXCHANGE=exchange)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         _resnet_run(world, rank, out)
@@ -111,13 +117,18 @@ def _resnet_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single():
+@pytest.mark.parametrize("exchange", ["ipc", "rccl"])
+def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single(exchange):
+    """2 ranks sharing cuda:0 vs one process accumulating both micro-batches. exchange="ipc": the bucket all-reduces
+    are the peer-memory kernels on the side stream, captured with the backward and SGD in ONE graph (steps 3+);
+    "rccl": the process group's collective (gloo here) eager between graph A and graph B."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
-        mp.start_processes(_resnet_worker, args=(2, _port(), out), nprocs=2, start_method="spawn")
+        mp.start_processes(_resnet_worker, args=(2, _port(), out, exchange), nprocs=2, start_method="spawn")
         mp.start_processes(_resnet_worker, args=(1, _port(), out), nprocs=1, start_method="spawn")
         r0, r1 = (torch.load(f"{out}.2.{r}", weights_only=True) for r in range(2))
         one = torch.load(f"{out}.1.0", weights_only=True)
+    assert r0["info"]["exchange"] == exchange and r0["info"]["graphs"] == (True, exchange == "rccl"), r0["info"]
     assert all(torch.isfinite(torch.tensor(r0["losses"])))
     # rank r trains micro-batch r of every step's global sample; the single process accumulates both micro-batches
     # (loss / 2 each): the averaged DP gradient (g0 + g1) / 2 and the accumulated g0 / 2 + g1 / 2 are the same
