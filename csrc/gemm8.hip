@@ -93,19 +93,44 @@ __device__ __forceinline__ v8bf tr_frag(const unsigned char* p1, const unsigned 
   return __builtin_bit_cast(v8bf, r);
 }
 
+// Implicit-GEMM 3x3 convolution over NHWC activations (ResNet-50's bottleneck conv2, BASELINE config 5): input
+// [Nb][H][W][C] (C a power of two >= 64), output pixels [Nb][OH][OW], taps (r, s) in 0..2, stride / pad. The GEMM's
+// reduction index is k = (3 r + s) C + c, so a 64-deep K-tile is one tap and a 64-channel slice: each DMA row of the
+// gathered operand is one pixel shifted by the tap -- or, outside the image, the zero page below (the DMA then fills
+// the LDS row with zeros; no predicated loads, no separate padding pass). CV 1 (NT, forward / stride-1 input
+// gradient): the X rows are output pixels, gathered per K-tile; weights [Cout][3][3][C] (channels_last). CV 2 (TN,
+// weight gradient dW[Cout][3][3][C] = sum_pixels dY^T . X_tap): the B token rows are output pixels, gathered from X;
+// a BN-wide column block is one tap (C % BN == 0). Divisions by OW and OH OW in the gather are multiply-high
+// (`ow_mul` / `ohw_mul`, host-computed; exact for x < 2^31).
+struct Geo {
+  int H, W, C, OH, OW, stride, pad, cshift;
+  unsigned ow_mul;
+  int ow_sh;
+  unsigned ohw_mul;
+  int ohw_sh;
+};
+__device__ __attribute__((aligned(16))) bf16 g_zero_page[64] = {};
+__device__ __forceinline__ int fdiv(int x, unsigned mul, int sh) {
+  return (int)((__umulhi((unsigned)x, mul) + (unsigned)x) >> sh);
+}
+
 // grouped TN problems: C[M, N] (bf16, ldc N) = A[T, M]^T B[T, N]; tiles of problem i are [first[i], first[i + 1])
-constexpr int MAXP = 64;
+constexpr int MAXP = 48;  // (the problem table travels in the kernel arguments: 48 x 64 bytes)
 // Problem i: C_i[M, N] = A_i[T, M]^T B_i[T, N]. bf16 problems (F32 clear): C bf16, one token split, staged bf16
 // stores. fp32 problems (F32 set): the token range is cut into S chunks of `chunk` rows (the last shorter), each
 // (tile, chunk) item stores its fp32 partial into P[s][M][N]; gemm8_tn_reduce then ADDS sum_s P[s] (fixed order) into
 // the fp32 destination C -- the weight gradients of convolutions, whose token count (N H W = 12k-800k rows) is far
 // longer than their output is wide. TILE128: 128 x 128 tiles for this problem (dimensions % 256 != 0).
 constexpr int F32 = 1, TILE128 = 2, ACCUM = 4;  // ACCUM: C += sum of the partials (else C = the sum)
+// CONV: B is a 3x3 convolution's input gathered per output pixel (CV 2, geometry in device memory at `geo`); the
+// problem is dW[M = Cout][N = 9 C] = dY^T . X_taps, F32 only
+constexpr int CONV = 8;
 struct Prob {
   const bf16* A;
   const bf16* B;
   void* C;
   float* P;
+  const Geo* geo;
   int M, N, T, chunk, S, flags;
 };
 struct Group {
@@ -121,12 +146,14 @@ struct Group {
 constexpr int vm_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
 
 // The body: one BM x BN tile of Y = X W^T (NT: X [M, K], W [N, K] row-major) or of C = A^T B (TN: A [K, M],
-// B [K, N] row-major; X := A, W := B, "K" = tokens), m0 / n0 its origin.
-template <int BM, int BN, int EPI, typename P, bool TN>
+// B [K, N] row-major; X := A, W := B, "K" = tokens), m0 / n0 its origin. CV: implicit-convolution operand (above);
+// tok0: the first token of this item's chunk (CV 2: B is then the whole conv input, gathered by pixel index).
+template <int BM, int BN, int EPI, typename P, bool TN, int CV = 0>
 __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                            const P* __restrict__ bias, bf16* __restrict__ Y, bf16* __restrict__ Z,
                                            int M, int N, int K, float* __restrict__ part, int m0, int n0,
-                                           unsigned char* lds) {
+                                           unsigned char* lds, const Geo& geo = Geo{}, int tok0 = 0) {
+  static_assert(CV == 0 || (CV == 1 && !TN) || (CV == 2 && TN), "conv gather: NT rows (1) or TN B rows (2)");
   constexpr int HA = BM / 2, HB = BN / 2;            // rows (NT) / columns (TN) per half-tile
   constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // NT: 64 bf16 per row; TN: 64 token rows of HA bf16
   constexpr int XR = HA * 8 / NT, WR = HB * 8 / NT;    // DMAs per thread per half-tile
@@ -170,10 +197,72 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       boff[i] = (n0 + row) * K + 8 * swz(row, qq & 7);
     }
   }
+  // CV 1: each A DMA row's output pixel, decoded once: image base pixel, top-left input coordinate, swizzled chunk
+  int cpix[CV == 1 ? 2 : 1][CV == 1 ? XR : 1], cih[CV == 1 ? 2 : 1][CV == 1 ? XR : 1],
+      ciw[CV == 1 ? 2 : 1][CV == 1 ? XR : 1], cch[CV == 1 ? XR : 1];
+  if constexpr (CV == 1) {
+    const int ohw = geo.OH * geo.OW;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int qq = i * NT + tid, row = qq >> 3;
+      cch[i] = 8 * swz(row, qq & 7);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int m = m0 + hh * HA + row, nb = m / ohw, rem = m - nb * ohw, oh = rem / geo.OW, ow = rem - oh * geo.OW;
+        cpix[hh][i] = nb * geo.H * geo.W;
+        cih[hh][i] = oh * geo.stride - geo.pad;
+        ciw[hh][i] = ow * geo.stride - geo.pad;
+      }
+    }
+  }
+  // CV 2: each B DMA's token row within the K-tile and its logical chunk
+  int btok[CV == 2 ? WR : 1], bcol[CV == 2 ? WR : 1];
+  if constexpr (CV == 2) {
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const int qq = i * NT + tid, t = qq / CPB, pc = qq % CPB;
+      int c = pc - rot<CPB>(t);
+      c = c < 0 ? c + CPB : c;
+      btok[i] = t;
+      bcol[i] = 8 * c;
+    }
+  }
   // half h (0 A0, 1 B0, 2 A1, 3 B1) of K-tile t into LDS buffer t & 1
   auto stage = [&](int h, int t) {
     unsigned char* buf = lds + (t & 1) * BUF;
     const int k0 = t * BK;
+    if (CV == 1 && (h == 0 || h == 2)) {  // gathered pixel rows of tap k0 / C, channels [k0 % C, + 64)
+      unsigned char* dst = buf + (h == 0 ? OFF_A0 : OFF_A1);
+      const int hh = h >> 1, tap = k0 >> geo.cshift, c0 = k0 & (geo.C - 1), r = tap / 3, sx = tap - 3 * r;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        const int ih = cih[hh][i] + r, iw = ciw[hh][i] + sx;
+        const bool ok = (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
+        const bf16* src = ok ? X + ((size_t)(cpix[hh][i] + ih * geo.W + iw) << geo.cshift) + c0 + cch[i] : g_zero_page;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(dst + (i * NT + 64 * w) * 16), 16,
+                                         0, 0);
+      }
+      return;
+    }
+    if (CV == 2 && (h == 1 || h == 3)) {  // gathered token (pixel) rows for this tile's tap
+      unsigned char* dst = buf + (h == 1 ? OFF_B0 : OFF_B1);
+      const int col = n0 + (h == 3 ? HB : 0), tap = col >> geo.cshift, c0 = col & (geo.C - 1), r = tap / 3,
+                sx = tap - 3 * r, ohw = geo.OH * geo.OW;
+#pragma unroll
+      for (int i = 0; i < WR; ++i) {
+        const int x = tok0 + k0 + btok[i], nb = fdiv(x, geo.ohw_mul, geo.ohw_sh), rem = x - nb * ohw,
+                  oh = fdiv(rem, geo.ow_mul, geo.ow_sh), ow = rem - oh * geo.OW;
+        const int ih = oh * geo.stride - geo.pad + r, iw = ow * geo.stride - geo.pad + sx;
+        const bool ok = (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
+        const bf16* src =
+            ok ? W + ((size_t)((nb * geo.H + ih) * geo.W + iw) << geo.cshift) + c0 + bcol[i] : g_zero_page;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(dst + (i * NT + 64 * w) * 16), 16,
+                                         0, 0);
+      }
+      return;
+    }
     if (h == 0 || h == 2) {
       unsigned char* dst = buf + (h == 0 ? OFF_A0 : OFF_A1);
       const bf16* src = TN ? X + (size_t)k0 * M + (h == 2 ? HA : 0) : X + (h == 2 ? HA * K : 0) + k0;
@@ -563,6 +652,18 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
   gemm8_tile<BM, BN, EPI, P, false>(X, W, bias, Y, Z, M, N, K, part, (tile / nb_n) * BM, (tile % nb_n) * BN, lds);
 }
 
+// implicit-GEMM 3x3 convolution (CV 1): Y[Nb OH OW, N] = gathered X . W[N, 9 C]^T, epilogues as gemm8_nt
+template <int BM, int BN, int EPI, typename P>
+__global__ __launch_bounds__(NT, 1) void gemm8_conv(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                    const P* __restrict__ bias, bf16* __restrict__ Y,
+                                                    bf16* __restrict__ Z, int M, int N, int K,
+                                                    float* __restrict__ part, const Geo geo) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tile = xcd_tile(), nb_n = N / BN;
+  gemm8_tile<BM, BN, EPI, P, false, 1>(X, W, bias, Y, Z, M, N, K, part, (tile / nb_n) * BM, (tile % nb_n) * BN, lds,
+                                       geo);
+}
+
 // grouped TN: each workgroup's (problem, item) from the table by binary search; an item is (tile, token chunk); tiles
 // of a problem run m-fastest in groups of 4 m-blocks (an XCD's consecutive tiles share B column strips in its L2)
 template <int BM, int BN, bool TN>
@@ -576,6 +677,17 @@ __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, 
   const int m0 = (first_m + wi % gsz) * bm, n0 = (wi / gsz) * bn;
   const int t0 = sp * p.chunk, len = min(p.chunk, p.T - t0);
   const bf16* A = p.A + (size_t)t0 * p.M;
+  if (p.flags & CONV) {  // (F32 only; the B rows are gathered from the whole input by pixel index t0 + ...)
+    const Geo geo = *p.geo;
+    float* P = p.P + (size_t)sp * p.M * p.N;
+    if (p.flags & TILE128)
+      gemm8_tile<BM / 2, BN / 2, EPI_F32, bf16, true, 2>(A, p.B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0,
+                                                         lds, geo, t0);
+    else
+      gemm8_tile<BM, BN, EPI_F32, bf16, true, 2>(A, p.B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
+                                                 geo, t0);
+    return;
+  }
   const bf16* B = p.B + (size_t)t0 * p.N;
   if (p.flags & F32) {
     float* P = p.P + (size_t)sp * p.M * p.N;
@@ -659,6 +771,51 @@ int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int
   return (int)hipGetLastError();
 }
 
+template <int BM, int BN, int EPI>
+int launch_conv(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, float* part,
+                const Geo& geo, hipStream_t st) {
+  constexpr int LDS = lds_bytes<BM, BN, EPI>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8_conv<BM, BN, EPI, bf16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm8_conv<BM, BN, EPI, bf16>), dim3((M / BM) * (N / BN)), dim3(NT), LDS, st, (const bf16*)X,
+                     (const bf16*)W, (const bf16*)bias, (bf16*)Y, (bf16*)Z, M, N, K, part, geo);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN>
+int dispatch_conv(int epi, const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K,
+                  float* part, const Geo& geo, hipStream_t st) {
+  switch (epi) {
+    case EPI_NONE: return launch_conv<BM, BN, EPI_NONE>(X, W, nullptr, Y, nullptr, M, N, K, nullptr, geo, st);
+    case EPI_STATS: return launch_conv<BM, BN, EPI_STATS>(X, W, nullptr, Y, nullptr, M, N, K, part, geo, st);
+    case EPI_BNBWD: return launch_conv<BM, BN, EPI_BNBWD>(X, W, bias, Y, Z, M, N, K, part, geo, st);
+  }
+  return -1;
+}
+
+Geo make_geo(int H, int W, int C, int OH, int OW, int stride, int pad) {
+  Geo g{H, W, C, OH, OW, stride, pad, 0, 0u, 0, 0u, 0};
+  while ((1 << g.cshift) < C) ++g.cshift;
+  auto magic = [](unsigned d, unsigned& mul, int& sh) {  // x / d == (umulhi(x, mul) + x) >> sh for x < 2^31
+    sh = 0;
+    while ((1ull << sh) < d) ++sh;
+    mul = (unsigned)(((1ull << 32) * ((1ull << sh) - d)) / d + 1);
+  };
+  magic((unsigned)OW, g.ow_mul, g.ow_sh);
+  magic((unsigned)(OH * OW), g.ohw_mul, g.ohw_sh);
+  return g;
+}
+
+bool geo_ok(int Nb, int H, int W, int C, int OH, int OW, int stride, int pad) {
+  return Nb > 0 && H > 0 && W > 0 && C >= 64 && (C & (C - 1)) == 0 && stride >= 1 && stride <= 2 && pad >= 0 &&
+         pad <= 2 && OH == (H + 2 * pad - 3) / stride + 1 && OW == (W + 2 * pad - 3) / stride + 1 &&
+         (long long)Nb * H * W * C < (1ll << 31) && (long long)Nb * OH * OW < (1ll << 31);
+}
+
 template <int BM, int BN>
 int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N,
              int K, float* part, hipStream_t st) {
@@ -730,6 +887,42 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
   }
 }
 
+// 3x3 convolution as an implicit GEMM (see Geo): x bf16 NHWC [Nb][H][W][C], w bf16 [N][3][3][C] (channels_last
+// weight), y bf16 [Nb OH OW][N]; epi 0 none, 5 per-tile BatchNorm statistics of y (as mifx_gemm8_nt), 8 y is a
+// BatchNorm + ReLU output gradient (bias = that BatchNorm's input [Nb OH OW][N], Z = its statistics) with the per-tile
+// backward sums. Nb OH OW % BM == 0, N % BN == 0.
+int mifx_gemm8_conv3x3(int cfg, int epi, const void* x, const void* w, const void* bias, void* y, void* Z, float* part,
+                       int Nb, int H, int W, int C, int N, int stride, int pad, hipStream_t st) {
+  const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
+  if (cfg < 0 || cfg >= m || x == nullptr || w == nullptr || y == nullptr) return -1;
+  const int OH = (H + 2 * pad - 3) / stride + 1, OW = (W + 2 * pad - 3) / stride + 1;
+  if (!geo_ok(Nb, H, W, C, OH, OW, stride, pad)) return -1;
+  const Cfg c = kCfgs[cfg];
+  const int M = Nb * OH * OW, K = 9 * C;
+  if (M % c.bm || N <= 0 || N % c.bn || (long long)N * K >= (1ll << 31)) return -1;
+  if (epi != 0 && epi != 5 && epi != 8) return -1;
+  if (epi != 0 && part == nullptr) return -1;
+  if (epi == 8 && (bias == nullptr || Z == nullptr || (uintptr_t)bias % 16)) return -1;
+  if ((uintptr_t)x % 16 || (uintptr_t)w % 16 || (uintptr_t)y % 16) return -1;
+  const Geo g = make_geo(H, W, C, OH, OW, stride, pad);
+  switch (cfg) {
+    case 0: return dispatch_conv<256, 256>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+    case 1: return dispatch_conv<256, 128>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+    case 2: return dispatch_conv<128, 256>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+    default: return dispatch_conv<128, 128>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+  }
+}
+
+// The device-side geometry record of a 3x3 convolution for mifx_gemm8_tn_grouped's CONV problems (48 bytes).
+int mifx_gemm8_geo_bytes() { return (int)sizeof(Geo); }
+int mifx_gemm8_geo(int Nb, int H, int W, int C, int stride, int pad, void* out) {
+  const int OH = (H + 2 * pad - 3) / stride + 1, OW = (W + 2 * pad - 3) / stride + 1;
+  if (out == nullptr || !geo_ok(Nb, H, W, C, OH, OW, stride, pad)) return -1;
+  const Geo g = make_geo(H, W, C, OH, OW, stride, pad);
+  __builtin_memcpy(out, &g, sizeof(Geo));
+  return 0;
+}
+
 // Grouped TN GEMM: for i < n, C_i[M_i, N_i] = A_i[T_i, M_i]^T B_i[T_i, N_i] (bf16 row-major operands, fp32
 // accumulation), all in ONE launch. flags_i: bit 0 F32 -- C_i is fp32 and receives the product (+= with bit 2 ACCUM,
 // else =), computed in
@@ -738,7 +931,8 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
 // == 0, 16-byte aligned operands, n <= 64. ws: fp32 workspace of sum over F32 problems of S_i M_i N_i floats
 // (S_i = ceil(T_i / chunk_i)), may be null without F32 problems. Returns the number of work items (> 0) or < 0.
 int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, void* const* C, const int* M,
-                          const int* N, const int* T, const int* chunk, const int* flags, float* ws, hipStream_t st) {
+                          const int* N, const int* T, const int* chunk, const int* flags, float* ws,
+                          const void* const* geos, hipStream_t st) {
   if (n <= 0 || n > MAXP) return -1;
   Group g{};
   RedGroup rg{};
@@ -751,7 +945,13 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
     if (M[i] % tb || N[i] % tb || T[i] % BK || chunk[i] <= 0 || chunk[i] % BK) return -1;
     if (!(fl & F32) && chunk[i] != T[i]) return -1;
     if ((uintptr_t)A[i] % 16 || (uintptr_t)B[i] % 16 || (uintptr_t)C[i] % 16) return -1;
-    if ((long long)T[i] * M[i] >= (1ll << 31) || (long long)T[i] * N[i] >= (1ll << 31)) return -1;
+    if ((long long)T[i] * M[i] >= (1ll << 31)) return -1;
+    if (!(fl & CONV) && (long long)T[i] * N[i] >= (1ll << 31)) return -1;
+    const Geo* geo = nullptr;
+    if (fl & CONV) {  // geometry in device memory; N = 9 C with C % (tile width) == 0 (one tap per column block)
+      if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % 9 || (N[i] / 9) % tb) return -1;
+      geo = (const Geo*)geos[i];
+    }
     const int S = (T[i] + chunk[i] - 1) / chunk[i];
     float* P = nullptr;
     if (fl & F32) {
@@ -764,7 +964,7 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
       uniform256 = false;
     }
     if (fl & TILE128) uniform256 = false;
-    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], C[i], P, M[i], N[i], T[i], chunk[i], S, fl};
+    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], C[i], P, geo, M[i], N[i], T[i], chunk[i], S, fl};
     g.first[i] = items;
     items += (M[i] / tb) * (N[i] / tb) * S;
   }

@@ -95,6 +95,14 @@ def _fused_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
         and conv.groups == 1 and conv1x1.eligible(x, conv.weight)
 
 
+def _fused3_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    from ..ops import conv3x3
+
+    return FUSED_1X1 and conv.kernel_size == (3, 3) and conv.padding == (1, 1) and conv.bias is None \
+        and conv.groups == 1 and conv.stride[0] == conv.stride[1] and conv.dilation == (1, 1) \
+        and conv3x3.eligible(x, conv.weight, conv.stride[0], 1)
+
+
 class PreActBottleneck(nn.Module):
     expansion = 4
 
@@ -115,6 +123,7 @@ class PreActBottleneck(nn.Module):
         producing GEMM already reduced. Returns the un-added (branch, shortcut) pair, or a `Fused` sum when conv3 ran
         on the GEMM kernel, for the next block / the final BN."""
         from ..ops.conv1x1 import conv1x1
+        from ..ops.conv3x3 import conv3x3
 
         if isinstance(x, Fused):
             pre, s = self.bn0.forward_tiles(x.t, x.part)
@@ -134,7 +143,12 @@ class PreActBottleneck(nn.Module):
             h = self.bn1.forward_tiles(y, part)[0]
         else:
             h = self.bn1(self.conv1(pre))
-        h = self.bn2(self.conv2(h))
+        if _fused3_ok(self.conv2, h):
+            # 3x3 on the implicit-GEMM kernel: BN2's statistics in its epilogue; h (BN1's output) feeds only conv2
+            y, part = conv3x3(h, self.conv2.weight, self.conv2.stride[0], stats=True, bn_input=True)
+            h = self.bn2.forward_tiles(y, part)[0]
+        else:
+            h = self.bn2(self.conv2(h))
         if _fused_ok(self.conv3, h) and sc.shape[1] == self.conv3.out_channels:
             return Fused(*conv1x1(h, self.conv3.weight, residual=sc, stats=True, bn_input=True))
         return self.conv3(h), sc

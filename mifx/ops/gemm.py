@@ -282,20 +282,48 @@ def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor):
     return ph
 
 
+def defer_conv3x3_weight_grad_f32(dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int):
+    """As defer_weight_grad_f32 for a 3x3 convolution: dy2 [Nb OH OW, Cout] bf16, x the NHWC bf16 input [Nb, H, W, C],
+    w the fp32 channels_last [Cout, C, 3, 3] weight; the flush gathers x per output pixel and tap. None when not
+    deferring."""
+    if not (_DEFER["on"] and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and w.dtype == torch.float32 and w.is_contiguous(memory_format=torch.channels_last)
+            and os.environ.get("MIFX_DEFER_DW", "1") != "0"):
+        return None
+    nb, h, w_, c = x.shape
+    cout = w.shape[0]
+    if cout % 128 or c % 128 or dy2.shape[0] % 64:
+        return None
+    geo = conv_geo(nb, h, w_, c, stride, pad, x.device)
+    native_stats.count("conv3x3_dW", True)
+    overwrite = w.grad is None
+    ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
+    _DEFER["pending_f32"].append((dy2.contiguous(), x.contiguous(), w, ph.data_ptr() if overwrite else None, geo))
+    return ph
+
+
 def flush_weight_grads() -> int:
     """Run every recorded weight gradient as one grouped launch into the weights' .grad; returns how many."""
     pf, _DEFER["pending_f32"] = _DEFER.get("pending_f32", []), []
     nf = 0
     if pf:
         probs, acc = [], []
-        for dy, x, w, ph in pf:
+        for rec in pf:
+            dy, x, w, ph = rec[:4]
+            geo = rec[4] if len(rec) > 4 else None
             g = w.grad
-            if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != w.shape:
+            lay_ok = g is not None and (g.is_contiguous(memory_format=torch.channels_last) if geo is not None
+                                        else g.is_contiguous())
+            if g is None or g.dtype != torch.float32 or not lay_ok or g.shape != w.shape:
                 raise RuntimeError("deferred weight gradients: the fp32 weight's .grad is missing or not contiguous")
             if ph is not None and g.data_ptr() != ph:
                 raise RuntimeError("deferred weight gradients: autograd did not keep the uninitialised placeholder "
                                    "as .grad (was the gradient accumulated?)")
-            probs.append((dy, x, g.view(dy.shape[1], x.shape[1])))
+            if geo is not None:  # [Cout][3][3][C] storage of the channels_last gradient
+                flat = g.permute(0, 2, 3, 1).reshape(g.shape[0], -1)
+                probs.append((dy, x, flat, geo))
+            else:
+                probs.append((dy, x, g.view(dy.shape[1], x.shape[1])))
             acc.append(ph is None)
         gemm8_tn_grouped(probs, accumulate=acc)
         nf = len(pf)
@@ -614,7 +642,11 @@ def _g8_fns():
     lib = _lib.load("gemm8")
     return {"configs": sig(lib, "mifx_gemm8_configs", [VP, I32]),
             "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
-            "tn": sig(lib, "mifx_gemm8_tn_grouped", [I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP])}
+            "tn": sig(lib, "mifx_gemm8_tn_grouped", [I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+            "conv": sig(lib, "mifx_gemm8_conv3x3", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, I32, I32, I32,
+                                                    I32, VP]),
+            "geo_bytes": sig(lib, "mifx_gemm8_geo_bytes", []),
+            "geo": sig(lib, "mifx_gemm8_geo", [I32, I32, I32, I32, I32, I32, VP])}
 
 
 @functools.lru_cache(maxsize=None)
@@ -640,46 +672,114 @@ def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
     return best
 
 
+_G8_MAXP = 48  # problems per grouped launch (the table travels in the kernel arguments)
+
+
 def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, accumulate=True) -> int:
     """problems: [(a [T, M], b [T, N], c [M, N]), ...] CUDA tensors on one device (a, b bf16) -> for every problem, in
     ONE launch of csrc/gemm8.hip's pipelined TN kernel: c = a^T b when c is bf16; c += a^T b when c is fp32 (c = a^T b
     where `accumulate` -- a bool or one per problem -- is False), the token range cut into `chunk`-row pieces whose
     fp32 partials a second launch sums in order. 256 x 256 tiles where M and N allow (tile128=True forces 128 x 128).
-    Returns the number of work items."""
+    A 4-tuple (dy [T, Cout], x NHWC [Nb, H, W, C], c fp32 [Cout, 9 C], geo) is a 3x3 convolution's weight gradient
+    with the input rows gathered per output pixel and tap (geo = conv_geo(...)). Returns the number of work items."""
     n = len(problems)
     if n == 0:
         return 0
     accs = list(accumulate) if isinstance(accumulate, (list, tuple)) else [bool(accumulate)] * n
-    if n > 64:
-        return sum(gemm8_tn_grouped(problems[i:i + 64], chunk, tile128, accs[i:i + 64]) for i in range(0, n, 64))
-    Ms, Ns, Ts, chunks, flags, ws_floats = [], [], [], [], [], 0
-    for a, b, c in problems:
-        if not (a.is_contiguous() and b.is_contiguous() and c.is_contiguous()) or a.shape[0] != b.shape[0] or \
-                c.numel() != a.shape[1] * b.shape[1] or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 \
-                or c.dtype not in (torch.bfloat16, torch.float32):
-            raise ValueError("gemm8_tn_grouped: need contiguous bf16 a [T, M], b [T, N] and c [M, N] (bf16 / fp32)")
-        T, M = a.shape
-        N = b.shape[1]
+    if n > _G8_MAXP:
+        return sum(gemm8_tn_grouped(problems[i:i + _G8_MAXP], chunk, tile128, accs[i:i + _G8_MAXP])
+                   for i in range(0, n, _G8_MAXP))
+    Ms, Ns, Ts, chunks, flags, geos, ws_floats = [], [], [], [], [], [], 0
+    for pr in problems:
+        a, b, c = pr[:3]
+        geo = pr[3] if len(pr) > 3 else None
+        if geo is not None:
+            T, M = a.shape
+            N = c.numel() // M
+            if not (a.is_contiguous() and b.is_contiguous() and a.dtype == torch.bfloat16
+                    and b.dtype == torch.bfloat16 and c.dtype == torch.float32 and N * M == c.numel()
+                    and N % 9 == 0 and b.shape[-1] == N // 9):
+                raise ValueError("gemm8_tn_grouped: a conv problem needs bf16 dy [T, Cout], NHWC bf16 x [.., C] and "
+                                 "fp32 c [Cout, 9 C]")
+        else:
+            if not (a.is_contiguous() and b.is_contiguous() and c.is_contiguous()) or a.shape[0] != b.shape[0] or \
+                    c.numel() != a.shape[1] * b.shape[1] or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 \
+                    or c.dtype not in (torch.bfloat16, torch.float32):
+                raise ValueError("gemm8_tn_grouped: need contiguous bf16 a [T, M], b [T, N] and c [M, N] (bf16 / "
+                                 "fp32)")
+            T, M = a.shape
+            N = b.shape[1]
         f32 = c.dtype == torch.float32
-        t128 = tile128 if tile128 is not None else (M % 256 or N % 256)
+        t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // 9) % 256))
         ck = chunk if f32 else T
         Ms.append(M)
         Ns.append(N)
         Ts.append(T)
         chunks.append(ck)
-        flags.append((1 if f32 else 0) | (2 if t128 else 0) | (4 if f32 and accs[len(flags)] else 0))
+        flags.append((1 if f32 else 0) | (2 if t128 else 0) | (4 if f32 and accs[len(flags)] else 0)
+                     | (8 if geo is not None else 0))
+        geos.append(geo.data_ptr() if geo is not None else None)
         if f32:
             ws_floats += -(-T // ck) * M * N
     dev = problems[0][0].device
     ws = torch.empty(ws_floats, device=dev, dtype=torch.float32) if ws_floats else None
     arr = lambda xs, t=ctypes.c_int: (t * n)(*xs)  # noqa: E731
-    rc = _g8_fns()["tn"](n, arr([a.data_ptr() for a, _, _ in problems], VP),
-                         arr([b.data_ptr() for _, b, _ in problems], VP),
-                         arr([c.data_ptr() for _, _, c in problems], VP), arr(Ms), arr(Ns), arr(Ts), arr(chunks),
-                         arr(flags), ptr(ws), stream_handle(dev))
+    rc = _g8_fns()["tn"](n, arr([pr[0].data_ptr() for pr in problems], VP),
+                         arr([pr[1].data_ptr() for pr in problems], VP),
+                         arr([pr[2].data_ptr() for pr in problems], VP), arr(Ms), arr(Ns), arr(Ts), arr(chunks),
+                         arr(flags), ptr(ws), arr(geos, VP), stream_handle(dev))
     if rc <= 0:
         raise RuntimeError(f"mifx_gemm8_tn_grouped failed ({rc})")
     return rc
+
+
+_GEO: dict = {}
+
+
+def conv_geo(nb: int, h: int, w: int, c: int, stride: int, pad: int, device) -> torch.Tensor:
+    """The device-resident geometry record of a 3x3 convolution for the grouped weight-gradient launch (created once
+    per shape, before any graph capture reads it)."""
+    key = (nb, h, w, c, stride, pad, str(device))
+    g = _GEO.get(key)
+    if g is None:
+        nbytes = _g8_fns()["geo_bytes"]()
+        host = (ctypes.c_ubyte * nbytes)()
+        if _g8_fns()["geo"](nb, h, w, c, stride, pad, host) != 0:
+            raise ValueError(f"no 3x3 convolution geometry for {key}")
+        g = torch.tensor(list(bytes(host)), dtype=torch.uint8).to(device)
+        _GEO[key] = g
+    return g
+
+
+def gemm8_conv3x3(x: torch.Tensor, w9: torch.Tensor, stride: int = 1, pad: int = 1, epi: int = 0,
+                  cfg: int | None = None, bias: torch.Tensor | None = None, z: torch.Tensor | None = None,
+                  out: torch.Tensor | None = None):
+    """3x3 convolution of NHWC bf16 x [Nb, H, W, C] (C a power of two >= 64) with w9 [Cout, 9 C] bf16 (a
+    channels_last [Cout, C, 3, 3] weight's storage) as an implicit GEMM on csrc/gemm8.hip -> (y [Nb OH OW, Cout] bf16,
+    part). epi 0; 5: part = [2, tiles, Cout] per-tile BatchNorm statistics of y; 8: y is a BatchNorm + ReLU output
+    gradient, bias = that BatchNorm's input [Nb OH OW, Cout], z = its statistics, part = per-tile backward sums."""
+    nb, h, w_, c = x.shape
+    cout = w9.shape[0]
+    oh, ow = (h + 2 * pad - 3) // stride + 1, (w_ + 2 * pad - 3) // stride + 1
+    M = nb * oh * ow
+    if cfg is None:
+        cfg = gemm8_pick(M, cout, 9 * c)
+    if cfg is None:
+        raise ValueError(f"no gemm8 tile configuration for the {M}x{cout}x{9 * c} convolution")
+    bm = gemm8_configs()[cfg][0]
+    y = out if out is not None else torch.empty(M, cout, device=x.device, dtype=torch.bfloat16)
+    part = torch.empty(2, M // bm, cout, device=x.device, dtype=torch.float32) if epi in (5, 8) else None
+    b = None
+    if epi == 8:
+        b = bias.reshape(M, cout)
+        if not (b.dtype == torch.bfloat16 and b.is_contiguous() and z is not None and z.dtype == torch.float32
+                and z.numel() == 4 * cout and z.is_contiguous()):
+            raise ValueError("gemm8_conv3x3 epi 8: need a contiguous bf16 [M, Cout] input and fp32 [4, Cout] stats")
+    if not (x.is_contiguous() and w9.is_contiguous() and x.dtype == torch.bfloat16 and w9.dtype == torch.bfloat16):
+        raise ValueError("gemm8_conv3x3: contiguous bf16 NHWC input and [Cout, 9 C] weight")
+    check(_g8_fns()["conv"](int(cfg), int(epi), ptr(x), ptr(w9), ptr(b), ptr(y), ptr(z), ptr(part), nb, h, w_, c,
+                            cout, stride, pad, stream_handle(x.device)), "mifx_gemm8_conv3x3")
+    return y, part
 
 
 def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0,
