@@ -12,9 +12,11 @@ profiles/resnet_steady_r5g.md) and BN2 / BN1 each needed a reduction pass. Here:
 * input gradient (stride 1): the same kernel over dY with the flipped, transposed weight [C][3][3][Cout]; when the
   input is a BatchNorm + ReLU output consumed only by this convolution (`bn_input=True`), the epilogue also reduces
   that BatchNorm's backward sums (mifx.ops.conv1x1 does the same for 1x1). Stride 2: the phase-split hand-written
-  kernel (mifx.ops.gconv.dgrad_strided);
+  kernel (mifx.ops.gconv.dgrad_strided) where it measured faster, else MIOpen;
 * weight gradient: dW[Cout][3][3][C] = sum over output pixels of dY^T . X_tap, deferred into the grouped split-K TN
-  launch with the 1x1 weight gradients (inside mifx.ops.gemm.deferred_weight_grads(); MIOpen's otherwise).
+  launch with the 1x1 weight gradients (inside mifx.ops.gemm.deferred_weight_grads(), C and Cout % 256: 2048-pixel
+  chunks of 256 x 256 tiles); MIOpen's otherwise (it beats the 128-wide tiles). Per-shape timings of every pass:
+  profiles/conv3x3_routes_r5.jsonl (tools/bench_conv3x3.py).
 
 Eligible: bf16 channels_last CUDA input, C a power of two >= 128, Cout % 128 == 0, padding 1, stride 1 or 2, and
 N OH OW a multiple of a tile height."""
@@ -29,6 +31,11 @@ from . import native_stats
 
 # MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B)
 ENABLED = os.environ.get("MIFX_CONV3X3", "1") != "0"
+
+
+# stride-2 input gradients where the phase-split hand-written kernel measured faster than MIOpen, (input H, C, Cout)
+# (profiles/resnet_conv_routes_r4.jsonl); the others stay on MIOpen
+_HIP_DGRAD_S2 = {(56, 128, 128), (28, 256, 256)}
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -112,11 +119,15 @@ class _Conv3x3(torch.autograd.Function):
                     offer_bwd_tiles(bn, dx, part)
                 else:
                     hg.gemm8_conv3x3(_nhwc(dyc), wt, 1, 1, epi=0, out=_rows(dx))
-            else:
+            elif (h, c, cout) in _HIP_DGRAD_S2:
                 from . import gconv
 
                 wb = w9.view(cout, 3, 3, c).permute(0, 3, 1, 2).contiguous()
                 dx = gconv.dgrad_strided(dyc, wb, n, h, w_, 1, c, cout, 3, 3, 1, stride)
+            else:
+                wb = w9.view(cout, 3, 3, c).permute(0, 3, 1, 2)
+                dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [1, 1], [1, 1], False,
+                                                         [0, 0], 1, [True, False, False])[0]
         return dx, dw, None, None, None
 
 

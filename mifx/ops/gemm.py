@@ -292,13 +292,17 @@ def defer_conv3x3_weight_grad_f32(dy2: torch.Tensor, x: torch.Tensor, w: torch.T
         return None
     nb, h, w_, c = x.shape
     cout = w.shape[0]
-    if cout % 128 or c % 128 or dy2.shape[0] % 64:
+    # 256 x 256 tiles (C, Cout % 256) in 2048-pixel chunks measured 99-106 us vs MIOpen's 121-138 on ResNet-50's
+    # shapes; 128-wide tiles (C = 128) lose to it (167 vs 130 us): left to the library
+    # (profiles/conv3x3_routes_r5.jsonl)
+    if cout % 256 or c % 256 or dy2.shape[0] % 64:
         return None
     geo = conv_geo(nb, h, w_, c, stride, pad, x.device)
     native_stats.count("conv3x3_dW", True)
     overwrite = w.grad is None
     ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
-    _DEFER["pending_f32"].append((dy2.contiguous(), x.contiguous(), w, ph.data_ptr() if overwrite else None, geo))
+    _DEFER["pending_f32"].append((dy2.contiguous(), x.contiguous(), w, ph.data_ptr() if overwrite else None, geo,
+                                  2048))
     return ph
 
 
@@ -311,6 +315,7 @@ def flush_weight_grads() -> int:
         for rec in pf:
             dy, x, w, ph = rec[:4]
             geo = rec[4] if len(rec) > 4 else None
+            ck = rec[5] if len(rec) > 5 else 4096
             g = w.grad
             lay_ok = g is not None and (g.is_contiguous(memory_format=torch.channels_last) if geo is not None
                                         else g.is_contiguous())
@@ -321,7 +326,7 @@ def flush_weight_grads() -> int:
                                    "as .grad (was the gradient accumulated?)")
             if geo is not None:  # [Cout][3][3][C] storage of the channels_last gradient
                 flat = g.permute(0, 2, 3, 1).reshape(g.shape[0], -1)
-                probs.append((dy, x, flat, geo))
+                probs.append((dy, x, flat, geo, ck))
             else:
                 probs.append((dy, x, g.view(dy.shape[1], x.shape[1])))
             acc.append(ph is None)
@@ -657,16 +662,24 @@ def gemm8_configs() -> tuple[tuple[int, int], ...]:
     return tuple((buf[2 * i], buf[2 * i + 1]) for i in range(n))
 
 
+# Relative throughput of each tile shape when it fills the chip (4096^3: 1174 / 875 / 962 / 866 TFLOP/s, adjusted by
+# the ResNet 3x3 / 1x1 sweeps in profiles/conv3x3_routes_r5.jsonl) and workgroups per CU (128 x 128: <= 128 VGPRs and
+# 64 KB of LDS, two co-resident)
+_G8_EFF = {(256, 256): 1.0, (256, 128): 0.745, (128, 256): 0.78, (128, 128): 0.85}
+_G8_OCC = {(128, 128): 2}
+
+
 def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
-    """The csrc/gemm8.hip configuration for an M x N x K product: fewest waves of workgroups, then the largest
-    tile (operand reuse per byte staged); None if none tiles the shape."""
+    """The csrc/gemm8.hip configuration for an M x N x K product: the highest (fraction of the last wave's slots
+    filled) x (the tile's relative throughput); None if none tiles the shape."""
     best, best_score = None, None
     for i, (bm, bn) in enumerate(gemm8_configs()):
         if M % bm or N % bn or K % 64:
             continue
         tiles = (M // bm) * (N // bn)
-        waves = -(-tiles // cus)
-        score = (tiles / (waves * cus) * (bm * bn) ** 0.5, bm * bn)
+        slots = cus * _G8_OCC.get((bm, bn), 1)
+        waves = -(-tiles // slots)
+        score = (tiles / (waves * slots) * _G8_EFF.get((bm, bn), 0.5), bm * bn)
         if best_score is None or score > best_score:
             best, best_score = i, score
     return best
@@ -693,6 +706,7 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
     for pr in problems:
         a, b, c = pr[:3]
         geo = pr[3] if len(pr) > 3 else None
+        pchunk = pr[4] if len(pr) > 4 else chunk
         if geo is not None:
             T, M = a.shape
             N = c.numel() // M
@@ -711,7 +725,7 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
             N = b.shape[1]
         f32 = c.dtype == torch.float32
         t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // 9) % 256))
-        ck = chunk if f32 else T
+        ck = pchunk if f32 else T
         Ms.append(M)
         Ns.append(N)
         Ts.append(T)

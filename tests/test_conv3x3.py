@@ -24,7 +24,8 @@ def _w(cout, cin, seed):
 
 
 @pytest.mark.parametrize("n,cin,hw,cout,stride", [(4, 128, 16, 128, 1), (4, 128, 16, 256, 1), (2, 256, 16, 128, 1),
-                                                   (4, 128, 32, 128, 2), (2, 256, 16, 256, 2), (8, 512, 4, 512, 1)])
+                                                   (4, 128, 32, 128, 2), (2, 256, 16, 256, 2), (8, 512, 4, 512, 1),
+                                                   (4, 256, 16, 256, 1), (8, 512, 8, 512, 2)])
 def test_conv3x3_forward_stats_backward(n, cin, hw, cout, stride):
     from mifx.ops import gemm as hg
     from mifx.ops.conv3x3 import conv3x3, eligible
@@ -56,6 +57,7 @@ def test_conv3x3_forward_stats_backward(n, cin, hw, cout, stride):
     torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * wr.grad.abs().max().item())
     # deferred weight gradient: the grouped TN launch gathering x per output pixel and tap (overwrite, then
     # accumulate into an existing gradient)
+    deferred = cin % 256 == 0 and cout % 256 == 0  # (128-wide weight gradients stay on the library)
     for acc in (False, True):
         w2 = w.detach().clone().requires_grad_()
         if acc:
@@ -63,7 +65,7 @@ def test_conv3x3_forward_stats_backward(n, cin, hw, cout, stride):
         y2, _ = conv3x3(x.detach(), w2, stride)
         with hg.deferred_weight_grads():
             y2.backward(gy)
-        assert hg.flush_weight_grads() == 1
+        assert hg.flush_weight_grads() == (1 if deferred else 0)
         assert w2.grad.is_contiguous(memory_format=torch.channels_last)
         torch.testing.assert_close(w2.grad, wr.grad + (1 if acc else 0), rtol=2e-2,
                                    atol=2e-2 * wr.grad.abs().max().item())

@@ -87,6 +87,9 @@ def _resnet_run(world: int, rank: int, out: str) -> None:
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
 
     os.environ["MIFX_DP_EXCHANGE"] = os.environ.get("MIFX_TEST_EXCHANGE", "auto")
+    # the data-parallel backward does not defer weight gradients (buckets exchange as gradients complete): the single
+    # process must take the same weight-gradient kernels, or this chaotic toy run amplifies their rounding difference
+    os.environ["MIFX_DEFER_DW"] = "0"
 
     imgs, labels = synthetic_imagenet(64, size=72, classes=10, seed=0)  # same data on every rank
     # one process accumulates the 2 micro-batches that the 2 ranks train on (ResNetTrainer's global sample)

@@ -134,3 +134,87 @@ def test_bert_tp_step_captured_with_ipc_allreduce_bit_identical_to_eager(world):
         for n in pe:
             assert torch.equal(pe[n], pg[n]), (r, n)
     assert res[0][True][0] == res[1][True][0]  # every TP rank reports the same loss
+
+
+def _ar32_worker(rank, world, port, out):
+    from mifx.parallel.tp_ipc import IpcAllReduce
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        ar = IpcAllReduce(dist.group.WORLD, dev, 1 << 20, dtype=torch.float32)
+        res = {}
+        for i, n in enumerate((2, 2048 * 3 + 2, 1 << 20, 100002)):
+            g = torch.Generator().manual_seed(1000 * i + rank)
+            x = (torch.randn(n, generator=g) * (rank + 1)).to(dev)
+            res[f"x{i}"] = x.cpu()
+            ar.all_reduce(x, out=x, scale=1.0 / world)
+            res[f"y{i}"] = x.cpu()
+        ar.check()
+        dist.barrier()
+        ar.close()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_allreduce_fp32_scaled_rank_order_sum(world):
+    """The fp32 mode (data-parallel gradient buckets): sum in rank order, times the scale, in place -- bit-exact."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "ar32")
+        mp.start_processes(_ar32_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for i in range(4):
+        want = torch.zeros_like(res[0][f"x{i}"])
+        for r in range(world):
+            want = want + res[r][f"x{i}"]
+        want = want * (1.0 / world)
+        for r in range(world):
+            assert torch.equal(res[r][f"y{i}"], want), (i, r, (res[r][f"y{i}"] - want).abs().max())
+
+
+def _ddp_ipc_worker(rank, world, port, out):
+    from mifx.parallel.ddp import DataParallel
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        res = {}
+        for exch in ("ipc", "rccl"):
+            torch.manual_seed(0)
+            net = torch.nn.Sequential(torch.nn.Linear(64, 512), torch.nn.ReLU(), torch.nn.Linear(512, 512),
+                                      torch.nn.ReLU(), torch.nn.Linear(512, 16)).to(dev)
+            dp = DataParallel(net, bucket_cap_mb=0.25, grad_as_bucket_view=True, exchange=exch)
+            assert dp.exchange == exch and len(dp.buckets) > 2
+            g = torch.Generator().manual_seed(7 + rank)
+            grads = []
+            for step in range(3):
+                dp.zero_grad()
+                x = torch.randn(256, 64, generator=g).to(dev)
+                net(x).square().mean().backward()
+                dp.finish()
+                grads.append([p.grad.detach().cpu().clone() for p in net.parameters()])
+            if dp._ipc is not None:
+                dp._ipc.check()
+            res[exch] = grads
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_ipc_exchange_bit_identical_to_process_group():
+    """DataParallel(exchange="ipc") -- bucket all-reduces as peer-memory kernels on the side stream while the
+    backward runs -- gives bit-identical averaged gradients to the process group's all-reduce, on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "dpi")
+        mp.start_processes(_ddp_ipc_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for r in range(world):
+        for step, (gi, gr) in enumerate(zip(res[r]["ipc"], res[r]["rccl"])):
+            for k, (a, b) in enumerate(zip(gi, gr)):
+                assert torch.equal(a, b), (r, step, k, (a - b).abs().max())
+                assert torch.equal(a, res[0]["ipc"][step][k])
