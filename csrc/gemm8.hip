@@ -59,7 +59,7 @@ constexpr int BK = 64;
 constexpr int NT = 512;
 
 enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_ADD_R = 3, EPI_GELU_BWD = 4, EPI_STATS = 5,
-           EPI_ADD_STATS = 6, EPI_F32 = 7, EPI_BNBWD = 8 };
+           EPI_ADD_STATS = 6, EPI_F32 = 7, EPI_BNBWD = 8, EPI_ADD_BNBWD = 9 };
 
 __device__ __forceinline__ float erf_fast(float x) {  // Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, branch-free
   const float ax = fabsf(x);
@@ -152,7 +152,8 @@ template <int BM, int BN, int EPI, typename P, bool TN, int CV = 0>
 __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                            const P* __restrict__ bias, bf16* __restrict__ Y, bf16* __restrict__ Z,
                                            int M, int N, int K, float* __restrict__ part, int m0, int n0,
-                                           unsigned char* lds, const Geo& geo = Geo{}, int tok0 = 0) {
+                                           unsigned char* lds, const Geo& geo = Geo{}, int tok0 = 0,
+                                           const bf16* __restrict__ R2 = nullptr) {
   static_assert(CV == 0 || (CV == 1 && !TN) || (CV == 2 && TN), "conv gather: NT rows (1) or TN B rows (2)");
   constexpr int HA = BM / 2, HB = BN / 2;            // rows (NT) / columns (TN) per half-tile
   constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // NT: 64 bf16 per row; TN: 64 token rows of HA bf16
@@ -515,7 +516,9 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   // shift). Besides storing dY, the epilogue reduces the BatchNorm backward's per-tile sums over the tile rows:
   // part[0][m0 / BM][n] = sum g, part[1][...] = sum g xhat, g = dY [x scale + shift > 0], xhat = (x - mean) rstd --
   // what bn_bwd_reduce would otherwise re-read dY and x for.
-  constexpr bool BNB = EPI == EPI_BNBWD;
+  // ADD_BNBWD: as BNBWD for dY = X W^T + R2 (bf16 [M, N]) -- the BatchNorm output feeds two convolutions (a
+  // projection block's conv1 and shortcut) and R2 is the other one's input gradient, added before the reduction
+  constexpr bool BNB = EPI == EPI_BNBWD || EPI == EPI_ADD_BNBWD;
   auto tslot = [&](int row, int c) -> unsigned char* {
     return lds + (size_t)row * (BN * 2) + ((c ^ (row & (CPR_O - 1))) << 4);
   };
@@ -570,6 +573,11 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     if constexpr (STATS) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
+    }
+    if constexpr (EPI == EPI_ADD_BNBWD) {  // one rounding of the fp32-exact sum of two bf16 values
+      const v8bf rv = *(const v8bf*)(R2 + g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[e]);
     }
     if constexpr (BNB) {  // the BatchNorm backward's reduction, with its mask computed as the forward's fmaf
       const v8bf xv = *(const v8bf*)((const bf16*)bias + g);
@@ -646,10 +654,11 @@ template <int BM, int BN, int EPI, typename P>
 __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                                   const P* __restrict__ bias, bf16* __restrict__ Y,
                                                   bf16* __restrict__ Z, int M, int N, int K,
-                                                  float* __restrict__ part) {
+                                                  float* __restrict__ part, const bf16* __restrict__ R2) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tile = xcd_tile(), nb_n = N / BN;
-  gemm8_tile<BM, BN, EPI, P, false>(X, W, bias, Y, Z, M, N, K, part, (tile / nb_n) * BM, (tile % nb_n) * BN, lds);
+  gemm8_tile<BM, BN, EPI, P, false>(X, W, bias, Y, Z, M, N, K, part, (tile / nb_n) * BM, (tile % nb_n) * BN, lds,
+                                    Geo{}, 0, R2);
 }
 
 // implicit-GEMM 3x3 convolution (CV 1): Y[Nb OH OW, N] = gathered X . W[N, 9 C]^T, epilogues as gemm8_nt
@@ -753,13 +762,15 @@ __global__ __launch_bounds__(256) void gemm8_tn_reduce(const RedGroup g, long lo
 template <int BM, int BN, int EPI>
 constexpr int lds_bytes() {
   const int loop = 2 * 2 * (BM / 2 + BN / 2) * 128;
-  const int epi = BM * BN * 2 + ((EPI == EPI_STATS || EPI == EPI_ADD_STATS || EPI == EPI_BNBWD) ? 9 * BN * 4 : 0);
+  const int epi = BM * BN * 2 +
+                  ((EPI == EPI_STATS || EPI == EPI_ADD_STATS || EPI == EPI_BNBWD || EPI == EPI_ADD_BNBWD) ? 9 * BN * 4
+                                                                                                         : 0);
   return loop > epi ? loop : epi;
 }
 
 template <int BM, int BN, int EPI, typename P>
 int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N, int K, float* part,
-           hipStream_t st) {
+           hipStream_t st, const void* R2 = nullptr) {
   constexpr int LDS = lds_bytes<BM, BN, EPI>();
   static bool attr = false;
   if (!attr) {
@@ -767,7 +778,7 @@ int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int
     attr = true;
   }
   hipLaunchKernelGGL((gemm8_nt<BM, BN, EPI, P>), dim3((M / BM) * (N / BN)), dim3(NT), LDS, st, (const bf16*)X,
-                     (const bf16*)W, (const P*)bias, (bf16*)Y, (bf16*)Z, M, N, K, part);
+                     (const bf16*)W, (const P*)bias, (bf16*)Y, (bf16*)Z, M, N, K, part, (const bf16*)R2);
   return (int)hipGetLastError();
 }
 
@@ -818,7 +829,7 @@ bool geo_ok(int Nb, int H, int W, int C, int OH, int OW, int stride, int pad) {
 
 template <int BM, int BN>
 int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z, int M, int N,
-             int K, float* part, hipStream_t st) {
+             int K, float* part, hipStream_t st, const void* R2) {
   switch (epi) {
     case EPI_NONE: return launch<BM, BN, EPI_NONE, bf16>(X, W, nullptr, Y, nullptr, M, N, K, nullptr, st);
     case EPI_BIAS:
@@ -834,6 +845,7 @@ int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bi
     case EPI_STATS: return launch<BM, BN, EPI_STATS, bf16>(X, W, nullptr, Y, nullptr, M, N, K, part, st);
     case EPI_ADD_STATS: return launch<BM, BN, EPI_ADD_STATS, bf16>(X, W, bias, Y, nullptr, M, N, K, part, st);
     case EPI_BNBWD: return launch<BM, BN, EPI_BNBWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
+    case EPI_ADD_BNBWD: return launch<BM, BN, EPI_ADD_BNBWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st, R2);
   }
   return -1;
 }
@@ -861,29 +873,30 @@ int mifx_gemm8_configs(int* out, int n) {
 // per-tile column sums of dZ; 5 part[2][M / BM][N] = per-tile column mean / sum of squared deviations (M2) of the
 // stored Y; 6 = 3 and 5: Y = X W^T + R with the statistics of the stored sum; 8: Y = X W^T is the gradient of a
 // BatchNorm + ReLU output, bias = the BatchNorm's input (bf16 [M, N]), Z = its statistics (fp32 [4][N]: mean, rstd,
-// scale, shift), part[2][M / BM][N] = per-tile (sum g, sum g xhat) of the BatchNorm backward.
-// bias bf16 or fp32 (bias_f32). M % BM == 0, N % BN == 0, K % 64 == 0, 16-byte aligned operands.
+// scale, shift), part[2][M / BM][N] = per-tile (sum g, sum g xhat) of the BatchNorm backward; 9: as 8 for
+// Y = X W^T + R2 (bf16 [M, N]). bias bf16 or fp32 (bias_f32). M % BM == 0, N % BN == 0, K % 64 == 0, 16-byte aligned operands.
 int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, const void* bias, void* Y, void* Z,
-                  float* part, int M, int N, int K, hipStream_t st) {
+                  float* part, int M, int N, int K, const void* R2, hipStream_t st) {
   const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
   if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || X == nullptr || W == nullptr || Y == nullptr) return -1;
   const Cfg c = kCfgs[cfg];
   if (M % c.bm || N % c.bn || K % BK) return -1;
-  if (epi < 0 || epi > 8 || epi == 7) return -1;
-  if ((epi >= 1 && epi <= 4) || epi == 6 || epi == 8) {
+  if (epi < 0 || epi > 9 || epi == 7) return -1;
+  if ((epi >= 1 && epi <= 4) || epi == 6 || epi >= 8) {
     if (bias == nullptr) return -1;
   }
-  if ((epi == 2 || epi == 4 || epi == 8) && Z == nullptr) return -1;
+  if ((epi == 2 || epi == 4 || epi >= 8) && Z == nullptr) return -1;
   if (epi >= 4 && part == nullptr) return -1;
-  if (epi == 8 && (uintptr_t)bias % 16) return -1;
+  if (epi >= 8 && (uintptr_t)bias % 16) return -1;
+  if (epi == 9 && (R2 == nullptr || (uintptr_t)R2 % 16)) return -1;
   if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 16 || (Z != nullptr && (uintptr_t)Z % 8)) return -1;
   if ((epi == 3 || epi == 6) && (uintptr_t)bias % 16) return -1;
   if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;  // 32-bit element offsets
   switch (cfg) {
-    case 0: return dispatch<256, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
-    case 1: return dispatch<256, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
-    case 2: return dispatch<128, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
-    default: return dispatch<128, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st);
+    case 0: return dispatch<256, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
+    case 1: return dispatch<256, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
+    case 2: return dispatch<128, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
+    default: return dispatch<128, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
   }
 }
 

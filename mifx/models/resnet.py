@@ -131,13 +131,25 @@ class PreActBottleneck(nn.Module):
             pre, s = self.bn0.forward_add(*x)
         else:
             pre, s = self.bn0(x), x
+        from ..ops.conv1x1 import proj_pair, proj_pair_eligible
+
+        h = None
         if self.shortcut is None:
             sc = s
+        elif FUSED_1X1 and _fused_ok(self.conv1, pre) and self.shortcut.bias is None \
+                and proj_pair_eligible(pre, self.shortcut.weight, self.shortcut.stride[0], self.conv1.weight):
+            # strided shortcut + conv1 as one node: the two input gradients are summed inside conv1's dX GEMM, which
+            # also reduces bn0's backward sums (pre feeds only this pair)
+            sc, y, part = proj_pair(pre, self.shortcut.weight, self.shortcut.stride[0], self.conv1.weight,
+                                    bn_input=True)
+            h = self.bn1.forward_tiles(y, part)[0]
         elif _fused_ok(self.shortcut, pre):
             sc = conv1x1(pre, self.shortcut.weight)[0]
         else:
             sc = self.shortcut(pre)
-        if _fused_ok(self.conv1, pre):
+        if h is not None:
+            pass
+        elif _fused_ok(self.conv1, pre):
             # pre feeds only conv1 when the shortcut is the identity (the shortcut then takes bn0's alias output s)
             y, part = conv1x1(pre, self.conv1.weight, stats=True, bn_input=self.shortcut is None)
             h = self.bn1.forward_tiles(y, part)[0]

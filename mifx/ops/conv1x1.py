@@ -24,7 +24,7 @@ import os
 import torch
 
 from . import gemm as hg
-from . import native_stats
+from . import native_stats, weight_prep
 
 # dX backend for tileable shapes: "gemm8" (default) or "miopen" (A/B)
 DGRAD = os.environ.get("MIFX_CONV1X1_DGRAD", "gemm8")
@@ -50,7 +50,9 @@ class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, r, stats, bn):
         cout, cin = w.shape[0], w.shape[1]
-        wb = w.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        im = weight_prep.images(w)  # this step's bf16 images (one launch for every convolution), else cast here
+        wb = im[0] if im is not None else w.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        ctx.wt = im[1] if im is not None else None
         x2 = _rows(x)
         M = x2.shape[0]
         cfg = hg.gemm8_pick(M, cout, cin)
@@ -93,11 +95,12 @@ class _Conv1x1(torch.autograd.Function):
                         and xbn.is_contiguous(memory_format=torch.channels_last)):
                     xbn = None
             if xbn is not None:
-                _, part = hg.gemm8_nt(dy2, hg.transpose(wb), _rows(xbn), 8, cfg=cfg, z=stats, out=_rows(dx))
+                wt = ctx.wt if ctx.wt is not None else hg.transpose(wb)
+                _, part = hg.gemm8_nt(dy2, wt, _rows(xbn), 8, cfg=cfg, z=stats, out=_rows(dx))
                 from .bn_relu import offer_bwd_tiles
                 offer_bwd_tiles(bn, dx, part)
             else:
-                hg.gemm8_nt(dy2, hg.transpose(wb), None, 0, cfg=cfg, out=_rows(dx))
+                hg.gemm8_nt(dy2, ctx.wt if ctx.wt is not None else hg.transpose(wb), None, 0, cfg=cfg, out=_rows(dx))
             want_dx = False
         if want_dx or want_dw:
             # the input gradient (and a weight gradient the grouped flush does not take: Cin = 64) on MIOpen's NHWC
@@ -126,3 +129,108 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = No
     if bn is not None and not getattr(bn, "mifx_bn", False):
         bn = None
     return _Conv1x1.apply(x, w, residual, stats, bn)
+
+
+# stride-2 1x1 shortcuts whose input gradient measured faster on the phase-split hand-written kernel,
+# (input H, C, Cout) (profiles/resnet_conv_routes_r4.jsonl); others MIOpen
+_HIP_DGRAD_S2 = {(56, 256, 512), (28, 512, 1024), (14, 1024, 2048)}
+
+
+class _ProjPair(torch.autograd.Function):
+    """A projection block's two consumers of the pre-activation: the strided 1x1 shortcut (MIOpen forward / weight
+    gradient, hand-written or MIOpen input gradient) and conv1 (the GEMM kernel with BN1's statistics in its
+    epilogue), as ONE autograd node. Its backward computes the shortcut's input gradient first and hands it to conv1's
+    input-gradient GEMM as the addend R2 (csrc/gemm8.hip EPI_ADD_BNBWD): the summed gradient of the pre-activation is
+    written once -- no separate add of the two branches' gradients (autograd's, ~100 us each at B = 256) -- and, when
+    the pre-activation is a BatchNorm + ReLU output feeding only this pair, the same epilogue reduces that BatchNorm's
+    backward sums."""
+
+    @staticmethod
+    def forward(ctx, x, w_sc, w1, stride, bn):
+        n, cin, h, w_ = x.shape
+        c1 = w1.shape[0]
+        wsb = w_sc.to(torch.bfloat16)
+        sc = torch.ops.aten.convolution(x, wsb, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1)
+        im = weight_prep.images(w1)
+        wb1 = im[0] if im is not None else w1.reshape(c1, cin).to(torch.bfloat16).contiguous()
+        ctx.wt1 = im[1] if im is not None else None
+        x2 = _rows(x)
+        y1 = torch.empty(n, c1, h, w_, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        _, part = hg.gemm8_nt(x2, wb1, None, 5, cfg=hg.gemm8_pick(x2.shape[0], c1, cin), out=_rows(y1))
+        ctx.save_for_backward(x, wsb, wb1)
+        ctx.w_sc, ctx.w1, ctx.stride, ctx.bn = w_sc, w1, stride, bn
+        ctx.mark_non_differentiable(part)
+        return sc, y1, part
+
+    @staticmethod
+    def backward(ctx, dsc, dy1, dpart):
+        x, wsb, wb1 = ctx.saved_tensors
+        n, cin, h, w_ = x.shape
+        stride = ctx.stride
+        dx = dwsc = dw1 = None
+        dx_sc = None
+        if dsc is not None:
+            dscc = dsc.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+            cs = wsb.shape[0]
+            if ctx.needs_input_grad[0] and (h, cin, cs) in _HIP_DGRAD_S2:
+                from . import gconv
+
+                dx_sc = gconv.dgrad_strided(dscc, wsb.contiguous(), n, h, w_, 1, cin, cs, 1, 1, 0, stride)
+            want_dx = ctx.needs_input_grad[0] and dx_sc is None
+            if want_dx or ctx.needs_input_grad[1]:
+                gx, gw, _ = torch.ops.aten.convolution_backward(dscc, x, wsb, None, [stride, stride], [0, 0], [1, 1],
+                                                                False, [0, 0], 1,
+                                                                [want_dx, ctx.needs_input_grad[1], False])
+                if want_dx:
+                    dx_sc = gx
+                if ctx.needs_input_grad[1]:
+                    dwsc = gw.to(ctx.w_sc.dtype)
+        if dy1 is not None:
+            dy1c = dy1.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+            dy2 = _rows(dy1c)
+            x2 = _rows(x)
+            if ctx.needs_input_grad[2]:
+                dw1 = hg.defer_weight_grad_f32(dy2, x2, ctx.w1)
+                if dw1 is None:
+                    dw1 = torch.ops.aten.convolution_backward(dy1c, x, wb1.view(wb1.shape[0], cin, 1, 1), None, [1, 1],
+                                                              [0, 0], [1, 1], False, [0, 0], 1,
+                                                              [False, True, False])[1].to(ctx.w1.dtype)
+            if ctx.needs_input_grad[0]:
+                wt = ctx.wt1 if ctx.wt1 is not None else hg.transpose(wb1)
+                cfg = hg.gemm8_pick(dy2.shape[0], cin, wb1.shape[0])
+                dx = torch.empty(n, cin, h, w_, device=x.device, dtype=torch.bfloat16,
+                                 memory_format=torch.channels_last)
+                bn, xbn, stats = ctx.bn, None, None
+                if bn is not None:
+                    xbn, _, stats = bn.saved_tensors
+                    if not (xbn.dtype == torch.bfloat16 and tuple(xbn.shape) == tuple(x.shape)
+                            and xbn.is_contiguous(memory_format=torch.channels_last)):
+                        xbn = None
+                r2 = dx_sc.contiguous(memory_format=torch.channels_last) if dx_sc is not None else None
+                if xbn is not None and r2 is not None:
+                    _, part = hg.gemm8_nt(dy2, wt, _rows(xbn), 9, cfg=cfg, z=stats, out=_rows(dx), r2=_rows(r2))
+                    from .bn_relu import offer_bwd_tiles
+
+                    offer_bwd_tiles(bn, dx, part)
+                elif r2 is not None:
+                    hg.gemm8_nt(dy2, wt, _rows(r2), 3, cfg=cfg, out=_rows(dx))
+                else:
+                    hg.gemm8_nt(dy2, wt, None, 0, cfg=cfg, out=_rows(dx))
+        elif ctx.needs_input_grad[0]:
+            dx = dx_sc
+        return dx, dwsc, dw1, None, None
+
+
+def proj_pair_eligible(x: torch.Tensor, w_sc: torch.Tensor, stride: int, w1: torch.Tensor) -> bool:
+    """A strided 1x1 shortcut and a GEMM-eligible 1x1 conv1 on the same bf16 channels_last input."""
+    return stride > 1 and tuple(w_sc.shape[2:]) == (1, 1) and eligible(x, w1) and w_sc.shape[1] == x.shape[1]
+
+
+def proj_pair(x: torch.Tensor, w_sc: torch.Tensor, stride: int, w1: torch.Tensor, bn_input: bool = False):
+    """(shortcut(x), conv1(x), conv1's per-tile BatchNorm statistics) as one node whose backward writes the summed
+    input gradient once (see _ProjPair). bn_input: x is a BatchNorm + ReLU output consumed only by this pair."""
+    native_stats.count("conv1x1_fwd", True)
+    bn = x.grad_fn if bn_input else None
+    if bn is not None and not getattr(bn, "mifx_bn", False):
+        bn = None
+    return _ProjPair.apply(x, w_sc, w1, int(stride), bn)

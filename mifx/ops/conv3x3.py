@@ -27,7 +27,7 @@ import os
 import torch
 
 from . import gemm as hg
-from . import native_stats
+from . import native_stats, weight_prep
 
 # MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B)
 ENABLED = os.environ.get("MIFX_CONV3X3", "1") != "0"
@@ -72,7 +72,9 @@ class _Conv3x3(torch.autograd.Function):
         n, c, h, w_ = x.shape
         cout = w.shape[0]
         oh, ow = (h - 1) // stride + 1, (w_ - 1) // stride + 1
-        w9 = _w9(w)
+        im = weight_prep.images(w)  # this step's bf16 images (one launch for every convolution), else cast here
+        w9 = im[0] if im is not None else _w9(w)
+        ctx.wt = im[1] if im is not None else None
         out = torch.empty(n, cout, oh, ow, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
         _, part = hg.gemm8_conv3x3(_nhwc(x), w9, stride, 1, epi=5 if stats else 0, out=_rows(out))
         ctx.save_for_backward(x, w9)
@@ -103,7 +105,8 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if stride == 1:
                 # dX = conv(dY, W flipped and transposed): [C][3][3][Cout], the same implicit GEMM over dY's pixels
-                wt = w9.view(cout, 3, 3, c).flip(1, 2).permute(3, 1, 2, 0).reshape(c, 9 * cout).contiguous()
+                wt = ctx.wt if ctx.wt is not None else \
+                    w9.view(cout, 3, 3, c).flip(1, 2).permute(3, 1, 2, 0).reshape(c, 9 * cout).contiguous()
                 dx = torch.empty(n, c, h, w_, device=dy.device, dtype=torch.bfloat16,
                                  memory_format=torch.channels_last)
                 bn, xbn, stats = ctx.bn, None, None

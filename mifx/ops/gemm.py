@@ -646,7 +646,7 @@ def tn_eligible(a2: torch.Tensor, b2: torch.Tensor) -> bool:
 def _g8_fns():
     lib = _lib.load("gemm8")
     return {"configs": sig(lib, "mifx_gemm8_configs", [VP, I32]),
-            "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP]),
+            "nt": sig(lib, "mifx_gemm8_nt", [I32, I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, VP, VP]),
             "tn": sig(lib, "mifx_gemm8_tn_grouped", [I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
             "conv": sig(lib, "mifx_gemm8_conv3x3", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, I32, I32, I32,
                                                     I32, VP]),
@@ -797,14 +797,15 @@ def gemm8_conv3x3(x: torch.Tensor, w9: torch.Tensor, stride: int = 1, pad: int =
 
 
 def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0,
-             cfg: int | None = None, z: torch.Tensor | None = None, out: torch.Tensor | None = None):
+             cfg: int | None = None, z: torch.Tensor | None = None, out: torch.Tensor | None = None,
+             r2: torch.Tensor | None = None):
     """x2 [M, K] bf16, w [N, K] bf16 -> (Y [M, N] bf16, aux). epi 0: X W^T; 1: + bias; 2: GELU(X W^T + bias), aux
     = Z = bf16(X W^T); 3: + bias as a bf16 [M, N] matrix; 4: dZ = (X W^T) o GELU'(z + bias), aux = per-tile column sums
     [M / BM, N] fp32; 5: aux = per-tile BatchNorm statistics of the stored Y, [2, M / BM, N] fp32 = (tile column mean,
     tile sum of squared deviations M2); 6: 3 and 5 (Y = X W^T + bias-matrix, statistics of the stored sum); 8: Y = X W^T
     is the output gradient of a BatchNorm + ReLU whose input is `bias` (bf16 [M, N]) and whose forward statistics are
     `z` (fp32 [4, N]: mean, rstd, scale, shift): aux = [2, M / BM, N] fp32 per-tile (sum g, sum g xhat) of its
-    backward (csrc/bn_relu.hip mifx_bn_relu_bwd_tiles consumes them)."""
+    backward (csrc/bn_relu.hip mifx_bn_relu_bwd_tiles consumes them); 9: as 8 for Y = X W^T + r2 (bf16 [M, N])."""
     M, K = x2.shape
     N = w.shape[0]
     if cfg is None:
@@ -825,15 +826,20 @@ def gemm8_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None
         b = b.contiguous()
     if epi == 4:
         part = aux = torch.empty(M // bm, N, device=x2.device, dtype=torch.float32)
-    if epi in (5, 6, 8):
+    if epi in (5, 6, 8, 9):
         part = aux = torch.empty(2, M // bm, N, device=x2.device, dtype=torch.float32)
-    if epi == 8:
+    if epi == 9:
+        r2 = r2.reshape(M, N)
+        if not (r2.dtype == torch.bfloat16 and r2.is_contiguous()):
+            raise ValueError("gemm8_nt epi 9: r2 must be a contiguous bf16 [M, N] matrix")
+    if epi in (8, 9):
         b = bias.reshape(M, N)
         if not (b.dtype == torch.bfloat16 and b.is_contiguous() and z is not None and z.dtype == torch.float32
                 and z.numel() == 4 * N and z.is_contiguous()):
             raise ValueError("gemm8_nt epi 8: need a contiguous bf16 [M, N] input and fp32 [4, N] statistics")
     check(_g8_fns()["nt"](int(cfg), int(epi), int(b is not None and b.dtype == torch.float32), ptr(x2), ptr(w),
-                          ptr(b), ptr(y), ptr(z), ptr(part), M, N, K, stream_handle(x2.device)), "mifx_gemm8_nt")
+                          ptr(b), ptr(y), ptr(z), ptr(part), M, N, K, ptr(r2 if epi == 9 else None),
+                          stream_handle(x2.device)), "mifx_gemm8_nt")
     return y, aux
 
 

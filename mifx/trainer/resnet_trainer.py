@@ -69,6 +69,16 @@ class ResNetTrainer:
         self.opt = torch.optim.SGD([{"params": decay, "weight_decay": weight_decay},
                                     {"params": no_decay, "weight_decay": 0.0}], lr=lr, momentum=momentum,
                                    nesterov=True)
+        # bf16 images of the GEMM-shaped convolutions' weights, refreshed in one launch at the start of every step
+        self.prep = None
+        if self.device.type == "cuda" and os.environ.get("MIFX_WEIGHT_PREP", "1") != "0":
+            from ..ops.weight_prep import WeightPrep
+
+            ws = [m.weight for m in self.model.modules() if isinstance(m, torch.nn.Conv2d) and m.groups == 1
+                  and ((m.kernel_size == (1, 1) and m.stride == (1, 1))
+                       or (m.kernel_size == (3, 3) and m.in_channels >= 128))
+                  and WeightPrep.supported(m.weight)]
+            self.prep = WeightPrep(ws) if ws else None
         self.base_lr, self.warmup = lr, warmup_steps
         self.images, self.labels = images.to(self.device), labels.to(self.device)
         self.mean, self.std = mean, std
@@ -116,6 +126,8 @@ class ResNetTrainer:
         else:
             self.opt.zero_grad(set_to_none=True)
         total = 0.0
+        if self.prep is not None:
+            self.prep.refresh()
         for m in range(self.accum):
             mb = self.rank * self.accum + m
             idx = glob[mb * self.batch:(mb + 1) * self.batch].to(self.device)
@@ -177,6 +189,8 @@ class ResNetTrainer:
         else:
             torch._foreach_zero_([p.grad for p in self.model.parameters() if p.grad is not None])
         total = None
+        if self.prep is not None:
+            self.prep.refresh()
         in_graph = self.dp is not None and self.dp.exchange == "ipc"  # the exchange captures with the backward
         ctx = self.dp.no_sync() if self.dp is not None and not in_graph else contextlib.nullcontext()
         with ctx:

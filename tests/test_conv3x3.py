@@ -102,3 +102,31 @@ def test_conv3x3_bn_coupled_backward():
     (F.conv2d(pre, w.to(torch.bfloat16).float(), padding=1) * gy.float()).sum().backward()
     for a, b in zip(grads[1][:3], (xr.grad, wr.grad, br.grad)):
         torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2 * b.abs().max().item())
+
+
+def test_weight_prep_images_exact():
+    """One launch writes every registered weight's bf16 images: 1x1 [Cout, C] and its transpose, 3x3 [Cout, 9 C]
+    (channels_last storage) and the flipped transpose [C, 9 Cout] -- bit-equal to the per-weight torch casts; a weight
+    changed after the refresh has no image (stale version)."""
+    from mifx.ops import weight_prep as wp
+
+    ws = [torch.randn(256, 128, 1, 1, device="cuda"), torch.randn(128, 512, 1, 1, device="cuda"),
+          torch.randn(256, 128, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last),
+          torch.randn(128, 256, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)]
+    prep = wp.WeightPrep(ws)
+    prep.refresh()
+    for w in ws:
+        fwd, bwd = wp.images(w)
+        cout, c = w.shape[:2]
+        wb = w.to(torch.bfloat16)
+        if w.shape[2] == 1:
+            assert torch.equal(fwd, wb.view(cout, c))
+            assert torch.equal(bwd, wb.view(cout, c).t().contiguous())
+        else:
+            assert torch.equal(fwd, wb.permute(0, 2, 3, 1).reshape(cout, 9 * c))
+            want = wb.permute(0, 2, 3, 1).flip(1, 2).permute(3, 1, 2, 0).reshape(c, 9 * cout)
+            assert torch.equal(bwd, want)
+    ws[0].add_(1.0)
+    assert wp.images(ws[0]) is None and wp.images(ws[1]) is not None
+    prep.close()
+    assert wp.images(ws[1]) is None
