@@ -218,3 +218,41 @@ def test_ddp_ipc_exchange_bit_identical_to_process_group():
             for k, (a, b) in enumerate(zip(gi, gr)):
                 assert torch.equal(a, b), (r, step, k, (a - b).abs().max())
                 assert torch.equal(a, res[0]["ipc"][step][k])
+
+
+def _timeout_worker(rank, world, port, out):
+    from mifx.parallel.tp_ipc import IpcAllReduce
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        ar = IpcAllReduce(dist.group.WORLD, dev, 1 << 16)
+        res = {}
+        if rank == 0:  # rank 1 never joins this all-reduce: the bounded wait expires, err is set, y becomes NaN
+            x = torch.ones(8192, dtype=torch.bfloat16, device=dev)
+            y = ar.all_reduce(x)
+            z = ar.all_reduce(x)  # a later call on the failed group does nothing but poison its output
+            torch.cuda.synchronize(dev)
+            res["nan_y"] = bool(torch.isnan(y.float()).all())
+            res["nan_z"] = bool(torch.isnan(z.float()).all())
+            try:
+                ar.check()
+                res["raised"] = False
+            except RuntimeError:
+                res["raised"] = True
+        dist.barrier()  # rank 1 keeps its buffers mapped until rank 0 is done
+        ar.close()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ipc_allreduce_peer_never_arrives_sets_error_and_poisons():
+    """A peer that never publishes: the waits are bounded (10 s wall clock), the sticky error flag is set, the outputs
+    are NaN (whatever consumes them goes non-finite) and check() raises -- no hang, no silent garbage."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "to")
+        mp.start_processes(_timeout_worker, args=(2, _port(), out), nprocs=2, start_method="spawn")
+        r0 = torch.load(f"{out}.0", weights_only=True)
+    assert r0 == {"nan_y": True, "nan_z": True, "raised": True}, r0
