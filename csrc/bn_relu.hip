@@ -260,16 +260,37 @@ __global__ __launch_bounds__(1024) void bn_tiles_partial(const float* __restrict
   const int t0 = gb + (int)((long long)(ge - gb) * sl / 16), t1 = gb + (int)((long long)(ge - gb) * (sl + 1) / 16);
   double mu = 0.0, m2 = 0.0;
   if (c < C && t1 > t0) {
-    double s = 0.0;
-    for (int t = t0; t < t1; ++t) s += (double)pmean[(size_t)t * C + c];
-    mu = s / (double)(t1 - t0);
-    double d2 = 0.0;
-    for (int t = t0; t < t1; ++t) {
-      const double d = (double)pmean[(size_t)t * C + c] - mu;
-      m2 += (double)pm2[(size_t)t * C + c];
-      d2 += d * d;
+    // one pass, shifted by the first tile's mean (fp64: no cancellation at these sizes), 8 tiles' loads in flight
+    // at a time -- the two dependent passes of one load per tile were latency-bound (~12 us per BatchNorm,
+    // profiles/resnet_steady_r5m.md)
+    const double K0 = (double)pmean[(size_t)t0 * C + c];
+    double sd = 0.0, sd2 = 0.0;
+    int t = t0;
+    for (; t + 8 <= t1; t += 8) {
+      float a[8], q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = pmean[(size_t)(t + u) * C + c];
+        q[u] = pm2[(size_t)(t + u) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double d = (double)a[u] - K0;
+        sd += d;
+        sd2 += d * d;
+        m2 += (double)q[u];
+      }
     }
-    m2 += (double)nt * d2;
+    for (; t < t1; ++t) {
+      const double d = (double)pmean[(size_t)t * C + c] - K0;
+      sd += d;
+      sd2 += d * d;
+      m2 += (double)pm2[(size_t)t * C + c];
+    }
+    const double k = (double)(t1 - t0);
+    mu = K0 + sd / k;
+    const double d2 = sd2 - sd * sd / k;
+    m2 += (double)nt * (d2 > 0.0 ? d2 : 0.0);
   }
   sm[sl][cl] = mu;
   sq[sl][cl] = m2;
@@ -293,7 +314,20 @@ __global__ __launch_bounds__(256) void bn_tiles_final(const double* __restrict__
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   double n = 0.0, mean = 0.0, M2 = 0.0;
-  for (int g = 0; g < G; ++g) {
+  int g = 0;
+  for (; g + 4 <= G; g += 4) {  // four groups' records loaded before the (ordered) merges
+    double r[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double* o = ws + ((size_t)(g + u) * C + c) * 3;
+      r[u][0] = o[0];
+      r[u][1] = o[1];
+      r[u][2] = o[2];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) chan_merge(n, mean, M2, r[u][0], r[u][1], r[u][2]);
+  }
+  for (; g < G; ++g) {
     const double* o = ws + ((size_t)g * C + c) * 3;
     chan_merge(n, mean, M2, o[0], o[1], o[2]);
   }

@@ -30,6 +30,29 @@ def make_step(model: str, batch: int, seq: int):
     raise ValueError(model)
 
 
+def report_sources(step, active: int, pats) -> None:
+    """For every kernel whose name contains one of `pats`: the launching CPU op and its Python stack, with counts."""
+    from collections import Counter
+
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        for _ in range(active):
+            step()
+        torch.cuda.synchronize()
+    hits = Counter()
+    for ev in prof.events():
+        for k in getattr(ev, "kernels", []) or []:
+            name = getattr(k, "name", str(k))
+            for p in pats:
+                if p in name:
+                    stack = [f for f in (ev.stack or []) if "mifx" in f or "tools/" in f][:6]
+                    hits[(p, ev.name, " <- ".join(stack))] += 1
+    print(f"# kernel sources over {active} steps")
+    for (p, op, stack), n in hits.most_common():
+        print(f"- [{p}] x{n / active:.1f}/step  op `{op}`  {stack}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet")
@@ -38,6 +61,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--active", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--sources", default="", help="comma-separated kernel-name substrings: report the Python "
+                    "stacks (and CPU ops) that launched them instead of the table")
     a = ap.parse_args()
     from mifx.utils.meter import heartbeat
 
@@ -49,6 +74,8 @@ def main():
             print(f"[{a.model}] warmup step {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
     from torch.profiler import ProfilerActivity, profile
 
+    if a.sources:
+        return report_sources(step, a.active, [p for p in a.sources.split(",") if p])
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
         for _ in range(a.active):
             step()
