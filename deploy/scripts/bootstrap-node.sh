@@ -50,6 +50,7 @@ if [ "$K8S" = 1 ]; then
   command -v kubectl >/dev/null || { echo "kubectl not found" >&2; exit 1; }
   kubectl get namespace kubeflow >/dev/null 2>&1 || kubectl create namespace kubeflow
   kubectl apply -f "$REPO/deploy/crd/mifxjob-crd.yaml"
+  kubectl apply -f "$REPO/deploy/crd/studyjob-notebook-crds.yaml"
   kubectl label node "$(hostname)" amd.com/gpu.present=true --overwrite || true
   kubectl apply -k "$REPO/deploy/k8s"
   for i in $(seq 1 60); do

@@ -253,11 +253,15 @@ def main(argv=None):
     import argparse
 
     ap = argparse.ArgumentParser(prog="python -m mifx.hpo.study")
-    ap.add_argument("spec")
+    ap.add_argument("spec", nargs="?", help="StudyJob YAML file")
+    ap.add_argument("--spec-json", default=None, help="the StudyJob as JSON (the operator's rendered Job)")
     ap.add_argument("--workdir", default="/tmp/mifx_hpo")
     ap.add_argument("--num-gpus", type=int, default=None)
     a = ap.parse_args(argv)
-    res = StudyRunner(StudySpec.from_yaml(a.spec), workdir=a.workdir, num_gpus=a.num_gpus).run()
+    if (a.spec is None) == (a.spec_json is None):
+        ap.error("give a spec file or --spec-json")
+    spec = StudySpec.from_yaml(a.spec) if a.spec else StudySpec.from_dict(json.loads(a.spec_json))
+    res = StudyRunner(spec, workdir=a.workdir, num_gpus=a.num_gpus).run()
     print(json.dumps(res["best"], indent=1))
     return res
 

@@ -364,3 +364,106 @@ def test_reverse_proxy_and_bootstrap_cover_every_service():
                 "mifx.launch.operator", "mifx.serving.resp_server", "mifx.serving.server"):
         assert mod in text, mod
     assert "kubectl apply -k" in text and "mifxjob-crd.yaml" in text
+
+
+def test_operator_local_studyjob_and_notebook(tmp_path):
+    """Katib StudyJob CR -> a hyper-parameter study (trials parse `name=value` metrics from their logs), status
+    Succeeded with the best trial; Notebook CR -> a supervised notebook server that answers on its port and is
+    restarted if it exits."""
+    import socket
+    import sys
+    import time as _time
+
+    import requests
+
+    from mifx.launch import operator as op
+
+    crs = tmp_path / "crs"
+    crs.mkdir()
+    trial = "import sys; lr = float(sys.argv[1].split('=')[1]); print(f'accuracy={1 - abs(lr - 0.02):.6f}')"
+    study = {"apiVersion": "kubeflow.org/v1alpha1", "kind": "StudyJob", "metadata": {"name": "random-search"},
+             "spec": {"studyName": "random-search", "optimizationtype": "maximize", "objectivevaluename": "accuracy",
+                      "optimizationgoal": 0.9999, "requestcount": 2, "metricsnames": ["accuracy"],
+                      "parameterconfigs": [{"name": "--lr", "parametertype": "double",
+                                            "feasible": {"min": "0.01", "max": "0.03"}}],
+                      "suggestionSpec": {"suggestionAlgorithm": "random", "requestNumber": 3},
+                      "workerSpec": {"command": [sys.executable, "-c", trial]}}}
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    nb = {"apiVersion": "kubeflow.org/v1alpha1", "kind": "Notebook", "metadata": {"name": "nb"},
+          "spec": {"template": {"spec": {"containers": [{"ports": [{"containerPort": port}]}]}}}}
+    for cr in (study, nb):
+        (crs / f"{cr['metadata']['name']}.yaml").write_text(yaml.safe_dump(cr))
+    be = op.LocalBackend(str(crs), num_gpus=0)
+    try:
+        deadline = _time.time() + 120
+        while op.reconcile_all(be) and _time.time() < deadline:
+            _time.sleep(0.2)
+        st = {n: s for n, _, s in be.list()}
+        s = st["random-search"]
+        assert s["phase"] == "Succeeded" and s["trials"] == 6, s
+        assert s["bestTrial"]["metrics"]["accuracy"] > 0.99 and "--lr" in s["bestTrial"]["parameters"]
+        assert st["nb"]["phase"] == "Running" and st["nb"]["url"].endswith(f":{port}/")
+        ok = False
+        for _ in range(100):
+            try:
+                ok = requests.get(f"http://127.0.0.1:{port}/api/notebooks", timeout=2).status_code == 200
+                break
+            except requests.RequestException:
+                _time.sleep(0.3)
+        assert ok
+        be._procs["nb"].terminate()  # the server exits: the next pass restarts it
+        be._procs["nb"].wait(timeout=10)
+        op.reconcile_all(be)
+        st = {n: s for n, _, s in be.list()}
+        assert st["nb"]["restarts"] == 1 and st["nb"]["phase"] == "Running"
+        assert be._procs["nb"].poll() is None
+    finally:
+        be.stop()
+
+
+def test_operator_kube_backend_studyjob_and_notebook():
+    from mifx.launch import operator as op
+
+    class FakeApi:
+        def __init__(self, crs):
+            self.objs, self.crs = {}, crs
+
+        def get(self, path):
+            for plural, kind in (("/studyjobs", "StudyJob"), ("/notebooks", "Notebook")):
+                if path.endswith(plural):
+                    return {"items": [c for c in self.crs if c["kind"] == kind]}
+            if path.endswith(("/mifxjobs", "/tfjobs", "/pytorchjobs")):
+                return None
+            return self.objs.get(path)
+
+        def post(self, path, body):
+            self.objs[f"{path}/{body['metadata']['name']}"] = body
+            return body
+
+        def patch_status(self, path, status):
+            for c in self.crs:
+                if path.endswith(f"/{c['metadata']['name']}"):
+                    c["status"] = status
+
+    study = {"kind": "StudyJob", "metadata": {"name": "s1", "uid": "u2"},
+             "spec": {"studyName": "s1", "objectivevaluename": "accuracy", "requestcount": 1,
+                      "parameterconfigs": [{"name": "--lr", "parametertype": "double",
+                                            "feasible": {"min": "0.01", "max": "0.03"}}],
+                      "workerSpec": {"command": ["python3", "train.py"]}}}
+    nb = {"kind": "Notebook", "metadata": {"name": "nb1", "uid": "u3"}, "spec": {}}
+    api = FakeApi([study, nb])
+    be = op.KubeBackend(api, "kubeflow", image="img")
+    op.reconcile_all(be)
+    job = api.objs["/apis/batch/v1/namespaces/kubeflow/jobs/s1"]
+    cmd = job["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert cmd[:4] == ["python3", "-m", "mifx.hpo.study", "--spec-json"]
+    assert json.loads(cmd[4])["spec"]["studyName"] == "s1" and study["status"]["phase"] == "Created"
+    dep = api.objs["/apis/apps/v1/namespaces/kubeflow/deployments/nb1"]
+    assert dep["spec"]["template"]["spec"]["containers"][0]["ports"][0]["containerPort"] == 8888
+    assert "/api/v1/namespaces/kubeflow/services/nb1" in api.objs and nb["status"]["phase"] == "Created"
+    dep["status"] = {"readyReplicas": 1}
+    job["status"] = {"succeeded": 1}
+    op.reconcile_all(be)
+    assert nb["status"]["phase"] == "Running" and study["status"]["phase"] == "Succeeded"
