@@ -5,7 +5,7 @@ Reference: the KFP API server the workshop deploys (`install-kubeflow/ks_app/ven
 prototypes, api-server on 8888) and the client calls in `sdk/python/kfp/_client.py:124-316`
 (experiments create/get/list, runs create/get/list with resource references, pipeline upload).
 Run: `python -m mifx.kfp.server --port 8888 --root /var/lib/mifx/pipelines`, then
-`Client(host="http://<host>:8888")`."""
+`Client(host="http://<host>:8888")`; the same port serves the pipelines UI (mifx.kfp.ui) at `/`."""
 import argparse
 import email.parser
 import email.policy
@@ -90,6 +90,29 @@ def create_app(root: str, max_parallel: int = 4):
     @app.get("/apis/v1beta1/healthz")
     def healthz():
         return {"status": "ok", "backend": "local", "root": backend.root}
+
+    # ---- pipelines UI (mifx.kfp.ui): read-only HTML views
+    from fastapi.responses import HTMLResponse
+
+    from . import ui
+
+    @app.get("/", response_class=HTMLResponse)
+    def ui_index():
+        return ui.index(backend)
+
+    @app.get("/ui/runs/{run_id}", response_class=HTMLResponse)
+    def ui_run(run_id: str):
+        try:
+            return ui.run_page(backend, run_id)
+        except ValueError as e:
+            raise HTTPException(404, str(e)) from e
+
+    @app.get("/ui/pipelines/{pid}", response_class=HTMLResponse)
+    def ui_pipeline(pid: str):
+        try:
+            return ui.pipeline_page(backend, pid)
+        except ValueError as e:
+            raise HTTPException(404, str(e)) from e
 
     app.state.backend = backend
     return app

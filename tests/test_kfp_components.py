@@ -354,9 +354,29 @@ def test_pipelines_api_server_with_rest_client(tmp_path):
         assert client.list_runs(experiment_id=exp.id).runs[0].id == run.id
         pl = client.upload_pipeline(pkg, "retry")
         assert any(p.id == pl.id for p in client.list_pipelines().pipelines)
+        # the pipelines UI on the same port: index, the run's graph (an SVG box per executed node), the pipeline DAG
+        import requests
+
+        idx = requests.get(f"http://127.0.0.1:{port}/", timeout=10)
+        assert idx.status_code == 200 and "rest-run" in idx.text and f"/ui/runs/{run.id}" in idx.text
+        page = requests.get(f"http://127.0.0.1:{port}/ui/runs/{run.id}", timeout=10).text
+        wf = client._get_workflow_json(run.id)
+        assert "<svg" in page and page.count("<rect") >= 1 and detail.run.status in page
+        assert page.count("<rect") == len(wf["status"]["nodes"])
+        pp = requests.get(f"http://127.0.0.1:{port}/ui/pipelines/{pl.id}", timeout=10)
+        assert pp.status_code == 200 and "<table>" in pp.text
+        assert requests.get(f"http://127.0.0.1:{port}/ui/runs/nope", timeout=10).status_code == 404
     finally:
         server.should_exit = True
         th.join(timeout=10)
+
+
+def test_pipelines_ui_layout_and_escaping():
+    from mifx.kfp import ui
+
+    pos = ui.layout({"a": ["b", "c"], "b": ["d"], "c": ["d"], "d": []})
+    assert pos["a"][0] == 0 and pos["b"][0] == pos["c"][0] == 1 and pos["d"][0] == 2
+    assert ui._e("<script>") == "&lt;script&gt;"
 
 
 def test_local_executor_deep_recursion_keeps_step_dirs_short(tmp_path):
