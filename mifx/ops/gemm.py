@@ -238,6 +238,8 @@ def _dw_tensor(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 # result into the weight's .grad -- whatever tensor autograd ended up storing there -- so the gradients must be reset
 # (None or zero) before the backward and each weight may receive ONE recorded product per flush.
 _DEFER: dict = {"on": False, "pending": [], "pending_f32": []}
+# token rows per split-K item of the fp32 (convolution) weight gradients; MIFX_WGRAD_CHUNK overrides (A/B)
+_WGRAD_CHUNK = int(os.environ.get("MIFX_WGRAD_CHUNK", "4096"))
 
 
 class deferred_weight_grads:
@@ -315,7 +317,7 @@ def flush_weight_grads() -> int:
         for rec in pf:
             dy, x, w, ph = rec[:4]
             geo = rec[4] if len(rec) > 4 else None
-            ck = rec[5] if len(rec) > 5 else 4096
+            ck = rec[5] if len(rec) > 5 else _WGRAD_CHUNK
             g = w.grad
             lay_ok = g is not None and (g.is_contiguous(memory_format=torch.channels_last) if geo is not None
                                         else g.is_contiguous())
