@@ -874,6 +874,7 @@ def matmul_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 # (csrc/gemm.hip EPI_GELU_BWD on the transposed W2 copy): the unfused path writes dH [tokens, 3072] and the
 # bias_gelu backward kernel reads it back with Z. (M, N, K) of the dH GEMM -> NT configuration.
 GELU_BWD_TUNED: dict[tuple[int, int, int], int] = {(4096, 3072, 768): 9}
+_GELU_BWD_G8 = os.environ.get("MIFX_GELU_BWD_G8", "0") == "1"
 
 
 def _gelu_bwd_gemm(dout2: torch.Tensor, w2: torch.Tensor, z: torch.Tensor, b1: torch.Tensor, cfg: int):
@@ -881,8 +882,15 @@ def _gelu_bwd_gemm(dout2: torch.Tensor, w2: torch.Tensor, z: torch.Tensor, b1: t
     [out, in]), z [M, N] bf16."""
     M, K = dout2.shape
     N = w2.shape[1]
-    bm = configs()[cfg][0]
     bp = b1 if b1.dtype in (torch.float32, torch.bfloat16) else b1.float()
+    if _GELU_BWD_G8:  # the pipelined kernel's GELU-backward epilogue (A/B: MIFX_GELU_BWD_G8=1)
+        g8 = gemm8_pick(M, N, K)
+        if g8 is not None:
+            dz, part = gemm8_nt(dout2.contiguous(), transposed(w2), bp.contiguous(), 4, cfg=g8, z=z)
+            from .fused_bert import col_sum
+
+            return dz, col_sum(part, b1.dtype if b1.dtype in (torch.float32, torch.bfloat16) else torch.float32)
+    bm = configs()[cfg][0]
     dz = torch.empty(M, N, device=dout2.device, dtype=torch.bfloat16)
     part = torch.empty(M // bm, N, device=dout2.device, dtype=torch.float32)
     check(_fns()["gelu_bwd"](int(cfg), int(bp.dtype == torch.float32), ptr(dout2.contiguous()), ptr(transposed(w2)),
