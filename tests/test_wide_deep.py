@@ -188,11 +188,22 @@ def test_fused_gradients_match_torch(batch, kernel):
     named = wdm.canonical_grad_to_torch(g_tn, m, gidx)
     mref = wdm.unpack_canonical(tr.param.cpu(), wdm.WideDeepModel(seed=1))
     _, ref = _torch_grads(mref, rec)
-    lim = 0.15 if batch < 1000 else 0.06
+    #    Bounds from the measured errors (round 5, every kernel: B 40 <= 0.103, 64 <= 0.096, 1000 <= 0.050,
+    #    8192 <= 0.0057) with ~20 % margin; and, since a Frobenius bound alone would pass a systematic scaling of the
+    #    gradient of that size, the projection <g, r> / <r, r> of each gradient on the reference must be 1 to within
+    #    a few noise standard deviations (rounding noise is unbiased; a 10 % bias gives 0.9).
+    lim = 0.125 if batch < 1000 else (0.06 if batch < 8192 else 0.008)
+    plim = 0.05 if batch < 1000 else 0.02
+    rels, projs = {}, {}
     for name, r in ref.items():
         gk = named[name].reshape(r.shape)
         rel = np.linalg.norm(gk - r) / (np.linalg.norm(r) + 1e-8)
+        proj = float(np.sum(gk * r) / (np.sum(r * r) + 1e-30))
+        rels[name], projs[name] = float(rel), proj
         assert rel < lim, f"{name}: relative Frobenius err {rel:.4f}"
+        assert abs(proj - 1.0) < plim, f"{name}: gradient projection on the fp32 reference {proj:.4f}"
+    print(f"[wd-grad-rel] batch {batch} kernel {kernel} " + " ".join(f"{k}={v:.4f}/{projs[k]:.4f}"
+                                                                     for k, v in rels.items()))
 
 
 @pytest.mark.gpu
