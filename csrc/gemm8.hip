@@ -157,17 +157,28 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   static_assert(CV == 0 || (CV == 1 && !TN) || (CV == 2 && TN), "conv gather: NT rows (1) or TN B rows (2)");
   constexpr int HA = BM / 2, HB = BN / 2;            // rows (NT) / columns (TN) per half-tile
   constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // NT: 64 bf16 per row; TN: 64 token rows of HA bf16
-  constexpr int XR = HA * 8 / NT, WR = HB * 8 / NT;    // DMAs per thread per half-tile
+  // NARROW (NT, BN = 64: the 64-channel convolutions of ResNet-50's first stage): the 8 waves tile a quadrant 4 x 2
+  // instead of 2 x 4 (each wave 16 columns), and the 32-row B half-tile is staged by half the threads, the other half
+  // re-issuing the same DMAs (same source, same LDS bytes) so every wave's counted vmcnt stays uniform
+  constexpr bool NARROW = !TN && BN == 64;
+  constexpr int WROWS = NARROW ? 4 : 2, WCOLS = NARROW ? 2 : 4;  // wave grid inside a quadrant
+  constexpr int RPW = HA / WROWS, CPW = HB / WCOLS;              // rows / columns per wave per quadrant
+  constexpr int BDMA = HB * 8;                                   // B DMAs per half-tile
+  constexpr int XR = HA * 8 / NT, WR = (BDMA + NT - 1) / NT;     // DMAs per thread per half-tile
+  constexpr bool WDUP = BDMA < NT;
   constexpr int CPA = HA / 8, CPB = HB / 8;            // TN: 16-byte chunks per token row
-  static_assert(HA * 8 % NT == 0 && HB * 8 % NT == 0, "whole DMA rounds per half-tile");
-  constexpr int MF = HA / 32, NF = HB / 64;  // 16-row fragments per wave per quadrant (2 x 4 waves)
-  static_assert(MF >= 1 && NF >= 1, "tile too small for 8 waves");
+  static_assert(HA * 8 % NT == 0 && (BDMA % NT == 0 || NT % BDMA == 0), "whole DMA rounds per half-tile");
+  static_assert(!WDUP || NARROW, "duplicated B DMAs are the narrow layout's");
+  constexpr int MF = RPW / 16, NF = CPW / 16;  // 16-row fragments per wave per quadrant
+  static_assert(MF >= 1 && NF >= 1 && RPW % 16 == 0 && CPW % 16 == 0, "tile too small for 8 waves");
+  static_assert(!NARROW || EPI != EPI_GELU_BWD, "the GELU-backward epilogue's column sums assume 2 wave rows");
   constexpr int BUF = 2 * (ABYTES + BBYTES);
   constexpr int OFF_A0 = 0, OFF_B0 = ABYTES, OFF_A1 = ABYTES + BBYTES, OFF_B1 = 2 * ABYTES + BBYTES;
   constexpr int KTILE_DMAS = 2 * (XR + WR);  // DMAs per thread per K-tile = per 4 consecutive phases
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int wm = w >> 2, wn = w & 3;  // wave position inside a quadrant; wm is also the stagger group
+  const int grp = w >> 2;  // stagger group (waves 4-7 run one barrier behind waves 0-3)
+  const int wm = NARROW ? (w & 3) : (w >> 2), wn = NARROW ? (w >> 2) : (w & 3);  // wave position in a quadrant
   const int KT = K / BK;
 
   // per-lane DMA source offsets (elements, K-tile 0) of each half, pre-swizzled / pre-rotated
@@ -187,7 +198,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   }
 #pragma unroll
   for (int i = 0; i < WR; ++i) {
-    const int qq = i * NT + tid;
+    const int qq = WDUP ? tid % BDMA : i * NT + tid;
     if constexpr (TN) {
       const int t = qq / CPB, pc = qq % CPB;
       int c = pc - rot<CPB>(t);
@@ -277,9 +288,10 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       const bf16* src = TN ? W + (size_t)k0 * N + (h == 3 ? HB : 0) : W + (h == 3 ? HB * K : 0) + k0;
 #pragma unroll
       for (int i = 0; i < WR; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(src + boff[i]),
-                                         (__attribute__((address_space(3))) void*)(dst + (i * NT + 64 * w) * 16), 16,
-                                         0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(src + boff[i]),
+            (__attribute__((address_space(3))) void*)(dst + (WDUP ? (64 * w) % BDMA : i * NT + 64 * w) * 16), 16, 0,
+            0);
     }
   };
 
@@ -309,11 +321,11 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   auto read_a = [&](const unsigned char* half, v8bf (&r)[MF][2]) {
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
-      const int row = wm * (HA / 2) + 16 * f + fr;
+      const int row = wm * RPW + 16 * f + fr;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         if constexpr (TN)
-          r[f][ks] = tn_frag(half, CPA, wm * (HA / 2) + 16 * f, ks);
+          r[f][ks] = tn_frag(half, CPA, wm * RPW + 16 * f, ks);
         else
           r[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
       }
@@ -322,11 +334,11 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   auto read_b = [&](const unsigned char* half) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const int row = wn * (HB / 4) + 16 * f + fr;
+      const int row = wn * CPW + 16 * f + fr;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         if constexpr (TN)
-          rb[f][ks] = tn_frag(half, CPB, wn * (HB / 4) + 16 * f, ks);
+          rb[f][ks] = tn_frag(half, CPB, wn * CPW + 16 * f, ks);
         else
           rb[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
       }
@@ -361,7 +373,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   barrier();
-  if (wm == 1) barrier();  // the stagger: waves 4-7 one barrier behind
+  if (grp == 1) barrier();  // the stagger: waves 4-7 one barrier behind
 
   for (int t = 0; t < KT; ++t) {
     const unsigned char* buf = lds + (t & 1) * BUF;
@@ -400,7 +412,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     phase(std::integral_constant<int, 2>{});
     phase(std::integral_constant<int, 3>{});
   }
-  if (wm == 0) barrier();  // equal barrier counts for both groups
+  if (grp == 0) barrier();  // equal barrier counts for both groups
 
   // ---- epilogue: acc[mq][nq][a][b][r] = Y[m0 + mq HA + wm HA/2 + 16 b + fr][n0 + nq HB + wn HB/4 + 16 a + 4 fc + r]
   if constexpr (EPI == EPI_GELU_BWD) {
@@ -411,7 +423,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
       for (int a = 0; a < NF; ++a) {
-        const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+        const int n = n0 + nq * HB + wn * CPW + 16 * a + 4 * fc;
         float bv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -422,7 +434,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
         for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
           for (int b = 0; b < MF; ++b) {
-            const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            const int m = m0 + mq * HA + wm * RPW + 16 * b + fr;
             const v4bf zv = *(const v4bf*)(Z + (size_t)m * N + n);
             v4bf o;
 #pragma unroll
@@ -454,7 +466,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
 #pragma unroll
         for (int a = 0; a < NF; ++a)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) red[wm * BN + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc + r] = cs[nq][a][r];
+          for (int r = 0; r < 4; ++r) red[wm * BN + nq * HB + wn * CPW + 16 * a + 4 * fc + r] = cs[nq][a][r];
     }
     __syncthreads();
     for (int c = tid; c < BN; c += NT) part[(size_t)(m0 / BM) * N + n0 + c] = red[c] + red[BN + c];
@@ -465,12 +477,12 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
       for (int a = 0; a < NF; ++a) {
-        const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+        const int n = n0 + nq * HB + wn * CPW + 16 * a + 4 * fc;
 #pragma unroll
         for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
           for (int b = 0; b < MF; ++b) {
-            const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            const int m = m0 + mq * HA + wm * RPW + 16 * b + fr;
             *(v4f*)(part + (size_t)m * N + n) = acc[mq][nq][a][b];
           }
       }
@@ -481,7 +493,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
       for (int a = 0; a < NF; ++a) {
-        const int n = n0 + nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+        const int n = n0 + nq * HB + wn * CPW + 16 * a + 4 * fc;
         float bv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[r] = (float)bias[n + r];
@@ -489,7 +501,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
         for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
           for (int b = 0; b < MF; ++b) {
-            const int m = m0 + mq * HA + wm * (HA / 2) + 16 * b + fr;
+            const int m = m0 + mq * HA + wm * RPW + 16 * b + fr;
             v4bf o, z;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -526,7 +538,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
     for (int a = 0; a < NF; ++a) {
-      const int col = nq * HB + wn * (HB / 4) + 16 * a + 4 * fc;
+      const int col = nq * HB + wn * CPW + 16 * a + 4 * fc;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI == EPI_BIAS) {
 #pragma unroll
@@ -536,7 +548,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
         for (int b = 0; b < MF; ++b) {
-          const int row = mq * HA + wm * (HA / 2) + 16 * b + fr;
+          const int row = mq * HA + wm * RPW + 16 * b + fr;
           v4bf o;
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mq][nq][a][b][r] + bv[r]);
@@ -600,6 +612,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     auto reduce_cols = [&](float (&v)[8], float* outc, float scale) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
+        if constexpr (CPR_O <= 8) v[e] += __shfl_xor(v[e], 8);
         if constexpr (CPR_O <= 16) v[e] += __shfl_xor(v[e], 16);
         v[e] += __shfl_xor(v[e], 32);
       }
@@ -840,8 +853,12 @@ int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bi
                       : launch<BM, BN, EPI_BIAS_GELU, bf16>(X, W, bias, Y, Z, M, N, K, nullptr, st);
     case EPI_ADD_R: return launch<BM, BN, EPI_ADD_R, bf16>(X, W, bias, Y, nullptr, M, N, K, nullptr, st);
     case EPI_GELU_BWD:
-      return bias_f32 ? launch<BM, BN, EPI_GELU_BWD, float>(X, W, bias, Y, Z, M, N, K, part, st)
-                      : launch<BM, BN, EPI_GELU_BWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
+      if constexpr (BN == 64) {
+        return -1;  // (not built for the narrow tiles)
+      } else {
+        return bias_f32 ? launch<BM, BN, EPI_GELU_BWD, float>(X, W, bias, Y, Z, M, N, K, part, st)
+                        : launch<BM, BN, EPI_GELU_BWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
+      }
     case EPI_STATS: return launch<BM, BN, EPI_STATS, bf16>(X, W, nullptr, Y, nullptr, M, N, K, part, st);
     case EPI_ADD_STATS: return launch<BM, BN, EPI_ADD_STATS, bf16>(X, W, bias, Y, nullptr, M, N, K, part, st);
     case EPI_BNBWD: return launch<BM, BN, EPI_BNBWD, bf16>(X, W, bias, Y, Z, M, N, K, part, st);
@@ -853,7 +870,7 @@ int dispatch(int epi, int bias_f32, const void* X, const void* W, const void* bi
 struct Cfg {
   int bm, bn;
 };
-constexpr Cfg kCfgs[] = {{256, 256}, {256, 128}, {128, 256}, {128, 128}};
+constexpr Cfg kCfgs[] = {{256, 256}, {256, 128}, {128, 256}, {128, 128}, {256, 64}, {128, 64}};
 
 }  // namespace
 
@@ -896,7 +913,9 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
     case 0: return dispatch<256, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
     case 1: return dispatch<256, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
     case 2: return dispatch<128, 256>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
-    default: return dispatch<128, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
+    case 3: return dispatch<128, 128>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
+    case 4: return dispatch<256, 64>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
+    default: return dispatch<128, 64>(epi, bias_f32, X, W, bias, Y, Z, M, N, K, part, st, R2);
   }
 }
 
@@ -922,7 +941,9 @@ int mifx_gemm8_conv3x3(int cfg, int epi, const void* x, const void* w, const voi
     case 0: return dispatch_conv<256, 256>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
     case 1: return dispatch_conv<256, 128>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
     case 2: return dispatch_conv<128, 256>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
-    default: return dispatch_conv<128, 128>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+    case 3: return dispatch_conv<128, 128>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+    case 4: return dispatch_conv<256, 64>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
+    default: return dispatch_conv<128, 64>(epi, x, w, bias, y, Z, M, N, K, part, g, st);
   }
 }
 

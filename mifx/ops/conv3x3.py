@@ -18,8 +18,8 @@ profiles/resnet_steady_r5g.md) and BN2 / BN1 each needed a reduction pass. Here:
   chunks of 256 x 256 tiles); MIOpen's otherwise (it beats the 128-wide tiles). Per-shape timings of every pass:
   profiles/conv3x3_routes_r5.jsonl (tools/bench_conv3x3.py).
 
-Eligible: bf16 channels_last CUDA input, C a power of two >= 128, Cout % 128 == 0, padding 1, stride 1 or 2, and
-N OH OW a multiple of a tile height."""
+Eligible: bf16 channels_last CUDA input, C a power of two >= 128 (>= 64 with MIFX_CONV3X3_64=1: the narrow tiles),
+Cout % 128 == 0 (% 64), padding 1, stride 1 or 2, and N OH OW a multiple of a tile height."""
 from __future__ import annotations
 
 import os
@@ -29,8 +29,10 @@ import torch
 from . import gemm as hg
 from . import native_stats, weight_prep
 
-# MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B)
+# MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B); MIFX_CONV3X3_64=1 also takes
+# the 64-channel ones (stage 1, on the narrow tiles)
 ENABLED = os.environ.get("MIFX_CONV3X3", "1") != "0"
+_SMALL = os.environ.get("MIFX_CONV3X3_64", "0") == "1"
 
 
 # stride-2 input gradients where the phase-split hand-written kernel measured faster than MIOpen, (input H, C, Cout)
@@ -54,8 +56,10 @@ def eligible(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int) -> boo
         return False
     n, c, h, w_ = x.shape
     cout = w.shape[0]
-    if c < 128 or c & (c - 1) or cout % 128 or w.shape[1] != c or (stride == 1 and cout & (cout - 1)):
+    if c < 64 or c & (c - 1) or cout % 64 or w.shape[1] != c or (stride == 1 and cout & (cout - 1)):
         return False  # (stride 1: the input gradient gathers dY, whose channel count must be a power of two too)
+    if (c < 128 or cout < 128) and not _SMALL:
+        return False
     oh, ow = (h + 2 - 3) // stride + 1, (w_ + 2 - 3) // stride + 1
     return hg.gemm8_pick(n * oh * ow, cout, 9 * c) is not None
 

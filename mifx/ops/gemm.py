@@ -667,8 +667,11 @@ def gemm8_configs() -> tuple[tuple[int, int], ...]:
 # Relative throughput of each tile shape when it fills the chip (4096^3: 1174 / 875 / 962 / 866 TFLOP/s, adjusted by
 # the ResNet 3x3 / 1x1 sweeps in profiles/conv3x3_routes_r5.jsonl) and workgroups per CU (128 x 128: <= 128 VGPRs and
 # 64 KB of LDS, two co-resident)
-_G8_EFF = {(256, 256): 1.0, (256, 128): 0.745, (128, 256): 0.78, (128, 128): 0.85}
-_G8_OCC = {(128, 128): 2}
+_G8_EFF = {(256, 256): 1.0, (256, 128): 0.745, (128, 256): 0.78, (128, 128): 0.85, (256, 64): 0.5, (128, 64): 0.45}
+_G8_OCC = {(128, 128): 2, (256, 64): 2, (128, 64): 2}
+# the 64-wide (narrow) tiles: the only configurations for N = 64 (ResNet-50 stage 1); MIFX_G8_NARROW=0 leaves those
+# products to the library (A/B)
+_G8_NARROW = os.environ.get("MIFX_G8_NARROW", "1") != "0"
 
 
 def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
@@ -676,7 +679,7 @@ def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
     filled) x (the tile's relative throughput); None if none tiles the shape."""
     best, best_score = None, None
     for i, (bm, bn) in enumerate(gemm8_configs()):
-        if M % bm or N % bn or K % 64:
+        if M % bm or N % bn or K % 64 or (bn == 64 and not _G8_NARROW):
             continue
         tiles = (M // bm) * (N // bn)
         slots = cus * _G8_OCC.get((bm, bn), 1)

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mifx.ops import gemm as hg  # noqa: E402
 
 # (input H, C, Cout, stride) of every eligible ResNet-50 v2 conv2, with its count per network
-SHAPES = [(56, 128, 128, 2, 1), (28, 128, 128, 1, 3), (28, 256, 256, 2, 1), (14, 256, 256, 1, 5),
+SHAPES = [(56, 64, 64, 1, 3), (56, 128, 128, 2, 1), (28, 128, 128, 1, 3), (28, 256, 256, 2, 1), (14, 256, 256, 1, 5),
           (14, 512, 512, 2, 1), (7, 512, 512, 1, 2)]
 
 
