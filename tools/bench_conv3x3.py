@@ -100,7 +100,7 @@ def main():
             geo = hg.conv_geo(n, h, h, c, stride, 1, x.device)
             dy2 = dy.permute(0, 2, 3, 1).reshape(M, cout)
             dw = torch.empty(cout, 3, 3, c, device="cuda")
-            for chunk in (2048, 4096, 8192, 16384):
+            for chunk in ((2048, 4096, 8192, 16384) if c >= 128 and cout >= 128 else ()):  # (TN tiles >= 128)
                 fn = lambda: hg.gemm8_tn_grouped([(dy2, xn, dw.view(cout, 9 * c), geo)], chunk=chunk,  # noqa
                                                  accumulate=False)
                 fn()
