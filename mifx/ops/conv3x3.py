@@ -18,7 +18,7 @@ profiles/resnet_steady_r5g.md) and BN2 / BN1 each needed a reduction pass. Here:
   chunks of 256 x 256 tiles); MIOpen's otherwise (it beats the 128-wide tiles). Per-shape timings of every pass:
   profiles/conv3x3_routes_r5.jsonl (tools/bench_conv3x3.py).
 
-Eligible: bf16 channels_last CUDA input, C a power of two >= 128 (>= 64 with MIFX_CONV3X3_64=1: the narrow tiles),
+Eligible: bf16 channels_last CUDA input, C a power of two >= 128 (>= 64: the narrow tiles; MIFX_CONV3X3_64=0 for >= 128),
 Cout % 128 == 0 (% 64), padding 1, stride 1 or 2, and N OH OW a multiple of a tile height."""
 from __future__ import annotations
 
@@ -29,10 +29,10 @@ import torch
 from . import gemm as hg
 from . import native_stats, weight_prep
 
-# MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B); MIFX_CONV3X3_64=1 also takes
-# the 64-channel ones (stage 1, on the narrow tiles)
+# MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B); MIFX_CONV3X3_64=0 leaves
+# the 64-channel ones (stage 1, on the narrow tiles: a tie with MIOpen in the step, profiles/resnet_narrow_ab_r5.txt)
 ENABLED = os.environ.get("MIFX_CONV3X3", "1") != "0"
-_SMALL = os.environ.get("MIFX_CONV3X3_64", "0") == "1"
+_SMALL = os.environ.get("MIFX_CONV3X3_64", "1") == "1"
 
 
 # stride-2 input gradients where the phase-split hand-written kernel measured faster than MIOpen, (input H, C, Cout)
