@@ -82,7 +82,9 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 // fragment read touches 64 distinct banks; tools/lds_banks_tn.py)
 template <int CPR>
 __device__ __forceinline__ int rot(int t) {
-  static_assert(CPR == 8 || CPR == 16, "chunks per token row");
+  static_assert(CPR == 4 || CPR == 8 || CPR == 16, "chunks per token row");
+  if constexpr (CPR == 4) return 2 * ((t >> 3) & 1);  // 64-byte rows (narrow tiles): the 16-lane groups of a half
+                                                      // read tokens 8 apart, shifted 8 banks
   if constexpr (CPR == 8) return ((t & 3) + 4 * ((t >> 3) & 3)) & 7;
   return (2 * (t & 3) + 8 * ((t >> 3) & 3)) & 15;
 }
@@ -122,6 +124,8 @@ constexpr int MAXP = 48;  // (the problem table travels in the kernel arguments:
 // the fp32 destination C -- the weight gradients of convolutions, whose token count (N H W = 12k-800k rows) is far
 // longer than their output is wide. TILE128: 128 x 128 tiles for this problem (dimensions % 256 != 0).
 constexpr int F32 = 1, TILE128 = 2, ACCUM = 4;  // ACCUM: C += sum of the partials (else C = the sum)
+// NARROW_N / NARROW_M: 256 x 64 / 64 x 256 tiles (a 64-wide weight-gradient dimension: ResNet-50's first stage)
+constexpr int NARROW_N = 16, NARROW_M = 32;
 // CONV: B is a 3x3 convolution's input gathered per output pixel (CV 2, geometry in device memory at `geo`); the
 // problem is dW[M = Cout][N = 9 C] = dY^T . X_taps, F32 only
 constexpr int CONV = 8;
@@ -160,15 +164,17 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   // NARROW (NT, BN = 64: the 64-channel convolutions of ResNet-50's first stage): the 8 waves tile a quadrant 4 x 2
   // instead of 2 x 4 (each wave 16 columns), and the 32-row B half-tile is staged by half the threads, the other half
   // re-issuing the same DMAs (same source, same LDS bytes) so every wave's counted vmcnt stays uniform
-  constexpr bool NARROW = !TN && BN == 64;
+  constexpr bool NARROW = BN == 64;
   constexpr int WROWS = NARROW ? 4 : 2, WCOLS = NARROW ? 2 : 4;  // wave grid inside a quadrant
   constexpr int RPW = HA / WROWS, CPW = HB / WCOLS;              // rows / columns per wave per quadrant
-  constexpr int BDMA = HB * 8;                                   // B DMAs per half-tile
-  constexpr int XR = HA * 8 / NT, WR = (BDMA + NT - 1) / NT;     // DMAs per thread per half-tile
-  constexpr bool WDUP = BDMA < NT;
+  constexpr int ADMA = HA * 8, BDMA = HB * 8;                   // A / B DMAs per half-tile
+  constexpr int XR = (ADMA + NT - 1) / NT, WR = (BDMA + NT - 1) / NT;  // DMAs per thread per half-tile
+  constexpr bool ADUP = ADMA < NT, WDUP = BDMA < NT;  // half the threads re-issue the other half's DMAs
   constexpr int CPA = HA / 8, CPB = HB / 8;            // TN: 16-byte chunks per token row
-  static_assert(HA * 8 % NT == 0 && (BDMA % NT == 0 || NT % BDMA == 0), "whole DMA rounds per half-tile");
+  static_assert((ADMA % NT == 0 || NT % ADMA == 0) && (BDMA % NT == 0 || NT % BDMA == 0),
+                "whole DMA rounds per half-tile");
   static_assert(!WDUP || NARROW, "duplicated B DMAs are the narrow layout's");
+  static_assert(!ADUP || (TN && CV == 0), "duplicated A DMAs: the TN narrow-M tiles only");
   constexpr int MF = RPW / 16, NF = CPW / 16;  // 16-row fragments per wave per quadrant
   static_assert(MF >= 1 && NF >= 1 && RPW % 16 == 0 && CPW % 16 == 0, "tile too small for 8 waves");
   static_assert(!NARROW || EPI != EPI_GELU_BWD, "the GELU-backward epilogue's column sums assume 2 wave rows");
@@ -185,7 +191,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   int aoff[XR], boff[WR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
-    const int qq = i * NT + tid;
+    const int qq = ADUP ? tid % ADMA : i * NT + tid;
     if constexpr (TN) {
       const int t = qq / CPA, pc = qq % CPA;  // token row, physical chunk
       int c = pc - rot<CPA>(t);
@@ -280,9 +286,10 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       const bf16* src = TN ? X + (size_t)k0 * M + (h == 2 ? HA : 0) : X + (h == 2 ? HA * K : 0) + k0;
 #pragma unroll
       for (int i = 0; i < XR; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(src + aoff[i]),
-                                         (__attribute__((address_space(3))) void*)(dst + (i * NT + 64 * w) * 16), 16,
-                                         0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(src + aoff[i]),
+            (__attribute__((address_space(3))) void*)(dst + (ADUP ? (64 * w) % ADMA : i * NT + 64 * w) * 16), 16, 0,
+            0);
     } else {
       unsigned char* dst = buf + (h == 1 ? OFF_B0 : OFF_B1);
       const bf16* src = TN ? W + (size_t)k0 * N + (h == 3 ? HB : 0) : W + (h == 3 ? HB * K : 0) + k0;
@@ -313,7 +320,8 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   auto tn_frag = [&](const unsigned char* half, int cpr_rot, int col0, int ks) -> v8bf {
     const int t1 = 32 * ks + 8 * fc + tq, t2 = t1 + 4;
     const int c = col0 / 8 + (tp >> 1);
-    int s1 = c + (cpr_rot == 16 ? rot<16>(t1) : rot<8>(t1)), s2 = c + (cpr_rot == 16 ? rot<16>(t2) : rot<8>(t2));
+    int s1 = c + (cpr_rot == 16 ? rot<16>(t1) : cpr_rot == 8 ? rot<8>(t1) : rot<4>(t1)),
+        s2 = c + (cpr_rot == 16 ? rot<16>(t2) : cpr_rot == 8 ? rot<8>(t2) : rot<4>(t2));
     s1 = s1 >= cpr_rot ? s1 - cpr_rot : s1;
     s2 = s2 >= cpr_rot ? s2 - cpr_rot : s2;
     return tr_frag(half + (t1 * cpr_rot + s1) * 16 + 8 * (tp & 1), half + (t2 * cpr_rot + s2) * 16 + 8 * (tp & 1));
@@ -691,7 +699,8 @@ __global__ __launch_bounds__(NT, 1) void gemm8_conv(const bf16* __restrict__ X, 
 template <int BM, int BN, bool TN>
 __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, unsigned char* lds) {
   constexpr int GM = 4;
-  const int bm = (p.flags & TILE128) ? BM / 2 : BM, bn = (p.flags & TILE128) ? BN / 2 : BN;
+  const int bm = (p.flags & TILE128) ? BM / 2 : (p.flags & NARROW_M) ? 64 : BM,
+            bn = (p.flags & TILE128) ? BN / 2 : (p.flags & NARROW_N) ? 64 : BN;
   const int nb_m = p.M / bm, nb_n = p.N / bn, tiles = nb_m * nb_n;
   const int sp = item / tiles, t = item - sp * tiles;
   const int per_group = GM * nb_n, grp = t / per_group, first_m = grp * GM, gsz = min(GM, nb_m - first_m);
@@ -702,7 +711,10 @@ __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, 
   if (p.flags & CONV) {  // (F32 only; the B rows are gathered from the whole input by pixel index t0 + ...)
     const Geo geo = *p.geo;
     float* P = p.P + (size_t)sp * p.M * p.N;
-    if (p.flags & TILE128)
+    if (p.flags & NARROW_N)
+      gemm8_tile<BM, 64, EPI_F32, bf16, true, 2>(A, p.B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
+                                                 geo, t0);
+    else if (p.flags & TILE128)
       gemm8_tile<BM / 2, BN / 2, EPI_F32, bf16, true, 2>(A, p.B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0,
                                                          lds, geo, t0);
     else
@@ -713,7 +725,11 @@ __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, 
   const bf16* B = p.B + (size_t)t0 * p.N;
   if (p.flags & F32) {
     float* P = p.P + (size_t)sp * p.M * p.N;
-    if (p.flags & TILE128)
+    if (p.flags & NARROW_N)
+      gemm8_tile<BM, 64, EPI_F32, bf16, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds);
+    else if (p.flags & NARROW_M)
+      gemm8_tile<64, BN, EPI_F32, bf16, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds);
+    else if (p.flags & TILE128)
       gemm8_tile<BM / 2, BN / 2, EPI_F32, bf16, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds);
     else
       gemm8_tile<BM, BN, EPI_F32, bf16, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds);
@@ -975,15 +991,19 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
   long long woff = 0, r4 = 0;
   for (int i = 0; i < n; ++i) {
     const int fl = flags[i], tb = (fl & TILE128) ? 128 : 256;
+    const int tm = (fl & NARROW_M) ? 64 : tb, tn = (fl & NARROW_N) ? 64 : tb;
     if (A[i] == nullptr || B[i] == nullptr || C[i] == nullptr || M[i] <= 0 || N[i] <= 0 || T[i] <= 0) return -1;
-    if (M[i] % tb || N[i] % tb || T[i] % BK || chunk[i] <= 0 || chunk[i] % BK) return -1;
+    if (M[i] % tm || N[i] % tn || T[i] % BK || chunk[i] <= 0 || chunk[i] % BK) return -1;
+    if ((fl & (NARROW_M | NARROW_N)) && (!(fl & F32) || (fl & TILE128) || (fl & NARROW_M && fl & NARROW_N) ||
+                                         (fl & NARROW_M && fl & CONV)))
+      return -1;
     if (!(fl & F32) && chunk[i] != T[i]) return -1;
     if ((uintptr_t)A[i] % 16 || (uintptr_t)B[i] % 16 || (uintptr_t)C[i] % 16) return -1;
     if ((long long)T[i] * M[i] >= (1ll << 31)) return -1;
     if (!(fl & CONV) && (long long)T[i] * N[i] >= (1ll << 31)) return -1;
     const Geo* geo = nullptr;
     if (fl & CONV) {  // geometry in device memory; N = 9 C with C % (tile width) == 0 (one tap per column block)
-      if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % 9 || (N[i] / 9) % tb) return -1;
+      if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % 9 || (N[i] / 9) % tn) return -1;
       geo = (const Geo*)geos[i];
     }
     const int S = (T[i] + chunk[i] - 1) / chunk[i];
@@ -997,10 +1017,10 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
       woff += (long long)S * M[i] * N[i];
       uniform256 = false;
     }
-    if (fl & TILE128) uniform256 = false;
+    if (fl & (TILE128 | NARROW_M | NARROW_N)) uniform256 = false;
     g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], C[i], P, geo, M[i], N[i], T[i], chunk[i], S, fl};
     g.first[i] = items;
-    items += (M[i] / tb) * (N[i] / tb) * S;
+    items += (M[i] / tm) * (N[i] / tn) * S;
   }
   g.first[n] = items;
   g.n = n;

@@ -272,7 +272,8 @@ def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor):
         return None
     T, N = dy2.shape
     K = x2.shape[1]
-    if N % 128 or K % 128 or T % 64 or N * K != w.numel():
+    tiles = (N % 128 == 0 and K % 128 == 0) or (N % 256 == 0 and K % 64 == 0) or (N % 64 == 0 and K % 256 == 0)
+    if not tiles or T % 64 or N * K != w.numel():  # (the last two: the narrow 256 x 64 / 64 x 256 tiles)
         return None
     native_stats.count("conv1x1_dW", True)
     # w.grad None (the trainer zeroes with set_to_none): autograd stores the returned tensor as .grad untouched, so
@@ -730,13 +731,19 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
             N = b.shape[1]
         f32 = c.dtype == torch.float32
         t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // 9) % 256))
+        # a 64-wide dimension (ResNet-50 stage 1): the narrow 256 x 64 / 64 x 256 tiles (fp32 problems)
+        cw = N // 9 if geo is not None else N
+        nar_n = f32 and tile128 is None and cw % 128 and cw % 64 == 0 and M % 256 == 0
+        nar_m = f32 and tile128 is None and geo is None and M % 128 and M % 64 == 0 and N % 256 == 0
+        if nar_n or nar_m:
+            t128 = False
         ck = pchunk if f32 else T
         Ms.append(M)
         Ns.append(N)
         Ts.append(T)
         chunks.append(ck)
         flags.append((1 if f32 else 0) | (2 if t128 else 0) | (4 if f32 and accs[len(flags)] else 0)
-                     | (8 if geo is not None else 0))
+                     | (8 if geo is not None else 0) | (16 if nar_n else 0) | (32 if nar_m else 0))
         geos.append(geo.data_ptr() if geo is not None else None)
         if f32:
             ws_floats += -(-T // ck) * M * N

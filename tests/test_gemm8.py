@@ -188,3 +188,18 @@ def test_gemm8_tn_grouped_fp32_split_accumulates():
     for (_, _, c), ref in zip(probs, refs):
         err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
         assert err < (1e-5 if c.dtype == torch.float32 else 1e-2), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(256, 64), (512, 192), (64, 256), (192, 512)])
+def test_gemm8_tn_grouped_narrow_fp32(M, N):
+    """fp32 split-K weight gradients with a 64-wide dimension on the narrow 256 x 64 / 64 x 256 tiles (duplicated
+    DMAs, 64-byte rotated token rows), accumulating into an existing gradient, against fp32."""
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    T = 4096 + 640
+    a = (torch.rand(T, M, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+    b = (torch.rand(T, N, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+    c = torch.randn(M, N, device="cuda", generator=g)
+    want = c + a.float().t() @ b.float()
+    gemm.gemm8_tn_grouped([(a, b, c)], chunk=2048)
+    torch.testing.assert_close(c, want, rtol=1e-4, atol=1e-3)
