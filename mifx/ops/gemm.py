@@ -272,7 +272,8 @@ def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor):
         return None
     T, N = dy2.shape
     K = x2.shape[1]
-    tiles = (N % 128 == 0 and K % 128 == 0) or (N % 256 == 0 and K % 64 == 0) or (N % 64 == 0 and K % 256 == 0)
+    tiles = (N % 128 == 0 and K % 128 == 0) or (_G8_NARROW and ((N % 256 == 0 and K % 64 == 0)
+                                                                 or (N % 64 == 0 and K % 256 == 0)))
     if not tiles or T % 64 or N * K != w.numel():  # (the last two: the narrow 256 x 64 / 64 x 256 tiles)
         return None
     native_stats.count("conv1x1_dW", True)
@@ -733,8 +734,9 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
         t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // 9) % 256))
         # a 64-wide dimension (ResNet-50 stage 1): the narrow 256 x 64 / 64 x 256 tiles (fp32 problems)
         cw = N // 9 if geo is not None else N
-        nar_n = f32 and tile128 is None and cw % 128 and cw % 64 == 0 and M % 256 == 0
-        nar_m = f32 and tile128 is None and geo is None and M % 128 and M % 64 == 0 and N % 256 == 0
+        nar_n = _G8_NARROW and f32 and tile128 is None and cw % 128 and cw % 64 == 0 and M % 256 == 0
+        nar_m = _G8_NARROW and f32 and tile128 is None and geo is None and M % 128 and M % 64 == 0 \
+            and N % 256 == 0
         if nar_n or nar_m:
             t128 = False
         ck = pchunk if f32 else T

@@ -1,0 +1,13 @@
+# round 5: narrow TN weight-gradient tiles; tests; ResNet A/B (narrow on/off) + steady table; shared multi-rank bench
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests/test_gemm8.py tests/test_conv1x1.py tests/test_conv3x3.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r5u_tests.log 2>&1; rc=$?
+tail -2 gpurun_out/r5u_tests.log; [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/r5u_tests.log | head -30; tail -30 gpurun_out/r5u_tests.log; exit $rc; }
+for v in 1 0 1 0; do
+  MIFX_G8_NARROW=$v timeout -k 10 400 python -u -m mifx.trainer.resnet_trainer --steps 20 --warmup 5 > gpurun_out/r5u_resnet_$v.json 2> gpurun_out/r5u_resnet_$v.err || { tail -20 gpurun_out/r5u_resnet_$v.err; exit 1; }
+  python -c "import json; r=json.loads([l for l in open('gpurun_out/r5u_resnet_$v.json') if l.startswith('{')][-1]); print('narrow', $v, round(r['value'],1), round(r['ms_per_step'],3), 'ms')"
+done
+timeout -k 10 300 python -u tools/torch_kernel_table.py --model resnet --batch 256 --warmup 8 --active 3 > gpurun_out/resnet_steady_r5u.md 2> gpurun_out/resnet_steady_r5u.err || { tail -5 gpurun_out/resnet_steady_r5u.err; exit 1; }
+head -40 gpurun_out/resnet_steady_r5u.md
+bash tools/gpu_batches/r5t.sh
