@@ -51,7 +51,8 @@ def test_conv1x1_forward_stats_backward(cin, cout, res):
     y2, _ = conv1x1(x.detach(), w2, r.detach() if res else None, stats=True)
     with hg.deferred_weight_grads():
         y2.backward(gy)
-    assert hg.flush_weight_grads() == (1 if cin % 128 == 0 else 0)  # K = 64 stays on the library
+    # (Cin = 64 with Cout % 256: the narrow 256 x 64 grouped tiles)
+    assert hg.flush_weight_grads() == (1 if cin % 128 == 0 or cout % 256 == 0 else 0)
     torch.testing.assert_close(w2.grad, wr.grad, rtol=2e-2, atol=2e-2 * wr.grad.abs().max().item())
 
 
