@@ -110,6 +110,8 @@ struct Geo {
   int ow_sh;
   unsigned ohw_mul;
   int ohw_sh;
+  int tap0;  // first tap: 0 for a 3x3 convolution (K = 9 C); 4 (the center of a pad-1 3x3) for a strided 1x1 (K = C)
+  int ntaps;
 };
 __device__ __attribute__((aligned(16))) bf16 g_zero_page[64] = {};
 __device__ __forceinline__ int fdiv(int x, unsigned mul, int sh) {
@@ -251,7 +253,8 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     const int k0 = t * BK;
     if (CV == 1 && (h == 0 || h == 2)) {  // gathered pixel rows of tap k0 / C, channels [k0 % C, + 64)
       unsigned char* dst = buf + (h == 0 ? OFF_A0 : OFF_A1);
-      const int hh = h >> 1, tap = k0 >> geo.cshift, c0 = k0 & (geo.C - 1), r = tap / 3, sx = tap - 3 * r;
+      const int hh = h >> 1, tap = (k0 >> geo.cshift) + geo.tap0, c0 = k0 & (geo.C - 1), r = tap / 3,
+                sx = tap - 3 * r;
 #pragma unroll
       for (int i = 0; i < XR; ++i) {
         const int ih = cih[hh][i] + r, iw = ciw[hh][i] + sx;
@@ -265,7 +268,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     }
     if (CV == 2 && (h == 1 || h == 3)) {  // gathered token (pixel) rows for this tile's tap
       unsigned char* dst = buf + (h == 1 ? OFF_B0 : OFF_B1);
-      const int col = n0 + (h == 3 ? HB : 0), tap = col >> geo.cshift, c0 = col & (geo.C - 1), r = tap / 3,
+      const int col = n0 + (h == 3 ? HB : 0), tap = (col >> geo.cshift) + geo.tap0, c0 = col & (geo.C - 1), r = tap / 3,
                 sx = tap - 3 * r, ohw = geo.OH * geo.OW;
 #pragma unroll
       for (int i = 0; i < WR; ++i) {
@@ -837,8 +840,8 @@ int dispatch_conv(int epi, const void* X, const void* W, const void* bias, void*
   return -1;
 }
 
-Geo make_geo(int H, int W, int C, int OH, int OW, int stride, int pad) {
-  Geo g{H, W, C, OH, OW, stride, pad, 0, 0u, 0, 0u, 0};
+Geo make_geo(int H, int W, int C, int OH, int OW, int stride, int pad, int tap0 = 0, int ntaps = 9) {
+  Geo g{H, W, C, OH, OW, stride, pad, 0, 0u, 0, 0u, 0, tap0, ntaps};
   while ((1 << g.cshift) < C) ++g.cshift;
   auto magic = [](unsigned d, unsigned& mul, int& sh) {  // x / d == (umulhi(x, mul) + x) >> sh for x < 2^31
     sh = 0;
@@ -963,14 +966,41 @@ int mifx_gemm8_conv3x3(int cfg, int epi, const void* x, const void* w, const voi
   }
 }
 
-// The device-side geometry record of a 3x3 convolution for mifx_gemm8_tn_grouped's CONV problems (48 bytes).
+// The device-side geometry record of a convolution for mifx_gemm8_tn_grouped's CONV problems: a 3x3 pad-`pad`
+// convolution (center1x1 = 0, N = 9 C), or a strided 1x1 (center1x1 = 1: the center tap of a pad-1 3x3, N = C).
 int mifx_gemm8_geo_bytes() { return (int)sizeof(Geo); }
-int mifx_gemm8_geo(int Nb, int H, int W, int C, int stride, int pad, void* out) {
+int mifx_gemm8_geo(int Nb, int H, int W, int C, int stride, int pad, int center1x1, void* out) {
+  if (center1x1) pad = 1;
   const int OH = (H + 2 * pad - 3) / stride + 1, OW = (W + 2 * pad - 3) / stride + 1;
   if (out == nullptr || !geo_ok(Nb, H, W, C, OH, OW, stride, pad)) return -1;
-  const Geo g = make_geo(H, W, C, OH, OW, stride, pad);
+  const Geo g = center1x1 ? make_geo(H, W, C, OH, OW, stride, pad, 4, 1) : make_geo(H, W, C, OH, OW, stride, pad);
   __builtin_memcpy(out, &g, sizeof(Geo));
   return 0;
+}
+
+// Strided 1x1 convolution (stride 2 ResNet shortcuts) as the center tap of the implicit GEMM: y [Nb OH OW][N] =
+// x[Nb][stride oh][stride ow][:] . w[N][C]^T, OH = (H - 1) / stride + 1; epi 0 or 5 (statistics).
+int mifx_gemm8_conv1x1s(int cfg, int epi, const void* x, const void* w, void* y, float* part, int Nb, int H, int W,
+                        int C, int N, int stride, hipStream_t st) {
+  const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
+  if (cfg < 0 || cfg >= m || x == nullptr || w == nullptr || y == nullptr || stride < 1 || stride > 2) return -1;
+  const int OH = (H - 1) / stride + 1, OW = (W - 1) / stride + 1;
+  if (!geo_ok(Nb, H, W, C, OH, OW, stride, 1)) return -1;
+  const Cfg c = kCfgs[cfg];
+  const int M = Nb * OH * OW;
+  if (M % c.bm || N <= 0 || N % c.bn || (long long)N * C >= (1ll << 31)) return -1;
+  if (epi != 0 && epi != 5) return -1;
+  if (epi == 5 && part == nullptr) return -1;
+  if ((uintptr_t)x % 16 || (uintptr_t)w % 16 || (uintptr_t)y % 16) return -1;
+  const Geo g = make_geo(H, W, C, OH, OW, stride, 1, 4, 1);
+  switch (cfg) {
+    case 0: return dispatch_conv<256, 256>(epi, x, w, nullptr, y, nullptr, M, N, C, part, g, st);
+    case 1: return dispatch_conv<256, 128>(epi, x, w, nullptr, y, nullptr, M, N, C, part, g, st);
+    case 2: return dispatch_conv<128, 256>(epi, x, w, nullptr, y, nullptr, M, N, C, part, g, st);
+    case 3: return dispatch_conv<128, 128>(epi, x, w, nullptr, y, nullptr, M, N, C, part, g, st);
+    case 4: return dispatch_conv<256, 64>(epi, x, w, nullptr, y, nullptr, M, N, C, part, g, st);
+    default: return dispatch_conv<128, 64>(epi, x, w, nullptr, y, nullptr, M, N, C, part, g, st);
+  }
 }
 
 // Grouped TN GEMM: for i < n, C_i[M_i, N_i] = A_i[T_i, M_i]^T B_i[T_i, N_i] (bf16 row-major operands, fp32
@@ -1003,7 +1033,7 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
     if (!(fl & CONV) && (long long)T[i] * N[i] >= (1ll << 31)) return -1;
     const Geo* geo = nullptr;
     if (fl & CONV) {  // geometry in device memory; N = 9 C with C % (tile width) == 0 (one tap per column block)
-      if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % 9 || (N[i] / 9) % tn) return -1;
+      if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % tn) return -1;  // (N = taps x C, host-side)
       geo = (const Geo*)geos[i];
     }
     const int S = (T[i] + chunk[i] - 1) / chunk[i];

@@ -30,6 +30,10 @@ from . import native_stats, weight_prep
 DGRAD = os.environ.get("MIFX_CONV1X1_DGRAD", "gemm8")
 
 
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    return t.permute(0, 2, 3, 1)
+
+
 def _rows(t: torch.Tensor) -> torch.Tensor:
     """[N, C, H, W] channels_last -> the [N H W, C] storage view."""
     n, c, h, w = t.shape
@@ -134,11 +138,15 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = No
 # stride-2 1x1 shortcuts whose input gradient measured faster on the phase-split hand-written kernel,
 # (input H, C, Cout) (profiles/resnet_conv_routes_r4.jsonl); others MIOpen
 _HIP_DGRAD_S2 = {(56, 256, 512), (28, 512, 1024), (14, 1024, 2048)}
+# the strided shortcut's forward and weight gradient on csrc/gemm8.hip (center-tap implicit GEMM, deferred grouped
+# dW); MIFX_SC_G8=0 leaves both on MIOpen (A/B)
+_SC_G8 = os.environ.get("MIFX_SC_G8", "1") != "0"
 
 
 class _ProjPair(torch.autograd.Function):
-    """A projection block's two consumers of the pre-activation: the strided 1x1 shortcut (MIOpen forward / weight
-    gradient, hand-written or MIOpen input gradient) and conv1 (the GEMM kernel with BN1's statistics in its
+    """A projection block's two consumers of the pre-activation: the strided 1x1 shortcut (forward: the center tap of
+    the implicit-GEMM kernel; weight gradient: deferred into the grouped TN flush -- MIOpen's with MIFX_SC_G8=0; input
+    gradient hand-written or MIOpen) and conv1 (the GEMM kernel with BN1's statistics in its
     epilogue), as ONE autograd node. Its backward computes the shortcut's input gradient first and hands it to conv1's
     input-gradient GEMM as the addend R2 (csrc/gemm8.hip EPI_ADD_BNBWD): the summed gradient of the pre-activation is
     written once -- no separate add of the two branches' gradients (autograd's, ~100 us each at B = 256) -- and, when
@@ -148,9 +156,17 @@ class _ProjPair(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_sc, w1, stride, bn):
         n, cin, h, w_ = x.shape
-        c1 = w1.shape[0]
-        wsb = w_sc.to(torch.bfloat16)
-        sc = torch.ops.aten.convolution(x, wsb, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1)
+        c1, cs = w1.shape[0], w_sc.shape[0]
+        oh, ow = (h - 1) // stride + 1, (w_ - 1) // stride + 1
+        cfg_sc = hg.gemm8_pick(n * oh * ow, cs, cin) if _SC_G8 and cin >= 64 and not cin & (cin - 1) else None
+        if cfg_sc is not None:  # the center tap of the implicit 3x3 GEMM: pixel (stride oh, stride ow)
+            im_sc = weight_prep.images(w_sc)
+            wsb = im_sc[0].view(cs, cin, 1, 1) if im_sc is not None else w_sc.to(torch.bfloat16)
+            sc = torch.empty(n, cs, oh, ow, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+            hg.gemm8_conv1x1_strided(_nhwc(x), wsb.view(cs, cin), stride, 0, cfg=cfg_sc, out=_rows(sc))
+        else:
+            wsb = w_sc.to(torch.bfloat16)
+            sc = torch.ops.aten.convolution(x, wsb, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1)
         im = weight_prep.images(w1)
         wb1 = im[0] if im is not None else w1.reshape(c1, cin).to(torch.bfloat16).contiguous()
         ctx.wt1 = im[1] if im is not None else None
@@ -177,13 +193,16 @@ class _ProjPair(torch.autograd.Function):
 
                 dx_sc = gconv.dgrad_strided(dscc, wsb.contiguous(), n, h, w_, 1, cin, cs, 1, 1, 0, stride)
             want_dx = ctx.needs_input_grad[0] and dx_sc is None
-            if want_dx or ctx.needs_input_grad[1]:
+            want_dw = ctx.needs_input_grad[1]
+            if want_dw and _SC_G8:
+                dwsc = hg.defer_strided1x1_weight_grad_f32(_rows(dscc), _nhwc(x), ctx.w_sc, stride)
+                want_dw = dwsc is None
+            if want_dx or want_dw:
                 gx, gw, _ = torch.ops.aten.convolution_backward(dscc, x, wsb, None, [stride, stride], [0, 0], [1, 1],
-                                                                False, [0, 0], 1,
-                                                                [want_dx, ctx.needs_input_grad[1], False])
+                                                                False, [0, 0], 1, [want_dx, want_dw, False])
                 if want_dx:
                     dx_sc = gx
-                if ctx.needs_input_grad[1]:
+                if want_dw:
                     dwsc = gw.to(ctx.w_sc.dtype)
         if dy1 is not None:
             dy1c = dy1.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)

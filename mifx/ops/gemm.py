@@ -310,6 +310,26 @@ def defer_conv3x3_weight_grad_f32(dy2: torch.Tensor, x: torch.Tensor, w: torch.T
     return ph
 
 
+def defer_strided1x1_weight_grad_f32(dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int):
+    """As defer_conv3x3_weight_grad_f32 for a strided 1x1 convolution (ResNet's projection shortcuts): dy2 [Nb OH OW,
+    Cout] bf16, x NHWC bf16 [Nb, H, W, C], w fp32 [Cout, C, 1, 1]; the flush gathers x's pixel (stride oh, stride ow)
+    per output row (the center-tap geometry). C and Cout % 256 (full tiles); None otherwise / when not deferring."""
+    if not (_DEFER["on"] and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and w.dtype == torch.float32 and w.is_contiguous() and os.environ.get("MIFX_DEFER_DW", "1") != "0"):
+        return None
+    nb, h, w_, c = x.shape
+    cout = w.shape[0]
+    if cout % 256 or c % 256 or c & (c - 1) or dy2.shape[0] % 64:
+        return None
+    geo = conv_geo(nb, h, w_, c, stride, 1, x.device, center1x1=True)
+    native_stats.count("conv1x1_dW", True)
+    overwrite = w.grad is None
+    ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
+    _DEFER["pending_f32"].append((dy2.contiguous(), x.contiguous(), w, ph.data_ptr() if overwrite else None, geo,
+                                  _WGRAD_CHUNK))
+    return ph
+
+
 def flush_weight_grads() -> int:
     """Run every recorded weight gradient as one grouped launch into the weights' .grad; returns how many."""
     pf, _DEFER["pending_f32"] = _DEFER.get("pending_f32", []), []
@@ -321,15 +341,15 @@ def flush_weight_grads() -> int:
             geo = rec[4] if len(rec) > 4 else None
             ck = rec[5] if len(rec) > 5 else _WGRAD_CHUNK
             g = w.grad
-            lay_ok = g is not None and (g.is_contiguous(memory_format=torch.channels_last) if geo is not None
-                                        else g.is_contiguous())
+            lay_ok = g is not None and (g.is_contiguous(memory_format=torch.channels_last)
+                                        if geo is not None and geo.mifx_taps == 9 else g.is_contiguous())
             if g is None or g.dtype != torch.float32 or not lay_ok or g.shape != w.shape:
                 raise RuntimeError("deferred weight gradients: the fp32 weight's .grad is missing or not contiguous")
             if ph is not None and g.data_ptr() != ph:
                 raise RuntimeError("deferred weight gradients: autograd did not keep the uninitialised placeholder "
                                    "as .grad (was the gradient accumulated?)")
-            if geo is not None:  # [Cout][3][3][C] storage of the channels_last gradient
-                flat = g.permute(0, 2, 3, 1).reshape(g.shape[0], -1)
+            if geo is not None:  # [Cout][3][3][C] storage of the channels_last gradient ([Cout][C]: strided 1x1)
+                flat = g.permute(0, 2, 3, 1).reshape(g.shape[0], -1) if geo.mifx_taps == 9 else g.view(g.shape[0], -1)
                 probs.append((dy, x, flat, geo, ck))
             else:
                 probs.append((dy, x, g.view(dy.shape[1], x.shape[1])))
@@ -655,7 +675,8 @@ def _g8_fns():
             "conv": sig(lib, "mifx_gemm8_conv3x3", [I32, I32, VP, VP, VP, VP, VP, VP, I32, I32, I32, I32, I32, I32,
                                                     I32, VP]),
             "geo_bytes": sig(lib, "mifx_gemm8_geo_bytes", []),
-            "geo": sig(lib, "mifx_gemm8_geo", [I32, I32, I32, I32, I32, I32, VP])}
+            "geo": sig(lib, "mifx_gemm8_geo", [I32, I32, I32, I32, I32, I32, I32, VP]),
+            "conv1x1s": sig(lib, "mifx_gemm8_conv1x1s", [I32, I32, VP, VP, VP, VP, I32, I32, I32, I32, I32, I32, VP])}
 
 
 @functools.lru_cache(maxsize=None)
@@ -714,14 +735,15 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
         a, b, c = pr[:3]
         geo = pr[3] if len(pr) > 3 else None
         pchunk = pr[4] if len(pr) > 4 else chunk
+        taps = getattr(geo, "mifx_taps", 9)
         if geo is not None:
             T, M = a.shape
             N = c.numel() // M
             if not (a.is_contiguous() and b.is_contiguous() and a.dtype == torch.bfloat16
                     and b.dtype == torch.bfloat16 and c.dtype == torch.float32 and N * M == c.numel()
-                    and N % 9 == 0 and b.shape[-1] == N // 9):
+                    and N % taps == 0 and b.shape[-1] == N // taps):
                 raise ValueError("gemm8_tn_grouped: a conv problem needs bf16 dy [T, Cout], NHWC bf16 x [.., C] and "
-                                 "fp32 c [Cout, 9 C]")
+                                 "fp32 c [Cout, taps C]")
         else:
             if not (a.is_contiguous() and b.is_contiguous() and c.is_contiguous()) or a.shape[0] != b.shape[0] or \
                     c.numel() != a.shape[1] * b.shape[1] or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 \
@@ -731,9 +753,9 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
             T, M = a.shape
             N = b.shape[1]
         f32 = c.dtype == torch.float32
-        t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // 9) % 256))
+        t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // taps) % 256))
         # a 64-wide dimension (ResNet-50 stage 1): the narrow 256 x 64 / 64 x 256 tiles (fp32 problems)
-        cw = N // 9 if geo is not None else N
+        cw = N // taps if geo is not None else N
         nar_n = _G8_NARROW and f32 and tile128 is None and cw % 128 and cw % 64 == 0 and M % 256 == 0
         nar_m = _G8_NARROW and f32 and tile128 is None and geo is None and M % 128 and M % 64 == 0 \
             and N % 256 == 0
@@ -764,19 +786,45 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
 _GEO: dict = {}
 
 
-def conv_geo(nb: int, h: int, w: int, c: int, stride: int, pad: int, device) -> torch.Tensor:
-    """The device-resident geometry record of a 3x3 convolution for the grouped weight-gradient launch (created once
-    per shape, before any graph capture reads it)."""
-    key = (nb, h, w, c, stride, pad, str(device))
+def conv_geo(nb: int, h: int, w: int, c: int, stride: int, pad: int, device, center1x1: bool = False) -> torch.Tensor:
+    """The device-resident geometry record of a 3x3 convolution -- or, center1x1, of a strided 1x1 one (the center
+    tap of a pad-1 3x3: weight gradient [Cout, C]) -- for the grouped weight-gradient launch (created once per shape,
+    before any graph capture reads it; `.mifx_taps` = taps per weight row)."""
+    key = (nb, h, w, c, stride, pad, bool(center1x1), str(device))
     g = _GEO.get(key)
     if g is None:
         nbytes = _g8_fns()["geo_bytes"]()
         host = (ctypes.c_ubyte * nbytes)()
-        if _g8_fns()["geo"](nb, h, w, c, stride, pad, host) != 0:
-            raise ValueError(f"no 3x3 convolution geometry for {key}")
+        if _g8_fns()["geo"](nb, h, w, c, stride, pad, int(bool(center1x1)), host) != 0:
+            raise ValueError(f"no convolution geometry for {key}")
         g = torch.tensor(list(bytes(host)), dtype=torch.uint8).to(device)
+        g.mifx_taps = 1 if center1x1 else 9
         _GEO[key] = g
     return g
+
+
+def gemm8_conv1x1_strided(x: torch.Tensor, w: torch.Tensor, stride: int = 2, epi: int = 0, cfg: int | None = None,
+                          out: torch.Tensor | None = None):
+    """Strided 1x1 convolution of NHWC bf16 x [Nb, H, W, C] (C a power of two >= 64) with w [Cout, C] bf16 on
+    csrc/gemm8.hip (the center tap of the implicit 3x3 GEMM) -> (y [Nb OH OW, Cout] bf16, part); epi 5: part = per-tile
+    BatchNorm statistics of y."""
+    nb, h, w_, c = x.shape
+    cout = w.shape[0]
+    oh, ow = (h - 1) // stride + 1, (w_ - 1) // stride + 1
+    M = nb * oh * ow
+    if cfg is None:
+        cfg = gemm8_pick(M, cout, c)
+    if cfg is None:
+        raise ValueError(f"no gemm8 tile configuration for the {M}x{cout}x{c} strided convolution")
+    if not (x.is_contiguous() and w.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and tuple(w.shape) == (cout, c)):
+        raise ValueError("gemm8_conv1x1_strided: contiguous bf16 NHWC input and [Cout, C] weight")
+    bm = gemm8_configs()[cfg][0]
+    y = out if out is not None else torch.empty(M, cout, device=x.device, dtype=torch.bfloat16)
+    part = torch.empty(2, M // bm, cout, device=x.device, dtype=torch.float32) if epi == 5 else None
+    check(_g8_fns()["conv1x1s"](int(cfg), int(epi), ptr(x), ptr(w), ptr(y), ptr(part), nb, h, w_, c, cout, stride,
+                                stream_handle(x.device)), "mifx_gemm8_conv1x1s")
+    return y, part
 
 
 def gemm8_conv3x3(x: torch.Tensor, w9: torch.Tensor, stride: int = 1, pad: int = 1, epi: int = 0,

@@ -75,8 +75,7 @@ class ResNetTrainer:
             from ..ops.weight_prep import WeightPrep
 
             ws = [m.weight for m in self.model.modules() if isinstance(m, torch.nn.Conv2d) and m.groups == 1
-                  and ((m.kernel_size == (1, 1) and m.stride == (1, 1))
-                       or (m.kernel_size == (3, 3) and m.in_channels >= 128))
+                  and (m.kernel_size == (1, 1) or (m.kernel_size == (3, 3) and m.in_channels >= 64))
                   and WeightPrep.supported(m.weight)]
             self.prep = WeightPrep(ws) if ws else None
         self.base_lr, self.warmup = lr, warmup_steps

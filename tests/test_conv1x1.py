@@ -250,3 +250,46 @@ def test_proj_pair_matches_separate_convs(couple):
     for got, want in ((x.grad.float(), xr.grad), (bn.weight.grad, wr.grad), (bn.bias.grad, br.grad),
                       (a.grad, ar.grad), (b.grad, b1r.grad)):
         torch.testing.assert_close(got, want, rtol=5e-2, atol=5e-2 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("nb,h,cin,cout", [(4, 16, 256, 512), (2, 15, 128, 256), (8, 14, 512, 1024)])
+def test_strided_1x1_center_tap(nb, h, cin, cout):
+    """Strided 1x1 convolution as the center tap of the implicit 3x3 GEMM (csrc/gemm8.hip, tap0 = 4): output and
+    per-tile BatchNorm statistics against an fp32 conv2d(stride 2), odd input sizes included."""
+    from mifx.ops import gemm as hg
+
+    torch.manual_seed(5)
+    x = torch.randn(nb, h, h, cin, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(cout, cin, device="cuda") * cin ** -0.5).to(torch.bfloat16)
+    y, part = hg.gemm8_conv1x1_strided(x, w, 2, epi=5)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.float()[:, :, None, None], stride=2)
+    ref2 = ref.permute(0, 2, 3, 1).reshape(-1, cout)
+    torch.testing.assert_close(y.float(), ref2, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(part[0].double().mean(0), y.float().double().mean(0), rtol=1e-5, atol=1e-5)
+
+
+def test_proj_pair_deferred_shortcut_weight_grad():
+    """Inside deferred_weight_grads(): the shortcut's weight gradient is recorded with the center-tap geometry and
+    computed by the grouped TN flush -- equal to the fp32 reference (and the node's other gradients unchanged)."""
+    from mifx.ops import gemm as hg
+    from mifx.ops.conv1x1 import proj_pair
+
+    torch.manual_seed(6)
+    x = _x(4, 256, 16, 16, 31).requires_grad_()
+    wsc = (torch.randn(512, 256, 1, 1, device="cuda") * 256 ** -0.5).requires_grad_()
+    w1 = (torch.randn(256, 256, 1, 1, device="cuda") * 256 ** -0.5).requires_grad_()
+    gsc, g1 = _x(4, 512, 8, 8, 32), _x(4, 256, 16, 16, 33)
+    before = len(hg._DEFER["pending_f32"])
+    with hg.deferred_weight_grads():
+        sc, y1, _ = proj_pair(x, wsc, 2, w1)
+        (sc.float() * gsc.float()).sum().add((y1.float() * g1.float()).sum()).backward()
+        assert len(hg._DEFER["pending_f32"]) - before == 2  # the shortcut's and conv1's
+    assert hg.flush_weight_grads() >= 2
+    xr = x.detach().float().requires_grad_()
+    ar, br = wsc.detach().clone().requires_grad_(), w1.detach().clone().requires_grad_()
+    scr = F.conv2d(xr, ar.to(torch.bfloat16).float(), stride=2)
+    y1r = F.conv2d(xr, br.to(torch.bfloat16).float())
+    (scr * gsc.float()).sum().add((y1r * g1.float()).sum()).backward()
+    torch.testing.assert_close(sc.float(), scr, rtol=3e-2, atol=3e-2)
+    for got, want in ((wsc.grad, ar.grad), (w1.grad, br.grad), (x.grad.float(), xr.grad)):
+        torch.testing.assert_close(got, want, rtol=3e-2, atol=3e-2 * want.abs().max().item())
