@@ -252,7 +252,7 @@ def test_proj_pair_matches_separate_convs(couple):
         torch.testing.assert_close(got, want, rtol=5e-2, atol=5e-2 * want.abs().max().item())
 
 
-@pytest.mark.parametrize("nb,h,cin,cout", [(4, 16, 256, 512), (2, 15, 128, 256), (8, 14, 512, 1024)])
+@pytest.mark.parametrize("nb,h,cin,cout", [(4, 16, 256, 512), (2, 15, 128, 256), (8, 16, 512, 1024)])
 def test_strided_1x1_center_tap(nb, h, cin, cout):
     """Strided 1x1 convolution as the center tap of the implicit 3x3 GEMM (csrc/gemm8.hip, tap0 = 4): output and
     per-tile BatchNorm statistics against an fp32 conv2d(stride 2), odd input sizes included."""
