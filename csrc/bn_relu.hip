@@ -367,7 +367,25 @@ __global__ __launch_bounds__(kThreads) void bn_apply(const T* __restrict__ x, co
   float sc[kVec], sh[kVec];
   ld8f(scale + c0, sc);
   ld8f(shift + c0, sh);
-  for (int r = r0 + slice; r < r1; r += rpb) {
+  int r = r0 + slice;
+  if (x2 == nullptr) {  // four rows' 16-byte loads in flight per thread before any store (the pass is latency-bound
+                        // at one load per thread: ~5 TB/s)
+    for (; r + 3 * rpb < r1; r += 4 * rpb) {
+      float u[4][kVec];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ldv(x + (size_t)(r + k * rpb) * C + c0, u[k]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          const float t = fmaf(u[k][e], sc[e], sh[e]);
+          u[k][e] = relu ? fmaxf(t, 0.f) : t;
+        }
+        stv(y + (size_t)(r + k * rpb) * C + c0, u[k]);
+      }
+    }
+  }
+  for (; r < r1; r += rpb) {
     float u[kVec];
     load_sum(x, x2, s_out, (size_t)r * C + c0, u);
 #pragma unroll
@@ -486,7 +504,27 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ d
   ld8f(k + c0, A);
   ld8f(k + C + c0, B);
   ld8f(k + 2 * C + c0, Cc);
-  for (int r = r0 + slice; r < r1; r += rpb) {
+  int r = r0 + slice;
+  for (; r + 3 * rpb < r1; r += 4 * rpb) {  // four rows in flight (8-12 16-byte loads per thread)
+    float d[4][kVec], u[4][kVec], rr[4][kVec];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ldv(dy + (size_t)(r + k * rpb) * C + c0, d[k]);
+      ldv(x + (size_t)(r + k * rpb) * C + c0, u[k]);
+      if (dres != nullptr) ldv(dres + (size_t)(r + k * rpb) * C + c0, rr[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        const float g = (relu && fmaf(u[k][e], sc[e], sh[e]) <= 0.f) ? 0.f : d[k][e];
+        d[k][e] = fmaf(A[e], g, fmaf(B[e], u[k][e], Cc[e]));
+        if (dres != nullptr) d[k][e] += rr[k][e];
+      }
+      stv(dx + (size_t)(r + k * rpb) * C + c0, d[k]);
+    }
+  }
+  for (; r < r1; r += rpb) {
     float d[kVec], u[kVec];
     ldv(dy + (size_t)r * C + c0, d);
     ldv(x + (size_t)r * C + c0, u);
@@ -523,9 +561,17 @@ int blocks_for(long long M, int C) {
   return nb < 1 ? 1 : (int)nb;
 }
 
+int apply_rows() {  // rows per thread of the apply passes (MIFX_BN_APPLY_ROWS, default 8: A/B)
+  static const int v = [] {
+    const char* e = getenv("MIFX_BN_APPLY_ROWS");
+    const int r = e ? atoi(e) : 8;
+    return r < 1 ? 1 : (r > 64 ? 64 : r);
+  }();
+  return v;
+}
 int apply_blocks(long long M, int C) {  // ~8 rows per thread, params loaded once per thread
-  const int rpb = kThreads / (C / kVec);
-  long long g = (M + (long long)rpb * 8 - 1) / ((long long)rpb * 8);
+  const int rpb = kThreads / (C / kVec), rpt = apply_rows();
+  long long g = (M + (long long)rpb * rpt - 1) / ((long long)rpb * rpt);
   if (g > 16384) g = 16384;
   return g < 1 ? 1 : (int)g;
 }
@@ -569,7 +615,7 @@ int mifx_bn_relu_fwd(int dtype, const void* x, const void* x2, void* sum_out, lo
 
 // Training forward from per-tile statistics (see bn_tiles_partial): part = [2][T][C] (tile means, tile M2), nt rows
 // per tile, x [M = T nt, C]; ws = fp64 scratch of mifx_bn_tiles_ws(T, C) doubles; writes stats = [mean, rstd, scale,
-// shift] and y = relu(x * scale + shift).
+// shift] and y = relu(x * scale + shift) (y null: the statistics only).
 int mifx_bn_tiles_ws(int T, int C) { return tile_groups(T) * C * 3; }
 
 int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const float* part, int T, int nt,
@@ -581,6 +627,7 @@ int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const f
                      ws);
   hipLaunchKernelGGL(bn_tiles_final, dim3((C + 255) / 256), dim3(256), 0, st, ws, G, C, w, b, eps, momentum, run_mean,
                      run_var, stats, stats + C, stats + 2 * C, stats + 3 * C);
+  if (y == nullptr) return (int)hipGetLastError();  // statistics only: the consumer GEMM applies (gemm8 AX operands)
   if (dtype)
     hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
                        (const __hip_bfloat16*)x, (const __hip_bfloat16*)nullptr, (__hip_bfloat16*)nullptr, M, C,

@@ -131,12 +131,15 @@ constexpr int NARROW_N = 16, NARROW_M = 32;
 // CONV: B is a 3x3 convolution's input gathered per output pixel (CV 2, geometry in device memory at `geo`); the
 // problem is dW[M = Cout][N = 9 C] = dY^T . X_taps, F32 only
 constexpr int CONV = 8;
+// BNX: B is a BatchNorm + ReLU INPUT; the operand is relu(B scale + shift), applied per column as B's fragments leave
+// LDS (aux = fp32 [scale[N], shift[N]]): the weight gradient of a convolution whose input activation is never stored
+constexpr int BNX = 64;
 struct Prob {
   const bf16* A;
   const bf16* B;
   void* C;
   float* P;
-  const Geo* geo;
+  const void* aux;  // CONV: the Geo; BNX: scale / shift
   int M, N, T, chunk, S, flags;
 };
 struct Group {
@@ -154,13 +157,20 @@ constexpr int vm_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4
 // The body: one BM x BN tile of Y = X W^T (NT: X [M, K], W [N, K] row-major) or of C = A^T B (TN: A [K, M],
 // B [K, N] row-major; X := A, W := B, "K" = tokens), m0 / n0 its origin. CV: implicit-convolution operand (above);
 // tok0: the first token of this item's chunk (CV 2: B is then the whole conv input, gathered by pixel index).
-template <int BM, int BN, int EPI, typename P, bool TN, int CV = 0>
+// AX: the BatchNorm + ReLU transform relu(v scale[c] + shift[c]) of the input channel c, applied to the fragments as
+// they leave LDS (ax = fp32 [scale, shift], each K (NT: the X operand's channels, staged in LDS after the two K-tile
+// buffers) or N (TN: the B operand's columns, in registers) long). The consumer convolution of a BatchNorm + ReLU thus
+// reads the BatchNorm's INPUT and the activation is never written (bit-identical to the stored-activation path: same
+// fused multiply-add and rounding as csrc/bn_relu.hip bn_apply).
+template <int BM, int BN, int EPI, typename P, bool TN, int CV = 0, bool AX = false>
 __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                            const P* __restrict__ bias, bf16* __restrict__ Y, bf16* __restrict__ Z,
                                            int M, int N, int K, float* __restrict__ part, int m0, int n0,
                                            unsigned char* lds, const Geo& geo = Geo{}, int tok0 = 0,
-                                           const bf16* __restrict__ R2 = nullptr) {
+                                           const bf16* __restrict__ R2 = nullptr,
+                                           const float* __restrict__ ax = nullptr) {
   static_assert(CV == 0 || (CV == 1 && !TN) || (CV == 2 && TN), "conv gather: NT rows (1) or TN B rows (2)");
+  static_assert(!AX || CV == 0, "the BatchNorm operand transform: plain (1x1) operands only (no zero-page rows)");
   constexpr int HA = BM / 2, HB = BN / 2;            // rows (NT) / columns (TN) per half-tile
   constexpr int ABYTES = HA * 128, BBYTES = HB * 128;  // NT: 64 bf16 per row; TN: 64 token rows of HA bf16
   // NARROW (NT, BN = 64: the 64-channel convolutions of ResNet-50's first stage): the 8 waves tile a quadrant 4 x 2
@@ -305,6 +315,33 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     }
   };
 
+  // AX operands, loaded before the prologue's DMAs (older than them: retired by its counted wait). NT: the [scale,
+  // shift] table of all K channels (<= 2048) -> LDS after the two K-tile buffers; TN: this lane's B columns, per
+  // (B half, fragment)
+  constexpr int AXV = AX && !TN ? 2 : 1;
+  float4 axv[AXV];
+  float axs[AX && TN ? 2 : 1][AX && TN ? NF : 1], axh[AX && TN ? 2 : 1][AX && TN ? NF : 1];
+  if constexpr (AX && !TN) {
+#pragma unroll
+    for (int i = 0; i < AXV; ++i) {
+      const int q = (i * NT + tid) * 4;
+      axv[i] = q < 2 * K ? *(const float4*)(ax + q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if constexpr (AX && TN) {
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int c = n0 + hb * HB + wn * CPW + 16 * f + (lane & 15);
+        axs[hb][f] = ax[c];
+        axh[hb][f] = ax[N + c];
+      }
+  }
+  (void)axv;
+  (void)axs;
+  (void)axh;
+
   v4f acc[2][2][NF][MF];  // [mq][nq][n-frag][m-frag]
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -329,7 +366,11 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     s2 = s2 >= cpr_rot ? s2 - cpr_rot : s2;
     return tr_frag(half + (t1 * cpr_rot + s1) * 16 + 8 * (tp & 1), half + (t2 * cpr_rot + s2) * 16 + 8 * (tp & 1));
   };
-  auto read_a = [&](const unsigned char* half, v8bf (&r)[MF][2]) {
+  auto bnrelu = [](v8bf& v, const float* sc, const float* sh) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf(fmaf((float)v[e], sc[e], sh[e]), 0.f);
+  };
+  auto read_a = [&](const unsigned char* half, v8bf (&r)[MF][2], int k0) {
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
       const int row = wm * RPW + 16 * f + fr;
@@ -341,8 +382,26 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
           r[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
       }
     }
+    if constexpr (AX && !TN) {  // channels k0 + 32 ks + 8 fc + e of every row: one scale / shift octet per k-step
+      const float* tab = (const float*)(lds + 2 * BUF);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // four channels at a time (register pressure of the 256 x 256 tile)
+          const int c = k0 + 32 * ks + 8 * fc + 4 * q;
+          const float4 sc = *(const float4*)(tab + c), sh = *(const float4*)(tab + K + c);
+#pragma unroll
+          for (int f = 0; f < MF; ++f) {
+            v8bf& v = r[f][ks];
+            v[4 * q + 0] = (bf16)fmaxf(fmaf((float)v[4 * q + 0], sc.x, sh.x), 0.f);
+            v[4 * q + 1] = (bf16)fmaxf(fmaf((float)v[4 * q + 1], sc.y, sh.y), 0.f);
+            v[4 * q + 2] = (bf16)fmaxf(fmaf((float)v[4 * q + 2], sc.z, sh.z), 0.f);
+            v[4 * q + 3] = (bf16)fmaxf(fmaf((float)v[4 * q + 3], sc.w, sh.w), 0.f);
+          }
+        }
+    }
   };
-  auto read_b = [&](const unsigned char* half) {
+  auto read_b = [&](const unsigned char* half, int hb) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       const int row = wn * CPW + 16 * f + fr;
@@ -352,6 +411,15 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
           rb[f][ks] = tn_frag(half, CPB, wn * CPW + 16 * f, ks);
         else
           rb[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
+        if constexpr (AX && TN) {  // one column (channel) per lane and fragment
+          float sc[8], sh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sc[e] = axs[hb][f];
+            sh[e] = axh[hb][f];
+          }
+          bnrelu(rb[f][ks], sc, sh);
+        }
       }
     }
   };
@@ -371,6 +439,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     __builtin_amdgcn_sched_barrier(0);
   };
 
+
   // prologue: K-tile 0 whole, K-tile 1 halves A0 / B0; retire K-tile 0's A0 / B0 (phase 0 reads them)
   stage(0, 0);
   stage(1, 0);
@@ -383,6 +452,13 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if constexpr (AX && !TN) {
+#pragma unroll
+    for (int i = 0; i < AXV; ++i) {
+      const int q = (i * NT + tid) * 4;
+      if (q < 2 * K) *(float4*)(lds + 2 * BUF + 4 * q) = axv[i];
+    }
+  }
   barrier();
   if (grp == 1) barrier();  // the stagger: waves 4-7 one barrier behind
 
@@ -393,12 +469,12 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       constexpr int j = decltype(J)::value;
       // LDS fragment reads of this phase's quadrant
       if constexpr (j == 0) {
-        read_a(buf + OFF_A0, ra0);
-        read_b(buf + OFF_B0);
+        read_a(buf + OFF_A0, ra0, t * BK);
+        read_b(buf + OFF_B0, 0);
       } else if constexpr (j == 1) {
-        read_a(buf + OFF_A1, ra1);
+        read_a(buf + OFF_A1, ra1, t * BK);
       } else if constexpr (j == 2) {
-        read_b(buf + OFF_B1);
+        read_b(buf + OFF_B1, 1);
       }
       // one half-tile of DMA into the slot freed two phases ago
       const bool issue = j < 2 ? st1 : st2;
@@ -685,6 +761,19 @@ __global__ __launch_bounds__(NT, 1) void gemm8_nt(const bf16* __restrict__ X, co
                                     Geo{}, 0, R2);
 }
 
+// Y = relu(X scale + shift) . W^T: the consumer 1x1 convolution of a BatchNorm + ReLU over the BatchNorm's input X
+// (ax = [scale[K], shift[K]] fp32, K <= 2048)
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm8_nt_bnx(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                      const bf16* __restrict__ bias, bf16* __restrict__ Y, int M,
+                                                      int N, int K, float* __restrict__ part,
+                                                      const float* __restrict__ ax) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tile = xcd_tile(), nb_n = N / BN;
+  gemm8_tile<BM, BN, EPI, bf16, false, 0, true>(X, W, bias, Y, nullptr, M, N, K, part, (tile / nb_n) * BM,
+                                                (tile % nb_n) * BN, lds, Geo{}, 0, nullptr, ax);
+}
+
 // implicit-GEMM 3x3 convolution (CV 1): Y[Nb OH OW, N] = gathered X . W[N, 9 C]^T, epilogues as gemm8_nt
 template <int BM, int BN, int EPI, typename P>
 __global__ __launch_bounds__(NT, 1) void gemm8_conv(const bf16* __restrict__ X, const bf16* __restrict__ W,
@@ -712,7 +801,7 @@ __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, 
   const int t0 = sp * p.chunk, len = min(p.chunk, p.T - t0);
   const bf16* A = p.A + (size_t)t0 * p.M;
   if (p.flags & CONV) {  // (F32 only; the B rows are gathered from the whole input by pixel index t0 + ...)
-    const Geo geo = *p.geo;
+    const Geo geo = *(const Geo*)p.aux;
     float* P = p.P + (size_t)sp * p.M * p.N;
     if (p.flags & NARROW_N)
       gemm8_tile<BM, 64, EPI_F32, bf16, true, 2>(A, p.B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
@@ -726,6 +815,23 @@ __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, 
     return;
   }
   const bf16* B = p.B + (size_t)t0 * p.N;
+  if (p.flags & BNX) {  // (F32 only: a convolution weight gradient over a BatchNorm + ReLU input)
+    float* P = p.P + (size_t)sp * p.M * p.N;
+    const float* bx = (const float*)p.aux;
+    if (p.flags & NARROW_N)
+      gemm8_tile<BM, 64, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
+                                                       Geo{}, 0, nullptr, bx);
+    else if (p.flags & NARROW_M)
+      gemm8_tile<64, BN, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
+                                                       Geo{}, 0, nullptr, bx);
+    else if (p.flags & TILE128)
+      gemm8_tile<BM / 2, BN / 2, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0,
+                                                               n0, lds, Geo{}, 0, nullptr, bx);
+    else
+      gemm8_tile<BM, BN, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
+                                                       Geo{}, 0, nullptr, bx);
+    return;
+  }
   if (p.flags & F32) {
     float* P = p.P + (size_t)sp * p.M * p.N;
     if (p.flags & NARROW_N)
@@ -812,6 +918,34 @@ int launch(const void* X, const void* W, const void* bias, void* Y, void* Z, int
   hipLaunchKernelGGL((gemm8_nt<BM, BN, EPI, P>), dim3((M / BM) * (N / BN)), dim3(NT), LDS, st, (const bf16*)X,
                      (const bf16*)W, (const P*)bias, (bf16*)Y, (bf16*)Z, M, N, K, part, (const bf16*)R2);
   return (int)hipGetLastError();
+}
+
+constexpr int BNX_MAXK = 2048;
+template <int BM, int BN, int EPI>
+int launch_bnx(const void* X, const void* W, const void* bias, void* Y, int M, int N, int K, float* part,
+               const float* ax, hipStream_t st) {
+  constexpr int LOOP = 2 * 2 * (BM / 2 + BN / 2) * 128, BASE = lds_bytes<BM, BN, EPI>();
+  constexpr int MAXL = (LOOP + 8 * BNX_MAXK > BASE ? LOOP + 8 * BNX_MAXK : BASE);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8_nt_bnx<BM, BN, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              MAXL);
+    attr = true;
+  }
+  const int lds = LOOP + 8 * K > BASE ? LOOP + 8 * K : BASE;
+  hipLaunchKernelGGL((gemm8_nt_bnx<BM, BN, EPI>), dim3((M / BM) * (N / BN)), dim3(NT), lds, st, (const bf16*)X,
+                     (const bf16*)W, (const bf16*)bias, (bf16*)Y, M, N, K, part, ax);
+  return (int)hipGetLastError();
+}
+template <int BM, int BN>
+int dispatch_bnx(int epi, const void* X, const void* W, const void* bias, void* Y, int M, int N, int K, float* part,
+                 const float* ax, hipStream_t st) {
+  switch (epi) {
+    case EPI_NONE: return launch_bnx<BM, BN, EPI_NONE>(X, W, nullptr, Y, M, N, K, nullptr, ax, st);
+    case EPI_STATS: return launch_bnx<BM, BN, EPI_STATS>(X, W, nullptr, Y, M, N, K, part, ax, st);
+    case EPI_ADD_STATS: return launch_bnx<BM, BN, EPI_ADD_STATS>(X, W, bias, Y, M, N, K, part, ax, st);
+  }
+  return -1;
 }
 
 template <int BM, int BN, int EPI>
@@ -938,6 +1072,32 @@ int mifx_gemm8_nt(int cfg, int epi, int bias_f32, const void* X, const void* W, 
   }
 }
 
+// Y[M, N] = relu(X scale + shift) . W[N, K]^T (+ R: epi 6) with ax = fp32 [scale[K], shift[K]] (a BatchNorm's
+// finalized statistics): the 1x1 convolution consuming a BatchNorm + ReLU, reading the BatchNorm's input X. epi 0, 5
+// (statistics of Y), 6 (bias = R bf16 [M, N], statistics of the stored sum). K <= 2048; otherwise as mifx_gemm8_nt.
+int mifx_gemm8_nt_bnx(int cfg, int epi, const void* X, const void* W, const void* bias, void* Y, float* part, int M,
+                      int N, int K, const float* ax, hipStream_t st) {
+  const int m = (int)(sizeof(kCfgs) / sizeof(Cfg));
+  if (cfg < 0 || cfg >= m || M <= 0 || N <= 0 || K <= 0 || K > BNX_MAXK || X == nullptr || W == nullptr ||
+      Y == nullptr || ax == nullptr)
+    return -1;
+  const Cfg c = kCfgs[cfg];
+  if (M % c.bm || N % c.bn || K % BK) return -1;
+  if (epi != 0 && epi != 5 && epi != 6) return -1;
+  if (epi != 0 && part == nullptr) return -1;
+  if (epi == 6 && (bias == nullptr || (uintptr_t)bias % 16)) return -1;
+  if ((uintptr_t)X % 16 || (uintptr_t)W % 16 || (uintptr_t)Y % 16 || (uintptr_t)ax % 16) return -1;
+  if ((long long)M * K >= (1ll << 31) || (long long)N * K >= (1ll << 31)) return -1;
+  switch (cfg) {
+    case 0: return dispatch_bnx<256, 256>(epi, X, W, bias, Y, M, N, K, part, ax, st);
+    case 1: return dispatch_bnx<256, 128>(epi, X, W, bias, Y, M, N, K, part, ax, st);
+    case 2: return dispatch_bnx<128, 256>(epi, X, W, bias, Y, M, N, K, part, ax, st);
+    case 3: return dispatch_bnx<128, 128>(epi, X, W, bias, Y, M, N, K, part, ax, st);
+    case 4: return dispatch_bnx<256, 64>(epi, X, W, bias, Y, M, N, K, part, ax, st);
+    default: return dispatch_bnx<128, 64>(epi, X, W, bias, Y, M, N, K, part, ax, st);
+  }
+}
+
 // 3x3 convolution as an implicit GEMM (see Geo): x bf16 NHWC [Nb][H][W][C], w bf16 [N][3][3][C] (channels_last
 // weight), y bf16 [Nb OH OW][N]; epi 0 none, 5 per-tile BatchNorm statistics of y (as mifx_gemm8_nt), 8 y is a
 // BatchNorm + ReLU output gradient (bias = that BatchNorm's input [Nb OH OW][N], Z = its statistics) with the per-tile
@@ -1008,7 +1168,8 @@ int mifx_gemm8_conv1x1s(int cfg, int epi, const void* x, const void* w, void* y,
 // else =), computed in
 // token chunks of chunk_i rows (fp32 partials in ws, summed in order by a second launch); bit 1 TILE128 -- 128 x 128
 // tiles (M_i, N_i % 128) instead of 256 x 256 (% 256). bf16 problems need chunk_i = T_i. T_i % 64 == 0, chunk_i % 64
-// == 0, 16-byte aligned operands, n <= 64. ws: fp32 workspace of sum over F32 problems of S_i M_i N_i floats
+// == 0, 16-byte aligned operands, n <= 64. Bit 3 CONV: B is a convolution input gathered by geos[i] (a Geo); bit 6
+// BNX: the B operand is relu(B scale + shift) per column, geos[i] = fp32 [scale[N], shift[N]]. ws: fp32 workspace of sum over F32 problems of S_i M_i N_i floats
 // (S_i = ceil(T_i / chunk_i)), may be null without F32 problems. Returns the number of work items (> 0) or < 0.
 int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, void* const* C, const int* M,
                           const int* N, const int* T, const int* chunk, const int* flags, float* ws,
@@ -1031,10 +1192,14 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
     if ((uintptr_t)A[i] % 16 || (uintptr_t)B[i] % 16 || (uintptr_t)C[i] % 16) return -1;
     if ((long long)T[i] * M[i] >= (1ll << 31)) return -1;
     if (!(fl & CONV) && (long long)T[i] * N[i] >= (1ll << 31)) return -1;
-    const Geo* geo = nullptr;
+    const void* aux = nullptr;
     if (fl & CONV) {  // geometry in device memory; N = 9 C with C % (tile width) == 0 (one tap per column block)
       if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % tn) return -1;  // (N = taps x C, host-side)
-      geo = (const Geo*)geos[i];
+      aux = geos[i];
+    }
+    if (fl & BNX) {  // aux[i]: the BatchNorm's fp32 [scale[N], shift[N]]
+      if (!(fl & F32) || (fl & CONV) || geos == nullptr || geos[i] == nullptr || (uintptr_t)geos[i] % 16) return -1;
+      aux = geos[i];
     }
     const int S = (T[i] + chunk[i] - 1) / chunk[i];
     float* P = nullptr;
@@ -1048,7 +1213,7 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
       uniform256 = false;
     }
     if (fl & (TILE128 | NARROW_M | NARROW_N)) uniform256 = false;
-    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], C[i], P, geo, M[i], N[i], T[i], chunk[i], S, fl};
+    g.p[i] = Prob{(const bf16*)A[i], (const bf16*)B[i], C[i], P, aux, M[i], N[i], T[i], chunk[i], S, fl};
     g.first[i] = items;
     items += (M[i] / tm) * (N[i] / tn) * S;
   }

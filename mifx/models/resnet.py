@@ -122,18 +122,22 @@ class PreActBottleneck(nn.Module):
         residual add then happens inside bn0's fused kernels (fwd and bwd) -- or a `Fused` sum whose statistics the
         producing GEMM already reduced. Returns the un-added (branch, shortcut) pair, or a `Fused` sum when conv3 ran
         on the GEMM kernel, for the next block / the final BN."""
-        from ..ops.conv1x1 import conv1x1
+        from ..ops.conv1x1 import bn_conv1x1, bn_conv_eligible, conv1x1, proj_pair, proj_pair_eligible
         from ..ops.conv3x3 import conv3x3
 
-        if isinstance(x, Fused):
+        h = None
+        if isinstance(x, Fused) and self.shortcut is None and bn_conv_eligible(x.t, x.part, self.bn0,
+                                                                               self.conv1.weight):
+            # bn0 + ReLU folded into conv1 (identity shortcut: the sum itself, through the alias output)
+            y, part, s = bn_conv1x1(x.t, x.part, self.bn0, self.conv1.weight)
+            h = self.bn1.forward_tiles(y, part)[0]
+            pre = None
+        elif isinstance(x, Fused):
             pre, s = self.bn0.forward_tiles(x.t, x.part)
         elif isinstance(x, tuple):
             pre, s = self.bn0.forward_add(*x)
         else:
             pre, s = self.bn0(x), x
-        from ..ops.conv1x1 import proj_pair, proj_pair_eligible
-
-        h = None
         if self.shortcut is None:
             sc = s
         elif FUSED_1X1 and _fused_ok(self.conv1, pre) and self.shortcut.bias is None \
@@ -158,6 +162,9 @@ class PreActBottleneck(nn.Module):
         if _fused3_ok(self.conv2, h):
             # 3x3 on the implicit-GEMM kernel: BN2's statistics in its epilogue; h (BN1's output) feeds only conv2
             y, part = conv3x3(h, self.conv2.weight, self.conv2.stride[0], stats=True, bn_input=True)
+            if sc.shape[1] == self.conv3.out_channels and bn_conv_eligible(y, part, self.bn2, self.conv3.weight):
+                # bn2 + ReLU folded into conv3 (+ the shortcut, BN statistics of the sum)
+                return Fused(*bn_conv1x1(y, part, self.bn2, self.conv3.weight, residual=sc)[:2])
             h = self.bn2.forward_tiles(y, part)[0]
         else:
             h = self.bn2(self.conv2(h))

@@ -146,16 +146,17 @@ def _bwd_any(ctx, dy, x, w32, stats, relu, dres):
     return _bwd(dy, x, w32, stats, relu, dres)
 
 
-def _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, relu):
+def _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, relu, apply=True):
     """Forward from per-tile statistics computed by the GEMM that produced x (mifx.ops.conv1x1): no statistics pass
-    over x. part: [2, T, C] fp32 (tile means, tile M2), T tiles of M / T rows."""
+    over x. part: [2, T, C] fp32 (tile means, tile M2), T tiles of M / T rows. apply=False: statistics (and running
+    statistics) only, y None -- the consumer GEMM applies them to its operand (mifx.ops.conv1x1.bn_conv1x1)."""
     v = _nhwc_view(x)
     M, C = v.shape
     T = part.shape[1]
     w32, b32 = weight.float().contiguous(), bias.float().contiguous()
     stats = torch.empty(4, C, device=x.device, dtype=torch.float32)
     ws = torch.empty(_fns()["tiles_ws"](T, C), device=x.device, dtype=torch.float64)
-    y = torch.empty_like(x)
+    y = torch.empty_like(x) if apply else None
     check(_fns()["fwd_tiles"](_dt(x), ptr(v), M, C, ptr(part), T, M // T, ptr(w32), ptr(b32), float(eps),
                               float(momentum), ptr(run_mean), ptr(run_var if run_mean is not None else None),
                               int(relu), ptr(stats), ptr(ws), ptr(y), stream_handle(x.device)), "mifx_bn_relu_fwd_tiles")

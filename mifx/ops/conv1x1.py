@@ -25,6 +25,7 @@ import torch
 
 from . import gemm as hg
 from . import native_stats, weight_prep
+from ._lib import check, ptr, stream_handle
 
 # dX backend for tileable shapes: "gemm8" (default) or "miopen" (A/B)
 DGRAD = os.environ.get("MIFX_CONV1X1_DGRAD", "gemm8")
@@ -253,3 +254,91 @@ def proj_pair(x: torch.Tensor, w_sc: torch.Tensor, stride: int, w1: torch.Tensor
     if bn is not None and not getattr(bn, "mifx_bn", False):
         bn = None
     return _ProjPair.apply(x, w_sc, w1, int(stride), bn)
+
+
+# BatchNorm + ReLU folded into the consumer 1x1 convolution: opt-in (MIFX_BN_FOLD=1). Measured slower in the ResNet-50
+# step (11,300 vs 12,159 img/s, profiles/resnet_bn_fold_ab_r5.txt): the per-lane operand transform is repeated by the
+# 4 waves sharing each A row and costs more MFMA-pipe time (128 x 128 EPI 6: 193 vs 113 us per call) than the apply
+# pass it removes (~6.3 TB/s streaming)
+BN_FOLD = os.environ.get("MIFX_BN_FOLD", "0") == "1"
+
+
+class _BNConv1x1(torch.autograd.Function):
+    """relu(bn(x)) -> 1x1 convolution (+ residual) as ONE node whose activation is never stored: the forward finalizes
+    the BatchNorm from the per-tile statistics of x (reduced by the GEMM that wrote x) and the convolution's GEMM
+    applies relu(x scale + shift) to its X fragments as they leave LDS (csrc/gemm8.hip AX operands); the backward's
+    input-gradient GEMM writes the activation's gradient with the BatchNorm's backward sums in its epilogue (EPI 8),
+    the deferred weight gradient applies the same transform to its B operand (grouped TN BNX problems), and one
+    finalize + apply pass gives dx (plus `dalias`: the gradient of the x alias output, e.g. the next identity
+    shortcut's). Saves the BatchNorm's apply pass (a read and a write of the activation) in the forward."""
+
+    @staticmethod
+    def forward(ctx, x, part_in, gamma, beta, run_mean, run_var, momentum, eps, w, r):
+        from . import bn_relu
+
+        w32, stats = bn_relu._fwd_tiles(x, part_in, gamma, beta, run_mean, run_var, momentum, eps, True,
+                                        apply=False)[1:]
+        n, cin, h, w_ = x.shape
+        cout = w.shape[0]
+        im = weight_prep.images(w)
+        wb = im[0] if im is not None else w.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        ctx.wt = im[1] if im is not None else None
+        out = torch.empty(n, cout, h, w_, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        rr = _rows(r.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)) if r is not None else None
+        _, part = hg.gemm8_nt_bnx(_rows(x), wb, stats[2:4], 6 if r is not None else 5, r=rr, out=_rows(out))
+        ctx.save_for_backward(x, w32, stats, wb)
+        ctx.w, ctx.has_r, ctx.wdtype = w, r is not None, gamma.dtype
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(part)
+        return out, part, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dout, dpart, dalias):
+        from . import bn_relu
+
+        x, w32, stats, wb = ctx.saved_tensors
+        if dout is None:
+            return (dalias, None, None, None) + (None,) * 6
+        n, cin, h, w_ = x.shape
+        cout = wb.shape[0]
+        dyc = dout.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+        dy2 = _rows(dyc)
+        x2 = _rows(x)
+        dw = None
+        if ctx.needs_input_grad[8]:
+            dw = hg.defer_weight_grad_f32(dy2, x2, ctx.w, bnx=stats[2:4])
+            if dw is None:  # materialize the activation for the library's weight gradient
+                native_stats.count("conv1x1_dW", False)
+                act = torch.empty_like(x)
+                check(bn_relu._fns()["apply"](1, ptr(x2), x2.shape[0], cin, ptr(stats[2]), ptr(stats[3]), 1,
+                                              ptr(_rows(act)), stream_handle(x.device)), "mifx_bn_relu_apply")
+                dw = torch.ops.aten.convolution_backward(dyc, act, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0],
+                                                         [1, 1], False, [0, 0], 1, [False, True, False])[1]
+                dw = dw.to(ctx.w.dtype)
+        wt = ctx.wt if ctx.wt is not None else hg.transpose(wb)
+        dact = torch.empty(n, cin, h, w_, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        _, bpart = hg.gemm8_nt(dy2, wt, x2, 8, cfg=hg.gemm8_pick(dy2.shape[0], cin, cout), z=stats, out=_rows(dact))
+        dx, dgb = bn_relu._bwd_tiles(dact, x, w32, stats, dalias, bpart)
+        return (dx, None, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None, dw,
+                dyc if ctx.has_r else None)
+
+
+def bn_conv_eligible(x: torch.Tensor, part, bn, w: torch.Tensor) -> bool:
+    """x (a BatchNorm + ReLU input with per-tile statistics `part`) -> 1x1 conv w foldable into one _BNConv1x1."""
+    from . import bn_relu
+
+    if not (BN_FOLD and part is not None and bn.training and bn.track_running_stats and bn_relu.native_ok(x)
+            and x.dtype == torch.bfloat16 and eligible(x, w) and w.shape[1] == x.shape[1] and x.shape[1] <= 2048):
+        return False
+    n, cin, h, ww = x.shape
+    M = n * h * ww
+    return hg.gemm8_pick(M, w.shape[0], cin, bnx=True) is not None and hg.gemm8_pick(M, cin, w.shape[0]) is not None
+
+
+def bn_conv1x1(x: torch.Tensor, part: torch.Tensor, bn, w: torch.Tensor, residual: torch.Tensor | None = None):
+    """(conv1x1(relu(bn(x))) [+ residual], the output's per-tile statistics, x alias) with the activation never stored
+    (see _BNConv1x1); bn: the BatchNormReLU2d (training, running statistics updated), part: x's per-tile statistics.
+    Use the alias output where x itself is consumed again (an identity shortcut)."""
+    native_stats.count("conv1x1_fwd", True)
+    rm, rv, _ = bn._args()
+    return _BNConv1x1.apply(x, part, bn.weight, bn.bias, rm, rv, bn.momentum, bn.eps, w, residual)

@@ -262,11 +262,12 @@ def _defer_ok(dy2: torch.Tensor, x2: torch.Tensor, w) -> bool:
     return N % 256 == 0 and K % 256 == 0 and T % 64 == 0 and len(_DEFER["pending"]) < 64
 
 
-def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor):
+def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bnx: torch.Tensor | None = None):
     """Inside `deferred_weight_grads()`: record dW = dY^T X for the fp32-ACCUMULATING grouped flush (convolution
     weights: fp32 parameters, token counts of 10^4-10^6 rows split into chunks) and return the ZERO placeholder
     gradient for autograd (shape / dtype of w; whatever .grad ends up holding, the flush adds the product into it).
-    None when not deferring (or the shape does not tile)."""
+    bnx: fp32 [2, K] (scale, shift): the product is dY^T relu(X scale + shift). None when not deferring (or the shape
+    does not tile)."""
     if not (_DEFER["on"] and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
             and w.dtype == torch.float32 and os.environ.get("MIFX_DEFER_DW", "1") != "0"):
         return None
@@ -282,7 +283,8 @@ def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor):
     # gradient (micro-batch accumulation, bucket views): then it is zeros and the flush ADDS
     overwrite = w.grad is None
     ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
-    _DEFER["pending_f32"].append((dy2.contiguous(), x2.contiguous(), w, ph.data_ptr() if overwrite else None))
+    rec = (dy2.contiguous(), x2.contiguous(), w, ph.data_ptr() if overwrite else None)
+    _DEFER["pending_f32"].append(rec if bnx is None else rec + (bnx, _WGRAD_CHUNK))
     return ph
 
 
@@ -338,7 +340,8 @@ def flush_weight_grads() -> int:
         probs, acc = [], []
         for rec in pf:
             dy, x, w, ph = rec[:4]
-            geo = rec[4] if len(rec) > 4 else None
+            aux = rec[4] if len(rec) > 4 else None
+            geo = aux if aux is not None and aux.dtype == torch.uint8 else None
             ck = rec[5] if len(rec) > 5 else _WGRAD_CHUNK
             g = w.grad
             lay_ok = g is not None and (g.is_contiguous(memory_format=torch.channels_last)
@@ -351,6 +354,8 @@ def flush_weight_grads() -> int:
             if geo is not None:  # [Cout][3][3][C] storage of the channels_last gradient ([Cout][C]: strided 1x1)
                 flat = g.permute(0, 2, 3, 1).reshape(g.shape[0], -1) if geo.mifx_taps == 9 else g.view(g.shape[0], -1)
                 probs.append((dy, x, flat, geo, ck))
+            elif aux is not None:  # BatchNorm-operand problem
+                probs.append((dy, x, g.view(dy.shape[1], x.shape[1]), aux, ck))
             else:
                 probs.append((dy, x, g.view(dy.shape[1], x.shape[1])))
             acc.append(ph is None)
@@ -676,7 +681,8 @@ def _g8_fns():
                                                     I32, VP]),
             "geo_bytes": sig(lib, "mifx_gemm8_geo_bytes", []),
             "geo": sig(lib, "mifx_gemm8_geo", [I32, I32, I32, I32, I32, I32, I32, VP]),
-            "conv1x1s": sig(lib, "mifx_gemm8_conv1x1s", [I32, I32, VP, VP, VP, VP, I32, I32, I32, I32, I32, I32, VP])}
+            "conv1x1s": sig(lib, "mifx_gemm8_conv1x1s", [I32, I32, VP, VP, VP, VP, I32, I32, I32, I32, I32, I32, VP]),
+            "nt_bnx": sig(lib, "mifx_gemm8_nt_bnx", [I32, I32, VP, VP, VP, VP, VP, I32, I32, I32, VP, VP])}
 
 
 @functools.lru_cache(maxsize=None)
@@ -697,12 +703,18 @@ _G8_OCC = {(128, 128): 2, (256, 64): 2, (128, 64): 2}
 _G8_NARROW = os.environ.get("MIFX_G8_NARROW", "1") != "0"
 
 
-def gemm8_pick(M: int, N: int, K: int, cus: int = 256) -> int | None:
+# the BatchNorm-operand (AX) build of the 256 x 256 tile spills registers: left out of its picks unless MIFX_BNX_256=1
+_BNX_256 = os.environ.get("MIFX_BNX_256", "0") == "1"
+
+
+def gemm8_pick(M: int, N: int, K: int, cus: int = 256, bnx: bool = False) -> int | None:
     """The csrc/gemm8.hip configuration for an M x N x K product: the highest (fraction of the last wave's slots
-    filled) x (the tile's relative throughput); None if none tiles the shape."""
+    filled) x (the tile's relative throughput); None if none tiles the shape. bnx: for gemm8_nt_bnx."""
     best, best_score = None, None
     for i, (bm, bn) in enumerate(gemm8_configs()):
         if M % bm or N % bn or K % 64 or (bn == 64 and not _G8_NARROW):
+            continue
+        if bnx and (bm, bn) == (256, 256) and not _BNX_256:
             continue
         tiles = (M // bm) * (N // bn)
         slots = cus * _G8_OCC.get((bm, bn), 1)
@@ -722,7 +734,9 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
     where `accumulate` -- a bool or one per problem -- is False), the token range cut into `chunk`-row pieces whose
     fp32 partials a second launch sums in order. 256 x 256 tiles where M and N allow (tile128=True forces 128 x 128).
     A 4-tuple (dy [T, Cout], x NHWC [Nb, H, W, C], c fp32 [Cout, 9 C], geo) is a 3x3 convolution's weight gradient
-    with the input rows gathered per output pixel and tap (geo = conv_geo(...)). Returns the number of work items."""
+    with the input rows gathered per output pixel and tap (geo = conv_geo(...)); (a, b, c fp32, ax) with ax an fp32
+    [2, N] (scale, shift) multiplies a by relu(b scale + shift) instead of b (a BatchNorm + ReLU input whose output was
+    never stored, mifx.ops.conv1x1.bn_conv1x1). A 5th element: the problem's token chunk. Returns the work items."""
     n = len(problems)
     if n == 0:
         return 0
@@ -733,7 +747,9 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
     Ms, Ns, Ts, chunks, flags, geos, ws_floats = [], [], [], [], [], [], 0
     for pr in problems:
         a, b, c = pr[:3]
-        geo = pr[3] if len(pr) > 3 else None
+        aux = pr[3] if len(pr) > 3 else None
+        bnx = aux if aux is not None and aux.dtype == torch.float32 else None  # BatchNorm (scale, shift) of B
+        geo = aux if bnx is None else None
         pchunk = pr[4] if len(pr) > 4 else chunk
         taps = getattr(geo, "mifx_taps", 9)
         if geo is not None:
@@ -752,6 +768,9 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
                                  "fp32)")
             T, M = a.shape
             N = b.shape[1]
+            if bnx is not None and not (c.dtype == torch.float32 and bnx.is_contiguous() and bnx.numel() == 2 * N):
+                raise ValueError("gemm8_tn_grouped: a BatchNorm-operand problem needs fp32 c and fp32 [2, N] scale / "
+                                 "shift")
         f32 = c.dtype == torch.float32
         t128 = tile128 if tile128 is not None else (M % 256 or N % 256 or (geo is not None and (N // taps) % 256))
         # a 64-wide dimension (ResNet-50 stage 1): the narrow 256 x 64 / 64 x 256 tiles (fp32 problems)
@@ -767,8 +786,9 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
         Ts.append(T)
         chunks.append(ck)
         flags.append((1 if f32 else 0) | (2 if t128 else 0) | (4 if f32 and accs[len(flags)] else 0)
-                     | (8 if geo is not None else 0) | (16 if nar_n else 0) | (32 if nar_m else 0))
-        geos.append(geo.data_ptr() if geo is not None else None)
+                     | (8 if geo is not None else 0) | (16 if nar_n else 0) | (32 if nar_m else 0)
+                     | (64 if bnx is not None else 0))
+        geos.append(aux.data_ptr() if aux is not None else None)
         if f32:
             ws_floats += -(-T // ck) * M * N
     dev = problems[0][0].device
@@ -855,6 +875,30 @@ def gemm8_conv3x3(x: torch.Tensor, w9: torch.Tensor, stride: int = 1, pad: int =
         raise ValueError("gemm8_conv3x3: contiguous bf16 NHWC input and [Cout, 9 C] weight")
     check(_g8_fns()["conv"](int(cfg), int(epi), ptr(x), ptr(w9), ptr(b), ptr(y), ptr(z), ptr(part), nb, h, w_, c,
                             cout, stride, pad, stream_handle(x.device)), "mifx_gemm8_conv3x3")
+    return y, part
+
+
+def gemm8_nt_bnx(x2: torch.Tensor, w: torch.Tensor, ax: torch.Tensor, epi: int = 0, r: torch.Tensor | None = None,
+                 cfg: int | None = None, out: torch.Tensor | None = None):
+    """relu(x2 scale + shift) . w^T on csrc/gemm8.hip, the BatchNorm + ReLU applied to the X fragments in the kernel:
+    x2 [M, K] bf16 (a BatchNorm's INPUT), w [N, K] bf16, ax fp32 [2, K] = (scale, shift) -> (Y [M, N] bf16, part). epi
+    0; 5: part = per-tile BatchNorm statistics of Y; 6: Y += r ([M, N] bf16) with the statistics of the sum. K <= 2048."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if cfg is None:
+        cfg = gemm8_pick(M, N, K, bnx=True)
+    if cfg is None:
+        raise ValueError(f"no gemm8 tile configuration for the {M}x{N}x{K} BatchNorm-operand product")
+    if not (x2.is_contiguous() and w.is_contiguous() and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and ax.dtype == torch.float32 and ax.is_contiguous() and ax.numel() == 2 * K):
+        raise ValueError("gemm8_nt_bnx: contiguous bf16 x2 [M, K] / w [N, K] and fp32 [2, K] scale / shift")
+    if epi == 6 and (r is None or not r.is_contiguous() or r.dtype != torch.bfloat16):
+        raise ValueError("gemm8_nt_bnx epi 6: a contiguous bf16 [M, N] addend")
+    bm = gemm8_configs()[cfg][0]
+    y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    part = torch.empty(2, M // bm, N, device=x2.device, dtype=torch.float32) if epi in (5, 6) else None
+    check(_g8_fns()["nt_bnx"](int(cfg), int(epi), ptr(x2), ptr(w), ptr(r), ptr(y), ptr(part), M, N, K, ptr(ax),
+                              stream_handle(x2.device)), "mifx_gemm8_nt_bnx")
     return y, part
 
 

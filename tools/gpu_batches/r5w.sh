@@ -1,0 +1,12 @@
+# round 5: BN apply passes with four rows in flight; tests; ResNet A/B of rows per thread; steady table
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests/test_bn_relu.py tests/test_conv1x1.py tests/test_resnet_infer.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r5w_tests.log 2>&1; rc=$?
+tail -2 gpurun_out/r5w_tests.log; [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/r5w_tests.log | head -30; tail -30 gpurun_out/r5w_tests.log; exit $rc; }
+for v in 8 16 8 16; do
+  MIFX_BN_APPLY_ROWS=$v timeout -k 10 400 python -u -m mifx.trainer.resnet_trainer --steps 20 --warmup 5 > gpurun_out/r5w_resnet_$v.json 2> gpurun_out/r5w_resnet_$v.err || { tail -20 gpurun_out/r5w_resnet_$v.err; exit 1; }
+  python -c "import json; r=json.loads([l for l in open('gpurun_out/r5w_resnet_$v.json') if l.startswith('{')][-1]); print('rows', $v, round(r['value'],1), round(r['ms_per_step'],3), 'ms')"
+done
+timeout -k 10 300 python -u tools/torch_kernel_table.py --model resnet --batch 256 --warmup 8 --active 3 > gpurun_out/resnet_steady_r5w.md 2> gpurun_out/resnet_steady_r5w.err || { tail -5 gpurun_out/resnet_steady_r5w.err; exit 1; }
+grep -E "GPU time|bn_" gpurun_out/resnet_steady_r5w.md
