@@ -491,7 +491,8 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ x,
                                                         long long M, int C, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, const float* __restrict__ k,
-                                                        int relu, const T* __restrict__ dres, T* __restrict__ dx) {
+                                                        int relu, const T* __restrict__ dres, T* __restrict__ dx,
+                                                        T* __restrict__ act) {
   const int tpr = C / kVec, rpb = kThreads / tpr;
   const int slice = threadIdx.x / tpr, cg = threadIdx.x % tpr;
   if (slice >= rpb) return;
@@ -515,22 +516,29 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ d
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      float a[kVec];
 #pragma unroll
       for (int e = 0; e < kVec; ++e) {
-        const float g = (relu && fmaf(u[k][e], sc[e], sh[e]) <= 0.f) ? 0.f : d[k][e];
+        const float t = fmaf(u[k][e], sc[e], sh[e]);
+        a[e] = relu ? fmaxf(t, 0.f) : t;
+        const float g = (relu && t <= 0.f) ? 0.f : d[k][e];
         d[k][e] = fmaf(A[e], g, fmaf(B[e], u[k][e], Cc[e]));
         if (dres != nullptr) d[k][e] += rr[k][e];
       }
       stv(dx + (size_t)(r + k * rpb) * C + c0, d[k]);
+      if (act != nullptr) stv(act + (size_t)(r + k * rpb) * C + c0, a);  // the forward's activation, re-derived
     }
   }
   for (; r < r1; r += rpb) {
     float d[kVec], u[kVec];
     ldv(dy + (size_t)r * C + c0, d);
     ldv(x + (size_t)r * C + c0, u);
+    float a[kVec];
 #pragma unroll
     for (int e = 0; e < kVec; ++e) {
-      const float g = (relu && fmaf(u[e], sc[e], sh[e]) <= 0.f) ? 0.f : d[e];
+      const float t = fmaf(u[e], sc[e], sh[e]);
+      a[e] = relu ? fmaxf(t, 0.f) : t;
+      const float g = (relu && t <= 0.f) ? 0.f : d[e];
       d[e] = fmaf(A[e], g, fmaf(B[e], u[e], Cc[e]));
     }
     if (dres != nullptr) {  // gradient arriving through the identity shortcut, accumulated here
@@ -540,6 +548,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply(const T* __restrict__ d
       for (int e = 0; e < kVec; ++e) d[e] += rr[e];
     }
     stv(dx + (size_t)r * C + c0, d);
+    if (act != nullptr) stv(act + (size_t)r * C + c0, a);
   }
 }
 
@@ -640,9 +649,11 @@ int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const f
 
 // Backward from per-tile reductions computed by the GEMM that produced dy (csrc/gemm8.hip EPI_BNBWD): pg / pgx [T][C]
 // = per-tile sum g and sum g xhat; then the same finalize and apply as mifx_bn_relu_bwd (no reduction pass over dy, x).
+// act non-null: also writes the forward's activation relu(x scale + shift) (for a consumer convolution whose forward
+// applied the BatchNorm in its GEMM and whose weight gradient needs the activation: mifx.ops.conv1x1.bn_conv1x1)
 int mifx_bn_relu_bwd_tiles(int dtype, const void* dy, const void* x, const void* dres, long long M, int C,
                            const float* w, const float* stats, int relu, const float* pg, const float* pgx, int T,
-                           float* kbuf, void* dx, float* dgamma, float* dbeta, hipStream_t st) {
+                           float* kbuf, void* dx, float* dgamma, float* dbeta, void* act, hipStream_t st) {
   if (!shape_ok(M, C) || T <= 0 || pg == nullptr || pgx == nullptr) return -1;
   const float *mean = stats, *rstd = stats + C, *scale = stats + 2 * C, *shift = stats + 3 * C;
   hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kFinCols - 1) / kFinCols), dim3(kThreads), 0, st, pg, pgx, T, M, C, w,
@@ -650,10 +661,10 @@ int mifx_bn_relu_bwd_tiles(int dtype, const void* dy, const void* x, const void*
   if (dtype)
     hipLaunchKernelGGL(bn_bwd_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
                        (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, M, C, scale, shift, kbuf, relu,
-                       (const __hip_bfloat16*)dres, (__hip_bfloat16*)dx);
+                       (const __hip_bfloat16*)dres, (__hip_bfloat16*)dx, (__hip_bfloat16*)act);
   else
     hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)dy,
-                       (const float*)x, M, C, scale, shift, kbuf, relu, (const float*)dres, (float*)dx);
+                       (const float*)x, M, C, scale, shift, kbuf, relu, (const float*)dres, (float*)dx, (float*)act);
   return (int)hipGetLastError();
 }
 
@@ -698,10 +709,11 @@ int mifx_bn_relu_bwd(int dtype, const void* dy, const void* x, const void* dres,
   if (dtype)
     hipLaunchKernelGGL(bn_bwd_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,
                        (const __hip_bfloat16*)dy, (const __hip_bfloat16*)x, M, C, scale, shift, kbuf, relu,
-                       (const __hip_bfloat16*)dres, (__hip_bfloat16*)dx);
+                       (const __hip_bfloat16*)dres, (__hip_bfloat16*)dx, (__hip_bfloat16*)nullptr);
   else
     hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st, (const float*)dy,
-                       (const float*)x, M, C, scale, shift, kbuf, relu, (const float*)dres, (float*)dx);
+                       (const float*)x, M, C, scale, shift, kbuf, relu, (const float*)dres, (float*)dx,
+                       (float*)nullptr);
   return (int)hipGetLastError();
 }
 

@@ -157,11 +157,16 @@ constexpr int vm_wait(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4
 // The body: one BM x BN tile of Y = X W^T (NT: X [M, K], W [N, K] row-major) or of C = A^T B (TN: A [K, M],
 // B [K, N] row-major; X := A, W := B, "K" = tokens), m0 / n0 its origin. CV: implicit-convolution operand (above);
 // tok0: the first token of this item's chunk (CV 2: B is then the whole conv input, gathered by pixel index).
-// AX: the BatchNorm + ReLU transform relu(v scale[c] + shift[c]) of the input channel c, applied to the fragments as
-// they leave LDS (ax = fp32 [scale, shift], each K (NT: the X operand's channels, staged in LDS after the two K-tile
-// buffers) or N (TN: the B operand's columns, in registers) long). The consumer convolution of a BatchNorm + ReLU thus
-// reads the BatchNorm's INPUT and the activation is never written (bit-identical to the stored-activation path: same
-// fused multiply-add and rounding as csrc/bn_relu.hip bn_apply).
+// AX: the BatchNorm + ReLU transform relu(v scale[c] + shift[c]) of channel c applied to one operand -- NT: X (c = the
+// K index), TN: B (c = the column) -- so the consumer convolution of a BatchNorm + ReLU reads the BatchNorm's INPUT and
+// the activation is never written (bit-identical to the stored-activation path: same fused multiply-add and rounding
+// as csrc/bn_relu.hip bn_apply). ax = fp32 [scale[L], shift[L]], L = K (NT) or N (TN); its slice is copied to LDS
+// after the two K-tile buffers. The transformed operand's half-tiles are DMA'd as usual; in the phase where a half is
+// guaranteed to have landed (its counted wait), each thread rewrites the 16-byte chunks ITS OWN DMAs delivered --
+// once per workgroup, not per consuming wave -- BEFORE that phase's first barrier, which precedes every wave's
+// fragment reads of that half in both stagger groups. (Staging through registers instead mixes plain loads with the
+// LDS DMAs, and the compiler then drains vmcnt to 0 every K-tile.) Duplicated DMAs (narrow B halves) of the
+// transformed operand land in a scratch area instead, so no raw copy can overwrite a transformed chunk.
 template <int BM, int BN, int EPI, typename P, bool TN, int CV = 0, bool AX = false>
 __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf16* __restrict__ W,
                                            const P* __restrict__ bias, bf16* __restrict__ Y, bf16* __restrict__ Z,
@@ -257,6 +262,22 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       bcol[i] = 8 * c;
     }
   }
+  // AX: table loads (before every DMA: retired by the prologue's counted wait)
+  constexpr int XS = AX ? (TN ? WR : XR) : 1;       // 16-byte chunks per thread per transformed half
+  constexpr int TABF = AX ? (TN ? 2 * BN : 0) : 0;  // TN table floats ([scale, shift] of this tile's columns)
+  float4 axv[2] = {};
+  if constexpr (AX && !TN) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = (i * NT + tid) * 4;
+      if (q < 2 * K) axv[i] = *(const float4*)(ax + q);
+    }
+  }
+  if constexpr (AX && TN) {
+    const int q = tid * 4;
+    if (q < TABF) axv[0] = *(const float4*)(ax + (q < BN ? n0 + q : N + n0 + q - BN));
+  }
+
   // half h (0 A0, 1 B0, 2 A1, 3 B1) of K-tile t into LDS buffer t & 1
   auto stage = [&](int h, int t) {
     unsigned char* buf = lds + (t & 1) * BUF;
@@ -307,40 +328,15 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       unsigned char* dst = buf + (h == 1 ? OFF_B0 : OFF_B1);
       const bf16* src = TN ? W + (size_t)k0 * N + (h == 3 ? HB : 0) : W + (h == 3 ? HB * K : 0) + k0;
 #pragma unroll
-      for (int i = 0; i < WR; ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const void*)(src + boff[i]),
-            (__attribute__((address_space(3))) void*)(dst + (WDUP ? (64 * w) % BDMA : i * NT + 64 * w) * 16), 16, 0,
-            0);
+      for (int i = 0; i < WR; ++i) {
+        // (AX TN: the duplicate DMAs of a transformed narrow half land in the scratch area after the table)
+        unsigned char* d = (AX && TN && WDUP && 64 * w >= BDMA) ? lds + 2 * BUF + 4 * TABF + (64 * w - BDMA) * 16
+                                                              : dst + (WDUP ? (64 * w) % BDMA : i * NT + 64 * w) * 16;
+        __builtin_amdgcn_global_load_lds((const void*)(src + boff[i]), (__attribute__((address_space(3))) void*)d,
+                                         16, 0, 0);
+      }
     }
   };
-
-  // AX operands, loaded before the prologue's DMAs (older than them: retired by its counted wait). NT: the [scale,
-  // shift] table of all K channels (<= 2048) -> LDS after the two K-tile buffers; TN: this lane's B columns, per
-  // (B half, fragment)
-  constexpr int AXV = AX && !TN ? 2 : 1;
-  float4 axv[AXV];
-  float axs[AX && TN ? 2 : 1][AX && TN ? NF : 1], axh[AX && TN ? 2 : 1][AX && TN ? NF : 1];
-  if constexpr (AX && !TN) {
-#pragma unroll
-    for (int i = 0; i < AXV; ++i) {
-      const int q = (i * NT + tid) * 4;
-      axv[i] = q < 2 * K ? *(const float4*)(ax + q) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  if constexpr (AX && TN) {
-#pragma unroll
-    for (int hb = 0; hb < 2; ++hb)
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        const int c = n0 + hb * HB + wn * CPW + 16 * f + (lane & 15);
-        axs[hb][f] = ax[c];
-        axh[hb][f] = ax[N + c];
-      }
-  }
-  (void)axv;
-  (void)axs;
-  (void)axh;
 
   v4f acc[2][2][NF][MF];  // [mq][nq][n-frag][m-frag]
 #pragma unroll
@@ -366,9 +362,37 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     s2 = s2 >= cpr_rot ? s2 - cpr_rot : s2;
     return tr_frag(half + (t1 * cpr_rot + s1) * 16 + 8 * (tp & 1), half + (t2 * cpr_rot + s2) * 16 + 8 * (tp & 1));
   };
-  auto bnrelu = [](v8bf& v, const float* sc, const float* sh) {
+  // AX commit: transform staged half x (0: A0 / B0, 1: A1 / B1) of K-tile t and write it to its LDS slots
+  auto commit = [&](int x, int t) {
+    unsigned char* buf = lds + (t & 1) * BUF;
+    const float* tab = (const float*)(lds + 2 * BUF);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf(fmaf((float)v[e], sc[e], sh[e]), 0.f);
+    for (int i = 0; i < XS; ++i) {
+      int slot, c;  // LDS chunk slot and its first channel (NT: K index; TN: table column)
+      if constexpr (!TN) {
+        slot = i * NT + tid;
+        const int row = slot >> 3;
+        c = t * BK + 8 * swz(row, slot & 7);
+      } else {
+        if (WDUP && tid >= BDMA) continue;  // (its duplicate DMAs went to the scratch area)
+        slot = WDUP ? tid : i * NT + tid;
+        const int tr = slot / CPB, pc = slot % CPB;
+        int cc = pc - rot<CPB>(tr);
+        cc = cc < 0 ? cc + CPB : cc;
+        c = x * HB + 8 * cc;
+      }
+      const int L = TN ? BN : K;
+      const float4 s0 = *(const float4*)(tab + c), s1 = *(const float4*)(tab + c + 4);
+      const float4 h0 = *(const float4*)(tab + L + c), h1 = *(const float4*)(tab + L + c + 4);
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      unsigned char* half = buf + (TN ? (x ? OFF_B1 : OFF_B0) : (x ? OFF_A1 : OFF_A0));
+      v8bf v = *(const v8bf*)(half + slot * 16);  // this thread's own DMA, landed (counted wait)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf(fmaf((float)v[e], sc[e], sh[e]), 0.f);
+      *(v8bf*)(half + slot * 16) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible at the next barrier
   };
   auto read_a = [&](const unsigned char* half, v8bf (&r)[MF][2], int k0) {
 #pragma unroll
@@ -382,24 +406,7 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
           r[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
       }
     }
-    if constexpr (AX && !TN) {  // channels k0 + 32 ks + 8 fc + e of every row: one scale / shift octet per k-step
-      const float* tab = (const float*)(lds + 2 * BUF);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {  // four channels at a time (register pressure of the 256 x 256 tile)
-          const int c = k0 + 32 * ks + 8 * fc + 4 * q;
-          const float4 sc = *(const float4*)(tab + c), sh = *(const float4*)(tab + K + c);
-#pragma unroll
-          for (int f = 0; f < MF; ++f) {
-            v8bf& v = r[f][ks];
-            v[4 * q + 0] = (bf16)fmaxf(fmaf((float)v[4 * q + 0], sc.x, sh.x), 0.f);
-            v[4 * q + 1] = (bf16)fmaxf(fmaf((float)v[4 * q + 1], sc.y, sh.y), 0.f);
-            v[4 * q + 2] = (bf16)fmaxf(fmaf((float)v[4 * q + 2], sc.z, sh.z), 0.f);
-            v[4 * q + 3] = (bf16)fmaxf(fmaf((float)v[4 * q + 3], sc.w, sh.w), 0.f);
-          }
-        }
-    }
+    (void)k0;
   };
   auto read_b = [&](const unsigned char* half, int hb) {
 #pragma unroll
@@ -411,17 +418,9 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
           rb[f][ks] = tn_frag(half, CPB, wn * CPW + 16 * f, ks);
         else
           rb[f][ks] = *(const v8bf*)(half + row * 128 + swz(row, 4 * ks + fc) * 16);
-        if constexpr (AX && TN) {  // one column (channel) per lane and fragment
-          float sc[8], sh[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            sc[e] = axs[hb][f];
-            sh[e] = axh[hb][f];
-          }
-          bnrelu(rb[f][ks], sc, sh);
-        }
       }
     }
+    (void)hb;
   };
   auto mma = [&](v4f (&c)[NF][MF], const v8bf (&ra)[MF][2]) {
     __builtin_amdgcn_s_setprio(1);
@@ -452,19 +451,26 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  if constexpr (AX && !TN) {
+  if constexpr (AX) {  // the table to LDS (all threads' parts visible after the barrier), then tile 0's half 0
 #pragma unroll
-    for (int i = 0; i < AXV; ++i) {
+    for (int i = 0; i < 2; ++i) {
       const int q = (i * NT + tid) * 4;
-      if (q < 2 * K) *(float4*)(lds + 2 * BUF + 4 * q) = axv[i];
+      if (q < (TN ? TABF : 2 * K)) *(float4*)(lds + 2 * BUF + 4 * q) = axv[i];
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    commit(0, 0);
   }
   barrier();
   if (grp == 1) barrier();  // the stagger: waves 4-7 one barrier behind
 
-  for (int t = 0; t < KT; ++t) {
+  // one K-tile: 4 phases. ST1 / ST2: K-tiles t + 1 / t + 2 exist (compile-time in the AX build's peeled loop, so every
+  // path through its main loop issues the same vector-memory operations and the compiler's own waits on the staging
+  // registers equal the counted ones instead of draining)
+  auto ktile = [&](int t, auto S1, auto S2, bool rst1, bool rst2) {
+    constexpr int cs1 = decltype(S1)::value, cs2 = decltype(S2)::value;  // 1 / 0, or -1: runtime (rst1 / rst2)
+    const bool st1 = cs1 < 0 ? rst1 : cs1 == 1, st2 = cs2 < 0 ? rst2 : cs2 == 1;
     const unsigned char* buf = lds + (t & 1) * BUF;
-    const bool st1 = t + 1 < KT, st2 = t + 2 < KT;
     auto phase = [&](auto J) {
       constexpr int j = decltype(J)::value;
       // LDS fragment reads of this phase's quadrant
@@ -487,6 +493,12 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail: nothing younger to count on
       }
+      if constexpr (AX) {  // landed now: j 0 -> A1(t), 1 -> B1(t), 2 -> A0(t + 1), 3 -> B0(t + 1)
+        if constexpr (!TN && j == 0) commit(1, t);
+        if constexpr (!TN && j == 2) if (st1) commit(0, t + 1);
+        if constexpr (TN && j == 1) commit(1, t);
+        if constexpr (TN && j == 3) if (st1) commit(0, t + 1);
+      }
       barrier();
       if constexpr (j == 0) mma(acc[0][0], ra0);
       if constexpr (j == 1) mma(acc[1][0], ra1);
@@ -498,6 +510,17 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
     phase(std::integral_constant<int, 1>{});
     phase(std::integral_constant<int, 2>{});
     phase(std::integral_constant<int, 3>{});
+  };
+  using c1 = std::integral_constant<int, 1>;
+  using c0 = std::integral_constant<int, 0>;
+  using cr = std::integral_constant<int, -1>;
+  if constexpr (AX) {
+    int t = 0;
+    for (; t + 2 < KT; ++t) ktile(t, c1{}, c1{}, true, true);
+    if (t + 1 < KT) ktile(t++, c1{}, c0{}, true, false);
+    if (t < KT) ktile(t, c0{}, c0{}, false, false);
+  } else {
+    for (int t = 0; t < KT; ++t) ktile(t, cr{}, cr{}, t + 1 < KT, t + 2 < KT);
   }
   if (grp == 0) barrier();  // equal barrier counts for both groups
 
@@ -824,12 +847,9 @@ __device__ __forceinline__ void grouped_item(const Prob& p, int item, int quad, 
     else if (p.flags & NARROW_M)
       gemm8_tile<64, BN, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
                                                        Geo{}, 0, nullptr, bx);
-    else if (p.flags & TILE128)
+    else  // (TILE128: the 256 x 256 build with the staging registers would exceed the register file)
       gemm8_tile<BM / 2, BN / 2, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0,
                                                                n0, lds, Geo{}, 0, nullptr, bx);
-    else
-      gemm8_tile<BM, BN, EPI_F32, bf16, true, 0, true>(A, B, nullptr, nullptr, nullptr, p.M, p.N, len, P, m0, n0, lds,
-                                                       Geo{}, 0, nullptr, bx);
     return;
   }
   if (p.flags & F32) {
@@ -1197,8 +1217,9 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
       if (!(fl & F32) || geos == nullptr || geos[i] == nullptr || N[i] % tn) return -1;  // (N = taps x C, host-side)
       aux = geos[i];
     }
-    if (fl & BNX) {  // aux[i]: the BatchNorm's fp32 [scale[N], shift[N]]
+    if (fl & BNX) {  // aux[i]: the BatchNorm's fp32 [scale[N], shift[N]]; 128 x 128 or narrow tiles only
       if (!(fl & F32) || (fl & CONV) || geos == nullptr || geos[i] == nullptr || (uintptr_t)geos[i] % 16) return -1;
+      if (!(fl & (TILE128 | NARROW_M | NARROW_N))) return -1;
       aux = geos[i];
     }
     const int S = (T[i] + chunk[i] - 1) / chunk[i];
@@ -1223,7 +1244,7 @@ int mifx_gemm8_tn_grouped(int n, const void* const* A, const void* const* B, voi
   const int cus = 256, rem = items % cus;
   g.n_big = (uniform256 && items > cus && rem > 0 && rem <= cus / 4) ? items - rem : items;
   const int grid = g.n_big + 4 * (items - g.n_big);
-  constexpr int LDS = lds_bytes<256, 256, EPI_NONE>();
+  constexpr int LDS = lds_bytes<256, 256, EPI_NONE>() + 2 * 256 * 4 + NT * 16;  // + BNX column table, dup scratch
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm8_tn_grouped, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);

@@ -30,7 +30,7 @@ def _fns():
                          [I32, VP, I64, I32, VP, I32, I32, VP, VP, F32, F32, VP, VP, I32, VP, VP, VP, VP]),
         "tiles_ws": sig(lib, "mifx_bn_tiles_ws", [I32, I32]),
         "bwd_tiles": sig(lib, "mifx_bn_relu_bwd_tiles",
-                         [I32, VP, VP, VP, I64, I32, VP, VP, I32, VP, VP, I32, VP, VP, VP, VP, VP]),
+                         [I32, VP, VP, VP, I64, I32, VP, VP, I32, VP, VP, I32, VP, VP, VP, VP, VP, VP]),
     }
 
 
@@ -121,8 +121,9 @@ def _take_tiles(ctx, dy):
     return part
 
 
-def _bwd_tiles(dy, x, w32, stats, dres, part):
-    """Backward of relu(bn(x)) from the per-tile sums the producing GEMM reduced: finalize + apply only."""
+def _bwd_tiles(dy, x, w32, stats, dres, part, act=None):
+    """Backward of relu(bn(x)) from the per-tile sums the producing GEMM reduced: finalize + apply only. act: also
+    write the forward's activation relu(bn(x)) there (same layout as x)."""
     if dres is not None:
         if dres.dim() == 4 and not dres.is_contiguous(memory_format=torch.channels_last):
             dres = dres.contiguous(memory_format=torch.channels_last)
@@ -135,7 +136,8 @@ def _bwd_tiles(dy, x, w32, stats, dres, part):
     dx = torch.empty_like(x)
     check(_fns()["bwd_tiles"](_dt(x), ptr(dv), ptr(v), ptr(_nhwc_view(dres) if dres is not None else None), M, C,
                               ptr(w32), ptr(stats), 1, ptr(part[0]), ptr(part[1]), T, ptr(kbuf), ptr(dx), ptr(dgb[0]),
-                              ptr(dgb[1]), stream_handle(x.device)), "mifx_bn_relu_bwd_tiles")
+                              ptr(dgb[1]), ptr(_nhwc_view(act) if act is not None else None),
+                              stream_handle(x.device)), "mifx_bn_relu_bwd_tiles")
     return dx, dgb
 
 

@@ -256,11 +256,16 @@ def proj_pair(x: torch.Tensor, w_sc: torch.Tensor, stride: int, w1: torch.Tensor
     return _ProjPair.apply(x, w_sc, w1, int(stride), bn)
 
 
-# BatchNorm + ReLU folded into the consumer 1x1 convolution: opt-in (MIFX_BN_FOLD=1). Measured slower in the ResNet-50
-# step (11,300 vs 12,159 img/s, profiles/resnet_bn_fold_ab_r5.txt): the per-lane operand transform is repeated by the
-# 4 waves sharing each A row and costs more MFMA-pipe time (128 x 128 EPI 6: 193 vs 113 us per call) than the apply
-# pass it removes (~6.3 TB/s streaming)
+# BatchNorm + ReLU folded into the consumer 1x1 convolution: opt-in (MIFX_BN_FOLD=1). Same-box ResNet-50 A/B
+# (profiles/resnet_bn_fold_ab_r5.txt): 11,954 vs 12,055 img/s without -- the forward apply passes it removes (~1.0 ms)
+# are paid back by the re-derived activation write in the backward (~0.46 ms) and the AX GEMMs' smaller tiles (the
+# 256 x 256 AX build spills registers: 128 x 128 runs conv3, +0.2 ms)
 BN_FOLD = os.environ.get("MIFX_BN_FOLD", "0") == "1"
+
+
+# weight gradient of a folded convolution from the grouped TN kernel's BatchNorm operand transform (MIFX_BNX_DW=1) or
+# from the activation the BatchNorm backward re-derives (default)
+_BNX_DW = os.environ.get("MIFX_BNX_DW", "0") == "1"
 
 
 class _BNConv1x1(torch.autograd.Function):
@@ -304,21 +309,29 @@ class _BNConv1x1(torch.autograd.Function):
         dyc = dout.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dyc)
         x2 = _rows(x)
-        dw = None
-        if ctx.needs_input_grad[8]:
-            dw = hg.defer_weight_grad_f32(dy2, x2, ctx.w, bnx=stats[2:4])
-            if dw is None:  # materialize the activation for the library's weight gradient
-                native_stats.count("conv1x1_dW", False)
-                act = torch.empty_like(x)
-                check(bn_relu._fns()["apply"](1, ptr(x2), x2.shape[0], cin, ptr(stats[2]), ptr(stats[3]), 1,
-                                              ptr(_rows(act)), stream_handle(x.device)), "mifx_bn_relu_apply")
-                dw = torch.ops.aten.convolution_backward(dyc, act, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0],
-                                                         [1, 1], False, [0, 0], 1, [False, True, False])[1]
-                dw = dw.to(ctx.w.dtype)
         wt = ctx.wt if ctx.wt is not None else hg.transpose(wb)
         dact = torch.empty(n, cin, h, w_, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
         _, bpart = hg.gemm8_nt(dy2, wt, x2, 8, cfg=hg.gemm8_pick(dy2.shape[0], cin, cout), z=stats, out=_rows(dact))
-        dx, dgb = bn_relu._bwd_tiles(dact, x, w32, stats, dalias, bpart)
+        # the BatchNorm backward's apply pass reads x anyway: it also re-derives the activation for the weight
+        # gradient (one extra write; the grouped TN kernel with the operand transform measured slower)
+        want_dw = ctx.needs_input_grad[8]
+        act = torch.empty_like(x) if want_dw and not _BNX_DW else None
+        dx, dgb = bn_relu._bwd_tiles(dact, x, w32, stats, dalias, bpart, act=act)
+        dw = None
+        if want_dw:
+            if act is not None:
+                dw = hg.defer_weight_grad_f32(dy2, _rows(act), ctx.w)
+            else:
+                dw = hg.defer_weight_grad_f32(dy2, x2, ctx.w, bnx=stats[2:4])
+            if dw is None:
+                native_stats.count("conv1x1_dW", False)
+                if act is None:
+                    act = torch.empty_like(x)
+                    check(bn_relu._fns()["apply"](1, ptr(x2), x2.shape[0], cin, ptr(stats[2]), ptr(stats[3]), 1,
+                                                  ptr(_rows(act)), stream_handle(x.device)), "mifx_bn_relu_apply")
+                dw = torch.ops.aten.convolution_backward(dyc, act, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0],
+                                                         [1, 1], False, [0, 0], 1, [False, True, False])[1]
+                dw = dw.to(ctx.w.dtype)
         return (dx, None, dgb[0].to(ctx.wdtype), dgb[1].to(ctx.wdtype), None, None, None, None, dw,
                 dyc if ctx.has_r else None)
 

@@ -780,6 +780,8 @@ def gemm8_tn_grouped(problems, chunk: int = 4096, tile128: bool | None = None, a
             and N % 256 == 0
         if nar_n or nar_m:
             t128 = False
+        elif bnx is not None:  # (the kernel builds BatchNorm-operand problems on 128 x 128 or narrow tiles only)
+            t128 = True
         ck = pchunk if f32 else T
         Ms.append(M)
         Ns.append(N)

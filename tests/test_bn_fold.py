@@ -51,7 +51,7 @@ def test_nt_bnx_equals_stored_activation(cfg, epi):
 
 @pytest.mark.parametrize("M,N,T", [(256, 256, 4096), (64, 256, 2048), (256, 64, 2048), (128, 384, 2048)])
 def test_grouped_bnx_equals_stored_activation(M, N, T):
-    """dW = dY^T relu(X scale + shift) in the grouped split-K launch (256 x 256, narrow-M, narrow-N, 128 x 128 tiles)
+    """dW = dY^T relu(X scale + shift) in the grouped split-K launch (128 x 128, narrow-M, narrow-N tiles)
     equals the product with the stored activation, bit for bit, and the fp32 reference."""
     from mifx.ops import gemm as hg
 
@@ -68,12 +68,16 @@ def test_grouped_bnx_equals_stored_activation(M, N, T):
     torch.testing.assert_close(c1, dy.float().t() @ act.float(), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("defer", [False, True])
+@pytest.mark.parametrize("defer,bnx_dw", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("res", [False, True])
-def test_bn_conv1x1_matches_bn_then_conv(defer, res):
+def test_bn_conv1x1_matches_bn_then_conv(defer, bnx_dw, res, monkeypatch):
     """bn_conv1x1 (activation never stored) vs BatchNormReLU2d + conv in fp32: output, output statistics, running
     statistics and the gradients of x (incl. an alias consumer), gamma, beta, w and the residual."""
+    from mifx.ops import conv1x1 as c1
     from mifx.ops import gemm as hg
+
+    monkeypatch.setattr(c1, "BN_FOLD", True)
+    monkeypatch.setattr(c1, "_BNX_DW", bnx_dw)  # dW from the grouped operand transform / the re-derived activation
     from mifx.ops.bn_relu import BatchNormReLU2d
     from mifx.ops.conv1x1 import bn_conv1x1, bn_conv_eligible
 
