@@ -294,7 +294,7 @@ class BatchNormReLU2d(nn.BatchNorm2d):
 def defer_batch_counts(model: nn.Module) -> torch.Tensor | None:
     """Re-home every BatchNormReLU2d's `num_batches_tracked` as one element of a single int64 tensor and stop the
     per-forward increments: the caller advances them all with one `add_(1)` per training forward -- one kernel instead
-    of one per BatchNorm (49 in ResNet-50: ~0.2 ms of a B=256 step, profiles/resnet_steady_r4b.md). Call after the
+    of one per BatchNorm (49 in ResNet-50: ~0.2 ms of a B=256 step, profiles/archive/resnet_steady_r4b.md). Call after the
     model reached its device. Returns the tensor (None without such BatchNorms)."""
     bns = [m for m in model.modules() if isinstance(m, BatchNormReLU2d) and m.track_running_stats]
     if not bns:

@@ -4,7 +4,7 @@ epilogues.
 
 ResNet-50 v2's bottleneck conv2 (3x3, stride 1, or 2 in the first block of stages 2-4) sits between BN1 and BN2. On
 MIOpen its forward, input gradient and weight gradient ran at ~13 % of the MFMA peak (the largest block of the step,
-profiles/resnet_steady_r5g.md) and BN2 / BN1 each needed a reduction pass. Here:
+profiles/archive/resnet_steady_r5g.md) and BN2 / BN1 each needed a reduction pass. Here:
 
 * forward: Y[Nb OH OW, Cout] = gathered X . W[Cout, 9 C]^T -- every 64-deep K-tile is one tap and a 64-channel slice,
   each gathered row one input pixel (or the zero page outside the image); the epilogue reduces BN2's per-tile

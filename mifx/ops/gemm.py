@@ -37,7 +37,7 @@ def _fns():
 class TransposeCache:
     """Transposed copies of a model's projection weights, refreshed in ONE launch per step (csrc/gemm.hip
     transpose_batch), for the dX GEMMs that run as NT products against W^T. Refreshing per step in one kernel replaces
-    a transpose launch per weight in the backward (47 per BERT-base step, ~200 us: profiles/bert_steady_r4b.md). The
+    a transpose launch per weight in the backward (47 per BERT-base step, ~200 us: profiles/archive/bert_steady_r4b.md). The
     owner (BertTrainer) calls refresh() right before every backward -- from the weights as they are then, so a weight
     change of any kind between steps (update, load_state_dict) is seen -- and runs the backward inside
     `use_transposes(cache)`."""

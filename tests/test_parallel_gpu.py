@@ -146,7 +146,7 @@ def test_resnet_captured_step_matches_eager():
     """ResNetTrainer's hipGraph step (graph A: input kernel + forward + backward with device-side step, indices and
     learning rate; SGD captured with the learning rate read from a device tensor) against ONE eager step from the
     same state: the same loss and the same parameter update up to the update's rounding (the check is per step:
-    trajectories of this tiny problem are chaotic, profiles/resnet_graph_diag_r4.jsonl). A checkpoint restore drops the graphs and re-captures them after fresh eager steps."""
+    trajectories of this tiny problem are chaotic, profiles/archive/resnet_graph_diag_r4.jsonl). A checkpoint restore drops the graphs and re-captures them after fresh eager steps."""
     import tempfile as _tf
 
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
@@ -158,7 +158,7 @@ def test_resnet_captured_step_matches_eager():
                            graph=graph, graph_warmup=2)
         torch.backends.cudnn.benchmark = False
         # MIOpen's default bf16 solvers are not run-to-run reproducible; with its deterministic ones the captured and
-        # the eager update agree to ~2e-7 (profiles/resnet_graph_diag2_r4.jsonl)
+        # the eager update agree to ~2e-7 (profiles/archive/resnet_graph_diag2_r4.jsonl)
         torch.backends.cudnn.deterministic = True
         return tr
 

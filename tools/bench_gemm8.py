@@ -4,7 +4,7 @@ input-gradient products) and ResNet-50's 1x1-convolution GEMMs at batch 256. Eac
 kernel against an fp32 reference, then times 50 back-to-back calls after 10 warmups (CUDA events). One JSON line per
 measurement.
 
-usage: python tools/bench_gemm8.py [--shapes calib,bert,dx,resnet] [--cfg i,j]"""
+usage: python tools/bench_gemm8.py [--shapes calib,bert,bertfwd,bertdw,dx,resnet] [--cfg i,j]"""
 import argparse
 import json
 import os
@@ -41,6 +41,52 @@ def timeit(fn, iters=50):
     return e0.elapsed_time(e1) * 1e3 / iters
 
 
+def bert_fwd():
+    """FFN-in (bias + GELU, the pre-activation kept for backward), QKV (+ bias) and attention-out (+ bias): the
+    current routes (hipBLASLt F.linear + the bias-GELU kernel; csrc/gemm.hip for attention-out) vs csrc/gemm8.hip
+    epilogues EPI 2 / EPI 1 per configuration."""
+    from mifx.ops import fused_bert as fb
+    from mifx.ops._lib import check, ptr, stream_handle
+
+    cfgs = gemm.gemm8_configs()
+    for name, M, N, K in [("ffn_in", 4096, 3072, 768), ("qkv", 4096, 2304, 768), ("attn_out", 4096, 768, 768)]:
+        x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device="cuda") * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+        b = (torch.rand(N, device="cuda") * 0.2 - 0.1).to(torch.bfloat16)
+        flop = 2.0 * M * N * K
+        rows = []
+        if name == "ffn_in":
+            def cur():
+                z = F.linear(x, w)
+                y1 = torch.empty_like(z)
+                check(fb._fns()["gelu"](1, 1, 1, None, ptr(z), ptr(b), M, N, ptr(y1), None, None,
+                                        stream_handle(x.device)), "gelu")
+                return y1, z
+            rows.append(("hipblaslt + bias_gelu kernel", cur))
+            ref_y, ref_z = cur()
+            epi = 2
+        else:
+            rows.append(("hipblaslt F.linear(bias)", lambda: F.linear(x, w, b)))
+            if gemm.preferred(x, w):
+                rows.append(("gemm.hip tuned", lambda: gemm.gemm_nt(x, w, b, 1)))
+            ref_y, ref_z = F.linear(x, w, b), None
+            epi = 1
+        for i, (bm, bn) in enumerate(cfgs):
+            if M % bm or N % bn:
+                continue
+            y, aux = gemm.gemm8_nt(x, w, b, epi, cfg=i)
+            err = ((y.float() - ref_y.float()).abs().max() / ref_y.float().abs().max()).item()
+            if err > 2e-2 or (ref_z is not None and not torch.equal(aux, ref_z) and
+                              ((aux.float() - ref_z.float()).abs().max() / ref_z.float().abs().max()).item() > 2e-2):
+                print(json.dumps({"gemm": name, "cfg": i, "ERROR_rel": err}), flush=True)
+                continue
+            rows.append((f"gemm8 cfg{i} {bm}x{bn} epi{epi}", lambda i=i: gemm.gemm8_nt(x, w, b, epi, cfg=i)))
+        for impl, fn in rows:
+            us = timeit(fn)
+            print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "impl": impl, "us": round(us, 2),
+                              "tflops": round(flop / us * 1e-6, 1)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="calib,bert")
@@ -53,6 +99,9 @@ def main():
     for group in a.shapes.split(","):
         if group == "bertdw":  # a BERT-base step's 48 weight gradients: one grouped launch vs 48 TN launches
             bert_dw()
+            continue
+        if group == "bertfwd":  # the forward as routed in the step: with bias / bias + GELU, vs the current routes
+            bert_fwd()
             continue
         for name, M, N, K in SHAPES[group]:
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)

@@ -1,5 +1,5 @@
 """The hand-written BERT-base GEMMs at their tuned shapes (4096 tokens), each launched `--reps` times, for a
-rocprofv3 --pmc pass (tools/gpu_batches/gpu_r4_step17.sh -> tools/pmc_summary.py): forward NT with the bias(+GELU) epilogue,
+rocprofv3 --pmc pass (a round-4 GPU batch -> tools/pmc_summary.py): forward NT with the bias(+GELU) epilogue,
 input-gradient NT against the transposed weight, weight-gradient TN with its split partials."""
 import argparse
 import os
