@@ -22,6 +22,7 @@
 // on how heads are split over tensor-parallel ranks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "counter_rng.h"
 
@@ -114,20 +115,25 @@ __device__ __forceinline__ uint32_t keep_bits(const Drop& dp, uint64_t key, uint
   return mifx_rng::keep4(key, (row_base + 16 * kt + 4 * h) >> 2, dp.thr);
 }
 
-template <int S>
-__global__ __launch_bounds__(64 * (S / 16)) void attn_fwd(const bf16* __restrict__ qkv, const float* __restrict__ kbias,
-                                                         float scale, Drop dp, int H, int h0, int Htot,
-                                                         bf16* __restrict__ out, float* __restrict__ lse_out) {
-  constexpr int NTHR = 64 * (S / 16), KT = S / 16, KS = S / 32;
+// QS: query split -- QS workgroups per (batch, head), each with S / 16 / QS waves over its S / QS queries (the K / V
+// images loaded by each): B H QS workgroups, so BERT-base's 384 (batch, head) pairs do not leave a half-empty second
+// wave on 256 CUs
+template <int S, int QS = 1>
+__global__ __launch_bounds__(64 * (S / 16) / QS) void attn_fwd(const bf16* __restrict__ qkv,
+                                                              const float* __restrict__ kbias, float scale, Drop dp,
+                                                              int H, int h0, int Htot, bf16* __restrict__ out,
+                                                              float* __restrict__ lse_out) {
+  constexpr int NTHR = 64 * (S / 16) / QS, KT = S / 16, KS = S / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[S * LD];
   __shared__ __attribute__((aligned(16))) bf16 Vs[S * LD];
-  const int b = blockIdx.x / H, hh = blockIdx.x % H;
+  const int bh = blockIdx.x / QS, qpart = blockIdx.x % QS;
+  const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
   const size_t tok = (size_t)3 * H * D;
   const bf16* base = qkv + (size_t)b * S * tok;
   load_rows<S, NTHR>(Ks, base + (size_t)(H + hh) * D, tok);
   load_rows<S, NTHR>(Vs, base + (size_t)(2 * H + hh) * D, tok);
-  const int qi = 16 * w + r;
+  const int qi = qpart * (S / QS) + 16 * w + r;
   v8bf qf[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const v8bf*)(base + (size_t)qi * tok + (size_t)hh * D + 32 * ks + 8 * h);
@@ -622,10 +628,25 @@ int mifx_attn_fwd(const void* qkv, const float* kbias, int B, int S, int H, int 
     }
     hipLaunchKernelGGL(attn_fwd_long, dim3(B * H * ((S + LQB - 1) / LQB)), dim3(LNT), long_lds(S), st,
                        (const bf16*)qkv, kbias, S, scale, dp, H, h0, Htot, (bf16*)out, lse);
-  } else if (S == 128)
-    hipLaunchKernelGGL(attn_fwd<128>, grid, dim3(512), 0, st, (const bf16*)qkv, kbias, scale, dp, H, h0, Htot,
-                       (bf16*)out, lse);
-  else
+  } else if (S == 128) {
+    // MIFX_ATTN_QSPLIT: 1 (default), 2 or 4 workgroups per (batch, head). BERT-base step: 6,206 / 6,179 seq/s at 1,
+    // 6,190 / 6,184 at 2, 5,992 / 6,004 at 4 (profiles/bert_attn_qsplit_ab_r5.txt): the kernel is latency-bound per
+    // workgroup, not by the 1.5-wave quantisation of 384 workgroups
+    static const int qs = [] {
+      const char* e = getenv("MIFX_ATTN_QSPLIT");
+      const int v = e ? atoi(e) : 1;
+      return v == 2 || v == 4 ? v : 1;
+    }();
+    if (qs == 1)
+      hipLaunchKernelGGL((attn_fwd<128, 1>), grid, dim3(512), 0, st, (const bf16*)qkv, kbias, scale, dp, H, h0, Htot,
+                         (bf16*)out, lse);
+    else if (qs == 2)
+      hipLaunchKernelGGL((attn_fwd<128, 2>), dim3(B * H * 2), dim3(256), 0, st, (const bf16*)qkv, kbias, scale, dp, H,
+                         h0, Htot, (bf16*)out, lse);
+    else
+      hipLaunchKernelGGL((attn_fwd<128, 4>), dim3(B * H * 4), dim3(128), 0, st, (const bf16*)qkv, kbias, scale, dp, H,
+                         h0, Htot, (bf16*)out, lse);
+  } else
     hipLaunchKernelGGL(attn_fwd<64>, grid, dim3(256), 0, st, (const bf16*)qkv, kbias, scale, dp, H, h0, Htot,
                        (bf16*)out, lse);
   return (int)hipGetLastError();
