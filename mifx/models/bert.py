@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from ..ops import fused_bert as fb
 from ..ops import gemm as hg
 from ..parallel.tensor_parallel import (ColumnParallelLinear, RowParallelLinear, TPGroup, VocabParallelEmbedding,
-                                        copy_to_tp, head_partition, reduce_from_tp, split_sizes)
+                                        copy_to_tp, head_partition, overlap_ok, reduce_from_tp, split_sizes)
 
 
 @dataclass
@@ -127,10 +127,19 @@ class BertLayer(nn.Module):
             amask = None if mask is None else mask[:, None, None, :].to(q.dtype)
             ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, dropout_p=adrop)
             ctx = ctx.transpose(1, 2).reshape(B, S, h * d)
-        a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp) if hip else self.attn_out(ctx, add_bias=False)
+        tokens = B * S
+        if hip and overlap_ok(self.tp, tokens, c.hidden):  # row-parallel GEMM + all-reduce overlapped in token chunks
+            a = hg.linear(ctx, self.attn_out.weight, tp=self.tp)
+        elif hip:
+            a = reduce_from_tp(hg.linear(ctx, self.attn_out.weight), self.tp)
+        else:
+            a = self.attn_out(ctx, add_bias=False)
         x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
                                           rng, site, slot=slot_a)
-        if hip:  # FFN-in + GELU + FFN-out as one autograd node (the dH GEMM and the GELU backward fused)
+        if hip and overlap_ok(self.tp, tokens, c.hidden):  # (FFN-out all-reduced inside, overlapped)
+            o = hg.ffn(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias, self.ffn_out.weight, slot=slot_f,
+                       tp=self.tp)
+        elif hip:  # FFN-in + GELU + FFN-out as one autograd node (the dH GEMM and the GELU backward fused)
             o = reduce_from_tp(hg.ffn(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias,
                                       self.ffn_out.weight, slot=slot_f), self.tp)
         else:

@@ -510,10 +510,17 @@ def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tens
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, hip_fwd=True, slot=None):
+    def forward(ctx, x, w, bias, hip_fwd=True, slot=None, tp=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        if hip_fwd:
+        if tp is not None:  # row-parallel: the product all-reduced over the TP group, overlapped chunk by chunk
+            from ..parallel.tensor_parallel import gemm_allreduce_overlapped
+
+            y = gemm_allreduce_overlapped(x2, lambda xc: gemm_nt(xc, w)[0] if hip_fwd else F.linear(xc, w),
+                                          w.shape[0], tp)
+            if bias is not None:
+                y = y + bias.to(y.dtype)
+        elif hip_fwd:
             y, _ = gemm_nt(x2, w, bias, 1 if bias is not None else 0)
         else:
             y = F.linear(x2, w, bias)
@@ -534,7 +541,7 @@ class _Linear(torch.autograd.Function):
             from .fused_bert import col_sum
 
             db = col_sum(dy2, ctx.bdtype if ctx.bdtype in (torch.float32, torch.bfloat16) else torch.float32)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 class _LinearBiasGelu(torch.autograd.Function):
@@ -568,15 +575,19 @@ class _LinearBiasGelu(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, force: bool = False,
-           slot: GradSlot | None = None) -> torch.Tensor:
+           slot: GradSlot | None = None, tp=None) -> torch.Tensor:
     """F.linear with the forward on the hand-written kernel (bias fused) where it is preferred (or, force=True,
     wherever it tiles the shape), and the weight gradient on the hand-written TN kernel where that is preferred.
-    slot: the input gradient also carries the residual gradient parked there (GradSlot)."""
+    slot: the input gradient also carries the residual gradient parked there (GradSlot). tp: a row-parallel
+    projection whose product is returned ALL-REDUCED over the group, the reduction overlapped with the GEMM in token
+    chunks (only where mifx.parallel.tensor_parallel.overlap_ok; elsewhere the caller applies reduce_from_tp)."""
     fwd = eligible(x, w) if force else preferred(x, w)
     if x.is_cuda:
         native_stats.count("gemm_fwd", fwd)
     bwd = (x.is_cuda and x.dtype == torch.bfloat16 and w.requires_grad and torch.is_grad_enabled()
            and tn_preferred(w.shape[0], w.shape[1], x.numel() // x.shape[-1]))
+    if tp is not None:
+        return _Linear.apply(x, w, bias, fwd, slot, tp)
     if fwd or bwd or slot is not None:
         return _Linear.apply(x, w, bias, fwd, slot)
     return F.linear(x, w, bias)
@@ -1011,7 +1022,7 @@ class _FFN(torch.autograd.Function):
     """out = GELU(x W1^T + b1) W2^T (no FFN-out bias: the caller fuses it into the next add + LayerNorm)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, slot=None):
+    def forward(ctx, x, w1, b1, w2, slot=None, tp=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         from .fused_bert import _fns as fb_fns, _dt, _param
@@ -1028,7 +1039,13 @@ class _FFN(torch.autograd.Function):
         native_stats.count("gemm_fwd_bias_gelu", preferred(x2, w1))
         fwd2 = preferred(y1, w2)
         native_stats.count("gemm_fwd", fwd2)
-        out = gemm_nt(y1, w2)[0] if fwd2 else F.linear(y1, w2)
+        if tp is not None:  # row-parallel FFN-out: all-reduced here, overlapped with its GEMM chunk by chunk
+            from ..parallel.tensor_parallel import gemm_allreduce_overlapped
+
+            out = gemm_allreduce_overlapped(y1, lambda yc: gemm_nt(yc, w2)[0] if fwd2 else F.linear(yc, w2),
+                                            w2.shape[0], tp)
+        else:
+            out = gemm_nt(y1, w2)[0] if fwd2 else F.linear(y1, w2)
         ctx.save_for_backward(x2, w1, b1, z, y1, w2)
         ctx.slot = slot
         return out.view(*shp[:-1], w2.shape[0])
@@ -1057,13 +1074,14 @@ class _FFN(torch.autograd.Function):
                                    ptr(dz), ptr(part), ptr(db1), stream_handle(z.device)), "mifx_bert_bias_gelu")
         dw1 = _dw(dz, x2, w1)
         dx = _dx(dz, w1, ctx.slot).view(*dout.shape[:-1], w1.shape[1]) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1.to(b1.dtype), dw2, None
+        return dx, dw1, db1.to(b1.dtype), dw2, None, None
 
 
 def ffn(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
-        slot: GradSlot | None = None) -> torch.Tensor:
+        slot: GradSlot | None = None, tp=None) -> torch.Tensor:
     """GELU(x W1^T + b1) W2^T as one autograd node on the GPU (bf16): the FFN-out input gradient and the bias-GELU
-    backward fused into one GEMM where tuned (GELU_BWD_TUNED); elsewhere the two-node composition."""
+    backward fused into one GEMM where tuned (GELU_BWD_TUNED); elsewhere the two-node composition. tp: FFN-out is
+    row-parallel and its product comes back all-reduced (overlapped chunk by chunk)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16:
-        return _FFN.apply(x, w1, b1, w2, slot)
+        return _FFN.apply(x, w1, b1, w2, slot, tp)
     return linear(linear_bias_gelu(x, w1, b1, slot=slot), w2)

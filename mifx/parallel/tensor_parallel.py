@@ -19,12 +19,17 @@ BERT-base fine-tune at TP=8, so this module provides the standard column/row spl
 
 Two all-reduces per transformer block (after attention-out and FFN-out), each of
 [tokens, hidden] activations — on MI355X the 8-GPU xGMI ring is ~7 links x ~150 GB/s, so a
-[32*128, 768] bf16 block reduction (6.3 MB) is ~10-15 us.
+[32*128, 768] bf16 block reduction (6.3 MB) is ~10-15 us. On the peer-memory path those two run OVERLAPPED with their
+row-parallel GEMMs: `gemm_allreduce_overlapped` computes the GEMM in token chunks and reduces chunk i on a side stream
+while chunk i+1 computes (mifx.ops.gemm.linear / ffn with tp=...; tools/tp_kernel_table.py reports how much of the
+all-reduce kernels' time runs concurrently with GEMMs).
 
 `TPGroup.enable_ipc(max_elems, device)` moves every bf16 TP all-reduce onto the two-shot peer-memory kernels of
 mifx.parallel.tp_ipc (no host collective: the TP step captures into a hipGraph); otherwise torch.distributed's
 all-reduce runs in place on the fresh GEMM output / gradient (no defensive copies either way)."""
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -77,6 +82,45 @@ def _all_reduce(x: torch.Tensor, tp: TPGroup) -> torch.Tensor:
         return tp.ipc.all_reduce(x)
     dist.all_reduce(x, group=tp.group)
     return x
+
+
+# Row-parallel GEMM + all-reduce overlap (TP > 1 on the peer-memory kernels): the GEMM runs in token chunks on the
+# compute stream and each chunk's all-reduce on a side stream as soon as the chunk is written, so chunk i's exchange
+# overlaps chunk i+1's GEMM; the compute stream joins the side stream before the reduced activation is used (no other
+# all-reduce of the group can then be in flight: the kernels' epochs stay in issue order). Graph-capturable (event
+# fork / join). MIFX_TP_OVERLAP_CHUNKS: chunks per GEMM (default 4; 1 = the plain GEMM-then-all-reduce).
+_OVERLAP_CHUNKS = int(os.environ.get("MIFX_TP_OVERLAP_CHUNKS", "4"))
+_SIDE: dict = {}
+
+
+def overlap_ok(tp: TPGroup | None, M: int, N: int) -> bool:
+    """The row-parallel product [M, N] can be reduced chunk-by-chunk on the peer-memory kernels."""
+    return (tp is not None and tp.size > 1 and tp.ipc is not None and _OVERLAP_CHUNKS > 1 and M % (64 * _OVERLAP_CHUNKS) == 0
+            and (M // _OVERLAP_CHUNKS) * N <= tp.ipc.npad and N % 4 == 0)
+
+
+def gemm_allreduce_overlapped(x2: torch.Tensor, gemm, N: int, tp: TPGroup) -> torch.Tensor:
+    """all_reduce(gemm(x2)) over the TP group, gemm: [m, K] -> [m, N] bf16 on the current stream, applied to token
+    chunks whose all-reduces run on a side stream (see above). Returns the reduced [M, N] (a new tensor)."""
+    M = x2.shape[0]
+    dev = x2.device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(dev)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    r0 = 0
+    for r in split_sizes(M, _OVERLAP_CHUNKS, 64):
+        part = gemm(x2[r0:r0 + r])
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            tp.ipc.all_reduce(part, out=y[r0:r0 + r])
+        part.record_stream(side)
+        r0 += r
+    main.wait_stream(side)
+    return y
 
 
 class _CopyToTP(torch.autograd.Function):

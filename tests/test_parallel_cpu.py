@@ -166,3 +166,33 @@ def test_ddp_buckets_launch_in_order_whatever_completes_first():
 def test_ddp_ipc_exchange_needs_cuda():
     with pytest.raises(ValueError):
         DataParallel(_Net(), exchange="nope")
+
+
+def test_tp_overlap_gate_needs_ipc_and_whole_chunks():
+    """The overlapped row-parallel reduction applies only with the peer-memory all-reduce, TP > 1, token counts that
+    split into whole 64-row chunks and chunks that fit the IPC buffer."""
+    from mifx.parallel import tensor_parallel as tpm
+
+    class FakeIpc:
+        npad = 4096 * 768
+
+    class FakeTP:
+        size, ipc = 2, FakeIpc()
+
+    saved = tpm._OVERLAP_CHUNKS
+    try:
+        tpm._OVERLAP_CHUNKS = 4
+        assert tpm.overlap_ok(FakeTP(), 4096, 768)
+        assert not tpm.overlap_ok(FakeTP(), 4096 + 64, 768)  # not whole 64-row chunks
+        assert not tpm.overlap_ok(None, 4096, 768)
+        t1 = FakeTP()
+        t1.size = 1
+        assert not tpm.overlap_ok(t1, 4096, 768)
+        t2 = FakeTP()
+        t2.ipc = None
+        assert not tpm.overlap_ok(t2, 4096, 768)
+        tpm._OVERLAP_CHUNKS = 1
+        assert not tpm.overlap_ok(FakeTP(), 4096, 768)
+        assert [sum(tpm.split_sizes(4096, 4, 64))] == [4096] and all(r % 64 == 0 for r in tpm.split_sizes(4096, 4, 64))
+    finally:
+        tpm._OVERLAP_CHUNKS = saved

@@ -256,3 +256,44 @@ def test_ipc_allreduce_peer_never_arrives_sets_error_and_poisons():
         mp.start_processes(_timeout_worker, args=(2, _port(), out), nprocs=2, start_method="spawn")
         r0 = torch.load(f"{out}.0", weights_only=True)
     assert r0 == {"nan_y": True, "nan_z": True, "raised": True}, r0
+
+
+def _overlap_worker(rank, world, port, out):
+    from mifx.models.bert import BertConfig
+    from mifx.parallel import tensor_parallel as tpm
+    from mifx.trainer.bert_trainer import BertTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        res = {}
+        for chunks in (1, 4):
+            tpm._OVERLAP_CHUNKS = chunks
+            tp = tpm.TPGroup()
+            torch.manual_seed(0)
+            tr = BertTrainer(BertConfig(layers=2, dropout=0.1), 4, 128, dev, tp, graph=False, tp_ipc=True)
+            assert tpm.overlap_ok(tp, 4 * 128, 768) == (chunks > 1)
+            res[chunks] = [float(tr.step()) for _ in range(4)]
+            torch.cuda.synchronize(dev)
+            tp.check()
+            dist.barrier()
+            tp.disable_ipc()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bert_tp_overlapped_row_parallel_reduce_matches_plain():
+    """Row-parallel GEMMs in token chunks whose peer-memory all-reduces run on a side stream (overlapped with the
+    next chunk's GEMM) give the losses of the plain GEMM-then-all-reduce step (bf16 tolerance: the chunked GEMMs may
+    take other library kernels), identical on both TP ranks."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "ov")
+        mp.start_processes(_overlap_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for r in range(world):
+        a, b = res[r][1], res[r][4]
+        assert all(abs(x - y) <= 2e-2 * max(1.0, abs(x)) for x, y in zip(a, b)), (r, a, b)
+    assert res[0][4] == res[1][4]

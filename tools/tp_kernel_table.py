@@ -60,12 +60,14 @@ def worker(rank, world, port, a, out):
                         rows.append((t, e.count, e.key))
                 rows.sort(reverse=True)
                 total = sum(r[0] for r in rows)
+                ov = overlap_summary(prof)
                 lines += [f"# TP={world} BERT step kernels (rank 0, eager, {a.active} steps; ranks share one GPU)", "",
                           f"batch {a.batch} seq {a.seq} layers {a.layers}; rank-0 GPU time per step "
                           f"{total / a.active / 1e3:.2f} ms", "",
                           "| kernel | calls/step | µs/step | % |", "|---|---|---|---|"]
                 for t, c, k in rows[:a.top]:
                     lines.append(f"| `{k[:100]}` | {c / a.active:g} | {t / a.active:.1f} | {100 * t / total:.1f} |")
+                lines += ["", "Streams (rank 0): " + ov]
             elif not graph:
                 for _ in range(a.active):
                     tr.step()
@@ -89,6 +91,47 @@ def worker(rank, world, port, a, out):
                 f.write("\n".join(lines) + "\n")
     finally:
         dist.destroy_process_group()
+
+
+def overlap_summary(prof) -> str:
+    """From the profiler's trace: kernels per GPU stream, and how much of the peer-memory all-reduce kernels' time
+    (tpar_*) runs concurrently with a kernel on another stream (the row-parallel GEMM chunks, MIFX_TP_OVERLAP_CHUNKS)."""
+    import json
+
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "trace.json")
+        prof.export_chrome_trace(path)
+        ev = json.load(open(path)).get("traceEvents", [])
+    ks = [e for e in ev if e.get("cat") == "kernel" and "dur" in e]
+    if not ks:
+        return "no kernel events in the trace"
+    by_stream: dict = {}
+    for e in ks:
+        by_stream.setdefault(e.get("tid"), []).append(e)
+    ar = [e for e in ks if e["name"].startswith(("tpar_", "void (anonymous namespace)::tpar", "(anonymous namespace)::tpar"))
+          or "tpar_" in e["name"]]
+    overlapped = 0.0
+    for a in ar:
+        a0, a1 = a["ts"], a["ts"] + a["dur"]
+        cover = []
+        for e in ks:
+            if e.get("tid") == a.get("tid") or "tpar_" in e["name"]:
+                continue
+            lo, hi = max(a0, e["ts"]), min(a1, e["ts"] + e["dur"])
+            if hi > lo:
+                cover.append((lo, hi))
+        cover.sort()
+        t, end = 0.0, a0
+        for lo, hi in cover:
+            lo = max(lo, end)
+            if hi > lo:
+                t += hi - lo
+                end = hi
+        overlapped += t
+    tot = sum(a["dur"] for a in ar)
+    streams = ", ".join(f"stream {k}: {len(v)} kernels" for k, v in sorted(by_stream.items(), key=lambda kv: str(kv[0])))
+    return (f"{streams}; all-reduce kernels {len(ar)}, {tot:.0f} us in total, {overlapped:.0f} us of it "
+            f"({100 * overlapped / max(tot, 1e-9):.0f} %) concurrent with kernels on another stream")
 
 
 def main():
