@@ -113,7 +113,8 @@ class BertLayer(nn.Module):
             # step) -- the first layer's input is the fp32 embedding LayerNorm output
             cdt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else self.qkv.weight.dtype
             xin = x if x.dtype == cdt or self.tp.size == 1 else x.to(cdt)
-            qkv = hg.linear(copy_to_tp(xin, self.tp), self.qkv.weight, self.qkv.bias, slot=slot_a).view(B, S, 3, h, d)
+            # (copy_to_tp folded into the projection: its input gradient is all-reduced, overlapped with its GEMM)
+            qkv = hg.linear(xin, self.qkv.weight, self.qkv.bias, slot=slot_a, tp_in=self.tp).view(B, S, 3, h, d)
         else:
             qkv = self.qkv(x).view(B, S, 3, h, d)
         if c.fused_attention:
@@ -137,11 +138,11 @@ class BertLayer(nn.Module):
         x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
                                           rng, site, slot=slot_a)
         if hip and overlap_ok(self.tp, tokens, c.hidden):  # (FFN-out all-reduced inside, overlapped)
-            o = hg.ffn(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias, self.ffn_out.weight, slot=slot_f,
-                       tp=self.tp)
+            o = hg.ffn(x, self.ffn_in.weight, self.ffn_in.bias, self.ffn_out.weight, slot=slot_f, tp=self.tp,
+                       tp_in=self.tp)
         elif hip:  # FFN-in + GELU + FFN-out as one autograd node (the dH GEMM and the GELU backward fused)
-            o = reduce_from_tp(hg.ffn(copy_to_tp(x, self.tp), self.ffn_in.weight, self.ffn_in.bias,
-                                      self.ffn_out.weight, slot=slot_f), self.tp)
+            o = reduce_from_tp(hg.ffn(x, self.ffn_in.weight, self.ffn_in.bias, self.ffn_out.weight, slot=slot_f,
+                                      tp_in=self.tp), self.tp)
         else:
             f = fb.bias_gelu(F.linear(copy_to_tp(x, self.tp), self.ffn_in.weight), self.ffn_in.bias)
             o = self.ffn_out(f, add_bias=False)

@@ -510,9 +510,10 @@ def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tens
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, hip_fwd=True, slot=None, tp=None):
+    def forward(ctx, x, w, bias, hip_fwd=True, slot=None, tp=None, tp_in=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        ctx.tp_in = tp_in
         if tp is not None:  # row-parallel: the product all-reduced over the TP group, overlapped chunk by chunk
             from ..parallel.tensor_parallel import gemm_allreduce_overlapped
 
@@ -534,14 +535,28 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype)
-        dx = _dx(dy2, w, ctx.slot).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _dx_reduced(dy2, w, ctx.slot, ctx.tp_in).view(*dy.shape[:-1], w.shape[1])
         dw = _dw(dy2.contiguous(), x2, w) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             from .fused_bert import col_sum
 
             db = col_sum(dy2, ctx.bdtype if ctx.bdtype in (torch.float32, torch.bfloat16) else torch.float32)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
+
+
+def _dx_reduced(dy2: torch.Tensor, w: torch.Tensor, slot, tp_in) -> torch.Tensor:
+    """_dx, then (column-parallel input, tp_in) its all-reduce over the TP group -- overlapped with the dX GEMM in
+    token chunks on the peer-memory path (mifx.parallel.tensor_parallel.gemm_allreduce_overlapped)."""
+    if tp_in is None:
+        return _dx(dy2, w, slot)
+    from ..parallel import tensor_parallel as tpm
+
+    if slot is None and tpm.overlap_ok(tp_in, dy2.shape[0], w.shape[1]) and dy2.dtype == torch.bfloat16:
+        return tpm.gemm_allreduce_overlapped(dy2, lambda dc: _dx(dc, w, None), w.shape[1], tp_in)
+    return tpm._all_reduce(_dx(dy2, w, slot), tp_in)
 
 
 class _LinearBiasGelu(torch.autograd.Function):
@@ -575,19 +590,21 @@ class _LinearBiasGelu(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, force: bool = False,
-           slot: GradSlot | None = None, tp=None) -> torch.Tensor:
+           slot: GradSlot | None = None, tp=None, tp_in=None) -> torch.Tensor:
     """F.linear with the forward on the hand-written kernel (bias fused) where it is preferred (or, force=True,
     wherever it tiles the shape), and the weight gradient on the hand-written TN kernel where that is preferred.
     slot: the input gradient also carries the residual gradient parked there (GradSlot). tp: a row-parallel
     projection whose product is returned ALL-REDUCED over the group, the reduction overlapped with the GEMM in token
-    chunks (only where mifx.parallel.tensor_parallel.overlap_ok; elsewhere the caller applies reduce_from_tp)."""
+    chunks (only where mifx.parallel.tensor_parallel.overlap_ok; elsewhere the caller applies reduce_from_tp). tp_in:
+    a column-parallel projection of a replicated input (Megatron's copy_to_tp folded in): the input gradient is
+    all-reduced over the group, overlapped with its GEMM in token chunks where possible."""
     fwd = eligible(x, w) if force else preferred(x, w)
     if x.is_cuda:
         native_stats.count("gemm_fwd", fwd)
     bwd = (x.is_cuda and x.dtype == torch.bfloat16 and w.requires_grad and torch.is_grad_enabled()
            and tn_preferred(w.shape[0], w.shape[1], x.numel() // x.shape[-1]))
-    if tp is not None:
-        return _Linear.apply(x, w, bias, fwd, slot, tp)
+    if tp is not None or (tp_in is not None and tp_in.size > 1):
+        return _Linear.apply(x, w, bias, fwd, slot, tp, tp_in if tp_in is not None and tp_in.size > 1 else None)
     if fwd or bwd or slot is not None:
         return _Linear.apply(x, w, bias, fwd, slot)
     return F.linear(x, w, bias)
@@ -1022,8 +1039,9 @@ class _FFN(torch.autograd.Function):
     """out = GELU(x W1^T + b1) W2^T (no FFN-out bias: the caller fuses it into the next add + LayerNorm)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, slot=None, tp=None):
+    def forward(ctx, x, w1, b1, w2, slot=None, tp=None, tp_in=None):
         shp = x.shape
+        ctx.tp_in = tp_in
         x2 = x.reshape(-1, shp[-1])
         from .fused_bert import _fns as fb_fns, _dt, _param
 
@@ -1073,15 +1091,22 @@ class _FFN(torch.autograd.Function):
             check(fb_fns()["gelu"](_dt(z), _dt(bp), 0, ptr(dh.to(z.dtype).contiguous()), ptr(z), ptr(bp), M, N,
                                    ptr(dz), ptr(part), ptr(db1), stream_handle(z.device)), "mifx_bert_bias_gelu")
         dw1 = _dw(dz, x2, w1)
-        dx = _dx(dz, w1, ctx.slot).view(*dout.shape[:-1], w1.shape[1]) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1.to(b1.dtype), dw2, None, None
+        dx = _dx_reduced(dz, w1, ctx.slot, ctx.tp_in).view(*dout.shape[:-1], w1.shape[1]) \
+            if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1.to(b1.dtype), dw2, None, None, None
 
 
 def ffn(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
-        slot: GradSlot | None = None, tp=None) -> torch.Tensor:
+        slot: GradSlot | None = None, tp=None, tp_in=None) -> torch.Tensor:
     """GELU(x W1^T + b1) W2^T as one autograd node on the GPU (bf16): the FFN-out input gradient and the bias-GELU
     backward fused into one GEMM where tuned (GELU_BWD_TUNED); elsewhere the two-node composition. tp: FFN-out is
-    row-parallel and its product comes back all-reduced (overlapped chunk by chunk)."""
+    row-parallel and its product comes back all-reduced (overlapped chunk by chunk); tp_in: x is replicated over the
+    group (copy_to_tp folded in: the input gradient comes back all-reduced, overlapped with the dX GEMM)."""
+    tin = tp_in if tp_in is not None and tp_in.size > 1 else None
     if x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16:
-        return _FFN.apply(x, w1, b1, w2, slot, tp)
+        return _FFN.apply(x, w1, b1, w2, slot, tp, tin)
+    if tin is not None:
+        from ..parallel.tensor_parallel import copy_to_tp
+
+        x = copy_to_tp(x, tin)
     return linear(linear_bias_gelu(x, w1, b1, slot=slot), w2)

@@ -45,14 +45,19 @@ def worker(rank, world, port, a, out):
             for _ in range(a.warmup):
                 tr.step()
             torch.cuda.synchronize(dev)
-            dist.barrier()
-            if not graph and rank == 0:
+            prof = None
+            if not graph and rank == 0:  # (started before the barrier: the peers' kernels must not wait on rank 0
+                # while it initialises the tracer -- the peer-memory waits time out after 10 s)
                 from torch.profiler import ProfilerActivity, profile
 
-                with profile(activities=[ProfilerActivity.CUDA]) as prof:
-                    for _ in range(a.active):
-                        tr.step()
-                    torch.cuda.synchronize(dev)
+                prof = profile(activities=[ProfilerActivity.CUDA])
+                prof.__enter__()
+            dist.barrier()
+            if prof is not None:
+                for _ in range(a.active):
+                    tr.step()
+                torch.cuda.synchronize(dev)
+                prof.__exit__(None, None, None)
                 rows = []
                 for e in prof.key_averages():
                     t = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
