@@ -42,11 +42,16 @@ def worker(rank, world, port, a, out):
             tp = TPGroup()
             torch.manual_seed(0)
             tr = BertTrainer(BertConfig(layers=a.layers), a.batch, a.seq, dev, tp, graph=graph, tp_ipc=True)
-            for _ in range(a.warmup):
+            for i in range(a.warmup):
+                t0 = time.perf_counter()
                 tr.step()
+                if a.debug:  # host-synchronised warm-up steps with the group's health flag
+                    torch.cuda.synchronize(dev)
+                    print(f"[rank {rank}] graph={graph} warm-up step {i}: {time.perf_counter() - t0:.2f} s, "
+                          f"err={int(tp.ipc.err.item()) if tp.ipc is not None else 0}", file=sys.stderr, flush=True)
             torch.cuda.synchronize(dev)
             prof = None
-            if not graph and rank == 0:  # (started before the barrier: the peers' kernels must not wait on rank 0
+            if not graph and rank == 0 and not a.no_profile:  # (started before the barrier: the peers' kernels must not wait on rank 0
                 # while it initialises the tracer -- the peer-memory waits time out after 10 s)
                 from torch.profiler import ProfilerActivity, profile
 
@@ -149,6 +154,8 @@ def main():
     ap.add_argument("--active", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--no-profile", action="store_true", help="step times only (no torch.profiler on rank 0)")
+    ap.add_argument("--debug", action="store_true", help="per-rank warm-up step times and the all-reduce error flag")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "table.md")
