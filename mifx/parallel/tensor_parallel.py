@@ -88,8 +88,12 @@ def _all_reduce(x: torch.Tensor, tp: TPGroup) -> torch.Tensor:
 # compute stream and each chunk's all-reduce on a side stream as soon as the chunk is written, so chunk i's exchange
 # overlaps chunk i+1's GEMM; the compute stream joins the side stream before the reduced activation is used (no other
 # all-reduce of the group can then be in flight: the kernels' epochs stay in issue order). Graph-capturable (event
-# fork / join). MIFX_TP_OVERLAP_CHUNKS: chunks per GEMM (default 4; 1 = the plain GEMM-then-all-reduce).
-_OVERLAP_CHUNKS = int(os.environ.get("MIFX_TP_OVERLAP_CHUNKS", "4"))
+# fork / join). MIFX_TP_OVERLAP_CHUNKS: chunks per GEMM -- opt-in (default 1 = the plain GEMM-then-all-reduce). For
+# BERT-base at TP = 8 the row-parallel GEMM chunks are ~1 us (4096 x 768 x 96 split in 4), too short to hide an
+# all-reduce behind, while chunking multiplies the all-reduce launches by 4; on the one-GPU rehearsal (ranks sharing
+# the device) the chunked step measured slower (TP=2: 38.1 vs 13.2 ms eager, profiles/bert_tp2_overlap_r5.md /
+# bert_tp2_nooverlap_r5.md). It pays where a chunk's GEMM outlasts its all-reduce (wider models, separate GPUs).
+_OVERLAP_CHUNKS = int(os.environ.get("MIFX_TP_OVERLAP_CHUNKS", "1"))
 _SIDE: dict = {}
 
 
