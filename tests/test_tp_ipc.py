@@ -91,11 +91,13 @@ def test_ipc_allreduce_exact_rank_order_sum(world):
             assert torch.equal(yb, torch.full((4,), sb, dtype=torch.bfloat16)), (r, k)
 
 
-def _bert_worker(rank, world, port, out):
+def _bert_worker(rank, world, port, out, chunks=1):
     from mifx.models.bert import BertConfig
+    from mifx.parallel import tensor_parallel as tpm
     from mifx.parallel.tensor_parallel import TPGroup
     from mifx.trainer.bert_trainer import BertTrainer
 
+    tpm._OVERLAP_CHUNKS = chunks  # (the row-parallel GEMM + all-reduce overlap: MIFX_TP_OVERLAP_CHUNKS)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -119,13 +121,14 @@ def _bert_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_bert_tp_step_captured_with_ipc_allreduce_bit_identical_to_eager(world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (4, 1), (2, 4)])
+def test_bert_tp_step_captured_with_ipc_allreduce_bit_identical_to_eager(world, chunks):
     """BertTrainer at TP=world with the peer-memory all-reduces: the step captured into one hipGraph (the TP>1
-    default now) and the same step run eagerly give bit-identical losses and weights."""
+    default now) and the same step run eagerly give bit-identical losses and weights (chunks 4: with the row-parallel
+    GEMM / all-reduce overlap on a side stream)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "bt")
-        mp.start_processes(_bert_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        mp.start_processes(_bert_worker, args=(world, _port(), out, chunks), nprocs=world, start_method="spawn")
         res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     for r in range(world):
         (le, pe), (lg, pg) = res[r][False], res[r][True]
