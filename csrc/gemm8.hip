@@ -681,37 +681,49 @@ __device__ __forceinline__ void gemm8_tile(const bf16* __restrict__ X, const bf1
       bsh[e] = st[3 * N + c];
     }
   }
-#pragma unroll 4
-  for (int i = 0; i < BM / RPI; ++i) {
-    const int row = rr0 + i * RPI;
-    v8bf v = *(const v8bf*)tslot(row, cc);
-    const size_t g = (size_t)(m0 + row) * N + n0 + 8 * cc;
-    if constexpr (ADD) {  // Y = X W^T + R, one rounding of the fp32-exact sum of two bf16 values
-      const v8bf rv = *(const v8bf*)((const bf16*)bias + g);
+  // rows in groups of G: the group's global operand loads (R, the BatchNorm input x, R2) are all issued before any
+  // is used -- the accumulators are dead here, so G x 16 bytes per operand stay in flight per thread (a small-K
+  // product is bound by this pass: with one load in flight per row it streamed at ~3.5 TB/s)
+  constexpr int NI = BM / RPI, G = NI < 8 ? NI : 8;
+  constexpr bool LD1 = ADD || BNB, LD2 = EPI == EPI_ADD_BNBWD;
+#pragma unroll 1
+  for (int i0 = 0; i0 < NI; i0 += G) {
+    v8bf l1[LD1 ? G : 1], l2[LD2 ? G : 1];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[e]);
-      if constexpr (STATS) *(v8bf*)tslot(row, cc) = v;  // the stored sum, re-read by the second statistics pass
+    for (int j = 0; j < G; ++j) {
+      const size_t g = (size_t)(m0 + rr0 + (i0 + j) * RPI) * N + n0 + 8 * cc;
+      if constexpr (LD1) l1[j] = *(const v8bf*)((const bf16*)bias + g);
+      if constexpr (LD2) l2[j] = *(const v8bf*)(R2 + g);
     }
-    if constexpr (STATS) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
-    }
-    if constexpr (EPI == EPI_ADD_BNBWD) {  // one rounding of the fp32-exact sum of two bf16 values
-      const v8bf rv = *(const v8bf*)(R2 + g);
+    for (int j = 0; j < G; ++j) {
+      const int row = rr0 + (i0 + j) * RPI;
+      v8bf v = *(const v8bf*)tslot(row, cc);
+      const size_t g = (size_t)(m0 + row) * N + n0 + 8 * cc;
+      if constexpr (ADD) {  // Y = X W^T + R, one rounding of the fp32-exact sum of two bf16 values
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rv[e]);
-    }
-    if constexpr (BNB) {  // the BatchNorm backward's reduction, with its mask computed as the forward's fmaf
-      const v8bf xv = *(const v8bf*)((const bf16*)bias + g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float u = (float)xv[e];
-        const float gg = fmaf(u, bsc[e], bsh[e]) <= 0.f ? 0.f : (float)v[e];
-        cs[e] += gg;
-        cq[e] += gg * ((u - bmu[e]) * brs[e]);
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)l1[j][e]);
+        if constexpr (STATS) *(v8bf*)tslot(row, cc) = v;  // the stored sum, re-read by the second statistics pass
       }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
+      }
+      if constexpr (EPI == EPI_ADD_BNBWD) {  // one rounding of the fp32-exact sum of two bf16 values
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)l2[j][e]);
+      }
+      if constexpr (BNB) {  // the BatchNorm backward's reduction, with its mask computed as the forward's fmaf
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float u = (float)l1[j][e];
+          const float gg = fmaf(u, bsc[e], bsh[e]) <= 0.f ? 0.f : (float)v[e];
+          cs[e] += gg;
+          cq[e] += gg * ((u - bmu[e]) * brs[e]);
+        }
+      }
+      *(v8bf*)(Y + g) = v;
     }
-    *(v8bf*)(Y + g) = v;
   }
   if constexpr (STATS || BNB) {
     // per-tile BatchNorm statistics of the STORED values, two-pass (mean, then the sum of squared deviations from
