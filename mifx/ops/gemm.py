@@ -735,9 +735,27 @@ _G8_NARROW = os.environ.get("MIFX_G8_NARROW", "1") != "0"
 _BNX_256 = os.environ.get("MIFX_BNX_256", "0") == "1"
 
 
+# measured winners for ResNet-50's 1x1 products at B = 256 (tools/bench_gemm8.py --shapes resnet,
+# profiles/gemm8_resnet_1x1_configs_r5.jsonl): with K <= 512 the 128 x 128 tiles (two workgroups per CU, so one's
+# epilogue overlaps the other's loads) beat the 256 x 256 tiles the throughput heuristic prefers -- e.g. 802816 x 256 x 64
+# 118.9 vs 136.1 us, 50176 x 1024 x 256 41.4 vs 49.2, 12544 x 512 x 2048 33.7 vs 44.4. MIFX_G8_TUNED=0: heuristic only
+_G8_TUNED_ON = os.environ.get("MIFX_G8_TUNED", "1") != "0"
+_G8_TUNED: dict[tuple[int, int, int], tuple[int, int]] = {
+    (802816, 256, 64): (128, 128), (200704, 128, 512): (128, 128), (200704, 512, 128): (128, 128),
+    (50176, 256, 1024): (256, 256), (50176, 1024, 256): (128, 128), (12544, 512, 2048): (128, 128),
+    (12544, 2048, 512): (256, 256),
+}
+
+
 def gemm8_pick(M: int, N: int, K: int, cus: int = 256, bnx: bool = False) -> int | None:
-    """The csrc/gemm8.hip configuration for an M x N x K product: the highest (fraction of the last wave's slots
-    filled) x (the tile's relative throughput); None if none tiles the shape. bnx: for gemm8_nt_bnx."""
+    """The csrc/gemm8.hip configuration for an M x N x K product: a measured winner (_G8_TUNED), else the highest
+    (fraction of the last wave's slots filled) x (the tile's relative throughput); None if none tiles the shape.
+    bnx: for gemm8_nt_bnx."""
+    t = _G8_TUNED.get((M, N, K)) if _G8_TUNED_ON else None
+    if t is not None and not (bnx and t == (256, 256) and not _BNX_256):
+        cfgs = gemm8_configs()
+        if t in cfgs:
+            return cfgs.index(t)
     best, best_score = None, None
     for i, (bm, bn) in enumerate(gemm8_configs()):
         if M % bm or N % bn or K % 64 or (bn == 64 and not _G8_NARROW):
