@@ -7,11 +7,14 @@
 //    1-byte window position (0..8) per channel -> the index traffic is 1/8 of int64 indices;
 //  * backward in gather form: one thread per (n, ih, iw, 8 channels) visits the (at most 2x2) output
 //    windows that contain its input position and adds dout where the stored position points at it.
-//    Every input gradient is written exactly once (no zero-fill, no atomics: deterministic).
+//    Every input gradient is written exactly once (no zero-fill, no atomics: deterministic). For the stem's
+//    even-sized image a thread owns a 2 x 2 input block and loads its four windows once (maxpool_bwd_even:
+//    278 -> 145 us at B=256, bit-identical, profiles/resnet_pool_bwd_ab_r5.txt).
 // Semantics follow PyTorch: padding never wins, ties keep the first position in window order, NaN wins.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -26,14 +29,17 @@ struct alignas(8) U8x8 {
   uint8_t v[kVec];
 };
 
+// I: the flat thread-index type -- 32-bit whenever the element count allows (the ResNet stem's 25.7 M work items:
+// three 64-bit divisions per item are emulated in ~100 VALU instructions each, so the int64 build is ALU-bound)
+template <typename I>
 __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __restrict__ x, int N, int H, int W, int C,
                                                        int OH, int OW, int pt, int pl, int relu,
                                                        __hip_bfloat16* __restrict__ y, uint8_t* __restrict__ idx) {
   const int cg = C / kVec;
-  const long long total = (long long)N * OH * OW * cg;
-  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+  const I total = (I)N * OH * OW * cg;
+  for (I t = (I)blockIdx.x * kThreads + threadIdx.x; t < total; t += (I)gridDim.x * kThreads) {
     const int g = (int)(t % cg);
-    long long p = t / cg;
+    I p = t / cg;
     const int ow = (int)(p % OW);
     p /= OW;
     const int oh = (int)(p % OH);
@@ -84,14 +90,15 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __
   }
 }
 
+template <typename I>
 __global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __restrict__ dy,
                                                        const uint8_t* __restrict__ idx, int N, int H, int W, int C,
                                                        int OH, int OW, int pt, int pl, __hip_bfloat16* __restrict__ dx) {
   const int cg = C / kVec;
-  const long long total = (long long)N * H * W * cg;
-  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+  const I total = (I)N * H * W * cg;
+  for (I t = (I)blockIdx.x * kThreads + threadIdx.x; t < total; t += (I)gridDim.x * kThreads) {
     const int g = (int)(t % cg);
-    long long p = t / cg;
+    I p = t / cg;
     const int iw = (int)(p % W);
     p /= W;
     const int ih = (int)(p % H);
@@ -127,11 +134,78 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __
   }
 }
 
+// Backward of the pad-1 pool over an even-sized image (H = 2 OH, W = 2 OW: the ResNet stem), one thread per
+// (n, a, b, 8 channels) owning the 2 x 2 input block rows 2a, 2a + 1 x columns 2b, 2b + 1: row 2a lies only in window
+// row a (tap row 1), row 2a + 1 in window rows a (tap row 2) and a + 1 (tap row 0); columns likewise. The four windows
+// (a | a + 1) x (b | b + 1) are loaded once for the four input pixels instead of once per input pixel, and the
+// per-pixel sums run in the general kernel's window order (bit-identical results).
+template <typename I>
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_even(const __hip_bfloat16* __restrict__ dy,
+                                                            const uint8_t* __restrict__ idx, int N, int C, int OH,
+                                                            int OW, __hip_bfloat16* __restrict__ dx) {
+  const int cg = C / kVec, H = 2 * OH, W = 2 * OW;
+  const I total = (I)N * OH * OW * cg;
+  for (I t = (I)blockIdx.x * kThreads + threadIdx.x; t < total; t += (I)gridDim.x * kThreads) {
+    const int g = (int)(t % cg);
+    I p = t / cg;
+    const int b = (int)(p % OW);
+    p /= OW;
+    const int a = (int)(p % OH);
+    const int n = (int)(p / OH);
+    // windows [wa][wb] = (a + wa, b + wb); absent ones (past the last row / column) route nothing
+    U8x8 k8[2][2];
+    Bf8 d8[2][2];
+#pragma unroll
+    for (int wa = 0; wa < 2; ++wa)
+#pragma unroll
+      for (int wb = 0; wb < 2; ++wb) {
+        if (a + wa < OH && b + wb < OW) {
+          const size_t off = (((size_t)n * OH + a + wa) * OW + b + wb) * C + g * kVec;
+          k8[wa][wb] = *(const U8x8*)(idx + off);
+          d8[wa][wb] = *(const Bf8*)(dy + off);
+        } else {
+#pragma unroll
+          for (int e = 0; e < kVec; ++e) k8[wa][wb].v[e] = kNone;
+        }
+      }
+    // input pixel (2a + sh, 2b + sw): window (a + wa, b + wb) contributes when it contains it -- wa = 0 always,
+    // wa = 1 only for sh = 1 (likewise columns) -- at tap (sh ? (wa ? 0 : 2) : 1, sw ? (wb ? 0 : 2) : 1)
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+      for (int sw = 0; sw < 2; ++sw) {
+        float acc[kVec];
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int wa = 0; wa <= sh; ++wa)
+#pragma unroll
+          for (int wb = 0; wb <= sw; ++wb) {
+            const uint8_t k = (uint8_t)((sh ? (wa ? 0 : 2) : 1) * 3 + (sw ? (wb ? 0 : 2) : 1));
+#pragma unroll
+            for (int e = 0; e < kVec; ++e)
+              if (k8[wa][wb].v[e] == k) acc[e] += __bfloat162float(d8[wa][wb].v[e]);
+          }
+        Bf8 o;
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) o.v[e] = __float2bfloat16(acc[e]);
+        *(Bf8*)(dx + (((size_t)n * H + 2 * a + sh) * W + 2 * b + sw) * C + g * kVec) = o;
+      }
+  }
+}
+
 int grid_for(long long total) {
   long long g = (total + kThreads - 1) / kThreads;
   if (g > 65536) g = 65536;
   return g < 1 ? 1 : (int)g;
 }
+
+// 32-bit indices when total + one grid stride stays below 2^32 (the grid-stride loop's last increment)
+bool even_off() {  // MIFX_POOL_EVEN=0: the general gather kernel for the stem too (A/B)
+  static const bool off = getenv("MIFX_POOL_EVEN") && getenv("MIFX_POOL_EVEN")[0] == '0';
+  return off;
+}
+bool small_index(long long total) { return total + 65536LL * kThreads < (1LL << 32); }
 
 }  // namespace
 
@@ -146,8 +220,13 @@ int mifx_maxpool3s2p_fwd(const void* x, int N, int H, int W, int C, int pt, int 
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec || pt < 0 || pt > 2 || pl < 0 || pl > 2 || OH <= 0 ||
       OW <= 0 || 2 * (OH - 1) - pt >= H || 2 * (OW - 1) - pl >= W)
     return -1;
-  hipLaunchKernelGGL(maxpool_fwd, dim3(grid_for((long long)N * OH * OW * (C / kVec))), dim3(kThreads), 0, st,
-                     (const __hip_bfloat16*)x, N, H, W, C, OH, OW, pt, pl, relu, (__hip_bfloat16*)y, (uint8_t*)idx);
+  const long long total = (long long)N * OH * OW * (C / kVec);
+  if (small_index(total))
+    hipLaunchKernelGGL(maxpool_fwd<uint32_t>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const __hip_bfloat16*)x, N,
+                       H, W, C, OH, OW, pt, pl, relu, (__hip_bfloat16*)y, (uint8_t*)idx);
+  else
+    hipLaunchKernelGGL(maxpool_fwd<long long>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const __hip_bfloat16*)x,
+                       N, H, W, C, OH, OW, pt, pl, relu, (__hip_bfloat16*)y, (uint8_t*)idx);
   return (int)hipGetLastError();
 }
 
@@ -156,8 +235,23 @@ int mifx_maxpool3s2p_bwd(const void* dy, const void* idx, int N, int H, int W, i
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec || pt < 0 || pt > 2 || pl < 0 || pl > 2 || OH <= 0 ||
       OW <= 0)
     return -1;
-  hipLaunchKernelGGL(maxpool_bwd, dim3(grid_for((long long)N * H * W * (C / kVec))), dim3(kThreads), 0, st,
-                     (const __hip_bfloat16*)dy, (const uint8_t*)idx, N, H, W, C, OH, OW, pt, pl, (__hip_bfloat16*)dx);
+  if (pt == 1 && pl == 1 && H == 2 * OH && W == 2 * OW && !even_off()) {
+    const long long te = (long long)N * OH * OW * (C / kVec);
+    if (small_index(te))
+      hipLaunchKernelGGL(maxpool_bwd_even<uint32_t>, dim3(grid_for(te)), dim3(kThreads), 0, st,
+                         (const __hip_bfloat16*)dy, (const uint8_t*)idx, N, C, OH, OW, (__hip_bfloat16*)dx);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_even<long long>, dim3(grid_for(te)), dim3(kThreads), 0, st,
+                         (const __hip_bfloat16*)dy, (const uint8_t*)idx, N, C, OH, OW, (__hip_bfloat16*)dx);
+    return (int)hipGetLastError();
+  }
+  const long long total = (long long)N * H * W * (C / kVec);
+  if (small_index(total))
+    hipLaunchKernelGGL(maxpool_bwd<uint32_t>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const __hip_bfloat16*)dy,
+                       (const uint8_t*)idx, N, H, W, C, OH, OW, pt, pl, (__hip_bfloat16*)dx);
+  else
+    hipLaunchKernelGGL(maxpool_bwd<long long>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const __hip_bfloat16*)dy,
+                       (const uint8_t*)idx, N, H, W, C, OH, OW, pt, pl, (__hip_bfloat16*)dx);
   return (int)hipGetLastError();
 }
 
