@@ -90,6 +90,85 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd(const __hip_bfloat16* __
   }
 }
 
+// Forward over PAIRS of horizontally adjacent windows (ow = 2q, 2q + 1): their 3 x 5 input patch shares one column,
+// so a thread issues 15 loads for two outputs instead of 18, all before the first compare (clamped addresses, so
+// every load is unconditional; out-of-image taps are masked at the compare). Per-window tap order, tie and NaN
+// rules are those of maxpool_fwd (bit-identical outputs and positions).
+template <typename I>
+__global__ __launch_bounds__(kThreads) void maxpool_fwd2(const __hip_bfloat16* __restrict__ x, int N, int H, int W,
+                                                        int C, int OH, int OW, int pt, int pl, int relu,
+                                                        __hip_bfloat16* __restrict__ y, uint8_t* __restrict__ idx) {
+  const int cg = C / kVec, OQ = (OW + 1) >> 1;
+  const I total = (I)N * OH * OQ * cg;
+  for (I t = (I)blockIdx.x * kThreads + threadIdx.x; t < total; t += (I)gridDim.x * kThreads) {
+    const int g = (int)(t % cg);
+    I p = t / cg;
+    const int q = (int)(p % OQ);
+    p /= OQ;
+    const int oh = (int)(p % OH);
+    const int n = (int)(p / OH);
+    const bool two = 2 * q + 1 < OW;
+    Bf8 v[3][5];
+    bool ok[3][5];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - pt + kh;
+      const bool rok = ih >= 0 && ih < H;
+      const int ihc = min(max(ih, 0), H - 1);
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        const int iw = 4 * q - pl + c;
+        ok[kh][c] = rok && iw >= 0 && iw < W && (c < 3 || two);
+        const int iwc = min(max(iw, 0), W - 1);
+        v[kh][c] = *(const Bf8*)(x + (((size_t)n * H + ihc) * W + iwc) * C + g * kVec);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (s2 == 1 && !two) break;
+      float m[kVec];
+      U8x8 k8;
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        m[e] = -INFINITY;
+        k8.v[e] = 0;
+      }
+      bool first = true;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          if (!ok[kh][2 * s2 + kw]) continue;
+          const Bf8& v8 = v[kh][2 * s2 + kw];
+#pragma unroll
+          for (int e = 0; e < kVec; ++e) {
+            const float f = __bfloat162float(v8.v[e]);
+            if (first || f > m[e] || f != f) {
+              m[e] = f;
+              k8.v[e] = (uint8_t)(kh * 3 + kw);
+            }
+          }
+          first = false;
+        }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          if (!(m[e] > 0.f)) {
+            k8.v[e] = kNone;
+            if (m[e] == m[e]) m[e] = 0.f;
+          }
+        }
+      }
+      Bf8 o;
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) o.v[e] = __float2bfloat16(m[e]);
+      const size_t off = (((size_t)n * OH + oh) * OW + 2 * q + s2) * C + g * kVec;
+      *(Bf8*)(y + off) = o;
+      *(U8x8*)(idx + off) = k8;
+    }
+  }
+}
+
 template <typename I>
 __global__ __launch_bounds__(kThreads) void maxpool_bwd(const __hip_bfloat16* __restrict__ dy,
                                                        const uint8_t* __restrict__ idx, int N, int H, int W, int C,
@@ -201,6 +280,10 @@ int grid_for(long long total) {
 }
 
 // 32-bit indices when total + one grid stride stays below 2^32 (the grid-stride loop's last increment)
+bool pair_off() {  // MIFX_POOL_PAIR=0: one window per thread in the forward (A/B)
+  static const bool off = getenv("MIFX_POOL_PAIR") && getenv("MIFX_POOL_PAIR")[0] == '0';
+  return off;
+}
 bool even_off() {  // MIFX_POOL_EVEN=0: the general gather kernel for the stem too (A/B)
   static const bool off = getenv("MIFX_POOL_EVEN") && getenv("MIFX_POOL_EVEN")[0] == '0';
   return off;
@@ -220,6 +303,16 @@ int mifx_maxpool3s2p_fwd(const void* x, int N, int H, int W, int C, int pt, int 
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % kVec || pt < 0 || pt > 2 || pl < 0 || pl > 2 || OH <= 0 ||
       OW <= 0 || 2 * (OH - 1) - pt >= H || 2 * (OW - 1) - pl >= W)
     return -1;
+  if (!pair_off()) {
+    const long long tp = (long long)N * OH * ((OW + 1) / 2) * (C / kVec);
+    if (small_index(tp))
+      hipLaunchKernelGGL(maxpool_fwd2<uint32_t>, dim3(grid_for(tp)), dim3(kThreads), 0, st, (const __hip_bfloat16*)x, N,
+                         H, W, C, OH, OW, pt, pl, relu, (__hip_bfloat16*)y, (uint8_t*)idx);
+    else
+      hipLaunchKernelGGL(maxpool_fwd2<long long>, dim3(grid_for(tp)), dim3(kThreads), 0, st, (const __hip_bfloat16*)x,
+                         N, H, W, C, OH, OW, pt, pl, relu, (__hip_bfloat16*)y, (uint8_t*)idx);
+    return (int)hipGetLastError();
+  }
   const long long total = (long long)N * OH * OW * (C / kVec);
   if (small_index(total))
     hipLaunchKernelGGL(maxpool_fwd<uint32_t>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const __hip_bfloat16*)x, N,

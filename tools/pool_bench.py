@@ -32,6 +32,7 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / it
 
     dx = torch.autograd.grad(max_pool3s2(x), x, g)[0]
+    ydig = hashlib.sha256(max_pool3s2(x.detach()).contiguous().view(torch.int16).cpu().numpy().tobytes())
     digest = hashlib.sha256(dx.contiguous(memory_format=torch.channels_last).view(torch.int16).cpu().numpy().tobytes())
     fwd = t(lambda: max_pool3s2(x.detach()))
     both = t(lambda: torch.autograd.grad(max_pool3s2(x), x, g))
@@ -39,7 +40,9 @@ def main():
     print(json.dumps({"fwd_us": round(fwd, 1), "bwd_us": round(both - fwd, 1),
                       "fwd_TBps": round((xb + yb + yb / 2) / fwd / 1e6, 2),
                       "bwd_TBps": round((xb + yb + yb / 2) / (both - fwd) / 1e6, 2),
-                      "dx_sha256": digest.hexdigest()[:16], "even_kernel": os.environ.get("MIFX_POOL_EVEN", "1") != "0"}), flush=True)
+                      "y_sha256": ydig.hexdigest()[:16], "dx_sha256": digest.hexdigest()[:16],
+                      "pair_fwd": os.environ.get("MIFX_POOL_PAIR", "1") != "0",
+                      "even_bwd": os.environ.get("MIFX_POOL_EVEN", "1") != "0"}), flush=True)
 
 
 if __name__ == "__main__":
