@@ -219,10 +219,47 @@ class ResNetTrainer:
             self.dp.finish()  # joins the side stream: every bucket exchanged and averaged
         return total
 
+    def _sgd_prepare(self) -> None:
+        """Tables of the fused multi-tensor SGD (csrc/sgd.hip, one launch instead of 14 foreach passes), built
+        before a capture (they are host-to-device copies). MIFX_SGD_FUSED=0, or groups with different momentum
+        settings, keep the foreach update."""
+        self._sgd_tab = None
+        if os.environ.get("MIFX_SGD_FUSED", "1") == "0" or not self.device.type == "cuda":
+            return
+        groups = self.opt.param_groups
+        if len({(g["momentum"], g["dampening"], g["nesterov"]) for g in groups}) != 1:
+            return
+        from ..ops import _lib
+        from ..ops.sgd import FusedSGDTables
+
+        if not _lib.available("sgd"):
+            return
+        params, bufs, wds = [], [], []
+        for g in groups:
+            for p in g["params"]:
+                if not p.requires_grad:
+                    continue
+                params.append(p)
+                bufs.append(self.opt.state[p]["momentum_buffer"])
+                wds.append(g["weight_decay"])
+        try:
+            self._sgd_tab = FusedSGDTables(params, bufs, wds)
+        except ValueError:
+            self._sgd_tab = None
+
     @torch.no_grad()
     def _sgd_captured(self) -> None:
         """torch.optim.SGD's update (weight decay, momentum, Nesterov; its own momentum buffers) with the learning
         rate read from a device tensor, so a replayed graph follows the warmup schedule."""
+        tab = getattr(self, "_sgd_tab", None)
+        if tab is not None:
+            grads = [p.grad for p in tab.params]  # (with deferred weight gradients: produced inside this capture)
+            if tab.grads_ok(grads):
+                tab.set_grads(grads)
+                g0 = self.opt.param_groups[0]
+                tab.step(self._neg_lr, g0["momentum"], g0["dampening"], g0["nesterov"])
+                return
+            self._sgd_tab = None  # a gradient missing or laid out unlike its parameter: the foreach update
         for group in self.opt.param_groups:
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
@@ -245,6 +282,7 @@ class ResNetTrainer:
         if any("momentum_buffer" not in self.opt.state.get(p, {}) for p in self.model.parameters()
                if p.requires_grad):
             raise RuntimeError("capture needs the SGD momentum buffers of an eager step first")
+        self._sgd_prepare()
         torch.cuda.synchronize(self.device)
         self._gA = torch.cuda.CUDAGraph()
         one = self.dp is None or self.dp.exchange == "ipc"
@@ -379,6 +417,7 @@ def main(argv=None):
                           "parallelism": f"dp{env.world_size}", "hipgraph": tr.use_graph,
                           "dp_exchange": tr.dp.exchange if tr.dp is not None else "none",
                           "graphs_per_step": 0 if not tr.use_graph else (2 if tr._gB is not None else 1),
+                          "sgd": "fused" if getattr(tr, "_sgd_tab", None) is not None else "foreach",
                           "deterministic": bool(torch.backends.cudnn.deterministic)}), flush=True)
     mdist.shutdown()
 
