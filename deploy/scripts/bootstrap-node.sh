@@ -74,7 +74,11 @@ start metadata python3 -m mifx.metadata.server --port 8080 --db "$ROOT/metadata/
 start board python3 -m mifx.board --port 6006 --logdir "$ROOT/board"
 start notebooks python3 -m mifx.notebook_server --port 8889
 start operator python3 -m mifx.launch.operator --local "$ROOT/jobs"
-start tensor-store python3 -m mifx.serving.resp_server --port 6379
+# the tensor store loads models it is sent: loopback only, and a password because nginx proxies :9736 to it
+mkdir -p "$ROOT/secrets" && chmod 700 "$ROOT/secrets"
+[ -s "$ROOT/secrets/resp_password" ] || (umask 077; head -c 24 /dev/urandom | od -An -tx1 | tr -d ' \n' > "$ROOT/secrets/resp_password")
+MIFX_RESP_PASSWORD="$(cat "$ROOT/secrets/resp_password")" start tensor-store python3 -m mifx.serving.resp_server \
+  --host 127.0.0.1 --port 6379 --model-root "$ROOT/models"
 if [ -d "$ROOT/models/taxi" ]; then
   start model-server python3 -m mifx.serving.server --model_name taxi --model_base_path "$ROOT/models/taxi" \
     --rest_api_port 8500 --port 9000

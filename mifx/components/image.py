@@ -171,6 +171,7 @@ def run_image_rank(spec: dict) -> dict:
                 torch.distributed.barrier()
     if tr.device.type == "cuda":
         torch.cuda.synchronize(tr.device)
+    tr.check()
     secs = time.time() - t0
     res = {"final_loss": float(loss), "world": world, "steps": tr.step_idx, "resumed_from": ck,
            "train_images_per_sec": (tr.step_idx - s0) * tr.batch * tr.accum * world / max(secs, 1e-9)}

@@ -61,6 +61,7 @@ class FusedSGDTables:
         self.tp, self.to, self.tn = (torch.tensor(x, dtype=torch.int32, device=dev) for x in (tp, to, tn))
         self.nblocks = len(tp)
         self.grads = None
+        self._captured_hosts: list = []
         if grads is not None:
             self.set_grads(grads)
 
@@ -79,17 +80,29 @@ class FusedSGDTables:
         if not self.grads_ok(grads):
             raise ValueError("fused SGD: gradient layouts differ from their parameters'")
         capturing = torch.cuda.is_current_stream_capturing()
-        if not capturing:  # eager: the pinned buffer may still feed an earlier asynchronous copy
+        if capturing:
+            # the copy node re-reads its host buffer on every replay: give each capture a buffer of its own, kept
+            # alive with the tables and never written again, so a later set_grads cannot retarget a captured graph
+            host = torch.zeros(len(self.params), dtype=torch.int64).pin_memory()
+            self._captured_hosts.append(host)
+        else:  # eager: the pinned buffer may still feed an earlier asynchronous copy
             torch.cuda.current_stream(self.gp.device).synchronize()
+            host = self._gp_host
         for i, g in enumerate(grads):
-            self._gp_host[i] = g.data_ptr()
-        self.gp.copy_(self._gp_host, non_blocking=True)
+            host[i] = g.data_ptr()
+        self.gp.copy_(host, non_blocking=True)
         self.grads = list(grads)
 
     def step(self, neg_lr: torch.Tensor, momentum: float, dampening: float, nesterov: bool) -> None:
+        """One update. The kernel writes the parameters through raw addresses, so their version counters are bumped
+        here (at call / capture time): consumers keyed on w._version (mifx.ops.weight_prep bf16 images) then see
+        the weights as changed instead of serving images from before the update."""
+        if self.grads is None:
+            raise RuntimeError("fused SGD: set_grads() before step()")
         check(_fns()["run"](ptr(self.pp), ptr(self.gp), ptr(self.bp), ptr(self.wd), ptr(self.tp), ptr(self.to),
                             ptr(self.tn), self.nblocks, ptr(neg_lr), float(momentum), float(dampening),
                             int(bool(nesterov)), stream_handle(neg_lr.device)), "mifx_sgd_chunks")
+        torch.autograd.graph.increment_version(self.params)
 
 
 @torch.no_grad()

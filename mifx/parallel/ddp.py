@@ -257,6 +257,13 @@ class DataParallel:
 
     step_ready = finish
 
+    def check(self) -> None:
+        """Raise if the peer-memory exchange timed out on this rank. Its error flag is sticky: every later exchange
+        poisons its bucket with NaN instead of hanging, so a caller must check at each host synchronisation point
+        (after warmup, after timed steps, before writing a checkpoint) rather than train on or save NaN weights."""
+        if self._ipc is not None:
+            self._ipc.check()
+
     def remove_hooks(self) -> None:
         for h in self._hooks:
             h.remove()

@@ -91,7 +91,10 @@ class _Reader:
             raise ConnectionError("connection closed inside a bulk string")
         return b[:-2]
 
-    def value(self, max_bulk: int = 1 << 31):
+    MAX_DEPTH = 8            # nested arrays (a command is depth 1; replies here nest at most 3 deep)
+    MAX_ARRAY = 1 << 22      # elements per array (AI.TENSORSET ... VALUES v1 .. vn)
+
+    def value(self, max_bulk: int = 1 << 31, depth: int = 0):
         ln = self.line()
         t, rest = ln[:1], ln[1:]
         if t == b"+":
@@ -109,7 +112,11 @@ class _Reader:
             return self.exact(n)
         if t == b"*":
             n = int(rest)
-            return None if n < 0 else [self.value(max_bulk) for _ in range(n)]
+            if n > self.MAX_ARRAY:
+                raise ValueError("protocol error: array too long")
+            if depth >= self.MAX_DEPTH:
+                raise ValueError("protocol error: arrays nested too deep")
+            return None if n < 0 else [self.value(max_bulk, depth + 1) for _ in range(n)]
         # inline command (telnet style): space-separated words
         return ln.split()
 
@@ -121,14 +128,29 @@ def _s(x) -> str:
     return x.decode() if isinstance(x, (bytes, bytearray)) else str(x)
 
 
+def _loopback(host: str) -> bool:
+    return host in ("127.0.0.1", "::1", "localhost") or host.startswith("127.")
+
+
 class RespServer:
-    """Serve a TensorStore over RESP on host:port (port 0 picks a free one). start() returns the bound port."""
+    """Serve a TensorStore over RESP on host:port (port 0 picks a free one). start() returns the bound port.
+
+    Security model (a model server executes what it loads, so who may load matters):
+      * `requirepass`: like redis-server's, every command but AUTH / QUIT answers NOAUTH until the connection has
+        sent `AUTH <password>`. Binding a non-loopback address without a password is refused.
+      * AI.MODELSET BLOB payloads are plain (uncompressed) tars of saved-model exports; the class an export names must
+        be on the serving allow-list (`mifx.serving.saved_model.servable_classes`), enforced by LoadedModel itself.
+      * AI.MODELSET PATH reads server-side directories only under `model_roots` (none by default: PATH is off)."""
 
     def __init__(self, store: TensorStore | None = None, host: str = "127.0.0.1", port: int = 6379,
-                 max_bulk_mb: int = 512):
+                 max_bulk_mb: int = 512, requirepass: str | None = None, model_roots: list[str] | None = None):
+        if not _loopback(host) and not requirepass:
+            raise ValueError(f"refusing to serve on {host} without a password (requirepass)")
         self.store = store or TensorStore()
         self.host, self.port = host, port
         self.max_bulk = max_bulk_mb << 20
+        self.requirepass = requirepass
+        self.model_roots = [os.path.realpath(r) for r in (model_roots or [])]
         self._srv = None
         self._thread = None
         self._tmp = tempfile.TemporaryDirectory(prefix="mifx_resp_models_")
@@ -152,23 +174,35 @@ class RespServer:
         kw = [_s(x).upper() if isinstance(x, (bytes, str)) and len(x) < 16 else None for x in rest]
         if "BLOB" in kw:
             blob = bytes(rest[kw.index("BLOB") + 1])
-            d = os.path.join(self._tmp.name, f"{key}_{len(os.listdir(self._tmp.name))}")
+            d = os.path.join(self._tmp.name, f"m{len(os.listdir(self._tmp.name))}")
             os.makedirs(d)
-            with tarfile.open(fileobj=io.BytesIO(blob)) as tf:
+            try:  # "r:" = no decompression: the extracted size is bounded by the blob's own (max_bulk)
+                tf = tarfile.open(fileobj=io.BytesIO(blob), mode="r:")
+            except tarfile.TarError as e:
+                raise RespError(f"ERR model blob: not an uncompressed tar ({e})") from None
+            with tf:
+                total = 0
                 for m in tf.getmembers():  # regular files and directories only, inside the target
                     if not (m.isfile() or m.isdir()) or m.name.startswith(("/", "..")) or ".." in m.name.split("/"):
                         raise RespError("ERR model blob: unsafe tar member")
+                    total += m.size
+                if total > len(blob):
+                    raise RespError("ERR model blob: members larger than the blob")
                 tf.extractall(d)
             path = d
         elif "PATH" in kw:
-            path = _s(rest[kw.index("PATH") + 1])
+            path = os.path.realpath(_s(rest[kw.index("PATH") + 1]))
+            if not any(path == r or path.startswith(r + os.sep) for r in self.model_roots):
+                raise RespError("ERR AI.MODELSET PATH is outside the server's model roots")
         else:
             raise RespError("ERR AI.MODELSET needs BLOB <saved-model tar> or PATH <dir>")
         with open(os.path.join(path, "saved_model.json")) as f:
             meta = json.load(f)
+        from .saved_model import servable_classes
+
         cls = meta.get("model_class", "")
-        if meta.get("family") != "wide_deep" and not cls.startswith("mifx."):
-            raise RespError(f"ERR model class {cls!r} is outside the mifx package")
+        if meta.get("family") != "wide_deep" and cls not in servable_classes():
+            raise RespError(f"ERR model class {cls!r} is not on the serving allow-list")
         return self.store.modelset(key, "MIFX", device, path=path)
 
     def execute(self, args: list):
@@ -225,21 +259,34 @@ class RespServer:
 
     # -- connection loop
     def _handle(self, sock: socket.socket):
+        import hmac
+
         rd = _Reader(sock)
+        authed = self.requirepass is None
         while True:
             try:
                 req = rd.value(self.max_bulk)
             except (ConnectionError, OSError):
                 return
-            except ValueError as e:
+            except (ValueError, RecursionError) as e:
                 sock.sendall(encode(RespError(f"ERR {e}")))
                 return
-            if not isinstance(req, list):
-                sock.sendall(encode(RespError("ERR protocol error: expected an array")))
+            if not isinstance(req, list) or not all(isinstance(x, (bytes, str)) for x in req):
+                sock.sendall(encode(RespError("ERR protocol error: expected an array of bulk strings")))
                 continue
-            if req and _s(req[0]).upper() == "QUIT":
+            cmd = _s(req[0]).upper() if req else ""
+            if cmd == "QUIT":
                 sock.sendall(encode("OK"))
                 return
+            if cmd == "AUTH":
+                ok = self.requirepass is not None and len(req) == 2 and hmac.compare_digest(
+                    _s(req[1]).encode(), self.requirepass.encode())
+                authed = authed or ok
+                sock.sendall(encode("OK" if ok else RespError("WRONGPASS invalid password")))
+                continue
+            if not authed:
+                sock.sendall(encode(RespError("NOAUTH Authentication required.")))
+                continue
             try:
                 out = self.execute(req)
             except RespError as e:
@@ -280,10 +327,13 @@ class RespClient:
     """Minimal redis-py-style client: `execute_command(*args)` sends one RESP command and returns the decoded reply
     (bulk strings as bytes, arrays as lists); an error reply raises RespError."""
 
-    def __init__(self, host: str = "127.0.0.1", port: int = 6379, timeout: float | None = 60.0):
+    def __init__(self, host: str = "127.0.0.1", port: int = 6379, timeout: float | None = 60.0,
+                 password: str | None = None):
         self.sock = socket.create_connection((host, port), timeout=timeout)
         self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self.rd = _Reader(self.sock)
+        if password is not None:
+            self.execute_command("AUTH", password)
 
     def execute_command(self, *args):
         self.sock.sendall(encode_command(*args))
@@ -317,10 +367,14 @@ def main(argv=None):
     import argparse
 
     ap = argparse.ArgumentParser(prog="python -m mifx.serving.resp_server", description=__doc__.split("\n")[0])
-    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--host", default="127.0.0.1",
+                    help="bind address; a non-loopback address needs --requirepass (or MIFX_RESP_PASSWORD)")
     ap.add_argument("--port", type=int, default=6379)
+    ap.add_argument("--requirepass", default=os.environ.get("MIFX_RESP_PASSWORD"))
+    ap.add_argument("--model-root", action="append", default=[],
+                    help="server-side directory AI.MODELSET PATH may load from (repeatable; default: PATH disabled)")
     a = ap.parse_args(argv)
-    srv = RespServer(host=a.host, port=a.port)
+    srv = RespServer(host=a.host, port=a.port, requirepass=a.requirepass, model_roots=a.model_root)
     port = srv.start()
     print(f"mifx RESP tensor store listening on {a.host}:{port}", flush=True)
     try:

@@ -61,9 +61,51 @@ def save_module(path: str, model: torch.nn.Module, module_class: str, config: di
     return path
 
 
+# Model classes a "module" export may name. An export is data (JSON + safetensors); the class it names is imported and
+# called with the export's model_config as keyword arguments, so an open set of classes would let whoever writes an
+# export (or uploads one to a model server) run any importable callable. Only these classes -- plus any the serving
+# process itself adds with register_servable_class() -- are ever imported by LoadedModel.
+_SERVABLE = {
+    "mifx.models.cnn:FashionCNN",
+    "mifx.models.cnn:TpuMnistCNN",
+    "mifx.models.cnn:MnistDPCNN",
+    "mifx.models.taxi_dnn:TaxiDNN",
+    "mifx.models.resnet:ResNetV2",
+    "mifx.models.wide_deep:WideDeepModel",
+    "torch.nn:Linear",
+}
+
+
+def register_servable_class(class_path: str) -> None:
+    """Allow exports naming `module:Class` (an nn.Module subclass) to be loaded by this process."""
+    _SERVABLE.add(class_path)
+
+
+def servable_classes() -> frozenset:
+    return frozenset(_SERVABLE)
+
+
+def _json_plain(v, depth: int = 0) -> bool:
+    if depth > 8:
+        return False
+    if v is None or isinstance(v, (bool, int, float, str)):
+        return True
+    if isinstance(v, list):
+        return all(_json_plain(x, depth + 1) for x in v)
+    if isinstance(v, dict):
+        return all(isinstance(k, str) and _json_plain(x, depth + 1) for k, x in v.items())
+    return False
+
+
 def _import(path: str):
+    if path not in _SERVABLE:
+        raise PermissionError(f"model class {path!r} is not servable (allowed: {sorted(_SERVABLE)}; "
+                              "register_servable_class() adds one)")
     mod, _, name = path.partition(":")
-    return getattr(importlib.import_module(mod), name)
+    cls = getattr(importlib.import_module(mod), name)
+    if not (isinstance(cls, type) and issubclass(cls, torch.nn.Module)):
+        raise PermissionError(f"model class {path!r} is not a torch.nn.Module")
+    return cls
 
 
 class LoadedModel:
@@ -78,6 +120,8 @@ class LoadedModel:
         sd = load_file(os.path.join(path, "variables", "variables.safetensors"))
         self.family = self.meta["family"]
         self.transform = None
+        if self.family not in ("wide_deep", "module"):
+            raise ValueError(f"{path}: unknown model family {self.family!r}")
         if self.family == "wide_deep":
             from ..models import wide_deep as wdm
 
@@ -94,7 +138,10 @@ class LoadedModel:
             self._fused = None
         else:
             cls = _import(self.meta["model_class"])
-            self.model = cls(**self.meta.get("model_config", {}))
+            cfg = self.meta.get("model_config", {})
+            if not (isinstance(cfg, dict) and _json_plain(cfg)):
+                raise ValueError(f"{path}: model_config must be a JSON object of plain values")
+            self.model = cls(**cfg)
             self.model.load_state_dict(sd)
             self.model.to(self.device).eval()
 

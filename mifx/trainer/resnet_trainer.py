@@ -1,7 +1,9 @@
-"""ResNet-50 image-classification trainer (BASELINE config 5): data-parallel over the node's MI355X
-(one process per GPU, bucketed RCCL all-reduce overlapped with backward), HBM-resident uint8
-dataset with the fused crop/flip/normalize HIP kernel, bf16 autocast in channels_last
-(MIOpen NHWC MFMA convolutions), SGD + Nesterov momentum with linear warmup.
+"""ResNet-50 image-classification trainer (BASELINE config 5): data-parallel over the node's MI355X (one process per
+GPU), HBM-resident uint8 dataset with the fused crop/flip/normalize HIP kernel, bf16 channels_last. The convolutions
+run on the hand-written implicit-GEMM kernel (csrc/gemm8.hip, mifx.ops.conv1x1 / conv3x3) with BatchNorm statistics,
+BatchNorm-backward sums and residual adds in its epilogues; weight gradients are deferred to grouped launches
+(mifx.ops.gemm.deferred_weight_grads); SGD + Nesterov momentum with linear warmup is one fused multi-tensor kernel
+(csrc/sgd.hip). What MIOpen still runs is listed in README.md.
 
 On the GPU the step is captured into hipGraphs after `graph_warmup` eager steps (graph=True, the default there):
 graph A = gradient zeroing + every micro-batch's input kernel, forward and backward (the step counter, learning rate
@@ -295,6 +297,12 @@ class ResNetTrainer:
             with torch.cuda.graph(self._gB):
                 self._sgd_captured()
 
+    def check(self) -> None:
+        """Raise if the data-parallel peer-memory exchange timed out on this rank (sticky: the later steps' buckets
+        are NaN, so nothing trained since may be reported or saved)."""
+        if self.dp is not None:
+            self.dp.check()
+
     # ---------------------------------------------------------------- checkpoint / resume
     def state_dict(self) -> dict:
         """Weights, BatchNorm running statistics, the SGD momentum buffers and the step (flat tensor dict)."""
@@ -324,6 +332,7 @@ class ResNetTrainer:
 
         from safetensors.torch import save_file
 
+        self.check()  # never write weights trained on a failed exchange
         os.makedirs(model_dir, exist_ok=True)
         path = os.path.join(model_dir, f"ckpt-{self.step_idx}.safetensors")
         save_file({k: v.cpu().contiguous() for k, v in self.state_dict().items()}, path)
@@ -399,6 +408,7 @@ def main(argv=None):
         if env.rank == 0:
             print(f"[resnet] warmup step {i + 1}/{a.warmup}: {time.perf_counter() - t1:.2f}s", file=sys.stderr,
                   flush=True)
+    tr.check()  # a timed-out exchange during warmup fails the run here, outside the timed region
     mdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -409,6 +419,7 @@ def main(argv=None):
         torch.cuda.synchronize()
     mdist.barrier()
     dt = mdist.max_over_ranks(time.perf_counter() - t0)
+    tr.check()  # ... and during the timed steps: never report the throughput of NaN buckets
     if env.rank == 0:
         print(json.dumps({"metric": "ResNet-50 training images/sec (whole node)",
                           "value": a.batch * env.world_size * a.steps / dt, "unit": "images/s",

@@ -168,6 +168,28 @@ def test_ddp_ipc_exchange_needs_cuda():
         DataParallel(_Net(), exchange="nope")
 
 
+def test_ddp_check_forwards_the_exchange_error_and_guards_checkpoints(tmp_path):
+    """DataParallel.check() raises the peer-memory exchange's sticky timeout, and ResNetTrainer refuses to write a
+    checkpoint after one (the later buckets would be NaN)."""
+    dp = DataParallel(_Net())
+    dp.check()  # no exchange: nothing to report
+
+    class FailedIpc:
+        def check(self):
+            raise RuntimeError("IPC all-reduce: a peer never published")
+
+    dp._ipc = FailedIpc()
+    with pytest.raises(RuntimeError, match="never published"):
+        dp.check()
+    from mifx.trainer.resnet_trainer import ResNetTrainer
+
+    tr = ResNetTrainer.__new__(ResNetTrainer)
+    tr.dp = dp
+    with pytest.raises(RuntimeError, match="never published"):
+        tr.save_checkpoint(str(tmp_path))
+    assert not list(tmp_path.iterdir())
+
+
 def test_tp_overlap_gate_needs_ipc_and_whole_chunks():
     """The overlapped row-parallel reduction applies only with the peer-memory all-reduce, TP > 1, token counts that
     split into whole 64-row chunks and chunks that fit the IPC buffer."""

@@ -228,6 +228,66 @@ def test_resp_server_notebook18_flow_over_localhost(tmp_path):
         srv.stop()
 
 
+def test_resp_server_refuses_code_loading_and_unauthenticated_clients(tmp_path):
+    """An export naming a callable off the allow-list (here the rank launcher, which would start `python -c`), a
+    PATH outside the model roots, a compressed blob, deep nesting, and commands before AUTH are all refused."""
+    import io
+    import json as _json
+    import socket as _socket
+    import tarfile
+
+    from mifx.serving import saved_model as sm
+    from mifx.serving.resp_server import RespClient, RespError, RespServer, _Reader, encode, saved_model_blob
+
+    with pytest.raises(ValueError):
+        RespServer(host="0.0.0.0", port=0)  # no password on a non-loopback address
+    _export(str(tmp_path / "f"), 1, 3)
+    evil = tmp_path / "evil"
+    (evil / "variables").mkdir(parents=True)
+    from safetensors.torch import save_file
+
+    save_file({}, str(evil / "variables" / "variables.safetensors"))
+    (evil / "saved_model.json").write_text(_json.dumps({
+        "format": sm.FORMAT, "family": "module", "model_class": "mifx.trainer.distributed:run_ranks",
+        "model_config": {"args": ["-c", "open('/tmp/pwned','w')"], "num_procs": 1}, "signatures": {}}))
+    with pytest.raises(PermissionError):
+        sm.LoadedModel(str(evil), "cpu")  # the loader itself enforces the allow-list
+    srv = RespServer(port=0, requirepass="s3cret", model_roots=[str(tmp_path / "f")])
+    port = srv.start()
+    try:
+        c = RespClient("127.0.0.1", port)
+        with pytest.raises(RespError, match="NOAUTH"):
+            c.execute_command("KEYS", "*")
+        with pytest.raises(RespError, match="WRONGPASS"):
+            c.execute_command("AUTH", "nope")
+        assert c.execute_command("AUTH", "s3cret") == "OK"
+        with pytest.raises(RespError, match="allow-list"):
+            c.execute_command("AI.MODELSET", "m", "MIFX", "CPU", "BLOB", saved_model_blob(str(evil)))
+        with pytest.raises(RespError, match="model roots"):
+            c.execute_command("AI.MODELSET", "m", "MIFX", "CPU", "PATH", str(evil))
+        assert c.execute_command("AI.MODELSET", "m", "MIFX", "CPU", "PATH", str(tmp_path / "f" / "1")) == "OK"
+        gz = io.BytesIO()
+        with tarfile.open(fileobj=gz, mode="w:gz") as tf:
+            tf.add(str(tmp_path / "f" / "1"), arcname=".")
+        with pytest.raises(RespError, match="uncompressed"):
+            c.execute_command("AI.MODELSET", "m2", "MIFX", "CPU", "BLOB", gz.getvalue())
+        c.close()
+        c2 = RespClient("127.0.0.1", port, password="s3cret")
+        assert c2.ping()
+        c2.close()
+    finally:
+        srv.stop()
+    a, b = _socket.socketpair()
+    a.sendall(b"*1\r\n" * 64 + b":1\r\n")
+    with pytest.raises(ValueError, match="nested"):
+        _Reader(b).value()
+    a.sendall(encode([1]).replace(b"*1", b"*99999999"))
+    with pytest.raises(ValueError, match="too long"):
+        _Reader(b).value()
+    a.close()
+    b.close()
+
+
 def test_resp_codec_round_trip():
     import socket as _socket
 

@@ -82,3 +82,49 @@ def test_fused_sgd_in_captured_graph_follows_device_lr():
     torch.cuda.synchronize()
     torch.testing.assert_close(p[0], ref[0][0], rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(b[0], ref[1][0], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_fused_sgd_capture_keeps_addresses_and_invalidates_weight_images():
+    """(1) A set_grads after a capture does not retarget the captured graph (each capture owns its address buffer).
+    (2) The update bumps the parameters' version counters, so the bf16 weight images refreshed before it are stale:
+    an eager conv forward after the captured step equals F.conv2d with the CURRENT weights."""
+    import torch.nn.functional as F
+
+    from mifx.ops import conv1x1
+    from mifx.ops.sgd import FusedSGDTables
+    from mifx.ops.weight_prep import WeightPrep, images
+
+    torch.manual_seed(3)
+    w = torch.randn(128, 64, 1, 1, device="cuda") * 0.1
+    b = torch.zeros_like(w)
+    g = [torch.randn_like(w)]
+    other = [torch.randn_like(w) * 100]
+    prep = WeightPrep([w])
+    neg_lr = torch.tensor(-0.5, device="cuda")
+    tab = FusedSGDTables([w], [b], [0.0])
+    with pytest.raises(RuntimeError):
+        tab.step(neg_lr, 0.9, 0.0, False)  # no gradients yet
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            prep.refresh()
+            tab.set_grads(g)
+            tab.step(neg_lr, 0.9, 0.0, False)
+    torch.cuda.current_stream().wait_stream(s)
+    tab.set_grads(other)  # eager retarget: must not leak into the graph
+    w0 = w.clone()
+    graph.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(w, w0 - 0.5 * g[0], rtol=1e-6, atol=1e-6)  # momentum buffer was zero
+    assert images(w) is None  # the images predate the update
+    x = torch.randn(4, 64, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    assert conv1x1.eligible(x, w)
+    y = conv1x1.conv1x1(x, w)[0]
+    ref = F.conv2d(x.float(), w.float())
+    torch.testing.assert_close(y.float(), ref, rtol=3e-2, atol=3e-2)
+    stale = F.conv2d(x.float(), w0.float())
+    assert (y.float() - stale).abs().max() > 10 * (y.float() - ref).abs().max()  # the update is visible
+    prep.close()
