@@ -22,6 +22,18 @@
 // arrives sets the sticky err flag; every later kernel of this group then does nothing (the host raises at its
 // next check) instead of hanging the GPU. Data moves as 8-byte system-scope accesses (write-through stores, L2-
 // bypassing loads), so no cache maintenance is needed anywhere.
+//
+// Split waits (mifx_tpar_allreduce2 with waiters = 1): kernels B and C above spin inside their data-moving workgroups,
+// one per chunk -- thousands of waves that can hold every CU while a peer is late. A kernel that needs whole CUs
+// (csrc/gemm8.hip's 8-wave workgroups: the deferred weight-gradient flush) then cannot start, on another rank's stream
+// sharing the GPU or on this rank's own compute stream while the exchange runs on a side stream (data parallelism).
+// With split waits NO data-moving workgroup ever waits: each data kernel's last-arriving workgroup (an arrival
+// counter, no spinning) stamps ONE per-rank flag in every peer, and the waiting is done by a separate one-wave kernel
+// (tpar_wait: lane p polls peer p's stamp with s_sleep backoff, bounded by the same timeout) between the data kernels:
+//   publish -> wait(phase 0) -> reduce -> wait(phase 1) -> gather.
+// Two more launches per all-reduce, a footprint of one wave while waiting. The per-rank stamps reuse the chunk-0
+// flag slots; the double-buffering argument is unchanged (every data kernel of epoch e + 1 runs after a wait that saw
+// all peers' epoch e + 1 stamps, issued after their epoch e reads).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -193,6 +205,116 @@ __global__ __launch_bounds__(WG) void tpar_gather(uint64_t* __restrict__ y, long
   }
 }
 
+// ---- split waits (see the header): data kernels that never wait, and the one-wave waiter
+
+// the last of `n` arriving workgroups (counter reset for the next call) stamps epoch e as flag[phase][0][rank] in every
+// peer; every workgroup's own stores were acknowledged before its arrival
+__device__ __forceinline__ void arrive_and_stamp(unsigned int* cnt, unsigned int n, const Peers& pe, int world, int rank,
+                                                 int nchunks, int phase, unsigned int e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned int old = 0;
+  if (threadIdx.x == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0);
+  if (old != n - 1) return;
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < world) publish(pe.flag[threadIdx.x] + ((size_t)phase * nchunks + 0) * MAXW + rank, e);
+}
+
+__global__ __launch_bounds__(WG) void tpar_publish_s(const uint64_t* __restrict__ x, long long n4, Peers pe, int world,
+                                                     int rank, long long npad4, const long long* __restrict__ ep,
+                                                     const int* __restrict__ err, int nchunks,
+                                                     unsigned int* __restrict__ cnt) {
+  if (failed(err)) return;
+  const long long e = ep[0] + 1;
+  const int c = blockIdx.x;
+  uint64_t* dst = pe.buf[rank] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+  const long long base = (long long)c * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const long long q = base + i * WG + threadIdx.x;
+    st_sys64(dst + i * WG + threadIdx.x, q < n4 ? x[q] : 0ull);
+  }
+  arrive_and_stamp(cnt, gridDim.x, pe, world, rank, nchunks, 0, (unsigned int)e);
+}
+
+// one wave: lane p < world waits for peer p's stamp of `phase`; a timeout (or an earlier failure) leaves err set and
+// every later kernel of the group a no-op
+__global__ __launch_bounds__(WG) void tpar_wait(Peers pe, int world, int rank, const long long* __restrict__ ep,
+                                                int* __restrict__ err, int nchunks, int phase) {
+  if (failed(err)) return;
+  const unsigned int e = (unsigned int)(ep[0] + 1);
+  if (threadIdx.x < world) wait_flag(pe.flag[rank] + ((size_t)phase * nchunks + 0) * MAXW + threadIdx.x, e, err);
+}
+
+template <bool F32>
+__global__ __launch_bounds__(WG) void tpar_reduce_s(Peers pe, int world, int rank, long long npad4,
+                                                    const long long* __restrict__ ep, int* __restrict__ err,
+                                                    int nchunks, int nch, float scale, unsigned int* __restrict__ cnt) {
+  if (failed(err)) return;
+  const long long e = ep[0] + 1;
+  const int c = rank + world * blockIdx.x;
+  if (c < nch) {
+    const size_t off = (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+    uint64_t* dst = pe.red[rank] + off;
+#pragma unroll 4
+    for (int i = 0; i < PER_LANE; ++i) {
+      const int q = i * WG + threadIdx.x;
+      uint64_t v[MAXW];
+#pragma unroll
+      for (int p = 0; p < MAXW; ++p) v[p] = p < world ? ld_sys64(pe.buf[p] + off + q) : 0ull;
+      if constexpr (F32) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int p = 0; p < MAXW; ++p)  // rank order: the same fp32 sum on every rank
+          if (p < world) {
+            s0 += __uint_as_float((uint32_t)v[p]);
+            s1 += __uint_as_float((uint32_t)(v[p] >> 32));
+          }
+        st_sys64(dst + q, (uint64_t)__float_as_uint(s0 * scale) | ((uint64_t)__float_as_uint(s1 * scale) << 32));
+      } else {
+        float sm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < MAXW; ++p)
+          if (p < world) {
+            const float2 a = bf2f((uint32_t)v[p]), b = bf2f((uint32_t)(v[p] >> 32));
+            sm[0] += a.x;
+            sm[1] += a.y;
+            sm[2] += b.x;
+            sm[3] += b.y;
+          }
+        st_sys64(dst + q, (uint64_t)f2bf(sm[0], sm[1]) | ((uint64_t)f2bf(sm[2], sm[3]) << 32));
+      }
+    }
+  }
+  arrive_and_stamp(cnt, gridDim.x, pe, world, rank, nchunks, 1, (unsigned int)e);
+}
+
+__global__ __launch_bounds__(WG) void tpar_gather_s(uint64_t* __restrict__ y, long long n4, Peers pe, int world,
+                                                    int rank, long long npad4, long long* __restrict__ ep,
+                                                    int* __restrict__ err, unsigned int* __restrict__ done, int f32) {
+  const int c = blockIdx.x, owner = c % world;
+  if (failed(err)) {
+    poison(y, n4, c, f32);
+    return;
+  }
+  const long long e = ep[0] + 1;
+  const uint64_t* src = pe.red[owner] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+  const long long base = (long long)c * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const long long q = base + i * WG + threadIdx.x;
+    const uint64_t v = ld_sys64(src + i * WG + threadIdx.x);
+    if (q < n4) y[q] = v;
+  }
+  if (threadIdx.x == 0) {
+    const unsigned int old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned int)gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ep[0] = e;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -205,7 +327,7 @@ int mifx_tpar_chunk() { return CHUNK; }
 // zero), err: sticky int flag (device). Three kernels on `stream`.
 static int tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, void* const* reds,
                           void* const* flags, int world, int rank, long long npad, long long* ep, unsigned int* done,
-                          int* err, bool f32, float scale, hipStream_t stream) {
+                          int* err, bool f32, float scale, bool waiters, hipStream_t stream) {
   if (world < 1 || world > MAXW || rank < 0 || rank >= world || n <= 0 || n % 4 != 0 || npad % CHUNK != 0 ||
       n > npad || x == nullptr || y == nullptr || ep == nullptr || done == nullptr || err == nullptr)
     return -1;
@@ -220,6 +342,22 @@ static int tpar_allreduce(const void* x, void* y, long long n, void* const* bufs
   const int nchunks = (int)((n + CHUNK - 1) / CHUNK);
   const int nchunks_all = (int)(npad / CHUNK);  // the flag array's chunk dimension
   const long long n4 = n / 4, npad4 = npad / 4;
+  if (waiters) {  // done: [0] gather arrivals, [1] publish arrivals, [2] reduce arrivals
+    const int rgrid = (nchunks + world - 1) / world;
+    hipLaunchKernelGGL(tpar_publish_s, dim3(nchunks), dim3(WG), 0, stream, (const uint64_t*)x, n4, pe, world, rank,
+                       npad4, ep, err, nchunks_all, done + 1);
+    hipLaunchKernelGGL(tpar_wait, dim3(1), dim3(WG), 0, stream, pe, world, rank, ep, err, nchunks_all, 0);
+    if (f32)
+      hipLaunchKernelGGL(tpar_reduce_s<true>, dim3(rgrid), dim3(WG), 0, stream, pe, world, rank, npad4, ep, err,
+                         nchunks_all, nchunks, scale, done + 2);
+    else
+      hipLaunchKernelGGL(tpar_reduce_s<false>, dim3(rgrid), dim3(WG), 0, stream, pe, world, rank, npad4, ep, err,
+                         nchunks_all, nchunks, 1.f, done + 2);
+    hipLaunchKernelGGL(tpar_wait, dim3(1), dim3(WG), 0, stream, pe, world, rank, ep, err, nchunks_all, 1);
+    hipLaunchKernelGGL(tpar_gather_s, dim3(nchunks), dim3(WG), 0, stream, (uint64_t*)y, n4, pe, world, rank, npad4,
+                       ep, err, done, (int)f32);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(tpar_publish, dim3(nchunks), dim3(WG), 0, stream, (const uint64_t*)x, n4, pe, world, rank, npad4,
                      ep, err, nchunks_all);
   if (f32)
@@ -236,7 +374,7 @@ static int tpar_allreduce(const void* x, void* y, long long n, void* const* bufs
 int mifx_tpar_allreduce(const void* x, void* y, long long n, void* const* bufs, void* const* reds, void* const* flags,
                         int world, int rank, long long npad, long long* ep, unsigned int* done, int* err,
                         hipStream_t stream) {
-  return tpar_allreduce(x, y, n, bufs, reds, flags, world, rank, npad, ep, done, err, false, 1.f, stream);
+  return tpar_allreduce(x, y, n, bufs, reds, flags, world, rank, npad, ep, done, err, false, 1.f, false, stream);
 }
 
 // fp32 variant (DP gradient buckets): n = fp32 elements (even), npad = the buffers' capacity in bf16-element units
@@ -245,7 +383,23 @@ int mifx_tpar_allreduce_f32(const void* x, void* y, long long n, void* const* bu
                             void* const* flags, int world, int rank, long long npad, long long* ep, unsigned int* done,
                             int* err, float scale, hipStream_t stream) {
   if (n <= 0 || n % 2 != 0) return -1;
-  return tpar_allreduce(x, y, 2 * n, bufs, reds, flags, world, rank, npad, ep, done, err, true, scale, stream);
+  return tpar_allreduce(x, y, 2 * n, bufs, reds, flags, world, rank, npad, ep, done, err, true, scale, false, stream);
+}
+
+// Either dtype (f32: n = fp32 elements, even; else bf16, n % 4 == 0) and either wait placement: waiters = 1 runs the
+// split-wait sequence (publish / wait / reduce / wait / gather: no data-moving workgroup ever spins), 0 the three
+// kernels with the waits inside. done: uint32 [3] arrival counters (zero). scale: fp32 only.
+int mifx_tpar_allreduce2(const void* x, void* y, long long n, void* const* bufs, void* const* reds, void* const* flags,
+                         int world, int rank, long long npad, long long* ep, unsigned int* done, int* err, int f32,
+                         float scale, int waiters, hipStream_t stream) {
+  if (f32) {
+    if (n <= 0 || n % 2 != 0) return -1;
+    n *= 2;
+  } else if (scale != 1.f) {
+    return -1;
+  }
+  return tpar_allreduce(x, y, n, bufs, reds, flags, world, rank, npad, ep, done, err, f32 != 0, scale, waiters != 0,
+                        stream);
 }
 
 }  // extern "C"

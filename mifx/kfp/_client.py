@@ -100,11 +100,15 @@ class _RestBackend:
 class _LocalBackend:
     """Experiments/runs/pipelines as JSON files; runs execute through the local workflow executor."""
 
-    def __init__(self, root: str, max_parallel: int = 4):
+    def __init__(self, root: str, max_parallel: int = 4, steps_factory=None):
+        """steps_factory: () -> a step runner for each run (mifx.kfp.local.kube.KubeStepRunner: every step a Pod on
+        the cluster); None runs the steps on this host."""
         self.root = os.path.abspath(root)
         for d in ("experiments", "runs", "pipelines"):
             os.makedirs(os.path.join(self.root, d), exist_ok=True)
         self.max_parallel = max_parallel
+        self.steps_factory = steps_factory
+        self.executor = "kubernetes" if steps_factory is not None else "local"
         self._threads: dict[str, threading.Thread] = {}
         self._lock = threading.Lock()
 
@@ -176,7 +180,8 @@ class _LocalBackend:
 
         def body_fn():
             try:
-                st = LocalWorkflowExecutor(wf, run_dir, params, max_parallel=self.max_parallel).run()
+                steps = self.steps_factory() if self.steps_factory is not None else None
+                st = LocalWorkflowExecutor(wf, run_dir, params, max_parallel=self.max_parallel, steps=steps).run()
                 phase = st["phase"]
             except Exception as e:  # noqa: BLE001 - recorded as the run's failure
                 st, phase = {"phase": "Error", "message": str(e)}, "Error"

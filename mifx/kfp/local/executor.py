@@ -1,10 +1,12 @@
 """Local Argo-workflow executor: runs a compiled pipeline (the compiler's Workflow dict) on this host.
 
-This is the offline stand-in for the Argo controller the reference deploys
-(`sdk/python/kfp/compiler/compiler.py` emits the Workflow; Argo executes it in-cluster). Semantics
-implemented: `dag` templates (dependencies, `when` conditions, DAG output parameters), `container`
-templates run as host subprocesses (the image is recorded, not pulled), `resource` templates
-(manifest recorded, success/failure conditions not evaluated), `{{inputs.parameters.*}}`,
+This is the Argo controller's role for the pipelines the compiler emits (`sdk/python/kfp/compiler/compiler.py`
+emits the Workflow; the reference's Argo executes it in-cluster). Semantics implemented: `dag` templates
+(dependencies, `when` conditions, DAG output parameters), `container` and `resource` templates through a step runner
+-- by default on this host (containers as host subprocesses: the image is recorded, not pulled; resource manifests
+recorded), with `steps=mifx.kfp.local.kube.KubeStepRunner(api)` on a Kubernetes cluster (one Pod per step with its
+image, volumes / PVCs, `amd.com/gpu` limits and sidecars; resource templates applied with their success / failure
+conditions) -- `{{inputs.parameters.*}}`,
 `{{tasks.*.outputs.parameters.*}}`, `{{workflow.parameters.*}}` / name / uid substitution,
 `retryStrategy.limit`, `activeDeadlineSeconds`, `onExit`, recursion (graph components), and
 parallel execution of independent tasks.
@@ -89,7 +91,10 @@ class LocalWorkflowExecutor:
     """Execute one Workflow dict. `run()` returns the final workflow status dict."""
 
     def __init__(self, workflow: dict, run_dir: str, arguments: dict | None = None, max_parallel: int = 4,
-                 env: dict | None = None, timeout: float | None = None, max_depth: int = 64):
+                 env: dict | None = None, timeout: float | None = None, max_depth: int = 64, steps=None):
+        """steps: runner of the container / resource steps (`run_container(ex, tmpl, scope, display, node)`,
+        `run_resource(ex, tmpl, scope, display)`, e.g. kube.KubeStepRunner); None runs them on this host."""
+        self.steps = steps
         self.wf = workflow
         self.spec = workflow["spec"]
         self.templates = {t["name"]: t for t in self.spec["templates"]}
@@ -118,7 +123,8 @@ class LocalWorkflowExecutor:
     # ---- helpers -----------------------------------------------------------------------------
     def _global_scope(self) -> dict:
         s = {f"workflow.parameters.{k}": v for k, v in self.params.items()}
-        s.update({"workflow.name": self.name, "workflow.uid": self.uid, "workflow.namespace": "local"})
+        s.update({"workflow.name": self.name, "workflow.uid": self.uid,
+                  "workflow.namespace": getattr(self.steps, "ns", "local")})
         if self._wf_status is not None:
             s["workflow.status"] = self._wf_status
         return s
@@ -193,8 +199,13 @@ class LocalWorkflowExecutor:
                 try:
                     if "dag" in tmpl:
                         outputs = self._exec_dag(tmpl, scope, display, depth, node)
+                    elif "container" in tmpl and self.steps is not None:
+                        with self._slots:
+                            outputs = self.steps.run_container(self, tmpl, scope, display, node)
                     elif "container" in tmpl:
                         outputs = self._exec_container(tmpl, scope, display, node)
+                    elif "resource" in tmpl and self.steps is not None:
+                        outputs = self.steps.run_resource(self, tmpl, scope, display)
                     elif "resource" in tmpl:
                         outputs = self._exec_resource(tmpl, scope, display)
                     else:

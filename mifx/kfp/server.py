@@ -1,5 +1,5 @@
-"""Pipelines API server: the `ml-pipeline` REST API v1beta1 subset the SDK client uses, backed by the
-host-local executor.
+"""Pipelines API server: the `ml-pipeline` REST API v1beta1 subset the SDK client uses, backed by the workflow
+executor -- steps on this host, or (`--executor kubernetes`) one Pod per step on the cluster.
 
 Reference: the KFP API server the workshop deploys (`install-kubeflow/ks_app/vendor/kubeflow/pipeline`
 prototypes, api-server on 8888) and the client calls in `sdk/python/kfp/_client.py:124-316`
@@ -26,10 +26,11 @@ def parse_multipart(body: bytes, content_type: str) -> dict:
     return out
 
 
-def create_app(root: str, max_parallel: int = 4):
+def create_app(root: str, max_parallel: int = 4, steps_factory=None):
+    """steps_factory: per-run step runner (None: steps on this host; see `main --executor kubernetes`)."""
     from fastapi import FastAPI, HTTPException, Request
 
-    backend = _LocalBackend(root, max_parallel)
+    backend = _LocalBackend(root, max_parallel, steps_factory)
     app = FastAPI(title="mifx pipelines API")
 
     def _page(req: Request):
@@ -89,7 +90,7 @@ def create_app(root: str, max_parallel: int = 4):
 
     @app.get("/apis/v1beta1/healthz")
     def healthz():
-        return {"status": "ok", "backend": "local", "root": backend.root}
+        return {"status": "ok", "backend": backend.executor, "root": backend.root}
 
     # ---- pipelines UI (mifx.kfp.ui): read-only HTML views
     from fastapi.responses import HTMLResponse
@@ -123,10 +124,21 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=8888)
     ap.add_argument("--root", default=os.path.join(os.path.expanduser("~"), ".mifx", "pipelines"))
     ap.add_argument("--max-parallel", type=int, default=4)
+    ap.add_argument("--executor", choices=("local", "kubernetes"), default=os.environ.get("MIFX_KFP_EXECUTOR", "local"),
+                    help="where pipeline steps run: this host, or one Pod per step through the Kubernetes API "
+                         "(in-cluster service account; the Argo controller's role)")
+    ap.add_argument("--namespace", default=os.environ.get("POD_NAMESPACE", "kubeflow"))
     a = ap.parse_args(argv)
     import uvicorn
 
-    uvicorn.run(create_app(a.root, a.max_parallel), host="0.0.0.0", port=a.port, log_level="warning")
+    factory = None
+    if a.executor == "kubernetes":
+        from ..launch.operator import KubeApi
+        from .local.kube import KubeStepRunner
+
+        api = KubeApi()
+        factory = lambda: KubeStepRunner(api, a.namespace)  # noqa: E731
+    uvicorn.run(create_app(a.root, a.max_parallel, factory), host="0.0.0.0", port=a.port, log_level="warning")
 
 
 if __name__ == "__main__":

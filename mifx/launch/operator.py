@@ -234,6 +234,21 @@ class KubeApi:
         r.raise_for_status()
         return r.json()
 
+    def patch(self, path: str, body: dict, content_type: str = "application/merge-patch+json"):
+        r = self.s.patch(self.base + path, data=json.dumps(body), timeout=30, headers={"Content-Type": content_type})
+        r.raise_for_status()
+        return r.json()
+
+    def delete(self, path: str):
+        r = self.s.delete(self.base + path, timeout=30)
+        if r.status_code not in (200, 202, 404):
+            r.raise_for_status()
+
+    def get_text(self, path: str) -> str:
+        r = self.s.get(self.base + path, timeout=60)
+        r.raise_for_status()
+        return r.text
+
     def patch_status(self, path: str, status: dict):
         r = self.s.patch(self.base + path + "/status", data=json.dumps({"status": status}), timeout=30,
                          headers={"Content-Type": "application/merge-patch+json"})

@@ -237,20 +237,48 @@ def _dw_tensor(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 # and no second summing kernel, instead of one small launch per weight (BERT-base: 48 per step). The flush writes each
 # result into the weight's .grad -- whatever tensor autograd ended up storing there -- so the gradients must be reset
 # (None or zero) before the backward and each weight may receive ONE recorded product per flush.
-_DEFER: dict = {"on": False, "pending": [], "pending_f32": []}
+_DEFER: dict = {"on": False, "pending": [], "pending_f32": [], "view_of": None}
 # token rows per split-K item of the fp32 (convolution) weight gradients; MIFX_WGRAD_CHUNK overrides (A/B)
 _WGRAD_CHUNK = int(os.environ.get("MIFX_WGRAD_CHUNK", "4096"))
 
 
 class deferred_weight_grads:
+    """view_of: optional callable weight -> a FRESH tensor view of the memory that should hold its gradient (the
+    data-parallel bucket view, mifx.parallel.ddp.DataParallel.grad_view), or None. A weight whose .grad is None then
+    gets that view as its placeholder: autograd adopts it as .grad (no copy, no zero-fill + add) and the flush writes the
+    product straight into the bucket."""
+
+    def __init__(self, view_of=None):
+        self.view_of = view_of
+
     def __enter__(self):
-        self.prev = _DEFER["on"]
+        self.prev = (_DEFER["on"], _DEFER.get("view_of"))
         _DEFER["on"] = True
+        _DEFER["view_of"] = self.view_of
         return self
 
     def __exit__(self, *exc):
-        _DEFER["on"] = self.prev
+        _DEFER["on"], _DEFER["view_of"] = self.prev
         return False
+
+
+def _placeholder(w: torch.Tensor) -> tuple[torch.Tensor, bool]:
+    """(placeholder gradient for autograd, overwrite). w.grad None: autograd stores the returned tensor as .grad
+    untouched, so it may be uninitialised -- the bucket view when a provider gives one -- and the flush OVERWRITES it;
+    otherwise autograd adds the placeholder into the existing gradient (micro-batch accumulation): zeros, and the flush
+    ADDS."""
+    if w.grad is not None:
+        return torch.zeros_like(w), False
+    vf = _DEFER.get("view_of")
+    v = vf(w) if vf is not None else None
+    if v is not None and v.shape == w.shape and v.stride() == w.stride() and v.dtype == w.dtype:
+        return v, True
+    return torch.empty_like(w), True
+
+
+def pending_weights() -> set:
+    """ids of the weights with a recorded (not yet flushed) fp32 weight-gradient product."""
+    return {id(rec[2]) for rec in _DEFER.get("pending_f32", [])}
 
 
 def _defer_ok(dy2: torch.Tensor, x2: torch.Tensor, w) -> bool:
@@ -278,11 +306,7 @@ def defer_weight_grad_f32(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, 
     if not tiles or T % 64 or N * K != w.numel():  # (the last two: the narrow 256 x 64 / 64 x 256 tiles)
         return None
     native_stats.count("conv1x1_dW", True)
-    # w.grad None (the trainer zeroes with set_to_none): autograd stores the returned tensor as .grad untouched, so
-    # it may be uninitialised and the flush OVERWRITES it; otherwise autograd adds the placeholder into the existing
-    # gradient (micro-batch accumulation, bucket views): then it is zeros and the flush ADDS
-    overwrite = w.grad is None
-    ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
+    ph, overwrite = _placeholder(w)
     rec = (dy2.contiguous(), x2.contiguous(), w, ph.data_ptr() if overwrite else None)
     _DEFER["pending_f32"].append(rec if bnx is None else rec + (bnx, _WGRAD_CHUNK))
     return ph
@@ -305,8 +329,7 @@ def defer_conv3x3_weight_grad_f32(dy2: torch.Tensor, x: torch.Tensor, w: torch.T
         return None
     geo = conv_geo(nb, h, w_, c, stride, pad, x.device)
     native_stats.count("conv3x3_dW", True)
-    overwrite = w.grad is None
-    ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
+    ph, overwrite = _placeholder(w)
     _DEFER["pending_f32"].append((dy2.contiguous(), x.contiguous(), w, ph.data_ptr() if overwrite else None, geo,
                                   2048))
     return ph
@@ -325,16 +348,23 @@ def defer_strided1x1_weight_grad_f32(dy2: torch.Tensor, x: torch.Tensor, w: torc
         return None
     geo = conv_geo(nb, h, w_, c, stride, 1, x.device, center1x1=True)
     native_stats.count("conv1x1_dW", True)
-    overwrite = w.grad is None
-    ph = torch.empty_like(w) if overwrite else torch.zeros_like(w)
+    ph, overwrite = _placeholder(w)
     _DEFER["pending_f32"].append((dy2.contiguous(), x.contiguous(), w, ph.data_ptr() if overwrite else None, geo,
                                   _WGRAD_CHUNK))
     return ph
 
 
-def flush_weight_grads() -> int:
-    """Run every recorded weight gradient as one grouped launch into the weights' .grad; returns how many."""
-    pf, _DEFER["pending_f32"] = _DEFER.get("pending_f32", []), []
+def flush_weight_grads(weights=None) -> int:
+    """Run every recorded weight gradient as one grouped launch into the weights' .grad; returns how many.
+    weights: only the fp32 products of these weights (one data-parallel bucket: its exchange can start right after),
+    the others stay recorded."""
+    pf_all = _DEFER.get("pending_f32", [])
+    if weights is not None:
+        ids = {id(w) for w in weights}
+        pf = [r for r in pf_all if id(r[2]) in ids]
+        _DEFER["pending_f32"] = [r for r in pf_all if id(r[2]) not in ids]
+    else:
+        pf, _DEFER["pending_f32"] = pf_all, []
     nf = 0
     if pf:
         probs, acc = [], []
@@ -361,6 +391,8 @@ def flush_weight_grads() -> int:
             acc.append(ph is None)
         gemm8_tn_grouped(probs, accumulate=acc)
         nf = len(pf)
+    if weights is not None:
+        return nf
     pend, _DEFER["pending"] = _DEFER["pending"], []
     if not pend:
         return nf

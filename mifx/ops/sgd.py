@@ -34,6 +34,8 @@ class FusedSGDTables:
     weight decay; the gradients' addresses are set per step (`set_grads`). The tables hold raw addresses: rebuild
     them (`matches`) when a parameter or momentum buffer is reallocated."""
 
+    CAPTURES = 4  # graph captures one table set can serve (each keeps its own pinned address buffer)
+
     def __init__(self, params, bufs, wds, grads=None):
         dev = params[0].device
         # the update is elementwise, so any dense layout works (channels_last convolution weights) as long as a
@@ -62,6 +64,7 @@ class FusedSGDTables:
         self.nblocks = len(tp)
         self.grads = None
         self._captured_hosts: list = []
+        self._spare_hosts = [torch.zeros(len(params), dtype=torch.int64).pin_memory() for _ in range(self.CAPTURES)]
         if grads is not None:
             self.set_grads(grads)
 
@@ -81,9 +84,12 @@ class FusedSGDTables:
             raise ValueError("fused SGD: gradient layouts differ from their parameters'")
         capturing = torch.cuda.is_current_stream_capturing()
         if capturing:
-            # the copy node re-reads its host buffer on every replay: give each capture a buffer of its own, kept
-            # alive with the tables and never written again, so a later set_grads cannot retarget a captured graph
-            host = torch.zeros(len(self.params), dtype=torch.int64).pin_memory()
+            # the copy node re-reads its host buffer on every replay: give each capture a buffer of its own (pinned
+            # ahead of time: no host allocation inside a capture), never written again, so a later set_grads cannot
+            # retarget a captured graph
+            if not self._spare_hosts:
+                raise RuntimeError("fused SGD: more captures than reserved address buffers; rebuild the tables")
+            host = self._spare_hosts.pop()
             self._captured_hosts.append(host)
         else:  # eager: the pinned buffer may still feed an earlier asynchronous copy
             torch.cuda.current_stream(self.gp.device).synchronize()

@@ -96,6 +96,7 @@ class DataParallel:
         dev = params[0].device if params else torch.device("cpu")
         self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self._next = 0  # the next bucket to launch (buckets launch in order)
+        self.deferred = False  # set by a trainer whose backward records weight gradients for grouped flushes
         self._ipc = None
         if exchange != "rccl" and self.active:
             self._ipc = self._open_ipc(dev, required=exchange == "ipc")
@@ -118,7 +119,9 @@ class DataParallel:
         from .tp_ipc import IpcAllReduce
 
         try:
-            return IpcAllReduce(self.pg, dev, max(b.numel for b in self.buckets), dtype=torch.float32)
+            # split waits: the exchange runs on a side stream beside the backward's whole-CU GEMM kernels (the
+            # deferred weight-gradient flushes), so no exchange workgroup may spin on a late peer
+            return IpcAllReduce(self.pg, dev, max(b.numel for b in self.buckets), dtype=torch.float32, waiters=True)
         except RuntimeError:
             if required:
                 raise
@@ -163,12 +166,46 @@ class DataParallel:
             view.copy_(p.grad.reshape(-1))
         elif p.grad.data_ptr() != view.data_ptr():
             # views mode assumes p.grad IS the bucket view; something replaced it (optimizer.zero_grad() with
-            # set_to_none, a user assignment): copy the fresh gradient into the bucket and re-attach the view, so
-            # the all-reduced bucket and the gradient the optimizer reads stay the same memory
-            view.copy_(p.grad.reshape(-1))
-            p.grad = view.view_as(p)
+            # set_to_none, a weight released for a deferred flush that the flush did not take): copy the fresh
+            # gradient into the bucket and re-attach the view -- in the parameter's own layout (channels_last), so the
+            # all-reduced bucket and the gradient the optimizer reads stay the same memory, element for element
+            v = self._view(b, pi)
+            v.copy_(p.grad)
+            p.grad = v
         if len(b.ready) == len(b.params):
+            self._flush_deferred(b)
             self._launch_ready()
+
+    def _flush_deferred(self, b: _Bucket) -> None:
+        """Deferred weight gradients (mifx.ops.gemm.deferred_weight_grads): the bucket's recorded dW products run as
+        ONE grouped launch on the compute stream, written straight into the bucket views, before its exchange is
+        launched -- so each later bucket's flush overlaps the earlier buckets' exchanges."""
+        if not self.deferred:
+            return
+        from ..ops import gemm as hg
+
+        pend = hg.pending_weights()
+        mine = [p for p in b.params if id(p) in pend]
+        if mine:
+            hg.flush_weight_grads(mine)
+
+    def grad_view(self, p: torch.Tensor) -> torch.Tensor | None:
+        """A fresh view of p's slot in its bucket (bucket-view mode), the placeholder a deferred weight gradient is
+        written into; None for parameters this wrapper does not own."""
+        w = self._where.get(p)
+        if w is None or not self.views:
+            return None
+        return self._view(self.buckets[w[0]], w[1])
+
+    def release_grads_for_defer(self) -> None:
+        """Before a backward with deferred weight gradients: drop the 4-D weights' .grad (their bucket memory stays), so
+        autograd adopts the bucket view handed out as the placeholder (grad_view) instead of adding a zero tensor into
+        the existing view; a weight the flush does not take gets its computed gradient copied back into the bucket by
+        the post-accumulate hook."""
+        for b in self.buckets:
+            for p in b.params:
+                if p.dim() == 4:
+                    p.grad = None
 
     def _launch_ready(self) -> None:
         """Launch every complete bucket from the next one in bucket order on."""
@@ -211,6 +248,7 @@ class DataParallel:
         if not self.active or not self._sync:
             return
         for b in self.buckets[self._next:]:  # (in order: an incomplete bucket holds back its successors)
+            self._flush_deferred(b)
             if b.work is None and not self.views:  # unused params this step: contribute zeros for them
                 for pi, p in enumerate(b.params):
                     if pi not in b.ready:

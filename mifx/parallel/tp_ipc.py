@@ -28,14 +28,28 @@ def _fns():
     lib = _lib.load("tp_allreduce")
     return {"chunk": sig(lib, "mifx_tpar_chunk", []),
             "ar": sig(lib, "mifx_tpar_allreduce", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, VP]),
-            "ar32": sig(lib, "mifx_tpar_allreduce_f32", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, F32, VP])}
+            "ar32": sig(lib, "mifx_tpar_allreduce_f32", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, F32, VP]),
+            "ar2": sig(lib, "mifx_tpar_allreduce2", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, I32, F32, I32,
+                                                    VP])}
+
+
+def _device_key(device) -> str:
+    """Identity of the physical GPU behind `device`, comparable across processes."""
+    props = torch.cuda.get_device_properties(device)
+    u = getattr(props, "uuid", None)
+    return str(u) if u is not None else f"{getattr(props, 'pci_bus_id', '?')}:{getattr(props, 'pci_device_id', '?')}"
 
 
 class IpcAllReduce:
     """All-reduce (sum) of bf16 (or fp32) tensors of up to `max_elems` elements over the ranks of `pg`, one GPU each
     (or ranks sharing one GPU in rehearsals: the IPC path is the same)."""
 
-    def __init__(self, pg, device, max_elems: int, dtype: torch.dtype = torch.bfloat16):
+    def __init__(self, pg, device, max_elems: int, dtype: torch.dtype = torch.bfloat16, waiters: bool | None = None):
+        """waiters: split waits (csrc/tp_allreduce.hip header) -- no data-moving workgroup spins, a one-wave kernel
+        waits between them. Needed whenever the exchange can run concurrently with a kernel that needs whole CUs: the
+        data-parallel exchange on a side stream next to the backward (pass True), or ranks sharing one GPU (rehearsals).
+        None: split when any two ranks of the group share a device, else the three-kernel form (tensor parallelism on
+        the compute stream, one GPU per rank: nothing runs beside it)."""
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("IPC all-reduce: bf16 or fp32")
         self.dtype = dtype
@@ -67,9 +81,16 @@ class IpcAllReduce:
                 mine = tuple(hdl)
         except Exception as e:  # noqa: BLE001 -- agreed on below
             err = f"rank {self.rank}: {e}"
+        try:
+            dkey = _device_key(self.device)
+        except Exception:  # noqa: BLE001 -- unknown identity: treat as its own device
+            dkey = f"rank{self.rank}"
         handles = [None] * self.world
-        dist.all_gather_object(handles, (mine, err), group=pg)
-        self._agree([e for _, e in handles])
+        dist.all_gather_object(handles, (mine, err, dkey), group=pg)
+        self._agree([h[1] for h in handles])
+        self.shared_device = len({h[2] for h in handles}) < self.world
+        self.waiters = bool(self.shared_device if waiters is None else waiters)
+        handles = [(h[0], h[1]) for h in handles]
         cols = [[], [], []]
         try:
             with torch.cuda.device(self.device):
@@ -89,7 +110,7 @@ class IpcAllReduce:
         self._agree(errs)
         self.bufs, self.reds, self.flags = ((VP * self.world)(*c) for c in cols)
         self.ep = torch.zeros(1, dtype=torch.int64, device=self.device)
-        self.done = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.done = torch.zeros(3, dtype=torch.int32, device=self.device)  # gather / publish / reduce arrivals
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         dist.barrier(group=pg)  # every rank's buffers exist (zeroed) before any flag can be stored
 
@@ -117,20 +138,18 @@ class IpcAllReduce:
         x = x.contiguous()
         n = x.numel()
         y = torch.empty_like(x) if out is None else out
-        if self.dtype == torch.float32:
+        f32 = self.dtype == torch.float32
+        if f32:
             if n % 2 or 2 * n > self.npad:
                 raise ValueError(f"{n} fp32 elements: need an even count <= {self.npad // 2}")
-            check(_fns()["ar32"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank,
-                                 self.npad, ptr(self.ep), ptr(self.done), ptr(self.err), float(scale),
-                                 stream_handle(self.device)), "mifx_tpar_allreduce_f32")
-            return y
-        if scale != 1.0:
-            raise ValueError("scale is for the fp32 path")
-        if n % 4 or n > self.npad:
-            raise ValueError(f"{n} elements: need a multiple of 4 and <= {self.npad}")
-        check(_fns()["ar"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank, self.npad,
-                           ptr(self.ep), ptr(self.done), ptr(self.err), stream_handle(self.device)),
-              "mifx_tpar_allreduce")
+        else:
+            if scale != 1.0:
+                raise ValueError("scale is for the fp32 path")
+            if n % 4 or n > self.npad:
+                raise ValueError(f"{n} elements: need a multiple of 4 and <= {self.npad}")
+        check(_fns()["ar2"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank, self.npad,
+                            ptr(self.ep), ptr(self.done), ptr(self.err), int(f32), float(scale), int(self.waiters),
+                            stream_handle(self.device)), "mifx_tpar_allreduce2")
         return y
 
     def check(self) -> None:

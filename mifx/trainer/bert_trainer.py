@@ -109,11 +109,11 @@ class BertTrainer:
         # deferred weight gradients (mifx.ops.gemm.deferred_weight_grads; MIFX_DEFER_DW=0 turns it off): the flat
         # optimizer resets every gradient to None each step, which the flush relies on
         self.defer_dw = cuda and self.flat and not self.async_dw and os.environ.get("MIFX_DEFER_DW", "1") != "0"
-        # (TP ranks sharing one device -- the one-GPU rehearsals: the grouped launch's workgroups need a whole CU's
-        # register file, which the other ranks' spinning all-reduce waves never free, so the rank that flushes
-        # stalls until the peers' waits time out; the per-GEMM weight gradients co-reside with those waves)
-        if self.defer_dw and self.tp.size > 1 and self.tp.size > torch.cuda.device_count():
-            self.defer_dw = False
+        # (TP ranks sharing one device -- the one-GPU rehearsals -- used to need it off: the grouped launch's
+        # workgroups need a whole CU's register file, which the other ranks' spinning all-reduce waves held. The IPC
+        # all-reduce now switches itself to split waits when ranks share a device (mifx.parallel.tp_ipc: no
+        # data-moving workgroup spins, one wave waits), so the flush always finds whole CUs and the rehearsed step is
+        # the shipped one.)
 
     def set_batch(self, ids, tt, am, y) -> None:
         """Next training batch, copied INTO the step's input tensors (a captured hipGraph reads these same

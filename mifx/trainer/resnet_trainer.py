@@ -124,6 +124,9 @@ class ResNetTrainer:
             pg["lr"] = self._lr()
         if self.dp is not None:
             self.dp.zero_grad()  # the bucket buffers ARE the gradients (views): one memset per bucket
+            if self.defer_dw:
+                self.dp.deferred = True
+                self.dp.release_grads_for_defer()  # deferred products are written straight into the bucket views
         else:
             self.opt.zero_grad(set_to_none=True)
         total = 0.0
@@ -139,26 +142,39 @@ class ResNetTrainer:
                 loss = F.cross_entropy(self.model(x).float(), y) / self.accum
             self._count_forward()
             last = m == self.accum - 1
-            if self.dp is not None and not last:
-                with self.dp.no_sync():
-                    loss.backward()
-            elif self.dp is None and self.defer_dw:
-                # the 1x1 convolutions' weight gradients in ONE grouped split-K launch after the backward (fp32,
-                # accumulated into .grad); not under data parallelism, whose bucket all-reduces fire during the
-                # backward as gradients complete
-                from ..ops import gemm as hg
-
-                with hg.deferred_weight_grads():
-                    loss.backward()
-                hg.flush_weight_grads()
-            else:
-                loss.backward()
+            self._backward(loss, last)
             total = total + loss.detach()
         if self.dp is not None:
             self.dp.finish()
         self.opt.step()
         self.step_idx += 1
         return total
+
+    def _backward(self, loss: torch.Tensor, last: bool, sync: bool = True) -> None:
+        """One micro-batch's backward. Deferred weight gradients (the GEMM-shaped convolutions' dW recorded during the
+        backward and run as grouped split-K launches of csrc/gemm8.hip): without data parallelism ONE flush after the
+        backward; with it, each bucket's products are flushed the moment the bucket's last gradient is accumulated,
+        straight into the bucket views, and its exchange launched right after -- so the exchanges overlap the rest of
+        the backward and the later flushes. Micro-batches before the last accumulate locally (no_sync, one flush)."""
+        dp = self.dp if sync else None
+        if not self.defer_dw:
+            if dp is not None and not last:
+                with dp.no_sync():
+                    loss.backward()
+            else:
+                loss.backward()
+            return
+        from ..ops import gemm as hg
+
+        if dp is None or not last:
+            ctx = dp.no_sync() if dp is not None else contextlib.nullcontext()
+            with ctx, hg.deferred_weight_grads(view_of=self.dp.grad_view if self.dp is not None else None):
+                loss.backward()
+            hg.flush_weight_grads()
+            return
+        with hg.deferred_weight_grads(view_of=dp.grad_view):
+            loss.backward()  # the DataParallel hooks flush and exchange bucket by bucket
+        hg.flush_weight_grads()  # (the bf16 products of non-bucketed weights, if any)
 
     # ---------------------------------------------------------------- captured step
     def _graph_step(self) -> torch.Tensor:
@@ -178,10 +194,13 @@ class ResNetTrainer:
         return self._static_loss
 
     def _fwd_bwd_captured(self) -> torch.Tensor:
-        defer = self.dp is None and self.defer_dw
+        defer = self.defer_dw
         if self.dp is not None:
             for b in self.dp.buckets:  # param.grad are views of these
                 b.buf.zero_()
+            if defer:
+                self.dp.deferred = True
+                self.dp.release_grads_for_defer()
         elif defer:
             # gradients produced inside the graph (its private pool: the same addresses on every replay, which the
             # captured SGD reads); the deferred weight-gradient flush then overwrites instead of zero-fill + add
@@ -205,17 +224,9 @@ class ResNetTrainer:
                 with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
                     loss = F.cross_entropy(self.model(x).float(), y) / self.accum
                 self._count_forward()
-                if defer:  # the same backward as the eager steps (deferred grouped weight gradients)
-                    from ..ops import gemm as hg
-
-                    with hg.deferred_weight_grads():
-                        loss.backward()
-                    hg.flush_weight_grads()
-                elif in_graph and m < self.accum - 1:
-                    with self.dp.no_sync():
-                        loss.backward()
-                else:
-                    loss.backward()
+                # the same backward as the eager steps; the exchange captures with it only on the ipc path (RCCL:
+                # the whole graph runs under no_sync and the bucket all-reduces run eagerly between the graphs)
+                self._backward(loss, m == self.accum - 1, sync=in_graph)
                 total = loss.detach() if total is None else total + loss.detach()
         if in_graph:
             self.dp.finish()  # joins the side stream: every bucket exchanged and averaged

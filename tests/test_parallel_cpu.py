@@ -168,6 +168,71 @@ def test_ddp_ipc_exchange_needs_cuda():
         DataParallel(_Net(), exchange="nope")
 
 
+def test_ddp_deferred_flush_per_bucket_before_its_exchange(monkeypatch):
+    """Deferred weight gradients under DataParallel: a bucket's recorded products are flushed (into its views) when the
+    bucket's last gradient arrives, and its exchange is launched right after; a released 4-D weight whose gradient
+    autograd produced itself is copied back into the bucket in the parameter's own (channels_last) layout."""
+    from mifx.ops import gemm as hg
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Conv2d(8, 8, 1),
+                                  torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 4)).to(memory_format=torch.channels_last)
+        dp = DataParallel(net, bucket_cap_mb=0.001, grad_as_bucket_view=True, force=True)
+        assert len(dp.buckets) >= 3
+        dp.deferred = True
+        deferred_w = net[2].weight  # pretend the 1x1 conv's dW was recorded for a grouped flush
+        events, pending = [], {id(deferred_w)}
+        monkeypatch.setattr(hg, "pending_weights", lambda: set(pending))
+
+        def fake_flush(weights=None):
+            for w in weights:
+                events.append(("flush", id(w)))
+                w.grad.fill_(7.0)  # the product, written into the bucket view
+                pending.discard(id(w))
+            return len(weights)
+
+        monkeypatch.setattr(hg, "flush_weight_grads", fake_flush)
+        launch = dp._launch
+
+        def spy(b):
+            events.append(("launch", next(i for i, q in enumerate(dp.buckets) if q is b)))
+            launch(b)
+
+        dp._launch = spy
+        dp.zero_grad()
+        dp.release_grads_for_defer()
+        assert net[0].weight.grad is None and deferred_w.grad is None and net[4].weight.grad is not None
+        x = torch.randn(2, 3, 8, 8).to(memory_format=torch.channels_last)
+
+        class _Defer(torch.autograd.Function):  # what the conv ops do: a placeholder gradient, the product later
+            @staticmethod
+            def forward(ctx, w):
+                return w.clone()
+
+            @staticmethod
+            def backward(ctx, g):
+                return dp.grad_view(deferred_w)
+
+        h = torch.relu(torch.nn.functional.conv2d(x, net[0].weight, net[0].bias))
+        y = net[4](torch.nn.functional.conv2d(h, _Defer.apply(deferred_w), net[2].bias).flatten(1))
+        y.square().sum().backward()
+        dp.finish()
+        bi = dp._where[deferred_w][0]
+        assert events.index(("flush", id(deferred_w))) < events.index(("launch", bi)), events
+        assert [e[1] for e in events if e[0] == "launch"] == list(range(len(dp.buckets)))
+        assert torch.all(deferred_w.grad == 7.0)
+        for p in net.parameters():  # every gradient IS its bucket view, in the parameter's layout
+            b, pi = dp._where[p]
+            v = dp._view(dp.buckets[b], pi)
+            assert p.grad.data_ptr() == v.data_ptr() and p.grad.stride() == p.stride()
+        assert net[0].weight.grad.abs().sum() > 0  # the released weight's own gradient, copied into its bucket
+    finally:
+        dist.destroy_process_group()
+
+
 def test_ddp_check_forwards_the_exchange_error_and_guards_checkpoints(tmp_path):
     """DataParallel.check() raises the peer-memory exchange's sticky timeout, and ResNetTrainer refuses to write a
     checkpoint after one (the later buckets would be NaN)."""

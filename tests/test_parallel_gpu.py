@@ -87,9 +87,10 @@ def _resnet_run(world: int, rank: int, out: str) -> None:
     from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
 
     os.environ["MIFX_DP_EXCHANGE"] = os.environ.get("MIFX_TEST_EXCHANGE", "auto")
-    # the data-parallel backward does not defer weight gradients (buckets exchange as gradients complete): the single
-    # process must take the same weight-gradient kernels, or this chaotic toy run amplifies their rounding difference
-    os.environ["MIFX_DEFER_DW"] = "0"
+    # deferred weight gradients on (the shipped default: per-bucket grouped flushes into the bucket views, each bucket's
+    # exchange launched right after its flush) or off (every weight gradient from the backward itself); the single
+    # process takes the same choice, so both sides run the same weight-gradient kernels
+    os.environ["MIFX_DEFER_DW"] = os.environ.get("MIFX_TEST_DEFER", "1")
 
     imgs, labels = synthetic_imagenet(64, size=72, classes=10, seed=0)  # same data on every rank
     # one process accumulates the 2 micro-batches that the 2 ranks train on (ResNetTrainer's global sample)
@@ -111,8 +112,9 @@ def _resnet_run(world: int, rank: int, out: str) -> None:
     torch.save({"losses": losses, "state": params, "stats": stats, "info": info}, f"{out}.{world}.{rank}")
 
 
-def _resnet_worker(rank, world, port, out, exchange="auto"):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MIFX_TEST_EXCHANGE=exchange)
+def _resnet_worker(rank, world, port, out, exchange="auto", defer="1"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MIFX_TEST_EXCHANGE=exchange,
+                      MIFX_TEST_DEFER=defer)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         _resnet_run(world, rank, out)
@@ -120,15 +122,17 @@ def _resnet_worker(rank, world, port, out, exchange="auto"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["ipc", "rccl"])
-def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single(exchange):
+@pytest.mark.parametrize("exchange,defer", [("ipc", "1"), ("rccl", "1"), ("ipc", "0")])
+def test_resnet50_dp2_on_gpu_replicas_identical_and_match_single(exchange, defer):
     """2 ranks sharing cuda:0 vs one process accumulating both micro-batches. exchange="ipc": the bucket all-reduces
     are the peer-memory kernels on the side stream, captured with the backward and SGD in ONE graph (steps 3+);
-    "rccl": the process group's collective (gloo here) eager between graph A and graph B."""
+    "rccl": the process group's collective (gloo here) eager between graph A and graph B. defer "1": the weight
+    gradients are flushed bucket by bucket into the bucket views (the grouped gemm8 launches run while the other rank's
+    exchange waits on the same GPU: the split-wait exchange keeps whole CUs free for them)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
-        mp.start_processes(_resnet_worker, args=(2, _port(), out, exchange), nprocs=2, start_method="spawn")
-        mp.start_processes(_resnet_worker, args=(1, _port(), out), nprocs=1, start_method="spawn")
+        mp.start_processes(_resnet_worker, args=(2, _port(), out, exchange, defer), nprocs=2, start_method="spawn")
+        mp.start_processes(_resnet_worker, args=(1, _port(), out, "auto", defer), nprocs=1, start_method="spawn")
         r0, r1 = (torch.load(f"{out}.2.{r}", weights_only=True) for r in range(2))
         one = torch.load(f"{out}.1.0", weights_only=True)
     assert r0["info"]["exchange"] == exchange and r0["info"]["graphs"] == (True, exchange == "rccl"), r0["info"]

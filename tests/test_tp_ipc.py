@@ -20,14 +20,16 @@ def _port():
         return s.getsockname()[1]
 
 
-def _ar_worker(rank, world, port, out):
+def _ar_worker(rank, world, port, out, waiters=None):
     from mifx.parallel.tp_ipc import IpcAllReduce
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda", 0)
-        ar = IpcAllReduce(dist.group.WORLD, dev, 1 << 20)
+        ar = IpcAllReduce(dist.group.WORLD, dev, 1 << 20, waiters=waiters)
+        # ranks sharing cuda:0: the automatic choice is the split-wait form
+        assert ar.shared_device and ar.waiters == (True if waiters is None else waiters)
         res = {}
         for i, n in enumerate((4, 4096 * 3 + 8, 1 << 20, 100000)):
             g = torch.Generator().manual_seed(1000 * i + rank)
@@ -67,11 +69,13 @@ def _ar_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_ipc_allreduce_exact_rank_order_sum(world):
+@pytest.mark.parametrize("world,waiters", [(2, None), (4, None), (2, False), (4, False)])
+def test_ipc_allreduce_exact_rank_order_sum(world, waiters):
+    """Both wait placements: split waits (None -> automatic on a shared device: one-wave waiter kernels between
+    data kernels that never spin) and the three-kernel form with the waits inside (False)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "ar")
-        mp.start_processes(_ar_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        mp.start_processes(_ar_worker, args=(world, _port(), out, waiters), nprocs=world, start_method="spawn")
         res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     for i in range(4):
         want = res[0][f"x{i}"].float()
@@ -300,3 +304,57 @@ def test_bert_tp_overlapped_row_parallel_reduce_matches_plain():
         a, b = res[r][1], res[r][4]
         assert all(abs(x - y) <= 2e-2 * max(1.0, abs(x)) for x, y in zip(a, b)), (r, a, b)
     assert res[0][4] == res[1][4]
+
+
+def _hazard_worker(rank, world, port, out):
+    """rank 0 enters a 64 MB fp32 exchange at once; rank 1 first sleeps on the host, then runs a grouped gemm8
+    weight-gradient launch (8-wave workgroups that need a whole CU's register file) on the SAME GPU, and only then
+    joins. With split waits rank 0's exchange holds one waiting wave, so rank 1's launch gets whole CUs and finishes
+    in milliseconds; with the waits inside thousands of spinning waves it would stall until rank 0's 10 s bound."""
+    import time
+
+    from mifx.ops import gemm as hg
+    from mifx.parallel.tp_ipc import IpcAllReduce
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        n = 1 << 24
+        ar = IpcAllReduce(dist.group.WORLD, dev, n, dtype=torch.float32, waiters=True)
+        x = torch.full((n,), float(rank + 1), device=dev)
+        res = {}
+        dist.barrier()
+        if rank == 1:
+            time.sleep(2.0)
+            g = torch.Generator(device=dev).manual_seed(5)
+            a = torch.randn(8192, 1024, device=dev, generator=g).bfloat16()
+            b = torch.randn(8192, 2048, device=dev, generator=g).bfloat16()
+            c = torch.empty(1024, 2048, device=dev)
+            t0 = time.perf_counter()
+            hg.gemm8_tn_grouped([(a, b, c)], accumulate=False)
+            torch.cuda.synchronize(dev)
+            res["gemm_s"] = time.perf_counter() - t0
+            ref = a.float().t() @ b.float()
+            res["gemm_rel"] = float((c - ref).norm() / ref.norm())
+        ar.all_reduce(x, out=x, scale=1.0)
+        torch.cuda.synchronize(dev)
+        res["ok"] = bool(torch.all(x == 3.0))
+        res["err"] = int(ar.err.item())
+        dist.barrier()
+        ar.close()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_wait_exchange_never_starves_whole_cu_kernels():
+    """The co-residence hazard behind the old `defer dW off when TP ranks share a device` rule, exercised directly: a
+    grouped gemm8 flush runs on one rank while the other rank's exchange waits for it (deliberately delayed peer)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "hz")
+        mp.start_processes(_hazard_worker, args=(2, _port(), out), nprocs=2, start_method="spawn")
+        r0, r1 = (torch.load(f"{out}.{r}", weights_only=True) for r in range(2))
+    assert r0["ok"] and r1["ok"] and r0["err"] == 0 and r1["err"] == 0, (r0, r1)
+    assert r1["gemm_rel"] < 1e-2, r1
+    assert r1["gemm_s"] < 2.0, r1  # not held until the 10 s wait bound
