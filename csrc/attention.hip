@@ -37,7 +37,16 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 constexpr int D = 64;        // head dim
-constexpr int LD = D + 8;    // LDS row of a [token][d] image (elements): 144 B rows
+constexpr int LD = D + 8;    // LDS row of a [token][d] image (elements): 144 B rows (the S > 128 kernels)
+// the S <= 128 kernels' row: 160 B. With 144-B rows the score reads (ds_read_b128, rows 16 kt + r) and the transposed
+// V^T / K^T reads (rows 32 ks + 4 h + q) put two rows of a lane group on one bank set (2-way); 160-B rows are
+// conflict-free for both (bank model: tools/lds_banks_attn.py). The backward's 4 images then take 80 KB: still two
+// workgroups per CU. (The long kernels keep 144 B: K and V of S = 512 must fit 160 KB.)
+#ifndef ATTN_LD_SHORT
+#define ATTN_LD_SHORT 80
+#endif
+constexpr int LDS_ = ATTN_LD_SHORT;
+static_assert(LDS_ % 8 == 0 && LDS_ >= D, "16-B aligned rows");
 constexpr v4f kZero4 = {0.f, 0.f, 0.f, 0.f};
 
 __device__ __forceinline__ v4s tr_read(const bf16* p) {
@@ -74,12 +83,12 @@ struct Drop {
   float scale;   // 1 / (1 - p)
 };
 
-// load S rows x 64 of one [B, S, *, 64]-strided tensor into an LDS [S][LD] image (16-B chunks)
+// load S rows x 64 of one [B, S, *, 64]-strided tensor into an LDS [S][LDS_] image (16-B chunks)
 template <int S, int NTHR>
 __device__ __forceinline__ void load_rows(bf16* dst, const bf16* src, size_t row_stride) {
   for (int c = threadIdx.x; c < S * 8; c += NTHR) {
     const int row = c >> 3, ch = c & 7;
-    *(uint4*)(dst + row * LD + ch * 8) = *(const uint4*)(src + (size_t)row * row_stride + ch * 8);
+    *(uint4*)(dst + row * LDS_ + ch * 8) = *(const uint4*)(src + (size_t)row * row_stride + ch * 8);
   }
 }
 
@@ -90,7 +99,7 @@ __device__ __forceinline__ void scores(const bf16* Ks, const v8bf (&qf)[2], v4f 
   for (int kt = 0; kt < S / 16; ++kt) {
     v4f a = kZero4;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Ks + (16 * kt + r) * LD + 32 * ks + 8 * h), qf[ks], a);
+    for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Ks + (16 * kt + r) * LDS_ + 32 * ks + 8 * h), qf[ks], a);
     acc[kt] = a;
   }
 }
@@ -124,8 +133,8 @@ __global__ __launch_bounds__(64 * (S / 16) / QS) void attn_fwd(const bf16* __res
                                                               int H, int h0, int Htot, bf16* __restrict__ out,
                                                               float* __restrict__ lse_out) {
   constexpr int NTHR = 64 * (S / 16) / QS, KT = S / 16, KS = S / 32;
-  __shared__ __attribute__((aligned(16))) bf16 Ks[S * LD];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[S * LD];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[S * LDS_];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[S * LDS_];
   const int bh = blockIdx.x / QS, qpart = blockIdx.x % QS;
   const int b = bh / H, hh = bh % H;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, h = lane >> 4;
@@ -184,8 +193,8 @@ __global__ __launch_bounds__(64 * (S / 16) / QS) void attn_fwd(const bf16* __res
     v4f o = kZero4;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const bf16* pa = Vs + (32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
-      o = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), pb[ks], o);
+      const bf16* pa = Vs + (32 * ks + 4 * h + q) * LDS_ + 16 * dt + 4 * p;
+      o = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LDS_)), pb[ks], o);
     }
     *(v4bf*)(out + ((size_t)b * S + qi) * H * D + (size_t)hh * D + 16 * dt + 4 * h) = pack4(o);
   }
@@ -200,9 +209,9 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
   constexpr int NTHR = 64 * (S / 16), KT = S / 16, KS = S / 32, LP = S + 8;
   extern __shared__ __attribute__((aligned(16))) bf16 smem[];
   bf16* Qs = smem;
-  bf16* Ks = Qs + S * LD;
-  bf16* Vs = Ks + S * LD;
-  bf16* dOs = Vs + S * LD;
+  bf16* Ks = Qs + S * LDS_;
+  bf16* Vs = Ks + S * LDS_;
+  bf16* dOs = Vs + S * LDS_;
   // P_d and dS are staged, one after the other, over the K / V images once those are no longer read
   // ([query][key] rows of S + 8: 17 KB <= the 18 KB of K + V at S = 128): 74 KB of LDS -> two workgroups per CU
   bf16* KV = Ks;
@@ -233,8 +242,8 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
   v8bf qf[2], dof[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    qf[ks] = ld8(Qs + qi * LD + 32 * ks + 8 * h);
-    dof[ks] = ld8(dOs + qi * LD + 32 * ks + 8 * h);
+    qf[ks] = ld8(Qs + qi * LDS_ + 32 * ks + 8 * h);
+    dof[ks] = ld8(dOs + qi * LDS_ + 32 * ks + 8 * h);
   }
   v4f pp[KT];
   scores<S>(Ks, qf, pp, r, h);
@@ -245,7 +254,7 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
   for (int kt = 0; kt < KT; ++kt) {
     v4f a = kZero4;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Vs + (16 * kt + r) * LD + 32 * ks + 8 * h), dof[ks], a);
+    for (int ks = 0; ks < 2; ++ks) a = mfma(ld8(Vs + (16 * kt + r) * LDS_ + 32 * ks + 8 * h), dof[ks], a);
     dp_[kt] = a;
   }
   const uint64_t key = dp.thr ? mifx_rng::drop_key(dp.rng, dp.site) : 0;
@@ -277,8 +286,8 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
     v4f a = kZero4;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const bf16* pa = Ks + (32 * ks + 4 * h + q) * LD + 16 * dt + 4 * p;
-      a = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LD)), dsb[ks], a);
+      const bf16* pa = Ks + (32 * ks + 4 * h + q) * LDS_ + 16 * dt + 4 * p;
+      a = mfma(cat8(tr_read(pa), tr_read(pa + 16 * LDS_)), dsb[ks], a);
     }
     *(v4bf*)(dqkv + ((size_t)b * S + qi) * tok + (size_t)hh * D + 16 * dt + 4 * h) = pack4(a);
   }
@@ -295,9 +304,9 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int row = 32 * s + 8 * h + q;
-      const bf16* pdo = dOs + row * LD + 16 * dt + 4 * p;
+      const bf16* pdo = dOs + row * LDS_ + 16 * dt + 4 * p;
       const bf16* ppd = KV + row * LP + kj + 4 * p;
-      av = mfma(cat8(tr_read(pdo), tr_read(pdo + 4 * LD)), cat8(tr_read(ppd), tr_read(ppd + 4 * LP)), av);
+      av = mfma(cat8(tr_read(pdo), tr_read(pdo + 4 * LDS_)), cat8(tr_read(ppd), tr_read(ppd + 4 * LP)), av);
     }
     *(v4bf*)(dqkv + ((size_t)b * S + kj + r) * tok + (size_t)(2 * H + hh) * D + 16 * dt + 4 * h) = pack4(av);
   }
@@ -311,9 +320,9 @@ __global__ __launch_bounds__(64 * (S / 16)) void attn_bwd(const bf16* __restrict
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int row = 32 * s + 8 * h + q;
-      const bf16* pq = Qs + row * LD + 16 * dt + 4 * p;
+      const bf16* pq = Qs + row * LDS_ + 16 * dt + 4 * p;
       const bf16* pds = KV + row * LP + kj + 4 * p;
-      ak = mfma(cat8(tr_read(pq), tr_read(pq + 4 * LD)), cat8(tr_read(pds), tr_read(pds + 4 * LP)), ak);
+      ak = mfma(cat8(tr_read(pq), tr_read(pq + 4 * LDS_)), cat8(tr_read(pds), tr_read(pds + 4 * LP)), ak);
     }
     *(v4bf*)(dqkv + ((size_t)b * S + kj + r) * tok + (size_t)(H + hh) * D + 16 * dt + 4 * h) = pack4(ak);
   }
@@ -601,8 +610,8 @@ uint32_t drop_threshold(float p) {
 
 template <int S>
 constexpr int bwd_lds() {
-  static_assert(S * (S + 8) <= 2 * S * LD, "P_d / dS staging must fit over the K and V images");
-  return 4 * S * LD * 2;
+  static_assert(S * (S + 8) <= 2 * S * LDS_, "P_d / dS staging must fit over the K and V images");
+  return 4 * S * LDS_ * 2;
 }
 
 }  // namespace

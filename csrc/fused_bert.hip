@@ -85,6 +85,8 @@ using mifx_rng::keep4;
 
 // Drop: the optional (bias, dropout) prologue of the fused LayerNorm: s = keep ? (a + bias) * scale : 0, + r.
 // thr == 0 disables dropout (no hashing); bias == nullptr disables the bias.
+// eoff: the flat element index of row 0 in the full activation (sequence parallelism: a rank's token shard draws the
+// mask bits the whole tensor would, so the masks do not depend on the TP split; 0 otherwise; a multiple of 4)
 template <typename P>
 struct Drop {
   const P* bias;
@@ -92,6 +94,7 @@ struct Drop {
   int site;
   uint32_t thr;
   float scale;
+  unsigned long long eoff;
 };
 
 // ---- vectorised fused [bias +] [dropout +] residual-add + LayerNorm (H % 256 == 0): lane owns NC chunks of
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd_v(const T* __restrict__ a
       float t[4];
       ldv<T, 4>(a + base + c, v[j]);
       ldv<T, 4>(r + base + c, t);
-      const uint32_t k = dp.thr ? keep4(key, (base + c) >> 2, dp.thr) : 0xf;
+      const uint32_t k = dp.thr ? keep4(key, (dp.eoff + base + c) >> 2, dp.thr) : 0xf;
       const float sc = dp.thr ? dp.scale : 1.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd_v(const T* __restrict__ d
       ldv<T, 4>(dy + base + c, d);
       ldv<T, 4>(a + base + c, av);
       ldv<T, 4>(r + base + c, rv);
-      kp[j] = dp.thr ? keep4(key, (base + c) >> 2, dp.thr) : 0xf;
+      kp[j] = dp.thr ? keep4(key, (dp.eoff + base + c) >> 2, dp.thr) : 0xf;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float sv = ((kp[j] >> e) & 1 ? (av[e] + bias[j][e]) * sc : 0.f) + rv[e];
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_fwd(const T* __restrict__ a, 
       const int c = lane + k * 64;
       if (c < H) {
         float x = ld(a + base + c) + (dp.bias != nullptr ? ld(dp.bias + c) : 0.f);
-        if (dp.thr) x = keep1(key, base + c, dp.thr) ? x * dp.scale : 0.f;
+        if (dp.thr) x = keep1(key, dp.eoff + base + c, dp.thr) ? x * dp.scale : 0.f;
         v[k] = x + ld(r + base + c);
       } else {
         v[k] = 0.f;
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(kThreads) void add_ln_bwd(const T* __restrict__ dy,
         const float d = ld(dy + base + c);
         float x = ld(a + base + c) + (dp.bias != nullptr ? ld(dp.bias + c) : 0.f);
         if (dp.thr) {
-          kp[k] = keep1(key, base + c, dp.thr);
+          kp[k] = keep1(key, dp.eoff + base + c, dp.thr);
           x = kp[k] ? x * sc : 0.f;
         }
         xh[k] = (x + ld(r + base + c) - mean) * rstd;
@@ -672,6 +675,7 @@ struct LnArgs {
   int site;
   uint32_t thr;
   float scale;
+  unsigned long long eoff;
   int R, H;
   float eps;
   void *out, *da;  // fwd: y; bwd: dr (out) and da
@@ -682,7 +686,7 @@ struct LnArgs {
 
 template <typename T, typename P, int PER>
 int launch_add_ln(const LnArgs& x) {
-  const Drop<P> dp{(const P*)x.bias, x.rng, x.site, x.thr, x.scale};
+  const Drop<P> dp{(const P*)x.bias, x.rng, x.site, x.thr, x.scale, x.eoff};
   if (x.fwd)
     hipLaunchKernelGGL((add_ln_fwd<T, P, PER>), dim3(x.blocks), dim3(kThreads), 0, x.st, (const T*)x.a, (const T*)x.r,
                        (const P*)x.w, (const P*)x.b, dp, x.R, x.H, x.eps, (T*)x.out, x.mean, x.rstd);
@@ -695,7 +699,7 @@ int launch_add_ln(const LnArgs& x) {
 
 template <typename T, typename P, int NC>
 int launch_add_ln_v(const LnArgs& x) {
-  const Drop<P> dp{(const P*)x.bias, x.rng, x.site, x.thr, x.scale};
+  const Drop<P> dp{(const P*)x.bias, x.rng, x.site, x.thr, x.scale, x.eoff};
   if (x.fwd)
     hipLaunchKernelGGL((add_ln_fwd_v<T, P, NC>), dim3(x.blocks), dim3(kThreads), 0, x.st, (const T*)x.a,
                        (const T*)x.r, (const P*)x.w, (const P*)x.b, dp, x.R, x.eps, (T*)x.out, x.mean, x.rstd);
@@ -1003,10 +1007,19 @@ int mifx_bert_gelu_chunks(int M) { return M < 16 ? 1 : (M / 16 < 512 ? M / 16 : 
 // Fused y = LayerNorm(dropout_p(a [+ bias]) + r) * w + b, and its backward.
 // dtype: activations, pdt: gamma/beta/bias (and their gradients): 0 fp32, 1 bf16. bias may be null; p == 0
 // disables dropout (rng unused). rng: device int64 [seed, counter]; site distinguishes the call sites of a step.
+int mifx_bert_bdaln_fwd2(int dtype, int pdt, const void* a, const void* bias, const void* r, const void* w,
+                         const void* b, int R, int H, float eps, float p, const int64_t* rng, int site, long long eoff,
+                         void* y, float* mean, float* rstd, hipStream_t st);
 int mifx_bert_bdaln_fwd(int dtype, int pdt, const void* a, const void* bias, const void* r, const void* w,
                         const void* b, int R, int H, float eps, float p, const int64_t* rng, int site, void* y,
                         float* mean, float* rstd, hipStream_t st) {
-  if (H <= 0 || H > 64 * kMaxPer || R <= 0 || p < 0.f || p >= 1.f) return -1;
+  return mifx_bert_bdaln_fwd2(dtype, pdt, a, bias, r, w, b, R, H, eps, p, rng, site, 0, y, mean, rstd, st);
+}
+// ... with the dropout mask's element offset eoff (sequence-parallel token shards; % 4 == 0)
+int mifx_bert_bdaln_fwd2(int dtype, int pdt, const void* a, const void* bias, const void* r, const void* w,
+                         const void* b, int R, int H, float eps, float p, const int64_t* rng, int site, long long eoff,
+                         void* y, float* mean, float* rstd, hipStream_t st) {
+  if (H <= 0 || H > 64 * kMaxPer || R <= 0 || p < 0.f || p >= 1.f || eoff < 0 || eoff % 4 != 0) return -1;
   if (p > 0.f && rng == nullptr) return -1;
   const int need = (R + 3) / 4;
   LnArgs x{};
@@ -1020,6 +1033,7 @@ int mifx_bert_bdaln_fwd(int dtype, int pdt, const void* a, const void* bias, con
   x.site = site;
   x.thr = drop_threshold(p);
   x.scale = 1.f / (1.f - p);
+  x.eoff = (unsigned long long)eoff;
   x.R = R;
   x.H = H;
   x.eps = eps;
@@ -1033,10 +1047,21 @@ int mifx_bert_bdaln_fwd(int dtype, int pdt, const void* a, const void* bias, con
 
 // backward: dr = dL/dr, da = dL/da (da may alias dr when there is neither bias nor dropout), dw, db and dbias
 // ([H], parameter dtype; dbias only with a bias). scratch: part [3, mifx_bert_ln_blocks(R), H] fp32.
+int mifx_bert_bdaln_bwd2(int dtype, int pdt, const void* dy, const void* a, const void* bias, const void* r,
+                         const void* w, const float* mean, const float* rstd, int R, int H, float p,
+                         const int64_t* rng, int site, long long eoff, void* dr, void* da, float* part, void* dw,
+                         void* db, void* dbias, hipStream_t st);
 int mifx_bert_bdaln_bwd(int dtype, int pdt, const void* dy, const void* a, const void* bias, const void* r,
                         const void* w, const float* mean, const float* rstd, int R, int H, float p, const int64_t* rng,
                         int site, void* dr, void* da, float* part, void* dw, void* db, void* dbias, hipStream_t st) {
-  if (H <= 0 || H > 64 * kMaxPer || R <= 0 || p < 0.f || p >= 1.f) return -1;
+  return mifx_bert_bdaln_bwd2(dtype, pdt, dy, a, bias, r, w, mean, rstd, R, H, p, rng, site, 0, dr, da, part, dw, db,
+                              dbias, st);
+}
+int mifx_bert_bdaln_bwd2(int dtype, int pdt, const void* dy, const void* a, const void* bias, const void* r,
+                         const void* w, const float* mean, const float* rstd, int R, int H, float p,
+                         const int64_t* rng, int site, long long eoff, void* dr, void* da, float* part, void* dw,
+                         void* db, void* dbias, hipStream_t st) {
+  if (H <= 0 || H > 64 * kMaxPer || R <= 0 || p < 0.f || p >= 1.f || eoff < 0 || eoff % 4 != 0) return -1;
   if (p > 0.f && rng == nullptr) return -1;
   if ((p > 0.f || bias != nullptr) && da == dr) return -1;
   const int blocks = mifx_bert_ln_blocks(R);
@@ -1051,6 +1076,7 @@ int mifx_bert_bdaln_bwd(int dtype, int pdt, const void* dy, const void* a, const
   x.site = site;
   x.thr = drop_threshold(p);
   x.scale = 1.f / (1.f - p);
+  x.eoff = (unsigned long long)eoff;
   x.R = R;
   x.H = H;
   x.out = dr;

@@ -315,6 +315,123 @@ __global__ __launch_bounds__(WG) void tpar_gather_s(uint64_t* __restrict__ y, lo
   }
 }
 
+// ---- sequence parallelism (Megatron-SP): reduce-scatter / all-gather of a token-major [T, H] bf16 activation whose
+// T / world-token shards are contiguous: rank r owns elements [r m, (r + 1) m), m = n / world, m % CHUNK == 0 (so a
+// chunk has one owner: chunk c belongs to rank c / (m / CHUNK)). Both reuse the publish kernels above (the whole
+// partial for a reduce-scatter; for an all-gather only the own shard's chunks, tpar_publish_range) and take one epoch
+// each, like an all-reduce; the double-buffering argument is the all-reduce's (every waiting kernel of epoch e + 1
+// sees at least one stamp from every peer, issued after that peer's epoch-e reads).
+
+// publish chunks [c0, c0 + gridDim) of x (element offset c0 CHUNK of the tensor) into the own buffer half; per-chunk
+// stamps (fused waits) or one arrival-counted stamp (split waits, cnt != null)
+__global__ __launch_bounds__(WG) void tpar_publish_range(const uint64_t* __restrict__ x, int c0, Peers pe, int world,
+                                                         int rank, long long npad4, const long long* __restrict__ ep,
+                                                         const int* __restrict__ err, int nchunks,
+                                                         unsigned int* __restrict__ cnt) {
+  if (failed(err)) return;
+  const long long e = ep[0] + 1;
+  const int c = c0 + blockIdx.x;
+  uint64_t* dst = pe.buf[rank] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+  const uint64_t* src = x + (size_t)blockIdx.x * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) st_sys64(dst + i * WG + threadIdx.x, src[i * WG + threadIdx.x]);
+  if (cnt != nullptr) {
+    arrive_and_stamp(cnt, gridDim.x, pe, world, rank, nchunks, 0, (unsigned int)e);
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x < world) publish(pe.flag[threadIdx.x] + ((size_t)0 * nchunks + c) * MAXW + rank, (unsigned int)e);
+}
+
+// the last arriving workgroup of the epoch's final kernel advances the epoch counter
+__device__ __forceinline__ void finish_epoch(long long* ep, unsigned int* done, long long e) {
+  if (threadIdx.x == 0) {
+    const unsigned int old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned int)gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ep[0] = e;
+    }
+  }
+}
+
+// reduce-scatter, second kernel: chunk c = rank * cps + blockIdx of the own shard, rank-order fp32 sum of every peer's
+// published partial rounded once to bf16 into y (the shard, local). WAIT: per-chunk waits inside (fused form)
+template <bool WAIT>
+__global__ __launch_bounds__(WG) void tpar_rs_own(uint64_t* __restrict__ y, Peers pe, int world, int rank, int cps,
+                                                  long long npad4, long long* __restrict__ ep, int* __restrict__ err,
+                                                  int nchunks, unsigned int* __restrict__ done) {
+  const int c = rank * cps + blockIdx.x;
+  uint64_t* dst = y + (size_t)blockIdx.x * (CHUNK / 4);
+  if (failed(err)) {
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i) dst[i * WG + threadIdx.x] = 0x7FC07FC07FC07FC0ull;  // bf16 NaNs
+    return;
+  }
+  const long long e = ep[0] + 1;
+  if constexpr (WAIT) {
+    bool ok = true;
+    if (threadIdx.x < world) ok = wait_flag(pe.flag[rank] + ((size_t)0 * nchunks + c) * MAXW + threadIdx.x,
+                                            (unsigned int)e, err);
+    if (__ballot(!ok) != 0ull) {
+#pragma unroll
+      for (int i = 0; i < PER_LANE; ++i) dst[i * WG + threadIdx.x] = 0x7FC07FC07FC07FC0ull;
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  const size_t off = (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+#pragma unroll 4
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int q = i * WG + threadIdx.x;
+    uint64_t v[MAXW];
+#pragma unroll
+    for (int p = 0; p < MAXW; ++p) v[p] = p < world ? ld_sys64(pe.buf[p] + off + q) : 0ull;
+    float sm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < MAXW; ++p)
+      if (p < world) {
+        const float2 a = bf2f((uint32_t)v[p]), b = bf2f((uint32_t)(v[p] >> 32));
+        sm[0] += a.x;
+        sm[1] += a.y;
+        sm[2] += b.x;
+        sm[3] += b.y;
+      }
+    dst[q] = (uint64_t)f2bf(sm[0], sm[1]) | ((uint64_t)f2bf(sm[2], sm[3]) << 32);
+  }
+  finish_epoch(ep, done, e);
+}
+
+// all-gather, second kernel: every chunk of y from its owner's published shard (own chunks from the own buffer too)
+template <bool WAIT>
+__global__ __launch_bounds__(WG) void tpar_ag_gather(uint64_t* __restrict__ y, Peers pe, int world, int rank, int cps,
+                                                     long long npad4, long long* __restrict__ ep,
+                                                     int* __restrict__ err, int nchunks,
+                                                     unsigned int* __restrict__ done) {
+  const int c = blockIdx.x, owner = c / cps;
+  uint64_t* dst = y + (size_t)c * (CHUNK / 4);
+  if (failed(err)) {
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i) dst[i * WG + threadIdx.x] = 0x7FC07FC07FC07FC0ull;
+    return;
+  }
+  const long long e = ep[0] + 1;
+  if constexpr (WAIT) {
+    bool ok = true;
+    if (threadIdx.x == 0)
+      ok = wait_flag(pe.flag[rank] + ((size_t)0 * nchunks + c) * MAXW + owner, (unsigned int)e, err);
+    if (__ballot(!ok) != 0ull) {
+#pragma unroll
+      for (int i = 0; i < PER_LANE; ++i) dst[i * WG + threadIdx.x] = 0x7FC07FC07FC07FC0ull;
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  const uint64_t* src = pe.buf[owner] + (size_t)(e & 1) * npad4 + (size_t)c * (CHUNK / 4);
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) dst[i * WG + threadIdx.x] = ld_sys64(src + i * WG + threadIdx.x);
+  finish_epoch(ep, done, e);
+}
+
 }  // namespace
 
 extern "C" {
@@ -400,6 +517,69 @@ int mifx_tpar_allreduce2(const void* x, void* y, long long n, void* const* bufs,
   }
   return tpar_allreduce(x, y, n, bufs, reds, flags, world, rank, npad, ep, done, err, f32 != 0, scale, waiters != 0,
                         stream);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Sequence-parallel reduce-scatter of a bf16 [n] partial: y (n / world elements, this rank's contiguous shard) = rank-
+// order sum over the ranks of x's shard, rounded once to bf16. all-gather: y [n] = the ranks' shards x [n / world] in
+// rank order. n % (world * CHUNK) == 0 (whole chunks per shard). waiters: split waits as mifx_tpar_allreduce2.
+int mifx_tpar_reduce_scatter(const void* x, void* y, long long n, void* const* bufs, void* const* flags, int world,
+                             int rank, long long npad, long long* ep, unsigned int* done, int* err, int waiters,
+                             hipStream_t stream) {
+  if (world < 1 || world > MAXW || rank < 0 || rank >= world || n <= 0 || n % ((long long)world * CHUNK) != 0 ||
+      n > npad || npad % CHUNK != 0 || x == nullptr || y == nullptr || ep == nullptr || done == nullptr ||
+      err == nullptr || (uintptr_t)x % 8 != 0 || (uintptr_t)y % 8 != 0)
+    return -1;
+  Peers pe{};
+  for (int p = 0; p < world; ++p) {
+    if (bufs[p] == nullptr || flags[p] == nullptr) return -1;
+    pe.buf[p] = (uint64_t*)bufs[p];
+    pe.flag[p] = (unsigned int*)flags[p];
+  }
+  const int nchunks = (int)(n / CHUNK), nchunks_all = (int)(npad / CHUNK), cps = nchunks / world;
+  const long long npad4 = npad / 4;
+  hipLaunchKernelGGL(tpar_publish_range, dim3(nchunks), dim3(WG), 0, stream, (const uint64_t*)x, 0, pe, world, rank,
+                     npad4, ep, err, nchunks_all, waiters ? done + 1 : nullptr);
+  if (waiters) {
+    hipLaunchKernelGGL(tpar_wait, dim3(1), dim3(WG), 0, stream, pe, world, rank, ep, err, nchunks_all, 0);
+    hipLaunchKernelGGL(tpar_rs_own<false>, dim3(cps), dim3(WG), 0, stream, (uint64_t*)y, pe, world, rank, cps, npad4,
+                       ep, err, nchunks_all, done);
+  } else {
+    hipLaunchKernelGGL(tpar_rs_own<true>, dim3(cps), dim3(WG), 0, stream, (uint64_t*)y, pe, world, rank, cps, npad4,
+                       ep, err, nchunks_all, done);
+  }
+  return (int)hipGetLastError();
+}
+
+int mifx_tpar_all_gather(const void* x, void* y, long long n, void* const* bufs, void* const* flags, int world,
+                         int rank, long long npad, long long* ep, unsigned int* done, int* err, int waiters,
+                         hipStream_t stream) {
+  if (world < 1 || world > MAXW || rank < 0 || rank >= world || n <= 0 || n % ((long long)world * CHUNK) != 0 ||
+      n > npad || npad % CHUNK != 0 || x == nullptr || y == nullptr || ep == nullptr || done == nullptr ||
+      err == nullptr || (uintptr_t)x % 8 != 0 || (uintptr_t)y % 8 != 0)
+    return -1;
+  Peers pe{};
+  for (int p = 0; p < world; ++p) {
+    if (bufs[p] == nullptr || flags[p] == nullptr) return -1;
+    pe.buf[p] = (uint64_t*)bufs[p];
+    pe.flag[p] = (unsigned int*)flags[p];
+  }
+  const int nchunks = (int)(n / CHUNK), nchunks_all = (int)(npad / CHUNK), cps = nchunks / world;
+  const long long npad4 = npad / 4;
+  hipLaunchKernelGGL(tpar_publish_range, dim3(cps), dim3(WG), 0, stream, (const uint64_t*)x, rank * cps, pe, world,
+                     rank, npad4, ep, err, nchunks_all, waiters ? done + 1 : nullptr);
+  if (waiters) {
+    hipLaunchKernelGGL(tpar_wait, dim3(1), dim3(WG), 0, stream, pe, world, rank, ep, err, nchunks_all, 0);
+    hipLaunchKernelGGL(tpar_ag_gather<false>, dim3(nchunks), dim3(WG), 0, stream, (uint64_t*)y, pe, world, rank, cps,
+                       npad4, ep, err, nchunks_all, done);
+  } else {
+    hipLaunchKernelGGL(tpar_ag_gather<true>, dim3(nchunks), dim3(WG), 0, stream, (uint64_t*)y, pe, world, rank, cps,
+                       npad4, ep, err, nchunks_all, done);
+  }
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

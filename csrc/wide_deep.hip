@@ -945,6 +945,79 @@ __global__ __launch_bounds__(256) void wd_reduce_xcd(const float4* __restrict__ 
   if (t == 0) ok[x * nc1 + c] = (int)(xep[0] + 1);
 }
 
+// ---- residue-class two-level reduction (the register-chained trainer's default step tail on one GPU).
+// Level 1 (wd_reduce_res, 8 x nchunks workgroups): workgroup j sums, for its 256 columns (chunk j / 8), the slab rows
+// b == j (mod 8), ascending, into part[j % 8]. Level 2 (wd_res_opt_sc, one thread per column): part[0] + ... +
+// part[7] in that order, then the optimizer. Both sums run over fixed row sets in a fixed order whatever the
+// placement, so the step is deterministic with no record of where anything ran, and neither kernel has a dependent
+// load before its data loads (wd_reduce_xcd first reads xcd_of, wd_xcd_opt_sc orders the XCDs and checks epoch
+// stamps). Locality: the dispatcher hands workgroups to the XCDs round-robin from a pointer that carries over between
+// launches, and both the fused kernel's grid (256) and this one's (8 x nchunks) are multiples of 8, so fused
+// workgroup b and level-1 workgroup j with j == b (mod 8) run on the same XCD and the rows are L2 hits -- as in
+// wd_reduce_xcd. A placement that breaks this only costs cross-XCD reads, never a different result.
+__global__ __launch_bounds__(256) void wd_reduce_res(const float4* __restrict__ slab, int G, int stride,
+                                                     float4* __restrict__ part) {
+  __shared__ float4 red[4][X1C];
+  const int S4 = stride / 4;
+  const int k = blockIdx.x & 7, c = blockIdx.x >> 3;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int q = c * X1C + lane;
+  float4 a = make_float4(0, 0, 0, 0);
+  if (q < S4) {  // rows k + 8 (w + 4 i): 8 loads in flight per thread (32 rows per residue at G = 256: one round)
+    constexpr int U = 8;
+    for (int i0 = k + 8 * w; i0 < G; i0 += 32 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = i0 + 32 * u;
+        v[u] = r < G ? slab[(size_t)r * S4 + q] : make_float4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+  }
+  red[w][lane] = a;
+  __syncthreads();
+  if (w == 0 && q < S4) {
+    float4 sm = red[0][lane];
+#pragma unroll
+    for (int k2 = 1; k2 < 4; ++k2) {
+      sm.x += red[k2][lane].x; sm.y += red[k2][lane].y; sm.z += red[k2][lane].z; sm.w += red[k2][lane].w;
+    }
+    part[(size_t)k * S4 + q] = sm;
+  }
+}
+
+// level 2 of the residue-class reduction: MODE 0 plain sum into out, 1 optimizer on slab-order state
+template <int MODE>
+__global__ __launch_bounds__(256) void wd_res_opt_sc(const float* __restrict__ part, int stride, float* __restrict__ out,
+                                                     const int* __restrict__ wsc, float* __restrict__ param,
+                                                     float* __restrict__ s0, float* __restrict__ s1,
+                                                     uint16_t* __restrict__ wt_out, long long* __restrict__ step_ctr,
+                                                     OptHyper hd, OptHyper hw) {
+  const int t = threadIdx.x, gi = blockIdx.x * 256 + t;
+  const long long step = MODE == 1 ? step_ctr[blockIdx.x] + 1 : 0;
+  float pv[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) pv[x] = gi < stride ? part[(size_t)x * stride + gi] : 0.f;
+  ScState st{-1, 0.f, 0.f, 0.f};
+  if (MODE == 1) st = sc_load(gi, stride, wsc, param, s0, s1);
+  if (gi < stride) {
+    float g = pv[0];
+#pragma unroll
+    for (int x = 1; x < 8; ++x) g += pv[x];
+    if (MODE == 0) out[gi] = g;
+    if (MODE == 1) sc_update(gi, st, g, hd, hw, step, param, s0, s1, wt_out);
+  }
+  if (MODE == 1) {
+    if (t == 0) step_ctr[blockIdx.x] = step;
+    if (blockIdx.x == 0)
+      for (int i = gridDim.x + t; i < STEP_SLOTS; i += 256) step_ctr[i] = step;
+  }
+}
+
 // level 2: one thread per slab column. MODE 0: plain sum into out; 1: optimizer on slab-order state; 2: xGMI data
 // parallelism, publish half -- store the local sum into half (epoch & 1) of this rank's IPC buffer and stamp the 4
 // RQ-float4 chunks' flags in every peer, no wait (wd_xgmi_gather_opt waits, gathers and applies the optimizer in
@@ -1422,6 +1495,34 @@ int mifx_wd_reduce_xcd_opt(const float* slab, int G, int stride, const int* xcd_
   else
     hipLaunchKernelGGL(wd_xcd_opt_sc<1>, g2, dim3(256), 0, stream, part, ok, slab, G, stride, xcd_of, xep, out, wsc,
                        param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw, XgPeers{}, 0, 0, nullptr, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+
+// Residue-class two-level slab reduction [+ optimizer on slab-column-order state] (see wd_reduce_res). part: [8][stride]
+// fp32 scratch. wsc == null: plain sum into out [stride].
+int mifx_wd_reduce_res_opt(const float* slab, int G, int stride, float* part, float* out, const int* wsc, float* param,
+                           float* s0, float* s1, void* wt_out, long long* step_ctr, const float* hyper_dnn,
+                           const float* hyper_wide, hipStream_t stream) {
+  if (G <= 0 || stride <= 0 || stride > STRIDE || stride % 4 != 0 || part == nullptr) return -1;
+  if (wsc == nullptr && out == nullptr) return -1;
+  if (wsc != nullptr && (param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
+                         step_ctr == nullptr || hyper_dnn == nullptr || hyper_wide == nullptr))
+    return -1;
+  const int nc1 = mifx_wd_xcd_chunks(stride);
+  const dim3 g2((stride + 255) / 256);
+  if ((int)g2.x > STEP_SLOTS) return -1;
+  hipLaunchKernelGGL(wd_reduce_res, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, (float4*)part);
+  if (wsc == nullptr) {
+    hipLaunchKernelGGL(wd_res_opt_sc<0>, g2, dim3(256), 0, stream, part, stride, out, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, OptHyper{}, OptHyper{});
+  } else {
+    const OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                      hyper_dnn[6], hyper_dnn[7]};
+    const OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                      hyper_wide[6], hyper_wide[7]};
+    hipLaunchKernelGGL(wd_res_opt_sc<1>, g2, dim3(256), 0, stream, part, stride, nullptr, wsc, param, s0, s1,
+                       (uint16_t*)wt_out, step_ctr, hd, hw);
+  }
   return (int)hipGetLastError();
 }
 

@@ -26,6 +26,10 @@ def _fns():
                                                    VP, VP]),
         "ln_bwd": sig(lib, "mifx_bert_bdaln_bwd", [I32, I32, VP, VP, VP, VP, VP, VP, VP, I32, I32, F32, VP, I32, VP,
                                                    VP, VP, VP, VP, VP, VP]),
+        "ln_fwd2": sig(lib, "mifx_bert_bdaln_fwd2", [I32, I32, VP, VP, VP, VP, VP, I32, I32, F32, F32, VP, I32, I64,
+                                                     VP, VP, VP, VP]),
+        "ln_bwd2": sig(lib, "mifx_bert_bdaln_bwd2", [I32, I32, VP, VP, VP, VP, VP, VP, VP, I32, I32, F32, VP, I32, I64,
+                                                     VP, VP, VP, VP, VP, VP, VP]),
         "dropout": sig(lib, "mifx_bert_dropout", [I32, VP, I64, F32, VP, I32, VP, VP]),
         "gelu": sig(lib, "mifx_bert_bias_gelu", [I32, I32, I32, VP, VP, VP, I32, I32, VP, VP, VP, VP]),
         "colsum": sig(lib, "mifx_bert_col_sum", [I32, I32, VP, I32, I32, VP, VP, VP]),
@@ -126,7 +130,7 @@ class _BiasDropAddLN(torch.autograd.Function):
     dr, da and the gamma / beta / bias gradients); the dropout mask is recomputed in the backward."""
 
     @staticmethod
-    def forward(ctx, a, bias, r, w, b, eps, p, rng, site, slot=None):
+    def forward(ctx, a, bias, r, w, b, eps, p, rng, site, slot=None, eoff=0):
         a, r = a.contiguous(), r.contiguous().to(a.dtype)
         H = a.shape[-1]
         R = a.numel() // H
@@ -136,13 +140,13 @@ class _BiasDropAddLN(torch.autograd.Function):
         y = torch.empty_like(a)
         mean = torch.empty(R, device=a.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
-        check(_fns()["ln_fwd"](_dt(a), _dt(wp), ptr(a), ptr(biasp), ptr(r), ptr(wp), ptr(bp), R, H, float(eps),
-                               float(p), ptr(rng if p > 0 else None), int(site), ptr(y), ptr(mean), ptr(rstd),
-                               stream_handle(a.device)), "mifx_bert_bdaln_fwd")
+        check(_fns()["ln_fwd2"](_dt(a), _dt(wp), ptr(a), ptr(biasp), ptr(r), ptr(wp), ptr(bp), R, H, float(eps),
+                                float(p), ptr(rng if p > 0 else None), int(site), int(eoff), ptr(y), ptr(mean),
+                                ptr(rstd), stream_handle(a.device)), "mifx_bert_bdaln_fwd")
         ctx.save_for_backward(a, r, wp, biasp, mean, rstd)
         # snapshot of [seed, counter] at forward time (a device copy, graph-capturable): the backward recomputes
         # the forward's mask even if the live counter advanced in between (activation re-forward, 2 forwards)
-        ctx.rng, ctx.p, ctx.site = _snap(rng, p), float(p), int(site)
+        ctx.rng, ctx.p, ctx.site, ctx.eoff = _snap(rng, p), float(p), int(site), int(eoff)
         ctx.wdtype = w.dtype
         ctx.bdtype = None if bias is None else bias.dtype
         ctx.slot = slot
@@ -161,16 +165,17 @@ class _BiasDropAddLN(torch.autograd.Function):
         dw = torch.empty(H, device=a.device, dtype=wp.dtype)  # written in the parameter dtype by the kernel
         db = torch.empty(H, device=a.device, dtype=wp.dtype)
         dbias = None if biasp is None else torch.empty(H, device=a.device, dtype=wp.dtype)
-        check(_fns()["ln_bwd"](_dt(a), _dt(wp), ptr(dy), ptr(a), ptr(biasp), ptr(r), ptr(wp), ptr(mean), ptr(rstd), R,
-                               H, ctx.p, ptr(ctx.rng if ctx.p > 0 else None), ctx.site, ptr(dr), ptr(da), ptr(part),
-                               ptr(dw), ptr(db), ptr(dbias), stream_handle(a.device)), "mifx_bert_bdaln_bwd")
+        check(_fns()["ln_bwd2"](_dt(a), _dt(wp), ptr(dy), ptr(a), ptr(biasp), ptr(r), ptr(wp), ptr(mean), ptr(rstd),
+                                R, H, ctx.p, ptr(ctx.rng if ctx.p > 0 else None), ctx.site, ctx.eoff, ptr(dr), ptr(da),
+                                ptr(part), ptr(dw), ptr(db), ptr(dbias), stream_handle(a.device)),
+              "mifx_bert_bdaln_bwd")
         if wp.dtype != ctx.wdtype:
             dw, db = dw.to(ctx.wdtype), db.to(ctx.wdtype)
         if dbias is not None and dbias.dtype != ctx.bdtype:
             dbias = dbias.to(ctx.bdtype)
         if ctx.slot is not None:  # the residual's other consumer folds dr into its input-gradient GEMM
             ctx.slot.g, dr = dr, None
-        return da, dbias, dr, dw, db, None, None, None, None, None
+        return da, dbias, dr, dw, db, None, None, None, None, None, None
 
 
 class _Dropout(torch.autograd.Function):
@@ -180,7 +185,7 @@ class _Dropout(torch.autograd.Function):
         y = torch.empty_like(x)
         check(_fns()["dropout"](_dt(x), ptr(x), x.numel(), float(p), ptr(rng), int(site), ptr(y),
                                 stream_handle(x.device)), "mifx_bert_dropout")
-        ctx.rng, ctx.p, ctx.site = _snap(rng, p), float(p), int(site)
+        ctx.rng, ctx.p, ctx.site, ctx.eoff = _snap(rng, p), float(p), int(site), int(eoff)
         return y
 
     @staticmethod
@@ -350,7 +355,7 @@ _TORCH_OPS = os.environ.get("MIFX_BERT_TORCH_OPS") == "1"
 
 def bias_dropout_add_layernorm(a: torch.Tensor, bias, r: torch.Tensor, weight, ln_bias, eps: float = 1e-12,
                                p: float = 0.0, rng: torch.Tensor | None = None, site: int = 0,
-                               slot=None) -> torch.Tensor:
+                               slot=None, eoff: int = 0) -> torch.Tensor:
     """LayerNorm(dropout_p(a + bias) + r) * weight + ln_bias (bias optional; p > 0 needs rng = device int64
     [seed, counter]). The mask depends only on (seed, counter, site, element index): every tensor-parallel rank
     with the same seed drops the same elements of a replicated activation, and a captured hipGraph draws a new
@@ -359,12 +364,12 @@ def bias_dropout_add_layernorm(a: torch.Tensor, bias, r: torch.Tensor, weight, l
     if p > 0 and rng is None:
         raise ValueError("dropout p > 0 needs an rng state tensor [seed, counter]")
     if a.is_cuda and not _TORCH_OPS:
-        return _BiasDropAddLN.apply(a, bias, r, weight, ln_bias, eps, p, rng, site, slot)
+        return _BiasDropAddLN.apply(a, bias, r, weight, ln_bias, eps, p, rng, site, slot, eoff)
     if slot is not None:
         raise ValueError("a residual-gradient slot needs the fused GPU path")
     x = a if bias is None else a + bias.to(a.dtype)
-    if p > 0:
-        keep = _mask(x.numel(), rng, site, p, x.device).view(x.shape)
+    if p > 0:  # (eoff: this tensor is the slice [eoff, eoff + numel) of a larger activation's mask)
+        keep = _mask(eoff + x.numel(), rng, site, p, x.device)[eoff:].view(x.shape)
         x = torch.where(keep, x * _drop_scale(p), torch.zeros((), dtype=x.dtype, device=x.device))
     return F.layer_norm(x + r, (a.shape[-1],), weight, ln_bias, eps)
 

@@ -24,6 +24,8 @@ def _fns():
         "xcd_chunks": sig(lib, "mifx_wd_xcd_chunks", [I32]),
         "reduce_xcd_opt": sig(lib, "mifx_wd_reduce_xcd_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP,
                                                               VP, VP, VP, VP]),
+        "reduce_res_opt": sig(lib, "mifx_wd_reduce_res_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP,
+                                                              VP]),
         "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
         "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
                                                                 VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
@@ -147,6 +149,32 @@ class XcdReduce:
                                       ptr(s1_sc), ptr(wt_out), ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
                                       stream_handle(slab.device))
         check(rc, "mifx_wd_reduce_xcd_opt")
+
+    def apply_sc(self, slab: torch.Tensor, groups: int, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn,
+                 hyper_wide) -> None:
+        _check_step_ctr(step_ctr)
+        self._call(slab, groups, None, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide)
+
+    def sum_into(self, slab: torch.Tensor, groups: int, out: torch.Tensor) -> None:
+        self._call(slab, groups, out, None, None, None, None, None, None, None, None)
+
+
+class ResReduce:
+    """Scratch of the residue-class two-level slab reduction + optimizer (csrc/wide_deep.hip wd_reduce_res /
+    wd_res_opt_sc): per-residue partials [8, stride]. Same interface as XcdReduce."""
+
+    def __init__(self, stride: int, device):
+        self.stride = int(stride)
+        self.part = torch.zeros(8 * stride, device=device)
+        self.xcd_of = None  # (no placement record needed)
+
+    def _call(self, slab, groups, out, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide):
+        if slab.shape[-1] != self.stride or slab.numel() < groups * self.stride or not slab.is_contiguous():
+            raise ValueError("slab must be contiguous [>= groups, stride]")
+        rc = _fns()["reduce_res_opt"](ptr(slab), int(groups), self.stride, ptr(self.part), ptr(out), ptr(wsc),
+                                      ptr(param_sc), ptr(s0_sc), ptr(s1_sc), ptr(wt_out), ptr(step_ctr),
+                                      ptr(hyper_dnn), ptr(hyper_wide), stream_handle(slab.device))
+        check(rc, "mifx_wd_reduce_res_opt")
 
     def apply_sc(self, slab: torch.Tensor, groups: int, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn,
                  hyper_wide) -> None:

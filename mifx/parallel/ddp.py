@@ -153,25 +153,26 @@ class DataParallel:
 
     # ---- hooks ------------------------------------------------------------------------------
     def _on_grad(self, p: torch.Tensor) -> None:
-        if not self._sync or p.grad is None:
+        if p.grad is None:
             return
         bi, pi = self._where[p]
         b = self.buckets[bi]
-        if pi in b.ready:
-            return
-        b.ready.add(pi)
         off = b.offsets[pi]
         view = b.buf[off:off + p.numel()]
-        if not self.views:
-            view.copy_(p.grad.reshape(-1))
-        elif p.grad.data_ptr() != view.data_ptr():
+        if self.views and p.grad.data_ptr() != view.data_ptr():
             # views mode assumes p.grad IS the bucket view; something replaced it (optimizer.zero_grad() with
             # set_to_none, a weight released for a deferred flush that the flush did not take): copy the fresh
             # gradient into the bucket and re-attach the view -- in the parameter's own layout (channels_last), so the
-            # all-reduced bucket and the gradient the optimizer reads stay the same memory, element for element
+            # all-reduced bucket and the gradient the optimizer reads stay the same memory, element for element. Also
+            # under no_sync: the bucket must hold what the later (eager) exchange reduces.
             v = self._view(b, pi)
             v.copy_(p.grad)
             p.grad = v
+        if not self._sync or pi in b.ready:
+            return
+        b.ready.add(pi)
+        if not self.views:
+            view.copy_(p.grad.reshape(-1))
         if len(b.ready) == len(b.params):
             self._flush_deferred(b)
             self._launch_ready()

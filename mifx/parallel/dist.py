@@ -61,6 +61,8 @@ def barrier() -> None:
 def max_over_ranks(x: float, device=None) -> float:
     if not dist.is_initialized():
         return x
+    if device is None and dist.get_backend() == "nccl":  # RCCL reduces device tensors only
+        device = torch.device("cuda", torch.cuda.current_device())
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -30,7 +30,9 @@ def _fns():
             "ar": sig(lib, "mifx_tpar_allreduce", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, VP]),
             "ar32": sig(lib, "mifx_tpar_allreduce_f32", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, F32, VP]),
             "ar2": sig(lib, "mifx_tpar_allreduce2", [VP, VP, I64, VP, VP, VP, I32, I32, I64, VP, VP, VP, I32, F32, I32,
-                                                    VP])}
+                                                    VP]),
+            "rs": sig(lib, "mifx_tpar_reduce_scatter", [VP, VP, I64, VP, VP, I32, I32, I64, VP, VP, VP, I32, VP]),
+            "ag": sig(lib, "mifx_tpar_all_gather", [VP, VP, I64, VP, VP, I32, I32, I64, VP, VP, VP, I32, VP])}
 
 
 def _device_key(device) -> str:
@@ -60,6 +62,7 @@ class IpcAllReduce:
         if not 1 <= self.world <= MAX_WORLD:
             raise ValueError(f"IPC all-reduce supports 1..{MAX_WORLD} ranks")
         chunk = _fns()["chunk"]()
+        self.chunk = int(chunk)
         self.npad = -(-int(max_elems) // chunk) * chunk
         self.nchunks = self.npad // chunk
         xf = _xg_fns()
@@ -150,6 +153,36 @@ class IpcAllReduce:
         check(_fns()["ar2"](ptr(x), ptr(y), n, self.bufs, self.reds, self.flags, self.world, self.rank, self.npad,
                             ptr(self.ep), ptr(self.done), ptr(self.err), int(f32), float(scale), int(self.waiters),
                             stream_handle(self.device)), "mifx_tpar_allreduce2")
+        return y
+
+    # ---- sequence parallelism: token-major [T, H] bf16 activations, rank r owns tokens [r T / W, (r + 1) T / W)
+    def shard_ok(self, n: int) -> bool:
+        """n elements split into `world` contiguous shards of whole chunks (the reduce-scatter / all-gather layout)."""
+        return self.dtype == torch.bfloat16 and n % (self.world * self.chunk) == 0 and n <= self.npad
+
+    def reduce_scatter(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """This rank's shard (the n / world elements starting at rank * n / world, flattened) of the rank-order sum
+        of the ranks' bf16 x, rounded once to bf16. Stream-ordered, graph-capturable."""
+        x = x.contiguous()
+        n = x.numel()
+        if x.dtype != torch.bfloat16 or not self.shard_ok(n):
+            raise ValueError(f"reduce_scatter: bf16 with numel % (world x {self.chunk}) == 0 and <= {self.npad}")
+        y = torch.empty(n // self.world, dtype=x.dtype, device=x.device) if out is None else out
+        check(_fns()["rs"](ptr(x), ptr(y), n, self.bufs, self.flags, self.world, self.rank, self.npad, ptr(self.ep),
+                           ptr(self.done), ptr(self.err), int(self.waiters), stream_handle(self.device)),
+              "mifx_tpar_reduce_scatter")
+        return y
+
+    def all_gather(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """The ranks' shards concatenated in rank order (flattened, world x numel(x) elements)."""
+        x = x.contiguous()
+        n = x.numel() * self.world
+        if x.dtype != torch.bfloat16 or not self.shard_ok(n):
+            raise ValueError(f"all_gather: bf16 shards of whole chunks, total <= {self.npad}")
+        y = torch.empty(n, dtype=x.dtype, device=x.device) if out is None else out
+        check(_fns()["ag"](ptr(x), ptr(y), n, self.bufs, self.flags, self.world, self.rank, self.npad, ptr(self.ep),
+                           ptr(self.done), ptr(self.err), int(self.waiters), stream_handle(self.device)),
+              "mifx_tpar_all_gather")
         return y
 
     def check(self) -> None:
