@@ -20,7 +20,9 @@ import torch.nn.functional as F
 from ..ops import fused_bert as fb
 from ..ops import gemm as hg
 from ..parallel.tensor_parallel import (ColumnParallelLinear, RowParallelLinear, TPGroup, VocabParallelEmbedding,
-                                        copy_to_tp, head_partition, overlap_ok, reduce_from_tp, split_sizes)
+                                        all_reduce_grads, copy_to_tp, gather_seq, gather_seq_replicated,
+                                        head_partition, overlap_ok, reduce_from_tp, reduce_scatter_seq, scatter_to_seq,
+                                        split_sizes)
 
 
 @dataclass
@@ -43,6 +45,9 @@ class BertConfig:
     # MIFX_BERT_FOLD_RESIDUAL=0
     fold_residual_grad: bool = field(
         default_factory=lambda: os.environ.get("MIFX_BERT_FOLD_RESIDUAL", "1") != "0")
+    # sequence parallelism at TP > 1 (mifx.parallel.tensor_parallel): the residual stream, LayerNorms and hidden
+    # dropouts run on each rank's 1/TP of the tokens; all-reduces become reduce-scatter + all-gather pairs
+    sequence_parallel: bool = False
     num_labels: int = 2
     ln_eps: float = 1e-12
     init_std: float = 0.02
@@ -84,6 +89,44 @@ class BertLayer(nn.Module):
         self.ffn_out.load_full(sd[prefix + "ffn_out.weight"], sd[prefix + "ffn_out.bias"])
         for n in ("ln1", "ln2"):
             getattr(self, n).load_state_dict({"weight": sd[f"{prefix}{n}.weight"], "bias": sd[f"{prefix}{n}.bias"]})
+
+    def forward_sp(self, x, mask, rng, site, B: int, S: int):
+        """Sequence-parallel layer: x is this rank's [T / TP, H] token rows of the residual stream. The column-parallel
+        projections read the all-gathered [T, H] (their input gradients come back reduce-scattered), the row-parallel
+        products are reduce-scattered into the shard, and the bias + dropout + residual + LayerNorm run on the shard
+        with the dropout mask offset to the shard's first element -- the same mask bits as the replicated layer."""
+        c, tp = self.cfg, self.tp
+        h, d = self.local_heads, self.head_dim
+        drop = c.dropout if self.training else 0.0
+        adrop = (c.dropout if c.attn_dropout is None else c.attn_dropout) if self.training else 0.0
+        hip = (c.hip_gemm if c.hip_gemm is not None else os.environ.get("MIFX_BERT_HIP_GEMM", "1") == "1") and x.is_cuda
+        eoff = tp.rank * x.numel()
+        xg = gather_seq(x, tp)
+        qkv = (hg.linear(xg, self.qkv.weight, self.qkv.bias) if hip
+               else fb.linear(xg, self.qkv.weight, self.qkv.bias)).view(B, S, 3, h, d)
+        if c.fused_attention:
+            h0 = sum(self.heads_per_rank[:tp.rank])
+            ctx = fb.attention(qkv, mask, 1.0 / d ** 0.5, adrop, rng, 1000 + site, h0, c.heads).reshape(B * S, h * d)
+        else:
+            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+            amask = None if mask is None else mask[:, None, None, :].to(q.dtype)
+            ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=amask, dropout_p=adrop)
+            ctx = ctx.transpose(1, 2).reshape(B * S, h * d)
+        a = reduce_scatter_seq(hg.linear(ctx, self.attn_out.weight) if hip else F.linear(ctx, self.attn_out.weight), tp)
+        x = fb.bias_dropout_add_layernorm(a, self.attn_out.bias, x, self.ln1.weight, self.ln1.bias, c.ln_eps, drop,
+                                          rng, site, eoff=eoff)
+        xg = gather_seq(x, tp)
+        if hip:
+            o = hg.ffn(xg, self.ffn_in.weight, self.ffn_in.bias, self.ffn_out.weight)
+        else:
+            o = F.linear(fb.bias_gelu(F.linear(xg, self.ffn_in.weight), self.ffn_in.bias), self.ffn_out.weight)
+        o = reduce_scatter_seq(o, tp)
+        return fb.bias_dropout_add_layernorm(o, self.ffn_out.bias, x, self.ln2.weight, self.ln2.bias, c.ln_eps, drop,
+                                             rng, site + 1, eoff=eoff)
+
+    def sequence_parallel_params(self) -> list:
+        """Parameters applied to token shards under sequence parallelism (partial gradients per rank)."""
+        return [self.ln1.weight, self.ln1.bias, self.ln2.weight, self.ln2.bias, self.attn_out.bias, self.ffn_out.bias]
 
     def forward(self, x, mask, rng=None, site=0):
         """Dropout RNG: every mask is counter-based (model seed, step counter, site; csrc/counter_rng.h), never the
@@ -168,6 +211,17 @@ class BertForSequenceClassification(nn.Module):
         if seed is not None:
             self.init_weights(seed)
 
+    @property
+    def sequence_parallel(self) -> bool:
+        return self.cfg.sequence_parallel and self.tp.size > 1
+
+    def sync_sequence_parallel_grads(self) -> None:
+        """After the backward, before the update: sum the token-shard parameters' gradients over the TP group
+        (no-op without sequence parallelism). Once per optimizer step, after the last micro-batch's backward: the
+        sum is over whatever the gradients hold."""
+        if self.sequence_parallel:
+            all_reduce_grads([p for L in self.layers for p in L.sequence_parallel_params()], self.tp)
+
     def init_weights(self, seed: int) -> None:
         """Initialise as the full model would, then take this rank's shard (so any TP degree matches TP=1)."""
         full = full_init_state(self.cfg, seed)
@@ -194,8 +248,16 @@ class BertForSequenceClassification(nn.Module):
         mask = None
         if attention_mask is not None:  # additive key bias [B, S] (fp32; -1e30 on padding keys)
             mask = ((1.0 - attention_mask.float()) * -1e30).contiguous()
-        for i, layer in enumerate(self.layers):
-            x = layer(x, mask, rng, 1 + 2 * i)
+        if self.sequence_parallel:
+            # the layers' residual stream: this rank's token rows, in the dtype the projections compute in
+            cdt = torch.get_autocast_dtype("cuda") if x.is_cuda and torch.is_autocast_enabled("cuda") else x.dtype
+            x = scatter_to_seq(x.reshape(B * S, -1), self.tp, cdt)
+            for i, layer in enumerate(self.layers):
+                x = layer.forward_sp(x, mask, rng, 1 + 2 * i, B, S)
+            x = gather_seq_replicated(x, self.tp).view(B, S, -1)
+        else:
+            for i, layer in enumerate(self.layers):
+                x = layer(x, mask, rng, 1 + 2 * i)
         pooled = torch.tanh(self.pooler(x[:, 0]))
         return self.classifier(fb.dropout(pooled, drop, rng, 1 + 2 * len(self.layers)))
 

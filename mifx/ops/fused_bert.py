@@ -185,7 +185,7 @@ class _Dropout(torch.autograd.Function):
         y = torch.empty_like(x)
         check(_fns()["dropout"](_dt(x), ptr(x), x.numel(), float(p), ptr(rng), int(site), ptr(y),
                                 stream_handle(x.device)), "mifx_bert_dropout")
-        ctx.rng, ctx.p, ctx.site, ctx.eoff = _snap(rng, p), float(p), int(site), int(eoff)
+        ctx.rng, ctx.p, ctx.site = _snap(rng, p), float(p), int(site)
         return y
 
     @staticmethod

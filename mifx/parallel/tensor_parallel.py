@@ -17,6 +17,10 @@ BERT-base fine-tune at TP=8, so this module provides the standard column/row spl
   (the FFN's 3072 columns and the 768-wide activations divide by 8). Rebalancing would need heads split across
   ranks (extra all-to-alls per layer), which costs more than it saves at this size.
 
+Sequence parallelism (BertConfig.sequence_parallel): the residual stream between the TP regions is split over the
+ranks by token (gather_seq / reduce_scatter_seq / scatter_to_seq / gather_seq_replicated below; all_reduce_grads
+sums the gradients of the parameters that act on token shards).
+
 Two all-reduces per transformer block (after attention-out and FFN-out), each of
 [tokens, hidden] activations — on MI355X the 8-GPU xGMI ring is ~7 links x ~150 GB/s, so a
 [32*128, 768] bf16 block reduction (6.3 MB) is ~10-15 us. On the peer-memory path those two run OVERLAPPED with their
@@ -182,6 +186,151 @@ class _GatherFromTP(torch.autograd.Function):
             return g, None, None
         off = sum(ctx.sizes[:ctx.tp.rank])
         return g[..., off:off + ctx.sizes[ctx.tp.rank]].contiguous(), None, None
+
+
+# ---------------------------------------------------------------------------------------------- sequence parallelism
+# Megatron-style sequence parallelism (Korthikanti et al. 2022): between the tensor-parallel regions the residual
+# stream is split along the token dim -- rank r holds tokens [r T / W, (r + 1) T / W) of the token-major [T, H]
+# activation -- so the LayerNorms, dropouts and residual adds run on 1/W of the tokens and their activations are
+# stored once per rank instead of W times. Each row-parallel all-reduce becomes a reduce-scatter into the token shard
+# and each column-parallel input an all-gather of it (same bytes on the wire as the all-reduce it replaces: a ring
+# all-reduce IS reduce-scatter + all-gather). On the peer-memory path these are csrc/tp_allreduce.hip's
+# reduce-scatter / all-gather kernels (graph-capturable); otherwise torch.distributed.
+
+
+def _seq_rows(T: int, tp: TPGroup) -> int:
+    if T % tp.size:
+        raise ValueError(f"sequence parallelism: {T} tokens do not split over {tp.size} ranks")
+    return T // tp.size
+
+
+def _ipc_shard_ok(x: torch.Tensor, n: int, tp: TPGroup) -> bool:
+    return tp.ipc is not None and x.dtype == torch.bfloat16 and x.is_cuda and tp.ipc.shard_ok(n)
+
+
+def seq_reduce_scatter(x: torch.Tensor, tp: TPGroup) -> torch.Tensor:
+    """[T, ...] partial sums on every rank -> this rank's [T / W, ...] token rows of their sum."""
+    x = x.contiguous()
+    Ts = _seq_rows(x.shape[0], tp)
+    if _ipc_shard_ok(x, x.numel(), tp):
+        return tp.ipc.reduce_scatter(x).view(Ts, *x.shape[1:])
+    if dist.get_backend(tp.group) == "nccl":
+        y = x.new_empty(Ts, *x.shape[1:])
+        dist.reduce_scatter_tensor(y, x, group=tp.group)
+        return y
+    y = x.clone()  # gloo has no reduce-scatter: all-reduce a private copy, keep the own rows
+    dist.all_reduce(y, group=tp.group)
+    return y[tp.rank * Ts:(tp.rank + 1) * Ts].contiguous()
+
+
+def seq_all_gather(x: torch.Tensor, tp: TPGroup) -> torch.Tensor:
+    """This rank's [T / W, ...] token rows -> the full [T, ...] (rank-order concatenation)."""
+    x = x.contiguous()
+    T = x.shape[0] * tp.size
+    if _ipc_shard_ok(x, x.numel() * tp.size, tp):
+        return tp.ipc.all_gather(x).view(T, *x.shape[1:])
+    y = x.new_empty(T, *x.shape[1:])
+    if dist.get_backend(tp.group) == "nccl":
+        dist.all_gather_into_tensor(y, x, group=tp.group)
+    else:
+        dist.all_gather(list(y.chunk(tp.size)), x, group=tp.group)
+    return y
+
+
+class _GatherSeq(torch.autograd.Function):
+    """all-gather of the token shards forward, reduce-scatter of the (partial, per-rank) gradient backward: the input of
+    a column-parallel projection (replaces copy_to_tp)."""
+
+    @staticmethod
+    def forward(ctx, x, tp):
+        ctx.tp = tp
+        return seq_all_gather(x, tp)
+
+    @staticmethod
+    def backward(ctx, g):
+        return seq_reduce_scatter(g, ctx.tp), None
+
+
+class _ReduceScatterSeq(torch.autograd.Function):
+    """reduce-scatter into the token shard forward, all-gather of the shard gradients backward: the output of a
+    row-parallel projection (replaces reduce_from_tp)."""
+
+    @staticmethod
+    def forward(ctx, x, tp):
+        ctx.tp = tp
+        return seq_reduce_scatter(x, tp)
+
+    @staticmethod
+    def backward(ctx, g):
+        return seq_all_gather(g, ctx.tp), None
+
+
+class _ScatterToSeq(torch.autograd.Function):
+    """replicated [T, ...] -> own token rows (cast to `dtype`) forward; all-gather backward (every rank's gradient of
+    the replicated input is the concatenation of the shard gradients, so the replicated region's backward stays
+    identical on every rank)."""
+
+    @staticmethod
+    def forward(ctx, x, tp, dtype):
+        ctx.tp, ctx.dtype = tp, x.dtype
+        Ts = _seq_rows(x.shape[0], tp)
+        return x[tp.rank * Ts:(tp.rank + 1) * Ts].to(dtype).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return seq_all_gather(g, ctx.tp).to(ctx.dtype), None, None
+
+
+class _GatherSeqReplicated(torch.autograd.Function):
+    """token shards -> the replicated [T, ...] forward (into a replicated region: pooler / head); backward keeps the
+    own rows of the (identical on every rank) gradient."""
+
+    @staticmethod
+    def forward(ctx, x, tp):
+        ctx.tp = tp
+        return seq_all_gather(x, tp)
+
+    @staticmethod
+    def backward(ctx, g):
+        Ts = g.shape[0] // ctx.tp.size
+        return g[ctx.tp.rank * Ts:(ctx.tp.rank + 1) * Ts].contiguous(), None
+
+
+def gather_seq(x, tp: TPGroup):
+    return _GatherSeq.apply(x, tp)
+
+
+def reduce_scatter_seq(x, tp: TPGroup):
+    return _ReduceScatterSeq.apply(x, tp)
+
+
+def scatter_to_seq(x, tp: TPGroup, dtype=None):
+    return _ScatterToSeq.apply(x, tp, x.dtype if dtype is None else dtype)
+
+
+def gather_seq_replicated(x, tp: TPGroup):
+    return _GatherSeqReplicated.apply(x, tp)
+
+
+@torch.no_grad()
+def all_reduce_grads(params, tp: TPGroup) -> None:
+    """Sum the gradients of `params` over the TP group in place, one collective per dtype: the parameters that act on
+    token shards under sequence parallelism (LayerNorm weights / biases, row-parallel biases) get partial gradients
+    from their rank's tokens. Graph-capturable on the peer-memory path (the gradients keep their addresses)."""
+    if tp.size == 1:
+        return
+    by_dtype: dict = {}
+    for p in params:
+        if p.grad is not None:
+            by_dtype.setdefault(p.grad.dtype, []).append(p.grad)
+    for gs in by_dtype.values():
+        flat = torch.cat([g.reshape(-1) for g in gs])
+        pad = (-flat.numel()) % 4  # the IPC kernels move 4 bf16 per lane
+        if pad:
+            flat = F.pad(flat, (0, pad))
+        sizes = [g.numel() for g in gs]
+        flat = _all_reduce(flat, tp)[:sum(sizes)]
+        torch._foreach_copy_(gs, [v.view_as(g) for v, g in zip(flat.split(sizes), gs)])
 
 
 def copy_to_tp(x, tp: TPGroup):

@@ -91,6 +91,13 @@ class BertTrainer:
         else:
             self.opt = torch.optim.AdamW(self.model.parameters(), lr=lr, weight_decay=0.01, fused=cuda,
                                          capturable=self.use_graph)
+        if self.model.sequence_parallel:
+            if getattr(self.opt, "overlap", False):
+                raise ValueError("sequence parallelism: the overlapped AdamW buckets would update the token-shard "
+                                 "parameters before their gradients are summed over the group")
+            if self.tp.ipc is not None and not self.tp.ipc.shard_ok(batch * seq * cfg.hidden):
+                raise ValueError(f"sequence parallelism on the peer-memory path: batch x seq x hidden must split into "
+                                 f"{self.tp.size} shards of whole {self.tp.ipc.chunk}-element chunks")
         # transposed copies of the projection weights for the dX GEMMs, refreshed in one launch before each backward
         self.tcache = None
         if self.flat:
@@ -159,6 +166,8 @@ class BertTrainer:
                 hg.flush_weight_grads()
             else:
                 loss.backward()
+        # sequence parallelism: the LayerNorm / row-parallel-bias gradients are per-shard partial sums
+        self.model.sync_sequence_parallel_grads()
         self.opt.step()
         return loss.detach()
 
@@ -233,6 +242,8 @@ def main(argv=None):
                     help="do not load the bundled per-shape GEMM solution table (tunableop_bert_base_gfx950.csv)")
     ap.add_argument("--seed", type=int, default=None, help="torch.manual_seed before building the trainer")
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--sequence-parallel", action="store_true",
+                    help="at TP > 1: split the residual stream / LayerNorms / dropouts over the ranks by token")
     ap.add_argument("--sdpa", choices=["math", "efficient", "flash"], default=None,
                     help="pin the scaled-dot-product-attention backend (default: PyTorch's choice)")
     a = ap.parse_args(argv)
@@ -250,7 +261,8 @@ def main(argv=None):
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     tp = TPGroup(torch.distributed.group.WORLD if env.world_size > 1 else None)
-    tr = BertTrainer(BertConfig(layers=a.layers, dropout=a.dropout), a.batch, a.seq, dev, tp,
+    cfg = BertConfig(layers=a.layers, dropout=a.dropout, sequence_parallel=a.sequence_parallel)
+    tr = BertTrainer(cfg, a.batch, a.seq, dev, tp,
                      graph=False if a.no_graph else (True if a.graph else None),
                      flat_adamw=False if a.no_flat_adamw else None, sdpa=a.sdpa)
     from ..ops import native_stats
@@ -285,7 +297,8 @@ def main(argv=None):
     tr.check()  # ... and during the timed steps: never report a throughput of garbage activations
     if env.rank == 0:
         print(json.dumps({"metric": "BERT-base fine-tune sequences/sec (TP over the node)", "value": a.batch * a.steps / dt,
-                          "unit": "sequences/s", "n_gpus": env.world_size, "tp": tp.size, "batch": a.batch,
+                          "unit": "sequences/s", "n_gpus": env.world_size, "tp": tp.size,
+                          "sequence_parallel": tr.model.sequence_parallel, "batch": a.batch,
                           "seq_len": a.seq, "ms_per_step": 1e3 * dt / a.steps, "loss": float(loss),
                           "dtype": "bf16", "data": "synthetic", "layers": a.layers,
                           "hipgraph": tr.graph is not None,

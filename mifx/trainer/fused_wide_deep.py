@@ -162,10 +162,11 @@ class FusedWideDeepTrainer:
         # chained kernel, one rank: XCD-local two-level slab reduction (each XCD's slab rows summed where its L2
         # holds them; csrc/wide_deep.hip wd_reduce_xcd)
         # (small grids keep the one-pass reduce: below ~64 workgroups there is little slab to keep local)
-        # MIFX_WD_RES=1: the residue-class variant (rows b == k mod 8 per partial; no placement record, no XCD
-        # ordering: csrc/wide_deep.hip wd_reduce_res)
+        # default: the residue-class variant (rows b == k mod 8 per partial; no placement record, no XCD ordering:
+        # csrc/wide_deep.hip wd_reduce_res) -- 29.9 vs 32.4 us per headline step on MI355X
+        # (profiles/wd_res_ab_r6.jsonl); MIFX_WD_RES=0: the placement-recorded XCD reduction
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
-        red_cls = wdk.ResReduce if os.environ.get("MIFX_WD_RES", "0") == "1" else wdk.XcdReduce
+        red_cls = wdk.ResReduce if os.environ.get("MIFX_WD_RES", "1") == "1" else wdk.XcdReduce
         self._xcd = red_cls(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:

@@ -33,9 +33,11 @@ def _batch(cfg, B=3, S=16, seed=0):
 
 def _step(model, cfg, lr=0.1):
     ids, tt, am, y = _batch(cfg)
+    model.zero_grad(set_to_none=True)
     logits = model(ids, tt, am)
     loss = torch.nn.functional.cross_entropy(logits, y)
     loss.backward()
+    model.sync_sequence_parallel_grads()  # (sequence parallelism: token-shard parameters' partial gradients)
     with torch.no_grad():
         for p in model.parameters():
             p -= lr * p.grad
@@ -122,6 +124,42 @@ def test_tp_attention_dropout_keeps_replicated_params_identical():
     for k in reps[0]:
         assert torch.equal(reps[0][k], reps[1][k]) and torch.equal(reps[0][k], reps[2][k]), k
     torch.testing.assert_close(got["logits"], ref_logits, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sequence_parallel_matches_tp1_and_keeps_replicas_identical(world):
+    """Sequence parallelism (residual stream, LayerNorms and hidden dropouts on each rank's 1/TP of the tokens;
+    reduce-scatter / all-gather instead of all-reduces; token-shard parameter gradients summed over the group) with
+    hidden AND attention dropout on, uneven heads at TP=3: the trajectory equals TP=1 (the shard's dropout mask is
+    the replicated mask offset to the shard) and the replicated parameters stay bit-identical across ranks."""
+    kw = {"dropout": 0.1, "sequence_parallel": True}
+    cfg = BertConfig.tiny(**kw)
+    ref = BertForSequenceClassification(cfg, None, seed=1)
+    assert not ref.sequence_parallel  # (TP = 1: the plain layer)
+    for _ in range(2):
+        ref_logits = _step(ref, cfg)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_worker, args=(world, _port(), out, kw, 2), nprocs=world, start_method="spawn")
+        reps = [torch.load(f"{out}.repl{r}", weights_only=True) for r in range(world)]
+        got = torch.load(out, weights_only=True)
+    for r in range(1, world):
+        for k in reps[0]:
+            assert torch.equal(reps[0][k], reps[r][k]), k
+    torch.testing.assert_close(got["logits"], ref_logits, rtol=1e-4, atol=1e-5)
+    for k, v in gather_full_state(ref).items():
+        np.testing.assert_allclose(got["state"][k].numpy(), v.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
+
+
+def test_sequence_parallel_needs_divisible_tokens():
+    from mifx.parallel.tensor_parallel import _seq_rows
+
+    class _G:
+        size = 3
+
+    assert _seq_rows(48, _G()) == 16
+    with pytest.raises(ValueError):
+        _seq_rows(47, _G())
 
 
 def test_attention_reference_matches_sdpa_and_masks():

@@ -358,3 +358,129 @@ def test_split_wait_exchange_never_starves_whole_cu_kernels():
     assert r0["ok"] and r1["ok"] and r0["err"] == 0 and r1["err"] == 0, (r0, r1)
     assert r1["gemm_rel"] < 1e-2, r1
     assert r1["gemm_s"] < 2.0, r1  # not held until the 10 s wait bound
+
+
+def _rsag_worker(rank, world, port, out, waiters):
+    from mifx.parallel.tp_ipc import IpcAllReduce
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        ar = IpcAllReduce(dist.group.WORLD, dev, 1 << 21, waiters=waiters)
+        res = {}
+        ns = (world * 4096, world * 4096 * 7, 1 << 21)
+        for i, n in enumerate(ns):
+            assert ar.shard_ok(n)
+            g = torch.Generator().manual_seed(77 * i + rank)
+            x = (torch.randn(n, generator=g) * (rank + 1)).to(torch.bfloat16)
+            res[f"x{i}"] = x
+            res[f"rs{i}"] = ar.reduce_scatter(x.to(dev)).cpu()
+            res[f"ag{i}"] = ar.all_gather(x[:n // world].to(dev)).cpu()
+            # an all-reduce between them: the three collectives share the epoch counter and buffers
+            res[f"ar{i}"] = ar.all_reduce(x.to(dev)).cpu()
+        assert not ar.shard_ok(world * 4096 + 4) and not ar.shard_ok(1 << 22)
+        # captured: reduce-scatter -> all-gather of its result (= the all-reduce), replayed with new inputs
+        n = world * 4096 * 3
+        a = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        full = torch.empty_like(a)
+        torch.cuda.synchronize(dev)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            sh = ar.reduce_scatter(a)
+            ar.all_gather(sh, out=full)
+        outs = []
+        for k in range(4):
+            a.copy_(torch.arange(n, device=dev).remainder(97).to(torch.bfloat16) * (rank + 1) + k)
+            gr.replay()
+            torch.cuda.synchronize(dev)
+            outs.append(full.cpu().clone())
+        res["graph"] = outs
+        ar.check()
+        res["err"] = int(ar.err.item())
+        dist.barrier()
+        ar.close()
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,waiters", [(2, None), (4, None), (2, False), (4, False)])
+def test_ipc_reduce_scatter_all_gather_exact(world, waiters):
+    """Sequence-parallel collectives (csrc/tp_allreduce.hip): reduce-scatter gives this rank's contiguous 1/W of the
+    rank-order fp32 sum rounded once to bf16 (the all-reduce's bits), all-gather the rank-order concatenation of the
+    shards, interleaved with all-reduces on the same epoch counter and replayed from a captured graph."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "rs")
+        mp.start_processes(_rsag_worker, args=(world, _port(), out, waiters), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for i in range(3):
+        want = res[0][f"x{i}"].float()
+        for r in range(1, world):
+            want = want + res[r][f"x{i}"].float()
+        want = want.to(torch.bfloat16)
+        m = want.numel() // world
+        cat = torch.cat([res[r][f"x{i}"][:m] for r in range(world)])
+        for r in range(world):
+            assert torch.equal(res[r][f"rs{i}"], want[r * m:(r + 1) * m]), (i, r)
+            assert torch.equal(res[r][f"ag{i}"], cat), (i, r)
+            assert torch.equal(res[r][f"ar{i}"], want), (i, r)
+    n = world * 4096 * 3
+    base = torch.arange(n).remainder(97).to(torch.bfloat16)
+    for k in range(4):
+        want = torch.zeros(n)
+        for q in range(world):
+            want = want + (base * (q + 1) + k).float()
+        want = want.to(torch.bfloat16)
+        for r in range(world):
+            assert res[r]["err"] == 0
+            assert torch.equal(res[r]["graph"][k], want), (r, k)
+
+
+def _bert_sp_worker(rank, world, port, out):
+    from mifx.models.bert import BertConfig
+    from mifx.parallel.tensor_parallel import TPGroup
+    from mifx.trainer.bert_trainer import BertTrainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        res = {}
+        for sp, graph in ((False, False), (True, False), (True, True)):
+            tp = TPGroup()
+            torch.manual_seed(0)
+            tr = BertTrainer(BertConfig(layers=2, dropout=0.1, sequence_parallel=sp), 4, 128, dev, tp, graph=graph,
+                             tp_ipc=True)
+            assert tr.model.sequence_parallel == sp and tr.use_graph == graph
+            losses = [float(tr.step()) for _ in range(6 if graph else 9)]
+            torch.cuda.synchronize(dev)
+            tp.check()
+            res[(sp, graph)] = (losses, {n: p.detach().float().cpu() for n, p in tr.model.named_parameters()})
+            dist.barrier()
+            tp.disable_ipc()
+        torch.save({f"{int(k[0])}{int(k[1])}": v for k, v in res.items()}, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bert_sequence_parallel_captured_bit_identical_and_tracks_tp(world):
+    """BertTrainer with sequence parallelism on the peer-memory reduce-scatter / all-gather kernels: the captured step
+    is bit-identical to the eager one, the token-shard parameters (LayerNorms, row-parallel biases) stay identical on
+    every rank, and the loss trajectory tracks the plain TP step (same dropout masks; bf16 rounding differs)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "sp")
+        mp.start_processes(_bert_sp_worker, args=(world, _port(), out), nprocs=world, start_method="spawn")
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for r in range(world):
+        (lt, _), (le, pe), (lg, pg) = res[r]["00"], res[r]["10"], res[r]["11"]
+        assert all(torch.isfinite(torch.tensor(le)))
+        assert le[3:] == lg, (r, le, lg)
+        for n in pe:
+            assert torch.equal(pe[n], pg[n]), (r, n)
+        assert all(abs(x - y) <= 3e-2 * max(1.0, abs(x)) for x, y in zip(lt, le)), (r, lt, le)
+    for n, v in res[0]["11"][1].items():
+        if n.endswith(("ln1.weight", "ln1.bias", "ln2.weight", "ln2.bias", "attn_out.bias", "ffn_out.bias")):
+            for r in range(1, world):
+                assert torch.equal(v, res[r]["11"][1][n]), (r, n)

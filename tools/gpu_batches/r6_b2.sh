@@ -8,11 +8,11 @@ set -o pipefail
 mkdir -p gpurun_out/r6
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
+[ "$SKIP_TESTS" = 1 ] || { timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
   "tests/test_parallel_gpu.py::test_resnet50_dp2_on_gpu_replicas_identical_and_match_single" \
   "tests/test_bert_tp.py::test_fused_attention_gpu" \
   > gpurun_out/r6/b2_tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|assert" gpurun_out/r6/b2_tests.log | tail -30; tail -5 gpurun_out/r6/b2_tests.log; exit 1; }
-tail -2 gpurun_out/r6/b2_tests.log
+  tail -2 gpurun_out/r6/b2_tests.log; }
 timeout -k 10 300 python -u -m mifx.trainer.resnet_trainer --steps 20 --warmup 5 > gpurun_out/r6/resnet_1.json 2> gpurun_out/r6/resnet_1.err || { tail -20 gpurun_out/r6/resnet_1.err; exit 1; }
 grep '^{' gpurun_out/r6/resnet_1.json | tail -1
 MIFX_DP_FORCE=1 timeout -k 10 300 python -u -m mifx.trainer.resnet_trainer --steps 20 --warmup 5 > gpurun_out/r6/resnet_dpf.json 2> gpurun_out/r6/resnet_dpf.err || { tail -20 gpurun_out/r6/resnet_dpf.err; exit 1; }
