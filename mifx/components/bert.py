@@ -7,8 +7,9 @@
 * `BertTrainer`: fine-tunes `mifx.models.bert.BertForSequenceClassification` (bf16 autocast, fp32 master AdamW,
   fused HIP LayerNorm / GELU / attention kernels, whole step in one hipGraph at TP=1) on the examples and
   exports the TP=1 state as a ModelExportPath artifact. `custom_config={"tp": N}` runs Megatron-style tensor
-  parallelism over N ranks (one per GPU, RCCL over xGMI; gloo processes on a CPU host) launched by the
-  component itself (mifx.trainer.distributed); rank 0 gathers the full state and exports.
+  parallelism over N ranks (one per GPU, RCCL over xGMI; gloo processes on a CPU host; `"sequence_parallel": true`:
+  token-sharded LayerNorms / dropouts between the TP regions) launched by the component itself
+  (mifx.trainer.distributed); rank 0 gathers the full state and exports.
 
 Contract mirrored from the TFX Trainer of the reference (`airflow-dags/taxi_pipeline.py:92-99`: examples in,
 ModelExportPath out, lineage in MLMD; train_args / eval_args num_steps)."""
@@ -121,7 +122,8 @@ class TextExampleGen(_KwComponent):
 
 
 # ------------------------------------------------------------------------------------------ BertTrainer
-_CFG_KEYS = ("vocab_size", "hidden", "layers", "heads", "intermediate", "max_position", "dropout", "num_labels")
+_CFG_KEYS = ("vocab_size", "hidden", "layers", "heads", "intermediate", "max_position", "dropout", "num_labels",
+             "sequence_parallel")
 
 
 def run_bert_rank(spec: dict) -> dict:
@@ -244,7 +246,7 @@ def load_bert_export(path: str, device="cpu"):
 
     with open(os.path.join(path, "config.json")) as f:
         c = json.load(f)
-    cfg = BertConfig(**{k: c[k] for k in _CFG_KEYS})
+    cfg = BertConfig(**{k: c[k] for k in _CFG_KEYS if k in c})
     m = BertForSequenceClassification(cfg, None, seed=None)
     m.load_full(load_file(os.path.join(path, "variables.safetensors")))
     return m.to(device).eval(), int(c["seq_len"])

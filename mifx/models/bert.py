@@ -7,7 +7,10 @@ FFN 3072, vocab 30522, 512 positions, 2 token types, post-LN, GELU(erf).
 Per layer on each TP rank: one fused QKV column-parallel GEMM for the rank's heads (uneven head
 split when heads % tp != 0), SDPA on the local heads, row-parallel output projection (+1
 all-reduce), fused residual-add + LayerNorm (HIP), column-parallel FFN-in with fused bias+GELU
-(HIP), row-parallel FFN-out (+1 all-reduce), fused residual-add + LayerNorm."""
+(HIP), row-parallel FFN-out (+1 all-reduce), fused residual-add + LayerNorm. With
+`sequence_parallel=True` (TP > 1) each all-reduce is a reduce-scatter into the rank's token shard, the LayerNorms /
+dropouts / residual adds run on that shard, and an all-gather feeds the next column-parallel projection
+(BertLayer.forward_sp)."""
 from __future__ import annotations
 
 import os
@@ -248,7 +251,12 @@ class BertForSequenceClassification(nn.Module):
         mask = None
         if attention_mask is not None:  # additive key bias [B, S] (fp32; -1e30 on padding keys)
             mask = ((1.0 - attention_mask.float()) * -1e30).contiguous()
-        if self.sequence_parallel:
+        sp = self.sequence_parallel
+        if sp and (B * S) % self.tp.size:
+            if self.training and torch.is_grad_enabled():
+                raise ValueError(f"sequence parallelism: {B} x {S} tokens do not split over {self.tp.size} ranks")
+            sp = False  # (inference on an odd-sized batch: the replicated layers compute the same function)
+        if sp:
             # the layers' residual stream: this rank's token rows, in the dtype the projections compute in
             cdt = torch.get_autocast_dtype("cuda") if x.is_cuda and torch.is_autocast_enabled("cuda") else x.dtype
             x = scatter_to_seq(x.reshape(B * S, -1), self.tp, cdt)

@@ -77,7 +77,26 @@ def _fwd(x, x2, weight, bias, run_mean, run_var, momentum, eps, relu):
 _LAYOUT_DIAG = __import__("os").environ.get("MIFX_BN_LAYOUT_DIAG") == "1"
 
 
-def _bwd(dy, x, w32, stats, relu, dres):
+def _grad_dests(ctx):
+    """(dgamma, dbeta) output tensors: the data-parallel bucket views when the deferred-gradient context hands them out
+    (mifx.ops.gemm.grad_destination), else fresh [2, C] fp32 rows."""
+    wb = getattr(ctx, "mifx_wb", None)
+    if wb is None:
+        return None
+    from .gemm import grad_destination
+
+    dw, db = (grad_destination(t) for t in wb)
+    return (dw, db) if dw is not None and db is not None else None
+
+
+def _dgb(C, dev, dst):
+    if dst is not None:
+        return dst
+    d = torch.empty(2, C, device=dev, dtype=torch.float32)
+    return d[0], d[1]
+
+
+def _bwd(dy, x, w32, stats, relu, dres, dst=None):
     if _LAYOUT_DIAG:
         for nm, t in (("dy", dy), ("dres", dres)):
             if t is not None and t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
@@ -94,7 +113,7 @@ def _bwd(dy, x, w32, stats, relu, dres):
     nb = _fns()["blocks"](M, C)
     part = torch.empty(2, nb, C, device=x.device, dtype=torch.float32)
     kbuf = torch.empty(3, C, device=x.device, dtype=torch.float32)
-    dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    dgb = _dgb(C, x.device, dst)
     dx = torch.empty_like(x)
     check(_fns()["bwd"](_dt(x), ptr(dv), ptr(v), ptr(_nhwc_view(dres) if dres is not None else None), M, C, ptr(w32),
                         ptr(stats), int(relu), ptr(part), ptr(kbuf), ptr(dx), ptr(dgb[0]), ptr(dgb[1]),
@@ -121,7 +140,7 @@ def _take_tiles(ctx, dy):
     return part
 
 
-def _bwd_tiles(dy, x, w32, stats, dres, part, act=None):
+def _bwd_tiles(dy, x, w32, stats, dres, part, act=None, dst=None):
     """Backward of relu(bn(x)) from the per-tile sums the producing GEMM reduced: finalize + apply only. act: also
     write the forward's activation relu(bn(x)) there (same layout as x)."""
     if dres is not None:
@@ -132,7 +151,7 @@ def _bwd_tiles(dy, x, w32, stats, dres, part, act=None):
     M, C = v.shape
     T = part.shape[1]
     kbuf = torch.empty(3, C, device=x.device, dtype=torch.float32)
-    dgb = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    dgb = _dgb(C, x.device, dst)
     dx = torch.empty_like(x)
     check(_fns()["bwd_tiles"](_dt(x), ptr(dv), ptr(v), ptr(_nhwc_view(dres) if dres is not None else None), M, C,
                               ptr(w32), ptr(stats), 1, ptr(part[0]), ptr(part[1]), T, ptr(kbuf), ptr(dx), ptr(dgb[0]),
@@ -143,9 +162,10 @@ def _bwd_tiles(dy, x, w32, stats, dres, part, act=None):
 
 def _bwd_any(ctx, dy, x, w32, stats, relu, dres):
     part = _take_tiles(ctx, dy) if relu else None
+    dst = _grad_dests(ctx)
     if part is not None and x.dtype == torch.bfloat16 and _nhwc_view(dy) is not None:
-        return _bwd_tiles(dy, x, w32, stats, dres, part)
-    return _bwd(dy, x, w32, stats, relu, dres)
+        return _bwd_tiles(dy, x, w32, stats, dres, part, dst=dst)
+    return _bwd(dy, x, w32, stats, relu, dres, dst=dst)
 
 
 def _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, relu, apply=True):
@@ -175,7 +195,7 @@ class _BNReLUTiles(torch.autograd.Function):
     def forward(ctx, x, part, weight, bias, run_mean, run_var, momentum, eps):
         y, w32, stats = _fwd_tiles(x, part, weight, bias, run_mean, run_var, momentum, eps, True)
         ctx.save_for_backward(x, w32, stats)
-        ctx.wdtype, ctx.mifx_bn = weight.dtype, True
+        ctx.wdtype, ctx.mifx_bn, ctx.mifx_wb = weight.dtype, True, (weight, bias)
         ctx.set_materialize_grads(False)
         ctx.mark_non_differentiable(part)
         return y, x.view_as(x)
@@ -194,7 +214,7 @@ class _BNReLU(torch.autograd.Function):
     def forward(ctx, x, weight, bias, run_mean, run_var, momentum, eps, relu):
         y, _, w32, stats = _fwd(x, None, weight, bias, run_mean, run_var, momentum, eps, relu)
         ctx.save_for_backward(x, w32, stats)
-        ctx.relu, ctx.wdtype, ctx.mifx_bn = relu, weight.dtype, bool(relu)
+        ctx.relu, ctx.wdtype, ctx.mifx_bn, ctx.mifx_wb = relu, weight.dtype, bool(relu), (weight, bias)
         return y
 
     @staticmethod
@@ -214,7 +234,7 @@ class _AddBNReLU(torch.autograd.Function):
     def forward(ctx, a, b, weight, bias, run_mean, run_var, momentum, eps):
         y, s, w32, stats = _fwd(a, b.to(a.dtype), weight, bias, run_mean, run_var, momentum, eps, True)
         ctx.save_for_backward(s, w32, stats)
-        ctx.wdtype, ctx.mifx_bn = weight.dtype, True
+        ctx.wdtype, ctx.mifx_bn, ctx.mifx_wb = weight.dtype, True, (weight, bias)
         # an unused output (s, when the next block has a projection shortcut) arrives as None instead of
         # a materialised zero tensor: autograd created those in NCHW, forcing a full channels_last copy
         # (plus a read of zeros) in the backward of the first block of every stage

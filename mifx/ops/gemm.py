@@ -276,6 +276,20 @@ def _placeholder(w: torch.Tensor) -> tuple[torch.Tensor, bool]:
     return torch.empty_like(w), True
 
 
+def grad_destination(p: torch.Tensor) -> torch.Tensor | None:
+    """Inside deferred_weight_grads(view_of=...): the memory p's gradient should be written into (the data-parallel
+    bucket view) when autograd will adopt the returned tensor as p.grad (p.grad is None), for backward kernels that
+    produce a parameter gradient themselves (BatchNorm's dgamma / dbeta: written straight into the bucket instead of
+    into a fresh tensor that autograd then adds or the bucket hook copies in). None otherwise."""
+    if not _DEFER["on"] or p.grad is not None:
+        return None
+    vf = _DEFER.get("view_of")
+    v = vf(p) if vf is not None else None
+    if v is not None and v.shape == p.shape and v.dtype == torch.float32 and v.is_contiguous():
+        return v
+    return None
+
+
 def pending_weights() -> set:
     """ids of the weights with a recorded (not yet flushed) fp32 weight-gradient product."""
     return {id(rec[2]) for rec in _DEFER.get("pending_f32", [])}

@@ -199,14 +199,15 @@ class DataParallel:
         return self._view(self.buckets[w[0]], w[1])
 
     def release_grads_for_defer(self) -> None:
-        """Before a backward with deferred weight gradients: drop the 4-D weights' .grad (their bucket memory stays), so
-        autograd adopts the bucket view handed out as the placeholder (grad_view) instead of adding a zero tensor into
-        the existing view; a weight the flush does not take gets its computed gradient copied back into the bucket by
-        the post-accumulate hook."""
+        """Before a backward with deferred weight gradients, instead of zero_grad(): drop every parameter's .grad (the
+        bucket memory stays), so autograd adopts the bucket view handed out as the placeholder of a deferred product
+        (grad_view) or as the output of a kernel that writes a parameter gradient itself (BatchNorm's dgamma / dbeta,
+        mifx.ops.gemm.grad_destination) -- the gradient is WRITTEN into the bucket, with no memset of the buckets and no
+        zero-fill + add. A gradient produced elsewhere is copied into the bucket by the post-accumulate hook; a parameter
+        that gets no gradient has its slot zeroed by finish()."""
         for b in self.buckets:
             for p in b.params:
-                if p.dim() == 4:
-                    p.grad = None
+                p.grad = None
 
     def _launch_ready(self) -> None:
         """Launch every complete bucket from the next one in bucket order on."""
@@ -250,6 +251,12 @@ class DataParallel:
             return
         for b in self.buckets[self._next:]:  # (in order: an incomplete bucket holds back its successors)
             self._flush_deferred(b)
+            if self.views:  # released gradients that never arrived: a zero slot (see release_grads_for_defer)
+                for pi, p in enumerate(b.params):
+                    if p.grad is None:
+                        v = self._view(b, pi)
+                        v.zero_()
+                        p.grad = v
             if b.work is None and not self.views:  # unused params this step: contribute zeros for them
                 for pi, p in enumerate(b.params):
                     if pi not in b.ready:

@@ -123,10 +123,11 @@ class ResNetTrainer:
         for pg in self.opt.param_groups:
             pg["lr"] = self._lr()
         if self.dp is not None:
-            self.dp.zero_grad()  # the bucket buffers ARE the gradients (views): one memset per bucket
-            if self.defer_dw:
+            if self.defer_dw:  # gradients WRITTEN into the bucket views (deferred products, BatchNorm): no memset
                 self.dp.deferred = True
-                self.dp.release_grads_for_defer()  # deferred products are written straight into the bucket views
+                self.dp.release_grads_for_defer()
+            else:
+                self.dp.zero_grad()  # the bucket buffers ARE the gradients (views): one memset per bucket
         else:
             self.opt.zero_grad(set_to_none=True)
         total = 0.0
@@ -196,11 +197,12 @@ class ResNetTrainer:
     def _fwd_bwd_captured(self) -> torch.Tensor:
         defer = self.defer_dw
         if self.dp is not None:
-            for b in self.dp.buckets:  # param.grad are views of these
-                b.buf.zero_()
-            if defer:
+            if defer:  # gradients written into the bucket views (see _eager_step)
                 self.dp.deferred = True
                 self.dp.release_grads_for_defer()
+            else:
+                for b in self.dp.buckets:  # param.grad are views of these
+                    b.buf.zero_()
         elif defer:
             # gradients produced inside the graph (its private pool: the same addresses on every replay, which the
             # captured SGD reads); the deferred weight-gradient flush then overwrites instead of zero-fill + add

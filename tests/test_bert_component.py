@@ -17,11 +17,11 @@ from mifx.orchestration import LocalDagRunner, Pipeline
 TINY = dict(vocab_size=1000, hidden=64, layers=2, heads=4, intermediate=128, max_position=64, dropout=0.0)
 
 
-def _pipe(root, name, tp, steps=40, device="cpu"):
+def _pipe(root, name, tp, steps=40, device="cpu", **extra):
     eg = TextExampleGen(num_synthetic=480, seq_len=32, vocab_size=1000, num_labels=2, seed=3)
     tr = BertTrainer(examples=eg.outputs.examples, train_args=TrainArgs(num_steps=steps),
                      eval_args=EvalArgs(num_steps=5),
-                     custom_config=dict(TINY, tp=tp, batch_size=16, learning_rate=1e-3, graph=False))
+                     custom_config=dict(TINY, tp=tp, batch_size=16, learning_rate=1e-3, graph=False, **extra))
     p = Pipeline(pipeline_name=name, pipeline_root=str(root / name), components=[eg, tr],
                  metadata_db_root=str(root / f"md_{name}"))
     res = LocalDagRunner(device=device).run(p)
@@ -56,6 +56,18 @@ def test_bert_trainer_component_tp2_matches_tp1(tmp_path):
     m2, s2 = _export(a2)
     assert a2.custom_properties["tp"] == 2
     assert set(s1) == set(s2)
+    for k in s1:
+        np.testing.assert_allclose(s2[k].numpy(), s1[k].numpy(), rtol=1e-3, atol=2e-5, err_msg=k)
+    np.testing.assert_allclose(m2["losses"], m1["losses"], rtol=1e-4)
+
+
+def test_bert_trainer_component_tp2_sequence_parallel_matches_tp1(tmp_path):
+    """custom_config sequence_parallel: the token-sharded TP=2 trainer (gloo ranks) exports the TP=1 model."""
+    _, a1 = _pipe(tmp_path, "sp1", 1, steps=15)
+    _, a2 = _pipe(tmp_path, "sp2", 2, steps=15, sequence_parallel=True)
+    m1, s1 = _export(a1)
+    m2, s2 = _export(a2)
+    assert json.load(open(os.path.join(m2["export"], "config.json")))["sequence_parallel"] is True
     for k in s1:
         np.testing.assert_allclose(s2[k].numpy(), s1[k].numpy(), rtol=1e-3, atol=2e-5, err_msg=k)
     np.testing.assert_allclose(m2["losses"], m1["losses"], rtol=1e-4)

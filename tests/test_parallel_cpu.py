@@ -168,6 +168,29 @@ def test_ddp_ipc_exchange_needs_cuda():
         DataParallel(_Net(), exchange="nope")
 
 
+def test_ddp_released_gradients_unused_parameter_gets_zero_slot():
+    """release_grads_for_defer() replaces the per-step bucket memset: a parameter that receives no gradient in the step
+    finds its (stale) bucket slot zeroed by finish() and its .grad re-attached as the view."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.ModuleDict({"a": torch.nn.Linear(4, 4), "unused": torch.nn.Linear(4, 4)})
+        dp = DataParallel(net, grad_as_bucket_view=True, force=True)
+        for b in dp.buckets:
+            b.buf.fill_(5.0)  # stale contents from an earlier step
+        dp.release_grads_for_defer()
+        net["a"](torch.randn(3, 4)).sum().backward()
+        dp.finish()
+        for name, p in net.named_parameters():
+            b, pi = dp._where[p]
+            assert p.grad.data_ptr() == dp._view(dp.buckets[b], pi).data_ptr(), name
+        assert torch.all(net["unused"].weight.grad == 0) and torch.all(net["unused"].bias.grad == 0)
+        assert torch.all(net["a"].bias.grad == 3.0)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_ddp_deferred_flush_per_bucket_before_its_exchange(monkeypatch):
     """Deferred weight gradients under DataParallel: a bucket's recorded products are flushed (into its views) when the
     bucket's last gradient arrives, and its exchange is launched right after; a released 4-D weight whose gradient
@@ -204,7 +227,7 @@ def test_ddp_deferred_flush_per_bucket_before_its_exchange(monkeypatch):
         dp._launch = spy
         dp.zero_grad()
         dp.release_grads_for_defer()
-        assert net[0].weight.grad is None and deferred_w.grad is None and net[4].weight.grad is not None
+        assert all(p.grad is None for p in net.parameters())  # released: gradients are WRITTEN into the buckets
         x = torch.randn(2, 3, 8, 8).to(memory_format=torch.channels_last)
 
         class _Defer(torch.autograd.Function):  # what the conv ops do: a placeholder gradient, the product later
