@@ -290,6 +290,26 @@ def grad_destination(p: torch.Tensor) -> torch.Tensor | None:
     return None
 
 
+def pending_work(weights) -> int:
+    """Approximate workgroup count of the grouped flush of these weights' recorded fp32 products (256 x 256 output
+    tiles, 4x as many where a 128-wide dimension forces the small tiles, times the token chunks): how much of the GPU
+    one flush of them would fill (mifx.parallel.ddp coalesces bucket flushes until it is worth a launch)."""
+    ids = {id(w) for w in weights}
+    n = 0
+    for rec in _DEFER.get("pending_f32", []):
+        if id(rec[2]) not in ids:
+            continue
+        dy, w = rec[0], rec[2]
+        T, M = dy.shape
+        N = w.numel() // M
+        aux = rec[4] if len(rec) > 4 else None
+        ck = rec[5] if len(rec) > 5 else _WGRAD_CHUNK
+        taps = getattr(aux, "mifx_taps", 1) if aux is not None and aux.dtype == torch.uint8 else 1
+        small = M % 256 or (N // taps) % 256
+        n += -(-M // 256) * -(-N // 256) * (4 if small else 1) * -(-T // ck)
+    return n
+
+
 def pending_weights() -> set:
     """ids of the weights with a recorded (not yet flushed) fp32 weight-gradient product."""
     return {id(rec[2]) for rec in _DEFER.get("pending_f32", [])}

@@ -33,6 +33,7 @@ exercise it."""
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -96,6 +97,9 @@ class DataParallel:
         dev = params[0].device if params else torch.device("cpu")
         self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self._next = 0  # the next bucket to launch (buckets launch in order)
+        # coalesced deferred flushes: the smallest grouped launch worth issuing before the end of the backward
+        # (workgroups; 4 waves of the 256 CUs), MIFX_DP_FLUSH_MIN_WG overrides (0: one flush per bucket)
+        self.flush_min_wgs = int(os.environ.get("MIFX_DP_FLUSH_MIN_WG", "1024"))
         self.deferred = False  # set by a trainer whose backward records weight gradients for grouped flushes
         self._ipc = None
         if exchange != "rccl" and self.active:
@@ -174,19 +178,46 @@ class DataParallel:
         if not self.views:
             view.copy_(p.grad.reshape(-1))
         if len(b.ready) == len(b.params):
-            self._flush_deferred(b)
-            self._launch_ready()
+            self._complete_ready()
+
+    def _complete_ready(self) -> None:
+        """A bucket just completed. Without deferred products: launch every complete bucket in order. With them: the
+        run of complete, unlaunched buckets (from the next one in launch order) is flushed in ONE grouped launch and
+        their exchanges launched right after -- but only once the run's recorded work fills the GPU (flush_min_wgs
+        workgroups): a bucket of few, small products (the last stage's weights hold few output tiles) flushed alone
+        leaves most CUs idle, which measured +0.9 ms over one flush per step in the ResNet-50 DP step
+        (profiles/resnet_dp_census_r6.md). Later flushes still overlap the earlier buckets' exchanges."""
+        run = []
+        for b in self.buckets[self._next:]:
+            if len(b.ready) != len(b.params):
+                break
+            run.append(b)
+        if not run:
+            return
+        if self.deferred:
+            from ..ops import gemm as hg
+
+            pend = hg.pending_weights()
+            mine = [p for b in run for p in b.params if id(p) in pend]
+            if mine:
+                if hg.pending_work(mine) < self.flush_min_wgs:
+                    return  # wait for more buckets (finish() flushes whatever is left)
+                hg.flush_weight_grads(mine)
+        self._launch_ready()
 
     def _flush_deferred(self, b: _Bucket) -> None:
-        """Deferred weight gradients (mifx.ops.gemm.deferred_weight_grads): the bucket's recorded dW products run as
-        ONE grouped launch on the compute stream, written straight into the bucket views, before its exchange is
-        launched -- so each later bucket's flush overlaps the earlier buckets' exchanges."""
+        """Deferred weight gradients (mifx.ops.gemm.deferred_weight_grads): the bucket's recorded dW products as one
+        grouped launch on the compute stream, written straight into the bucket views (finish(): every remaining
+        bucket's at once)."""
+        self._flush_many([b])
+
+    def _flush_many(self, buckets) -> None:
         if not self.deferred:
             return
         from ..ops import gemm as hg
 
         pend = hg.pending_weights()
-        mine = [p for p in b.params if id(p) in pend]
+        mine = [p for b in buckets for p in b.params if id(p) in pend]
         if mine:
             hg.flush_weight_grads(mine)
 
@@ -249,8 +280,8 @@ class DataParallel:
         the averaged gradients back into `param.grad`."""
         if not self.active or not self._sync:
             return
+        self._flush_many(self.buckets[self._next:])  # ONE grouped launch for every bucket not launched yet
         for b in self.buckets[self._next:]:  # (in order: an incomplete bucket holds back its successors)
-            self._flush_deferred(b)
             if self.views:  # released gradients that never arrived: a zero slot (see release_grads_for_defer)
                 for pi, p in enumerate(b.params):
                     if p.grad is None:

@@ -168,6 +168,48 @@ def test_ddp_ipc_exchange_needs_cuda():
         DataParallel(_Net(), exchange="nope")
 
 
+def test_ddp_coalesces_small_deferred_flushes(monkeypatch):
+    """Buckets whose recorded products would not fill the GPU are not flushed alone: their flush (and exchange) waits
+    until the run of complete buckets carries flush_min_wgs workgroups of work, else it is ONE flush in finish()."""
+    from mifx.ops import gemm as hg
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(*[torch.nn.Linear(16, 16) for _ in range(4)])
+        dp = DataParallel(net, bucket_cap_mb=0.0005, grad_as_bucket_view=True, force=True)
+        assert len(dp.buckets) >= 4
+        dp.deferred = True
+        ws = [m.weight for m in net]
+        pending = {id(w) for w in ws}
+        calls, launches = [], []
+        monkeypatch.setattr(hg, "pending_weights", lambda: set(pending))
+        monkeypatch.setattr(hg, "pending_work", lambda weights: 300 * len(weights))
+
+        def fake_flush(weights=None):
+            calls.append(sorted(next(i for i, x in enumerate(ws) if x is w) for w in weights))
+            for w in weights:
+                pending.discard(id(w))
+            return len(weights)
+
+        monkeypatch.setattr(hg, "flush_weight_grads", fake_flush)
+        launch = dp._launch
+        dp._launch = lambda b: (launches.append((any(any(p is w for w in ws) for p in b.params), len(calls))),
+                                launch(b))
+        dp.flush_min_wgs = 1024  # 4 weights' worth (300 each)
+        dp.release_grads_for_defer()
+        net(torch.randn(2, 16)).sum().backward()
+        dp.finish()
+        # backward completes the last layer's bucket first; 4 x 300 >= 1024 only with all four weights
+        assert calls == [[0, 1, 2, 3]], calls
+        # every bucket holding a deferred weight is exchanged after the one flush (bias-only buckets go at once)
+        assert [n for has_w, n in launches if has_w] == [1, 1, 1, 1], launches
+        assert len(launches) == len(dp.buckets)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_ddp_released_gradients_unused_parameter_gets_zero_slot():
     """release_grads_for_defer() replaces the per-step bucket memset: a parameter that receives no gradient in the step
     finds its (stale) bucket slot zeroed by finish() and its .grad re-attached as the view."""
@@ -206,6 +248,7 @@ def test_ddp_deferred_flush_per_bucket_before_its_exchange(monkeypatch):
         dp = DataParallel(net, bucket_cap_mb=0.001, grad_as_bucket_view=True, force=True)
         assert len(dp.buckets) >= 3
         dp.deferred = True
+        dp.flush_min_wgs = 0  # every complete bucket flushed at once (the coalescing threshold: next test)
         deferred_w = net[2].weight  # pretend the 1x1 conv's dW was recorded for a grouped flush
         events, pending = [], {id(deferred_w)}
         monkeypatch.setattr(hg, "pending_weights", lambda: set(pending))

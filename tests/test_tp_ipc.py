@@ -464,7 +464,7 @@ def _bert_sp_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bert_sequence_parallel_captured_bit_identical_and_tracks_tp(world):
     """BertTrainer with sequence parallelism on the peer-memory reduce-scatter / all-gather kernels: the captured step
     is bit-identical to the eager one, the token-shard parameters (LayerNorms, row-parallel biases) stay identical on
