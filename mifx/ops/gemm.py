@@ -131,6 +131,31 @@ def config_details() -> tuple[tuple[int, int, int], ...]:
 # did not change that: profiles/archive/gemm_hip_r3c_fasterf.jsonl), FFN-out 28.9 vs 25.1 us. MIFX_HIP_GEMM=all routes every
 # eligible shape to the kernel (heuristic configuration) for A/B runs.
 TUNED: dict[tuple[int, int, int], int] = {(4096, 768, 768): 13}
+# forward products routed to the 8-wave pipelined kernel (csrc/gemm8.hip) instead: (M, N, K) -> gemm8 configuration.
+# MIFX_G8_FWD=1 (A/B) routes BERT-base's QKV / FFN-in / FFN-out shapes at 4096 tokens to the 256 x 256 tiles
+# (profiles/bert_fwd_routes_r5.jsonl: QKV 24.3 us standalone vs hipBLASLt 21.1, but 33.6 us per call inside the step
+# on the bundled TunableOp solution, profiles/bert_steady_r5.md)
+G8_FWD: dict[tuple[int, int, int], int] = {}
+_g8f = os.environ.get("MIFX_G8_FWD", "")
+if _g8f == "1":
+    G8_FWD.update({(4096, 2304, 768): 0, (4096, 3072, 768): 0, (4096, 768, 3072): 3})
+elif _g8f:  # "M:N:K=cfg+..." (A/B sweeps)
+    for _item in _g8f.split("+"):
+        _shape, _cfg = _item.split("=")
+        G8_FWD[tuple(int(v) for v in _shape.split(":"))] = int(_cfg)
+
+
+def _g8_fwd(M: int, N: int, K: int) -> int | None:
+    return G8_FWD.get((M, N, K))
+
+
+def fwd_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0):
+    """The forward product on the routed hand-written kernel: gemm8 where G8_FWD names the shape, else csrc/gemm.hip
+    (same (Y, Z) contract: epi 0 / 1 bias / 2 bias + GELU with Z)."""
+    cfg = _g8_fwd(x2.shape[0], w.shape[0], x2.shape[1])
+    if cfg is not None:
+        return gemm8_nt(x2, w, bias, epi, cfg=cfg)
+    return gemm_nt(x2, w, bias, epi)
 
 
 def pick_config(M: int, N: int, K: int, cus: int = 256) -> int | None:
@@ -156,7 +181,7 @@ def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
         return False
     M = x.numel() // x.shape[-1]
     N, K = w.shape
-    return x.shape[-1] == K and pick_config(M, N, K) is not None
+    return x.shape[-1] == K and (pick_config(M, N, K) is not None or (M, N, K) in G8_FWD)
 
 
 def preferred(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -165,7 +190,8 @@ def preferred(x: torch.Tensor, w: torch.Tensor) -> bool:
         return False
     if os.environ.get("MIFX_HIP_GEMM") == "all":
         return True
-    return (x.numel() // x.shape[-1], *w.shape) in TUNED
+    key = (x.numel() // x.shape[-1], *w.shape)
+    return key in TUNED or key in G8_FWD
 
 
 def gemm_nt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, epi: int = 0,
@@ -588,7 +614,7 @@ class _Linear(torch.autograd.Function):
             if bias is not None:
                 y = y + bias.to(y.dtype)
         elif hip_fwd:
-            y, _ = gemm_nt(x2, w, bias, 1 if bias is not None else 0)
+            y, _ = fwd_nt(x2, w, bias, 1 if bias is not None else 0)
         else:
             y = F.linear(x2, w, bias)
         ctx.save_for_backward(x2, w)
@@ -630,7 +656,7 @@ class _LinearBiasGelu(torch.autograd.Function):
     def forward(ctx, x, w, bias, slot=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        y, z = gemm_nt(x2, w, bias, 2)
+        y, z = fwd_nt(x2, w, bias, 2)
         ctx.slot = slot
         from .fused_bert import _param
 
@@ -1130,7 +1156,7 @@ class _FFN(torch.autograd.Function):
         from .fused_bert import _fns as fb_fns, _dt, _param
 
         if preferred(x2, w1):
-            y1, z = gemm_nt(x2, w1, b1, 2)
+            y1, z = fwd_nt(x2, w1, b1, 2)
         else:
             z = F.linear(x2, w1)
             bp = _param(b1)
@@ -1147,7 +1173,7 @@ class _FFN(torch.autograd.Function):
             out = gemm_allreduce_overlapped(y1, lambda yc: gemm_nt(yc, w2)[0] if fwd2 else F.linear(yc, w2),
                                             w2.shape[0], tp)
         else:
-            out = gemm_nt(y1, w2)[0] if fwd2 else F.linear(y1, w2)
+            out = fwd_nt(y1, w2)[0] if fwd2 else F.linear(y1, w2)
         ctx.save_for_backward(x2, w1, b1, z, y1, w2)
         ctx.slot = slot
         return out.view(*shp[:-1], w2.shape[0])

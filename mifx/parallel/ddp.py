@@ -40,6 +40,11 @@ import torch
 import torch.distributed as dist
 
 
+# diagnostic: where the bucket exchange runs -- "side" (default: the communication stream, overlapping the backward),
+# "main" (the compute stream), "join" (side stream, joined right after each launch)
+_COMM_DIAG = os.environ.get("MIFX_DP_COMM", "side")
+
+
 @dataclass
 class _Bucket:
     params: list
@@ -98,8 +103,16 @@ class DataParallel:
         self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
         self._next = 0  # the next bucket to launch (buckets launch in order)
         # coalesced deferred flushes: the smallest grouped launch worth issuing before the end of the backward
-        # (workgroups; 4 waves of the 256 CUs), MIFX_DP_FLUSH_MIN_WG overrides (0: one flush per bucket)
-        self.flush_min_wgs = int(os.environ.get("MIFX_DP_FLUSH_MIN_WG", "1024"))
+        # (workgroups), MIFX_DP_FLUSH_MIN_WG. Default: never -- ONE grouped flush after the backward, then the bucket
+        # exchanges. Measured on the ResNet-50 B=256 step forced onto one rank (profiles/resnet_dp_census_r6.md,
+        # profiles/resnet_dp_flush_r6.md): one flush + exchanges after the backward 21.46 ms vs 23.10 ms for a flush
+        # and an overlapped exchange per bucket (0), whose small grouped launches leave CUs idle (+0.9 ms of flush
+        # time). Thresholds in between (1024 / 2048: runs of buckets flushed together, their exchanges overlapping the
+        # rest of the backward) train correctly eagerly but diverge in captured replays -- unresolved, so not the
+        # default (tools/dp_flush_diag.py reproduces it).
+        self.flush_min_wgs = int(os.environ.get("MIFX_DP_FLUSH_MIN_WG", str(1 << 40)))
+        self._flush_last = os.environ.get("MIFX_DP_FLUSH_LAST", "0") == "1"  # (diagnostic switches, A/B)
+        self._launch_late = os.environ.get("MIFX_DP_LAUNCH_LATE", "0") == "1"
         self.deferred = False  # set by a trainer whose backward records weight gradients for grouped flushes
         self._ipc = None
         if exchange != "rccl" and self.active:
@@ -125,7 +138,8 @@ class DataParallel:
         try:
             # split waits: the exchange runs on a side stream beside the backward's whole-CU GEMM kernels (the
             # deferred weight-gradient flushes), so no exchange workgroup may spin on a late peer
-            return IpcAllReduce(self.pg, dev, max(b.numel for b in self.buckets), dtype=torch.float32, waiters=True)
+            return IpcAllReduce(self.pg, dev, max(b.numel for b in self.buckets), dtype=torch.float32,
+                                waiters=os.environ.get("MIFX_DP_WAITERS", "1") != "0")
         except RuntimeError:
             if required:
                 raise
@@ -199,11 +213,13 @@ class DataParallel:
 
             pend = hg.pending_weights()
             mine = [p for b in run for p in b.params if id(p) in pend]
+            last = run[-1] is self.buckets[-1]  # every bucket complete: flush now, whatever the size
             if mine:
-                if hg.pending_work(mine) < self.flush_min_wgs:
+                if hg.pending_work(mine) < self.flush_min_wgs and not (last and self._flush_last):
                     return  # wait for more buckets (finish() flushes whatever is left)
                 hg.flush_weight_grads(mine)
-        self._launch_ready()
+        if not self._launch_late:
+            self._launch_ready()
 
     def _flush_deferred(self, b: _Bucket) -> None:
         """Deferred weight gradients (mifx.ops.gemm.deferred_weight_grads): the bucket's recorded dW products as one
@@ -251,14 +267,20 @@ class DataParallel:
     def _launch(self, b: _Bucket) -> None:
         assert b is self.buckets[self._next], "buckets launch in order"
         self._next += 1
-        if self._comm_stream is not None:
-            self._comm_stream.wait_stream(torch.cuda.current_stream(b.buf.device))
+        if self._comm_stream is not None and self._ipc is not None and _COMM_DIAG == "main":
+            self._ipc.all_reduce(b.buf, out=b.buf, scale=1.0 / self.world if self.average else 1.0)
+            b.work = "ipc"
+        elif self._comm_stream is not None:
+            cur = torch.cuda.current_stream(b.buf.device)
+            self._comm_stream.wait_stream(cur)
             with torch.cuda.stream(self._comm_stream):
                 if self._ipc is not None:  # averaged in the kernel; stream-ordered, graph-capturable
                     self._ipc.all_reduce(b.buf, out=b.buf, scale=1.0 / self.world if self.average else 1.0)
                     b.work = "ipc"
                 else:
                     b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
+            if _COMM_DIAG == "join":
+                cur.wait_stream(self._comm_stream)
         else:
             b.work = dist.all_reduce(b.buf, group=self.pg, async_op=True)
 

@@ -254,7 +254,7 @@ def main(argv=None):
         torch.cuda.tunable.tuning_enable(True)
         torch.cuda.tunable.set_filename(a.tunable)
         torch.cuda.tunable.set_max_tuning_iterations(30)
-    elif not a.no_gemm_table and torch.cuda.is_available():
+    elif not a.no_gemm_table and os.environ.get("MIFX_BERT_GEMM_TABLE", "1") != "0" and torch.cuda.is_available():
         load_gemm_table()
     env = mdist.init()
     dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")

@@ -203,3 +203,34 @@ def test_gemm8_tn_grouped_narrow_fp32(M, N):
     want = c + a.float().t() @ b.float()
     gemm.gemm8_tn_grouped([(a, b, c)], chunk=2048)
     torch.testing.assert_close(c, want, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_forward_route_to_gemm8_matches_fp32(monkeypatch):
+    """G8_FWD (MIFX_G8_FWD): the BERT forward projections routed to the 8-wave kernel -- linear with bias, the fused
+    FFN (bias + GELU epilogue with its Z output, then FFN-out) -- against fp32 references, forward and backward."""
+    from mifx.ops import native_stats  # noqa: F401  (dispatch counters are exercised on the way)
+
+    dev = torch.device("cuda")
+    M, H, I = 512, 256, 512
+    monkeypatch.setattr(gemm, "G8_FWD", {(M, 3 * H, H): 0, (M, I, H): 3, (M, H, I): 5})
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = (torch.randn(M, H, device=dev, generator=g) * 0.5).bfloat16().requires_grad_()
+    w = (torch.randn(3 * H, H, device=dev, generator=g) * 0.05).bfloat16().requires_grad_()
+    b = (torch.randn(3 * H, device=dev, generator=g) * 0.1).bfloat16().requires_grad_()
+    y = gemm.linear(x, w, b)
+    ref = x.float() @ w.float().t() + b.float()
+    assert (y.float() - ref).norm() / ref.norm() < 1e-2
+    w1 = (torch.randn(I, H, device=dev, generator=g) * 0.05).bfloat16().requires_grad_()
+    b1 = (torch.randn(I, device=dev, generator=g) * 0.1).bfloat16().requires_grad_()
+    w2 = (torch.randn(H, I, device=dev, generator=g) * 0.05).bfloat16().requires_grad_()
+    o = gemm.ffn(x, w1, b1, w2)
+    xf = x.detach().float().requires_grad_()
+    w1f, b1f, w2f = (t.detach().float().requires_grad_() for t in (w1, b1, w2))
+    of = torch.nn.functional.gelu(xf @ w1f.t() + b1f) @ w2f.t()
+    assert (o.float() - of).norm() / of.norm() < 2e-2
+    go = torch.randn_like(of)
+    o.backward(go.bfloat16())
+    of.backward(go)
+    for a, r in ((w1.grad, w1f.grad), (b1.grad, b1f.grad), (w2.grad, w2f.grad)):
+        assert (a.float() - r).norm() / r.norm() < 3e-2

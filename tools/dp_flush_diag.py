@@ -1,0 +1,45 @@
+"""Diagnostic: the ResNet-50 DP step forced on one rank (IPC exchange) with a given coalescing threshold
+(MIFX_DP_FLUSH_MIN_WG): per-step losses, eager or captured, and the gradients after the first step saved for a diff
+across thresholds. usage: python tools/dp_flush_diag.py OUT.pt [--graph] [--batch 256] [--steps 3]"""
+import argparse
+import os
+import socket
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    from mifx.trainer.resnet_trainer import ResNetTrainer, synthetic_imagenet
+
+    dev = torch.device("cuda", 0)
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    imgs, labels = synthetic_imagenet(1024, seed=0, device=dev)
+    tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=torch.distributed.group.WORLD, warmup_steps=10,
+                       graph=a.graph, force_dp=True, seed=0)
+    losses, grads = [], None
+    for i in range(a.steps):
+        losses.append(float(tr.step()))
+        torch.cuda.synchronize()
+        if grads is None and (not a.graph or tr._gA is not None):
+            grads = {n: p.grad.detach().float().cpu().clone() for n, p in tr.model.named_parameters()
+                     if p.grad is not None}
+    tr.dp.check()
+    torch.save({"losses": losses, "grads": grads, "min_wg": tr.dp.flush_min_wgs, "graph": a.graph}, a.out)
+    print(os.environ.get("MIFX_DP_FLUSH_MIN_WG"), a.graph, losses, flush=True)
+    torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
