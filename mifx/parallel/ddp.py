@@ -41,7 +41,8 @@ import torch.distributed as dist
 
 
 # diagnostic: where the bucket exchange runs -- "side" (default: the communication stream, overlapping the backward),
-# "main" (the compute stream), "join" (side stream, joined right after each launch)
+# "main" (the compute stream), "join" (side stream, joined right after each launch), "copy" (no exchange: the bucket
+# copied out and back in place on the side stream)
 _COMM_DIAG = os.environ.get("MIFX_DP_COMM", "side")
 
 
@@ -267,6 +268,17 @@ class DataParallel:
     def _launch(self, b: _Bucket) -> None:
         assert b is self.buckets[self._next], "buckets launch in order"
         self._next += 1
+        if self._comm_stream is not None and _COMM_DIAG == "copy":  # diagnostic: a plain in-place round trip
+            if getattr(self, "_diag_tmp", None) is None:
+                self._diag_tmp = torch.empty(max(bb.numel for bb in self.buckets), dtype=b.buf.dtype,
+                                             device=b.buf.device)
+            self._comm_stream.wait_stream(torch.cuda.current_stream(b.buf.device))
+            with torch.cuda.stream(self._comm_stream):
+                t = self._diag_tmp[:b.numel]
+                t.copy_(b.buf)
+                b.buf.copy_(t)
+            b.work = "ipc"
+            return
         if self._comm_stream is not None and self._ipc is not None and _COMM_DIAG == "main":
             self._ipc.all_reduce(b.buf, out=b.buf, scale=1.0 / self.world if self.average else 1.0)
             b.work = "ipc"
