@@ -125,6 +125,8 @@ class XgmiExchange:
         from ..ops import wide_deep as wdk
 
         xr = getattr(tr, "_xcd", None)
+        if xr is not None and getattr(xr, "xcd_of", None) is None:
+            xr = None  # (a reduction scratch without a placement record: the kernel's one-pass local sum)
         xa = (ptr(xr.xcd_of), ptr(xr.part), ptr(xr.ok), ptr(xr.xep)) if xr is not None else (None,) * 4
         rc = wdk._fns()["reduce_xgmi_opt"](ptr(tr.slab), int(tr.grid), self.stride, self.parts, self.sigs, self.world,
                                            self.rank, self.sig, ptr(self.err), ptr(self.xctr), None, ptr(tr.wsc),

@@ -166,7 +166,9 @@ class FusedWideDeepTrainer:
         # csrc/wide_deep.hip wd_reduce_res) -- 29.9 vs 32.4 us per headline step on MI355X
         # (profiles/wd_res_ab_r6.jsonl); MIFX_WD_RES=0: the placement-recorded XCD reduction
         use_xcd = os.environ.get("MIFX_WD_XCD", "1") != "0"
-        red_cls = wdk.ResReduce if os.environ.get("MIFX_WD_RES", "1") == "1" else wdk.XcdReduce
+        # (data parallelism keeps the XCD-recorded scratch: the xGMI exchange kernel sums the per-XCD partials itself,
+        # mifx.parallel.xgmi.XgmiExchange.reduce_apply)
+        red_cls = wdk.ResReduce if os.environ.get("MIFX_WD_RES", "1") == "1" and self.world == 1 else wdk.XcdReduce
         self._xcd = red_cls(self.stride, dev) if use_xcd and self._sc and 64 <= self.grid <= 256 else None
         # in_kernel_tail=True (or MIFX_WD_TAIL=1): the whole step in ONE launch -- slab reduction + optimizer inside
         # the fused kernel after two grid-wide barriers (csrc/wd_chain.hip TailArgs; needs every workgroup resident:
