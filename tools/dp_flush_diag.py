@@ -29,6 +29,19 @@ def main():
     tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=torch.distributed.group.WORLD, warmup_steps=10,
                        graph=a.graph, force_dp=True, seed=0)
     losses, grads = [], None
+    if a.graph and os.environ.get("DIAG_CAPTURE_CHECK") == "1":
+        for _ in range(tr.graph_warmup):
+            losses.append(float(tr.step()))
+        torch.cuda.synchronize()
+        before = {n: p.detach().float().cpu().clone() for n, p in tr.model.named_parameters()}
+        gb = {n: p.grad.detach().float().cpu().clone() for n, p in tr.model.named_parameters() if p.grad is not None}
+        tr._capture()  # capture only: nothing should execute
+        torch.cuda.synchronize()
+        moved = [n for n, p in tr.model.named_parameters() if not torch.equal(before[n], p.detach().float().cpu())]
+        gmoved = [n for n, p in tr.model.named_parameters()
+                  if p.grad is not None and n in gb and not torch.equal(gb[n], p.grad.detach().float().cpu())]
+        print("weights changed by the capture:", len(moved), moved[:8], "grads changed:", len(gmoved), gmoved[:8],
+              flush=True)
     for i in range(a.steps):
         losses.append(float(tr.step()))
         torch.cuda.synchronize()
