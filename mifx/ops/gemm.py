@@ -573,6 +573,11 @@ def nn_preferred(M: int, N: int, K: int) -> bool:
 # (profiles/gemm_dx_r4.jsonl): QKV 23.5 vs 30.3 (addmm 35.2) us, attention-out 10.4 vs 19.4, FFN-in 29.7 vs 39.2
 # (addmm 70.2). FFN-out (N = 3072) ties and stays on the library. (M, N, K) -> NT configuration.
 DX_NT_TUNED: dict[tuple[int, int, int], int] = {(4096, 768, 2304): 13, (4096, 768, 768): 12, (4096, 768, 3072): 13}
+# input-gradient products routed to the 8-wave kernel instead (A/B: MIFX_G8_DX="M:N:K=cfg+...", none by default)
+G8_DX: dict[tuple[int, int, int], int] = {}
+for _item in filter(None, os.environ.get("MIFX_G8_DX", "").split("+")):
+    _shape, _cfg = _item.split("=")
+    G8_DX[tuple(int(v) for v in _shape.split(":"))] = int(_cfg)
 
 
 def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tensor:
@@ -587,6 +592,10 @@ def _dx(dy2: torch.Tensor, w: torch.Tensor, slot: GradSlot | None) -> torch.Tens
     M, K = dy2.shape
     N = w.shape[1]
     ok = dy2.is_cuda and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+    if ok and (M, N, K) in G8_DX:
+        native_stats.count("gemm_dX", True)
+        y, _ = gemm8_nt(dy2, transposed(w), g, 3 if g is not None else 0, cfg=G8_DX[(M, N, K)])
+        return y
     if ok and (M, N, K) in DX_NT_TUNED and os.environ.get("MIFX_HIP_GEMM_DX", "1") != "0":
         native_stats.count("gemm_dX", True)
         y, _ = gemm_nt(dy2, transposed(w), g, 3 if g is not None else 0, cfg=DX_NT_TUNED[(M, N, K)])

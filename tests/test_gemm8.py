@@ -234,3 +234,25 @@ def test_forward_route_to_gemm8_matches_fp32(monkeypatch):
     of.backward(go)
     for a, r in ((w1.grad, w1f.grad), (b1.grad, b1f.grad), (w2.grad, w2f.grad)):
         assert (a.float() - r).norm() / r.norm() < 3e-2
+
+
+@pytest.mark.gpu
+def test_dx_route_to_gemm8_matches_fp32(monkeypatch):
+    """G8_DX (MIFX_G8_DX): the projections' input gradient dY W on the 8-wave kernel against the transposed weight,
+    with and without the residual gradient folded in as the C operand (GradSlot), vs fp32."""
+    dev = torch.device("cuda")
+    M, K, N = 512, 768, 256  # dX [M, N] = dY [M, K] . W [K, N]
+    monkeypatch.setattr(gemm, "G8_DX", {(M, N, K): 5})
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = (torch.randn(M, N, device=dev, generator=g) * 0.5).bfloat16().requires_grad_()
+    w = (torch.randn(K, N, device=dev, generator=g) * 0.05).bfloat16().requires_grad_()
+    dy = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    gemm.linear(x, w, force=True).backward(dy)  # (force: the _Linear node, whose backward is _dx)
+    ref = dy.float() @ w.detach().float()
+    assert (x.grad.float() - ref).norm() / ref.norm() < 1e-2
+    r = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    slot = gemm.GradSlot()
+    slot.g = r
+    out = gemm._dx(dy, w.detach(), slot)
+    ref2 = ref + r.float()
+    assert (out.float() - ref2).norm() / ref2.norm() < 1e-2

@@ -29,6 +29,28 @@ def main():
     tr = ResNetTrainer(a.batch, dev, imgs, labels, process_group=torch.distributed.group.WORLD, warmup_steps=10,
                        graph=a.graph, force_dp=True, seed=0)
     losses, grads = [], None
+    if os.environ.get("DIAG_STREAMS") == "1":  # which stream the bucket hooks run on, vs the capturing stream
+        from mifx.parallel import ddp as ddpm
+
+        orig = ddpm.DataParallel._complete_ready
+        seen = set()
+
+        def spy(self):
+            s = torch.cuda.current_stream()
+            key = (s.cuda_stream, torch.cuda.is_current_stream_capturing())
+            if key not in seen:
+                seen.add(key)
+                print(f"hook stream {s.cuda_stream:#x} capturing={key[1]}", flush=True)
+            return orig(self)
+
+        ddpm.DataParallel._complete_ready = spy
+        orig_fb = tr._fwd_bwd_captured
+
+        def fb():
+            print(f"capture stream {torch.cuda.current_stream().cuda_stream:#x}", flush=True)
+            return orig_fb()
+
+        tr._fwd_bwd_captured = fb
     if a.graph and os.environ.get("DIAG_CAPTURE_CHECK") == "1":
         for _ in range(tr.graph_warmup):
             losses.append(float(tr.step()))
