@@ -44,6 +44,10 @@ import torch.distributed as dist
 # "main" (the compute stream), "join" (side stream, joined right after each launch), "copy" (no exchange: the bucket
 # copied out and back in place on the side stream)
 _COMM_DIAG = os.environ.get("MIFX_DP_COMM", "side")
+# several buckets launched together fork the communication stream ONCE: one wait per bucket with no compute-stream
+# work in between lost the ordering of the consecutive exchanges in captured graphs (they overlapped on the shared
+# peer buffers; profiles/resnet_dp_flush_r6.md). MIFX_DP_FORK_ONCE=0 restores the old form (diagnostic).
+_FORK_ONCE = os.environ.get("MIFX_DP_FORK_ONCE", "1") != "0"
 
 
 @dataclass
@@ -108,9 +112,8 @@ class DataParallel:
         # exchanges. Measured on the ResNet-50 B=256 step forced onto one rank (profiles/resnet_dp_census_r6.md,
         # profiles/resnet_dp_flush_r6.md): one flush + exchanges after the backward 21.46 ms vs 23.10 ms for a flush
         # and an overlapped exchange per bucket (0), whose small grouped launches leave CUs idle (+0.9 ms of flush
-        # time). Thresholds in between (1024 / 2048: runs of buckets flushed together, their exchanges overlapping the
-        # rest of the backward) train correctly eagerly but diverge in captured replays -- unresolved, so not the
-        # default (tools/dp_flush_diag.py reproduces it).
+        # time), and 21.92 / 22.23 ms for thresholds 2048 / 1024 (runs of buckets flushed together, their exchanges
+        # overlapping the rest of the backward: on one rank the exchange is cheap, the extra launches are not).
         self.flush_min_wgs = int(os.environ.get("MIFX_DP_FLUSH_MIN_WG", str(1 << 40)))
         self._flush_last = os.environ.get("MIFX_DP_FLUSH_LAST", "0") == "1"  # (diagnostic switches, A/B)
         self._launch_late = os.environ.get("MIFX_DP_LAUNCH_LATE", "0") == "1"
@@ -258,14 +261,17 @@ class DataParallel:
                 p.grad = None
 
     def _launch_ready(self) -> None:
-        """Launch every complete bucket from the next one in bucket order on."""
+        """Launch every complete bucket from the next one in bucket order on (one fork of the communication stream
+        for all of them: the compute stream has not moved in between)."""
+        fork = True
         while self._next < len(self.buckets):
             b = self.buckets[self._next]
             if len(b.ready) != len(b.params):
                 return
-            self._launch(b)
+            self._launch(b, fork or not _FORK_ONCE)
+            fork = False
 
-    def _launch(self, b: _Bucket) -> None:
+    def _launch(self, b: _Bucket, fork: bool = True) -> None:
         assert b is self.buckets[self._next], "buckets launch in order"
         self._next += 1
         if self._comm_stream is not None and _COMM_DIAG == "copy":  # diagnostic: a plain in-place round trip
@@ -284,7 +290,8 @@ class DataParallel:
             b.work = "ipc"
         elif self._comm_stream is not None:
             cur = torch.cuda.current_stream(b.buf.device)
-            self._comm_stream.wait_stream(cur)
+            if fork:
+                self._comm_stream.wait_stream(cur)
             with torch.cuda.stream(self._comm_stream):
                 if self._ipc is not None:  # averaged in the kernel; stream-ordered, graph-capturable
                     self._ipc.all_reduce(b.buf, out=b.buf, scale=1.0 / self.world if self.average else 1.0)
@@ -330,8 +337,9 @@ class DataParallel:
                             b.buf[off:off + p.numel()].zero_()
                         else:
                             b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
-            # (views: unused params' bucket views are still zero)
-            self._launch(b)
+        # (views: unused params' bucket views are still zero)
+        for i, b in enumerate(self.buckets[self._next:]):  # one fork of the communication stream for all of them
+            self._launch(b, i == 0 or not _FORK_ONCE)
         self._next = 0
         cur = torch.cuda.current_stream(self.buckets[0].buf.device) if self._comm_stream is not None else None
         scale = 1.0 / self.world if self.average else 1.0

@@ -133,9 +133,9 @@ def _order_worker(rank, world, port, out_dir):
     launched = []
     orig = dp._launch
 
-    def rec(b):
+    def rec(b, *a):
         launched.append(dp.buckets.index(b))
-        orig(b)
+        orig(b, *a)
 
     dp._launch = rec
     params = [p for b in dp.buckets for p in b.params]
@@ -195,8 +195,8 @@ def test_ddp_coalesces_small_deferred_flushes(monkeypatch):
 
         monkeypatch.setattr(hg, "flush_weight_grads", fake_flush)
         launch = dp._launch
-        dp._launch = lambda b: (launches.append((any(any(p is w for w in ws) for p in b.params), len(calls))),
-                                launch(b))
+        dp._launch = lambda b, *a: (launches.append((any(any(p is w for w in ws) for p in b.params), len(calls))),
+                                    launch(b, *a))
         dp.flush_min_wgs = 1024  # 4 weights' worth (300 each)
         dp.release_grads_for_defer()
         net(torch.randn(2, 16)).sum().backward()
@@ -263,9 +263,9 @@ def test_ddp_deferred_flush_per_bucket_before_its_exchange(monkeypatch):
         monkeypatch.setattr(hg, "flush_weight_grads", fake_flush)
         launch = dp._launch
 
-        def spy(b):
+        def spy(b, *a):
             events.append(("launch", next(i for i, q in enumerate(dp.buckets) if q is b)))
-            launch(b)
+            launch(b, *a)
 
         dp._launch = spy
         dp.zero_grad()
