@@ -17,6 +17,8 @@ all-reduce, PyTorchJob DDP (`tf-job-simple-v1beta2.jsonnet:22-74`
 
 * buckets launch in bucket order on every rank (a bucket completing early waits for its predecessors), so the
   collective sequence is the same on all ranks whatever order autograd finished them in;
+* with deferred weight gradients (grouped flushes, mifx.ops.gemm.deferred_weight_grads) the flushes of runs of complete
+  buckets are coalesced (flush_min_wgs); by default ONE flush after the backward, then every bucket's exchange;
 * exchange="ipc" replaces the RCCL collective by the peer-memory two-shot all-reduce of csrc/tp_allreduce.hip in fp32
   (publish / reduce-scatter / all-gather kernels synchronised by device-side epoch flags, rank-order sum scaled by
   1 / world in the kernel: identical bits on every rank): no host collective, so the whole data-parallel step --
