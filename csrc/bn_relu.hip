@@ -250,10 +250,65 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& M2, 
   n = nn;
 }
 
+// per-channel merge of the G group records + the outputs of bn_finalize_fwd (shared by both finalize forms)
+__device__ __forceinline__ void tiles_final_channel(int c, const double* __restrict__ ws, int G, int C,
+                                                    const float* __restrict__ w, const float* __restrict__ b, float eps,
+                                                    float momentum, float* __restrict__ run_mean,
+                                                    float* __restrict__ run_var, float* __restrict__ mean_out,
+                                                    float* __restrict__ rstd_out, float* __restrict__ scale,
+                                                    float* __restrict__ shift) {
+  double n = 0.0, mean = 0.0, M2 = 0.0;
+  int g = 0;
+  for (; g + 4 <= G; g += 4) {  // four groups' records loaded before the (ordered) merges
+    double r[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double* o = ws + ((size_t)(g + u) * C + c) * 3;
+      r[u][0] = o[0];
+      r[u][1] = o[1];
+      r[u][2] = o[2];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) chan_merge(n, mean, M2, r[u][0], r[u][1], r[u][2]);
+  }
+  for (; g < G; ++g) {
+    const double* o = ws + ((size_t)g * C + c) * 3;
+    chan_merge(n, mean, M2, o[0], o[1], o[2]);
+  }
+  double var = M2 / n;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rstd;
+  const float sc = w[c] * rstd;
+  scale[c] = sc;
+  shift[c] = b[c] - (float)mean * sc;
+  if (run_mean != nullptr) {
+    const double unbiased = n > 1 ? M2 / (n - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+  }
+}
+
+struct TilesFinal {
+  const float* w;
+  const float* b;
+  float eps, momentum;
+  float* run_mean;
+  float* run_var;
+  float* stats;  // [mean, rstd, scale, shift][C]
+};
+
+// LAST = true: the group workgroup that arrives last for its 64-channel block (an agent-scope ticket per block,
+// reset by that workgroup for the next call) also merges the G records of its channels -- the second launch folded
+// into the first (same fixed merge order, same bits); the records are published with a device-scope fence first.
+template <bool LAST>
 __global__ __launch_bounds__(1024) void bn_tiles_partial(const float* __restrict__ pmean, const float* __restrict__ pm2,
-                                                        int T, int nt, int C, double* __restrict__ ws) {
+                                                        int T, int nt, int C, double* __restrict__ ws, TilesFinal fin,
+                                                        unsigned int* __restrict__ ticket) {
   __shared__ double sm[16][64], sq[16][64];
   __shared__ int sk[16];
+  __shared__ int s_last;
   const int G = gridDim.y, g = blockIdx.y;
   const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
   const int gb = (int)((long long)T * g / G), ge = (int)((long long)T * (g + 1) / G);
@@ -296,13 +351,30 @@ __global__ __launch_bounds__(1024) void bn_tiles_partial(const float* __restrict
   sq[sl][cl] = m2;
   if (cl == 0) sk[sl] = t1 - t0;
   __syncthreads();
-  if (sl != 0 || c >= C) return;
-  double n = 0.0, mean = 0.0, M2 = 0.0;
-  for (int k = 0; k < 16; ++k) chan_merge(n, mean, M2, (double)sk[k] * nt, sm[k][cl], sq[k][cl]);
-  double* o = ws + ((size_t)g * C + c) * 3;
-  o[0] = n;
-  o[1] = mean;
-  o[2] = M2;
+  if (sl == 0 && c < C) {
+    double n = 0.0, mean = 0.0, M2 = 0.0;
+    for (int k = 0; k < 16; ++k) chan_merge(n, mean, M2, (double)sk[k] * nt, sm[k][cl], sq[k][cl]);
+    double* o = ws + ((size_t)g * C + c) * 3;
+    o[0] = n;
+    o[1] = mean;
+    o[2] = M2;
+  }
+  if constexpr (LAST) {
+    __threadfence();  // this group's records visible to the workgroup of any XCD that merges them
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int old =
+          __hip_atomic_fetch_add(ticket + blockIdx.x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (unsigned int)G - 1;
+      if (s_last) __hip_atomic_store(ticket + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // the other groups' records, published before their tickets
+    if (sl == 0 && c < C)
+      tiles_final_channel(c, ws, G, C, fin.w, fin.b, fin.eps, fin.momentum, fin.run_mean, fin.run_var, fin.stats,
+                          fin.stats + C, fin.stats + 2 * C, fin.stats + 3 * C);
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_tiles_final(const double* __restrict__ ws, int G, int C,
@@ -313,38 +385,12 @@ __global__ __launch_bounds__(256) void bn_tiles_final(const double* __restrict__
                                                      float* __restrict__ shift) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  double n = 0.0, mean = 0.0, M2 = 0.0;
-  int g = 0;
-  for (; g + 4 <= G; g += 4) {  // four groups' records loaded before the (ordered) merges
-    double r[4][3];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const double* o = ws + ((size_t)(g + u) * C + c) * 3;
-      r[u][0] = o[0];
-      r[u][1] = o[1];
-      r[u][2] = o[2];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) chan_merge(n, mean, M2, r[u][0], r[u][1], r[u][2]);
-  }
-  for (; g < G; ++g) {
-    const double* o = ws + ((size_t)g * C + c) * 3;
-    chan_merge(n, mean, M2, o[0], o[1], o[2]);
-  }
-  double var = M2 / n;
-  var = var > 0.0 ? var : 0.0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  mean_out[c] = (float)mean;
-  rstd_out[c] = rstd;
-  const float sc = w[c] * rstd;
-  scale[c] = sc;
-  shift[c] = b[c] - (float)mean * sc;
-  if (run_mean != nullptr) {
-    const double unbiased = n > 1 ? M2 / (n - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
-  }
+  tiles_final_channel(c, ws, G, C, w, b, eps, momentum, run_mean, run_var, mean_out, rstd_out, scale, shift);
 }
+
+// per-64-channel-block arrival tickets of the one-launch finalize (zero at load; each call's last arriver resets its
+// block's ticket; calls on one stream are ordered, and a process issues them on one stream)
+__device__ unsigned int g_tiles_ticket[64];
 
 // groups of tiles of the first finalize launch: ~12 tiles per thread (16 slices per group)
 int tile_groups(int T) { return T / 192 < 1 ? 1 : (T / 192 > 32 ? 32 : T / 192); }
@@ -632,10 +678,19 @@ int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const f
                            int relu, float* stats, double* ws, void* y, hipStream_t st) {
   if (!shape_ok(M, C) || T <= 0 || nt <= 0 || (long long)T * nt != M || part == nullptr || ws == nullptr) return -1;
   const int G = tile_groups(T);
-  hipLaunchKernelGGL(bn_tiles_partial, dim3((C + 63) / 64, G), dim3(1024), 0, st, part, part + (size_t)T * C, T, nt, C,
-                     ws);
-  hipLaunchKernelGGL(bn_tiles_final, dim3((C + 255) / 256), dim3(256), 0, st, ws, G, C, w, b, eps, momentum, run_mean,
-                     run_var, stats, stats + C, stats + 2 * C, stats + 3 * C);
+  const TilesFinal fin{w, b, eps, momentum, run_mean, run_var, stats};
+  static const bool two = getenv("MIFX_BN_TILES_TWO_LAUNCH") != nullptr;  // (A/B: the two-launch form)
+  if (two || (C + 63) / 64 > 64) {
+    hipLaunchKernelGGL(bn_tiles_partial<false>, dim3((C + 63) / 64, G), dim3(1024), 0, st, part, part + (size_t)T * C,
+                       T, nt, C, ws, fin, (unsigned int*)nullptr);
+    hipLaunchKernelGGL(bn_tiles_final, dim3((C + 255) / 256), dim3(256), 0, st, ws, G, C, w, b, eps, momentum,
+                       run_mean, run_var, stats, stats + C, stats + 2 * C, stats + 3 * C);
+  } else {
+    static unsigned int* ticket = nullptr;
+    if (ticket == nullptr && hipGetSymbolAddress((void**)&ticket, HIP_SYMBOL(g_tiles_ticket)) != hipSuccess) return -1;
+    hipLaunchKernelGGL(bn_tiles_partial<true>, dim3((C + 63) / 64, G), dim3(1024), 0, st, part, part + (size_t)T * C,
+                       T, nt, C, ws, fin, ticket);
+  }
   if (y == nullptr) return (int)hipGetLastError();  // statistics only: the consumer GEMM applies (gemm8 AX operands)
   if (dtype)
     hipLaunchKernelGGL(bn_apply<__hip_bfloat16>, dim3(apply_blocks(M, C)), dim3(kThreads), 0, st,

@@ -257,7 +257,9 @@ def main(argv=None):
     elif not a.no_gemm_table and os.environ.get("MIFX_BERT_GEMM_TABLE", "1") != "0" and torch.cuda.is_available():
         load_gemm_table()
     env = mdist.init()
-    dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    # MIFX_SHARED_GPU=1 (with MIFX_DIST_BACKEND=gloo): the multi-rank flow rehearsed with every rank on cuda:0
+    local = 0 if os.environ.get("MIFX_SHARED_GPU") == "1" else env.local_rank
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     tp = TPGroup(torch.distributed.group.WORLD if env.world_size > 1 else None)

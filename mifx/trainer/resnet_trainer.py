@@ -398,7 +398,9 @@ def main(argv=None):
     if a.deterministic:
         torch.backends.cudnn.deterministic = True
     env = mdist.init()
-    dev = torch.device("cuda", env.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    # MIFX_SHARED_GPU=1 (with MIFX_DIST_BACKEND=gloo): the multi-rank flow rehearsed with every rank on cuda:0
+    local = 0 if os.environ.get("MIFX_SHARED_GPU") == "1" else env.local_rank
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     imgs, labels = synthetic_imagenet(a.images, seed=env.rank, device=dev)
     force = os.environ.get("MIFX_DP_FORCE") == "1" and env.world_size == 1
     if force:  # the data-parallel machinery on one rank (hooks, bucket exchange): its overhead, measured
