@@ -299,9 +299,10 @@ struct TilesFinal {
   float* stats;  // [mean, rstd, scale, shift][C]
 };
 
-// LAST = true: the group workgroup that arrives last for its 64-channel block (an agent-scope ticket per block,
-// reset by that workgroup for the next call) also merges the G records of its channels -- the second launch folded
-// into the first (same fixed merge order, same bits); the records are published with a device-scope fence first.
+// LAST = true (opt-in, measured slower: see mifx_bn_relu_fwd_tiles): the group workgroup that arrives last for its
+// 64-channel block (an agent-scope ticket per block, reset by that workgroup for the next call) also merges the G
+// records of its channels -- the second launch folded into the first (same fixed merge order, same bits); the records
+// are published with a device-scope fence first.
 template <bool LAST>
 __global__ __launch_bounds__(1024) void bn_tiles_partial(const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                         int T, int nt, int C, double* __restrict__ ws, TilesFinal fin,
@@ -679,8 +680,11 @@ int mifx_bn_relu_fwd_tiles(int dtype, const void* x, long long M, int C, const f
   if (!shape_ok(M, C) || T <= 0 || nt <= 0 || (long long)T * nt != M || part == nullptr || ws == nullptr) return -1;
   const int G = tile_groups(T);
   const TilesFinal fin{w, b, eps, momentum, run_mean, run_var, stats};
-  static const bool two = getenv("MIFX_BN_TILES_TWO_LAUNCH") != nullptr;  // (A/B: the two-launch form)
-  if (two || (C + 63) / 64 > 64) {
+  // MIFX_BN_TILES_ONE_LAUNCH=1: the finalize folded into the partial kernel (last-arriving group merges) -- measured
+  // SLOWER in the ResNet-50 step (20.97 vs 20.61 ms, profiles/resnet_bn_one_launch_ab_r6.jsonl): its device-scope
+  // fences write back and invalidate the XCD's L2, which the BatchNorm apply pass right after then re-reads from HBM
+  static const bool one = getenv("MIFX_BN_TILES_ONE_LAUNCH") != nullptr;
+  if (!one || (C + 63) / 64 > 64) {
     hipLaunchKernelGGL(bn_tiles_partial<false>, dim3((C + 63) / 64, G), dim3(1024), 0, st, part, part + (size_t)T * C,
                        T, nt, C, ws, fin, (unsigned int*)nullptr);
     hipLaunchKernelGGL(bn_tiles_final, dim3((C + 255) / 256), dim3(256), 0, st, ws, G, C, w, b, eps, momentum,

@@ -9,6 +9,7 @@ import torch.nn.functional as F
 
 import os
 
+from ..ops.stem import eligible as stem_eligible, stem_conv
 from ..ops import gconv
 from ..ops.bn_relu import BatchNormReLU2d
 from ..ops.pool import max_pool3s2
@@ -188,7 +189,9 @@ class ResNetV2(nn.Module):
         self.fc = nn.Linear(cin, num_classes)
 
     def forward(self, x):  # x: [B, 3, H, W] in [0, 1] (NHWC memory format preferred)
-        y = max_pool3s2(self.stem(x))  # HIP NHWC kernels (1-byte argmax) on the GPU, F.max_pool2d elsewhere
+        # the stem on the hand-written MFMA kernel where eligible (bf16 channels_last 3-channel input, csrc/stem_conv.hip);
+        # max-pool on the HIP NHWC kernels (1-byte argmax) on the GPU, F.max_pool2d elsewhere
+        y = max_pool3s2(stem_conv(x, self.stem.weight) if stem_eligible(x, self.stem.weight) else self.stem(x))
         out = self.blocks(y)
         y, _ = self.post_bn.forward_tiles(out.t, out.part) if isinstance(out, Fused) else self.post_bn.forward_add(*out)
         # global average pool whose backward keeps the channels_last layout (a plain mean's backward
