@@ -10,10 +10,10 @@
 // row and meet zero weights. 7 K-steps of v_mfma_f32_16x16x32_bf16 per 16 x 16 output tile, 34 % of them on padding --
 // cheap next to the memory traffic, and no im2col gather or masking in the inner loop.
 //
-//  * Workgroup: ROWS = 2 output rows of one image (2 x OW pixels) x all 64 output channels, 4 waves. The 9 input rows
+//  * Workgroup: ROWS = 4 output rows of one image (4 x OW pixels) x all 64 output channels, 4 waves. The 11 input rows
 //    it needs (zero rows / columns outside the image) and the bf16 weight image [64][7][32] (+8 pad per channel row:
-//    conflict-free 16-byte fragment reads) are staged in LDS once; then each wave owns every 4th 16-pixel tile and
-//    runs 7 x 4 MFMAs per tile with no further barrier.
+//    conflict-free 16-byte fragment reads) are staged in LDS once; then each wave loads its 28 weight fragments into registers once
+//    and, for every 4th 16-pixel tile, runs 7 x 4 MFMAs fed by 4-byte window reads, with no further barrier.
 //  * The weight is the MFMA A operand (16 output channels x 32 taps: one 16-byte LDS read per lane) and the input
 //    window the B operand (32 taps x 16 pixels: 4 aligned 4-byte LDS reads per lane), so a lane's accumulator holds
 //    four consecutive output channels of one pixel: 8-byte NHWC stores.
@@ -32,8 +32,11 @@ constexpr int KH = 7, KW = 7, CIN = 3, COUT = 64, STR = 2, PAD = 3;
 constexpr int Q = KW * CIN;                 // 21 taps per kernel row
 constexpr int QP = 32;                      // one MFMA K-step
 constexpr int WROW = KH * QP + 8;           // weight image row (one output channel) in LDS, bf16 elements
-constexpr int ROWS = 2;                     // output rows per workgroup
-constexpr int IR = STR * (ROWS - 1) + KH;   // input rows staged: 9
+#ifndef STEM_ROWS
+#define STEM_ROWS 4
+#endif
+constexpr int ROWS = STEM_ROWS;             // output rows per workgroup
+constexpr int IR = STR * (ROWS - 1) + KH;   // input rows staged
 constexpr int NT = 256;
 
 __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
@@ -72,22 +75,46 @@ __global__ __launch_bounds__(NT) void stem_fwd(const bf16* __restrict__ x, const
     const int o = i / (KH * QP / 8), j = i % (KH * QP / 8);
     *(v8bf*)(wl + o * WROW + 8 * j) = *(const v8bf*)(wimg + (size_t)o * KH * QP + 8 * j);
   }
-  // ---- stage the input rows 2 oh0 - 3 .. 2 oh0 + 5 (zeros outside the image; element (iw + 3) * 3 + c)
+  // ---- stage the input rows 2 oh0 - 3 .. (zeros outside the image; element (iw + 3) * 3 + c). Rows whose 3W
+  // elements are 16-byte aligned in global memory (W % 8 == 0) move as 16-byte loads and 2-byte LDS stores (the LDS
+  // image starts 9 elements into the row, which keeps the B reads 4-byte aligned); others element by element.
   const int row_elems = W * CIN;
-  for (int ir = 0; ir < IR; ++ir) {
-    const int ih = STR * oh0 - PAD + ir;
-    bf16* dst = xl + ir * LR;
-    const bool in = ih >= 0 && ih < H;
-    const bf16* src = x + ((size_t)n * H + (in ? ih : 0)) * row_elems;
-    for (int e = t; e < LR; e += NT) {
-      const int j = e - PAD * CIN;  // element of the image row
-      dst[e] = (in && j >= 0 && j < row_elems) ? src[j] : (bf16)0.f;
+  if (row_elems % 8 == 0 && (uintptr_t)x % 16 == 0) {
+    const int nv = row_elems / 8;
+    for (int i = t; i < IR * LR; i += NT) {  // zero the padding columns / out-of-image rows / slack
+      const int ir = i / LR, e = i % LR, j = e - PAD * CIN, ih = STR * oh0 - PAD + ir;
+      if (!(ih >= 0 && ih < H && j >= 0 && j < row_elems)) xl[i] = (bf16)0.f;
+    }
+    for (int i = t; i < IR * nv; i += NT) {
+      const int ir = i / nv, v = i % nv, ih = STR * oh0 - PAD + ir;
+      if (ih < 0 || ih >= H) continue;
+      const v8bf d = *(const v8bf*)(x + ((size_t)n * H + ih) * row_elems + 8 * v);
+      bf16* dst = xl + ir * LR + PAD * CIN + 8 * v;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dst[u] = d[u];
+    }
+  } else {
+    for (int ir = 0; ir < IR; ++ir) {
+      const int ih = STR * oh0 - PAD + ir;
+      bf16* dst = xl + ir * LR;
+      const bool in = ih >= 0 && ih < H;
+      const bf16* src = x + ((size_t)n * H + (in ? ih : 0)) * row_elems;
+      for (int e = t; e < LR; e += NT) {
+        const int j = e - PAD * CIN;  // element of the image row
+        dst[e] = (in && j >= 0 && j < row_elems) ? src[j] : (bf16)0.f;
+      }
     }
   }
   __syncthreads();
 
   const int npix = ROWS * OW, ntiles = (npix + 15) / 16;
   const int pl = lane & 15, kg = lane >> 4;
+  // the wave's A operands for every (kernel row, 16-channel tile): read once, kept in registers over its pixel tiles
+  v8bf wa[KH][4];
+#pragma unroll
+  for (int r = 0; r < KH; ++r)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) wa[r][nt] = *(const v8bf*)(wl + (nt * 16 + pl) * WROW + r * QP + 8 * kg);
   for (int pt = wv; pt < ntiles; pt += 4) {
     const int p = pt * 16 + pl;
     const int orl = p < npix ? p / OW : 0, ow = p < npix ? p % OW : 0;
@@ -102,10 +129,7 @@ __global__ __launch_bounds__(NT) void stem_fwd(const bf16* __restrict__ x, const
       const uint32_t bw[4] = {bp[0], bp[1], bp[2], bp[3]};
       const v8bf b = __builtin_bit_cast(v8bf, bw);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const v8bf a = *(const v8bf*)(wl + (nt * 16 + pl) * WROW + r * QP + 8 * kg);
-        acc[nt] = mfma(a, b, acc[nt]);
-      }
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma(wa[r][nt], b, acc[nt]);
     }
     if (!valid) continue;
     // acc[nt][i] = y[pixel pl][channel nt 16 + 4 kg + i]
