@@ -15,7 +15,8 @@ profiles/archive/resnet_steady_r5g.md) and BN2 / BN1 each needed a reduction pas
   kernel (mifx.ops.gconv.dgrad_strided) where it measured faster, else MIOpen;
 * weight gradient: dW[Cout][3][3][C] = sum over output pixels of dY^T . X_tap, deferred into the grouped split-K TN
   launch with the 1x1 weight gradients (inside mifx.ops.gemm.deferred_weight_grads(), C and Cout % 256: 2048-pixel
-  chunks of 256 x 256 tiles); MIOpen's otherwise (it beats the 128-wide tiles). Per-shape timings of every pass:
+  chunks of 256 x 256 tiles); the 64/128-channel ones on the nine-tap kernel of mifx.ops.conv3_wgrad (one staged input
+  patch serves all taps; MIOpen's igemm_wrw before). Per-shape timings of every pass:
   profiles/conv3x3_routes_r5.jsonl (tools/bench_conv3x3.py).
 
 Eligible: bf16 channels_last CUDA input, C a power of two >= 128 (>= 64: the narrow tiles; MIFX_CONV3X3_64=0 for >= 128),
@@ -27,7 +28,7 @@ import os
 import torch
 
 from . import gemm as hg
-from . import native_stats, weight_prep
+from . import conv3_wgrad, native_stats, weight_prep
 
 # MIFX_CONV3X3=0 keeps the 3x3 convolutions on the routed MIOpen / gconv path (A/B); MIFX_CONV3X3_64=0 leaves
 # the 64-channel ones (stage 1, on the narrow tiles: a tie with MIOpen in the step, profiles/resnet_narrow_ab_r5.txt)
@@ -101,6 +102,9 @@ class _Conv3x3(torch.autograd.Function):
         dw = dx = None
         if ctx.needs_input_grad[1]:
             dw = hg.defer_conv3x3_weight_grad_f32(dy2, _nhwc(x), w, stride, 1)
+            if dw is None and conv3_wgrad.eligible(x, dyc, w, stride):
+                native_stats.count("conv3x3_dW", True)
+                dw = conv3_wgrad.wgrad(x, dyc, w, stride)
             if dw is None:
                 wb = w9.view(cout, 3, 3, c).permute(0, 3, 1, 2)
                 native_stats.count("conv3x3_dW", False)
