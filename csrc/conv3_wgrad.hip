@@ -18,7 +18,8 @@
 //    reduction elements are 8 pixels). Element j of lane group g is pixel 4 g + j (j < 4) / 16 + 4 g + j - 4, the same
 //    permutation for both operands, so a 32-lane half reads 8 CONSECUTIVE pixel rows; rows are 128 B with the
 //    32-byte block index XORed with (row >> 1) & 3, which puts any 8 consecutive rows on 8 distinct bank octets
-//    (conflict-free for dY and for stride-1 input reads; stride 2 reads every other row: 2-way).
+//    (conflict-free for dY and the input reads). Stride 2 stages each input row as its even columns then its odd
+//    ones, so consecutive output pixels read consecutive staged pixels for every tap there too.
 //  * A tap's B fragment is the table entry + the tap's staged-pixel offset: no im2col, no per-tap reload.
 //  * Each workgroup writes its fp32 partial [Cout][3][3][C] slice into part[split]; conv3_wgrad_sum adds the splits
 //    in split order (deterministic) into the parameter's layout (channels_last or contiguous).
@@ -55,7 +56,8 @@ __device__ __forceinline__ v8bf cat8(v4s a, v4s b) {
 __device__ __forceinline__ int sw(int row, int cb, int e) { return row * CS + 16 * (cb ^ ((row >> 1) & 3)) + e; }
 
 struct Geo {
-  int N, H, W, C, Cout, OH, OW, S, CR, XW, NPS;  // NPS: pixel slots per chunk (multiple of 32)
+  int N, H, W, C, Cout, OH, OW, S, CR, NPS;  // NPS: pixel slots per chunk (multiple of 32)
+  int XW, HW, c1, c2;  // staged row width; stride 2: phase width; staged column of taps s = 1, 2
   int splits, ncs, nslices;
 };
 
@@ -115,7 +117,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
       for (int k = 0; k < STAGE_BATCH; ++k) {
         const int i = i0 + k * NT, sp = i >> 3, ch = i & 7;
-        const int ir = sp / g.XW, ic = sp - ir * g.XW;
+        const int ir = sp / g.XW, sc = sp - ir * g.XW;
+        const int ic = g.S == 1 ? sc : (sc < g.HW ? 2 * sc : 2 * (sc - g.HW) + 1);  // stride 2: even | odd columns
         const int ih = ih0 + ir, iw = ic - 1;
         v[k] = (u4){0u, 0u, 0u, 0u};
         if (i < nx && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     for (int i = t; i < np32; i += NT) {
       const int pc = min(i, npix - 1), orl = pc / g.OW;
-      poff[i] = orl * g.S * g.XW + (pc - orl * g.OW) * g.S;  // slots past npix: any in-range pixel (dY is 0 there)
+      poff[i] = orl * g.S * g.XW + (pc - orl * g.OW);  // (slots past npix: any in-range pixel, dY is 0 there)
     }
     __syncthreads();
 
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
         const int J = 9 * wv + j, tap = J >> 2, cb = J & 3;
-        const int to = (tap / 3) * g.XW + tap % 3;
+        const int ts = tap % 3, to = (tap / 3) * g.XW + (ts == 0 ? 0 : ts == 1 ? g.c1 : g.c2);
         const v8bf bfr = cat8(tr_read(xs + sw(xa + to, cb, 4 * p)), tr_read(xs + sw(xb + to, cb, 4 * p)));
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt][j] = mfma(af[mt], bfr, acc[mt][j]);
@@ -217,8 +220,10 @@ __global__ __launch_bounds__(256) void conv3_wgrad_sum(const float4* __restrict_
 }
 
 // chunk rows and LDS bytes for a shape: the most output rows (<= 256 pixel slots) that keep two workgroups per CU
+int staged_width(int W, int S) { return S == 1 ? W + 2 : 2 * ((W + 3) / 2); }
+
 void plan(int W, int OW, int S, int OH, int* cr_out, int* nps_out, int* lds_out) {
-  const int XW = W + 2;
+  const int XW = staged_width(W, S);
   int cr = 256 / OW;
   cr = cr < 1 ? 1 : (cr > OH ? OH : cr);
   for (;; --cr) {
@@ -265,7 +270,8 @@ int mifx_conv3_wgrad(const void* x, const void* dy, float* part, float* dw, int 
   if ((long long)N * H * W * C >= (1ll << 31) || (long long)N * OH * OW * Cout >= (1ll << 31)) return -1;
   if (splits < 1 || splits > N * OH) return -1;
   Geo g;
-  g.N = N; g.H = H; g.W = W; g.C = C; g.Cout = Cout; g.OH = OH; g.OW = OW; g.S = S; g.XW = W + 2;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.Cout = Cout; g.OH = OH; g.OW = OW; g.S = S;
+  g.XW = staged_width(W, S); g.HW = (W + 3) / 2; g.c1 = S == 1 ? 1 : g.HW; g.c2 = S == 1 ? 2 : 1;
   int lds;
   plan(W, OW, S, OH, &g.CR, &g.NPS, &lds);
   if (lds > 160 * 1024) return -1;

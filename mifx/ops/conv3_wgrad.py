@@ -16,8 +16,8 @@ from . import _lib
 from ._lib import I32, VP, check, ptr, sig, stream_handle
 
 ENABLED = os.environ.get("MIFX_CONV3_WGRAD", "1") != "0"
-# stride 2 reads every other staged row (2-way bank conflicts) and measured slower than MIOpen (192 vs 147 us,
-# profiles/conv3_wgrad_shapes_r6.jsonl): opt-in
+# stride 2 measured slower than MIOpen (195-207 vs 147 us, profiles/conv3_wgrad_shapes_r6.jsonl: the 56-wide input
+# rows leave room for 3 output rows per chunk, 7 staged input rows for 84 pixels) and a tie in the step: opt-in
 _S2 = os.environ.get("MIFX_CONV3_WGRAD_S2", "0") == "1"
 
 
