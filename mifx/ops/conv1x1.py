@@ -73,6 +73,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.bn = bn
         if part is None:
             part = torch.empty(0, device=x.device)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.mark_non_differentiable(part)
         return out, part
 
@@ -176,6 +177,7 @@ class _ProjPair(torch.autograd.Function):
         _, part = hg.gemm8_nt(x2, wb1, None, 5, cfg=hg.gemm8_pick(x2.shape[0], c1, cin), out=_rows(y1))
         ctx.save_for_backward(x, wsb, wb1)
         ctx.w_sc, ctx.w1, ctx.stride, ctx.bn = w_sc, w1, stride, bn
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.mark_non_differentiable(part)
         return sc, y1, part
 

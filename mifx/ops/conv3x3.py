@@ -86,6 +86,7 @@ class _Conv3x3(torch.autograd.Function):
         ctx.w, ctx.stride, ctx.bn = w, stride, bn
         if part is None:
             part = torch.empty(0, device=x.device)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.mark_non_differentiable(part)
         return out, part
 
