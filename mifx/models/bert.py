@@ -156,9 +156,12 @@ class BertLayer(nn.Module):
         if hip:
             # the projection computes in the weight dtype anyway (autocast's cast of x); casting before the TP copy
             # makes its backward all-reduce a bf16 one (the peer-memory kernels: no host collective in the captured
-            # step) -- the first layer's input is the fp32 embedding LayerNorm output
+            # step) -- the first layer's input is the fp32 embedding LayerNorm output. Cast at TP = 1 too: an fp32
+            # input would send the first layer's QKV projection to the library (F.linear under autocast: weight
+            # gradient, bias sum and input gradient as three aten kernels, ~100 us) instead of the hand-written
+            # backward with its weight gradient in the grouped launch
             cdt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else self.qkv.weight.dtype
-            xin = x if x.dtype == cdt or self.tp.size == 1 else x.to(cdt)
+            xin = x if x.dtype == cdt else x.to(cdt)
             # (copy_to_tp folded into the projection: its input gradient is all-reduced, overlapped with its GEMM)
             qkv = hg.linear(xin, self.qkv.weight, self.qkv.bias, slot=slot_a, tp_in=self.tp).view(B, S, 3, h, d)
         else:
