@@ -1018,6 +1018,86 @@ __global__ __launch_bounds__(256) void wd_res_opt_sc(const float* __restrict__ p
   }
 }
 
+// Both levels in ONE launch (opt-in, MIFX_WD_RES_FUSED=1): level 1 exactly as wd_reduce_res; the LAST of a
+// chunk's 8 residue workgroups to finish (a per-chunk ticket) then adds the chunk's 8 partials in residue order and
+// applies the optimizer to its 256 columns -- wd_res_opt_sc<1>'s sums and state updates, bit for bit, without the
+// second launch. The partials are stored and loaded at agent scope (coherent across the XCDs' L2s) and completed
+// before the ticket increment; the last arriver resets the ticket. No workgroup ever waits for another.
+__global__ __launch_bounds__(256) void wd_reduce_res_fused(const float4* __restrict__ slab, int G, int stride,
+                                                           float* __restrict__ part, int* __restrict__ ticket,
+                                                           const int* __restrict__ wsc, float* __restrict__ param,
+                                                           float* __restrict__ s0, float* __restrict__ s1,
+                                                           uint16_t* __restrict__ wt_out,
+                                                           long long* __restrict__ step_ctr, OptHyper hd, OptHyper hw) {
+  __shared__ float4 red[4][X1C];
+  __shared__ int last;
+  const int S4 = stride / 4, nc1 = (S4 + X1C - 1) / X1C;
+  const int k = blockIdx.x & 7, c = blockIdx.x >> 3;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int q = c * X1C + lane;
+  float4 a = make_float4(0, 0, 0, 0);
+  if (q < S4) {
+    constexpr int U = 8;
+    for (int i0 = k + 8 * w; i0 < G; i0 += 32 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = i0 + 32 * u;
+        v[u] = r < G ? slab[(size_t)r * S4 + q] : make_float4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+  }
+  red[w][lane] = a;
+  __syncthreads();
+  if (w == 0 && q < S4) {
+    float4 sm = red[0][lane];
+#pragma unroll
+    for (int k2 = 1; k2 < 4; ++k2) {
+      sm.x += red[k2][lane].x; sm.y += red[k2][lane].y; sm.z += red[k2][lane].z; sm.w += red[k2][lane].w;
+    }
+    float* dst = part + (size_t)k * stride + 4 * q;
+    __hip_atomic_store(dst + 0, sm.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 1, sm.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 2, sm.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 3, sm.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (t == 0) {
+    // wave 0 made the partial stores; they are agent-scope (coherent across the XCDs' L2s), so completing them
+    // (vmcnt 0) before the increment orders them -- a release fence here (an L2 writeback) measured ~5 us slower
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const int old = __hip_atomic_fetch_add(ticket + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == 7;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int gi = c * 256 + t;
+  const long long step = step_ctr[c] + 1;
+  float pv[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+    pv[x] = gi < stride ? __hip_atomic_load(part + (size_t)x * stride + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.f;
+  ScState st = sc_load(gi, stride, wsc, param, s0, s1);
+  if (gi < stride) {
+    float g = pv[0];
+#pragma unroll
+    for (int x = 1; x < 8; ++x) g += pv[x];
+    sc_update(gi, st, g, hd, hw, step, param, s0, s1, wt_out);
+  }
+  if (t == 0) {
+    step_ctr[c] = step;
+    __hip_atomic_store(ticket + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (c == 0)
+    for (int i = nc1 + t; i < STEP_SLOTS; i += 256) step_ctr[i] = step;
+}
+
 // level 2: one thread per slab column. MODE 0: plain sum into out; 1: optimizer on slab-order state; 2: xGMI data
 // parallelism, publish half -- store the local sum into half (epoch & 1) of this rank's IPC buffer and stamp the 4
 // RQ-float4 chunks' flags in every peer, no wait (wd_xgmi_gather_opt waits, gathers and applies the optimizer in
@@ -1523,6 +1603,26 @@ int mifx_wd_reduce_res_opt(const float* slab, int G, int stride, float* part, fl
     hipLaunchKernelGGL(wd_res_opt_sc<1>, g2, dim3(256), 0, stream, part, stride, nullptr, wsc, param, s0, s1,
                        (uint16_t*)wt_out, step_ctr, hd, hw);
   }
+  return (int)hipGetLastError();
+}
+
+// The same with both levels in one launch (wd_reduce_res_fused; optimizer only). ticket: nchunks int32, all zero
+// before the first call (each call leaves them zero again).
+int mifx_wd_reduce_res_opt_fused(const float* slab, int G, int stride, float* part, int* ticket, const int* wsc,
+                                 float* param, float* s0, float* s1, void* wt_out, long long* step_ctr,
+                                 const float* hyper_dnn, const float* hyper_wide, hipStream_t stream) {
+  if (G <= 0 || stride <= 0 || stride > STRIDE || stride % 4 != 0 || part == nullptr || ticket == nullptr) return -1;
+  if (wsc == nullptr || param == nullptr || s0 == nullptr || s1 == nullptr || wt_out == nullptr ||
+      step_ctr == nullptr || hyper_dnn == nullptr || hyper_wide == nullptr)
+    return -1;
+  const int nc1 = mifx_wd_xcd_chunks(stride);
+  if (nc1 > STEP_SLOTS || nc1 != (stride + 255) / 256) return -1;
+  const OptHyper hd{(int)hyper_dnn[0], hyper_dnn[1], hyper_dnn[2], hyper_dnn[3], hyper_dnn[4], hyper_dnn[5],
+                    hyper_dnn[6], hyper_dnn[7]};
+  const OptHyper hw{(int)hyper_wide[0], hyper_wide[1], hyper_wide[2], hyper_wide[3], hyper_wide[4], hyper_wide[5],
+                    hyper_wide[6], hyper_wide[7]};
+  hipLaunchKernelGGL(wd_reduce_res_fused, dim3(8 * nc1), dim3(256), 0, stream, (const float4*)slab, G, stride, part,
+                     ticket, wsc, param, s0, s1, (uint16_t*)wt_out, step_ctr, hd, hw);
   return (int)hipGetLastError();
 }
 

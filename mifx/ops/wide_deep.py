@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import ctypes
 import functools
+import os
 
 import torch
 
@@ -26,6 +27,8 @@ def _fns():
                                                               VP, VP, VP, VP]),
         "reduce_res_opt": sig(lib, "mifx_wd_reduce_res_opt", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP,
                                                               VP]),
+        "reduce_res_opt_fused": sig(lib, "mifx_wd_reduce_res_opt_fused", [VP, I32, I32, VP, VP, VP, VP, VP, VP, VP,
+                                                                          VP, VP, VP, VP]),
         "xgmi_chunks": sig(lib, "mifx_wd_xgmi_chunks", [I32]),
         "reduce_xgmi_opt": sig(lib, "mifx_wd_reduce_xgmi_opt", [VP, I32, I32, VP, VP, I32, I32, VP, VP, VP, VP, VP,
                                                                 VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
@@ -153,6 +156,15 @@ class XcdReduce:
     def apply_sc(self, slab: torch.Tensor, groups: int, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn,
                  hyper_wide) -> None:
         _check_step_ctr(step_ctr)
+        if self.fused:
+            if slab.shape[-1] != self.stride or slab.numel() < groups * self.stride or not slab.is_contiguous():
+                raise ValueError("slab must be contiguous [>= groups, stride]")
+            rc = _fns()["reduce_res_opt_fused"](ptr(slab), int(groups), self.stride, ptr(self.part), ptr(self.ticket),
+                                                ptr(wsc), ptr(param_sc), ptr(s0_sc), ptr(s1_sc), ptr(wt_out),
+                                                ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
+                                                stream_handle(slab.device))
+            check(rc, "mifx_wd_reduce_res_opt_fused")
+            return
         self._call(slab, groups, None, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide)
 
     def sum_into(self, slab: torch.Tensor, groups: int, out: torch.Tensor) -> None:
@@ -163,10 +175,16 @@ class ResReduce:
     """Scratch of the residue-class two-level slab reduction + optimizer (csrc/wide_deep.hip wd_reduce_res /
     wd_res_opt_sc): per-residue partials [8, stride]. Same interface as XcdReduce."""
 
-    def __init__(self, stride: int, device):
+    def __init__(self, stride: int, device, fused: bool | None = None):
         self.stride = int(stride)
         self.part = torch.zeros(8 * stride, device=device)
         self.xcd_of = None  # (no placement record needed)
+        # fused (MIFX_WD_RES_FUSED=1): both levels in one launch, the optimizer run by the last of a chunk's residue
+        # workgroups (csrc/wide_deep.hip wd_reduce_res_fused); per-chunk tickets, zero between calls. Bit-identical
+        # to the two launches but measured slower on the headline step: 29.7-29.9 vs 28.3-28.5 us (release-fenced
+        # ticket: 33.4-33.6), profiles/wd_res_fused_ab_r6.jsonl -- opt-in
+        self.fused = os.environ.get("MIFX_WD_RES_FUSED", "0") == "1" if fused is None else bool(fused)
+        self.ticket = torch.zeros((self.stride + 255) // 256, dtype=torch.int32, device=device)
 
     def _call(self, slab, groups, out, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide):
         if slab.shape[-1] != self.stride or slab.numel() < groups * self.stride or not slab.is_contiguous():
@@ -179,6 +197,15 @@ class ResReduce:
     def apply_sc(self, slab: torch.Tensor, groups: int, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn,
                  hyper_wide) -> None:
         _check_step_ctr(step_ctr)
+        if self.fused:
+            if slab.shape[-1] != self.stride or slab.numel() < groups * self.stride or not slab.is_contiguous():
+                raise ValueError("slab must be contiguous [>= groups, stride]")
+            rc = _fns()["reduce_res_opt_fused"](ptr(slab), int(groups), self.stride, ptr(self.part), ptr(self.ticket),
+                                                ptr(wsc), ptr(param_sc), ptr(s0_sc), ptr(s1_sc), ptr(wt_out),
+                                                ptr(step_ctr), ptr(hyper_dnn), ptr(hyper_wide),
+                                                stream_handle(slab.device))
+            check(rc, "mifx_wd_reduce_res_opt_fused")
+            return
         self._call(slab, groups, None, wsc, param_sc, s0_sc, s1_sc, wt_out, step_ctr, hyper_dnn, hyper_wide)
 
     def sum_into(self, slab: torch.Tensor, groups: int, out: torch.Tensor) -> None:

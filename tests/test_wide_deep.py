@@ -649,3 +649,30 @@ def test_one_launch_step_bit_identical(batch):
         out[one] = (tr.param.clone(), tr.s0.clone(), tr.steps_done, tr.last_loss())
     assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
     assert out[True][2] == out[False][2] and out[True][3] == out[False][3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [16384, 65536])
+def test_res_reduce_fused_matches_two_launch(batch):
+    """The one-launch residue-class tail (last-arriving residue workgroup applies the optimizer) against the
+    two-launch default: bit-identical parameters, optimizer state and weight image after several steps, the graph
+    replays included, and the per-chunk tickets back at zero."""
+    from mifx.ops import wide_deep as wdk
+    from mifx.trainer.fused_wide_deep import FusedWideDeepTrainer
+
+    recs = synthetic_records(1 << 17, device="cuda", seed=21)
+    out = []
+    for fused in (False, True):
+        tr = FusedWideDeepTrainer(wdm.WideDeepModel(seed=5), batch=batch, device="cuda")
+        assert isinstance(tr._xcd, wdk.ResReduce)
+        tr._xcd.fused = fused
+        tr.set_data(recs)
+        for _ in range(3):
+            tr.step()
+        tr.run(12)
+        torch.cuda.synchronize()
+        out.append((tr.param_sc.clone(), tr.s0_sc.clone(), tr.s1_sc.clone(), tr.wt.clone()))
+        if fused:
+            assert int(tr._xcd.ticket.abs().sum()) == 0
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
