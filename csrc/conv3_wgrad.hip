@@ -43,6 +43,9 @@ constexpr int CS = 64;  // channels per slice (both operands): one 128-byte LDS 
 #ifndef STAGE_BATCH
 #define STAGE_BATCH 4
 #endif
+#ifndef C3_WS
+#define C3_WS 0  // the wave-specialised build (below): measured no faster, profiles/conv3_wgrad_shapes_r6.jsonl
+#endif
 
 __device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -61,12 +64,116 @@ struct Geo {
   int splits, ncs, nslices;
 };
 
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3_wgrad(
+// one staged chunk: dY rows [NPS][64], the pixel table [NPS], the input rows [XR][XW][64]
+struct Bufs {
+  bf16* ys;
+  int* poff;
+  bf16* xs;
+};
+__device__ __forceinline__ Bufs bufs_at(bf16* base, const Geo& g) {
+  Bufs r;
+  r.ys = base;
+  r.poff = (int*)(base + g.NPS * CS);
+  r.xs = (bf16*)(r.poff + g.NPS);
+  return r;
+}
+__host__ __device__ inline int buf_elems(int nps, int xr, int xw) { return nps * CS + nps * 2 + xr * xw * CS; }
+
+struct Chunk {
+  int n, oh0, cr;
+};
+__device__ __forceinline__ Chunk chunk_at(int gr, int r_end, const Geo& g) {
+  Chunk c;
+  c.n = gr / g.OH;
+  c.oh0 = gr - c.n * g.OH;
+  c.cr = min(min(g.CR, g.OH - c.oh0), r_end - gr);
+  return c;
+}
+
+// stage chunk ch into B: threads tl = 0 .. LT - 1 (STAGE_BATCH 16-byte loads in flight per thread before their
+// LDS stores)
+template <int LT>
+__device__ __forceinline__ void stage(const bf16* __restrict__ x, const bf16* __restrict__ dy, const Geo& g, int os,
+                                      int cs, Chunk ch, Bufs B, int tl) {
+  const int npix = ch.cr * g.OW, np32 = (npix + 31) & ~31;
+  const int xr = (ch.cr - 1) * g.S + 3;
+  // dY rows oh0 .. oh0 + cr - 1 of this output-channel slice; zero slots up to the K-step multiple
+  const bf16* dsrc = dy + ((size_t)ch.n * g.OH + ch.oh0) * g.OW * g.Cout + CS * os;
+  for (int i0 = tl; i0 < np32 * 8; i0 += STAGE_BATCH * LT) {
+    u4 v[STAGE_BATCH];
+#pragma unroll
+    for (int k = 0; k < STAGE_BATCH; ++k) {
+      const int i = i0 + k * LT, px = i >> 3, c8 = i & 7;
+      v[k] = (u4){0u, 0u, 0u, 0u};
+      if (px < npix) v[k] = *(const u4*)(dsrc + (size_t)px * g.Cout + 8 * c8);
+    }
+#pragma unroll
+    for (int k = 0; k < STAGE_BATCH; ++k) {
+      const int i = i0 + k * LT, px = i >> 3, c8 = i & 7;
+      if (px < np32) *(u4*)(B.ys + sw(px, c8 >> 1, 8 * (c8 & 1))) = v[k];
+    }
+  }
+  // input rows S oh0 - 1 .. of this input-channel slice, columns -1 .. W (zeros outside the image)
+  const int ih0 = g.S * ch.oh0 - 1;
+  const int nx = xr * g.XW * 8;
+  for (int i0 = tl; i0 < nx; i0 += STAGE_BATCH * LT) {
+    u4 v[STAGE_BATCH];
+#pragma unroll
+    for (int k = 0; k < STAGE_BATCH; ++k) {
+      const int i = i0 + k * LT, sp = i >> 3, c8 = i & 7;
+      const int ir = sp / g.XW, sc = sp - ir * g.XW;
+      const int ic = g.S == 1 ? sc : (sc < g.HW ? 2 * sc : 2 * (sc - g.HW) + 1);  // stride 2: even | odd columns
+      const int ih = ih0 + ir, iw = ic - 1;
+      v[k] = (u4){0u, 0u, 0u, 0u};
+      if (i < nx && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
+        v[k] = *(const u4*)(x + (((size_t)ch.n * g.H + ih) * g.W + iw) * g.C + CS * cs + 8 * c8);
+    }
+#pragma unroll
+    for (int k = 0; k < STAGE_BATCH; ++k) {
+      const int i = i0 + k * LT, sp = i >> 3, c8 = i & 7;
+      if (i < nx) *(u4*)(B.xs + sw(sp, c8 >> 1, 8 * (c8 & 1))) = v[k];
+    }
+  }
+  for (int i = tl; i < np32; i += LT) {
+    const int pc = min(i, npix - 1), orl = pc / g.OW;
+    B.poff[i] = orl * g.S * g.XW + (pc - orl * g.OW);  // (slots past npix: any in-range pixel, dY is 0 there)
+  }
+}
+
+// the compute wave wv (0..3) of one staged chunk: nine 16-column tiles x all four 16-row tiles
+__device__ __forceinline__ void compute(const Geo& g, Bufs B, int npix, int wv, int lane, v4f (&acc)[4][9]) {
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int np32 = (npix + 31) & ~31;
+  for (int p0 = 0; p0 < np32; p0 += 32) {
+    const int ra = p0 + 4 * grp + q, rb = ra + 16;  // this lane's transposed-read rows (pixel slots)
+    v8bf af[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = cat8(tr_read(B.ys + sw(ra, mt, 4 * p)), tr_read(B.ys + sw(rb, mt, 4 * p)));
+    const int xa = B.poff[ra], xb = B.poff[rb];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int J = 9 * wv + j, tap = J >> 2, cb = J & 3;
+      const int ts = tap % 3, to = (tap / 3) * g.XW + (ts == 0 ? 0 : ts == 1 ? g.c1 : g.c2);
+      const v8bf bfr = cat8(tr_read(B.xs + sw(xa + to, cb, 4 * p)), tr_read(B.xs + sw(xb + to, cb, 4 * p)));
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][j] = mfma(af[mt], bfr, acc[mt][j]);
+    }
+  }
+}
+
+#if C3_WS
+// Wave-specialised build (-DC3_WS=1): 8 waves, one workgroup per CU. Waves 0-3 multiply the staged chunk c while
+// waves 4-7 stage chunk c + 1 into the other LDS buffer; one barrier per chunk. Aimed at the staging latency of the
+// default 4-wave build (two workgroups per CU, 19 % MFMA busy: profiles/conv3_wgrad_pmc_r6.md), it measured no
+// faster (131 / 140 vs 137 / 123 us): one multiplying wave per SIMD exposes the transposed-read latency instead.
+constexpr int NTK = 512;
+#else
+constexpr int NTK = NT;
+#endif
+
+__global__ __launch_bounds__(NTK) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv3_wgrad(
     const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ part, Geo g) {
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
-  bf16* ys = lds;                                  // [NPS][64] dY
-  int* poff = (int*)(lds + g.NPS * CS);            // [NPS] staged input pixel of tap (0, 0)
-  bf16* xs = (bf16*)(poff + g.NPS);                // [XR][XW][64] input
   const int t = threadIdx.x, lane = t & 63;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   // XCD-aware work index: consecutive u share an XCD when the grid divides by 8
@@ -78,81 +185,62 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int r_begin = (int)((long long)rows_total * split / g.splits);
   const int r_end = (int)((long long)rows_total * (split + 1) / g.splits);
 
-  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#if C3_WS
+  // the two roles run separate loops with the same number of barriers (one per chunk, after the prologue), so the
+  // loaders carry no accumulators and the multipliers no staging registers
+  const int bel = buf_elems(g.NPS, (g.CR - 1) * g.S + 3, g.XW);
+  const Bufs B0 = bufs_at(lds, g), B1 = bufs_at(lds + bel, g);
+  if (wv >= 4) {
+    int gr = r_begin;
+    Chunk cur = chunk_at(gr, r_end, g);
+    if (gr < r_end) stage<256>(x, dy, g, os, cs, cur, B0, t - 256);
+    __syncthreads();
+    int bsel = 0;
+    while (gr < r_end) {
+      const int gn = gr + cur.cr;
+      const Chunk nxt = chunk_at(gn, r_end, g);
+      if (gn < r_end) stage<256>(x, dy, g, os, cs, nxt, bsel ? B0 : B1, t - 256);
+      __syncthreads();  // chunk c consumed, chunk c + 1 staged
+      gr = gn;
+      cur = nxt;
+      bsel ^= 1;
+    }
+    return;
+  }
   v4f acc[4][9];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-
-  for (int gr = r_begin; gr < r_end;) {
-    const int n = gr / g.OH, oh0 = gr - n * g.OH;
-    const int cr = min(min(g.CR, g.OH - oh0), r_end - gr);
-    gr += cr;
-    const int npix = cr * g.OW, np32 = (npix + 31) & ~31;
-    const int xr = (cr - 1) * g.S + 3;
-    __syncthreads();  // the previous chunk's reads are done
-    // dY rows oh0 .. oh0 + cr - 1 of this output-channel slice; zero slots up to the K-step multiple
-    const bf16* dsrc = dy + ((size_t)n * g.OH + oh0) * g.OW * g.Cout + CS * os;
-    // (STAGE_BATCH 16-byte loads in flight per thread before their LDS stores)
-    for (int i0 = t; i0 < np32 * 8; i0 += STAGE_BATCH * NT) {
-      u4 v[STAGE_BATCH];
-#pragma unroll
-      for (int k = 0; k < STAGE_BATCH; ++k) {
-        const int i = i0 + k * NT, px = i >> 3, ch = i & 7;
-        v[k] = (u4){0u, 0u, 0u, 0u};
-        if (px < npix) v[k] = *(const u4*)(dsrc + (size_t)px * g.Cout + 8 * ch);
-      }
-#pragma unroll
-      for (int k = 0; k < STAGE_BATCH; ++k) {
-        const int i = i0 + k * NT, px = i >> 3, ch = i & 7;
-        if (px < np32) *(u4*)(ys + sw(px, ch >> 1, 8 * (ch & 1))) = v[k];
-      }
-    }
-    // input rows S oh0 - 1 .. of this input-channel slice, columns -1 .. W (zeros outside the image)
-    const int ih0 = g.S * oh0 - 1;
-    const int nx = xr * g.XW * 8;
-    for (int i0 = t; i0 < nx; i0 += STAGE_BATCH * NT) {
-      u4 v[STAGE_BATCH];
-#pragma unroll
-      for (int k = 0; k < STAGE_BATCH; ++k) {
-        const int i = i0 + k * NT, sp = i >> 3, ch = i & 7;
-        const int ir = sp / g.XW, sc = sp - ir * g.XW;
-        const int ic = g.S == 1 ? sc : (sc < g.HW ? 2 * sc : 2 * (sc - g.HW) + 1);  // stride 2: even | odd columns
-        const int ih = ih0 + ir, iw = ic - 1;
-        v[k] = (u4){0u, 0u, 0u, 0u};
-        if (i < nx && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-          v[k] = *(const u4*)(x + (((size_t)n * g.H + ih) * g.W + iw) * g.C + CS * cs + 8 * ch);
-      }
-#pragma unroll
-      for (int k = 0; k < STAGE_BATCH; ++k) {
-        const int i = i0 + k * NT, sp = i >> 3, ch = i & 7;
-        if (i < nx) *(u4*)(xs + sw(sp, ch >> 1, 8 * (ch & 1))) = v[k];
-      }
-    }
-    for (int i = t; i < np32; i += NT) {
-      const int pc = min(i, npix - 1), orl = pc / g.OW;
-      poff[i] = orl * g.S * g.XW + (pc - orl * g.OW);  // (slots past npix: any in-range pixel, dY is 0 there)
-    }
-    __syncthreads();
-
-    for (int p0 = 0; p0 < np32; p0 += 32) {
-      const int ra = p0 + 4 * grp + q, rb = ra + 16;  // this lane's transposed-read rows (pixel slots)
-      v8bf af[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) af[mt] = cat8(tr_read(ys + sw(ra, mt, 4 * p)), tr_read(ys + sw(rb, mt, 4 * p)));
-      const int xa = poff[ra], xb = poff[rb];
-#pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const int J = 9 * wv + j, tap = J >> 2, cb = J & 3;
-        const int ts = tap % 3, to = (tap / 3) * g.XW + (ts == 0 ? 0 : ts == 1 ? g.c1 : g.c2);
-        const v8bf bfr = cat8(tr_read(xs + sw(xa + to, cb, 4 * p)), tr_read(xs + sw(xb + to, cb, 4 * p)));
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt][j] = mfma(af[mt], bfr, acc[mt][j]);
-      }
+  __syncthreads();  // chunk 0 staged
+  {
+    int bsel = 0;
+    for (int gr = r_begin; gr < r_end;) {
+      const Chunk cur = chunk_at(gr, r_end, g);
+      compute(g, bsel ? B1 : B0, cur.cr * g.OW, wv, lane, acc);
+      __syncthreads();
+      gr += cur.cr;
+      bsel ^= 1;
     }
   }
+#else
+  v4f acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  const Bufs B0 = bufs_at(lds, g);
+  for (int gr = r_begin; gr < r_end;) {
+    const Chunk cur = chunk_at(gr, r_end, g);
+    gr += cur.cr;
+    __syncthreads();  // the previous chunk's reads are done
+    stage<NT>(x, dy, g, os, cs, cur, B0, t);
+    __syncthreads();
+    compute(g, B0, cur.cr * g.OW, wv, lane, acc);
+  }
+#endif
   // acc[mt][j][e] = dW[co = 64 os + 16 mt + 4 grp + e][tap J >> 2][c = 64 cs + 16 (J & 3) + (lane & 15)]
+  const int grp = lane >> 4;
   float* dst = part + (size_t)split * g.Cout * 9 * g.C;
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
@@ -228,11 +316,11 @@ void plan(int W, int OW, int S, int OH, int* cr_out, int* nps_out, int* lds_out)
   cr = cr < 1 ? 1 : (cr > OH ? OH : cr);
   for (;; --cr) {
     const int nps = (cr * OW + 31) & ~31, xr = (cr - 1) * S + 3;
-    const int lds = nps * CS * 2 + nps * 4 + xr * XW * CS * 2;
+    const int lds = buf_elems(nps, xr, XW) * 2;  // one staged chunk (bytes)
     if (lds <= 78 * 1024 || cr == 1) {
       *cr_out = cr;
       *nps_out = nps;
-      *lds_out = lds;
+      *lds_out = C3_WS ? 2 * lds : lds;  // (wave-specialised: two buffers, one workgroup per CU)
       return;
     }
   }
@@ -242,11 +330,13 @@ void plan(int W, int OW, int S, int OH, int* cr_out, int* nps_out, int* lds_out)
 
 extern "C" {
 
-// pixel splits for a shape (~512 workgroups: two per CU), so the caller can size part = splits * Cout * 9 * C floats
+// pixel splits for a shape (~256 workgroups, one per CU, wave-specialised; 512 otherwise: two per CU), so the caller
+// can size part = splits * Cout * 9 * C floats
 int mifx_conv3_wgrad_splits(int N, int H, int W, int C, int Cout, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C % 64 || Cout % 64 || (S != 1 && S != 2)) return -1;
   const int OH = (H - 1) / S + 1, slices = (C / 64) * (Cout / 64);
-  int sp = (512 + slices - 1) / slices;
+  const int target = C3_WS ? 256 : 512;
+  int sp = (target + slices - 1) / slices;
   if (sp > N * OH) sp = N * OH;
   return sp < 1 ? 1 : sp;
 }
@@ -283,7 +373,7 @@ int mifx_conv3_wgrad(const void* x, const void* dy, float* part, float* dw, int 
     (void)hipFuncSetAttribute((const void*)conv3_wgrad, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_lds = lds;
   }
-  hipLaunchKernelGGL(conv3_wgrad, dim3((unsigned)blocks), dim3(NT), lds, st, (const bf16*)x, (const bf16*)dy, part, g);
+  hipLaunchKernelGGL(conv3_wgrad, dim3((unsigned)blocks), dim3(NTK), lds, st, (const bf16*)x, (const bf16*)dy, part, g);
   const int n4 = Cout * 9 * C / 4;
   hipLaunchKernelGGL(conv3_wgrad_sum, dim3(n4 / 16), dim3(256), 0, st, (const float4*)part, n4, splits, C, dw_cl, dw);
   return (int)hipGetLastError();
