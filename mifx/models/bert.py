@@ -244,13 +244,20 @@ class BertForSequenceClassification(nn.Module):
         B, S = input_ids.shape
         pos = torch.arange(S, device=input_ids.device)
         tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
-        x = self.word(input_ids) + fb.embedding(pos, self.pos.weight)[None] + fb.embedding(tt, self.tok_type.weight)
         drop = self.cfg.dropout if self.training else 0.0
         rng = self.drop_rng
         if drop > 0:
             self.drop_rng[1:].add_(1)  # new masks every step (captured into the step's hipGraph)
             rng = fb.rng_snapshot(self.drop_rng)  # this forward's state, shared by all its dropout sites
-        x = fb.dropout(self.ln_emb(x), drop, rng, 0)
+        a = self.word(input_ids) + fb.embedding(pos, self.pos.weight)[None]
+        te = fb.embedding(tt, self.tok_type.weight)
+        if a.is_cuda and a.dtype == torch.bfloat16 and te.dtype == a.dtype:
+            # LayerNorm(word + position + token type) as the fused add + LayerNorm kernel (bf16 out, fp32 inside): no
+            # fp32 activation and no library LayerNorm forward / backward with its casts (~40 us per step)
+            x = fb.add_layernorm(a, te, self.ln_emb.weight, self.ln_emb.bias, self.ln_emb.eps)
+        else:
+            x = self.ln_emb(a + te)
+        x = fb.dropout(x, drop, rng, 0)
         mask = None
         if attention_mask is not None:  # additive key bias [B, S] (fp32; -1e30 on padding keys)
             mask = ((1.0 - attention_mask.float()) * -1e30).contiguous()
