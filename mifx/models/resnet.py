@@ -163,7 +163,7 @@ class PreActBottleneck(nn.Module):
             sc = s
         elif FUSED_1X1 and _fused_ok(self.conv1, pre) and self.shortcut.bias is None \
                 and proj_pair_eligible(pre, self.shortcut.weight, self.shortcut.stride[0], self.conv1.weight):
-            # strided shortcut + conv1 as one node: the two input gradients are summed inside conv1's dX GEMM, which
+            # projection shortcut + conv1 as one node: the two input gradients are summed inside conv1's dX GEMM, which
             # also reduces bn0's backward sums (pre feeds only this pair)
             sc, y, part = proj_pair(pre, self.shortcut.weight, self.shortcut.stride[0], self.conv1.weight,
                                     bn_input=True)

@@ -161,7 +161,15 @@ class _ProjPair(torch.autograd.Function):
         c1, cs = w1.shape[0], w_sc.shape[0]
         oh, ow = (h - 1) // stride + 1, (w_ - 1) // stride + 1
         cfg_sc = hg.gemm8_pick(n * oh * ow, cs, cin) if _SC_G8 and cin >= 64 and not cin & (cin - 1) else None
-        if cfg_sc is not None:  # the center tap of the implicit 3x3 GEMM: pixel (stride oh, stride ow)
+        ctx.wtsc = None
+        if stride == 1:  # (stage 1's projection) a plain GEMM over the same pixel rows as conv1
+            im_sc = weight_prep.images(w_sc)
+            wsc2 = im_sc[0] if im_sc is not None else w_sc.reshape(cs, cin).to(torch.bfloat16).contiguous()
+            ctx.wtsc = im_sc[1] if im_sc is not None else None
+            sc = torch.empty(n, cs, h, w_, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+            hg.gemm8_nt(_rows(x), wsc2, None, 0, cfg=hg.gemm8_pick(n * h * w_, cs, cin), out=_rows(sc))
+            wsb = wsc2.view(cs, cin, 1, 1)
+        elif cfg_sc is not None:  # the center tap of the implicit 3x3 GEMM: pixel (stride oh, stride ow)
             im_sc = weight_prep.images(w_sc)
             wsb = im_sc[0].view(cs, cin, 1, 1) if im_sc is not None else w_sc.to(torch.bfloat16)
             sc = torch.empty(n, cs, oh, ow, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
@@ -188,7 +196,21 @@ class _ProjPair(torch.autograd.Function):
         stride = ctx.stride
         dx = dwsc = dw1 = None
         dx_sc = None
-        if dsc is not None:
+        if dsc is not None and stride == 1:
+            dscc = dsc.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+            cs = wsb.shape[0]
+            ds2 = _rows(dscc)
+            if ctx.needs_input_grad[1]:
+                dwsc = hg.defer_weight_grad_f32(ds2, _rows(x), ctx.w_sc)
+                if dwsc is None:
+                    dwsc = torch.ops.aten.convolution_backward(dscc, x, wsb, None, [1, 1], [0, 0], [1, 1], False,
+                                                               [0, 0], 1, [False, True, False])[1].to(ctx.w_sc.dtype)
+            if ctx.needs_input_grad[0]:  # the shortcut's input gradient: conv1's dX GEMM adds it (R2)
+                wt = ctx.wtsc if ctx.wtsc is not None else hg.transpose(wsb.view(cs, cin))
+                dx_sc = torch.empty(n, cin, h, w_, device=x.device, dtype=torch.bfloat16,
+                                    memory_format=torch.channels_last)
+                hg.gemm8_nt(ds2, wt, None, 0, cfg=hg.gemm8_pick(ds2.shape[0], cin, cs), out=_rows(dx_sc))
+        elif dsc is not None:
             dscc = dsc.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
             cs = wsb.shape[0]
             if ctx.needs_input_grad[0] and (h, cin, cs) in _HIP_DGRAD_S2:
@@ -243,9 +265,21 @@ class _ProjPair(torch.autograd.Function):
         return dx, dwsc, dw1, None, None
 
 
+# stride-1 projection shortcuts (ResNet-50 stage 1: 64 -> 256) in the pair too (MIFX_PAIR_S1=0: the separate node)
+_PAIR_S1 = os.environ.get("MIFX_PAIR_S1", "1") != "0"
+
+
 def proj_pair_eligible(x: torch.Tensor, w_sc: torch.Tensor, stride: int, w1: torch.Tensor) -> bool:
-    """A strided 1x1 shortcut and a GEMM-eligible 1x1 conv1 on the same bf16 channels_last input."""
-    return stride > 1 and tuple(w_sc.shape[2:]) == (1, 1) and eligible(x, w1) and w_sc.shape[1] == x.shape[1]
+    """A 1x1 projection shortcut (strided, or stride 1 on the GEMM kernel both ways) and a GEMM-eligible 1x1 conv1
+    on the same bf16 channels_last input."""
+    if not (tuple(w_sc.shape[2:]) == (1, 1) and eligible(x, w1) and w_sc.shape[1] == x.shape[1]):
+        return False
+    if stride > 1:
+        return True
+    if not (_PAIR_S1 and stride == 1 and w_sc.shape[0] != x.shape[1]):
+        return False
+    m, cin, cs = x.shape[0] * x.shape[2] * x.shape[3], x.shape[1], w_sc.shape[0]
+    return hg.gemm8_pick(m, cs, cin) is not None and hg.gemm8_pick(m, cin, cs) is not None
 
 
 def proj_pair(x: torch.Tensor, w_sc: torch.Tensor, stride: int, w1: torch.Tensor, bn_input: bool = False):

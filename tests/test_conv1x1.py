@@ -224,38 +224,39 @@ def test_conv1x1_bn_coupled_backward(second_consumer):
 
 
 @pytest.mark.parametrize("couple", [False, True])
-def test_proj_pair_matches_separate_convs(couple):
-    """Strided 1x1 shortcut + 1x1 conv1 as one node (mifx.ops.conv1x1.proj_pair): outputs, BN1 statistics, and the
-    summed input gradient written by conv1's dX GEMM (EPI_ADD_BNBWD, with the upstream BatchNorm's sums when coupled)
-    against fp32 PyTorch."""
+@pytest.mark.parametrize("stride,cin,cs,c1", [(2, 256, 512, 128), (1, 64, 256, 64)])
+def test_proj_pair_matches_separate_convs(couple, stride, cin, cs, c1):
+    """1x1 projection shortcut (strided, or stride 1 as in ResNet-50's stage 1) + 1x1 conv1 as one node
+    (mifx.ops.conv1x1.proj_pair): outputs, BN1 statistics, and the summed input gradient written by conv1's dX GEMM
+    (EPI_ADD_BNBWD, with the upstream BatchNorm's sums when coupled) against fp32 PyTorch."""
     from mifx.ops.bn_relu import BatchNormReLU2d
     from mifx.ops.conv1x1 import proj_pair, proj_pair_eligible
 
     torch.manual_seed(2)
-    x0 = _x(4, 256, 16, 16, 21, 1.2, 0.2)
-    wsc = (torch.randn(512, 256, 1, 1, device="cuda") * 256 ** -0.5).contiguous(memory_format=torch.channels_last)
-    w1 = (torch.randn(128, 256, 1, 1, device="cuda") * 256 ** -0.5).contiguous(memory_format=torch.channels_last)
-    gsc = _x(4, 512, 8, 8, 22)
-    g1 = _x(4, 128, 16, 16, 23)
-    bn = BatchNormReLU2d(256).cuda()
+    x0 = _x(4, cin, 16, 16, 21, 1.2, 0.2)
+    wsc = (torch.randn(cs, cin, 1, 1, device="cuda") * cin ** -0.5).contiguous(memory_format=torch.channels_last)
+    w1 = (torch.randn(c1, cin, 1, 1, device="cuda") * cin ** -0.5).contiguous(memory_format=torch.channels_last)
+    gsc = _x(4, cs, 16 // stride, 16 // stride, 22)
+    g1 = _x(4, c1, 16, 16, 23)
+    bn = BatchNormReLU2d(cin).cuda()
     x = x0.detach().clone().requires_grad_()
     a, b = wsc.detach().clone().requires_grad_(), w1.detach().clone().requires_grad_()
     pre = bn(x)
-    assert proj_pair_eligible(pre, a, 2, b)
-    sc, y1, part = proj_pair(pre, a, 2, b, bn_input=couple)
+    assert proj_pair_eligible(pre, a, stride, b)
+    sc, y1, part = proj_pair(pre, a, stride, b, bn_input=couple)
     (sc.float() * gsc.float()).sum().add((y1.float() * g1.float()).sum()).backward()
     # fp32 reference
     xr = x0.detach().float().requires_grad_()
     wr, br = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
     ar, b1r = wsc.detach().clone().requires_grad_(), w1.detach().clone().requires_grad_()
     pr = F.relu(F.batch_norm(xr, None, None, wr, br, True, 0.1, 1e-5))
-    scr = F.conv2d(pr, ar.to(torch.bfloat16).float(), stride=2)
+    scr = F.conv2d(pr, ar.to(torch.bfloat16).float(), stride=stride)
     y1r = F.conv2d(pr, b1r.to(torch.bfloat16).float())
     (scr * gsc.float()).sum().add((y1r * g1.float()).sum()).backward()
     torch.testing.assert_close(sc.float(), scr, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(y1.float(), y1r, rtol=3e-2, atol=3e-2)
     M, T = 4 * 16 * 16, part.shape[1]
-    yf = y1.float().permute(0, 2, 3, 1).reshape(M, 128).double()
+    yf = y1.float().permute(0, 2, 3, 1).reshape(M, c1).double()
     torch.testing.assert_close(part[0].double().mean(0), yf.mean(0), rtol=1e-5, atol=1e-5)
     for got, want in ((x.grad.float(), xr.grad), (bn.weight.grad, wr.grad), (bn.bias.grad, br.grad),
                       (a.grad, ar.grad), (b.grad, b1r.grad)):
