@@ -274,7 +274,10 @@ class _ScatterToSeq(torch.autograd.Function):
     def forward(ctx, x, tp, dtype):
         ctx.tp, ctx.dtype = tp, x.dtype
         Ts = _seq_rows(x.shape[0], tp)
-        return x[tp.rank * Ts:(tp.rank + 1) * Ts].to(dtype).contiguous()
+        y = x[tp.rank * Ts:(tp.rank + 1) * Ts]
+        # always a new tensor: an input already in `dtype` would otherwise come back as a VIEW of the replicated
+        # activation (a custom Function's output aliasing its input)
+        return y.to(dtype).contiguous() if y.dtype != dtype else y.clone(memory_format=torch.contiguous_format)
 
     @staticmethod
     def backward(ctx, g):
