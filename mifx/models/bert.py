@@ -251,10 +251,11 @@ class BertForSequenceClassification(nn.Module):
             rng = fb.rng_snapshot(self.drop_rng)  # this forward's state, shared by all its dropout sites
         a = self.word(input_ids) + fb.embedding(pos, self.pos.weight)[None]
         te = fb.embedding(tt, self.tok_type.weight)
-        if a.is_cuda and a.dtype == torch.bfloat16 and te.dtype == a.dtype:
+        if a.is_cuda and a.dtype == torch.bfloat16 and te.dtype == a.dtype and self.tp.size == 1:
             # LayerNorm(word + position + token type) as the fused add + LayerNorm kernel (bf16 out, fp32 inside): no
-            # fp32 activation and no library LayerNorm forward / backward with its casts (~40 us per step); every TP
-            # degree takes it, so TP > 1 and TP = 1 train the same function
+            # fp32 activation and no library LayerNorm forward / backward with its casts (~40 us per step). TP = 1
+            # (the measured configuration) only: TP > 1 keeps the path its multi-rank rehearsals were validated on
+            # (the 8-rank shared-GPU sequence-parallel test timed out twice with it, cause not isolated in round 6)
             x = fb.add_layernorm(a, te, self.ln_emb.weight, self.ln_emb.bias, self.ln_emb.eps)
         else:
             x = self.ln_emb(a + te)
