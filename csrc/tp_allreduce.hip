@@ -43,7 +43,7 @@ constexpr int MAXW = 8;
 constexpr int CHUNK = 4096;          // bf16 elements per chunk (8 KB)
 constexpr int WG = 64;               // one wave per workgroup
 constexpr int PER_LANE = CHUNK / 4 / WG;  // uint64 (4 x bf16) per lane per chunk = 16
-constexpr long long TIMEOUT_TICKS = 3000ll * 1000 * 1000;  // 30 s at the 100 MHz real-time clock (8 ranks time-sharing one
+constexpr long long TIMEOUT_TICKS = 12000ll * 1000 * 1000;  // 120 s at the 100 MHz real-time clock (8 ranks time-sharing one
 // GPU in the rehearsals: a rank held up on the host for seconds must not trip it)
 
 struct Peers {
