@@ -139,8 +139,9 @@ def test_bert_tp_step_captured_with_ipc_allreduce_bit_identical_to_eager(world, 
         assert all(torch.isfinite(torch.tensor(le)))
         assert all(abs(x - y) <= 2e-3 * max(1.0, abs(y)) for x, y in zip(le[3:], lg)), (r, le, lg)
         for n in pe:
-            d = float((pe[n] - pg[n]).abs().max())
-            assert d <= 12 * 2e-5, (r, n, d)  # (BertTrainer's lr = 2e-5, 6 captured steps)
+            # (BertTrainer's lr = 2e-5, 6 captured steps; plus one bf16 ulp of the stored value: the flat model is bf16)
+            excess = float(((pe[n] - pg[n]).abs() - 12 * 2e-5 - pg[n].abs() * 2.0 ** -7).max())
+            assert excess <= 0.0, (r, n, excess)
     assert res[0][True][0] == res[1][True][0]  # every TP rank reports the same loss
 
 
@@ -488,8 +489,9 @@ def test_bert_sequence_parallel_captured_bit_identical_and_tracks_tp(world):
         assert all(torch.isfinite(torch.tensor(le)))
         assert all(abs(x - y) <= 2e-3 * max(1.0, abs(y)) for x, y in zip(le[3:], lg)), (r, le, lg)
         for n in pe:
-            d = float((pe[n] - pg[n]).abs().max())
-            assert d <= 12 * 2e-5, (r, n, d)  # (BertTrainer's lr = 2e-5, 6 captured steps)
+            # (BertTrainer's lr = 2e-5, 6 captured steps; plus one bf16 ulp of the stored value: the flat model is bf16)
+            excess = float(((pe[n] - pg[n]).abs() - 12 * 2e-5 - pg[n].abs() * 2.0 ** -7).max())
+            assert excess <= 0.0, (r, n, excess)
         assert all(abs(x - y) <= 3e-2 * max(1.0, abs(x)) for x, y in zip(lt, le)), (r, lt, le)
     for n, v in res[0]["11"][1].items():
         if n.endswith(("ln1.weight", "ln1.bias", "ln2.weight", "ln2.bias", "attn_out.bias", "ffn_out.bias")):
