@@ -10,8 +10,8 @@
 // row and meet zero weights. 7 K-steps of v_mfma_f32_16x16x32_bf16 per 16 x 16 output tile, 34 % of them on padding --
 // cheap next to the memory traffic, and no im2col gather or masking in the inner loop.
 //
-//  * Workgroup: ROWS = 8 output rows of one image (8 x OW pixels) x all 64 output channels, 4 waves. Each wave loads
-//    its 28 weight fragments (bf16 image [64][7][32], L2-resident) into registers while the 21 input rows the
+//  * Workgroup: ROWS = 16 output rows of one image (16 x OW pixels) x all 64 output channels, 4 waves. Each wave loads
+//    its 28 weight fragments (bf16 image [64][7][32], L2-resident) into registers while the 37 input rows the
 //    workgroup needs (zero rows / columns outside the image) are staged in LDS; after one barrier it runs, for every
 //    4th 16-pixel tile, 7 x 4 MFMAs fed by 4-byte window reads.
 //  * The weight is the MFMA A operand (16 output channels x 32 taps: one 16-byte LDS read per lane) and the input
@@ -32,7 +32,7 @@ constexpr int KH = 7, KW = 7, CIN = 3, COUT = 64, STR = 2, PAD = 3;
 constexpr int Q = KW * CIN;                 // 21 taps per kernel row
 constexpr int QP = 32;                      // one MFMA K-step
 #ifndef STEM_ROWS
-#define STEM_ROWS 8
+#define STEM_ROWS 16  // (8 / 12 / 16 same-box step A/B: 16 fastest, profiles/resnet_stem_rows_ab_r6.jsonl)
 #endif
 constexpr int ROWS = STEM_ROWS;             // output rows per workgroup
 constexpr int IR = STR * (ROWS - 1) + KH;   // input rows staged
